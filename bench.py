@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: band-samples/s of the 4096-band Filterbank<double>.
+
+Workload (BASELINE.json configs[1]): Filterbank<double>(2, 4096),
+resonant band-pass bank f_i = 0.5 (i+1) SR / 4096, R = 0.999 (tests/resynthesis.cpp:48-54
+recipe), boost(all 1) + open(), k_p = 0.1, k_g = 1, synthetic white noise (uniform[-1,1)
+float32 -> double), kernel time tile = the reference's BSIZE 1024.
+
+One step = one Filterbank::process() call over 10 s of 48 kHz audio (480,000 samples),
+input already resident in HBM; the result is identical to 469 x {1024-sample block} calls
+(tests/test_filterbank_gpu.py::test_block_split_and_per_sample).  A streaming figure
+(one call per 1024-sample block) is reported beside it.
+
+Multi-GPU (torchrun, one process per GPU): the 4096 bands are split contiguously
+over ranks (strong scaling: total work fixed); each rank mixes its shard and the
+partial mixes are summed to rank 0 with an RCCL reduce over xGMI every step.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SR = 48000
+N_BANDS = 4096
+R_POLE = 0.999
+SAMPLES_PER_STEP = 480_000
+FP64_PEAK_TFLOPS = 78.6       # MI355X FP64 vector (= FP64 matrix) peak, SURVEY.md 8(d)
+HBM_PEAK_GBS = 8000.0
+FLOPS_PER_BAND_SAMPLE = 18    # 4*O + 10 with O = 2
+
+
+def c2_coefficients(N=N_BANDS, R=R_POLE):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden.spec_numpy import resonant_coefficients
+    return resonant_coefficients(N, R, 1.0)
+
+
+def shard_of(rank, world, N=N_BANDS):
+    base, rem = divmod(N, world)
+    begin = rank * base + min(rank, rem)
+    return begin, base + (1 if rank < rem else 0)
+
+
+def cpu_baseline(fwd, back, seconds_target=1.5):
+    """The oracle (C restatement, -O2, no FMA contraction) on the host cores: bands
+    split over threads (ctypes releases the GIL), one Filterbank per thread."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import OracleFilterbank
+    threads = max(1, min(16, os.cpu_count() or 1))
+    N = fwd.shape[0]
+    rng = np.random.default_rng(1)
+    nsamp = 96_000
+    x = rng.uniform(-1, 1, nsamp).astype(np.float32).astype(np.float64)
+    banks = []
+    for t in range(threads):
+        b0, cnt = shard_of(t, threads, N)
+        fb = OracleFilterbank(2, cnt)
+        for i in range(cnt):
+            fb.coefficients(i, fwd[b0 + i], back[b0 + i])
+        fb.boost(np.ones(cnt))
+        fb.open()
+        banks.append(fb)
+    outs = [None] * threads
+
+    def run(i):
+        outs[i] = banks[i].process(x)
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    return {"value": N * nsamp / dt, "unit": "band-samples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/hz_oracle.c restatement, {N} bands x {nsamp} samples "
+                      f"({nsamp / SR:.2f} s audio), bands split over {threads} threads, {dt:.2f} s wall"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--samples", type=int, default=SAMPLES_PER_STEP)
+    ap.add_argument("--stream-blocks", type=int, default=469, help="1024-sample calls for the streaming figure")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--bands-per-wave", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from huygens_amd import Filterbank
+    fwd, back = c2_coefficients()
+    b0, cnt = shard_of(rank, world)
+    fb = Filterbank(2, N_BANDS, 0.1, 1.0, device=local, shard=(b0, cnt))
+    for n in range(b0, b0 + cnt):
+        fb.coefficients(n, fwd[n], back[n])
+    fb.boost(np.ones(N_BANDS))
+    fb.open()
+    if args.waves or args.bands_per_wave:
+        fb.tune(args.waves, args.bands_per_wave)
+    stream = torch.cuda.current_stream(dev)
+    fb.set_stream(stream.cuda_stream)
+
+    S = args.samples
+    rng = np.random.default_rng(1234)
+    x = torch.from_numpy(rng.uniform(-1, 1, S).astype(np.float32).astype(np.float64)).to(dev)
+    y = torch.empty_like(x)
+
+    def step():
+        fb.process_device(x.data_ptr(), y.data_ptr(), S)
+        if world > 1:
+            dist.reduce(y, dst=0, op=dist.ReduceOp.SUM)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    fb.profile(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    seg_ms, mix_ms, red_ms, launches = fb.profile_read()
+    fb.profile(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        mm = torch.tensor([mix_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(mm, op=dist.ReduceOp.MAX)
+        mix_ms_max = float(mm.item())
+    else:
+        mix_ms_max = mix_ms
+
+    # streaming figure: one process() call per 1024-sample block
+    stream_rate = None
+    if args.stream_blocks > 0:
+        B = 1024
+        nb = min(args.stream_blocks, S // B)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        ts = time.perf_counter()
+        for i in range(nb):
+            fb.process_device(x.data_ptr() + 8 * B * i, y.data_ptr() + 8 * B * i, B)
+            if world > 1:
+                dist.reduce(y[i * B:(i + 1) * B], dst=0, op=dist.ReduceOp.SUM)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        tstream = time.perf_counter() - ts
+        if world > 1:
+            t = torch.tensor([tstream], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tstream = float(t.item())
+        stream_rate = N_BANDS * B * nb / tstream
+
+    total_band_samples = N_BANDS * S * args.steps
+    value = total_band_samples / elapsed
+    if rank == 0:
+        # dominant kernel: fb_mix_kernel; algorithmic flops per launch = 18 x band-samples
+        mix_avg_s = (mix_ms_max / 1e3) / max(1, launches)
+        flops_per_launch = FLOPS_PER_BAND_SAMPLE * cnt * S
+        achieved = flops_per_launch / mix_avg_s / 1e12 if mix_avg_s > 0 else None
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(fwd, back)
+        line = {
+            "metric": "band-samples/s (bands x frames/s) for 4096-band Filterbank",
+            "value": value,
+            "unit": "band-samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic white noise uniform[-1,1) (float32 -> double), seed 1234",
+            "config": {"workload": "C2 Filterbank<double>(order 2, 4096 bands), resonant band-pass "
+                                   "f_i=0.5(i+1)SR/4096 R=0.999, boost 1 + open, k_p=0.1 k_g=1",
+                       "samples_per_step": S, "block": 1024, "bands": N_BANDS,
+                       "bands_per_gpu": cnt, "parallelism": f"bands sharded x{world}, RCCL reduce"},
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
+                         "traffic": None,
+                         "kernel": "fb_mix_kernel<2,0,1,0>",
+                         "kernel_avg_ms": 1e3 * mix_avg_s,
+                         "segment_prepass_ms_per_launch": seg_ms / max(1, launches),
+                         "reduce_ms_per_launch": red_ms / max(1, launches),
+                         "flops_per_launch": flops_per_launch,
+                         "note": "FP64 vector peak (= FP64 MFMA peak); 18 flops per band-sample (SURVEY.md 8(d))"},
+            "streaming": {"band_samples_per_s": stream_rate, "block": 1024,
+                          "note": "one process() call per 1024-sample block, device-resident I/O"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

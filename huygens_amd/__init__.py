@@ -1,0 +1,10 @@
+"""huygens_amd -- MI355X-native (gfx950 HIP) engine for the amcerbu/huygens bank hot path.
+
+The product is libhuygens_hip.so (C ABI: include/huygens_hip.h) with the C++
+drop-in headers in include/soundmath/.  This package is the Python mirror of
+that ABI used by tests/ and bench.py.
+"""
+from ._lib import HZError, load, header_symbols  # noqa: F401
+from .filterbank import Filterbank  # noqa: F401
+
+__all__ = ["HZError", "load", "header_symbols", "Filterbank"]

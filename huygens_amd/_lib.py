@@ -1,0 +1,113 @@
+"""ctypes binding of libhuygens_hip.so (the C ABI declared in include/huygens_hip.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no gfx950
+device is visible, every call raises HZError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libhuygens_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "huygens_hip.h")
+
+HZ_OK = 0
+HZ_E_INVALID = -1
+HZ_E_RANGE = -2
+HZ_E_HIP = -3
+HZ_E_NODEV = -4
+HZ_E_ALLOC = -5
+HZ_E_UNSUPPORTED = -6
+
+HZ_DIST_NONE = 0
+HZ_DIST_SOFTCLIP = 1
+HZ_DIST_SATURATE = 2
+HZ_DIST_LIMITER = 3
+
+_ERRNAMES = {
+    HZ_E_INVALID: "HZ_E_INVALID", HZ_E_RANGE: "HZ_E_RANGE", HZ_E_HIP: "HZ_E_HIP",
+    HZ_E_NODEV: "HZ_E_NODEV", HZ_E_ALLOC: "HZ_E_ALLOC", HZ_E_UNSUPPORTED: "HZ_E_UNSUPPORTED",
+}
+
+
+class HZError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+D = C.c_double
+I = C.c_int
+L = C.c_long
+SZ = C.c_size_t
+VP = C.c_void_p
+PD = C.POINTER(C.c_double)
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "hz_last_error": (C.c_char_p, []),
+    "hz_version": (I, []),
+    "hz_device_count": (I, []),
+    # Filterbank
+    "hz_fb_create": (I, [I, I, D, D, I, C.POINTER(VP)]),
+    "hz_fb_create_shard": (I, [I, I, I, I, D, D, I, C.POINTER(VP)]),
+    "hz_fb_destroy": (I, [VP]),
+    "hz_fb_coefficients": (I, [VP, I, PD, I, PD, I]),
+    "hz_fb_boost": (I, [VP, I, D]),
+    "hz_fb_boost_all": (I, [VP, PD, I]),
+    "hz_fb_mix": (I, [VP, I, D]),
+    "hz_fb_mix_all": (I, [VP, PD, I]),
+    "hz_fb_open": (I, [VP]),
+    "hz_fb_set_distortion": (I, [VP, I, D]),
+    "hz_fb_process": (I, [VP, PD, PD, SZ]),
+    "hz_fb_process_device": (I, [VP, VP, VP, SZ]),
+    "hz_fb_set_stream": (I, [VP, VP]),
+    "hz_fb_get_stream": (I, [VP, C.POINTER(VP)]),
+    "hz_fb_synchronize": (I, [VP]),
+    "hz_fb_state_size": (I, [VP, C.POINTER(SZ)]),
+    "hz_fb_get_state": (I, [VP, PD, SZ]),
+    "hz_fb_set_state": (I, [VP, PD, SZ]),
+    "hz_fb_info": (I, [VP, C.POINTER(I), C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
+    "hz_fb_tune": (I, [VP, I, I]),
+    "hz_fb_profile": (I, [VP, I]),
+    "hz_fb_profile_read": (I, [VP, PD, PD, PD, C.POINTER(L)]),
+    "hz_fb_set_target_groups": (I, [VP, I]),
+}
+
+
+def load():
+    """Load (once) and return the ctypes library; raises HZError when absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HZError(HZ_E_UNSUPPORTED, f"{LIB_PATH} not built (run `make lib` or __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def header_symbols(path: str = HEADER_PATH):
+    """Every hz_* function declared in include/huygens_hip.h."""
+    txt = open(path).read()
+    return sorted(set(re.findall(r"\b(hz_[a-z0-9_]+)\s*\(", txt)))
+
+
+def check(code: int):
+    if code != HZ_OK:
+        msg = load().hz_last_error()
+        raise HZError(code, msg.decode() if msg else "")
+    return code
+
+
+def dptr(a):
+    """ctypes double* of a C-contiguous float64 numpy array."""
+    return a.ctypes.data_as(PD)

@@ -1,0 +1,987 @@
+// hz_filterbank.hip -- Filterbank<double> block engine for MI355X (gfx950).
+//
+// Replaces src/filterbank.h:16-188 (Filterbank<T>::compute/operator()/tick):
+//   pre_n[t] = (1-sp) pin_n + sp pre_n[t-1]                       (172)
+//   g_n[t]   = (1-sg) gin_n + sg g_n[t-1]                         (173)
+//   y_n[t]   = pre_n[t] * sum_i F[n][i] x[t-i] - sum_k B[n][k] y_n[t-1-k]   (178-179)
+//   out[t]   = sum_n dist(y_n[t] g_n[t])                          (130, 138)
+//
+// Kernel design (DESIGN.md "Filterbank"):
+//   * lanes are TIME: lane c of a wave owns samples [16c, 16c+16) of a 1024-sample
+//     tile, so the mixdown over bands needs no cross-lane reduction -- each lane
+//     accumulates its 16 outputs over the bands the wave visits.
+//   * the IIR time recurrence is split into a per-lane zero-state pass (registers),
+//     a 64-lane Hillis-Steele scan of the O x O companion-matrix carry (matrix powers
+//     M16^(2^s) precomputed per band on the host), and a per-lane fix-up with the
+//     per-band homogeneous responses h_k[j] (wave-uniform, scalar loads).
+//   * pre/gain smoothing is seeded per lane in closed form pin + sp^t (P0 - pin) and
+//     advanced by the reference's own one-pole recurrence inside the chunk.
+//   * waves of a workgroup visit different bands of the same tile; their 1024-sample
+//     partial mixes are summed through LDS, and one row per band group is written to
+//     a partial slab that a second kernel sums (deterministic, no atomics).
+//   * a wave walks the tiles of the call sequentially, carrying the band state in
+//     registers (readlane of lane 63's scanned end state).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "hz_common.h"
+
+namespace {
+
+constexpr int kL = 16;            // samples per lane chunk
+constexpr int kTile = 64 * kL;    // samples per wave tile (= reference BSIZE 1024)
+constexpr int kMaxOrder = 4;
+
+// Per-band record (doubles), O-dependent layout.
+template <int O>
+struct Rec {
+    static constexpr int B = 0;                  // b[0..O]           feed-forward
+    static constexpr int A = O + 1;              // a[0..O-1]         feedback
+    static constexpr int H = 2 * O + 1;          // h[k][j] k<O j<16  homogeneous responses
+    static constexpr int P = H + kL * O;         // P[s][r][c] s<6    (M16)^(2^s)
+    static constexpr int RAW = P + 6 * O * O;
+    static constexpr int SIZE = (RAW + 7) & ~7;  // 64-B aligned records
+};
+
+static int rec_size(int O) {
+    switch (O) {
+    case 0: return Rec<0>::SIZE;
+    case 1: return Rec<1>::SIZE;
+    case 2: return Rec<2>::SIZE;
+    case 3: return Rec<3>::SIZE;
+    default: return Rec<4>::SIZE;
+    }
+}
+
+struct MixArgs {
+    const double* rec;     // [N][REC]
+    const double* pin;     // [N]
+    const double* gin;     // [N]
+    double* ystate;        // [N][O]  y[-1-k]
+    double* pgstate;       // [N][2]  pre, gain
+    const double* x;       // [n] device input
+    const double* xhist;   // [O] x[-1-k]
+    double* xhist_next;    // [O]
+    double* partial;       // [G][n_pad]
+    double* segstate;      // [N][nseg][O] start state of each time segment (nseg > 1)
+    long n;
+    long n_pad;
+    long seg_len;          // samples per time segment (multiple of kTile)
+    int nseg;
+    int nbands;
+    double sp, sg;         // smoothing coefficients
+    double sp_tile, sg_tile;  // sp^1024, sg^1024
+    double sp_n, sg_n;     // sp^n, sg^n (final state)
+    double dist_param;
+};
+
+// Scalar (SGPR) copy of a wave-uniform double.
+__device__ __forceinline__ double uniform(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffff));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// MODE_MIX: full pass (zero-state pass, carry scan, fix-up, mixdown) over one
+//   time segment (blockIdx.y) of one band group (blockIdx.x).
+// MODE_SEGEND: zero-state end state of each segment but the last (no mixdown),
+//   feeding fb_seg_carry_kernel when the bank is too small to fill the chip
+//   with bands alone (e.g. 512-band shards on 8 GPUs).
+enum { MODE_MIX = 0, MODE_SEGEND = 1 };
+
+template <int O, int DIST, int NB, int MODE>
+__global__ __launch_bounds__(1024) void fb_mix_kernel(MixArgs a) {
+    using R = Rec<O>;
+    extern __shared__ __attribute__((aligned(16))) double lds[];  // [W][16][65]
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int W = blockDim.x >> 6;
+    const int band0 = (blockIdx.x * W + wave) * NB;
+    const long n = a.n;
+    const int seg = blockIdx.y;
+    const long seg_t0 = (long)seg * a.seg_len;
+    const long seg_n = min(a.seg_len, n - seg_t0);
+    const int ntiles = (int)((seg_n + kTile - 1) / kTile);
+    const bool last_seg = seg == a.nseg - 1;
+    double* my = lds + (long)wave * (kL * 65);  // this wave's 1024-sample partial mix
+
+    // per-lane smoothing powers sp^(16 lane); the tile factor is wave-uniform
+    const double sp_lane = pow(a.sp, (double)(kL * lane));
+    const double sg_lane = pow(a.sg, (double)(kL * lane));
+    double sp_t = seg_t0 ? uniform(pow(a.sp, (double)seg_t0)) : 1.0;
+    double sg_t = seg_t0 ? uniform(pow(a.sg, (double)seg_t0)) : 1.0;
+
+    // carried band state (wave-uniform)
+    double S[NB][O > 0 ? O : 1];
+    double P0[NB], G0[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int band = band0 + b;
+        const bool ok = band < a.nbands;
+        const double* s0 = (MODE == MODE_SEGEND) ? nullptr
+                         : (seg == 0) ? a.ystate + (long)band * O
+                                      : a.segstate + ((long)band * a.nseg + seg) * O;
+#pragma unroll
+        for (int k = 0; k < O; ++k) S[b][k] = (ok && s0) ? s0[k] : 0.0;
+        P0[b] = ok ? a.pgstate[2 * (long)band] : 0.0;
+        G0[b] = ok ? a.pgstate[2 * (long)band + 1] : 0.0;
+    }
+
+    for (int tile = 0; tile < ntiles; ++tile) {
+        const long t0 = seg_t0 + (long)tile * kTile;  // global sample index of the tile
+        const long tc = t0 + (long)kL * lane;
+        const bool last_tile = last_seg && tile == ntiles - 1;
+
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int band = band0 + b;
+            if (band >= a.nbands) {  // wave-uniform: contribute nothing
+                if (MODE == MODE_MIX && b == 0) {
+#pragma unroll
+                    for (int j = 0; j < kL; ++j) my[j * 65 + lane] = 0.0;
+                }
+                break;
+            }
+            const double* r = a.rec + (long)band * R::SIZE;
+            const double pin = a.pin[band];
+            const double gin = a.gin[band];
+
+            // ---- zero-state pass over the lane's 16 samples ----------------
+            double zsr[kL];
+            {
+                // input window x[tc-O .. tc+15]
+                double xv[kL + O];
+#pragma unroll
+                for (int k = 0; k < kL + O; ++k) {
+                    const long idx = tc - O + k;
+                    double v = 0.0;
+                    if (idx < 0) v = a.xhist[-idx - 1];
+                    else if (idx < seg_t0 + seg_n) v = a.x[idx];
+                    xv[k] = v;
+                }
+                double pre = pin + (sp_lane * sp_t) * (P0[b] - pin);
+                const double cp = (1.0 - a.sp) * pin;
+                double yh[O > 0 ? O : 1];
+#pragma unroll
+                for (int k = 0; k < O; ++k) yh[k] = 0.0;
+#pragma unroll
+                for (int j = 0; j < kL; ++j) {
+                    pre = fma(a.sp, pre, cp);
+                    double ff = r[R::B] * xv[j + O];
+#pragma unroll
+                    for (int i = 1; i <= O; ++i) ff = fma(r[R::B + i], xv[j + O - i], ff);
+                    double y = ff * pre;
+#pragma unroll
+                    for (int k = 0; k < O; ++k) y = fma(-r[R::A + k], yh[k], y);
+#pragma unroll
+                    for (int k = O - 1; k > 0; --k) yh[k] = yh[k - 1];
+                    if constexpr (O > 0) yh[0] = y;
+                    zsr[j] = y;
+                }
+            }
+
+            // ---- carry scan across the 64 chunks of the tile -----------------
+            double st[O > 0 ? O : 1];
+            if constexpr (O > 0) {
+                double z[O];
+#pragma unroll
+                for (int k = 0; k < O; ++k) z[k] = zsr[kL - 1 - k];
+                if (lane == 0) {
+#pragma unroll
+                    for (int rr = 0; rr < O; ++rr)
+#pragma unroll
+                        for (int c = 0; c < O; ++c) z[rr] = fma(r[R::P + rr * O + c], S[b][c], z[rr]);
+                }
+#pragma unroll
+                for (int s = 0; s < 6; ++s) {
+                    const int d = 1 << s;
+                    double nb[O];
+#pragma unroll
+                    for (int k = 0; k < O; ++k) nb[k] = __shfl_up(z[k], d, 64);
+                    if (lane >= d) {
+#pragma unroll
+                        for (int rr = 0; rr < O; ++rr)
+#pragma unroll
+                            for (int c = 0; c < O; ++c)
+                                z[rr] = fma(r[R::P + s * O * O + rr * O + c], nb[c], z[rr]);
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < O; ++k) {
+                    const double prev = __shfl_up(z[k], 1, 64);
+                    st[k] = (lane == 0) ? S[b][k] : prev;
+                }
+                // end state of the tile = lane 63 (the padded tail of a ragged last
+                // tile only matters after the final sample, where it is unused)
+#pragma unroll
+                for (int k = 0; k < O; ++k) S[b][k] = uniform(__shfl(z[k], 63, 64));
+            }
+            if constexpr (MODE == MODE_SEGEND) continue;
+
+            // ---- fix-up, gain smoothing and mixdown into the LDS tile --------
+            double g = gin + (sg_lane * sg_t) * (G0[b] - gin);
+            const double cg = (1.0 - a.sg) * gin;
+#pragma unroll
+            for (int j = 0; j < kL; ++j) {
+                double y = zsr[j];
+#pragma unroll
+                for (int k = 0; k < O; ++k) y = fma(r[R::H + k * kL + j], st[k], y);
+                g = fma(a.sg, g, cg);
+                double v;
+                if constexpr (DIST == HZ_DIST_NONE) v = g * y;
+                else v = hz::dist_apply<DIST>(g * y, a.dist_param);
+                if (b == 0) my[j * 65 + lane] = v;
+                else my[j * 65 + lane] += v;
+                if constexpr (O > 0) {
+                    if (last_tile) {
+                        const long t = tc + j;
+                        if (t >= n - O && t < n) a.ystate[(long)band * O + (n - 1 - t)] = y;
+                    }
+                }
+            }
+            if constexpr (O > 0) {
+                // n < O (e.g. per-sample calls): the older history entries shift along;
+                // n < O implies a single tile, so lane 0's chunk start state is the
+                // state at call start
+                if (last_tile && lane == 0 && n < O) {
+#pragma unroll
+                    for (int k = 0; k < O; ++k)
+                        if (k >= n) a.ystate[(long)band * O + k] = st[k - n];
+                }
+            }
+            if (last_tile && lane == 0) {
+                // closed-form end state of the one-pole smoothers after n samples
+                a.pgstate[2 * (long)band] = pin + a.sp_n * (P0[b] - pin);
+                a.pgstate[2 * (long)band + 1] = gin + a.sg_n * (G0[b] - gin);
+            }
+        }
+
+        if constexpr (MODE == MODE_MIX) {
+            // ---- workgroup reduction of the partial mixes over waves ---------
+            __syncthreads();
+            for (int tl = threadIdx.x; tl < kTile; tl += blockDim.x) {
+                const int src_lane = tl >> 4, j = tl & 15;
+                double s = 0.0;
+                for (int w = 0; w < W; ++w) s += lds[(long)w * (kL * 65) + j * 65 + src_lane];
+                const long t = t0 + tl;
+                if (t < n) a.partial[(long)blockIdx.x * a.n_pad + t] = s;
+            }
+            __syncthreads();
+        }
+        sp_t *= a.sp_tile;
+        sg_t *= a.sg_tile;
+    }
+
+    if constexpr (MODE == MODE_SEGEND) {
+        // zero-state end state of this segment -> segstate[band][seg + 1] (temporarily;
+        // fb_seg_carry_kernel turns it into the true start state of segment seg + 1)
+        if (lane == 0 && !last_seg) {
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const int band = band0 + b;
+                if (band >= a.nbands) break;
+#pragma unroll
+                for (int k = 0; k < O; ++k) a.segstate[((long)band * a.nseg + seg + 1) * O + k] = S[b][k];
+            }
+        }
+    } else if constexpr (O > 0) {
+        // ---- x history for the next call (ping-pong buffer) ------------------
+        if (last_seg && blockIdx.x == 0 && threadIdx.x < O) {
+            const int k = threadIdx.x;
+            const long idx = n - 1 - k;
+            a.xhist_next[k] = idx >= 0 ? a.x[idx] : a.xhist[-idx - 1];
+        }
+    }
+}
+
+// Sequential carry over time segments, one thread per band:
+//   start(s+1) = C^seg_len start(s) + zsr_end(s),  start(0) = ystate.
+// C^seg_len = (M16^64)^(seg_len/1024) by binary powering of the record's P[5]^2.
+template <int O>
+__global__ __launch_bounds__(256) void fb_seg_carry_kernel(const double* __restrict__ rec,
+                                                           const double* __restrict__ ystate,
+                                                           double* __restrict__ segstate, int nbands,
+                                                           int nseg, long seg_tiles) {
+    using R = Rec<O>;
+    const int band = blockIdx.x * blockDim.x + threadIdx.x;
+    if (band >= nbands) return;
+    const double* r = rec + (long)band * R::SIZE;
+    double M[O][O], Pw[O][O], T[O][O];
+    // M1024 = P[5] * P[5]
+#pragma unroll
+    for (int i = 0; i < O; ++i)
+#pragma unroll
+        for (int j = 0; j < O; ++j) {
+            double acc = 0;
+#pragma unroll
+            for (int q = 0; q < O; ++q) acc = fma(r[R::P + 5 * O * O + i * O + q], r[R::P + 5 * O * O + q * O + j], acc);
+            Pw[i][j] = acc;
+            M[i][j] = (i == j) ? 1.0 : 0.0;
+        }
+    for (long e = seg_tiles; e > 0; e >>= 1) {
+        if (e & 1) {
+            for (int i = 0; i < O; ++i)
+                for (int j = 0; j < O; ++j) {
+                    double acc = 0;
+                    for (int q = 0; q < O; ++q) acc = fma(M[i][q], Pw[q][j], acc);
+                    T[i][j] = acc;
+                }
+            for (int i = 0; i < O; ++i)
+                for (int j = 0; j < O; ++j) M[i][j] = T[i][j];
+        }
+        for (int i = 0; i < O; ++i)
+            for (int j = 0; j < O; ++j) {
+                double acc = 0;
+                for (int q = 0; q < O; ++q) acc = fma(Pw[i][q], Pw[q][j], acc);
+                T[i][j] = acc;
+            }
+        for (int i = 0; i < O; ++i)
+            for (int j = 0; j < O; ++j) Pw[i][j] = T[i][j];
+    }
+    double S[O];
+#pragma unroll
+    for (int k = 0; k < O; ++k) S[k] = ystate[(long)band * O + k];
+    for (int s = 1; s < nseg; ++s) {
+        double* slot = segstate + ((long)band * nseg + s) * O;
+        double nS[O];
+#pragma unroll
+        for (int i = 0; i < O; ++i) {
+            double acc = slot[i];
+#pragma unroll
+            for (int q = 0; q < O; ++q) acc = fma(M[i][q], S[q], acc);
+            nS[i] = acc;
+        }
+#pragma unroll
+        for (int i = 0; i < O; ++i) {
+            S[i] = nS[i];
+            slot[i] = nS[i];
+        }
+    }
+}
+
+// out[t] = sum_g partial[g][t]
+__global__ __launch_bounds__(256) void fb_reduce_kernel(const double* __restrict__ partial, long n_pad,
+                                                        int G, long n, double* __restrict__ out) {
+    __shared__ double red[4][64];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const long t = (long)blockIdx.x * 64 + tx;
+    double s = 0.0;
+    if (t < n)
+        for (int g = ty; g < G; g += 4) s += partial[(long)g * n_pad + t];
+    red[ty][tx] = s;
+    __syncthreads();
+    if (ty == 0 && t < n) out[t] = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+}
+
+// ---------------------------------------------------------------------------
+// host-side precompute of a band record (long double)
+// ---------------------------------------------------------------------------
+template <int O>
+void build_record(const double* b, const double* av, double* rec) {
+    using R = Rec<O>;
+    std::memset(rec, 0, sizeof(double) * R::SIZE);
+    for (int i = 0; i <= O; ++i) rec[R::B + i] = b[i];
+    if constexpr (O > 0) {
+        for (int k = 0; k < O; ++k) rec[R::A + k] = av[k];
+        long double h[O][kL];
+        for (int k = 0; k < O; ++k) {
+            long double yh[O];
+            for (int q = 0; q < O; ++q) yh[q] = (q == k) ? 1.0L : 0.0L;
+            for (int j = 0; j < kL; ++j) {
+                long double y = 0;
+                for (int q = 0; q < O; ++q) y -= (long double)av[q] * yh[q];
+                for (int q = O - 1; q > 0; --q) yh[q] = yh[q - 1];
+                yh[0] = y;
+                h[k][j] = y;
+                rec[R::H + k * kL + j] = (double)y;
+            }
+        }
+        long double M[O][O], T[O][O];
+        for (int rr = 0; rr < O; ++rr)
+            for (int c = 0; c < O; ++c) M[rr][c] = h[c][kL - 1 - rr];
+        for (int s = 0; s < 6; ++s) {
+            for (int rr = 0; rr < O; ++rr)
+                for (int c = 0; c < O; ++c) rec[R::P + s * O * O + rr * O + c] = (double)M[rr][c];
+            for (int rr = 0; rr < O; ++rr)
+                for (int c = 0; c < O; ++c) {
+                    long double acc = 0;
+                    for (int q = 0; q < O; ++q) acc += M[rr][q] * M[q][c];
+                    T[rr][c] = acc;
+                }
+            std::memcpy(M, T, sizeof(M));
+        }
+    }
+}
+
+static void build_record_any(int O, const double* b, const double* a, double* rec) {
+    switch (O) {
+    case 0: build_record<0>(b, a, rec); break;
+    case 1: build_record<1>(b, a, rec); break;
+    case 2: build_record<2>(b, a, rec); break;
+    case 3: build_record<3>(b, a, rec); break;
+    default: build_record<4>(b, a, rec); break;
+    }
+}
+
+typedef void (*MixKernel)(MixArgs);
+typedef void (*CarryKernel)(const double*, const double*, double*, int, int, long);
+
+template <int O, int NB>
+MixKernel pick_dist(int dist, int mode) {
+    if (mode == MODE_SEGEND) return fb_mix_kernel<O, HZ_DIST_NONE, NB, MODE_SEGEND>;
+    switch (dist) {
+    case HZ_DIST_SOFTCLIP: return fb_mix_kernel<O, HZ_DIST_SOFTCLIP, NB, MODE_MIX>;
+    case HZ_DIST_SATURATE: return fb_mix_kernel<O, HZ_DIST_SATURATE, NB, MODE_MIX>;
+    case HZ_DIST_LIMITER: return fb_mix_kernel<O, HZ_DIST_LIMITER, NB, MODE_MIX>;
+    default: return fb_mix_kernel<O, HZ_DIST_NONE, NB, MODE_MIX>;
+    }
+}
+
+template <int NB>
+MixKernel pick_order(int O, int dist, int mode) {
+    switch (O) {
+    case 0: return pick_dist<0, NB>(dist, mode);
+    case 1: return pick_dist<1, NB>(dist, mode);
+    case 2: return pick_dist<2, NB>(dist, mode);
+    case 3: return pick_dist<3, NB>(dist, mode);
+    default: return pick_dist<4, NB>(dist, mode);
+    }
+}
+
+static MixKernel pick_kernel(int O, int dist, int nb, int mode) {
+    switch (nb) {
+    case 2: return pick_order<2>(O, dist, mode);
+    case 4: return pick_order<4>(O, dist, mode);
+    default: return pick_order<1>(O, dist, mode);
+    }
+}
+
+static CarryKernel pick_carry(int O) {
+    switch (O) {
+    case 1: return fb_seg_carry_kernel<1>;
+    case 2: return fb_seg_carry_kernel<2>;
+    case 3: return fb_seg_carry_kernel<3>;
+    default: return fb_seg_carry_kernel<4>;
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// handle
+// ---------------------------------------------------------------------------
+struct hz_fb {
+    int order = 2, N = 0, N_total = 0, band_begin = 0, device = 0;
+    double sp = 0, sg = 0;
+    int rec = 8;
+    // host shadows of the staged parameters
+    std::vector<double> F, B, pin, gin;
+    bool dirty_coef = true, dirty_pin = true, dirty_gin = true;
+    int dist_id = HZ_DIST_NONE;
+    double dist_param = 0;
+    // geometry
+    int waves = 16, bands_per_wave = 1;
+    // device buffers
+    double *d_rec = nullptr, *d_pin = nullptr, *d_gin = nullptr, *d_ystate = nullptr, *d_pg = nullptr;
+    double* d_xhist[2] = {nullptr, nullptr};
+    int xcur = 0;
+    double* d_partial = nullptr;
+    size_t partial_cap = 0;  // doubles
+    double* d_seg = nullptr;  // segment start states
+    size_t seg_cap = 0;
+    int target_groups = 256;  // workgroups wanted per launch (CU count)
+    double *d_in = nullptr, *d_out = nullptr;
+    size_t io_cap = 0;       // doubles
+    std::vector<double> h_rec;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    // profiling
+    bool prof = false;
+    std::vector<hipEvent_t> ev;  // quadruplets
+    size_t ev_used = 0;
+    long prof_launches = 0;
+};
+
+namespace {
+
+int fb_groups(const hz_fb* h) {
+    const int per = h->waves * h->bands_per_wave;
+    return (h->N + per - 1) / per;
+}
+
+int fb_upload(hz_fb* h) {
+    if (h->dirty_coef) {
+        const int O = h->order;
+        h->h_rec.assign((size_t)h->N * h->rec, 0.0);
+        for (int n = 0; n < h->N; ++n)
+            build_record_any(O, &h->F[(size_t)n * (O + 1)], O > 0 ? &h->B[(size_t)n * O] : nullptr,
+                             &h->h_rec[(size_t)n * h->rec]);
+        HZ_TRY_HIP(hipMemcpyAsync(h->d_rec, h->h_rec.data(), sizeof(double) * h->h_rec.size(),
+                                  hipMemcpyHostToDevice, h->stream));
+        h->dirty_coef = false;
+    }
+    if (h->dirty_pin) {
+        HZ_TRY_HIP(hipMemcpyAsync(h->d_pin, h->pin.data(), sizeof(double) * h->N, hipMemcpyHostToDevice,
+                                  h->stream));
+        h->dirty_pin = false;
+    }
+    if (h->dirty_gin) {
+        HZ_TRY_HIP(hipMemcpyAsync(h->d_gin, h->gin.data(), sizeof(double) * h->N, hipMemcpyHostToDevice,
+                                  h->stream));
+        h->dirty_gin = false;
+    }
+    // the uploads read pageable host vectors that setters may change next: make them complete
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+// chunk bound so the partial slab stays <= ~1 GiB
+long fb_max_chunk(const hz_fb* h) {
+    const long G = fb_groups(h);
+    long c = (1L << 27) / std::max(1L, G);  // doubles per row
+    c = std::max<long>(kTile, (c / kTile) * kTile);
+    return c;
+}
+
+int fb_set_lds_attr(MixKernel k) {
+    static thread_local std::vector<const void*> done;
+    if (std::find(done.begin(), done.end(), (const void*)k) != done.end()) return HZ_OK;
+    HZ_TRY_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    done.push_back((const void*)k);
+    return HZ_OK;
+}
+
+int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
+    if (n <= 0) return HZ_OK;
+    const int G = fb_groups(h);
+    const int O = h->order;
+    const long chunk = fb_max_chunk(h);
+    const long n_pad_max = std::min<long>(((n + kTile - 1) / kTile) * kTile, chunk);
+    const size_t need = (size_t)G * n_pad_max;
+    if (need > h->partial_cap) {
+        if (h->d_partial) HZ_TRY_HIP(hipFree(h->d_partial));
+        h->d_partial = nullptr;
+        HZ_TRY_HIP(hipMalloc(&h->d_partial, sizeof(double) * need));
+        h->partial_cap = need;
+    }
+    MixKernel kmix = pick_kernel(O, h->dist_id, h->bands_per_wave, MODE_MIX);
+    MixKernel kend = pick_kernel(O, h->dist_id, h->bands_per_wave, MODE_SEGEND);
+    HZ_TRY(fb_set_lds_attr(kmix));
+    const size_t lds = sizeof(double) * (size_t)h->waves * kL * 65;
+    for (long off = 0; off < n; off += chunk) {
+        const long len = std::min(chunk, n - off);
+        const long ntiles = (len + kTile - 1) / kTile;
+        // time segments: enough workgroups to cover every CU at least once
+        long nseg = std::max<long>(1, std::min<long>(ntiles, (h->target_groups + G - 1) / G));
+        const long seg_tiles = (ntiles + nseg - 1) / nseg;
+        nseg = (ntiles + seg_tiles - 1) / seg_tiles;
+        if (nseg > 1 && O > 0) {
+            const size_t sneed = (size_t)h->N * nseg * O;
+            if (sneed > h->seg_cap) {
+                if (h->d_seg) HZ_TRY_HIP(hipFree(h->d_seg));
+                h->d_seg = nullptr;
+                HZ_TRY_HIP(hipMalloc(&h->d_seg, sizeof(double) * sneed));
+                h->seg_cap = sneed;
+            }
+        }
+        MixArgs a;
+        a.rec = h->d_rec;
+        a.pin = h->d_pin;
+        a.gin = h->d_gin;
+        a.ystate = h->d_ystate;
+        a.pgstate = h->d_pg;
+        a.x = d_in + off;
+        a.xhist = h->d_xhist[h->xcur];
+        a.xhist_next = h->d_xhist[h->xcur ^ 1];
+        a.partial = h->d_partial;
+        a.segstate = h->d_seg;
+        a.n = len;
+        a.n_pad = ntiles * kTile;
+        a.seg_len = seg_tiles * kTile;
+        a.nseg = (int)nseg;
+        a.nbands = h->N;
+        a.sp = h->sp;
+        a.sg = h->sg;
+        a.sp_tile = (double)powl((long double)h->sp, (long double)kTile);
+        a.sg_tile = (double)powl((long double)h->sg, (long double)kTile);
+        a.sp_n = (double)powl((long double)h->sp, (long double)len);
+        a.sg_n = (double)powl((long double)h->sg, (long double)len);
+        a.dist_param = h->dist_param;
+        hipEvent_t* e = nullptr;
+        if (h->prof) {
+            if (h->ev_used + 4 > h->ev.size()) {
+                for (int q = 0; q < 4 * 64; ++q) {
+                    hipEvent_t ne;
+                    HZ_TRY_HIP(hipEventCreate(&ne));
+                    h->ev.push_back(ne);
+                }
+            }
+            e = &h->ev[h->ev_used];
+            h->ev_used += 4;
+            HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
+        }
+        if (nseg > 1 && O > 0) {
+            // segment end states (zero-state), then the per-band carry over segments
+            hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg - 1)), dim3(64 * h->waves), 0, h->stream, a);
+            HZ_TRY_HIP(hipGetLastError());
+            hipLaunchKernelGGL(pick_carry(O), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0, h->stream,
+                               (const double*)h->d_rec, (const double*)h->d_ystate, h->d_seg, h->N, (int)nseg,
+                               seg_tiles);
+            HZ_TRY_HIP(hipGetLastError());
+        }
+        if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
+        hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * h->waves), lds, h->stream, a);
+        HZ_TRY_HIP(hipGetLastError());
+        if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
+        hipLaunchKernelGGL(fb_reduce_kernel, dim3((unsigned)((len + 63) / 64)), dim3(256), 0, h->stream,
+                           (const double*)h->d_partial, a.n_pad, G, len, d_out + off);
+        HZ_TRY_HIP(hipGetLastError());
+        if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
+        h->xcur ^= 1;
+        h->prof_launches += h->prof ? 1 : 0;
+    }
+    return HZ_OK;
+}
+
+int fb_check(hz_fb* h) {
+    if (!h) {
+        hz::set_error("null hz_fb handle");
+        return HZ_E_INVALID;
+    }
+    HZ_TRY_HIP(hipSetDevice(h->device));
+    return HZ_OK;
+}
+
+// global band index -> local, or -1 when outside this shard
+int fb_local(const hz_fb* h, int n) {
+    if (n < h->band_begin || n >= h->band_begin + h->N) return -1;
+    return n - h->band_begin;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hz_fb_create_shard(int order, int N_total, int band_begin, int band_count, double k_p, double k_g,
+                       int device, hz_fb** out) {
+    if (!out || order < 0 || order > kMaxOrder || N_total <= 0 || band_begin < 0 || band_count <= 0 ||
+        band_begin + band_count > N_total) {
+        hz::set_error("hz_fb_create: invalid arguments (order %d, N %d, shard [%d,+%d))", order, N_total,
+                      band_begin, band_count);
+        return HZ_E_INVALID;
+    }
+    *out = nullptr;
+    HZ_TRY(hz::select_device(device));
+    hz_fb* h = new (std::nothrow) hz_fb();
+    if (!h) return HZ_E_ALLOC;
+    h->order = order;
+    h->N = band_count;
+    h->N_total = N_total;
+    h->band_begin = band_begin;
+    h->device = device;
+    h->sp = hz::relaxation(k_p);
+    h->sg = hz::relaxation(k_g);
+    h->rec = rec_size(order);
+    const size_t N = band_count;
+    h->F.assign(N * (order + 1), 0.0);
+    h->B.assign(N * std::max(order, 1), 0.0);
+    h->pin.assign(N, 0.0);
+    h->gin.assign(N, 0.0);
+    // default geometry: 16 waves x 1 band; fewer waves when the bank is small
+    h->waves = 16;
+    h->bands_per_wave = 1;
+    while (h->waves > 1 && (long)fb_groups(h) * h->waves < 1024 && h->waves * 2 > band_count) h->waves /= 2;
+    auto fail = [&](int code) {
+        hz_fb_destroy(h);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        hz::set_error("hipStreamCreate failed");
+        return fail(HZ_E_HIP);
+    }
+    h->own_stream = true;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            h->target_groups = prop.multiProcessorCount;
+    }
+    const int O = std::max(order, 1);
+    if (hipMalloc(&h->d_rec, sizeof(double) * N * h->rec) != hipSuccess ||
+        hipMalloc(&h->d_pin, sizeof(double) * N) != hipSuccess ||
+        hipMalloc(&h->d_gin, sizeof(double) * N) != hipSuccess ||
+        hipMalloc(&h->d_ystate, sizeof(double) * N * O) != hipSuccess ||
+        hipMalloc(&h->d_pg, sizeof(double) * N * 2) != hipSuccess ||
+        hipMalloc(&h->d_xhist[0], sizeof(double) * O) != hipSuccess ||
+        hipMalloc(&h->d_xhist[1], sizeof(double) * O) != hipSuccess) {
+        hz::set_error("hipMalloc failed for filterbank state (%zu bands)", N);
+        return fail(HZ_E_ALLOC);
+    }
+    if (hipMemsetAsync(h->d_ystate, 0, sizeof(double) * N * O, h->stream) != hipSuccess ||
+        hipMemsetAsync(h->d_pg, 0, sizeof(double) * N * 2, h->stream) != hipSuccess ||
+        hipMemsetAsync(h->d_xhist[0], 0, sizeof(double) * O, h->stream) != hipSuccess ||
+        hipMemsetAsync(h->d_xhist[1], 0, sizeof(double) * O, h->stream) != hipSuccess ||
+        hipStreamSynchronize(h->stream) != hipSuccess) {
+        hz::set_error("hipMemset failed for filterbank state");
+        return fail(HZ_E_HIP);
+    }
+    *out = h;
+    return HZ_OK;
+}
+
+int hz_fb_create(int order, int N, double k_p, double k_g, int device, hz_fb** out) {
+    return hz_fb_create_shard(order, N, 0, N, k_p, k_g, device, out);
+}
+
+int hz_fb_destroy(hz_fb* h) {
+    if (!h) return HZ_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (double* p : {h->d_rec, h->d_pin, h->d_gin, h->d_ystate, h->d_pg, h->d_xhist[0], h->d_xhist[1],
+                      h->d_partial, h->d_seg, h->d_in, h->d_out})
+        if (p) (void)hipFree(p);
+    for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return HZ_OK;
+}
+
+int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double* back, int nb) {
+    if (!h || (nf > 0 && !fwd) || (nb > 0 && !back) || nf < 0 || nb < 0) {
+        hz::set_error("hz_fb_coefficients: invalid arguments");
+        return HZ_E_INVALID;
+    }
+    if (n < 0 || n >= h->N_total) {
+        hz::set_error("hz_fb_coefficients: band %d out of range [0,%d)", n, h->N_total);
+        return HZ_E_RANGE;
+    }
+    const int l = fb_local(h, n);
+    if (l < 0) return HZ_OK;
+    const int O = h->order;
+    for (int i = 0; i < std::min(O + 1, nf); ++i) h->F[(size_t)l * (O + 1) + i] = fwd[i];
+    for (int i = 0; i < std::min(O, nb); ++i) h->B[(size_t)l * O + i] = back[i];
+    h->dirty_coef = true;
+    return HZ_OK;
+}
+
+int hz_fb_boost(hz_fb* h, int n, double v) {
+    if (!h) return HZ_E_INVALID;
+    if (n < 0 || n >= h->N_total) {
+        hz::set_error("hz_fb_boost: band %d out of range [0,%d)", n, h->N_total);
+        return HZ_E_RANGE;
+    }
+    const int l = fb_local(h, n);
+    if (l >= 0) {
+        h->pin[l] = v;
+        h->dirty_pin = true;
+    }
+    return HZ_OK;
+}
+
+int hz_fb_boost_all(hz_fb* h, const double* v, int count) {
+    if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
+    for (int i = 0; i < std::min(h->N_total, count); ++i) {
+        const int l = fb_local(h, i);
+        if (l >= 0) h->pin[l] = v[i];
+    }
+    h->dirty_pin = true;
+    return HZ_OK;
+}
+
+int hz_fb_mix(hz_fb* h, int n, double v) {
+    if (!h) return HZ_E_INVALID;
+    if (n < 0 || n >= h->N_total) {
+        hz::set_error("hz_fb_mix: band %d out of range [0,%d)", n, h->N_total);
+        return HZ_E_RANGE;
+    }
+    const int l = fb_local(h, n);
+    if (l >= 0) {
+        h->gin[l] = v;
+        h->dirty_gin = true;
+    }
+    return HZ_OK;
+}
+
+int hz_fb_mix_all(hz_fb* h, const double* v, int count) {
+    if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
+    for (int i = 0; i < std::min(h->N_total, count); ++i) {
+        const int l = fb_local(h, i);
+        if (l >= 0) h->gin[l] = v[i];
+    }
+    h->dirty_gin = true;
+    return HZ_OK;
+}
+
+int hz_fb_open(hz_fb* h) {
+    if (!h) return HZ_E_INVALID;
+    std::fill(h->gin.begin(), h->gin.end(), 1.0);
+    h->dirty_gin = true;
+    return HZ_OK;
+}
+
+int hz_fb_set_distortion(hz_fb* h, int dist_id, double param) {
+    if (!h || dist_id < HZ_DIST_NONE || dist_id > HZ_DIST_LIMITER) {
+        hz::set_error("hz_fb_set_distortion: unknown functor %d", dist_id);
+        return HZ_E_INVALID;
+    }
+    h->dist_id = dist_id;
+    h->dist_param = param;
+    return HZ_OK;
+}
+
+int hz_fb_process_device(hz_fb* h, const double* d_in, double* d_out, size_t n) {
+    HZ_TRY(fb_check(h));
+    if (n == 0) return HZ_OK;
+    if (!d_in || !d_out) {
+        hz::set_error("hz_fb_process_device: null buffer");
+        return HZ_E_INVALID;
+    }
+    HZ_TRY(fb_upload(h));
+    return fb_launch(h, d_in, d_out, (long)n);
+}
+
+int hz_fb_process(hz_fb* h, const double* in, double* out, size_t n) {
+    HZ_TRY(fb_check(h));
+    if (n == 0) return HZ_OK;
+    if (!in || !out) {
+        hz::set_error("hz_fb_process: null buffer");
+        return HZ_E_INVALID;
+    }
+    if (n > h->io_cap) {
+        if (h->d_in) HZ_TRY_HIP(hipFree(h->d_in));
+        if (h->d_out) HZ_TRY_HIP(hipFree(h->d_out));
+        h->d_in = h->d_out = nullptr;
+        HZ_TRY_HIP(hipMalloc(&h->d_in, sizeof(double) * n));
+        HZ_TRY_HIP(hipMalloc(&h->d_out, sizeof(double) * n));
+        h->io_cap = n;
+    }
+    HZ_TRY(fb_upload(h));
+    HZ_TRY_HIP(hipMemcpyAsync(h->d_in, in, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
+    HZ_TRY(fb_launch(h, h->d_in, h->d_out, (long)n));
+    HZ_TRY_HIP(hipMemcpyAsync(out, h->d_out, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+int hz_fb_set_stream(hz_fb* h, void* s) {
+    HZ_TRY(fb_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    if (h->own_stream) HZ_TRY_HIP(hipStreamDestroy(h->stream));
+    if (s) {
+        h->stream = (hipStream_t)s;
+        h->own_stream = false;
+    } else {
+        HZ_TRY_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        h->own_stream = true;
+    }
+    return HZ_OK;
+}
+
+int hz_fb_get_stream(hz_fb* h, void** s) {
+    if (!h || !s) return HZ_E_INVALID;
+    *s = (void*)h->stream;
+    return HZ_OK;
+}
+
+int hz_fb_synchronize(hz_fb* h) {
+    HZ_TRY(fb_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+int hz_fb_state_size(hz_fb* h, size_t* count) {
+    if (!h || !count) return HZ_E_INVALID;
+    *count = (size_t)h->order + (size_t)h->N * h->order + (size_t)h->N * 2;
+    return HZ_OK;
+}
+
+int hz_fb_get_state(hz_fb* h, double* buf, size_t count) {
+    HZ_TRY(fb_check(h));
+    size_t need;
+    hz_fb_state_size(h, &need);
+    if (!buf || count < need) return HZ_E_INVALID;
+    const size_t O = h->order, N = h->N;
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    if (O) {
+        HZ_TRY_HIP(hipMemcpy(buf, h->d_xhist[h->xcur], sizeof(double) * O, hipMemcpyDeviceToHost));
+        HZ_TRY_HIP(hipMemcpy(buf + O, h->d_ystate, sizeof(double) * N * O, hipMemcpyDeviceToHost));
+    }
+    HZ_TRY_HIP(hipMemcpy(buf + O + N * O, h->d_pg, sizeof(double) * N * 2, hipMemcpyDeviceToHost));
+    return HZ_OK;
+}
+
+int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
+    HZ_TRY(fb_check(h));
+    size_t need;
+    hz_fb_state_size(h, &need);
+    if (!buf || count < need) return HZ_E_INVALID;
+    const size_t O = h->order, N = h->N;
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    if (O) {
+        HZ_TRY_HIP(hipMemcpy(h->d_xhist[h->xcur], buf, sizeof(double) * O, hipMemcpyHostToDevice));
+        HZ_TRY_HIP(hipMemcpy(h->d_ystate, buf + O, sizeof(double) * N * O, hipMemcpyHostToDevice));
+    }
+    HZ_TRY_HIP(hipMemcpy(h->d_pg, buf + O + N * O, sizeof(double) * N * 2, hipMemcpyHostToDevice));
+    return HZ_OK;
+}
+
+int hz_fb_info(hz_fb* h, int* order, int* N_local, int* band_begin, int* N_total) {
+    if (!h) return HZ_E_INVALID;
+    if (order) *order = h->order;
+    if (N_local) *N_local = h->N;
+    if (band_begin) *band_begin = h->band_begin;
+    if (N_total) *N_total = h->N_total;
+    return HZ_OK;
+}
+
+int hz_fb_tune(hz_fb* h, int waves_per_group, int bands_per_wave) {
+    if (!h) return HZ_E_INVALID;
+    if (waves_per_group < 0 || waves_per_group > 16 ||
+        !(bands_per_wave == 0 || bands_per_wave == 1 || bands_per_wave == 2 || bands_per_wave == 4)) {
+        hz::set_error("hz_fb_tune: waves in [1,16], bands per wave in {1,2,4}");
+        return HZ_E_INVALID;
+    }
+    if (waves_per_group) h->waves = waves_per_group;
+    if (bands_per_wave) h->bands_per_wave = bands_per_wave;
+    return HZ_OK;
+}
+
+int hz_fb_set_target_groups(hz_fb* h, int groups) {
+    if (!h || groups < 1) return HZ_E_INVALID;
+    h->target_groups = groups;
+    return HZ_OK;
+}
+
+int hz_fb_profile(hz_fb* h, int enable) {
+    HZ_TRY(fb_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    h->prof = enable != 0;
+    h->ev_used = 0;
+    h->prof_launches = 0;
+    return HZ_OK;
+}
+
+int hz_fb_profile_read(hz_fb* h, double* segment_ms, double* mix_ms, double* reduce_ms, long* launches) {
+    HZ_TRY(fb_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    double sg = 0, m = 0, r = 0;
+    for (size_t i = 0; i + 4 <= h->ev_used; i += 4) {
+        float a = 0, b = 0, c = 0;
+        HZ_TRY_HIP(hipEventElapsedTime(&a, h->ev[i], h->ev[i + 1]));
+        HZ_TRY_HIP(hipEventElapsedTime(&b, h->ev[i + 1], h->ev[i + 2]));
+        HZ_TRY_HIP(hipEventElapsedTime(&c, h->ev[i + 2], h->ev[i + 3]));
+        sg += a;
+        m += b;
+        r += c;
+    }
+    if (segment_ms) *segment_ms = sg;
+    if (mix_ms) *mix_ms = m;
+    if (reduce_ms) *reduce_ms = r;
+    if (launches) *launches = h->prof_launches;
+    return HZ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,144 @@
+"""Filterbank<double> over the HIP engine.
+
+Mirrors soundmath::Filterbank<T> (src/filterbank.h:16-188): the same
+constructor arguments, setters and operator()/tick() pair, plus the block
+method process(x) == n x {y[i] = F(x[i]); F.tick();} that runs on the GPU.
+The C++ drop-in is include/soundmath/filterbank.h; this Python mirror exists
+for tests and bench.py.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import HZ_DIST_NONE, check, dptr, load
+
+
+class Filterbank:
+    """Filterbank(order, N=1, k_p=0.1, k_g=1) -- src/filterbank.h:36-70.
+
+    shard=(band_begin, band_count) makes this object own only those bands of an
+    N-band bank (one process per GPU, partial mixes summed over RCCL)."""
+
+    def __init__(self, order: int, N: int = 1, k_p: float = 0.1, k_g: float = 1.0,
+                 device: int = 0, shard: tuple[int, int] | None = None):
+        lib = load()
+        h = C.c_void_p()
+        if shard is None:
+            check(lib.hz_fb_create(order, N, k_p, k_g, device, C.byref(h)))
+        else:
+            check(lib.hz_fb_create_shard(order, N, shard[0], shard[1], k_p, k_g, device, C.byref(h)))
+        self._h = h
+        self._lib = lib
+        self.order = order
+        self.N = N
+        self.shard = shard
+        self._dist = (HZ_DIST_NONE, 0.0)
+        self._computed = False
+        self._cached = 0.0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.hz_fb_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- setters (filterbank.h:73-116) ------------------------------------
+    def coefficients(self, n: int, forward, back):
+        f = np.ascontiguousarray(forward, dtype=np.float64)
+        b = np.ascontiguousarray(back, dtype=np.float64)
+        check(self._lib.hz_fb_coefficients(self._h, n, dptr(f), len(f), dptr(b), len(b)))
+
+    def boost(self, n_or_values, value: float | None = None):
+        if value is None:
+            v = np.ascontiguousarray(n_or_values, dtype=np.float64)
+            check(self._lib.hz_fb_boost_all(self._h, dptr(v), len(v)))
+        else:
+            check(self._lib.hz_fb_boost(self._h, int(n_or_values), float(value)))
+
+    def mix(self, n_or_values, value: float | None = None):
+        if value is None:
+            v = np.ascontiguousarray(n_or_values, dtype=np.float64)
+            check(self._lib.hz_fb_mix_all(self._h, dptr(v), len(v)))
+        else:
+            check(self._lib.hz_fb_mix(self._h, int(n_or_values), float(value)))
+
+    def open(self):
+        check(self._lib.hz_fb_open(self._h))
+
+    def distortion(self, dist_id: int, param: float = 0.0):
+        """Select the per-band T(*)(T) of operator()(T, T(*)(T)) (filterbank.h:133)."""
+        check(self._lib.hz_fb_set_distortion(self._h, dist_id, param))
+        self._dist = (dist_id, param)
+
+    def tune(self, waves: int = 0, bands_per_wave: int = 0):
+        check(self._lib.hz_fb_tune(self._h, waves, bands_per_wave))
+
+    # ---- processing ----------------------------------------------------------
+    def process(self, x) -> np.ndarray:
+        """n x {out[i] = F(x[i]); F.tick();} on the GPU (host buffers)."""
+        xi = np.ascontiguousarray(x, dtype=np.float64)
+        out = np.empty_like(xi)
+        if len(xi):
+            check(self._lib.hz_fb_process(self._h, dptr(xi), dptr(out), len(xi)))
+        self._computed = False
+        return out
+
+    def process_device(self, x_ptr: int, out_ptr: int, n: int):
+        """Device pointers, asynchronous on the handle's stream."""
+        check(self._lib.hz_fb_process_device(self._h, C.c_void_p(x_ptr), C.c_void_p(out_ptr), n))
+
+    def __call__(self, sample: float) -> float:
+        """T operator()(T) (filterbank.h:125-131): cached until tick()."""
+        if not self._computed:
+            xi = np.array([sample], dtype=np.float64)
+            out = np.empty(1)
+            check(self._lib.hz_fb_process(self._h, dptr(xi), dptr(out), 1))
+            self._cached = float(out[0])
+            self._computed = True
+        return self._cached
+
+    def tick(self):
+        """tick() (filterbank.h:142-148); the GPU state advanced in operator()."""
+        self._computed = False
+
+    # ---- stream / state ------------------------------------------------------
+    def set_stream(self, stream_ptr: int | None):
+        check(self._lib.hz_fb_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
+
+    def stream(self) -> int:
+        s = C.c_void_p()
+        check(self._lib.hz_fb_get_stream(self._h, C.byref(s)))
+        return s.value or 0
+
+    def synchronize(self):
+        check(self._lib.hz_fb_synchronize(self._h))
+
+    def get_state(self) -> np.ndarray:
+        n = C.c_size_t()
+        check(self._lib.hz_fb_state_size(self._h, C.byref(n)))
+        buf = np.zeros(n.value)
+        check(self._lib.hz_fb_get_state(self._h, dptr(buf), n.value))
+        return buf
+
+    def set_state(self, buf):
+        b = np.ascontiguousarray(buf, dtype=np.float64)
+        check(self._lib.hz_fb_set_state(self._h, dptr(b), len(b)))
+
+    def profile(self, enable: bool):
+        check(self._lib.hz_fb_profile(self._h, 1 if enable else 0))
+
+    def profile_read(self):
+        """-> (segment pre-pass ms, mix kernel ms, reduce kernel ms, launches)"""
+        s, m, r, c = C.c_double(), C.c_double(), C.c_double(), C.c_long()
+        check(self._lib.hz_fb_profile_read(self._h, C.byref(s), C.byref(m), C.byref(r), C.byref(c)))
+        return s.value, m.value, r.value, c.value
+
+    def set_target_groups(self, groups: int):
+        check(self._lib.hz_fb_set_target_groups(self._h, groups))

@@ -1,0 +1,101 @@
+/*
+ * huygens_hip.h -- C ABI of libhuygens_hip.so, the MI355X (gfx950) bank engine.
+ *
+ * This is the drop-in boundary for the per-sample bank hot path of
+ * amcerbu/huygens (namespace soundmath, header-only C++17).  The reference has
+ * no .so and no plugin registry: its "operator API" is operator() + tick() +
+ * setters on class templates.  Each entry point below names the reference
+ * member it replaces (file:line under /root/reference).  The C++ wrappers in
+ * include/soundmath/ *.h restore the reference class names and signatures on
+ * top of this ABI.
+ *
+ * Conventions
+ *   - Opaque handles; every call returns int: HZ_OK (0) or a negative HZ_E_*.
+ *     The reference aborts through Eigen asserts on out-of-range indices
+ *     (tests/build.sh:8 builds without NDEBUG); this ABI never aborts and
+ *     reports HZ_E_RANGE instead.  hz_last_error() gives a per-thread message.
+ *   - Setters are staged on the host and applied at the next process call
+ *     boundary (block-granular; the reference mutates state from the MIDI
+ *     thread with no synchronisation, tests/filterbank.cpp:236-244).
+ *   - *_process() take HOST pointers and are synchronous (H2D, kernels, D2H).
+ *     *_process_device() take DEVICE pointers and are asynchronous on the
+ *     handle's HIP stream (hz_*_set_stream / hz_*_get_stream).
+ *   - No torch types; plain pointers and sizes only.
+ */
+#ifndef HUYGENS_HIP_H
+#define HUYGENS_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HZ_OK 0
+#define HZ_E_INVALID (-1) /* bad argument (null handle, n < 0, bad order ...) */
+#define HZ_E_RANGE (-2)   /* index out of range (reference: Eigen assert abort) */
+#define HZ_E_HIP (-3)     /* a HIP runtime call failed                        */
+#define HZ_E_NODEV (-4)   /* no gfx950 device visible                         */
+#define HZ_E_ALLOC (-5)   /* device or host allocation failed                 */
+#define HZ_E_UNSUPPORTED (-6)
+
+/* per-band distortion functors replacing T(*)(T) in
+ * Filterbank::operator()(T, T(*)(T)) (src/filterbank.h:133-139) */
+#define HZ_DIST_NONE 0
+#define HZ_DIST_SOFTCLIP 1 /* tests/filterbank.cpp:158-166, param = width      */
+#define HZ_DIST_SATURATE 2 /* tests/filterbank.cpp:173-176                     */
+#define HZ_DIST_LIMITER 3  /* src/wave.h:150 limiter, FUNCTIONAL: 2/PI atan(x) */
+
+/* ---- library ---------------------------------------------------------- */
+const char* hz_last_error(void);
+int hz_version(void);
+/* number of visible gfx950 devices (0 when none; never errors) */
+int hz_device_count(void);
+
+/* ---- Filterbank<double>  (src/filterbank.h:16-188) --------------------- */
+typedef struct hz_fb hz_fb;
+
+/* Filterbank(int order, int N, double k_p, double k_g)  filterbank.h:36-70.
+ * order in [0, 4]. */
+int hz_fb_create(int order, int N, double k_p, double k_g, int device, hz_fb** out);
+/* band shard [band_begin, band_begin + band_count) of an N_total-band bank,
+ * for one process per GPU (partial mixes are summed by the caller over RCCL);
+ * setters take GLOBAL band indices and ignore bands outside the shard. */
+int hz_fb_create_shard(int order, int N_total, int band_begin, int band_count, double k_p,
+                       double k_g, int device, hz_fb** out);
+int hz_fb_destroy(hz_fb* h);                                        /* ~Filterbank 23-33 */
+/* coefficients(int n, const vector<T>& fwd, const vector<T>& back)  73-82 */
+int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double* back, int nb);
+int hz_fb_boost(hz_fb* h, int n, double v);                         /* boost(int,T)   85-88 */
+int hz_fb_boost_all(hz_fb* h, const double* v, int count);          /* boost(vector)  91-96 */
+int hz_fb_mix(hz_fb* h, int n, double v);                           /* mix(int,T)     99-102 */
+int hz_fb_mix_all(hz_fb* h, const double* v, int count);            /* mix(vector)   105-110 */
+int hz_fb_open(hz_fb* h);                                           /* open()        112-116 */
+/* selects the T(*)(T) of operator()(T, T(*)(T)) for subsequent process calls */
+int hz_fb_set_distortion(hz_fb* h, int dist_id, double param);
+/* n x { out[i] = operator()(in[i]); tick(); }  (filterbank.h:125-148) */
+int hz_fb_process(hz_fb* h, const double* in, double* out, size_t n);
+int hz_fb_process_device(hz_fb* h, const double* d_in, double* d_out, size_t n);
+int hz_fb_set_stream(hz_fb* h, void* hip_stream);
+int hz_fb_get_stream(hz_fb* h, void** hip_stream);
+int hz_fb_synchronize(hz_fb* h);
+/* state = [x history (order)] [y history (N*order)] [pre,gain (N*2)] */
+int hz_fb_state_size(hz_fb* h, size_t* count);
+int hz_fb_get_state(hz_fb* h, double* buf, size_t count);
+int hz_fb_set_state(hz_fb* h, const double* buf, size_t count);
+int hz_fb_info(hz_fb* h, int* order, int* N_local, int* band_begin, int* N_total);
+/* kernel geometry: waves per workgroup (1..16), bands per wave (1,2,4); 0 = default */
+int hz_fb_tune(hz_fb* h, int waves_per_group, int bands_per_wave);
+/* HIP-event timing of the launches of subsequent process calls, on the handle's
+ * stream: total ms of the time-segment pre-pass (segment end states + carry;
+ * 0 when the bank fills the GPU with bands alone), of the IIR/mixdown kernel,
+ * of the cross-group reduce kernel, and the number of process launches. */
+int hz_fb_profile(hz_fb* h, int enable);
+int hz_fb_profile_read(hz_fb* h, double* segment_ms, double* mix_ms, double* reduce_ms, long* launches);
+/* workgroups wanted per launch before time segmentation kicks in (default: CU count) */
+int hz_fb_set_target_groups(hz_fb* h, int groups);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,175 @@
+/*
+ * hz_oracle.c -- TEST INFRASTRUCTURE ONLY.  See hz_oracle.h for the parity
+ * status.  Compiled with -O2 -ffp-contract=off so rounding is deterministic
+ * (no FMA contraction), see oracle/Makefile.
+ *
+ * Every function cites the reference file:line it restates.
+ */
+#include "hz_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* src/includes.h:30-32 */
+#define ORC_PI 3.14159265359
+#define ORC_E 2.718281828459045
+#define ORC_SR 48000
+
+/* src/includes.h:38-48 : order = log2(DBL_EPSILON) = -52 */
+double orc_relaxation(double k)
+{
+    if (k == 0) return 0;
+    return pow(2.0, log2(DBL_EPSILON) / (fmax(0, k) * ORC_SR));
+}
+
+/* src/includes.h:51-59 */
+double orc_mtof(double m) { return 440.0 * pow(2, (m - 69) / 12); }
+double orc_ftom(double f) { return 69 + log2(f / 440.0) * 12; }
+
+/* Distortion functors used through Filterbank::operator()(T, T(*)(T))
+ * (src/filterbank.h:133-139).  Shapes from tests/filterbank.cpp:158-176
+ * (softclip, saturate) and src/wave.h:150 (limiter, FUNCTIONAL lookup).
+ * abs() is taken as fabs (macOS libc++ semantics). */
+static int orc_sgn(double v) { return (0.0 < v) - (v < 0.0); }
+double orc_dist(int id, double v, double param)
+{
+    switch (id) {
+    case 0: return v;
+    case 1: { /* softclip(sample, width) tests/filterbank.cpp:158-166 */
+        double width = param;
+        if (fabs(v) < width) return v;
+        int sign = orc_sgn(v);
+        double gap = v - sign * width;
+        return sign * width + (1 - width) * 2.0 / ORC_PI * atan(ORC_PI * gap / (2 * (1 - width)));
+    }
+    case 2: /* saturate tests/filterbank.cpp:173-176 */
+        return 2.0 / ORC_PI * atan(2 * ORC_PI * v / 2.0);
+    case 3: /* limiter src/wave.h:150 */
+        return 2.0 / ORC_PI * atan(v);
+    default: return v;
+    }
+}
+
+/* ---- Filterbank<double>  src/filterbank.h:16-188 ---------------------- */
+struct orc_fb {
+    int order, N;
+    double sp, sg;          /* smoothing_p, smoothing_g (filterbank.h:36-37,165) */
+    double* F;              /* forwards  N x (O+1)  (filterbank.h:49)  F[n*(O+1)+i] */
+    double* Bk;             /* backs     N x O      (filterbank.h:50)  Bk[n*O+k]    */
+    double* xr;             /* input     2(O+1)     (filterbank.h:51)               */
+    double* Y;              /* outputs   2(O+1) x N (filterbank.h:52)  Y[r*N+n]     */
+    double *pin, *pout, *gin, *gout;
+    double* temp;
+    int origin, computed;
+};
+
+orc_fb* orc_fb_create(int order, int N, double k_p, double k_g)
+{
+    orc_fb* fb = (orc_fb*)calloc(1, sizeof(orc_fb));
+    int R = 2 * (order + 1);
+    fb->order = order;
+    fb->N = N;
+    fb->sp = orc_relaxation(k_p);
+    fb->sg = orc_relaxation(k_g);
+    fb->F = (double*)calloc((size_t)N * (order + 1), sizeof(double));
+    fb->Bk = (double*)calloc((size_t)N * (order > 0 ? order : 1), sizeof(double));
+    fb->xr = (double*)calloc(R, sizeof(double));
+    fb->Y = (double*)calloc((size_t)R * N, sizeof(double));
+    fb->pin = (double*)calloc(N, sizeof(double));
+    fb->pout = (double*)calloc(N, sizeof(double));
+    fb->gin = (double*)calloc(N, sizeof(double));
+    fb->gout = (double*)calloc(N, sizeof(double));
+    fb->temp = (double*)calloc(N, sizeof(double));
+    return fb;
+}
+
+void orc_fb_destroy(orc_fb* fb)
+{
+    if (!fb) return;
+    free(fb->F); free(fb->Bk); free(fb->xr); free(fb->Y);
+    free(fb->pin); free(fb->pout); free(fb->gin); free(fb->gout); free(fb->temp);
+    free(fb);
+}
+
+/* filterbank.h:73-82 */
+void orc_fb_coefficients(orc_fb* fb, int n, const double* fwd, int nf, const double* back, int nb)
+{
+    int O = fb->order;
+    int c = nf < O + 1 ? nf : O + 1;
+    for (int i = 0; i < c; i++) fb->F[(size_t)n * (O + 1) + i] = fwd[i];
+    c = nb < O ? nb : O;
+    for (int i = 0; i < c; i++) fb->Bk[(size_t)n * O + i] = back[i];
+}
+
+/* filterbank.h:85-116 */
+void orc_fb_boost(orc_fb* fb, int n, double v) { fb->pin[n] = v; }
+void orc_fb_boost_all(orc_fb* fb, const double* v, int count)
+{
+    for (int i = 0; i < (fb->N < count ? fb->N : count); i++) fb->pin[i] = v[i];
+}
+void orc_fb_mix(orc_fb* fb, int n, double v) { fb->gin[n] = v; }
+void orc_fb_mix_all(orc_fb* fb, const double* v, int count)
+{
+    for (int i = 0; i < (fb->N < count ? fb->N : count); i++) fb->gin[i] = v[i];
+}
+void orc_fb_open(orc_fb* fb)
+{
+    for (int i = 0; i < fb->N; i++) fb->gin[i] = 1;
+}
+
+/* compute(): filterbank.h:170-187 */
+static void orc_fb_compute(orc_fb* fb, double sample)
+{
+    const int O = fb->order, N = fb->N, o = fb->origin;
+    const double sp = fb->sp, sg = fb->sg;
+    for (int n = 0; n < N; n++) {                                   /* 172 */
+        fb->pout[n] = (1 - sp) * fb->pin[n] + sp * fb->pout[n];
+        fb->gout[n] = (1 - sg) * fb->gin[n] + sg * fb->gout[n];     /* 173 */
+    }
+    fb->xr[o] = sample;                                             /* 175 */
+    fb->xr[o + O + 1] = sample;                                     /* 176 */
+    for (int n = 0; n < N; n++) {                                   /* 178-179 */
+        const double* f = fb->F + (size_t)n * (O + 1);
+        double ff = f[0] * fb->xr[o];
+        for (int i = 1; i <= O; i++) ff += f[i] * fb->xr[o + i];
+        double bsum = 0;
+        const double* b = fb->Bk + (size_t)n * O;
+        for (int k = 0; k < O; k++) bsum += b[k] * fb->Y[(size_t)(o + 1 + k) * N + n];
+        fb->temp[n] = ff * fb->pout[n] - bsum;
+    }
+    memcpy(fb->Y + (size_t)o * N, fb->temp, sizeof(double) * N);           /* 183 */
+    memcpy(fb->Y + (size_t)(o + O + 1) * N, fb->temp, sizeof(double) * N); /* 184 */
+    fb->computed = 1;
+}
+
+/* operator(): filterbank.h:125-139 */
+double orc_fb_sample(orc_fb* fb, double x, int dist_id, double dist_param)
+{
+    if (!fb->computed) orc_fb_compute(fb, x);
+    const double* row = fb->Y + (size_t)fb->origin * fb->N;
+    double s = 0;
+    if (dist_id == 0)
+        for (int n = 0; n < fb->N; n++) s += row[n] * fb->gout[n];
+    else
+        for (int n = 0; n < fb->N; n++) s += orc_dist(dist_id, row[n] * fb->gout[n], dist_param);
+    return s;
+}
+
+/* tick(): filterbank.h:142-148 */
+void orc_fb_tick(orc_fb* fb)
+{
+    fb->origin--;
+    if (fb->origin < 0) fb->origin += fb->order + 1;
+    fb->computed = 0;
+}
+
+/* the demo block loop (tests/resynthesis.cpp:35-39) */
+void orc_fb_process(orc_fb* fb, const double* in, double* out, long n, int dist_id, double dist_param)
+{
+    for (long i = 0; i < n; i++) {
+        out[i] = orc_fb_sample(fb, in[i], dist_id, dist_param);
+        orc_fb_tick(fb);
+    }
+}

@@ -1,0 +1,52 @@
+/*
+ * hz_oracle.h -- TEST INFRASTRUCTURE ONLY (never linked into the product).
+ *
+ * Scalar C restatement of the amcerbu/huygens bank hot path, op for op, used
+ * as the parity checker for the HIP kernels in huygens_amd/csrc.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ *
+ * Parity status: the reference itself cannot be compiled in this image
+ * (Eigen >= 3.4, FFTW3, PortAudio and RtMidi headers are absent; see
+ * DESIGN.md "Oracle") and its tests hold no golden vectors.  This
+ * restatement is therefore pinned against (a) an independent numpy
+ * restatement that writes tests/golden/ fixtures, (b) scipy.signal.lfilter /
+ * numpy.fft / scipy.fft.dct known-answer checks of the third-party maths
+ * (Eigen GEMV, FFTW DFT/REDFT conventions), and (c) closed-form known
+ * answers.  Strictly, by the reference's own fixtures: parity unpinned.
+ *
+ * Constants follow /root/reference/src/includes.h:30-48 (truncated PI,
+ * integer SR, relaxation()).
+ */
+#ifndef HZ_ORACLE_H
+#define HZ_ORACLE_H
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+double orc_relaxation(double k);
+double orc_mtof(double m);
+double orc_ftom(double f);
+
+/* ---- Filterbank<double> (src/filterbank.h:16-188) ---------------------- */
+typedef struct orc_fb orc_fb;
+orc_fb* orc_fb_create(int order, int N, double k_p, double k_g);
+void    orc_fb_destroy(orc_fb* fb);
+void    orc_fb_coefficients(orc_fb* fb, int n, const double* fwd, int nf, const double* back, int nb);
+void    orc_fb_boost(orc_fb* fb, int n, double v);
+void    orc_fb_boost_all(orc_fb* fb, const double* v, int count);
+void    orc_fb_mix(orc_fb* fb, int n, double v);
+void    orc_fb_mix_all(orc_fb* fb, const double* v, int count);
+void    orc_fb_open(orc_fb* fb);
+double  orc_fb_sample(orc_fb* fb, double x, int dist_id, double dist_param);
+void    orc_fb_tick(orc_fb* fb);
+void    orc_fb_process(orc_fb* fb, const double* in, double* out, long n, int dist_id, double dist_param);
+
+/* distortion functors (tests/filterbank.cpp:158-176, src/wave.h:150) */
+double orc_dist(int id, double v, double param);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,152 @@
+"""ctypes binding of the CPU restatement oracle/hz_oracle.c (TEST INFRASTRUCTURE).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "oracle", "_build", "libhz_oracle.so")
+
+D, I, L, VP = C.c_double, C.c_int, C.c_long, C.c_void_p
+PD = C.POINTER(C.c_double)
+
+_SIGS = {
+    "orc_relaxation": (D, [D]),
+    "orc_mtof": (D, [D]),
+    "orc_ftom": (D, [D]),
+    "orc_dist": (D, [I, D, D]),
+    "orc_fb_create": (VP, [I, I, D, D]),
+    "orc_fb_destroy": (None, [VP]),
+    "orc_fb_coefficients": (None, [VP, I, PD, I, PD, I]),
+    "orc_fb_boost": (None, [VP, I, D]),
+    "orc_fb_boost_all": (None, [VP, PD, I]),
+    "orc_fb_mix": (None, [VP, I, D]),
+    "orc_fb_mix_all": (None, [VP, PD, I]),
+    "orc_fb_open": (None, [VP]),
+    "orc_fb_sample": (D, [VP, D, I, D]),
+    "orc_fb_tick": (None, [VP]),
+    "orc_fb_process": (None, [VP, PD, PD, L, I, D]),
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SO):
+            import subprocess
+            subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+        _lib = C.CDLL(SO)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(_lib, name)
+            fn.restype = res
+            fn.argtypes = args
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(PD)
+
+
+class OracleFilterbank:
+    """CPU restatement of Filterbank<double> (src/filterbank.h:16-188)."""
+
+    def __init__(self, order, N, k_p=0.1, k_g=1.0):
+        self.l = lib()
+        self.h = self.l.orc_fb_create(order, N, k_p, k_g)
+        self.order, self.N = order, N
+        self.dist = (0, 0.0)
+
+    def __del__(self):
+        try:
+            self.l.orc_fb_destroy(self.h)
+        except Exception:
+            pass
+
+    def coefficients(self, n, fwd, back):
+        f = np.ascontiguousarray(fwd, dtype=np.float64)
+        b = np.ascontiguousarray(back, dtype=np.float64)
+        self.l.orc_fb_coefficients(self.h, n, _p(f), len(f), _p(b), len(b))
+
+    def boost(self, n_or_values, value=None):
+        if value is None:
+            v = np.ascontiguousarray(n_or_values, dtype=np.float64)
+            self.l.orc_fb_boost_all(self.h, _p(v), len(v))
+        else:
+            self.l.orc_fb_boost(self.h, n_or_values, value)
+
+    def mix(self, n_or_values, value=None):
+        if value is None:
+            v = np.ascontiguousarray(n_or_values, dtype=np.float64)
+            self.l.orc_fb_mix_all(self.h, _p(v), len(v))
+        else:
+            self.l.orc_fb_mix(self.h, n_or_values, value)
+
+    def open(self):
+        self.l.orc_fb_open(self.h)
+
+    def distortion(self, dist_id, param=0.0):
+        self.dist = (dist_id, param)
+
+    def process(self, x):
+        xi = np.ascontiguousarray(x, dtype=np.float64)
+        out = np.empty_like(xi)
+        self.l.orc_fb_process(self.h, _p(xi), _p(out), len(xi), self.dist[0], self.dist[1])
+        return out
+
+
+def run_schedule(fb, x, sched_t, sched_kind, sched_band, sched_val, fwd=None, back=None):
+    """Drive a Filterbank-like object (oracle or GPU) through a golden fixture's
+    setter schedule, splitting process() calls at every change point."""
+    if fwd is not None:
+        for n in range(fwd.shape[0]):
+            fb.coefficients(n, fwd[n], back[n])
+    out = np.zeros(len(x))
+    pos = 0
+    events = sorted(zip(sched_t.tolist(), range(len(sched_t))))
+    N = fwd.shape[0] if fwd is not None else None
+    for t, idx in events + [(len(x), None)]:
+        if t > pos:
+            out[pos:t] = fb.process(x[pos:t])
+            pos = t
+        if idx is None:
+            break
+        kind = str(sched_kind[idx])
+        if kind == "boost_all":
+            fb.boost(np.ones(N))
+        elif kind == "mix_all":
+            fb.mix(np.ones(N))
+        elif kind == "open":
+            fb.open()
+        elif kind == "boost":
+            fb.boost(int(sched_band[idx]), float(sched_val[idx]))
+        elif kind == "mix":
+            fb.mix(int(sched_band[idx]), float(sched_val[idx]))
+    return out
+
+
+def load_golden(name):
+    path = os.path.join(ROOT, "tests", "golden", name + ".npz")
+    with np.load(path, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def golden_names(prefix):
+    d = os.path.join(ROOT, "tests", "golden")
+    return sorted(f[:-4] for f in os.listdir(d) if f.startswith(prefix) and f.endswith(".npz"))
+
+
+def rel_err(got, ref):
+    """norm-wise parity metric of SURVEY.md 8(d): ||got-ref||_inf / ||ref||_inf."""
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    den = np.max(np.abs(ref)) if ref.size else 0.0
+    if den == 0.0:
+        return float(np.max(np.abs(got))) if got.size else 0.0
+    return float(np.max(np.abs(got - ref)) / den)

@@ -1,0 +1,86 @@
+"""CPU tests: the oracle (C restatement) against the golden fixtures written by
+the independent numpy restatement (tests/golden/make_golden.py), plus the
+scipy/closed-form known answers.  No GPU needed."""
+import math
+
+import numpy as np
+import pytest
+from scipy import signal
+
+from oracle import OracleFilterbank, golden_names, lib, load_golden, rel_err, run_schedule
+from golden.spec_numpy import PI, SR, dist as spec_dist, relaxation as spec_relaxation
+
+
+def test_constants_and_relaxation():
+    L = lib()
+    for k in [0.0, 1e-4, 0.001, 0.1, 1.0, 2.0 / SR, 50.0, -1.0]:
+        if k < 0:
+            # fmax(0,k) = 0 -> division by zero -> 2^-inf = 0
+            assert L.orc_relaxation(k) == 0.0
+            continue
+        assert L.orc_relaxation(k) == spec_relaxation(k)
+    # relaxation(50) = 1 - 1.5e-5 (tests/filterbank.cpp:136)
+    assert abs(L.orc_relaxation(50) - (1 - 1.5e-5)) < 1e-6
+    assert abs(L.orc_mtof(69) - 440.0) < 1e-12
+    assert abs(L.orc_ftom(880.0) - 81.0) < 1e-12
+
+
+@pytest.mark.parametrize("dist_id,param", [(0, 0), (1, 0.125), (1, 0.5), (2, 0), (3, 0)])
+def test_distortions(dist_id, param):
+    L = lib()
+    v = np.linspace(-3, 3, 601)
+    got = np.array([L.orc_dist(dist_id, float(a), param) for a in v])
+    assert np.max(np.abs(got - spec_dist(dist_id, v, param))) < 1e-15
+
+
+@pytest.mark.parametrize("name", golden_names("fb_"))
+def test_filterbank_oracle_matches_golden(name):
+    g = load_golden(name)
+    fb = OracleFilterbank(int(g["order"]), int(g["N"]), float(g["kp"]), float(g["kg"]))
+    fb.distortion(int(g["dist"]), float(g["dist_param"]))
+    y = run_schedule(fb, g["x"], g["sched_t"], g["sched_kind"], g["sched_band"], g["sched_val"],
+                     g["fwd"], g["back"])
+    assert rel_err(y, g["y"]) < 1e-12
+
+
+def test_filterbank_oracle_lfilter_known_answer():
+    """k_p = k_g = 0: pre = gain = target immediately -> plain lfilter."""
+    rng = np.random.default_rng(11)
+    x = rng.uniform(-1, 1, 3000)
+    b = np.array([0.3, -0.2, 0.1])
+    a = np.array([-1.5, 0.7])
+    fb = OracleFilterbank(2, 1, 0.0, 0.0)
+    fb.coefficients(0, b, a)
+    fb.boost(0, 2.0)
+    fb.mix(0, 0.5)
+    y = fb.process(x)
+    ref = 0.5 * signal.lfilter(2.0 * b, np.concatenate(([1.0], a)), x)
+    assert rel_err(y, ref) < 1e-13
+
+
+def test_filterbank_oracle_silent_without_boost():
+    """resynthesis.cpp as written (no boost/mix/open) is silent."""
+    fb = OracleFilterbank(2, 4)
+    fb.coefficients(0, [1, 0, -1], [-1.9, 0.99])
+    y = fb.process(np.random.default_rng(0).uniform(-1, 1, 500))
+    assert np.all(y == 0.0)
+
+
+def test_filterbank_oracle_block_split_invariance():
+    g = load_golden("fb_o2_n16_r0999")
+    fb1 = OracleFilterbank(2, 16)
+    fb2 = OracleFilterbank(2, 16)
+    for fb in (fb1, fb2):
+        for n in range(16):
+            fb.coefficients(n, g["fwd"][n], g["back"][n])
+        fb.boost(np.ones(16))
+        fb.open()
+    x = g["x"]
+    y1 = fb1.process(x)
+    parts = []
+    pos = 0
+    for L in [1, 2, 3, 500, 1024, 7]:
+        parts.append(fb2.process(x[pos:pos + L]))
+        pos += L
+    parts.append(fb2.process(x[pos:]))
+    assert np.array_equal(y1, np.concatenate(parts))
