@@ -84,6 +84,14 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch-ROCm ships its own libamdhip64.so.7
+    # (same SONAME as /opt/rocm's).  Whichever loads first serves both, and
+    # torch refuses to initialise on top of the newer system runtime, so let
+    # torch (when installed) load first.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     if not os.path.exists(LIB_PATH):
         raise HZError(HZ_E_UNSUPPORTED, f"{LIB_PATH} not built (run `make lib` or __graft_entry__.build())")
     lib = C.CDLL(LIB_PATH)

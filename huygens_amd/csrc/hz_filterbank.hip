@@ -42,7 +42,8 @@ struct Rec {
     static constexpr int A = O + 1;              // a[0..O-1]         feedback
     static constexpr int H = 2 * O + 1;          // h[k][j] k<O j<16  homogeneous responses
     static constexpr int P = H + kL * O;         // P[s][r][c] s<6    (M16)^(2^s)
-    static constexpr int RAW = P + 6 * O * O;
+    static constexpr int Q = P + 6 * O * O;      // Q[p][r][c] p<16   (M16)^p
+    static constexpr int RAW = Q + kL * O * O;
     static constexpr int SIZE = (RAW + 7) & ~7;  // 64-B aligned records
 };
 
@@ -86,6 +87,38 @@ __device__ __forceinline__ double uniform(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// DPP lane moves on a double (two 32-bit halves).  bound_ctrl: lanes whose
+// source is outside the pattern read 0.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int kDppRowShr = 0x110;   // row_shr:n = 0x110 + n (within 16-lane rows)
+// (wave-wide DPP shifts / row_bcast do not exist on CDNA; cross-row moves use
+//  ds_bpermute or v_readlane)
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// LDS layout of one workgroup:
+//   xs   : the tile's input x[t0-16 .. t0+1023], padded one slot per 16 samples so
+//          lane c's reads (17c + k) hit 64 distinct banks (ds_read_b64)
+//   part : [W][16][65] per-wave partial mixes (65: conflict-free transposed reads)
+constexpr int kXsLen = 1040;                     // 16 halo + 1024
+constexpr int kXsPad = ((kXsLen + kXsLen / 16) + 1) & ~1;  // 1106 doubles (16-B multiple)
+constexpr int kPartWave = kL * 65;
+__host__ __device__ constexpr size_t lds_bytes(int waves, bool mix) {
+    return sizeof(double) * (kXsPad + (mix ? (size_t)waves * kPartWave : 0));
+}
+__device__ __forceinline__ int xs_pos(int li) { return li + (li >> 4); }
+
 // MODE_MIX: full pass (zero-state pass, carry scan, fix-up, mixdown) over one
 //   time segment (blockIdx.y) of one band group (blockIdx.x).
 // MODE_SEGEND: zero-state end state of each segment but the last (no mixdown),
@@ -96,7 +129,9 @@ enum { MODE_MIX = 0, MODE_SEGEND = 1 };
 template <int O, int DIST, int NB, int MODE>
 __global__ __launch_bounds__(1024) void fb_mix_kernel(MixArgs a) {
     using R = Rec<O>;
-    extern __shared__ __attribute__((aligned(16))) double lds[];  // [W][16][65]
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* xs = lds;
+    double* part = lds + kXsPad;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int W = blockDim.x >> 6;
@@ -104,10 +139,10 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(MixArgs a) {
     const long n = a.n;
     const int seg = blockIdx.y;
     const long seg_t0 = (long)seg * a.seg_len;
-    const long seg_n = min(a.seg_len, n - seg_t0);
-    const int ntiles = (int)((seg_n + kTile - 1) / kTile);
+    const long seg_end = min(seg_t0 + a.seg_len, n);
+    const int ntiles = (int)((seg_end - seg_t0 + kTile - 1) / kTile);
     const bool last_seg = seg == a.nseg - 1;
-    double* my = lds + (long)wave * (kL * 65);  // this wave's 1024-sample partial mix
+    double* my = part + (long)wave * kPartWave;
 
     // per-lane smoothing powers sp^(16 lane); the tile factor is wave-uniform
     const double sp_lane = pow(a.sp, (double)(kL * lane));
@@ -116,19 +151,23 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(MixArgs a) {
     double sg_t = seg_t0 ? uniform(pow(a.sg, (double)seg_t0)) : 1.0;
 
     // carried band state (wave-uniform)
+    bool live[NB];
     double S[NB][O > 0 ? O : 1];
-    double P0[NB], G0[NB];
+    double P0[NB], G0[NB], pin[NB], gin[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         const int band = band0 + b;
-        const bool ok = band < a.nbands;
+        live[b] = band < a.nbands;
+        const int bb = live[b] ? band : 0;
         const double* s0 = (MODE == MODE_SEGEND) ? nullptr
-                         : (seg == 0) ? a.ystate + (long)band * O
-                                      : a.segstate + ((long)band * a.nseg + seg) * O;
+                         : (seg == 0) ? a.ystate + (long)bb * O
+                                      : a.segstate + ((long)bb * a.nseg + seg) * O;
 #pragma unroll
-        for (int k = 0; k < O; ++k) S[b][k] = (ok && s0) ? s0[k] : 0.0;
-        P0[b] = ok ? a.pgstate[2 * (long)band] : 0.0;
-        G0[b] = ok ? a.pgstate[2 * (long)band + 1] : 0.0;
+        for (int k = 0; k < O; ++k) S[b][k] = (live[b] && s0) ? s0[k] : 0.0;
+        P0[b] = live[b] ? a.pgstate[2 * (long)bb] : 0.0;
+        G0[b] = live[b] ? a.pgstate[2 * (long)bb + 1] : 0.0;
+        pin[b] = live[b] ? a.pin[bb] : 0.0;
+        gin[b] = live[b] ? a.gin[bb] : 0.0;
     }
 
     for (int tile = 0; tile < ntiles; ++tile) {
@@ -136,142 +175,178 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(MixArgs a) {
         const long tc = t0 + (long)kL * lane;
         const bool last_tile = last_seg && tile == ntiles - 1;
 
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const int band = band0 + b;
-            if (band >= a.nbands) {  // wave-uniform: contribute nothing
-                if (MODE == MODE_MIX && b == 0) {
-#pragma unroll
-                    for (int j = 0; j < kL; ++j) my[j * 65 + lane] = 0.0;
-                }
-                break;
-            }
-            const double* r = a.rec + (long)band * R::SIZE;
-            const double pin = a.pin[band];
-            const double gin = a.gin[band];
+        // ---- stage the tile's input in LDS (coalesced, once per workgroup) -----
+        for (int li = threadIdx.x; li < kXsLen; li += blockDim.x) {
+            const long idx = t0 - 16 + li;
+            double v = 0.0;
+            if (idx < 0) v = (idx >= -O) ? a.xhist[-idx - 1] : 0.0;
+            else if (idx < seg_end) v = a.x[idx];
+            xs[xs_pos(li)] = v;
+        }
+        __syncthreads();
 
-            // ---- zero-state pass over the lane's 16 samples ----------------
-            double zsr[kL];
-            {
-                // input window x[tc-O .. tc+15]
-                double xv[kL + O];
+        // ---- zero-state pass over the lane's 16 samples, all NB bands ----------
+        double zsr[NB][kL];
+        {
+            double xw[O + 1];  // x[t], x[t-1], ... sliding window
 #pragma unroll
-                for (int k = 0; k < kL + O; ++k) {
-                    const long idx = tc - O + k;
-                    double v = 0.0;
-                    if (idx < 0) v = a.xhist[-idx - 1];
-                    else if (idx < seg_t0 + seg_n) v = a.x[idx];
-                    xv[k] = v;
-                }
-                double pre = pin + (sp_lane * sp_t) * (P0[b] - pin);
-                const double cp = (1.0 - a.sp) * pin;
-                double yh[O > 0 ? O : 1];
+            for (int k = 1; k <= O; ++k) xw[k] = xs[17 * lane + 16 - k];
+            double pre[NB];
+            double yh[NB][O > 0 ? O : 1];
 #pragma unroll
-                for (int k = 0; k < O; ++k) yh[k] = 0.0;
+            for (int b = 0; b < NB; ++b) {
+                pre[b] = pin[b] + (sp_lane * sp_t) * (P0[b] - pin[b]);
 #pragma unroll
-                for (int j = 0; j < kL; ++j) {
-                    pre = fma(a.sp, pre, cp);
-                    double ff = r[R::B] * xv[j + O];
-#pragma unroll
-                    for (int i = 1; i <= O; ++i) ff = fma(r[R::B + i], xv[j + O - i], ff);
-                    double y = ff * pre;
-#pragma unroll
-                    for (int k = 0; k < O; ++k) y = fma(-r[R::A + k], yh[k], y);
-#pragma unroll
-                    for (int k = O - 1; k > 0; --k) yh[k] = yh[k - 1];
-                    if constexpr (O > 0) yh[0] = y;
-                    zsr[j] = y;
-                }
+                for (int k = 0; k < O; ++k) yh[b][k] = 0.0;
             }
-
-            // ---- carry scan across the 64 chunks of the tile -----------------
-            double st[O > 0 ? O : 1];
-            if constexpr (O > 0) {
-                double z[O];
-#pragma unroll
-                for (int k = 0; k < O; ++k) z[k] = zsr[kL - 1 - k];
-                if (lane == 0) {
-#pragma unroll
-                    for (int rr = 0; rr < O; ++rr)
-#pragma unroll
-                        for (int c = 0; c < O; ++c) z[rr] = fma(r[R::P + rr * O + c], S[b][c], z[rr]);
-                }
-#pragma unroll
-                for (int s = 0; s < 6; ++s) {
-                    const int d = 1 << s;
-                    double nb[O];
-#pragma unroll
-                    for (int k = 0; k < O; ++k) nb[k] = __shfl_up(z[k], d, 64);
-                    if (lane >= d) {
-#pragma unroll
-                        for (int rr = 0; rr < O; ++rr)
-#pragma unroll
-                            for (int c = 0; c < O; ++c)
-                                z[rr] = fma(r[R::P + s * O * O + rr * O + c], nb[c], z[rr]);
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < O; ++k) {
-                    const double prev = __shfl_up(z[k], 1, 64);
-                    st[k] = (lane == 0) ? S[b][k] : prev;
-                }
-                // end state of the tile = lane 63 (the padded tail of a ragged last
-                // tile only matters after the final sample, where it is unused)
-#pragma unroll
-                for (int k = 0; k < O; ++k) S[b][k] = uniform(__shfl(z[k], 63, 64));
-            }
-            if constexpr (MODE == MODE_SEGEND) continue;
-
-            // ---- fix-up, gain smoothing and mixdown into the LDS tile --------
-            double g = gin + (sg_lane * sg_t) * (G0[b] - gin);
-            const double cg = (1.0 - a.sg) * gin;
 #pragma unroll
             for (int j = 0; j < kL; ++j) {
-                double y = zsr[j];
+                xw[0] = xs[17 * lane + 17 + j];
 #pragma unroll
-                for (int k = 0; k < O; ++k) y = fma(r[R::H + k * kL + j], st[k], y);
-                g = fma(a.sg, g, cg);
-                double v;
-                if constexpr (DIST == HZ_DIST_NONE) v = g * y;
-                else v = hz::dist_apply<DIST>(g * y, a.dist_param);
-                if (b == 0) my[j * 65 + lane] = v;
-                else my[j * 65 + lane] += v;
-                if constexpr (O > 0) {
-                    if (last_tile) {
-                        const long t = tc + j;
-                        if (t >= n - O && t < n) a.ystate[(long)band * O + (n - 1 - t)] = y;
+                for (int b = 0; b < NB; ++b) {
+                    const double* r = a.rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
+                    pre[b] = fma(a.sp, pre[b], (1.0 - a.sp) * pin[b]);
+                    double ff = r[R::B] * xw[0];
+#pragma unroll
+                    for (int i = 1; i <= O; ++i) ff = fma(r[R::B + i], xw[i], ff);
+                    double y = ff * pre[b];
+#pragma unroll
+                    for (int k = 0; k < O; ++k) y = fma(-r[R::A + k], yh[b][k], y);
+#pragma unroll
+                    for (int k = O - 1; k > 0; --k) yh[b][k] = yh[b][k - 1];
+                    if constexpr (O > 0) yh[b][0] = y;
+                    zsr[b][j] = y;
+                }
+#pragma unroll
+                for (int k = O; k > 0; --k) xw[k] = xw[k - 1];
+            }
+        }
+
+        // ---- carry scan across the 64 chunks of the tile -----------------------
+        //   1. intra-row (16 lanes) inclusive scan of the chunk end states with DPP
+        //      row_shr 1,2,4,8 (zero fill, no select), matrices M16^(2^s);
+        //   2. row totals by v_readlane; the row carries C_0 = S, C_{r+1} =
+        //      M16^16 C_r + total_r are wave-uniform (C_4 = the tile end state);
+        //   3. chunk start state st(r,p) = Z(r,p-1) + M16^p C_r (row_shr:1 + the
+        //      per-band table Q[p] = M16^p).
+        double st[NB][O > 0 ? O : 1];
+        if constexpr (O > 0) {
+            const int row = lane >> 4, p = lane & 15;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const double* r = a.rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
+                double qm[O * O];  // this lane's M16^p (issued early, used last)
+#pragma unroll
+                for (int e = 0; e < O * O; ++e) qm[e] = r[R::Q + p * O * O + e];
+                double z[O];
+#pragma unroll
+                for (int k = 0; k < O; ++k) z[k] = zsr[b][kL - 1 - k];
+#define HZ_ROW_STEP(SIDX, D)                                                                 \
+    {                                                                                        \
+        double nb_[O];                                                                       \
+        _Pragma("unroll") for (int k = 0; k < O; ++k) nb_[k] = dpp_d<kDppRowShr + (D)>(z[k]); \
+        _Pragma("unroll") for (int rr = 0; rr < O; ++rr)                                     \
+            _Pragma("unroll") for (int c = 0; c < O; ++c)                                    \
+                z[rr] = fma(r[R::P + (SIDX) * O * O + rr * O + c], nb_[c], z[rr]);           \
+    }
+                HZ_ROW_STEP(0, 1)
+                HZ_ROW_STEP(1, 2)
+                HZ_ROW_STEP(2, 4)
+                HZ_ROW_STEP(3, 8)
+#undef HZ_ROW_STEP
+                // row carries (wave-uniform)
+                double C[5][O];
+#pragma unroll
+                for (int k = 0; k < O; ++k) C[0][k] = S[b][k];
+#pragma unroll
+                for (int rw = 0; rw < 4; ++rw) {
+#pragma unroll
+                    for (int i = 0; i < O; ++i) {
+                        double acc = readlane_d(z[i], 16 * rw + 15);
+#pragma unroll
+                        for (int q = 0; q < O; ++q) acc = fma(r[R::P + 4 * O * O + i * O + q], C[rw][q], acc);
+                        C[rw + 1][i] = acc;
                     }
                 }
-            }
-            if constexpr (O > 0) {
-                // n < O (e.g. per-sample calls): the older history entries shift along;
-                // n < O implies a single tile, so lane 0's chunk start state is the
-                // state at call start
-                if (last_tile && lane == 0 && n < O) {
+                double Cr[O];
 #pragma unroll
-                    for (int k = 0; k < O; ++k)
-                        if (k >= n) a.ystate[(long)band * O + k] = st[k - n];
+                for (int k = 0; k < O; ++k)
+                    Cr[k] = row == 0 ? C[0][k] : row == 1 ? C[1][k] : row == 2 ? C[2][k] : C[3][k];
+#pragma unroll
+                for (int k = 0; k < O; ++k) {
+                    double v = dpp_d<kDppRowShr + 1>(z[k]);  // Z(r, p-1), 0 at p == 0
+#pragma unroll
+                    for (int c = 0; c < O; ++c) v = fma(qm[k * O + c], Cr[c], v);
+                    st[b][k] = v;
                 }
-            }
-            if (last_tile && lane == 0) {
-                // closed-form end state of the one-pole smoothers after n samples
-                a.pgstate[2 * (long)band] = pin + a.sp_n * (P0[b] - pin);
-                a.pgstate[2 * (long)band + 1] = gin + a.sg_n * (G0[b] - gin);
+                // tile end state (the padded tail of a ragged last tile only matters
+                // after the final sample, where it is unused)
+#pragma unroll
+                for (int k = 0; k < O; ++k) S[b][k] = C[4][k];
             }
         }
 
         if constexpr (MODE == MODE_MIX) {
-            // ---- workgroup reduction of the partial mixes over waves ---------
+            // ---- fix-up, gain smoothing and mixdown (bands summed in registers) ---
+            double g[NB];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) g[b] = gin[b] + (sg_lane * sg_t) * (G0[b] - gin[b]);
+#pragma unroll
+            for (int j = 0; j < kL; ++j) {
+                double v = 0.0;
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    const double* r = a.rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
+                    double y = zsr[b][j];
+#pragma unroll
+                    for (int k = 0; k < O; ++k) y = fma(r[R::H + k * kL + j], st[b][k], y);
+                    g[b] = fma(a.sg, g[b], (1.0 - a.sg) * gin[b]);
+                    double gy = g[b] * y;
+                    if constexpr (DIST != HZ_DIST_NONE) gy = hz::dist_apply<DIST>(gy, a.dist_param);
+                    v += live[b] ? gy : 0.0;
+                    if constexpr (O > 0) {
+                        if (last_tile && live[b]) {
+                            const long t = tc + j;
+                            if (t >= n - O && t < n) a.ystate[(long)(band0 + b) * O + (n - 1 - t)] = y;
+                        }
+                    }
+                }
+                my[j * 65 + lane] = v;
+            }
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                if (!last_tile || lane != 0 || !live[b]) continue;
+                const long band = band0 + b;
+                if constexpr (O > 0) {
+                    // n < O (e.g. per-sample calls): older history entries shift along;
+                    // n < O implies one tile, so lane 0's chunk start = call start state
+                    if (n < O) {
+#pragma unroll
+                        for (int k = 0; k < O; ++k)
+                            if (k >= n) a.ystate[band * O + k] = st[b][k - n];
+                    }
+                }
+                // closed-form end state of the one-pole smoothers after n samples
+                a.pgstate[2 * band] = pin[b] + a.sp_n * (P0[b] - pin[b]);
+                a.pgstate[2 * band + 1] = gin[b] + a.sg_n * (G0[b] - gin[b]);
+            }
+
+            // ---- workgroup reduction of the partial mixes over waves ---------------
             __syncthreads();
             for (int tl = threadIdx.x; tl < kTile; tl += blockDim.x) {
                 const int src_lane = tl >> 4, j = tl & 15;
-                double s = 0.0;
-                for (int w = 0; w < W; ++w) s += lds[(long)w * (kL * 65) + j * 65 + src_lane];
+                const double* q = part + j * 65 + src_lane;
+                double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+                for (int w = 0; w < 16; w += 2) {
+                    if (w < W) s0 += q[w * kPartWave];
+                    if (w + 1 < W) s1 += q[(w + 1) * kPartWave];
+                }
                 const long t = t0 + tl;
-                if (t < n) a.partial[(long)blockIdx.x * a.n_pad + t] = s;
+                if (t < n) a.partial[(long)blockIdx.x * a.n_pad + t] = s0 + s1;
             }
-            __syncthreads();
         }
+        __syncthreads();  // xs / part are rewritten by the next tile
         sp_t *= a.sp_tile;
         sg_t *= a.sg_tile;
     }
@@ -282,14 +357,14 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(MixArgs a) {
         if (lane == 0 && !last_seg) {
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
-                const int band = band0 + b;
-                if (band >= a.nbands) break;
+                if (!live[b]) continue;
 #pragma unroll
-                for (int k = 0; k < O; ++k) a.segstate[((long)band * a.nseg + seg + 1) * O + k] = S[b][k];
+                for (int k = 0; k < O; ++k)
+                    a.segstate[((long)(band0 + b) * a.nseg + seg + 1) * O + k] = S[b][k];
             }
         }
     } else if constexpr (O > 0) {
-        // ---- x history for the next call (ping-pong buffer) ------------------
+        // ---- x history for the next call (ping-pong buffer) ----------------------
         if (last_seg && blockIdx.x == 0 && threadIdx.x < O) {
             const int k = threadIdx.x;
             const long idx = n - 1 - k;
@@ -400,9 +475,23 @@ void build_record(const double* b, const double* av, double* rec) {
                 rec[R::H + k * kL + j] = (double)y;
             }
         }
-        long double M[O][O], T[O][O];
+        long double M[O][O], T[O][O], Qp[O][O];
         for (int rr = 0; rr < O; ++rr)
-            for (int c = 0; c < O; ++c) M[rr][c] = h[c][kL - 1 - rr];
+            for (int c = 0; c < O; ++c) {
+                M[rr][c] = h[c][kL - 1 - rr];
+                Qp[rr][c] = (rr == c) ? 1.0L : 0.0L;
+            }
+        for (int p = 0; p < kL; ++p) {
+            for (int rr = 0; rr < O; ++rr)
+                for (int c = 0; c < O; ++c) rec[R::Q + p * O * O + rr * O + c] = (double)Qp[rr][c];
+            for (int rr = 0; rr < O; ++rr)
+                for (int c = 0; c < O; ++c) {
+                    long double acc = 0;
+                    for (int q = 0; q < O; ++q) acc += Qp[rr][q] * M[q][c];
+                    T[rr][c] = acc;
+                }
+            std::memcpy(Qp, T, sizeof(Qp));
+        }
         for (int s = 0; s < 6; ++s) {
             for (int rr = 0; rr < O; ++rr)
                 for (int c = 0; c < O; ++c) rec[R::P + s * O * O + rr * O + c] = (double)M[rr][c];
@@ -455,7 +544,6 @@ MixKernel pick_order(int O, int dist, int mode) {
 static MixKernel pick_kernel(int O, int dist, int nb, int mode) {
     switch (nb) {
     case 2: return pick_order<2>(O, dist, mode);
-    case 4: return pick_order<4>(O, dist, mode);
     default: return pick_order<1>(O, dist, mode);
     }
 }
@@ -571,7 +659,8 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
     MixKernel kmix = pick_kernel(O, h->dist_id, h->bands_per_wave, MODE_MIX);
     MixKernel kend = pick_kernel(O, h->dist_id, h->bands_per_wave, MODE_SEGEND);
     HZ_TRY(fb_set_lds_attr(kmix));
-    const size_t lds = sizeof(double) * (size_t)h->waves * kL * 65;
+    const size_t lds = lds_bytes(h->waves, true);
+    const size_t lds_end = lds_bytes(h->waves, false);
     for (long off = 0; off < n; off += chunk) {
         const long len = std::min(chunk, n - off);
         const long ntiles = (len + kTile - 1) / kTile;
@@ -626,7 +715,7 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
         }
         if (nseg > 1 && O > 0) {
             // segment end states (zero-state), then the per-band carry over segments
-            hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg - 1)), dim3(64 * h->waves), 0, h->stream, a);
+            hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg - 1)), dim3(64 * h->waves), lds_end, h->stream, a);
             HZ_TRY_HIP(hipGetLastError());
             hipLaunchKernelGGL(pick_carry(O), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0, h->stream,
                                (const double*)h->d_rec, (const double*)h->d_ystate, h->d_seg, h->N, (int)nseg,
@@ -940,8 +1029,8 @@ int hz_fb_info(hz_fb* h, int* order, int* N_local, int* band_begin, int* N_total
 int hz_fb_tune(hz_fb* h, int waves_per_group, int bands_per_wave) {
     if (!h) return HZ_E_INVALID;
     if (waves_per_group < 0 || waves_per_group > 16 ||
-        !(bands_per_wave == 0 || bands_per_wave == 1 || bands_per_wave == 2 || bands_per_wave == 4)) {
-        hz::set_error("hz_fb_tune: waves in [1,16], bands per wave in {1,2,4}");
+        !(bands_per_wave == 0 || bands_per_wave == 1 || bands_per_wave == 2)) {
+        hz::set_error("hz_fb_tune: waves in [1,16], bands per wave in {1,2}");
         return HZ_E_INVALID;
     }
     if (waves_per_group) h->waves = waves_per_group;

@@ -84,7 +84,7 @@ int hz_fb_state_size(hz_fb* h, size_t* count);
 int hz_fb_get_state(hz_fb* h, double* buf, size_t count);
 int hz_fb_set_state(hz_fb* h, const double* buf, size_t count);
 int hz_fb_info(hz_fb* h, int* order, int* N_local, int* band_begin, int* N_total);
-/* kernel geometry: waves per workgroup (1..16), bands per wave (1,2,4); 0 = default */
+/* kernel geometry: waves per workgroup (1..16), bands per wave (1,2); 0 = default */
 int hz_fb_tune(hz_fb* h, int waves_per_group, int bands_per_wave);
 /* HIP-event timing of the launches of subsequent process calls, on the handle's
  * stream: total ms of the time-segment pre-pass (segment end states + carry;

@@ -23,7 +23,7 @@ timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
 rc=$?; tail -3 "$OUT/bench.log"; echo "bench rc=$rc"
 if fatal $rc; then exit $rc; fi
 
-if [ -n "${PROFILE:-1}" ]; then
+if [ -n "${PROFILE-1}" ]; then
   echo "== rocprofv3 kernel trace"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o trace --output-format csv -- \
       python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --stream-blocks 64 > "$OUT/prof.log" 2>&1

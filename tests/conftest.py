@@ -4,6 +4,11 @@ import sys
 
 import pytest
 
+try:  # one HIP runtime per process: let torch-ROCm load it first (see huygens_amd/_lib.py)
+    import torch  # noqa: F401
+except Exception:
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))

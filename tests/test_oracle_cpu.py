@@ -84,3 +84,31 @@ def test_filterbank_oracle_block_split_invariance():
         pos += L
     parts.append(fb2.process(x[pos:]))
     assert np.array_equal(y1, np.concatenate(parts))
+
+
+@pytest.mark.parametrize("order,N,n", [(2, 5, 2500), (1, 3, 1100), (3, 3, 2100), (0, 2, 1500)])
+def test_kernel_algorithm_model(order, N, n):
+    """The chunked-scan algebra of fb_mix_kernel (numpy lane model) == sequential oracle."""
+    from kernel_model import mix_model
+    rng = np.random.default_rng(order)
+    fwd = rng.uniform(-1, 1, (N, order + 1))
+    back = np.zeros((N, order))
+    for b in range(N):
+        roots = []
+        for _ in range(order // 2):
+            p = 0.99 * np.exp(1j * rng.uniform(0, np.pi))
+            roots += [p, np.conj(p)]
+        if order % 2:
+            roots.append(0.99 * rng.uniform(-1, 1))
+        if order:
+            back[b] = np.real(np.poly(roots))[1:]
+    x = rng.uniform(-1, 1, n)
+    fb = OracleFilterbank(order, N, 0.1, 1.0)
+    for b in range(N):
+        fb.coefficients(b, fwd[b], back[b])
+    fb.boost(np.ones(N))
+    fb.open()
+    ref = fb.process(x)
+    from golden.spec_numpy import relaxation
+    got = mix_model(fwd, back, relaxation(0.1), relaxation(1.0), np.ones(N), np.ones(N), x)
+    assert rel_err(got, ref) < 1e-10
