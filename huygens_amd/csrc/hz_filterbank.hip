@@ -110,10 +110,12 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // LDS layout of one workgroup:
 //   xs   : the tile's input x[t0-16 .. t0+1023], padded one slot per 16 samples so
 //          lane c's reads (17c + k) hit 64 distinct banks (ds_read_b64)
-//   part : [W][16][65] per-wave partial mixes (65: conflict-free transposed reads)
+//   part : [W][16][66] per-wave partial mixes (pad 66: conflict-free ds_write_b64 rows
+//          and ds_read_b64 transposed reads)
 constexpr int kXsLen = 1040;                     // 16 halo + 1024
 constexpr int kXsPad = ((kXsLen + kXsLen / 16) + 1) & ~1;  // 1106 doubles (16-B multiple)
-constexpr int kPartWave = kL * 65;
+constexpr int kPartPad = 66;
+constexpr int kPartWave = kL * kPartPad;
 __host__ __device__ constexpr size_t lds_bytes(int waves, bool mix) {
     return sizeof(double) * (kXsPad + (mix ? (size_t)waves * kPartWave : 0));
 }
@@ -127,7 +129,9 @@ __device__ __forceinline__ int xs_pos(int li) { return li + (li >> 4); }
 enum { MODE_MIX = 0, MODE_SEGEND = 1 };
 
 template <int O, int DIST, int NB, int MODE>
-__global__ __launch_bounds__(1024) void fb_mix_kernel(MixArgs a) {
+__global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__ rec, MixArgs a) {
+    // rec is passed as its own __restrict__ argument so the compiler can prove the
+    // kernel's stores never clobber it: wave-uniform record reads become s_load.
     using R = Rec<O>;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* xs = lds;
@@ -204,7 +208,7 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(MixArgs a) {
                 xw[0] = xs[17 * lane + 17 + j];
 #pragma unroll
                 for (int b = 0; b < NB; ++b) {
-                    const double* r = a.rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
+                    const double* r = rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
                     pre[b] = fma(a.sp, pre[b], (1.0 - a.sp) * pin[b]);
                     double ff = r[R::B] * xw[0];
 #pragma unroll
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(MixArgs a) {
             const int row = lane >> 4, p = lane & 15;
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
-                const double* r = a.rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
+                const double* r = rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
                 double qm[O * O];  // this lane's M16^p (issued early, used last)
 #pragma unroll
                 for (int e = 0; e < O * O; ++e) qm[e] = r[R::Q + p * O * O + e];
@@ -291,27 +295,53 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(MixArgs a) {
             double g[NB];
 #pragma unroll
             for (int b = 0; b < NB; ++b) g[b] = gin[b] + (sg_lane * sg_t) * (G0[b] - gin[b]);
+            // correction c = y - zsr obeys the homogeneous recurrence seeded with the
+            // chunk start state: c_j = -sum_k a_k c_{j-1-k}, c_{-1-k} = st[k]
+            double cr[NB][O > 0 ? O : 1];
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int k = 0; k < O; ++k) cr[b][k] = st[b][k];
 #pragma unroll
             for (int j = 0; j < kL; ++j) {
                 double v = 0.0;
 #pragma unroll
                 for (int b = 0; b < NB; ++b) {
-                    const double* r = a.rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
+                    const double* r = rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
                     double y = zsr[b][j];
+                    if constexpr (O > 0) {
+                        double c = -r[R::A] * cr[b][0];
 #pragma unroll
-                    for (int k = 0; k < O; ++k) y = fma(r[R::H + k * kL + j], st[b][k], y);
+                        for (int k = 1; k < O; ++k) c = fma(-r[R::A + k], cr[b][k], c);
+#pragma unroll
+                        for (int k = O - 1; k > 0; --k) cr[b][k] = cr[b][k - 1];
+                        cr[b][0] = c;
+                        y += c;
+                    }
                     g[b] = fma(a.sg, g[b], (1.0 - a.sg) * gin[b]);
                     double gy = g[b] * y;
                     if constexpr (DIST != HZ_DIST_NONE) gy = hz::dist_apply<DIST>(gy, a.dist_param);
                     v += live[b] ? gy : 0.0;
-                    if constexpr (O > 0) {
-                        if (last_tile && live[b]) {
-                            const long t = tc + j;
-                            if (t >= n - O && t < n) a.ystate[(long)(band0 + b) * O + (n - 1 - t)] = y;
+                    zsr[b][j] = y;  // keep y for the end-of-signal state capture
+                }
+                my[j * kPartPad + lane] = v;
+            }
+            if constexpr (O > 0) {
+                if (last_tile) {  // wave-uniform: y history at the last O samples
+                    for (int k = 0; k < O; ++k) {
+                        const long t = n - 1 - k;
+                        if (t < tc || t >= tc + kL) continue;
+                        const int jj = (int)(t - tc);
+#pragma unroll
+                        for (int b = 0; b < NB; ++b) {
+                            if (!live[b]) continue;
+                            double y = 0.0;
+#pragma unroll
+                            for (int j = 0; j < kL; ++j) y = (j == jj) ? zsr[b][j] : y;
+                            a.ystate[(long)(band0 + b) * O + k] = y;
                         }
                     }
                 }
-                my[j * 65 + lane] = v;
             }
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
@@ -335,7 +365,7 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(MixArgs a) {
             __syncthreads();
             for (int tl = threadIdx.x; tl < kTile; tl += blockDim.x) {
                 const int src_lane = tl >> 4, j = tl & 15;
-                const double* q = part + j * 65 + src_lane;
+                const double* q = part + j * kPartPad + src_lane;
                 double s0 = 0.0, s1 = 0.0;
 #pragma unroll
                 for (int w = 0; w < 16; w += 2) {
@@ -516,7 +546,7 @@ static void build_record_any(int O, const double* b, const double* a, double* re
     }
 }
 
-typedef void (*MixKernel)(MixArgs);
+typedef void (*MixKernel)(const double*, MixArgs);
 typedef void (*CarryKernel)(const double*, const double*, double*, int, int, long);
 
 template <int O, int NB>
@@ -715,7 +745,8 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
         }
         if (nseg > 1 && O > 0) {
             // segment end states (zero-state), then the per-band carry over segments
-            hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg - 1)), dim3(64 * h->waves), lds_end, h->stream, a);
+            hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg - 1)), dim3(64 * h->waves), lds_end, h->stream,
+                               (const double*)h->d_rec, a);
             HZ_TRY_HIP(hipGetLastError());
             hipLaunchKernelGGL(pick_carry(O), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0, h->stream,
                                (const double*)h->d_rec, (const double*)h->d_ystate, h->d_seg, h->N, (int)nseg,
@@ -723,7 +754,8 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
             HZ_TRY_HIP(hipGetLastError());
         }
         if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
-        hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * h->waves), lds, h->stream, a);
+        hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * h->waves), lds, h->stream,
+                           (const double*)h->d_rec, a);
         HZ_TRY_HIP(hipGetLastError());
         if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
         hipLaunchKernelGGL(fb_reduce_kernel, dim3((unsigned)((len + 63) / 64)), dim3(256), 0, h->stream,
