@@ -22,6 +22,7 @@
 //   * a wave walks the tiles of the call sequentially, carrying the band state in
 //     registers (readlane of lane 63's scanned end state).
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -61,8 +62,10 @@ struct MixArgs {
     const double* rec;     // [N][REC]
     const double* pin;     // [N]
     const double* gin;     // [N]
-    double* ystate;        // [N][O]  y[-1-k]
-    double* pgstate;       // [N][2]  pre, gain
+    const double* ystate;  // [N][O]  y[-1-k] at call start
+    const double* pgstate; // [N][2]  pre, gain at call start
+    double* ystate_next;   // end-of-call state: separate buffers (ping-pong), because
+    double* pgstate_next;  // other workgroups of the same launch still read the start state
     const double* x;       // [n] device input
     const double* xhist;   // [O] x[-1-k]
     double* xhist_next;    // [O]
@@ -190,16 +193,28 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__
         __syncthreads();
 
         // ---- zero-state pass over the lane's 16 samples, all NB bands ----------
+        // Fast path once the pre-amp smoother has converged for this tile
+        // (sp^t |P0 - pin| <= 2^-60 |pin|: pre == pin to ~1e-18): pin folds into b.
+        bool pfast = true, gfast = true;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            pfast = pfast && (sp_t * fabs(P0[b] - pin[b]) <= 0x1p-60 * fabs(pin[b]));
+            gfast = gfast && (sg_t * fabs(G0[b] - gin[b]) <= 0x1p-60 * fabs(gin[b]));
+        }
         double zsr[NB][kL];
-        {
+        auto zsr_pass = [&](auto fast_tag) {
+            constexpr bool FAST = decltype(fast_tag)::value;
             double xw[O + 1];  // x[t], x[t-1], ... sliding window
 #pragma unroll
             for (int k = 1; k <= O; ++k) xw[k] = xs[17 * lane + 16 - k];
-            double pre[NB];
+            double pre[NB], bp[NB][O + 1];
             double yh[NB][O > 0 ? O : 1];
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
+                const double* r = rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
                 pre[b] = pin[b] + (sp_lane * sp_t) * (P0[b] - pin[b]);
+#pragma unroll
+                for (int i = 0; i <= O; ++i) bp[b][i] = FAST ? pin[b] * r[R::B + i] : r[R::B + i];
 #pragma unroll
                 for (int k = 0; k < O; ++k) yh[b][k] = 0.0;
             }
@@ -209,11 +224,14 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__
 #pragma unroll
                 for (int b = 0; b < NB; ++b) {
                     const double* r = rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
-                    pre[b] = fma(a.sp, pre[b], (1.0 - a.sp) * pin[b]);
-                    double ff = r[R::B] * xw[0];
+                    double ff = bp[b][0] * xw[0];
 #pragma unroll
-                    for (int i = 1; i <= O; ++i) ff = fma(r[R::B + i], xw[i], ff);
-                    double y = ff * pre[b];
+                    for (int i = 1; i <= O; ++i) ff = fma(bp[b][i], xw[i], ff);
+                    double y = ff;
+                    if constexpr (!FAST) {
+                        pre[b] = fma(a.sp, pre[b], (1.0 - a.sp) * pin[b]);
+                        y = ff * pre[b];
+                    }
 #pragma unroll
                     for (int k = 0; k < O; ++k) y = fma(-r[R::A + k], yh[b][k], y);
 #pragma unroll
@@ -224,7 +242,9 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__
 #pragma unroll
                 for (int k = O; k > 0; --k) xw[k] = xw[k - 1];
             }
-        }
+        };
+        if (pfast) zsr_pass(std::true_type{});
+        else zsr_pass(std::false_type{});
 
         // ---- carry scan across the 64 chunks of the tile -----------------------
         //   1. intra-row (16 lanes) inclusive scan of the chunk end states with DPP
@@ -292,39 +312,49 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__
 
         if constexpr (MODE == MODE_MIX) {
             // ---- fix-up, gain smoothing and mixdown (bands summed in registers) ---
-            double g[NB];
-#pragma unroll
-            for (int b = 0; b < NB; ++b) g[b] = gin[b] + (sg_lane * sg_t) * (G0[b] - gin[b]);
             // correction c = y - zsr obeys the homogeneous recurrence seeded with the
-            // chunk start state: c_j = -sum_k a_k c_{j-1-k}, c_{-1-k} = st[k]
-            double cr[NB][O > 0 ? O : 1];
-#pragma unroll
-            for (int b = 0; b < NB; ++b)
-#pragma unroll
-                for (int k = 0; k < O; ++k) cr[b][k] = st[b][k];
-#pragma unroll
-            for (int j = 0; j < kL; ++j) {
-                double v = 0.0;
+            // chunk start state: c_j = -sum_k a_k c_{j-1-k}, c_{-1-k} = st[k].
+            // Gain fast path once the gain smoother has converged (as for pre).
+            auto fix_pass = [&](auto fast_tag) {
+                constexpr bool FAST = decltype(fast_tag)::value;
+                double g[NB], cr[NB][O > 0 ? O : 1];
 #pragma unroll
                 for (int b = 0; b < NB; ++b) {
-                    const double* r = rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
-                    double y = zsr[b][j];
-                    if constexpr (O > 0) {
-                        double c = -r[R::A] * cr[b][0];
+                    g[b] = FAST ? gin[b] : gin[b] + (sg_lane * sg_t) * (G0[b] - gin[b]);
 #pragma unroll
-                        for (int k = 1; k < O; ++k) c = fma(-r[R::A + k], cr[b][k], c);
-#pragma unroll
-                        for (int k = O - 1; k > 0; --k) cr[b][k] = cr[b][k - 1];
-                        cr[b][0] = c;
-                        y += c;
-                    }
-                    g[b] = fma(a.sg, g[b], (1.0 - a.sg) * gin[b]);
-                    double gy = g[b] * y;
-                    if constexpr (DIST != HZ_DIST_NONE) gy = hz::dist_apply<DIST>(gy, a.dist_param);
-                    v += live[b] ? gy : 0.0;
-                    zsr[b][j] = y;  // keep y for the end-of-signal state capture
+                    for (int k = 0; k < O; ++k) cr[b][k] = st[b][k];
                 }
-                my[j * kPartPad + lane] = v;
+#pragma unroll
+                for (int j = 0; j < kL; ++j) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) {
+                        const double* r = rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
+                        double y = zsr[b][j];
+                        if constexpr (O > 0) {
+                            double c = -r[R::A] * cr[b][0];
+#pragma unroll
+                            for (int k = 1; k < O; ++k) c = fma(-r[R::A + k], cr[b][k], c);
+#pragma unroll
+                            for (int k = O - 1; k > 0; --k) cr[b][k] = cr[b][k - 1];
+                            cr[b][0] = c;
+                            y += c;
+                        }
+                        if constexpr (!FAST) g[b] = fma(a.sg, g[b], (1.0 - a.sg) * gin[b]);
+                        double gy = g[b] * y;
+                        if constexpr (DIST != HZ_DIST_NONE) gy = hz::dist_apply<DIST>(gy, a.dist_param);
+                        if constexpr (NB == 1) v = gy;  // a dead wave's row is zeroed below
+                        else v += live[b] ? gy : 0.0;
+                        zsr[b][j] = y;  // keep y for the end-of-signal state capture
+                    }
+                    my[j * kPartPad + lane] = v;
+                }
+            };
+            if (gfast) fix_pass(std::true_type{});
+            else fix_pass(std::false_type{});
+            if (NB == 1 && !live[0]) {  // wave-uniform: padding wave past the last band
+#pragma unroll
+                for (int j = 0; j < kL; ++j) my[j * kPartPad + lane] = 0.0;
             }
             if constexpr (O > 0) {
                 if (last_tile) {  // wave-uniform: y history at the last O samples
@@ -338,7 +368,7 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__
                             double y = 0.0;
 #pragma unroll
                             for (int j = 0; j < kL; ++j) y = (j == jj) ? zsr[b][j] : y;
-                            a.ystate[(long)(band0 + b) * O + k] = y;
+                            a.ystate_next[(long)(band0 + b) * O + k] = y;
                         }
                     }
                 }
@@ -353,12 +383,12 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__
                     if (n < O) {
 #pragma unroll
                         for (int k = 0; k < O; ++k)
-                            if (k >= n) a.ystate[band * O + k] = st[b][k - n];
+                            if (k >= n) a.ystate_next[band * O + k] = st[b][k - n];
                     }
                 }
                 // closed-form end state of the one-pole smoothers after n samples
-                a.pgstate[2 * band] = pin[b] + a.sp_n * (P0[b] - pin[b]);
-                a.pgstate[2 * band + 1] = gin[b] + a.sg_n * (G0[b] - gin[b]);
+                a.pgstate_next[2 * band] = pin[b] + a.sp_n * (P0[b] - pin[b]);
+                a.pgstate_next[2 * band + 1] = gin[b] + a.sg_n * (G0[b] - gin[b]);
             }
 
             // ---- workgroup reduction of the partial mixes over waves ---------------
@@ -604,7 +634,9 @@ struct hz_fb {
     // geometry
     int waves = 16, bands_per_wave = 1;
     // device buffers
-    double *d_rec = nullptr, *d_pin = nullptr, *d_gin = nullptr, *d_ystate = nullptr, *d_pg = nullptr;
+    double *d_rec = nullptr, *d_pin = nullptr, *d_gin = nullptr;
+    double *d_ystate[2] = {nullptr, nullptr}, *d_pg[2] = {nullptr, nullptr};
+    int scur = 0;  // current state buffer (ping-pong per launch)
     double* d_xhist[2] = {nullptr, nullptr};
     int xcur = 0;
     double* d_partial = nullptr;
@@ -711,8 +743,10 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
         a.rec = h->d_rec;
         a.pin = h->d_pin;
         a.gin = h->d_gin;
-        a.ystate = h->d_ystate;
-        a.pgstate = h->d_pg;
+        a.ystate = h->d_ystate[h->scur];
+        a.pgstate = h->d_pg[h->scur];
+        a.ystate_next = h->d_ystate[h->scur ^ 1];
+        a.pgstate_next = h->d_pg[h->scur ^ 1];
         a.x = d_in + off;
         a.xhist = h->d_xhist[h->xcur];
         a.xhist_next = h->d_xhist[h->xcur ^ 1];
@@ -749,7 +783,7 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
                                (const double*)h->d_rec, a);
             HZ_TRY_HIP(hipGetLastError());
             hipLaunchKernelGGL(pick_carry(O), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0, h->stream,
-                               (const double*)h->d_rec, (const double*)h->d_ystate, h->d_seg, h->N, (int)nseg,
+                               (const double*)h->d_rec, (const double*)h->d_ystate[h->scur], h->d_seg, h->N, (int)nseg,
                                seg_tiles);
             HZ_TRY_HIP(hipGetLastError());
         }
@@ -763,6 +797,7 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
         HZ_TRY_HIP(hipGetLastError());
         if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
         h->xcur ^= 1;
+        h->scur ^= 1;
         h->prof_launches += h->prof ? 1 : 0;
     }
     return HZ_OK;
@@ -834,15 +869,19 @@ int hz_fb_create_shard(int order, int N_total, int band_begin, int band_count, d
     if (hipMalloc(&h->d_rec, sizeof(double) * N * h->rec) != hipSuccess ||
         hipMalloc(&h->d_pin, sizeof(double) * N) != hipSuccess ||
         hipMalloc(&h->d_gin, sizeof(double) * N) != hipSuccess ||
-        hipMalloc(&h->d_ystate, sizeof(double) * N * O) != hipSuccess ||
-        hipMalloc(&h->d_pg, sizeof(double) * N * 2) != hipSuccess ||
+        hipMalloc(&h->d_ystate[0], sizeof(double) * N * O) != hipSuccess ||
+        hipMalloc(&h->d_ystate[1], sizeof(double) * N * O) != hipSuccess ||
+        hipMalloc(&h->d_pg[0], sizeof(double) * N * 2) != hipSuccess ||
+        hipMalloc(&h->d_pg[1], sizeof(double) * N * 2) != hipSuccess ||
         hipMalloc(&h->d_xhist[0], sizeof(double) * O) != hipSuccess ||
         hipMalloc(&h->d_xhist[1], sizeof(double) * O) != hipSuccess) {
         hz::set_error("hipMalloc failed for filterbank state (%zu bands)", N);
         return fail(HZ_E_ALLOC);
     }
-    if (hipMemsetAsync(h->d_ystate, 0, sizeof(double) * N * O, h->stream) != hipSuccess ||
-        hipMemsetAsync(h->d_pg, 0, sizeof(double) * N * 2, h->stream) != hipSuccess ||
+    if (hipMemsetAsync(h->d_ystate[0], 0, sizeof(double) * N * O, h->stream) != hipSuccess ||
+        hipMemsetAsync(h->d_ystate[1], 0, sizeof(double) * N * O, h->stream) != hipSuccess ||
+        hipMemsetAsync(h->d_pg[0], 0, sizeof(double) * N * 2, h->stream) != hipSuccess ||
+        hipMemsetAsync(h->d_pg[1], 0, sizeof(double) * N * 2, h->stream) != hipSuccess ||
         hipMemsetAsync(h->d_xhist[0], 0, sizeof(double) * O, h->stream) != hipSuccess ||
         hipMemsetAsync(h->d_xhist[1], 0, sizeof(double) * O, h->stream) != hipSuccess ||
         hipStreamSynchronize(h->stream) != hipSuccess) {
@@ -861,7 +900,8 @@ int hz_fb_destroy(hz_fb* h) {
     if (!h) return HZ_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (double* p : {h->d_rec, h->d_pin, h->d_gin, h->d_ystate, h->d_pg, h->d_xhist[0], h->d_xhist[1],
+    for (double* p : {h->d_rec, h->d_pin, h->d_gin, h->d_ystate[0], h->d_ystate[1], h->d_pg[0], h->d_pg[1],
+                      h->d_xhist[0], h->d_xhist[1],
                       h->d_partial, h->d_seg, h->d_in, h->d_out})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
@@ -1028,9 +1068,9 @@ int hz_fb_get_state(hz_fb* h, double* buf, size_t count) {
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
     if (O) {
         HZ_TRY_HIP(hipMemcpy(buf, h->d_xhist[h->xcur], sizeof(double) * O, hipMemcpyDeviceToHost));
-        HZ_TRY_HIP(hipMemcpy(buf + O, h->d_ystate, sizeof(double) * N * O, hipMemcpyDeviceToHost));
+        HZ_TRY_HIP(hipMemcpy(buf + O, h->d_ystate[h->scur], sizeof(double) * N * O, hipMemcpyDeviceToHost));
     }
-    HZ_TRY_HIP(hipMemcpy(buf + O + N * O, h->d_pg, sizeof(double) * N * 2, hipMemcpyDeviceToHost));
+    HZ_TRY_HIP(hipMemcpy(buf + O + N * O, h->d_pg[h->scur], sizeof(double) * N * 2, hipMemcpyDeviceToHost));
     return HZ_OK;
 }
 
@@ -1043,9 +1083,9 @@ int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
     if (O) {
         HZ_TRY_HIP(hipMemcpy(h->d_xhist[h->xcur], buf, sizeof(double) * O, hipMemcpyHostToDevice));
-        HZ_TRY_HIP(hipMemcpy(h->d_ystate, buf + O, sizeof(double) * N * O, hipMemcpyHostToDevice));
+        HZ_TRY_HIP(hipMemcpy(h->d_ystate[h->scur], buf + O, sizeof(double) * N * O, hipMemcpyHostToDevice));
     }
-    HZ_TRY_HIP(hipMemcpy(h->d_pg, buf + O + N * O, sizeof(double) * N * 2, hipMemcpyHostToDevice));
+    HZ_TRY_HIP(hipMemcpy(h->d_pg[h->scur], buf + O + N * O, sizeof(double) * N * 2, hipMemcpyHostToDevice));
     return HZ_OK;
 }
 
