@@ -6,5 +6,6 @@ that ABI used by tests/ and bench.py.
 """
 from ._lib import HZError, load, header_symbols  # noqa: F401
 from .filterbank import Filterbank  # noqa: F401
+from .oscbank import Oscbank  # noqa: F401
 
-__all__ = ["HZError", "load", "header_symbols", "Filterbank"]
+__all__ = ["HZError", "load", "header_symbols", "Filterbank", "Oscbank"]

@@ -76,6 +76,25 @@ _SIGS = {
     "hz_fb_profile": (I, [VP, I]),
     "hz_fb_profile_read": (I, [VP, PD, PD, PD, C.POINTER(L)]),
     "hz_fb_set_target_groups": (I, [VP, I]),
+    # Oscbank
+    "hz_osc_create": (I, [I, D, I, C.POINTER(VP)]),
+    "hz_osc_create_shard": (I, [I, I, I, D, I, C.POINTER(VP)]),
+    "hz_osc_destroy": (I, [VP]),
+    "hz_osc_freqmod": (I, [VP, I, D]),
+    "hz_osc_activate": (I, [VP, C.POINTER(I), I]),
+    "hz_osc_deactivate": (I, [VP, C.POINTER(I), I]),
+    "hz_osc_open": (I, [VP]),
+    "hz_osc_close": (I, [VP]),
+    "hz_osc_active_count": (I, [VP, C.POINTER(I)]),
+    "hz_osc_fill": (I, [VP, PD, PD, SZ]),
+    "hz_osc_fill_device": (I, [VP, VP, VP, SZ]),
+    "hz_osc_phases": (I, [VP, PD]),
+    "hz_osc_set_phases": (I, [VP, PD]),
+    "hz_osc_set_stream": (I, [VP, VP]),
+    "hz_osc_synchronize": (I, [VP]),
+    "hz_osc_set_target_groups": (I, [VP, I]),
+    "hz_osc_profile": (I, [VP, I]),
+    "hz_osc_profile_read": (I, [VP, PD, C.POINTER(L)]),
 }
 
 

@@ -117,10 +117,11 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 //          and ds_read_b64 transposed reads)
 constexpr int kXsLen = 1040;                     // 16 halo + 1024
 constexpr int kXsPad = ((kXsLen + kXsLen / 16) + 1) & ~1;  // 1106 doubles (16-B multiple)
+
 constexpr int kPartPad = 66;
 constexpr int kPartWave = kL * kPartPad;
 __host__ __device__ constexpr size_t lds_bytes(int waves, bool mix) {
-    return sizeof(double) * (kXsPad + (mix ? (size_t)waves * kPartWave : 0));
+    return sizeof(double) * (2 * kXsPad + (mix ? (size_t)waves * kPartWave : 0));
 }
 __device__ __forceinline__ int xs_pos(int li) { return li + (li >> 4); }
 
@@ -131,14 +132,13 @@ __device__ __forceinline__ int xs_pos(int li) { return li + (li >> 4); }
 //   with bands alone (e.g. 512-band shards on 8 GPUs).
 enum { MODE_MIX = 0, MODE_SEGEND = 1 };
 
-template <int O, int DIST, int NB, int MODE>
+template <int O, int DIST, int NB, int MODE, int PF>
 __global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__ rec, MixArgs a) {
     // rec is passed as its own __restrict__ argument so the compiler can prove the
     // kernel's stores never clobber it: wave-uniform record reads become s_load.
     using R = Rec<O>;
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* xs = lds;
-    double* part = lds + kXsPad;
+    double* part = lds + 2 * kXsPad;  // xs double buffer: lds[0..kXsPad), lds[kXsPad..2 kXsPad)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int W = blockDim.x >> 6;
@@ -177,20 +177,44 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__
         gin[b] = live[b] ? a.gin[bb] : 0.0;
     }
 
+    // input tiles are double-buffered in LDS; tile k+1 is loaded into registers while
+    // tile k computes and written to the other buffer before the tile's barrier
+    // PF = x values per thread = ceil(1040 / blockDim)
+    auto load_x = [&](long t0x, double (&pf)[PF]) {
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+            const int li = threadIdx.x + q * blockDim.x;
+            const long idx = t0x - 16 + li;
+            double v = 0.0;
+            if (li < kXsLen) {
+                if (idx < 0) v = (idx >= -O) ? a.xhist[-idx - 1] : 0.0;
+                else if (idx < seg_end) v = a.x[idx];
+            }
+            pf[q] = v;
+        }
+    };
+    auto store_x = [&](double* xbuf, const double (&pf)[PF]) {
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+            const int li = threadIdx.x + q * blockDim.x;
+            if (li < kXsLen) xbuf[xs_pos(li)] = pf[q];
+        }
+    };
+    {
+        double pf0[PF];
+        load_x(seg_t0, pf0);
+        store_x(lds, pf0);
+        __syncthreads();
+    }
+
     for (int tile = 0; tile < ntiles; ++tile) {
         const long t0 = seg_t0 + (long)tile * kTile;  // global sample index of the tile
         const long tc = t0 + (long)kL * lane;
         const bool last_tile = last_seg && tile == ntiles - 1;
-
-        // ---- stage the tile's input in LDS (coalesced, once per workgroup) -----
-        for (int li = threadIdx.x; li < kXsLen; li += blockDim.x) {
-            const long idx = t0 - 16 + li;
-            double v = 0.0;
-            if (idx < 0) v = (idx >= -O) ? a.xhist[-idx - 1] : 0.0;
-            else if (idx < seg_end) v = a.x[idx];
-            xs[xs_pos(li)] = v;
-        }
-        __syncthreads();
+        const double* xs = lds + (tile & 1) * kXsPad;
+        double pf[PF];
+        const bool more = tile + 1 < ntiles;
+        if (more) load_x(t0 + kTile, pf);  // in flight during this tile's compute
 
         // ---- zero-state pass over the lane's 16 samples, all NB bands ----------
         // Fast path once the pre-amp smoother has converged for this tile
@@ -392,6 +416,7 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__
             }
 
             // ---- workgroup reduction of the partial mixes over waves ---------------
+            if (more) store_x(lds + ((tile + 1) & 1) * kXsPad, pf);
             __syncthreads();
             for (int tl = threadIdx.x; tl < kTile; tl += blockDim.x) {
                 const int src_lane = tl >> 4, j = tl & 15;
@@ -406,7 +431,10 @@ __global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__
                 if (t < n) a.partial[(long)blockIdx.x * a.n_pad + t] = s0 + s1;
             }
         }
-        __syncthreads();  // xs / part are rewritten by the next tile
+        if constexpr (MODE == MODE_SEGEND) {
+            if (more) store_x(lds + ((tile + 1) & 1) * kXsPad, pf);
+        }
+        __syncthreads();  // part is rewritten / the next xs buffer becomes readable
         sp_t *= a.sp_tile;
         sg_t *= a.sg_tile;
     }
@@ -579,32 +607,34 @@ static void build_record_any(int O, const double* b, const double* a, double* re
 typedef void (*MixKernel)(const double*, MixArgs);
 typedef void (*CarryKernel)(const double*, const double*, double*, int, int, long);
 
-template <int O, int NB>
+template <int O, int PF>
 MixKernel pick_dist(int dist, int mode) {
-    if (mode == MODE_SEGEND) return fb_mix_kernel<O, HZ_DIST_NONE, NB, MODE_SEGEND>;
+    if (mode == MODE_SEGEND) return fb_mix_kernel<O, HZ_DIST_NONE, 1, MODE_SEGEND, PF>;
     switch (dist) {
-    case HZ_DIST_SOFTCLIP: return fb_mix_kernel<O, HZ_DIST_SOFTCLIP, NB, MODE_MIX>;
-    case HZ_DIST_SATURATE: return fb_mix_kernel<O, HZ_DIST_SATURATE, NB, MODE_MIX>;
-    case HZ_DIST_LIMITER: return fb_mix_kernel<O, HZ_DIST_LIMITER, NB, MODE_MIX>;
-    default: return fb_mix_kernel<O, HZ_DIST_NONE, NB, MODE_MIX>;
+    case HZ_DIST_SOFTCLIP: return fb_mix_kernel<O, HZ_DIST_SOFTCLIP, 1, MODE_MIX, PF>;
+    case HZ_DIST_SATURATE: return fb_mix_kernel<O, HZ_DIST_SATURATE, 1, MODE_MIX, PF>;
+    case HZ_DIST_LIMITER: return fb_mix_kernel<O, HZ_DIST_LIMITER, 1, MODE_MIX, PF>;
+    default: return fb_mix_kernel<O, HZ_DIST_NONE, 1, MODE_MIX, PF>;
     }
 }
 
-template <int NB>
+template <int PF>
 MixKernel pick_order(int O, int dist, int mode) {
     switch (O) {
-    case 0: return pick_dist<0, NB>(dist, mode);
-    case 1: return pick_dist<1, NB>(dist, mode);
-    case 2: return pick_dist<2, NB>(dist, mode);
-    case 3: return pick_dist<3, NB>(dist, mode);
-    default: return pick_dist<4, NB>(dist, mode);
+    case 0: return pick_dist<0, PF>(dist, mode);
+    case 1: return pick_dist<1, PF>(dist, mode);
+    case 2: return pick_dist<2, PF>(dist, mode);
+    case 3: return pick_dist<3, PF>(dist, mode);
+    default: return pick_dist<4, PF>(dist, mode);
     }
 }
 
-static MixKernel pick_kernel(int O, int dist, int nb, int mode) {
-    switch (nb) {
-    case 2: return pick_order<2>(O, dist, mode);
-    default: return pick_order<1>(O, dist, mode);
+// waves per workgroup in {4, 8, 16}: x prefetch depth ceil(1040 / (64 waves))
+static MixKernel pick_kernel(int O, int dist, int waves, int mode) {
+    switch (waves) {
+    case 16: return pick_order<2>(O, dist, mode);
+    case 8: return pick_order<3>(O, dist, mode);
+    default: return pick_order<5>(O, dist, mode);
     }
 }
 
@@ -718,8 +748,8 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
         HZ_TRY_HIP(hipMalloc(&h->d_partial, sizeof(double) * need));
         h->partial_cap = need;
     }
-    MixKernel kmix = pick_kernel(O, h->dist_id, h->bands_per_wave, MODE_MIX);
-    MixKernel kend = pick_kernel(O, h->dist_id, h->bands_per_wave, MODE_SEGEND);
+    MixKernel kmix = pick_kernel(O, h->dist_id, h->waves, MODE_MIX);
+    MixKernel kend = pick_kernel(O, h->dist_id, h->waves, MODE_SEGEND);
     HZ_TRY(fb_set_lds_attr(kmix));
     const size_t lds = lds_bytes(h->waves, true);
     const size_t lds_end = lds_bytes(h->waves, false);
@@ -850,7 +880,7 @@ int hz_fb_create_shard(int order, int N_total, int band_begin, int band_count, d
     // default geometry: 16 waves x 1 band; fewer waves when the bank is small
     h->waves = 16;
     h->bands_per_wave = 1;
-    while (h->waves > 1 && (long)fb_groups(h) * h->waves < 1024 && h->waves * 2 > band_count) h->waves /= 2;
+    while (h->waves > 4 && (long)fb_groups(h) * h->waves < 1024 && h->waves * 2 > band_count) h->waves /= 2;
     auto fail = [&](int code) {
         hz_fb_destroy(h);
         return code;
@@ -1100,9 +1130,9 @@ int hz_fb_info(hz_fb* h, int* order, int* N_local, int* band_begin, int* N_total
 
 int hz_fb_tune(hz_fb* h, int waves_per_group, int bands_per_wave) {
     if (!h) return HZ_E_INVALID;
-    if (waves_per_group < 0 || waves_per_group > 16 ||
-        !(bands_per_wave == 0 || bands_per_wave == 1 || bands_per_wave == 2)) {
-        hz::set_error("hz_fb_tune: waves in [1,16], bands per wave in {1,2}");
+    if (!(waves_per_group == 0 || waves_per_group == 4 || waves_per_group == 8 || waves_per_group == 16) ||
+        !(bands_per_wave == 0 || bands_per_wave == 1)) {
+        hz::set_error("hz_fb_tune: waves in {4,8,16}, bands per wave 1");
         return HZ_E_INVALID;
     }
     if (waves_per_group) h->waves = waves_per_group;

@@ -84,7 +84,7 @@ int hz_fb_state_size(hz_fb* h, size_t* count);
 int hz_fb_get_state(hz_fb* h, double* buf, size_t count);
 int hz_fb_set_state(hz_fb* h, const double* buf, size_t count);
 int hz_fb_info(hz_fb* h, int* order, int* N_local, int* band_begin, int* N_total);
-/* kernel geometry: waves per workgroup (1..16), bands per wave (1,2); 0 = default */
+/* kernel geometry: waves per workgroup (4, 8, 16), bands per wave (1); 0 = default */
 int hz_fb_tune(hz_fb* h, int waves_per_group, int bands_per_wave);
 /* HIP-event timing of the launches of subsequent process calls, on the handle's
  * stream: total ms of the time-segment pre-pass (segment end states + carry;
@@ -94,6 +94,34 @@ int hz_fb_profile(hz_fb* h, int enable);
 int hz_fb_profile_read(hz_fb* h, double* segment_ms, double* mix_ms, double* reduce_ms, long* launches);
 /* workgroups wanted per launch before time segmentation kicks in (default: CU count) */
 int hz_fb_set_target_groups(hz_fb* h, int groups);
+
+/* ---- Oscbank<double,N>  (src/oscbank.h:15-97, src/multichannel.h:16-159) -- */
+typedef struct hz_osc hz_osc;
+
+/* Oscbank(double k = 2.0/SR)  oscbank.h:37-47 (k's stiffness is unused there too) */
+int hz_osc_create(int N, double k, int device, hz_osc** out);
+/* oscillators [begin, begin+count) of an N_total bank; indices stay global */
+int hz_osc_create_shard(int N_total, int begin, int count, double k, int device, hz_osc** out);
+int hz_osc_destroy(hz_osc* h);                                   /* ~Oscbank 30-34 */
+/* freqmod(int index, T hz)  49-56: out-of-range indices are ignored (HZ_OK) */
+int hz_osc_freqmod(hz_osc* h, int index, double hz);
+int hz_osc_activate(hz_osc* h, const int* idx, int count);      /* multichannel.h:87-92 */
+int hz_osc_deactivate(hz_osc* h, const int* idx, int count);    /* multichannel.h:95-100 */
+int hz_osc_open(hz_osc* h);                                      /* multichannel.h:103-109 */
+int hz_osc_close(hz_osc* h);                                     /* multichannel.h:112-118 */
+int hz_osc_active_count(hz_osc* h, int* count);
+/* n x { mix[t] = mixdown(); per_band[t][:] = operator()(); tick(); }  (65-90, 59-63)
+ * mix: 2n doubles (complex interleaved) or NULL; per_band: 2nN doubles or NULL */
+int hz_osc_fill(hz_osc* h, double* mix, double* per_band, size_t n);
+int hz_osc_fill_device(hz_osc* h, double* d_mix, double* d_per_band, size_t n);
+/* operator()(): the N phasors (2N doubles, complex interleaved) */
+int hz_osc_phases(hz_osc* h, double* z);
+int hz_osc_set_phases(hz_osc* h, const double* z);
+int hz_osc_set_stream(hz_osc* h, void* hip_stream);
+int hz_osc_synchronize(hz_osc* h);
+int hz_osc_set_target_groups(hz_osc* h, int groups);
+int hz_osc_profile(hz_osc* h, int enable);
+int hz_osc_profile_read(hz_osc* h, double* ms, long* launches);
 
 #ifdef __cplusplus
 }

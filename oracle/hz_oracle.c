@@ -173,3 +173,121 @@ void orc_fb_process(orc_fb* fb, const double* in, double* out, long n, int dist_
         orc_fb_tick(fb);
     }
 }
+
+/* ---- Oscbank<double,N>  src/oscbank.h:15-97 ------------------------------
+ * Active set: Multichannel<T,N>::where, kept sorted ascending by insert/popout
+ * (src/multichannel.h:51-118); tick/mixdown visit it in that order. */
+struct orc_osc {
+    int N;
+    double* zr; double* zi;   /* phases      (oscbank.h:39-46, setOnes) */
+    double* wr; double* wi;   /* frequencies (oscbank.h:40-46, setOnes) */
+    char* active;             /* multichannel.h:22-24 */
+    int* where; int nwhere;   /* sorted active indices */
+};
+
+orc_osc* orc_osc_create(int N, double k)
+{
+    (void)k; /* stiffness = relaxation(k) is stored but never used (oscbank.h:37,96) */
+    orc_osc* o = (orc_osc*)calloc(1, sizeof(orc_osc));
+    o->N = N;
+    o->zr = (double*)malloc(sizeof(double) * N); o->zi = (double*)calloc(N, sizeof(double));
+    o->wr = (double*)malloc(sizeof(double) * N); o->wi = (double*)calloc(N, sizeof(double));
+    for (int i = 0; i < N; i++) { o->zr[i] = 1.0; o->wr[i] = 1.0; }
+    o->active = (char*)calloc(N, 1);
+    o->where = (int*)malloc(sizeof(int) * (N > 0 ? N : 1));
+    return o;
+}
+
+void orc_osc_destroy(orc_osc* o)
+{
+    if (!o) return;
+    free(o->zr); free(o->zi); free(o->wr); free(o->wi); free(o->active); free(o->where); free(o);
+}
+
+/* oscbank.h:49-56 */
+void orc_osc_freqmod(orc_osc* o, int index, double hz)
+{
+    if (0 <= index && index < o->N) {
+        o->wr[index] = cos(2 * ORC_PI * hz / ORC_SR);
+        o->wi[index] = sin(2 * ORC_PI * hz / ORC_SR);
+    }
+}
+
+/* multichannel.h:87-92 (insert keeps where sorted) */
+void orc_osc_activate(orc_osc* o, const int* idx, int count)
+{
+    for (int c = 0; c < count; c++) {
+        int i = idx[c];
+        if (0 <= i && i < o->N && !o->active[i]) {
+            int pos = o->nwhere;
+            while (pos > 0 && o->where[pos - 1] > i) { o->where[pos] = o->where[pos - 1]; pos--; }
+            o->where[pos] = i;
+            o->nwhere++;
+            o->active[i] = 1;
+        }
+    }
+}
+
+/* multichannel.h:95-100 (popout) */
+void orc_osc_deactivate(orc_osc* o, const int* idx, int count)
+{
+    for (int c = 0; c < count; c++) {
+        int i = idx[c];
+        if (0 <= i && i < o->N && o->active[i]) {
+            int pos = 0;
+            while (o->where[pos] != i) pos++;
+            for (; pos + 1 < o->nwhere; pos++) o->where[pos] = o->where[pos + 1];
+            o->nwhere--;
+            o->active[i] = 0;
+        }
+    }
+}
+
+void orc_osc_open(orc_osc* o)
+{
+    for (int i = 0; i < o->N; i++) orc_osc_activate(o, &i, 1);
+}
+
+void orc_osc_close(orc_osc* o)
+{
+    for (int i = 0; i < o->N; i++) orc_osc_deactivate(o, &i, 1);
+}
+
+int orc_osc_active_count(orc_osc* o) { return o->nwhere; }
+
+/* oscbank.h:59-63: z *= w; z /= (1 + |z|^2) / 2  (Eigen abs2 = re^2 + im^2) */
+void orc_osc_tick(orc_osc* o)
+{
+    for (int c = 0; c < o->nwhere; c++) {
+        int i = o->where[c];
+        double ar = o->zr[i], ai = o->zi[i];
+        double br = o->wr[i], bi = o->wi[i];
+        double zr = ar * br - ai * bi;
+        double zi = ar * bi + ai * br;
+        double d = (1.0 + (zr * zr + zi * zi)) / 2;
+        o->zr[i] = zr / d;
+        o->zi[i] = zi / d;
+    }
+}
+
+/* oscbank.h:81-90 */
+void orc_osc_mixdown(orc_osc* o, double* re, double* im)
+{
+    double r = 0, m = 0;
+    for (int c = 0; c < o->nwhere; c++) { r += o->zr[o->where[c]]; m += o->zi[o->where[c]]; }
+    *re = r; *im = m;
+}
+
+void orc_osc_phases(orc_osc* o, double* z)
+{
+    for (int i = 0; i < o->N; i++) { z[2 * i] = o->zr[i]; z[2 * i + 1] = o->zi[i]; }
+}
+
+void orc_osc_fill(orc_osc* o, double* mix, double* per_band, long n)
+{
+    for (long t = 0; t < n; t++) {
+        orc_osc_mixdown(o, mix + 2 * t, mix + 2 * t + 1);
+        if (per_band) orc_osc_phases(o, per_band + 2 * t * o->N);
+        orc_osc_tick(o);
+    }
+}

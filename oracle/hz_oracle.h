@@ -43,6 +43,22 @@ double  orc_fb_sample(orc_fb* fb, double x, int dist_id, double dist_param);
 void    orc_fb_tick(orc_fb* fb);
 void    orc_fb_process(orc_fb* fb, const double* in, double* out, long n, int dist_id, double dist_param);
 
+/* ---- Oscbank<double,N> (src/oscbank.h:15-97, src/multichannel.h:16-159) */
+typedef struct orc_osc orc_osc;
+orc_osc* orc_osc_create(int N, double k);
+void     orc_osc_destroy(orc_osc* o);
+void     orc_osc_freqmod(orc_osc* o, int index, double hz);
+void     orc_osc_activate(orc_osc* o, const int* idx, int count);
+void     orc_osc_deactivate(orc_osc* o, const int* idx, int count);
+void     orc_osc_open(orc_osc* o);
+void     orc_osc_close(orc_osc* o);
+void     orc_osc_tick(orc_osc* o);
+void     orc_osc_mixdown(orc_osc* o, double* re, double* im);
+void     orc_osc_phases(orc_osc* o, double* z /* 2N interleaved */);
+int      orc_osc_active_count(orc_osc* o);
+/* n x { mix[i] = mixdown(); per_band[i][:] = phases; tick(); } (per_band may be NULL) */
+void     orc_osc_fill(orc_osc* o, double* mix /* 2n */, double* per_band /* 2nN */, long n);
+
 /* distortion functors (tests/filterbank.cpp:158-176, src/wave.h:150) */
 double orc_dist(int id, double v, double param);
 

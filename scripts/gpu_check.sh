@@ -26,7 +26,7 @@ if fatal $rc; then exit $rc; fi
 if [ -n "${PROFILE-1}" ]; then
   echo "== rocprofv3 kernel trace"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o trace --output-format csv -- \
-      python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --stream-blocks 64 > "$OUT/prof.log" 2>&1
+      python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-traffic --stream-blocks 0 > "$OUT/prof.log" 2>&1
   rc=$?; tail -3 "$OUT/prof.log"; echo "rocprof rc=$rc"
   find "$OUT/prof" -name "*stats*" | head
 fi

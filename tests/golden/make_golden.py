@@ -25,7 +25,7 @@ from scipy import signal
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from spec_numpy import (  # noqa: E402
-    PI, SR, relaxation, filterbank_run, resonant_coefficients, white_noise_f32,
+    PI, SR, relaxation, filterbank_run, resonant_coefficients, white_noise_f32, oscbank_run,
 )
 
 
@@ -105,8 +105,50 @@ def make_filterbank():
     return out
 
 
+def osc_events_to_arrays(events):
+    """Encode an event list as flat arrays for the .npz (no pickles)."""
+    kinds = {"freqmod": 0, "activate": 1, "deactivate": 2, "open": 3, "close": 4}
+    t, k, i, v = [], [], [], []
+    for (tt, kind, arg) in events:
+        if kind == "freqmod":
+            t.append(tt); k.append(0); i.append(arg[0]); v.append(arg[1])
+        elif kind in ("activate", "deactivate"):
+            for ii in arg:
+                t.append(tt); k.append(kinds[kind]); i.append(ii); v.append(0.0)
+        else:
+            t.append(tt); k.append(kinds[kind]); i.append(-1); v.append(0.0)
+    return dict(ev_t=np.array(t), ev_kind=np.array(k), ev_index=np.array(i), ev_value=np.array(v))
+
+
+def make_oscbank():
+    out = {}
+    rng = np.random.default_rng(21)
+    # 1. N = 32 partials, all open, harmonic frequencies, 4096 samples; check the
+    #    phasor trajectory against the exact rotation e^{i 2 PI f t / SR}
+    N, n = 32, 4096
+    freqs = 110.0 * (1 + np.arange(N))
+    ev = [(0, "freqmod", (i, float(freqs[i]))) for i in range(N)] + [(0, "open", None)]
+    mix, z = oscbank_run(N, ev, n)
+    t = np.arange(n)[:, None]
+    exact = np.exp(1j * 2 * PI * freqs[None, :] * t / SR).sum(axis=1)
+    assert np.max(np.abs(mix - exact)) / N < 1e-9
+    out["osc_n32_open"] = dict(N=N, n=n, mix=mix, z_final=z, **osc_events_to_arrays(ev))
+    # 2. N = 64, partial activation, deactivation and freqmod changes mid-stream,
+    #    out-of-range indices ignored (oscbank.h:51, multichannel.h:87-100)
+    N, n = 64, 3000
+    ev = [(0, "freqmod", (i, float(rng.uniform(20, 20000)))) for i in range(N)]
+    ev += [(0, "activate", sorted(rng.choice(N, 20, replace=False).tolist()) + [N + 3, -1])]
+    ev += [(700, "freqmod", (5, 1234.5)), (700, "freqmod", (N, 99.0)), (700, "activate", [5, 6, 7])]
+    ev += [(1500, "deactivate", [5, 6, 40, 41]), (2222, "open", None), (2600, "close", None),
+           (2700, "activate", [0, 63])]
+    mix, z = oscbank_run(N, ev, n)
+    out["osc_n64_events"] = dict(N=N, n=n, mix=mix, z_final=z, **osc_events_to_arrays(ev))
+    return out
+
+
 def main():
     fixtures = make_filterbank()
+    fixtures.update(make_oscbank())
     for name, d in fixtures.items():
         np.savez(os.path.join(HERE, name + ".npz"), **d)
         print("wrote", name, {k: (v.shape if hasattr(v, "shape") else v) for k, v in d.items() if k in ("x", "y")})

@@ -121,3 +121,41 @@ def filterbank_run(order, N, kp, kg, fwd, back, x, sched, dist_id=0, dist_param=
         ph[t] = pre
         out[t] = np.sum(dist(dist_id, y * g, dist_param))
     return out, yb, ph
+
+
+def oscbank_run(N, events, n):
+    """Oscbank<double,N> (src/oscbank.h:37-90) driven by
+    n x { mix[t] = mixdown(); tick(); } with setter events applied before sample t.
+    events: list of (t, kind, arg): freqmod((i, hz)), activate([i...]), deactivate([i...]),
+    open(None), close(None).  Returns (mix [n] complex, final phases [N] complex)."""
+    z = np.ones(N, dtype=np.complex128)
+    w = np.ones(N, dtype=np.complex128)
+    active = np.zeros(N, dtype=bool)
+    mix = np.zeros(n, dtype=np.complex128)
+    ev = sorted(events, key=lambda e: e[0])
+    ei = 0
+    for t in range(n):
+        while ei < len(ev) and ev[ei][0] == t:
+            _, kind, arg = ev[ei]
+            if kind == "freqmod":
+                i, hz = arg
+                if 0 <= i < N:
+                    w[i] = complex(math.cos(2 * PI * hz / SR), math.sin(2 * PI * hz / SR))
+            elif kind == "activate":
+                for i in arg:
+                    if 0 <= i < N:
+                        active[i] = True
+            elif kind == "deactivate":
+                for i in arg:
+                    if 0 <= i < N:
+                        active[i] = False
+            elif kind == "open":
+                active[:] = True
+            elif kind == "close":
+                active[:] = False
+            ei += 1
+        idx = np.nonzero(active)[0]           # `where`, ascending
+        mix[t] = np.sum(z[idx]) if len(idx) else 0.0
+        zz = z[idx] * w[idx]
+        z[idx] = zz / ((1.0 + (zz.real ** 2 + zz.imag ** 2)) / 2)
+    return mix, z

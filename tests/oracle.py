@@ -150,3 +150,109 @@ def rel_err(got, ref):
     if den == 0.0:
         return float(np.max(np.abs(got))) if got.size else 0.0
     return float(np.max(np.abs(got - ref)) / den)
+
+
+_OSC_SIGS = {
+    "orc_osc_create": (VP, [I, D]),
+    "orc_osc_destroy": (None, [VP]),
+    "orc_osc_freqmod": (None, [VP, I, D]),
+    "orc_osc_activate": (None, [VP, C.POINTER(C.c_int), I]),
+    "orc_osc_deactivate": (None, [VP, C.POINTER(C.c_int), I]),
+    "orc_osc_open": (None, [VP]),
+    "orc_osc_close": (None, [VP]),
+    "orc_osc_tick": (None, [VP]),
+    "orc_osc_mixdown": (None, [VP, PD, PD]),
+    "orc_osc_phases": (None, [VP, PD]),
+    "orc_osc_active_count": (I, [VP]),
+    "orc_osc_fill": (None, [VP, PD, PD, L]),
+}
+
+
+def _bind(sigs):
+    l = lib()
+    for name, (res, args) in sigs.items():
+        fn = getattr(l, name)
+        fn.restype = res
+        fn.argtypes = args
+    return l
+
+
+class OracleOscbank:
+    """CPU restatement of Oscbank<double,N> (src/oscbank.h:15-97)."""
+
+    def __init__(self, N, k=2.0 / 48000):
+        self.l = _bind(_OSC_SIGS)
+        self.h = self.l.orc_osc_create(N, k)
+        self.N = self.local_N = N
+
+    def __del__(self):
+        try:
+            self.l.orc_osc_destroy(self.h)
+        except Exception:
+            pass
+
+    def freqmod(self, i, hz):
+        self.l.orc_osc_freqmod(self.h, int(i), float(hz))
+
+    def activate(self, idx):
+        a = np.ascontiguousarray(idx, dtype=np.int32)
+        self.l.orc_osc_activate(self.h, a.ctypes.data_as(C.POINTER(C.c_int)), len(a))
+
+    def deactivate(self, idx):
+        a = np.ascontiguousarray(idx, dtype=np.int32)
+        self.l.orc_osc_deactivate(self.h, a.ctypes.data_as(C.POINTER(C.c_int)), len(a))
+
+    def open(self):
+        self.l.orc_osc_open(self.h)
+
+    def close_all(self):
+        self.l.orc_osc_close(self.h)
+
+    def active_count(self):
+        return self.l.orc_osc_active_count(self.h)
+
+    def fill(self, n, per_band=False):
+        mix = np.zeros(2 * n)
+        pb = np.zeros(2 * n * self.N) if per_band else None
+        self.l.orc_osc_fill(self.h, _p(mix), _p(pb) if pb is not None else None, n)
+        m = mix.view(np.complex128)
+        if per_band:
+            return m, pb.view(np.complex128).reshape(n, self.N)
+        return m
+
+    def phases(self):
+        z = np.zeros(2 * self.N)
+        self.l.orc_osc_phases(self.h, _p(z))
+        return z.view(np.complex128)
+
+
+def run_osc_events(bank, g):
+    """Drive an Oscbank-like object through a golden fixture's events, splitting
+    fill() at every event time."""
+    t_ev, kind, index, value = g["ev_t"], g["ev_kind"], g["ev_index"], g["ev_value"]
+    n = int(g["n"])
+    out = np.zeros(n, dtype=np.complex128)
+    pos = 0
+    order = np.argsort(t_ev, kind="stable")
+    times = sorted(set(t_ev.tolist())) + [n]
+    for t in times:
+        if t > pos:
+            out[pos:t] = bank.fill(t - pos)
+            pos = t
+        if t >= n:
+            break
+        for e in order:
+            if t_ev[e] != t:
+                continue
+            k = int(kind[e])
+            if k == 0:
+                bank.freqmod(int(index[e]), float(value[e]))
+            elif k == 1:
+                bank.activate([int(index[e])])
+            elif k == 2:
+                bank.deactivate([int(index[e])])
+            elif k == 3:
+                bank.open()
+            elif k == 4:
+                bank.close_all()
+    return out
