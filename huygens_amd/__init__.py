@@ -7,5 +7,6 @@ that ABI used by tests/ and bench.py.
 from ._lib import HZError, load, header_symbols  # noqa: F401
 from .filterbank import Filterbank  # noqa: F401
 from .oscbank import Oscbank  # noqa: F401
+from .additive import Additive, Sinusoids  # noqa: F401
 
-__all__ = ["HZError", "load", "header_symbols", "Filterbank", "Oscbank"]
+__all__ = ["HZError", "load", "header_symbols", "Filterbank", "Oscbank", "Additive", "Sinusoids"]

@@ -95,6 +95,27 @@ _SIGS = {
     "hz_osc_set_target_groups": (I, [VP, I]),
     "hz_osc_profile": (I, [VP, I]),
     "hz_osc_profile_read": (I, [VP, PD, C.POINTER(L)]),
+    # Additive / Sinusoids
+    "hz_add_create": (I, [I, I, D, D, D, I, C.POINTER(VP)]),
+    "hz_add_create_shard": (I, [I, I, I, I, D, D, D, I, C.POINTER(VP)]),
+    "hz_add_destroy": (I, [VP]),
+    "hz_add_request": (I, [VP, D, D, C.POINTER(I)]),
+    "hz_add_release": (I, [VP, I]),
+    "hz_add_makenote": (I, [VP, D, D, C.POINTER(I)]),
+    "hz_add_endnote": (I, [VP, D]),
+    "hz_add_fill": (I, [VP, PD, SZ]),
+    "hz_add_fill_device": (I, [VP, VP, SZ]),
+    "hz_add_set_stream": (I, [VP, VP]),
+    "hz_add_set_target_groups": (I, [VP, I]),
+    "hz_add_profile": (I, [VP, I]),
+    "hz_add_profile_read": (I, [VP, PD, C.POINTER(L)]),
+    "hz_sin_create": (I, [D, I, D, D, D, I, C.POINTER(VP)]),
+    "hz_sin_destroy": (I, [VP]),
+    "hz_sin_fundmod": (I, [VP, D]),
+    "hz_sin_decaymod": (I, [VP, D]),
+    "hz_sin_harmmod": (I, [VP, D]),
+    "hz_sin_fill": (I, [VP, PD, SZ]),
+    "hz_sin_fill_device": (I, [VP, VP, SZ]),
 }
 
 

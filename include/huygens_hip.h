@@ -123,6 +123,42 @@ int hz_osc_set_target_groups(hz_osc* h, int groups);
 int hz_osc_profile(hz_osc* h, int enable);
 int hz_osc_profile_read(hz_osc* h, double* ms, long* launches);
 
+/* ---- Additive<double>  (src/additive.h:11-71 + Minimizer note API,
+ *      src/minimizer.h:111-187; physics() is out of scope) ------------------- */
+typedef struct hz_add hz_add;
+/* Additive(Wave* = &cycle, voices, overtones, decay, harmonicity = 1, k = 0.1)  additive.h:24-36 */
+int hz_add_create(int voices, int overtones, double decay, double harmonicity, double k, int device,
+                  hz_add** out);
+/* overtones [o_begin, o_begin + o_count) of every voice (one process per GPU; the
+ * note API is replicated on every rank so voice allocation agrees) */
+int hz_add_create_shard(int voices, int overtones, int o_begin, int o_count, double decay, double harmonicity,
+                        double k, int device, hz_add** out);
+int hz_add_destroy(hz_add* h);
+int hz_add_request(hz_add* h, double fundamental, double amplitude, int* voice);   /* minimizer.h:111-158 */
+int hz_add_release(hz_add* h, int voice);                                          /* 161-172, -1 = all */
+int hz_add_makenote(hz_add* h, double pitch, double amplitude, int* voice);        /* 174-179 */
+int hz_add_endnote(hz_add* h, double pitch);                                       /* 182-187 */
+/* n x { out[t] = operator()(); tick(); }  additive.h:38-62 (tests/additive.cpp:27-37) */
+int hz_add_fill(hz_add* h, double* out, size_t n);
+int hz_add_fill_device(hz_add* h, double* d_out, size_t n);
+int hz_add_set_stream(hz_add* h, void* hip_stream);
+int hz_add_set_target_groups(hz_add* h, int groups);
+int hz_add_profile(hz_add* h, int enable);
+int hz_add_profile_read(hz_add* h, double* ms, long* launches);
+
+/* ---- Sinusoids<double>  (src/sinusoids.h:10-79), waveform cycle ------------ */
+typedef struct hz_sin hz_sin;
+/* Sinusoids(Wave*, fundamental, overtones, decay, harmonicity = 1, k = 2.0/SR) 16-31 */
+int hz_sin_create(double fundamental, int overtones, double decay, double harmonicity, double k, int device,
+                  hz_sin** out);
+int hz_sin_destroy(hz_sin* h);
+int hz_sin_fundmod(hz_sin* h, double target);    /* 67-68 */
+int hz_sin_decaymod(hz_sin* h, double target);   /* 61-62 */
+int hz_sin_harmmod(hz_sin* h, double target);    /* 64-65 */
+/* n x { out[t] = operator()(); tick(); }  34-57 */
+int hz_sin_fill(hz_sin* h, double* out, size_t n);
+int hz_sin_fill_device(hz_sin* h, double* d_out, size_t n);
+
 #ifdef __cplusplus
 }
 #endif

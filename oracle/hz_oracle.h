@@ -59,6 +59,29 @@ int      orc_osc_active_count(orc_osc* o);
 /* n x { mix[i] = mixdown(); per_band[i][:] = phases; tick(); } (per_band may be NULL) */
 void     orc_osc_fill(orc_osc* o, double* mix /* 2n */, double* per_band /* 2nN */, long n);
 
+/* ---- Additive<double> (src/additive.h:11-71 + src/minimizer.h note API) - */
+typedef struct orc_add orc_add;
+orc_add* orc_add_create(int voices, int overtones, double decay, double harmonicity, double k);
+void     orc_add_destroy(orc_add* a);
+int      orc_add_request(orc_add* a, double fundamental, double amplitude);
+void     orc_add_release(orc_add* a, int voice);
+int      orc_add_makenote(orc_add* a, double pitch, double amplitude);
+void     orc_add_endnote(orc_add* a, double pitch);
+double   orc_add_sample(orc_add* a);
+void     orc_add_tick(orc_add* a);
+void     orc_add_fill(orc_add* a, double* out, long n);
+
+/* ---- Sinusoids<double> (src/sinusoids.h:10-79) -------------------------- */
+typedef struct orc_sin orc_sin;
+orc_sin* orc_sin_create(double fundamental, int overtones, double decay, double harmonicity, double k);
+void     orc_sin_destroy(orc_sin* s);
+void     orc_sin_fundmod(orc_sin* s, double target);
+void     orc_sin_decaymod(orc_sin* s, double target);
+void     orc_sin_harmmod(orc_sin* s, double target);
+double   orc_sin_sample(orc_sin* s);
+void     orc_sin_tick(orc_sin* s);
+void     orc_sin_fill(orc_sin* s, double* out, long n);
+
 /* distortion functors (tests/filterbank.cpp:158-176, src/wave.h:150) */
 double orc_dist(int id, double v, double param);
 

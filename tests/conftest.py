@@ -18,8 +18,9 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (MI355X) and libhuygens_hip.so")
     # the oracle is test infrastructure: build it on demand (gcc, seconds)
     so = os.path.join(ROOT, "oracle", "_build", "libhz_oracle.so")
-    src = os.path.join(ROOT, "oracle", "hz_oracle.c")
-    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+    odir = os.path.join(ROOT, "oracle")
+    newest = max(os.path.getmtime(os.path.join(odir, f)) for f in os.listdir(odir) if f.endswith((".c", ".h")))
+    if not os.path.exists(so) or os.path.getmtime(so) < newest:
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
 
 

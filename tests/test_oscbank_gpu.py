@@ -48,9 +48,10 @@ def test_per_band_output(gpu_lib):
     N, n = 96, 700
     rng = np.random.default_rng(3)
     g, o = Oscbank(N), OracleOscbank(N)
+    f = rng.uniform(50, 5000, N)
     for b in (g, o):
         for i in range(N):
-            b.freqmod(i, rng.uniform(50, 5000))
+            b.freqmod(i, f[i])
         b.activate(list(range(0, N, 3)))
     mg, pg = g.fill(n, per_band=True)
     mo, po = o.fill(n, per_band=True)
