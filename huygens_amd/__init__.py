@@ -8,5 +8,6 @@ from ._lib import HZError, load, header_symbols  # noqa: F401
 from .filterbank import Filterbank  # noqa: F401
 from .oscbank import Oscbank  # noqa: F401
 from .additive import Additive, Sinusoids  # noqa: F401
+from .bowl import Bowl  # noqa: F401
 
-__all__ = ["HZError", "load", "header_symbols", "Filterbank", "Oscbank", "Additive", "Sinusoids"]
+__all__ = ["HZError", "load", "header_symbols", "Filterbank", "Oscbank", "Additive", "Sinusoids", "Bowl"]

@@ -116,6 +116,19 @@ _SIGS = {
     "hz_sin_harmmod": (I, [VP, D]),
     "hz_sin_fill": (I, [VP, PD, SZ]),
     "hz_sin_fill_device": (I, [VP, VP, SZ]),
+    # Bowl
+    "hz_bowl_create": (I, [I, PD, PD, PD, I, I, I, C.POINTER(VP)]),
+    "hz_bowl_destroy": (I, [VP]),
+    "hz_bowl_trigger": (I, [VP]),
+    "hz_bowl_fill": (I, [VP, C.POINTER(C.c_float), SZ]),
+    "hz_bowl_fill_device": (I, [VP, VP, SZ]),
+    "hz_bowl_render": (I, [VP, PD, SZ]),
+    "hz_bowl_render_device": (I, [VP, VP, SZ]),
+    "hz_bowl_phase": (I, [VP, PD]),
+    "hz_bowl_set_stream": (I, [VP, VP]),
+    "hz_bowl_set_target_groups": (I, [VP, I]),
+    "hz_bowl_profile": (I, [VP, I]),
+    "hz_bowl_profile_read": (I, [VP, PD, C.POINTER(L)]),
 }
 
 

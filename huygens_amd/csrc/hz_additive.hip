@@ -67,6 +67,9 @@ struct AddArgs {
     const double* ft;      // [P] target frequency
     const double* amp0;    // [V] envelope value at call start
     const double* act;     // [V] envelope target (Minimizer::active)
+    const double* c0;      // [P] output weights of the call's first sample, or null when
+                           // equal to the records' (Sinusoids::operator() runs before tick()
+                           // applies a decaymod, sinusoids.h:34-57)
     double* partial;       // [G][n_pad]
     long n, n_pad, seg_len;
     int ntasks, nseg;
@@ -150,6 +153,7 @@ __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __re
                 myzt[2 * q + 1] = ni;
             }
             __builtin_amdgcn_wave_barrier();
+            if (a.c0 && tc == 0) acc[0] = fma(a.c0[pi] - c, sinpi(2.0 * a.phi[pi]), acc[0]);
             if (fabs(D) * s_tc > 0x1p-60) {
                 // frequency transient: exact closed form per sample (first chunks only)
                 const double phi0 = a.phi[pi];
@@ -263,6 +267,8 @@ struct PhaseBank {
     double a = 0;      // envelope smoothing (Additive attack); 0 for Sinusoids
     std::vector<double> ft;      // [V*OL] target frequency (Hz)
     std::vector<double> c;       // [V*OL] output weight
+    std::vector<double> c_first; // weights of the next call's first sample
+    double* d_c0 = nullptr;
     std::vector<double> amp, act;
     std::vector<char> alive;
     double scale = 1.0;
@@ -293,6 +299,7 @@ struct PhaseBank {
         const size_t P = (size_t)V * OL;
         ft.assign(P, 0.0);
         c.assign(P, 0.0);
+        c_first.assign(P, 0.0);
         amp.assign(V, 0.0);
         act.assign(V, 0.0);
         alive.assign(V, 0);
@@ -309,6 +316,7 @@ struct PhaseBank {
         HZ_TRY_HIP(hipMalloc(&d_ft, sizeof(double) * P));
         HZ_TRY_HIP(hipMalloc(&d_amp, sizeof(double) * V));
         HZ_TRY_HIP(hipMalloc(&d_act, sizeof(double) * V));
+        HZ_TRY_HIP(hipMalloc(&d_c0, sizeof(double) * P));
         HZ_TRY_HIP(hipMemset(d_phi, 0, sizeof(double) * P));
         HZ_TRY_HIP(hipMemset(d_f, 0, sizeof(double) * P));
         return HZ_OK;
@@ -318,7 +326,7 @@ struct PhaseBank {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         for (void* p : {(void*)d_rec, (void*)d_phi, (void*)d_f, (void*)d_ft, (void*)d_amp, (void*)d_act,
-                        (void*)d_partial, (void*)d_out, (void*)d_tasks})
+                        (void*)d_partial, (void*)d_out, (void*)d_tasks, (void*)d_c0})
             if (p) (void)hipFree(p);
         for (hipEvent_t e : ev) (void)hipEventDestroy(e);
         if (own_stream && stream) (void)hipStreamDestroy(stream);
@@ -365,6 +373,9 @@ struct PhaseBank {
             }
             HZ_TRY_HIP(hipMemcpyAsync(d_tasks, tasks.data(), sizeof(Task) * ntasks, hipMemcpyHostToDevice, stream));
         }
+        const bool c0_differs = c_first != c;
+        if (c0_differs)
+            HZ_TRY_HIP(hipMemcpyAsync(d_c0, c_first.data(), sizeof(double) * P, hipMemcpyHostToDevice, stream));
         HZ_TRY_HIP(hipStreamSynchronize(stream));  // pageable host sources above are reused
 
         hipEvent_t* e = nullptr;
@@ -409,6 +420,7 @@ struct PhaseBank {
             args.ft = d_ft;
             args.amp0 = d_amp;
             args.act = d_act;
+            args.c0 = c0_differs ? d_c0 : nullptr;
             args.partial = d_partial;
             args.n = n;
             args.n_pad = n_pad;
@@ -430,6 +442,7 @@ struct PhaseBank {
         }
         if (e) HZ_TRY_HIP(hipEventRecord(e[1], stream));
         launches += prof ? 1 : 0;
+        c_first = c;
         // envelopes (V scalars): closed form, alive is sticky (a released envelope decays
         // to a denormal fixed point > 0 in the reference and never reaches 0)
         const long double an = powl((long double)a, (long double)n);
@@ -519,6 +532,7 @@ int hz_add_create_shard(int voices, int overtones, int o_begin, int o_count, dou
     for (int v = 0; v < voices; ++v)
         for (int jl = 0; jl < o_count; ++jl)
             h->bank.c[(size_t)v * o_count + jl] = std::pow(decay, o_begin + jl);
+    h->bank.c_first = h->bank.c;
     h->bank.scale = 1.0 / (voices * h->norm);
     h->active.assign(voices, 0.0);
     h->pitches.assign(voices, 0.0);
@@ -714,6 +728,7 @@ int hz_sin_create(double fundamental, int overtones, double decay, double harmon
     h->bank.alive[0] = 1;
     h->bank.scale = 1.0;
     sin_retarget(h);
+    h->bank.c_first = h->bank.c;
     // oscillators start at their target frequency, phase 0 (oscillator.h:16-24)
     std::vector<double> f0(h->bank.ft);
     HZ_TRY_HIP(hipMemcpy(h->bank.d_f, f0.data(), sizeof(double) * overtones, hipMemcpyHostToDevice));

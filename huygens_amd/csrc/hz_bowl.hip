@@ -1,0 +1,466 @@
+// hz_bowl.hip -- Bowl<T> modal resonance bank for MI355X (gfx950).
+//
+// Replaces src/bowl.h:10-74:  s(n) = sum_i a_i pow(E, -d_i n/SR) form(f_i n/SR), n = the
+// `phase` counter (T), reset by trigger(); fill(float*, bsize) writes float.
+//
+// Bowl<double>, form = cycle: every mode is a decaying phasor, so
+//     a_i E^{-d_i n/SR} sin(2 PI f_i n/SR) = a_i Im(w_i^n),  w_i = E^{-d_i/SR} e^{i 2 PI f_i/SR}
+// (the reference's own truncated PI), evaluated by rotation: lanes are TIME (16-sample
+// chunks), a wave walks up to 64 modes per 1024-sample tile, chunk seeds from per-mode
+// tables w^(16p), w^(256r), tile seeds z(t0) w^1024 kept in LDS; no transcendental in the
+// loop.
+// Bowl<float>, form = a Wave<float> lambda sin(2 PI p) (double in, float out): the
+// reference rounds p = f n / SR and x = -d n / SR in float, which moves the phase by up to
+// ulp(p)/2 (0.008 cycles at n ~ 5e5) -- that rounding is part of its output, so the float
+// model is evaluated per mode-sample: float mul + correctly rounded float divide, then
+// sin(2 PI p) in double with p split exactly as k + r (k = floor p) so the argument stays
+// in [0, 2 PI): sin(2 PI r + 2 k (PI - pi)), rounded to float; the decay E^x uses a
+// per-chunk exp seed and a per-sample factor (x's float rounding changes the term by
+// < 2.5e-8 a_i).  The sum is kept in double (the reference rounds it to float after every
+// mode; that accumulation differs by ~1e-7 relative, see tests).  The float counter
+// saturates at 2^24 (phase++ stops incrementing), as in the reference.
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "hz_common.h"
+
+namespace {
+
+constexpr int kL = 16;
+constexpr int kTile = 64 * kL;
+constexpr int kWaves = 8;
+constexpr int kMaxPerWave = 64;
+constexpr int kPad = 66;
+constexpr double kPiM = 3.141592653589793115997963468544185161590576171875;  // M_PI (double)
+
+// per-mode record: a, W1 (2), T1[16] (32), T2[4] (8), WT (2), f, d, |w|  (48 doubles)
+struct BRec {
+    static constexpr int AMP = 0;
+    static constexpr int W1 = 1;
+    static constexpr int T1 = 3;
+    static constexpr int T2 = T1 + 32;
+    static constexpr int WT = T2 + 8;
+    static constexpr int F = WT + 2;     // 45
+    static constexpr int D = F + 1;      // 46
+    static constexpr int R = D + 1;      // 47  per-sample decay factor E^{-d/SR}
+    static constexpr int SIZE = 48;
+};
+
+struct BowlArgs {
+    double* partial;  // [G][n_pad]
+    long n, n_pad, seg_len;
+    double n0;        // phase counter at call start
+    int M, nseg, per_wave, is_float;
+};
+
+__device__ __forceinline__ void cmul(double ar, double ai, double br, double bi, double& cr, double& ci) {
+    const double r = fma(ar, br, -ai * bi);
+    const double i = fma(ar, bi, ai * br);
+    cr = r;
+    ci = i;
+}
+
+// float phase counter after t increments from n0 (saturates at 2^24)
+__device__ __forceinline__ float phase_f(double n0, long t) {
+    const double v = n0 + (double)t;
+    return (float)(v < 16777216.0 ? v : 16777216.0);
+}
+
+__global__ __launch_bounds__(64 * kWaves) void bowl_mix_kernel(const double* __restrict__ rec, BowlArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* part = lds;                     // [W][16][66]
+    double* zt = lds + kWaves * kL * kPad;  // [W][64][2]
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int p16 = lane & 15, r4 = lane >> 4;
+    const int seg = blockIdx.y;
+    const long seg_t0 = (long)seg * a.seg_len;
+    const long seg_end = min(seg_t0 + a.seg_len, a.n);
+    const int ntiles = (int)((seg_end - seg_t0 + kTile - 1) / kTile);
+    const int first = (blockIdx.x * kWaves + wave) * a.per_wave;
+    const int count = max(0, min(a.per_wave, a.M - first));
+    double* myzt = zt + wave * (2 * kMaxPerWave);
+
+    if (!a.is_float) {
+        // tile-start phasors w^(n0 + seg_t0) by binary powering (n0: the phase counter)
+        const unsigned long long e0 = (unsigned long long)(a.n0 + (double)seg_t0);
+        for (int q = 0; q < count; ++q) {
+            const double* rr = rec + (long)(first + q) * BRec::SIZE;
+            double zr = 1.0, zi = 0.0, br = rr[BRec::W1], bi = rr[BRec::W1 + 1];
+            for (unsigned long long e = e0; e > 0; e >>= 1) {
+                if (e & 1) cmul(zr, zi, br, bi, zr, zi);
+                cmul(br, bi, br, bi, br, bi);
+            }
+            if (lane == 0) {
+                myzt[2 * q] = zr;
+                myzt[2 * q + 1] = zi;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    for (int tile = 0; tile < ntiles; ++tile) {
+        const long t0 = seg_t0 + (long)tile * kTile;
+        const long tc = t0 + (long)kL * lane;
+        double acc[kL];
+#pragma unroll
+        for (int j = 0; j < kL; ++j) acc[j] = 0.0;
+        if (!a.is_float) {
+            for (int q = 0; q < count; ++q) {
+                const double* rr = rec + (long)(first + q) * BRec::SIZE;
+                const double sr = myzt[2 * q], si = myzt[2 * q + 1];
+                double nr, ni;
+                cmul(sr, si, rr[BRec::WT], rr[BRec::WT + 1], nr, ni);
+                if (lane == 0) {
+                    myzt[2 * q] = nr;
+                    myzt[2 * q + 1] = ni;
+                }
+                __builtin_amdgcn_wave_barrier();
+                double ur, ui, zr, zi;
+                cmul(rr[BRec::T1 + 2 * p16], rr[BRec::T1 + 2 * p16 + 1], rr[BRec::T2 + 2 * r4],
+                     rr[BRec::T2 + 2 * r4 + 1], ur, ui);
+                cmul(sr, si, ur, ui, zr, zi);
+                const double amp = rr[BRec::AMP], wr = rr[BRec::W1], wi = rr[BRec::W1 + 1];
+#pragma unroll
+                for (int j = 0; j < kL; ++j) {
+                    acc[j] = fma(amp, zi, acc[j]);
+                    cmul(zr, zi, wr, wi, zr, zi);
+                }
+            }
+        } else {
+            const float sr_f = 48000.0f;
+            for (int q = 0; q < count; ++q) {
+                const double* rr = rec + (long)(first + q) * BRec::SIZE;
+                const float fq = (float)rr[BRec::F], dq = (float)rr[BRec::D], aq = (float)rr[BRec::AMP];
+                // decay magnitude: exp seed at the chunk start (from the float exponent, as
+                // the reference), advanced by E^{-d/SR} per sample
+                const float ph0 = phase_f(a.n0, tc);
+                const float x0 = -dq * ph0 / sr_f;
+                double mag = exp((double)x0);
+                const double rstep = rr[BRec::R];
+#pragma unroll
+                for (int j = 0; j < kL; ++j) {
+                    const float ph = phase_f(a.n0, tc + j);
+                    const float p = fq * ph / sr_f;  // float mul, correctly rounded float divide
+                    const float k = floorf(p);
+                    const float rp = p - k;          // exact
+                    const double arg = fma(2.0 * 3.14159265359, (double)rp, 2.0 * (double)k * (3.14159265359 - kPiM));
+                    const float wv = (float)sin(arg);  // Wave<float>: sin in double, float out
+                    acc[j] = fma((double)aq * mag, (double)wv, acc[j]);
+                    mag *= rstep;
+                }
+            }
+        }
+        double* my = part + wave * (kL * kPad);
+#pragma unroll
+        for (int j = 0; j < kL; ++j) my[j * kPad + lane] = acc[j];
+        __syncthreads();
+        for (int tl = threadIdx.x; tl < kTile; tl += blockDim.x) {
+            const int src = tl >> 4, j = tl & 15;
+            double s0 = 0.0;
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) s0 += part[w * (kL * kPad) + j * kPad + src];
+            const long t = t0 + tl;
+            if (t < a.n) a.partial[(long)blockIdx.x * a.n_pad + t] = s0;
+        }
+        __syncthreads();
+    }
+}
+
+template <typename OutT>
+__global__ __launch_bounds__(256) void bowl_reduce_kernel(const double* __restrict__ partial, long n_pad, int G,
+                                                          long n, OutT* __restrict__ out) {
+    __shared__ double red[4][64];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const long t = (long)blockIdx.x * 64 + tx;
+    double s = 0.0;
+    if (t < n)
+        for (int g = ty; g < G; g += 4) s += partial[(long)g * n_pad + t];
+    red[ty][tx] = s;
+    __syncthreads();
+    if (ty == 0 && t < n) out[t] = (OutT)((red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]));
+}
+
+void build_brec(double f, double amp, double d, bool is_float, double* rec) {
+    using C = std::complex<long double>;
+    std::memset(rec, 0, sizeof(double) * BRec::SIZE);
+    const long double PIr = 3.14159265359L;  // src/includes.h:30
+    const long double E = 2.718281828459045L;
+    const long double mag = powl(E, -(long double)d / 48000.0L);
+    const long double th = 2.0L * PIr * (long double)f / 48000.0L;
+    const C w(mag * cosl(th), mag * sinl(th));
+    rec[BRec::AMP] = amp;
+    rec[BRec::W1] = (double)w.real();
+    rec[BRec::W1 + 1] = (double)w.imag();
+    C w16(1, 0);
+    for (int k = 0; k < 16; ++k) w16 *= w;
+    C acc(1, 0);
+    for (int p = 0; p < 16; ++p) {
+        rec[BRec::T1 + 2 * p] = (double)acc.real();
+        rec[BRec::T1 + 2 * p + 1] = (double)acc.imag();
+        acc *= w16;
+    }
+    const C w256 = acc;
+    acc = C(1, 0);
+    for (int r = 0; r < 4; ++r) {
+        rec[BRec::T2 + 2 * r] = (double)acc.real();
+        rec[BRec::T2 + 2 * r + 1] = (double)acc.imag();
+        acc *= w256;
+    }
+    rec[BRec::WT] = (double)acc.real();
+    rec[BRec::WT + 1] = (double)acc.imag();
+    rec[BRec::F] = f;
+    rec[BRec::D] = d;
+    // float model: per-sample decay factor from the float decay constant
+    rec[BRec::R] = (double)expl(-(long double)(is_float ? (float)d : d) / 48000.0L);
+}
+
+}  // namespace
+
+struct hz_bowl {
+    int M = 0, device = 0, is_float = 0;
+    double n0 = 0;  // phase counter (T) at the next call
+    double *d_rec = nullptr, *d_partial = nullptr;
+    void* d_out = nullptr;
+    size_t partial_cap = 0, out_cap = 0;
+    int target_groups = 256;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    bool prof = false;
+    std::vector<hipEvent_t> ev;
+    size_t ev_used = 0;
+    long launches = 0;
+};
+
+namespace {
+
+int bowl_check(hz_bowl* h) {
+    if (!h) {
+        hz::set_error("null hz_bowl handle");
+        return HZ_E_INVALID;
+    }
+    HZ_TRY_HIP(hipSetDevice(h->device));
+    return HZ_OK;
+}
+
+// out_kind: 0 = float samples (fill), 1 = double samples (operator() in T's precision)
+int bowl_launch(hz_bowl* h, void* d_dst, long n, int out_kind) {
+    if (n <= 0) return HZ_OK;
+    const int M = h->M;
+    const int per_wave = std::min(kMaxPerWave, std::max(1, (M + kWaves * 32 - 1) / (kWaves * 32)));
+    const int G = std::max(1, (M + kWaves * per_wave - 1) / (kWaves * per_wave));
+    const long ntiles = (n + kTile - 1) / kTile;
+    long nseg = std::max<long>(1, std::min<long>(ntiles, (h->target_groups + G - 1) / G));
+    const long seg_tiles = (ntiles + nseg - 1) / nseg;
+    nseg = (ntiles + seg_tiles - 1) / seg_tiles;
+    const long n_pad = ntiles * kTile;
+    const size_t need = (size_t)G * n_pad;
+    if (need > h->partial_cap) {
+        if (h->d_partial) HZ_TRY_HIP(hipFree(h->d_partial));
+        h->d_partial = nullptr;
+        HZ_TRY_HIP(hipMalloc(&h->d_partial, sizeof(double) * need));
+        h->partial_cap = need;
+    }
+    const size_t lds = sizeof(double) * (kWaves * kL * kPad + kWaves * 2 * kMaxPerWave);
+    static bool attr = false;
+    if (!attr) {
+        HZ_TRY_HIP(hipFuncSetAttribute((const void*)bowl_mix_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
+        attr = true;
+    }
+    hipEvent_t* e = nullptr;
+    if (h->prof) {
+        if (h->ev_used + 2 > h->ev.size())
+            for (int q = 0; q < 128; ++q) {
+                hipEvent_t ne;
+                HZ_TRY_HIP(hipEventCreate(&ne));
+                h->ev.push_back(ne);
+            }
+        e = &h->ev[h->ev_used];
+        h->ev_used += 2;
+        HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
+    }
+    BowlArgs args;
+    args.partial = h->d_partial;
+    args.n = n;
+    args.n_pad = n_pad;
+    args.seg_len = seg_tiles * kTile;
+    args.n0 = h->n0;
+    args.M = M;
+    args.nseg = (int)nseg;
+    args.per_wave = per_wave;
+    args.is_float = h->is_float;
+    hipLaunchKernelGGL(bowl_mix_kernel, dim3(G, (unsigned)nseg), dim3(64 * kWaves), lds, h->stream,
+                       (const double*)h->d_rec, args);
+    HZ_TRY_HIP(hipGetLastError());
+    if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
+    if (out_kind == 0)
+        hipLaunchKernelGGL(bowl_reduce_kernel<float>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, h->stream,
+                           (const double*)h->d_partial, n_pad, G, n, (float*)d_dst);
+    else
+        hipLaunchKernelGGL(bowl_reduce_kernel<double>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, h->stream,
+                           (const double*)h->d_partial, n_pad, G, n, (double*)d_dst);
+    HZ_TRY_HIP(hipGetLastError());
+    // phase counter: T = double counts exactly; T = float saturates at 2^24
+    h->n0 += (double)n;
+    if (h->is_float && h->n0 > 16777216.0) h->n0 = 16777216.0;
+    h->launches += h->prof ? 1 : 0;
+    return HZ_OK;
+}
+
+int bowl_host(hz_bowl* h, void* out, size_t elem, long n, int kind) {
+    if (n <= 0) return HZ_OK;
+    if ((size_t)n * elem > h->out_cap) {
+        if (h->d_out) HZ_TRY_HIP(hipFree(h->d_out));
+        h->d_out = nullptr;
+        HZ_TRY_HIP(hipMalloc(&h->d_out, elem * n));
+        h->out_cap = elem * n;
+    }
+    HZ_TRY(bowl_launch(h, h->d_out, n, kind));
+    HZ_TRY_HIP(hipMemcpyAsync(out, h->d_out, elem * n, hipMemcpyDeviceToHost, h->stream));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hz_bowl_create(int overtones, const double* f, const double* a, const double* d, int count, int is_float,
+                   int device, hz_bowl** out) {
+    if (!out || overtones <= 0 || count < 0 || (count > 0 && (!f || !a || !d))) {
+        hz::set_error("hz_bowl_create: invalid arguments");
+        return HZ_E_INVALID;
+    }
+    *out = nullptr;
+    HZ_TRY(hz::select_device(device));
+    hz_bowl* h = new (std::nothrow) hz_bowl();
+    if (!h) return HZ_E_ALLOC;
+    h->M = overtones;
+    h->device = device;
+    h->is_float = is_float ? 1 : 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        h->target_groups = prop.multiProcessorCount;
+    std::vector<double> rec((size_t)overtones * BRec::SIZE, 0.0);
+    for (int i = 0; i < overtones; ++i) {  // vectors resized to `overtones`, padded with 0 (bowl.h:19-22)
+        const bool have = i < count;
+        double fi = have ? f[i] : 0.0, ai = have ? a[i] : 0.0, di = have ? d[i] : 0.0;
+        if (h->is_float) {  // Bowl<float> stores float coefficients
+            fi = (float)fi;
+            ai = (float)ai;
+            di = (float)di;
+        }
+        build_brec(fi, ai, di, h->is_float, &rec[(size_t)i * BRec::SIZE]);
+    }
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&h->d_rec, sizeof(double) * rec.size()) != hipSuccess ||
+        hipMemcpy(h->d_rec, rec.data(), sizeof(double) * rec.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        hz::set_error("hz_bowl_create: device allocation failed");
+        if (h->stream) (void)hipStreamDestroy(h->stream);
+        if (h->d_rec) (void)hipFree(h->d_rec);
+        delete h;
+        return HZ_E_ALLOC;
+    }
+    h->own_stream = true;
+    *out = h;
+    return HZ_OK;
+}
+
+int hz_bowl_destroy(hz_bowl* h) {
+    if (!h) return HZ_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (void* p : {(void*)h->d_rec, (void*)h->d_partial, h->d_out})
+        if (p) (void)hipFree(p);
+    for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return HZ_OK;
+}
+
+int hz_bowl_trigger(hz_bowl* h) {   // bowl.h:25-28
+    if (!h) return HZ_E_INVALID;
+    h->n0 = 0;
+    return HZ_OK;
+}
+
+int hz_bowl_fill(hz_bowl* h, float* buffer, size_t bsize) {   // bowl.h:50-63
+    HZ_TRY(bowl_check(h));
+    if (bsize && !buffer) return HZ_E_INVALID;
+    return bowl_host(h, buffer, sizeof(float), (long)bsize, 0);
+}
+
+int hz_bowl_fill_device(hz_bowl* h, float* d_buffer, size_t bsize) {
+    HZ_TRY(bowl_check(h));
+    if (bsize && !d_buffer) return HZ_E_INVALID;
+    return bowl_launch(h, d_buffer, (long)bsize, 0);
+}
+
+// n x { out[j] = operator()(); tick(); }  bowl.h:30-48, samples widened to double
+int hz_bowl_render(hz_bowl* h, double* out, size_t n) {
+    HZ_TRY(bowl_check(h));
+    if (n && !out) return HZ_E_INVALID;
+    return bowl_host(h, out, sizeof(double), (long)n, 1);
+}
+
+int hz_bowl_render_device(hz_bowl* h, double* d_out, size_t n) {
+    HZ_TRY(bowl_check(h));
+    if (n && !d_out) return HZ_E_INVALID;
+    return bowl_launch(h, d_out, (long)n, 1);
+}
+
+int hz_bowl_phase(hz_bowl* h, double* phase) {
+    if (!h || !phase) return HZ_E_INVALID;
+    *phase = h->n0;
+    return HZ_OK;
+}
+
+int hz_bowl_set_stream(hz_bowl* h, void* s) {
+    HZ_TRY(bowl_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    if (h->own_stream) HZ_TRY_HIP(hipStreamDestroy(h->stream));
+    if (s) {
+        h->stream = (hipStream_t)s;
+        h->own_stream = false;
+    } else {
+        HZ_TRY_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        h->own_stream = true;
+    }
+    return HZ_OK;
+}
+
+int hz_bowl_set_target_groups(hz_bowl* h, int groups) {
+    if (!h || groups < 1) return HZ_E_INVALID;
+    h->target_groups = groups;
+    return HZ_OK;
+}
+
+int hz_bowl_profile(hz_bowl* h, int enable) {
+    HZ_TRY(bowl_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    h->prof = enable != 0;
+    h->ev_used = 0;
+    h->launches = 0;
+    return HZ_OK;
+}
+
+int hz_bowl_profile_read(hz_bowl* h, double* ms, long* launches) {
+    HZ_TRY(bowl_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    double m = 0;
+    for (size_t i = 0; i + 2 <= h->ev_used; i += 2) {
+        float x = 0;
+        HZ_TRY_HIP(hipEventElapsedTime(&x, h->ev[i], h->ev[i + 1]));
+        m += x;
+    }
+    if (ms) *ms = m;
+    if (launches) *launches = h->launches;
+    return HZ_OK;
+}
+
+}  // extern "C"

@@ -159,6 +159,26 @@ int hz_sin_harmmod(hz_sin* h, double target);    /* 64-65 */
 int hz_sin_fill(hz_sin* h, double* out, size_t n);
 int hz_sin_fill_device(hz_sin* h, double* d_out, size_t n);
 
+/* ---- Bowl<T>  (src/bowl.h:10-74), T = double (is_float 0) or float (1) ----
+ * Bowl(int overtones, const vector<T>& f, const vector<T>& a, const vector<T>& d,
+ *      Wave<T>* form = &cycle)  bowl.h:16-23; the form is cycle (sin 2 PI p) for double and
+ * the Wave<float> lambda sin(2 PI p) for float (&cycle does not compile for float). */
+typedef struct hz_bowl hz_bowl;
+int hz_bowl_create(int overtones, const double* f, const double* a, const double* d, int count, int is_float,
+                   int device, hz_bowl** out);
+int hz_bowl_destroy(hz_bowl* h);
+int hz_bowl_trigger(hz_bowl* h);                                        /* 25-28 */
+int hz_bowl_fill(hz_bowl* h, float* buffer, size_t bsize);              /* int fill(float*, int) 50-63 */
+int hz_bowl_fill_device(hz_bowl* h, float* d_buffer, size_t bsize);
+/* n x { out[j] = operator()(); tick(); }  30-48 (T's precision, widened to double) */
+int hz_bowl_render(hz_bowl* h, double* out, size_t n);
+int hz_bowl_render_device(hz_bowl* h, double* d_out, size_t n);
+int hz_bowl_phase(hz_bowl* h, double* phase);
+int hz_bowl_set_stream(hz_bowl* h, void* hip_stream);
+int hz_bowl_set_target_groups(hz_bowl* h, int groups);
+int hz_bowl_profile(hz_bowl* h, int enable);
+int hz_bowl_profile_read(hz_bowl* h, double* ms, long* launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,6 +82,15 @@ double   orc_sin_sample(orc_sin* s);
 void     orc_sin_tick(orc_sin* s);
 void     orc_sin_fill(orc_sin* s, double* out, long n);
 
+/* ---- Bowl<T> (src/bowl.h:10-74), T = double (is_float 0) or float (1) ---- */
+typedef struct orc_bowl orc_bowl;
+orc_bowl* orc_bowl_create(int overtones, const double* f, const double* a, const double* d, int count,
+                          int is_float);
+void      orc_bowl_destroy(orc_bowl* b);
+void      orc_bowl_trigger(orc_bowl* b);
+int       orc_bowl_fill(orc_bowl* b, float* buffer, long bsize);
+void      orc_bowl_render(orc_bowl* b, double* out, long n);
+
 /* distortion functors (tests/filterbank.cpp:158-176, src/wave.h:150) */
 double orc_dist(int id, double v, double param);
 
