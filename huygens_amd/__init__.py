@@ -9,5 +9,6 @@ from .filterbank import Filterbank  # noqa: F401
 from .oscbank import Oscbank  # noqa: F401
 from .additive import Additive, Sinusoids  # noqa: F401
 from .bowl import Bowl  # noqa: F401
+from .delay import Delay, Delaybank  # noqa: F401
 
-__all__ = ["HZError", "load", "header_symbols", "Filterbank", "Oscbank", "Additive", "Sinusoids", "Bowl"]
+__all__ = ["HZError", "load", "header_symbols", "Filterbank", "Oscbank", "Additive", "Sinusoids", "Bowl", "Delay", "Delaybank"]

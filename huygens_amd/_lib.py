@@ -129,6 +129,21 @@ _SIGS = {
     "hz_bowl_set_target_groups": (I, [VP, I]),
     "hz_bowl_profile": (I, [VP, I]),
     "hz_bowl_profile_read": (I, [VP, PD, C.POINTER(L)]),
+    "hz_dly_create": (I, [I, C.c_uint, C.c_uint, I, I, C.POINTER(VP)]),
+    "hz_dly_destroy": (I, [VP]),
+    "hz_dly_coefficients": (I, [VP, I, C.POINTER(C.c_uint), PD, I, C.POINTER(C.c_uint), PD, I]),
+    "hz_dly_modulate_forward": (I, [VP, I, C.c_uint, C.c_uint, D]),
+    "hz_dly_modulate_back": (I, [VP, I, C.c_uint, C.c_uint, D]),
+    "hz_dly_process": (I, [VP, VP, VP, SZ, I, I]),
+    "hz_dly_process_device": (I, [VP, VP, VP, SZ, I, I]),
+    "hz_dly_origin": (I, [VP, C.POINTER(C.c_uint)]),
+    "hz_dly_info": (I, [VP, C.POINTER(L), C.POINTER(C.c_uint)]),
+    "hz_dly_set_split": (I, [VP, I]),
+    "hz_dly_set_stream": (I, [VP, VP]),
+    "hz_dly_synchronize": (I, [VP]),
+    "hz_dly_set_target_groups": (I, [VP, I]),
+    "hz_dly_profile": (I, [VP, I]),
+    "hz_dly_profile_read": (I, [VP, PD, C.POINTER(L)]),
 }
 
 

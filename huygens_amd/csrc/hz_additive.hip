@@ -38,7 +38,6 @@ constexpr int kTile = 64 * kL;
 constexpr int kWaves = 8;
 constexpr int kMaxPerWave = 64;
 constexpr int kPad = 66;
-constexpr double kTwoPi = 6.283185307179586476925286766559;
 
 // per-partial record (depends only on the target frequency and the output weight):
 // A = f_target/SR (cycles/sample), c (output weight), W1 = e^{2 pi i A},

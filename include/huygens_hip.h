@@ -179,6 +179,35 @@ int hz_bowl_set_target_groups(hz_bowl* h, int groups);
 int hz_bowl_profile(hz_bowl* h, int enable);
 int hz_bowl_profile_read(hz_bowl* h, double* ms, long* launches);
 
+/* ---- Delay<T> / Delaybank<T,N>  (src/delay.h:10-108 over src/buffer.h:9-86) ----
+ * A Delaybank is N independent Delay<T> lines (the reference's src/delaybank.h:15-54 is a
+ * non-functional stub); Delay<T> is the N = 1 case.  T = double (is_float 0)
+ * or float (1).  Delaybank(uint sparsity, uint time): rings of time+1 samples per line
+ * (delay.h:21-35); time < 2^31 - 1.  Taps are (uint time, T gain) pairs; a zero-time
+ * feedback tap becomes {0,0} (delay.h:48-51, 64-67).  Ring indexing is bit-exact with
+ * buffer.h:40-47, including the uint32 wrap of delays longer than the ring. */
+typedef struct hz_dly hz_dly;
+int hz_dly_create(int lines, unsigned sparsity, unsigned time, int is_float, int device, hz_dly** out);
+int hz_dly_destroy(hz_dly* h);
+/* coefficients(forward, back) of one line (delay.h:37-56); missing taps are zeroed */
+int hz_dly_coefficients(hz_dly* h, int line, const unsigned* fwd_time, const double* fwd_gain, int nf,
+                        const unsigned* back_time, const double* back_gain, int nb);
+int hz_dly_modulate_forward(hz_dly* h, int line, unsigned n, unsigned time, double gain); /* 59-60 */
+int hz_dly_modulate_back(hz_dly* h, int line, unsigned n, unsigned time, double gain);    /* 63-68 */
+/* n x { y_k = line_k(x); tick(); } for every line (delay.h:71-97).  Samples are T.
+ * in: mono [n] (in_per_line 0) or line-major [N][n]; out: line-major [N][n] (mix 0) or
+ * the mixdown sum_k y_k / N, summed in line order in T (mix 1). */
+int hz_dly_process(hz_dly* h, const void* in, void* out, size_t n, int in_per_line, int mix);
+int hz_dly_process_device(hz_dly* h, const void* d_in, void* d_out, size_t n, int in_per_line, int mix);
+int hz_dly_origin(hz_dly* h, unsigned* origin);            /* Buffer::origin after the last call */
+int hz_dly_info(hz_dly* h, long* chunk, unsigned* size);   /* sub-block length (-1: unbounded), ring size */
+int hz_dly_set_split(hz_dly* h, int mode);                 /* 0 auto, 1 workgroup per line, 2 launch per sub-block */
+int hz_dly_set_stream(hz_dly* h, void* hip_stream);
+int hz_dly_synchronize(hz_dly* h);
+int hz_dly_set_target_groups(hz_dly* h, int groups);
+int hz_dly_profile(hz_dly* h, int enable);
+int hz_dly_profile_read(hz_dly* h, double* ms, long* launches);
+
 #ifdef __cplusplus
 }
 #endif

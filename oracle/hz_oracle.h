@@ -91,6 +91,17 @@ void      orc_bowl_trigger(orc_bowl* b);
 int       orc_bowl_fill(orc_bowl* b, float* buffer, long bsize);
 void      orc_bowl_render(orc_bowl* b, double* out, long n);
 
+/* ---- Delay<T> / Delaybank<T,N> (src/delay.h:10-108, src/buffer.h:9-86) ---- */
+typedef struct orc_dly orc_dly;
+orc_dly* orc_dly_create(int lines, unsigned sparsity, unsigned time, int is_float);
+void     orc_dly_destroy(orc_dly* b);
+void     orc_dly_coefficients(orc_dly* b, int line, const unsigned* ft, const double* fg, int nf,
+                              const unsigned* bt, const double* bg, int nb);
+void     orc_dly_modulate_forward(orc_dly* b, int line, unsigned n, unsigned t, double g);
+void     orc_dly_modulate_back(orc_dly* b, int line, unsigned n, unsigned t, double g);
+void     orc_dly_process(orc_dly* b, const void* in, void* out, long n, int in_per_line, int mix);
+unsigned orc_dly_origin(orc_dly* b);
+
 /* distortion functors (tests/filterbank.cpp:158-176, src/wave.h:150) */
 double orc_dist(int id, double v, double param);
 
