@@ -10,5 +10,6 @@ from .oscbank import Oscbank  # noqa: F401
 from .additive import Additive, Sinusoids  # noqa: F401
 from .bowl import Bowl  # noqa: F401
 from .delay import Delay, Delaybank  # noqa: F401
+from .stft import Cosine, Fourier, StaticSTFT  # noqa: F401
 
-__all__ = ["HZError", "load", "header_symbols", "Filterbank", "Oscbank", "Additive", "Sinusoids", "Bowl", "Delay", "Delaybank"]
+__all__ = ["HZError", "load", "header_symbols", "Filterbank", "Oscbank", "Additive", "Sinusoids", "Bowl", "Delay", "Delaybank", "Fourier", "StaticSTFT", "Cosine"]

@@ -144,6 +144,23 @@ _SIGS = {
     "hz_dly_set_target_groups": (I, [VP, I]),
     "hz_dly_profile": (I, [VP, I]),
     "hz_dly_profile_read": (I, [VP, PD, C.POINTER(L)]),
+    "hz_stft_create": (I, [I, I, I, I, D, D, I, C.POINTER(VP)]),
+    "hz_stft_destroy": (I, [VP]),
+    "hz_stft_set_processor": (I, [VP, VP]),
+    "hz_stft_process_block": (I, [VP, PD, PD, PD, PD, SZ]),
+    "hz_stft_process_block_device": (I, [VP, VP, VP, VP, VP, SZ]),
+    "hz_stft_frames": (I, [VP, C.POINTER(L), C.POINTER(L)]),
+    "hz_stft_set_stream": (I, [VP, VP]),
+    "hz_stft_synchronize": (I, [VP]),
+    "hz_stft_profile": (I, [VP, I]),
+    "hz_stft_profile_read": (I, [VP, PD, PD, C.POINTER(L)]),
+    "hz_dct_create": (I, [I, I, C.POINTER(VP)]),
+    "hz_dct_destroy": (I, [VP]),
+    "hz_dct_buffers": (I, [VP, C.POINTER(PD), C.POINTER(PD)]),
+    "hz_dct_forward": (I, [VP]),
+    "hz_dct_backward": (I, [VP]),
+    "hz_dct_forward_device": (I, [VP, VP, VP, I]),
+    "hz_dct_backward_device": (I, [VP, VP, VP, I]),
 }
 
 

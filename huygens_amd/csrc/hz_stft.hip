@@ -1,0 +1,800 @@
+// hz_stft.hip -- Fourier / StaticSTFT overlap-add engines and Cosine (DCT) for MI355X.
+//
+// Replaces src/fourier.h:50-194 (Fourier, halfhann windows, processor callback),
+// src/staticSTFT.h:10-177 (hann windows, built-in gate) and src/fourier.h:197-234 (Cosine).
+//
+// The reference runs a per-sample state machine over 2*laps slots (write() then read()
+// per sample).  Its schedule has a closed form: frame f = c*2*laps + i of
+// slot i covers input [s, s+N-1], s = stride*i + c*(2N-1), and emits its IFFT sample k,
+// weighted by w(k/N), at t = s+N-1+k; frames are ordered by completion time, so the
+// frames completing inside a block are a contiguous range [f_lo, f_hi).  A block is:
+//   1. stage the block's input behind the previous N-1 samples (history);
+//   2. one workgroup per completing frame: window -> FFT -> processor -> IFFT entirely in
+//      LDS (bit-reversed spectrum between the two transforms, hz_fft.h), frame output to a
+//      ring of R frame buffers in HBM;
+//   3. overlap-add: one thread per output sample sums the (<= 2 laps) reading slots in slot
+//      order, in double-double (the reference accumulates in long double), and divides by
+//      the int N*laps/2.
+// Processors: identity, the StaticSTFT gate (staticSTFT.h:99-128), the spectral.cpp 625
+// gate (tests/spectral.cpp:32-72), the Hilbert half-band (tests/SFML/hilbert.cpp:37-49) as
+// device code; any other host function pointer runs per frame, in frame order, on the host
+// between a forward-only and an inverse-only kernel, with each slot's `out` buffer kept
+// between frames as in the reference (fourier.h:57-59).
+//
+// Cosine: REDFT10 (DCT-II) and REDFT01 (DCT-III) through one complex FFT of length N
+// (Makhoul's even/odd reordering), in LDS, batched one transform per workgroup.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "hz_common.h"
+#include "hz_fft.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxN = 8192;          // complex FP64 frame fully resident in LDS (128 KB)
+constexpr long kChunk = 1L << 18;    // samples per internal block (bounds the frame ring)
+
+struct StftArgs {
+    const double2* x;     // history: x[k] = input at time T0 - (N-1) + k
+    double2* fo;          // frame-output ring [R][N]
+    double2* spec;        // host-processor path: spectra [frames][N] (natural order)
+    const double* win;    // [N]
+    const double2* tw;    // [N/2]  e^{-2 pi i k/N}
+    long f_lo, T0;
+    int N, lg, laps, stride, R;
+    double p0, p1;
+};
+
+__device__ __forceinline__ long frame_start(long f, int laps, int stride, int N) {
+    const long c = f / (2 * laps);
+    const int i = (int)(f - c * 2 * laps);
+    return (long)stride * i + c * (2L * N - 1);
+}
+
+// block-wide sum (wave64 shuffles + LDS across waves); all threads get the result
+__device__ __forceinline__ double block_sum(double v, double* scratch) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) scratch[wave] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += scratch[w];
+    return s;
+}
+
+__device__ __forceinline__ void block_sum_dd(double& hi, double& lo, double* scratch) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const double oh = __shfl_xor(hi, o, 64), ol = __shfl_xor(lo, o, 64);
+        hz::dd_add(hi, lo, oh);
+        hz::dd_add(hi, lo, ol);
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) {
+        scratch[2 * wave] = hi;
+        scratch[2 * wave + 1] = lo;
+    }
+    __syncthreads();
+    double h = 0.0, l = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        hz::dd_add(h, l, scratch[2 * w]);
+        hz::dd_add(h, l, scratch[2 * w + 1]);
+    }
+    hi = h;
+    lo = l;
+}
+
+// processors on the bit-reversed spectrum in LDS
+template <int PROC>
+__device__ __forceinline__ void apply_proc(double* re, double* im, int N, int lg, double p0, double p1,
+                                           double* scratch) {
+#pragma clang fp contract(off)
+    if constexpr (PROC == HZ_PROC_STATIC_GATE) {   // staticSTFT.h:99-128
+        double part = 0.0;
+        for (int p = threadIdx.x; p < N; p += blockDim.x) part += sqrt(re[p] * re[p] + im[p] * im[p]) / N;
+        const double average = block_sum(part, scratch);
+        const double thr = p0 * average * average;
+        for (int p = threadIdx.x; p < N; p += blockDim.x) {
+            const double b0 = re[p], b1 = im[p];
+            if (b0 * b0 + b1 * b1 < thr) {
+                re[p] = b0 * p1;
+                im[p] = b1 * p1;
+            }
+        }
+    } else if constexpr (PROC == HZ_PROC_GATE_KEEP) {   // tests/spectral.cpp:32-72
+        double hi = 0.0, lo = 0.0;
+        for (int p = threadIdx.x; p < N; p += blockDim.x) hz::dd_add(hi, lo, hypot(re[p], im[p]));
+        block_sum_dd(hi, lo, scratch);
+        // average = sum / N (long double in the reference); thr = p0 * average^2
+        const double q = hi / N;
+        const double avg = q + (fma(-q, (double)N, hi) + lo) / N;
+        const double thr = p0 * avg * avg;
+        for (int p = threadIdx.x; p < N; p += blockDim.x) {
+            const double nrm = re[p] * re[p] + im[p] * im[p];
+            if (!(nrm > thr)) {
+                re[p] = 0.0;
+                im[p] = 0.0;
+            }
+        }
+    } else if constexpr (PROC == HZ_PROC_HILBERT) {   // bins k < N/2 kept; k = bitrev(p)
+        for (int p = threadIdx.x; p < N; p += blockDim.x)
+            if (p & 1) {
+                re[p] = 0.0;
+                im[p] = 0.0;
+            }
+    }
+    (void)lg;
+}
+
+// MODE 0: fused (window, FFT, device processor, IFFT -> ring)
+// MODE 1: forward only (window, FFT -> spec, natural order)
+// MODE 2: inverse only (spec -> IFFT -> ring)
+template <int PROC, int MODE>
+__global__ __launch_bounds__(kThreads) void stft_frame_kernel(StftArgs a) {
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int N = a.N;
+    double* re = lds;
+    double* im = lds + N;
+    double* scratch = lds + 2 * N;
+    const long f = a.f_lo + blockIdx.x;
+    if constexpr (MODE != 2) {
+        const long off = frame_start(f, a.laps, a.stride, N) - a.T0 + (N - 1);
+        for (int k = threadIdx.x; k < N; k += blockDim.x) {
+            const double2 v = a.x[off + k];
+            const double w = a.win[k];
+            re[k] = w * v.x;   // fourier.h:110-112: window * real, window * imag
+            im[k] = w * v.y;
+        }
+        __syncthreads();
+        hz::lds_fft_fwd(re, im, N, a.lg, a.tw);
+        if constexpr (MODE == 1) {
+            double2* sp = a.spec + (long)blockIdx.x * N;
+            for (int p = threadIdx.x; p < N; p += blockDim.x) sp[hz::bitrev(p, a.lg)] = make_double2(re[p], im[p]);
+            return;
+        }
+        apply_proc<PROC>(re, im, N, a.lg, a.p0, a.p1, scratch);
+        __syncthreads();
+    } else {
+        const double2* sp = a.spec + (long)blockIdx.x * N;
+        for (int p = threadIdx.x; p < N; p += blockDim.x) {
+            const double2 v = sp[hz::bitrev(p, a.lg)];
+            re[p] = v.x;
+            im[p] = v.y;
+        }
+        __syncthreads();
+    }
+    hz::lds_fft_inv(re, im, N, a.lg, a.tw);
+    double2* out = a.fo + (f % a.R) * N;
+    for (int k = threadIdx.x; k < N; k += blockDim.x) out[k] = make_double2(re[k], im[k]);
+}
+
+struct OlaArgs {
+    const double2* fo;
+    const double* win;
+    double* out_re;
+    double* out_im;
+    long T0, n;
+    int N, laps, stride, R;
+};
+
+__global__ __launch_bounds__(256) void stft_ola_kernel(OlaArgs a) {
+    const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= a.n) return;
+    const long t = a.T0 + j;
+    const long P = 2L * a.N - 1;
+    const long u0 = t - (a.N - 1);
+    double rh = 0.0, rl = 0.0, ih = 0.0, il = 0.0;
+    if (u0 >= 0) {
+        long c = u0 / P;
+        long r = u0 - c * P;
+        for (int i = 0; i < 2 * a.laps; ++i) {   // fourier.h:153-172, slot order
+            if (i) {
+                r -= a.stride;
+                while (r < 0) {
+                    r += P;
+                    --c;
+                }
+            }
+            if (c < 0) break;
+            if (r >= a.N) continue;
+            const long f = c * 2 * a.laps + i;
+            const double2 v = a.fo[(f % a.R) * a.N + r];
+            const double w = a.win[r];
+            hz::dd_add(rh, rl, w * v.x);
+            hz::dd_add(ih, il, w * v.y);
+        }
+    }
+    const double D = (double)(a.N * a.laps / 2);   // int expression, fourier.h:174-175
+    double q = rh / D;
+    q += (fma(-q, D, rh) + rl) / D;
+    a.out_re[j] = q;
+    if (a.out_im) {
+        double qi = ih / D;
+        qi += (fma(-qi, D, ih) + il) / D;
+        a.out_im[j] = qi;
+    }
+}
+
+__global__ void stft_stage_kernel(const double* __restrict__ re, const double* __restrict__ im, long n,
+                                  double2* __restrict__ dst) {
+    const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) dst[j] = make_double2(re[j], im ? im[j] : 0.0);
+}
+
+__global__ void copy_c_kernel(const double2* __restrict__ src, long n, double2* __restrict__ dst) {
+    const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) dst[j] = src[j];
+}
+
+// ---- Cosine: REDFT10 / REDFT01 via a length-N complex FFT (one workgroup per transform)
+__global__ __launch_bounds__(kThreads) void dct2_kernel(const double* __restrict__ x, double* __restrict__ y, int N,
+                                                        int lg, const double2* __restrict__ tw,
+                                                        const double2* __restrict__ rot) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* re = lds;
+    double* im = lds + N;
+    const double* xb = x + (long)blockIdx.x * N;
+    double* yb = y + (long)blockIdx.x * N;
+    for (int k = threadIdx.x; k < N / 2; k += blockDim.x) {   // v[k] = x[2k], v[N-1-k] = x[2k+1]
+        re[k] = xb[2 * k];
+        re[N - 1 - k] = xb[2 * k + 1];
+        im[k] = 0.0;
+        im[N - 1 - k] = 0.0;
+    }
+    __syncthreads();
+    hz::lds_fft_fwd(re, im, N, lg, tw);
+    for (int p = threadIdx.x; p < N; p += blockDim.x) {   // Y_k = 2 Re(V_k e^{-i pi k/2N})
+        const int k = hz::bitrev(p, lg);
+        const double2 w = rot[k];
+        yb[k] = 2.0 * (re[p] * w.x - im[p] * w.y);
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void dct3_kernel(const double* __restrict__ x, double* __restrict__ y, int N,
+                                                        int lg, const double2* __restrict__ tw,
+                                                        const double2* __restrict__ rot) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* re = lds;
+    double* im = lds + N;
+    const double* xb = x + (long)blockIdx.x * N;
+    double* yb = y + (long)blockIdx.x * N;
+    for (int p = threadIdx.x; p < N; p += blockDim.x) {   // V_j = e^{i pi j/2N} (x_j - i x_{N-j})
+        const int j = hz::bitrev(p, lg);
+        const double a = xb[j], b = j ? xb[N - j] : 0.0;
+        const double2 w = rot[j];   // e^{-i pi j / 2N}; use its conjugate
+        re[p] = a * w.x + b * (-w.y);
+        im[p] = -a * w.y - b * w.x;
+    }
+    __syncthreads();
+    hz::lds_fft_inv(re, im, N, lg, tw);
+    for (int k = threadIdx.x; k < N / 2; k += blockDim.x) {
+        yb[2 * k] = re[k];
+        yb[2 * k + 1] = re[N - 1 - k];
+    }
+}
+
+int ilog2(int N) {
+    int lg = 0;
+    while ((1 << lg) < N) ++lg;
+    return lg;
+}
+
+bool pow2(int N) { return N >= 4 && (N & (N - 1)) == 0; }
+
+std::vector<double2> twiddles(int N) {
+    std::vector<double2> tw(N / 2);
+    const long double pi = acosl(-1.0L);
+    for (int k = 0; k < N / 2; ++k) {
+        const long double a = -2.0L * pi * k / N;
+        tw[k] = make_double2((double)cosl(a), (double)sinl(a));
+    }
+    return tw;
+}
+
+}  // namespace
+
+struct hz_stft {
+    int N = 0, laps = 0, stride = 0, lg = 0, window = 0, proc = 0, device = 0, R = 0;
+    double p0 = 0, p1 = 0;
+    hz_stft_proc host_proc = nullptr;
+    long T = 0;        // samples processed
+    long frames = 0;   // frames completed
+    double* d_win = nullptr;
+    double2 *d_tw = nullptr, *d_fo = nullptr, *d_x[2] = {nullptr, nullptr}, *d_spec = nullptr;
+    int xcur = 0;
+    size_t x_cap = 0, spec_cap = 0;
+    double *d_in = nullptr, *d_out = nullptr;
+    size_t io_cap = 0;
+    std::vector<double2> h_spec, h_out;   // host-processor path: spectra + per-slot out buffers
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    bool prof = false;
+    std::vector<hipEvent_t> ev;
+    size_t ev_used = 0;
+    long launches = 0;
+};
+
+namespace {
+
+int stft_check(hz_stft* h) {
+    if (!h) {
+        hz::set_error("null hz_stft handle");
+        return HZ_E_INVALID;
+    }
+    HZ_TRY_HIP(hipSetDevice(h->device));
+    return HZ_OK;
+}
+
+// number of frames with completion time e_f = s_f + N - 1 < T
+long frames_before(const hz_stft* h, long T) {
+    const long P = 2L * h->N - 1;
+    long cnt = 0;
+    for (int i = 0; i < 2 * h->laps; ++i) {
+        const long lim = T - (h->N - 1) - (long)h->stride * i;   // c*P < lim
+        if (lim > 0) cnt += (lim + P - 1) / P;
+    }
+    return cnt;
+}
+
+template <int PROC, int MODE>
+void launch_frames(hz_stft* h, const StftArgs& a, long nf, size_t lds) {
+    hipLaunchKernelGGL((stft_frame_kernel<PROC, MODE>), dim3((unsigned)nf), dim3(kThreads), lds, h->stream, a);
+}
+
+int frames_fused(hz_stft* h, const StftArgs& a, long nf, size_t lds) {
+    switch (h->proc) {
+    case HZ_PROC_STATIC_GATE: launch_frames<HZ_PROC_STATIC_GATE, 0>(h, a, nf, lds); break;
+    case HZ_PROC_GATE_KEEP: launch_frames<HZ_PROC_GATE_KEEP, 0>(h, a, nf, lds); break;
+    case HZ_PROC_HILBERT: launch_frames<HZ_PROC_HILBERT, 0>(h, a, nf, lds); break;
+    default: launch_frames<HZ_PROC_IDENTITY, 0>(h, a, nf, lds); break;
+    }
+    HZ_TRY_HIP(hipGetLastError());
+    return HZ_OK;
+}
+
+int ensure_dev(void** p, size_t* cap, size_t bytes) {
+    if (bytes <= *cap) return HZ_OK;
+    if (*p) HZ_TRY_HIP(hipFree(*p));
+    *p = nullptr;
+    HZ_TRY_HIP(hipMalloc(p, bytes));
+    *cap = bytes;
+    return HZ_OK;
+}
+
+int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore, double* d_oim, long n) {
+    const int N = h->N;
+    // history buffers hold N-1 + n samples
+    const size_t need = sizeof(double2) * (size_t)(N - 1 + n);
+    if (need > h->x_cap) {
+        double2* nb[2] = {nullptr, nullptr};
+        HZ_TRY_HIP(hipMalloc(&nb[0], need));
+        HZ_TRY_HIP(hipMalloc(&nb[1], need));
+        if (h->d_x[h->xcur])
+            HZ_TRY_HIP(hipMemcpyAsync(nb[0], h->d_x[h->xcur], sizeof(double2) * (N - 1), hipMemcpyDeviceToDevice,
+                                      h->stream));
+        else
+            HZ_TRY_HIP(hipMemsetAsync(nb[0], 0, sizeof(double2) * (N - 1), h->stream));
+        HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+        for (double2* p : h->d_x)
+            if (p) HZ_TRY_HIP(hipFree(p));
+        h->d_x[0] = nb[0];
+        h->d_x[1] = nb[1];
+        h->xcur = 0;
+        h->x_cap = need;
+    }
+    double2* xc = h->d_x[h->xcur];
+    double2* xn = h->d_x[h->xcur ^ 1];
+    hipLaunchKernelGGL(stft_stage_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, d_re, d_im, n,
+                       xc + (N - 1));
+    HZ_TRY_HIP(hipGetLastError());
+
+    hipEvent_t* e = nullptr;
+    if (h->prof) {
+        if (h->ev_used + 3 > h->ev.size())
+            for (int q = 0; q < 96; ++q) {
+                hipEvent_t ne;
+                HZ_TRY_HIP(hipEventCreate(&ne));
+                h->ev.push_back(ne);
+            }
+        e = &h->ev[h->ev_used];
+        h->ev_used += 3;
+        HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
+    }
+    const long f_lo = frames_before(h, h->T), f_hi = frames_before(h, h->T + n);
+    const long nf = f_hi - f_lo;
+    StftArgs a;
+    a.x = xc;
+    a.fo = h->d_fo;
+    a.spec = h->d_spec;
+    a.win = h->d_win;
+    a.tw = h->d_tw;
+    a.f_lo = f_lo;
+    a.T0 = h->T;
+    a.N = N;
+    a.lg = h->lg;
+    a.laps = h->laps;
+    a.stride = h->stride;
+    a.R = h->R;
+    a.p0 = h->p0;
+    a.p1 = h->p1;
+    const size_t lds = sizeof(double) * (2 * (size_t)N + 2 * (kThreads / 64));
+    if (nf > 0) {
+        if (h->proc != HZ_PROC_HOST) {
+            HZ_TRY(frames_fused(h, a, nf, lds));
+        } else {
+            HZ_TRY(ensure_dev((void**)&h->d_spec, &h->spec_cap, sizeof(double2) * (size_t)nf * N));
+            a.spec = h->d_spec;
+            launch_frames<HZ_PROC_IDENTITY, 1>(h, a, nf, lds);
+            HZ_TRY_HIP(hipGetLastError());
+            h->h_spec.resize((size_t)nf * N);
+            HZ_TRY_HIP(hipMemcpyAsync(h->h_spec.data(), h->d_spec, sizeof(double2) * (size_t)nf * N,
+                                      hipMemcpyDeviceToHost, h->stream));
+            HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+            for (long f = f_lo; f < f_hi; ++f) {   // frame order == the reference's order
+                const int slot = (int)(f % (2 * h->laps));
+                double2* so = &h->h_out[(size_t)slot * N];
+                double2* sp = &h->h_spec[(size_t)(f - f_lo) * N];
+                h->host_proc((const double*)sp, (double*)so);
+                std::memcpy(sp, so, sizeof(double2) * N);
+            }
+            HZ_TRY_HIP(hipMemcpyAsync(h->d_spec, h->h_spec.data(), sizeof(double2) * (size_t)nf * N,
+                                      hipMemcpyHostToDevice, h->stream));
+            launch_frames<HZ_PROC_IDENTITY, 2>(h, a, nf, lds);
+            HZ_TRY_HIP(hipGetLastError());
+        }
+    }
+    if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
+    OlaArgs o;
+    o.fo = h->d_fo;
+    o.win = h->d_win;
+    o.out_re = d_ore;
+    o.out_im = d_oim;
+    o.T0 = h->T;
+    o.n = n;
+    o.N = N;
+    o.laps = h->laps;
+    o.stride = h->stride;
+    o.R = h->R;
+    hipLaunchKernelGGL(stft_ola_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, o);
+    HZ_TRY_HIP(hipGetLastError());
+    if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
+    // history for the next block: the last N-1 samples of [T0-N+1, T0+n)
+    hipLaunchKernelGGL(copy_c_kernel, dim3((unsigned)((N - 1 + 255) / 256)), dim3(256), 0, h->stream,
+                       (const double2*)(xc + n), (long)(N - 1), xn);
+    HZ_TRY_HIP(hipGetLastError());
+    h->xcur ^= 1;
+    h->T += n;
+    h->frames = f_hi;
+    h->launches += h->prof ? 1 : 0;
+    return HZ_OK;
+}
+
+int stft_run(hz_stft* h, const double* d_re, const double* d_im, double* d_ore, double* d_oim, long n) {
+    for (long o = 0; o < n; o += kChunk) {
+        const long m = std::min(kChunk, n - o);
+        HZ_TRY(stft_block(h, d_re + o, d_im ? d_im + o : nullptr, d_ore + o, d_oim ? d_oim + o : nullptr, m));
+    }
+    return HZ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hz_stft_create(int N, int laps, int window, int proc, double p0, double p1, int device, hz_stft** out) {
+    if (!out || !pow2(N) || N > kMaxN || laps <= 0 || laps > N || (window != HZ_WIN_HALFHANN && window != HZ_WIN_HANN) ||
+        proc < HZ_PROC_IDENTITY || proc > HZ_PROC_HOST) {
+        hz::set_error("hz_stft_create: invalid arguments (N must be a power of two in [4, %d])", kMaxN);
+        return HZ_E_INVALID;
+    }
+    *out = nullptr;
+    HZ_TRY(hz::select_device(device));
+    hz_stft* h = new (std::nothrow) hz_stft();
+    if (!h) return HZ_E_ALLOC;
+    h->N = N;
+    h->laps = laps;
+    h->stride = N / laps;
+    h->lg = ilog2(N);
+    h->window = window;
+    h->proc = proc;
+    h->p0 = p0;
+    h->p1 = p1;
+    h->device = device;
+    // frames completing inside one internal block, plus those still being read
+    const long P = 2L * N - 1;
+    h->R = (int)((kChunk + P - 1) / P * 2 * laps + 2 * laps + 2);
+    h->h_out.assign((size_t)2 * laps * N, make_double2(0.0, 0.0));
+    std::vector<double> win(N);
+    for (int k = 0; k < N; ++k) {   // src/wave.h:148-149 with the truncated PI, in double
+        const double p = k / (double)N;
+        const double hann = 0.5 * (1 - cos(2 * hz::kPI * p));
+        win[k] = window == HZ_WIN_HANN ? hann : sqrt(hann);
+    }
+    const std::vector<double2> tw = twiddles(N);
+    bool ok = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipMalloc(&h->d_win, sizeof(double) * N) == hipSuccess;
+    ok = ok && hipMalloc(&h->d_tw, sizeof(double2) * (N / 2)) == hipSuccess;
+    ok = ok && hipMalloc(&h->d_fo, sizeof(double2) * (size_t)h->R * N) == hipSuccess;
+    ok = ok && hipMemcpy(h->d_win, win.data(), sizeof(double) * N, hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMemcpy(h->d_tw, tw.data(), sizeof(double2) * (N / 2), hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMemset(h->d_fo, 0, sizeof(double2) * (size_t)h->R * N) == hipSuccess;
+    if (!ok) {
+        hz::set_error("hz_stft_create: device allocation failed");
+        if (h->stream) (void)hipStreamDestroy(h->stream);
+        for (void* p : {(void*)h->d_win, (void*)h->d_tw, (void*)h->d_fo})
+            if (p) (void)hipFree(p);
+        delete h;
+        return HZ_E_ALLOC;
+    }
+    h->own_stream = true;
+    static bool attr = false;
+    if (!attr) {   // 2N doubles of LDS per workgroup (128 KB at N = 8192)
+        const int lds = (int)(sizeof(double) * (2 * kMaxN + 2 * (kThreads / 64)));
+        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_IDENTITY, 0>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_STATIC_GATE, 0>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_GATE_KEEP, 0>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_HILBERT, 0>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_IDENTITY, 1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_IDENTITY, 2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        (void)hipFuncSetAttribute((const void*)dct2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        (void)hipFuncSetAttribute((const void*)dct3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr = true;
+    }
+    *out = h;
+    return HZ_OK;
+}
+
+int hz_stft_destroy(hz_stft* h) {
+    if (!h) return HZ_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (void* p : {(void*)h->d_win, (void*)h->d_tw, (void*)h->d_fo, (void*)h->d_x[0], (void*)h->d_x[1],
+                    (void*)h->d_spec, (void*)h->d_in, (void*)h->d_out})
+        if (p) (void)hipFree(p);
+    for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return HZ_OK;
+}
+
+int hz_stft_set_processor(hz_stft* h, hz_stft_proc fn) {
+    if (!h || !fn) {
+        hz::set_error("hz_stft_set_processor: null argument");
+        return HZ_E_INVALID;
+    }
+    h->host_proc = fn;
+    h->proc = HZ_PROC_HOST;
+    return HZ_OK;
+}
+
+int hz_stft_process_block_device(hz_stft* h, const double* d_re, const double* d_im, double* d_out_re,
+                                 double* d_out_im, size_t n) {
+    HZ_TRY(stft_check(h));
+    if (n == 0) return HZ_OK;
+    if (!d_re || !d_out_re) return HZ_E_INVALID;
+    if (h->proc == HZ_PROC_HOST && !h->host_proc) {
+        hz::set_error("hz_stft: HZ_PROC_HOST without hz_stft_set_processor");
+        return HZ_E_INVALID;
+    }
+    return stft_run(h, d_re, d_im, d_out_re, d_out_im, (long)n);
+}
+
+int hz_stft_process_block(hz_stft* h, const double* re, const double* im, double* out_re, double* out_im,
+                          size_t n) {
+    HZ_TRY(stft_check(h));
+    if (n == 0) return HZ_OK;
+    if (!re || !out_re) return HZ_E_INVALID;
+    const size_t bytes = sizeof(double) * n * 2;
+    if (bytes > h->io_cap) {
+        for (double** p : {&h->d_in, &h->d_out})
+            if (*p) HZ_TRY_HIP(hipFree(*p));
+        h->d_in = h->d_out = nullptr;
+        HZ_TRY_HIP(hipMalloc(&h->d_in, bytes));
+        HZ_TRY_HIP(hipMalloc(&h->d_out, bytes));
+        h->io_cap = bytes;
+    }
+    HZ_TRY_HIP(hipMemcpyAsync(h->d_in, re, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
+    if (im) HZ_TRY_HIP(hipMemcpyAsync(h->d_in + n, im, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
+    HZ_TRY(hz_stft_process_block_device(h, h->d_in, im ? h->d_in + n : nullptr, h->d_out, out_im ? h->d_out + n : nullptr,
+                                        n));
+    HZ_TRY_HIP(hipMemcpyAsync(out_re, h->d_out, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
+    if (out_im)
+        HZ_TRY_HIP(hipMemcpyAsync(out_im, h->d_out + n, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+int hz_stft_frames(hz_stft* h, long* frames, long* samples) {
+    if (!h) return HZ_E_INVALID;
+    if (frames) *frames = h->frames;
+    if (samples) *samples = h->T;
+    return HZ_OK;
+}
+
+int hz_stft_set_stream(hz_stft* h, void* stream) {
+    HZ_TRY(stft_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    if (h->own_stream) HZ_TRY_HIP(hipStreamDestroy(h->stream));
+    h->stream = (hipStream_t)stream;
+    h->own_stream = false;
+    return HZ_OK;
+}
+
+int hz_stft_synchronize(hz_stft* h) {
+    HZ_TRY(stft_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+int hz_stft_profile(hz_stft* h, int enable) {
+    HZ_TRY(stft_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    h->prof = enable != 0;
+    h->ev_used = 0;
+    h->launches = 0;
+    return HZ_OK;
+}
+
+int hz_stft_profile_read(hz_stft* h, double* frame_ms, double* ola_ms, long* blocks) {
+    HZ_TRY(stft_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    double fm = 0.0, om = 0.0;
+    for (size_t i = 0; i + 2 < h->ev_used; i += 3) {
+        float t0 = 0.f, t1 = 0.f;
+        HZ_TRY_HIP(hipEventElapsedTime(&t0, h->ev[i], h->ev[i + 1]));
+        HZ_TRY_HIP(hipEventElapsedTime(&t1, h->ev[i + 1], h->ev[i + 2]));
+        fm += t0;
+        om += t1;
+    }
+    if (frame_ms) *frame_ms = fm;
+    if (ola_ms) *ola_ms = om;
+    if (blocks) *blocks = h->launches;
+    h->ev_used = 0;
+    h->launches = 0;
+    return HZ_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Cosine
+// ---------------------------------------------------------------------------
+struct hz_dct {
+    int N = 0, lg = 0, device = 0;
+    double *h_in = nullptr, *h_out = nullptr;   // pinned, owned (fourier.h:201-207)
+    double *d_a = nullptr, *d_b = nullptr;
+    double2 *d_tw = nullptr, *d_rot = nullptr;
+    hipStream_t stream = nullptr;
+};
+
+namespace {
+
+int dct_launch(hz_dct* h, const double* d_x, double* d_y, int batch, int kind) {
+    const size_t lds = sizeof(double) * 2 * (size_t)h->N;
+    if (kind == 10)
+        hipLaunchKernelGGL(dct2_kernel, dim3((unsigned)batch), dim3(kThreads), lds, h->stream, d_x, d_y, h->N, h->lg,
+                           (const double2*)h->d_tw, (const double2*)h->d_rot);
+    else
+        hipLaunchKernelGGL(dct3_kernel, dim3((unsigned)batch), dim3(kThreads), lds, h->stream, d_x, d_y, h->N, h->lg,
+                           (const double2*)h->d_tw, (const double2*)h->d_rot);
+    HZ_TRY_HIP(hipGetLastError());
+    return HZ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hz_dct_create(int N, int device, hz_dct** out) {
+    if (!out || !pow2(N) || N > kMaxN) {
+        hz::set_error("hz_dct_create: N must be a power of two in [4, %d]", kMaxN);
+        return HZ_E_INVALID;
+    }
+    *out = nullptr;
+    HZ_TRY(hz::select_device(device));
+    hz_dct* h = new (std::nothrow) hz_dct();
+    if (!h) return HZ_E_ALLOC;
+    h->N = N;
+    h->lg = ilog2(N);
+    h->device = device;
+    const std::vector<double2> tw = twiddles(N);
+    std::vector<double2> rot(N);
+    const long double pi = acosl(-1.0L);
+    for (int k = 0; k < N; ++k) {
+        const long double a = -pi * k / (2.0L * N);
+        rot[k] = make_double2((double)cosl(a), (double)sinl(a));
+    }
+    bool ok = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipHostMalloc(&h->h_in, sizeof(double) * N) == hipSuccess;
+    ok = ok && hipHostMalloc(&h->h_out, sizeof(double) * N) == hipSuccess;
+    ok = ok && hipMalloc(&h->d_a, sizeof(double) * N) == hipSuccess;
+    ok = ok && hipMalloc(&h->d_b, sizeof(double) * N) == hipSuccess;
+    ok = ok && hipMalloc(&h->d_tw, sizeof(double2) * (N / 2)) == hipSuccess;
+    ok = ok && hipMalloc(&h->d_rot, sizeof(double2) * N) == hipSuccess;
+    ok = ok && hipMemcpy(h->d_tw, tw.data(), sizeof(double2) * (N / 2), hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMemcpy(h->d_rot, rot.data(), sizeof(double2) * N, hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) {
+        hz::set_error("hz_dct_create: allocation failed");
+        if (h->stream) (void)hipStreamDestroy(h->stream);
+        for (double* p : {h->h_in, h->h_out})
+            if (p) (void)hipHostFree(p);
+        for (void* p : {(void*)h->d_a, (void*)h->d_b, (void*)h->d_tw, (void*)h->d_rot})
+            if (p) (void)hipFree(p);
+        delete h;
+        return HZ_E_ALLOC;
+    }
+    std::memset(h->h_in, 0, sizeof(double) * N);
+    std::memset(h->h_out, 0, sizeof(double) * N);
+    *out = h;
+    return HZ_OK;
+}
+
+int hz_dct_destroy(hz_dct* h) {
+    if (!h) return HZ_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (double* p : {h->h_in, h->h_out})
+        if (p) (void)hipHostFree(p);
+    for (void* p : {(void*)h->d_a, (void*)h->d_b, (void*)h->d_tw, (void*)h->d_rot})
+        if (p) (void)hipFree(p);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return HZ_OK;
+}
+
+int hz_dct_buffers(hz_dct* h, double** in, double** out) {   // Cosine(N, &in, &out)
+    if (!h) return HZ_E_INVALID;
+    if (in) *in = h->h_in;
+    if (out) *out = h->h_out;
+    return HZ_OK;
+}
+
+int hz_dct_forward(hz_dct* h) {   // REDFT10: in -> out
+    if (!h) return HZ_E_INVALID;
+    HZ_TRY_HIP(hipSetDevice(h->device));
+    HZ_TRY_HIP(hipMemcpyAsync(h->d_a, h->h_in, sizeof(double) * h->N, hipMemcpyHostToDevice, h->stream));
+    HZ_TRY(dct_launch(h, h->d_a, h->d_b, 1, 10));
+    HZ_TRY_HIP(hipMemcpyAsync(h->h_out, h->d_b, sizeof(double) * h->N, hipMemcpyDeviceToHost, h->stream));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+int hz_dct_backward(hz_dct* h) {   // REDFT01: out -> in
+    if (!h) return HZ_E_INVALID;
+    HZ_TRY_HIP(hipSetDevice(h->device));
+    HZ_TRY_HIP(hipMemcpyAsync(h->d_b, h->h_out, sizeof(double) * h->N, hipMemcpyHostToDevice, h->stream));
+    HZ_TRY(dct_launch(h, h->d_b, h->d_a, 1, 1));
+    HZ_TRY_HIP(hipMemcpyAsync(h->h_in, h->d_a, sizeof(double) * h->N, hipMemcpyDeviceToHost, h->stream));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+int hz_dct_forward_device(hz_dct* h, const double* d_in, double* d_out, int batch) {
+    if (!h || !d_in || !d_out || batch < 0) return HZ_E_INVALID;
+    HZ_TRY_HIP(hipSetDevice(h->device));
+    if (batch) HZ_TRY(dct_launch(h, d_in, d_out, batch, 10));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+int hz_dct_backward_device(hz_dct* h, const double* d_in, double* d_out, int batch) {
+    if (!h || !d_in || !d_out || batch < 0) return HZ_E_INVALID;
+    HZ_TRY_HIP(hipSetDevice(h->device));
+    if (batch) HZ_TRY(dct_launch(h, d_in, d_out, batch, 1));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+}  // extern "C"

@@ -208,6 +208,47 @@ int hz_dly_set_target_groups(hz_dly* h, int groups);
 int hz_dly_profile(hz_dly* h, int enable);
 int hz_dly_profile_read(hz_dly* h, double* ms, long* launches);
 
+/* ---- Fourier / StaticSTFT (src/fourier.h:50-194, src/staticSTFT.h:10-177) ----
+ * Fourier(int (*processor)(const complex<double>*, complex<double>*), int N, int laps):
+ *   window HZ_WIN_HALFHANN; StaticSTFT(int N, int laps): window HZ_WIN_HANN with
+ *   HZ_PROC_STATIC_GATE(100, 0.1).  N a power of two in [4, 8192], 1 <= laps <= N.
+ * process_block == n x { write(re[t], im[t]); read(&out_re[t], &out_im[t]); }
+ * (fourier.h:102-177); im / out_im may be NULL (zero imaginary input / discarded). */
+#define HZ_WIN_HALFHANN 0
+#define HZ_WIN_HANN 1
+#define HZ_PROC_IDENTITY 0
+#define HZ_PROC_STATIC_GATE 1 /* p0 = 100, p1 = 0.1: staticSTFT.h:99-128 */
+#define HZ_PROC_GATE_KEEP 2   /* p0 = 625: tests/spectral.cpp:32-72 */
+#define HZ_PROC_HILBERT 3     /* tests/SFML/hilbert.cpp:37-49 */
+#define HZ_PROC_HOST 4        /* host function pointer, per frame, in frame order */
+/* the reference's processor type; complex<double>* passed as interleaved double* */
+typedef int (*hz_stft_proc)(const double* in, double* out);
+typedef struct hz_stft hz_stft;
+int hz_stft_create(int N, int laps, int window, int proc, double p0, double p1, int device, hz_stft** out);
+int hz_stft_destroy(hz_stft* h);
+int hz_stft_set_processor(hz_stft* h, hz_stft_proc fn);
+int hz_stft_process_block(hz_stft* h, const double* re, const double* im, double* out_re, double* out_im, size_t n);
+int hz_stft_process_block_device(hz_stft* h, const double* d_re, const double* d_im, double* d_out_re,
+                                 double* d_out_im, size_t n);
+int hz_stft_frames(hz_stft* h, long* frames, long* samples);
+int hz_stft_set_stream(hz_stft* h, void* hip_stream);
+int hz_stft_synchronize(hz_stft* h);
+int hz_stft_profile(hz_stft* h, int enable);
+int hz_stft_profile_read(hz_stft* h, double* frame_ms, double* ola_ms, long* blocks);
+
+/* ---- Cosine (src/fourier.h:197-234): Cosine(int N, double** in, double** out) ----
+ * forward = FFTW REDFT10 in -> out (DCT-II, unnormalised), backward = REDFT01 out -> in
+ * (DCT-III); the round trip is 2N x identity.  The buffers are pinned host memory owned
+ * by the handle.  N a power of two in [4, 8192]. */
+typedef struct hz_dct hz_dct;
+int hz_dct_create(int N, int device, hz_dct** out);
+int hz_dct_destroy(hz_dct* h);
+int hz_dct_buffers(hz_dct* h, double** in, double** out);
+int hz_dct_forward(hz_dct* h);
+int hz_dct_backward(hz_dct* h);
+int hz_dct_forward_device(hz_dct* h, const double* d_in, double* d_out, int batch);
+int hz_dct_backward_device(hz_dct* h, const double* d_in, double* d_out, int batch);
+
 #ifdef __cplusplus
 }
 #endif

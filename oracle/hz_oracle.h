@@ -102,6 +102,25 @@ void     orc_dly_modulate_back(orc_dly* b, int line, unsigned n, unsigned t, dou
 void     orc_dly_process(orc_dly* b, const void* in, void* out, long n, int in_per_line, int mix);
 unsigned orc_dly_origin(orc_dly* b);
 
+/* ---- Fourier / StaticSTFT / Cosine (src/fourier.h:50-234, src/staticSTFT.h:10-177) ---- */
+#define ORC_PROC_IDENTITY 0
+#define ORC_PROC_STATIC_GATE 1   /* p0 = 100, p1 = 0.1 */
+#define ORC_PROC_GATE_KEEP 2     /* p0 = 625 */
+#define ORC_PROC_HILBERT 3
+#define ORC_PROC_CALLBACK 4
+typedef int (*orc_stft_cb)(const double* in, double* out);
+typedef struct orc_stft orc_stft;
+orc_stft* orc_stft_create(int N, int laps, int window, int proc, double p0, double p1);
+void      orc_stft_set_callback(orc_stft* s, orc_stft_cb cb);
+void      orc_stft_destroy(orc_stft* s);
+void      orc_stft_write(orc_stft* s, double re, double im);
+void      orc_stft_read(orc_stft* s, double* re, double* im);
+void      orc_stft_process_block(orc_stft* s, const double* re, const double* im, double* out_re,
+                                 double* out_im, long n);
+long      orc_stft_frames(orc_stft* s);
+void      orc_dft(const double* x, double* y, int N, int sign);
+void      orc_dct(const double* x, double* y, int N, int kind);
+
 /* distortion functors (tests/filterbank.cpp:158-176, src/wave.h:150) */
 double orc_dist(int id, double v, double param);
 
