@@ -45,9 +45,8 @@ def c2_coefficients(N=N_BANDS, R=R_POLE):
 
 
 def shard_of(rank, world, N=N_BANDS):
-    base, rem = divmod(N, world)
-    begin = rank * base + min(rank, rem)
-    return begin, base + (1 if rank < rem else 0)
+    from huygens_amd.shard import shard_of as _shard_of
+    return _shard_of(rank, world, N)
 
 
 def cpu_baseline(fwd, back, seconds_target=1.5):

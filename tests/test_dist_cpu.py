@@ -1,0 +1,57 @@
+"""Multi-rank decomposition on CPU: world_size 2 (and 3) over gloo, one process per rank,
+each rank computing its contiguous shard of units (huygens_amd.shard.shard_of) and the
+partial mixes summed to rank 0 by dist.reduce -- the same decomposition bench.py runs over
+RCCL on one GPU per rank."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from huygens_amd.shard import shard_of
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(kind, world, tmp_path):
+    port = _free_port()
+    out = tmp_path / f"{kind}.json"
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), kind, str(out)],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    for p in procs:
+        o, _ = p.communicate(timeout=240)
+        assert p.returncode == 0, o.decode()[-2000:]
+    return json.loads(out.read_text())
+
+
+@pytest.mark.parametrize("kind", ["filterbank", "oscbank", "bowl", "delaybank"])
+def test_world2_reduce_matches_unsharded(kind, tmp_path):
+    res = _run(kind, 2, tmp_path)
+    assert res["err"] < 1e-12
+    assert sum(c for _, c in res["shards"]) == {"filterbank": 96, "oscbank": 50, "bowl": 40, "delaybank": 6}[kind]
+
+
+def test_world3_uneven(tmp_path):
+    res = _run("filterbank", 3, tmp_path)
+    assert res["err"] < 1e-12
+    assert [c for _, c in res["shards"]] == [32, 32, 32]
+
+
+def test_shard_of():
+    assert [shard_of(r, 3, 10) for r in range(3)] == [(0, 4), (4, 3), (7, 3)]
+    assert [shard_of(r, 8, 4096)[1] for r in range(8)] == [512] * 8
+    assert shard_of(1, 4, 2) == (1, 1) and shard_of(3, 4, 2) == (2, 0)
+    with pytest.raises(ValueError):
+        shard_of(2, 2, 5)
