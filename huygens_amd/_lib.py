@@ -88,6 +88,7 @@ _SIGS = {
     "hz_osc_active_count": (I, [VP, C.POINTER(I)]),
     "hz_osc_fill": (I, [VP, PD, PD, SZ]),
     "hz_osc_fill_device": (I, [VP, VP, VP, SZ]),
+    "hz_osc_mixdown": (I, [VP, PD]),
     "hz_osc_phases": (I, [VP, PD]),
     "hz_osc_set_phases": (I, [VP, PD]),
     "hz_osc_set_stream": (I, [VP, VP]),

@@ -537,6 +537,23 @@ int hz_osc_phases(hz_osc* h, double* z) {
     return HZ_OK;
 }
 
+int hz_osc_mixdown(hz_osc* h, double* mix) {   // oscbank.h:81-90, without advancing
+    HZ_TRY(osc_check(h));
+    if (!mix) return HZ_E_INVALID;
+    std::vector<double> z(2 * (size_t)h->N);
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    HZ_TRY_HIP(hipMemcpy(z.data(), h->d_z, sizeof(double) * z.size(), hipMemcpyDeviceToHost));
+    double re = 0.0, im = 0.0;
+    for (int i = 0; i < h->N; ++i)   // ascending active indices, as `where`
+        if (h->active[i]) {
+            re += z[2 * i];
+            im += z[2 * i + 1];
+        }
+    mix[0] = re;
+    mix[1] = im;
+    return HZ_OK;
+}
+
 int hz_osc_set_phases(hz_osc* h, const double* z) {
     HZ_TRY(osc_check(h));
     if (!z) return HZ_E_INVALID;

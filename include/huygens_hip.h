@@ -116,6 +116,8 @@ int hz_osc_fill(hz_osc* h, double* mix, double* per_band, size_t n);
 int hz_osc_fill_device(hz_osc* h, double* d_mix, double* d_per_band, size_t n);
 /* operator()(): the N phasors (2N doubles, complex interleaved) */
 int hz_osc_phases(hz_osc* h, double* z);
+/* mixdown() of the current phasors (sum over the active set in index order) without a tick */
+int hz_osc_mixdown(hz_osc* h, double* mix);
 int hz_osc_set_phases(hz_osc* h, const double* z);
 int hz_osc_set_stream(hz_osc* h, void* hip_stream);
 int hz_osc_synchronize(hz_osc* h);

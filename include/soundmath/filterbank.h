@@ -1,0 +1,73 @@
+// soundmath/filterbank.h -- drop-in Filterbank<T> (src/filterbank.h:16-188) over the HIP
+// engine.  T = double (the engine's arithmetic).  process() is the GPU path; the
+// per-sample operator()/tick() pair is kept with its caching semantics (a repeated
+// operator() before tick() returns the cached sample) and runs one-sample launches.
+// operator()(T, T(*)(T)) takes a device functor id instead of a host function pointer
+// (HZ_DIST_SOFTCLIP / SATURATE / LIMITER, see huygens_hip.h).
+#pragma once
+
+#include <cstdio>
+
+#include "hz.h"
+
+namespace soundmath {
+
+template <typename T>
+class Filterbank {
+    static_assert(std::is_same<T, double>::value, "the HIP Filterbank computes in double");
+
+public:
+    Filterbank(int order, int N = 1, double k_p = 0.1, double k_g = 1, int device = 0) : N_(N), order_(order) {
+        hz_fb* h = nullptr;
+        detail::check(hz_fb_create(order, N, k_p, k_g, device, &h), "Filterbank");
+        h_ = decltype(h_)(h);
+    }
+    void coefficients(int n, const std::vector<T>& forward, const std::vector<T>& back) {
+        detail::check(hz_fb_coefficients(h_.get(), n, forward.data(), (int)forward.size(), back.data(),
+                                         (int)back.size()),
+                      "Filterbank::coefficients");
+    }
+    void boost(int n, T v) { detail::check(hz_fb_boost(h_.get(), n, v), "Filterbank::boost"); }
+    void boost(const std::vector<T>& v) {
+        detail::check(hz_fb_boost_all(h_.get(), v.data(), (int)v.size()), "Filterbank::boost");
+    }
+    void mix(int n, T v) { detail::check(hz_fb_mix(h_.get(), n, v), "Filterbank::mix"); }
+    void mix(const std::vector<T>& v) {
+        detail::check(hz_fb_mix_all(h_.get(), v.data(), (int)v.size()), "Filterbank::mix");
+    }
+    void open() { detail::check(hz_fb_open(h_.get()), "Filterbank::open"); }
+    void print() { std::printf("Filterbank<double>(order %d, %d bands) on HIP\n", order_, N_); }
+
+    T operator()(T sample) { return sample_with(sample, HZ_DIST_NONE, 0.0); }
+    T operator()(T sample, int dist_id, double param = 0.0) { return sample_with(sample, dist_id, param); }
+    void tick() {
+        if (!computed_) {   // the reference's tick() without operator(): the sample is 0 input
+            T zero = 0, y;
+            detail::check(hz_fb_process(h_.get(), &zero, &y, 1), "Filterbank::tick");
+        }
+        computed_ = false;
+    }
+
+    // n x { out[i] = operator()(in[i]); tick(); }
+    void process(const T* in, T* out, std::size_t n, int dist_id = HZ_DIST_NONE, double param = 0.0) {
+        detail::check(hz_fb_set_distortion(h_.get(), dist_id, param), "Filterbank::process");
+        detail::check(hz_fb_process(h_.get(), in, out, n), "Filterbank::process");
+    }
+    hz_fb* native() const { return h_.get(); }
+
+private:
+    T sample_with(T sample, int dist_id, double param) {
+        if (!computed_) {
+            detail::check(hz_fb_set_distortion(h_.get(), dist_id, param), "Filterbank::operator()");
+            detail::check(hz_fb_process(h_.get(), &sample, &last_, 1), "Filterbank::operator()");
+            computed_ = true;
+        }
+        return last_;
+    }
+    handle<hz_fb, hz_fb_destroy> h_;
+    int N_, order_;
+    bool computed_ = false;
+    T last_ = 0;
+};
+
+}  // namespace soundmath

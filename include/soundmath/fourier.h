@@ -1,0 +1,76 @@
+// soundmath/fourier.h -- drop-in Fourier (src/fourier.h:50-194), StaticSTFT
+// (src/staticSTFT.h:10-177) and Cosine (src/fourier.h:197-234) over the HIP engine.
+//
+// process_block() is the GPU path.  write()/read() keep the reference's per-sample pair
+// for the usual alternation (write(x_t) then read()); each read() processes the pending
+// write as a one-sample block.  forward(i)/backward(i)/process(i) act on slots of the
+// per-sample state machine and have no block counterpart; they are not provided.
+// A processor is the reference's int(*)(const complex<double>*, complex<double>*), run on
+// the host per frame in frame order, or a built-in device processor (HZ_PROC_*).
+#pragma once
+
+#include "hz.h"
+
+namespace soundmath {
+
+class Fourier {
+public:
+    typedef int (*processor_t)(const std::complex<double>*, std::complex<double>*);
+
+    Fourier(processor_t processor, int N, int laps, int device = 0) { init(HZ_PROC_HOST, N, laps, HZ_WIN_HALFHANN, device, processor); }
+    // built-in device processor: HZ_PROC_IDENTITY, HZ_PROC_GATE_KEEP (625), HZ_PROC_HILBERT
+    Fourier(int builtin, int N, int laps, int device = 0) { init(builtin, N, laps, HZ_WIN_HALFHANN, device, nullptr); }
+
+    void write(double real, double imag = 0) {
+        pre_ = real;
+        pim_ = imag;
+        pending_ = true;
+    }
+    void read(double* real, double* imag) {
+        const double re = pending_ ? pre_ : 0.0, im = pending_ ? pim_ : 0.0;
+        detail::check(hz_stft_process_block(h_.get(), &re, &im, real, imag, 1), "Fourier::read");
+        pending_ = false;
+    }
+    void process_block(const double* re, const double* im, double* out_re, double* out_im, std::size_t n) {
+        detail::check(hz_stft_process_block(h_.get(), re, im, out_re, out_im, n), "Fourier::process_block");
+    }
+    hz_stft* native() const { return h_.get(); }
+
+protected:
+    Fourier() = default;
+    void init(int proc, int N, int laps, int window, int device, processor_t fn) {
+        const double p0 = proc == HZ_PROC_STATIC_GATE ? 100.0 : (proc == HZ_PROC_GATE_KEEP ? 625.0 : 0.0);
+        const double p1 = proc == HZ_PROC_STATIC_GATE ? 0.1 : 0.0;
+        hz_stft* h = nullptr;
+        detail::check(hz_stft_create(N, laps, window, proc, p0, p1, device, &h), "Fourier");
+        h_ = decltype(h_)(h);
+        if (fn)   // complex<double>* and double* (interleaved) are layout-compatible
+            detail::check(hz_stft_set_processor(h, reinterpret_cast<hz_stft_proc>(fn)), "Fourier");
+    }
+    handle<hz_stft, hz_stft_destroy> h_;
+    double pre_ = 0, pim_ = 0;
+    bool pending_ = false;
+};
+
+class StaticSTFT : public Fourier {
+public:
+    StaticSTFT(int N, int laps, int device = 0) { init(HZ_PROC_STATIC_GATE, N, laps, HZ_WIN_HANN, device, nullptr); }
+};
+
+class Cosine {
+public:
+    Cosine(int N, double** in, double** out, int device = 0) {
+        hz_dct* h = nullptr;
+        detail::check(hz_dct_create(N, device, &h), "Cosine");
+        h_ = decltype(h_)(h);
+        detail::check(hz_dct_buffers(h, in, out), "Cosine");
+    }
+    void forward() { detail::check(hz_dct_forward(h_.get()), "Cosine::forward"); }
+    void backward() { detail::check(hz_dct_backward(h_.get()), "Cosine::backward"); }
+    hz_dct* native() const { return h_.get(); }
+
+private:
+    handle<hz_dct, hz_dct_destroy> h_;
+};
+
+}  // namespace soundmath

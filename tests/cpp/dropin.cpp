@@ -1,0 +1,147 @@
+// dropin.cpp -- the drop-in headers used as the reference's demos use src/*.h
+// (tests/resynthesis.cpp, tests/delay.cpp, tests/bowl.cpp, tests/spectral.cpp,
+// tests/fft.cpp).  Writes raw little-endian outputs into argv[1]; tests/test_cpp_gpu.py
+// replays the same scenarios through the oracle.  Build: tests/test_cpp_cpu.py.
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "soundmath/additive.h"
+#include "soundmath/bowl.h"
+#include "soundmath/delay.h"
+#include "soundmath/filterbank.h"
+#include "soundmath/fourier.h"
+#include "soundmath/oscbank.h"
+#include "soundmath/sinusoids.h"
+
+using namespace soundmath;
+
+static std::string dir;
+
+template <typename T>
+static void dump(const char* name, const std::vector<T>& v) {
+    FILE* f = std::fopen((dir + "/" + name + ".bin").c_str(), "wb");
+    std::fwrite(v.data(), sizeof(T), v.size(), f);
+    std::fclose(f);
+}
+
+static double input(int t) { return std::sin(0.01 * t) + 0.5 * (((t * 7919) % 13) - 6) / 6.0; }
+
+static int hilbert64(const std::complex<double>* in, std::complex<double>* out) {
+    for (int i = 0; i < 64; i++) out[i] = i < 32 ? in[i] : 0.0;
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) return 2;
+    dir = argv[1];
+
+    {   // Filterbank: per-sample operator()/tick, then process()
+        Filterbank<double> fb(2, 16);
+        for (int i = 0; i < 16; i++) {
+            const double g = 0.01 * (i + 1), R = 0.99, th = 2 * PI * (i + 1) / 40.0;
+            fb.coefficients(i, {g, 0, -g}, {-2 * R * std::cos(th), R * R});
+        }
+        fb.boost(std::vector<double>(16, 1.0));
+        fb.open();
+        std::vector<double> y(1000), x(1000);
+        for (int t = 0; t < 1000; t++) x[t] = input(t);
+        for (int t = 0; t < 100; t++) {
+            y[t] = fb(x[t]);
+            (void)fb(x[t]);   // cached until tick()
+            fb.tick();
+        }
+        fb.process(x.data() + 100, y.data() + 100, 900);
+        dump("filterbank", y);
+    }
+    {   // Delay: tests/delay.cpp:18,41
+        Delay<double> delay(10, 2 * SR);
+        delay.coefficients({{0, 1}}, {{20000, 0.5}, {10000, 0.5}});
+        std::vector<double> x(50000, 0.0), y(50000);
+        x[0] = 1.0;
+        for (int t = 0; t < 10; t++) {
+            y[t] = delay(x[t]);
+            delay.tick();
+        }
+        delay.process(x.data() + 10, y.data() + 10, 49990);
+        dump("delay", y);
+    }
+    {   // Bowl<float>: tests/bowl.cpp pattern with fill(float*, BSIZE)
+        std::vector<float> f, a, d;
+        for (int i = 0; i < 8; i++) {
+            f.push_back(100.0f * (i + 1) * 1.01f);
+            a.push_back(0.01f * (i + 1));
+            d.push_back(0.5f * (i + 1));
+        }
+        Bowl<float> bowl(8, f, a, d);
+        bowl.trigger();
+        std::vector<float> y(2048);
+        for (int b = 0; b < 2; b++) bowl.fill(y.data() + 1024 * b, 1024);
+        dump("bowl", y);
+    }
+    {   // Fourier with a host processor (pointer of the reference's type), StaticSTFT
+        Fourier F(hilbert64, 64, 4);
+        std::vector<double> yr(1000), yi(1000), x(1000), z(1000, 0.0);
+        for (int t = 0; t < 1000; t++) x[t] = input(t);
+        for (int t = 0; t < 300; t++) {
+            F.write(x[t]);
+            F.read(&yr[t], &yi[t]);
+        }
+        F.process_block(x.data() + 300, z.data() + 300, yr.data() + 300, yi.data() + 300, 700);
+        dump("fourier_re", yr);
+        dump("fourier_im", yi);
+        StaticSTFT S(64, 4);
+        std::vector<double> sr(1000), si(1000);
+        S.process_block(x.data(), nullptr, sr.data(), si.data(), 1000);
+        dump("static_re", sr);
+    }
+    {   // Cosine: tests/fft.cpp (Cosine dct(N, &dct_in, &dct_out))
+        double *in, *out;
+        Cosine dct(64, &in, &out);
+        for (int i = 0; i < 64; i++) in[i] = input(i);
+        dct.forward();
+        std::vector<double> y(out, out + 64);
+        dct.backward();
+        y.insert(y.end(), in, in + 64);
+        dump("cosine", y);
+    }
+    {   // Oscbank<double, 8>: per-sample operator()/mixdown/tick, then fill
+        Oscbank<double, 8> osc;
+        for (int i = 0; i < 8; i++) osc.freqmod(i, 110.0 * (i + 1));
+        osc.open();
+        std::vector<double> m;
+        for (int t = 0; t < 10; t++) {
+            const std::complex<double> s = osc.mixdown();
+            const std::complex<double> z3 = osc()(3);
+            m.push_back(s.real());
+            m.push_back(s.imag());
+            m.push_back(z3.real());
+            osc.tick();
+        }
+        std::vector<std::complex<double>> mix(100);
+        osc.fill(mix.data(), 100);
+        for (auto& c : mix) {
+            m.push_back(c.real());
+            m.push_back(c.imag());
+        }
+        dump("oscbank", m);
+    }
+    {   // Additive (tests/additive.cpp shape, small) and Sinusoids
+        Additive<double> add(&cycle, 4, 8, 0.75, 1.0);
+        add.makenote(48, 1.0);
+        add.makenote(55, 0.5);
+        std::vector<double> y(2000);
+        for (int t = 0; t < 50; t++) {
+            y[t] = add();
+            add.tick();
+        }
+        add.fill(y.data() + 50, 1950);
+        dump("additive", y);
+        Sinusoids<double> sins(&cycle, 220.0, 6, 0.8);
+        std::vector<double> s(1000);
+        sins.fill(s.data(), 1000);
+        dump("sinusoids", s);
+    }
+    std::printf("dropin ok\n");
+    return 0;
+}

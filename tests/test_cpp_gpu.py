@@ -1,0 +1,106 @@
+"""GPU: the C++ drop-in headers end to end -- tests/cpp/dropin.cpp (reference-style demo
+code over include/soundmath/*.h) runs on the device and every output is replayed through
+the oracle (tolerances as in the per-engine tests; Delay bit-exact)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import scipy.fft
+
+from oracle import OracleFilterbank, OracleOscbank, rel_err
+from oracle_bowl import OracleBowl
+from oracle_delay import OracleDelaybank
+from oracle_osc import OracleAdditive, OracleSinusoids
+from oracle_stft import OracleSTFT
+from test_cpp_cpu import EXE, build_dropin
+
+pytestmark = pytest.mark.gpu
+PI = 3.14159265359
+
+
+def x_input(n):
+    t = np.arange(n)
+    return np.sin(0.01 * t) + 0.5 * (((t * 7919) % 13) - 6) / 6.0
+
+
+@pytest.fixture(scope="module")
+def outputs(tmp_path_factory):
+    r = build_dropin()
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = tmp_path_factory.mktemp("dropin")
+    p = subprocess.run([EXE, str(d)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "dropin ok" in p.stdout, p.stdout + p.stderr
+
+    def load(name, dtype=np.float64):
+        return np.fromfile(os.path.join(d, name + ".bin"), dtype=dtype)
+    return load
+
+
+def test_filterbank(outputs):
+    o = OracleFilterbank(2, 16)
+    for i in range(16):
+        g, R, th = 0.01 * (i + 1), 0.99, 2 * PI * (i + 1) / 40.0
+        o.coefficients(i, [g, 0, -g], [-2 * R * np.cos(th), R * R])
+    o.boost(np.ones(16))
+    o.open()
+    assert rel_err(outputs("filterbank"), o.process(x_input(1000))) < 1e-9
+
+
+def test_delay_bit_exact(outputs):
+    o = OracleDelaybank(1, 10, 2 * 48000)
+    o.coefficients(0, [(0, 1.0)], [(20000, 0.5), (10000, 0.5)])
+    x = np.zeros(50000)
+    x[0] = 1.0
+    y = outputs("delay")
+    assert np.array_equal(y, o.process(x)[0])
+    assert list(np.flatnonzero(y)[:3]) == [0, 10000, 20000]
+
+
+def test_bowl_float(outputs):
+    f = [np.float32(100.0) * np.float32(i + 1) * np.float32(1.01) for i in range(8)]
+    a = [np.float32(0.01) * np.float32(i + 1) for i in range(8)]
+    d = [np.float32(0.5) * np.float32(i + 1) for i in range(8)]
+    o = OracleBowl(8, np.float64(f), np.float64(a), np.float64(d), np.float32)
+    assert rel_err(outputs("bowl", np.float32), o.fill(2048)) < 1e-5
+
+
+def test_fourier_host_processor_and_static(outputs):
+    x = x_input(1000)
+    o = OracleSTFT(64, 4, 0, 3)   # the C++ hilbert64 callback == the built-in half-band
+    orr, oi = o.process_block(x, np.zeros(1000))
+    assert rel_err(outputs("fourier_re"), orr) < 1e-10
+    assert np.max(np.abs(outputs("fourier_im") - oi)) <= 1e-10 * np.max(np.abs(oi))
+    s = OracleSTFT(64, 4, 1, 1)
+    assert rel_err(outputs("static_re"), s.process_block(x)[0]) < 1e-10
+
+
+def test_cosine(outputs):
+    y = outputs("cosine")
+    x = x_input(64)
+    assert rel_err(y[:64], scipy.fft.dct(x, type=2)) < 1e-13
+    assert rel_err(y[64:], 128 * x) < 1e-13
+
+
+def test_oscbank(outputs):
+    o = OracleOscbank(8)
+    for i in range(8):
+        o.freqmod(i, 110.0 * (i + 1))
+    o.open()
+    ref = []
+    for _ in range(10):
+        z3 = o.phases()[3]
+        m = o.fill(1)[0]
+        ref += [m.real, m.imag, z3.real]
+    mix = o.fill(100)
+    ref += list(np.stack([mix.real, mix.imag], -1).reshape(-1))
+    assert rel_err(outputs("oscbank"), np.array(ref)) < 1e-9
+
+
+def test_additive_and_sinusoids(outputs):
+    o = OracleAdditive(4, 8, 0.75, 1.0)
+    o.makenote(48, 1.0)
+    o.makenote(55, 0.5)
+    assert rel_err(outputs("additive"), o.fill(2000)) < 1e-8
+    s = OracleSinusoids(220.0, 6, 0.8)
+    assert rel_err(outputs("sinusoids"), s.fill(1000)) < 1e-8
