@@ -138,7 +138,11 @@ def main():
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 --pmc child passes")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--bands-per-wave", type=int, default=0)
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2 = the BASELINE.json metric (default); c3/c4/c5 = the other SURVEY.md 8(d) rows")
     args = ap.parse_args()
+    if args.workload != "c2":
+        return run_row(args)
 
     import torch
     import torch.distributed as dist
@@ -275,6 +279,22 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def run_row(args):
+    """One 1-GPU line for a secondary config (bench_rows.py)."""
+    import torch
+    import bench_rows
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--workload c3/c4/c5 are single-GPU configs (SURVEY.md 8(d))")
+    dev = torch.device("cuda", 0)
+    fn = {"c3": bench_rows.run_c3, "c4": bench_rows.run_c4, "c5": bench_rows.run_c5}[args.workload]
+    body = fn(args, torch, dev)
+    line = {"metric": body.pop("metric"), "value": body.pop("value"), "unit": body.pop("unit"), "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": body.pop("ms_per_step"),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None}
+    line.update(body)
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

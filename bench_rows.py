@@ -1,0 +1,268 @@
+"""Secondary bench workloads for `bench.py --workload ...`.
+
+Each returns the same JSON shape as the headline C2 line: value = whole-job throughput in
+the config's unit with inputs resident in HBM, `roofline` for the dominant kernel from
+HIP-event kernel time on the engine's stream, and a bounded `cpu_baseline` from the
+oracle.  Only bench.py's C2 line is the BASELINE.json metric; these are per-row
+measurements of the other configs.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+SR = 48000
+FP64_PEAK = 78.6      # TFLOP/s
+FP32_PEAK = 157.3     # TFLOP/s (vector)
+HBM_PEAK = 8000.0     # GB/s
+
+
+def _tests_path():
+    p = os.path.join(ROOT, "tests")
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def _timed(step, steps, warmup, torch, dev):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    return time.perf_counter() - t0
+
+
+# --------------------------------------------------------------------------- C3
+def run_c3(args, torch, dev):
+    """Additive<double>(&cycle, 64, 256, 0.75, 1.0), all voices via makenote(36+v, 1),
+    voices 0-7 released at sample 24,000; one step = 480,000 samples."""
+    from huygens_amd import Additive
+    V, O, S = 64, 256, args.samples
+    add = Additive(V, O, 0.75, 1.0)
+    for v in range(V):
+        add.makenote(36 + v, 1.0)
+    stream = torch.cuda.current_stream(dev)
+    add.set_stream(stream.cuda_stream)
+    y = torch.empty(S, dtype=torch.float64, device=dev)
+    rel = min(24000, S)
+
+    def step():
+        add.fill_device(y.data_ptr(), rel)
+        for v in range(8):
+            add.release(v)
+        add.fill_device(y.data_ptr() + 8 * rel, S - rel)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    add.profile(True)
+    elapsed = _timed(step, args.steps, 0, torch, dev)
+    ms, launches = add.profile_read()
+    add.profile(False)
+    units = V * O * S * args.steps
+    kern_s = ms / 1e3
+    flops = 22.0 * units   # 22 flops (+ 3 transcendentals) per partial-sample
+    achieved = flops / kern_s / 1e12 if kern_s > 0 else None
+    cpu = None
+    if not args.no_cpu_baseline:
+        _tests_path()
+        from oracle_osc import OracleAdditive
+        o = OracleAdditive(V, O, 0.75, 1.0)
+        for v in range(V):
+            o.makenote(36 + v, 1.0)
+        n = 1500
+        t0 = time.perf_counter()
+        o.fill(n)
+        dt = time.perf_counter() - t0
+        cpu = {"value": V * O * n / dt, "unit": "partial-samples/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/hz_oracle_osc.c Additive, {V}x{O} partials x {n} samples, 1 thread, {dt:.2f} s"}
+    return {
+        "metric": "partial-samples/s for 64-voice x 256-overtone Additive",
+        "value": units / elapsed, "unit": "partial-samples/s",
+        "ms_per_step": 1e3 * elapsed / args.steps, "dtype": "f64",
+        "data": "synthetic: makenote(36+v, 1.0) for 64 voices, voices 0-7 released at sample 24000",
+        "config": {"workload": "C3 Additive<double>(&cycle, 64, 256, 0.75, 1.0), physics off",
+                   "samples_per_step": S, "voices": V, "overtones": O},
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK if achieved else None, "traffic": None,
+                     "kernel": "add_mix_kernel (+ add_reduce_kernel, add_advance_kernel)",
+                     "kernel_avg_ms": ms / max(1, launches), "launches": launches,
+                     "flops_per_unit": 22,
+                     "note": "algorithmic flops of the reference's per-sample update (SURVEY.md 8(d)); the engine's "
+                             "closed-form rotation does fewer"},
+        "cpu_baseline": cpu,
+    }
+
+
+# --------------------------------------------------------------------------- C4
+def c4_signal(n, seed=3):
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / float(SR)
+    x = 0.1 * rng.standard_normal(n)
+    for k in range(1, 9):
+        x += 0.5 * np.sin(2 * np.pi * 220 * k ** 1.5 * t)
+    return x
+
+
+def run_c4(args, torch, dev):
+    """StaticSTFT(4096, 4) with its built-in gate over 480,000 samples (C4 (i)); the
+    Fourier(gate625) variant (ii) is timed beside it."""
+    from huygens_amd import Fourier, StaticSTFT
+    N, laps, S = 4096, 4, args.samples
+    x = torch.from_numpy(c4_signal(S)).to(dev)
+    yr = torch.empty_like(x)
+    yi = torch.empty_like(x)
+    stream = torch.cuda.current_stream(dev)
+    out = {}
+    for name, eng in (("static", StaticSTFT(N, laps)), ("gate625", Fourier(2, N, laps))):
+        eng.set_stream(stream.cuda_stream)
+
+        def step():
+            eng.process_block_device(x.data_ptr(), 0, yr.data_ptr(), yi.data_ptr(), S)
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        f0 = eng.frames()[0]
+        eng.profile(True)
+        elapsed = _timed(step, args.steps, 0, torch, dev)
+        fms, oms, blocks = eng.profile_read()
+        eng.profile(False)
+        frames = eng.frames()[0] - f0
+        out[name] = (elapsed, fms, oms, blocks, frames)
+    elapsed, fms, oms, blocks, frames = out["static"]
+    flops = 491520.0 * frames   # 2 x 5 N log2 N per frame
+    achieved = flops / (fms / 1e3) / 1e12 if fms > 0 else None
+    cpu = None
+    if not args.no_cpu_baseline:
+        _tests_path()
+        from oracle_stft import OracleSTFT
+        o = OracleSTFT(N, laps, 1, 1)
+        n = 96000
+        xs = c4_signal(n)
+        t0 = time.perf_counter()
+        o.process_block(xs)
+        dt = time.perf_counter() - t0
+        cpu = {"value": o.frames() / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/hz_oracle_stft.c StaticSTFT(4096,4), {n} samples ({o.frames()} frames), "
+                         f"long double radix-2 FFT, 1 thread, {dt:.2f} s"}
+    e2, f2, o2, b2, fr2 = out["gate625"]
+    return {
+        "metric": "STFT frames/s, StaticSTFT 4096-pt / 75% overlap spectral gate",
+        "value": frames / elapsed, "unit": "frames/s",
+        "ms_per_step": 1e3 * elapsed / args.steps, "dtype": "f64",
+        "samples_per_s": S * args.steps / elapsed,
+        "data": "synthetic: white noise sigma 0.1 + 8 sinusoids 0.5 sin(2 pi 220 k^1.5 t), seed 3",
+        "config": {"workload": "C4 StaticSTFT(4096, 4) built-in gate (100, 0.1)", "samples_per_step": S,
+                   "frames_per_step": frames // args.steps},
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK if achieved else None, "traffic": None,
+                     "kernel": "stft_frame_kernel<STATIC_GATE,0> (window+FFT+gate+IFFT in LDS)",
+                     "kernel_ms_per_step": fms / args.steps, "ola_ms_per_step": oms / args.steps,
+                     "flops_per_frame": 491520},
+        "variant_fourier_gate625": {"frames_per_s": fr2 / e2, "kernel_ms_per_step": f2 / args.steps,
+                                    "ola_ms_per_step": o2 / args.steps},
+        "cpu_baseline": cpu,
+    }
+
+
+# --------------------------------------------------------------------------- C5
+def c5_model(M=2048, seed=5):
+    rng = np.random.default_rng(seed)
+    f = np.exp(rng.uniform(np.log(20.0), np.log(16000.0), M))
+    a = rng.uniform(1e-4, 5e-2, M)
+    d = rng.uniform(0.05, 15.0, M)
+    return f, a, d
+
+
+def run_c5(args, torch, dev):
+    """Bowl<float>(2048) fill(buf, 1024) x 469 with trigger() at t = 0, feeding
+    Delaybank<float,64>: line k = Delay<float>(3, 2 SR), fwd {(0,1)},
+    fb {(10000+37k, .5), (20000+53k, .5)}, lines mixed / 64.  One step = the 469 blocks."""
+    from huygens_amd import Bowl, Delaybank
+    M, L, B = 2048, 64, 1024
+    nb = max(1, args.samples // B)
+    f, a, d = c5_model(M)
+    bowl = Bowl(M, f, a, d, np.float32)
+    bank = Delaybank(L, 3, 2 * SR, np.float32)
+    for k in range(L):
+        bank.coefficients(k, [(0, 1.0)], [(10000 + 37 * k, 0.5), (20000 + 53 * k, 0.5)])
+    stream = torch.cuda.current_stream(dev)
+    bowl.set_stream(stream.cuda_stream)
+    bank.set_stream(stream.cuda_stream)
+    buf = torch.empty(nb * B, dtype=torch.float32, device=dev)
+    mix = torch.empty(nb * B, dtype=torch.float32, device=dev)
+
+    def step():
+        bowl.trigger()
+        for i in range(nb):
+            bowl.fill_device(buf.data_ptr() + 4 * B * i, B)
+            bank.process_device(buf.data_ptr() + 4 * B * i, mix.data_ptr() + 4 * B * i, B, False, True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    bowl.profile(True)
+    bank.profile(True)
+    elapsed = _timed(step, args.steps, 0, torch, dev)
+    bms, bl = bowl.profile_read()
+    dms, dl = bank.profile_read()
+    bowl.profile(False)
+    bank.profile(False)
+
+    # whole-signal kernels (one call each), the rates the roofline is quoted on
+    n = nb * B
+    bowl.profile(True)
+    bank.profile(True)
+    torch.cuda.synchronize(dev)
+    for _ in range(max(1, args.steps)):
+        bowl.trigger()
+        bowl.fill_device(buf.data_ptr(), n)
+        bank.process_device(buf.data_ptr(), mix.data_ptr(), n, False, True)
+    torch.cuda.synchronize(dev)
+    bms_w, bl_w = bowl.profile_read()
+    dms_w, dl_w = bank.profile_read()
+    bowl.profile(False)
+    bank.profile(False)
+    bowl_rate = M * n * bl_w / (bms_w / 1e3) if bms_w > 0 else None
+    dly_rate = L * n * dl_w / (dms_w / 1e3) if dms_w > 0 else None
+    achieved = bowl_rate * 8 / 1e12 if bowl_rate else None
+    cpu = None
+    if not args.no_cpu_baseline:
+        _tests_path()
+        from oracle_bowl import OracleBowl
+        o = OracleBowl(M, f, a, d, np.float32)
+        ns = 4096
+        t0 = time.perf_counter()
+        o.fill(ns)
+        dt = time.perf_counter() - t0
+        cpu = {"value": M * ns / dt, "unit": "mode-samples/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/hz_oracle_bowl.c Bowl<float>(2048), {ns} samples, 1 thread, {dt:.2f} s"}
+    return {
+        "metric": "mode-samples/s for Bowl<float>(2048) streamed in 1024-sample blocks into Delaybank<float,64>",
+        "value": M * n * args.steps / elapsed, "unit": "mode-samples/s",
+        "ms_per_step": 1e3 * elapsed / args.steps, "dtype": "f32 (phase model) / f64 accumulation",
+        "line_samples_per_s": L * n * args.steps / elapsed,
+        "data": "synthetic modal model seed 5: f log-uniform [20,16000] Hz, a U[1e-4,5e-2], d U[0.05,15]",
+        "config": {"workload": "C5 Bowl<float>(2048) fill x 469 blocks + Delaybank<float,64>(3, 2SR), mix /64",
+                   "samples_per_step": n, "block": B, "modes": M, "lines": L},
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": FP32_PEAK, "unit": "TFLOP/s",
+                     "frac": achieved / FP32_PEAK if achieved else None, "traffic": None,
+                     "kernel": "bowl_mix_kernel (float phase model)",
+                     "kernel_ms_whole_signal": bms_w / max(1, bl_w), "flops_per_unit": 8,
+                     "mode_samples_per_s_kernel": bowl_rate,
+                     "note": "8 flops per mode-sample (+ exp + sin), FP32 vector peak (SURVEY.md 8(d) C5)"},
+        "roofline_delaybank": {"bound": "hbm", "achieved": dly_rate * 20 / 1e9 if dly_rate else None,
+                               "peak": HBM_PEAK, "unit": "GB/s",
+                               "frac": dly_rate * 20 / 1e9 / HBM_PEAK if dly_rate else None,
+                               "kernel": "dly_line_kernel<float>", "kernel_ms_whole_signal": dms_w / max(1, dl_w),
+                               "line_samples_per_s_kernel": dly_rate, "bytes_per_unit": 20},
+        "streamed_kernel_ms_per_step": {"bowl": bms / args.steps, "delaybank": dms / args.steps},
+        "cpu_baseline": cpu,
+    }
