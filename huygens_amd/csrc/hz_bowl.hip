@@ -251,9 +251,13 @@ int bowl_check(hz_bowl* h) {
 int bowl_launch(hz_bowl* h, void* d_dst, long n, int out_kind) {
     if (n <= 0) return HZ_OK;
     const int M = h->M;
-    const int per_wave = std::min(kMaxPerWave, std::max(1, (M + kWaves * 32 - 1) / (kWaves * 32)));
-    const int G = std::max(1, (M + kWaves * per_wave - 1) / (kWaves * per_wave));
     const long ntiles = (n + kTile - 1) / kTile;
+    // modes per wave: up to 64 when time segments alone fill the chip; fewer (down to one)
+    // for short calls so that modes x segments still give ~2 workgroups per CU
+    int per_wave = std::min(kMaxPerWave, std::max(1, (M + kWaves * 32 - 1) / (kWaves * 32)));
+    const long par = (long)M * ntiles / ((long)kWaves * 2 * h->target_groups);
+    if (par < per_wave) per_wave = (int)std::max<long>(1, par);
+    const int G = std::max(1, (M + kWaves * per_wave - 1) / (kWaves * per_wave));
     long nseg = std::max<long>(1, std::min<long>(ntiles, (h->target_groups + G - 1) / G));
     const long seg_tiles = (ntiles + nseg - 1) / nseg;
     nseg = (ntiles + seg_tiles - 1) / seg_tiles;

@@ -38,6 +38,7 @@
 namespace {
 
 constexpr int kThreads = 1024;
+constexpr int kBatch = 8;
 
 struct DlyArgs {
     const void* in;      // mono [n] or line-major [N][n]
@@ -75,26 +76,48 @@ __global__ __launch_bounds__(kThreads) void dly_line_kernel(DlyArgs a) {
         const long s0 = k * a.Lc, s1 = min(a.n, s0 + a.Lc);
         const long per = (s1 - s0 + Gt - 1) / Gt;
         const long b0 = s0 + g * per, b1 = min(s1, b0 + per);
-        for (long j = b0 + threadIdx.x; j < b1; j += blockDim.x) {
-            const unsigned o = (unsigned)((a.o0 + (unsigned long)j) % size);
-            T acc = (T)0;
+        // kBatch samples per thread: every read of a tap is issued before any store, so
+        // the gathers of a batch overlap (the stores of this sub-block are never read in it)
+        for (long base = b0; base < b1; base += (long)blockDim.x * kBatch) {
+            long jj[kBatch];
+            unsigned oo[kBatch];
+            T acc[kBatch];
+#pragma unroll
+            for (int m = 0; m < kBatch; ++m) {
+                jj[m] = min(base + threadIdx.x + (long)m * blockDim.x, b1 - 1);
+                oo[m] = (a.o0 + (unsigned)jj[m]) % size;
+                acc[m] = (T)0;
+            }
             for (int i = 0; i < S; ++i) {
                 const int4 qf = tp[i];
-                const unsigned af = tap_age<T>(qf, o);
-                const T xr = ((long)af <= j) ? xin[j - af] : rx[o >= af ? o - af : o + size - af];
                 const T f = gn[i];
                 const T b = gn[S + i];
-                T yr = (T)0;
+                T xv[kBatch], yv[kBatch];
+#pragma unroll
+                for (int m = 0; m < kBatch; ++m) {
+                    const unsigned o = oo[m], af = tap_age<T>(qf, o);
+                    xv[m] = ((long)af <= jj[m]) ? xin[jj[m] - af] : rx[o >= af ? o - af : o + size - af];
+                    yv[m] = (T)0;
+                }
                 if (b != (T)0) {   // uniform over the workgroup (one line)
                     const int4 qb = tp[S + i];
-                    const unsigned ab = tap_age<T>(qb, o);
-                    yr = (ab == 0) ? acc : (((long)ab <= j) ? yout[j - ab] : ry[o >= ab ? o - ab : o + size - ab]);
+#pragma unroll
+                    for (int m = 0; m < kBatch; ++m) {
+                        const unsigned o = oo[m], ab = tap_age<T>(qb, o);
+                        yv[m] = (ab == 0) ? acc[m]
+                                          : (((long)ab <= jj[m]) ? yout[jj[m] - ab] : ry[o >= ab ? o - ab : o + size - ab]);
+                    }
                 }
-                const T fx = f * xr;
-                const T by = b * yr;
-                acc = acc + (fx - by);
+#pragma unroll
+                for (int m = 0; m < kBatch; ++m) {
+                    const T fx = f * xv[m];
+                    const T by = b * yv[m];
+                    acc[m] = acc[m] + (fx - by);
+                }
             }
-            yout[j] = acc;
+#pragma unroll
+            for (int m = 0; m < kBatch; ++m)
+                if (base + threadIdx.x + (long)m * blockDim.x < b1) yout[jj[m]] = acc[m];
         }
         if (k + 1 < a.k1) __syncthreads();   // sub-block k visible to k+1 (same CU, same L1)
     }
