@@ -230,6 +230,17 @@ def run_c5(args, torch, dev):
     dms_w, dl_w = bank.profile_read()
     bowl.profile(False)
     bank.profile(False)
+    split_ms = {}
+    for mode in (1, 2):   # one workgroup per line looping over sub-blocks / a launch per sub-block
+        bank.set_split(mode)
+        bank.profile(True)
+        for _ in range(max(1, args.steps)):
+            bank.process_device(buf.data_ptr(), mix.data_ptr(), n, False, True)
+        torch.cuda.synchronize(dev)
+        ms_, l_ = bank.profile_read()
+        bank.profile(False)
+        split_ms[str(mode)] = ms_ / max(1, l_)
+    bank.set_split(0)
     bowl_rate = M * n * bl_w / (bms_w / 1e3) if bms_w > 0 else None
     dly_rate = L * n * dl_w / (dms_w / 1e3) if dms_w > 0 else None
     achieved = bowl_rate * 8 / 1e12 if bowl_rate else None
@@ -262,7 +273,8 @@ def run_c5(args, torch, dev):
                                "peak": HBM_PEAK, "unit": "GB/s",
                                "frac": dly_rate * 20 / 1e9 / HBM_PEAK if dly_rate else None,
                                "kernel": "dly_line_kernel<float>", "kernel_ms_whole_signal": dms_w / max(1, dl_w),
-                               "line_samples_per_s_kernel": dly_rate, "bytes_per_unit": 20},
+                               "line_samples_per_s_kernel": dly_rate, "bytes_per_unit": 20,
+                               "whole_signal_ms_by_split": split_ms},
         "streamed_kernel_ms_per_step": {"bowl": bms / args.steps, "delaybank": dms / args.steps},
         "cpu_baseline": cpu,
     }

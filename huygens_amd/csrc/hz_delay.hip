@@ -38,7 +38,6 @@
 namespace {
 
 constexpr int kThreads = 1024;
-constexpr int kBatch = 8;
 
 struct DlyArgs {
     const void* in;      // mono [n] or line-major [N][n]
@@ -58,7 +57,7 @@ __device__ __forceinline__ unsigned tap_age(const int4& q, unsigned o) {
     return ((int)o < q.x) ? (unsigned)q.z : (unsigned)q.y;
 }
 
-template <typename T>
+template <typename T, int kBatch>
 __global__ __launch_bounds__(kThreads) void dly_line_kernel(DlyArgs a) {
 #pragma clang fp contract(off)
     const int line = blockIdx.y;
@@ -96,7 +95,8 @@ __global__ __launch_bounds__(kThreads) void dly_line_kernel(DlyArgs a) {
 #pragma unroll
                 for (int m = 0; m < kBatch; ++m) {
                     const unsigned o = oo[m], af = tap_age<T>(qf, o);
-                    xv[m] = ((long)af <= jj[m]) ? xin[jj[m] - af] : rx[o >= af ? o - af : o + size - af];
+                    const T* src = ((long)af <= jj[m]) ? xin + (jj[m] - af) : rx + (o >= af ? o - af : o + size - af);
+                    xv[m] = *src;   // one branch-free gather: the pointer is selected, not the load
                     yv[m] = (T)0;
                 }
                 if (b != (T)0) {   // uniform over the workgroup (one line)
@@ -104,8 +104,10 @@ __global__ __launch_bounds__(kThreads) void dly_line_kernel(DlyArgs a) {
 #pragma unroll
                     for (int m = 0; m < kBatch; ++m) {
                         const unsigned o = oo[m], ab = tap_age<T>(qb, o);
-                        yv[m] = (ab == 0) ? acc[m]
-                                          : (((long)ab <= jj[m]) ? yout[jj[m] - ab] : ry[o >= ab ? o - ab : o + size - ab]);
+                        const T* src = ((long)ab <= jj[m]) ? yout + (jj[m] - (long)(ab ? ab : 0))
+                                                           : ry + (o >= ab ? o - ab : o + size - ab);
+                        const T v = *src;   // age 0 reads yout[j] (stale); replaced by the partial sum
+                        yv[m] = (ab == 0) ? acc[m] : v;
                     }
                 }
 #pragma unroll
@@ -298,18 +300,21 @@ int dly_launch_t(hz_dly* h, const void* d_in, void* d_out, long n, int in_per_li
     a.in_per_line = in_per_line;
     a.size = h->size;
     a.o0 = h->origin;
+    // samples per thread per pass: 8 when a workgroup's slice of a sub-block is long
+    const long slice = (mode == 1) ? Lc : (Lc + gt_max - 1) / gt_max;
+    auto kern = slice >= 4L * kThreads ? dly_line_kernel<T, 8> : (slice > kThreads ? dly_line_kernel<T, 2> : dly_line_kernel<T, 1>);
     if (mode == 1) {
         a.k0 = 0;
         a.k1 = nsub;
         a.commit = 1;
-        hipLaunchKernelGGL(dly_line_kernel<T>, dim3(1, N), dim3(kThreads), 0, h->stream, a);
+        hipLaunchKernelGGL(kern, dim3(1, N), dim3(kThreads), 0, h->stream, a);
         HZ_TRY_HIP(hipGetLastError());
     } else {
         a.commit = 0;
         for (long k = 0; k < nsub; ++k) {
             a.k0 = k;
             a.k1 = k + 1;
-            hipLaunchKernelGGL(dly_line_kernel<T>, dim3((unsigned)gt_max, N), dim3(kThreads), 0, h->stream, a);
+            hipLaunchKernelGGL(kern, dim3((unsigned)gt_max, N), dim3(kThreads), 0, h->stream, a);
             HZ_TRY_HIP(hipGetLastError());
         }
         const long span = std::min<long>(n, (long)h->size);
