@@ -272,7 +272,9 @@ int dly_launch_t(hz_dly* h, const void* d_in, void* d_out, long n, int in_per_li
     const long gt_max = std::max<long>(1, std::min<long>((Lc + kThreads - 1) / kThreads,
                                                          (2L * h->target_groups + N - 1) / N));
     int mode = h->split;
-    if (mode == 0) mode = (gt_max > 1 && nsub <= 8) ? 2 : 1;
+    // auto: several workgroups per line (a launch per sub-block) unless the lines alone fill
+    // the chip; measured 2x faster for C5's 64 lines x 480k samples (bench c5 split table)
+    if (mode == 0) mode = (gt_max > 1 && (nsub <= 8 || N < h->target_groups)) ? 2 : 1;
     if (mode == 2 && gt_max == 1) mode = 1;
 
     hipEvent_t* e = nullptr;
