@@ -132,8 +132,13 @@ __device__ __forceinline__ int xs_pos(int li) { return li + (li >> 4); }
 //   with bands alone (e.g. 512-band shards on 8 GPUs).
 enum { MODE_MIX = 0, MODE_SEGEND = 1 };
 
+// PF (x values prefetched per thread) fixes the workgroup size: 2 -> 16 waves, 3 -> 8, 5 -> 4;
+// the launch bound follows it, so 4-wave groups get the whole VGPR file (NB > 1 bands per
+// wave interleaved for ILP instead of occupancy).
+constexpr int wg_threads(int PF) { return PF == 2 ? 1024 : (PF == 3 ? 512 : 256); }
+
 template <int O, int DIST, int NB, int MODE, int PF>
-__global__ __launch_bounds__(1024) void fb_mix_kernel(const double* __restrict__ rec, MixArgs a) {
+__global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __restrict__ rec, MixArgs a) {
     // rec is passed as its own __restrict__ argument so the compiler can prove the
     // kernel's stores never clobber it: wave-uniform record reads become s_load.
     using R = Rec<O>;
@@ -607,34 +612,38 @@ static void build_record_any(int O, const double* b, const double* a, double* re
 typedef void (*MixKernel)(const double*, MixArgs);
 typedef void (*CarryKernel)(const double*, const double*, double*, int, int, long);
 
-template <int O, int PF>
+template <int O, int PF, int NB>
 MixKernel pick_dist(int dist, int mode) {
-    if (mode == MODE_SEGEND) return fb_mix_kernel<O, HZ_DIST_NONE, 1, MODE_SEGEND, PF>;
+    if (mode == MODE_SEGEND) return fb_mix_kernel<O, HZ_DIST_NONE, NB, MODE_SEGEND, PF>;
     switch (dist) {
-    case HZ_DIST_SOFTCLIP: return fb_mix_kernel<O, HZ_DIST_SOFTCLIP, 1, MODE_MIX, PF>;
-    case HZ_DIST_SATURATE: return fb_mix_kernel<O, HZ_DIST_SATURATE, 1, MODE_MIX, PF>;
-    case HZ_DIST_LIMITER: return fb_mix_kernel<O, HZ_DIST_LIMITER, 1, MODE_MIX, PF>;
-    default: return fb_mix_kernel<O, HZ_DIST_NONE, 1, MODE_MIX, PF>;
+    case HZ_DIST_SOFTCLIP: return fb_mix_kernel<O, HZ_DIST_SOFTCLIP, NB, MODE_MIX, PF>;
+    case HZ_DIST_SATURATE: return fb_mix_kernel<O, HZ_DIST_SATURATE, NB, MODE_MIX, PF>;
+    case HZ_DIST_LIMITER: return fb_mix_kernel<O, HZ_DIST_LIMITER, NB, MODE_MIX, PF>;
+    default: return fb_mix_kernel<O, HZ_DIST_NONE, NB, MODE_MIX, PF>;
     }
 }
 
-template <int PF>
+template <int PF, int NB>
 MixKernel pick_order(int O, int dist, int mode) {
     switch (O) {
-    case 0: return pick_dist<0, PF>(dist, mode);
-    case 1: return pick_dist<1, PF>(dist, mode);
-    case 2: return pick_dist<2, PF>(dist, mode);
-    case 3: return pick_dist<3, PF>(dist, mode);
-    default: return pick_dist<4, PF>(dist, mode);
+    case 0: return pick_dist<0, PF, NB>(dist, mode);
+    case 1: return pick_dist<1, PF, NB>(dist, mode);
+    case 2: return pick_dist<2, PF, NB>(dist, mode);
+    case 3: return pick_dist<3, PF, NB>(dist, mode);
+    default: return pick_dist<4, PF, NB>(dist, mode);
     }
 }
 
-// waves per workgroup in {4, 8, 16}: x prefetch depth ceil(1040 / (64 waves))
-static MixKernel pick_kernel(int O, int dist, int waves, int mode) {
+// waves per workgroup in {4, 8, 16}: x prefetch depth ceil(1040 / (64 waves)); several
+// bands per wave only with 4-wave groups (register file)
+static MixKernel pick_kernel(int O, int dist, int waves, int nb, int mode) {
     switch (waves) {
-    case 16: return pick_order<2>(O, dist, mode);
-    case 8: return pick_order<3>(O, dist, mode);
-    default: return pick_order<5>(O, dist, mode);
+    case 16: return pick_order<2, 1>(O, dist, mode);
+    case 8: return pick_order<3, 1>(O, dist, mode);
+    default:
+        if (nb == 4) return pick_order<5, 4>(O, dist, mode);
+        if (nb == 2) return pick_order<5, 2>(O, dist, mode);
+        return pick_order<5, 1>(O, dist, mode);
     }
 }
 
@@ -748,8 +757,8 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
         HZ_TRY_HIP(hipMalloc(&h->d_partial, sizeof(double) * need));
         h->partial_cap = need;
     }
-    MixKernel kmix = pick_kernel(O, h->dist_id, h->waves, MODE_MIX);
-    MixKernel kend = pick_kernel(O, h->dist_id, h->waves, MODE_SEGEND);
+    MixKernel kmix = pick_kernel(O, h->dist_id, h->waves, h->bands_per_wave, MODE_MIX);
+    MixKernel kend = pick_kernel(O, h->dist_id, h->waves, h->bands_per_wave, MODE_SEGEND);
     HZ_TRY(fb_set_lds_attr(kmix));
     const size_t lds = lds_bytes(h->waves, true);
     const size_t lds_end = lds_bytes(h->waves, false);
@@ -1130,13 +1139,14 @@ int hz_fb_info(hz_fb* h, int* order, int* N_local, int* band_begin, int* N_total
 
 int hz_fb_tune(hz_fb* h, int waves_per_group, int bands_per_wave) {
     if (!h) return HZ_E_INVALID;
-    if (!(waves_per_group == 0 || waves_per_group == 4 || waves_per_group == 8 || waves_per_group == 16) ||
-        !(bands_per_wave == 0 || bands_per_wave == 1)) {
-        hz::set_error("hz_fb_tune: waves in {4,8,16}, bands per wave 1");
+    const int w = waves_per_group ? waves_per_group : h->waves;
+    const int nb = bands_per_wave ? bands_per_wave : (waves_per_group && waves_per_group != 4 ? 1 : h->bands_per_wave);
+    if (!(w == 4 || w == 8 || w == 16) || !(nb == 1 || (w == 4 && (nb == 2 || nb == 4)))) {
+        hz::set_error("hz_fb_tune: waves in {4,8,16}; bands per wave 1, or 2/4 with 4 waves");
         return HZ_E_INVALID;
     }
-    if (waves_per_group) h->waves = waves_per_group;
-    if (bands_per_wave) h->bands_per_wave = bands_per_wave;
+    h->waves = w;
+    h->bands_per_wave = nb;
     return HZ_OK;
 }
 

@@ -206,3 +206,25 @@ def test_time_segments(gpu_lib, N, n, groups):
     x = white_noise_f32(n, seed=10)
     assert rel_err(g.process(x[:n // 3]), o.process(x[:n // 3])) < TOL
     assert rel_err(g.process(x[n // 3:]), o.process(x[n // 3:])) < TOL
+
+
+@pytest.mark.parametrize("waves,nb", [(4, 1), (4, 2), (4, 4), (8, 1), (16, 1)])
+@pytest.mark.parametrize("order,N", [(2, 4096), (2, 37), (1, 9), (3, 130)])
+def test_geometries(gpu_lib, waves, nb, order, N):
+    """Every workgroup geometry (waves x bands per wave) on ragged banks and signals,
+    with pre/gain ramps, two calls, time segments for small banks."""
+    rng = np.random.default_rng(order * 1000 + N)
+    fwd = rng.uniform(-0.05, 0.05, (N, order + 1))
+    back = []
+    for n in range(N):
+        r = rng.uniform(0.5, 0.99, order)
+        back.append(np.poly(r)[1:] if order else np.zeros(0))
+    back = np.array(back)
+    g, o = make_pair(order, N, fwd, back, boost=False)
+    g.tune(waves, nb)
+    for fb in (g, o):
+        fb.boost(rng.uniform(0.5, 1.5, N))
+    x = white_noise_f32(3000, seed=3)
+    assert rel_err(g.process(x), o.process(x)) < TOL
+    x2 = white_noise_f32(2100, seed=4)
+    assert rel_err(g.process(x2), o.process(x2)) < TOL
