@@ -222,8 +222,9 @@ def test_geometries(gpu_lib, waves, nb, order, N):
     back = np.array(back)
     g, o = make_pair(order, N, fwd, back, boost=False)
     g.tune(waves, nb)
+    boost = rng.uniform(0.5, 1.5, N)
     for fb in (g, o):
-        fb.boost(rng.uniform(0.5, 1.5, N))
+        fb.boost(boost)
     x = white_noise_f32(3000, seed=3)
     assert rel_err(g.process(x), o.process(x)) < TOL
     x2 = white_noise_f32(2100, seed=4)
