@@ -234,8 +234,9 @@ def main():
     value = total_band_samples / elapsed
     if rank == 0:
         # dominant kernel: fb_mix_kernel; algorithmic flops per launch = 18 x band-samples
+        # one process() call can be several launches (the partial slab bounds a launch's length)
         mix_avg_s = (mix_ms_max / 1e3) / max(1, launches)
-        flops_per_launch = FLOPS_PER_BAND_SAMPLE * cnt * S
+        flops_per_launch = FLOPS_PER_BAND_SAMPLE * cnt * S * args.steps / max(1, launches)
         achieved = flops_per_launch / mix_avg_s / 1e12 if mix_avg_s > 0 else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -264,7 +265,8 @@ def main():
                          "unit": "TFLOP/s", "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic,
                          "traffic_detail": traffic_detail,
-                         "algorithmic_bytes_per_launch": 16 * S + 120 * cnt,
+                         "algorithmic_bytes_per_launch": (16 * S + 120 * cnt) * args.steps / max(1, launches),
+                         "launches_per_step": launches / max(1, args.steps),
                          "kernel": "fb_mix_kernel<2,0,1,0>",
                          "kernel_avg_ms": 1e3 * mix_avg_s,
                          "segment_prepass_ms_per_launch": seg_ms / max(1, launches),
