@@ -635,11 +635,11 @@ MixKernel pick_order(int O, int dist, int mode) {
 }
 
 // waves per workgroup in {4, 8, 16}: x prefetch depth ceil(1040 / (64 waves)); several
-// bands per wave only with 4-wave groups (register file)
+// bands per wave only with 4- or 8-wave groups (register file)
 static MixKernel pick_kernel(int O, int dist, int waves, int nb, int mode) {
     switch (waves) {
     case 16: return pick_order<2, 1>(O, dist, mode);
-    case 8: return pick_order<3, 1>(O, dist, mode);
+    case 8: return nb == 2 ? pick_order<3, 2>(O, dist, mode) : pick_order<3, 1>(O, dist, mode);
     default:
         if (nb == 4) return pick_order<5, 4>(O, dist, mode);
         if (nb == 2) return pick_order<5, 2>(O, dist, mode);
@@ -1140,9 +1140,9 @@ int hz_fb_info(hz_fb* h, int* order, int* N_local, int* band_begin, int* N_total
 int hz_fb_tune(hz_fb* h, int waves_per_group, int bands_per_wave) {
     if (!h) return HZ_E_INVALID;
     const int w = waves_per_group ? waves_per_group : h->waves;
-    const int nb = bands_per_wave ? bands_per_wave : (waves_per_group && waves_per_group != 4 ? 1 : h->bands_per_wave);
-    if (!(w == 4 || w == 8 || w == 16) || !(nb == 1 || (w == 4 && (nb == 2 || nb == 4)))) {
-        hz::set_error("hz_fb_tune: waves in {4,8,16}; bands per wave 1, or 2/4 with 4 waves");
+    const int nb = bands_per_wave ? bands_per_wave : (waves_per_group ? 1 : h->bands_per_wave);
+    if (!(w == 4 || w == 8 || w == 16) || !(nb == 1 || (w == 4 && (nb == 2 || nb == 4)) || (w == 8 && nb == 2))) {
+        hz::set_error("hz_fb_tune: waves in {4,8,16}; bands per wave 1, 2 (4 or 8 waves) or 4 (4 waves)");
         return HZ_E_INVALID;
     }
     h->waves = w;

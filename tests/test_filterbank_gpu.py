@@ -208,7 +208,7 @@ def test_time_segments(gpu_lib, N, n, groups):
     assert rel_err(g.process(x[n // 3:]), o.process(x[n // 3:])) < TOL
 
 
-@pytest.mark.parametrize("waves,nb", [(4, 1), (4, 2), (4, 4), (8, 1), (16, 1)])
+@pytest.mark.parametrize("waves,nb", [(4, 1), (4, 2), (4, 4), (8, 1), (8, 2), (16, 1)])
 @pytest.mark.parametrize("order,N", [(2, 4096), (2, 37), (1, 9), (3, 130)])
 def test_geometries(gpu_lib, waves, nb, order, N):
     """Every workgroup geometry (waves x bands per wave) on ragged banks and signals,
