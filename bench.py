@@ -138,6 +138,8 @@ def main():
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 --pmc child passes")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--bands-per-wave", type=int, default=0)
+    ap.add_argument("--lti", default="", help="LTI engine geometry 'chunk,bands_per_wave,waves' (default engine choice)")
+    ap.add_argument("--general", action="store_true", help="force the general engine (no converged fast path)")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2 = the BASELINE.json metric (default); c3/c4/c5 = the other SURVEY.md 8(d) rows")
     args = ap.parse_args()
@@ -166,6 +168,11 @@ def main():
     fb.open()
     if args.waves or args.bands_per_wave:
         fb.tune(args.waves, args.bands_per_wave)
+    if args.lti:
+        fb.tune_lti(*[int(v) for v in args.lti.split(",")])
+    if args.general:
+        from huygens_amd._lib import HZ_FB_PATH_GENERAL
+        fb.set_path(HZ_FB_PATH_GENERAL)
     stream = torch.cuda.current_stream(dev)
     fb.set_stream(stream.cuda_stream)
 

@@ -21,6 +21,10 @@ HZ_E_NODEV = -4
 HZ_E_ALLOC = -5
 HZ_E_UNSUPPORTED = -6
 
+HZ_FB_PATH_AUTO = 0
+HZ_FB_PATH_GENERAL = 1
+HZ_FB_PATH_LTI = 2
+
 HZ_DIST_NONE = 0
 HZ_DIST_SOFTCLIP = 1
 HZ_DIST_SATURATE = 2
@@ -76,6 +80,9 @@ _SIGS = {
     "hz_fb_profile": (I, [VP, I]),
     "hz_fb_profile_read": (I, [VP, PD, PD, PD, C.POINTER(L)]),
     "hz_fb_set_target_groups": (I, [VP, I]),
+    "hz_fb_set_path": (I, [VP, I]),
+    "hz_fb_last_path": (I, [VP, C.POINTER(I)]),
+    "hz_fb_tune_lti": (I, [VP, I, I, I]),
     # Oscbank
     "hz_osc_create": (I, [I, D, I, C.POINTER(VP)]),
     "hz_osc_create_shard": (I, [I, I, I, D, I, C.POINTER(VP)]),

@@ -140,5 +140,17 @@ class Filterbank:
         check(self._lib.hz_fb_profile_read(self._h, C.byref(s), C.byref(m), C.byref(r), C.byref(c)))
         return s.value, m.value, r.value, c.value
 
+    def set_path(self, path: int):
+        """HZ_FB_PATH_AUTO (converged LTI engine when eligible) or HZ_FB_PATH_GENERAL."""
+        check(self._lib.hz_fb_set_path(self._h, int(path)))
+
+    def last_path(self) -> int:
+        p = C.c_int()
+        check(self._lib.hz_fb_last_path(self._h, C.byref(p)))
+        return p.value
+
+    def tune_lti(self, chunk: int = 0, bands_per_wave: int = 0, waves: int = 0):
+        check(self._lib.hz_fb_tune_lti(self._h, chunk, bands_per_wave, waves))
+
     def set_target_groups(self, groups: int):
         check(self._lib.hz_fb_set_target_groups(self._h, groups))

@@ -94,6 +94,20 @@ int hz_fb_profile(hz_fb* h, int enable);
 int hz_fb_profile_read(hz_fb* h, double* segment_ms, double* mix_ms, double* reduce_ms, long* launches);
 /* workgroups wanted per launch before time segmentation kicks in (default: CU count) */
 int hz_fb_set_target_groups(hz_fb* h, int groups);
+/* Execution path of process calls.  HZ_FB_PATH_AUTO: the converged ("LTI") engine
+ * whenever every band's pre-amp and gain smoother has converged to its target
+ * (|pre - pin| <= 2^-60 max|pin|, same for gains) and no distortion functor is set,
+ * the general engine otherwise (hz_fb_lti.h).  HZ_FB_PATH_GENERAL: always the
+ * general engine.  hz_fb_last_path reports the path the last process call took
+ * (HZ_FB_PATH_LTI if any of its samples went through the LTI engine). */
+#define HZ_FB_PATH_AUTO 0
+#define HZ_FB_PATH_GENERAL 1
+#define HZ_FB_PATH_LTI 2
+int hz_fb_set_path(hz_fb* h, int path);
+int hz_fb_last_path(hz_fb* h, int* path);
+/* LTI engine geometry: (chunk length, bands per wave, waves per group) in
+ * {(16,1,16), (32,4,4), (16,2,8)}; 0s = default */
+int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group);
 
 /* ---- Oscbank<double,N>  (src/oscbank.h:15-97, src/multichannel.h:16-159) -- */
 typedef struct hz_osc hz_osc;
