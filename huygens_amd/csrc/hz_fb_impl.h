@@ -1,0 +1,114 @@
+// hz_fb_impl.h -- private header shared by the two Filterbank<double> translation units:
+//   hz_filterbank.hip  general engine (time-varying smoothers, distortion functors) + C ABI
+//   hz_fb_lti.hip      converged ("LTI") engine
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "hz_common.h"
+
+namespace hz_fbi {
+
+constexpr int kMaxOrder = 4;
+
+// MODE_MIX: full pass (mixdown) over one time segment (blockIdx.y) of one band group
+//   (blockIdx.x).
+// MODE_SEGEND: zero-state end state of each segment but the last (no mixdown), feeding a
+//   per-band carry kernel when the bank is too small to fill the chip with bands alone
+//   (e.g. 512-band shards on 8 GPUs).
+enum { MODE_MIX = 0, MODE_SEGEND = 1 };
+
+// Scalar (SGPR) copy of a wave-uniform double.
+__device__ __forceinline__ double uniform(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffff));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// DPP lane moves on a double (two 32-bit halves).  bound_ctrl: lanes whose
+// source is outside the pattern read 0.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int kDppRowShr = 0x110;   // row_shr:n = 0x110 + n (within 16-lane rows)
+// (wave-wide DPP shifts / row_bcast do not exist on CDNA; cross-row moves use
+//  ds_bpermute or v_readlane)
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+}  // namespace hz_fbi
+
+// ---------------------------------------------------------------------------
+// handle (the opaque hz_fb of include/huygens_hip.h)
+// ---------------------------------------------------------------------------
+struct hz_fb {
+    int order = 2, N = 0, N_total = 0, band_begin = 0, device = 0;
+    double sp = 0, sg = 0;
+    int rec = 8;
+    // host shadows of the staged parameters
+    std::vector<double> F, B, pin, gin;
+    bool dirty_coef = true, dirty_pin = true, dirty_gin = true;
+    int dist_id = HZ_DIST_NONE;
+    double dist_param = 0;
+    // geometry
+    int waves = 16, bands_per_wave = 1;
+    // device buffers
+    double *d_rec = nullptr, *d_pin = nullptr, *d_gin = nullptr;
+    double *d_ystate[2] = {nullptr, nullptr}, *d_pg[2] = {nullptr, nullptr};
+    int scur = 0;  // current state buffer (ping-pong per launch)
+    double* d_xhist[2] = {nullptr, nullptr};
+    int xcur = 0;
+    double* d_partial = nullptr;
+    size_t partial_cap = 0;  // doubles
+    double* d_seg = nullptr;  // segment start states
+    size_t seg_cap = 0;
+    int target_groups = 256;  // workgroups wanted per launch (CU count)
+    double *d_in = nullptr, *d_out = nullptr;
+    size_t io_cap = 0;       // doubles
+    std::vector<double> h_rec;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    // profiling
+    bool prof = false;
+    std::vector<hipEvent_t> ev;  // quadruplets
+    size_t ev_used = 0;
+    long prof_launches = 0;
+    // converged (LTI) path, hz_fb_lti.hip
+    int path_mode = HZ_FB_PATH_AUTO;
+    int last_path = HZ_FB_PATH_GENERAL;
+    int lti_geom = 0;                // index into kLtiGeoms (hz_fb_lti.hip)
+    int lti_rec = 0, lti_rec_L = 0;  // record size / chunk length the LTI records were built for
+    bool dirty_lti = true;           // coefficients changed since the LTI records were built
+    bool fmix_valid = false;         // Fmix matches the current coefficients, pin and gin
+    double* d_rec_lti = nullptr;
+    size_t rec_lti_cap = 0;
+    double* d_fmix = nullptr;        // [L][L+O]
+    std::vector<double> h_rec_lti;
+    std::vector<double> pg_host;     // host mirror of the smoother state [N][2] (pre, gain)
+};
+
+namespace hz_fbi {
+
+// hz_filterbank.hip
+int fb_set_lds_attr(const void* kernel);
+void fb_mirror_advance(hz_fb* h, long len);
+int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n);
+// hz_fb_lti.hip
+int fb_lti_chunk(const hz_fb* h);  // samples per lane chunk of the selected LTI geometry
+bool fb_converged(const hz_fb* h);
+int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n);
+
+}  // namespace hz_fbi

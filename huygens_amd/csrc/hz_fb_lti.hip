@@ -1,6 +1,4 @@
-// hz_fb_lti.h -- the converged ("LTI") path of the Filterbank<double> engine.
-//
-// Included by hz_filterbank.hip (uses its uniform / dpp_d / readlane_d helpers).
+// hz_fb_lti.hip -- the converged ("LTI") path of the Filterbank<double> engine.
 //
 // When every band's pre-amp and gain smoother has converged to its target
 // (src/filterbank.h:172-173 one-pole recurrences; |pre - pin| <= 2^-60 max|pin|,
@@ -28,9 +26,11 @@
 // i.e. O(L+O) + O L FMAs per chunk instead of running the recurrence twice per
 // sample (hz_filterbank.hip's general kernel).  The result is the same linear map
 // evaluated in another association order (parity: tests/test_filterbank_lti_gpu.py).
-#pragma once
+#include "hz_fb_impl.h"
 
 namespace {
+
+using namespace hz_fbi;
 
 // LTI band record (doubles), built on the host in long double.
 template <int O, int L>
@@ -184,12 +184,24 @@ template <int O, int L>
 __host__ __device__ constexpr int lti_xs_pad() {
     return ((lti_xs_len<O, L>() + lti_xs_len<O, L>() / L + 1) + 1) & ~1;
 }
-constexpr int kLtiPartPad = 66;  // per-wave partial rows [L][66]
+// gs rows [KD = W NB O][64 chunks + 16 pad]: the MFMA A-operand reads (16 chunks of
+// two rows per 32-lane group) land on disjoint bank halves; double-buffered.
+constexpr int kGsRow = 80;
 template <int O, int L>
-__host__ __device__ constexpr size_t lti_lds_bytes(int waves, bool mix) {
-    return sizeof(double) * (2 * (size_t)lti_xs_pad<O, L>() + (mix ? (size_t)waves * L * kLtiPartPad : 0));
+__host__ __device__ constexpr size_t lti_lds_bytes(int waves, int nb, bool mix) {
+    return sizeof(double) * (2 * (size_t)lti_xs_pad<O, L>() + (mix ? 2 * (size_t)waves * nb * O * kGsRow : 0));
 }
 
+typedef double hz_f64x4 __attribute__((ext_vector_type(4)));
+
+// One workgroup = W waves x NB bands (band group g = blockIdx.x) over one time
+// segment (blockIdx.y); a wave walks the segment's tiles carrying its bands' state.
+// Per tile: each wave computes, for its bands, the chunk zero-state end states (E, VALU
+// with wave-uniform coefficients), the carry scan and the chunk start states st; it
+// stores gs = gin st to LDS.  After the barrier the bank group's correction mix
+//   D[chunk][j] = sum_{(band,k)} gs[(band,k)][chunk] K_band[j][k]
+// is a (64 x KD) x (KD x L) product on the FP64 matrix cores (v_mfma_f64_16x16x4f64):
+// the reduction over the group's bands happens inside the MFMA, no per-band LDS rows.
 template <int O, int L, int NB, int W, int MODE>
 __global__ __launch_bounds__(64 * W) void fb_lti_kernel(const double* __restrict__ rec, LtiArgs a) {
     using R = RecL<O, L>;
@@ -198,18 +210,23 @@ __global__ __launch_bounds__(64 * W) void fb_lti_kernel(const double* __restrict
     constexpr int XS = lti_xs_len<O, L>();
     constexpr int XSP = lti_xs_pad<O, L>();
     constexpr int PF = (XS + 64 * W - 1) / (64 * W);  // x values staged per thread
+    constexpr int KD = W * NB * O;                     // MFMA reduction length
+    constexpr int KSTEPS = KD / 4;
+    constexpr int NBLK = 4 * (L / 16);                 // 16x16 output blocks per tile
+    constexpr int BPW = (NBLK + W - 1) / W;            // blocks per mixing wave
+    static_assert(KD % 4 == 0, "KD multiple of 4");
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* part = lds + 2 * XSP;
+    double* gsb = lds + 2 * XSP;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int band0 = (blockIdx.x * W + wave) * NB;
+    const int grp_band0 = blockIdx.x * W * NB;
+    const int band0 = grp_band0 + wave * NB;
     const long n = a.n;
     const int seg = blockIdx.y;
     const long seg_t0 = (long)seg * a.seg_len;
     const long seg_end = min(seg_t0 + a.seg_len, n);
     const int ntiles = (int)((seg_end - seg_t0 + T - 1) / T);
     const bool last_seg = seg == a.nseg - 1;
-    double* my = part + (long)wave * L * kLtiPartPad;
 
     bool live[NB];
     double S[NB][O], pb[NB], gb[NB];
@@ -225,6 +242,23 @@ __global__ __launch_bounds__(64 * W) void fb_lti_kernel(const double* __restrict
         for (int k = 0; k < O; ++k) S[b][k] = (live[b] && s0) ? s0[k] : 0.0;
         pb[b] = live[b] ? a.pin[bb] : 0.0;
         gb[b] = live[b] ? a.gin[bb] : 0.0;
+    }
+
+    // MFMA B operands (constant over the launch): lane l of k-step q holds
+    // K_band[j][k] for kd = 4q + (l >> 4) = band_local O + k, j = 16 nblk + (l & 15)
+    double bk[MODE == MODE_MIX ? BPW : 1][MODE == MODE_MIX ? KSTEPS : 1];
+    if constexpr (MODE == MODE_MIX) {
+#pragma unroll
+        for (int u = 0; u < BPW; ++u) {
+            const int blk = wave + u * W;
+            const int j = 16 * (blk >> 2) + (lane & 15);
+#pragma unroll
+            for (int q = 0; q < KSTEPS; ++q) {
+                const int kd = 4 * q + (lane >> 4);
+                const int band = grp_band0 + kd / O;
+                bk[u][q] = (blk < NBLK && band < a.nbands) ? rec[(long)band * R::SIZE + R::K + j * O + kd % O] : 0.0;
+            }
+        }
     }
 
     auto load_x = [&](long t0x, double (&pf)[PF]) {
@@ -258,6 +292,7 @@ __global__ __launch_bounds__(64 * W) void fb_lti_kernel(const double* __restrict
         const long t0 = seg_t0 + (long)tile * T;
         const bool last_tile = last_seg && tile == ntiles - 1;
         const double* xs = lds + (tile & 1) * XSP;
+        double* gs_tile = gsb + (tile & 1) * KD * kGsRow;
         double pf[PF];
         const bool more = tile + 1 < ntiles;
         if (more) load_x(t0 + T, pf);
@@ -267,29 +302,32 @@ __global__ __launch_bounds__(64 * W) void fb_lti_kernel(const double* __restrict
 #pragma unroll
         for (int i = 0; i < XW; ++i) xw[i] = xs[lane * (L + 1) + i + i / L];
 
-        double v[L];
-#pragma unroll
-        for (int j = 0; j < L; ++j) v[j] = 0.0;
-
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-            if (!live[b]) continue;  // wave-uniform
-            const double* r = rec + (long)(band0 + b) * R::SIZE;
-            // zero-state end state of the lane's chunk: z[k] = y_zs[tc + L-1-k]
-            double z[O];
+            double st[O];
+            if (live[b]) {  // wave-uniform
+                const double* r = rec + (long)(band0 + b) * R::SIZE;
+                // zero-state end state of the lane's chunk: z[k] = y_zs[tc + L-1-k]
+                // (two interleaved partial sums per k: half the FMA dependency chain)
+                double z[O];
 #pragma unroll
-            for (int k = 0; k < O; ++k) {
-                double acc = r[R::E + k * XW] * xw[0];
+                for (int k = 0; k < O; ++k) {
+                    double acc0 = r[R::E + k * XW] * xw[0];
+                    double acc1 = r[R::E + k * XW + 1] * xw[1];
 #pragma unroll
-                for (int i = 1; i < XW; ++i) acc = fma(r[R::E + k * XW + i], xw[i], acc);
-                z[k] = pb[b] * acc;
-            }
-            // carry scan over the 64 chunks (as fb_mix_kernel): intra-row DPP scan with
-            // M^(2^s), wave-uniform row carries, chunk start st = Z(p-1) + M^p C_row
-            const int row = lane >> 4, p = lane & 15;
-            double qm[O * O];
+                    for (int i = 2; i + 1 < XW; i += 2) {
+                        acc0 = fma(r[R::E + k * XW + i], xw[i], acc0);
+                        acc1 = fma(r[R::E + k * XW + i + 1], xw[i + 1], acc1);
+                    }
+                    if constexpr (XW % 2) acc0 = fma(r[R::E + k * XW + XW - 1], xw[XW - 1], acc0);
+                    z[k] = pb[b] * (acc0 + acc1);
+                }
+                // carry scan over the 64 chunks (as fb_mix_kernel): intra-row DPP scan with
+                // M^(2^s), wave-uniform row carries, chunk start st = Z(p-1) + M^p C_row
+                const int row = lane >> 4, p = lane & 15;
+                double qm[O * O];
 #pragma unroll
-            for (int e = 0; e < O * O; ++e) qm[e] = r[R::Q + p * O * O + e];
+                for (int e = 0; e < O * O; ++e) qm[e] = r[R::Q + p * O * O + e];
 #define HZ_LTI_ROW_STEP(SIDX, D)                                                              \
     {                                                                                         \
         double nb_[O];                                                                        \
@@ -298,61 +336,60 @@ __global__ __launch_bounds__(64 * W) void fb_lti_kernel(const double* __restrict
             _Pragma("unroll") for (int c = 0; c < O; ++c)                                     \
                 z[rr] = fma(r[R::P + (SIDX) * O * O + rr * O + c], nb_[c], z[rr]);            \
     }
-            HZ_LTI_ROW_STEP(0, 1)
-            HZ_LTI_ROW_STEP(1, 2)
-            HZ_LTI_ROW_STEP(2, 4)
-            HZ_LTI_ROW_STEP(3, 8)
+                HZ_LTI_ROW_STEP(0, 1)
+                HZ_LTI_ROW_STEP(1, 2)
+                HZ_LTI_ROW_STEP(2, 4)
+                HZ_LTI_ROW_STEP(3, 8)
 #undef HZ_LTI_ROW_STEP
-            double C[5][O];
+                double C[5][O];
 #pragma unroll
-            for (int k = 0; k < O; ++k) C[0][k] = S[b][k];
+                for (int k = 0; k < O; ++k) C[0][k] = S[b][k];
 #pragma unroll
-            for (int rw = 0; rw < 4; ++rw) {
+                for (int rw = 0; rw < 4; ++rw) {
 #pragma unroll
-                for (int i = 0; i < O; ++i) {
-                    double acc = readlane_d(z[i], 16 * rw + 15);
+                    for (int i = 0; i < O; ++i) {
+                        double acc = readlane_d(z[i], 16 * rw + 15);
 #pragma unroll
-                    for (int q = 0; q < O; ++q) acc = fma(r[R::P + 4 * O * O + i * O + q], C[rw][q], acc);
-                    C[rw + 1][i] = acc;
-                }
-            }
-            double Cr[O], st[O];
-#pragma unroll
-            for (int k = 0; k < O; ++k)
-                Cr[k] = row == 0 ? C[0][k] : row == 1 ? C[1][k] : row == 2 ? C[2][k] : C[3][k];
-#pragma unroll
-            for (int k = 0; k < O; ++k) {
-                double vv = dpp_d<kDppRowShr + 1>(z[k]);  // Z(r, p-1), 0 at p == 0
-#pragma unroll
-                for (int c = 0; c < O; ++c) vv = fma(qm[k * O + c], Cr[c], vv);
-                st[k] = vv;
-            }
-#pragma unroll
-            for (int k = 0; k < O; ++k) S[b][k] = C[4][k];
-
-            if constexpr (MODE == MODE_MIX) {
-                // correction mix: v[j] += sum_k K[j][k] gin st[k]
-                double gs[O];
-#pragma unroll
-                for (int k = 0; k < O; ++k) gs[k] = gb[b] * st[k];
-#pragma unroll
-                for (int j = 0; j < L; ++j)
-#pragma unroll
-                    for (int k = 0; k < O; ++k) v[j] = fma(r[R::K + j * O + k], gs[k], v[j]);
-                if (last_tile) {
-                    // end-of-call y history = the start state of the chunk beginning at n
-                    // (n is a multiple of L; chunks past n see zero input)
-                    const int cn = (int)((n - t0) / L);  // in [1, 64]
-                    const long band = band0 + b;
-                    if (cn < 64) {
-                        if (lane == cn)
-#pragma unroll
-                            for (int k = 0; k < O; ++k) a.ystate_next[band * O + k] = st[k];
-                    } else if (lane == 0) {
-#pragma unroll
-                        for (int k = 0; k < O; ++k) a.ystate_next[band * O + k] = C[4][k];
+                        for (int q = 0; q < O; ++q) acc = fma(r[R::P + 4 * O * O + i * O + q], C[rw][q], acc);
+                        C[rw + 1][i] = acc;
                     }
                 }
+                double Cr[O];
+#pragma unroll
+                for (int k = 0; k < O; ++k)
+                    Cr[k] = row == 0 ? C[0][k] : row == 1 ? C[1][k] : row == 2 ? C[2][k] : C[3][k];
+#pragma unroll
+                for (int k = 0; k < O; ++k) {
+                    double vv = dpp_d<kDppRowShr + 1>(z[k]);  // Z(r, p-1), 0 at p == 0
+#pragma unroll
+                    for (int c = 0; c < O; ++c) vv = fma(qm[k * O + c], Cr[c], vv);
+                    st[k] = vv;
+                }
+#pragma unroll
+                for (int k = 0; k < O; ++k) S[b][k] = C[4][k];
+                if constexpr (MODE == MODE_MIX) {
+                    if (last_tile) {
+                        // end-of-call y history = the start state of the chunk beginning at n
+                        // (n is a multiple of L; chunks past n see zero input)
+                        const int cn = (int)((n - t0) / L);  // in [1, 64]
+                        const long band = band0 + b;
+                        if (cn < 64) {
+                            if (lane == cn)
+#pragma unroll
+                                for (int k = 0; k < O; ++k) a.ystate_next[band * O + k] = st[k];
+                        } else if (lane == 0) {
+#pragma unroll
+                            for (int k = 0; k < O; ++k) a.ystate_next[band * O + k] = C[4][k];
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < O; ++k) st[k] = 0.0;
+            }
+            if constexpr (MODE == MODE_MIX) {
+#pragma unroll
+                for (int k = 0; k < O; ++k) gs_tile[((wave * NB + b) * O + k) * kGsRow + lane] = gb[b] * st[k];
             }
         }
 
@@ -367,27 +404,35 @@ __global__ __launch_bounds__(64 * W) void fb_lti_kernel(const double* __restrict
                     a.pgstate_next[2 * band + 1] = gb[b] + a.sg_n * (G0 - gb[b]);
                 }
             }
-            // ---- workgroup reduction of the per-wave mixes --------------------------
-#pragma unroll
-            for (int j = 0; j < L; ++j) my[j * kLtiPartPad + lane] = v[j];
-            if (more) store_x(lds + ((tile + 1) & 1) * XSP, pf);
-            __syncthreads();
-            for (int tl = threadIdx.x; tl < T; tl += 64 * W) {
-                const int src_lane = tl / L, j = tl % L;
-                const double* q = part + j * kLtiPartPad + src_lane;
-                double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-                for (int w = 0; w < W; w += 2) {
-                    s0 += q[w * L * kLtiPartPad];
-                    if (w + 1 < W) s1 += q[(w + 1) * L * kLtiPartPad];
-                }
-                const long t = t0 + tl;
-                if (t < n) a.partial[(long)blockIdx.x * a.n_pad + t] = s0 + s1;
-            }
-        } else {
-            if (more) store_x(lds + ((tile + 1) & 1) * XSP, pf);
         }
+        if (more) store_x(lds + ((tile + 1) & 1) * XSP, pf);
         __syncthreads();
+        if constexpr (MODE == MODE_MIX) {
+            // ---- group mix on the matrix cores: D[16 chunks][16 samples] per block --------
+#pragma unroll
+            for (int u = 0; u < BPW; ++u) {
+                const int blk = wave + u * W;  // wave-uniform
+                if (blk < NBLK) {
+                    const int m = blk & 3, nblk = blk >> 2;
+                    hz_f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+                    const double* ga = gs_tile + (lane >> 4) * kGsRow + 16 * m + (lane & 15);
+#pragma unroll
+                    for (int q = 0; q < KSTEPS; q += 2) {
+                        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * q * kGsRow], bk[u][q], acc0, 0, 0, 0);
+                        if (q + 1 < KSTEPS)
+                            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * (q + 1) * kGsRow], bk[u][q + 1], acc1,
+                                                                       0, 0, 0);
+                    }
+                    // D row = chunk 16 m + (lane >> 4) + 4 r, column = sample j of the chunk
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        const int chunk = 16 * m + (lane >> 4) + 4 * rr;
+                        const long t = t0 + (long)chunk * L + 16 * nblk + (lane & 15);
+                        if (t < n) a.partial[(long)blockIdx.x * a.n_pad + t] = acc0[rr] + acc1[rr];
+                    }
+                }
+            }
+        }
     }
 
     if constexpr (MODE == MODE_SEGEND) {
@@ -530,4 +575,239 @@ __global__ __launch_bounds__(256) void fb_lti_reduce_kernel(const double* __rest
     if (ty == 0 && t < n) out[t] = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
 }
 
+// ---- kernel selection -------------------------------------------
+typedef void (*CarryKernel)(const double*, const double*, double*, int, int, long);
+typedef void (*LtiKernel)(const double*, LtiArgs);
+typedef void (*FmixKernel)(const double*, const double*, const double*, int, double*);
+typedef void (*LtiReduceKernel)(const double*, long, int, long, const double*, const double*, const double*,
+                                double*);
+
+// geometries: (L, bands per wave, waves per group)
+struct LtiGeom {
+    int L, nb, waves;
+};
+static const LtiGeom kLtiGeoms[] = {{16, 1, 16}, {32, 1, 16}, {16, 2, 8}};
+constexpr int kNumLtiGeoms = 3;
+
+template <int O, int L, int NB, int W>
+LtiKernel lti_kernel_mode(int mode) {
+    static_assert(lti_lds_bytes<O, L>(W, NB, true) <= 160 * 1024, "LTI kernel LDS over 160 KiB");
+    return mode == MODE_SEGEND ? fb_lti_kernel<O, L, NB, W, MODE_SEGEND> : fb_lti_kernel<O, L, NB, W, MODE_MIX>;
+}
+
+template <int O>
+LtiKernel lti_kernel_geom(int geom, int mode) {
+    switch (geom) {
+    case 1: return lti_kernel_mode<O, 32, 1, 16>(mode);
+    case 2: return lti_kernel_mode<O, 16, 2, 8>(mode);
+    default: return lti_kernel_mode<O, 16, 1, 16>(mode);
+    }
+}
+
+static LtiKernel pick_lti(int O, int geom, int mode) {
+    switch (O) {
+    case 1: return lti_kernel_geom<1>(geom, mode);
+    case 2: return lti_kernel_geom<2>(geom, mode);
+    case 3: return lti_kernel_geom<3>(geom, mode);
+    default: return lti_kernel_geom<4>(geom, mode);
+    }
+}
+
+static size_t lti_lds(int O, int geom, bool mix) {
+    const LtiGeom g = kLtiGeoms[geom];
+#define HZ_LTI_LDS(OO)                                                                                  \
+    case OO:                                                                                            \
+        return g.L == 16 ? lti_lds_bytes<OO, 16>(g.waves, g.nb, mix) : lti_lds_bytes<OO, 32>(g.waves, g.nb, mix);
+    switch (O) {
+        HZ_LTI_LDS(1)
+        HZ_LTI_LDS(2)
+        HZ_LTI_LDS(3)
+    default:
+        return g.L == 16 ? lti_lds_bytes<4, 16>(g.waves, g.nb, mix) : lti_lds_bytes<4, 32>(g.waves, g.nb, mix);
+    }
+#undef HZ_LTI_LDS
+}
+
+#define HZ_LTI_OL(TEMPLATE, O, L)                                                                    \
+    (L == 16 ? (O == 1 ? TEMPLATE<1, 16> : O == 2 ? TEMPLATE<2, 16> : O == 3 ? TEMPLATE<3, 16> : TEMPLATE<4, 16>) \
+             : (O == 1 ? TEMPLATE<1, 32> : O == 2 ? TEMPLATE<2, 32> : O == 3 ? TEMPLATE<3, 32> : TEMPLATE<4, 32>))
+static CarryKernel pick_lti_carry(int O, int L) { return HZ_LTI_OL(fb_lti_seg_carry_kernel, O, L); }
+static FmixKernel pick_fmix(int O, int L) { return HZ_LTI_OL(fb_fmix_kernel, O, L); }
+static LtiReduceKernel pick_lti_reduce(int O, int L) { return HZ_LTI_OL(fb_lti_reduce_kernel, O, L); }
+#undef HZ_LTI_OL
+
 }  // namespace
+
+namespace hz_fbi {
+
+int fb_lti_chunk(const hz_fb* h) { return kLtiGeoms[h->lti_geom].L; }
+
+// every band's smoothers at their targets (host mirror), relative to the bank's
+// largest target: the LTI engine then computes the same outputs to ~2^-60
+bool fb_converged(const hz_fb* h) {
+    double pmax = 0, gmax = 0;
+    for (int b = 0; b < h->N; ++b) {
+        pmax = std::max(pmax, std::fabs(h->pin[b]));
+        gmax = std::max(gmax, std::fabs(h->gin[b]));
+    }
+    const double tp = 0x1p-60 * pmax, tg = 0x1p-60 * gmax;
+    for (int b = 0; b < h->N; ++b) {
+        if (!(std::fabs(h->pg_host[2 * (size_t)b] - h->pin[b]) <= tp)) return false;
+        if (!(std::fabs(h->pg_host[2 * (size_t)b + 1] - h->gin[b]) <= tg)) return false;
+    }
+    return true;
+}
+
+int fb_prepare_lti(hz_fb* h) {
+    const int O = h->order;
+    const int L = kLtiGeoms[h->lti_geom].L;
+    if (h->dirty_lti || h->lti_rec_L != L) {
+        const int rs = lti_rec_size(O, L);
+        const size_t need = (size_t)h->N * rs;
+        h->h_rec_lti.assign(need, 0.0);
+        for (int b = 0; b < h->N; ++b)
+            build_record_lti_any(O, L, &h->F[(size_t)b * (O + 1)], &h->B[(size_t)b * O], &h->h_rec_lti[(size_t)b * rs]);
+        if (need > h->rec_lti_cap) {
+            if (h->d_rec_lti) HZ_TRY_HIP(hipFree(h->d_rec_lti));
+            h->d_rec_lti = nullptr;
+            HZ_TRY_HIP(hipMalloc(&h->d_rec_lti, sizeof(double) * need));
+            h->rec_lti_cap = need;
+        }
+        if (!h->d_fmix) HZ_TRY_HIP(hipMalloc(&h->d_fmix, sizeof(double) * 32 * (32 + kMaxOrder)));
+        HZ_TRY_HIP(hipMemcpyAsync(h->d_rec_lti, h->h_rec_lti.data(), sizeof(double) * need, hipMemcpyHostToDevice,
+                                  h->stream));
+        HZ_TRY_HIP(hipStreamSynchronize(h->stream));  // pageable source
+        h->lti_rec = rs;
+        h->lti_rec_L = L;
+        h->dirty_lti = false;
+        h->fmix_valid = false;
+    }
+    if (!h->fmix_valid) {
+        hipLaunchKernelGGL(pick_fmix(O, L), dim3((unsigned)(L * (L + O))), dim3(256), 0, h->stream,
+                           (const double*)h->d_rec_lti, (const double*)h->d_pin, (const double*)h->d_gin, h->N,
+                           h->d_fmix);
+        HZ_TRY_HIP(hipGetLastError());
+        h->fmix_valid = true;
+    }
+    return HZ_OK;
+}
+
+// the converged engine over n samples (n a positive multiple of the chunk length)
+int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
+    HZ_TRY(fb_prepare_lti(h));
+    const int O = h->order;
+    const LtiGeom geom = kLtiGeoms[h->lti_geom];
+    const int L = geom.L;
+    const long T = 64L * L;
+    const int per = geom.waves * geom.nb;
+    const int G = (h->N + per - 1) / per;
+    // partial slab <= 2^27 doubles per launch
+    long chunk = std::max<long>(T, (((1L << 27) / std::max(1, G)) / T) * T);
+    const long n_pad_max = std::min<long>(((n + T - 1) / T) * T, chunk);
+    const size_t need = (size_t)G * n_pad_max;
+    if (need > h->partial_cap) {
+        if (h->d_partial) HZ_TRY_HIP(hipFree(h->d_partial));
+        h->d_partial = nullptr;
+        HZ_TRY_HIP(hipMalloc(&h->d_partial, sizeof(double) * need));
+        h->partial_cap = need;
+    }
+    LtiKernel kmix = pick_lti(O, h->lti_geom, MODE_MIX);
+    LtiKernel kend = pick_lti(O, h->lti_geom, MODE_SEGEND);
+    HZ_TRY(fb_set_lds_attr((const void*)kmix));
+    HZ_TRY(fb_set_lds_attr((const void*)kend));
+    const size_t lds = lti_lds(O, h->lti_geom, true);
+    const size_t lds_end = lti_lds(O, h->lti_geom, false);
+    for (long off = 0; off < n; off += chunk) {
+        const long len = std::min(chunk, n - off);
+        const long ntiles = (len + T - 1) / T;
+        long nseg = std::max<long>(1, std::min<long>(ntiles, (h->target_groups + G - 1) / G));
+        const long seg_tiles = (ntiles + nseg - 1) / nseg;
+        nseg = (ntiles + seg_tiles - 1) / seg_tiles;
+        if (nseg > 1) {
+            const size_t sneed = (size_t)h->N * nseg * O;
+            if (sneed > h->seg_cap) {
+                if (h->d_seg) HZ_TRY_HIP(hipFree(h->d_seg));
+                h->d_seg = nullptr;
+                HZ_TRY_HIP(hipMalloc(&h->d_seg, sizeof(double) * sneed));
+                h->seg_cap = sneed;
+            }
+        }
+        LtiArgs a;
+        a.pin = h->d_pin;
+        a.gin = h->d_gin;
+        a.ystate = h->d_ystate[h->scur];
+        a.ystate_next = h->d_ystate[h->scur ^ 1];
+        a.pgstate = h->d_pg[h->scur];
+        a.pgstate_next = h->d_pg[h->scur ^ 1];
+        a.x = d_in + off;
+        a.xhist = h->d_xhist[h->xcur];
+        a.xhist_next = h->d_xhist[h->xcur ^ 1];
+        a.partial = h->d_partial;
+        a.segstate = h->d_seg;
+        a.n = len;
+        a.n_pad = ntiles * T;
+        a.seg_len = seg_tiles * T;
+        a.nseg = (int)nseg;
+        a.nbands = h->N;
+        a.sp_n = (double)powl((long double)h->sp, (long double)len);
+        a.sg_n = (double)powl((long double)h->sg, (long double)len);
+        hipEvent_t* e = nullptr;
+        if (h->prof) {
+            if (h->ev_used + 4 > h->ev.size()) {
+                for (int q = 0; q < 4 * 64; ++q) {
+                    hipEvent_t ne;
+                    HZ_TRY_HIP(hipEventCreate(&ne));
+                    h->ev.push_back(ne);
+                }
+            }
+            e = &h->ev[h->ev_used];
+            h->ev_used += 4;
+            HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
+        }
+        if (nseg > 1) {
+            hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg - 1)), dim3(64 * geom.waves), lds_end, h->stream,
+                               (const double*)h->d_rec_lti, a);
+            HZ_TRY_HIP(hipGetLastError());
+            hipLaunchKernelGGL(pick_lti_carry(O, L), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0, h->stream,
+                               (const double*)h->d_rec_lti, (const double*)h->d_ystate[h->scur], h->d_seg, h->N,
+                               (int)nseg, seg_tiles);
+            HZ_TRY_HIP(hipGetLastError());
+        }
+        if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
+        hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * geom.waves), lds, h->stream,
+                           (const double*)h->d_rec_lti, a);
+        HZ_TRY_HIP(hipGetLastError());
+        if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
+        hipLaunchKernelGGL(pick_lti_reduce(O, L), dim3((unsigned)((len + 63) / 64)), dim3(256), 0, h->stream,
+                           (const double*)h->d_partial, a.n_pad, G, len, a.x, a.xhist, (const double*)h->d_fmix,
+                           d_out + off);
+        HZ_TRY_HIP(hipGetLastError());
+        if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
+        h->xcur ^= 1;
+        h->scur ^= 1;
+        h->prof_launches += h->prof ? 1 : 0;
+        fb_mirror_advance(h, len);
+    }
+    return HZ_OK;
+}
+
+}  // namespace hz_fbi
+
+extern "C" {
+
+int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group) {
+    if (!h) return HZ_E_INVALID;
+    if (!chunk && !bands_per_wave && !waves_per_group) {
+        h->lti_geom = 0;
+        return HZ_OK;
+    }
+    for (int g = 0; g < kNumLtiGeoms; ++g)
+        if (kLtiGeoms[g].L == chunk && kLtiGeoms[g].nb == bands_per_wave && kLtiGeoms[g].waves == waves_per_group) {
+            h->lti_geom = g;
+            return HZ_OK;
+        }
+    hz::set_error("hz_fb_tune_lti: (chunk, bands/wave, waves) must be one of (16,1,16), (32,1,16), (16,2,8)");
+    return HZ_E_INVALID;
+}
+
+}  // extern "C"

@@ -28,13 +28,14 @@
 #include <new>
 #include <vector>
 
-#include "hz_common.h"
+#include "hz_fb_impl.h"
 
 namespace {
 
+using namespace hz_fbi;
+
 constexpr int kL = 16;            // samples per lane chunk
 constexpr int kTile = 64 * kL;    // samples per wave tile (= reference BSIZE 1024)
-constexpr int kMaxOrder = 4;
 
 // Per-band record (doubles), O-dependent layout.
 template <int O>
@@ -82,34 +83,6 @@ struct MixArgs {
     double dist_param;
 };
 
-// Scalar (SGPR) copy of a wave-uniform double.
-__device__ __forceinline__ double uniform(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffff));
-    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// DPP lane moves on a double (two 32-bit halves).  bound_ctrl: lanes whose
-// source is outside the pattern read 0.
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, true);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-constexpr int kDppRowShr = 0x110;   // row_shr:n = 0x110 + n (within 16-lane rows)
-// (wave-wide DPP shifts / row_bcast do not exist on CDNA; cross-row moves use
-//  ds_bpermute or v_readlane)
-
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
 // LDS layout of one workgroup:
 //   xs   : the tile's input x[t0-16 .. t0+1023], padded one slot per 16 samples so
 //          lane c's reads (17c + k) hit 64 distinct banks (ds_read_b64)
@@ -130,11 +103,6 @@ __device__ __forceinline__ int xs_pos(int li) { return li + (li >> 4); }
 // MODE_SEGEND: zero-state end state of each segment but the last (no mixdown),
 //   feeding fb_seg_carry_kernel when the bank is too small to fill the chip
 //   with bands alone (e.g. 512-band shards on 8 GPUs).
-enum { MODE_MIX = 0, MODE_SEGEND = 1 };
-
-}  // namespace
-#include "hz_fb_lti.h"
-namespace {
 
 // PF (x values prefetched per thread) fixes the workgroup size: 2 -> 16 waves, 3 -> 8, 5 -> 4;
 // the launch bound follows it, so 4-wave groups get the whole VGPR file (NB > 1 bands per
@@ -660,116 +628,7 @@ static CarryKernel pick_carry(int O) {
     }
 }
 
-// ---- LTI path kernels (hz_fb_lti.h) -------------------------------------------
-typedef void (*LtiKernel)(const double*, LtiArgs);
-typedef void (*FmixKernel)(const double*, const double*, const double*, int, double*);
-typedef void (*LtiReduceKernel)(const double*, long, int, long, const double*, const double*, const double*,
-                                double*);
-
-// geometries: (L, bands per wave, waves per group)
-struct LtiGeom {
-    int L, nb, waves;
-};
-static const LtiGeom kLtiGeoms[] = {{16, 1, 16}, {32, 4, 4}, {16, 2, 8}};
-constexpr int kNumLtiGeoms = 3;
-
-template <int O, int L, int NB, int W>
-LtiKernel lti_kernel_mode(int mode) {
-    static_assert(lti_lds_bytes<O, L>(W, true) <= 160 * 1024, "LTI kernel LDS over 160 KiB");
-    return mode == MODE_SEGEND ? fb_lti_kernel<O, L, NB, W, MODE_SEGEND> : fb_lti_kernel<O, L, NB, W, MODE_MIX>;
-}
-
-template <int O>
-LtiKernel lti_kernel_geom(int geom, int mode) {
-    switch (geom) {
-    case 1: return lti_kernel_mode<O, 32, 4, 4>(mode);
-    case 2: return lti_kernel_mode<O, 16, 2, 8>(mode);
-    default: return lti_kernel_mode<O, 16, 1, 16>(mode);
-    }
-}
-
-static LtiKernel pick_lti(int O, int geom, int mode) {
-    switch (O) {
-    case 1: return lti_kernel_geom<1>(geom, mode);
-    case 2: return lti_kernel_geom<2>(geom, mode);
-    case 3: return lti_kernel_geom<3>(geom, mode);
-    default: return lti_kernel_geom<4>(geom, mode);
-    }
-}
-
-static size_t lti_lds(int O, int geom, bool mix) {
-    const LtiGeom g = kLtiGeoms[geom];
-#define HZ_LTI_LDS(OO)                                                                                  \
-    case OO:                                                                                            \
-        return g.L == 16 ? lti_lds_bytes<OO, 16>(g.waves, mix) : lti_lds_bytes<OO, 32>(g.waves, mix);
-    switch (O) {
-        HZ_LTI_LDS(1)
-        HZ_LTI_LDS(2)
-        HZ_LTI_LDS(3)
-    default:
-        return g.L == 16 ? lti_lds_bytes<4, 16>(g.waves, mix) : lti_lds_bytes<4, 32>(g.waves, mix);
-    }
-#undef HZ_LTI_LDS
-}
-
-#define HZ_LTI_OL(TEMPLATE, O, L)                                                                    \
-    (L == 16 ? (O == 1 ? TEMPLATE<1, 16> : O == 2 ? TEMPLATE<2, 16> : O == 3 ? TEMPLATE<3, 16> : TEMPLATE<4, 16>) \
-             : (O == 1 ? TEMPLATE<1, 32> : O == 2 ? TEMPLATE<2, 32> : O == 3 ? TEMPLATE<3, 32> : TEMPLATE<4, 32>))
-static CarryKernel pick_lti_carry(int O, int L) { return HZ_LTI_OL(fb_lti_seg_carry_kernel, O, L); }
-static FmixKernel pick_fmix(int O, int L) { return HZ_LTI_OL(fb_fmix_kernel, O, L); }
-static LtiReduceKernel pick_lti_reduce(int O, int L) { return HZ_LTI_OL(fb_lti_reduce_kernel, O, L); }
-#undef HZ_LTI_OL
-
 }  // namespace
-
-// ---------------------------------------------------------------------------
-// handle
-// ---------------------------------------------------------------------------
-struct hz_fb {
-    int order = 2, N = 0, N_total = 0, band_begin = 0, device = 0;
-    double sp = 0, sg = 0;
-    int rec = 8;
-    // host shadows of the staged parameters
-    std::vector<double> F, B, pin, gin;
-    bool dirty_coef = true, dirty_pin = true, dirty_gin = true;
-    int dist_id = HZ_DIST_NONE;
-    double dist_param = 0;
-    // geometry
-    int waves = 16, bands_per_wave = 1;
-    // device buffers
-    double *d_rec = nullptr, *d_pin = nullptr, *d_gin = nullptr;
-    double *d_ystate[2] = {nullptr, nullptr}, *d_pg[2] = {nullptr, nullptr};
-    int scur = 0;  // current state buffer (ping-pong per launch)
-    double* d_xhist[2] = {nullptr, nullptr};
-    int xcur = 0;
-    double* d_partial = nullptr;
-    size_t partial_cap = 0;  // doubles
-    double* d_seg = nullptr;  // segment start states
-    size_t seg_cap = 0;
-    int target_groups = 256;  // workgroups wanted per launch (CU count)
-    double *d_in = nullptr, *d_out = nullptr;
-    size_t io_cap = 0;       // doubles
-    std::vector<double> h_rec;
-    hipStream_t stream = nullptr;
-    bool own_stream = false;
-    // profiling
-    bool prof = false;
-    std::vector<hipEvent_t> ev;  // quadruplets
-    size_t ev_used = 0;
-    long prof_launches = 0;
-    // converged (LTI) path, hz_fb_lti.h
-    int path_mode = HZ_FB_PATH_AUTO;
-    int last_path = HZ_FB_PATH_GENERAL;
-    int lti_geom = 0;                // index into kLtiGeoms
-    int lti_rec = 0, lti_rec_L = 0;  // record size / chunk length the LTI records were built for
-    bool dirty_lti = true;           // coefficients changed since the LTI records were built
-    bool fmix_valid = false;         // Fmix matches the current coefficients, pin and gin
-    double* d_rec_lti = nullptr;
-    size_t rec_lti_cap = 0;
-    double* d_fmix = nullptr;        // [L][L+O]
-    std::vector<double> h_rec_lti;
-    std::vector<double> pg_host;     // host mirror of the smoother state [N][2] (pre, gain)
-};
 
 namespace {
 
@@ -814,6 +673,10 @@ long fb_max_chunk(const hz_fb* h) {
     c = std::max<long>(kTile, (c / kTile) * kTile);
     return c;
 }
+
+}  // namespace
+
+namespace hz_fbi {
 
 int fb_set_lds_attr(const void* k) {
     static thread_local std::vector<const void*> done;
@@ -935,159 +798,14 @@ int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n) {
     return HZ_OK;
 }
 
-// every band's smoothers at their targets (host mirror), relative to the bank's
-// largest target: the LTI engine then computes the same outputs to ~2^-60
-bool fb_converged(const hz_fb* h) {
-    double pmax = 0, gmax = 0;
-    for (int b = 0; b < h->N; ++b) {
-        pmax = std::max(pmax, std::fabs(h->pin[b]));
-        gmax = std::max(gmax, std::fabs(h->gin[b]));
-    }
-    const double tp = 0x1p-60 * pmax, tg = 0x1p-60 * gmax;
-    for (int b = 0; b < h->N; ++b) {
-        if (!(std::fabs(h->pg_host[2 * (size_t)b] - h->pin[b]) <= tp)) return false;
-        if (!(std::fabs(h->pg_host[2 * (size_t)b + 1] - h->gin[b]) <= tg)) return false;
-    }
-    return true;
-}
+}  // namespace hz_fbi
 
-int fb_prepare_lti(hz_fb* h) {
-    const int O = h->order;
-    const int L = kLtiGeoms[h->lti_geom].L;
-    if (h->dirty_lti || h->lti_rec_L != L) {
-        const int rs = lti_rec_size(O, L);
-        const size_t need = (size_t)h->N * rs;
-        h->h_rec_lti.assign(need, 0.0);
-        for (int b = 0; b < h->N; ++b)
-            build_record_lti_any(O, L, &h->F[(size_t)b * (O + 1)], &h->B[(size_t)b * O], &h->h_rec_lti[(size_t)b * rs]);
-        if (need > h->rec_lti_cap) {
-            if (h->d_rec_lti) HZ_TRY_HIP(hipFree(h->d_rec_lti));
-            h->d_rec_lti = nullptr;
-            HZ_TRY_HIP(hipMalloc(&h->d_rec_lti, sizeof(double) * need));
-            h->rec_lti_cap = need;
-        }
-        if (!h->d_fmix) HZ_TRY_HIP(hipMalloc(&h->d_fmix, sizeof(double) * 32 * (32 + kMaxOrder)));
-        HZ_TRY_HIP(hipMemcpyAsync(h->d_rec_lti, h->h_rec_lti.data(), sizeof(double) * need, hipMemcpyHostToDevice,
-                                  h->stream));
-        HZ_TRY_HIP(hipStreamSynchronize(h->stream));  // pageable source
-        h->lti_rec = rs;
-        h->lti_rec_L = L;
-        h->dirty_lti = false;
-        h->fmix_valid = false;
-    }
-    if (!h->fmix_valid) {
-        hipLaunchKernelGGL(pick_fmix(O, L), dim3((unsigned)(L * (L + O))), dim3(256), 0, h->stream,
-                           (const double*)h->d_rec_lti, (const double*)h->d_pin, (const double*)h->d_gin, h->N,
-                           h->d_fmix);
-        HZ_TRY_HIP(hipGetLastError());
-        h->fmix_valid = true;
-    }
-    return HZ_OK;
-}
-
-// the converged engine over n samples (n a positive multiple of the chunk length)
-int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
-    HZ_TRY(fb_prepare_lti(h));
-    const int O = h->order;
-    const LtiGeom geom = kLtiGeoms[h->lti_geom];
-    const int L = geom.L;
-    const long T = 64L * L;
-    const int per = geom.waves * geom.nb;
-    const int G = (h->N + per - 1) / per;
-    // partial slab <= 2^27 doubles per launch
-    long chunk = std::max<long>(T, (((1L << 27) / std::max(1, G)) / T) * T);
-    const long n_pad_max = std::min<long>(((n + T - 1) / T) * T, chunk);
-    const size_t need = (size_t)G * n_pad_max;
-    if (need > h->partial_cap) {
-        if (h->d_partial) HZ_TRY_HIP(hipFree(h->d_partial));
-        h->d_partial = nullptr;
-        HZ_TRY_HIP(hipMalloc(&h->d_partial, sizeof(double) * need));
-        h->partial_cap = need;
-    }
-    LtiKernel kmix = pick_lti(O, h->lti_geom, MODE_MIX);
-    LtiKernel kend = pick_lti(O, h->lti_geom, MODE_SEGEND);
-    HZ_TRY(fb_set_lds_attr((const void*)kmix));
-    HZ_TRY(fb_set_lds_attr((const void*)kend));
-    const size_t lds = lti_lds(O, h->lti_geom, true);
-    const size_t lds_end = lti_lds(O, h->lti_geom, false);
-    for (long off = 0; off < n; off += chunk) {
-        const long len = std::min(chunk, n - off);
-        const long ntiles = (len + T - 1) / T;
-        long nseg = std::max<long>(1, std::min<long>(ntiles, (h->target_groups + G - 1) / G));
-        const long seg_tiles = (ntiles + nseg - 1) / nseg;
-        nseg = (ntiles + seg_tiles - 1) / seg_tiles;
-        if (nseg > 1) {
-            const size_t sneed = (size_t)h->N * nseg * O;
-            if (sneed > h->seg_cap) {
-                if (h->d_seg) HZ_TRY_HIP(hipFree(h->d_seg));
-                h->d_seg = nullptr;
-                HZ_TRY_HIP(hipMalloc(&h->d_seg, sizeof(double) * sneed));
-                h->seg_cap = sneed;
-            }
-        }
-        LtiArgs a;
-        a.pin = h->d_pin;
-        a.gin = h->d_gin;
-        a.ystate = h->d_ystate[h->scur];
-        a.ystate_next = h->d_ystate[h->scur ^ 1];
-        a.pgstate = h->d_pg[h->scur];
-        a.pgstate_next = h->d_pg[h->scur ^ 1];
-        a.x = d_in + off;
-        a.xhist = h->d_xhist[h->xcur];
-        a.xhist_next = h->d_xhist[h->xcur ^ 1];
-        a.partial = h->d_partial;
-        a.segstate = h->d_seg;
-        a.n = len;
-        a.n_pad = ntiles * T;
-        a.seg_len = seg_tiles * T;
-        a.nseg = (int)nseg;
-        a.nbands = h->N;
-        a.sp_n = (double)powl((long double)h->sp, (long double)len);
-        a.sg_n = (double)powl((long double)h->sg, (long double)len);
-        hipEvent_t* e = nullptr;
-        if (h->prof) {
-            if (h->ev_used + 4 > h->ev.size()) {
-                for (int q = 0; q < 4 * 64; ++q) {
-                    hipEvent_t ne;
-                    HZ_TRY_HIP(hipEventCreate(&ne));
-                    h->ev.push_back(ne);
-                }
-            }
-            e = &h->ev[h->ev_used];
-            h->ev_used += 4;
-            HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
-        }
-        if (nseg > 1) {
-            hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg - 1)), dim3(64 * geom.waves), lds_end, h->stream,
-                               (const double*)h->d_rec_lti, a);
-            HZ_TRY_HIP(hipGetLastError());
-            hipLaunchKernelGGL(pick_lti_carry(O, L), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0, h->stream,
-                               (const double*)h->d_rec_lti, (const double*)h->d_ystate[h->scur], h->d_seg, h->N,
-                               (int)nseg, seg_tiles);
-            HZ_TRY_HIP(hipGetLastError());
-        }
-        if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
-        hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * geom.waves), lds, h->stream,
-                           (const double*)h->d_rec_lti, a);
-        HZ_TRY_HIP(hipGetLastError());
-        if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
-        hipLaunchKernelGGL(pick_lti_reduce(O, L), dim3((unsigned)((len + 63) / 64)), dim3(256), 0, h->stream,
-                           (const double*)h->d_partial, a.n_pad, G, len, a.x, a.xhist, (const double*)h->d_fmix,
-                           d_out + off);
-        HZ_TRY_HIP(hipGetLastError());
-        if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
-        h->xcur ^= 1;
-        h->scur ^= 1;
-        h->prof_launches += h->prof ? 1 : 0;
-        fb_mirror_advance(h, len);
-    }
-    return HZ_OK;
-}
+namespace {
 
 int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
     if (n <= 0) return HZ_OK;
     h->last_path = HZ_FB_PATH_GENERAL;
-    const int L = kLtiGeoms[h->lti_geom].L;
+    const int L = fb_lti_chunk(h);
     const long n_lti = n - n % L;
     if (h->path_mode == HZ_FB_PATH_AUTO && h->order > 0 && h->dist_id == HZ_DIST_NONE && n_lti > 0 &&
         fb_converged(h)) {
@@ -1427,21 +1145,6 @@ int hz_fb_last_path(hz_fb* h, int* path) {
     if (!h || !path) return HZ_E_INVALID;
     *path = h->last_path;
     return HZ_OK;
-}
-
-int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group) {
-    if (!h) return HZ_E_INVALID;
-    if (!chunk && !bands_per_wave && !waves_per_group) {
-        h->lti_geom = 0;
-        return HZ_OK;
-    }
-    for (int g = 0; g < kNumLtiGeoms; ++g)
-        if (kLtiGeoms[g].L == chunk && kLtiGeoms[g].nb == bands_per_wave && kLtiGeoms[g].waves == waves_per_group) {
-            h->lti_geom = g;
-            return HZ_OK;
-        }
-    hz::set_error("hz_fb_tune_lti: (chunk, bands/wave, waves) must be one of (16,1,16), (32,4,4), (16,2,8)");
-    return HZ_E_INVALID;
 }
 
 int hz_fb_profile(hz_fb* h, int enable) {
