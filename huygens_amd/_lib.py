@@ -10,7 +10,7 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libhuygens_hip.so")
+LIB_PATH = os.environ.get("HZ_LIB_PATH") or os.path.join(_HERE, "lib", "libhuygens_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "huygens_hip.h")
 
 HZ_OK = 0

@@ -36,11 +36,15 @@ using namespace hz_fbi;
 template <int O, int L>
 struct RecL {
     static constexpr int XW = L + O;            // chunk input window x[tc-O .. tc+L-1]
-    static constexpr int E = 0;                 // E[k][i]  k<O, i<XW : F[L-1-k][i]
-    static constexpr int K = E + O * XW;        // K[j][k]  j<L, k<O  : homogeneous response
-    static constexpr int P = K + L * O;         // P[s] = M^(2^s), s<6 (M: chunk transition)
-    static constexpr int Q = P + 6 * O * O;     // Q[p] = M^p, p<16
-    static constexpr int H = Q + 16 * O * O;    // H[d], d<XW : FIR*IIR impulse response
+    // scalar block, read by the mix kernel every tile (kept small and contiguous so the
+    // 16 bands of a CU stay resident in the scalar cache):
+    static constexpr int E0 = 0;                // E[0][m], m < XW (E[k][i] = E[0][i+k], i >= O)
+    static constexpr int EH = E0 + XW;          // E[k][i], k, i < O (history taps)
+    static constexpr int PS = EH + O * O;       // M^1, M^2, M^4, M^8, M^64
+    static constexpr int SC_END = PS + 5 * O * O;
+    static constexpr int K = SC_END;            // K[j][k]  j<L, k<O  : homogeneous response
+    static constexpr int QC = K + L * O;        // QC[e] = M^e, e <= 64 (M: chunk transition)
+    static constexpr int H = QC + 65 * O * O;   // H[d], d<XW : FIR*IIR impulse response
     static constexpr int GE = H + XW;           // GE[i][j], i<O, j<L : F[j][i] (history taps)
     static constexpr int RAW = GE + O * L;
     static constexpr int SIZE = (RAW + 7) & ~7;
@@ -93,8 +97,9 @@ void build_record_lti(const double* b, const double* av, double* rec) {
     for (int i = 0; i < O; ++i)
         for (int j = 0; j < L; ++j) rec[R::GE + i * L + j] = (double)F(j, i);
     if constexpr (O > 0) {
+        for (int m = 0; m < XW; ++m) rec[R::E0 + m] = (double)F(L - 1, m);
         for (int k = 0; k < O; ++k)
-            for (int i = 0; i < XW; ++i) rec[R::E + k * XW + i] = (double)F(L - 1 - k, i);
+            for (int i = 0; i < O; ++i) rec[R::EH + k * O + i] = (double)F(L - 1 - k, i);
         // homogeneous responses: y[-1-k] = 1, zero input
         long double Kh[L][O];
         for (int k = 0; k < O; ++k) {
@@ -115,9 +120,13 @@ void build_record_lti(const double* b, const double* av, double* rec) {
                 M[r][c] = Kh[L - 1 - r][c];
                 Qp[r][c] = (r == c) ? 1.0L : 0.0L;
             }
-        for (int p = 0; p < 16; ++p) {
+        for (int e = 0; e <= 64; ++e) {
+            const int ps = e == 1 ? 0 : e == 2 ? 1 : e == 4 ? 2 : e == 8 ? 3 : e == 64 ? 4 : -1;
             for (int r = 0; r < O; ++r)
-                for (int c = 0; c < O; ++c) rec[R::Q + p * O * O + r * O + c] = (double)Qp[r][c];
+                for (int c = 0; c < O; ++c) {
+                    rec[R::QC + e * O * O + r * O + c] = (double)Qp[r][c];
+                    if (ps >= 0) rec[R::PS + ps * O * O + r * O + c] = (double)Qp[r][c];
+                }
             for (int r = 0; r < O; ++r)
                 for (int c = 0; c < O; ++c) {
                     long double acc = 0;
@@ -125,17 +134,6 @@ void build_record_lti(const double* b, const double* av, double* rec) {
                     T[r][c] = acc;
                 }
             std::memcpy(Qp, T, sizeof(Qp));
-        }
-        for (int s = 0; s < 6; ++s) {
-            for (int r = 0; r < O; ++r)
-                for (int c = 0; c < O; ++c) rec[R::P + s * O * O + r * O + c] = (double)M[r][c];
-            for (int r = 0; r < O; ++r)
-                for (int c = 0; c < O; ++c) {
-                    long double acc = 0;
-                    for (int q = 0; q < O; ++q) acc += M[r][q] * M[q][c];
-                    T[r][c] = acc;
-                }
-            std::memcpy(M, T, sizeof(M));
         }
     }
 }
@@ -184,43 +182,71 @@ template <int O, int L>
 __host__ __device__ constexpr int lti_xs_pad() {
     return ((lti_xs_len<O, L>() + lti_xs_len<O, L>() / L + 1) + 1) & ~1;
 }
-// gs rows [KD = W NB O][64 chunks + 16 pad]: the MFMA A-operand reads (16 chunks of
-// two rows per 32-lane group) land on disjoint bank halves; double-buffered.
+// gs rows [KD = 16 O][64 chunks + 16 pad]: the MFMA B-operand reads (16 chunks of two
+// rows per 32-lane group) land on disjoint bank halves.  Double-buffered by tile.
 constexpr int kGsRow = 80;
+constexpr int kLtiWaves = 16;  // one band per wave, 16 bands per workgroup
+template <int L>
+__host__ __device__ constexpr int lti_nblk() { return 4 * (L / 16); }  // 16x16 output blocks per tile
+template <int L>
+__host__ __device__ constexpr int lti_parts() { return kLtiWaves / lti_nblk<L>(); }  // k-split of a block
 template <int O, int L>
-__host__ __device__ constexpr size_t lti_lds_bytes(int waves, int nb, bool mix) {
-    return sizeof(double) * (2 * (size_t)lti_xs_pad<O, L>() + (mix ? 2 * (size_t)waves * nb * O * kGsRow : 0));
+__host__ __device__ constexpr size_t lti_lds_bytes(bool mix) {
+    return sizeof(double) *
+           (2 * (size_t)lti_xs_pad<O, L>() +
+            (mix ? 2 * (size_t)kLtiWaves * O * kGsRow + 2 * (size_t)(lti_parts<L>() - 1) * lti_nblk<L>() * 256 : 0));
 }
 
 typedef double hz_f64x4 __attribute__((ext_vector_type(4)));
 
-// One workgroup = W waves x NB bands (band group g = blockIdx.x) over one time
-// segment (blockIdx.y); a wave walks the segment's tiles carrying its bands' state.
-// Per tile: each wave computes, for its bands, the chunk zero-state end states (E, VALU
-// with wave-uniform coefficients), the carry scan and the chunk start states st; it
-// stores gs = gin st to LDS.  After the barrier the bank group's correction mix
-//   D[chunk][j] = sum_{(band,k)} gs[(band,k)][chunk] K_band[j][k]
-// is a (64 x KD) x (KD x L) product on the FP64 matrix cores (v_mfma_f64_16x16x4f64):
-// the reduction over the group's bands happens inside the MFMA, no per-band LDS rows.
-template <int O, int L, int NB, int W, int MODE>
-__global__ __launch_bounds__(64 * W) void fb_lti_kernel(const double* __restrict__ rec, LtiArgs a) {
+// DPP move of a double with a row mask: rows outside ROWMASK keep 0 (old), lanes whose
+// source is outside the pattern read 0 (bound_ctrl).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_dm(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, ROWMASK, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWMASK, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int kDppWaveShr1 = 0x138;   // lane l <- lane l-1 across rows (gfx950: probed)
+constexpr int kDppRowBcast15 = 0x142; // rows 1, 3 <- lane 15 of the row below (row_mask 0xa)
+constexpr int kDppRowBcast31 = 0x143; // rows 2, 3 <- lane 31 (row_mask 0xc)
+
+// One workgroup = 16 waves = 16 bands (band group g = blockIdx.x) over one time segment
+// (blockIdx.y); each wave walks the segment's tiles carrying its band's state.
+// Per tile (64 lane chunks of L samples) a wave computes its band's chunk zero-state end
+// states z (VALU, E row from scalar loads), the inclusive 64-lane prefix of the chunk
+// recurrence s' = M s + z entirely in VGPRs (row_shr 1,2,4,8 with M^(2^s), row_bcast:15
+// with M^(p+1), row_bcast:31 with M^(l-31)), the chunk start states st = Z(l-1) + M^l S
+// (wave_shr:1) and the tile end state S' = Z(63) + M^64 S, and stores gs = gin st.
+// The group's correction mix D[chunk][j] = sum_(band,k) gs K_band[j][k] runs on the FP64
+// matrix cores one tile behind (v_mfma_f64_16x16x4f64): every wave owns one 16x16 output
+// block and one k-slice of it, the k-slices are summed through LDS one more tile behind.
+// All LDS images are double-buffered, so there is one barrier per tile.
+template <int O, int L, int MODE>
+__global__ __launch_bounds__(64 * kLtiWaves) void fb_lti_kernel(const double* __restrict__ rec, LtiArgs a) {
     using R = RecL<O, L>;
+    constexpr int W = kLtiWaves;
     constexpr int XW = R::XW;
     constexpr int T = 64 * L;
     constexpr int XS = lti_xs_len<O, L>();
     constexpr int XSP = lti_xs_pad<O, L>();
     constexpr int PF = (XS + 64 * W - 1) / (64 * W);  // x values staged per thread
-    constexpr int KD = W * NB * O;                     // MFMA reduction length
-    constexpr int KSTEPS = KD / 4;
-    constexpr int NBLK = 4 * (L / 16);                 // 16x16 output blocks per tile
-    constexpr int BPW = (NBLK + W - 1) / W;            // blocks per mixing wave
-    static_assert(KD % 4 == 0, "KD multiple of 4");
+    constexpr int KD = W * O;                          // MFMA reduction length (band states)
+    constexpr int NBLK = lti_nblk<L>();
+    constexpr int PARTS = lti_parts<L>();
+    constexpr int KPP = KD / 4 / PARTS;                // k-steps per wave
+    static_assert(KD % (4 * PARTS) == 0, "k-split");
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* gsb = lds + 2 * XSP;
+    double* dxb = gsb + 2 * KD * kGsRow;  // [2][PARTS-1][NBLK][64 lanes][4]
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int grp_band0 = blockIdx.x * W * NB;
-    const int band0 = grp_band0 + wave * NB;
+    const int grp_band0 = blockIdx.x * W;
+    const int band = grp_band0 + wave;
+    const bool live = band < a.nbands;
+    const int bandc = live ? band : a.nbands - 1;  // dead waves run a live band's numbers, gs = 0
+    const double* r = rec + (long)bandc * R::SIZE;
     const long n = a.n;
     const int seg = blockIdx.y;
     const long seg_t0 = (long)seg * a.seg_len;
@@ -228,223 +254,207 @@ __global__ __launch_bounds__(64 * W) void fb_lti_kernel(const double* __restrict
     const int ntiles = (int)((seg_end - seg_t0 + T - 1) / T);
     const bool last_seg = seg == a.nseg - 1;
 
-    bool live[NB];
-    double S[NB][O], pb[NB], gb[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const int band = band0 + b;
-        live[b] = band < a.nbands;
-        const int bb = live[b] ? band : 0;
+    double S[O];
+    {
         const double* s0 = (MODE == MODE_SEGEND) ? nullptr
-                         : (seg == 0) ? a.ystate + (long)bb * O
-                                      : a.segstate + ((long)bb * a.nseg + seg) * O;
+                         : (seg == 0) ? a.ystate + (long)bandc * O
+                                      : a.segstate + ((long)bandc * a.nseg + seg) * O;
 #pragma unroll
-        for (int k = 0; k < O; ++k) S[b][k] = (live[b] && s0) ? s0[k] : 0.0;
-        pb[b] = live[b] ? a.pin[bb] : 0.0;
-        gb[b] = live[b] ? a.gin[bb] : 0.0;
+        for (int k = 0; k < O; ++k) S[k] = (live && s0) ? s0[k] : 0.0;
     }
+    const double pb = live ? a.pin[band] : 0.0;
+    const double gb = live ? a.gin[band] : 0.0;
 
-    // MFMA B operands (constant over the launch): lane l of k-step q holds
-    // K_band[j][k] for kd = 4q + (l >> 4) = band_local O + k, j = 16 nblk + (l & 15)
-    double bk[MODE == MODE_MIX ? BPW : 1][MODE == MODE_MIX ? KSTEPS : 1];
-    if constexpr (MODE == MODE_MIX) {
+    // per-lane chunk-transition powers: M^l (carry-in), M^(p+1) (row_bcast:15), M^(l-31)
+    // (row_bcast:31); loop-invariant
+    double qc[O * O], qa[O * O], qb[O * O];
+    {
+        const int ea = (lane & 15) + 1, eb = lane >= 32 ? lane - 31 : 0;
 #pragma unroll
-        for (int u = 0; u < BPW; ++u) {
-            const int blk = wave + u * W;
-            const int j = 16 * (blk >> 2) + (lane & 15);
-#pragma unroll
-            for (int q = 0; q < KSTEPS; ++q) {
-                const int kd = 4 * q + (lane >> 4);
-                const int band = grp_band0 + kd / O;
-                bk[u][q] = (blk < NBLK && band < a.nbands) ? rec[(long)band * R::SIZE + R::K + j * O + kd % O] : 0.0;
-            }
+        for (int e = 0; e < O * O; ++e) {
+            qc[e] = r[R::QC + lane * O * O + e];
+            qa[e] = r[R::QC + ea * O * O + e];
+            qb[e] = r[R::QC + eb * O * O + e];
         }
     }
 
+    // MFMA B operands of this wave's (block, k-slice): lane l of k-step q holds K_band[j][k]
+    // for kd = 4 (part KPP + q) + (l >> 4) = band_local O + k, j = 16 (blk >> 2) + (l & 15)
+    const int blk = wave % NBLK, part = wave / NBLK;
+    double bk[MODE == MODE_MIX ? KPP : 1];
+    if constexpr (MODE == MODE_MIX) {
+        const int j = 16 * (blk >> 2) + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < KPP; ++q) {
+            const int kd = 4 * (part * KPP + q) + (lane >> 4);
+            const int bnd = grp_band0 + kd / O;
+            bk[q] = bnd < a.nbands ? rec[(long)bnd * R::SIZE + R::K + j * O + kd % O] : 0.0;
+        }
+    }
+
+    // x staging: unconditional loads from clamped addresses + a select for the zero tail
+    // (a load under a branch makes the compiler wait for it on the spot); the O history
+    // taps before the call's first sample are patched in after the store (first tile only)
     auto load_x = [&](long t0x, double (&pf)[PF]) {
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
             const int li = threadIdx.x + q * 64 * W;
             const long idx = t0x - O + li;
-            double v = 0.0;
-            if (li < XS) {
-                if (idx < 0) v = a.xhist[-idx - 1];
-                else if (idx < seg_end) v = a.x[idx];
-            }
-            pf[q] = v;
+            const long ci = idx < 0 ? 0 : (idx < seg_end ? idx : seg_end - 1);
+            pf[q] = a.x[ci];
         }
     };
-    auto store_x = [&](double* xbuf, const double (&pf)[PF]) {
+    auto store_x = [&](double* xbuf, const double (&pf)[PF], long t0x) {
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
             const int li = threadIdx.x + q * 64 * W;
-            if (li < XS) xbuf[li + li / L] = pf[q];
+            const long idx = t0x - O + li;
+            if (li < XS) xbuf[li + li / L] = idx < seg_end ? pf[q] : 0.0;
         }
+        if (t0x == 0 && threadIdx.x < O) xbuf[threadIdx.x] = a.xhist[O - 1 - threadIdx.x];  // x[-O+li]
     };
     {
         double pf0[PF];
         load_x(seg_t0, pf0);
-        store_x(lds, pf0);
+        store_x(lds, pf0, seg_t0);
         __syncthreads();
     }
 
-    for (int tile = 0; tile < ntiles; ++tile) {
-        const long t0 = seg_t0 + (long)tile * T;
-        const bool last_tile = last_seg && tile == ntiles - 1;
-        const double* xs = lds + (tile & 1) * XSP;
-        double* gs_tile = gsb + (tile & 1) * KD * kGsRow;
-        double pf[PF];
-        const bool more = tile + 1 < ntiles;
-        if (more) load_x(t0 + T, pf);
-
-        // the lane's chunk window x[tc-O .. tc+L-1] (li = L lane + i -> lane (L+1) + i + i/L)
-        double xw[XW];
+    double st[O];          // chunk start states of the last tile processed
+    hz_f64x4 dhold = {0.0, 0.0, 0.0, 0.0};  // part-0 waves: own k-slice of the previous tile
+    const int niter = (MODE == MODE_MIX) ? ntiles + 2 : ntiles;
+    for (int it = 0; it < niter; ++it) {
+        // ---- (C) tile it-2: sum the k-slices of this wave's block, store the group mix ----
+        if constexpr (MODE == MODE_MIX) {
+            if (part == 0 && it >= 2) {
+                const double* dx = dxb + ((it - 2) & 1) * (PARTS - 1) * NBLK * 256;
+                hz_f64x4 acc = dhold;
 #pragma unroll
-        for (int i = 0; i < XW; ++i) xw[i] = xs[lane * (L + 1) + i + i / L];
-
+                for (int pp = 0; pp < PARTS - 1; ++pp)
 #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            double st[O];
-            if (live[b]) {  // wave-uniform
-                const double* r = rec + (long)(band0 + b) * R::SIZE;
-                // zero-state end state of the lane's chunk: z[k] = y_zs[tc + L-1-k]
-                // (two interleaved partial sums per k: half the FMA dependency chain)
-                double z[O];
+                    for (int rr = 0; rr < 4; ++rr) acc[rr] += dx[((pp * NBLK + blk) * 64 + lane) * 4 + rr];
+                const long t0m = seg_t0 + (long)(it - 2) * T;
+                const int m = blk & 3, nb = blk >> 2;
 #pragma unroll
-                for (int k = 0; k < O; ++k) {
-                    double acc0 = r[R::E + k * XW] * xw[0];
-                    double acc1 = r[R::E + k * XW + 1] * xw[1];
-#pragma unroll
-                    for (int i = 2; i + 1 < XW; i += 2) {
-                        acc0 = fma(r[R::E + k * XW + i], xw[i], acc0);
-                        acc1 = fma(r[R::E + k * XW + i + 1], xw[i + 1], acc1);
-                    }
-                    if constexpr (XW % 2) acc0 = fma(r[R::E + k * XW + XW - 1], xw[XW - 1], acc0);
-                    z[k] = pb[b] * (acc0 + acc1);
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int chunk = 16 * m + (lane >> 4) + 4 * rr;
+                    const long t = t0m + (long)chunk * L + 16 * nb + (lane & 15);
+                    if (t < n) a.partial[(long)blockIdx.x * a.n_pad + t] = acc[rr];
                 }
-                // carry scan over the 64 chunks (as fb_mix_kernel): intra-row DPP scan with
-                // M^(2^s), wave-uniform row carries, chunk start st = Z(p-1) + M^p C_row
-                const int row = lane >> 4, p = lane & 15;
-                double qm[O * O];
+            }
+            // ---- (B) tile it-1: this wave's k-slice of its output block on the MFMA --------
+            if (it >= 1 && it <= ntiles) {
+                const double* gs = gsb + ((it - 1) & 1) * KD * kGsRow;
+                const int m = blk & 3;
+                const double* ga = gs + (4 * part * KPP + (lane >> 4)) * kGsRow + 16 * m + (lane & 15);
+                hz_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int e = 0; e < O * O; ++e) qm[e] = r[R::Q + p * O * O + e];
-#define HZ_LTI_ROW_STEP(SIDX, D)                                                              \
+                for (int q = 0; q < KPP; ++q)
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * q * kGsRow], bk[q], acc, 0, 0, 0);
+                if (part == 0) {
+                    dhold = acc;
+                } else {
+                    double* dx = dxb + ((it - 1) & 1) * (PARTS - 1) * NBLK * 256;
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) dx[(((part - 1) * NBLK + blk) * 64 + lane) * 4 + rr] = acc[rr];
+                }
+            }
+        }
+        // ---- (A) tile it: band work --------------------------------------------------------
+        const bool has_tile = it < ntiles;
+        const long t0 = seg_t0 + (long)it * T;
+        double pf[PF];
+        const bool more = it + 1 < ntiles;
+        if (more) load_x(t0 + T, pf);
+        if (has_tile) {
+            const double* xs = lds + (it & 1) * XSP;
+            // the lane's chunk window x[tc-O .. tc+L-1] (li = L lane + i -> lane (L+1) + i + i/L)
+            double xw[XW];
+#pragma unroll
+            for (int i = 0; i < XW; ++i) xw[i] = xs[lane * (L + 1) + i + i / L];
+            // zero-state end state of the lane's chunk: z[k] = y_zs[tc + L-1-k]
+            double z[O];
+#pragma unroll
+            for (int k = 0; k < O; ++k) {
+                double acc0 = r[R::EH + k * O] * xw[0], acc1 = 0.0;
+#pragma unroll
+                for (int i = 1; i < O; ++i) acc0 = fma(r[R::EH + k * O + i], xw[i], acc0);
+#pragma unroll
+                for (int i = O; i + k < XW; ++i) {
+                    if ((i - O) & 1) acc1 = fma(r[R::E0 + i + k], xw[i], acc1);
+                    else acc0 = fma(r[R::E0 + i + k], xw[i], acc0);
+                }
+                z[k] = pb * (acc0 + acc1);
+            }
+            // inclusive prefix over the 64 chunks (zero carry-in)
+#define HZ_LTI_SCAN_STEP(CTRL, RM, MAT)                                                       \
     {                                                                                         \
         double nb_[O];                                                                        \
-        _Pragma("unroll") for (int k = 0; k < O; ++k) nb_[k] = dpp_d<kDppRowShr + (D)>(z[k]); \
+        _Pragma("unroll") for (int k = 0; k < O; ++k) nb_[k] = dpp_dm<CTRL, RM>(z[k]);        \
         _Pragma("unroll") for (int rr = 0; rr < O; ++rr)                                      \
-            _Pragma("unroll") for (int c = 0; c < O; ++c)                                     \
-                z[rr] = fma(r[R::P + (SIDX) * O * O + rr * O + c], nb_[c], z[rr]);            \
+            _Pragma("unroll") for (int c = 0; c < O; ++c) z[rr] = fma(MAT[rr * O + c], nb_[c], z[rr]); \
     }
-                HZ_LTI_ROW_STEP(0, 1)
-                HZ_LTI_ROW_STEP(1, 2)
-                HZ_LTI_ROW_STEP(2, 4)
-                HZ_LTI_ROW_STEP(3, 8)
-#undef HZ_LTI_ROW_STEP
-                double C[5][O];
+            const double* p1 = r + R::PS;
+            const double* p2 = r + R::PS + O * O;
+            const double* p4 = r + R::PS + 2 * O * O;
+            const double* p8 = r + R::PS + 3 * O * O;
+            HZ_LTI_SCAN_STEP(kDppRowShr + 1, 0xf, p1)
+            HZ_LTI_SCAN_STEP(kDppRowShr + 2, 0xf, p2)
+            HZ_LTI_SCAN_STEP(kDppRowShr + 4, 0xf, p4)
+            HZ_LTI_SCAN_STEP(kDppRowShr + 8, 0xf, p8)
+            HZ_LTI_SCAN_STEP(kDppRowBcast15, 0xa, qa)
+            HZ_LTI_SCAN_STEP(kDppRowBcast31, 0xc, qb)
+#undef HZ_LTI_SCAN_STEP
+            // chunk start states and the tile end state
+            double Sn[O];
 #pragma unroll
-                for (int k = 0; k < O; ++k) C[0][k] = S[b][k];
+            for (int k = 0; k < O; ++k) {
+                double vv = dpp_dm<kDppWaveShr1, 0xf>(z[k]);  // Z(l-1), 0 at lane 0
+                double sn = readlane_d(z[k], 63);
 #pragma unroll
-                for (int rw = 0; rw < 4; ++rw) {
-#pragma unroll
-                    for (int i = 0; i < O; ++i) {
-                        double acc = readlane_d(z[i], 16 * rw + 15);
-#pragma unroll
-                        for (int q = 0; q < O; ++q) acc = fma(r[R::P + 4 * O * O + i * O + q], C[rw][q], acc);
-                        C[rw + 1][i] = acc;
-                    }
+                for (int c = 0; c < O; ++c) {
+                    vv = fma(qc[k * O + c], S[c], vv);
+                    sn = fma(r[R::PS + 4 * O * O + k * O + c], S[c], sn);
                 }
-                double Cr[O];
-#pragma unroll
-                for (int k = 0; k < O; ++k)
-                    Cr[k] = row == 0 ? C[0][k] : row == 1 ? C[1][k] : row == 2 ? C[2][k] : C[3][k];
-#pragma unroll
-                for (int k = 0; k < O; ++k) {
-                    double vv = dpp_d<kDppRowShr + 1>(z[k]);  // Z(r, p-1), 0 at p == 0
-#pragma unroll
-                    for (int c = 0; c < O; ++c) vv = fma(qm[k * O + c], Cr[c], vv);
-                    st[k] = vv;
-                }
-#pragma unroll
-                for (int k = 0; k < O; ++k) S[b][k] = C[4][k];
-                if constexpr (MODE == MODE_MIX) {
-                    if (last_tile) {
-                        // end-of-call y history = the start state of the chunk beginning at n
-                        // (n is a multiple of L; chunks past n see zero input)
-                        const int cn = (int)((n - t0) / L);  // in [1, 64]
-                        const long band = band0 + b;
-                        if (cn < 64) {
-                            if (lane == cn)
-#pragma unroll
-                                for (int k = 0; k < O; ++k) a.ystate_next[band * O + k] = st[k];
-                        } else if (lane == 0) {
-#pragma unroll
-                            for (int k = 0; k < O; ++k) a.ystate_next[band * O + k] = C[4][k];
-                        }
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < O; ++k) st[k] = 0.0;
+                st[k] = vv;
+                Sn[k] = sn;
             }
+#pragma unroll
+            for (int k = 0; k < O; ++k) S[k] = Sn[k];
             if constexpr (MODE == MODE_MIX) {
+                double* gs = gsb + (it & 1) * KD * kGsRow;
 #pragma unroll
-                for (int k = 0; k < O; ++k) gs_tile[((wave * NB + b) * O + k) * kGsRow + lane] = gb[b] * st[k];
-            }
-        }
-
-        if constexpr (MODE == MODE_MIX) {
-            if (last_tile && lane == 0) {
+                for (int k = 0; k < O; ++k) gs[(wave * O + k) * kGsRow + lane] = gb * st[k];
+                if (last_seg && it == ntiles - 1 && live) {
+                    // end-of-call y history = the start state of the chunk beginning at n
+                    // (n is a multiple of L; chunks past n see zero input)
+                    const int cn = (int)((n - t0) / L);  // in [1, 64]
+                    if (cn < 64) {
+                        if (lane == cn)
 #pragma unroll
-                for (int b = 0; b < NB; ++b) {
-                    if (!live[b]) continue;
-                    const long band = band0 + b;
-                    const double P0 = a.pgstate[2 * band], G0 = a.pgstate[2 * band + 1];
-                    a.pgstate_next[2 * band] = pb[b] + a.sp_n * (P0 - pb[b]);
-                    a.pgstate_next[2 * band + 1] = gb[b] + a.sg_n * (G0 - gb[b]);
+                            for (int k = 0; k < O; ++k) a.ystate_next[(long)band * O + k] = st[k];
+                    } else if (lane == 0) {
+#pragma unroll
+                        for (int k = 0; k < O; ++k) a.ystate_next[(long)band * O + k] = S[k];
+                    }
                 }
             }
         }
-        if (more) store_x(lds + ((tile + 1) & 1) * XSP, pf);
+        if (more) store_x(lds + ((it + 1) & 1) * XSP, pf, t0 + T);
         __syncthreads();
-        if constexpr (MODE == MODE_MIX) {
-            // ---- group mix on the matrix cores: D[16 chunks][16 samples] per block --------
-#pragma unroll
-            for (int u = 0; u < BPW; ++u) {
-                const int blk = wave + u * W;  // wave-uniform
-                if (blk < NBLK) {
-                    const int m = blk & 3, nblk = blk >> 2;
-                    hz_f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-                    const double* ga = gs_tile + (lane >> 4) * kGsRow + 16 * m + (lane & 15);
-#pragma unroll
-                    for (int q = 0; q < KSTEPS; q += 2) {
-                        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * q * kGsRow], bk[u][q], acc0, 0, 0, 0);
-                        if (q + 1 < KSTEPS)
-                            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * (q + 1) * kGsRow], bk[u][q + 1], acc1,
-                                                                       0, 0, 0);
-                    }
-                    // D row = chunk 16 m + (lane >> 4) + 4 r, column = sample j of the chunk
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) {
-                        const int chunk = 16 * m + (lane >> 4) + 4 * rr;
-                        const long t = t0 + (long)chunk * L + 16 * nblk + (lane & 15);
-                        if (t < n) a.partial[(long)blockIdx.x * a.n_pad + t] = acc0[rr] + acc1[rr];
-                    }
-                }
-            }
-        }
     }
 
     if constexpr (MODE == MODE_SEGEND) {
-        if (lane == 0 && !last_seg) {
+        if (lane == 0 && !last_seg && live) {
 #pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                if (!live[b]) continue;
-#pragma unroll
-                for (int k = 0; k < O; ++k) a.segstate[((long)(band0 + b) * a.nseg + seg + 1) * O + k] = S[b][k];
-            }
+            for (int k = 0; k < O; ++k) a.segstate[((long)band * a.nseg + seg + 1) * O + k] = S[k];
         }
     } else {
+        if (last_seg && lane == 0 && live) {
+            const double P0 = a.pgstate[2 * (long)band], G0 = a.pgstate[2 * (long)band + 1];
+            a.pgstate_next[2 * (long)band] = pb + a.sp_n * (P0 - pb);
+            a.pgstate_next[2 * (long)band + 1] = gb + a.sg_n * (G0 - gb);
+        }
         if (last_seg && blockIdx.x == 0 && threadIdx.x < O) {
             const int k = threadIdx.x;
             const long idx = n - 1 - k;
@@ -454,7 +464,7 @@ __global__ __launch_bounds__(64 * W) void fb_lti_kernel(const double* __restrict
 }
 
 // Sequential carry over time segments (one thread per band), LTI records:
-//   start(s+1) = M_tile^seg_tiles start(s) + zsr_end(s), M_tile = P[5]^2 = M^64.
+//   start(s+1) = M_tile^seg_tiles start(s) + zsr_end(s), M_tile = M^64 = QC[64].
 template <int O, int L>
 __global__ __launch_bounds__(256) void fb_lti_seg_carry_kernel(const double* __restrict__ rec,
                                                                const double* __restrict__ ystate,
@@ -469,10 +479,7 @@ __global__ __launch_bounds__(256) void fb_lti_seg_carry_kernel(const double* __r
     for (int i = 0; i < O; ++i)
 #pragma unroll
         for (int j = 0; j < O; ++j) {
-            double acc = 0;
-#pragma unroll
-            for (int q = 0; q < O; ++q) acc = fma(r[R::P + 5 * O * O + i * O + q], r[R::P + 5 * O * O + q * O + j], acc);
-            Pw[i][j] = acc;
+            Pw[i][j] = r[R::QC + 64 * O * O + i * O + j];
             M[i][j] = (i == j) ? 1.0 : 0.0;
         }
     for (long e = seg_tiles; e > 0; e >>= 1) {
@@ -582,26 +589,22 @@ typedef void (*FmixKernel)(const double*, const double*, const double*, int, dou
 typedef void (*LtiReduceKernel)(const double*, long, int, long, const double*, const double*, const double*,
                                 double*);
 
-// geometries: (L, bands per wave, waves per group)
+// geometries: (L, bands per wave, waves per group); one band per wave, 16 waves
 struct LtiGeom {
     int L, nb, waves;
 };
-static const LtiGeom kLtiGeoms[] = {{16, 1, 16}, {32, 1, 16}, {16, 2, 8}};
-constexpr int kNumLtiGeoms = 3;
+static const LtiGeom kLtiGeoms[] = {{16, 1, 16}, {32, 1, 16}};
+constexpr int kNumLtiGeoms = 2;
 
-template <int O, int L, int NB, int W>
+template <int O, int L>
 LtiKernel lti_kernel_mode(int mode) {
-    static_assert(lti_lds_bytes<O, L>(W, NB, true) <= 160 * 1024, "LTI kernel LDS over 160 KiB");
-    return mode == MODE_SEGEND ? fb_lti_kernel<O, L, NB, W, MODE_SEGEND> : fb_lti_kernel<O, L, NB, W, MODE_MIX>;
+    static_assert(lti_lds_bytes<O, L>(true) <= 160 * 1024, "LTI kernel LDS over 160 KiB");
+    return mode == MODE_SEGEND ? fb_lti_kernel<O, L, MODE_SEGEND> : fb_lti_kernel<O, L, MODE_MIX>;
 }
 
 template <int O>
 LtiKernel lti_kernel_geom(int geom, int mode) {
-    switch (geom) {
-    case 1: return lti_kernel_mode<O, 32, 1, 16>(mode);
-    case 2: return lti_kernel_mode<O, 16, 2, 8>(mode);
-    default: return lti_kernel_mode<O, 16, 1, 16>(mode);
-    }
+    return kLtiGeoms[geom].L == 32 ? lti_kernel_mode<O, 32>(mode) : lti_kernel_mode<O, 16>(mode);
 }
 
 static LtiKernel pick_lti(int O, int geom, int mode) {
@@ -614,18 +617,13 @@ static LtiKernel pick_lti(int O, int geom, int mode) {
 }
 
 static size_t lti_lds(int O, int geom, bool mix) {
-    const LtiGeom g = kLtiGeoms[geom];
-#define HZ_LTI_LDS(OO)                                                                                  \
-    case OO:                                                                                            \
-        return g.L == 16 ? lti_lds_bytes<OO, 16>(g.waves, g.nb, mix) : lti_lds_bytes<OO, 32>(g.waves, g.nb, mix);
+    const bool l32 = kLtiGeoms[geom].L == 32;
     switch (O) {
-        HZ_LTI_LDS(1)
-        HZ_LTI_LDS(2)
-        HZ_LTI_LDS(3)
-    default:
-        return g.L == 16 ? lti_lds_bytes<4, 16>(g.waves, g.nb, mix) : lti_lds_bytes<4, 32>(g.waves, g.nb, mix);
+    case 1: return l32 ? lti_lds_bytes<1, 32>(mix) : lti_lds_bytes<1, 16>(mix);
+    case 2: return l32 ? lti_lds_bytes<2, 32>(mix) : lti_lds_bytes<2, 16>(mix);
+    case 3: return l32 ? lti_lds_bytes<3, 32>(mix) : lti_lds_bytes<3, 16>(mix);
+    default: return l32 ? lti_lds_bytes<4, 32>(mix) : lti_lds_bytes<4, 16>(mix);
     }
-#undef HZ_LTI_LDS
 }
 
 #define HZ_LTI_OL(TEMPLATE, O, L)                                                                    \
@@ -806,7 +804,7 @@ int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group)
             h->lti_geom = g;
             return HZ_OK;
         }
-    hz::set_error("hz_fb_tune_lti: (chunk, bands/wave, waves) must be one of (16,1,16), (32,1,16), (16,2,8)");
+    hz::set_error("hz_fb_tune_lti: (chunk, bands/wave, waves) must be one of (16,1,16), (32,1,16)");
     return HZ_E_INVALID;
 }
 

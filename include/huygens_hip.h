@@ -106,7 +106,7 @@ int hz_fb_set_target_groups(hz_fb* h, int groups);
 int hz_fb_set_path(hz_fb* h, int path);
 int hz_fb_last_path(hz_fb* h, int* path);
 /* LTI engine geometry: (chunk length, bands per wave, waves per group) in
- * {(16,1,16), (32,1,16), (16,2,8)}; 0s = default */
+ * {(16,1,16), (32,1,16)}; 0s = default */
 int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group);
 
 /* ---- Oscbank<double,N>  (src/oscbank.h:15-97, src/multichannel.h:16-159) -- */
