@@ -26,7 +26,10 @@
 // i.e. O(L+O) + O L FMAs per chunk instead of running the recurrence twice per
 // sample (hz_filterbank.hip's general kernel).  The result is the same linear map
 // evaluated in another association order (parity: tests/test_filterbank_lti_gpu.py).
+#include <cstdlib>
+
 #include "hz_fb_impl.h"
+
 
 namespace {
 
@@ -182,19 +185,16 @@ template <int O, int L>
 __host__ __device__ constexpr int lti_xs_pad() {
     return ((lti_xs_len<O, L>() + lti_xs_len<O, L>() / L + 1) + 1) & ~1;
 }
-// gs rows [KD = 16 O][64 chunks + 16 pad]: the MFMA B-operand reads (16 chunks of two
-// rows per 32-lane group) land on disjoint bank halves.  Double-buffered by tile.
-constexpr int kGsRow = 80;
-constexpr int kLtiWaves = 16;  // one band per wave, 16 bands per workgroup
-template <int L>
-__host__ __device__ constexpr int lti_nblk() { return 4 * (L / 16); }  // 16x16 output blocks per tile
-template <int L>
-__host__ __device__ constexpr int lti_parts() { return kLtiWaves / lti_nblk<L>(); }  // k-split of a block
+// Workgroup geometry: one band per wave; 16 waves (bands) per workgroup for O <= 2,
+// 8 for O >= 3 (LDS).  BS = band states of a group, padded to the 16-wide MFMA blocks.
+__host__ __device__ constexpr int lti_waves(int O) { return O <= 2 ? 16 : 8; }
+__host__ __device__ constexpr int lti_bsp(int O) { return (lti_waves(O) * O + 15) / 16 * 16; }
+constexpr int kZRow = 65;   // z rows [BSP][64 chunks + 1]: E-block writes hit 16 banks apart
+constexpr int kGsRow = 80;  // gs rows [BSP][64 chunks + 16]: mix A-operand reads on disjoint bank halves
 template <int O, int L>
 __host__ __device__ constexpr size_t lti_lds_bytes(bool mix) {
-    return sizeof(double) *
-           (2 * (size_t)lti_xs_pad<O, L>() +
-            (mix ? 2 * (size_t)kLtiWaves * O * kGsRow + 2 * (size_t)(lti_parts<L>() - 1) * lti_nblk<L>() * 256 : 0));
+    return sizeof(double) * (2 * (size_t)lti_xs_pad<O, L>() + 2 * (size_t)lti_bsp(O) * kZRow +
+                             (mix ? 2 * (size_t)lti_bsp(O) * kGsRow : 0));
 }
 
 typedef double hz_f64x4 __attribute__((ext_vector_type(4)));
@@ -212,34 +212,39 @@ constexpr int kDppWaveShr1 = 0x138;   // lane l <- lane l-1 across rows (gfx950:
 constexpr int kDppRowBcast15 = 0x142; // rows 1, 3 <- lane 15 of the row below (row_mask 0xa)
 constexpr int kDppRowBcast31 = 0x143; // rows 2, 3 <- lane 31 (row_mask 0xc)
 
-// One workgroup = 16 waves = 16 bands (band group g = blockIdx.x) over one time segment
-// (blockIdx.y); each wave walks the segment's tiles carrying its band's state.
-// Per tile (64 lane chunks of L samples) a wave computes its band's chunk zero-state end
-// states z (VALU, E row from scalar loads), the inclusive 64-lane prefix of the chunk
-// recurrence s' = M s + z entirely in VGPRs (row_shr 1,2,4,8 with M^(2^s), row_bcast:15
-// with M^(p+1), row_bcast:31 with M^(l-31)), the chunk start states st = Z(l-1) + M^l S
-// (wave_shr:1) and the tile end state S' = Z(63) + M^64 S, and stores gs = gin st.
-// The group's correction mix D[chunk][j] = sum_(band,k) gs K_band[j][k] runs on the FP64
-// matrix cores one tile behind (v_mfma_f64_16x16x4f64): every wave owns one 16x16 output
-// block and one k-slice of it, the k-slices are summed through LDS one more tile behind.
-// All LDS images are double-buffered, so there is one barrier per tile.
+// One workgroup = W waves = W bands (group g = blockIdx.x) over one time segment
+// (blockIdx.y).  Per tile of 64 lane chunks x L samples, three phases run one tile
+// apart (one barrier per tile, every LDS image double-buffered):
+//  (E) zero-state end states of every chunk for every band of the group, on the FP64
+//      matrix cores: Z[chunk][bs] = X[chunk][tap] . E[tap][bs]  (v_mfma_f64_16x16x4f64;
+//      A = the chunk windows read from the staged x tile, B = the group's E rows, held
+//      in registers for the whole launch), written to LDS as z[bs][chunk];
+//  (S) per band (wave) and chunk (lane): the inclusive 64-lane prefix of the chunk
+//      recurrence s' = M s + pin z, entirely in VGPRs (row_shr 1,2,4,8 with M^(2^s),
+//      row_bcast:15 with M^(p+1), row_bcast:31 with M^(l-31)), the chunk start states
+//      st = Z(l-1) + M^l S (wave_shr:1) and the tile end state S' = Z(63) + M^64 S;
+//      gs = gin st to LDS;
+//  (M) the group's correction mix D[chunk][j] = sum_bs gs[bs][chunk] K[bs][j] on the
+//      matrix cores, stored as this group's row of the partial slab.
+// The (E) and (M) blocks are spread over the waves as independent work items.
 template <int O, int L, int MODE>
-__global__ __launch_bounds__(64 * kLtiWaves) void fb_lti_kernel(const double* __restrict__ rec, LtiArgs a) {
+__global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double* __restrict__ rec, LtiArgs a) {
     using R = RecL<O, L>;
-    constexpr int W = kLtiWaves;
+    constexpr int W = lti_waves(O);
     constexpr int XW = R::XW;
     constexpr int T = 64 * L;
     constexpr int XS = lti_xs_len<O, L>();
     constexpr int XSP = lti_xs_pad<O, L>();
     constexpr int PF = (XS + 64 * W - 1) / (64 * W);  // x values staged per thread
-    constexpr int KD = W * O;                          // MFMA reduction length (band states)
-    constexpr int NBLK = lti_nblk<L>();
-    constexpr int PARTS = lti_parts<L>();
-    constexpr int KPP = KD / 4 / PARTS;                // k-steps per wave
-    static_assert(KD % (4 * PARTS) == 0, "k-split");
+    constexpr int BSP = lti_bsp(O);
+    constexpr int KE = (XW + 3) / 4;                  // E k-steps (taps, zero padded)
+    constexpr int NE = 4 * (BSP / 16);                // E blocks (4 chunk blocks x state blocks)
+    constexpr int KM = BSP / 4;                       // mix k-steps (band states)
+    constexpr int NM = (MODE == MODE_MIX) ? 4 * (L / 16) : 0;  // mix blocks (chunk blocks x sample blocks)
+    constexpr int IPW = (NE + NM + W - 1) / W;        // MFMA work items per wave
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* gsb = lds + 2 * XSP;
-    double* dxb = gsb + 2 * KD * kGsRow;  // [2][PARTS-1][NBLK][64 lanes][4]
+    double* zb = lds + 2 * XSP;      // [2][BSP][kZRow]
+    double* gsb = zb + 2 * BSP * kZRow;  // [2][BSP][kGsRow]
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int grp_band0 = blockIdx.x * W;
@@ -278,23 +283,35 @@ __global__ __launch_bounds__(64 * kLtiWaves) void fb_lti_kernel(const double* __
         }
     }
 
-    // MFMA B operands of this wave's (block, k-slice): lane l of k-step q holds K_band[j][k]
-    // for kd = 4 (part KPP + q) + (l >> 4) = band_local O + k, j = 16 (blk >> 2) + (l & 15)
-    const int blk = wave % NBLK, part = wave / NBLK;
-    double bk[MODE == MODE_MIX ? KPP : 1];
-    if constexpr (MODE == MODE_MIX) {
-        const int j = 16 * (blk >> 2) + (lane & 15);
+    // MFMA B operands of this wave's work items (item u = wave + W v): E items hold
+    // E[tap][bs] (tap = 4q + (l >> 4), bs = 16 sb + (l & 15)), mix items K[bs][j]
+    // (bs = 4q + (l >> 4), j = 16 jb + (l & 15)); zero outside the group / taps.
+    constexpr int KB = KE > KM ? KE : KM;
+    double bop[IPW][KB];
 #pragma unroll
-        for (int q = 0; q < KPP; ++q) {
-            const int kd = 4 * (part * KPP + q) + (lane >> 4);
-            const int bnd = grp_band0 + kd / O;
-            bk[q] = bnd < a.nbands ? rec[(long)bnd * R::SIZE + R::K + j * O + kd % O] : 0.0;
+    for (int v = 0; v < IPW; ++v) {
+        const int item = wave + W * v;
+#pragma unroll
+        for (int q = 0; q < KB; ++q) {
+            double val = 0.0;
+            if (item < NE) {
+                const int sb = item >> 2, tap = 4 * q + (lane >> 4), bs = 16 * sb + (lane & 15);
+                const int bl = bs / O, k = bs % O, bnd = grp_band0 + bl;
+                if (q < KE && bl < W && bnd < a.nbands && tap < XW) {
+                    const double* rb = rec + (long)bnd * R::SIZE;
+                    val = tap < O ? rb[R::EH + k * O + tap] : (tap + k < XW ? rb[R::E0 + tap + k] : 0.0);
+                }
+            } else if (item < NE + NM) {
+                const int jb = (item - NE) >> 2, bs = 4 * q + (lane >> 4), j = 16 * jb + (lane & 15);
+                const int bl = bs / O, k = bs % O, bnd = grp_band0 + bl;
+                if (q < KM && bl < W && bnd < a.nbands) val = rec[(long)bnd * R::SIZE + R::K + j * O + k];
+            }
+            bop[v][q] = val;
         }
     }
 
-    // x staging: unconditional loads from clamped addresses + a select for the zero tail
-    // (a load under a branch makes the compiler wait for it on the spot); the O history
-    // taps before the call's first sample are patched in after the store (first tile only)
+    // x staging: unconditional loads from clamped addresses, the zero-tail select at
+    // store time; the O history taps before the call's first sample are patched in
     auto load_x = [&](long t0x, double (&pf)[PF]) {
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
@@ -313,86 +330,99 @@ __global__ __launch_bounds__(64 * kLtiWaves) void fb_lti_kernel(const double* __
         }
         if (t0x == 0 && threadIdx.x < O) xbuf[threadIdx.x] = a.xhist[O - 1 - threadIdx.x];  // x[-O+li]
     };
-    {
-        double pf0[PF];
-        load_x(seg_t0, pf0);
-        store_x(lds, pf0, seg_t0);
-        __syncthreads();
-    }
 
-    double st[O];          // chunk start states of the last tile processed
-    hz_f64x4 dhold = {0.0, 0.0, 0.0, 0.0};  // part-0 waves: own k-slice of the previous tile
-    const int niter = (MODE == MODE_MIX) ? ntiles + 2 : ntiles;
-    for (int it = 0; it < niter; ++it) {
-        // ---- (C) tile it-2: sum the k-slices of this wave's block, store the group mix ----
-        if constexpr (MODE == MODE_MIX) {
-            if (part == 0 && it >= 2) {
-                const double* dx = dxb + ((it - 2) & 1) * (PARTS - 1) * NBLK * 256;
-                hz_f64x4 acc = dhold;
+    // (E) for tile te: this wave's E blocks -> z buffer (te & 1)
+    auto phase_e = [&](int te) {
+        const double* xs = lds + (te & 1) * XSP;
+        double* z = zb + (te & 1) * BSP * kZRow;
 #pragma unroll
-                for (int pp = 0; pp < PARTS - 1; ++pp)
+        for (int v = 0; v < IPW; ++v) {
+            const int item = wave + W * v;  // wave-uniform
+            if (item < NE) {
+                const int m = item & 3, sb = item >> 2;
+                // A: lane l holds X[chunk 16m + (l & 15)][tap 4q + (l >> 4)]
+                const int li0 = (16 * m + (lane & 15)) * L + (lane >> 4);
+                hz_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) acc[rr] += dx[((pp * NBLK + blk) * 64 + lane) * 4 + rr];
-                const long t0m = seg_t0 + (long)(it - 2) * T;
-                const int m = blk & 3, nb = blk >> 2;
+                for (int q = 0; q < KE; ++q) {
+                    const int li = li0 + 4 * q;
+                    const double xa = (4 * q + (lane >> 4) < XW) ? xs[li + li / L] : 0.0;
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, bop[v][q], acc, 0, 0, 0);
+                }
+                // D: col = band state 16 sb + (l & 15), row = chunk 16 m + (l >> 4) + 4 rr
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                    z[(16 * sb + (lane & 15)) * kZRow + 16 * m + (lane >> 4) + 4 * rr] = acc[rr];
+            }
+        }
+    };
+    // (M) for tile tm: this wave's mix blocks -> partial slab
+    auto phase_m = [&](int tm) {
+        const double* gs = gsb + (tm & 1) * BSP * kGsRow;
+        const long t0m = seg_t0 + (long)tm * T;
+#pragma unroll
+        for (int v = 0; v < IPW; ++v) {
+            const int item = wave + W * v - NE;  // wave-uniform
+            if (item >= 0 && item < NM) {
+                const int m = item & 3, jb = item >> 2;
+                const double* ga = gs + (lane >> 4) * kGsRow + 16 * m + (lane & 15);
+                hz_f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int q = 0; q < KM; q += 2) {
+                    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * q * kGsRow], bop[v][q], acc0, 0, 0, 0);
+                    if (q + 1 < KM)
+                        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * (q + 1) * kGsRow], bop[v][q + 1], acc1, 0,
+                                                                   0, 0);
+                }
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
                     const int chunk = 16 * m + (lane >> 4) + 4 * rr;
-                    const long t = t0m + (long)chunk * L + 16 * nb + (lane & 15);
-                    if (t < n) a.partial[(long)blockIdx.x * a.n_pad + t] = acc[rr];
-                }
-            }
-            // ---- (B) tile it-1: this wave's k-slice of its output block on the MFMA --------
-            if (it >= 1 && it <= ntiles) {
-                const double* gs = gsb + ((it - 1) & 1) * KD * kGsRow;
-                const int m = blk & 3;
-                const double* ga = gs + (4 * part * KPP + (lane >> 4)) * kGsRow + 16 * m + (lane & 15);
-                hz_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int q = 0; q < KPP; ++q)
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * q * kGsRow], bk[q], acc, 0, 0, 0);
-                if (part == 0) {
-                    dhold = acc;
-                } else {
-                    double* dx = dxb + ((it - 1) & 1) * (PARTS - 1) * NBLK * 256;
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) dx[(((part - 1) * NBLK + blk) * 64 + lane) * 4 + rr] = acc[rr];
+                    const long t = t0m + (long)chunk * L + 16 * jb + (lane & 15);
+                    if (t < n) a.partial[(long)blockIdx.x * a.n_pad + t] = acc0[rr] + acc1[rr];
                 }
             }
         }
-        // ---- (A) tile it: band work --------------------------------------------------------
-        const bool has_tile = it < ntiles;
+    };
+
+    // prologue: x tiles 0 and 1 staged, gs padding rows zeroed, (E) of tile 0
+    {
+        double pf0[PF], pf1[PF];
+        load_x(seg_t0, pf0);
+        if (ntiles > 1) load_x(seg_t0 + T, pf1);
+        store_x(lds, pf0, seg_t0);
+        if (ntiles > 1) store_x(lds + XSP, pf1, seg_t0 + T);
+        if constexpr (MODE == MODE_MIX && BSP > W * O) {
+            for (int e = threadIdx.x; e < 2 * BSP * kGsRow; e += 64 * W)
+                if ((e % (BSP * kGsRow)) / kGsRow >= W * O) gsb[e] = 0.0;
+        }
+        __syncthreads();
+        phase_e(0);
+        __syncthreads();
+    }
+
+    double st[O];
+    const int niter = (MODE == MODE_MIX) ? ntiles + 1 : ntiles;
+    for (int it = 0; it < niter; ++it) {
         const long t0 = seg_t0 + (long)it * T;
         double pf[PF];
-        const bool more = it + 1 < ntiles;
-        if (more) load_x(t0 + T, pf);
-        if (has_tile) {
-            const double* xs = lds + (it & 1) * XSP;
-            // the lane's chunk window x[tc-O .. tc+L-1] (li = L lane + i -> lane (L+1) + i + i/L)
-            double xw[XW];
+        const bool stage = it + 2 < ntiles;
+        if (stage) load_x(t0 + 2 * T, pf);
+        if (it + 1 < ntiles) phase_e(it + 1);
+        if constexpr (MODE == MODE_MIX) {
+            if (it >= 1) phase_m(it - 1);
+        }
+        if (it < ntiles) {
+            // ---- (S) tile it: this wave's band ----
+            const double* z = zb + (it & 1) * BSP * kZRow;
+            double zz[O];
 #pragma unroll
-            for (int i = 0; i < XW; ++i) xw[i] = xs[lane * (L + 1) + i + i / L];
-            // zero-state end state of the lane's chunk: z[k] = y_zs[tc + L-1-k]
-            double z[O];
-#pragma unroll
-            for (int k = 0; k < O; ++k) {
-                double acc0 = r[R::EH + k * O] * xw[0], acc1 = 0.0;
-#pragma unroll
-                for (int i = 1; i < O; ++i) acc0 = fma(r[R::EH + k * O + i], xw[i], acc0);
-#pragma unroll
-                for (int i = O; i + k < XW; ++i) {
-                    if ((i - O) & 1) acc1 = fma(r[R::E0 + i + k], xw[i], acc1);
-                    else acc0 = fma(r[R::E0 + i + k], xw[i], acc0);
-                }
-                z[k] = pb * (acc0 + acc1);
-            }
-            // inclusive prefix over the 64 chunks (zero carry-in)
-#define HZ_LTI_SCAN_STEP(CTRL, RM, MAT)                                                       \
-    {                                                                                         \
-        double nb_[O];                                                                        \
-        _Pragma("unroll") for (int k = 0; k < O; ++k) nb_[k] = dpp_dm<CTRL, RM>(z[k]);        \
-        _Pragma("unroll") for (int rr = 0; rr < O; ++rr)                                      \
-            _Pragma("unroll") for (int c = 0; c < O; ++c) z[rr] = fma(MAT[rr * O + c], nb_[c], z[rr]); \
+            for (int k = 0; k < O; ++k) zz[k] = pb * z[(wave * O + k) * kZRow + lane];
+#define HZ_LTI_SCAN_STEP(CTRL, RM, MAT)                                                               \
+    {                                                                                                 \
+        double nb_[O];                                                                                \
+        _Pragma("unroll") for (int k = 0; k < O; ++k) nb_[k] = dpp_dm<CTRL, RM>(zz[k]);               \
+        _Pragma("unroll") for (int rr = 0; rr < O; ++rr)                                              \
+            _Pragma("unroll") for (int c = 0; c < O; ++c) zz[rr] = fma(MAT[rr * O + c], nb_[c], zz[rr]); \
     }
             const double* p1 = r + R::PS;
             const double* p2 = r + R::PS + O * O;
@@ -405,12 +435,11 @@ __global__ __launch_bounds__(64 * kLtiWaves) void fb_lti_kernel(const double* __
             HZ_LTI_SCAN_STEP(kDppRowBcast15, 0xa, qa)
             HZ_LTI_SCAN_STEP(kDppRowBcast31, 0xc, qb)
 #undef HZ_LTI_SCAN_STEP
-            // chunk start states and the tile end state
             double Sn[O];
 #pragma unroll
             for (int k = 0; k < O; ++k) {
-                double vv = dpp_dm<kDppWaveShr1, 0xf>(z[k]);  // Z(l-1), 0 at lane 0
-                double sn = readlane_d(z[k], 63);
+                double vv = dpp_dm<kDppWaveShr1, 0xf>(zz[k]);  // Z(l-1), 0 at lane 0
+                double sn = readlane_d(zz[k], 63);
 #pragma unroll
                 for (int c = 0; c < O; ++c) {
                     vv = fma(qc[k * O + c], S[c], vv);
@@ -422,7 +451,7 @@ __global__ __launch_bounds__(64 * kLtiWaves) void fb_lti_kernel(const double* __
 #pragma unroll
             for (int k = 0; k < O; ++k) S[k] = Sn[k];
             if constexpr (MODE == MODE_MIX) {
-                double* gs = gsb + (it & 1) * KD * kGsRow;
+                double* gs = gsb + (it & 1) * BSP * kGsRow;
 #pragma unroll
                 for (int k = 0; k < O; ++k) gs[(wave * O + k) * kGsRow + lane] = gb * st[k];
                 if (last_seg && it == ntiles - 1 && live) {
@@ -440,7 +469,7 @@ __global__ __launch_bounds__(64 * kLtiWaves) void fb_lti_kernel(const double* __
                 }
             }
         }
-        if (more) store_x(lds + ((it + 1) & 1) * XSP, pf, t0 + T);
+        if (stage) store_x(lds + (it & 1) * XSP, pf, t0 + 2 * T);
         __syncthreads();
     }
 
@@ -593,7 +622,7 @@ typedef void (*LtiReduceKernel)(const double*, long, int, long, const double*, c
 struct LtiGeom {
     int L, nb, waves;
 };
-static const LtiGeom kLtiGeoms[] = {{16, 1, 16}, {32, 1, 16}};
+static const LtiGeom kLtiGeoms[] = {{16, 1, 16}, {32, 1, 16}};  // waves: lti_waves(O)
 constexpr int kNumLtiGeoms = 2;
 
 template <int O, int L>
@@ -697,10 +726,15 @@ int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
     const LtiGeom geom = kLtiGeoms[h->lti_geom];
     const int L = geom.L;
     const long T = 64L * L;
-    const int per = geom.waves * geom.nb;
+    const int per = lti_waves(O);
     const int G = (h->N + per - 1) / per;
     // partial slab <= 2^27 doubles per launch
-    long chunk = std::max<long>(T, (((1L << 27) / std::max(1, G)) / T) * T);
+    static const int slab_log2 = [] {
+        const char* e = std::getenv("HZ_FB_SLAB_LOG2");  // tuning experiments
+        const int v = e ? std::atoi(e) : 27;
+        return v >= 16 && v <= 30 ? v : 27;
+    }();
+    long chunk = std::max<long>(T, (((1L << slab_log2) / std::max(1, G)) / T) * T);
     const long n_pad_max = std::min<long>(((n + T - 1) / T) * T, chunk);
     const size_t need = (size_t)G * n_pad_max;
     if (need > h->partial_cap) {
@@ -763,7 +797,7 @@ int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
             HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
         }
         if (nseg > 1) {
-            hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg - 1)), dim3(64 * geom.waves), lds_end, h->stream,
+            hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg - 1)), dim3(64 * lti_waves(O)), lds_end, h->stream,
                                (const double*)h->d_rec_lti, a);
             HZ_TRY_HIP(hipGetLastError());
             hipLaunchKernelGGL(pick_lti_carry(O, L), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0, h->stream,
@@ -772,7 +806,7 @@ int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
             HZ_TRY_HIP(hipGetLastError());
         }
         if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
-        hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * geom.waves), lds, h->stream,
+        hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * lti_waves(O)), lds, h->stream,
                            (const double*)h->d_rec_lti, a);
         HZ_TRY_HIP(hipGetLastError());
         if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
