@@ -85,7 +85,20 @@ def cpu_baseline(fwd, back, seconds_target=1.5):
                       f"({nsamp / SR:.2f} s audio), bands split over {threads} threads, {dt:.2f} s wall"}
 
 
-def pmc_traffic(kernel_substr="fb_mix_kernel", min_band_samples=1):
+def fb_executed_flops(lti, L=32, O=2):
+    """FP64 flops the kernel actually issues per band-sample.  LTI engine:
+    chunk end states on the matrix cores 2 O ceil((L+O)/4) 4 / L, group mix 2 O, the
+    64-lane scan 2 (6 O^2 + 2 O^2) 64 / (64 L) per chunk; general engine ~2 x 10."""
+    if not lti:
+        return 20.0
+    import math
+    e = 2.0 * O * 4 * math.ceil((L + O) / 4) / L
+    mix = 2.0 * O
+    scan = 2.0 * 8 * O * O / L
+    return e + mix + scan
+
+
+def pmc_traffic(kernel_substr="fb_mix_kernel", extra=()):
     """HBM bytes per launch of the dominant kernel from two separate rocprofv3 --pmc
     passes (FETCH_SIZE, WRITE_SIZE; kernel-trace only), run as child processes on a
     short bench.  Correction per MI355X_MICROARCH.md 'HBM': FETCH_SIZE counts wide
@@ -103,7 +116,7 @@ def pmc_traffic(kernel_substr="fb_mix_kernel", min_band_samples=1):
         d = tempfile.mkdtemp(prefix="hz_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
         cmd = [exe, "--pmc", counter, "--kernel-trace", "-d", d, "-o", "pmc", "--output-format", "csv",
                "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
-               "--no-cpu-baseline", "--stream-blocks", "0", "--no-traffic"]
+               "--no-cpu-baseline", "--stream-blocks", "0", "--no-traffic", *extra]
         try:
             subprocess.run(cmd, check=True, capture_output=True, timeout=300,
                            env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
@@ -203,6 +216,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     seg_ms, mix_ms, red_ms, launches = fb.profile_read()
+    from huygens_amd._lib import HZ_FB_PATH_LTI
+    lti = fb.last_path() == HZ_FB_PATH_LTI
     fb.profile(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -248,9 +263,11 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(fwd, back)
+        kname = "fb_lti_kernel" if lti else "fb_mix_kernel"
         traffic, traffic_detail = None, "skipped"
         if not args.no_traffic and world == 1 and S == SAMPLES_PER_STEP:
-            traffic, traffic_detail = pmc_traffic()
+            traffic, traffic_detail = pmc_traffic(kname, extra=(["--lti", args.lti] if args.lti else [])
+                                                  + (["--general"] if args.general else []))
         line = {
             "metric": "band-samples/s (bands x frames/s) for 4096-band Filterbank",
             "value": value,
@@ -274,12 +291,18 @@ def main():
                          "traffic_detail": traffic_detail,
                          "algorithmic_bytes_per_launch": (16 * S + 120 * cnt) * args.steps / max(1, launches),
                          "launches_per_step": launches / max(1, args.steps),
-                         "kernel": "fb_mix_kernel<2,0,1,0>",
+                         "kernel": ("fb_lti_kernel<2,%d,MIX> (converged LTI engine)" % fb.lti_chunk()) if lti
+                                   else "fb_mix_kernel<2,NONE,1,MIX> (general engine)",
+                         "executed_flops_per_band_sample": fb_executed_flops(lti, fb.lti_chunk()),
                          "kernel_avg_ms": 1e3 * mix_avg_s,
                          "segment_prepass_ms_per_launch": seg_ms / max(1, launches),
                          "reduce_ms_per_launch": red_ms / max(1, launches),
                          "flops_per_launch": flops_per_launch,
-                         "note": "FP64 vector peak (= FP64 MFMA peak); 18 flops per band-sample (SURVEY.md 8(d))"},
+                         "note": "achieved = algorithmic 18 FP64 flops per band-sample (SURVEY.md 8(d), the "
+                                 "reference recurrence) / mix-kernel time; peak = FP64 vector = FP64 MFMA peak. "
+                                 "The converged engine issues executed_flops_per_band_sample instead (chunked "
+                                 "state-space form, DESIGN.md 3.3); the combined zero-state term runs in the "
+                                 "reduce kernel (reduce_ms_per_launch)."},
             "streaming": {"band_samples_per_s": stream_rate, "block": 1024,
                           "note": "one process() call per 1024-sample block, device-resident I/O"},
             "cpu_baseline": cpu,

@@ -83,13 +83,13 @@ struct hz_fb {
     bool own_stream = false;
     // profiling
     bool prof = false;
-    std::vector<hipEvent_t> ev;  // quadruplets
+    std::vector<hipEvent_t> ev;  // quintuplets: start, mix start, mix end, reduce start, reduce end
     size_t ev_used = 0;
     long prof_launches = 0;
     // converged (LTI) path, hz_fb_lti.hip
     int path_mode = HZ_FB_PATH_AUTO;
     int last_path = HZ_FB_PATH_GENERAL;
-    int lti_geom = 0;                // index into kLtiGeoms (hz_fb_lti.hip)
+    int lti_geom = 1;                // index into kLtiGeoms (hz_fb_lti.hip): chunk 32
     int lti_rec = 0, lti_rec_L = 0;  // record size / chunk length the LTI records were built for
     bool dirty_lti = true;           // coefficients changed since the LTI records were built
     bool fmix_valid = false;         // Fmix matches the current coefficients, pin and gin
@@ -98,12 +98,18 @@ struct hz_fb {
     double* d_fmix = nullptr;        // [L][L+O]
     std::vector<double> h_rec_lti;
     std::vector<double> pg_host;     // host mirror of the smoother state [N][2] (pre, gain)
+    // LTI launches are split in chunks whose cross-group reduce runs on a second stream,
+    // overlapped with the next chunk's mix kernel (double-buffered partial slab)
+    hipStream_t stream_red = nullptr;
+    std::vector<hipEvent_t> sync_ev;  // ordering events (no timing)
+    double* d_xhist_red = nullptr;    // x history at the call start, for the first chunk's reduce
 };
 
 namespace hz_fbi {
 
 // hz_filterbank.hip
 int fb_set_lds_attr(const void* kernel);
+int fb_prof_events(hz_fb* h, hipEvent_t** e);
 void fb_mirror_advance(hz_fb* h, long len);
 int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n);
 // hz_fb_lti.hip

@@ -581,34 +581,50 @@ __global__ __launch_bounds__(256) void fb_fmix_kernel(const double* __restrict__
 }
 
 // out[t] = sum_g partial[g][t] + sum_i Fmix[t mod L][i] x[t - t mod L - O + i]
+// One thread per pair of samples (16-B loads down the slab's columns, 8 rows in flight),
+// 128 threads per block; the group order of the sum is fixed (deterministic).
 template <int O, int L>
-__global__ __launch_bounds__(256) void fb_lti_reduce_kernel(const double* __restrict__ partial, long n_pad, int G,
+__global__ __launch_bounds__(128) void fb_lti_reduce_kernel(const double* __restrict__ partial, long n_pad, int G,
                                                             long n, const double* __restrict__ x,
                                                             const double* __restrict__ xhist,
                                                             const double* __restrict__ fmix,
                                                             double* __restrict__ out) {
     constexpr int XW = L + O;
-    __shared__ double red[4][64];
     __shared__ double fm[L * XW];
-    for (int e = threadIdx.x; e < L * XW; e += 256) fm[e] = fmix[e];
+    for (int e = threadIdx.x; e < L * XW; e += 128) fm[e] = fmix[e];
     __syncthreads();
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    const long t = (long)blockIdx.x * 64 + tx;
-    double s = 0.0;
-    if (t < n) {
-        for (int g = ty; g < G; g += 4) s += partial[(long)g * n_pad + t];
-        // zero-state mix, split over the 4 row groups
-        const int j = (int)(t % L);
-        const long base = t - j - O;
-        for (int i = ty; i < XW; i += 4) {
-            const long idx = base + i;
-            const double xv = idx >= 0 ? x[idx] : xhist[-idx - 1];
-            s = fma(fm[j * XW + i], xv, s);
+    const long t = 2 * ((long)blockIdx.x * 128 + threadIdx.x);
+    if (t >= n) return;
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    d2 s0 = {0.0, 0.0}, s1 = {0.0, 0.0};
+    const double* col = partial + t;  // n_pad is a multiple of the tile: t + 1 < n_pad
+    int g = 0;
+    for (; g + 8 <= G; g += 8) {
+        d2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *(const d2*)(col + (long)(g + u) * n_pad);
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            s0 += v[u];
+            s1 += v[u + 1];
         }
     }
-    red[ty][tx] = s;
-    __syncthreads();
-    if (ty == 0 && t < n) out[t] = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+    for (; g < G; ++g) s0 += *(const d2*)(col + (long)g * n_pad);
+    d2 acc = s0 + s1;
+    // zero-state mix (t and t + 1 are in the same chunk: L even, t even)
+    const int j = (int)(t % L);
+    const long base = t - j - O;
+#pragma unroll 4
+    for (int i = 0; i < XW; ++i) {
+        const long idx = base + i;
+        // before the launch's first sample: the call's x history (first chunk) or the
+        // previous chunk of the same input buffer (xhist == nullptr)
+        const double xv = idx >= 0 || !xhist ? x[idx] : xhist[-idx - 1];
+        acc[0] = fma(fm[j * XW + i], xv, acc[0]);
+        acc[1] = fma(fm[(j + 1) * XW + i], xv, acc[1]);
+    }
+    out[t] = acc[0];
+    if (t + 1 < n) out[t + 1] = acc[1];
 }
 
 // ---- kernel selection -------------------------------------------
@@ -728,28 +744,55 @@ int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
     const long T = 64L * L;
     const int per = lti_waves(O);
     const int G = (h->N + per - 1) / per;
-    // partial slab <= 2^27 doubles per launch
+    // Chunks: the partial slab is bounded to 2^27 doubles per buffer; HZ_FB_LTI_SPLIT > 1
+    // splits a long call further so that each chunk's cross-group reduce (HBM-bound) runs on
+    // a second stream under the next chunk's mix kernel (FP64-bound).  Measured on MI355X
+    // (C2, 480k samples): split 1 0.859 ms, 2 0.868, 3 0.857, 4 0.873 -- the reduce then
+    // competes with the mix kernel for CU slots, so the default is 1.
     static const int slab_log2 = [] {
         const char* e = std::getenv("HZ_FB_SLAB_LOG2");  // tuning experiments
         const int v = e ? std::atoi(e) : 27;
         return v >= 16 && v <= 30 ? v : 27;
     }();
+    static const int nsplit = [] {
+        const char* e = std::getenv("HZ_FB_LTI_SPLIT");  // tuning experiments
+        const int v = e ? std::atoi(e) : 1;
+        return v >= 1 && v <= 64 ? v : 1;
+    }();
+    const long ntiles_all = (n + T - 1) / T;
     long chunk = std::max<long>(T, (((1L << slab_log2) / std::max(1, G)) / T) * T);
-    const long n_pad_max = std::min<long>(((n + T - 1) / T) * T, chunk);
-    const size_t need = (size_t)G * n_pad_max;
-    if (need > h->partial_cap) {
+    if (ntiles_all >= 8 * nsplit) chunk = std::min(chunk, ((ntiles_all + nsplit - 1) / nsplit) * T);
+    const long n_pad_max = std::min<long>(ntiles_all * T, chunk);
+    const size_t slab = (size_t)G * n_pad_max;
+    if (2 * slab > h->partial_cap) {
         if (h->d_partial) HZ_TRY_HIP(hipFree(h->d_partial));
         h->d_partial = nullptr;
-        HZ_TRY_HIP(hipMalloc(&h->d_partial, sizeof(double) * need));
-        h->partial_cap = need;
+        HZ_TRY_HIP(hipMalloc(&h->d_partial, sizeof(double) * 2 * slab));
+        h->partial_cap = 2 * slab;
     }
+    if (!h->stream_red) HZ_TRY_HIP(hipStreamCreateWithFlags(&h->stream_red, hipStreamNonBlocking));
+    if (!h->d_xhist_red) HZ_TRY_HIP(hipMalloc(&h->d_xhist_red, sizeof(double) * kMaxOrder));
+    const long nchunks = (n + chunk - 1) / chunk;
+    if ((size_t)(2 * nchunks) > h->sync_ev.size()) {
+        while (h->sync_ev.size() < (size_t)(2 * nchunks)) {
+            hipEvent_t ne;
+            HZ_TRY_HIP(hipEventCreateWithFlags(&ne, hipEventDisableTiming));
+            h->sync_ev.push_back(ne);
+        }
+    }
+    hipEvent_t* ev_mix = h->sync_ev.data();
+    hipEvent_t* ev_red = h->sync_ev.data() + nchunks;
     LtiKernel kmix = pick_lti(O, h->lti_geom, MODE_MIX);
     LtiKernel kend = pick_lti(O, h->lti_geom, MODE_SEGEND);
     HZ_TRY(fb_set_lds_attr((const void*)kmix));
     HZ_TRY(fb_set_lds_attr((const void*)kend));
     const size_t lds = lti_lds(O, h->lti_geom, true);
     const size_t lds_end = lti_lds(O, h->lti_geom, false);
-    for (long off = 0; off < n; off += chunk) {
+    // the first chunk's reduce reads the call's x history after later mixes rotated it
+    HZ_TRY_HIP(hipMemcpyAsync(h->d_xhist_red, h->d_xhist[h->xcur], sizeof(double) * O, hipMemcpyDeviceToDevice,
+                              h->stream));
+    long k = 0;
+    for (long off = 0; off < n; off += chunk, ++k) {
         const long len = std::min(chunk, n - off);
         const long ntiles = (len + T - 1) / T;
         long nseg = std::max<long>(1, std::min<long>(ntiles, (h->target_groups + G - 1) / G));
@@ -758,12 +801,14 @@ int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
         if (nseg > 1) {
             const size_t sneed = (size_t)h->N * nseg * O;
             if (sneed > h->seg_cap) {
+                HZ_TRY_HIP(hipStreamSynchronize(h->stream));
                 if (h->d_seg) HZ_TRY_HIP(hipFree(h->d_seg));
                 h->d_seg = nullptr;
                 HZ_TRY_HIP(hipMalloc(&h->d_seg, sizeof(double) * sneed));
                 h->seg_cap = sneed;
             }
         }
+        double* slab_k = h->d_partial + (size_t)(k & 1) * slab;
         LtiArgs a;
         a.pin = h->d_pin;
         a.gin = h->d_gin;
@@ -774,7 +819,7 @@ int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
         a.x = d_in + off;
         a.xhist = h->d_xhist[h->xcur];
         a.xhist_next = h->d_xhist[h->xcur ^ 1];
-        a.partial = h->d_partial;
+        a.partial = slab_k;
         a.segstate = h->d_seg;
         a.n = len;
         a.n_pad = ntiles * T;
@@ -784,16 +829,10 @@ int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
         a.sp_n = (double)powl((long double)h->sp, (long double)len);
         a.sg_n = (double)powl((long double)h->sg, (long double)len);
         hipEvent_t* e = nullptr;
+        if (k >= 2) HZ_TRY_HIP(hipStreamWaitEvent(h->stream, ev_red[k - 2], 0));  // slab buffer k & 1 free
+        (void)0;
         if (h->prof) {
-            if (h->ev_used + 4 > h->ev.size()) {
-                for (int q = 0; q < 4 * 64; ++q) {
-                    hipEvent_t ne;
-                    HZ_TRY_HIP(hipEventCreate(&ne));
-                    h->ev.push_back(ne);
-                }
-            }
-            e = &h->ev[h->ev_used];
-            h->ev_used += 4;
+            HZ_TRY(fb_prof_events(h, &e));
             HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
         }
         if (nseg > 1) {
@@ -810,16 +849,26 @@ int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
                            (const double*)h->d_rec_lti, a);
         HZ_TRY_HIP(hipGetLastError());
         if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
-        hipLaunchKernelGGL(pick_lti_reduce(O, L), dim3((unsigned)((len + 63) / 64)), dim3(256), 0, h->stream,
-                           (const double*)h->d_partial, a.n_pad, G, len, a.x, a.xhist, (const double*)h->d_fmix,
-                           d_out + off);
+        // one chunk: the reduce stays on the caller's stream (no cross-stream round trip)
+        hipStream_t rs = nchunks > 1 ? h->stream_red : h->stream;
+        if (nchunks > 1) {
+            HZ_TRY_HIP(hipEventRecord(ev_mix[k], h->stream));
+            HZ_TRY_HIP(hipStreamWaitEvent(rs, ev_mix[k], 0));
+        }
+        if (e) HZ_TRY_HIP(hipEventRecord(e[3], rs));
+        hipLaunchKernelGGL(pick_lti_reduce(O, L), dim3((unsigned)((len + 255) / 256)), dim3(128), 0, rs,
+                           (const double*)slab_k, a.n_pad, G, len, a.x, off == 0 ? (const double*)h->d_xhist_red : nullptr,
+                           (const double*)h->d_fmix, d_out + off);
         HZ_TRY_HIP(hipGetLastError());
-        if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
+        if (e) HZ_TRY_HIP(hipEventRecord(e[4], rs));
+        if (nchunks > 1) HZ_TRY_HIP(hipEventRecord(ev_red[k], rs));
         h->xcur ^= 1;
         h->scur ^= 1;
         h->prof_launches += h->prof ? 1 : 0;
         fb_mirror_advance(h, len);
     }
+    // the caller's stream sees the whole output
+    if (nchunks > 1) HZ_TRY_HIP(hipStreamWaitEvent(h->stream, ev_red[nchunks - 1], 0));
     return HZ_OK;
 }
 
@@ -830,7 +879,7 @@ extern "C" {
 int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group) {
     if (!h) return HZ_E_INVALID;
     if (!chunk && !bands_per_wave && !waves_per_group) {
-        h->lti_geom = 0;
+        h->lti_geom = 1;
         return HZ_OK;
     }
     for (int g = 0; g < kNumLtiGeoms; ++g)

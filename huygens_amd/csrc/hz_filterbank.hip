@@ -678,6 +678,20 @@ long fb_max_chunk(const hz_fb* h) {
 
 namespace hz_fbi {
 
+// five timing events per launch (start, mix start, mix end, reduce start, reduce end)
+int fb_prof_events(hz_fb* h, hipEvent_t** e) {
+    if (h->ev_used + 5 > h->ev.size()) {
+        for (int q = 0; q < 5 * 64; ++q) {
+            hipEvent_t ne;
+            HZ_TRY_HIP(hipEventCreate(&ne));
+            h->ev.push_back(ne);
+        }
+    }
+    *e = &h->ev[h->ev_used];
+    h->ev_used += 5;
+    return HZ_OK;
+}
+
 int fb_set_lds_attr(const void* k) {
     static thread_local std::vector<const void*> done;
     if (std::find(done.begin(), done.end(), k) != done.end()) return HZ_OK;
@@ -760,15 +774,7 @@ int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n) {
         a.dist_param = h->dist_param;
         hipEvent_t* e = nullptr;
         if (h->prof) {
-            if (h->ev_used + 4 > h->ev.size()) {
-                for (int q = 0; q < 4 * 64; ++q) {
-                    hipEvent_t ne;
-                    HZ_TRY_HIP(hipEventCreate(&ne));
-                    h->ev.push_back(ne);
-                }
-            }
-            e = &h->ev[h->ev_used];
-            h->ev_used += 4;
+            HZ_TRY(fb_prof_events(h, &e));
             HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
         }
         if (nseg > 1 && O > 0) {
@@ -786,10 +792,11 @@ int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n) {
                            (const double*)h->d_rec, a);
         HZ_TRY_HIP(hipGetLastError());
         if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
+        if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
         hipLaunchKernelGGL(fb_reduce_kernel, dim3((unsigned)((len + 63) / 64)), dim3(256), 0, h->stream,
                            (const double*)h->d_partial, a.n_pad, G, len, d_out + off);
         HZ_TRY_HIP(hipGetLastError());
-        if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
+        if (e) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
         h->xcur ^= 1;
         h->scur ^= 1;
         h->prof_launches += h->prof ? 1 : 0;
@@ -918,7 +925,11 @@ int hz_fb_destroy(hz_fb* h) {
                       h->d_xhist[0], h->d_xhist[1],
                       h->d_partial, h->d_seg, h->d_in, h->d_out, h->d_rec_lti, h->d_fmix})
         if (p) (void)hipFree(p);
+    if (h->stream_red) (void)hipStreamSynchronize(h->stream_red);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : h->sync_ev) (void)hipEventDestroy(e);
+    if (h->stream_red) (void)hipStreamDestroy(h->stream_red);
+    if (h->d_xhist_red) (void)hipFree(h->d_xhist_red);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return HZ_OK;
@@ -1159,12 +1170,13 @@ int hz_fb_profile(hz_fb* h, int enable) {
 int hz_fb_profile_read(hz_fb* h, double* segment_ms, double* mix_ms, double* reduce_ms, long* launches) {
     HZ_TRY(fb_check(h));
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    if (h->stream_red) HZ_TRY_HIP(hipStreamSynchronize(h->stream_red));
     double sg = 0, m = 0, r = 0;
-    for (size_t i = 0; i + 4 <= h->ev_used; i += 4) {
+    for (size_t i = 0; i + 5 <= h->ev_used; i += 5) {
         float a = 0, b = 0, c = 0;
         HZ_TRY_HIP(hipEventElapsedTime(&a, h->ev[i], h->ev[i + 1]));
         HZ_TRY_HIP(hipEventElapsedTime(&b, h->ev[i + 1], h->ev[i + 2]));
-        HZ_TRY_HIP(hipEventElapsedTime(&c, h->ev[i + 2], h->ev[i + 3]));
+        HZ_TRY_HIP(hipEventElapsedTime(&c, h->ev[i + 3], h->ev[i + 4]));
         sg += a;
         m += b;
         r += c;

@@ -37,6 +37,7 @@ class Filterbank:
         self._dist = (HZ_DIST_NONE, 0.0)
         self._computed = False
         self._cached = 0.0
+        self._lti_geom = 1
 
     def close(self):
         if getattr(self, "_h", None):
@@ -151,6 +152,11 @@ class Filterbank:
 
     def tune_lti(self, chunk: int = 0, bands_per_wave: int = 0, waves: int = 0):
         check(self._lib.hz_fb_tune_lti(self._h, chunk, bands_per_wave, waves))
+        self._lti_geom = 0 if chunk == 16 else 1
+
+    def lti_chunk(self) -> int:
+        """Samples per lane chunk of the selected LTI geometry."""
+        return {0: 16, 1: 32}.get(self._lti_geom, 32)
 
     def set_target_groups(self, groups: int):
         check(self._lib.hz_fb_set_target_groups(self._h, groups))
