@@ -112,3 +112,33 @@ def test_kernel_algorithm_model(order, N, n):
     from golden.spec_numpy import relaxation
     got = mix_model(fwd, back, relaxation(0.1), relaxation(1.0), np.ones(N), np.ones(N), x)
     assert rel_err(got, ref) < 1e-10
+
+
+@pytest.mark.parametrize("order,N,L,n", [(2, 4, 32, 2 * 2048 + 32 * 5), (1, 3, 16, 1024 + 48), (3, 2, 16, 2048),
+                                         (4, 2, 32, 2048 + 64)])
+def test_lti_algorithm_model(order, N, L, n):
+    """The converged engine's algebra (hz_fb_lti.hip: chunk end states, 64-lane DPP prefix
+    with row_bcast, bank-wide zero-state matrix) == the sequential oracle once the
+    smoothers have converged (k_p = k_g = 0: pre = pin and gain = gin from sample 0)."""
+    from lti_model import lti_mix_model
+    rng = np.random.default_rng(10 + order)
+    fwd = rng.uniform(-1, 1, (N, order + 1))
+    back = np.zeros((N, order))
+    for b in range(N):
+        roots = []
+        for _ in range(order // 2):
+            p = 0.98 * np.exp(1j * rng.uniform(0, np.pi))
+            roots += [p, np.conj(p)]
+        if order % 2:
+            roots.append(0.98 * rng.uniform(-1, 1))
+        back[b] = np.real(np.poly(roots))[1:]
+    pin, gin = rng.uniform(0.5, 2, N), rng.uniform(-1, 1, N)
+    fb = OracleFilterbank(order, N, 0.0, 0.0)
+    for b in range(N):
+        fb.coefficients(b, fwd[b], back[b])
+    fb.boost(pin)
+    fb.mix(gin)
+    x = rng.uniform(-1, 1, n)
+    ref = fb.process(x)
+    got = lti_mix_model(fwd, back, pin, gin, x, L=L)
+    assert rel_err(got, ref) < 1e-10
