@@ -89,15 +89,18 @@ struct hz_fb {
     // converged (LTI) path, hz_fb_lti.hip
     int path_mode = HZ_FB_PATH_AUTO;
     int last_path = HZ_FB_PATH_GENERAL;
-    int lti_geom = 1;                // index into kLtiGeoms (hz_fb_lti.hip): chunk 32
-    int lti_rec = 0, lti_rec_L = 0;  // record size / chunk length the LTI records were built for
-    bool dirty_lti = true;           // coefficients changed since the LTI records were built
-    bool fmix_valid = false;         // Fmix matches the current coefficients, pin and gin
-    double* d_rec_lti = nullptr;
-    size_t rec_lti_cap = 0;
-    double* d_fmix = nullptr;        // [L][L+O]
-    std::vector<double> h_rec_lti;
+    int lti_geom = -1;               // index into kLtiGeoms (hz_fb_lti.hip); -1 = by call length
+    struct LtiRecSet {               // LTI records + Fmix per chunk length (geometry)
+        bool dirty = true;           // coefficients changed since the records were built
+        bool fmix_valid = false;     // Fmix matches the current coefficients, pin and gin
+        int rs = 0;                  // record size (doubles)
+        double* d_rec = nullptr;
+        size_t cap = 0;
+        double* d_fmix = nullptr;    // [L][L+O]
+    } lti_set[2];
     std::vector<double> pg_host;     // host mirror of the smoother state [N][2] (pre, gain)
+    long mirror_pending = 0;         // samples processed since pg_host was last brought up to date
+    bool converged = false;          // pg_host at the targets; cleared by every setter
     // LTI launches are split in chunks whose cross-group reduce runs on a second stream,
     // overlapped with the next chunk's mix kernel (double-buffered partial slab)
     hipStream_t stream_red = nullptr;
@@ -110,11 +113,13 @@ namespace hz_fbi {
 // hz_filterbank.hip
 int fb_set_lds_attr(const void* kernel);
 int fb_prof_events(hz_fb* h, hipEvent_t** e);
-void fb_mirror_advance(hz_fb* h, long len);
+void fb_mirror_advance(hz_fb* h, long len);  // O(1): the closed form is applied lazily
+void fb_mirror_sync(hz_fb* h);               // bring pg_host up to date (before a setter)
 int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n);
 // hz_fb_lti.hip
-int fb_lti_chunk(const hz_fb* h);  // samples per lane chunk of the selected LTI geometry
-bool fb_converged(const hz_fb* h);
-int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n);
+int fb_lti_geom(const hz_fb* h, long n);  // LTI geometry for a call of n samples
+int fb_lti_chunk(int geom);                // samples per lane chunk of a geometry
+bool fb_converged(hz_fb* h);
+int fb_launch_lti(hz_fb* h, int geom, const double* d_in, double* d_out, long n);
 
 }  // namespace hz_fbi

@@ -683,11 +683,20 @@ static LtiReduceKernel pick_lti_reduce(int O, int L) { return HZ_LTI_OL(fb_lti_r
 
 namespace hz_fbi {
 
-int fb_lti_chunk(const hz_fb* h) { return kLtiGeoms[h->lti_geom].L; }
+// geometry by call length unless pinned (hz_fb_tune_lti): chunk 32 for calls of at least two
+// of its 2048-sample tiles, chunk 16 (1024-sample tiles) for the short streaming blocks
+int fb_lti_geom(const hz_fb* h, long n) {
+    if (h->lti_geom >= 0) return h->lti_geom;
+    return n >= 2 * 64L * 32 ? 1 : 0;
+}
+
+int fb_lti_chunk(int geom) { return kLtiGeoms[geom].L; }
 
 // every band's smoothers at their targets (host mirror), relative to the bank's
 // largest target: the LTI engine then computes the same outputs to ~2^-60
-bool fb_converged(const hz_fb* h) {
+bool fb_converged(hz_fb* h) {
+    if (h->converged) return true;  // targets unchanged since: the smoothers only get closer
+    fb_mirror_sync(h);
     double pmax = 0, gmax = 0;
     for (int b = 0; b < h->N; ++b) {
         pmax = std::max(pmax, std::fabs(h->pin[b]));
@@ -698,48 +707,49 @@ bool fb_converged(const hz_fb* h) {
         if (!(std::fabs(h->pg_host[2 * (size_t)b] - h->pin[b]) <= tp)) return false;
         if (!(std::fabs(h->pg_host[2 * (size_t)b + 1] - h->gin[b]) <= tg)) return false;
     }
+    h->converged = true;
     return true;
 }
 
-int fb_prepare_lti(hz_fb* h) {
+int fb_prepare_lti(hz_fb* h, int gi) {
     const int O = h->order;
-    const int L = kLtiGeoms[h->lti_geom].L;
-    if (h->dirty_lti || h->lti_rec_L != L) {
+    const int L = kLtiGeoms[gi].L;
+    hz_fb::LtiRecSet& set = h->lti_set[gi];
+    if (set.dirty) {
         const int rs = lti_rec_size(O, L);
         const size_t need = (size_t)h->N * rs;
-        h->h_rec_lti.assign(need, 0.0);
+        std::vector<double> host(need, 0.0);
         for (int b = 0; b < h->N; ++b)
-            build_record_lti_any(O, L, &h->F[(size_t)b * (O + 1)], &h->B[(size_t)b * O], &h->h_rec_lti[(size_t)b * rs]);
-        if (need > h->rec_lti_cap) {
-            if (h->d_rec_lti) HZ_TRY_HIP(hipFree(h->d_rec_lti));
-            h->d_rec_lti = nullptr;
-            HZ_TRY_HIP(hipMalloc(&h->d_rec_lti, sizeof(double) * need));
-            h->rec_lti_cap = need;
+            build_record_lti_any(O, L, &h->F[(size_t)b * (O + 1)], &h->B[(size_t)b * O], &host[(size_t)b * rs]);
+        if (need > set.cap) {
+            if (set.d_rec) HZ_TRY_HIP(hipFree(set.d_rec));
+            set.d_rec = nullptr;
+            HZ_TRY_HIP(hipMalloc(&set.d_rec, sizeof(double) * need));
+            set.cap = need;
         }
-        if (!h->d_fmix) HZ_TRY_HIP(hipMalloc(&h->d_fmix, sizeof(double) * 32 * (32 + kMaxOrder)));
-        HZ_TRY_HIP(hipMemcpyAsync(h->d_rec_lti, h->h_rec_lti.data(), sizeof(double) * need, hipMemcpyHostToDevice,
-                                  h->stream));
+        if (!set.d_fmix) HZ_TRY_HIP(hipMalloc(&set.d_fmix, sizeof(double) * L * (L + kMaxOrder)));
+        HZ_TRY_HIP(hipMemcpyAsync(set.d_rec, host.data(), sizeof(double) * need, hipMemcpyHostToDevice, h->stream));
         HZ_TRY_HIP(hipStreamSynchronize(h->stream));  // pageable source
-        h->lti_rec = rs;
-        h->lti_rec_L = L;
-        h->dirty_lti = false;
-        h->fmix_valid = false;
+        set.rs = rs;
+        set.dirty = false;
+        set.fmix_valid = false;
     }
-    if (!h->fmix_valid) {
+    if (!set.fmix_valid) {
         hipLaunchKernelGGL(pick_fmix(O, L), dim3((unsigned)(L * (L + O))), dim3(256), 0, h->stream,
-                           (const double*)h->d_rec_lti, (const double*)h->d_pin, (const double*)h->d_gin, h->N,
-                           h->d_fmix);
+                           (const double*)set.d_rec, (const double*)h->d_pin, (const double*)h->d_gin, h->N,
+                           set.d_fmix);
         HZ_TRY_HIP(hipGetLastError());
-        h->fmix_valid = true;
+        set.fmix_valid = true;
     }
     return HZ_OK;
 }
 
 // the converged engine over n samples (n a positive multiple of the chunk length)
-int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
-    HZ_TRY(fb_prepare_lti(h));
+int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
+    HZ_TRY(fb_prepare_lti(h, gi));
+    const hz_fb::LtiRecSet& set = h->lti_set[gi];
     const int O = h->order;
-    const LtiGeom geom = kLtiGeoms[h->lti_geom];
+    const LtiGeom geom = kLtiGeoms[gi];
     const int L = geom.L;
     const long T = 64L * L;
     const int per = lti_waves(O);
@@ -782,15 +792,20 @@ int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
     }
     hipEvent_t* ev_mix = h->sync_ev.data();
     hipEvent_t* ev_red = h->sync_ev.data() + nchunks;
-    LtiKernel kmix = pick_lti(O, h->lti_geom, MODE_MIX);
-    LtiKernel kend = pick_lti(O, h->lti_geom, MODE_SEGEND);
+    LtiKernel kmix = pick_lti(O, gi, MODE_MIX);
+    LtiKernel kend = pick_lti(O, gi, MODE_SEGEND);
     HZ_TRY(fb_set_lds_attr((const void*)kmix));
     HZ_TRY(fb_set_lds_attr((const void*)kend));
-    const size_t lds = lti_lds(O, h->lti_geom, true);
-    const size_t lds_end = lti_lds(O, h->lti_geom, false);
-    // the first chunk's reduce reads the call's x history after later mixes rotated it
-    HZ_TRY_HIP(hipMemcpyAsync(h->d_xhist_red, h->d_xhist[h->xcur], sizeof(double) * O, hipMemcpyDeviceToDevice,
-                              h->stream));
+    const size_t lds = lti_lds(O, gi, true);
+    const size_t lds_end = lti_lds(O, gi, false);
+    // with the reduce on a second stream, the first chunk's reduce reads the call's x history
+    // after later mixes rotated the ping-pong buffers: keep a copy
+    const double* xhist_call = h->d_xhist[h->xcur];
+    if (nchunks > 1) {
+        HZ_TRY_HIP(hipMemcpyAsync(h->d_xhist_red, xhist_call, sizeof(double) * O, hipMemcpyDeviceToDevice,
+                                  h->stream));
+        xhist_call = h->d_xhist_red;
+    }
     long k = 0;
     for (long off = 0; off < n; off += chunk, ++k) {
         const long len = std::min(chunk, n - off);
@@ -837,16 +852,16 @@ int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
         }
         if (nseg > 1) {
             hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg - 1)), dim3(64 * lti_waves(O)), lds_end, h->stream,
-                               (const double*)h->d_rec_lti, a);
+                               (const double*)set.d_rec, a);
             HZ_TRY_HIP(hipGetLastError());
             hipLaunchKernelGGL(pick_lti_carry(O, L), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0, h->stream,
-                               (const double*)h->d_rec_lti, (const double*)h->d_ystate[h->scur], h->d_seg, h->N,
+                               (const double*)set.d_rec, (const double*)h->d_ystate[h->scur], h->d_seg, h->N,
                                (int)nseg, seg_tiles);
             HZ_TRY_HIP(hipGetLastError());
         }
         if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
         hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * lti_waves(O)), lds, h->stream,
-                           (const double*)h->d_rec_lti, a);
+                           (const double*)set.d_rec, a);
         HZ_TRY_HIP(hipGetLastError());
         if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
         // one chunk: the reduce stays on the caller's stream (no cross-stream round trip)
@@ -857,8 +872,8 @@ int fb_launch_lti(hz_fb* h, const double* d_in, double* d_out, long n) {
         }
         if (e) HZ_TRY_HIP(hipEventRecord(e[3], rs));
         hipLaunchKernelGGL(pick_lti_reduce(O, L), dim3((unsigned)((len + 255) / 256)), dim3(128), 0, rs,
-                           (const double*)slab_k, a.n_pad, G, len, a.x, off == 0 ? (const double*)h->d_xhist_red : nullptr,
-                           (const double*)h->d_fmix, d_out + off);
+                           (const double*)slab_k, a.n_pad, G, len, a.x, off == 0 ? xhist_call : nullptr,
+                           (const double*)set.d_fmix, d_out + off);
         HZ_TRY_HIP(hipGetLastError());
         if (e) HZ_TRY_HIP(hipEventRecord(e[4], rs));
         if (nchunks > 1) HZ_TRY_HIP(hipEventRecord(ev_red[k], rs));
@@ -879,7 +894,7 @@ extern "C" {
 int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group) {
     if (!h) return HZ_E_INVALID;
     if (!chunk && !bands_per_wave && !waves_per_group) {
-        h->lti_geom = 1;
+        h->lti_geom = -1;  // by call length
         return HZ_OK;
     }
     for (int g = 0; g < kNumLtiGeoms; ++g)

@@ -638,6 +638,7 @@ int fb_groups(const hz_fb* h) {
 }
 
 int fb_upload(hz_fb* h) {
+    bool uploaded = false;
     if (h->dirty_coef) {
         const int O = h->order;
         h->h_rec.assign((size_t)h->N * h->rec, 0.0);
@@ -647,22 +648,29 @@ int fb_upload(hz_fb* h) {
         HZ_TRY_HIP(hipMemcpyAsync(h->d_rec, h->h_rec.data(), sizeof(double) * h->h_rec.size(),
                                   hipMemcpyHostToDevice, h->stream));
         h->dirty_coef = false;
-        h->dirty_lti = true;
-        h->fmix_valid = false;
+        for (auto& st : h->lti_set) {
+            st.dirty = true;
+            st.fmix_valid = false;
+        }
+        uploaded = true;
     }
-    if (h->dirty_pin || h->dirty_gin) h->fmix_valid = false;
+    if (h->dirty_pin || h->dirty_gin)
+        for (auto& st : h->lti_set) st.fmix_valid = false;
     if (h->dirty_pin) {
         HZ_TRY_HIP(hipMemcpyAsync(h->d_pin, h->pin.data(), sizeof(double) * h->N, hipMemcpyHostToDevice,
                                   h->stream));
         h->dirty_pin = false;
+        uploaded = true;
     }
     if (h->dirty_gin) {
         HZ_TRY_HIP(hipMemcpyAsync(h->d_gin, h->gin.data(), sizeof(double) * h->N, hipMemcpyHostToDevice,
                                   h->stream));
         h->dirty_gin = false;
+        uploaded = true;
     }
-    // the uploads read pageable host vectors that setters may change next: make them complete
-    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    // the uploads read pageable host vectors that setters may change next: make them
+    // complete (only when something was uploaded: streaming calls stay asynchronous)
+    if (uploaded) HZ_TRY_HIP(hipStreamSynchronize(h->stream));
     return HZ_OK;
 }
 
@@ -702,15 +710,19 @@ int fb_set_lds_attr(const void* k) {
 
 // host mirror of the closed-form smoother end state written by every launch
 // (pgstate_next = pin + sp^n (pre - pin), likewise for the gains)
-void fb_mirror_advance(hz_fb* h, long len) {
-    const double spn = (double)powl((long double)h->sp, (long double)len);
-    const double sgn = (double)powl((long double)h->sg, (long double)len);
+void fb_mirror_advance(hz_fb* h, long len) { h->mirror_pending += len; }
+
+void fb_mirror_sync(hz_fb* h) {
+    if (h->mirror_pending == 0) return;
+    const double spn = (double)powl((long double)h->sp, (long double)h->mirror_pending);
+    const double sgn = (double)powl((long double)h->sg, (long double)h->mirror_pending);
     for (int b = 0; b < h->N; ++b) {
         double& P = h->pg_host[2 * (size_t)b];
         double& G = h->pg_host[2 * (size_t)b + 1];
         P = h->pin[b] + spn * (P - h->pin[b]);
         G = h->gin[b] + sgn * (G - h->gin[b]);
     }
+    h->mirror_pending = 0;
 }
 
 int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n) {
@@ -812,11 +824,12 @@ namespace {
 int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
     if (n <= 0) return HZ_OK;
     h->last_path = HZ_FB_PATH_GENERAL;
-    const int L = fb_lti_chunk(h);
+    const int geom = fb_lti_geom(h, n);
+    const int L = fb_lti_chunk(geom);
     const long n_lti = n - n % L;
     if (h->path_mode == HZ_FB_PATH_AUTO && h->order > 0 && h->dist_id == HZ_DIST_NONE && n_lti > 0 &&
         fb_converged(h)) {
-        HZ_TRY(fb_launch_lti(h, d_in, d_out, n_lti));
+        HZ_TRY(fb_launch_lti(h, geom, d_in, d_out, n_lti));
         h->last_path = HZ_FB_PATH_LTI;
         return fb_launch_general(h, d_in + n_lti, d_out + n_lti, n - n_lti);
     }
@@ -923,7 +936,8 @@ int hz_fb_destroy(hz_fb* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (double* p : {h->d_rec, h->d_pin, h->d_gin, h->d_ystate[0], h->d_ystate[1], h->d_pg[0], h->d_pg[1],
                       h->d_xhist[0], h->d_xhist[1],
-                      h->d_partial, h->d_seg, h->d_in, h->d_out, h->d_rec_lti, h->d_fmix})
+                      h->d_partial, h->d_seg, h->d_in, h->d_out, h->lti_set[0].d_rec, h->lti_set[0].d_fmix,
+                      h->lti_set[1].d_rec, h->lti_set[1].d_fmix})
         if (p) (void)hipFree(p);
     if (h->stream_red) (void)hipStreamSynchronize(h->stream_red);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
@@ -955,6 +969,8 @@ int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double*
 
 int hz_fb_boost(hz_fb* h, int n, double v) {
     if (!h) return HZ_E_INVALID;
+    fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
+    h->converged = false;
     if (n < 0 || n >= h->N_total) {
         hz::set_error("hz_fb_boost: band %d out of range [0,%d)", n, h->N_total);
         return HZ_E_RANGE;
@@ -969,6 +985,8 @@ int hz_fb_boost(hz_fb* h, int n, double v) {
 
 int hz_fb_boost_all(hz_fb* h, const double* v, int count) {
     if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
+    fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
+    h->converged = false;
     for (int i = 0; i < std::min(h->N_total, count); ++i) {
         const int l = fb_local(h, i);
         if (l >= 0) h->pin[l] = v[i];
@@ -979,6 +997,8 @@ int hz_fb_boost_all(hz_fb* h, const double* v, int count) {
 
 int hz_fb_mix(hz_fb* h, int n, double v) {
     if (!h) return HZ_E_INVALID;
+    fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
+    h->converged = false;
     if (n < 0 || n >= h->N_total) {
         hz::set_error("hz_fb_mix: band %d out of range [0,%d)", n, h->N_total);
         return HZ_E_RANGE;
@@ -993,6 +1013,8 @@ int hz_fb_mix(hz_fb* h, int n, double v) {
 
 int hz_fb_mix_all(hz_fb* h, const double* v, int count) {
     if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
+    fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
+    h->converged = false;
     for (int i = 0; i < std::min(h->N_total, count); ++i) {
         const int l = fb_local(h, i);
         if (l >= 0) h->gin[l] = v[i];
@@ -1003,6 +1025,8 @@ int hz_fb_mix_all(hz_fb* h, const double* v, int count) {
 
 int hz_fb_open(hz_fb* h) {
     if (!h) return HZ_E_INVALID;
+    fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
+    h->converged = false;
     std::fill(h->gin.begin(), h->gin.end(), 1.0);
     h->dirty_gin = true;
     return HZ_OK;
@@ -1112,6 +1136,8 @@ int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
     }
     HZ_TRY_HIP(hipMemcpy(h->d_pg[h->scur], buf + O + N * O, sizeof(double) * N * 2, hipMemcpyHostToDevice));
     std::memcpy(h->pg_host.data(), buf + O + N * O, sizeof(double) * N * 2);
+    h->mirror_pending = 0;
+    h->converged = false;
     return HZ_OK;
 }
 
