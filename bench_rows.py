@@ -130,11 +130,15 @@ def run_c4(args, torch, dev):
             step()
         torch.cuda.synchronize(dev)
         f0 = eng.frames()[0]
-        eng.profile(True)
         elapsed = _timed(step, args.steps, 0, torch, dev)
+        frames = eng.frames()[0] - f0
+        # kernel times from a separate profiled pass: each block's frame launch repeated 8x
+        # between one event pair (an event pair costs about as much as one ~20 us launch)
+        eng.profile(True, repeat=8)
+        for _ in range(args.steps):
+            step()
         fms, oms, blocks = eng.profile_read()
         eng.profile(False)
-        frames = eng.frames()[0] - f0
         out[name] = (elapsed, fms, oms, blocks, frames)
     elapsed, fms, oms, blocks, frames = out["static"]
     flops = 491520.0 * frames   # 2 x 5 N log2 N per frame
@@ -153,6 +157,11 @@ def run_c4(args, torch, dev):
                "sample": f"oracle/hz_oracle_stft.c StaticSTFT(4096,4), {n} samples ({o.frames()} frames), "
                          f"long double radix-2 FFT, 1 thread, {dt:.2f} s"}
     e2, f2, o2, b2, fr2 = out["gate625"]
+    traffic, tdetail = None, "not collected (--no-traffic)"
+    if not args.no_traffic:
+        import bench
+        tb, tdetail = bench.pmc_traffic("stft_frame_kernel<1,", extra=("--workload", "c4"))
+        traffic = tb   # HBM bytes per frame launch (one launch per step here)
     return {
         "metric": "STFT frames/s, StaticSTFT 4096-pt / 75% overlap spectral gate",
         "value": frames / elapsed, "unit": "frames/s",
@@ -162,7 +171,8 @@ def run_c4(args, torch, dev):
         "config": {"workload": "C4 StaticSTFT(4096, 4) built-in gate (100, 0.1)", "samples_per_step": S,
                    "frames_per_step": frames // args.steps},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK if achieved else None, "traffic": None,
+                     "frac": achieved / FP64_PEAK if achieved else None,
+                     "traffic": traffic, "traffic_detail": tdetail,
                      "kernel": "stft_frame_kernel<STATIC_GATE,0> (window+FFT+gate+IFFT in LDS)",
                      "kernel_ms_per_step": fms / args.steps, "ola_ms_per_step": oms / args.steps,
                      "flops_per_frame": 491520},

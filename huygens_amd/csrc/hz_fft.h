@@ -15,6 +15,9 @@
 namespace hz {
 
 __device__ __forceinline__ void cmul_tw(double& r, double& i, double2 w, bool conj) {
+#if defined(HZ_STFT_ABLATE) && (HZ_STFT_ABLATE & 16)
+    w = make_double2(0.70710678118654752, -0.70710678118654752);
+#endif
     const double wi = conj ? -w.y : w.y;
     const double nr = r * w.x - i * wi;
     const double ni = r * wi + i * w.x;
@@ -135,6 +138,210 @@ __device__ __forceinline__ void lds_fft_inv(double* re, double* im, int N, int l
     for (; h < N; h <<= 2) {
         dit4_stage(re, im, N, h, tw);
         __syncthreads();
+    }
+}
+
+// ---- register-blocked passes over a padded LDS layout (the STFT frame kernel) ----------
+// A pass runs R radix-2 stages (radix 2^R, R <= 4) on 2^R elements held in registers, so
+// each element makes one LDS round trip per pass instead of one per stage.  Stage twiddles
+// are one table lookup per stage, W_N^(p 2^s), times compile-time roots W_L^m of the pass.
+// The table is compact (W_N^k for k <= N/8, the rest by symmetry) and lives in LDS.
+// Layout: element i lives at pad16(i) = i + i/16 so 2^R-apart strides spread over banks.
+__device__ __forceinline__ int pad16(int i) { return i + (i >> 4); }
+__host__ __device__ constexpr int padded_len(int N) { return N + (N >> 4); }
+
+// compact twiddle table length: W_N^k for k in [0, N/8] (N >= 8), k in [0, N/4) (N = 4)
+__host__ __device__ constexpr int twc_len(int lg) { return lg >= 3 ? (1 << (lg - 3)) + 1 : 1 << (lg - 2); }
+
+// W_N^k for k in [0, N/2) from the compact table
+__device__ __forceinline__ double2 twc(const double2* T, int k, int lg) {
+    const int q = 1 << (lg - 2);                       // N/4: W^k = -i W^(k - N/4)
+    const int e = lg >= 3 ? 1 << (lg - 3) : q;         // N/8: W^m = -i conj(W^(N/4 - m)) above it
+    const bool hi = k >= q;
+    const int m = hi ? k - q : k;
+    const bool mir = m > e;
+    const double2 t = T[mir ? q - m : m];
+    const double x = mir ? -t.y : t.x, y = mir ? -t.x : t.y;
+    return hi ? make_double2(y, -x) : make_double2(x, y);
+}
+
+// (x + iy) *= W_16^q = e^(-2 pi i q/16), q in [0, 8) a compile-time constant after
+// unrolling (the conjugate root when conj)
+__device__ __forceinline__ void mul_root16(double& x, double& y, int q, bool conj) {
+    constexpr double r2 = 0.70710678118654752440, c1 = 0.92387953251128675613, s1 = 0.38268343236508977173;
+    if (q == 0) return;
+    double c, s;   // W = c - i s
+    switch (q) {
+    case 4: {
+        const double t = x;
+        x = conj ? -y : y;
+        y = conj ? t : -t;
+        return;
+    }
+    case 2: c = r2; s = r2; break;
+    case 6: c = -r2; s = r2; break;
+    case 1: c = c1; s = s1; break;
+    case 3: c = s1; s = c1; break;
+    case 5: c = -s1; s = c1; break;
+    default: c = -c1; s = s1; break;   // 7
+    }
+    if (conj) s = -s;
+    const double nx = x * c + y * s, ny = y * c - x * s;
+    x = nx;
+    y = ny;
+}
+
+// DIF stages of spans h, h/2, ..., h >> (R-1) (h = 2^lh) on one group in registers; p is
+// the group's offset within its span (BASE false: p = 0, every stage twiddle is a root)
+template <int R, bool BASE>
+__device__ __forceinline__ void dif_regs(double* xr, double* xi, int lg, int lh, int p, const double2* T) {
+    constexpr int M = 1 << R;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int S = M >> (k + 1);
+        double2 w = make_double2(1.0, 0.0);
+        if (BASE) w = twc(T, p << (lg - 1 - lh + k), lg);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            if (j & S) continue;
+            const double ar = xr[j], ai = xi[j], cr = xr[j + S], ci = xi[j + S];
+            double dr = ar - cr, di = ai - ci;
+            if (BASE) cmul_tw(dr, di, w, false);
+            mul_root16(dr, di, (j & (S - 1)) << (4 - R + k), false);
+            xr[j] = ar + cr;
+            xi[j] = ai + ci;
+            xr[j + S] = dr;
+            xi[j + S] = di;
+        }
+    }
+}
+
+// DIT stages of spans h, 2h, ..., h << (R-1) with conjugate twiddles
+template <int R, bool BASE>
+__device__ __forceinline__ void dit_regs(double* xr, double* xi, int lg, int lh, int p, const double2* T) {
+    constexpr int M = 1 << R;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int S = 1 << k;
+        double2 w = make_double2(1.0, 0.0);
+        if (BASE) w = twc(T, p << (lg - 1 - lh - k), lg);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            if (j & S) continue;
+            double cr = xr[j + S], ci = xi[j + S];
+            if (BASE) cmul_tw(cr, ci, w, true);
+            mul_root16(cr, ci, (j & (S - 1)) << (3 - k), true);
+            const double ar = xr[j], ai = xi[j];
+            xr[j] = ar + cr;
+            xi[j] = ai + ci;
+            xr[j + S] = ar - cr;
+            xi[j + S] = ai - ci;
+        }
+    }
+}
+
+// one DIF pass over the frame: group b owns {g 2h + p + j d}, d = h >> (R-1)
+template <int R>
+__device__ __forceinline__ void dif_pass(double* re, double* im, int lg, int lh, const double2* T) {
+    constexpr int M = 1 << R;
+    const int ld = lh - (R - 1);
+    for (int b = threadIdx.x; b < (1 << (lg - R)); b += blockDim.x) {
+        const int p = b & ((1 << ld) - 1), base = ((b >> ld) << (lh + 1)) + p;
+        double xr[M], xi[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const int e = pad16(base + (j << ld));
+            xr[j] = re[e];
+            xi[j] = im[e];
+        }
+        dif_regs<R, true>(xr, xi, lg, lh, p, T);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const int e = pad16(base + (j << ld));
+            re[e] = xr[j];
+            im[e] = xi[j];
+        }
+    }
+}
+
+// one DIT pass over the frame: group b owns {g h 2^R + p + j h}
+template <int R>
+__device__ __forceinline__ void dit_pass(double* re, double* im, int lg, int lh, const double2* T) {
+    constexpr int M = 1 << R;
+    for (int b = threadIdx.x; b < (1 << (lg - R)); b += blockDim.x) {
+        const int p = b & ((1 << lh) - 1), base = ((b >> lh) << (lh + R)) + p;
+        double xr[M], xi[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const int e = pad16(base + (j << lh));
+            xr[j] = re[e];
+            xi[j] = im[e];
+        }
+        dit_regs<R, true>(xr, xi, lg, lh, p, T);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const int e = pad16(base + (j << lh));
+            re[e] = xr[j];
+            im[e] = xi[j];
+        }
+    }
+}
+
+// Pass plan for N = 2^lg: forward = [lg mod RMAX (if nonzero)], RMAX, ..., RMAX; inverse is
+// its mirror.  The last forward and first inverse passes (size fft_rlast) then touch the
+// same contiguous groups {b 2^R + j}, which lets a caller fuse them (and a processor) in
+// registers.  Each helper ends with a barrier.
+template <int RMAX>
+__host__ __device__ constexpr int fft_rlast(int lg) { return lg >= RMAX ? RMAX : lg; }
+
+template <int R, bool INV>
+__device__ __forceinline__ void fft_pass(double* re, double* im, int lg, int lh, const double2* T) {
+    if constexpr (INV) dit_pass<R>(re, im, lg, lh, T);
+    else dif_pass<R>(re, im, lg, lh, T);
+}
+
+template <int RMAX, bool INV>
+__device__ __forceinline__ void fft_pass_r(int R, double* re, double* im, int lg, int lh, const double2* T) {
+    switch (R) {
+    case 4: if constexpr (RMAX >= 4) fft_pass<4, INV>(re, im, lg, lh, T); break;
+    case 3: fft_pass<3, INV>(re, im, lg, lh, T); break;
+    case 2: fft_pass<2, INV>(re, im, lg, lh, T); break;
+    default: fft_pass<1, INV>(re, im, lg, lh, T); break;
+    }
+}
+
+// forward passes; `all` false stops before the last one (caller fuses it)
+template <int RMAX>
+__device__ __forceinline__ void fft_fwd_lead(double* re, double* im, int lg, const double2* T, bool all) {
+    int lh = lg - 1, left = lg;
+    const int rem = lg % RMAX;
+    if (rem && lg > RMAX) {
+        fft_pass_r<RMAX, false>(rem, re, im, lg, lh, T);
+        __syncthreads();
+        lh -= rem;
+        left -= rem;
+    }
+    for (; left > (all ? 0 : fft_rlast<RMAX>(lg)); left -= RMAX, lh -= RMAX) {
+        fft_pass_r<RMAX, false>(left < RMAX ? left : RMAX, re, im, lg, lh, T);
+        __syncthreads();
+    }
+}
+
+// inverse passes; `all` false skips the first one (caller fused it)
+template <int RMAX>
+__device__ __forceinline__ void fft_inv_tail(double* re, double* im, int lg, const double2* T, bool all) {
+    const int r0 = fft_rlast<RMAX>(lg);
+    int lh = 0, left = lg;
+    if (!all) {
+        lh = r0;
+        left -= r0;
+    }
+    for (; left > 0;) {
+        const int R = left >= RMAX ? RMAX : left;   // the remainder pass comes last
+        fft_pass_r<RMAX, true>(R, re, im, lg, lh, T);
+        __syncthreads();
+        lh += R;
+        left -= R;
     }
 }
 

@@ -32,14 +32,23 @@
 #include "hz_common.h"
 #include "hz_fft.h"
 
+// Experiment builds only (-DHZ_STFT_ABLATE=mask; wrong results): 1 skip the processor,
+// 2 skip the inverse FFT, 4 skip the forward FFT, 8 skip the ring store, 16 twiddles = tw[0].
+#ifndef HZ_STFT_ABLATE
+#define HZ_STFT_ABLATE 0
+#endif
+
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 1024;       // DCT workgroups: one radix-4 butterfly per thread at N = 4096
+constexpr int kFrameThreads = 512;   // STFT frame workgroups (N/8 threads at N = 4096, N/16 at 8192)
 constexpr int kMaxN = 8192;          // complex FP64 frame fully resident in LDS (128 KB)
-constexpr long kChunk = 1L << 18;    // samples per internal block (bounds the frame ring)
+constexpr long kChunkMax = 1L << 20;          // samples per internal block: one frame launch each
+constexpr size_t kRingBytes = 128u << 20;     // frame-ring budget that caps the block below kChunkMax
 
 struct StftArgs {
-    const double2* x;     // history: x[k] = input at time T0 - (N-1) + k
+    const double* xr;     // planar history: xr[k] = Re input at time T0 - (N-1) + k
+    const double* xi;     // Im plane; null when every sample this launch reads is real
     double2* fo;          // frame-output ring [R][N]
     double2* spec;        // host-processor path: spectra [frames][N] (natural order)
     const double* win;    // [N]
@@ -49,7 +58,7 @@ struct StftArgs {
     double p0, p1;
 };
 
-__device__ __forceinline__ long frame_start(long f, int laps, int stride, int N) {
+__host__ __device__ __forceinline__ long frame_start(long f, int laps, int stride, int N) {
     const long c = f / (2 * laps);
     const int i = (int)(f - c * 2 * laps);
     return (long)stride * i + c * (2L * N - 1);
@@ -89,89 +98,170 @@ __device__ __forceinline__ void block_sum_dd(double& hi, double& lo, double* scr
     lo = l;
 }
 
-// processors on the bit-reversed spectrum in LDS
-template <int PROC>
-__device__ __forceinline__ void apply_proc(double* re, double* im, int N, int lg, double p0, double p1,
+// Device processors on one group of spectrum slots held in registers: slots e0 + j
+// (bit-reversed order, bin k = bitrev(e0 + j)); `act` false for threads without a group.
+// Every thread calls this (the gates reduce over the whole frame).
+template <int PROC, int M>
+__device__ __forceinline__ void apply_proc(double* xr, double* xi, bool act, int e0, int N, double p0, double p1,
                                            double* scratch) {
 #pragma clang fp contract(off)
     if constexpr (PROC == HZ_PROC_STATIC_GATE) {   // staticSTFT.h:99-128
+        const double inv_n = 1.0 / N;   // exact (N = 2^lg): same as the reference's / N
         double part = 0.0;
-        for (int p = threadIdx.x; p < N; p += blockDim.x) part += sqrt(re[p] * re[p] + im[p] * im[p]) / N;
+        if (act)
+#pragma unroll
+            for (int j = 0; j < M; ++j) part += sqrt(xr[j] * xr[j] + xi[j] * xi[j]) * inv_n;
         const double average = block_sum(part, scratch);
         const double thr = p0 * average * average;
-        for (int p = threadIdx.x; p < N; p += blockDim.x) {
-            const double b0 = re[p], b1 = im[p];
-            if (b0 * b0 + b1 * b1 < thr) {
-                re[p] = b0 * p1;
-                im[p] = b1 * p1;
-            }
-        }
+        if (act)
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+                if (xr[j] * xr[j] + xi[j] * xi[j] < thr) {
+                    xr[j] = xr[j] * p1;
+                    xi[j] = xi[j] * p1;
+                }
     } else if constexpr (PROC == HZ_PROC_GATE_KEEP) {   // tests/spectral.cpp:32-72
         double hi = 0.0, lo = 0.0;
-        for (int p = threadIdx.x; p < N; p += blockDim.x) hz::dd_add(hi, lo, hypot(re[p], im[p]));
+        if (act)
+#pragma unroll
+            for (int j = 0; j < M; ++j) hz::dd_add(hi, lo, hypot(xr[j], xi[j]));
         block_sum_dd(hi, lo, scratch);
         // average = sum / N (long double in the reference); thr = p0 * average^2
         const double q = hi / N;
         const double avg = q + (fma(-q, (double)N, hi) + lo) / N;
         const double thr = p0 * avg * avg;
-        for (int p = threadIdx.x; p < N; p += blockDim.x) {
-            const double nrm = re[p] * re[p] + im[p] * im[p];
-            if (!(nrm > thr)) {
-                re[p] = 0.0;
-                im[p] = 0.0;
-            }
-        }
-    } else if constexpr (PROC == HZ_PROC_HILBERT) {   // bins k < N/2 kept; k = bitrev(p)
-        for (int p = threadIdx.x; p < N; p += blockDim.x)
-            if (p & 1) {
-                re[p] = 0.0;
-                im[p] = 0.0;
-            }
+        if (act)
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+                if (!(xr[j] * xr[j] + xi[j] * xi[j] > thr)) {
+                    xr[j] = 0.0;
+                    xi[j] = 0.0;
+                }
+    } else if constexpr (PROC == HZ_PROC_HILBERT) {   // bins k < N/2 kept: even slots
+        if (act)
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+                if ((e0 + j) & 1) {
+                    xr[j] = 0.0;
+                    xi[j] = 0.0;
+                }
     }
-    (void)lg;
+    (void)e0;
 }
 
+// The fused middle of a frame: last forward pass, processor, first inverse pass, all on the
+// same contiguous group {b 2^R + j} in registers (one group per thread)
+template <int R, int PROC>
+__device__ __forceinline__ void frame_middle(double* re, double* im, int lg, double p0, double p1, double* scratch,
+                                             const double2* T) {
+    constexpr int M = 1 << R;
+    const int b = threadIdx.x, e0 = b << R;
+    const bool act = b < (1 << (lg - R));
+    double xr[M], xi[M];
+    if (act) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            xr[j] = re[hz::pad16(e0 + j)];
+            xi[j] = im[hz::pad16(e0 + j)];
+        }
+        if constexpr (!(HZ_STFT_ABLATE & 4)) hz::dif_regs<R, false>(xr, xi, lg, R - 1, 0, T);
+    }
+    if constexpr (!(HZ_STFT_ABLATE & 1)) apply_proc<PROC, M>(xr, xi, act, e0, 1 << lg, p0, p1, scratch);
+    if (act) {
+        if constexpr (!(HZ_STFT_ABLATE & 2)) hz::dit_regs<R, false>(xr, xi, lg, 0, 0, T);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            re[hz::pad16(e0 + j)] = xr[j];
+            im[hz::pad16(e0 + j)] = xi[j];
+        }
+    }
+}
+
+// stages per LDS pass: radix 8 up to N = 4096 (512 threads, 8 waves per frame), radix 16 above
+inline int frame_rmax(int N) { return N > 4096 ? 4 : 3; }
+
+// XCD-aware frame order: workgroups go round-robin over the 8 XCDs, so give each XCD a
+// contiguous run of frames -- overlapping frames then share input lines in that XCD's L2
+__device__ __forceinline__ int frame_of_block(int b, int nf) {
+    const int x = b & 7, q = nf >> 3, r = nf & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
+// threads per frame workgroup: one radix-2^rmax group per thread, at least one wave
+inline int frame_threads(int N) {
+    const int t = N >> frame_rmax(N);
+    return t < 64 ? 64 : (t > kFrameThreads ? kFrameThreads : t);
+}
+
+// dynamic LDS of a frame workgroup: padded re/im, the block-sum scratch, the compact twiddles
+inline size_t frame_lds(int N) {
+    int lg = 0;
+    while ((1 << lg) < N) ++lg;
+    return sizeof(double) * (2 * (size_t)hz::padded_len(N) + 2 * (size_t)(frame_threads(N) / 64)) +
+           sizeof(double2) * (size_t)hz::twc_len(lg);
+}
+
+// One workgroup per frame; the frame stays in LDS from the window to the overlap-add ring.
 // MODE 0: fused (window, FFT, device processor, IFFT -> ring)
 // MODE 1: forward only (window, FFT -> spec, natural order)
 // MODE 2: inverse only (spec -> IFFT -> ring)
-template <int PROC, int MODE>
-__global__ __launch_bounds__(kThreads) void stft_frame_kernel(StftArgs a) {
+template <int PROC, int MODE, int RMAX>
+__global__ __launch_bounds__(kFrameThreads) void stft_frame_kernel(StftArgs a) {
 #pragma clang fp contract(off)
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int N = a.N;
+    const int N = a.N, lg = a.lg;
     double* re = lds;
-    double* im = lds + N;
-    double* scratch = lds + 2 * N;
-    const long f = a.f_lo + blockIdx.x;
+    double* im = lds + hz::padded_len(N);
+    double* scratch = im + hz::padded_len(N);
+    double2* T = (double2*)(scratch + 2 * (blockDim.x >> 6));
+    for (int k = threadIdx.x; k < hz::twc_len(lg); k += blockDim.x) T[k] = a.tw[k];
+    const int fl = frame_of_block(blockIdx.x, gridDim.x);   // frame within the launch
+    const long f = a.f_lo + fl;
     if constexpr (MODE != 2) {
         const long off = frame_start(f, a.laps, a.stride, N) - a.T0 + (N - 1);
         for (int k = threadIdx.x; k < N; k += blockDim.x) {
-            const double2 v = a.x[off + k];
+            const double vr = a.xr[off + k], vi = a.xi ? a.xi[off + k] : 0.0;
             const double w = a.win[k];
-            re[k] = w * v.x;   // fourier.h:110-112: window * real, window * imag
-            im[k] = w * v.y;
+            const int e = hz::pad16(k);
+            re[e] = w * vr;   // fourier.h:110-112: window * real, window * imag
+            im[e] = w * vi;
         }
-        __syncthreads();
-        hz::lds_fft_fwd(re, im, N, a.lg, a.tw);
-        if constexpr (MODE == 1) {
-            double2* sp = a.spec + (long)blockIdx.x * N;
-            for (int p = threadIdx.x; p < N; p += blockDim.x) sp[hz::bitrev(p, a.lg)] = make_double2(re[p], im[p]);
-            return;
-        }
-        apply_proc<PROC>(re, im, N, a.lg, a.p0, a.p1, scratch);
-        __syncthreads();
     } else {
-        const double2* sp = a.spec + (long)blockIdx.x * N;
+        const double2* sp = a.spec + (long)fl * N;
         for (int p = threadIdx.x; p < N; p += blockDim.x) {
-            const double2 v = sp[hz::bitrev(p, a.lg)];
-            re[p] = v.x;
-            im[p] = v.y;
+            const double2 v = sp[hz::bitrev(p, lg)];
+            const int e = hz::pad16(p);
+            re[e] = v.x;
+            im[e] = v.y;
+        }
+    }
+    __syncthreads();
+    if constexpr (MODE == 1) {
+        hz::fft_fwd_lead<RMAX>(re, im, lg, T, true);
+        double2* sp = a.spec + (long)fl * N;
+        for (int p = threadIdx.x; p < N; p += blockDim.x) {
+            const int e = hz::pad16(p);
+            sp[hz::bitrev(p, lg)] = make_double2(re[e], im[e]);
+        }
+        return;
+    } else if constexpr (MODE == 2) {
+        hz::fft_inv_tail<RMAX>(re, im, lg, T, true);
+    } else {
+        if constexpr (!(HZ_STFT_ABLATE & 4)) hz::fft_fwd_lead<RMAX>(re, im, lg, T, false);
+        switch (hz::fft_rlast<RMAX>(lg)) {
+        case 4: if constexpr (RMAX >= 4) frame_middle<4, PROC>(re, im, lg, a.p0, a.p1, scratch, T); break;
+        case 3: frame_middle<3, PROC>(re, im, lg, a.p0, a.p1, scratch, T); break;
+        default: frame_middle<2, PROC>(re, im, lg, a.p0, a.p1, scratch, T); break;   // N = 4
         }
         __syncthreads();
+        if constexpr (!(HZ_STFT_ABLATE & 2)) hz::fft_inv_tail<RMAX>(re, im, lg, T, false);
     }
-    hz::lds_fft_inv(re, im, N, a.lg, a.tw);
     double2* out = a.fo + (f % a.R) * N;
-    for (int k = threadIdx.x; k < N; k += blockDim.x) out[k] = make_double2(re[k], im[k]);
+    if constexpr ((HZ_STFT_ABLATE & 8) != 0) return;
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+        const int e = hz::pad16(k);
+        out[k] = make_double2(re[e], im[e]);
+    }
 }
 
 struct OlaArgs {
@@ -222,14 +312,21 @@ __global__ __launch_bounds__(256) void stft_ola_kernel(OlaArgs a) {
 }
 
 __global__ void stft_stage_kernel(const double* __restrict__ re, const double* __restrict__ im, long n,
-                                  double2* __restrict__ dst) {
+                                  double* __restrict__ dst_re, double* __restrict__ dst_im) {
     const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n) dst[j] = make_double2(re[j], im ? im[j] : 0.0);
+    if (j < n) {
+        dst_re[j] = re[j];
+        dst_im[j] = im ? im[j] : 0.0;
+    }
 }
 
-__global__ void copy_c_kernel(const double2* __restrict__ src, long n, double2* __restrict__ dst) {
+// history carry: n samples of both planes (plane stride `cap` in both buffers)
+__global__ void copy_hist_kernel(const double* __restrict__ src, long n, long cap, double* __restrict__ dst) {
     const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n) dst[j] = src[j];
+    if (j < n) {
+        dst[j] = src[j];
+        dst[cap + j] = src[cap + j];
+    }
 }
 
 // ---- Cosine: REDFT10 / REDFT01 via a length-N complex FFT (one workgroup per transform)
@@ -306,7 +403,9 @@ struct hz_stft {
     long T = 0;        // samples processed
     long frames = 0;   // frames completed
     double* d_win = nullptr;
-    double2 *d_tw = nullptr, *d_fo = nullptr, *d_x[2] = {nullptr, nullptr}, *d_spec = nullptr;
+    double2 *d_tw = nullptr, *d_fo = nullptr, *d_spec = nullptr;
+    double* d_x[2] = {nullptr, nullptr};   // planar history buffers [Re plane | Im plane], x_cap samples each
+    long last_cplx = -1;                   // last sample index that came with an imaginary part
     int xcur = 0;
     size_t x_cap = 0, spec_cap = 0;
     double *d_in = nullptr, *d_out = nullptr;
@@ -315,6 +414,8 @@ struct hz_stft {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     bool prof = false;
+    long chunk = 0;        // samples per internal block (a frame launch covers one)
+    int prof_repeat = 1;   // frame launches per block while profiling (hz_stft_profile)
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     long launches = 0;
@@ -343,16 +444,29 @@ long frames_before(const hz_stft* h, long T) {
 }
 
 template <int PROC, int MODE>
-void launch_frames(hz_stft* h, const StftArgs& a, long nf, size_t lds) {
-    hipLaunchKernelGGL((stft_frame_kernel<PROC, MODE>), dim3((unsigned)nf), dim3(kThreads), lds, h->stream, a);
+void frame_attr(int lds) {
+    (void)hipFuncSetAttribute((const void*)stft_frame_kernel<PROC, MODE, 3>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)stft_frame_kernel<PROC, MODE, 4>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
-int frames_fused(hz_stft* h, const StftArgs& a, long nf, size_t lds) {
+template <int PROC, int MODE>
+void launch_frames(hz_stft* h, const StftArgs& a, long nf) {
+    if (frame_rmax(h->N) == 3)
+        hipLaunchKernelGGL((stft_frame_kernel<PROC, MODE, 3>), dim3((unsigned)nf), dim3(frame_threads(h->N)),
+                           frame_lds(h->N), h->stream, a);
+    else
+        hipLaunchKernelGGL((stft_frame_kernel<PROC, MODE, 4>), dim3((unsigned)nf), dim3(frame_threads(h->N)),
+                           frame_lds(h->N), h->stream, a);
+}
+
+int frames_fused(hz_stft* h, const StftArgs& a, long nf) {
     switch (h->proc) {
-    case HZ_PROC_STATIC_GATE: launch_frames<HZ_PROC_STATIC_GATE, 0>(h, a, nf, lds); break;
-    case HZ_PROC_GATE_KEEP: launch_frames<HZ_PROC_GATE_KEEP, 0>(h, a, nf, lds); break;
-    case HZ_PROC_HILBERT: launch_frames<HZ_PROC_HILBERT, 0>(h, a, nf, lds); break;
-    default: launch_frames<HZ_PROC_IDENTITY, 0>(h, a, nf, lds); break;
+    case HZ_PROC_STATIC_GATE: launch_frames<HZ_PROC_STATIC_GATE, 0>(h, a, nf); break;
+    case HZ_PROC_GATE_KEEP: launch_frames<HZ_PROC_GATE_KEEP, 0>(h, a, nf); break;
+    case HZ_PROC_HILBERT: launch_frames<HZ_PROC_HILBERT, 0>(h, a, nf); break;
+    default: launch_frames<HZ_PROC_IDENTITY, 0>(h, a, nf); break;
     }
     HZ_TRY_HIP(hipGetLastError());
     return HZ_OK;
@@ -369,30 +483,34 @@ int ensure_dev(void** p, size_t* cap, size_t bytes) {
 
 int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore, double* d_oim, long n) {
     const int N = h->N;
-    // history buffers hold N-1 + n samples
-    const size_t need = sizeof(double2) * (size_t)(N - 1 + n);
-    if (need > h->x_cap) {
-        double2* nb[2] = {nullptr, nullptr};
-        HZ_TRY_HIP(hipMalloc(&nb[0], need));
-        HZ_TRY_HIP(hipMalloc(&nb[1], need));
-        if (h->d_x[h->xcur])
-            HZ_TRY_HIP(hipMemcpyAsync(nb[0], h->d_x[h->xcur], sizeof(double2) * (N - 1), hipMemcpyDeviceToDevice,
-                                      h->stream));
-        else
-            HZ_TRY_HIP(hipMemsetAsync(nb[0], 0, sizeof(double2) * (N - 1), h->stream));
+    // history buffers hold N-1 + n samples per plane
+    const long need = N - 1 + n;
+    if ((size_t)need > h->x_cap) {
+        double* nb[2] = {nullptr, nullptr};
+        HZ_TRY_HIP(hipMalloc(&nb[0], 2 * sizeof(double) * need));
+        HZ_TRY_HIP(hipMalloc(&nb[1], 2 * sizeof(double) * need));
+        for (int pl = 0; pl < 2; ++pl) {
+            if (h->d_x[h->xcur])
+                HZ_TRY_HIP(hipMemcpyAsync(nb[0] + pl * need, h->d_x[h->xcur] + pl * h->x_cap, sizeof(double) * (N - 1),
+                                          hipMemcpyDeviceToDevice, h->stream));
+            else
+                HZ_TRY_HIP(hipMemsetAsync(nb[0] + pl * need, 0, sizeof(double) * (N - 1), h->stream));
+        }
         HZ_TRY_HIP(hipStreamSynchronize(h->stream));
-        for (double2* p : h->d_x)
+        for (double* p : h->d_x)
             if (p) HZ_TRY_HIP(hipFree(p));
         h->d_x[0] = nb[0];
         h->d_x[1] = nb[1];
         h->xcur = 0;
-        h->x_cap = need;
+        h->x_cap = (size_t)need;
     }
-    double2* xc = h->d_x[h->xcur];
-    double2* xn = h->d_x[h->xcur ^ 1];
+    const long cap = (long)h->x_cap;
+    double* xc = h->d_x[h->xcur];
+    double* xn = h->d_x[h->xcur ^ 1];
     hipLaunchKernelGGL(stft_stage_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, d_re, d_im, n,
-                       xc + (N - 1));
+                       xc + (N - 1), xc + cap + (N - 1));
     HZ_TRY_HIP(hipGetLastError());
+    if (d_im) h->last_cplx = h->T + n - 1;
 
     hipEvent_t* e = nullptr;
     if (h->prof) {
@@ -409,12 +527,15 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
     const long f_lo = frames_before(h, h->T), f_hi = frames_before(h, h->T + n);
     const long nf = f_hi - f_lo;
     StftArgs a;
-    a.x = xc;
+    a.xr = xc;
+    a.xi = nullptr;
     a.fo = h->d_fo;
     a.spec = h->d_spec;
     a.win = h->d_win;
     a.tw = h->d_tw;
     a.f_lo = f_lo;
+    // frames start in increasing order: the first one decides whether any reads an Im part
+    if (nf > 0 && frame_start(f_lo, h->laps, h->stride, N) <= h->last_cplx) a.xi = xc + cap;
     a.T0 = h->T;
     a.N = N;
     a.lg = h->lg;
@@ -423,14 +544,15 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
     a.R = h->R;
     a.p0 = h->p0;
     a.p1 = h->p1;
-    const size_t lds = sizeof(double) * (2 * (size_t)N + 2 * (kThreads / 64));
     if (nf > 0) {
         if (h->proc != HZ_PROC_HOST) {
-            HZ_TRY(frames_fused(h, a, nf, lds));
+            // profiling may repeat the (idempotent) frame launch so the event pair brackets
+            // several back-to-back launches: per-launch time without the event overhead
+            for (int r = 0; r < (h->prof ? h->prof_repeat : 1); ++r) HZ_TRY(frames_fused(h, a, nf));
         } else {
             HZ_TRY(ensure_dev((void**)&h->d_spec, &h->spec_cap, sizeof(double2) * (size_t)nf * N));
             a.spec = h->d_spec;
-            launch_frames<HZ_PROC_IDENTITY, 1>(h, a, nf, lds);
+            launch_frames<HZ_PROC_IDENTITY, 1>(h, a, nf);
             HZ_TRY_HIP(hipGetLastError());
             h->h_spec.resize((size_t)nf * N);
             HZ_TRY_HIP(hipMemcpyAsync(h->h_spec.data(), h->d_spec, sizeof(double2) * (size_t)nf * N,
@@ -445,7 +567,7 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
             }
             HZ_TRY_HIP(hipMemcpyAsync(h->d_spec, h->h_spec.data(), sizeof(double2) * (size_t)nf * N,
                                       hipMemcpyHostToDevice, h->stream));
-            launch_frames<HZ_PROC_IDENTITY, 2>(h, a, nf, lds);
+            launch_frames<HZ_PROC_IDENTITY, 2>(h, a, nf);
             HZ_TRY_HIP(hipGetLastError());
         }
     }
@@ -465,8 +587,8 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
     HZ_TRY_HIP(hipGetLastError());
     if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     // history for the next block: the last N-1 samples of [T0-N+1, T0+n)
-    hipLaunchKernelGGL(copy_c_kernel, dim3((unsigned)((N - 1 + 255) / 256)), dim3(256), 0, h->stream,
-                       (const double2*)(xc + n), (long)(N - 1), xn);
+    hipLaunchKernelGGL(copy_hist_kernel, dim3((unsigned)((N - 1 + 255) / 256)), dim3(256), 0, h->stream,
+                       (const double*)(xc + n), (long)(N - 1), cap, xn);
     HZ_TRY_HIP(hipGetLastError());
     h->xcur ^= 1;
     h->T += n;
@@ -476,8 +598,8 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
 }
 
 int stft_run(hz_stft* h, const double* d_re, const double* d_im, double* d_ore, double* d_oim, long n) {
-    for (long o = 0; o < n; o += kChunk) {
-        const long m = std::min(kChunk, n - o);
+    for (long o = 0; o < n; o += h->chunk) {
+        const long m = std::min(h->chunk, n - o);
         HZ_TRY(stft_block(h, d_re + o, d_im ? d_im + o : nullptr, d_ore + o, d_oim ? d_oim + o : nullptr, m));
     }
     return HZ_OK;
@@ -508,7 +630,10 @@ int hz_stft_create(int N, int laps, int window, int proc, double p0, double p1, 
     h->device = device;
     // frames completing inside one internal block, plus those still being read
     const long P = 2L * N - 1;
-    h->R = (int)((kChunk + P - 1) / P * 2 * laps + 2 * laps + 2);
+    auto ring = [&](long c) { return (c + P - 1) / P * 2 * laps + 2 * laps + 2; };
+    h->chunk = kChunkMax;
+    while (h->chunk > 4L * N && (size_t)ring(h->chunk) * N * sizeof(double2) > kRingBytes) h->chunk >>= 1;
+    h->R = (int)ring(h->chunk);
     h->h_out.assign((size_t)2 * laps * N, make_double2(0.0, 0.0));
     std::vector<double> win(N);
     for (int k = 0; k < N; ++k) {   // src/wave.h:148-149 with the truncated PI, in double
@@ -534,20 +659,14 @@ int hz_stft_create(int N, int laps, int window, int proc, double p0, double p1, 
     }
     h->own_stream = true;
     static bool attr = false;
-    if (!attr) {   // 2N doubles of LDS per workgroup (128 KB at N = 8192)
-        const int lds = (int)(sizeof(double) * (2 * kMaxN + 2 * (kThreads / 64)));
-        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_IDENTITY, 0>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_STATIC_GATE, 0>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_GATE_KEEP, 0>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_HILBERT, 0>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_IDENTITY, 1>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        (void)hipFuncSetAttribute((const void*)stft_frame_kernel<HZ_PROC_IDENTITY, 2>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (!attr) {   // padded frame: 2 (N + N/16) doubles of LDS per workgroup (136 KB at N = 8192)
+        const int lds = (int)std::max(frame_lds(kMaxN), sizeof(double) * (2 * kMaxN + 2 * (kThreads / 64)));
+        frame_attr<HZ_PROC_IDENTITY, 0>(lds);
+        frame_attr<HZ_PROC_STATIC_GATE, 0>(lds);
+        frame_attr<HZ_PROC_GATE_KEEP, 0>(lds);
+        frame_attr<HZ_PROC_HILBERT, 0>(lds);
+        frame_attr<HZ_PROC_IDENTITY, 1>(lds);
+        frame_attr<HZ_PROC_IDENTITY, 2>(lds);
         (void)hipFuncSetAttribute((const void*)dct2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         (void)hipFuncSetAttribute((const void*)dct3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr = true;
@@ -642,6 +761,7 @@ int hz_stft_profile(hz_stft* h, int enable) {
     HZ_TRY(stft_check(h));
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
     h->prof = enable != 0;
+    h->prof_repeat = enable > 1 ? enable : 1;
     h->ev_used = 0;
     h->launches = 0;
     return HZ_OK;
@@ -658,7 +778,7 @@ int hz_stft_profile_read(hz_stft* h, double* frame_ms, double* ola_ms, long* blo
         fm += t0;
         om += t1;
     }
-    if (frame_ms) *frame_ms = fm;
+    if (frame_ms) *frame_ms = fm / (h->proc != HZ_PROC_HOST ? h->prof_repeat : 1);   // per single launch
     if (ola_ms) *ola_ms = om;
     if (blocks) *blocks = h->launches;
     h->ev_used = 0;

@@ -80,8 +80,10 @@ class Fourier:
     def synchronize(self):
         check(self._lib.hz_stft_synchronize(self._h))
 
-    def profile(self, enable: bool):
-        check(self._lib.hz_stft_profile(self._h, 1 if enable else 0))
+    def profile(self, enable: bool, repeat: int = 1):
+        """Event-time the frame / overlap-add kernels; repeat > 1 launches each block's frame
+        kernel `repeat` times back to back (per-launch time without the event overhead)."""
+        check(self._lib.hz_stft_profile(self._h, max(1, int(repeat)) if enable else 0))
 
     def profile_read(self):
         a, b, c = C.c_double(), C.c_double(), C.c_long()

@@ -249,6 +249,9 @@ int hz_stft_process_block_device(hz_stft* h, const double* d_re, const double* d
 int hz_stft_frames(hz_stft* h, long* frames, long* samples);
 int hz_stft_set_stream(hz_stft* h, void* hip_stream);
 int hz_stft_synchronize(hz_stft* h);
+/* Event timing of the frame and overlap-add kernels.  enable > 1 repeats each block's
+ * (idempotent) device-processor frame launch `enable` times between the events, so the
+ * event overhead is amortised; profile_read then reports frame_ms per single launch. */
 int hz_stft_profile(hz_stft* h, int enable);
 int hz_stft_profile_read(hz_stft* h, double* frame_ms, double* ola_ms, long* blocks);
 

@@ -70,4 +70,16 @@ private:
     T last_ = 0;
 };
 
+// FFilterbank<T, N, order> (src/filterbank.h:191-319): the fixed-size variant.  The
+// reference keeps the same maths in fixed-size Eigen types (its smoothing factors are T
+// rather than double: identical for T = double), so it is the same engine with N and the
+// order fixed at compile time; the API is Filterbank's minus print().
+template <typename T, std::size_t N, std::size_t order>
+class FFilterbank : public Filterbank<T> {
+public:
+    explicit FFilterbank(double k_p = 0.1, double k_g = 1, int device = 0)
+        : Filterbank<T>((int)order, (int)N, k_p, k_g, device) {}
+    void print() = delete;
+};
+
 }  // namespace soundmath

@@ -53,6 +53,18 @@ int main(int argc, char** argv) {
         }
         fb.process(x.data() + 100, y.data() + 100, 900);
         dump("filterbank", y);
+
+        // FFilterbank<double, 16, 2> (tests/filterbank.cpp:184,194 pattern), block form only
+        FFilterbank<double, 16, 2> ff;
+        for (int i = 0; i < 16; i++) {
+            const double g = 0.01 * (i + 1), R = 0.99, th = 2 * PI * (i + 1) / 40.0;
+            ff.coefficients(i, {g, 0, -g}, {-2 * R * std::cos(th), R * R});
+        }
+        ff.boost(std::vector<double>(16, 1.0));
+        ff.open();
+        std::vector<double> z(1000);
+        ff.process(x.data(), z.data(), 1000);
+        dump("ffilterbank", z);
     }
     {   // Delay: tests/delay.cpp:18,41
         Delay<double> delay(10, 2 * SR);

@@ -47,6 +47,17 @@ def test_filterbank(outputs):
     assert rel_err(outputs("filterbank"), o.process(x_input(1000))) < 1e-9
 
 
+def test_ffilterbank(outputs):
+    """FFilterbank<double, 16, 2>: the same bank in one process() call."""
+    o = OracleFilterbank(2, 16)
+    for i in range(16):
+        g, R, th = 0.01 * (i + 1), 0.99, 2 * PI * (i + 1) / 40.0
+        o.coefficients(i, [g, 0, -g], [-2 * R * np.cos(th), R * R])
+    o.boost(np.ones(16))
+    o.open()
+    assert rel_err(outputs("ffilterbank"), o.process(x_input(1000))) < 1e-9
+
+
 def test_delay_bit_exact(outputs):
     o = OracleDelaybank(1, 10, 2 * 48000)
     o.coefficients(0, [(0, 1.0)], [(20000, 0.5), (10000, 0.5)])

@@ -63,7 +63,23 @@ def test_identity_vs_oracle_blocks(gpu_lib, N, laps, window):
     assert g.frames()[0] == o.frames()
 
 
-@pytest.mark.parametrize("N,laps", [(4096, 4), (8192, 4), (512, 4)])
+@pytest.mark.parametrize("N,laps", [(64, 4), (4096, 4)])
+def test_real_then_complex_calls(gpu_lib, N, laps):
+    """Real-only calls skip the Im history plane; a complex call must switch it back on for
+    every frame that reads one of its samples, including frames straddling later real calls."""
+    g, o = make(N, laps, 0, 0)
+    rng = np.random.default_rng(7)
+    for n, cplx in ((3 * N + 1, False), (N // 2 + 3, True), (5, False), (4 * N, False), (N + 9, True), (3 * N, False)):
+        re = rng.standard_normal(n)
+        im = rng.standard_normal(n) if cplx else None
+        gr, gi = g.process_block(re, im)
+        orr, oi = o.process_block(re, im)
+        scale = max(np.max(np.abs(orr)), np.max(np.abs(oi)), 1e-300)   # Im of a real call is ~0: use one scale
+        assert np.max(np.abs(gr - orr)) < TOL * scale and np.max(np.abs(gi - oi)) < TOL * scale
+    assert g.frames()[0] == o.frames()
+
+
+@pytest.mark.parametrize("N,laps", [(4096, 4), (8192, 4), (512, 4), (8192, 32)])
 def test_static_stft_c4(gpu_lib, N, laps):
     from huygens_amd import StaticSTFT
     g = StaticSTFT(N, laps)
