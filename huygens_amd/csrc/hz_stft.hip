@@ -47,9 +47,11 @@ constexpr long kChunkMax = 1L << 20;          // samples per internal block: one
 constexpr size_t kRingBytes = 128u << 20;     // frame-ring budget that caps the block below kChunkMax
 
 struct StftArgs {
-    const double* xr;     // planar history: xr[k] = Re input at time T0 - (N-1) + k
-    const double* xi;     // Im plane; null when every sample this launch reads is real
-    double2* fo;          // frame-output ring [R][N]
+    const double* hr;     // history: hr[k] = Re input at time T0 - (N-1) + k, k < N-1
+    const double* hi;     // its Im plane; null when every sample this launch reads is real
+    const double* inr;    // this block's input (caller memory): time T0 + k
+    const double* ini;    // its Im part (may be null: real input)
+    double* fo;           // frame-output ring, planar: Re [R][N] then Im [R][N]
     double2* spec;        // host-processor path: spectra [frames][N] (natural order)
     const double* win;    // [N]
     const double2* tw;    // [N/2]  e^{-2 pi i k/N}
@@ -178,7 +180,10 @@ __device__ __forceinline__ void frame_middle(double* re, double* im, int lg, dou
 }
 
 // stages per LDS pass: radix 8 up to N = 4096 (512 threads, 8 waves per frame), radix 16 above
-inline int frame_rmax(int N) { return N > 4096 ? 4 : 3; }
+#ifndef HZ_STFT_R4_ABOVE
+#define HZ_STFT_R4_ABOVE 4096
+#endif
+inline int frame_rmax(int N) { return N > HZ_STFT_R4_ABOVE ? 4 : 3; }
 
 // XCD-aware frame order: workgroups go round-robin over the 8 XCDs, so give each XCD a
 // contiguous run of frames -- overlapping frames then share input lines in that XCD's L2
@@ -220,7 +225,15 @@ __global__ __launch_bounds__(kFrameThreads) void stft_frame_kernel(StftArgs a) {
     if constexpr (MODE != 2) {
         const long off = frame_start(f, a.laps, a.stride, N) - a.T0 + (N - 1);
         for (int k = threadIdx.x; k < N; k += blockDim.x) {
-            const double vr = a.xr[off + k], vi = a.xi ? a.xi[off + k] : 0.0;
+            const long u = off + k;   // position in [history (N-1) | block input]
+            double vr, vi = 0.0;
+            if (u < N - 1) {
+                vr = a.hr[u];
+                if (a.hi) vi = a.hi[u];
+            } else {
+                vr = a.inr[u - (N - 1)];
+                if (a.hi && a.ini) vi = a.ini[u - (N - 1)];
+            }
             const double w = a.win[k];
             const int e = hz::pad16(k);
             re[e] = w * vr;   // fourier.h:110-112: window * real, window * imag
@@ -256,48 +269,84 @@ __global__ __launch_bounds__(kFrameThreads) void stft_frame_kernel(StftArgs a) {
         __syncthreads();
         if constexpr (!(HZ_STFT_ABLATE & 2)) hz::fft_inv_tail<RMAX>(re, im, lg, T, false);
     }
-    double2* out = a.fo + (f % a.R) * N;
+    double* out = a.fo + (f % a.R) * N;
+    const long plane = (long)a.R * N;
     if constexpr ((HZ_STFT_ABLATE & 8) != 0) return;
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
         const int e = hz::pad16(k);
-        out[k] = make_double2(re[e], im[e]);
+        out[k] = re[e];
+        out[plane + k] = im[e];
     }
 }
 
 struct OlaArgs {
-    const double2* fo;
+    const double* fo;   // planar ring (Re plane, then Im plane of R*N)
     const double* win;
     double* out_re;
     double* out_im;
     long T0, n;
     int N, laps, stride, R;
+    // history carry for the next block (folded in to save a launch): the last N-1 samples of
+    // [history (N-1) | block input (n)] from hist_old / in_re / in_im into hist_new
+    const double* hist_old;
+    const double* in_re;
+    const double* in_im;
+    double* hist_new;
 };
 
 __global__ __launch_bounds__(256) void stft_ola_kernel(OlaArgs a) {
     const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < a.N - 1) {
+        const int N1 = a.N - 1;
+        const long s = j + a.n;
+        if (s < N1) {
+            a.hist_new[j] = a.hist_old[s];
+            a.hist_new[N1 + j] = a.hist_old[N1 + s];
+        } else {
+            a.hist_new[j] = a.in_re[s - N1];
+            a.hist_new[N1 + j] = a.in_im ? a.in_im[s - N1] : 0.0;
+        }
+    }
     if (j >= a.n) return;
     const long t = a.T0 + j;
     const long P = 2L * a.N - 1;
     const long u0 = t - (a.N - 1);
     double rh = 0.0, rl = 0.0, ih = 0.0, il = 0.0;
     if (u0 >= 0) {
-        long c = u0 / P;
+        // u0 = c P + r without a 64-bit divide: double quotient, then one correction step
+        long c = (long)((double)u0 / (double)P);
         long r = u0 - c * P;
+        if (r < 0) {
+            r += P;
+            --c;
+        } else if (r >= P) {
+            r -= P;
+            ++c;
+        }
+        // ring row of frame f = c 2 laps + i is (f mod R); track (c 2 laps) mod R incrementally
+        const long cf = c * 2 * a.laps;
+        int base = (int)(cf - (long)((double)cf / (double)a.R) * a.R);
+        if (base < 0) base += a.R;
+        if (base >= a.R) base -= a.R;
+        const long plane = (long)a.R * a.N;
         for (int i = 0; i < 2 * a.laps; ++i) {   // fourier.h:153-172, slot order
             if (i) {
                 r -= a.stride;
-                while (r < 0) {
+                if (r < 0) {   // stride < P: at most one wrap per slot
                     r += P;
                     --c;
+                    base -= 2 * a.laps;
+                    if (base < 0) base += a.R;
                 }
             }
             if (c < 0) break;
             if (r >= a.N) continue;
-            const long f = c * 2 * a.laps + i;
-            const double2 v = a.fo[(f % a.R) * a.N + r];
+            int row = base + i;
+            if (row >= a.R) row -= a.R;
+            const long q = (long)row * a.N + r;
             const double w = a.win[r];
-            hz::dd_add(rh, rl, w * v.x);
-            hz::dd_add(ih, il, w * v.y);
+            hz::dd_add(rh, rl, w * a.fo[q]);
+            if (a.out_im) hz::dd_add(ih, il, w * a.fo[plane + q]);
         }
     }
     const double D = (double)(a.N * a.laps / 2);   // int expression, fourier.h:174-175
@@ -308,24 +357,6 @@ __global__ __launch_bounds__(256) void stft_ola_kernel(OlaArgs a) {
         double qi = ih / D;
         qi += (fma(-qi, D, ih) + il) / D;
         a.out_im[j] = qi;
-    }
-}
-
-__global__ void stft_stage_kernel(const double* __restrict__ re, const double* __restrict__ im, long n,
-                                  double* __restrict__ dst_re, double* __restrict__ dst_im) {
-    const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n) {
-        dst_re[j] = re[j];
-        dst_im[j] = im ? im[j] : 0.0;
-    }
-}
-
-// history carry: n samples of both planes (plane stride `cap` in both buffers)
-__global__ void copy_hist_kernel(const double* __restrict__ src, long n, long cap, double* __restrict__ dst) {
-    const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n) {
-        dst[j] = src[j];
-        dst[cap + j] = src[cap + j];
     }
 }
 
@@ -403,11 +434,12 @@ struct hz_stft {
     long T = 0;        // samples processed
     long frames = 0;   // frames completed
     double* d_win = nullptr;
-    double2 *d_tw = nullptr, *d_fo = nullptr, *d_spec = nullptr;
-    double* d_x[2] = {nullptr, nullptr};   // planar history buffers [Re plane | Im plane], x_cap samples each
-    long last_cplx = -1;                   // last sample index that came with an imaginary part
-    int xcur = 0;
-    size_t x_cap = 0, spec_cap = 0;
+    double2 *d_tw = nullptr, *d_spec = nullptr;
+    double* d_fo = nullptr;                    // planar frame ring: Re [R][N], Im [R][N]
+    double* d_hist[2] = {nullptr, nullptr};    // last N-1 input samples, [Re | Im] (ping-pong)
+    long last_cplx = -1;                       // last sample index that came with an imaginary part
+    int hcur = 0;
+    size_t spec_cap = 0;
     double *d_in = nullptr, *d_out = nullptr;
     size_t io_cap = 0;
     std::vector<double2> h_spec, h_out;   // host-processor path: spectra + per-slot out buffers
@@ -483,33 +515,8 @@ int ensure_dev(void** p, size_t* cap, size_t bytes) {
 
 int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore, double* d_oim, long n) {
     const int N = h->N;
-    // history buffers hold N-1 + n samples per plane
-    const long need = N - 1 + n;
-    if ((size_t)need > h->x_cap) {
-        double* nb[2] = {nullptr, nullptr};
-        HZ_TRY_HIP(hipMalloc(&nb[0], 2 * sizeof(double) * need));
-        HZ_TRY_HIP(hipMalloc(&nb[1], 2 * sizeof(double) * need));
-        for (int pl = 0; pl < 2; ++pl) {
-            if (h->d_x[h->xcur])
-                HZ_TRY_HIP(hipMemcpyAsync(nb[0] + pl * need, h->d_x[h->xcur] + pl * h->x_cap, sizeof(double) * (N - 1),
-                                          hipMemcpyDeviceToDevice, h->stream));
-            else
-                HZ_TRY_HIP(hipMemsetAsync(nb[0] + pl * need, 0, sizeof(double) * (N - 1), h->stream));
-        }
-        HZ_TRY_HIP(hipStreamSynchronize(h->stream));
-        for (double* p : h->d_x)
-            if (p) HZ_TRY_HIP(hipFree(p));
-        h->d_x[0] = nb[0];
-        h->d_x[1] = nb[1];
-        h->xcur = 0;
-        h->x_cap = (size_t)need;
-    }
-    const long cap = (long)h->x_cap;
-    double* xc = h->d_x[h->xcur];
-    double* xn = h->d_x[h->xcur ^ 1];
-    hipLaunchKernelGGL(stft_stage_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, d_re, d_im, n,
-                       xc + (N - 1), xc + cap + (N - 1));
-    HZ_TRY_HIP(hipGetLastError());
+    double* hc = h->d_hist[h->hcur];
+    double* hn = h->d_hist[h->hcur ^ 1];
     if (d_im) h->last_cplx = h->T + n - 1;
 
     hipEvent_t* e = nullptr;
@@ -527,15 +534,17 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
     const long f_lo = frames_before(h, h->T), f_hi = frames_before(h, h->T + n);
     const long nf = f_hi - f_lo;
     StftArgs a;
-    a.xr = xc;
-    a.xi = nullptr;
+    a.hr = hc;
+    a.hi = nullptr;
+    a.inr = d_re;
+    a.ini = d_im;
     a.fo = h->d_fo;
     a.spec = h->d_spec;
     a.win = h->d_win;
     a.tw = h->d_tw;
     a.f_lo = f_lo;
     // frames start in increasing order: the first one decides whether any reads an Im part
-    if (nf > 0 && frame_start(f_lo, h->laps, h->stride, N) <= h->last_cplx) a.xi = xc + cap;
+    if (nf > 0 && frame_start(f_lo, h->laps, h->stride, N) <= h->last_cplx) a.hi = hc + (N - 1);
     a.T0 = h->T;
     a.N = N;
     a.lg = h->lg;
@@ -583,14 +592,15 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
     o.laps = h->laps;
     o.stride = h->stride;
     o.R = h->R;
-    hipLaunchKernelGGL(stft_ola_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, o);
+    o.hist_old = hc;
+    o.in_re = d_re;
+    o.in_im = d_im;
+    o.hist_new = hn;
+    const long threads = std::max(n, (long)N - 1);
+    hipLaunchKernelGGL(stft_ola_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, o);
     HZ_TRY_HIP(hipGetLastError());
     if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
-    // history for the next block: the last N-1 samples of [T0-N+1, T0+n)
-    hipLaunchKernelGGL(copy_hist_kernel, dim3((unsigned)((N - 1 + 255) / 256)), dim3(256), 0, h->stream,
-                       (const double*)(xc + n), (long)(N - 1), cap, xn);
-    HZ_TRY_HIP(hipGetLastError());
-    h->xcur ^= 1;
+    h->hcur ^= 1;   // the overlap-add launch wrote the next block's history
     h->T += n;
     h->frames = f_hi;
     h->launches += h->prof ? 1 : 0;
@@ -646,13 +656,17 @@ int hz_stft_create(int N, int laps, int window, int proc, double p0, double p1, 
     ok = ok && hipMalloc(&h->d_win, sizeof(double) * N) == hipSuccess;
     ok = ok && hipMalloc(&h->d_tw, sizeof(double2) * (N / 2)) == hipSuccess;
     ok = ok && hipMalloc(&h->d_fo, sizeof(double2) * (size_t)h->R * N) == hipSuccess;
+    for (double*& p : h->d_hist) {
+        ok = ok && hipMalloc(&p, 2 * sizeof(double) * (N - 1)) == hipSuccess;
+        ok = ok && hipMemset(p, 0, 2 * sizeof(double) * (N - 1)) == hipSuccess;
+    }
     ok = ok && hipMemcpy(h->d_win, win.data(), sizeof(double) * N, hipMemcpyHostToDevice) == hipSuccess;
     ok = ok && hipMemcpy(h->d_tw, tw.data(), sizeof(double2) * (N / 2), hipMemcpyHostToDevice) == hipSuccess;
     ok = ok && hipMemset(h->d_fo, 0, sizeof(double2) * (size_t)h->R * N) == hipSuccess;
     if (!ok) {
         hz::set_error("hz_stft_create: device allocation failed");
         if (h->stream) (void)hipStreamDestroy(h->stream);
-        for (void* p : {(void*)h->d_win, (void*)h->d_tw, (void*)h->d_fo})
+        for (void* p : {(void*)h->d_win, (void*)h->d_tw, (void*)h->d_fo, (void*)h->d_hist[0], (void*)h->d_hist[1]})
             if (p) (void)hipFree(p);
         delete h;
         return HZ_E_ALLOC;
@@ -679,7 +693,7 @@ int hz_stft_destroy(hz_stft* h) {
     if (!h) return HZ_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (void* p : {(void*)h->d_win, (void*)h->d_tw, (void*)h->d_fo, (void*)h->d_x[0], (void*)h->d_x[1],
+    for (void* p : {(void*)h->d_win, (void*)h->d_tw, (void*)h->d_fo, (void*)h->d_hist[0], (void*)h->d_hist[1],
                     (void*)h->d_spec, (void*)h->d_in, (void*)h->d_out})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
