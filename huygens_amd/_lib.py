@@ -169,6 +169,17 @@ _SIGS = {
     "hz_dct_backward": (I, [VP]),
     "hz_dct_forward_device": (I, [VP, VP, VP, I]),
     "hz_dct_backward_device": (I, [VP, VP, VP, I]),
+    # Granulator
+    "hz_gran_create": (I, [C.c_uint, C.c_uint, I, C.POINTER(VP)]),
+    "hz_gran_destroy": (I, [VP]),
+    "hz_gran_request": (I, [VP, D, D, D, D, D, I, C.POINTER(I)]),
+    "hz_gran_process": (I, [VP, PD, PD, SZ, VP, I, C.POINTER(I)]),
+    "hz_gran_process_device": (I, [VP, VP, VP, SZ, VP, I, C.POINTER(I)]),
+    "hz_gran_activity": (I, [VP, C.POINTER(C.c_uint)]),
+    "hz_gran_set_stream": (I, [VP, VP]),
+    "hz_gran_synchronize": (I, [VP]),
+    "hz_gran_profile": (I, [VP, I]),
+    "hz_gran_profile_read": (I, [VP, PD, C.POINTER(L), C.POINTER(L)]),
 }
 
 

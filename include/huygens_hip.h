@@ -268,6 +268,38 @@ int hz_dct_backward(hz_dct* h);
 int hz_dct_forward_device(hz_dct* h, const double* d_in, double* d_out, int batch);
 int hz_dct_backward_device(hz_dct* h, const double* d_in, double* d_out, int batch);
 
+/* ---- Granulator<double> (src/granulator.h:12-127) reading a Buffer<double> source
+ * (src/buffer.h:9-86) through the FUNCTIONAL hann window (src/wave.h:148).
+ * Granulator(Wave* window = &hann, Buffer* source (size buffer_size), bool realtime,
+ * uint polyphony = 512).  The handle owns the source ring on the device.  One processed
+ * sample is the tests/granny.cpp:34-56 loop body:
+ *     source.write(in[i]); out[i] = granny(); <requests at i>; source.tick(); granny.tick();
+ * A request {at = i, ...} in hz_gran_process is made after the read of sample i (ticks 1
+ * at its first read).  hz_gran_request between calls is made after the last processed
+ * sample's read and, with ticked = 0, after its tick (ticks 0 at its first read) or, with
+ * ticked = 1, before it (the per-sample order operator(); request(); tick()).  Voice
+ * allocation is the reference's (first inactive voice; -1 when none is free or size == 0). */
+typedef struct hz_gran hz_gran;
+typedef struct {
+    long at;                                    /* sample index in the call, ascending */
+    double offset, size, speed, gain, pan;      /* granulator.h:51 (seconds, ratio, gain) */
+} hz_grain_req;
+int hz_gran_create(unsigned polyphony, unsigned buffer_size, int device, hz_gran** out);   /* 28-48 */
+int hz_gran_destroy(hz_gran* h);
+int hz_gran_request(hz_gran* h, double offset, double size, double speed, double gain, double pan, int ticked,
+                    int* voice);                                                          /* 51-79 */
+/* host pointers, synchronous; voices[k] receives request k's voice (may be NULL) */
+int hz_gran_process(hz_gran* h, const double* in, double* out, size_t n, const hz_grain_req* reqs, int nreq,
+                    int* voices);
+/* device in/out, asynchronous on the handle's stream (requests and voices stay on the host) */
+int hz_gran_process_device(hz_gran* h, const double* d_in, double* d_out, size_t n, const hz_grain_req* reqs,
+                           int nreq, int* voices);
+int hz_gran_activity(hz_gran* h, unsigned* activity);   /* active voices; idle() 106-109 is == 0 */
+int hz_gran_set_stream(hz_gran* h, void* hip_stream);
+int hz_gran_synchronize(hz_gran* h);
+int hz_gran_profile(hz_gran* h, int enable);
+int hz_gran_profile_read(hz_gran* h, double* ms, long* launches, long* grain_samples);
+
 #ifdef __cplusplus
 }
 #endif

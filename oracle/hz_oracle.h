@@ -121,6 +121,20 @@ long      orc_stft_frames(orc_stft* s);
 void      orc_dft(const double* x, double* y, int N, int sign);
 void      orc_dct(const double* x, double* y, int N, int kind);
 
+/* ---- Granulator<double> (src/granulator.h:12-127) over Buffer<double> (src/buffer.h) ---- */
+typedef struct orc_gran orc_gran;
+orc_gran* orc_gran_create(unsigned polyphony, unsigned buffer_size);
+void      orc_gran_destroy(orc_gran* g);
+int       orc_gran_request(orc_gran* g, double offset, double size, double speed, double gain, double pan);
+void      orc_gran_write(orc_gran* g, double x);
+double    orc_gran_sample(orc_gran* g);
+void      orc_gran_tick(orc_gran* g);
+unsigned  orc_gran_activity(orc_gran* g);
+/* n x { write(in[i]); out[i] = sample(); requests k with at[k] == i, in order (req: 5
+ * doubles offset, size, speed, gain, pan; voices[k] = returned voice); tick(); }  (at sorted) */
+void      orc_gran_process(orc_gran* g, const double* in, double* out, long n, const long* at, const double* req,
+                           int nreq, int* voices);
+
 /* distortion functors (tests/filterbank.cpp:158-176, src/wave.h:150) */
 double orc_dist(int id, double v, double param);
 
