@@ -153,8 +153,8 @@ def main():
     ap.add_argument("--bands-per-wave", type=int, default=0)
     ap.add_argument("--lti", default="", help="LTI engine geometry 'chunk,bands_per_wave,waves' (default engine choice)")
     ap.add_argument("--general", action="store_true", help="force the general engine (no converged fast path)")
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
-                    help="c2 = the BASELINE.json metric (default); c3/c4/c5 = the other SURVEY.md 8(d) rows")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "c6"], default="c2",
+                    help="c2 = the BASELINE.json metric (default); c3/c4/c5 = the other SURVEY.md 8(d) rows; c6 = Granulator (8(f) row 1)")
     args = ap.parse_args()
     if args.workload != "c2":
         return run_row(args)
@@ -320,7 +320,8 @@ def run_row(args):
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--workload c3/c4/c5 are single-GPU configs (SURVEY.md 8(d))")
     dev = torch.device("cuda", 0)
-    fn = {"c3": bench_rows.run_c3, "c4": bench_rows.run_c4, "c5": bench_rows.run_c5}[args.workload]
+    fn = {"c3": bench_rows.run_c3, "c4": bench_rows.run_c4, "c5": bench_rows.run_c5,
+          "c6": bench_rows.run_c6}[args.workload]
     body = fn(args, torch, dev)
     line = {"metric": body.pop("metric"), "value": body.pop("value"), "unit": body.pop("unit"), "n_gpus": 1,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": body.pop("ms_per_step"),

@@ -288,3 +288,76 @@ def run_c5(args, torch, dev):
         "streamed_kernel_ms_per_step": {"bowl": bms / args.steps, "delaybank": dms / args.steps},
         "cpu_baseline": cpu,
     }
+
+
+# --------------------------------------------------------------------------- C6
+def c6_requests(n, seed=6, every=26):
+    """Granary-like grain stream: one request every `every` samples (about what keeps 512
+    voices busy at a 275 ms mean grain), sizes U[50,500] ms, speeds U[0.5,2], offsets
+    U[0,1] s, gains U[0,1].  Requests with no free voice return -1, as in the reference."""
+    from huygens_amd import GRAIN_REQ
+    rng = np.random.default_rng(seed)
+    at = np.arange(0, n, every)
+    r = np.zeros(at.size, dtype=GRAIN_REQ)
+    r["at"] = at
+    r["offset"] = rng.uniform(0.0, 1.0, at.size)
+    r["size"] = rng.uniform(0.05, 0.5, at.size)
+    r["speed"] = rng.uniform(0.5, 2.0, at.size)
+    r["gain"] = rng.uniform(0.0, 1.0, at.size)
+    return r
+
+
+def run_c6(args, torch, dev):
+    """Granulator<double>(&hann, Buffer(3 SR), polyphony 512) over 480,000 samples per step
+    with the c6_requests grain stream (tests/granny.cpp loop body per sample)."""
+    from huygens_amd import Granulator
+    P, S = 512, args.samples
+    rng = np.random.default_rng(7)
+    x = torch.from_numpy(rng.uniform(-1.0, 1.0, S)).to(dev)
+    y = torch.empty_like(x)
+    reqs = c6_requests(S)
+    g = Granulator(3 * SR, P)
+    g.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+
+    def step():
+        g.process_device(x.data_ptr(), y.data_ptr(), S, reqs)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    g.profile(True)
+    elapsed = _timed(step, args.steps, 0, torch, dev)
+    ms, launches, gs = g.profile_read()
+    g.profile(False)
+    flops = 16.0 * gs   # per grain-sample: 16 FP64 flops + 1 cos + 1 divide (see DESIGN.md)
+    achieved = flops / (ms / 1e3) / 1e12 if ms > 0 else None
+    cpu = None
+    if not args.no_cpu_baseline:
+        _tests_path()
+        from oracle_gran import OracleGranulator
+        o = OracleGranulator(3 * SR, P)
+        n = 96000
+        rq = c6_requests(n)
+        xs = rng.uniform(-1.0, 1.0, n)
+        reqs_t = [(int(r["at"]), r["offset"], r["size"], r["speed"], r["gain"], 0.0) for r in rq]
+        t0 = time.perf_counter()
+        o.process(xs, reqs_t)
+        dt = time.perf_counter() - t0
+        cpu = {"value": n / dt, "unit": "samples/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/hz_oracle_gran.c Granulator(512), {n} samples of the same grain stream "
+                         f"(voices fill up over the sample), 1 thread, {dt:.2f} s"}
+    return {
+        "metric": "grain-samples/s, Granulator<double>(hann, Buffer(3 SR), polyphony 512)",
+        "value": gs / elapsed, "unit": "grain-samples/s",
+        "ms_per_step": 1e3 * elapsed / args.steps, "dtype": "f64",
+        "samples_per_s": S * args.steps / elapsed,
+        "data": "synthetic: uniform[-1,1) input seed 7; c6_requests grain stream seed 6 (one request / 26 samples)",
+        "config": {"workload": "C6 Granulator<double>(&hann, Buffer(3*SR), 512) (SURVEY.md 8(f) row 1)",
+                   "samples_per_step": S, "requests_per_step": int(reqs.size), "polyphony": P},
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK if achieved else None, "traffic": None,
+                     "kernel": "gran_kernel", "kernel_ms_per_step": ms / args.steps, "launches": launches,
+                     "grain_samples_per_step": gs / args.steps, "flops_per_unit": 16,
+                     "note": "16 FP64 flops + cos + divide per grain-sample; transcendental-bound"},
+        "cpu_baseline": cpu,
+    }

@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <deque>
 #include <limits>
 #include <new>
 #include <vector>
@@ -37,6 +38,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr long kChunk = 1L << 18;             // samples per launch
+constexpr long kTile = 4096;                  // samples sharing one grain list (multiple of kThreads)
 constexpr long kNever = 1L << 62;             // t_end of a grain that never finishes (NaN/inf size)
 
 struct alignas(16) GrainDev {
@@ -51,18 +53,29 @@ struct GranArgs {
     const double* in;     // block input: time T0 + j
     double* out;
     double* ring;         // time-indexed source ring (C = mask + 1 samples)
-    const GrainDev* g;
-    int ng;
+    const GrainDev* g;    // the call's grains, voice-major
+    const int* tile_off;  // per kTile samples of the call: [tile_off[k], tile_off[k+1]) in tile_idx
+    const int* tile_idx;  // grains overlapping the tile, in voice order
+    long tile_base;       // tile index of this launch's first sample
     long T0, n, mask;
     unsigned size, o0;    // Buffer size and origin at time T0
+    unsigned long fm;     // fastmod multiplier for `size`: 2^64 / size rounded up (0 for size 1)
+    unsigned wrap1;       // (2^32 - 1) % size: the second tap's slot when the first index is 0 mod 2^32
 };
 
-// x(tau) for tau <= t: the block input, the ring, or 0 before the first write
-__device__ __forceinline__ double src_at(const GranArgs& a, long tau) {
-    if (tau < 0) return 0.0;
-    if (tau >= a.T0) return a.in[tau - a.T0];
-    return a.ring[tau & a.mask];
+// x mod size for any uint32 x, without a divide (Lemire, Kaser & Kurz 2019, "fastmod")
+__device__ __forceinline__ unsigned fastmod(unsigned x, unsigned long fm, unsigned size) {
+    const unsigned long low = fm * (unsigned long)x;
+    return (unsigned)__umul64hi(low, (unsigned long)size);
 }
+
+// Address of x(tau) for tau <= t (block input or ring); tau < 0 maps to a valid ring slot
+// and is zeroed by the caller, so the loads need no branch
+__device__ __forceinline__ const double* src_ptr(const GranArgs& a, long tau) {
+    return tau >= a.T0 ? a.in + (tau - a.T0) : a.ring + (tau & a.mask);
+}
+
+constexpr int kUnroll = 4;   // grains in flight per thread: their 2 x 4 gathers issue together
 
 __global__ __launch_bounds__(kThreads) void gran_kernel(GranArgs a) {
 #pragma clang fp contract(off)
@@ -72,22 +85,42 @@ __global__ __launch_bounds__(kThreads) void gran_kernel(GranArgs a) {
     const unsigned size = a.size;
     const unsigned origin = (unsigned)(((unsigned long)a.o0 + (unsigned long)j) % size);
     double out = 0;
-    for (int e = 0; e < a.ng; ++e) {
-        const GrainDev g = a.g[e];   // wave-uniform: scalar loads
-        if (t < g.t_first || t >= g.t_end) continue;
-        const unsigned ticks = g.ticks0 + (unsigned)(t - g.t_first);
-        const double phase = (double)ticks / g.sizes;
-        const double position = g.offsets + (1 - g.speeds) * ticks;
-        // buffer.h:40-47 with its unsigned wrap
-        const int center = (int)position;
-        const int before = center + 1;
-        const double disp = position - center;
-        const unsigned s0 = (origin - (unsigned)center + size) % size;
-        const unsigned s1 = (origin - (unsigned)before + size) % size;
-        const double v0 = src_at(a, t - (long)(origin >= s0 ? origin - s0 : origin + size - s0));
-        const double v1 = src_at(a, t - (long)(origin >= s1 ? origin - s1 : origin + size - s1));
-        const double src = v0 * (1 - disp) + v1 * disp;
-        out += g.gains * src * (0.5 * (1 - cos(2 * hz::kPI * phase)));   // wave.h:148
+    const long k = a.tile_base + (long)blockIdx.x * blockDim.x / kTile;
+    const int i0 = a.tile_off[k], ng = a.tile_off[k + 1] - i0;
+    const int* idx = a.tile_idx + i0;
+    for (int e0 = 0; e0 < ng; e0 += kUnroll) {
+        bool act[kUnroll];
+        unsigned ticks[kUnroll];
+        double disp[kUnroll], v0[kUnroll], v1[kUnroll];
+        long tau0[kUnroll], tau1[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {   // phase 1: indices and gathers of kUnroll grains
+            const GrainDev g = a.g[idx[e0 + u < ng ? e0 + u : ng - 1]];   // block-uniform: scalar loads
+            act[u] = e0 + u < ng && t >= g.t_first && t < g.t_end;
+            // inactive lanes use ticks 0: their (discarded) cos stays on the short argument path
+            ticks[u] = act[u] ? g.ticks0 + (unsigned)(t - g.t_first) : 0u;
+            const double position = g.offsets + (1 - g.speeds) * ticks[u];
+            // buffer.h:40-47 with its unsigned wrap; the second tap reads center + 1
+            const int center = (int)position;
+            disp[u] = position - center;
+            const unsigned x0 = origin - (unsigned)center + size;
+            const unsigned s0 = fastmod(x0, a.fm, size);
+            // x1 = x0 - 1 (mod 2^32), so x1 % size follows from s0 unless x0 wrapped to 0
+            const unsigned s1 = x0 == 0u ? a.wrap1 : (s0 == 0u ? size - 1u : s0 - 1u);
+            tau0[u] = t - (long)(origin >= s0 ? origin - s0 : origin + size - s0);
+            tau1[u] = t - (long)(origin >= s1 ? origin - s1 : origin + size - s1);
+            v0[u] = *src_ptr(a, tau0[u]);
+            v1[u] = *src_ptr(a, tau1[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {   // phase 2: weights, in voice order
+            const GrainDev& g = a.g[idx[e0 + u < ng ? e0 + u : ng - 1]];
+            const double x0 = tau0[u] < 0 ? 0.0 : v0[u], x1 = tau1[u] < 0 ? 0.0 : v1[u];
+            const double src = x0 * (1 - disp[u]) + x1 * disp[u];
+            const double phase = (double)ticks[u] / g.sizes;
+            const double term = g.gains * src * (0.5 * (1 - cos(2 * hz::kPI * phase)));   // wave.h:148
+            if (act[u]) out += term;
+        }
     }
     a.out[j] = out;
     a.ring[t & a.mask] = a.in[j];   // no thread of this block reads this slot (C >= size + kChunk)
@@ -100,13 +133,14 @@ struct hz_gran {
     int device = 0;
     long T = 0;                       // samples processed
     std::vector<long> busy_until;     // per voice: t_end of its latest grain
-    std::vector<GrainDev> grains;     // grains that may still read (t_end > T)
-    std::vector<int> grain_voice;     // voice of each grain (sort key)
+    std::vector<long> tree;           // min-segment tree over busy_until (first free voice in O(log P))
+    unsigned leaves = 1;
+    std::vector<std::deque<GrainDev>> vg;   // per voice, its grains that may still read, in time order
     long mask = 0;
     double* d_ring = nullptr;
-    GrainDev* d_g = nullptr;
+    GrainDev* d_g = nullptr;          // the call's grains + tile lists (bytes)
     size_t g_cap = 0;
-    GrainDev* h_g = nullptr;          // pinned staging of the call's grain lists
+    GrainDev* h_g = nullptr;          // pinned staging of the same (bytes)
     size_t hg_cap = 0;
     hipEvent_t up_ev = nullptr;
     bool up_pending = false;
@@ -137,13 +171,11 @@ int gran_alloc(hz_gran* h, long t, unsigned ticks0, double offset, double size, 
     if (size == 0) return -1;
     const double lo = size * (speed - 1);
     offset = (offset < lo) ? lo : offset;   // std::max(offset, size * (speed - 1))
-    int voice = -1;
-    for (unsigned v = 0; v < h->polyphony; ++v)
-        if (h->busy_until[v] <= t + 1) {   // its last read was at or before t
-            voice = (int)v;
-            break;
-        }
-    if (voice < 0) return -1;
+    // first voice whose last read was at or before t (granulator.h:58-63's first inactive voice)
+    if (h->polyphony == 0 || h->tree[1] > t + 1) return -1;
+    unsigned node = 1;
+    while (node < h->leaves) node = h->tree[2 * node] <= t + 1 ? 2 * node : 2 * node + 1;
+    const int voice = (int)(node - h->leaves);
     GrainDev g{};
     g.offsets = hz::kSR * offset;
     g.sizes = hz::kSR * size;
@@ -158,8 +190,9 @@ int gran_alloc(hz_gran* h, long t, unsigned ticks0, double offset, double size, 
     else m = (long)std::ceil(g.sizes) - ticks0 + 1;
     g.t_end = m >= kNever - g.t_first ? kNever : g.t_first + m;
     h->busy_until[voice] = g.t_end;
-    h->grains.push_back(g);
-    h->grain_voice.push_back(voice);
+    h->tree[node] = g.t_end;
+    for (unsigned q = node >> 1; q >= 1; q >>= 1) h->tree[q] = std::min(h->tree[2 * q], h->tree[2 * q + 1]);
+    h->vg[voice].push_back(g);
     return voice;
 }
 
@@ -184,75 +217,80 @@ int gran_run(hz_gran* h, const double* d_in, double* d_out, long n, const hz_gra
             return HZ_E_INVALID;
         }
     // drop finished grains, then apply the call's requests in order (closed-form lifetimes)
-    {
-        size_t w = 0;
-        for (size_t i = 0; i < h->grains.size(); ++i)
-            if (h->grains[i].t_end > h->T) {
-                h->grains[w] = h->grains[i];
-                h->grain_voice[w++] = h->grain_voice[i];
-            }
-        h->grains.resize(w);
-        h->grain_voice.resize(w);
-    }
+    for (auto& q : h->vg)
+        while (!q.empty() && q.front().t_end <= h->T) q.pop_front();
     for (int k = 0; k < nreq; ++k) {
         const hz_grain_req& r = reqs[k];
         const int v = gran_alloc(h, h->T + r.at, 1u, r.offset, r.size, r.speed, r.gain);
         if (voices) voices[k] = v;
     }
-    // voice order (the reference's summation order); a voice's grains never overlap in time
-    std::vector<int> order(h->grains.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
-    std::sort(order.begin(), order.end(), [&](int x, int y) {
-        return h->grain_voice[x] != h->grain_voice[y] ? h->grain_voice[x] < h->grain_voice[y]
-                                                      : h->grains[x].t_first < h->grains[y].t_first;
-    });
-    // per-launch grain lists, staged in one pinned buffer and uploaded once
-    const long nchunks = (n + kChunk - 1) / kChunk;
-    std::vector<size_t> off(nchunks + 1, 0);
-    std::vector<GrainDev> all;
-    for (long c = 0; c < nchunks; ++c) {
-        const long T0 = h->T + c * kChunk, T1 = std::min(h->T + n, T0 + kChunk);
-        for (int i : order) {
-            const GrainDev& g = h->grains[i];
-            if (g.t_first < T1 && g.t_end > T0) all.push_back(g);
+    // the call's grains (voice-major) and per-tile lists in voice order (CSR), staged in
+    // one pinned buffer and uploaded once
+    const long nchunks = (n + kChunk - 1) / kChunk, ntiles = (n + kTile - 1) / kTile;
+    std::vector<GrainDev> recs;
+    std::vector<int> cnt(ntiles + 1, 0);
+    for (const auto& q : h->vg)   // voice order (the reference's summation order)
+        for (const GrainDev& g : q) {
+            if (g.t_first >= h->T + n) break;   // a voice's grains are in time order
+            if (g.t_end <= h->T) continue;
+            recs.push_back(g);
+            const long k0 = std::max(0L, (g.t_first - h->T) / kTile);
+            const long k1 = std::min(ntiles, (g.t_end - 1 - h->T) / kTile + 1);
+            for (long k = k0; k < k1; ++k) ++cnt[k + 1];
         }
-        off[c + 1] = all.size();
+    for (long k = 0; k < ntiles; ++k) cnt[k + 1] += cnt[k];
+    std::vector<int> idx(cnt[ntiles]);
+    {
+        std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+        for (size_t r = 0; r < recs.size(); ++r) {
+            const long k0 = std::max(0L, (recs[r].t_first - h->T) / kTile);
+            const long k1 = std::min(ntiles, (recs[r].t_end - 1 - h->T) / kTile + 1);
+            for (long k = k0; k < k1; ++k) idx[fill[k]++] = (int)r;
+        }
     }
+    const size_t b_rec = recs.size() * sizeof(GrainDev), b_off = cnt.size() * sizeof(int);
+    const size_t bytes = b_rec + b_off + idx.size() * sizeof(int);
     if (h->up_pending) HZ_TRY_HIP(hipEventSynchronize(h->up_ev));   // staging buffer reuse
-    if (all.size() > h->hg_cap) {
+    if (bytes > h->hg_cap) {
         if (h->h_g) HZ_TRY_HIP(hipHostFree(h->h_g));
         h->h_g = nullptr;
-        const size_t cap = std::max<size_t>(all.size(), 2 * h->hg_cap);
-        HZ_TRY_HIP(hipHostMalloc((void**)&h->h_g, cap * sizeof(GrainDev)));
+        const size_t cap = std::max<size_t>(bytes, 2 * h->hg_cap);
+        HZ_TRY_HIP(hipHostMalloc((void**)&h->h_g, cap));
         h->hg_cap = cap;
     }
-    if (all.size() > h->g_cap) {
+    if (bytes > h->g_cap) {
         HZ_TRY_HIP(hipStreamSynchronize(h->stream));
         if (h->d_g) HZ_TRY_HIP(hipFree(h->d_g));
         h->d_g = nullptr;
-        const size_t cap = std::max<size_t>(all.size(), 2 * h->g_cap);
-        HZ_TRY_HIP(hipMalloc(&h->d_g, cap * sizeof(GrainDev)));
+        const size_t cap = std::max<size_t>(bytes, 2 * h->g_cap);
+        HZ_TRY_HIP(hipMalloc((void**)&h->d_g, cap));
         h->g_cap = cap;
     }
-    if (!all.empty()) {
-        std::memcpy(h->h_g, all.data(), all.size() * sizeof(GrainDev));
-        HZ_TRY_HIP(hipMemcpyAsync(h->d_g, h->h_g, all.size() * sizeof(GrainDev), hipMemcpyHostToDevice, h->stream));
-        HZ_TRY_HIP(hipEventRecord(h->up_ev, h->stream));
-        h->up_pending = true;
-    }
+    char* hs = (char*)h->h_g;
+    std::memcpy(hs, recs.data(), b_rec);
+    std::memcpy(hs + b_rec, cnt.data(), b_off);
+    std::memcpy(hs + b_rec + b_off, idx.data(), idx.size() * sizeof(int));
+    HZ_TRY_HIP(hipMemcpyAsync(h->d_g, hs, bytes, hipMemcpyHostToDevice, h->stream));
+    HZ_TRY_HIP(hipEventRecord(h->up_ev, h->stream));
+    h->up_pending = true;
+    const char* ds = (const char*)h->d_g;
     for (long c = 0; c < nchunks; ++c) {
         const long T0 = h->T + c * kChunk, m = std::min(n - c * kChunk, kChunk);
         GranArgs a;
         a.in = d_in + c * kChunk;
         a.out = d_out + c * kChunk;
         a.ring = h->d_ring;
-        a.g = h->d_g + off[c];
-        a.ng = (int)(off[c + 1] - off[c]);
+        a.g = (const GrainDev*)ds;
+        a.tile_off = (const int*)(ds + b_rec);
+        a.tile_idx = (const int*)(ds + b_rec + b_off);
+        a.tile_base = c * kChunk / kTile;
         a.T0 = T0;
         a.n = m;
         a.mask = h->mask;
         a.size = h->size;
         a.o0 = (unsigned)(T0 % (long)h->size);
+        a.fm = h->size == 1u ? 0ul : ~0ul / h->size + 1ul;
+        a.wrap1 = 0xffffffffu % h->size;
         hipEvent_t* e = nullptr;
         if (h->prof) {
             if (h->ev_used + 2 > h->ev.size())
@@ -271,8 +309,8 @@ int gran_run(hz_gran* h, const double* d_in, double* d_out, long n, const hz_gra
         if (e) {
             HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
             ++h->launches;
-            for (size_t i = off[c]; i < off[c + 1]; ++i)   // grain-samples of this launch
-                h->grain_samples += std::min(all[i].t_end, T0 + m) - std::max(all[i].t_first, T0);
+            for (const GrainDev& g : recs)   // grain-samples of this launch
+                h->grain_samples += std::max(0L, std::min(g.t_end, T0 + m) - std::max(g.t_first, T0));
         }
     }
     h->T += n;
@@ -296,6 +334,11 @@ int hz_gran_create(unsigned polyphony, unsigned buffer_size, int device, hz_gran
     h->size = buffer_size + (buffer_size == 0 ? 1u : 0u);   // buffer.h:21 (size zero disallowed)
     h->device = device;
     h->busy_until.assign(polyphony, 0);
+    while (h->leaves < polyphony) h->leaves <<= 1;
+    h->tree.assign(2 * (size_t)h->leaves, std::numeric_limits<long>::max());   // padding leaves never free
+    for (unsigned v = 0; v < polyphony; ++v) h->tree[h->leaves + v] = 0;
+    for (unsigned q = h->leaves - 1; q >= 1; --q) h->tree[q] = std::min(h->tree[2 * q], h->tree[2 * q + 1]);
+    h->vg.resize(polyphony);
     long C = 1;
     while (C < (long)h->size + kChunk) C <<= 1;
     h->mask = C - 1;
