@@ -11,6 +11,7 @@
 #include "soundmath/delay.h"
 #include "soundmath/filterbank.h"
 #include "soundmath/fourier.h"
+#include "soundmath/granulator.h"
 #include "soundmath/oscbank.h"
 #include "soundmath/sinusoids.h"
 
@@ -153,6 +154,39 @@ int main(int argc, char** argv) {
         std::vector<double> s(1000);
         sins.fill(s.data(), 1000);
         dump("sinusoids", s);
+    }
+    {   // Granulator: tests/granny.cpp:34-56 per sample (write; granny(); request; tick), then process()
+        Buffer<double> source(3000);
+        Granulator<double> granny(&hann, &source, true, 16);
+        auto par = [](int t) {
+            return hz_grain_req{0, 0.001 * (t % 7), 0.002 + 0.0005 * (t % 11), 0.5 + 0.25 * (t % 5), 0.3, 0.0};
+        };
+        std::vector<double> y(4000);
+        std::vector<double> v;
+        for (int t = 0; t < 2000; t++) {
+            source.write(input(t));
+            y[t] = granny();
+            if (t % 97 == 0) {
+                const hz_grain_req r = par(t);
+                v.push_back((double)(int)granny.request(r.offset, r.size, r.speed, r.gain, r.pan));
+            }
+            source.tick();
+            granny.tick();
+        }
+        std::vector<hz_grain_req> reqs;
+        std::vector<double> x(2000);
+        for (int i = 0; i < 2000; i++) {
+            x[i] = input(2000 + i);
+            if ((2000 + i) % 97 == 0) {
+                reqs.push_back(par(2000 + i));
+                reqs.back().at = i;
+            }
+        }
+        std::vector<int> voices;
+        granny.process(x.data(), y.data() + 2000, 2000, reqs, &voices);
+        for (int vv : voices) v.push_back(vv);
+        dump("granulator", y);
+        dump("granulator_voices", v);
     }
     std::printf("dropin ok\n");
     return 0;

@@ -115,3 +115,14 @@ def test_additive_and_sinusoids(outputs):
     assert rel_err(outputs("additive"), o.fill(2000)) < 1e-8
     s = OracleSinusoids(220.0, 6, 0.8)
     assert rel_err(outputs("sinusoids"), s.fill(1000)) < 1e-8
+
+
+def test_granulator(outputs):
+    """Granulator<double> + Buffer<double>: per-sample write/granny()/request/tick, then process()."""
+    from oracle_gran import OracleGranulator
+    o = OracleGranulator(3000, 16)
+    reqs = [(t, 0.001 * (t % 7), 0.002 + 0.0005 * (t % 11), 0.5 + 0.25 * (t % 5), 0.3, 0.0)
+            for t in range(4000) if t % 97 == 0]
+    y, voices = o.process(x_input(4000), reqs)
+    assert rel_err(outputs("granulator"), y) < 1e-12
+    assert list(outputs("granulator_voices").astype(int)) == list(voices)
