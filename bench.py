@@ -153,6 +153,9 @@ def main():
     ap.add_argument("--bands-per-wave", type=int, default=0)
     ap.add_argument("--lti", default="", help="LTI engine geometry 'chunk,bands_per_wave,waves' (default engine choice)")
     ap.add_argument("--general", action="store_true", help="force the general engine (no converged fast path)")
+    ap.add_argument("--target-groups", type=int, default=0, help="(tuning) workgroups wanted per launch")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="(1 GPU, diagnostics) run rank 0's shard of an N-GPU job alone: per-GPU time at N")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "c6"], default="c2",
                     help="c2 = the BASELINE.json metric (default); c3/c4/c5 = the other SURVEY.md 8(d) rows; c6 = Granulator (8(f) row 1)")
     args = ap.parse_args()
@@ -173,7 +176,7 @@ def main():
 
     from huygens_amd import Filterbank
     fwd, back = c2_coefficients()
-    b0, cnt = shard_of(rank, world)
+    b0, cnt = shard_of(rank, world) if not args.emulate_world else shard_of(0, args.emulate_world)
     fb = Filterbank(2, N_BANDS, 0.1, 1.0, device=local, shard=(b0, cnt))
     for n in range(b0, b0 + cnt):
         fb.coefficients(n, fwd[n], back[n])
@@ -183,6 +186,8 @@ def main():
         fb.tune(args.waves, args.bands_per_wave)
     if args.lti:
         fb.tune_lti(*[int(v) for v in args.lti.split(",")])
+    if args.target_groups:
+        fb.set_target_groups(args.target_groups)
     if args.general:
         from huygens_amd._lib import HZ_FB_PATH_GENERAL
         fb.set_path(HZ_FB_PATH_GENERAL)
