@@ -180,6 +180,16 @@ _SIGS = {
     "hz_gran_synchronize": (I, [VP]),
     "hz_gran_profile": (I, [VP, I]),
     "hz_gran_profile_read": (I, [VP, PD, C.POINTER(L), C.POINTER(L)]),
+    # Freezer
+    "hz_frz_create": (I, [I, I, D, I, C.POINTER(VP)]),
+    "hz_frz_destroy": (I, [VP]),
+    "hz_frz_freeze": (I, [VP]),
+    "hz_frz_unfreeze": (I, [VP]),
+    "hz_frz_process": (I, [VP, PD, PD, SZ, VP, I]),
+    "hz_frz_process_device": (I, [VP, VP, VP, SZ, VP, I]),
+    "hz_frz_info": (I, [VP, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
+    "hz_frz_set_stream": (I, [VP, VP]),
+    "hz_frz_synchronize": (I, [VP]),
 }
 
 

@@ -300,6 +300,29 @@ int hz_gran_synchronize(hz_gran* h);
 int hz_gran_profile(hz_gran* h, int enable);
 int hz_gran_profile_read(hz_gran* h, double* ms, long* launches, long* grain_samples);
 
+/* ---- Freezer<N> (src/fourier.h:389-562) with FFrame / IFrame / DFrame (236-387) ----
+ * Freezer(laps, width) for N a power of two in [4, 8192].  hz_frz_process runs
+ * n x operator()(in[i]) (write; frozen ? slot sum / N : Delay(N)); an event
+ * {at, HZ_FRZ_FREEZE | HZ_FRZ_UNFREEZE} is the freeze() / unfreeze() call made before
+ * sample `at` (0 <= at <= n, ascending).  The frame choice draws std::rand() on the host,
+ * in the reference's order, so srand() seeds both alike. */
+#define HZ_FRZ_UNFREEZE 0
+#define HZ_FRZ_FREEZE 1
+typedef struct hz_frz hz_frz;
+typedef struct {
+    long at;
+    int kind;
+} hz_frz_event;
+int hz_frz_create(int N, int laps, double width, int device, hz_frz** out);   /* 395-427 */
+int hz_frz_destroy(hz_frz* h);
+int hz_frz_freeze(hz_frz* h);                                                  /* 468-479 */
+int hz_frz_unfreeze(hz_frz* h);                                                /* 481-485 */
+int hz_frz_process(hz_frz* h, const double* in, double* out, size_t n, const hz_frz_event* ev, int nev);
+int hz_frz_process_device(hz_frz* h, const double* d_in, double* d_out, size_t n, const hz_frz_event* ev, int nev);
+int hz_frz_info(hz_frz* h, int* stride, int* frames, int* frozen);
+int hz_frz_set_stream(hz_frz* h, void* hip_stream);
+int hz_frz_synchronize(hz_frz* h);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,4 +73,31 @@ private:
     handle<hz_dct, hz_dct_destroy> h_;
 };
 
+// Freezer<N> (src/fourier.h:389-562): spectral freeze.  operator()(x) is one sample
+// (a one-sample block); process() is the block form with freeze()/unfreeze() calls placed
+// before given samples.  FFrame/IFrame/DFrame are internal to the engine.
+template <int N>
+class Freezer {
+public:
+    Freezer(int laps, double width, int device = 0) {
+        hz_frz* h = nullptr;
+        detail::check(hz_frz_create(N, laps, width, device, &h), "Freezer");
+        h_ = decltype(h_)(h);
+    }
+    void freeze() { detail::check(hz_frz_freeze(h_.get()), "Freezer::freeze"); }
+    void unfreeze() { detail::check(hz_frz_unfreeze(h_.get()), "Freezer::unfreeze"); }
+    double operator()(double sample) {
+        double y = 0;
+        detail::check(hz_frz_process(h_.get(), &sample, &y, 1, nullptr, 0), "Freezer::operator()");
+        return y;
+    }
+    void process(const double* in, double* out, std::size_t n, const std::vector<hz_frz_event>& events = {}) {
+        detail::check(hz_frz_process(h_.get(), in, out, n, events.data(), (int)events.size()), "Freezer::process");
+    }
+    hz_frz* native() const { return h_.get(); }
+
+private:
+    handle<hz_frz, hz_frz_destroy> h_;
+};
+
 }  // namespace soundmath

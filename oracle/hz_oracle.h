@@ -135,6 +135,18 @@ unsigned  orc_gran_activity(orc_gran* g);
 void      orc_gran_process(orc_gran* g, const double* in, double* out, long n, const long* at, const double* req,
                            int nreq, int* voices);
 
+/* ---- Freezer<N> / FFrame / IFrame / DFrame (src/fourier.h:236-562) ---------- */
+typedef struct orc_frz orc_frz;
+orc_frz* orc_frz_create(int N, int laps, double width);
+void     orc_frz_destroy(orc_frz* z);
+int      orc_frz_geometry(orc_frz* z, int* stride, int* M);   /* returns size = M * stride */
+void     orc_frz_freeze(orc_frz* z);
+void     orc_frz_unfreeze(orc_frz* z);
+int      orc_frz_frozen(orc_frz* z);
+double   orc_frz_sample(orc_frz* z, double sample);
+/* n x { events k with at[k] == i (kind 1 freeze, 0 unfreeze), in order; out[i] = sample(in[i]) } */
+void     orc_frz_process(orc_frz* z, const double* in, double* out, long n, const long* at, const int* kind, int nev);
+
 /* distortion functors (tests/filterbank.cpp:158-176, src/wave.h:150) */
 double orc_dist(int id, double v, double param);
 

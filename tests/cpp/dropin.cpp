@@ -188,6 +188,20 @@ int main(int argc, char** argv) {
         dump("granulator", y);
         dump("granulator_voices", v);
     }
+    {   // Freezer<64>(4, 1): tests/freezer.cpp pattern (per-sample operator(), freeze/unfreeze), then process()
+        std::srand(11);
+        Freezer<64> fr(4, 1);
+        std::vector<double> y(3000);
+        for (int t = 0; t < 1000; t++) {
+            if (t == 400) fr.freeze();
+            if (t == 900) fr.unfreeze();
+            y[t] = fr(input(t));
+        }
+        std::vector<double> x(2000);
+        for (int i = 0; i < 2000; i++) x[i] = input(1000 + i);
+        fr.process(x.data(), y.data() + 1000, 2000, {{300, HZ_FRZ_FREEZE}, {1500, HZ_FRZ_UNFREEZE}});
+        dump("freezer", y);
+    }
     std::printf("dropin ok\n");
     return 0;
 }

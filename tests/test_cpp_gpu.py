@@ -126,3 +126,12 @@ def test_granulator(outputs):
     y, voices = o.process(x_input(4000), reqs)
     assert rel_err(outputs("granulator"), y) < 1e-12
     assert list(outputs("granulator_voices").astype(int)) == list(voices)
+
+
+def test_freezer(outputs):
+    """Freezer<64>(4, 1): per-sample operator() with freeze()/unfreeze(), then process()."""
+    from oracle_frz import OracleFreezer, libc_srand
+    o = OracleFreezer(64, 4, 1.0)
+    libc_srand(11)
+    y = o.process(x_input(3000), [(400, 1), (900, 0), (1300, 1), (2500, 0)])
+    assert np.max(np.abs(outputs("freezer") - y)) <= 1e-9 * np.max(np.abs(y))
