@@ -361,3 +361,50 @@ def run_c6(args, torch, dev):
                      "note": "16 FP64 flops + cos + divide per grain-sample; transcendental-bound"},
         "cpu_baseline": cpu,
     }
+
+
+# --------------------------------------------------------------------------- C7
+def run_c7(args, torch, dev):
+    """Freezer<2048>(8, 1) (tests/freezer.cpp) over 480,000 samples per step: dry for 2 s,
+    frozen for 6 s, dry again (freeze() before sample 96,000, unfreeze() before 384,000)."""
+    import ctypes
+    from huygens_amd import Freezer
+    N, laps, S = 2048, 8, args.samples
+    t = np.arange(S)
+    rng = np.random.default_rng(8)
+    x = torch.from_numpy(0.3 * np.sin(2 * np.pi * 440 * t / SR) + 0.05 * rng.standard_normal(S)).to(dev)
+    y = torch.empty_like(x)
+    ev = [(S // 5, 1), (4 * S // 5, 0)]
+    fr = Freezer(N, laps, 1.0)
+    fr.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ctypes.CDLL(None).srand(1)
+
+    def step():
+        fr.process_device(x.data_ptr(), y.data_ptr(), S, ev)
+
+    elapsed = _timed(step, args.steps, args.warmup, torch, dev)
+    cpu = None
+    if not args.no_cpu_baseline:
+        _tests_path()
+        from oracle_frz import OracleFreezer
+        o = OracleFreezer(N, laps, 1.0)
+        n = 48000
+        xs = x.cpu().numpy()[:n]
+        t0 = time.perf_counter()
+        o.process(xs, [(n // 5, 1), (4 * n // 5, 0)])
+        dt = time.perf_counter() - t0
+        cpu = {"value": n / dt, "unit": "samples/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/hz_oracle_frz.c Freezer<2048>(8, 1), {n} samples (same freeze pattern), "
+                         f"long double DFTs, 1 thread, {dt:.2f} s"}
+    achieved = 16.0 * S * args.steps / elapsed / 1e9   # GB/s: 8 B in + 8 B out per sample
+    return {
+        "metric": "samples/s, Freezer<2048>(8, 1) spectral freeze",
+        "value": S * args.steps / elapsed, "unit": "samples/s",
+        "ms_per_step": 1e3 * elapsed / args.steps, "dtype": "f64",
+        "data": "synthetic: 0.3 sin(2 pi 440 t) + 0.05 N(0,1) seed 8; freeze at 2 s, unfreeze at 8 s",
+        "config": {"workload": "C7 Freezer<2048>(laps 8, width 1) (SURVEY.md 8(f) row 2)", "samples_per_step": S},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK, "traffic": None, "kernel": "frz_out_kernel (+ host bookkeeping)",
+                     "note": "whole-step time (host run/slot-map bookkeeping included); 16 B per sample"},
+        "cpu_baseline": cpu,
+    }
