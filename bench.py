@@ -290,7 +290,7 @@ def main():
                                    "f_i=0.5(i+1)SR/4096 R=0.999, boost 1 + open, k_p=0.1 k_g=1",
                        "samples_per_step": S, "block": 1024, "bands": N_BANDS,
                        "bands_per_gpu": cnt, "parallelism": f"bands sharded x{world}, RCCL reduce"},
-            "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+            "roofline": {"bound": "mfma" if lti else "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic,
                          "traffic_detail": traffic_detail,
