@@ -239,6 +239,8 @@ def main():
     if args.stream_blocks > 0:
         B = 1024
         nb = min(args.stream_blocks, S // B)
+        for i in range(min(8, nb)):   # untimed: the short-call geometry's records are built on first use
+            fb.process_device(x.data_ptr() + 8 * B * i, y.data_ptr() + 8 * B * i, B)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()

@@ -627,6 +627,49 @@ __global__ __launch_bounds__(128) void fb_lti_reduce_kernel(const double* __rest
     if (t + 1 < n) out[t + 1] = acc[1];
 }
 
+// Short calls (a streaming block is 4 x 256 samples): the kernel above would run on a
+// handful of workgroups, each walking all G slab rows.  Here a workgroup takes 32 samples
+// and splits the G rows over 16 slices (16 x 16 threads), summing the slices in a fixed
+// order through LDS (deterministic; a different order than the long-call kernel).
+template <int O, int L>
+__global__ __launch_bounds__(256) void fb_lti_reduce_short_kernel(const double* __restrict__ partial, long n_pad,
+                                                                  int G, long n, const double* __restrict__ x,
+                                                                  const double* __restrict__ xhist,
+                                                                  const double* __restrict__ fmix,
+                                                                  double* __restrict__ out) {
+    constexpr int XW = L + O;
+    constexpr int SL = 16;   // group slices
+    __shared__ double fm[L * XW];
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    __shared__ d2 part[SL][16];
+    for (int e = threadIdx.x; e < L * XW; e += 256) fm[e] = fmix[e];
+    const int pr = threadIdx.x & 15, sl = threadIdx.x >> 4;
+    const long t = 2 * ((long)blockIdx.x * 16 + pr);
+    d2 s = {0.0, 0.0};
+    if (t < n) {
+        const double* col = partial + t;
+#pragma unroll 4
+        for (int g = sl; g < G; g += SL) s += *(const d2*)(col + (long)g * n_pad);
+    }
+    part[sl][pr] = s;
+    __syncthreads();
+    if (sl != 0 || t >= n) return;
+    d2 acc = part[0][pr];
+#pragma unroll
+    for (int q = 1; q < SL; ++q) acc += part[q][pr];
+    const int j = (int)(t % L);
+    const long base = t - j - O;
+#pragma unroll 4
+    for (int i = 0; i < XW; ++i) {
+        const long idx = base + i;
+        const double xv = idx >= 0 || !xhist ? x[idx] : xhist[-idx - 1];
+        acc[0] = fma(fm[j * XW + i], xv, acc[0]);
+        acc[1] = fma(fm[(j + 1) * XW + i], xv, acc[1]);
+    }
+    out[t] = acc[0];
+    if (t + 1 < n) out[t + 1] = acc[1];
+}
+
 // ---- kernel selection -------------------------------------------
 typedef void (*CarryKernel)(const double*, const double*, double*, int, int, long);
 typedef void (*LtiKernel)(const double*, LtiArgs);
@@ -677,6 +720,7 @@ static size_t lti_lds(int O, int geom, bool mix) {
 static CarryKernel pick_lti_carry(int O, int L) { return HZ_LTI_OL(fb_lti_seg_carry_kernel, O, L); }
 static FmixKernel pick_fmix(int O, int L) { return HZ_LTI_OL(fb_fmix_kernel, O, L); }
 static LtiReduceKernel pick_lti_reduce(int O, int L) { return HZ_LTI_OL(fb_lti_reduce_kernel, O, L); }
+static LtiReduceKernel pick_lti_reduce_short(int O, int L) { return HZ_LTI_OL(fb_lti_reduce_short_kernel, O, L); }
 #undef HZ_LTI_OL
 
 }  // namespace
@@ -745,6 +789,8 @@ int fb_prepare_lti(hz_fb* h, int gi) {
 }
 
 // the converged engine over n samples (n a positive multiple of the chunk length)
+constexpr long kShortReduce = 1L << 16;   // calls up to this length use the sliced reduce
+
 int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
     HZ_TRY(fb_prepare_lti(h, gi));
     const hz_fb::LtiRecSet& set = h->lti_set[gi];
@@ -873,9 +919,14 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             HZ_TRY_HIP(hipStreamWaitEvent(rs, ev_mix[k], 0));
         }
         if (e) HZ_TRY_HIP(hipEventRecord(e[3], rs));
-        hipLaunchKernelGGL(pick_lti_reduce(O, L), dim3((unsigned)((len + 255) / 256)), dim3(128), 0, rs,
-                           (const double*)slab_k, a.n_pad, G, len, a.x, off == 0 ? xhist_call : nullptr,
-                           (const double*)set.d_fmix, d_out + off);
+        if (len <= kShortReduce)   // streaming blocks: slices of the slab rows per workgroup
+            hipLaunchKernelGGL(pick_lti_reduce_short(O, L), dim3((unsigned)((len + 31) / 32)), dim3(256), 0, rs,
+                               (const double*)slab_k, a.n_pad, G, len, a.x, off == 0 ? xhist_call : nullptr,
+                               (const double*)set.d_fmix, d_out + off);
+        else
+            hipLaunchKernelGGL(pick_lti_reduce(O, L), dim3((unsigned)((len + 255) / 256)), dim3(128), 0, rs,
+                               (const double*)slab_k, a.n_pad, G, len, a.x, off == 0 ? xhist_call : nullptr,
+                               (const double*)set.d_fmix, d_out + off);
         HZ_TRY_HIP(hipGetLastError());
         if (e) HZ_TRY_HIP(hipEventRecord(e[4], rs));
         if (nchunks > 1) HZ_TRY_HIP(hipEventRecord(ev_red[k], rs));
