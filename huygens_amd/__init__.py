@@ -13,5 +13,6 @@ from .delay import Delay, Delaybank  # noqa: F401
 from .stft import Cosine, Fourier, StaticSTFT  # noqa: F401
 from .granulator import GRAIN_REQ, Granulator  # noqa: F401
 from .freezer import Freezer  # noqa: F401
+from .heterodyne import Heterodyne, harmbank  # noqa: F401
 
-__all__ = ["HZError", "load", "header_symbols", "Filterbank", "Oscbank", "Additive", "Sinusoids", "Bowl", "Delay", "Delaybank", "Fourier", "StaticSTFT", "Cosine", "Granulator", "GRAIN_REQ", "Freezer"]
+__all__ = ["HZError", "load", "header_symbols", "Filterbank", "Oscbank", "Additive", "Sinusoids", "Bowl", "Delay", "Delaybank", "Fourier", "StaticSTFT", "Cosine", "Granulator", "GRAIN_REQ", "Freezer", "Heterodyne", "harmbank"]

@@ -180,6 +180,20 @@ _SIGS = {
     "hz_gran_synchronize": (I, [VP]),
     "hz_gran_profile": (I, [VP, I]),
     "hz_gran_profile_read": (I, [VP, PD, C.POINTER(L), C.POINTER(L)]),
+    # heterodyne chain
+    "hz_het_create": (I, [I, I, PD, D, D, C.c_uint, I, D, D, D, I, C.POINTER(VP)]),
+    "hz_het_destroy": (I, [VP]),
+    "hz_het_setup": (I, [VP, I, PD]),
+    "hz_het_freqmod": (I, [VP, I, C.POINTER(I), PD, I]),
+    "hz_het_activate": (I, [VP, I, C.POINTER(I), I, I]),
+    "hz_het_open": (I, [VP, I, I]),
+    "hz_het_process": (I, [VP, PD, PD, SZ]),
+    "hz_het_process_device": (I, [VP, VP, VP, SZ]),
+    "hz_het_state": (I, [VP, I, PD]),
+    "hz_het_set_stream": (I, [VP, VP]),
+    "hz_het_synchronize": (I, [VP]),
+    "hz_het_profile": (I, [VP, I]),
+    "hz_het_profile_read": (I, [VP, PD, C.POINTER(L), C.POINTER(L)]),
     # Freezer
     "hz_frz_create": (I, [I, I, D, I, C.POINTER(VP)]),
     "hz_frz_destroy": (I, [VP]),

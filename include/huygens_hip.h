@@ -323,6 +323,44 @@ int hz_frz_info(hz_frz* h, int* stride, int* frames, int* frozen);
 int hz_frz_set_stream(hz_frz* h, void* hip_stream);
 int hz_frz_synchronize(hz_frz* h);
 
+/* ---- heterodyne bank chain of tests/harmbank.cpp:77-101, fused over `channels` ----
+ * Per sample x:  y = limiter(dry x + gain mixdown(demodulators(synthesis(),
+ *     smoothbank(latchbank(&rmsbank, slidebank(modulators(x, analysis())))))))
+ * then analysis / synthesis / slidebank / smoothbank / rmsbank tick, with
+ *   Oscbank analysis, synthesis   src/oscbank.h:37-68  (two banks: HZ_HET_ANALYSIS, _SYNTHESIS)
+ *   Slidebank(order, radii)       src/slidebank.h:60-175 (order <= 8; radii: 2 x channels, re/im)
+ *   RMSbank(width)                src/rmsbank.h:29-66
+ *   Latchbank(thresh, ratio)      src/latchbank.h:34-85 (the (RMSbank*, signal) form)
+ *   Stickbank(stick_order, rad)   src/stickbank.h:44-190 (stick_order <= 4)
+ *   Mixer, limiter                src/mixer.h:30-33, src/wave.h:150
+ * The oscillator banks start closed at phase 1 with frequency 1 (setOnes); freqmod /
+ * activate / open replace Oscbank::freqmod and Multichannel::activate/deactivate/open/close. */
+#define HZ_HET_ANALYSIS 0
+#define HZ_HET_SYNTHESIS 1
+/* hz_het_state: what -> layout (channel-major, doubles) */
+#define HZ_HET_STATE_ANALYSIS 0    /* [channels][2] phasors */
+#define HZ_HET_STATE_SYNTHESIS 1   /* [channels][2] */
+#define HZ_HET_STATE_SLIDE 2       /* [channels][order][2] stage outputs */
+#define HZ_HET_STATE_RMS 3         /* [channels] running sums of |s|^2 */
+#define HZ_HET_STATE_LATCH 4       /* [channels][2] armed, engaged (0 / 1) */
+#define HZ_HET_STATE_STICK 5       /* [channels][stick_order][2] outputs y[t-1-k] */
+#define HZ_HET_STATE_HISTORY 6     /* [channels][width] |s|^2, newest first */
+typedef struct hz_het hz_het;
+int hz_het_create(int channels, int order, const double* radii, double thresh, double ratio, unsigned width,
+                  int stick_order, double stick_rad, double dry, double gain, int device, hz_het** out);
+int hz_het_destroy(hz_het* h);
+int hz_het_setup(hz_het* h, int order, const double* radii);                     /* slidebank.h:63-100 */
+int hz_het_freqmod(hz_het* h, int bank, const int* index, const double* hz, int count);   /* oscbank.h:49-56 */
+int hz_het_activate(hz_het* h, int bank, const int* index, int count, int on);  /* multichannel.h */
+int hz_het_open(hz_het* h, int bank, int on);                                    /* open() / close() */
+int hz_het_process(hz_het* h, const double* in, double* out, size_t n);
+int hz_het_process_device(hz_het* h, const double* d_in, double* d_out, size_t n);
+int hz_het_state(hz_het* h, int what, double* dst);
+int hz_het_set_stream(hz_het* h, void* hip_stream);
+int hz_het_synchronize(hz_het* h);
+int hz_het_profile(hz_het* h, int enable);
+int hz_het_profile_read(hz_het* h, double* ms, long* launches, long* channel_samples);
+
 #ifdef __cplusplus
 }
 #endif

@@ -147,6 +147,20 @@ double   orc_frz_sample(orc_frz* z, double sample);
 /* n x { events k with at[k] == i (kind 1 freeze, 0 unfreeze), in order; out[i] = sample(in[i]) } */
 void     orc_frz_process(orc_frz* z, const double* in, double* out, long n, const long* at, const int* kind, int nev);
 
+/* ---- heterodyne chain (tests/harmbank.cpp:77-101): Oscbank x2, Modbank, Slidebank, RMSbank,
+ * Latchbank, Stickbank, Mixer, limiter ---- */
+typedef struct orc_het orc_het;
+orc_het* orc_het_create(int N, int order, const double* radii, double thresh, double ratio, unsigned width,
+                        int stick_order, double stick_rad, double dry, double gain);
+void     orc_het_destroy(orc_het* h);
+void     orc_het_setup(orc_het* h, int order, const double* radii);        /* Slidebank::setup */
+void     orc_het_freqmod(orc_het* h, int bank, int index, double hz);      /* bank 0 analysis, 1 synthesis */
+void     orc_het_activate(orc_het* h, int bank, const int* idx, int count, int on);
+double   orc_het_sample(orc_het* h, double x);
+void     orc_het_process(orc_het* h, const double* in, double* out, long n);
+/* state readback in the layouts of hz_het_state (include/huygens_hip.h) */
+void     orc_het_state(orc_het* h, int what, double* dst);
+
 /* distortion functors (tests/filterbank.cpp:158-176, src/wave.h:150) */
 double orc_dist(int id, double v, double param);
 
