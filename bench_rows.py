@@ -408,3 +408,118 @@ def run_c7(args, torch, dev):
                      "note": "whole-step time (host run/slot-map bookkeeping included); 16 B per sample"},
         "cpu_baseline": cpu,
     }
+
+
+# --------------------------------------------------------------------------- C8
+C8_CHANNELS = 262144
+C8_SAMPLES = 48000
+
+
+def c8_bank(N, seed=8):
+    """harmbank chain parameters (tests/harmbank.cpp: Slidebank order 4, RMSbank SR/20,
+    Latchbank(0.0005), Stickbank(1, -0.9)) over N channels with partials spread 40 Hz-8 kHz;
+    gain 3 x 96 / N keeps the mix at the 96-channel instrument's level."""
+    rng = np.random.default_rng(seed)
+    radii = np.zeros(2 * N)
+    fa = rng.uniform(40.0, 8000.0, N) * np.where(rng.random(N) < 0.5, -1.0, 1.0)
+    radii[0::2] = np.minimum(0.999, np.exp((np.log(0.5) - 4 - 1) / (25 * SR / np.abs(fa))))   # measure()
+    return fa, radii, dict(thresh=0.0005, ratio=0.2, width=SR // 20, stick_order=1, stick_rad=-0.9, dry=0.0,
+                           gain=3.0 * 96 / N)
+
+
+def run_c8(args, torch, dev):
+    """Heterodyne bank chain (tests/harmbank.cpp:77-101) fused over 262,144 channels; one step
+    = 1 s of 48 kHz audio.  The reference's own 96-channel instrument is timed beside it."""
+    from huygens_amd import Heterodyne, harmbank
+    N = C8_CHANNELS
+    S = C8_SAMPLES if args.samples == 480000 else args.samples
+    fa, radii, kw = c8_bank(N)
+    g = Heterodyne(N, 4, radii, **kw)
+    for h in (g,):
+        h.freqmod(0, np.arange(N), fa)
+        h.freqmod(1, np.arange(N), -2 * fa)
+        h.open(0)
+        h.open(1)
+    rng = np.random.default_rng(8)
+    x = torch.from_numpy(0.2 * rng.standard_normal(S)).to(dev)
+    y = torch.empty_like(x)
+    g.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+
+    def step():
+        g.process_device(x.data_ptr(), y.data_ptr(), S)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    g.profile(True)
+    elapsed = _timed(step, args.steps, 0, torch, dev)
+    ms, launches, cs = g.profile_read()
+    g.profile(False)
+    # dominant kernel het_chain_kernel<4,1,true>: algorithmic HBM bytes = the RMS ring's read +
+    # write, 16 B per channel-sample; FP64 work 108 flops + 5 divides + 1 sqrt (DESIGN.md 4.4)
+    gbs = 16.0 * cs / (ms / 1e3) / 1e9 if ms > 0 else None
+    tflops = 114.0 * cs / (ms / 1e3) / 1e12 if ms > 0 else None
+    traffic, tdetail = None, "not collected (--no-traffic)"
+    if not args.no_traffic:
+        import bench
+        tb, tdetail = bench.pmc_traffic("het_chain_kernel", extra=("--workload", "c8"))
+        traffic = tb
+    # the reference's instrument: 96 channels, 1 s of audio (latency-bound: one wave)
+    n96, fa96, fs96, r96 = harmbank()
+    h96 = Heterodyne(n96, 4, r96, 0.0005, 0.2, SR // 20, 1, -0.9, 0.0, 3.0)
+    h96.freqmod(0, np.arange(n96), fa96)
+    h96.freqmod(1, np.arange(n96), fs96)
+    h96.open(0)
+    h96.open(1)
+    h96.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    x96 = x[:min(S, SR)]
+    y96 = torch.empty_like(x96)
+    h96.process_device(x96.data_ptr(), y96.data_ptr(), x96.numel())
+    e96 = _timed(lambda: h96.process_device(x96.data_ptr(), y96.data_ptr(), x96.numel()), 3, 0, torch, dev)
+    inst = {"channels": n96, "gpu_samples_per_s": 3 * x96.numel() / e96}
+    cpu = None
+    if not args.no_cpu_baseline:
+        _tests_path()
+        from oracle_het import OracleHet
+        n = 1024
+        o = OracleHet(N, 4, radii, kw["thresh"], kw["ratio"], kw["width"], 1, -0.9, 0.0, kw["gain"])
+        o.freqmod(0, np.arange(N), fa)
+        o.freqmod(1, np.arange(N), -2 * fa)
+        o.open(0)
+        o.open(1)
+        xs = x[:n].cpu().numpy()
+        t0 = time.perf_counter()
+        o.process(xs)
+        dt = time.perf_counter() - t0
+        cpu = {"value": N * n / dt, "unit": "channel-samples/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/hz_oracle_het.c, the same {N}-channel chain over {n} samples, 1 thread, "
+                         f"{dt:.2f} s"}
+        o96 = OracleHet(n96, 4, r96, 0.0005, 0.2, SR // 20, 1, -0.9, 0.0, 3.0)
+        o96.freqmod(0, np.arange(n96), fa96)
+        o96.freqmod(1, np.arange(n96), fs96)
+        o96.open(0)
+        o96.open(1)
+        xs = x96.cpu().numpy()
+        t0 = time.perf_counter()
+        o96.process(xs)
+        inst["cpu_samples_per_s"] = xs.size / (time.perf_counter() - t0)
+    return {
+        "metric": "channel-samples/s, heterodyne bank chain (harmbank: Oscbank x2, Modbank, Slidebank(4), "
+                  "RMSbank, Latchbank, Stickbank, Mixer)",
+        "value": N * S * args.steps / elapsed, "unit": "channel-samples/s",
+        "ms_per_step": 1e3 * elapsed / args.steps, "dtype": "f64",
+        "samples_per_s": S * args.steps / elapsed,
+        "data": "synthetic: N(0, 0.2^2) input seed 8; partials uniform 40 Hz-8 kHz, random sign, seed 8",
+        "config": {"workload": "C8 heterodyne chain (tests/harmbank.cpp:77-101) over 262144 channels "
+                               "(SURVEY.md 8(f) row 3)", "channels": N, "samples_per_step": S, "order": 4,
+                   "rms_width": SR // 20},
+        "roofline": {"bound": "valu", "achieved": tflops, "peak": FP64_PEAK, "unit": "TFLOP/s",
+                     "frac": tflops / FP64_PEAK if tflops else None, "traffic": traffic,
+                     "traffic_detail": tdetail, "kernel": "het_chain_kernel<4,1,true>",
+                     "kernel_ms_per_step": ms / args.steps, "launches_per_step": launches / args.steps,
+                     "flops_per_unit": 114, "algorithmic_bytes_per_unit": 16,
+                     "hbm_achieved_gbs": gbs, "hbm_frac": gbs / HBM_PEAK if gbs else None,
+                     "note": "flops count div/sqrt as 1; each expands to ~11 VALU instructions"},
+        "instrument_96ch": inst,
+        "cpu_baseline": cpu,
+    }

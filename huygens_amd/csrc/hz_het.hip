@@ -18,10 +18,10 @@
 // registers.  Per-channel arithmetic is written without FMA contraction in the reference's
 // operation order, so every channel's state is bit-exact with the restatement
 // (oracle/hz_oracle_het.c); only the channel sum's order differs (fixed and deterministic:
-// 32-channel runs per LDS row, an xor tree of 8 runs per 256-channel group, then groups in
-// order in het_mix_kernel).
+// 16-channel runs per LDS row, an xor tree of 4 runs per 64-channel group, then 4 strided
+// slices of the groups in het_mix_kernel).
 //
-// Layout in HBM: channel state SoA [field][Np] (Np = channels rounded up to 256); the
+// Layout in HBM: channel state SoA [field][Np] (Np = channels rounded up to 64); the
 // RMSbank history ring [width + 1][Np] (slot-major, so the 64 lanes of a wave read and
 // write one contiguous 512 B row per sample); per-group partial mixes [G][chunk].
 // Algorithmic traffic per channel-sample: the ring's one read + one write (16 B).
@@ -40,14 +40,16 @@
 
 namespace {
 
-constexpr int kThreads = 256;    // channels per workgroup (one partial-mix row)
-constexpr int kCH = 32;          // samples per LDS mix round (kThreads / 8)
-constexpr int kRun = 33;         // LDS doubles per 32-channel run (+1 pad: 8 runs hit 8 banks)
-constexpr int kRow = 8 * kRun;   // LDS doubles per sample row
+constexpr int kThreads = 64;     // channels per workgroup: one wave, one partial-mix row
+constexpr int kCH = 16;          // samples per LDS mix round
+constexpr int kLanes = kThreads / kCH;   // lanes summing one sample (4)
+constexpr int kRunLen = kThreads / kLanes;   // channels per run (16)
+constexpr int kRun = kRunLen + 1;        // LDS doubles per run (+1 pad: the runs start on different banks)
+constexpr int kRow = kLanes * kRun + 1;  // LDS doubles per sample row (odd)
 constexpr int kMaxOrder = 8;
 constexpr int kMaxStick = 4;
-constexpr int kDist = 8;         // ring-load prefetch distance (samples); needs width > kDist
-constexpr long kPartBytes = 64L << 20;   // partial-mix slab cap
+constexpr int kDist = 4;         // ring-load prefetch distance (samples); needs width > kDist
+constexpr long kPartBytes = 256L << 20;   // partial-mix slab cap
 
 // SoA field indices (each Np doubles)
 enum : int {
@@ -65,49 +67,79 @@ struct HetArgs {
     const unsigned char* act;   // [2][Np] analysis, synthesis activity
     unsigned char* latch;       // [Np] bit 0 armed, bit 1 engaged
     long n, Np, pstride;
-    int N, order, sorder;
+    int N;
     unsigned W1, r0;       // ring slots; write slot of the launch's first sample
     double lo, hi;         // thresh * ratio, thresh * (1 - ratio)
     double width, sgain;   // (double)width; pow(1 + rad, stick_order)
     double back[kMaxStick];
 };
 
+// The two quotients r / nrm and m / nrm share one reciprocal.  This is the f64 divide's own
+// sequence (v_rcp + two Newton steps, q0 = n y, e = n - d q0, q = q0 + e y: what div_fmas
+// computes when div_scale leaves its operands alone) with the reciprocal computed once.
+// div_scale only rescales for exponents near the ends of the range and div_fixup only acts
+// on 0 / inf / NaN divisors; nrm = (1 + |z w|^2) / 2 lies in [1/2, 3/2] (|z| <= 1, |w| = 1),
+// so every quotient is the correctly rounded one the divide instruction sequence returns.
+__device__ __forceinline__ double rcp_newton(double d) {
+    const double y0 = __builtin_amdgcn_rcp(d);
+    const double e0 = fma(-d, y0, 1.0);
+    const double y1 = fma(y0, e0, y0);
+    const double e1 = fma(-d, y1, 1.0);
+    return fma(y1, e1, y1);
+}
+
+__device__ __forceinline__ double div_with(double n, double d, double y) {
+    const double q0 = n * y;
+    const double e = fma(-d, q0, n);
+    return fma(e, y, q0);
+}
+
 __device__ __forceinline__ void osc_tick(double& zr, double& zi, double wr, double wi) {
     // oscbank.h:61-62 (Eigen's complex packet product: re = ar br - ai bi, im = ar bi + ai br)
     const double r = zr * wr - zi * wi, m = zr * wi + zi * wr;
     const double nrm = (1.0 + (r * r + m * m)) / 2;
+#ifdef HZ_HET_PLAIN_DIV
     zr = r / nrm;
     zi = m / nrm;
+#else
+    const double y = rcp_newton(nrm);
+    zr = div_with(r, nrm, y);
+    zi = div_with(m, nrm, y);
+#endif
 }
 
-template <bool PREF>
-__global__ __launch_bounds__(kThreads) void het_chain_kernel(HetArgs a) {
+// O Slidebank stages, S Stickbank taps (compile-time: only the live state occupies VGPRs);
+// PREF: the ring read of sample t is issued kDist samples ahead (width > kDist)
+template <int O, int S, bool PREF>
+__global__ __launch_bounds__(kThreads, 24) void het_chain_kernel(HetArgs a) {
     __shared__ double buf[kCH * kRow];
     __shared__ double xs[kCH];
     const int tid = threadIdx.x;
     const long c = (long)blockIdx.x * kThreads + tid;
     const long Np = a.Np;
     double* st = a.st + c;
-    double zar = st[F_ZAR * Np], zai = st[F_ZAI * Np], war = st[F_WAR * Np], wai = st[F_WAI * Np];
+    double zar = st[F_ZAR * Np], zai = st[F_ZAI * Np];
+    const double war = st[F_WAR * Np], wai = st[F_WAI * Np];
     double zsr = st[F_ZSR * Np], zsi = st[F_ZSI * Np];
     const double wsr = st[F_WSR * Np], wsi = st[F_WSI * Np];
     const double rr = st[F_RR * Np], ri = st[F_RI * Np];
     double rsum = st[F_RSUM * Np];
-    double slr[kMaxOrder], sli[kMaxOrder], ykr[kMaxStick], yki[kMaxStick];
+    double slr[O], sli[O], ykr[S], yki[S];
 #pragma unroll
-    for (int q = 0; q < kMaxOrder; ++q) {
-        slr[q] = q < a.order ? st[(F_SLIDE + 2 * q) * Np] : 0.0;
-        sli[q] = q < a.order ? st[(F_SLIDE + 2 * q + 1) * Np] : 0.0;
+    for (int q = 0; q < O; ++q) {
+        slr[q] = st[(F_SLIDE + 2 * q) * Np];
+        sli[q] = st[(F_SLIDE + 2 * q + 1) * Np];
     }
 #pragma unroll
-    for (int k = 0; k < kMaxStick; ++k) {
-        ykr[k] = k < a.sorder ? st[(F_STICK + 2 * k) * Np] : 0.0;
-        yki[k] = k < a.sorder ? st[(F_STICK + 2 * k + 1) * Np] : 0.0;
+    for (int k = 0; k < S; ++k) {
+        ykr[k] = st[(F_STICK + 2 * k) * Np];
+        yki[k] = st[(F_STICK + 2 * k + 1) * Np];
     }
     const bool act_a = a.act[c] != 0, act_s = a.act[Np + c] != 0;
     bool armed = (a.latch[c] & 1) != 0, engaged = (a.latch[c] & 2) != 0;
     const bool live = c < a.N;
     const double cr = 1.0 - rr, ci = 0.0 - ri;   // std::complex(1, 0) - radii (slidebank.h:77)
+    const double lo = a.lo, hi = a.hi, width = a.width, sgain = a.sgain;
     double* ring = a.ring + c;
     const unsigned W1 = a.W1;
     // write slot of sample t: (r0 - t) mod W1; read slot (the sample `width` ago): one less
@@ -115,65 +147,52 @@ __global__ __launch_bounds__(kThreads) void het_chain_kernel(HetArgs a) {
     unsigned sr = sw == 0 ? W1 - 1 : sw - 1;
     double pre[kDist];
     if constexpr (PREF) {
-        unsigned s = sr;
 #pragma unroll
         for (int d = 0; d < kDist; ++d) {
-            pre[d] = d < a.n ? ring[(long)s * Np] : 0.0;
-            s = s == 0 ? W1 - 1 : s - 1;
+            pre[d] = ring[(long)sr * Np];   // slots are always in range; values past n are unused
+            sr = sr == 0 ? W1 - 1 : sr - 1;
         }
-        sr = s;   // read slot of sample kDist
     }
-    const int run = tid >> 5, lane32 = tid & 31;
-    double* brow = buf + run * kRun + lane32;   // this channel's column
+    double* bcol = buf + (tid / kRunLen) * kRun + tid % kRunLen;   // this channel's column
     for (long t0 = 0; t0 < a.n; t0 += kCH) {
         const int m = (int)min((long)kCH, a.n - t0);
         if (tid < m) xs[tid] = a.x[t0 + tid];
         __syncthreads();   // xs ready; the previous round's buf reads done
         for (int j = 0; j < m; ++j) {
-            const long t = t0 + j;
             double old;
             if constexpr (PREF) {
                 old = pre[0];
 #pragma unroll
                 for (int d = 0; d + 1 < kDist; ++d) pre[d] = pre[d + 1];
-                pre[kDist - 1] = t + kDist < a.n ? ring[(long)sr * Np] : 0.0;
-                sr = sr == 0 ? W1 - 1 : sr - 1;
+                pre[kDist - 1] = ring[(long)sr * Np];
             } else {
                 old = ring[(long)sr * Np];
-                sr = sr == 0 ? W1 - 1 : sr - 1;
             }
+            sr = sr == 0 ? W1 - 1 : sr - 1;
             const double x = xs[j];
             // modulators(x, analysis()) (modbank.h: T * complex)
             double inr = x * zar, ini = x * zai;
             // slidebank (sparse product, column order: (1 - r) in_q, then r old_q)
 #pragma unroll
-            for (int q = 0; q < kMaxOrder; ++q) {
-                if (q < a.order) {
-                    const double ar = cr * inr - ci * ini, ai = cr * ini + ci * inr;
-                    const double br = rr * slr[q] - ri * sli[q], bi = rr * sli[q] + ri * slr[q];
-                    inr = slr[q];
-                    ini = sli[q];
-                    slr[q] = ar + br;
-                    sli[q] = ai + bi;
-                }
+            for (int q = 0; q < O; ++q) {
+                const double ar = cr * inr - ci * ini, ai = cr * ini + ci * inr;
+                const double br = rr * slr[q] - ri * sli[q], bi = rr * sli[q] + ri * slr[q];
+                inr = slr[q];
+                ini = sli[q];
+                slr[q] = ar + br;
+                sli[q] = ai + bi;
             }
-            double sre = 0.0, sim = 0.0;
-#pragma unroll
-            for (int q = 0; q < kMaxOrder; ++q)
-                if (q == a.order - 1) {
-                    sre = slr[q];
-                    sim = sli[q];
-                }
+            const double sre = slr[O - 1], sim = sli[O - 1];
             // rmsbank: inputs(origin) = |s|^2; out = inputs(origin) - inputs(origin + width) + lastout
             const double a2 = sre * sre + sim * sim;
             ring[(long)sw * Np] = a2;
             sw = sw == 0 ? W1 - 1 : sw - 1;
             rsum = a2 - old + rsum;
-            const double rms = sqrt(rsum / a.width);
+            const double rms = sqrt(rsum / width);
             // latchbank(&rmsbank, signal)
-            armed = armed || rms < a.lo;
-            const bool t1 = engaged && rms < a.lo;
-            const bool t2 = !engaged && rms > a.hi && armed;
+            armed = armed || rms < lo;
+            const bool t1 = engaged && rms < lo;
+            const bool t2 = !engaged && rms > hi && armed;
             engaged = engaged && !t1;
             armed = armed && !t1;
             engaged = engaged || t2;
@@ -182,15 +201,14 @@ __global__ __launch_bounds__(kThreads) void het_chain_kernel(HetArgs a) {
             // smoothbank: y = (1 + rad)^order l - block * back (back real, as complex b + 0i)
             double accr = 0.0, acci = 0.0;
 #pragma unroll
-            for (int k = 0; k < kMaxStick; ++k)
-                if (k < a.sorder) {
-                    const double pr = ykr[k] * a.back[k] - yki[k] * 0.0, pi = ykr[k] * 0.0 + yki[k] * a.back[k];
-                    accr = accr + pr;
-                    acci = acci + pi;
-                }
-            const double yr = a.sgain * lr - accr, yi = a.sgain * li - acci;
+            for (int k = 0; k < S; ++k) {
+                const double pr = ykr[k] * a.back[k] - yki[k] * 0.0, pi = ykr[k] * 0.0 + yki[k] * a.back[k];
+                accr = accr + pr;
+                acci = acci + pi;
+            }
+            const double yr = sgain * lr - accr, yi = sgain * li - acci;
 #pragma unroll
-            for (int k = kMaxStick - 1; k > 0; --k) {
+            for (int k = S - 1; k > 0; --k) {
                 ykr[k] = ykr[k - 1];
                 yki[k] = yki[k - 1];
             }
@@ -198,23 +216,22 @@ __global__ __launch_bounds__(kThreads) void het_chain_kernel(HetArgs a) {
             yki[0] = yi;
             // demodulators(synthesis(), y); mixdown takes the real part
             const double dr = zsr * yr - zsi * yi;
-            brow[j * kRow] = live ? dr : 0.0;
+            bcol[j * kRow] = live ? dr : 0.0;
             // analysis.tick(); synthesis.tick() (active channels only)
             if (act_a) osc_tick(zar, zai, war, wai);
             if (act_s) osc_tick(zsr, zsi, wsr, wsi);
         }
         __syncthreads();   // buf complete
         {
-            const int j = tid >> 3, p = tid & 7;   // 8 lanes per sample: run p of 32 channels
+            const int j = tid / kLanes, p = tid % kLanes;   // kLanes lanes per sample: run p
             double s = 0.0;
             if (j < m) {
                 const double* row = buf + j * kRow + p * kRun;
-#pragma unroll 8
-                for (int k = 0; k < 32; ++k) s += row[k];
+#pragma unroll
+                for (int k = 0; k < kRunLen; ++k) s += row[k];
             }
-            s += __shfl_xor(s, 1);
-            s += __shfl_xor(s, 2);
-            s += __shfl_xor(s, 4);
+#pragma unroll
+            for (int w = 1; w < kLanes; w <<= 1) s += __shfl_xor(s, w);
             if (p == 0 && j < m) a.part[blockIdx.x * a.pstride + t0 + j] = s;
         }
     }
@@ -224,29 +241,74 @@ __global__ __launch_bounds__(kThreads) void het_chain_kernel(HetArgs a) {
     st[F_ZSI * Np] = zsi;
     st[F_RSUM * Np] = rsum;
 #pragma unroll
-    for (int q = 0; q < kMaxOrder; ++q)
-        if (q < a.order) {
-            st[(F_SLIDE + 2 * q) * Np] = slr[q];
-            st[(F_SLIDE + 2 * q + 1) * Np] = sli[q];
-        }
+    for (int q = 0; q < O; ++q) {
+        st[(F_SLIDE + 2 * q) * Np] = slr[q];
+        st[(F_SLIDE + 2 * q + 1) * Np] = sli[q];
+    }
 #pragma unroll
-    for (int k = 0; k < kMaxStick; ++k)
-        if (k < a.sorder) {
-            st[(F_STICK + 2 * k) * Np] = ykr[k];
-            st[(F_STICK + 2 * k + 1) * Np] = yki[k];
-        }
+    for (int k = 0; k < S; ++k) {
+        st[(F_STICK + 2 * k) * Np] = ykr[k];
+        st[(F_STICK + 2 * k + 1) * Np] = yki[k];
+    }
     a.latch[c] = (unsigned char)((armed ? 1 : 0) | (engaged ? 2 : 0));
 }
 
-// out[t] = limiter(dry x[t] + gain sum_g part[g][t]) (groups in order)
-__global__ __launch_bounds__(256) void het_mix_kernel(const double* __restrict__ x, const double* __restrict__ part,
-                                                      double* __restrict__ out, long n, long pstride, int G,
-                                                      double dry, double gain) {
-    const long t = (long)blockIdx.x * 256 + threadIdx.x;
-    if (t >= n) return;
-    double mix = 0.0;
-    for (int g = 0; g < G; ++g) mix += part[g * pstride + t];
-    out[t] = hz::dist_apply<HZ_DIST_LIMITER>(dry * x[t] + gain * mix, 0.0);
+typedef void (*chain_fn)(HetArgs);
+
+template <int O, int S>
+constexpr chain_fn chain_pick(bool pref) {
+    return pref ? het_chain_kernel<O, S, true> : het_chain_kernel<O, S, false>;
+}
+
+template <int S>
+chain_fn chain_for_order(int order, bool pref) {
+    switch (order) {
+    case 1: return chain_pick<1, S>(pref);
+    case 2: return chain_pick<2, S>(pref);
+    case 3: return chain_pick<3, S>(pref);
+    case 4: return chain_pick<4, S>(pref);
+    case 5: return chain_pick<5, S>(pref);
+    case 6: return chain_pick<6, S>(pref);
+    case 7: return chain_pick<7, S>(pref);
+    default: return chain_pick<8, S>(pref);
+    }
+}
+
+chain_fn chain_kernel(int order, int sorder, bool pref) {
+    switch (sorder) {
+    case 1: return chain_for_order<1>(order, pref);
+    case 2: return chain_for_order<2>(order, pref);
+    case 3: return chain_for_order<3>(order, pref);
+    default: return chain_for_order<4>(order, pref);
+    }
+}
+
+// out[t] = limiter(dry x[t] + gain mix[t]); mix[t] = four strided slices of the group rows
+// (g = sl mod 4, in order), added in slice order: fixed, deterministic.  64 samples x 4
+// slices per block, so a launch has n / 64 blocks and each lane streams G / 4 rows.
+constexpr int kMixSamples = 64, kMixSlices = 4;
+
+__global__ __launch_bounds__(kMixSamples* kMixSlices) void het_mix_kernel(const double* __restrict__ x,
+                                                                        const double* __restrict__ part,
+                                                                        double* __restrict__ out, long n,
+                                                                        long pstride, int G, double dry,
+                                                                        double gain) {
+    __shared__ double red[kMixSlices][kMixSamples];
+    const int s = threadIdx.x % kMixSamples, sl = threadIdx.x / kMixSamples;
+    const long t = (long)blockIdx.x * kMixSamples + s;
+    double acc = 0.0;
+    if (t < n) {
+#pragma unroll 8
+        for (int g = sl; g < G; g += kMixSlices) acc += part[g * pstride + t];
+    }
+    red[sl][s] = acc;
+    __syncthreads();
+    if (sl == 0 && t < n) {
+        double mix = red[0][s];
+#pragma unroll
+        for (int k = 1; k < kMixSlices; ++k) mix += red[k][s];
+        out[t] = hz::dist_apply<HZ_DIST_LIMITER>(dry * x[t] + gain * mix, 0.0);
+    }
 }
 
 }  // namespace
@@ -373,8 +435,6 @@ int het_run(hz_het* h, const double* d_in, double* d_out, long n) {
         a.Np = h->Np;
         a.pstride = h->chunk;
         a.N = h->N;
-        a.order = h->order;
-        a.sorder = h->sorder;
         a.W1 = h->W1;
         a.r0 = h->r;
         a.lo = h->thresh * h->ratio;
@@ -394,17 +454,16 @@ int het_run(hz_het* h, const double* d_in, double* d_out, long n) {
             h->ev_used += 2;
             HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
         }
-        if (h->width > (unsigned)kDist)
-            hipLaunchKernelGGL(het_chain_kernel<true>, dim3((unsigned)h->G), dim3(kThreads), 0, h->stream, a);
-        else
-            hipLaunchKernelGGL(het_chain_kernel<false>, dim3((unsigned)h->G), dim3(kThreads), 0, h->stream, a);
+        hipLaunchKernelGGL(chain_kernel(h->order, h->sorder, h->width > (unsigned)kDist), dim3((unsigned)h->G),
+                           dim3(kThreads), 0, h->stream, a);
         HZ_TRY_HIP(hipGetLastError());
         if (e) {
             HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
             ++h->launches;
             h->channel_samples += (long)h->N * m;
         }
-        hipLaunchKernelGGL(het_mix_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, h->stream, d_in + c0,
+        hipLaunchKernelGGL(het_mix_kernel, dim3((unsigned)((m + kMixSamples - 1) / kMixSamples)),
+                           dim3(kMixSamples * kMixSlices), 0, h->stream, d_in + c0,
                            (const double*)h->d_part, d_out + c0, m, h->chunk, (int)h->G, h->dry, h->gain);
         HZ_TRY_HIP(hipGetLastError());
         h->r = (unsigned)(((long)h->r - m % h->W1 + h->W1) % h->W1);

@@ -10,7 +10,7 @@ for w in ${ROWS:-c3 c4 c5}; do
   rc=$?; tail -2 "$OUT/bench_$w.log"; echo "rc=$rc"
   [ $rc -ne 0 ] && exit $rc
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$w" -o trace --output-format csv -- \
-      python3 bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/prof_$w.log" 2>&1
+      python3 bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline --no-traffic > "$OUT/prof_$w.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done

@@ -12,6 +12,7 @@
 #include "soundmath/filterbank.h"
 #include "soundmath/fourier.h"
 #include "soundmath/granulator.h"
+#include "soundmath/harmbank.h"
 #include "soundmath/oscbank.h"
 #include "soundmath/sinusoids.h"
 
@@ -201,6 +202,34 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 2000; i++) x[i] = input(1000 + i);
         fr.process(x.data(), y.data() + 1000, 2000, {{300, HZ_FRZ_FREEZE}, {1500, HZ_FRZ_UNFREEZE}});
         dump("freezer", y);
+    }
+    {   // tests/harmbank.cpp: 96 channels, transpose() / measure(), both banks open; per-sample, then blocks
+        const int octaves = 4, division = 12, parities = 2, n = parities * division * octaves;
+        const double frequency = mtof(24), detune = 0.125;
+        std::vector<std::complex<double>> radii(n);
+        std::vector<double> fa(n), fs(n);
+        for (int i = 0; i < division * octaves; i++)
+            for (int l = 0; l < parities; l++) {
+                const double midi = (i + detune * std::pow(2 * (0 + 0.5) / 1.0 - 1, 1)) / division;
+                const double partial = frequency * std::pow(2, midi) * 1 * std::pow(-1, l);
+                const int idx = parities * i + l;
+                fa[idx] = partial;
+                fs[idx] = -1 * partial * std::pow(2, (double)division / division);
+                radii[idx] = std::min(0.999, std::exp((std::log(0.5) - 4 - 1) / (25 * SR / std::abs(partial))));
+            }
+        Heterodyne<96> het(4, radii);
+        for (int i = 0; i < n; i++) {
+            het.analysis().freqmod(i, fa[i]);
+            het.synthesis().freqmod(i, fs[i]);
+        }
+        het.analysis().open();
+        het.synthesis().open();
+        std::vector<double> y(4000);
+        for (int t = 0; t < 500; t++) y[t] = het(0.3 * input(t));
+        std::vector<double> x(3500);
+        for (int i = 0; i < 3500; i++) x[i] = 0.3 * input(500 + i);
+        het.process(x.data(), y.data() + 500, 3500);
+        dump("heterodyne", y);
     }
     std::printf("dropin ok\n");
     return 0;

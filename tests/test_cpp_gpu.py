@@ -135,3 +135,18 @@ def test_freezer(outputs):
     libc_srand(11)
     y = o.process(x_input(3000), [(400, 1), (900, 0), (1300, 1), (2500, 0)])
     assert np.max(np.abs(outputs("freezer") - y)) <= 1e-9 * np.max(np.abs(y))
+
+
+def test_heterodyne(outputs):
+    """Heterodyne<96> (tests/harmbank.cpp instrument): per-sample operator(), then process()."""
+    from huygens_amd import harmbank
+    from oracle_het import OracleHet
+    n, fa, fs, radii = harmbank()
+    o = OracleHet(n, 4, radii, 0.0005, 0.2, 2400, 1, -0.9, 0.0, 3.0)
+    o.freqmod(0, np.arange(n), fa)
+    o.freqmod(1, np.arange(n), fs)
+    o.open(0)
+    o.open(1)
+    y = o.process(0.3 * x_input(4000))
+    assert np.max(np.abs(y)) > 1e-3
+    assert np.max(np.abs(outputs("heterodyne") - y)) <= 1e-12
