@@ -69,6 +69,8 @@ _SIGS = {
     "hz_fb_set_distortion": (I, [VP, I, D]),
     "hz_fb_process": (I, [VP, PD, PD, SZ]),
     "hz_fb_process_device": (I, [VP, VP, VP, SZ]),
+    "hz_fb_process_tv": (I, [VP, PD, PD, SZ, I, PD, D]),
+    "hz_fb_process_tv_device": (I, [VP, VP, VP, SZ, I, VP, D]),
     "hz_fb_set_stream": (I, [VP, VP]),
     "hz_fb_get_stream": (I, [VP, C.POINTER(VP)]),
     "hz_fb_synchronize": (I, [VP]),

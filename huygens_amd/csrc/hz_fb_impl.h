@@ -116,6 +116,7 @@ int fb_prof_events(hz_fb* h, hipEvent_t** e);
 void fb_mirror_advance(hz_fb* h, long len);  // O(1): the closed form is applied lazily
 void fb_mirror_sync(hz_fb* h);               // bring pg_host up to date (before a setter)
 int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n);
+int fb_upload_staged(hz_fb* h);              // staged setters -> device
 // hz_fb_lti.hip
 int fb_lti_geom(const hz_fb* h, long n);  // LTI geometry for a call of n samples
 int fb_lti_chunk(int geom);                // samples per lane chunk of a geometry

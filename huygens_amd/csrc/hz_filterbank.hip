@@ -708,6 +708,9 @@ int fb_set_lds_attr(const void* k) {
     return HZ_OK;
 }
 
+// staged setters -> device (the per-sample coefficient path, hz_fb_tv.hip, reads pin / gin)
+int fb_upload_staged(hz_fb* h) { return fb_upload(h); }
+
 // host mirror of the closed-form smoother end state written by every launch
 // (pgstate_next = pin + sp^n (pre - pin), likewise for the gains)
 void fb_mirror_advance(hz_fb* h, long len) { h->mirror_pending += len; }

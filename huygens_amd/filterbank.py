@@ -15,6 +15,9 @@ import numpy as np
 from ._lib import HZ_DIST_NONE, check, dptr, load
 
 
+TV_COEFFS, TV_RESONANT = 0, 1   # HZ_FB_TV_*
+
+
 class Filterbank:
     """Filterbank(order, N=1, k_p=0.1, k_g=1) -- src/filterbank.h:36-70.
 
@@ -94,6 +97,21 @@ class Filterbank:
     def process_device(self, x_ptr: int, out_ptr: int, n: int):
         """Device pointers, asynchronous on the handle's stream."""
         check(self._lib.hz_fb_process_device(self._h, C.c_void_p(x_ptr), C.c_void_p(out_ptr), n))
+
+    def process_tv(self, x, kind: int, stream, param: float = 0.0) -> np.ndarray:
+        """Per-sample coefficient streams (hz_fb_process_tv): kind TV_COEFFS with stream
+        [n][2*order+1][N] (forward then back, band-minor) or TV_RESONANT with stream [n][N]
+        frequencies in Hz (order 2; Subtractive's resonant filters, R = param)."""
+        xi = np.ascontiguousarray(x, dtype=np.float64)
+        st = np.ascontiguousarray(stream, dtype=np.float64)
+        out = np.empty_like(xi)
+        check(self._lib.hz_fb_process_tv(self._h, dptr(xi), dptr(out), len(xi), kind, dptr(st), float(param)))
+        self._computed = False
+        return out
+
+    def process_tv_device(self, x_ptr: int, out_ptr: int, n: int, kind: int, stream_ptr: int, param: float = 0.0):
+        check(self._lib.hz_fb_process_tv_device(self._h, C.c_void_p(x_ptr), C.c_void_p(out_ptr), n, kind,
+                                                C.c_void_p(stream_ptr), float(param)))
 
     def __call__(self, sample: float) -> float:
         """T operator()(T) (filterbank.h:125-131): cached until tick()."""

@@ -323,6 +323,24 @@ int hz_frz_info(hz_frz* h, int* stride, int* frames, int* frozen);
 int hz_frz_set_stream(hz_frz* h, void* hip_stream);
 int hz_frz_synchronize(hz_frz* h);
 
+/* ---- Filterbank with per-sample coefficient streams ----
+ * Subtractive ALLINONE / ONEPERVOICE (src/subtractive.h:215-228, 300-317) retune every band
+ * between samples.  hz_fb_process_tv runs n samples with row t of `stream` holding the
+ * coefficients in effect at sample t (the staged coefficients are ignored; afterwards the
+ * stream's last row is the staged set, as after the reference's last coefficients() call):
+ *   HZ_FB_TV_COEFFS    stream [n][2*order+1][N]: forward (order+1) then back (order), band-minor
+ *   HZ_FB_TV_RESONANT  stream [n][N] frequencies in Hz, order 2 only: {g, 0, -g},
+ *                      {-2 R cos(2 PI f / SR), R^2}, g = resonant(f, R) (subtractive.h:240-249),
+ *                      R = param.
+ * Smoothers (boost / mix targets), distortion and state are the handle's, shared with
+ * hz_fb_process.  _device takes device pointers (asynchronous on the handle's stream). */
+#define HZ_FB_TV_COEFFS 0
+#define HZ_FB_TV_RESONANT 1
+int hz_fb_process_tv(hz_fb* h, const double* in, double* out, size_t n, int kind, const double* stream,
+                     double param);
+int hz_fb_process_tv_device(hz_fb* h, const double* d_in, double* d_out, size_t n, int kind,
+                            const double* d_stream, double param);
+
 /* ---- heterodyne bank chain of tests/harmbank.cpp:77-101, fused over `channels` ----
  * Per sample x:  y = limiter(dry x + gain mixdown(demodulators(synthesis(),
  *     smoothbank(latchbank(&rmsbank, slidebank(modulators(x, analysis())))))))

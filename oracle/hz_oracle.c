@@ -291,3 +291,69 @@ void orc_osc_fill(orc_osc* o, double* mix, double* per_band, long n)
         orc_osc_tick(o);
     }
 }
+
+/* ---- per-sample coefficient streams ----------------
+ * Subtractive ALLINONE / ONEPERVOICE (src/subtractive.h:215-228, 300-317) set every band's
+ * coefficients in tick(), i.e. between samples.  Row t of the stream holds the coefficients
+ * in effect at sample t:
+ *   kind 0: stream[t][k][n], k < O+1 forward then k < O back (band-minor rows);
+ *   kind 1: stream[t][n] = frequency (Hz), order 2: {g, 0, -g}, {-2 R cos(2 PI f / SR), R^2},
+ *           g = resonant(f, R) (subtractive.h:240-249), R = param.
+ * resonant(): maximum = 1/(Q-1) - 1/(Q - cos2 - i sin2); 1 / sqrt(|maximum|), with the
+ * complex quotient by Smith's algorithm as libgcc's __divdc3 (g++ on Linux) and |.| = hypot. */
+static void orc_cdiv(double a, double b, double c, double d, double* x, double* y)
+{
+    if (fabs(c) < fabs(d)) {
+        const double ratio = c / d, denom = (c * ratio) + d;
+        *x = ((a * ratio) + b) / denom;
+        *y = ((b * ratio) - a) / denom;
+    } else {
+        const double ratio = d / c, denom = (d * ratio) + c;
+        *x = ((b * ratio) + a) / denom;
+        *y = (b - (a * ratio)) / denom;
+    }
+}
+
+double orc_resonant(double frequency, double Q)
+{
+    const double c2 = cos(4 * ORC_PI * frequency / ORC_SR), s2 = sin(4 * ORC_PI * frequency / ORC_SR);
+    /* Q - cosine2 - 1.0i * sine2: (Q - c2, -0) - (0 * s2 - 1 * 0, 0 * 0 + 1 * s2) */
+    const double ir = 0.0 * s2 - 1.0 * 0.0, ii = 0.0 * 0.0 + 1.0 * s2;
+    const double dr = (Q - c2) - ir, di = -0.0 - ii;
+    double qr, qi;
+    orc_cdiv(1.0, 0.0, dr, di, &qr, &qi);
+    const double mr = 1.0 / (Q - 1) - qr, mi = 0.0 - qi;
+    return 1 / sqrt(hypot(mr, mi));
+}
+
+void orc_fb_resonant_coefficients(double frequency, double R, double* fwd, double* back)
+{
+    const double cosine = cos(2 * ORC_PI * frequency / ORC_SR);
+    const double gain = orc_resonant(frequency, R);
+    fwd[0] = gain;
+    fwd[1] = 0;
+    fwd[2] = -gain;
+    back[0] = -2 * R * cosine;
+    back[1] = R * R;
+}
+
+void orc_fb_process_tv(orc_fb* fb, const double* in, double* out, long n, int kind, const double* stream,
+                       double param, int dist_id, double dist_param)
+{
+    const int O = fb->order, N = fb->N;
+    for (long t = 0; t < n; t++) {
+        for (int b = 0; b < N; b++) {
+            double f[5], bk[4];
+            if (kind == 0) {
+                const double* row = stream + (size_t)t * (2 * O + 1) * N;
+                for (int k = 0; k <= O; k++) f[k] = row[(size_t)k * N + b];
+                for (int k = 0; k < O; k++) bk[k] = row[(size_t)(O + 1 + k) * N + b];
+            } else {
+                orc_fb_resonant_coefficients(stream[(size_t)t * N + b], param, f, bk);
+            }
+            orc_fb_coefficients(fb, b, f, O + 1, bk, O);
+        }
+        out[t] = orc_fb_sample(fb, in[t], dist_id, dist_param);
+        orc_fb_tick(fb);
+    }
+}

@@ -42,6 +42,12 @@ void    orc_fb_open(orc_fb* fb);
 double  orc_fb_sample(orc_fb* fb, double x, int dist_id, double dist_param);
 void    orc_fb_tick(orc_fb* fb);
 void    orc_fb_process(orc_fb* fb, const double* in, double* out, long n, int dist_id, double dist_param);
+/* per-sample coefficient streams (kind 0: [n][2O+1][N] coefficients; kind 1: [n][N] resonant
+ * frequencies, order 2, R = param); see hz_oracle.c */
+void    orc_fb_process_tv(orc_fb* fb, const double* in, double* out, long n, int kind, const double* stream,
+                          double param, int dist_id, double dist_param);
+double  orc_resonant(double frequency, double Q);
+void    orc_fb_resonant_coefficients(double frequency, double R, double* fwd, double* back);
 
 /* ---- Oscbank<double,N> (src/oscbank.h:15-97, src/multichannel.h:16-159) */
 typedef struct orc_osc orc_osc;

@@ -31,6 +31,9 @@ _SIGS = {
     "orc_fb_sample": (D, [VP, D, I, D]),
     "orc_fb_tick": (None, [VP]),
     "orc_fb_process": (None, [VP, PD, PD, L, I, D]),
+    "orc_fb_process_tv": (None, [VP, PD, PD, L, I, PD, D, I, D]),
+    "orc_resonant": (D, [D, D]),
+    "orc_fb_resonant_coefficients": (None, [D, D, PD, PD]),
 }
 
 _lib = None
@@ -98,6 +101,13 @@ class OracleFilterbank:
         xi = np.ascontiguousarray(x, dtype=np.float64)
         out = np.empty_like(xi)
         self.l.orc_fb_process(self.h, _p(xi), _p(out), len(xi), self.dist[0], self.dist[1])
+        return out
+
+    def process_tv(self, x, kind, stream, param=0.0):
+        xi = np.ascontiguousarray(x, dtype=np.float64)
+        st = np.ascontiguousarray(stream, dtype=np.float64)
+        out = np.empty_like(xi)
+        self.l.orc_fb_process_tv(self.h, _p(xi), _p(out), len(xi), kind, _p(st), param, self.dist[0], self.dist[1])
         return out
 
 
