@@ -156,8 +156,8 @@ def main():
     ap.add_argument("--target-groups", type=int, default=0, help="(tuning) workgroups wanted per launch")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="(1 GPU, diagnostics) run rank 0's shard of an N-GPU job alone: per-GPU time at N")
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "c6", "c7", "c8"], default="c2",
-                    help="c2 = the BASELINE.json metric (default); c3/c4/c5 = the other SURVEY.md 8(d) rows; c6 = Granulator, c7 = Freezer, c8 = heterodyne chain (8(f) rows 1-3)")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "c6", "c7", "c8", "c9"], default="c2",
+                    help="c2 = the BASELINE.json metric (default); c3/c4/c5 = the other SURVEY.md 8(d) rows; c6 = Granulator, c7 = Freezer, c8 = heterodyne chain, c9 = per-sample coefficient streams (8(f) rows 1-4)")
     args = ap.parse_args()
     if args.workload != "c2":
         return run_row(args)
@@ -328,7 +328,8 @@ def run_row(args):
         raise SystemExit("--workload c3/c4/c5 are single-GPU configs (SURVEY.md 8(d))")
     dev = torch.device("cuda", 0)
     fn = {"c3": bench_rows.run_c3, "c4": bench_rows.run_c4, "c5": bench_rows.run_c5,
-          "c6": bench_rows.run_c6, "c7": bench_rows.run_c7, "c8": bench_rows.run_c8}[args.workload]
+          "c6": bench_rows.run_c6, "c7": bench_rows.run_c7, "c8": bench_rows.run_c8,
+          "c9": bench_rows.run_c9}[args.workload]
     body = fn(args, torch, dev)
     line = {"metric": body.pop("metric"), "value": body.pop("value"), "unit": body.pop("unit"), "n_gpus": 1,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": body.pop("ms_per_step"),

@@ -523,3 +523,122 @@ def run_c8(args, torch, dev):
         "instrument_96ch": inst,
         "cpu_baseline": cpu,
     }
+
+
+# --------------------------------------------------------------------------- C9
+C9_BANDS = 16384
+C9_SAMPLES = 48000
+
+
+def run_c9(args, torch, dev):
+    """Filterbank(2, N) with per-sample resonant-frequency streams (Subtractive ALLINONE,
+    src/subtractive.h:215-228): every band retuned every sample; one step = 1 s of audio.
+    The reference's instrument size (7 voices x 7 overtones = 49 bands) is timed beside it, and
+    the raw-coefficient stream kind (40 B per band-sample) on a shorter step."""
+    from huygens_amd import Filterbank
+    from huygens_amd.filterbank import TV_COEFFS, TV_RESONANT
+    N = C9_BANDS
+    S = C9_SAMPLES if args.samples == 480000 else args.samples
+    R = 0.99999
+    rng = np.random.default_rng(9)
+    base = torch.from_numpy(rng.uniform(60.0, 3000.0, N)).to(dev)
+    phase = torch.from_numpy(rng.uniform(0.0, 1.0, N)).to(dev)
+    t = torch.arange(S, device=dev, dtype=torch.float64)[:, None]
+    freqs = (base[None, :] * (1 + 0.05 * torch.sin(2 * np.pi * (t / 4800.0 + phase[None, :])))).contiguous()
+    del t
+    x = torch.from_numpy(rng.uniform(-1.0, 1.0, S)).to(dev)
+    y = torch.empty_like(x)
+    g = Filterbank(2, N, 0.1, 1.0)
+    g.boost([0.7 ** (i % 7) for i in range(N)])   # boost(i * overtones + j, decay^j)
+    g.open()
+    g.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+
+    def step():
+        g.process_tv_device(x.data_ptr(), y.data_ptr(), S, TV_RESONANT, freqs.data_ptr(), R)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    g.profile(True)
+    elapsed = _timed(step, args.steps, 0, torch, dev)
+    seg_ms, mix_ms, red_ms, launches = g.profile_read()
+    g.profile(False)
+    bs = N * S * args.steps
+    tflops = 49.0 * bs / (mix_ms / 1e3) / 1e12 if mix_ms > 0 else None
+    gbs = 8.0 * bs / (mix_ms / 1e3) / 1e9 if mix_ms > 0 else None
+    traffic, tdetail = None, "not collected (--no-traffic)"
+    if not args.no_traffic:
+        import bench
+        traffic, tdetail = bench.pmc_traffic("fb_tv_kernel", extra=("--workload", "c9"))
+    # raw coefficient streams: [n][5][N] (40 B per band-sample), 4800 samples
+    n2 = min(S, 4800)
+    st = torch.zeros((n2, 5, N), dtype=torch.float64, device=dev)
+    st[:, 0, :] = 1 - R
+    st[:, 2, :] = -(1 - R)
+    st[:, 3, :] = -2 * R * torch.cos(2 * np.pi * freqs[:n2] / SR)
+    st[:, 4, :] = R * R
+    g.process_tv_device(x.data_ptr(), y.data_ptr(), n2, TV_COEFFS, st.data_ptr(), 0.0)
+    g.profile(True)
+    e2 = _timed(lambda: g.process_tv_device(x.data_ptr(), y.data_ptr(), n2, TV_COEFFS, st.data_ptr(), 0.0), 3, 0,
+                torch, dev)
+    _, m2, _, _ = g.profile_read()
+    g.profile(False)
+    coeffs = {"band_samples_per_s": 3 * N * n2 / e2, "kernel_ms": m2 / 3,
+              "hbm_achieved_gbs": 40.0 * N * n2 / (m2 / 3 / 1e3) / 1e9 if m2 > 0 else None,
+              "algorithmic_bytes_per_unit": 40}
+    del st
+    # the reference's instrument: Subtractive(7, 7, ...) = 49 bands, 1 s of audio
+    g49 = Filterbank(2, 49, 0.1, 1.0)
+    g49.boost([0.7 ** (i % 7) for i in range(49)])
+    g49.open()
+    g49.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    f49 = freqs[:, :49].contiguous()
+    g49.process_tv_device(x.data_ptr(), y.data_ptr(), S, TV_RESONANT, f49.data_ptr(), R)
+    e49 = _timed(lambda: g49.process_tv_device(x.data_ptr(), y.data_ptr(), S, TV_RESONANT, f49.data_ptr(), R), 3, 0,
+                 torch, dev)
+    inst = {"bands": 49, "gpu_samples_per_s": 3 * S / e49}
+    cpu = None
+    if not args.no_cpu_baseline:
+        _tests_path()
+        from oracle import OracleFilterbank
+        n = 960
+        o = OracleFilterbank(2, N, 0.1, 1.0)
+        o.boost([0.7 ** (i % 7) for i in range(N)])
+        o.open()
+        xs, fs = x[:n].cpu().numpy(), freqs[:n].cpu().numpy()
+        t0 = time.perf_counter()
+        o.process_tv(xs, TV_RESONANT, fs, R)
+        dt = time.perf_counter() - t0
+        cpu = {"value": N * n / dt, "unit": "band-samples/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/hz_oracle.c orc_fb_process_tv, the same {N}-band resonant streams over {n} "
+                         f"samples, 1 thread, {dt:.2f} s"}
+        o49 = OracleFilterbank(2, 49, 0.1, 1.0)
+        o49.boost([0.7 ** (i % 7) for i in range(49)])
+        o49.open()
+        m = min(S, 24000)
+        f49h = f49[:m].cpu().numpy()
+        t0 = time.perf_counter()
+        o49.process_tv(x[:m].cpu().numpy(), TV_RESONANT, f49h, R)
+        inst["cpu_samples_per_s"] = m / (time.perf_counter() - t0)
+    return {
+        "metric": "band-samples/s, Filterbank(2, N) retuned every sample (resonant-frequency streams, "
+                  "Subtractive ALLINONE)",
+        "value": bs / elapsed, "unit": "band-samples/s",
+        "ms_per_step": 1e3 * elapsed / args.steps, "dtype": "f64",
+        "samples_per_s": S * args.steps / elapsed,
+        "data": "synthetic: uniform[-1,1) input seed 9; per-band frequency tracks base uniform 60-3000 Hz, "
+                "5 % vibrato at 10 Hz, generated on the device",
+        "config": {"workload": "C9 per-sample coefficient streams (SURVEY.md 8(f) row 4)", "bands": N,
+                   "samples_per_step": S, "order": 2, "R": R, "kind": "HZ_FB_TV_RESONANT"},
+        "roofline": {"bound": "valu", "achieved": tflops, "peak": FP64_PEAK, "unit": "TFLOP/s",
+                     "frac": tflops / FP64_PEAK if tflops else None, "traffic": traffic,
+                     "traffic_detail": tdetail, "kernel": "fb_tv_kernel<2, RESONANT, NONE>",
+                     "kernel_ms_per_step": mix_ms / args.steps, "mix_reduce_ms_per_step": red_ms / args.steps,
+                     "launches_per_step": launches / args.steps, "flops_per_unit": 49,
+                     "algorithmic_bytes_per_unit": 8, "hbm_achieved_gbs": gbs,
+                     "note": "one wave per 64 bands, sequential in time: 256 waves for 16384 bands; "
+                             "cos, sincos, 4 divides, hypot, sqrt counted as 1 flop each"},
+        "variant_coeff_stream": coeffs,
+        "instrument_49_bands": inst,
+        "cpu_baseline": cpu,
+    }

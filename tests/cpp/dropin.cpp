@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "soundmath/additive.h"
+#include "soundmath/audio.h"
 #include "soundmath/bowl.h"
 #include "soundmath/delay.h"
 #include "soundmath/filterbank.h"
@@ -31,6 +32,14 @@ static double input(int t) { return std::sin(0.01 * t) + 0.5 * (((t * 7919) % 13
 
 static int hilbert64(const std::complex<double>* in, std::complex<double>* out) {
     for (int i = 0; i < 64; i++) out[i] = i < 32 ? in[i] : 0.0;
+    return 0;
+}
+
+// tests/harmbank.cpp's process() callback shape: BSIZE frames of mono float in, float out
+#define BSIZE 32
+static Heterodyne<96>* g_het = nullptr;
+static int het_process(const float* in, float* out) {
+    g_het->process(in, out, BSIZE);
     return 0;
 }
 
@@ -230,6 +239,24 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 3500; i++) x[i] = 0.3 * input(500 + i);
         het.process(x.data(), y.data() + 500, 3500);
         dump("heterodyne", y);
+
+        // the same instrument behind the offline Audio engine (src/audio.h stand-in): a
+        // fresh chain, a 1000-frame float WAV in, float WAV out
+        Heterodyne<96> het2(4, radii);
+        for (int i = 0; i < n; i++) {
+            het2.analysis().freqmod(i, fa[i]);
+            het2.synthesis().freqmod(i, fs[i]);
+        }
+        het2.analysis().open();
+        het2.synthesis().open();
+        std::vector<float> xin(1000);
+        for (int t = 0; t < 1000; t++) xin[t] = (float)(0.3 * input(t));
+        wav::write(dir + "/audio_in.wav", xin.data(), xin.size(), 1, SR);
+        g_het = &het2;
+        Audio A(het_process, BSIZE);
+        Audio::offline(dir + "/audio_in.wav", dir + "/audio_out.wav");
+        A.startup(1, 1, false);
+        A.shutdown();
     }
     std::printf("dropin ok\n");
     return 0;

@@ -27,7 +27,7 @@ def test_dropin_headers_build():
 
 
 @pytest.mark.parametrize("hdr", ["filterbank.h", "oscbank.h", "additive.h", "sinusoids.h", "bowl.h", "delay.h",
-                                 "delaybank.h", "fourier.h", "staticSTFT.h", "granulator.h", "harmbank.h"])
+                                 "delaybank.h", "fourier.h", "staticSTFT.h", "granulator.h", "harmbank.h", "audio.h"])
 def test_each_header_standalone(hdr, tmp_path):
     src = tmp_path / "one.cpp"
     src.write_text(f'#include "soundmath/{hdr}"\nint main() {{ return 0; }}\n')

@@ -34,6 +34,7 @@ def outputs(tmp_path_factory):
 
     def load(name, dtype=np.float64):
         return np.fromfile(os.path.join(d, name + ".bin"), dtype=dtype)
+    load.dir = str(d)
     return load
 
 
@@ -150,3 +151,22 @@ def test_heterodyne(outputs):
     y = o.process(0.3 * x_input(4000))
     assert np.max(np.abs(y)) > 1e-3
     assert np.max(np.abs(outputs("heterodyne") - y)) <= 1e-12
+
+
+def test_offline_audio_engine(outputs):
+    """Heterodyne<96> as the process() callback of the offline Audio engine (src/audio.h
+    stand-in): float32 WAV in -> float32 WAV out equals the restatement on the same floats."""
+    from huygens_amd import harmbank
+    from oracle_het import OracleHet
+    from test_audio_cpu import read_f32
+    y, rate = read_f32(os.path.join(outputs.dir, "audio_out.wav"))
+    n, fa, fs, radii = harmbank()
+    o = OracleHet(n, 4, radii, 0.0005, 0.2, 2400, 1, -0.9, 0.0, 3.0)
+    o.freqmod(0, np.arange(n), fa)
+    o.freqmod(1, np.arange(n), fs)
+    o.open(0)
+    o.open(1)
+    x = (0.3 * x_input(1000)).astype(np.float32).astype(np.float64)
+    want = o.process(x).astype(np.float32)
+    assert rate == 48000 and y.shape == (1000, 1)
+    assert np.max(np.abs(y[:, 0] - want)) <= 1e-6
