@@ -12,9 +12,10 @@
 // Bowl<float>, form = a Wave<float> lambda sin(2 PI p) (double in, float out): the
 // reference rounds p = f n / SR and x = -d n / SR in float, which moves the phase by up to
 // ulp(p)/2 (0.008 cycles at n ~ 5e5) -- that rounding is part of its output, so the float
-// model is evaluated per mode-sample: float mul + correctly rounded float divide, then
-// sin(2 PI p) in double with p split exactly as k + r (k = floor p) so the argument stays
-// in [0, 2 PI): sin(2 PI r + 2 k (PI - pi)), rounded to float; the decay E^x uses a
+// model is evaluated per mode-sample: float mul + correctly rounded float divide (FMA
+// residual form, div_sr), then sin(2 PI p) in double with p split exactly as k + r
+// (k = floor p), r folded to a quarter period and a Taylor polynomial (sin2pi_ref), rounded
+// to float -- no library sin or IEEE divide sequence in the loop; the decay E^x uses a
 // per-chunk exp seed and a per-sample factor (x's float rounding changes the term by
 // < 2.5e-8 a_i).  The sum is kept in double (the reference rounds it to float after every
 // mode; that accumulation differs by ~1e-7 relative, see tests).  The float counter
@@ -62,6 +63,48 @@ __device__ __forceinline__ void cmul(double ar, double ai, double br, double bi,
     const double i = fma(ar, bi, ai * br);
     cr = r;
     ci = i;
+}
+
+// x / 48000 correctly rounded (binary32) without the IEEE divide sequence: q = x * RN(1/SR),
+// then one FMA residual step (Markstein).  Checked exhaustively against x / 48000.0f over all
+// positive finite floats on the host: the only mismatches have subnormal quotients (x < 2^-110),
+// and the phase / exponent arguments here are 0 or >= 20 * 1.
+__device__ __forceinline__ float div_sr(float x) {
+    const float inv = 1.0f / 48000.0f;
+    const float q = x * inv;
+    const float r = __builtin_fmaf(-q, 48000.0f, x);
+    return __builtin_fmaf(r, inv, q);
+}
+
+// sin(2 PI p) in double for the reference's PI = 3.14159265359 (src/includes.h:30) and a float
+// p >= 0: 2 PI p = 2 pi (p + p e) with e = PI / pi - 1, so with k = floor(p), r = p - k
+// (exact) the value is sin(2 pi (r + p e)).  r is folded into [-1/4, 1/4] by exact float
+// reflections (tracking the sign of the p e term), then an odd Taylor polynomial through x^15
+// on |x| <= pi/2 + 1e-6 (truncation < 7e-12) -- far below the float rounding that follows.
+__device__ __forceinline__ double sin2pi_ref(float p) {
+    constexpr double kE = 3.14159265359 / kPiM - 1.0;
+    const float k = floorf(p);
+    float u = p - k;                      // [0, 1), exact
+    if (u >= 0.5f) u = u - 1.0f;          // [-1/2, 1/2), exact
+    double sgn = 1.0;
+    if (u > 0.25f) {
+        u = 0.5f - u;                     // exact (Sterbenz)
+        sgn = -1.0;
+    } else if (u < -0.25f) {
+        u = -0.5f - u;
+        sgn = -1.0;
+    }
+    const double x = 2.0 * kPiM * fma(sgn * kE, (double)p, (double)u);
+    const double x2 = x * x;
+    double s = 1.0 / 1307674368000.0;     // 1/15!
+    s = fma(s, -x2, 1.0 / 6227020800.0);  // 1/13!
+    s = fma(s, -x2, 1.0 / 39916800.0);
+    s = fma(s, -x2, 1.0 / 362880.0);
+    s = fma(s, -x2, 1.0 / 5040.0);
+    s = fma(s, -x2, 1.0 / 120.0);
+    s = fma(s, -x2, 1.0 / 6.0);
+    s = fma(s, -x2, 1.0);
+    return x * s;
 }
 
 // float phase counter after t increments from n0 (saturates at 2^24)
@@ -132,26 +175,24 @@ __global__ __launch_bounds__(64 * kWaves) void bowl_mix_kernel(const double* __r
                 }
             }
         } else {
-            const float sr_f = 48000.0f;
+            // the float phase counter of the chunk's samples (mode-independent)
+            float ph[kL];
+#pragma unroll
+            for (int j = 0; j < kL; ++j) ph[j] = phase_f(a.n0, tc + j);
             for (int q = 0; q < count; ++q) {
                 const double* rr = rec + (long)(first + q) * BRec::SIZE;
                 const float fq = (float)rr[BRec::F], dq = (float)rr[BRec::D], aq = (float)rr[BRec::AMP];
                 // decay magnitude: exp seed at the chunk start (from the float exponent, as
                 // the reference), advanced by E^{-d/SR} per sample
-                const float ph0 = phase_f(a.n0, tc);
-                const float x0 = -dq * ph0 / sr_f;
-                double mag = exp((double)x0);
+                const float x0 = div_sr(-dq * ph[0]);
+                double amag = (double)aq * exp((double)x0);
                 const double rstep = rr[BRec::R];
 #pragma unroll
                 for (int j = 0; j < kL; ++j) {
-                    const float ph = phase_f(a.n0, tc + j);
-                    const float p = fq * ph / sr_f;  // float mul, correctly rounded float divide
-                    const float k = floorf(p);
-                    const float rp = p - k;          // exact
-                    const double arg = fma(2.0 * 3.14159265359, (double)rp, 2.0 * (double)k * (3.14159265359 - kPiM));
-                    const float wv = (float)sin(arg);  // Wave<float>: sin in double, float out
-                    acc[j] = fma((double)aq * mag, (double)wv, acc[j]);
-                    mag *= rstep;
+                    const float p = div_sr(fq * ph[j]);   // float mul, correctly rounded float divide
+                    const float wv = (float)sin2pi_ref(p);  // Wave<float>: sin in double, float out
+                    acc[j] = fma(amag, (double)wv, acc[j]);
+                    amag *= rstep;
                 }
             }
         }
@@ -183,6 +224,41 @@ __global__ __launch_bounds__(256) void bowl_reduce_kernel(const double* __restri
     red[ty][tx] = s;
     __syncthreads();
     if (ty == 0 && t < n) out[t] = (OutT)((red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]));
+}
+
+// short calls (a streamed 1024-sample block): 16 row slices per 64 samples, the loads of a
+// slice issued 8 at a time, then a fixed-order LDS sum over the slices
+constexpr int kShortSlices = 16;
+constexpr long kShortMax = 16384;
+
+template <typename OutT>
+__global__ __launch_bounds__(64 * kShortSlices) void bowl_reduce_short_kernel(const double* __restrict__ partial,
+                                                                              long n_pad, int G, long n,
+                                                                              OutT* __restrict__ out) {
+    __shared__ double red[kShortSlices][64];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const long t = (long)blockIdx.x * 64 + tx;
+    double s = 0.0;
+    if (t < n) {
+        const double* col = partial + t;
+        int g = ty;
+        for (; g + 7 * kShortSlices < G; g += 8 * kShortSlices) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = col[(long)(g + u * kShortSlices) * n_pad];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; g < G; g += kShortSlices) s += col[(long)g * n_pad];
+    }
+    red[ty][tx] = s;
+    __syncthreads();
+    if (ty == 0 && t < n) {
+        double m = red[0][tx];
+#pragma unroll
+        for (int k = 1; k < kShortSlices; ++k) m += red[k][tx];
+        out[t] = (OutT)m;
+    }
 }
 
 void build_brec(double f, double amp, double d, bool is_float, double* rec) {
@@ -302,7 +378,16 @@ int bowl_launch(hz_bowl* h, void* d_dst, long n, int out_kind) {
                        (const double*)h->d_rec, args);
     HZ_TRY_HIP(hipGetLastError());
     if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
-    if (out_kind == 0)
+    if (n <= kShortMax) {
+        if (out_kind == 0)
+            hipLaunchKernelGGL(bowl_reduce_short_kernel<float>, dim3((unsigned)((n + 63) / 64)),
+                               dim3(64 * kShortSlices), 0, h->stream, (const double*)h->d_partial, n_pad, G, n,
+                               (float*)d_dst);
+        else
+            hipLaunchKernelGGL(bowl_reduce_short_kernel<double>, dim3((unsigned)((n + 63) / 64)),
+                               dim3(64 * kShortSlices), 0, h->stream, (const double*)h->d_partial, n_pad, G, n,
+                               (double*)d_dst);
+    } else if (out_kind == 0)
         hipLaunchKernelGGL(bowl_reduce_kernel<float>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, h->stream,
                            (const double*)h->d_partial, n_pad, G, n, (float*)d_dst);
     else

@@ -106,6 +106,14 @@ struct hz_fb {
     hipStream_t stream_red = nullptr;
     std::vector<hipEvent_t> sync_ev;  // ordering events (no timing)
     double* d_xhist_red = nullptr;    // x history at the call start, for the first chunk's reduce
+    // a coefficient-stream call leaves its last row staged as the coefficients; the row is
+    // copied back asynchronously and turned into F/B only when they are next needed
+    double* tv_row = nullptr;         // pinned host copy of the stream's last row
+    size_t tv_row_cap = 0;            // doubles
+    hipEvent_t tv_ev = nullptr;       // the copy's completion
+    bool tv_pending = false;
+    int tv_kind = 0;
+    double tv_param = 0;
 };
 
 namespace hz_fbi {
@@ -117,6 +125,7 @@ void fb_mirror_advance(hz_fb* h, long len);  // O(1): the closed form is applied
 void fb_mirror_sync(hz_fb* h);               // bring pg_host up to date (before a setter)
 int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n);
 int fb_upload_staged(hz_fb* h);              // staged setters -> device
+int fb_tv_materialize(hz_fb* h);             // pending stream row -> F/B (hz_fb_tv.hip)
 // hz_fb_lti.hip
 int fb_lti_geom(const hz_fb* h, long n);  // LTI geometry for a call of n samples
 int fb_lti_chunk(int geom);                // samples per lane chunk of a geometry

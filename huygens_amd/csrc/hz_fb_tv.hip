@@ -165,6 +165,122 @@ __global__ __launch_bounds__(kThreads) void fb_tv_kernel(TvArgs a) {
     }
 }
 
+// HZ_FB_TV_RESONANT, producer/consumer form.  The coefficients of sample t depend only on the
+// frequency stream at t, not on the recurrence, so they are computed time-parallel: per
+// workgroup of 64 bands, kResProd producer waves evaluate g = resonant(f, R) and
+// b0 = -2 R cos(2 PI f / SR) for a kResTL-sample tile (kResPer samples each, stream loads
+// issued together) into LDS, while wave 0 runs the band recurrence over the previous tile from
+// LDS (three dependent FP64 ops per sample), and the first producer lanes sum the tile before
+// that into the partial mix.  Three tiles in flight, double-buffered, one barrier per tile.
+// The per-band arithmetic is fb_tv_kernel's, op for op; the mix order is the same.
+constexpr int kResProd = 15;   // 16 waves per workgroup: 4 per SIMD to cover the libm latency
+constexpr int kResPer = 2;
+constexpr int kResTL = kResProd * kResPer;
+static_assert(kResTL * kLanes <= 64 * kResProd, "mix lanes");
+constexpr int kResThreads = 64 * (1 + kResProd);
+
+template <int DIST>
+__global__ __launch_bounds__(kResThreads) void fb_tv_res_kernel(TvArgs a) {
+    constexpr int O = 2;
+    __shared__ double gb[2][kResTL][kThreads];
+    __shared__ double bb[2][kResTL][kThreads];
+    __shared__ double xs[2][kResTL + O];
+    __shared__ double vb[2][kResTL * kRow];
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const long band = (long)blockIdx.x * kThreads + lane;
+    const bool live = band < a.N;
+    const long bb_ = live ? band : 0;
+    const long ntiles = (a.n + kResTL - 1) / kResTL;
+    if (wave == 0) {
+        double y0 = a.ystate[bb_ * O], y1 = a.ystate[bb_ * O + 1];
+        double pre = a.pg[2 * bb_], gain = a.pg[2 * bb_ + 1];
+        const double pin = a.pin[bb_], gin = a.gin[bb_];
+        const double sp = a.sp, sg = a.sg, b1 = a.param * a.param;
+        const int vcol = (lane / kRunLen) * kRun + lane % kRunLen;
+        for (long it = 0; it <= ntiles + 1; ++it) {
+            if (it >= 1 && it - 1 < ntiles) {
+                const int c = (int)((it - 1) & 1);
+                const int m = (int)min((long)kResTL, a.n - (it - 1) * kResTL);
+                const double* x = xs[c];
+                double* v = vb[c] + vcol;
+                for (int j = 0; j < m; ++j) {
+                    const double g = gb[c][j][lane], b0 = bb[c][j][lane];
+                    pre = (1 - sp) * pin + sp * pre;
+                    gain = (1 - sg) * gin + sg * gain;
+                    double ff = g * x[j + O];
+                    ff += 0.0 * x[j + O - 1];
+                    ff += -g * x[j];
+                    double bsum = 0;
+                    bsum += b0 * y0;
+                    bsum += b1 * y1;
+                    const double yn = ff * pre - bsum;
+                    y1 = y0;
+                    y0 = yn;
+                    const double o = hz::dist_apply<DIST>(yn * gain, a.dist_param);
+                    v[j * kRow] = live ? o : 0.0;
+                }
+            }
+            __syncthreads();
+        }
+        if (live) {
+            a.ystate_next[band * O] = y0;
+            a.ystate_next[band * O + 1] = y1;
+            a.pg_next[2 * band] = pre;
+            a.pg_next[2 * band + 1] = gain;
+        }
+    } else {
+        const int pw = wave - 1;
+        const double R = a.param;
+        const double* srow = a.stream + bb_;
+        for (long it = 0; it <= ntiles + 1; ++it) {
+            if (it < ntiles) {
+                const int c = (int)(it & 1);
+                const long t0 = it * kResTL;
+                const int m = (int)min((long)kResTL, a.n - t0);
+                double fr[kResPer];
+#pragma unroll
+                for (int i = 0; i < kResPer; ++i) {
+                    const int j = pw * kResPer + i;
+                    fr[i] = j < m ? srow[(t0 + j) * a.stream_row] : 0.0;
+                }
+#pragma unroll
+                for (int i = 0; i < kResPer; ++i) {
+                    const int j = pw * kResPer + i;
+                    const double cosine = cos(2 * hz::kPI * fr[i] / hz::kSR);
+                    const double g = resonant(fr[i], R);
+                    gb[c][j][lane] = g;
+                    bb[c][j][lane] = -2 * R * cosine;
+                }
+                if (pw == kResProd - 1 && lane < kResTL + O) {   // x[t0 - O .. t0 + TL - 1]
+                    const long i = t0 - O + lane;
+                    xs[c][lane] = i >= 0 ? (i < a.n ? a.x[i] : 0.0) : a.xhist[-i - 1];
+                }
+            }
+            if (it >= 2 && tid - 64 < kResTL * kLanes) {   // partial mix of tile it - 2
+                const int r = tid - 64, j = r / kLanes, p = r % kLanes;
+                const long t0 = (it - 2) * kResTL;
+                const int m = (int)min((long)kResTL, a.n - t0);
+                double s = 0.0;
+                if (j < m) {
+                    const double* row = vb[it & 1] + j * kRow + p * kRun;
+#pragma unroll
+                    for (int k = 0; k < kRunLen; ++k) s += row[k];
+                }
+#pragma unroll
+                for (int w = 1; w < kLanes; w <<= 1) s += __shfl_xor(s, w);
+                if (p == 0 && j < m) a.part[blockIdx.x * a.pstride + t0 + j] = s;
+            }
+            __syncthreads();
+        }
+    }
+    if (blockIdx.x == 0 && tid < O) {   // x[-1-k] for the next call
+        const long i = a.n - 1 - tid;
+        a.xhist_next[tid] = i >= 0 ? a.x[i] : a.xhist[-i - 1];
+    }
+}
+
 __global__ __launch_bounds__(kMixSamples* kMixSlices) void fb_tv_mix_kernel(const double* __restrict__ part,
                                                                           double* __restrict__ out, long n,
                                                                           long pstride, int G) {
@@ -198,8 +314,17 @@ tv_fn tv_pick_dist(int dist) {
     }
 }
 
+tv_fn tv_pick_res(int dist) {
+    switch (dist) {
+    case HZ_DIST_SOFTCLIP: return fb_tv_res_kernel<HZ_DIST_SOFTCLIP>;
+    case HZ_DIST_SATURATE: return fb_tv_res_kernel<HZ_DIST_SATURATE>;
+    case HZ_DIST_LIMITER: return fb_tv_res_kernel<HZ_DIST_LIMITER>;
+    default: return fb_tv_res_kernel<HZ_DIST_NONE>;
+    }
+}
+
 tv_fn tv_pick(int O, int kind, int dist) {
-    if (kind == HZ_FB_TV_RESONANT) return tv_pick_dist<2, HZ_FB_TV_RESONANT>(dist);
+    if (kind == HZ_FB_TV_RESONANT) return tv_pick_res(dist);
     switch (O) {
     case 0: return tv_pick_dist<0, HZ_FB_TV_COEFFS>(dist);
     case 1: return tv_pick_dist<1, HZ_FB_TV_COEFFS>(dist);
@@ -235,6 +360,31 @@ void resonant_host(double f, double R, double* fwd, double* back) {
 
 }  // namespace
 
+namespace hz_fbi {
+
+int fb_tv_materialize(hz_fb* h) {
+    if (!h->tv_pending) return HZ_OK;
+    HZ_TRY_HIP(hipEventSynchronize(h->tv_ev));
+    const long N = h->N;
+    const int O = h->order;
+    const double* last = h->tv_row;
+    for (long b = 0; b < N; ++b) {
+        double* F = &h->F[(size_t)b * (O + 1)];
+        double* B = O > 0 ? &h->B[(size_t)b * O] : nullptr;
+        if (h->tv_kind == HZ_FB_TV_COEFFS) {
+            for (int q = 0; q <= O; ++q) F[q] = last[(size_t)q * N + b];
+            for (int q = 0; q < O; ++q) B[q] = last[(size_t)(O + 1 + q) * N + b];
+        } else {
+            resonant_host(last[b], h->tv_param, F, B);
+        }
+    }
+    h->tv_pending = false;
+    h->dirty_coef = true;
+    return HZ_OK;
+}
+
+}  // namespace hz_fbi
+
 extern "C" {
 
 int hz_fb_process_tv_device(hz_fb* h, const double* d_in, double* d_out, size_t n, int kind,
@@ -255,7 +405,14 @@ int hz_fb_process_tv_device(hz_fb* h, const double* d_in, double* d_out, size_t 
         hz::set_error("hz_fb_process_tv: null buffer");
         return HZ_E_INVALID;
     }
-    HZ_TRY(hz_fbi::fb_upload_staged(h));   // pin / gin (and coefficients for later calls)
+    // pin / gin.  This call's last row supersedes a pending one, and the stream kernel does not
+    // read the staged coefficients, so their rebuild waits for the next plain call.
+    h->tv_pending = false;
+    const bool dirty_coef = h->dirty_coef;
+    h->dirty_coef = false;
+    const int up = hz_fbi::fb_upload_staged(h);
+    h->dirty_coef = dirty_coef;
+    HZ_TRY(up);
     const long N = h->N, G = (N + kThreads - 1) / kThreads;
     const long chunk = std::max(1L, std::min(1L << 20, kPartBytes / (long)sizeof(double) / G));
     const long row = kind == HZ_FB_TV_COEFFS ? (2 * O + 1) * N : N;
@@ -296,7 +453,8 @@ int hz_fb_process_tv_device(hz_fb* h, const double* d_in, double* d_out, size_t 
             HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
             HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
         }
-        hipLaunchKernelGGL(k, dim3((unsigned)G), dim3(kThreads), 0, h->stream, a);
+        hipLaunchKernelGGL(k, dim3((unsigned)G), dim3(kind == HZ_FB_TV_RESONANT ? kResThreads : kThreads), 0,
+                           h->stream, a);
         HZ_TRY_HIP(hipGetLastError());
         if (e) {
             HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
@@ -315,21 +473,22 @@ int hz_fb_process_tv_device(hz_fb* h, const double* d_in, double* d_out, size_t 
         hz_fbi::fb_mirror_advance(h, len);
     }
     h->last_path = HZ_FB_PATH_GENERAL;
-    // the coefficients last set (the stream's final row) stay staged for later calls
-    std::vector<double> last(row);
-    HZ_TRY_HIP(hipMemcpyAsync(last.data(), d_stream + ((long)n - 1) * row, sizeof(double) * row,
-                              hipMemcpyDeviceToHost, h->stream));
-    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
-    for (long b = 0; b < N; ++b) {
-        double* F = &h->F[(size_t)b * (O + 1)];
-        double* B = O > 0 ? &h->B[(size_t)b * O] : nullptr;
-        if (kind == HZ_FB_TV_COEFFS) {
-            for (int q = 0; q <= O; ++q) F[q] = last[(size_t)q * N + b];
-            for (int q = 0; q < O; ++q) B[q] = last[(size_t)(O + 1 + q) * N + b];
-        } else {
-            resonant_host(last[b], param, F, B);
-        }
+    // the coefficients last set (the stream's final row) stay staged for later calls: copied
+    // back without blocking, turned into F/B by fb_tv_materialize when next needed
+    if ((size_t)row > h->tv_row_cap) {
+        if (h->tv_row) HZ_TRY_HIP(hipHostFree(h->tv_row));
+        h->tv_row = nullptr;
+        h->tv_row_cap = 0;
+        HZ_TRY_HIP(hipHostMalloc(&h->tv_row, sizeof(double) * row, hipHostMallocDefault));
+        h->tv_row_cap = row;
     }
+    if (!h->tv_ev) HZ_TRY_HIP(hipEventCreateWithFlags(&h->tv_ev, hipEventDisableTiming));
+    HZ_TRY_HIP(hipMemcpyAsync(h->tv_row, d_stream + ((long)n - 1) * row, sizeof(double) * row,
+                              hipMemcpyDeviceToHost, h->stream));
+    HZ_TRY_HIP(hipEventRecord(h->tv_ev, h->stream));
+    h->tv_pending = true;
+    h->tv_kind = kind;
+    h->tv_param = param;
     h->dirty_coef = true;
     h->converged = false;
     return HZ_OK;

@@ -639,6 +639,7 @@ int fb_groups(const hz_fb* h) {
 
 int fb_upload(hz_fb* h) {
     bool uploaded = false;
+    HZ_TRY(hz_fbi::fb_tv_materialize(h));
     if (h->dirty_coef) {
         const int O = h->order;
         h->h_rec.assign((size_t)h->N * h->rec, 0.0);
@@ -947,6 +948,8 @@ int hz_fb_destroy(hz_fb* h) {
     for (hipEvent_t e : h->sync_ev) (void)hipEventDestroy(e);
     if (h->stream_red) (void)hipStreamDestroy(h->stream_red);
     if (h->d_xhist_red) (void)hipFree(h->d_xhist_red);
+    if (h->tv_row) (void)hipHostFree(h->tv_row);
+    if (h->tv_ev) (void)hipEventDestroy(h->tv_ev);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return HZ_OK;
@@ -963,6 +966,7 @@ int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double*
     }
     const int l = fb_local(h, n);
     if (l < 0) return HZ_OK;
+    HZ_TRY(hz_fbi::fb_tv_materialize(h));
     const int O = h->order;
     for (int i = 0; i < std::min(O + 1, nf); ++i) h->F[(size_t)l * (O + 1) + i] = fwd[i];
     for (int i = 0; i < std::min(O, nb); ++i) h->B[(size_t)l * O + i] = back[i];
