@@ -218,9 +218,11 @@ def run_c5(args, torch, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    elapsed = _timed(step, args.steps, 0, torch, dev)   # no event records in the timed region
+    # kernel times of the streamed blocks: a separate profiled pass
     bowl.profile(True)
     bank.profile(True)
-    elapsed = _timed(step, args.steps, 0, torch, dev)
+    _timed(step, args.steps, 0, torch, dev)
     bms, bl = bowl.profile_read()
     dms, dl = bank.profile_read()
     bowl.profile(False)

@@ -53,6 +53,22 @@ public:
         detail::check(hz_fb_set_distortion(h_.get(), dist_id, param), "Filterbank::process");
         detail::check(hz_fb_process(h_.get(), in, out, n), "Filterbank::process");
     }
+    // n x { coefficients(b, row t) for every band b; out[t] = operator()(in[t]); tick(); } --
+    // the Subtractive ALLINONE / ONEPERVOICE pattern (src/subtractive.h:215-228, 300-317) as one
+    // call.  coeffs: [n][2*order+1][N] (forward then back, band-minor).  The last row stays set.
+    void process_stream(const T* in, T* out, std::size_t n, const T* coeffs, int dist_id = HZ_DIST_NONE,
+                        double param = 0.0) {
+        detail::check(hz_fb_set_distortion(h_.get(), dist_id, param), "Filterbank::process_stream");
+        detail::check(hz_fb_process_tv(h_.get(), in, out, n, HZ_FB_TV_COEFFS, coeffs, 0.0),
+                      "Filterbank::process_stream");
+    }
+    // the same with every band retuned to resonant(freqs[t][b], R) (order 2, subtractive.h:240-264)
+    void process_resonant(const T* in, T* out, std::size_t n, const T* freqs, double R,
+                          int dist_id = HZ_DIST_NONE, double param = 0.0) {
+        detail::check(hz_fb_set_distortion(h_.get(), dist_id, param), "Filterbank::process_resonant");
+        detail::check(hz_fb_process_tv(h_.get(), in, out, n, HZ_FB_TV_RESONANT, freqs, R),
+                      "Filterbank::process_resonant");
+    }
     hz_fb* native() const { return h_.get(); }
 
 private:

@@ -76,6 +76,17 @@ int main(int argc, char** argv) {
         std::vector<double> z(1000);
         ff.process(x.data(), z.data(), 1000);
         dump("ffilterbank", z);
+
+        // Subtractive ALLINONE pattern (src/subtractive.h:215-228): every band retuned every
+        // sample, here as one process_resonant() call over per-sample frequency rows
+        Filterbank<double> sub(2, 16);
+        sub.boost(std::vector<double>(16, 1.0));
+        sub.open();
+        std::vector<double> fr(1000 * 16), w(1000);
+        for (int t = 0; t < 1000; t++)
+            for (int b = 0; b < 16; b++) fr[t * 16 + b] = 110.0 * (b + 1) * (1 + 0.02 * std::sin(0.003 * t + b));
+        sub.process_resonant(x.data(), w.data(), 1000, fr.data(), 0.999);
+        dump("subtractive", w);
     }
     {   // Delay: tests/delay.cpp:18,41
         Delay<double> delay(10, 2 * SR);

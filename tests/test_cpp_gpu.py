@@ -59,6 +59,16 @@ def test_ffilterbank(outputs):
     assert rel_err(outputs("ffilterbank"), o.process(x_input(1000))) < 1e-9
 
 
+def test_subtractive_resonant_stream(outputs):
+    """Filterbank::process_resonant: every band retuned every sample (hz_fb_process_tv)."""
+    o = OracleFilterbank(2, 16)
+    o.boost(np.ones(16))
+    o.open()
+    t, b = np.arange(1000)[:, None], np.arange(16)[None, :]
+    fr = 110.0 * (b + 1) * (1 + 0.02 * np.sin(0.003 * t + b))
+    assert rel_err(outputs("subtractive"), o.process_tv(x_input(1000), 1, fr, 0.999)) < 1e-10   # host sin of the tracks may differ by an ulp
+
+
 def test_delay_bit_exact(outputs):
     o = OracleDelaybank(1, 10, 2 * 48000)
     o.coefficients(0, [(0, 1.0)], [(20000, 0.5), (10000, 0.5)])
