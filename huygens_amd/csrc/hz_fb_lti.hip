@@ -583,6 +583,8 @@ __global__ __launch_bounds__(256) void fb_fmix_kernel(const double* __restrict__
 // out[t] = sum_g partial[g][t] + sum_i Fmix[t mod L][i] x[t - t mod L - O + i]
 // One thread per pair of samples (16-B loads down the slab's columns, 8 rows in flight),
 // 128 threads per block; the group order of the sum is fixed (deterministic).
+constexpr int kRedRows = 32;
+
 template <int O, int L>
 __global__ __launch_bounds__(128) void fb_lti_reduce_kernel(const double* __restrict__ partial, long n_pad, int G,
                                                             long n, const double* __restrict__ x,
@@ -599,12 +601,15 @@ __global__ __launch_bounds__(128) void fb_lti_reduce_kernel(const double* __rest
     d2 s0 = {0.0, 0.0}, s1 = {0.0, 0.0};
     const double* col = partial + t;  // n_pad is a multiple of the tile: t + 1 < n_pad
     int g = 0;
-    for (; g + 8 <= G; g += 8) {
-        d2 v[8];
+    // kRedRows slab rows in flight per thread; the slab is read once, so the loads are
+    // non-temporal (no L2 / MALL allocation for data nobody reads again)
+    for (; g + kRedRows <= G; g += kRedRows) {
+        d2 v[kRedRows];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = *(const d2*)(col + (long)(g + u) * n_pad);
+        for (int u = 0; u < kRedRows; ++u)
+            v[u] = __builtin_nontemporal_load((const d2*)(col + (long)(g + u) * n_pad));
 #pragma unroll
-        for (int u = 0; u < 8; u += 2) {
+        for (int u = 0; u < kRedRows; u += 2) {
             s0 += v[u];
             s1 += v[u + 1];
         }
