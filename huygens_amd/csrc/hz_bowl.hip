@@ -14,7 +14,7 @@
 // ulp(p)/2 (0.008 cycles at n ~ 5e5) -- that rounding is part of its output, so the float
 // model is evaluated per mode-sample: float mul + correctly rounded float divide (FMA
 // residual form, div_sr), then sin(2 PI p) in double with p split exactly as k + r
-// (k = floor p), r folded to a quarter period and a Taylor polynomial (sin2pi_ref), rounded
+// (k = floor p), r folded to a quarter period and an odd polynomial (sin2pi_ref), rounded
 // to float -- no library sin or IEEE divide sequence in the loop; the decay E^x uses a
 // per-chunk exp seed and a per-sample factor (x's float rounding changes the term by
 // < 2.5e-8 a_i).  The sum is kept in double (the reference rounds it to float after every
@@ -79,32 +79,27 @@ __device__ __forceinline__ float div_sr(float x) {
 // sin(2 PI p) in double for the reference's PI = 3.14159265359 (src/includes.h:30) and a float
 // p >= 0: 2 PI p = 2 pi (p + p e) with e = PI / pi - 1, so with k = floor(p), r = p - k
 // (exact) the value is sin(2 pi (r + p e)).  r is folded into [-1/4, 1/4] by exact float
-// reflections (tracking the sign of the p e term), then an odd Taylor polynomial through x^15
-// on |x| <= pi/2 + 1e-6 (truncation < 7e-12) -- far below the float rounding that follows.
+// reflections (tracking the sign of the p e term), then an odd degree-11 polynomial in r
+// (|error| < 1.4e-11) -- far below the float rounding that follows.
 __device__ __forceinline__ double sin2pi_ref(float p) {
     constexpr double kE = 3.14159265359 / kPiM - 1.0;
     const float k = floorf(p);
     float u = p - k;                      // [0, 1), exact
-    if (u >= 0.5f) u = u - 1.0f;          // [-1/2, 1/2), exact
-    double sgn = 1.0;
-    if (u > 0.25f) {
-        u = 0.5f - u;                     // exact (Sterbenz)
-        sgn = -1.0;
-    } else if (u < -0.25f) {
-        u = -0.5f - u;
-        sgn = -1.0;
-    }
-    const double x = 2.0 * kPiM * fma(sgn * kE, (double)p, (double)u);
-    const double x2 = x * x;
-    double s = 1.0 / 1307674368000.0;     // 1/15!
-    s = fma(s, -x2, 1.0 / 6227020800.0);  // 1/13!
-    s = fma(s, -x2, 1.0 / 39916800.0);
-    s = fma(s, -x2, 1.0 / 362880.0);
-    s = fma(s, -x2, 1.0 / 5040.0);
-    s = fma(s, -x2, 1.0 / 120.0);
-    s = fma(s, -x2, 1.0 / 6.0);
-    s = fma(s, -x2, 1.0);
-    return x * s;
+    u = u >= 0.5f ? u - 1.0f : u;         // [-1/2, 1/2), exact
+    // reflect |u| > 1/4 about +-1/2 (exact, Sterbenz); selects, not branches
+    const bool refl = fabsf(u) > 0.25f;
+    u = refl ? copysignf(0.5f, u) - u : u;
+    const double y = fma(refl ? -kE : kE, (double)p, (double)u);   // revolutions, |y| <= 1/4 + 1e-7
+    // sin(2 pi y) = y P(y^2), P a degree-5 least-squares (near-minimax) fit on |y| <= 1/4:
+    // max |error| 1.35e-11
+    const double z = y * y;
+    double s = -14.337175761608114;
+    s = fma(s, z, 42.000013938078347);
+    s = fma(s, z, -76.703669216302146);
+    s = fma(s, z, 81.605209465741268);
+    s = fma(s, z, -41.341701930121658);
+    s = fma(s, z, 6.2831853064884768);
+    return y * s;
 }
 
 // float phase counter after t increments from n0 (saturates at 2^24)
