@@ -168,11 +168,13 @@ struct LtiArgs {
     const double* xhist;    // [O]
     double* xhist_next;     // [O]
     double* partial;        // [G][n_pad] (n_pad = row stride)
-    double* segstate;       // [N][nseg][O]
+    double* segstate;       // [N][nseg_state][O] start states of the (prepass-fine) segments
     long n;                 // samples in this launch (multiple of L)
     long n_pad;             // slab row stride (the tile-padded length)
     long seg_len;           // multiple of the tile (64 L)
     int nseg;
+    int nseg_state;         // segments in segstate (the prepass splits a segment in seg_stride)
+    int seg_stride;         // segstate index of segment s: s * seg_stride
     int nbands;
     double sp_n, sg_n;      // sp^n, sg^n (closed-form smoother end state)
 };
@@ -263,7 +265,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     {
         const double* s0 = (MODE == MODE_SEGEND) ? nullptr
                          : (seg == 0) ? a.ystate + (long)bandc * O
-                                      : a.segstate + ((long)bandc * a.nseg + seg) * O;
+                                      : a.segstate + ((long)bandc * a.nseg_state + (long)seg * a.seg_stride) * O;
 #pragma unroll
         for (int k = 0; k < O; ++k) S[k] = (live && s0) ? s0[k] : 0.0;
     }
@@ -476,7 +478,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     if constexpr (MODE == MODE_SEGEND) {
         if (lane == 0 && !last_seg && live) {
 #pragma unroll
-            for (int k = 0; k < O; ++k) a.segstate[((long)band * a.nseg + seg + 1) * O + k] = S[k];
+            for (int k = 0; k < O; ++k) a.segstate[((long)band * a.nseg_state + seg + 1) * O + k] = S[k];
         }
     } else {
         if (last_seg && lane == 0 && live) {
@@ -864,10 +866,37 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         const long len = std::min(chunk, n - off);
         const long ntiles = (len + T - 1) / T;
         long nseg = std::max<long>(1, std::min<long>(ntiles, (h->target_groups + G - 1) / G));
-        const long seg_tiles = (ntiles + nseg - 1) / nseg;
+        long seg_tiles = (ntiles + nseg - 1) / nseg;
         nseg = (ntiles + seg_tiles - 1) / seg_tiles;
+        // The prepass (zero-start end states of segments 0 .. nseg-2) runs on G (nseg - 1)
+        // workgroups, a fraction of the chip when few segments are needed (2 GPUs: 128 of 256
+        // CUs).  Split each prepass segment in m equal parts, m minimising the prepass rounds
+        // per unit of work, ceil(G (nseg-1) m / CUs) / m; the carry kernel runs over the fine
+        // segments and the mix reads every m-th start.
+        // (the coarse segment may grow to a multiple of m tiles, by at most 1/32: fine boundaries
+        // must fall on coarse ones)
+        int m = 1;
         if (nseg > 1) {
-            const size_t sneed = (size_t)h->N * nseg * O;
+            double best = 1.0;
+            long best_tiles = seg_tiles;
+            for (int c = 2; c <= 8; ++c) {
+                const long st = (seg_tiles + c - 1) / c;   // fine segment, tiles
+                if (st < 4 || (st * c - seg_tiles) * 32 > seg_tiles) continue;
+                const long ns = (ntiles + st * c - 1) / (st * c);
+                const double cost = (double)((G * (ns - 1) * c + h->target_groups - 1) / h->target_groups) / c *
+                                    ((double)(st * c) / seg_tiles);
+                if (ns > 1 && cost < best - 1e-3) {
+                    best = cost;
+                    m = c;
+                    best_tiles = st * c;
+                }
+            }
+            seg_tiles = best_tiles;
+            nseg = (ntiles + seg_tiles - 1) / seg_tiles;
+        }
+        const long nseg_state = (nseg - 1) * m + 1;
+        if (nseg > 1) {
+            const size_t sneed = (size_t)h->N * nseg_state * O;
             if (sneed > h->seg_cap) {
                 HZ_TRY_HIP(hipStreamSynchronize(h->stream));
                 if (h->d_seg) HZ_TRY_HIP(hipFree(h->d_seg));
@@ -893,6 +922,8 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         a.n_pad = ntiles * T;
         a.seg_len = seg_tiles * T;
         a.nseg = (int)nseg;
+        a.nseg_state = (int)nseg_state;
+        a.seg_stride = m;
         a.nbands = h->N;
         a.sp_n = (double)powl((long double)h->sp, (long double)len);
         a.sg_n = (double)powl((long double)h->sg, (long double)len);
@@ -904,12 +935,16 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
         }
         if (nseg > 1) {
-            hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg - 1)), dim3(64 * lti_waves(O)), lds_end, h->stream,
-                               (const double*)set.d_rec, a);
+            LtiArgs af = a;   // the prepass over fine segments (never the last one)
+            af.seg_len = seg_tiles / m * T;
+            af.nseg = (int)nseg_state + 1;
+            af.seg_stride = 1;
+            hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg_state - 1)), dim3(64 * lti_waves(O)), lds_end,
+                               h->stream, (const double*)set.d_rec, af);
             HZ_TRY_HIP(hipGetLastError());
             hipLaunchKernelGGL(pick_lti_carry(O, L), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0, h->stream,
                                (const double*)set.d_rec, (const double*)h->d_ystate[h->scur], h->d_seg, h->N,
-                               (int)nseg, seg_tiles);
+                               (int)nseg_state, seg_tiles / m);
             HZ_TRY_HIP(hipGetLastError());
         }
         if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));

@@ -101,6 +101,16 @@ def test_time_segments_lti(gpu_lib, N, groups):
     run_calls(g, o, [500, 30000, 12345, 2048 * 5], seed=21)
 
 
+@pytest.mark.parametrize("N,groups,calls", [(128, 16, [500, 40960, 5000]), (64, 16, [500, 98304, 700])])
+def test_fine_prepass_segments_lti(gpu_lib, N, groups, calls):
+    """Shard-sized banks: the segment prepass splits each segment in m fine parts (m = 2
+    here) and the mix starts from every m-th carried state (hz_fb_lti.hip, fb_launch_lti)."""
+    fwd, back = resonant_coefficients(N, 0.9995, 0.5)
+    g, o = make_pair(2, N, fwd, back)
+    g.set_target_groups(groups)
+    run_calls(g, o, calls, seed=22)
+
+
 def test_path_switches_with_setters(gpu_lib):
     """A setter change un-converges the smoothers: the next call runs the general
     engine, later calls return to LTI; the mixes stay on the oracle throughout."""
