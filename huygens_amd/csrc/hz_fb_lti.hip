@@ -380,7 +380,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                 for (int rr = 0; rr < 4; ++rr) {
                     const int chunk = 16 * m + (lane >> 4) + 4 * rr;
                     const long t = t0m + (long)chunk * L + 16 * jb + (lane & 15);
-                    if (t < n) a.partial[(long)blockIdx.x * a.n_pad + t] = acc0[rr] + acc1[rr];
+                    if (t < n) __builtin_nontemporal_store(acc0[rr] + acc1[rr], &a.partial[(long)blockIdx.x * a.n_pad + t]);
                 }
             }
         }
