@@ -324,18 +324,35 @@ def run_row(args):
     """One 1-GPU line for a secondary config (bench_rows.py)."""
     import torch
     import bench_rows
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        raise SystemExit("--workload c3/c4/c5 are single-GPU configs (SURVEY.md 8(d))")
-    dev = torch.device("cuda", 0)
-    fn = {"c3": bench_rows.run_c3, "c4": bench_rows.run_c4, "c5": bench_rows.run_c5,
-          "c6": bench_rows.run_c6, "c7": bench_rows.run_c7, "c8": bench_rows.run_c8,
-          "c9": bench_rows.run_c9}[args.workload]
-    body = fn(args, torch, dev)
-    line = {"metric": body.pop("metric"), "value": body.pop("value"), "unit": body.pop("unit"), "n_gpus": 1,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": body.pop("ms_per_step"),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None}
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.workload != "c3":
+        raise SystemExit("--workload c4..c9 are single-GPU configs (SURVEY.md 8(d)); c3 shards")
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=dev)
+        body = bench_rows.run_c3(args, torch, dev, rank, world)
+    elif args.workload == "c3" and args.emulate_world:
+        body = bench_rows.run_c3(args, torch, dev, 0, 1, args.emulate_world)
+    else:
+        fn = {"c3": bench_rows.run_c3, "c4": bench_rows.run_c4, "c5": bench_rows.run_c5,
+              "c6": bench_rows.run_c6, "c7": bench_rows.run_c7, "c8": bench_rows.run_c8,
+              "c9": bench_rows.run_c9}[args.workload]
+        body = fn(args, torch, dev)
+    line = {"metric": body.pop("metric"), "value": body.pop("value"), "unit": body.pop("unit"),
+            "n_gpus": body.pop("n_gpus", 1), "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": body.pop("ms_per_step"), "higher_is_better": True,
+            "scaling": body.pop("scaling", "weak"), "vs_baseline": None}
     line.update(body)
-    print(json.dumps(line), flush=True)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -39,12 +39,17 @@ def _timed(step, steps, warmup, torch, dev):
 
 
 # --------------------------------------------------------------------------- C3
-def run_c3(args, torch, dev):
+def run_c3(args, torch, dev, rank=0, world=1, shard_world=None):
     """Additive<double>(&cycle, 64, 256, 0.75, 1.0), all voices via makenote(36+v, 1),
-    voices 0-7 released at sample 24,000; one step = 480,000 samples."""
+    voices 0-7 released at sample 24,000; one step = 480,000 samples.  With world > 1 (the
+    BASELINE config: 8 GPUs) each rank owns a contiguous overtone range (huygens_amd.shard,
+    hz_add_create_shard) and the partial mixes are summed to rank 0 by an RCCL reduce."""
     from huygens_amd import Additive
+    from huygens_amd.shard import shard_of
     V, O, S = 64, 256, args.samples
-    add = Additive(V, O, 0.75, 1.0)
+    sw = shard_world or world   # --emulate-world P: rank 0's shard of P, on one GPU, no reduce
+    o0, oc = shard_of(rank, sw, O)
+    add = Additive(V, O, 0.75, 1.0, device=dev.index or 0, shard=(o0, oc) if sw > 1 else None)
     for v in range(V):
         add.makenote(36 + v, 1.0)
     stream = torch.cuda.current_stream(dev)
@@ -57,20 +62,33 @@ def run_c3(args, torch, dev):
         for v in range(8):
             add.release(v)
         add.fill_device(y.data_ptr() + 8 * rel, S - rel)
+        if world > 1:
+            dist.reduce(y, dst=0, op=dist.ReduceOp.SUM)
 
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    add.profile(True)
+    if world > 1:
+        dist.barrier()
     elapsed = _timed(step, args.steps, 0, torch, dev)
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    add.profile(True)   # kernel times: a separate profiled pass (no events in the timed region)
+    _timed(step, args.steps, 0, torch, dev)
     ms, launches = add.profile_read()
     add.profile(False)
-    units = V * O * S * args.steps
+    units = V * (O if shard_world is None else oc * sw) * S * args.steps
     kern_s = ms / 1e3
-    flops = 22.0 * units   # 22 flops (+ 3 transcendentals) per partial-sample
+    flops = 22.0 * V * oc * S * args.steps   # 22 flops (+ 3 transcendentals) per partial-sample
     achieved = flops / kern_s / 1e12 if kern_s > 0 else None
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         _tests_path()
         from oracle_osc import OracleAdditive
         o = OracleAdditive(V, O, 0.75, 1.0)
@@ -88,7 +106,9 @@ def run_c3(args, torch, dev):
         "ms_per_step": 1e3 * elapsed / args.steps, "dtype": "f64",
         "data": "synthetic: makenote(36+v, 1.0) for 64 voices, voices 0-7 released at sample 24000",
         "config": {"workload": "C3 Additive<double>(&cycle, 64, 256, 0.75, 1.0), physics off",
-                   "samples_per_step": S, "voices": V, "overtones": O},
+                   "samples_per_step": S, "voices": V, "overtones": O, "overtones_per_gpu": oc,
+                   "parallelism": f"overtones sharded x{world}, RCCL reduce"},
+        "n_gpus": world, "scaling": "strong", "emulated_world": shard_world,
         "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK if achieved else None, "traffic": None,
                      "kernel": "add_mix_kernel (+ add_reduce_kernel, add_advance_kernel)",
