@@ -24,6 +24,7 @@
 // Cosine: REDFT10 (DCT-II) and REDFT01 (DCT-III) through one complex FFT of length N
 // (Makhoul's even/odd reordering), in LDS, batched one transform per workgroup.
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -279,6 +280,136 @@ __global__ __launch_bounds__(kFrameThreads) void stft_frame_kernel(StftArgs a) {
     }
 }
 
+// Two real frames per complex transform (real input, symmetric gates).  While every sample a
+// launch reads is real (StftArgs::hi == nullptr) and the processor is a magnitude gate (its
+// keep/scale decision is the same for bins k and N - k of a real frame), frames f and f + 1
+// share one FFT pair: z = w x_f + i w x_{f+1}, Z = FFT(z), then per bin pair (k, N - k)
+//     X_f = (Z_k + conj Z_{N-k}) / 2,   X_{f+1} = (Z_k - conj Z_{N-k}) / 2i,
+// each frame's gate on its own spectrum (its own average), Y = Y_f + i Y_{f+1} (both Hermitian),
+// and one inverse FFT gives y_f + i y_{f+1}.  Half the FFT work per frame; the Im output of a
+// real frame is written as 0 (the reference's complex transform leaves ~1e-17 there).
+constexpr int kPairItems = 5;   // bin pairs per thread: ceil((N/2 + 1) / (N/8)) for N >= 16
+
+template <int PROC>
+__device__ __forceinline__ void pair_gate(double* re, double* im, int lg, double p0, double p1, double* scratch) {
+#pragma clang fp contract(off)
+    const int N = 1 << lg, H = N >> 1;
+    double ar[kPairItems], ai[kPairItems], br[kPairItems], bi[kPairItems];
+    double pa = 0.0, pb = 0.0, la = 0.0, lb = 0.0;   // magnitude sums (GATE_KEEP: double-double)
+#pragma unroll
+    for (int i = 0; i < kPairItems; ++i) {
+        const int k = threadIdx.x + i * blockDim.x;
+        ar[i] = ai[i] = br[i] = bi[i] = 0.0;
+        if (k <= H) {
+            const int m = (N - k) & (N - 1);
+            const int ek = hz::pad16(hz::bitrev(k, lg)), em = hz::pad16(hz::bitrev(m, lg));
+            const double zr = re[ek], zi = im[ek], wr = re[em], wi = im[em];
+            ar[i] = (zr + wr) * 0.5;   // X_f
+            ai[i] = (zi - wi) * 0.5;
+            br[i] = (zi + wi) * 0.5;   // X_{f+1}
+            bi[i] = (wr - zr) * 0.5;
+            const double c = (k == 0 || k == H) ? 1.0 : 2.0;   // bins k and N - k
+            if constexpr (PROC == HZ_PROC_STATIC_GATE) {
+                pa += c * (sqrt(ar[i] * ar[i] + ai[i] * ai[i]) / N);
+                pb += c * (sqrt(br[i] * br[i] + bi[i] * bi[i]) / N);
+            } else {
+                const double ha = hypot(ar[i], ai[i]), hb = hypot(br[i], bi[i]);
+                hz::dd_add(pa, la, ha);
+                hz::dd_add(pb, lb, hb);
+                if (c == 2.0) {
+                    hz::dd_add(pa, la, ha);
+                    hz::dd_add(pb, lb, hb);
+                }
+            }
+        }
+    }
+    double thra, thrb;
+    if constexpr (PROC == HZ_PROC_STATIC_GATE) {   // staticSTFT.h:99-128
+        const double avga = block_sum(pa, scratch), avgb = block_sum(pb, scratch);
+        thra = p0 * avga * avga;
+        thrb = p0 * avgb * avgb;
+    } else {   // tests/spectral.cpp:32-72 (sum / N in long double)
+        block_sum_dd(pa, la, scratch);
+        block_sum_dd(pb, lb, scratch);
+        const double qa = pa / N, qb = pb / N;
+        const double avga = qa + (fma(-qa, (double)N, pa) + la) / N;
+        const double avgb = qb + (fma(-qb, (double)N, pb) + lb) / N;
+        thra = p0 * avga * avga;
+        thrb = p0 * avgb * avgb;
+    }
+#pragma unroll
+    for (int i = 0; i < kPairItems; ++i) {
+        const int k = threadIdx.x + i * blockDim.x;
+        if (k > H) continue;
+        double xr = ar[i], xi = ai[i], yr = br[i], yi = bi[i];
+        if constexpr (PROC == HZ_PROC_STATIC_GATE) {
+            if (xr * xr + xi * xi < thra) {
+                xr = xr * p1;
+                xi = xi * p1;
+            }
+            if (yr * yr + yi * yi < thrb) {
+                yr = yr * p1;
+                yi = yi * p1;
+            }
+        } else {
+            if (!(xr * xr + xi * xi > thra)) xr = xi = 0.0;
+            if (!(yr * yr + yi * yi > thrb)) yr = yi = 0.0;
+        }
+        const int m = (N - k) & (N - 1);
+        const int ek = hz::pad16(hz::bitrev(k, lg)), em = hz::pad16(hz::bitrev(m, lg));
+        // Y_k = X_f + i X_{f+1};  Y_{N-k} = conj X_f + i conj X_{f+1}
+        re[ek] = xr - yi;
+        im[ek] = xi + yr;
+        if (m != k) {
+            re[em] = xr + yi;
+            im[em] = yr - xi;
+        }
+    }
+}
+
+template <int PROC, int RMAX>
+__global__ __launch_bounds__(kFrameThreads) void stft_pair_kernel(StftArgs a, long nf) {
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int N = a.N, lg = a.lg;
+    double* re = lds;
+    double* im = lds + hz::padded_len(N);
+    double* scratch = im + hz::padded_len(N);
+    double2* T = (double2*)(scratch + 2 * (blockDim.x >> 6));
+    for (int k = threadIdx.x; k < hz::twc_len(lg); k += blockDim.x) T[k] = a.tw[k];
+    const int pl = frame_of_block(blockIdx.x, gridDim.x);   // frame pair within the launch
+    const long f0 = a.f_lo + 2L * pl;
+    const bool two = 2L * pl + 1 < nf;
+    const long off0 = frame_start(f0, a.laps, a.stride, N) - a.T0 + (N - 1);
+    const long off1 = two ? frame_start(f0 + 1, a.laps, a.stride, N) - a.T0 + (N - 1) : 0;
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+        const long u0 = off0 + k, u1 = off1 + k;   // positions in [history (N-1) | block input]
+        const double v0 = u0 < N - 1 ? a.hr[u0] : a.inr[u0 - (N - 1)];
+        const double v1 = two ? (u1 < N - 1 ? a.hr[u1] : a.inr[u1 - (N - 1)]) : 0.0;
+        const double w = a.win[k];
+        const int e = hz::pad16(k);
+        re[e] = w * v0;   // fourier.h:110-112, real input
+        im[e] = w * v1;
+    }
+    __syncthreads();
+    hz::fft_fwd_lead<RMAX>(re, im, lg, T, true);
+    pair_gate<PROC>(re, im, lg, a.p0, a.p1, scratch);
+    __syncthreads();
+    hz::fft_inv_tail<RMAX>(re, im, lg, T, true);
+    const long plane = (long)a.R * N;
+    double* o0 = a.fo + (f0 % a.R) * N;
+    double* o1 = a.fo + ((f0 + 1) % a.R) * N;
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+        const int e = hz::pad16(k);
+        o0[k] = re[e];
+        o0[plane + k] = 0.0;
+        if (two) {
+            o1[k] = im[e];
+            o1[plane + k] = 0.0;
+        }
+    }
+}
+
 struct OlaArgs {
     const double* fo;   // planar ring (Re plane, then Im plane of R*N)
     const double* win;
@@ -448,6 +579,7 @@ struct hz_stft {
     bool prof = false;
     long chunk = 0;        // samples per internal block (a frame launch covers one)
     int prof_repeat = 1;   // frame launches per block while profiling (hz_stft_profile)
+    bool pair_ok = true;   // two real frames per transform (stft_pair_kernel); HZ_STFT_PAIR=0 turns it off
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     long launches = 0;
@@ -493,7 +625,28 @@ void launch_frames(hz_stft* h, const StftArgs& a, long nf) {
                            frame_lds(h->N), h->stream, a);
 }
 
+template <int PROC>
+void launch_pairs(hz_stft* h, const StftArgs& a, long nf) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)stft_pair_kernel<PROC, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)frame_lds(kMaxN));
+        attr = true;
+    }
+    hipLaunchKernelGGL((stft_pair_kernel<PROC, 3>), dim3((unsigned)((nf + 1) / 2)), dim3(frame_threads(h->N)),
+                       frame_lds(h->N), h->stream, a, nf);
+}
+
 int frames_fused(hz_stft* h, const StftArgs& a, long nf) {
+    // real input and a magnitude gate: two frames per transform (stft_pair_kernel)
+    const bool pair = h->pair_ok && !a.hi && frame_rmax(h->N) == 3 && h->N >= 16 &&
+                      (h->proc == HZ_PROC_STATIC_GATE || h->proc == HZ_PROC_GATE_KEEP);
+    if (pair) {
+        if (h->proc == HZ_PROC_STATIC_GATE) launch_pairs<HZ_PROC_STATIC_GATE>(h, a, nf);
+        else launch_pairs<HZ_PROC_GATE_KEEP>(h, a, nf);
+        HZ_TRY_HIP(hipGetLastError());
+        return HZ_OK;
+    }
     switch (h->proc) {
     case HZ_PROC_STATIC_GATE: launch_frames<HZ_PROC_STATIC_GATE, 0>(h, a, nf); break;
     case HZ_PROC_GATE_KEEP: launch_frames<HZ_PROC_GATE_KEEP, 0>(h, a, nf); break;
@@ -638,6 +791,7 @@ int hz_stft_create(int N, int laps, int window, int proc, double p0, double p1, 
     h->p0 = p0;
     h->p1 = p1;
     h->device = device;
+    if (const char* e = std::getenv("HZ_STFT_PAIR")) h->pair_ok = std::atoi(e) != 0;
     // frames completing inside one internal block, plus those still being read
     const long P = 2L * N - 1;
     auto ring = [&](long c) { return (c + P - 1) / P * 2 * laps + 2 * laps + 2; };
