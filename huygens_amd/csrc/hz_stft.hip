@@ -288,9 +288,11 @@ __global__ __launch_bounds__(kFrameThreads) void stft_frame_kernel(StftArgs a) {
 // each frame's gate on its own spectrum (its own average), Y = Y_f + i Y_{f+1} (both Hermitian),
 // and one inverse FFT gives y_f + i y_{f+1}.  Half the FFT work per frame; the Im output of a
 // real frame is written as 0 (the reference's complex transform leaves ~1e-17 there).
-constexpr int kPairItems = 5;   // bin pairs per thread: ceil((N/2 + 1) / (N/8)) for N >= 16
+// bin pairs per thread: ceil((N/2 + 1) / threads), threads = N/8 (radix 8) or N/16 (radix 16)
+template <int RMAX>
+__host__ __device__ constexpr int pair_items() { return RMAX == 3 ? 5 : 9; }
 
-template <int PROC>
+template <int PROC, int kPairItems>
 __device__ __forceinline__ void pair_gate(double* re, double* im, int lg, double p0, double p1, double* scratch) {
 #pragma clang fp contract(off)
     const int N = 1 << lg, H = N >> 1;
@@ -393,7 +395,7 @@ __global__ __launch_bounds__(kFrameThreads) void stft_pair_kernel(StftArgs a, lo
     }
     __syncthreads();
     hz::fft_fwd_lead<RMAX>(re, im, lg, T, true);
-    pair_gate<PROC>(re, im, lg, a.p0, a.p1, scratch);
+    pair_gate<PROC, pair_items<RMAX>()>(re, im, lg, a.p0, a.p1, scratch);
     __syncthreads();
     hz::fft_inv_tail<RMAX>(re, im, lg, T, true);
     const long plane = (long)a.R * N;
@@ -631,15 +633,21 @@ void launch_pairs(hz_stft* h, const StftArgs& a, long nf) {
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)stft_pair_kernel<PROC, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)frame_lds(kMaxN));
+        (void)hipFuncSetAttribute((const void*)stft_pair_kernel<PROC, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)frame_lds(kMaxN));
         attr = true;
     }
-    hipLaunchKernelGGL((stft_pair_kernel<PROC, 3>), dim3((unsigned)((nf + 1) / 2)), dim3(frame_threads(h->N)),
-                       frame_lds(h->N), h->stream, a, nf);
+    if (frame_rmax(h->N) == 3)
+        hipLaunchKernelGGL((stft_pair_kernel<PROC, 3>), dim3((unsigned)((nf + 1) / 2)), dim3(frame_threads(h->N)),
+                           frame_lds(h->N), h->stream, a, nf);
+    else
+        hipLaunchKernelGGL((stft_pair_kernel<PROC, 4>), dim3((unsigned)((nf + 1) / 2)), dim3(frame_threads(h->N)),
+                           frame_lds(h->N), h->stream, a, nf);
 }
 
 int frames_fused(hz_stft* h, const StftArgs& a, long nf) {
     // real input and a magnitude gate: two frames per transform (stft_pair_kernel)
-    const bool pair = h->pair_ok && !a.hi && frame_rmax(h->N) == 3 && h->N >= 16 &&
+    const bool pair = h->pair_ok && !a.hi && h->N >= 16 &&
                       (h->proc == HZ_PROC_STATIC_GATE || h->proc == HZ_PROC_GATE_KEEP);
     if (pair) {
         if (h->proc == HZ_PROC_STATIC_GATE) launch_pairs<HZ_PROC_STATIC_GATE>(h, a, nf);

@@ -108,6 +108,22 @@ def test_fourier_gates_c4(gpu_lib, proc):
     assert peak_err(gr, orr) < TOL and peak_err(gi, oi) < TOL
 
 
+@pytest.mark.parametrize("N,laps", [(4096, 4), (8192, 32), (256, 4)])
+def test_gate_keep_real_pairs(gpu_lib, N, laps):
+    """spectral.cpp 625 gate on real input: two frames share one transform
+    (stft_pair_kernel, radix 8 and radix 16); ragged calls, odd frame counts per launch."""
+    g, o = make(N, laps, 0, 2)
+    n = 7 * N + 5
+    x = c4_signal(n)
+    if N < 1024:   # a short frame needs one dominant bin to clear 25x the average magnitude
+        x = np.sin(2 * np.pi * 8 * np.arange(n) / N) + 0.01 * np.random.default_rng(5).standard_normal(n)
+    cut = [0, N // 3, 3 * N + 1, n]
+    parts = [g.process_block(x[a:b])[0] for a, b in zip(cut[:-1], cut[1:])]
+    ref = o.process_block(x)[0]
+    assert np.max(np.abs(ref)) > 0.05
+    assert peak_err(np.concatenate(parts), ref) < TOL
+
+
 def test_host_callback_stateful(gpu_lib):
     """A host processor runs per frame in frame order with each slot's `out` persisting
     (fourier.h:57-59): this one accumulates into out instead of overwriting it."""
