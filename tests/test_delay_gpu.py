@@ -51,6 +51,29 @@ def test_c5_bank(gpu_lib, split):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_streamed_mix_calls(gpu_lib, dtype):
+    """Streamed mixed calls (C5's pattern): bit-exact against the restatement across calls,
+    incl. an age-0 feedback tap (delay = ring size: the partial sum), per-line input, a call
+    longer than the shortest feedback age (serial sub-blocks) and one-sample calls."""
+    rng = np.random.default_rng(11)
+    N, S, time = 70, 3, 3000
+    g, o = _pair(N, S, time, dtype)
+    for k in range(N):
+        fwd = [(int(rng.integers(0, 1800)), float(rng.uniform(-1, 1))) for _ in range(S)]
+        back = [(int(rng.integers(1100, 1900)), float(rng.uniform(-0.3, 0.3))) for _ in range(S - 1)]
+        if k == 5:
+            back[1] = (time + 1, 0.25)   # age 0: reads the sample's own partial sum
+        g.coefficients(k, fwd, back)
+        o.coefficients(k, fwd, back)
+    for i, n in enumerate([1024, 1024, 1000, 64, 1, 1024, 2500, 1024]):
+        x = rng.standard_normal((N, n) if i % 3 == 2 else n).astype(dtype)
+        assert np.array_equal(g.process(x, mix=True), o.process(x, mix=True)), (i, n)
+    assert g.origin() == o.origin()
+    x = rng.standard_normal(1024).astype(dtype)   # the per-line outputs after fused calls
+    assert np.array_equal(g.process(x), o.process(x))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_random_taps_wrap_and_short_feedback(gpu_lib, dtype):
     """Random taps incl. delays longer than the ring (uint wrap), feedback age 1 (serial
     sub-blocks), zero-time feedback, per-line input, calls longer than the ring."""
