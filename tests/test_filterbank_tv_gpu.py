@@ -85,6 +85,23 @@ def test_smoothers_and_distortion(gpu_lib):
     assert rel_err(g.process_tv(x[1000:], 0, st[1000:]), o.process_tv(x[1000:], 0, st[1000:])) <= TOL
 
 
+@pytest.mark.parametrize("dist", ["HZ_DIST_SOFTCLIP", "HZ_DIST_SATURATE", "HZ_DIST_LIMITER"])
+def test_resonant_stream_distortion(gpu_lib, dist):
+    """Resonant streams through the producer/consumer kernel with each per-band distortion
+    functor, ragged calls (tile remainders, a 1-sample call) and a bank of 130 bands (partial
+    last workgroup)."""
+    from huygens_amd import _lib
+    N = 130
+    g, o = pair(2, N, 29, k_p=0.02, k_g=0.03)
+    for fb in (g, o):
+        fb.distortion(getattr(_lib, dist), 0.3)
+    n = 2000
+    fr = subtractive_freqs(n, N, 29)
+    x = 4 * np.random.default_rng(29).uniform(-1, 1, n)
+    for a, b in [(0, 31), (31, 32), (32, 1500), (1500, n)]:
+        assert rel_err(g.process_tv(x[a:b], 1, fr[a:b], 0.999), o.process_tv(x[a:b], 1, fr[a:b], 0.999)) <= TOL
+
+
 def test_device_pointers(gpu_lib):
     import torch
     O, N, n = 2, 128, 2048
