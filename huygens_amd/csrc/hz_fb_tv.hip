@@ -69,10 +69,19 @@ __device__ __forceinline__ void cdiv(double a, double b, double c, double d, dou
     }
 }
 
+// x / SR correctly rounded without the IEEE divide sequence: q = x RN(1/SR), then one FMA
+// residual step (Markstein; x >= 0 normal here).  Equal to x / 48000.0 -- checked on the
+// host over 2e8 random doubles, no mismatch.
+__device__ __forceinline__ double div_sr(double x) {
+    constexpr double inv = 1.0 / hz::kSR;
+    const double q = x * inv;
+    return __builtin_fma(__builtin_fma(-q, (double)hz::kSR, x), inv, q);
+}
+
 // subtractive.h:240-249
 __device__ __forceinline__ double resonant(double frequency, double Q) {
     double s2, c2;
-    sincos(4 * hz::kPI * frequency / hz::kSR, &s2, &c2);
+    sincos(div_sr(4 * hz::kPI * frequency), &s2, &c2);
     const double ir = 0.0 * s2 - 1.0 * 0.0, ii = 0.0 * 0.0 + 1.0 * s2;   // 1.0i * sine2
     const double dr = (Q - c2) - ir, di = -0.0 - ii;
     double qr, qi;
@@ -248,7 +257,7 @@ __global__ __launch_bounds__(kResThreads) void fb_tv_res_kernel(TvArgs a) {
 #pragma unroll
                 for (int i = 0; i < kResPer; ++i) {
                     const int j = pw * kResPer + i;
-                    const double cosine = cos(2 * hz::kPI * fr[i] / hz::kSR);
+                    const double cosine = cos(div_sr(2 * hz::kPI * fr[i]));
                     const double g = resonant(fr[i], R);
                     gb[c][j][lane] = g;
                     bb[c][j][lane] = -2 * R * cosine;
