@@ -174,6 +174,7 @@ struct LtiArgs {
     long seg_len;           // multiple of the tile (64 L)
     int nseg;
     int nseg_state;         // segments in segstate (the prepass splits a segment in seg_stride)
+    long seg_skip;          // prepass only: start this many samples into the segment (horizon)
     int seg_stride;         // segstate index of segment s: s * seg_stride
     int nbands;
     double sp_n, sg_n;      // sp^n, sg^n (closed-form smoother end state)
@@ -256,8 +257,11 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     const double* r = rec + (long)bandc * R::SIZE;
     const long n = a.n;
     const int seg = blockIdx.y;
-    const long seg_t0 = (long)seg * a.seg_len;
-    const long seg_end = min(seg_t0 + a.seg_len, n);
+    const long seg_base = (long)seg * a.seg_len;
+    // the prepass may start past the segment's head: older input reaches the end state only
+    // through M^k with ||M^k|| < 2^-100 (fb_lti_horizon)
+    const long seg_t0 = seg_base + (MODE == MODE_SEGEND ? a.seg_skip : 0);
+    const long seg_end = min(seg_base + a.seg_len, n);
     const int ntiles = (int)((seg_end - seg_t0 + T - 1) / T);
     const bool last_seg = seg == a.nseg - 1;
 
@@ -762,6 +766,55 @@ bool fb_converged(hz_fb* h) {
     return true;
 }
 
+// Samples K (a multiple of 4096) after which every band's state transition satisfies
+// ||M^K||_inf < 2^-100 (long double, powers of M^4096); -1 if some band needs more than 2^18.
+// Segment start states then depend on the last K samples of input only (to 2^-100 of the
+// state), so the prepass can skip a segment's head.
+static long fb_lti_horizon(const hz_fb* h) {
+    const int O = h->order;
+    if (O == 0) return 0;
+    typedef long double ld;
+    long K = 0;
+    for (int b = 0; b < h->N; ++b) {
+        ld M[kMaxOrder][kMaxOrder] = {}, P[kMaxOrder][kMaxOrder], Q[kMaxOrder][kMaxOrder], T[kMaxOrder][kMaxOrder];
+        for (int k = 0; k < O; ++k) M[0][k] = -(ld)h->B[(size_t)b * O + k];
+        for (int k = 1; k < O; ++k) M[k][k - 1] = 1;
+        auto mul = [&](ld (*A)[kMaxOrder], ld (*B)[kMaxOrder], ld (*C)[kMaxOrder]) {
+            for (int i = 0; i < O; ++i)
+                for (int j = 0; j < O; ++j) {
+                    ld acc = 0;
+                    for (int q = 0; q < O; ++q) acc += A[i][q] * B[q][j];
+                    T[i][j] = acc;
+                }
+            for (int i = 0; i < O; ++i)
+                for (int j = 0; j < O; ++j) C[i][j] = T[i][j];
+        };
+        for (int i = 0; i < O; ++i)
+            for (int j = 0; j < O; ++j) P[i][j] = M[i][j];
+        for (int s = 0; s < 12; ++s) mul(P, P, P);   // M^4096
+        for (int i = 0; i < O; ++i)
+            for (int j = 0; j < O; ++j) Q[i][j] = (i == j);
+        long kb = -1;
+        for (int it = 1; it <= 64; ++it) {
+            mul(Q, P, Q);
+            ld nrm = 0;
+            for (int i = 0; i < O; ++i) {
+                ld r = 0;
+                for (int j = 0; j < O; ++j) r += std::fabs(Q[i][j]);
+                nrm = std::max(nrm, r);
+            }
+            if (!(nrm == nrm)) break;   // NaN: unstable
+            if (nrm < 0x1p-100L) {
+                kb = 4096L * it;
+                break;
+            }
+        }
+        if (kb < 0) return -1;
+        K = std::max(K, kb);
+    }
+    return K;
+}
+
 int fb_prepare_lti(hz_fb* h, int gi) {
     const int O = h->order;
     const int L = kLtiGeoms[gi].L;
@@ -783,6 +836,7 @@ int fb_prepare_lti(hz_fb* h, int gi) {
         HZ_TRY_HIP(hipStreamSynchronize(h->stream));  // pageable source
         set.rs = rs;
         set.dirty = false;
+        set.horizon = -2;
         set.fmix_valid = false;
     }
     if (!set.fmix_valid) {
@@ -800,7 +854,7 @@ constexpr long kShortReduce = 1L << 16;   // calls up to this length use the sli
 
 int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
     HZ_TRY(fb_prepare_lti(h, gi));
-    const hz_fb::LtiRecSet& set = h->lti_set[gi];
+    hz_fb::LtiRecSet& set = h->lti_set[gi];
     const int O = h->order;
     const LtiGeom geom = kLtiGeoms[gi];
     const int L = geom.L;
@@ -876,7 +930,9 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         // (the coarse segment may grow to a multiple of m tiles, by at most 1/32: fine boundaries
         // must fall on coarse ones)
         int m = 1;
+        long skip_tiles = 0;
         if (nseg > 1) {
+            const long seg_tiles0 = seg_tiles, nseg0 = nseg;
             double best = 1.0;
             long best_tiles = seg_tiles;
             for (int c = 2; c <= 8; ++c) {
@@ -893,6 +949,20 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             }
             seg_tiles = best_tiles;
             nseg = (ntiles + seg_tiles - 1) / seg_tiles;
+            // ... or, when every band forgets its state within a horizon K shorter than a
+            // segment, a prepass over only the last ceil(K / T) + 1 tiles of each segment
+            if (set.horizon == -2) set.horizon = fb_lti_horizon(h);
+            if (set.horizon >= 0) {
+                const long kt = (set.horizon + T - 1) / T + 1;
+                const double cost =
+                    (double)((G * (nseg0 - 1) + h->target_groups - 1) / h->target_groups) * kt / seg_tiles0;
+                if (kt < seg_tiles0 && cost < best - 1e-3) {
+                    m = 1;
+                    seg_tiles = seg_tiles0;
+                    nseg = nseg0;
+                    skip_tiles = seg_tiles0 - kt;
+                }
+            }
         }
         const long nseg_state = (nseg - 1) * m + 1;
         if (nseg > 1) {
@@ -924,6 +994,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         a.nseg = (int)nseg;
         a.nseg_state = (int)nseg_state;
         a.seg_stride = m;
+        a.seg_skip = 0;
         a.nbands = h->N;
         a.sp_n = (double)powl((long double)h->sp, (long double)len);
         a.sg_n = (double)powl((long double)h->sg, (long double)len);
@@ -939,6 +1010,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             af.seg_len = seg_tiles / m * T;
             af.nseg = (int)nseg_state + 1;
             af.seg_stride = 1;
+            af.seg_skip = skip_tiles * T;
             hipLaunchKernelGGL(kend, dim3(G, (unsigned)(nseg_state - 1)), dim3(64 * lti_waves(O)), lds_end,
                                h->stream, (const double*)set.d_rec, af);
             HZ_TRY_HIP(hipGetLastError());

@@ -111,6 +111,18 @@ def test_fine_prepass_segments_lti(gpu_lib, N, groups, calls):
     run_calls(g, o, calls, seed=22)
 
 
+@pytest.mark.parametrize("R", [0.99, 0.995])
+def test_horizon_prepass_lti(gpu_lib, R):
+    """Fast-decaying banks: every band forgets its state within a horizon K shorter than a
+    segment (||M^K|| < 2^-100), so the segment prepass covers only each segment's last
+    ceil(K / T) + 1 tiles (hz_fb_lti.hip, fb_lti_horizon)."""
+    N = 64
+    fwd, back = resonant_coefficients(N, R, 0.5)
+    g, o = make_pair(2, N, fwd, back)
+    g.set_target_groups(16)
+    run_calls(g, o, [500, 98304, 2048 * 40 + 96, 3000], seed=23)
+
+
 def test_path_switches_with_setters(gpu_lib):
     """A setter change un-converges the smoothers: the next call runs the general
     engine, later calls return to LTI; the mixes stay on the oracle throughout."""
