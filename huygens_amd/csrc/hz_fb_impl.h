@@ -97,7 +97,7 @@ struct hz_fb {
         double* d_rec = nullptr;
         size_t cap = 0;
         double* d_fmix = nullptr;    // [L][L+O]
-        long horizon = -2;           // samples after which ||M^k|| < 2^-100 for every band
+        long horizon = -2;           // samples after which ||M^k|| < 2^-64 for every band
                                      // (-1: none within 2^18; -2: not computed yet)
     } lti_set[2];
     std::vector<double> pg_host;     // host mirror of the smoother state [N][2] (pre, gain)

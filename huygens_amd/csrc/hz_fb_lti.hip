@@ -259,7 +259,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     const int seg = blockIdx.y;
     const long seg_base = (long)seg * a.seg_len;
     // the prepass may start past the segment's head: older input reaches the end state only
-    // through M^k with ||M^k|| < 2^-100 (fb_lti_horizon)
+    // through M^k with ||M^k|| < 2^-64 (fb_lti_horizon)
     const long seg_t0 = seg_base + (MODE == MODE_SEGEND ? a.seg_skip : 0);
     const long seg_end = min(seg_base + a.seg_len, n);
     const int ntiles = (int)((seg_end - seg_t0 + T - 1) / T);
@@ -767,8 +767,8 @@ bool fb_converged(hz_fb* h) {
 }
 
 // Samples K (a multiple of 4096) after which every band's state transition satisfies
-// ||M^K||_inf < 2^-100 (long double, powers of M^4096); -1 if some band needs more than 2^18.
-// Segment start states then depend on the last K samples of input only (to 2^-100 of the
+// ||M^K||_inf < 2^-64 (long double, powers of M^4096); -1 if some band needs more than 2^18.
+// Segment start states then depend on the last K samples of input only (to 2^-64 of the
 // state), so the prepass can skip a segment's head.
 static long fb_lti_horizon(const hz_fb* h) {
     const int O = h->order;
@@ -804,7 +804,7 @@ static long fb_lti_horizon(const hz_fb* h) {
                 nrm = std::max(nrm, r);
             }
             if (!(nrm == nrm)) break;   // NaN: unstable
-            if (nrm < 0x1p-100L) {
+            if (nrm < 0x1p-64L) {
                 kb = 4096L * it;
                 break;
             }

@@ -114,7 +114,7 @@ def test_fine_prepass_segments_lti(gpu_lib, N, groups, calls):
 @pytest.mark.parametrize("R", [0.99, 0.995])
 def test_horizon_prepass_lti(gpu_lib, R):
     """Fast-decaying banks: every band forgets its state within a horizon K shorter than a
-    segment (||M^K|| < 2^-100), so the segment prepass covers only each segment's last
+    segment (||M^K|| < 2^-64), so the segment prepass covers only each segment's last
     ceil(K / T) + 1 tiles (hz_fb_lti.hip, fb_lti_horizon)."""
     N = 64
     fwd, back = resonant_coefficients(N, R, 0.5)
