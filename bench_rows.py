@@ -180,7 +180,7 @@ def run_c4(args, torch, dev):
     traffic, tdetail = None, "not collected (--no-traffic)"
     if not args.no_traffic:
         import bench
-        tb, tdetail = bench.pmc_traffic("stft_frame_kernel<1,", extra=("--workload", "c4"))
+        tb, tdetail = bench.pmc_traffic("stft_pair_kernel<1,", extra=("--workload", "c4"))
         traffic = tb   # HBM bytes per frame launch (one launch per step here)
     return {
         "metric": "STFT frames/s, StaticSTFT 4096-pt / 75% overlap spectral gate",
@@ -193,7 +193,8 @@ def run_c4(args, torch, dev):
         "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK if achieved else None,
                      "traffic": traffic, "traffic_detail": tdetail,
-                     "kernel": "stft_frame_kernel<STATIC_GATE,0> (window+FFT+gate+IFFT in LDS)",
+                     "kernel": "stft_pair_kernel<STATIC_GATE,3> (two real frames per transform: window, "
+                               "FFT, split + gate + merge, IFFT in LDS)",
                      "kernel_ms_per_step": fms / args.steps, "ola_ms_per_step": oms / args.steps,
                      "flops_per_frame": 491520},
         "variant_fourier_gate625": {"frames_per_s": fr2 / e2, "kernel_ms_per_step": f2 / args.steps,
