@@ -592,7 +592,7 @@ def run_c9(args, torch, dev):
     traffic, tdetail = None, "not collected (--no-traffic)"
     if not args.no_traffic:
         import bench
-        traffic, tdetail = bench.pmc_traffic("fb_tv_kernel", extra=("--workload", "c9"))
+        traffic, tdetail = bench.pmc_traffic("fb_tv_res_kernel", extra=("--workload", "c9"))
     # raw coefficient streams: [n][5][N] (40 B per band-sample), 4800 samples
     n2 = min(S, 4800)
     st = torch.zeros((n2, 5, N), dtype=torch.float64, device=dev)
@@ -655,12 +655,13 @@ def run_c9(args, torch, dev):
                    "samples_per_step": S, "order": 2, "R": R, "kind": "HZ_FB_TV_RESONANT"},
         "roofline": {"bound": "valu", "achieved": tflops, "peak": FP64_PEAK, "unit": "TFLOP/s",
                      "frac": tflops / FP64_PEAK if tflops else None, "traffic": traffic,
-                     "traffic_detail": tdetail, "kernel": "fb_tv_kernel<2, RESONANT, NONE>",
+                     "traffic_detail": tdetail, "kernel": "fb_tv_res_kernel<NONE> (15 producer waves + 1 recurrence wave per 64 bands)",
                      "kernel_ms_per_step": mix_ms / args.steps, "mix_reduce_ms_per_step": red_ms / args.steps,
                      "launches_per_step": launches / args.steps, "flops_per_unit": 49,
                      "algorithmic_bytes_per_unit": 8, "hbm_achieved_gbs": gbs,
-                     "note": "one wave per 64 bands, sequential in time: 256 waves for 16384 bands; "
-                             "cos, sincos, 4 divides, hypot, sqrt counted as 1 flop each"},
+                     "note": "coefficients time-parallel in 15 producer waves, the recurrence sequential "
+                             "in one wave per 64 bands (DESIGN.md 4.5); cos, sincos, 4 divides, hypot, sqrt "
+                             "counted as 1 flop each"},
         "variant_coeff_stream": coeffs,
         "instrument_49_bands": inst,
         "cpu_baseline": cpu,
