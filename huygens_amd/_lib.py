@@ -206,6 +206,8 @@ _SIGS = {
     "hz_frz_info": (I, [VP, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
     "hz_frz_set_stream": (I, [VP, VP]),
     "hz_frz_synchronize": (I, [VP]),
+    "hz_frz_profile": (I, [VP, I]),
+    "hz_frz_profile_read": (I, [VP, C.POINTER(C.c_double), C.POINTER(C.c_long)]),
 }
 
 

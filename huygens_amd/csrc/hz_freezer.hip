@@ -226,6 +226,10 @@ struct hz_frz {
     size_t in_cap = 0, out_cap = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    bool prof = false;                 // HIP events around each frz_out_kernel launch
+    std::vector<hipEvent_t> ev;
+    size_t ev_used = 0;
+    long launches = 0;
 };
 
 namespace {
@@ -403,9 +407,25 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
     a.stride = h->stride;
     a.readsize = h->size;
     if (n > 0) {
+        hipEvent_t* e = nullptr;
+        if (h->prof) {
+            if (h->ev_used + 2 > h->ev.size())
+                for (int q = 0; q < 64; ++q) {
+                    hipEvent_t ne;
+                    HZ_TRY_HIP(hipEventCreate(&ne));
+                    h->ev.push_back(ne);
+                }
+            e = &h->ev[h->ev_used];
+            h->ev_used += 2;
+            HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
+        }
         hipLaunchKernelGGL(frz_out_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
                            h->stream, a);
         HZ_TRY_HIP(hipGetLastError());
+        if (e) {
+            HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
+            ++h->launches;
+        }
     }
     // carry: IFrame state <- latest content (before the open period's frames are replaced)
     for (int q = 0; q < M; ++q)
@@ -520,8 +540,32 @@ int hz_frz_destroy(hz_frz* h) {
                     (void*)h->d_ifnew, (void*)h->d_snap, h->d_tab, (void*)h->d_in,
                     (void*)h->d_out})
         if (p) (void)hipFree(p);
+    for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
+    return HZ_OK;
+}
+
+int hz_frz_profile(hz_frz* h, int enable) {
+    HZ_TRY(frz_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    h->prof = enable != 0;
+    h->ev_used = 0;
+    h->launches = 0;
+    return HZ_OK;
+}
+
+int hz_frz_profile_read(hz_frz* h, double* ms, long* launches) {
+    HZ_TRY(frz_check(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    double m = 0;
+    for (size_t i = 0; i + 2 <= h->ev_used; i += 2) {
+        float x = 0;
+        HZ_TRY_HIP(hipEventElapsedTime(&x, h->ev[i], h->ev[i + 1]));
+        m += x;
+    }
+    if (ms) *ms = m;
+    if (launches) *launches = h->launches;
     return HZ_OK;
 }
 

@@ -69,3 +69,12 @@ class Freezer:
 
     def synchronize(self):
         check(self._lib.hz_frz_synchronize(self._h))
+
+    def profile(self, enable: bool):
+        """HIP-event timing of the output kernel's launches while enabled."""
+        check(self._lib.hz_frz_profile(self._h, 1 if enable else 0))
+
+    def profile_read(self):
+        ms, n = C.c_double(), C.c_long()
+        check(self._lib.hz_frz_profile_read(self._h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value

@@ -322,6 +322,9 @@ int hz_frz_process_device(hz_frz* h, const double* d_in, double* d_out, size_t n
 int hz_frz_info(hz_frz* h, int* stride, int* frames, int* frozen);
 int hz_frz_set_stream(hz_frz* h, void* hip_stream);
 int hz_frz_synchronize(hz_frz* h);
+/* HIP-event timing of the output kernel (frz_out_kernel) launches while enabled */
+int hz_frz_profile(hz_frz* h, int enable);
+int hz_frz_profile_read(hz_frz* h, double* ms, long* launches);
 
 /* ---- Filterbank with per-sample coefficient streams ----
  * Subtractive ALLINONE / ONEPERVOICE (src/subtractive.h:215-228, 300-317) retune every band
