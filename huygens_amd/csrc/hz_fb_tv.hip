@@ -78,6 +78,21 @@ __device__ __forceinline__ double div_sr(double x) {
     return __builtin_fma(__builtin_fma(-q, (double)hz::kSR, x), inv, q);
 }
 
+// cdiv(1, 0, c, d): both quotients share the denominator, so one IEEE reciprocal r = RN(1/den)
+// serves both: -1/den = -r exactly, and n/den = RN(n r + RN(n - den RN(n r)) r) (Markstein: the
+// FMA residual step of a correctly rounded reciprocal gives the correctly rounded quotient).
+// Equal to cdiv(1.0, 0.0, c, d) up to the sign of a zero, which nothing downstream sees.
+__device__ __forceinline__ void cdiv_one(double c, double d, double& x, double& y) {
+    const bool lt = fabs(c) < fabs(d);
+    const double ratio = lt ? c / d : d / c;
+    const double den = lt ? (c * ratio) + d : (d * ratio) + c;
+    const double r = 1.0 / den;
+    const double q0 = ratio * r;
+    const double q = __builtin_fma(__builtin_fma(-q0, den, ratio), r, q0);   // RN(ratio / den)
+    x = lt ? q : r;
+    y = lt ? -r : -q;
+}
+
 // subtractive.h:240-249
 __device__ __forceinline__ double resonant(double frequency, double Q) {
     double s2, c2;
@@ -85,7 +100,7 @@ __device__ __forceinline__ double resonant(double frequency, double Q) {
     const double ir = 0.0 * s2 - 1.0 * 0.0, ii = 0.0 * 0.0 + 1.0 * s2;   // 1.0i * sine2
     const double dr = (Q - c2) - ir, di = -0.0 - ii;
     double qr, qi;
-    cdiv(1.0, 0.0, dr, di, qr, qi);
+    cdiv_one(dr, di, qr, qi);
     const double mr = 1.0 / (Q - 1) - qr, mi = 0.0 - qi;
     return 1 / sqrt(hypot(mr, mi));
 }
