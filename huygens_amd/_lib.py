@@ -20,6 +20,7 @@ HZ_E_HIP = -3
 HZ_E_NODEV = -4
 HZ_E_ALLOC = -5
 HZ_E_UNSUPPORTED = -6
+HZ_E_STATE = -7
 
 HZ_FB_PATH_AUTO = 0
 HZ_FB_PATH_GENERAL = 1
@@ -33,6 +34,7 @@ HZ_DIST_LIMITER = 3
 _ERRNAMES = {
     HZ_E_INVALID: "HZ_E_INVALID", HZ_E_RANGE: "HZ_E_RANGE", HZ_E_HIP: "HZ_E_HIP",
     HZ_E_NODEV: "HZ_E_NODEV", HZ_E_ALLOC: "HZ_E_ALLOC", HZ_E_UNSUPPORTED: "HZ_E_UNSUPPORTED",
+    HZ_E_STATE: "HZ_E_STATE",
 }
 
 
@@ -69,6 +71,7 @@ _SIGS = {
     "hz_fb_set_distortion": (I, [VP, I, D]),
     "hz_fb_process": (I, [VP, PD, PD, SZ]),
     "hz_fb_process_device": (I, [VP, VP, VP, SZ]),
+    "hz_fb_tick": (I, [VP]),
     "hz_fb_process_tv": (I, [VP, PD, PD, SZ, I, PD, D]),
     "hz_fb_process_tv_device": (I, [VP, VP, VP, SZ, I, VP, D]),
     "hz_fb_set_stream": (I, [VP, VP]),
@@ -85,6 +88,7 @@ _SIGS = {
     "hz_fb_set_path": (I, [VP, I]),
     "hz_fb_last_path": (I, [VP, C.POINTER(I)]),
     "hz_fb_tune_lti": (I, [VP, I, I, I]),
+    "hz_fb_lti_plan": (I, [VP, C.POINTER(C.c_long), C.POINTER(C.c_long), C.POINTER(C.c_int)]),
     # Oscbank
     "hz_osc_create": (I, [I, D, I, C.POINTER(VP)]),
     "hz_osc_create_shard": (I, [I, I, I, D, I, C.POINTER(VP)]),

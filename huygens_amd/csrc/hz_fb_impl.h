@@ -71,6 +71,14 @@ struct hz_fb {
     int scur = 0;  // current state buffer (ping-pong per launch)
     double* d_xhist[2] = {nullptr, nullptr};
     int xcur = 0;
+    // the reference's rings hold O+1 rows; the row the engine state (O rows) leaves out sits in
+    // d_ystate[scur ^ 1][.][O-1] / d_xhist[xcur ^ 1][O-1] after a 1-sample call or a tick
+    // (hz_fb_tick), and is not kept after longer calls
+    bool spare_ok = true;
+    // plan of the last LTI launch (hz_fb_lti_plan): time segments, prepass tiles skipped per
+    // segment (horizon), fine prepass parts per segment
+    long plan_nseg = 0, plan_skip_tiles = 0;
+    int plan_fine = 0;
     double* d_partial = nullptr;
     size_t partial_cap = 0;  // doubles
     double* d_seg = nullptr;  // segment start states

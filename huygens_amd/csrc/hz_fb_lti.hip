@@ -965,6 +965,9 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             }
         }
         const long nseg_state = (nseg - 1) * m + 1;
+        h->plan_nseg = nseg;
+        h->plan_skip_tiles = skip_tiles;
+        h->plan_fine = m;
         if (nseg > 1) {
             const size_t sneed = (size_t)h->N * nseg_state * O;
             if (sneed > h->seg_cap) {
@@ -1055,6 +1058,14 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
 }  // namespace hz_fbi
 
 extern "C" {
+
+int hz_fb_lti_plan(hz_fb* h, long* nseg, long* skip_tiles, int* fine_parts) {
+    if (!h) return HZ_E_INVALID;
+    if (nseg) *nseg = h->plan_nseg;
+    if (skip_tiles) *skip_tiles = h->plan_skip_tiles;
+    if (fine_parts) *fine_parts = h->plan_fine;
+    return HZ_OK;
+}
 
 int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group) {
     if (!h) return HZ_E_INVALID;

@@ -71,7 +71,7 @@ __device__ __forceinline__ void cdiv(double a, double b, double c, double d, dou
 
 // x / SR correctly rounded without the IEEE divide sequence: q = x RN(1/SR), then one FMA
 // residual step (Markstein; x >= 0 normal here).  Equal to x / 48000.0 -- checked on the
-// host over 2e8 random doubles, no mismatch.
+// host (tests/cpp/divcheck.c: random exponents, no mismatch).
 __device__ __forceinline__ double div_sr(double x) {
     constexpr double inv = 1.0 / hz::kSR;
     const double q = x * inv;
@@ -79,9 +79,12 @@ __device__ __forceinline__ double div_sr(double x) {
 }
 
 // cdiv(1, 0, c, d): both quotients share the denominator, so one IEEE reciprocal r = RN(1/den)
-// serves both: -1/den = -r exactly, and n/den = RN(n r + RN(n - den RN(n r)) r) (Markstein: the
-// FMA residual step of a correctly rounded reciprocal gives the correctly rounded quotient).
-// Equal to cdiv(1.0, 0.0, c, d) up to the sign of a zero, which nothing downstream sees.
+// serves both: -1/den = -r exactly, and ratio/den is taken as RN(q0 + RN(ratio - den q0) r),
+// q0 = RN(ratio r) (one FMA residual step).  Markstein's exactness theorem needs q0 within 1 ulp,
+// which RN(ratio r) does not guarantee (up to ~1.5 ulp), so exactness is checked, not proven:
+// tests/cpp/divcheck.c compares it bit for bit with the Smith quotient on random resonant()
+// operands, generic operands and targeted hard cases (quotient mantissa near 2, reciprocal error
+// near 1/2 ulp) -- no mismatch in ~1e9 trials.  The sign of a zero may differ; nothing sees it.
 __device__ __forceinline__ void cdiv_one(double c, double d, double& x, double& y) {
     const bool lt = fabs(c) < fabs(d);
     const double ratio = lt ? c / d : d / c;
@@ -497,6 +500,7 @@ int hz_fb_process_tv_device(hz_fb* h, const double* d_in, double* d_out, size_t 
         hz_fbi::fb_mirror_advance(h, len);
     }
     h->last_path = HZ_FB_PATH_GENERAL;
+    h->spare_ok = n == 1;   // see hz_fb_tick
     // the coefficients last set (the stream's final row) stay staged for later calls: copied
     // back without blocking, turned into F/B by fb_tv_materialize when next needed
     if ((size_t)row > h->tv_row_cap) {

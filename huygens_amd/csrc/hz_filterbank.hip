@@ -825,8 +825,31 @@ int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n) {
 
 namespace {
 
+// hz_fb_tick: the ring rotation of a tick() without compute (filterbank.h:142-148).  New
+// history = (spare row, cur[0 .. O-2]) into the other buffer; the smoothers are copied
+// unchanged.  The other buffer's oldest row is the spare and is read before it is overwritten.
+__global__ __launch_bounds__(256) void fb_tick_kernel(const double* __restrict__ ycur, double* __restrict__ yoth,
+                                                      const double* __restrict__ pgcur, double* __restrict__ pgoth,
+                                                      const double* __restrict__ xcur, double* __restrict__ xoth,
+                                                      int N, int O) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < N) {
+        const double spare = yoth[(long)b * O + O - 1];
+        for (int k = O - 1; k >= 1; --k) yoth[(long)b * O + k] = ycur[(long)b * O + k - 1];
+        yoth[(long)b * O] = spare;
+        pgoth[2 * (long)b] = pgcur[2 * (long)b];
+        pgoth[2 * (long)b + 1] = pgcur[2 * (long)b + 1];
+    }
+    if (b == 0) {
+        const double spare = xoth[O - 1];
+        for (int k = O - 1; k >= 1; --k) xoth[k] = xcur[k - 1];
+        xoth[0] = spare;
+    }
+}
+
 int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
     if (n <= 0) return HZ_OK;
+    h->spare_ok = n == 1;   // one launch, one state flip: the pre-call state is the spare row
     h->last_path = HZ_FB_PATH_GENERAL;
     const int geom = fb_lti_geom(h, n);
     const int L = fb_lti_chunk(geom);
@@ -1145,6 +1168,26 @@ int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
     std::memcpy(h->pg_host.data(), buf + O + N * O, sizeof(double) * N * 2);
     h->mirror_pending = 0;
     h->converged = false;
+    h->spare_ok = false;
+    return HZ_OK;
+}
+
+int hz_fb_tick(hz_fb* h) {
+    HZ_TRY(fb_check(h));
+    const int O = h->order;
+    if (O == 0) return HZ_OK;   // one-row rings: origin stays 0, nothing moves
+    if (!h->spare_ok) {
+        hz::set_error("hz_fb_tick: tick() without operator() after a block call or set_state: the ring row "
+                      "it would reuse (O+1 samples back) is not kept");
+        return HZ_E_STATE;
+    }
+    const int N = h->N;
+    hipLaunchKernelGGL(fb_tick_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, h->stream,
+                       (const double*)h->d_ystate[h->scur], h->d_ystate[h->scur ^ 1], (const double*)h->d_pg[h->scur],
+                       h->d_pg[h->scur ^ 1], (const double*)h->d_xhist[h->xcur], h->d_xhist[h->xcur ^ 1], N, O);
+    HZ_TRY_HIP(hipGetLastError());
+    h->scur ^= 1;
+    h->xcur ^= 1;
     return HZ_OK;
 }
 

@@ -124,7 +124,11 @@ class Filterbank:
         return self._cached
 
     def tick(self):
-        """tick() (filterbank.h:142-148); the GPU state advanced in operator()."""
+        """tick() (filterbank.h:142-148).  After operator() the GPU state already advanced
+        there; without one, hz_fb_tick moves the ring as the reference does (nothing computed,
+        smoothers still, the row from O+1 samples back becomes the newest history row)."""
+        if not self._computed:
+            check(self._lib.hz_fb_tick(self._h))
         self._computed = False
 
     # ---- stream / state ------------------------------------------------------
@@ -175,6 +179,13 @@ class Filterbank:
     def lti_chunk(self) -> int:
         """Samples per lane chunk of the selected LTI geometry."""
         return {0: 16, 1: 32}.get(self._lti_geom, 32)
+
+    def lti_plan(self):
+        """-> (time segments, prepass tiles skipped per segment, fine prepass parts) of the
+        last LTI launch (hz_fb_lti_plan)."""
+        a, b, c = C.c_long(), C.c_long(), C.c_int()
+        check(self._lib.hz_fb_lti_plan(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
 
     def set_target_groups(self, groups: int):
         check(self._lib.hz_fb_set_target_groups(self._h, groups))

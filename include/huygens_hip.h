@@ -38,6 +38,7 @@ extern "C" {
 #define HZ_E_NODEV (-4)   /* no gfx950 device visible                         */
 #define HZ_E_ALLOC (-5)   /* device or host allocation failed                 */
 #define HZ_E_UNSUPPORTED (-6)
+#define HZ_E_STATE (-7)   /* the call needs state the handle does not keep        */
 
 /* per-band distortion functors replacing T(*)(T) in
  * Filterbank::operator()(T, T(*)(T)) (src/filterbank.h:133-139) */
@@ -76,6 +77,14 @@ int hz_fb_set_distortion(hz_fb* h, int dist_id, double param);
 /* n x { out[i] = operator()(in[i]); tick(); }  (filterbank.h:125-148) */
 int hz_fb_process(hz_fb* h, const double* in, double* out, size_t n);
 int hz_fb_process_device(hz_fb* h, const double* d_in, double* d_out, size_t n);
+/* tick() WITHOUT a preceding operator()  (filterbank.h:142-148): origin moves and nothing is
+ * computed, so the smoothers stand still and the next sample reads, as its newest history
+ * row (x and every band's y), the ring row left from O+1 samples earlier (the reference's
+ * rings hold O+1 rows).  The handle keeps that row after a 1-sample process call, after
+ * another hz_fb_tick and at creation; after a call of n >= 2 samples or hz_fb_set_state it
+ * is not kept and hz_fb_tick returns HZ_E_STATE.  (A tick() that follows operator() is
+ * already part of every process call.) */
+int hz_fb_tick(hz_fb* h);
 int hz_fb_set_stream(hz_fb* h, void* hip_stream);
 int hz_fb_get_stream(hz_fb* h, void** hip_stream);
 int hz_fb_synchronize(hz_fb* h);
@@ -108,6 +117,9 @@ int hz_fb_last_path(hz_fb* h, int* path);
 /* LTI engine geometry: (chunk length, bands per wave, waves per group) in
  * {(16,1,16), (32,1,16)}; 0s = default */
 int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group);
+/* (diagnostics) plan of the last LTI launch: time segments, segment-prepass tiles skipped
+ * at the head of each segment (the horizon prepass; 0 = full prepass), fine prepass parts */
+int hz_fb_lti_plan(hz_fb* h, long* nseg, long* skip_tiles, int* fine_parts);
 
 /* ---- Oscbank<double,N>  (src/oscbank.h:15-97, src/multichannel.h:16-159) -- */
 typedef struct hz_osc hz_osc;

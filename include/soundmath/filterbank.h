@@ -40,11 +40,12 @@ public:
 
     T operator()(T sample) { return sample_with(sample, HZ_DIST_NONE, 0.0); }
     T operator()(T sample, int dist_id, double param = 0.0) { return sample_with(sample, dist_id, param); }
+    // After operator() the engine already advanced.  Without one, the reference's tick() only
+    // moves origin: nothing is computed, the smoothers stand still and the next sample reads the
+    // ring row left from O+1 samples earlier -- hz_fb_tick does exactly that (HZ_E_STATE after
+    // a block process() call, whose last O+1 rows the handle does not keep).
     void tick() {
-        if (!computed_) {   // the reference's tick() without operator(): the sample is 0 input
-            T zero = 0, y;
-            detail::check(hz_fb_process(h_.get(), &zero, &y, 1), "Filterbank::tick");
-        }
+        if (!computed_) detail::check(hz_fb_tick(h_.get()), "Filterbank::tick");
         computed_ = false;
     }
 

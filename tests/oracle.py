@@ -103,6 +103,14 @@ class OracleFilterbank:
         self.l.orc_fb_process(self.h, _p(xi), _p(out), len(xi), self.dist[0], self.dist[1])
         return out
 
+    def __call__(self, sample):
+        """operator()(T) (filterbank.h:125-131), cached until tick()."""
+        return self.l.orc_fb_sample(self.h, float(sample), self.dist[0], self.dist[1])
+
+    def tick(self):
+        """tick() (filterbank.h:142-148): origin moves; no compute if operator() was not called."""
+        self.l.orc_fb_tick(self.h)
+
     def process_tv(self, x, kind, stream, param=0.0):
         xi = np.ascontiguousarray(x, dtype=np.float64)
         st = np.ascontiguousarray(stream, dtype=np.float64)

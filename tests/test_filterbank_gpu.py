@@ -229,3 +229,46 @@ def test_geometries(gpu_lib, waves, nb, order, N):
     assert rel_err(g.process(x), o.process(x)) < TOL
     x2 = white_noise_f32(2100, seed=4)
     assert rel_err(g.process(x2), o.process(x2)) < TOL
+
+
+@pytest.mark.parametrize("order", [1, 2, 4])
+def test_tick_without_operator(gpu_lib, order):
+    """tick() without operator() (filterbank.h:142-148): the ring rotates with its stale row,
+    nothing is computed and the smoothers stand still (hz_fb_tick); bare ticks at the start,
+    in runs and between 1-sample calls; HZ_E_STATE after a block call."""
+    from huygens_amd import Filterbank
+    from huygens_amd._lib import HZ_E_STATE, HZError
+    rng = np.random.default_rng(40 + order)
+    N = 70
+    fwd = rng.uniform(-1, 1, (N, order + 1))
+    back = rng.uniform(-0.3, 0.3, (N, order)) / order
+    boost = rng.uniform(0.5, 1.5, N)
+    g = Filterbank(order, N, 0.1, 1.0)
+    o = OracleFilterbank(order, N, 0.1, 1.0)
+    for fb in (g, o):
+        for n in range(N):
+            fb.coefficients(n, fwd[n], back[n])
+        fb.boost(boost)
+        fb.open()
+    outs_g, outs_o = [], []
+    ops = ["tick", "tick"] + list(rng.choice(["op", "tick", "op2"], 200, p=[0.6, 0.25, 0.15]))
+    for op in ops:
+        if op == "tick":
+            g.tick()
+            o.tick()
+        else:
+            x = float(rng.uniform(-1, 1))
+            outs_g.append(g(x))
+            outs_o.append(o(x))
+            if op == "op2":   # repeated operator() before tick(): cached
+                assert g(x + 1) == outs_g[-1]
+                o(x + 1)
+            g.tick()
+            o.tick()
+    err = rel_err(np.array(outs_g), np.array(outs_o))
+    assert err < TOL, err
+    # after a block call the spare ring row is not kept
+    g.process(white_noise_f32(64, seed=5))
+    with pytest.raises(HZError) as ei:
+        g.tick()
+    assert ei.value.code == HZ_E_STATE

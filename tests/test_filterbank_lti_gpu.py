@@ -121,6 +121,27 @@ def test_horizon_prepass_lti(gpu_lib, R):
     g, o = make_pair(2, N, fwd, back)
     g.set_target_groups(16)
     run_calls(g, o, [500, 98304, 2048 * 40 + 96, 3000], seed=23)
+    g.process(white_noise_f32(98304, seed=24))
+    nseg, skip, _ = g.lti_plan()
+    assert nseg > 1 and skip > 0, (nseg, skip)
+
+
+@pytest.mark.parametrize("N,n", [(2048, 240_000), (512, 480_000)])
+def test_horizon_prepass_shard_shapes(gpu_lib, N, n):
+    """The emulated 2-GPU (2048 bands, 2 segments) and 8-GPU (512 bands, 8 segments) shard
+    shapes of C2 at R = 0.999 on 256 CUs: K = 53,248 samples (26 tiles) is shorter than a
+    segment, so the prepass starts skip_tiles > 0 tiles into each segment; parity vs the
+    restatement over the whole call."""
+    fwd, back = resonant_coefficients(N, 0.999, 0.5)
+    g, o = make_pair(2, N, fwd, back)
+    g.set_target_groups(256)
+    x0 = white_noise_f32(500, seed=30)
+    assert rel_err(g.process(x0), o.process(x0)) < TOL
+    x = white_noise_f32(n, seed=31)
+    err = rel_err(g.process(x), o.process(x))
+    nseg, skip, fine = g.lti_plan()
+    assert nseg == 4096 // N and skip > 0 and fine == 1, (nseg, skip, fine)
+    assert err < TOL, err
 
 
 def test_path_switches_with_setters(gpu_lib):

@@ -142,3 +142,72 @@ def test_lti_algorithm_model(order, N, L, n):
     ref = fb.process(x)
     got = lti_mix_model(fwd, back, pin, gin, x, L=L)
     assert rel_err(got, ref) < 1e-10
+
+
+def _ring_model_ops(order, N, F, B, pin, gin, sp, sg, ops):
+    """Pure-Python restatement of Filterbank's rings (src/filterbank.h:125-187): input ring of
+    2(O+1), outputs ring of 2(O+1) x N, origin; ops = sequence of ('op', x) / ('tick',)."""
+    R = order + 1
+    xr = [0.0] * (2 * R)
+    Y = [[0.0] * N for _ in range(2 * R)]
+    pre, gain = [0.0] * N, [0.0] * N
+    origin, computed, outs = 0, False, []
+    for op in ops:
+        if op[0] == "op":
+            if not computed:
+                for n in range(N):
+                    pre[n] = (1 - sp) * pin[n] + sp * pre[n]
+                    gain[n] = (1 - sg) * gin[n] + sg * gain[n]
+                xr[origin] = xr[origin + R] = op[1]
+                row = []
+                for n in range(N):
+                    ff = F[n][0] * xr[origin]
+                    for i in range(1, order + 1):
+                        ff += F[n][i] * xr[origin + i]
+                    bs = 0.0
+                    for k in range(order):
+                        bs += B[n][k] * Y[origin + 1 + k][n]
+                    row.append(ff * pre[n] - bs)
+                Y[origin] = list(row)
+                Y[origin + R] = list(row)
+                computed = True
+            s = 0.0
+            for n in range(N):
+                s += Y[origin][n] * gain[n]
+            outs.append(s)
+        else:
+            origin -= 1
+            if origin < 0:
+                origin += R
+            computed = False
+    return np.array(outs)
+
+
+@pytest.mark.parametrize("order", [1, 2, 3])
+def test_filterbank_oracle_tick_without_operator(order):
+    """tick() without operator() (filterbank.h:142-148) reuses the stale ring row: the C
+    restatement follows an independent Python model of the rings on ops with bare ticks."""
+    from oracle import OracleFilterbank
+    rng = np.random.default_rng(7 + order)
+    N = 5
+    F = rng.uniform(-1, 1, (N, order + 1))
+    B = rng.uniform(-0.3, 0.3, (N, order)) / order
+    pin, gin = rng.uniform(0.5, 1.5, N), rng.uniform(0.5, 1.5, N)
+    ops = []
+    for _ in range(300):
+        r = rng.uniform()
+        if r < 0.25:
+            ops.append(("tick",))
+        elif r < 0.35:
+            ops.append(("op", float(rng.uniform(-1, 1))))   # repeated operator(): cached
+        else:
+            ops += [("op", float(rng.uniform(-1, 1))), ("tick",)]
+    o = OracleFilterbank(order, N, 0.1, 1.0)
+    for n in range(N):
+        o.coefficients(n, F[n], B[n])
+    o.boost(pin)
+    o.mix(gin)
+    got = [o(op[1]) if op[0] == "op" else o.tick() for op in ops]
+    got = np.array([v for v, op in zip(got, ops) if op[0] == "op"])
+    want = _ring_model_ops(order, N, F, B, pin, gin, o.l.orc_relaxation(0.1), o.l.orc_relaxation(1.0), ops)
+    assert np.array_equal(got, want)
