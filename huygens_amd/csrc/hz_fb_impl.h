@@ -107,7 +107,7 @@ struct hz_fb {
         double* d_fmix = nullptr;    // [L][L+O]
         long horizon = -2;           // samples after which ||M^k|| < 2^-64 for every band
                                      // (-1: none within 2^18; -2: not computed yet)
-    } lti_set[2];
+    } lti_set[3];
     std::vector<double> pg_host;     // host mirror of the smoother state [N][2] (pre, gain)
     long mirror_pending = 0;         // samples processed since pg_host was last brought up to date
     bool converged = false;          // pg_host at the targets; cleared by every setter

@@ -54,22 +54,18 @@ struct RecL {
 };
 
 static int lti_rec_size(int O, int L) {
-    if (L == 16) {
-        switch (O) {
-        case 0: return RecL<0, 16>::SIZE;
-        case 1: return RecL<1, 16>::SIZE;
-        case 2: return RecL<2, 16>::SIZE;
-        case 3: return RecL<3, 16>::SIZE;
-        default: return RecL<4, 16>::SIZE;
-        }
+#define HZ_LTI_RS(LL)                                                           \
+    switch (O) {                                                                \
+    case 0: return RecL<0, LL>::SIZE;                                           \
+    case 1: return RecL<1, LL>::SIZE;                                           \
+    case 2: return RecL<2, LL>::SIZE;                                           \
+    case 3: return RecL<3, LL>::SIZE;                                           \
+    default: return RecL<4, LL>::SIZE;                                          \
     }
-    switch (O) {
-    case 0: return RecL<0, 32>::SIZE;
-    case 1: return RecL<1, 32>::SIZE;
-    case 2: return RecL<2, 32>::SIZE;
-    case 3: return RecL<3, 32>::SIZE;
-    default: return RecL<4, 32>::SIZE;
-    }
+    if (L == 16) HZ_LTI_RS(16)
+    if (L == 32) HZ_LTI_RS(32)
+    HZ_LTI_RS(64)
+#undef HZ_LTI_RS
 }
 
 template <int O, int L>
@@ -145,7 +141,8 @@ static void build_record_lti_any(int O, int L, const double* b, const double* a,
 #define HZ_LTI_REC(OO)                                                          \
     case OO:                                                                    \
         if (L == 16) build_record_lti<OO, 16>(b, a, rec);                       \
-        else build_record_lti<OO, 32>(b, a, rec);                               \
+        else if (L == 32) build_record_lti<OO, 32>(b, a, rec);                  \
+        else build_record_lti<OO, 64>(b, a, rec);                               \
         break;
     switch (O) {
         HZ_LTI_REC(0)
@@ -194,10 +191,18 @@ __host__ __device__ constexpr int lti_waves(int O) { return O <= 2 ? 16 : 8; }
 __host__ __device__ constexpr int lti_bsp(int O) { return (lti_waves(O) * O + 15) / 16 * 16; }
 constexpr int kZRow = 65;   // z rows [BSP][64 chunks + 1]: E-block writes hit 16 banks apart
 constexpr int kGsRow = 80;  // gs rows [BSP][64 chunks + 16]: mix A-operand reads on disjoint bank halves
+// chunk 64: the mix B operands (K rows) live in LDS instead of registers (the chunk's 17-step E
+// operands leave no room for them below 128 VGPRs); K rows [BSP][L + 16]: the two 16-lane
+// halves of a ds_read_b64 hit disjoint banks
+template <int O, int L>
+__host__ __device__ constexpr bool lti_k_lds() { return L == 64; }
+template <int L>
+__host__ __device__ constexpr int lti_krow() { return L + 16; }
 template <int O, int L>
 __host__ __device__ constexpr size_t lti_lds_bytes(bool mix) {
     return sizeof(double) * (2 * (size_t)lti_xs_pad<O, L>() + 2 * (size_t)lti_bsp(O) * kZRow +
-                             (mix ? 2 * (size_t)lti_bsp(O) * kGsRow : 0));
+                             (mix ? 2 * (size_t)lti_bsp(O) * kGsRow : 0) +
+                             (mix && lti_k_lds<O, L>() ? (size_t)lti_bsp(O) * lti_krow<L>() : 0));
 }
 
 typedef double hz_f64x4 __attribute__((ext_vector_type(4)));
@@ -244,10 +249,16 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     constexpr int NE = 4 * (BSP / 16);                // E blocks (4 chunk blocks x state blocks)
     constexpr int KM = BSP / 4;                       // mix k-steps (band states)
     constexpr int NM = (MODE == MODE_MIX) ? 4 * (L / 16) : 0;  // mix blocks (chunk blocks x sample blocks)
-    constexpr int IPW = (NE + NM + W - 1) / W;        // MFMA work items per wave
+    // work items: E block e on wave e % W (slot e / W); mix block m on wave (NE + m) % W (slot
+    // (NE % W + m) / W ... see m_item), so a wave holds at most IPE + IPM B operands
+    constexpr int IPE = (NE + W - 1) / W;
+    constexpr int IPM = (NM + W - 1) / W;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* zb = lds + 2 * XSP;      // [2][BSP][kZRow]
     double* gsb = zb + 2 * BSP * kZRow;  // [2][BSP][kGsRow]
+    constexpr bool KL = lti_k_lds<O, L>() && MODE == MODE_MIX;
+    constexpr int KR = lti_krow<L>();
+    double* kb = gsb + 2 * BSP * kGsRow;  // [BSP][KR] (KL only)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int grp_band0 = blockIdx.x * W;
@@ -289,50 +300,71 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         }
     }
 
-    // MFMA B operands of this wave's work items (item u = wave + W v): E items hold
-    // E[tap][bs] (tap = 4q + (l >> 4), bs = 16 sb + (l & 15)), mix items K[bs][j]
-    // (bs = 4q + (l >> 4), j = 16 jb + (l & 15)); zero outside the group / taps.
-    constexpr int KB = KE > KM ? KE : KM;
-    double bop[IPW][KB];
+    // MFMA B operands of this wave's work items: E items hold E[tap][bs] (tap = 4q + (l >> 4),
+    // bs = 16 sb + (l & 15)), mix items K[bs][j] (bs = 4q + (l >> 4), j = 16 jb + (l & 15));
+    // zero outside the group / taps.  Loop-invariant: held in registers for the whole launch.
+    auto e_item = [&](int v) { return wave + W * v; };                         // < NE: valid
+    auto m_item = [&](int v) { return (wave - NE % W + W) % W + W * v; };     // < NM: valid
+    constexpr int IPMR = KL ? 0 : IPM;   // mix B operands held in registers
+    double bop_e[IPE > 0 ? IPE : 1][KE], bop_m[IPMR > 0 ? IPMR : 1][KM > 0 ? KM : 1];
 #pragma unroll
-    for (int v = 0; v < IPW; ++v) {
-        const int item = wave + W * v;
+    for (int v = 0; v < IPE; ++v) {
+        const int item = e_item(v);
 #pragma unroll
-        for (int q = 0; q < KB; ++q) {
+        for (int q = 0; q < KE; ++q) {
             double val = 0.0;
-            if (item < NE) {
-                const int sb = item >> 2, tap = 4 * q + (lane >> 4), bs = 16 * sb + (lane & 15);
-                const int bl = bs / O, k = bs % O, bnd = grp_band0 + bl;
-                if (q < KE && bl < W && bnd < a.nbands && tap < XW) {
-                    const double* rb = rec + (long)bnd * R::SIZE;
-                    val = tap < O ? rb[R::EH + k * O + tap] : (tap + k < XW ? rb[R::E0 + tap + k] : 0.0);
-                }
-            } else if (item < NE + NM) {
-                const int jb = (item - NE) >> 2, bs = 4 * q + (lane >> 4), j = 16 * jb + (lane & 15);
-                const int bl = bs / O, k = bs % O, bnd = grp_band0 + bl;
-                if (q < KM && bl < W && bnd < a.nbands) val = rec[(long)bnd * R::SIZE + R::K + j * O + k];
+            const int sb = item >> 2, tap = 4 * q + (lane >> 4), bs = 16 * sb + (lane & 15);
+            const int bl = bs / O, k = bs % O, bnd = grp_band0 + bl;
+            if (item < NE && bl < W && bnd < a.nbands && tap < XW) {
+                const double* rb = rec + (long)bnd * R::SIZE;
+                val = tap < O ? rb[R::EH + k * O + tap] : (tap + k < XW ? rb[R::E0 + tap + k] : 0.0);
             }
-            bop[v][q] = val;
+            bop_e[v][q] = val;
+        }
+    }
+    if constexpr (KL) {
+        for (int e = threadIdx.x; e < BSP * L; e += 64 * W) {
+            const int bs = e / L, j = e % L, bl = bs / O, k = bs % O, bnd = grp_band0 + bl;
+            kb[bs * KR + j] = (bl < W && bnd < a.nbands) ? rec[(long)bnd * R::SIZE + R::K + j * O + k] : 0.0;
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < IPMR; ++v) {
+        const int item = m_item(v);
+#pragma unroll
+        for (int q = 0; q < KM; ++q) {
+            double val = 0.0;
+            const int jb = item >> 2, bs = 4 * q + (lane >> 4), j = 16 * jb + (lane & 15);
+            const int bl = bs / O, k = bs % O, bnd = grp_band0 + bl;
+            if (item < NM && bl < W && bnd < a.nbands) val = rec[(long)bnd * R::SIZE + R::K + j * O + k];
+            bop_m[v][q] = val;
         }
     }
 
-    // x staging: unconditional loads from clamped addresses, the zero-tail select at
-    // store time; the O history taps before the call's first sample are patched in
+    // x staging through a buffer descriptor over x[0 .. seg_end): one 32-bit lane offset per
+    // load, the segment's zero tail and the samples before the call (offsets that wrap past
+    // 2^32) come back as 0 from the range check; the O history taps before the call's first
+    // sample are patched in at store time.  (No 64-bit addresses or clamps in registers.)
+    const __amdgpu_buffer_rsrc_t xrsrc = [&] {
+        const unsigned long long xb = (unsigned long long)a.x;
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)xb);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(xb >> 32));
+        const int bytes = __builtin_amdgcn_readfirstlane((int)(seg_end * (long)sizeof(double)));
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, bytes,
+                                                 0x00020000);
+    }();
     auto load_x = [&](long t0x, double (&pf)[PF]) {
+        const int v0 = (int)((t0x - O) * (long)sizeof(double)) + (int)threadIdx.x * (int)sizeof(double);
 #pragma unroll
-        for (int q = 0; q < PF; ++q) {
-            const int li = threadIdx.x + q * 64 * W;
-            const long idx = t0x - O + li;
-            const long ci = idx < 0 ? 0 : (idx < seg_end ? idx : seg_end - 1);
-            pf[q] = a.x[ci];
-        }
+        for (int q = 0; q < PF; ++q)
+            pf[q] = __builtin_bit_cast(   // the whole offset in voffset: soffset is outside the range check
+                double, __builtin_amdgcn_raw_buffer_load_b64(xrsrc, v0 + q * 64 * W * (int)sizeof(double), 0, 0));
     };
     auto store_x = [&](double* xbuf, const double (&pf)[PF], long t0x) {
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
             const int li = threadIdx.x + q * 64 * W;
-            const long idx = t0x - O + li;
-            if (li < XS) xbuf[li + li / L] = idx < seg_end ? pf[q] : 0.0;
+            if (li < XS) xbuf[li + li / L] = pf[q];
         }
         if (t0x == 0 && threadIdx.x < O) xbuf[threadIdx.x] = a.xhist[O - 1 - threadIdx.x];  // x[-O+li]
     };
@@ -342,8 +374,8 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         const double* xs = lds + (te & 1) * XSP;
         double* z = zb + (te & 1) * BSP * kZRow;
 #pragma unroll
-        for (int v = 0; v < IPW; ++v) {
-            const int item = wave + W * v;  // wave-uniform
+        for (int v = 0; v < IPE; ++v) {
+            const int item = e_item(v);  // wave-uniform
             if (item < NE) {
                 const int m = item & 3, sb = item >> 2;
                 // A: lane l holds X[chunk 16m + (l & 15)][tap 4q + (l >> 4)]
@@ -353,7 +385,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                 for (int q = 0; q < KE; ++q) {
                     const int li = li0 + 4 * q;
                     const double xa = (4 * q + (lane >> 4) < XW) ? xs[li + li / L] : 0.0;
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, bop[v][q], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, bop_e[v][q], acc, 0, 0, 0);
                 }
                 // D: col = band state 16 sb + (l & 15), row = chunk 16 m + (l >> 4) + 4 rr
 #pragma unroll
@@ -367,18 +399,27 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         const double* gs = gsb + (tm & 1) * BSP * kGsRow;
         const long t0m = seg_t0 + (long)tm * T;
 #pragma unroll
-        for (int v = 0; v < IPW; ++v) {
-            const int item = wave + W * v - NE;  // wave-uniform
-            if (item >= 0 && item < NM) {
+        for (int v = 0; v < IPM; ++v) {
+            const int item = m_item(v);  // wave-uniform
+            if (item < NM) {
                 const int m = item & 3, jb = item >> 2;
                 const double* ga = gs + (lane >> 4) * kGsRow + 16 * m + (lane & 15);
+                const double* kbl = kb + (lane >> 4) * KR + 16 * jb + (lane & 15);
+                auto bm = [&](int q) { return KL ? kbl[4 * q * KR] : bop_m[KL ? 0 : v][q]; };
+                // two accumulation chains (ILP) while registers allow; one for L = 64
+                constexpr bool kTwo = L <= 32;
                 hz_f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
                 for (int q = 0; q < KM; q += 2) {
-                    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * q * kGsRow], bop[v][q], acc0, 0, 0, 0);
-                    if (q + 1 < KM)
-                        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * (q + 1) * kGsRow], bop[v][q + 1], acc1, 0,
-                                                                   0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * q * kGsRow], bm(q), acc0, 0, 0, 0);
+                    if (q + 1 < KM) {
+                        if constexpr (kTwo)
+                            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * (q + 1) * kGsRow], bm(q + 1), acc1, 0,
+                                                                       0, 0);
+                        else
+                            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[4 * (q + 1) * kGsRow], bm(q + 1), acc0, 0,
+                                                                       0, 0);
+                    }
                 }
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
@@ -413,16 +454,16 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         double pf[PF];
         const bool stage = it + 2 < ntiles;
         if (stage) load_x(t0 + 2 * T, pf);
-        if (it + 1 < ntiles) phase_e(it + 1);
-        if constexpr (MODE == MODE_MIX) {
-            if (it >= 1) phase_m(it - 1);
-        }
-        if (it < ntiles) {
-            // ---- (S) tile it: this wave's band ----
-            const double* z = zb + (it & 1) * BSP * kZRow;
-            double zz[O];
+        // the three phases of an iteration touch disjoint LDS images.  Order E, M, S for every
+        // wave: measured against scan-first orders for the E waves (0.554 vs 0.522 ms per C2
+        // step) and for the mix-only waves (0.581)
+        auto phase_s = [&]() {
+            if (it < ntiles) {
+                // ---- (S) tile it: this wave's band ----
+                const double* z = zb + (it & 1) * BSP * kZRow;
+                double zz[O];
 #pragma unroll
-            for (int k = 0; k < O; ++k) zz[k] = pb * z[(wave * O + k) * kZRow + lane];
+                for (int k = 0; k < O; ++k) zz[k] = pb * z[(wave * O + k) * kZRow + lane];
 #define HZ_LTI_SCAN_STEP(CTRL, RM, MAT)                                                               \
     {                                                                                                 \
         double nb_[O];                                                                                \
@@ -430,51 +471,57 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         _Pragma("unroll") for (int rr = 0; rr < O; ++rr)                                              \
             _Pragma("unroll") for (int c = 0; c < O; ++c) zz[rr] = fma(MAT[rr * O + c], nb_[c], zz[rr]); \
     }
-            const double* p1 = r + R::PS;
-            const double* p2 = r + R::PS + O * O;
-            const double* p4 = r + R::PS + 2 * O * O;
-            const double* p8 = r + R::PS + 3 * O * O;
-            HZ_LTI_SCAN_STEP(kDppRowShr + 1, 0xf, p1)
-            HZ_LTI_SCAN_STEP(kDppRowShr + 2, 0xf, p2)
-            HZ_LTI_SCAN_STEP(kDppRowShr + 4, 0xf, p4)
-            HZ_LTI_SCAN_STEP(kDppRowShr + 8, 0xf, p8)
-            HZ_LTI_SCAN_STEP(kDppRowBcast15, 0xa, qa)
-            HZ_LTI_SCAN_STEP(kDppRowBcast31, 0xc, qb)
+                const double* p1 = r + R::PS;
+                const double* p2 = r + R::PS + O * O;
+                const double* p4 = r + R::PS + 2 * O * O;
+                const double* p8 = r + R::PS + 3 * O * O;
+                HZ_LTI_SCAN_STEP(kDppRowShr + 1, 0xf, p1)
+                HZ_LTI_SCAN_STEP(kDppRowShr + 2, 0xf, p2)
+                HZ_LTI_SCAN_STEP(kDppRowShr + 4, 0xf, p4)
+                HZ_LTI_SCAN_STEP(kDppRowShr + 8, 0xf, p8)
+                HZ_LTI_SCAN_STEP(kDppRowBcast15, 0xa, qa)
+                HZ_LTI_SCAN_STEP(kDppRowBcast31, 0xc, qb)
 #undef HZ_LTI_SCAN_STEP
-            double Sn[O];
+                double Sn[O];
 #pragma unroll
-            for (int k = 0; k < O; ++k) {
-                double vv = dpp_dm<kDppWaveShr1, 0xf>(zz[k]);  // Z(l-1), 0 at lane 0
-                double sn = readlane_d(zz[k], 63);
+                for (int k = 0; k < O; ++k) {
+                    double vv = dpp_dm<kDppWaveShr1, 0xf>(zz[k]);  // Z(l-1), 0 at lane 0
+                    double sn = readlane_d(zz[k], 63);
 #pragma unroll
-                for (int c = 0; c < O; ++c) {
-                    vv = fma(qc[k * O + c], S[c], vv);
-                    sn = fma(r[R::PS + 4 * O * O + k * O + c], S[c], sn);
+                    for (int c = 0; c < O; ++c) {
+                        vv = fma(qc[k * O + c], S[c], vv);
+                        sn = fma(r[R::PS + 4 * O * O + k * O + c], S[c], sn);
+                    }
+                    st[k] = vv;
+                    Sn[k] = sn;
                 }
-                st[k] = vv;
-                Sn[k] = sn;
-            }
 #pragma unroll
-            for (int k = 0; k < O; ++k) S[k] = Sn[k];
-            if constexpr (MODE == MODE_MIX) {
-                double* gs = gsb + (it & 1) * BSP * kGsRow;
+                for (int k = 0; k < O; ++k) S[k] = Sn[k];
+                if constexpr (MODE == MODE_MIX) {
+                    double* gs = gsb + (it & 1) * BSP * kGsRow;
 #pragma unroll
-                for (int k = 0; k < O; ++k) gs[(wave * O + k) * kGsRow + lane] = gb * st[k];
-                if (last_seg && it == ntiles - 1 && live) {
-                    // end-of-call y history = the start state of the chunk beginning at n
-                    // (n is a multiple of L; chunks past n see zero input)
-                    const int cn = (int)((n - t0) / L);  // in [1, 64]
-                    if (cn < 64) {
-                        if (lane == cn)
+                    for (int k = 0; k < O; ++k) gs[(wave * O + k) * kGsRow + lane] = gb * st[k];
+                    if (last_seg && it == ntiles - 1 && live) {
+                        // end-of-call y history = the start state of the chunk beginning at n
+                        // (n is a multiple of L; chunks past n see zero input)
+                        const int cn = (int)((n - t0) / L);  // in [1, 64]
+                        if (cn < 64) {
+                            if (lane == cn)
 #pragma unroll
-                            for (int k = 0; k < O; ++k) a.ystate_next[(long)band * O + k] = st[k];
-                    } else if (lane == 0) {
+                                for (int k = 0; k < O; ++k) a.ystate_next[(long)band * O + k] = st[k];
+                        } else if (lane == 0) {
 #pragma unroll
-                        for (int k = 0; k < O; ++k) a.ystate_next[(long)band * O + k] = S[k];
+                            for (int k = 0; k < O; ++k) a.ystate_next[(long)band * O + k] = S[k];
+                        }
                     }
                 }
             }
+        };
+        if (it + 1 < ntiles) phase_e(it + 1);
+        if constexpr (MODE == MODE_MIX) {
+            if (it >= 1) phase_m(it - 1);
         }
+        phase_s();
         if (stage) store_x(lds + (it & 1) * XSP, pf, t0 + 2 * T);
         __syncthreads();
     }
@@ -587,8 +634,10 @@ __global__ __launch_bounds__(256) void fb_fmix_kernel(const double* __restrict__
 }
 
 // out[t] = sum_g partial[g][t] + sum_i Fmix[t mod L][i] x[t - t mod L - O + i]
-// One thread per pair of samples (16-B loads down the slab's columns, 8 rows in flight),
-// 128 threads per block; the group order of the sum is fixed (deterministic).
+// One thread per pair of samples (16-B loads down the slab's columns, kRedRows rows in flight),
+// 128 threads = 256 samples per block; the group order of the sum is fixed (deterministic).
+// The block's input window x[t0 - O .. t0 + 255] is staged in LDS once (every chunk window of
+// the zero-state term reads it there: L + O taps per sample).
 constexpr int kRedRows = 32;
 
 template <int O, int L>
@@ -598,10 +647,19 @@ __global__ __launch_bounds__(128) void fb_lti_reduce_kernel(const double* __rest
                                                             const double* __restrict__ fmix,
                                                             double* __restrict__ out) {
     constexpr int XW = L + O;
+    constexpr int NS = 256;   // samples per block (a multiple of L)
     __shared__ double fm[L * XW];
+    __shared__ double xs[NS + O];
+    const long t0 = (long)blockIdx.x * NS;
     for (int e = threadIdx.x; e < L * XW; e += 128) fm[e] = fmix[e];
+    for (int e = threadIdx.x; e < NS + O; e += 128) {
+        const long idx = t0 - O + e;
+        // before the launch's first sample: the call's x history (first chunk) or the previous
+        // chunk of the same input buffer (xhist == nullptr); past n: never read
+        xs[e] = idx >= n ? 0.0 : (idx >= 0 || !xhist) ? x[idx] : xhist[-idx - 1];
+    }
     __syncthreads();
-    const long t = 2 * ((long)blockIdx.x * 128 + threadIdx.x);
+    const long t = t0 + 2 * threadIdx.x;
     if (t >= n) return;
     typedef double d2 __attribute__((ext_vector_type(2)));
     d2 s0 = {0.0, 0.0}, s1 = {0.0, 0.0};
@@ -624,13 +682,10 @@ __global__ __launch_bounds__(128) void fb_lti_reduce_kernel(const double* __rest
     d2 acc = s0 + s1;
     // zero-state mix (t and t + 1 are in the same chunk: L even, t even)
     const int j = (int)(t % L);
-    const long base = t - j - O;
-#pragma unroll 4
+    const double* xw = xs + (t - j - t0);   // x[t - j - O + i] = xw[i]
+#pragma unroll 6
     for (int i = 0; i < XW; ++i) {
-        const long idx = base + i;
-        // before the launch's first sample: the call's x history (first chunk) or the
-        // previous chunk of the same input buffer (xhist == nullptr)
-        const double xv = idx >= 0 || !xhist ? x[idx] : xhist[-idx - 1];
+        const double xv = xw[i];
         acc[0] = fma(fm[j * XW + i], xv, acc[0]);
         acc[1] = fma(fm[(j + 1) * XW + i], xv, acc[1]);
     }
@@ -692,8 +747,8 @@ typedef void (*LtiReduceKernel)(const double*, long, int, long, const double*, c
 struct LtiGeom {
     int L, nb, waves;
 };
-static const LtiGeom kLtiGeoms[] = {{16, 1, 16}, {32, 1, 16}};  // waves: lti_waves(O)
-constexpr int kNumLtiGeoms = 2;
+static const LtiGeom kLtiGeoms[] = {{16, 1, 16}, {32, 1, 16}, {64, 1, 16}};  // waves: lti_waves(O)
+constexpr int kNumLtiGeoms = 3;
 
 template <int O, int L>
 LtiKernel lti_kernel_mode(int mode) {
@@ -703,7 +758,8 @@ LtiKernel lti_kernel_mode(int mode) {
 
 template <int O>
 LtiKernel lti_kernel_geom(int geom, int mode) {
-    return kLtiGeoms[geom].L == 32 ? lti_kernel_mode<O, 32>(mode) : lti_kernel_mode<O, 16>(mode);
+    const int L = kLtiGeoms[geom].L;
+    return L == 64 ? lti_kernel_mode<O, 64>(mode) : L == 32 ? lti_kernel_mode<O, 32>(mode) : lti_kernel_mode<O, 16>(mode);
 }
 
 static LtiKernel pick_lti(int O, int geom, int mode) {
@@ -716,18 +772,24 @@ static LtiKernel pick_lti(int O, int geom, int mode) {
 }
 
 static size_t lti_lds(int O, int geom, bool mix) {
-    const bool l32 = kLtiGeoms[geom].L == 32;
-    switch (O) {
-    case 1: return l32 ? lti_lds_bytes<1, 32>(mix) : lti_lds_bytes<1, 16>(mix);
-    case 2: return l32 ? lti_lds_bytes<2, 32>(mix) : lti_lds_bytes<2, 16>(mix);
-    case 3: return l32 ? lti_lds_bytes<3, 32>(mix) : lti_lds_bytes<3, 16>(mix);
-    default: return l32 ? lti_lds_bytes<4, 32>(mix) : lti_lds_bytes<4, 16>(mix);
+    const int L = kLtiGeoms[geom].L;
+#define HZ_LTI_LDS(LL)                                                          \
+    switch (O) {                                                                \
+    case 1: return lti_lds_bytes<1, LL>(mix);                                   \
+    case 2: return lti_lds_bytes<2, LL>(mix);                                   \
+    case 3: return lti_lds_bytes<3, LL>(mix);                                   \
+    default: return lti_lds_bytes<4, LL>(mix);                                  \
     }
+    if (L == 16) HZ_LTI_LDS(16)
+    if (L == 32) HZ_LTI_LDS(32)
+    HZ_LTI_LDS(64)
+#undef HZ_LTI_LDS
 }
 
 #define HZ_LTI_OL(TEMPLATE, O, L)                                                                    \
     (L == 16 ? (O == 1 ? TEMPLATE<1, 16> : O == 2 ? TEMPLATE<2, 16> : O == 3 ? TEMPLATE<3, 16> : TEMPLATE<4, 16>) \
-             : (O == 1 ? TEMPLATE<1, 32> : O == 2 ? TEMPLATE<2, 32> : O == 3 ? TEMPLATE<3, 32> : TEMPLATE<4, 32>))
+     : L == 32 ? (O == 1 ? TEMPLATE<1, 32> : O == 2 ? TEMPLATE<2, 32> : O == 3 ? TEMPLATE<3, 32> : TEMPLATE<4, 32>) \
+               : (O == 1 ? TEMPLATE<1, 64> : O == 2 ? TEMPLATE<2, 64> : O == 3 ? TEMPLATE<3, 64> : TEMPLATE<4, 64>))
 static CarryKernel pick_lti_carry(int O, int L) { return HZ_LTI_OL(fb_lti_seg_carry_kernel, O, L); }
 static FmixKernel pick_fmix(int O, int L) { return HZ_LTI_OL(fb_fmix_kernel, O, L); }
 static LtiReduceKernel pick_lti_reduce(int O, int L) { return HZ_LTI_OL(fb_lti_reduce_kernel, O, L); }
@@ -738,11 +800,21 @@ static LtiReduceKernel pick_lti_reduce_short(int O, int L) { return HZ_LTI_OL(fb
 
 namespace hz_fbi {
 
-// geometry by call length unless pinned (hz_fb_tune_lti): chunk 32 for calls of at least two
-// of its 2048-sample tiles, chunk 16 (1024-sample tiles) for the short streaming blocks
+// geometry by call length unless pinned (hz_fb_tune_lti): chunk 64 for calls of at least two of
+// its 4096-sample tiles (C2: mix 0.609 -> 0.522 ms per 10 s step against chunk 32: half the scan
+// work and barriers per sample), chunk 32 from two 2048-sample tiles, chunk 16 (1024-sample
+// tiles) for the short streaming blocks
 int fb_lti_geom(const hz_fb* h, long n) {
     if (h->lti_geom >= 0) return h->lti_geom;
-    return n >= 2 * 64L * 32 ? 1 : 0;
+    static const int env_geom = [] {   // tuning experiments: HZ_FB_LTI_L = 16 / 32 / 64 for long calls
+        const char* e = std::getenv("HZ_FB_LTI_L");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 16 ? 0 : v == 64 ? 2 : v == 32 ? 1 : -1;
+    }();
+    if (n >= 2 * 64L * 32 && env_geom >= 0) return env_geom;
+    if (n >= 2 * 64L * 64) return 2;   // chunk 64 for calls of at least two of its 4096-sample tiles
+    if (n >= 2 * 64L * 32) return 1;
+    return 0;
 }
 
 int fb_lti_chunk(int geom) { return kLtiGeoms[geom].L; }
@@ -1078,7 +1150,7 @@ int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group)
             h->lti_geom = g;
             return HZ_OK;
         }
-    hz::set_error("hz_fb_tune_lti: (chunk, bands/wave, waves) must be one of (16,1,16), (32,1,16)");
+    hz::set_error("hz_fb_tune_lti: (chunk, bands/wave, waves) must be one of (16,1,16), (32,1,16), (64,1,16)");
     return HZ_E_INVALID;
 }
 

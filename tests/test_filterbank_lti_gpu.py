@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 TOL = 1e-9
 TOL_STIFF = 1e-7  # Nyquist double pole (see test_filterbank_gpu.py)
-LTI_GEOMS = [(16, 1, 16), (32, 1, 16)]
+LTI_GEOMS = [(16, 1, 16), (32, 1, 16), (64, 1, 16)]
 
 
 def make_pair(order, N, fwd, back, kp=0.001, kg=0.001, boost=None, gains=None):
@@ -60,7 +60,7 @@ def run_calls(g, o, lengths, seed, expect_lti=True, tol=TOL):
         yg, yo = g.process(x), o.process(x)
         err = rel_err(yg, yo)
         assert err < tol, (i, n, err)
-        if i > 0 and expect_lti and n >= 32:
+        if i > 0 and expect_lti and n >= g.lti_chunk():
             assert g.last_path() == HZ_FB_PATH_LTI, (i, n)
         if i == 0:
             # the first call starts from pre = gain = 0: general engine
