@@ -18,7 +18,11 @@ lib: $(LIBDIR)/libhuygens_hip.so
 
 $(OBJDIR)/%.o: huygens_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(HIPFLAGS_$*) -c $< -o $@
+
+# per-file flags: the correction GEMM keeps its MFMA accumulators in VGPRs (no AGPR copies
+# around the k loop)
+HIPFLAGS_hz_fb_gemm := -mllvm -amdgpu-mfma-vgpr-form=1
 
 $(LIBDIR)/libhuygens_hip.so: $(OBJS)
 	@mkdir -p $(LIBDIR)

@@ -19,7 +19,9 @@ constexpr int kMaxOrder = 4;
 // MODE_SEGEND: zero-state end state of each segment but the last (no mixdown), feeding a
 //   per-band carry kernel when the bank is too small to fill the chip with bands alone
 //   (e.g. 512-band shards on 8 GPUs).
-enum { MODE_MIX = 0, MODE_SEGEND = 1 };
+// MODE_STATE (converged engine only): chunk start states x gain of every band to HBM, for the
+//   bank-wide correction GEMM (hz_fb_lti.hip, fb_lti_gemm_kernel) instead of a per-group mix.
+enum { MODE_MIX = 0, MODE_SEGEND = 1, MODE_STATE = 2 };
 
 // Scalar (SGPR) copy of a wave-uniform double.
 __device__ __forceinline__ double uniform(double v) {
@@ -105,6 +107,8 @@ struct hz_fb {
         double* d_rec = nullptr;
         size_t cap = 0;
         double* d_fmix = nullptr;    // [L][L+O]
+        double* d_kt = nullptr;      // [N O padded to 4][L] homogeneous responses (correction GEMM)
+        size_t kt_cap = 0;
         long horizon = -2;           // samples after which ||M^k|| < 2^-64 for every band
                                      // (-1: none within 2^18; -2: not computed yet)
     } lti_set[3];
@@ -139,6 +143,10 @@ int fb_tv_materialize(hz_fb* h);             // pending stream row -> F/B (hz_fb
 // hz_fb_lti.hip
 int fb_lti_geom(const hz_fb* h, long n);  // LTI geometry for a call of n samples
 int fb_lti_chunk(int geom);                // samples per lane chunk of a geometry
+bool fb_lti_gemm_geom(int geom);           // geometry runs the correction GEMM path
+// hz_fb_gemm.hip: part[s][t] = correction of chunk t / 64 over band-state slice s (chunk 64)
+int fb_lti_gemm_launch(const double* gs, const double* kt, int kslice, int bs_pad, double* part, long n_pad,
+                       int ntiles, int slices, hipStream_t stream);
 bool fb_converged(hz_fb* h);
 int fb_launch_lti(hz_fb* h, int geom, const double* d_in, double* d_out, long n);
 

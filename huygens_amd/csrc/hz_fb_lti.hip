@@ -68,6 +68,21 @@ static int lti_rec_size(int O, int L) {
 #undef HZ_LTI_RS
 }
 
+static int lti_k_offset(int O, int L) {
+#define HZ_LTI_KO(LL)                                                           \
+    switch (O) {                                                                \
+    case 0: return RecL<0, LL>::K;                                              \
+    case 1: return RecL<1, LL>::K;                                              \
+    case 2: return RecL<2, LL>::K;                                              \
+    case 3: return RecL<3, LL>::K;                                              \
+    default: return RecL<4, LL>::K;                                             \
+    }
+    if (L == 16) HZ_LTI_KO(16)
+    if (L == 32) HZ_LTI_KO(32)
+    HZ_LTI_KO(64)
+#undef HZ_LTI_KO
+}
+
 template <int O, int L>
 void build_record_lti(const double* b, const double* av, double* rec) {
     using R = RecL<O, L>;
@@ -165,6 +180,8 @@ struct LtiArgs {
     const double* xhist;    // [O]
     double* xhist_next;     // [O]
     double* partial;        // [G][n_pad] (n_pad = row stride)
+    double* gs_out;         // MODE_STATE: [tile][bs_pad][64 chunks] gin x chunk start states
+    int bs_pad;             // band-state rows per tile (N O rounded up to 4; pad rows written 0)
     double* segstate;       // [N][nseg_state][O] start states of the (prepass-fine) segments
     long n;                 // samples in this launch (multiple of L)
     long n_pad;             // slab row stride (the tile-padded length)
@@ -497,10 +514,18 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                 }
 #pragma unroll
                 for (int k = 0; k < O; ++k) S[k] = Sn[k];
-                if constexpr (MODE == MODE_MIX) {
-                    double* gs = gsb + (it & 1) * BSP * kGsRow;
+                if constexpr (MODE != MODE_SEGEND) {
+                    if constexpr (MODE == MODE_MIX) {
+                        double* gs = gsb + (it & 1) * BSP * kGsRow;
 #pragma unroll
-                    for (int k = 0; k < O; ++k) gs[(wave * O + k) * kGsRow + lane] = gb * st[k];
+                        for (int k = 0; k < O; ++k) gs[(wave * O + k) * kGsRow + lane] = gb * st[k];
+                    } else {   // MODE_STATE: tile-major rows of 64 chunks, row band O + k (dead
+                               // waves write the zero pad rows: gb = 0)
+                        double* go = a.gs_out + ((t0 / T) * a.bs_pad + (long)band * O) * 64 + lane;
+#pragma unroll
+                        for (int k = 0; k < O; ++k)
+                            if (band * O + k < a.bs_pad) __builtin_nontemporal_store(gb * st[k], go + 64 * k);
+                    }
                     if (last_seg && it == ntiles - 1 && live) {
                         // end-of-call y history = the start state of the chunk beginning at n
                         // (n is a multiple of L; chunks past n see zero input)
@@ -753,7 +778,9 @@ constexpr int kNumLtiGeoms = 3;
 template <int O, int L>
 LtiKernel lti_kernel_mode(int mode) {
     static_assert(lti_lds_bytes<O, L>(true) <= 160 * 1024, "LTI kernel LDS over 160 KiB");
-    return mode == MODE_SEGEND ? fb_lti_kernel<O, L, MODE_SEGEND> : fb_lti_kernel<O, L, MODE_MIX>;
+    return mode == MODE_SEGEND ? fb_lti_kernel<O, L, MODE_SEGEND>
+         : mode == MODE_STATE  ? fb_lti_kernel<O, L, MODE_STATE>
+                               : fb_lti_kernel<O, L, MODE_MIX>;
 }
 
 template <int O>
@@ -818,6 +845,17 @@ int fb_lti_geom(const hz_fb* h, long n) {
 }
 
 int fb_lti_chunk(int geom) { return kLtiGeoms[geom].L; }
+
+// chunk 64 runs the bank-wide correction as a GEMM over all band states (MODE_STATE +
+// fb_lti_gemm_kernel) instead of per-group mixes and the G-row slab; HZ_FB_LTI_GEMM=0 restores
+// the slab path (A/B measurements)
+bool fb_lti_gemm_geom(int geom) {
+    static const bool off = [] {
+        const char* e = std::getenv("HZ_FB_LTI_GEMM");
+        return e && e[0] == '0';
+    }();
+    return kLtiGeoms[geom].L == 64 && !off;
+}
 
 // every band's smoothers at their targets (host mirror), relative to the bank's
 // largest target: the LTI engine then computes the same outputs to ~2^-60
@@ -906,6 +944,23 @@ int fb_prepare_lti(hz_fb* h, int gi) {
         if (!set.d_fmix) HZ_TRY_HIP(hipMalloc(&set.d_fmix, sizeof(double) * L * (L + kMaxOrder)));
         HZ_TRY_HIP(hipMemcpyAsync(set.d_rec, host.data(), sizeof(double) * need, hipMemcpyHostToDevice, h->stream));
         HZ_TRY_HIP(hipStreamSynchronize(h->stream));  // pageable source
+        if (fb_lti_gemm_geom(gi) && O > 0) {   // K rows of every band state, zero-padded to 4
+            const int bs_pad = (h->N * O + 3) & ~3, ko = lti_k_offset(O, L);
+            std::vector<double> kt((size_t)bs_pad * L, 0.0);
+            for (int b = 0; b < h->N; ++b)
+                for (int k = 0; k < O; ++k)
+                    for (int j = 0; j < L; ++j)
+                        kt[((size_t)b * O + k) * L + j] = host[(size_t)b * rs + ko + j * O + k];
+            if (kt.size() > set.kt_cap) {
+                if (set.d_kt) HZ_TRY_HIP(hipFree(set.d_kt));
+                set.d_kt = nullptr;
+                HZ_TRY_HIP(hipMalloc(&set.d_kt, sizeof(double) * kt.size()));
+                set.kt_cap = kt.size();
+            }
+            HZ_TRY_HIP(hipMemcpyAsync(set.d_kt, kt.data(), sizeof(double) * kt.size(), hipMemcpyHostToDevice,
+                                      h->stream));
+            HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+        }
         set.rs = rs;
         set.dirty = false;
         set.horizon = -2;
@@ -949,17 +1004,23 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         return v >= 1 && v <= 64 ? v : 1;
     }();
     const long ntiles_all = (n + T - 1) / T;
+    // correction GEMM path: per chunk GS [bs_pad][chunks] + part [S][n_pad] instead of two slabs
+    const bool gemm = fb_lti_gemm_geom(gi) && O > 0;
+    const int bs_pad = (h->N * O + 3) & ~3;
     long chunk = std::max<long>(T, (((1L << slab_log2) / std::max(1, G)) / T) * T);
-    if (ntiles_all >= 8 * nsplit) chunk = std::min(chunk, ((ntiles_all + nsplit - 1) / nsplit) * T);
+    if (gemm) chunk = std::max<long>(T, (((1L << slab_log2) / bs_pad * L) / T) * T);
+    if (!gemm && ntiles_all >= 8 * nsplit) chunk = std::min(chunk, ((ntiles_all + nsplit - 1) / nsplit) * T);
     // (row skews of 32..2050 doubles were measured: no effect on the reduce, which moves the
     // slab plus the mix kernel's dirty write-back at about 5.4 TB/s)
     const long n_pad_max = std::min<long>(ntiles_all * T, chunk);
     const size_t slab = (size_t)G * n_pad_max;
-    if (2 * slab > h->partial_cap) {
+    constexpr int kMaxSlices = 32;   // GEMM band-state slices (rows of part)
+    const size_t need = gemm ? (size_t)bs_pad * (n_pad_max / L) + (size_t)kMaxSlices * n_pad_max : 2 * slab;
+    if (need > h->partial_cap) {
         if (h->d_partial) HZ_TRY_HIP(hipFree(h->d_partial));
         h->d_partial = nullptr;
-        HZ_TRY_HIP(hipMalloc(&h->d_partial, sizeof(double) * 2 * slab));
-        h->partial_cap = 2 * slab;
+        HZ_TRY_HIP(hipMalloc(&h->d_partial, sizeof(double) * need));
+        h->partial_cap = need;
     }
     if (!h->stream_red) HZ_TRY_HIP(hipStreamCreateWithFlags(&h->stream_red, hipStreamNonBlocking));
     if (!h->d_xhist_red) HZ_TRY_HIP(hipMalloc(&h->d_xhist_red, sizeof(double) * kMaxOrder));
@@ -973,16 +1034,16 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
     }
     hipEvent_t* ev_mix = h->sync_ev.data();
     hipEvent_t* ev_red = h->sync_ev.data() + nchunks;
-    LtiKernel kmix = pick_lti(O, gi, MODE_MIX);
+    LtiKernel kmix = pick_lti(O, gi, gemm ? MODE_STATE : MODE_MIX);
     LtiKernel kend = pick_lti(O, gi, MODE_SEGEND);
     HZ_TRY(fb_set_lds_attr((const void*)kmix));
     HZ_TRY(fb_set_lds_attr((const void*)kend));
-    const size_t lds = lti_lds(O, gi, true);
+    const size_t lds = lti_lds(O, gi, !gemm);
     const size_t lds_end = lti_lds(O, gi, false);
     // with the reduce on a second stream, the first chunk's reduce reads the call's x history
     // after later mixes rotated the ping-pong buffers: keep a copy
     const double* xhist_call = h->d_xhist[h->xcur];
-    if (nchunks > 1) {
+    if (nchunks > 1 && !gemm) {
         HZ_TRY_HIP(hipMemcpyAsync(h->d_xhist_red, xhist_call, sizeof(double) * O, hipMemcpyDeviceToDevice,
                                   h->stream));
         xhist_call = h->d_xhist_red;
@@ -1051,6 +1112,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             }
         }
         double* slab_k = h->d_partial + (size_t)(k & 1) * slab;
+        const long nc_pad = ntiles * 64;   // chunks of the launch (GEMM path)
         LtiArgs a;
         a.pin = h->d_pin;
         a.gin = h->d_gin;
@@ -1062,6 +1124,8 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         a.xhist = h->d_xhist[h->xcur];
         a.xhist_next = h->d_xhist[h->xcur ^ 1];
         a.partial = slab_k;
+        a.gs_out = h->d_partial;
+        a.bs_pad = bs_pad;
         a.segstate = h->d_seg;
         a.n = len;
         a.n_pad = ntiles * T;
@@ -1074,7 +1138,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         a.sp_n = (double)powl((long double)h->sp, (long double)len);
         a.sg_n = (double)powl((long double)h->sg, (long double)len);
         hipEvent_t* e = nullptr;
-        if (k >= 2) HZ_TRY_HIP(hipStreamWaitEvent(h->stream, ev_red[k - 2], 0));  // slab buffer k & 1 free
+        if (k >= 2 && !gemm) HZ_TRY_HIP(hipStreamWaitEvent(h->stream, ev_red[k - 2], 0));  // slab buffer k & 1 free
         (void)0;
         if (h->prof) {
             HZ_TRY(fb_prof_events(h, &e));
@@ -1095,10 +1159,38 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             HZ_TRY_HIP(hipGetLastError());
         }
         if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
+        static const bool diag_state = std::getenv("HZ_FB_LTI_DIAG_STATE") != nullptr;
+        if (diag_state && nseg == 1 && !gemm) {   // (diagnostics) the E + scan work alone, timed by rocprof
+            LtiArgs ad = a;
+            hipLaunchKernelGGL(kend, dim3(G, 1), dim3(64 * lti_waves(O)), lds_end, h->stream, (const double*)set.d_rec,
+                               ad);
+        }
         hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * lti_waves(O)), lds, h->stream,
                            (const double*)set.d_rec, a);
         HZ_TRY_HIP(hipGetLastError());
         if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
+        if (gemm) {
+            // correction GEMM over band-state slices (>= 4 workgroups per CU), then the slice sum
+            // + zero-state term in the reduce kernel; one stream, chunks in sequence
+            int S = (int)std::min<long>(kMaxSlices, std::max<long>(1, (4L * h->target_groups + ntiles - 1) / ntiles));
+            S = std::min(S, bs_pad / 4);
+            const int kslice = ((bs_pad + S - 1) / S + 3) & ~3;
+            S = (bs_pad + kslice - 1) / kslice;
+            double* part = h->d_partial + (size_t)bs_pad * nc_pad;
+            if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
+            HZ_TRY(fb_lti_gemm_launch(h->d_partial, set.d_kt, kslice, bs_pad, part, a.n_pad, (int)ntiles, S,
+                                      h->stream));
+            hipLaunchKernelGGL(pick_lti_reduce(O, L), dim3((unsigned)((len + 255) / 256)), dim3(128), 0, h->stream,
+                               (const double*)part, a.n_pad, S, len, a.x, off == 0 ? xhist_call : nullptr,
+                               (const double*)set.d_fmix, d_out + off);
+            HZ_TRY_HIP(hipGetLastError());
+            if (e) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
+            h->xcur ^= 1;
+            h->scur ^= 1;
+            h->prof_launches += h->prof ? 1 : 0;
+            fb_mirror_advance(h, len);
+            continue;
+        }
         // one chunk: the reduce stays on the caller's stream (no cross-stream round trip)
         hipStream_t rs = nchunks > 1 ? h->stream_red : h->stream;
         if (nchunks > 1) {
@@ -1123,7 +1215,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         fb_mirror_advance(h, len);
     }
     // the caller's stream sees the whole output
-    if (nchunks > 1) HZ_TRY_HIP(hipStreamWaitEvent(h->stream, ev_red[nchunks - 1], 0));
+    if (nchunks > 1 && !gemm) HZ_TRY_HIP(hipStreamWaitEvent(h->stream, ev_red[nchunks - 1], 0));
     return HZ_OK;
 }
 
