@@ -87,8 +87,9 @@ def cpu_baseline(fwd, back, seconds_target=1.5):
 
 def fb_executed_flops(lti, L=32, O=2):
     """FP64 flops the kernel actually issues per band-sample.  LTI engine:
-    chunk end states on the matrix cores 2 O ceil((L+O)/4) 4 / L, group mix 2 O, the
-    64-lane scan 2 (6 O^2 + 2 O^2) 64 / (64 L) per chunk; general engine ~2 x 10."""
+    chunk end states on the matrix cores 2 O ceil((L+O)/4) 4 / L, the correction (group mix,
+    or the bank-wide GEMM at L = 64) 2 O, the 64-lane scan 2 (6 O^2 + 2 O^2) 64 / (64 L) per
+    chunk; general engine ~2 x 10."""
     if not lti:
         return 20.0
     import math
@@ -286,7 +287,8 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(fwd, back)
-        kernels = ("fb_lti_kernel", "fb_lti_reduce", "fb_lti_seg_carry") if lti else ("fb_mix_kernel", "fb_reduce")
+        kernels = (("fb_lti_kernel", "fb_lti_gemm", "fb_lti_reduce", "fb_lti_seg_carry") if lti
+                   else ("fb_mix_kernel", "fb_reduce"))
         traffic, traffic_detail = None, "skipped"
         if not args.no_traffic and world == 1 and S == SAMPLES_PER_STEP:
             traffic, traffic_detail = pmc_traffic(kernels, extra=(["--lti", args.lti] if args.lti else [])
@@ -314,13 +316,15 @@ def main():
                          "traffic_detail": traffic_detail,
                          "algorithmic_bytes_per_launch": (16 * S + 120 * cnt) * args.steps / max(1, launches),
                          "launches_per_step": launches / max(1, args.steps),
-                         "kernel": ("LTI engine step: fb_lti_kernel<2,%d,MIX> + fb_lti_reduce_kernel (+ segment "
-                                    "prepass)" % fb.lti_chunk()) if lti
-                                   else "general engine step: fb_mix_kernel<2,NONE,1,MIX> + fb_reduce_kernel",
+                         "kernel": (("LTI engine step: fb_lti_kernel<2,64,STATE> + fb_lti_gemm_kernel + "
+                                     "fb_lti_reduce_kernel (+ segment prepass)") if lti and fb.lti_chunk() == 64 else
+                                    ("LTI engine step: fb_lti_kernel<2,%d,MIX> + fb_lti_reduce_kernel (+ segment "
+                                     "prepass)" % fb.lti_chunk()) if lti
+                                    else "general engine step: fb_mix_kernel<2,NONE,1,MIX> + fb_reduce_kernel"),
                          "kernel_avg_ms": 1e3 * launch_avg_s,
                          "components_ms_per_launch": {"segment_prepass": seg_ms / max(1, launches),
-                                                      "mix": mix_ms / max(1, launches),
-                                                      "reduce": red_ms / max(1, launches)},
+                                                      "mix_or_state": mix_ms / max(1, launches),
+                                                      "gemm_and_reduce": red_ms / max(1, launches)},
                          "flops_per_launch": flops_per_launch,
                          "executed": {"flops_per_band_sample": xflops, "achieved": executed,
                                       "frac": (executed / FP64_PEAK_TFLOPS) if executed else None},

@@ -89,6 +89,7 @@ _SIGS = {
     "hz_fb_last_path": (I, [VP, C.POINTER(I)]),
     "hz_fb_tune_lti": (I, [VP, I, I, I]),
     "hz_fb_lti_plan": (I, [VP, C.POINTER(C.c_long), C.POINTER(C.c_long), C.POINTER(C.c_int)]),
+    "hz_fb_lti_last_chunk": (I, [VP, C.POINTER(C.c_int)]),
     # Oscbank
     "hz_osc_create": (I, [I, D, I, C.POINTER(VP)]),
     "hz_osc_create_shard": (I, [I, I, I, D, I, C.POINTER(VP)]),

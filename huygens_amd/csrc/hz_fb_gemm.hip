@@ -9,6 +9,8 @@
 // Reducing over ALL band states inside the MFMA K dimension leaves no per-group slab: the only
 // intermediate is GS, N O (n / 64) doubles -- 4x fewer bytes than the G x n slab of the
 // per-group mix at chunk 64.
+#include <cstdlib>
+
 #include "hz_fb_impl.h"
 
 namespace {
@@ -23,53 +25,77 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // buffered: the next stage's A and B loads are in flight under this stage's MFMAs.
 // GS and K rows past N O are zero (bs_pad is a multiple of 4); part[slice][t] is summed, with
 // the zero-state term, by fb_lti_reduce_kernel.
-constexpr int kD = 4;                 // k-steps (4 band states each) per stage
-constexpr int kRows = 4 * kD;         // band states per stage
 constexpr int kBRow = 64 + 16;        // LDS row: the two 16-lane halves of a ds_read_b64 on disjoint banks
 
+// RB: tiles (16-chunk row blocks per wave) per workgroup; kD: k-steps (4 band states each) per stage
+template <int RB, int kD>
 __global__ __launch_bounds__(256) void fb_lti_gemm_kernel(const double* __restrict__ gs,
                                                           const double* __restrict__ kt, int kslice, int bs_pad,
-                                                          double* __restrict__ part, long n_pad) {
+                                                          int ntiles, double* __restrict__ part, long n_pad) {
     constexpr int L = 64;
+    constexpr int kRows = 4 * kD;         // band states per stage
     __shared__ __attribute__((aligned(16))) double bsh[2][kRows * kBRow];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const long c0 = (long)blockIdx.x * 64 + 16 * wave;   // this wave's 16 chunks
+    const int tile0 = blockIdx.x * RB;
     const int b0 = blockIdx.y * kslice;
     const int b1 = min(bs_pad, b0 + kslice);
     const int nst = (b1 - b0 + kRows - 1) / kRows;       // stages; rows past b1 read as 0
-    f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
-    // A: lane (r = l >> 4, c = l & 15) of k-step u in stage s: GS row b0 + 16 s + 4 u + r
-    const double* ap = gs + ((long)blockIdx.x * bs_pad + b0 + (lane >> 4)) * 64 + 16 * wave + (lane & 15);
-    // B staging: thread t moves K[b0 + 16 s + (t >> 4)][4 (t & 15) .. + 3] (two 16-B loads)
+    f64x4 acc[RB][4];
+#pragma unroll
+    for (int t = 0; t < RB; ++t)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) acc[t][jb] = f64x4{0.0, 0.0, 0.0, 0.0};
+    // A: lane (r = l >> 4, c = l & 15) of k-step u in stage s, tile t: GS row b0 + 16 s + 4 u + r
+    // of tile tile0 + t (a last odd tile reads tile0's rows again and is not stored)
+    const double* ap[RB];
+#pragma unroll
+    for (int t = 0; t < RB; ++t) {
+        const int tt = tile0 + t < ntiles ? tile0 + t : tile0;
+        ap[t] = gs + ((long)tt * bs_pad + b0 + (lane >> 4)) * 64 + 16 * wave + (lane & 15);
+    }
+    // B staging: thread t moves K[b0 + kRows s + 16 h + (t >> 4)][4 (t & 15) .. + 3], h < kD / 4
+    constexpr int BH = kD / 4;
     const int brow = threadIdx.x >> 4, bcol = 4 * (threadIdx.x & 15);
     const double* bp = kt + (long)(b0 + brow) * L + bcol;
     typedef double d2 __attribute__((ext_vector_type(2)));
     // full stages load unguarded; only a slice's last stage can hold rows past b1
     const int nfull = (b1 - b0) / kRows;
-    auto load_a = [&](int s, double (&av)[kD]) {
-        if (s < nfull) {
+    auto load_a = [&](int s, double (&av)[RB][kD]) {
 #pragma unroll
-            for (int u = 0; u < kD; ++u) av[u] = __builtin_nontemporal_load(ap + (long)(16 * s + 4 * u) * 64);
-        } else {
+        for (int t = 0; t < RB; ++t) {
+            if (s < nfull) {
 #pragma unroll
-            for (int u = 0; u < kD; ++u) {
-                const int row = 16 * s + 4 * u + (lane >> 4);
-                av[u] = b0 + row < b1 ? __builtin_nontemporal_load(ap + (long)(16 * s + 4 * u) * 64) : 0.0;
+                for (int u = 0; u < kD; ++u)
+                    av[t][u] = __builtin_nontemporal_load(ap[t] + (long)(kRows * s + 4 * u) * 64);
+            } else {
+#pragma unroll
+                for (int u = 0; u < kD; ++u) {
+                    const int row = kRows * s + 4 * u + (lane >> 4);
+                    av[t][u] = b0 + row < b1 ? __builtin_nontemporal_load(ap[t] + (long)(kRows * s + 4 * u) * 64)
+                                             : 0.0;
+                }
             }
         }
     };
-    auto load_b = [&](int s, d2 (&bv)[2]) {
-        const bool ok = s < nfull || b0 + 16 * s + brow < b1;
-        const d2 z = {0.0, 0.0};
-        bv[0] = ok ? *(const d2*)(bp + (long)16 * s * L) : z;
-        bv[1] = ok ? *(const d2*)(bp + (long)16 * s * L + 2) : z;
+    auto load_b = [&](int s, d2 (&bv)[BH][2]) {
+#pragma unroll
+        for (int h = 0; h < BH; ++h) {
+            const bool ok = s < nfull || b0 + kRows * s + 16 * h + brow < b1;
+            const d2 z = {0.0, 0.0};
+            const double* q = bp + (long)(kRows * s + 16 * h) * L;
+            bv[h][0] = ok ? *(const d2*)q : z;
+            bv[h][1] = ok ? *(const d2*)(q + 2) : z;
+        }
     };
-    auto store_b = [&](int buf, const d2 (&bv)[2]) {
-        *(d2*)&bsh[buf][brow * kBRow + bcol] = bv[0];
-        *(d2*)&bsh[buf][brow * kBRow + bcol + 2] = bv[1];
+    auto store_b = [&](int buf, const d2 (&bv)[BH][2]) {
+#pragma unroll
+        for (int h = 0; h < BH; ++h) {
+            *(d2*)&bsh[buf][(16 * h + brow) * kBRow + bcol] = bv[h][0];
+            *(d2*)&bsh[buf][(16 * h + brow) * kBRow + bcol + 2] = bv[h][1];
+        }
     };
-    double an[kD];
-    d2 bn[2];
+    double an[RB][kD];
+    d2 bn[BH][2];
     if (nst > 0) {
         load_a(0, an);
         load_b(0, bn);
@@ -77,9 +103,11 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_kernel(const double* __restri
     }
     __syncthreads();
     for (int s = 0; s < nst; ++s) {
-        double ac[kD];
+        double ac[RB][kD];
 #pragma unroll
-        for (int u = 0; u < kD; ++u) ac[u] = an[u];
+        for (int t = 0; t < RB; ++t)
+#pragma unroll
+            for (int u = 0; u < kD; ++u) ac[t][u] = an[t][u];
         const bool more = s + 1 < nst;
         if (more) {
             load_a(s + 1, an);
@@ -89,22 +117,28 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_kernel(const double* __restri
 #pragma unroll
         for (int u = 0; u < kD; ++u) {
             const double* bu = bs + 4 * u * kBRow;
-            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[u], bu[0], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[u], bu[16], acc1, 0, 0, 0);
-            acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[u], bu[32], acc2, 0, 0, 0);
-            acc3 = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[u], bu[48], acc3, 0, 0, 0);
+            double bv[4];
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) bv[jb] = bu[16 * jb];
+#pragma unroll
+            for (int t = 0; t < RB; ++t)
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb)
+                    acc[t][jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[t][u], bv[jb], acc[t][jb], 0, 0, 0);
         }
         if (more) store_b((s + 1) & 1, bn);
         __syncthreads();
     }
-    // D: row = chunk c0 + (l >> 4) + 4 rr, column = sample 16 jb + (l & 15) of the chunk
-    double* out = part + (long)blockIdx.y * n_pad + (c0 + (lane >> 4)) * L + (lane & 15);
+    // D: row = chunk (tile 64 + 16 wave) + (l >> 4) + 4 rr, column = sample 16 jb + (l & 15)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        out[4 * rr * L] = acc0[rr];
-        out[4 * rr * L + 16] = acc1[rr];
-        out[4 * rr * L + 32] = acc2[rr];
-        out[4 * rr * L + 48] = acc3[rr];
+    for (int t = 0; t < RB; ++t) {
+        if (tile0 + t >= ntiles) break;
+        const long c0 = (long)(tile0 + t) * 64 + 16 * wave;
+        double* out = part + (long)blockIdx.y * n_pad + (c0 + (lane >> 4)) * L + (lane & 15);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) out[4 * rr * L + 16 * jb] = acc[t][jb][rr];
     }
 }
 
@@ -112,15 +146,39 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_kernel(const double* __restri
 
 namespace hz_fbi {
 
-int fb_lti_gemm_launch(const double* gs, const double* kt, int kslice, int bs_pad, double* part, long n_pad,
-                       int ntiles, int slices, hipStream_t stream) {
-    if (bs_pad % 4 != 0 || kslice % 4 != 0 || ntiles <= 0 || slices <= 0) {
-        hz::set_error("fb_lti_gemm_launch: bad geometry (bs_pad %d, kslice %d)", bs_pad, kslice);
+int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* part, long n_pad, int ntiles,
+                       int target_groups, int max_slices, hipStream_t stream, int* slices_out) {
+    static const int rb = [] {   // tuning experiments: HZ_FB_GEMM_RB = 1 or 2 tiles per workgroup
+        const char* e = std::getenv("HZ_FB_GEMM_RB");
+        return e && e[0] == '2' ? 2 : 1;
+    }();
+    // (measured on C2: 2 tiles per workgroup, 8-step stages and 2 or 8 workgroups per CU were all
+    // slower than 1 / 4 / 4: 0.224 / 0.224 / 0.237 / 0.219 vs 0.219 ms with the reduce)
+    static const int kd = [] {   // HZ_FB_GEMM_KD = 4 or 8 k-steps per stage
+        const char* e = std::getenv("HZ_FB_GEMM_KD");
+        return e && e[0] == '8' ? 8 : 4;
+    }();
+    static const int occ = [] {  // HZ_FB_GEMM_OCC: workgroups wanted per CU (slice count)
+        const char* e = std::getenv("HZ_FB_GEMM_OCC");
+        const int v = e ? std::atoi(e) : 4;
+        return v >= 1 && v <= 16 ? v : 4;
+    }();
+    if (bs_pad % 4 != 0 || ntiles <= 0) {
+        hz::set_error("fb_lti_gemm_launch: bad geometry (bs_pad %d, tiles %d)", bs_pad, ntiles);
         return HZ_E_INVALID;
     }
-    hipLaunchKernelGGL(fb_lti_gemm_kernel, dim3((unsigned)ntiles, (unsigned)slices), dim3(256), 0, stream, gs, kt,
-                       kslice, bs_pad, part, n_pad);
+    // band-state slices: >= 4 workgroups per CU, each slice a multiple of 4 band states
+    const int gx = (ntiles + rb - 1) / rb;
+    int S = std::min(max_slices, std::max(1, (occ * target_groups + gx - 1) / gx));
+    S = std::min(S, bs_pad / 4);
+    const int kslice = ((bs_pad + S - 1) / S + 3) & ~3;   // (stages past b1 read as 0)
+    S = (bs_pad + kslice - 1) / kslice;
+    auto k = rb == 2 ? (kd == 8 ? fb_lti_gemm_kernel<2, 8> : fb_lti_gemm_kernel<2, 4>)
+                     : (kd == 8 ? fb_lti_gemm_kernel<1, 8> : fb_lti_gemm_kernel<1, 4>);
+    hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)S), dim3(256), 0, stream, gs, kt, kslice, bs_pad, ntiles, part,
+                       n_pad);
     HZ_TRY_HIP(hipGetLastError());
+    *slices_out = S;
     return HZ_OK;
 }
 

@@ -80,7 +80,7 @@ struct hz_fb {
     // plan of the last LTI launch (hz_fb_lti_plan): time segments, prepass tiles skipped per
     // segment (horizon), fine prepass parts per segment
     long plan_nseg = 0, plan_skip_tiles = 0;
-    int plan_fine = 0;
+    int plan_fine = 0, plan_chunk = 0;
     double* d_partial = nullptr;
     size_t partial_cap = 0;  // doubles
     double* d_seg = nullptr;  // segment start states
@@ -144,9 +144,10 @@ int fb_tv_materialize(hz_fb* h);             // pending stream row -> F/B (hz_fb
 int fb_lti_geom(const hz_fb* h, long n);  // LTI geometry for a call of n samples
 int fb_lti_chunk(int geom);                // samples per lane chunk of a geometry
 bool fb_lti_gemm_geom(int geom);           // geometry runs the correction GEMM path
-// hz_fb_gemm.hip: part[s][t] = correction of chunk t / 64 over band-state slice s (chunk 64)
-int fb_lti_gemm_launch(const double* gs, const double* kt, int kslice, int bs_pad, double* part, long n_pad,
-                       int ntiles, int slices, hipStream_t stream);
+// hz_fb_gemm.hip: part[s][t] = correction of sample t over band-state slice s (chunk 64); picks
+// the slice count (<= max_slices, reported in *slices_out)
+int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* part, long n_pad, int ntiles,
+                       int target_groups, int max_slices, hipStream_t stream, int* slices_out);
 bool fb_converged(hz_fb* h);
 int fb_launch_lti(hz_fb* h, int geom, const double* d_in, double* d_out, long n);
 

@@ -268,6 +268,9 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     constexpr int NM = (MODE == MODE_MIX) ? 4 * (L / 16) : 0;  // mix blocks (chunk blocks x sample blocks)
     // work items: E block e on wave e % W (slot e / W); mix block m on wave (NE + m) % W (slot
     // (NE % W + m) / W ... see m_item), so a wave holds at most IPE + IPM B operands
+    // (Splitting the E blocks' k-steps over two waves when there are no mix blocks measured
+    // slower: C2 state kernel 0.283 -> 0.351 ms.  The mix-free waves 8-15 scanning while waves
+    // 0-7 run the E chains is the better overlap.)
     constexpr int IPE = (NE + W - 1) / W;
     constexpr int IPM = (NM + W - 1) / W;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -1101,6 +1104,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         h->plan_nseg = nseg;
         h->plan_skip_tiles = skip_tiles;
         h->plan_fine = m;
+        h->plan_chunk = L;
         if (nseg > 1) {
             const size_t sneed = (size_t)h->N * nseg_state * O;
             if (sneed > h->seg_cap) {
@@ -1172,14 +1176,11 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         if (gemm) {
             // correction GEMM over band-state slices (>= 4 workgroups per CU), then the slice sum
             // + zero-state term in the reduce kernel; one stream, chunks in sequence
-            int S = (int)std::min<long>(kMaxSlices, std::max<long>(1, (4L * h->target_groups + ntiles - 1) / ntiles));
-            S = std::min(S, bs_pad / 4);
-            const int kslice = ((bs_pad + S - 1) / S + 3) & ~3;
-            S = (bs_pad + kslice - 1) / kslice;
             double* part = h->d_partial + (size_t)bs_pad * nc_pad;
             if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
-            HZ_TRY(fb_lti_gemm_launch(h->d_partial, set.d_kt, kslice, bs_pad, part, a.n_pad, (int)ntiles, S,
-                                      h->stream));
+            int S = 1;
+            HZ_TRY(fb_lti_gemm_launch(h->d_partial, set.d_kt, bs_pad, part, a.n_pad, (int)ntiles, h->target_groups,
+                                      kMaxSlices, h->stream, &S));
             hipLaunchKernelGGL(pick_lti_reduce(O, L), dim3((unsigned)((len + 255) / 256)), dim3(128), 0, h->stream,
                                (const double*)part, a.n_pad, S, len, a.x, off == 0 ? xhist_call : nullptr,
                                (const double*)set.d_fmix, d_out + off);
@@ -1222,6 +1223,12 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
 }  // namespace hz_fbi
 
 extern "C" {
+
+int hz_fb_lti_last_chunk(hz_fb* h, int* chunk) {
+    if (!h || !chunk) return HZ_E_INVALID;
+    *chunk = h->plan_chunk;
+    return HZ_OK;
+}
 
 int hz_fb_lti_plan(hz_fb* h, long* nseg, long* skip_tiles, int* fine_parts) {
     if (!h) return HZ_E_INVALID;

@@ -177,8 +177,11 @@ class Filterbank:
         self._lti_geom = {16: 0, 32: 1, 64: 2}.get(chunk, 1)
 
     def lti_chunk(self) -> int:
-        """Samples per lane chunk of the selected LTI geometry."""
-        return {0: 16, 1: 32, 2: 64}.get(self._lti_geom, 32)
+        """Samples per lane chunk of the last LTI launch (hz_fb_lti_last_chunk; the geometry
+        is picked by call length unless pinned with tune_lti)."""
+        c = C.c_int()
+        check(self._lib.hz_fb_lti_last_chunk(self._h, C.byref(c)))
+        return c.value or {0: 16, 1: 32, 2: 64}.get(self._lti_geom, 32)
 
     def lti_plan(self):
         """-> (time segments, prepass tiles skipped per segment, fine prepass parts) of the
