@@ -39,6 +39,12 @@ def _timed(step, steps, warmup, torch, dev):
 
 
 # --------------------------------------------------------------------------- C3
+# FP64 flops the Additive engine executes per partial-sample, measured with PMC counters on the
+# C3 row (profiles/r2/flops_pmc.txt: add_mix_kernel 3.59e11 flops over 5 steps of 7.86e9
+# partial-samples; transcendentals 2e-3 per partial-sample)
+EXEC_C3 = 9.1
+
+
 def run_c3(args, torch, dev, rank=0, world=1, shard_world=None):
     """Additive<double>(&cycle, 64, 256, 0.75, 1.0), all voices via makenote(36+v, 1),
     voices 0-7 released at sample 24,000; one step = 480,000 samples.  With world > 1 (the
@@ -114,8 +120,14 @@ def run_c3(args, torch, dev, rank=0, world=1, shard_world=None):
                      "kernel": "add_mix_kernel (+ add_reduce_kernel, add_advance_kernel)",
                      "kernel_avg_ms": ms / max(1, launches), "launches": launches,
                      "flops_per_unit": 22,
-                     "note": "algorithmic flops of the reference's per-sample update (SURVEY.md 8(d)); the engine's "
-                             "closed-form rotation does fewer"},
+                     "executed": {"flops_per_unit": EXEC_C3,
+                                  "achieved": EXEC_C3 * units / kern_s / 1e12 if kern_s > 0 else None,
+                                  "frac": EXEC_C3 * units / kern_s / 1e12 / FP64_PEAK if kern_s > 0 else None,
+                                  "source": "rocprofv3 --pmc SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 on this row "
+                                            "(profiles/r2/flops_pmc.txt)"},
+                     "note": "achieved = reference-equivalent rate: the algorithmic 22 flops (+ 3 transcendentals) "
+                             "of the reference's per-sample update (SURVEY.md 8(d)) over the whole launch (mix + "
+                             "reduce + advance); executed = the FP64 work the closed-form engine issues"},
         "cpu_baseline": cpu,
     }
 
