@@ -268,9 +268,11 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     constexpr int NM = (MODE == MODE_MIX) ? 4 * (L / 16) : 0;  // mix blocks (chunk blocks x sample blocks)
     // work items: E block e on wave e % W (slot e / W); mix block m on wave (NE + m) % W (slot
     // (NE % W + m) / W ... see m_item), so a wave holds at most IPE + IPM B operands
-    // (Splitting the E blocks' k-steps over two waves when there are no mix blocks measured
-    // slower: C2 state kernel 0.283 -> 0.351 ms.  The mix-free waves 8-15 scanning while waves
-    // 0-7 run the E chains is the better overlap.)
+    // (Measured slower on the C2 state kernel, 0.283 ms: splitting the E blocks' k-steps over
+    // two waves, 0.351 ms; wave roles -- waves 0-7 E blocks only, waves 8-15 two scans each in
+    // separate loops -- 0.320 ms.  FP64 MFMA and FP64 VALU share a pipe, so overlapping them
+    // across waves buys little; what the roles lose is the scan latency hidden behind the E
+    // chains of the same SIMD's other waves.)
     constexpr int IPE = (NE + W - 1) / W;
     constexpr int IPM = (NM + W - 1) / W;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -401,10 +403,21 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                 // A: lane l holds X[chunk 16m + (l & 15)][tap 4q + (l >> 4)]
                 const int li0 = (16 * m + (lane & 15)) * L + (lane >> 4);
                 hz_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+                // A operands read EP k-steps ahead of their MFMA (LDS latency under the chain)
+                constexpr int EP = 4;
+                auto xa_at = [&](int q) {
+                    const int li = li0 + 4 * q;
+                    return (4 * q + (lane >> 4) < XW) ? xs[li + li / L] : 0.0;
+                };
+                double xq[EP];
+#pragma unroll
+                for (int q = 0; q < EP && q < KE; ++q) xq[q] = xa_at(q);
+                __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead (the scheduler sinks them)
 #pragma unroll
                 for (int q = 0; q < KE; ++q) {
-                    const int li = li0 + 4 * q;
-                    const double xa = (4 * q + (lane >> 4) < XW) ? xs[li + li / L] : 0.0;
+                    const double xa = xq[q % EP];
+                    if (q + EP < KE) xq[q % EP] = xa_at(q + EP);
+                    __builtin_amdgcn_sched_barrier(0);
                     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, bop_e[v][q], acc, 0, 0, 0);
                 }
                 // D: col = band state 16 sb + (l & 15), row = chunk 16 m + (l >> 4) + 4 rr
