@@ -169,7 +169,16 @@ int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* p
     }
     // band-state slices: >= 4 workgroups per CU, each slice a multiple of 4 band states
     const int gx = (ntiles + rb - 1) / rb;
+    // at least 512 band states per slice: shard-sized banks (bs_pad 1024-4096) gain from fewer
+    // slices for the reduce to sum (emulated 2 / 4 / 8-GPU shard steps 0.323 / 0.206 / 0.155 ->
+    // 0.313 / 0.204 / 0.148 ms); C2 on one GPU keeps 9 slices
+    static const int mink = [] {  // HZ_FB_GEMM_MINK: fewest band states per slice
+        const char* e = std::getenv("HZ_FB_GEMM_MINK");
+        const int v = e ? std::atoi(e) : 512;
+        return v >= 0 ? v : 512;
+    }();
     int S = std::min(max_slices, std::max(1, (occ * target_groups + gx - 1) / gx));
+    if (mink > 0) S = std::max(1, std::min(S, bs_pad / mink));
     S = std::min(S, bs_pad / 4);
     const int kslice = ((bs_pad + S - 1) / S + 3) & ~3;   // (stages past b1 read as 0)
     S = (bs_pad + kslice - 1) / kslice;
