@@ -61,6 +61,7 @@ int main(int argc, char** argv) {
             y[t] = fb(x[t]);
             (void)fb(x[t]);   // cached until tick()
             fb.tick();
+            if (t == 40 || t == 41) fb.tick();   // tick() without operator(): the stale ring row
         }
         fb.process(x.data() + 100, y.data() + 100, 900);
         dump("filterbank", y);

@@ -39,13 +39,22 @@ def outputs(tmp_path_factory):
 
 
 def test_filterbank(outputs):
+    """Per-sample operator()/tick() with two bare ticks after t = 40 and 41, then process()."""
     o = OracleFilterbank(2, 16)
     for i in range(16):
         g, R, th = 0.01 * (i + 1), 0.99, 2 * PI * (i + 1) / 40.0
         o.coefficients(i, [g, 0, -g], [-2 * R * np.cos(th), R * R])
     o.boost(np.ones(16))
     o.open()
-    assert rel_err(outputs("filterbank"), o.process(x_input(1000))) < 1e-9
+    x = x_input(1000)
+    want = np.empty(1000)
+    for t in range(100):
+        want[t] = o(x[t])
+        o.tick()
+        if t in (40, 41):
+            o.tick()
+    want[100:] = o.process(x[100:])
+    assert rel_err(outputs("filterbank"), want) < 1e-9
 
 
 def test_ffilterbank(outputs):
