@@ -350,17 +350,18 @@ def run_row(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and args.workload != "c3":
-        raise SystemExit("--workload c4..c9 are single-GPU configs (SURVEY.md 8(d)); c3 shards")
+    if world > 1 and args.workload not in ("c3", "c4"):
+        raise SystemExit("--workload c5..c9 are single-GPU configs (SURVEY.md 8(d)); c3 and c4 shard")
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=dev)
-        body = bench_rows.run_c3(args, torch, dev, rank, world)
-    elif args.workload == "c3" and args.emulate_world:
-        body = bench_rows.run_c3(args, torch, dev, 0, 1, args.emulate_world)
+        body = (bench_rows.run_c3 if args.workload == "c3" else bench_rows.run_c4)(args, torch, dev, rank, world)
+    elif args.workload in ("c3", "c4") and args.emulate_world:
+        body = (bench_rows.run_c3 if args.workload == "c3" else bench_rows.run_c4)(args, torch, dev, 0, 1,
+                                                                                  args.emulate_world)
     else:
         fn = {"c3": bench_rows.run_c3, "c4": bench_rows.run_c4, "c5": bench_rows.run_c5,
               "c6": bench_rows.run_c6, "c7": bench_rows.run_c7, "c8": bench_rows.run_c8,

@@ -27,15 +27,28 @@ def _tests_path():
         sys.path.insert(0, p)
 
 
-def _timed(step, steps, warmup, torch, dev):
+def _timed(step, steps, warmup, torch, dev, world=1):
+    """Wall time of `steps` steps after `warmup`, barrier + synchronize on both sides; the
+    max over ranks when world > 1."""
+    if world > 1:
+        import torch.distributed as dist
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize(dev)
-    return time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
 
 
 # --------------------------------------------------------------------------- C3
@@ -142,10 +155,14 @@ def c4_signal(n, seed=3):
     return x
 
 
-def run_c4(args, torch, dev):
+def run_c4(args, torch, dev, rank=0, world=1, shard_world=None):
     """StaticSTFT(4096, 4) with its built-in gate over 480,000 samples (C4 (i)); the
-    Fourier(gate625) variant (ii) is timed beside it."""
+    Fourier(gate625) variant (ii) is timed beside it.  Under torchrun (world > 1) every rank
+    streams the whole input but computes only its runs of frames (runs of ceil(frames per
+    step / world) frames rotate over the ranks: hz_stft_set_frame_shard, SURVEY.md 8(e) STFT
+    row) and the partial outputs are summed to rank 0 over RCCL."""
     from huygens_amd import Fourier, StaticSTFT
+    from huygens_amd.stft import frames_before
     N, laps, S = 4096, 4, args.samples
     x = torch.from_numpy(c4_signal(S)).to(dev)
     yr = torch.empty_like(x)
@@ -154,15 +171,21 @@ def run_c4(args, torch, dev):
     out = {}
     for name, eng in (("static", StaticSTFT(N, laps)), ("gate625", Fourier(2, N, laps))):
         eng.set_stream(stream.cuda_stream)
+        sw = shard_world or world   # --emulate-world: rank 0's share of an sw-GPU job, no reduce
+        if sw > 1:
+            eng.set_frame_shard(rank, sw, -(-frames_before(N, laps, S) // sw))
 
         def step():
             eng.process_block_device(x.data_ptr(), 0, yr.data_ptr(), yi.data_ptr(), S)
+            if world > 1:
+                import torch.distributed as dist
+                dist.reduce(yr, dst=0, op=dist.ReduceOp.SUM)
 
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize(dev)
         f0 = eng.frames()[0]
-        elapsed = _timed(step, args.steps, 0, torch, dev)
+        elapsed = _timed(step, args.steps, 0, torch, dev, world)
         frames = eng.frames()[0] - f0
         # kernel times from a separate profiled pass: each block's frame launch repeated 8x
         # between one event pair (an event pair costs about as much as one ~20 us launch)
@@ -173,10 +196,11 @@ def run_c4(args, torch, dev):
         eng.profile(False)
         out[name] = (elapsed, fms, oms, blocks, frames)
     elapsed, fms, oms, blocks, frames = out["static"]
-    flops = 491520.0 * frames   # 2 x 5 N log2 N per frame
+    sw = shard_world or world
+    flops = 491520.0 * frames / sw   # 2 x 5 N log2 N per frame, this rank's share
     achieved = flops / (fms / 1e3) / 1e12 if fms > 0 else None
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and sw == 1:
         _tests_path()
         from oracle_stft import OracleSTFT
         o = OracleSTFT(N, laps, 1, 1)
@@ -190,9 +214,9 @@ def run_c4(args, torch, dev):
                          f"long double radix-2 FFT, 1 thread, {dt:.2f} s"}
     e2, f2, o2, b2, fr2 = out["gate625"]
     traffic, tdetail = None, "not collected (--no-traffic)"
-    if not args.no_traffic:
+    if not args.no_traffic and sw == 1:
         import bench
-        tb, tdetail = bench.pmc_traffic("stft_pair_kernel<1,", extra=("--workload", "c4"))
+        tb, tdetail = bench.pmc_traffic(("stft_pair_kernel<1,",), extra=("--workload", "c4"))
         traffic = tb   # HBM bytes per frame launch (one launch per step here)
     return {
         "metric": "STFT frames/s, StaticSTFT 4096-pt / 75% overlap spectral gate",
@@ -201,7 +225,9 @@ def run_c4(args, torch, dev):
         "samples_per_s": S * args.steps / elapsed,
         "data": "synthetic: white noise sigma 0.1 + 8 sinusoids 0.5 sin(2 pi 220 k^1.5 t), seed 3",
         "config": {"workload": "C4 StaticSTFT(4096, 4) built-in gate (100, 0.1)", "samples_per_step": S,
-                   "frames_per_step": frames // args.steps},
+                   "frames_per_step": frames // args.steps,
+                   "parallelism": f"frames by time range x{world}, RCCL reduce" if world > 1 else "1 GPU"},
+        "n_gpus": world, "scaling": "strong", "emulated_world": shard_world,
         "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK if achieved else None,
                      "traffic": traffic, "traffic_detail": tdetail,
@@ -506,7 +532,7 @@ def run_c8(args, torch, dev):
     traffic, tdetail = None, "not collected (--no-traffic)"
     if not args.no_traffic:
         import bench
-        tb, tdetail = bench.pmc_traffic("het_chain_kernel", extra=("--workload", "c8"))
+        tb, tdetail = bench.pmc_traffic(("het_chain_kernel",), extra=("--workload", "c8"))
         traffic = tb
     # the reference's instrument: 96 channels, 1 s of audio (latency-bound: one wave)
     n96, fa96, fs96, r96 = harmbank()
@@ -613,7 +639,7 @@ def run_c9(args, torch, dev):
     traffic, tdetail = None, "not collected (--no-traffic)"
     if not args.no_traffic:
         import bench
-        traffic, tdetail = bench.pmc_traffic("fb_tv_res_kernel", extra=("--workload", "c9"))
+        traffic, tdetail = bench.pmc_traffic(("fb_tv_res_kernel",), extra=("--workload", "c9"))
     # raw coefficient streams: [n][5][N] (40 B per band-sample), 4800 samples
     n2 = min(S, 4800)
     st = torch.zeros((n2, 5, N), dtype=torch.float64, device=dev)

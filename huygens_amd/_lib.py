@@ -165,6 +165,8 @@ _SIGS = {
     "hz_stft_process_block": (I, [VP, PD, PD, PD, PD, SZ]),
     "hz_stft_process_block_device": (I, [VP, VP, VP, VP, VP, SZ]),
     "hz_stft_frames": (I, [VP, C.POINTER(L), C.POINTER(L)]),
+    "hz_stft_set_frame_shard": (I, [VP, I, I, C.c_long]),
+    "hz_stft_frames_before": (I, [I, I, C.c_long, C.POINTER(C.c_long)]),
     "hz_stft_set_stream": (I, [VP, VP]),
     "hz_stft_synchronize": (I, [VP]),
     "hz_stft_profile": (I, [VP, I]),

@@ -24,6 +24,7 @@
 // Cosine: REDFT10 (DCT-II) and REDFT01 (DCT-III) through one complex FFT of length N
 // (Makhoul's even/odd reordering), in LDS, batched one transform per workgroup.
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -59,7 +60,18 @@ struct StftArgs {
     long f_lo, T0;
     int N, lg, laps, stride, R;
     double p0, p1;
+    // time-range shards: the launch's frames are this rank's runs of sh_block frames, the
+    // first run (index sh_q0) entered sh_off frames in; sh_world <= 1: f_lo, f_lo + 1, ...
+    long sh_q0, sh_block;
+    int sh_off, sh_world;
 };
+
+// the launch's i-th frame (one 64-bit divide per workgroup when sharded)
+__device__ __forceinline__ long frame_at(const StftArgs& a, long i) {
+    if (a.sh_world <= 1) return a.f_lo + i;
+    const long p = i + a.sh_off, k = p / a.sh_block;
+    return (a.sh_q0 + k * a.sh_world) * a.sh_block + (p - k * a.sh_block);
+}
 
 __host__ __device__ __forceinline__ long frame_start(long f, int laps, int stride, int N) {
     const long c = f / (2 * laps);
@@ -222,7 +234,7 @@ __global__ __launch_bounds__(kFrameThreads) void stft_frame_kernel(StftArgs a) {
     double2* T = (double2*)(scratch + 2 * (blockDim.x >> 6));
     for (int k = threadIdx.x; k < hz::twc_len(lg); k += blockDim.x) T[k] = a.tw[k];
     const int fl = frame_of_block(blockIdx.x, gridDim.x);   // frame within the launch
-    const long f = a.f_lo + fl;
+    const long f = frame_at(a, fl);
     if constexpr (MODE != 2) {
         const long off = frame_start(f, a.laps, a.stride, N) - a.T0 + (N - 1);
         for (int k = threadIdx.x; k < N; k += blockDim.x) {
@@ -380,10 +392,11 @@ __global__ __launch_bounds__(kFrameThreads) void stft_pair_kernel(StftArgs a, lo
     double2* T = (double2*)(scratch + 2 * (blockDim.x >> 6));
     for (int k = threadIdx.x; k < hz::twc_len(lg); k += blockDim.x) T[k] = a.tw[k];
     const int pl = frame_of_block(blockIdx.x, gridDim.x);   // frame pair within the launch
-    const long f0 = a.f_lo + 2L * pl;
+    const long f0 = frame_at(a, 2L * pl);
     const bool two = 2L * pl + 1 < nf;
+    const long f1 = two ? frame_at(a, 2L * pl + 1) : f0;
     const long off0 = frame_start(f0, a.laps, a.stride, N) - a.T0 + (N - 1);
-    const long off1 = two ? frame_start(f0 + 1, a.laps, a.stride, N) - a.T0 + (N - 1) : 0;
+    const long off1 = two ? frame_start(f1, a.laps, a.stride, N) - a.T0 + (N - 1) : 0;
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
         const long u0 = off0 + k, u1 = off1 + k;   // positions in [history (N-1) | block input]
         const double v0 = u0 < N - 1 ? a.hr[u0] : a.inr[u0 - (N - 1)];
@@ -400,7 +413,7 @@ __global__ __launch_bounds__(kFrameThreads) void stft_pair_kernel(StftArgs a, lo
     hz::fft_inv_tail<RMAX>(re, im, lg, T, true);
     const long plane = (long)a.R * N;
     double* o0 = a.fo + (f0 % a.R) * N;
-    double* o1 = a.fo + ((f0 + 1) % a.R) * N;
+    double* o1 = a.fo + (f1 % a.R) * N;
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
         const int e = hz::pad16(k);
         o0[k] = re[e];
@@ -425,7 +438,20 @@ struct OlaArgs {
     const double* in_re;
     const double* in_im;
     double* hist_new;
+    // time-range shards (hz_stft_set_frame_shard): frame f is this handle's iff
+    // (f / sh_block) % sh_world == sh_rank; the others contribute nothing
+    long sh_block;
+    int sh_world, sh_rank;
+    double sh_inv;   // 1 / sh_block
 };
+
+__device__ __forceinline__ bool frame_owned(long f, long block, int world, int rank, double inv) {
+    if (world <= 1) return true;
+    long q = (long)((double)f * inv);   // f / block without a 64-bit divide (exact after the fix)
+    if (q * block > f) --q;
+    else if ((q + 1) * block <= f) ++q;
+    return (int)(q % world) == rank;
+}
 
 __global__ __launch_bounds__(256) void stft_ola_kernel(OlaArgs a) {
     const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -474,6 +500,7 @@ __global__ __launch_bounds__(256) void stft_ola_kernel(OlaArgs a) {
             }
             if (c < 0) break;
             if (r >= a.N) continue;
+            if (!frame_owned(c * 2 * a.laps + i, a.sh_block, a.sh_world, a.sh_rank, a.sh_inv)) continue;
             int row = base + i;
             if (row >= a.R) row -= a.R;
             const long q = (long)row * a.N + r;
@@ -585,6 +612,9 @@ struct hz_stft {
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     long launches = 0;
+    // time-range shards: frame f is computed here iff (f / sh_block) % sh_world == sh_rank
+    long sh_block = 1;
+    int sh_world = 1, sh_rank = 0;
 };
 
 namespace {
@@ -692,8 +722,7 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
         h->ev_used += 3;
         HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
     }
-    const long f_lo = frames_before(h, h->T), f_hi = frames_before(h, h->T + n);
-    const long nf = f_hi - f_lo;
+    const long f_first = frames_before(h, h->T), f_done = frames_before(h, h->T + n);
     StftArgs a;
     a.hr = hc;
     a.hi = nullptr;
@@ -703,9 +732,6 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
     a.spec = h->d_spec;
     a.win = h->d_win;
     a.tw = h->d_tw;
-    a.f_lo = f_lo;
-    // frames start in increasing order: the first one decides whether any reads an Im part
-    if (nf > 0 && frame_start(f_lo, h->laps, h->stride, N) <= h->last_cplx) a.hi = hc + (N - 1);
     a.T0 = h->T;
     a.N = N;
     a.lg = h->lg;
@@ -714,31 +740,54 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
     a.R = h->R;
     a.p0 = h->p0;
     a.p1 = h->p1;
-    if (nf > 0) {
-        if (h->proc != HZ_PROC_HOST) {
-            // profiling may repeat the (idempotent) frame launch so the event pair brackets
-            // several back-to-back launches: per-launch time without the event overhead
-            for (int r = 0; r < (h->prof ? h->prof_repeat : 1); ++r) HZ_TRY(frames_fused(h, a, nf));
-        } else {
-            HZ_TRY(ensure_dev((void**)&h->d_spec, &h->spec_cap, sizeof(double2) * (size_t)nf * N));
-            a.spec = h->d_spec;
-            launch_frames<HZ_PROC_IDENTITY, 1>(h, a, nf);
-            HZ_TRY_HIP(hipGetLastError());
-            h->h_spec.resize((size_t)nf * N);
-            HZ_TRY_HIP(hipMemcpyAsync(h->h_spec.data(), h->d_spec, sizeof(double2) * (size_t)nf * N,
-                                      hipMemcpyDeviceToHost, h->stream));
-            HZ_TRY_HIP(hipStreamSynchronize(h->stream));
-            for (long f = f_lo; f < f_hi; ++f) {   // frame order == the reference's order
-                const int slot = (int)(f % (2 * h->laps));
-                double2* so = &h->h_out[(size_t)slot * N];
-                double2* sp = &h->h_spec[(size_t)(f - f_lo) * N];
-                h->host_proc((const double*)sp, (double*)so);
-                std::memcpy(sp, so, sizeof(double2) * N);
+    // time-range shards: this handle's frames of the block, as one launch (frame_at maps the
+    // launch's frames onto its runs); unsharded: the whole block
+    long f_lo = f_first, nf = f_done - f_first;
+    a.sh_world = h->sh_world;
+    a.sh_block = h->sh_block;
+    a.sh_q0 = 0;
+    a.sh_off = 0;
+    if (h->sh_world > 1 && nf > 0) {
+        const long B = h->sh_block, W = h->sh_world;
+        long q = f_first / B;
+        const long q0 = q + ((h->sh_rank - q % W) % W + W) % W;   // first run of this rank
+        a.sh_q0 = q0;
+        a.sh_off = q0 == q ? (int)(f_first - q * B) : 0;
+        f_lo = q0 * B + a.sh_off;
+        nf = 0;
+        for (q = q0; q * B < f_done; q += W) nf += std::min(f_done, (q + 1) * B) - std::max(f_first, q * B);
+    }
+    {
+        const long f_hi = f_lo + nf;   // (unsharded: host-processor frames are f_lo .. f_hi - 1)
+        a.f_lo = f_lo;
+        // frames start in increasing order: the first one decides whether any reads an Im part
+        a.hi = (nf > 0 && frame_start(f_lo, h->laps, h->stride, N) <= h->last_cplx) ? hc + (N - 1) : nullptr;
+        if (nf > 0) {
+            if (h->proc != HZ_PROC_HOST) {
+                // profiling may repeat the (idempotent) frame launch so the event pair brackets
+                // several back-to-back launches: per-launch time without the event overhead
+                for (int r = 0; r < (h->prof ? h->prof_repeat : 1); ++r) HZ_TRY(frames_fused(h, a, nf));
+            } else {
+                HZ_TRY(ensure_dev((void**)&h->d_spec, &h->spec_cap, sizeof(double2) * (size_t)nf * N));
+                a.spec = h->d_spec;
+                launch_frames<HZ_PROC_IDENTITY, 1>(h, a, nf);
+                HZ_TRY_HIP(hipGetLastError());
+                h->h_spec.resize((size_t)nf * N);
+                HZ_TRY_HIP(hipMemcpyAsync(h->h_spec.data(), h->d_spec, sizeof(double2) * (size_t)nf * N,
+                                          hipMemcpyDeviceToHost, h->stream));
+                HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+                for (long f = f_lo; f < f_hi; ++f) {   // frame order == the reference's order
+                    const int slot = (int)(f % (2 * h->laps));
+                    double2* so = &h->h_out[(size_t)slot * N];
+                    double2* sp = &h->h_spec[(size_t)(f - f_lo) * N];
+                    h->host_proc((const double*)sp, (double*)so);
+                    std::memcpy(sp, so, sizeof(double2) * N);
+                }
+                HZ_TRY_HIP(hipMemcpyAsync(h->d_spec, h->h_spec.data(), sizeof(double2) * (size_t)nf * N,
+                                          hipMemcpyHostToDevice, h->stream));
+                launch_frames<HZ_PROC_IDENTITY, 2>(h, a, nf);
+                HZ_TRY_HIP(hipGetLastError());
             }
-            HZ_TRY_HIP(hipMemcpyAsync(h->d_spec, h->h_spec.data(), sizeof(double2) * (size_t)nf * N,
-                                      hipMemcpyHostToDevice, h->stream));
-            launch_frames<HZ_PROC_IDENTITY, 2>(h, a, nf);
-            HZ_TRY_HIP(hipGetLastError());
         }
     }
     if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
@@ -757,13 +806,17 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
     o.in_re = d_re;
     o.in_im = d_im;
     o.hist_new = hn;
+    o.sh_block = h->sh_block;
+    o.sh_world = h->sh_world;
+    o.sh_rank = h->sh_rank;
+    o.sh_inv = 1.0 / (double)h->sh_block;
     const long threads = std::max(n, (long)N - 1);
     hipLaunchKernelGGL(stft_ola_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, o);
     HZ_TRY_HIP(hipGetLastError());
     if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     h->hcur ^= 1;   // the overlap-add launch wrote the next block's history
     h->T += n;
-    h->frames = f_hi;
+    h->frames = f_done;
     h->launches += h->prof ? 1 : 0;
     return HZ_OK;
 }
@@ -908,6 +961,32 @@ int hz_stft_process_block(hz_stft* h, const double* re, const double* im, double
     if (out_im)
         HZ_TRY_HIP(hipMemcpyAsync(out_im, h->d_out + n, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+int hz_stft_set_frame_shard(hz_stft* h, int rank, int world, long block) {
+    HZ_TRY(stft_check(h));
+    if (world < 1 || rank < 0 || rank >= world || block < 1) {
+        hz::set_error("hz_stft_set_frame_shard: bad shard (rank %d of %d, block %ld)", rank, world, block);
+        return HZ_E_INVALID;
+    }
+    if (h->proc == HZ_PROC_HOST && world > 1) {
+        hz::set_error("hz_stft_set_frame_shard: a host processor sees every frame in order (replicas only)");
+        return HZ_E_UNSUPPORTED;
+    }
+    h->sh_rank = rank;
+    h->sh_world = world;
+    h->sh_block = block;
+    return HZ_OK;
+}
+
+int hz_stft_frames_before(int N, int laps, long samples, long* frames) {
+    if (!frames || !pow2(N) || laps <= 0 || laps > N || samples < 0) return HZ_E_INVALID;
+    hz_stft tmp;
+    tmp.N = N;
+    tmp.laps = laps;
+    tmp.stride = N / laps;
+    *frames = frames_before(&tmp, samples);
     return HZ_OK;
 }
 

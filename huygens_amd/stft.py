@@ -74,6 +74,11 @@ class Fourier:
         check(self._lib.hz_stft_frames(self._h, C.byref(f), C.byref(t)))
         return f.value, t.value
 
+    def set_frame_shard(self, rank: int, world: int, block: int):
+        """Time-range shard: compute frame f iff (f // block) % world == rank
+        (hz_stft_set_frame_shard); the ranks' outputs sum to the unsharded output."""
+        check(self._lib.hz_stft_set_frame_shard(self._h, int(rank), int(world), int(block)))
+
     def set_stream(self, stream_ptr):
         check(self._lib.hz_stft_set_stream(self._h, C.c_void_p(stream_ptr or 0)))
 
@@ -89,6 +94,13 @@ class Fourier:
         a, b, c = C.c_double(), C.c_double(), C.c_long()
         check(self._lib.hz_stft_profile_read(self._h, C.byref(a), C.byref(b), C.byref(c)))
         return a.value, b.value, c.value
+
+
+def frames_before(N: int, laps: int, samples: int) -> int:
+    """Frames completing within the first `samples` samples (hz_stft_frames_before)."""
+    f = C.c_long()
+    check(load().hz_stft_frames_before(N, laps, int(samples), C.byref(f)))
+    return f.value
 
 
 class StaticSTFT(Fourier):

@@ -261,6 +261,17 @@ int hz_stft_process_block(hz_stft* h, const double* re, const double* im, double
 int hz_stft_process_block_device(hz_stft* h, const double* d_re, const double* d_im, double* d_out_re,
                                  double* d_out_im, size_t n);
 int hz_stft_frames(hz_stft* h, long* frames, long* samples);
+/* Time-range shards (STFT): runs of `block` consecutive frames rotate over
+ * `world` ranks; this handle computes frame f iff (f / block) % world == rank.  Its other
+ * frames are skipped and add nothing to its overlap-add -- in this call or the later calls a
+ * frame's window still overlaps -- so the ranks' outputs sum (RCCL reduce) to the unsharded
+ * output for any call sizes.  Every rank still streams the whole input (the frame schedule and
+ * the history are the reference's).  world == 1: every frame (the default).  Device
+ * processors only: HZ_E_UNSUPPORTED with a host processor (it sees every frame in order --
+ * replicas only). */
+int hz_stft_set_frame_shard(hz_stft* h, int rank, int world, long block);
+/* frames completing within the first `samples` input samples of an (N, laps) engine */
+int hz_stft_frames_before(int N, int laps, long samples, long* frames);
 int hz_stft_set_stream(hz_stft* h, void* hip_stream);
 int hz_stft_synchronize(hz_stft* h);
 /* Event timing of the frame and overlap-add kernels.  enable > 1 repeats each block's

@@ -199,3 +199,52 @@ def test_errors(gpu_lib):
         Fourier(0, 16384, 4)
     with pytest.raises(HZError):
         Cosine(12)
+
+
+@pytest.mark.parametrize("world,block,kind", [(2, 5, "static"), (3, 16, "static"), (3, 1000, "static"),
+                                              (2, 3, "hilbert"), (4, 7, "gate")])
+def test_time_range_shards_sum(gpu_lib, world, block, kind):
+    """SURVEY.md 8(e) STFT row: frames by time range.  Runs of `block` frames rotate over
+    `world` handles (hz_stft_set_frame_shard); their outputs sum to the unsharded engine's
+    output across ragged calls -- a frame's overlap-add tail that lands in a later call stays
+    with the rank that computed it.  static: two frames per transform (real input); hilbert:
+    one frame per transform over complex input; gate: Fourier(gate625), real input."""
+    from huygens_amd.stft import PROC_GATE_KEEP, PROC_HILBERT, Fourier, StaticSTFT
+    N, laps = 1024, 4
+    rng = np.random.default_rng(50 + world)
+    x = rng.standard_normal(30000) * 0.1 + np.sin(np.arange(30000) * 0.05)
+    xi = rng.standard_normal(30000) * 0.1 if kind == "hilbert" else None
+    make = {"static": lambda: StaticSTFT(N, laps), "hilbert": lambda: Fourier(PROC_HILBERT, N, laps),
+            "gate": lambda: Fourier(PROC_GATE_KEEP, N, laps)}[kind]
+    full = make()
+    shards = [make() for _ in range(world)]
+    for r, sh in enumerate(shards):
+        sh.set_frame_shard(r, world, block)
+    t = 0
+    for n in (5000, 333, 1, 12000, 12666):
+        sl = slice(t, t + n)
+        ref = full.process_block(x[sl], None if xi is None else xi[sl])
+        got = [np.zeros(n), np.zeros(n)]
+        for sh in shards:
+            o = sh.process_block(x[sl], None if xi is None else xi[sl])
+            got[0] += o[0]
+            got[1] += o[1]
+        for g, rf in zip(got, ref):
+            assert np.max(np.abs(g - rf)) <= 1e-12 * max(1.0, np.max(np.abs(rf))), n
+        t += n
+    assert all(sh.frames() == full.frames() for sh in shards)
+
+
+def test_frame_shard_args(gpu_lib):
+    from huygens_amd._lib import HZ_E_INVALID, HZ_E_UNSUPPORTED, HZError
+    from huygens_amd.stft import Fourier, StaticSTFT
+    f = Fourier(lambda a, b: b.__setitem__(slice(None), a), 64, 4)
+    with pytest.raises(HZError) as ei:
+        f.set_frame_shard(0, 2, 10)
+    assert ei.value.code == HZ_E_UNSUPPORTED
+    f.set_frame_shard(0, 1, 10)   # one rank: every frame, allowed
+    s = StaticSTFT(64, 4)
+    for bad in ((2, 2, 1), (-1, 2, 1), (0, 0, 1), (0, 2, 0)):
+        with pytest.raises(HZError) as ei:
+            s.set_frame_shard(*bad)
+        assert ei.value.code == HZ_E_INVALID
