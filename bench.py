@@ -233,6 +233,7 @@ def main():
     seg_ms, mix_ms, red_ms, launches = fb.profile_read()
     from huygens_amd._lib import HZ_FB_PATH_LTI
     lti = fb.last_path() == HZ_FB_PATH_LTI
+    chunk = fb.lti_chunk()   # the timed steps' chunk (the streaming calls below use a shorter one)
     fb.profile(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -282,7 +283,7 @@ def main():
         band_samples_per_launch = cnt * S * args.steps / max(1, launches)
         flops_per_launch = FLOPS_PER_BAND_SAMPLE * band_samples_per_launch
         achieved = flops_per_launch / launch_avg_s / 1e12 if launch_avg_s > 0 else None
-        xflops = fb_executed_flops(lti, fb.lti_chunk())
+        xflops = fb_executed_flops(lti, chunk)
         executed = xflops * band_samples_per_launch / launch_avg_s / 1e12 if launch_avg_s > 0 else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -317,9 +318,9 @@ def main():
                          "algorithmic_bytes_per_launch": (16 * S + 120 * cnt) * args.steps / max(1, launches),
                          "launches_per_step": launches / max(1, args.steps),
                          "kernel": (("LTI engine step: fb_lti_kernel<2,64,STATE> + fb_lti_gemm_kernel + "
-                                     "fb_lti_reduce_kernel (+ segment prepass)") if lti and fb.lti_chunk() == 64 else
+                                     "fb_lti_reduce_kernel (+ segment prepass)") if lti and chunk == 64 else
                                     ("LTI engine step: fb_lti_kernel<2,%d,MIX> + fb_lti_reduce_kernel (+ segment "
-                                     "prepass)" % fb.lti_chunk()) if lti
+                                     "prepass)" % chunk) if lti
                                     else "general engine step: fb_mix_kernel<2,NONE,1,MIX> + fb_reduce_kernel"),
                          "kernel_avg_ms": 1e3 * launch_avg_s,
                          "components_ms_per_launch": {"segment_prepass": seg_ms / max(1, launches),
