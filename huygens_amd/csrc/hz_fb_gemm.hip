@@ -27,8 +27,9 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // the zero-state term, by fb_lti_reduce_kernel.
 constexpr int kBRow = 64 + 16;        // LDS row: the two 16-lane halves of a ds_read_b64 on disjoint banks
 
-// RB: tiles (16-chunk row blocks per wave) per workgroup; kD: k-steps (4 band states each) per stage
-template <int RB, int kD>
+// RB: tiles (16-chunk row blocks per wave) per workgroup; kD: k-steps (4 band states each) per stage;
+// ABL (diagnostics, HZ_FB_GEMM_ABL; wrong results): bit 0 skips the GS loads, bit 1 the K loads
+template <int RB, int kD, int ABL = 0>
 __global__ __launch_bounds__(256) void fb_lti_gemm_kernel(const double* __restrict__ gs,
                                                           const double* __restrict__ kt, int kslice, int bs_pad,
                                                           int ntiles, double* __restrict__ part, long n_pad) {
@@ -61,6 +62,13 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_kernel(const double* __restri
     // full stages load unguarded; only a slice's last stage can hold rows past b1
     const int nfull = (b1 - b0) / kRows;
     auto load_a = [&](int s, double (&av)[RB][kD]) {
+        if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+            for (int t = 0; t < RB; ++t)
+#pragma unroll
+                for (int u = 0; u < kD; ++u) av[t][u] = 1e-3 * (u + s);
+            return;
+        }
 #pragma unroll
         for (int t = 0; t < RB; ++t) {
             if (s < nfull) {
@@ -78,6 +86,11 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_kernel(const double* __restri
         }
     };
     auto load_b = [&](int s, d2 (&bv)[BH][2]) {
+        if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+            for (int h = 0; h < BH; ++h) bv[h][0] = bv[h][1] = d2{1e-3 * s, 2e-3};
+            return;
+        }
 #pragma unroll
         for (int h = 0; h < BH; ++h) {
             const bool ok = s < nfull || b0 + kRows * s + 16 * h + brow < b1;
@@ -182,8 +195,12 @@ int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* p
     S = std::min(S, bs_pad / 4);
     const int kslice = ((bs_pad + S - 1) / S + 3) & ~3;   // (stages past b1 read as 0)
     S = (bs_pad + kslice - 1) / kslice;
+    static const int abl = std::getenv("HZ_FB_GEMM_ABL") ? std::atoi(std::getenv("HZ_FB_GEMM_ABL")) : 0;
     auto k = rb == 2 ? (kd == 8 ? fb_lti_gemm_kernel<2, 8> : fb_lti_gemm_kernel<2, 4>)
                      : (kd == 8 ? fb_lti_gemm_kernel<1, 8> : fb_lti_gemm_kernel<1, 4>);
+    if (abl == 1) k = fb_lti_gemm_kernel<1, 4, 1>;
+    if (abl == 2) k = fb_lti_gemm_kernel<1, 4, 2>;
+    if (abl == 3) k = fb_lti_gemm_kernel<1, 4, 3>;
     hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)S), dim3(256), 0, stream, gs, kt, kslice, bs_pad, ntiles, part,
                        n_pad);
     HZ_TRY_HIP(hipGetLastError());

@@ -26,6 +26,7 @@
 // i.e. O(L+O) + O L FMAs per chunk instead of running the recurrence twice per
 // sample (hz_filterbank.hip's general kernel).  The result is the same linear map
 // evaluated in another association order (parity: tests/test_filterbank_lti_gpu.py).
+#include <cstdio>
 #include <cstdlib>
 
 #include "hz_fb_impl.h"
@@ -181,7 +182,7 @@ struct LtiArgs {
     double* xhist_next;     // [O]
     double* partial;        // [G][n_pad] (n_pad = row stride)
     double* gs_out;         // MODE_STATE: [tile][bs_pad][64 chunks] gin x chunk start states
-    int bs_pad;             // band-state rows per tile (N O rounded up to 4; pad rows written 0)
+    int bs_pad;             // band-state rows per tile (lti_bs_rows: every wave's O rows; pad rows written 0)
     double* segstate;       // [N][nseg_state][O] start states of the (prepass-fine) segments
     long n;                 // samples in this launch (multiple of L)
     long n_pad;             // slab row stride (the tile-padded length)
@@ -192,6 +193,8 @@ struct LtiArgs {
     int seg_stride;         // segstate index of segment s: s * seg_stride
     int nbands;
     double sp_n, sg_n;      // sp^n, sg^n (closed-form smoother end state)
+    long long* dbg;         // diagnostics (ABL bit 4): per-wave phase timestamps of one workgroup
+    int scan_first;         // MODE_STATE: (S) of tile it before (E) of tile it + 1
 };
 
 // LDS: x tile x[t0-O .. t0+64L-1] stored at pos(li) = li + li / L (one pad slot per
@@ -206,6 +209,10 @@ __host__ __device__ constexpr int lti_xs_pad() {
 // 8 for O >= 3 (LDS).  BS = band states of a group, padded to the 16-wide MFMA blocks.
 __host__ __device__ constexpr int lti_waves(int O) { return O <= 2 ? 16 : 8; }
 __host__ __device__ constexpr int lti_bsp(int O) { return (lti_waves(O) * O + 15) / 16 * 16; }
+// GS / Kt rows (band states) of a bank: O rows for every wave of every group, so the state
+// kernel's stores need no row guard (a conditional store makes the compiler's x-staging
+// waits drain them: vmcnt(0) instead of vmcnt(2))
+static inline int lti_bs_rows(int N, int O) { return (N + lti_waves(O) - 1) / lti_waves(O) * lti_waves(O) * O; }
 constexpr int kZRow = 65;   // z rows [BSP][64 chunks + 1]: E-block writes hit 16 banks apart
 constexpr int kGsRow = 80;  // gs rows [BSP][64 chunks + 16]: mix A-operand reads on disjoint bank halves
 // chunk 64: the mix B operands (K rows) live in LDS instead of registers (the chunk's 17-step E
@@ -233,6 +240,15 @@ __device__ __forceinline__ double dpp_dm(double v) {
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWMASK, 0xf, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// the same move with an explicit old value for the rows outside ROWMASK (a dead register of the
+// caller: no zero materialised; the caller's coefficients for those rows are 0)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_dm_old(double old, double v) {
+    const long long b = __double_as_longlong(v), o = __double_as_longlong(old);
+    const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffff), (int)(b & 0xffffffff), CTRL, ROWMASK, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, ROWMASK, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 constexpr int kDppWaveShr1 = 0x138;   // lane l <- lane l-1 across rows (gfx950: probed)
 constexpr int kDppRowBcast15 = 0x142; // rows 1, 3 <- lane 15 of the row below (row_mask 0xa)
 constexpr int kDppRowBcast31 = 0x143; // rows 2, 3 <- lane 31 (row_mask 0xc)
@@ -252,7 +268,11 @@ constexpr int kDppRowBcast31 = 0x143; // rows 2, 3 <- lane 31 (row_mask 0xc)
 //  (M) the group's correction mix D[chunk][j] = sum_bs gs[bs][chunk] K[bs][j] on the
 //      matrix cores, stored as this group's row of the partial slab.
 // The (E) and (M) blocks are spread over the waves as independent work items.
-template <int O, int L, int MODE>
+// ABL (diagnostics, HZ_FB_LTI_ABL): bit 0 skips the (E) MFMA chains, bit 1 the (S) scan steps,
+// bit 2 the GS stores, bit 3 the x tile loads; bit 4 records s_memtime stamps per wave and
+// iteration for workgroup 100 (loop top, after E, after S, after the x store) --
+// wrong results, timed by rocprof to split the state kernel's time (scripts/abl_state.sh)
+template <int O, int L, int MODE, int ABL = 0>
 __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double* __restrict__ rec, LtiArgs a) {
     using R = RecL<O, L>;
     constexpr int W = lti_waves(O);
@@ -275,6 +295,12 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     // chains of the same SIMD's other waves.)
     constexpr int IPE = (NE + W - 1) / W;
     constexpr int IPM = (NM + W - 1) / W;
+    // MODE_STATE with fewer E blocks than half the waves: the waves without E blocks stage the
+    // x tiles alone, at the top of the iteration, from registers loaded one iteration earlier, so
+    // the E waves (the critical path: MFMA chain, then their scan) never wait on x staging
+    constexpr bool kSplit = MODE == MODE_STATE && NE <= W / 2 && (64 * (W - NE)) % L == 0;
+    constexpr int WS = kSplit ? W - NE : W;                  // staging waves
+    constexpr int PF2 = (XS + 64 * WS - 1) / (64 * WS);      // x values per staging thread
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* zb = lds + 2 * XSP;      // [2][BSP][kZRow]
     double* gsb = zb + 2 * BSP * kZRow;  // [2][BSP][kGsRow]
@@ -311,14 +337,17 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
 
     // per-lane chunk-transition powers: M^l (carry-in), M^(p+1) (row_bcast:15), M^(l-31)
     // (row_bcast:31); loop-invariant
+    // (qa is 0 on rows 0, 2 and qb on rows 0, 1: the bcast moves leave those rows' old values,
+    // which are finite, and the FMAs then add exactly 0)
     double qc[O * O], qa[O * O], qb[O * O];
     {
         const int ea = (lane & 15) + 1, eb = lane >= 32 ? lane - 31 : 0;
+        const bool wa = (lane >> 4) & 1, wb = lane >= 32;
 #pragma unroll
         for (int e = 0; e < O * O; ++e) {
             qc[e] = r[R::QC + lane * O * O + e];
-            qa[e] = r[R::QC + ea * O * O + e];
-            qb[e] = r[R::QC + eb * O * O + e];
+            qa[e] = wa ? r[R::QC + ea * O * O + e] : 0.0;
+            qb[e] = wb ? r[R::QC + eb * O * O + e] : 0.0;
         }
     }
 
@@ -338,8 +367,9 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
             const int sb = item >> 2, tap = 4 * q + (lane >> 4), bs = 16 * sb + (lane & 15);
             const int bl = bs / O, k = bs % O, bnd = grp_band0 + bl;
             if (item < NE && bl < W && bnd < a.nbands && tap < XW) {
+                // pin folded in: the E blocks produce pin z (the scan's input) directly
                 const double* rb = rec + (long)bnd * R::SIZE;
-                val = tap < O ? rb[R::EH + k * O + tap] : (tap + k < XW ? rb[R::E0 + tap + k] : 0.0);
+                val = a.pin[bnd] * (tap < O ? rb[R::EH + k * O + tap] : (tap + k < XW ? rb[R::E0 + tap + k] : 0.0));
             }
             bop_e[v][q] = val;
         }
@@ -376,23 +406,66 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                                                  0x00020000);
     }();
     auto load_x = [&](long t0x, double (&pf)[PF]) {
+        if constexpr ((ABL & 8) != 0) {
+#pragma unroll
+            for (int q = 0; q < PF; ++q) pf[q] = (double)q;
+            return;
+        }
         const int v0 = (int)((t0x - O) * (long)sizeof(double)) + (int)threadIdx.x * (int)sizeof(double);
 #pragma unroll
         for (int q = 0; q < PF; ++q)
             pf[q] = __builtin_bit_cast(   // the whole offset in voffset: soffset is outside the range check
                 double, __builtin_amdgcn_raw_buffer_load_b64(xrsrc, v0 + q * 64 * W * (int)sizeof(double), 0, 0));
     };
+    // in-loop tiles (t0x >= O): a descriptor based at x[t0x - O] (scalar math per tile) with
+    // loop-invariant lane offsets; records past seg_end read 0
+    // staging thread index: all threads, or (kSplit) the threads of waves NE .. W-1
+    const int sid = kSplit ? (int)threadIdx.x - 64 * NE : (int)threadIdx.x;
+    const int vq0 = sid * (int)sizeof(double);
+    auto load_x_loop = [&](long t0x, double (&pf)[PF2]) {
+        if constexpr ((ABL & 8) != 0) {
+#pragma unroll
+            for (int q = 0; q < PF2; ++q) pf[q] = (double)q;
+            return;
+        }
+        const unsigned long long xb = (unsigned long long)(a.x + (t0x - O));
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)xb);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(xb >> 32));
+        const long rem = (seg_end - (t0x - O)) * (long)sizeof(double);
+        const int bytes = __builtin_amdgcn_readfirstlane((int)(rem > 0 ? rem : 0));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(((unsigned long long)hi << 32) | lo), (short)0, bytes, 0x00020000);
+#pragma unroll
+        for (int q = 0; q < PF2; ++q)
+            pf[q] = __builtin_bit_cast(
+                double, __builtin_amdgcn_raw_buffer_load_b64(rs, vq0 + q * 64 * WS * (int)sizeof(double), 0, 0));
+    };
+    // LDS position of x[t0x - O + li] is li + li / L; li = tid + q 64 W with 64 W a multiple of L,
+    // so position = (tid + tid / L) + q (64 W + 64 W / L): one base, immediate offsets per q
+    const int xpos0 = (int)threadIdx.x + (int)threadIdx.x / L;
+    const int xposs = sid + sid / L;
+    auto store_x_loop = [&](double* xbuf, const double (&pf)[PF2]) {   // in-loop tiles (t0x > 0)
+        double* xb = xbuf + xposs;
+#pragma unroll
+        for (int q = 0; q < PF2; ++q) {
+            const int li = sid + q * 64 * WS;
+            if (li < XS) xb[q * (64 * WS + 64 * WS / L)] = pf[q];
+        }
+    };
     auto store_x = [&](double* xbuf, const double (&pf)[PF], long t0x) {
+        static_assert((64 * W) % L == 0, "x staging stride must be a multiple of the chunk");
+        double* xb = xbuf + xpos0;
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
             const int li = threadIdx.x + q * 64 * W;
-            if (li < XS) xbuf[li + li / L] = pf[q];
+            if (li < XS) xb[q * (64 * W + 64 * W / L)] = pf[q];
         }
         if (t0x == 0 && threadIdx.x < O) xbuf[threadIdx.x] = a.xhist[O - 1 - threadIdx.x];  // x[-O+li]
     };
 
     // (E) for tile te: this wave's E blocks -> z buffer (te & 1)
     auto phase_e = [&](int te) {
+        if constexpr ((ABL & 1) != 0) return;
         const double* xs = lds + (te & 1) * XSP;
         double* z = zb + (te & 1) * BSP * kZRow;
 #pragma unroll
@@ -479,14 +552,33 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         phase_e(0);
         __syncthreads();
     }
+    const bool stager = !kSplit || wave >= NE;
+    double pf[PF2];   // staging registers: x tile it + 2, loaded during iteration it - 1 (kSplit)
+    if (kSplit && stager && ntiles > 2) load_x_loop(seg_t0 + 2 * T, pf);
 
     double st[O];
+    double* go_run = MODE == MODE_STATE ? a.gs_out + ((seg_t0 / T) * a.bs_pad + (long)band * O) * 64 + lane : nullptr;
     const int niter = (MODE == MODE_MIX) ? ntiles + 1 : ntiles;
+    auto stamp = [&](int it, int slot) {
+        if constexpr ((ABL & 16) != 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            const long long tt = __builtin_amdgcn_s_memtime();
+            if (blockIdx.x == 100 && lane == 0 && it < 64) a.dbg[((long)wave * 64 + it) * 4 + slot] = tt;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
     for (int it = 0; it < niter; ++it) {
         const long t0 = seg_t0 + (long)it * T;
-        double pf[PF];
+        stamp(it, 0);
         const bool stage = it + 2 < ntiles;
-        if (stage) load_x(t0 + 2 * T, pf);
+        if constexpr (kSplit) {
+            if (stager) {
+                if (stage) store_x_loop(lds + (it & 1) * XSP, pf);   // tile it + 2 (its buffer's tile it is done)
+                if (it + 3 < ntiles) load_x_loop(t0 + 3 * T, pf);
+            }
+        } else {
+            if (stage) load_x_loop(t0 + 2 * T, pf);
+        }
         // the three phases of an iteration touch disjoint LDS images.  Order E, M, S for every
         // wave: measured against scan-first orders for the E waves (0.554 vs 0.522 ms per C2
         // step) and for the mix-only waves (0.581)
@@ -496,24 +588,27 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                 const double* z = zb + (it & 1) * BSP * kZRow;
                 double zz[O];
 #pragma unroll
-                for (int k = 0; k < O; ++k) zz[k] = pb * z[(wave * O + k) * kZRow + lane];
+                for (int k = 0; k < O; ++k) zz[k] = z[(wave * O + k) * kZRow + lane];   // pin z (E operands)
 #define HZ_LTI_SCAN_STEP(CTRL, RM, MAT)                                                               \
     {                                                                                                 \
-        double nb_[O];                                                                                \
-        _Pragma("unroll") for (int k = 0; k < O; ++k) nb_[k] = dpp_dm<CTRL, RM>(zz[k]);               \
+        _Pragma("unroll") for (int k = 0; k < O; ++k) nb_[k] = RM == 0xf ? dpp_dm<CTRL, RM>(zz[k])    \
+                                                                       : dpp_dm_old<CTRL, RM>(nb_[k], zz[k]); \
         _Pragma("unroll") for (int rr = 0; rr < O; ++rr)                                              \
             _Pragma("unroll") for (int c = 0; c < O; ++c) zz[rr] = fma(MAT[rr * O + c], nb_[c], zz[rr]); \
     }
+                double nb_[O];
                 const double* p1 = r + R::PS;
                 const double* p2 = r + R::PS + O * O;
                 const double* p4 = r + R::PS + 2 * O * O;
                 const double* p8 = r + R::PS + 3 * O * O;
+                if constexpr ((ABL & 2) == 0) {
                 HZ_LTI_SCAN_STEP(kDppRowShr + 1, 0xf, p1)
                 HZ_LTI_SCAN_STEP(kDppRowShr + 2, 0xf, p2)
                 HZ_LTI_SCAN_STEP(kDppRowShr + 4, 0xf, p4)
                 HZ_LTI_SCAN_STEP(kDppRowShr + 8, 0xf, p8)
                 HZ_LTI_SCAN_STEP(kDppRowBcast15, 0xa, qa)
                 HZ_LTI_SCAN_STEP(kDppRowBcast31, 0xc, qb)
+                }
 #undef HZ_LTI_SCAN_STEP
                 double Sn[O];
 #pragma unroll
@@ -536,11 +631,13 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
 #pragma unroll
                         for (int k = 0; k < O; ++k) gs[(wave * O + k) * kGsRow + lane] = gb * st[k];
                     } else {   // MODE_STATE: tile-major rows of 64 chunks, row band O + k (dead
-                               // waves write the zero pad rows: gb = 0)
-                        double* go = a.gs_out + ((t0 / T) * a.bs_pad + (long)band * O) * 64 + lane;
+                               // waves write the zero pad rows: gb = 0; every wave has its rows)
+                        double* go = go_run;   // = gs_out + ((t0 / T) bs_pad + band O) 64 + lane
+                        go_run += (long)a.bs_pad * 64;
 #pragma unroll
                         for (int k = 0; k < O; ++k)
-                            if (band * O + k < a.bs_pad) __builtin_nontemporal_store(gb * st[k], go + 64 * k);
+                            if constexpr ((ABL & 4) == 0)   // unconditional: the x staging waits below
+                                __builtin_nontemporal_store(gb * st[k], go + 64 * k);   // count them exactly
                     }
                     if (last_seg && it == ntiles - 1 && live) {
                         // end-of-call y history = the start state of the chunk beginning at n
@@ -558,12 +655,24 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                 }
             }
         };
-        if (it + 1 < ntiles) phase_e(it + 1);
-        if constexpr (MODE == MODE_MIX) {
-            if (it >= 1) phase_m(it - 1);
+        if (MODE == MODE_STATE && a.scan_first) {
+            phase_s();
+            stamp(it, 1);
+            if (it + 1 < ntiles) phase_e(it + 1);
+            stamp(it, 2);
+        } else {
+            if (it + 1 < ntiles) phase_e(it + 1);
+            stamp(it, 1);
+            if constexpr (MODE == MODE_MIX) {
+                if (it >= 1) phase_m(it - 1);
+            }
+            phase_s();
+            stamp(it, 2);
         }
-        phase_s();
-        if (stage) store_x(lds + (it & 1) * XSP, pf, t0 + 2 * T);
+        if constexpr (!kSplit) {
+            if (stage) store_x_loop(lds + (it & 1) * XSP, pf);
+        }
+        stamp(it, 3);
         __syncthreads();
     }
 
@@ -794,6 +903,17 @@ constexpr int kNumLtiGeoms = 3;
 template <int O, int L>
 LtiKernel lti_kernel_mode(int mode) {
     static_assert(lti_lds_bytes<O, L>(true) <= 160 * 1024, "LTI kernel LDS over 160 KiB");
+    if constexpr (O == 2 && L == 64) {   // diagnostics: ablated state kernels (HZ_FB_LTI_ABL=1..3)
+        static const int abl = std::getenv("HZ_FB_LTI_ABL") ? std::atoi(std::getenv("HZ_FB_LTI_ABL")) : 0;
+        if (mode == MODE_STATE && abl == 1) return fb_lti_kernel<O, L, MODE_STATE, 1>;
+        if (mode == MODE_STATE && abl == 2) return fb_lti_kernel<O, L, MODE_STATE, 2>;
+        if (mode == MODE_STATE && abl == 3) return fb_lti_kernel<O, L, MODE_STATE, 3>;
+        if (mode == MODE_STATE && abl == 7) return fb_lti_kernel<O, L, MODE_STATE, 7>;
+        if (mode == MODE_STATE && abl == 11) return fb_lti_kernel<O, L, MODE_STATE, 11>;
+        if (mode == MODE_STATE && abl == 15) return fb_lti_kernel<O, L, MODE_STATE, 15>;
+        if (mode == MODE_STATE && abl == 4) return fb_lti_kernel<O, L, MODE_STATE, 4>;
+        if (mode == MODE_STATE && abl == 16) return fb_lti_kernel<O, L, MODE_STATE, 16>;
+    }
     return mode == MODE_SEGEND ? fb_lti_kernel<O, L, MODE_SEGEND>
          : mode == MODE_STATE  ? fb_lti_kernel<O, L, MODE_STATE>
                                : fb_lti_kernel<O, L, MODE_MIX>;
@@ -961,7 +1081,7 @@ int fb_prepare_lti(hz_fb* h, int gi) {
         HZ_TRY_HIP(hipMemcpyAsync(set.d_rec, host.data(), sizeof(double) * need, hipMemcpyHostToDevice, h->stream));
         HZ_TRY_HIP(hipStreamSynchronize(h->stream));  // pageable source
         if (fb_lti_gemm_geom(gi) && O > 0) {   // K rows of every band state, zero-padded to 4
-            const int bs_pad = (h->N * O + 3) & ~3, ko = lti_k_offset(O, L);
+            const int bs_pad = lti_bs_rows(h->N, O), ko = lti_k_offset(O, L);
             std::vector<double> kt((size_t)bs_pad * L, 0.0);
             for (int b = 0; b < h->N; ++b)
                 for (int k = 0; k < O; ++k)
@@ -1022,7 +1142,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
     const long ntiles_all = (n + T - 1) / T;
     // correction GEMM path: per chunk GS [bs_pad][chunks] + part [S][n_pad] instead of two slabs
     const bool gemm = fb_lti_gemm_geom(gi) && O > 0;
-    const int bs_pad = (h->N * O + 3) & ~3;
+    const int bs_pad = lti_bs_rows(h->N, O);
     long chunk = std::max<long>(T, (((1L << slab_log2) / std::max(1, G)) / T) * T);
     if (gemm) chunk = std::max<long>(T, (((1L << slab_log2) / bs_pad * L) / T) * T);
     if (!gemm && ntiles_all >= 8 * nsplit) chunk = std::min(chunk, ((ntiles_all + nsplit - 1) / nsplit) * T);
@@ -1131,6 +1251,9 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         double* slab_k = h->d_partial + (size_t)(k & 1) * slab;
         const long nc_pad = ntiles * 64;   // chunks of the launch (GEMM path)
         LtiArgs a;
+        a.dbg = nullptr;
+        static const int scan_first = std::getenv("HZ_FB_LTI_ORDER") ? std::atoi(std::getenv("HZ_FB_LTI_ORDER")) : 0;
+        a.scan_first = scan_first;
         a.pin = h->d_pin;
         a.gin = h->d_gin;
         a.ystate = h->d_ystate[h->scur];
@@ -1182,9 +1305,39 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             hipLaunchKernelGGL(kend, dim3(G, 1), dim3(64 * lti_waves(O)), lds_end, h->stream, (const double*)set.d_rec,
                                ad);
         }
+        static const bool stamps = std::getenv("HZ_FB_LTI_ABL") && std::atoi(std::getenv("HZ_FB_LTI_ABL")) == 16;
+        static long long* d_dbg = nullptr;
+        if (stamps && gemm && G > 100) {   // (diagnostics) phase timestamps, printed to stderr
+            if (!d_dbg) HZ_TRY_HIP(hipMalloc(&d_dbg, sizeof(long long) * 16 * 64 * 4));
+            HZ_TRY_HIP(hipMemsetAsync(d_dbg, 0, sizeof(long long) * 16 * 64 * 4, h->stream));
+            a.dbg = d_dbg;
+        }
         hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * lti_waves(O)), lds, h->stream,
                            (const double*)set.d_rec, a);
         HZ_TRY_HIP(hipGetLastError());
+        if (stamps && a.dbg) {
+            std::vector<long long> hd(16 * 64 * 4);
+            HZ_TRY_HIP(hipMemcpyAsync(hd.data(), d_dbg, sizeof(long long) * hd.size(), hipMemcpyDeviceToHost, h->stream));
+            HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+            for (int w = 0; w < 16; ++w) {
+                double ph[4] = {0, 0, 0, 0};
+                int cnt = 0;
+                for (int it = 8; it < 56; ++it) {
+                    const long long* q = &hd[((size_t)w * 64 + it) * 4];
+                    const long long nx = hd[((size_t)w * 64 + it + 1) * 4];
+                    if (!q[0] || !nx) continue;
+                    ph[0] += q[1] - q[0];
+                    ph[1] += q[2] - q[1];
+                    ph[2] += q[3] - q[2];
+                    ph[3] += nx - q[3];
+                    ++cnt;
+                }
+                if (cnt)
+                    std::fprintf(stderr, "stamps wave %2d: ph1 %7.0f  ph2 %7.0f  xstore %7.0f  barrier %7.0f  (cycles, %d its)\n",
+                                 w, ph[0] / cnt, ph[1] / cnt, ph[2] / cnt, ph[3] / cnt, cnt);
+            }
+            a.dbg = nullptr;
+        }
         if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
         if (gemm) {
             // correction GEMM over band-state slices (>= 4 workgroups per CU), then the slice sum
