@@ -155,6 +155,82 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_kernel(const double* __restri
     }
 }
 
+// Full-stage variant: every slice is an even number of 16-band-state stages (bs_pad and kslice
+// multiples of 32), so no load is guarded, and the loop is unrolled by two over ping-pong A
+// registers and B buffers with no exit between the halves (no register copies between stages).
+__global__ __launch_bounds__(256) void fb_lti_gemm_pp_kernel(const double* __restrict__ gs,
+                                                             const double* __restrict__ kt, int kslice, int bs_pad,
+                                                             int ntiles, double* __restrict__ part, long n_pad) {
+    constexpr int L = 64, kD = 4, kRows = 16;
+    __shared__ __attribute__((aligned(16))) double bsh[2][kRows * kBRow];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tile = blockIdx.x;
+    const int b0 = blockIdx.y * kslice;
+    const int nst = (min(bs_pad, b0 + kslice) - b0) / kRows;
+    f64x4 acc[4];
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) acc[jb] = f64x4{0.0, 0.0, 0.0, 0.0};
+    const double* ap = gs + ((long)tile * bs_pad + b0 + (lane >> 4)) * 64 + 16 * wave + (lane & 15);
+    const int brow = threadIdx.x >> 4, bcol = 4 * (threadIdx.x & 15);
+    const double* bp = kt + (long)(b0 + brow) * L + bcol;
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    auto load_a = [&](int st, double (&av)[kD]) {
+#pragma unroll
+        for (int u = 0; u < kD; ++u) av[u] = __builtin_nontemporal_load(ap + (long)(kRows * st + 4 * u) * 64);
+    };
+    auto load_b = [&](int st, d2 (&bv)[2]) {
+        const double* q = bp + (long)(kRows * st) * L;
+        bv[0] = *(const d2*)q;
+        bv[1] = *(const d2*)(q + 2);
+    };
+    auto store_b = [&](int buf, const d2 (&bv)[2]) {
+        *(d2*)&bsh[buf][brow * kBRow + bcol] = bv[0];
+        *(d2*)&bsh[buf][brow * kBRow + bcol + 2] = bv[1];
+    };
+    auto compute = [&](int buf, const double (&av)[kD]) {
+        const double* bs = bsh[buf] + (lane >> 4) * kBRow + (lane & 15);
+#pragma unroll
+        for (int u = 0; u < kD; ++u) {
+            const double* bu = bs + 4 * u * kBRow;
+            double bv[4];
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) bv[jb] = bu[16 * jb];
+#pragma unroll
+            for (int jb = 0; jb < 4; ++jb) acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[jb], acc[jb], 0, 0, 0);
+        }
+    };
+    double a0[kD], a1[kD];
+    d2 bq[2];
+    if (nst > 0) {
+        load_a(0, a0);
+        load_b(0, bq);
+        store_b(0, bq);
+    }
+    if (nst > 1) {
+        load_a(1, a1);
+        load_b(1, bq);
+    }
+    __syncthreads();
+    for (int st = 0; st < nst; st += 2) {   // nst is even
+        compute(0, a0);   // stage st
+        if (st + 2 < nst) load_a(st + 2, a0);
+        store_b(1, bq);
+        if (st + 2 < nst) load_b(st + 2, bq);
+        __syncthreads();
+        compute(1, a1);   // stage st + 1
+        if (st + 3 < nst) load_a(st + 3, a1);
+        if (st + 2 < nst) store_b(0, bq);
+        if (st + 3 < nst) load_b(st + 3, bq);
+        __syncthreads();
+    }
+    const long c0 = (long)tile * 64 + 16 * wave;
+    double* out = part + (long)blockIdx.y * n_pad + (c0 + (lane >> 4)) * L + (lane & 15);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) out[4 * rr * L + 16 * jb] = acc[jb][rr];
+}
+
 }  // namespace
 
 namespace hz_fbi {
@@ -173,14 +249,14 @@ int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* p
     }();
     static const int occ = [] {  // HZ_FB_GEMM_OCC: workgroups wanted per CU (slice count)
         const char* e = std::getenv("HZ_FB_GEMM_OCC");
-        const int v = e ? std::atoi(e) : 4;
-        return v >= 1 && v <= 16 ? v : 4;
+        const int v = e ? std::atoi(e) : 6;   // (C2, full-stage kernel: 3 / 4 / 5 / 6 per CU ->
+        return v >= 1 && v <= 16 ? v : 6;      //  0.222 / 0.215 / 0.214 / 0.210 ms with the reduce)
     }();
     if (bs_pad % 4 != 0 || ntiles <= 0) {
         hz::set_error("fb_lti_gemm_launch: bad geometry (bs_pad %d, tiles %d)", bs_pad, ntiles);
         return HZ_E_INVALID;
     }
-    // band-state slices: >= 4 workgroups per CU, each slice a multiple of 4 band states
+    // band-state slices: >= occ workgroups per CU, each slice a multiple of 4 band states
     const int gx = (ntiles + rb - 1) / rb;
     // at least 512 band states per slice: shard-sized banks (bs_pad 1024-4096) gain from fewer
     // slices for the reduce to sum (emulated 2 / 4 / 8-GPU shard steps 0.323 / 0.206 / 0.155 ->
@@ -193,7 +269,11 @@ int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* p
     int S = std::min(max_slices, std::max(1, (occ * target_groups + gx - 1) / gx));
     if (mink > 0) S = std::max(1, std::min(S, bs_pad / mink));
     S = std::min(S, bs_pad / 4);
-    const int kslice = ((bs_pad + S - 1) / S + 3) & ~3;   // (stages past b1 read as 0)
+    // full-stage kernel (default): slices of whole 16-row stages; HZ_FB_GEMM_PP=0 keeps the guarded one
+    static const bool pp = !(std::getenv("HZ_FB_GEMM_PP") && std::getenv("HZ_FB_GEMM_PP")[0] == '0');
+    const bool full = pp && bs_pad % 32 == 0 && rb == 1 && kd == 4;
+    const int kslice = full ? ((bs_pad + S - 1) / S + 31) & ~31
+                            : ((bs_pad + S - 1) / S + 3) & ~3;   // (stages past b1 read as 0)
     S = (bs_pad + kslice - 1) / kslice;
     static const int abl = std::getenv("HZ_FB_GEMM_ABL") ? std::atoi(std::getenv("HZ_FB_GEMM_ABL")) : 0;
     auto k = rb == 2 ? (kd == 8 ? fb_lti_gemm_kernel<2, 8> : fb_lti_gemm_kernel<2, 4>)
@@ -201,6 +281,7 @@ int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* p
     if (abl == 1) k = fb_lti_gemm_kernel<1, 4, 1>;
     if (abl == 2) k = fb_lti_gemm_kernel<1, 4, 2>;
     if (abl == 3) k = fb_lti_gemm_kernel<1, 4, 3>;
+    if (full && abl == 0) k = fb_lti_gemm_pp_kernel;
     hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)S), dim3(256), 0, stream, gs, kt, kslice, bs_pad, ntiles, part,
                        n_pad);
     HZ_TRY_HIP(hipGetLastError());
