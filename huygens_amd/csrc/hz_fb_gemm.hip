@@ -158,49 +158,51 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_kernel(const double* __restri
 // Full-stage variant: every slice is an even number of 16-band-state stages (bs_pad and kslice
 // multiples of 32), so no load is guarded, and the loop is unrolled by two over ping-pong A
 // registers and B buffers with no exit between the halves (no register copies between stages).
+// L = 64 or 128 samples per chunk (L / 16 accumulator blocks per wave).
+template <int L>
 __global__ __launch_bounds__(256) void fb_lti_gemm_pp_kernel(const double* __restrict__ gs,
                                                              const double* __restrict__ kt, int kslice, int bs_pad,
                                                              int ntiles, double* __restrict__ part, long n_pad) {
-    constexpr int L = 64, kD = 4, kRows = 16;
-    __shared__ __attribute__((aligned(16))) double bsh[2][kRows * kBRow];
+    constexpr int kD = 4, kRows = 16, JB = L / 16, BR = L + 16, BV = L / 32;   // BV d2 per thread
+    __shared__ __attribute__((aligned(16))) double bsh[2][kRows * BR];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int tile = blockIdx.x;
     const int b0 = blockIdx.y * kslice;
     const int nst = (min(bs_pad, b0 + kslice) - b0) / kRows;
-    f64x4 acc[4];
+    f64x4 acc[JB];
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb) acc[jb] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int jb = 0; jb < JB; ++jb) acc[jb] = f64x4{0.0, 0.0, 0.0, 0.0};
     const double* ap = gs + ((long)tile * bs_pad + b0 + (lane >> 4)) * 64 + 16 * wave + (lane & 15);
-    const int brow = threadIdx.x >> 4, bcol = 4 * (threadIdx.x & 15);
+    const int brow = threadIdx.x >> 4, bcol = 2 * BV * (threadIdx.x & 15);
     const double* bp = kt + (long)(b0 + brow) * L + bcol;
     typedef double d2 __attribute__((ext_vector_type(2)));
     auto load_a = [&](int st, double (&av)[kD]) {
 #pragma unroll
         for (int u = 0; u < kD; ++u) av[u] = __builtin_nontemporal_load(ap + (long)(kRows * st + 4 * u) * 64);
     };
-    auto load_b = [&](int st, d2 (&bv)[2]) {
+    auto load_b = [&](int st, d2 (&bv)[BV]) {
         const double* q = bp + (long)(kRows * st) * L;
-        bv[0] = *(const d2*)q;
-        bv[1] = *(const d2*)(q + 2);
+#pragma unroll
+        for (int v = 0; v < BV; ++v) bv[v] = *(const d2*)(q + 2 * v);
     };
-    auto store_b = [&](int buf, const d2 (&bv)[2]) {
-        *(d2*)&bsh[buf][brow * kBRow + bcol] = bv[0];
-        *(d2*)&bsh[buf][brow * kBRow + bcol + 2] = bv[1];
+    auto store_b = [&](int buf, const d2 (&bv)[BV]) {
+#pragma unroll
+        for (int v = 0; v < BV; ++v) *(d2*)&bsh[buf][brow * BR + bcol + 2 * v] = bv[v];
     };
     auto compute = [&](int buf, const double (&av)[kD]) {
-        const double* bs = bsh[buf] + (lane >> 4) * kBRow + (lane & 15);
+        const double* bs = bsh[buf] + (lane >> 4) * BR + (lane & 15);
 #pragma unroll
         for (int u = 0; u < kD; ++u) {
-            const double* bu = bs + 4 * u * kBRow;
-            double bv[4];
+            const double* bu = bs + 4 * u * BR;
+            double bv[JB];
 #pragma unroll
-            for (int jb = 0; jb < 4; ++jb) bv[jb] = bu[16 * jb];
+            for (int jb = 0; jb < JB; ++jb) bv[jb] = bu[16 * jb];
 #pragma unroll
-            for (int jb = 0; jb < 4; ++jb) acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[jb], acc[jb], 0, 0, 0);
+            for (int jb = 0; jb < JB; ++jb) acc[jb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[jb], acc[jb], 0, 0, 0);
         }
     };
     double a0[kD], a1[kD];
-    d2 bq[2];
+    d2 bq[BV];
     if (nst > 0) {
         load_a(0, a0);
         load_b(0, bq);
@@ -228,14 +230,14 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_pp_kernel(const double* __res
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb) out[4 * rr * L + 16 * jb] = acc[jb][rr];
+        for (int jb = 0; jb < JB; ++jb) out[4 * rr * L + 16 * jb] = acc[jb][rr];
 }
 
 }  // namespace
 
 namespace hz_fbi {
 
-int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* part, long n_pad, int ntiles,
+int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* part, long n_pad, int ntiles, int L,
                        int target_groups, int max_slices, hipStream_t stream, int* slices_out) {
     static const int rb = [] {   // tuning experiments: HZ_FB_GEMM_RB = 1 or 2 tiles per workgroup
         const char* e = std::getenv("HZ_FB_GEMM_RB");
@@ -271,7 +273,11 @@ int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* p
     S = std::min(S, bs_pad / 4);
     // full-stage kernel (default): slices of whole 16-row stages; HZ_FB_GEMM_PP=0 keeps the guarded one
     static const bool pp = !(std::getenv("HZ_FB_GEMM_PP") && std::getenv("HZ_FB_GEMM_PP")[0] == '0');
-    const bool full = pp && bs_pad % 32 == 0 && rb == 1 && kd == 4;
+    const bool full = (pp && rb == 1 && kd == 4) || L != 64;   // chunk 128: the full-stage kernel only
+    if (bs_pad % 32 != 0 || (L != 64 && L != 128)) {
+        hz::set_error("fb_lti_gemm_launch: bad geometry (bs_pad %d, chunk %d)", bs_pad, L);
+        return HZ_E_INVALID;
+    }
     const int kslice = full ? ((bs_pad + S - 1) / S + 31) & ~31
                             : ((bs_pad + S - 1) / S + 3) & ~3;   // (stages past b1 read as 0)
     S = (bs_pad + kslice - 1) / kslice;
@@ -281,7 +287,7 @@ int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* p
     if (abl == 1) k = fb_lti_gemm_kernel<1, 4, 1>;
     if (abl == 2) k = fb_lti_gemm_kernel<1, 4, 2>;
     if (abl == 3) k = fb_lti_gemm_kernel<1, 4, 3>;
-    if (full && abl == 0) k = fb_lti_gemm_pp_kernel;
+    if (full && abl == 0) k = L == 128 ? fb_lti_gemm_pp_kernel<128> : fb_lti_gemm_pp_kernel<64>;
     hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)S), dim3(256), 0, stream, gs, kt, kslice, bs_pad, ntiles, part,
                        n_pad);
     HZ_TRY_HIP(hipGetLastError());

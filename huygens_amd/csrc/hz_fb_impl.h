@@ -111,7 +111,9 @@ struct hz_fb {
         size_t kt_cap = 0;
         long horizon = -2;           // samples after which ||M^k|| < 2^-64 for every band
                                      // (-1: none within 2^18; -2: not computed yet)
-    } lti_set[3];
+    };
+    static constexpr int kLtiSets = 4;   // chunks 16, 32, 64, 128
+    LtiRecSet lti_set[kLtiSets];
     std::vector<double> pg_host;     // host mirror of the smoother state [N][2] (pre, gain)
     long mirror_pending = 0;         // samples processed since pg_host was last brought up to date
     bool converged = false;          // pg_host at the targets; cleared by every setter
@@ -146,7 +148,7 @@ int fb_lti_chunk(int geom);                // samples per lane chunk of a geomet
 bool fb_lti_gemm_geom(int geom);           // geometry runs the correction GEMM path
 // hz_fb_gemm.hip: part[s][t] = correction of sample t over band-state slice s (chunk 64); picks
 // the slice count (<= max_slices, reported in *slices_out)
-int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* part, long n_pad, int ntiles,
+int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* part, long n_pad, int ntiles, int L,
                        int target_groups, int max_slices, hipStream_t stream, int* slices_out);
 bool fb_converged(hz_fb* h);
 int fb_launch_lti(hz_fb* h, int geom, const double* d_in, double* d_out, long n);

@@ -65,6 +65,7 @@ static int lti_rec_size(int O, int L) {
     }
     if (L == 16) HZ_LTI_RS(16)
     if (L == 32) HZ_LTI_RS(32)
+    if (L == 128) HZ_LTI_RS(128)
     HZ_LTI_RS(64)
 #undef HZ_LTI_RS
 }
@@ -80,6 +81,7 @@ static int lti_k_offset(int O, int L) {
     }
     if (L == 16) HZ_LTI_KO(16)
     if (L == 32) HZ_LTI_KO(32)
+    if (L == 128) HZ_LTI_KO(128)
     HZ_LTI_KO(64)
 #undef HZ_LTI_KO
 }
@@ -158,6 +160,7 @@ static void build_record_lti_any(int O, int L, const double* b, const double* a,
     case OO:                                                                    \
         if (L == 16) build_record_lti<OO, 16>(b, a, rec);                       \
         else if (L == 32) build_record_lti<OO, 32>(b, a, rec);                  \
+        else if (L == 128) build_record_lti<OO, 128>(b, a, rec);                \
         else build_record_lti<OO, 64>(b, a, rec);                               \
         break;
     switch (O) {
@@ -194,7 +197,6 @@ struct LtiArgs {
     int nbands;
     double sp_n, sg_n;      // sp^n, sg^n (closed-form smoother end state)
     long long* dbg;         // diagnostics (ABL bit 4): per-wave phase timestamps of one workgroup
-    int scan_first;         // MODE_STATE: (S) of tile it before (E) of tile it + 1
 };
 
 // LDS: x tile x[t0-O .. t0+64L-1] stored at pos(li) = li + li / L (one pad slot per
@@ -211,8 +213,10 @@ __host__ __device__ constexpr int lti_waves(int O) { return O <= 2 ? 16 : 8; }
 __host__ __device__ constexpr int lti_bsp(int O) { return (lti_waves(O) * O + 15) / 16 * 16; }
 // GS / Kt rows (band states) of a bank: O rows for every wave of every group, so the state
 // kernel's stores need no row guard (a conditional store makes the compiler's x-staging
-// waits drain them: vmcnt(0) instead of vmcnt(2))
-static inline int lti_bs_rows(int N, int O) { return (N + lti_waves(O) - 1) / lti_waves(O) * lti_waves(O) * O; }
+// waits drain them: vmcnt(0) instead of vmcnt(2)); rounded up to 32 (whole pairs of 16-row
+// GEMM stages), the rows past the groups' zeroed per call (fb_launch_lti)
+static inline int lti_group_rows(int N, int O) { return (N + lti_waves(O) - 1) / lti_waves(O) * lti_waves(O) * O; }
+static inline int lti_bs_rows(int N, int O) { return (lti_group_rows(N, O) + 31) / 32 * 32; }
 constexpr int kZRow = 65;   // z rows [BSP][64 chunks + 1]: E-block writes hit 16 banks apart
 constexpr int kGsRow = 80;  // gs rows [BSP][64 chunks + 16]: mix A-operand reads on disjoint bank halves
 // chunk 64: the mix B operands (K rows) live in LDS instead of registers (the chunk's 17-step E
@@ -222,8 +226,17 @@ template <int O, int L>
 __host__ __device__ constexpr bool lti_k_lds() { return L == 64; }
 template <int L>
 __host__ __device__ constexpr int lti_krow() { return L + 16; }
+// chunk 128 (8192-sample tiles, state / prepass modes only): ONE x buffer (two barriers per
+// tile) and the E operands in LDS ([taps][BSP + 8]) -- their 33 k-steps do not fit registers
+template <int L>
+__host__ __device__ constexpr bool lti_x1() { return L >= 128; }
+template <int O, int L>
+__host__ __device__ constexpr int lti_ebr() { return lti_bsp(O) + 8; }
 template <int O, int L>
 __host__ __device__ constexpr size_t lti_lds_bytes(bool mix) {
+    if (lti_x1<L>())
+        return sizeof(double) * ((size_t)lti_xs_pad<O, L>() + 2 * (size_t)lti_bsp(O) * kZRow +
+                                 (size_t)((L + O + 3) / 4 * 4) * lti_ebr<O, L>());
     return sizeof(double) * (2 * (size_t)lti_xs_pad<O, L>() + 2 * (size_t)lti_bsp(O) * kZRow +
                              (mix ? 2 * (size_t)lti_bsp(O) * kGsRow : 0) +
                              (mix && lti_k_lds<O, L>() ? (size_t)lti_bsp(O) * lti_krow<L>() : 0));
@@ -298,11 +311,17 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     // MODE_STATE with fewer E blocks than half the waves: the waves without E blocks stage the
     // x tiles alone, at the top of the iteration, from registers loaded one iteration earlier, so
     // the E waves (the critical path: MFMA chain, then their scan) never wait on x staging
-    constexpr bool kSplit = MODE == MODE_STATE && NE <= W / 2 && (64 * (W - NE)) % L == 0;
+    constexpr bool X1 = lti_x1<L>();   // chunk 128: one x buffer, E operands in LDS
+    static_assert(!X1 || MODE != MODE_MIX, "chunk 128 runs the state / prepass modes only");
+    constexpr bool kSplit = (MODE == MODE_STATE || (X1 && MODE == MODE_SEGEND)) && NE <= W / 2 &&
+                            (64 * (W - NE)) % L == 0;
     constexpr int WS = kSplit ? W - NE : W;                  // staging waves
     constexpr int PF2 = (XS + 64 * WS - 1) / (64 * WS);      // x values per staging thread
+    constexpr int EBR = lti_ebr<O, L>();
+    constexpr int KER = X1 ? 1 : KE;                         // E k-steps held in registers
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* zb = lds + 2 * XSP;      // [2][BSP][kZRow]
+    double* zb = lds + (X1 ? 1 : 2) * XSP;      // [2][BSP][kZRow]
+    double* eb = zb + 2 * BSP * kZRow;          // X1: E rows [4 KE][EBR]
     double* gsb = zb + 2 * BSP * kZRow;  // [2][BSP][kGsRow]
     constexpr bool KL = lti_k_lds<O, L>() && MODE == MODE_MIX;
     constexpr int KR = lti_krow<L>();
@@ -357,21 +376,26 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     auto e_item = [&](int v) { return wave + W * v; };                         // < NE: valid
     auto m_item = [&](int v) { return (wave - NE % W + W) % W + W * v; };     // < NM: valid
     constexpr int IPMR = KL ? 0 : IPM;   // mix B operands held in registers
-    double bop_e[IPE > 0 ? IPE : 1][KE], bop_m[IPMR > 0 ? IPMR : 1][KM > 0 ? KM : 1];
+    double bop_e[IPE > 0 ? IPE : 1][KER], bop_m[IPMR > 0 ? IPMR : 1][KM > 0 ? KM : 1];
+    // E[tap][bs] with pin folded in: the E blocks produce pin z (the scan's input) directly
+    auto e_val = [&](int tap, int bs) {
+        const int bl = bs / O, k = bs % O, bnd = grp_band0 + bl;
+        if (bl < W && bnd < a.nbands && tap < XW) {
+            const double* rb = rec + (long)bnd * R::SIZE;
+            return a.pin[bnd] * (tap < O ? rb[R::EH + k * O + tap] : (tap + k < XW ? rb[R::E0 + tap + k] : 0.0));
+        }
+        return 0.0;
+    };
+    if constexpr (X1) {
+        for (int e = threadIdx.x; e < 4 * KE * BSP; e += 64 * W) eb[(e / BSP) * EBR + e % BSP] = e_val(e / BSP, e % BSP);
+    }
 #pragma unroll
-    for (int v = 0; v < IPE; ++v) {
+    for (int v = 0; v < (X1 ? 0 : IPE); ++v) {
         const int item = e_item(v);
 #pragma unroll
-        for (int q = 0; q < KE; ++q) {
-            double val = 0.0;
+        for (int q = 0; q < KER; ++q) {
             const int sb = item >> 2, tap = 4 * q + (lane >> 4), bs = 16 * sb + (lane & 15);
-            const int bl = bs / O, k = bs % O, bnd = grp_band0 + bl;
-            if (item < NE && bl < W && bnd < a.nbands && tap < XW) {
-                // pin folded in: the E blocks produce pin z (the scan's input) directly
-                const double* rb = rec + (long)bnd * R::SIZE;
-                val = a.pin[bnd] * (tap < O ? rb[R::EH + k * O + tap] : (tap + k < XW ? rb[R::E0 + tap + k] : 0.0));
-            }
-            bop_e[v][q] = val;
+            bop_e[v][q] = item < NE ? e_val(tap, bs) : 0.0;
         }
     }
     if constexpr (KL) {
@@ -466,7 +490,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     // (E) for tile te: this wave's E blocks -> z buffer (te & 1)
     auto phase_e = [&](int te) {
         if constexpr ((ABL & 1) != 0) return;
-        const double* xs = lds + (te & 1) * XSP;
+        const double* xs = lds + (X1 ? 0 : (te & 1) * XSP);
         double* z = zb + (te & 1) * BSP * kZRow;
 #pragma unroll
         for (int v = 0; v < IPE; ++v) {
@@ -482,16 +506,26 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                     const int li = li0 + 4 * q;
                     return (4 * q + (lane >> 4) < XW) ? xs[li + li / L] : 0.0;
                 };
-                double xq[EP];
+                // X1: B = E[tap 4q + (l >> 4)][bs 16 sb + (l & 15)] from LDS, read with A
+                const double* ebl = eb + (lane >> 4) * EBR + 16 * sb + (lane & 15);
+                auto eb_at = [&](int q) { return X1 ? ebl[4 * q * EBR] : 0.0; };
+                double xq[EP], bq[EP];
 #pragma unroll
-                for (int q = 0; q < EP && q < KE; ++q) xq[q] = xa_at(q);
+                for (int q = 0; q < EP && q < KE; ++q) {
+                    xq[q] = xa_at(q);
+                    if constexpr (X1) bq[q] = eb_at(q);
+                }
                 __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead (the scheduler sinks them)
 #pragma unroll
                 for (int q = 0; q < KE; ++q) {
                     const double xa = xq[q % EP];
-                    if (q + EP < KE) xq[q % EP] = xa_at(q + EP);
+                    const double bb = X1 ? bq[q % EP] : bop_e[v][X1 ? 0 : q];
+                    if (q + EP < KE) {
+                        xq[q % EP] = xa_at(q + EP);
+                        if constexpr (X1) bq[q % EP] = eb_at(q + EP);
+                    }
                     __builtin_amdgcn_sched_barrier(0);
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, bop_e[v][q], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, bb, acc, 0, 0, 0);
                 }
                 // D: col = band state 16 sb + (l & 15), row = chunk 16 m + (l >> 4) + 4 rr
 #pragma unroll
@@ -537,13 +571,19 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         }
     };
 
-    // prologue: x tiles 0 and 1 staged, gs padding rows zeroed, (E) of tile 0
+    // prologue: x tiles 0 and 1 staged (chunk 128: tile 1 after (E) of tile 0, one buffer), gs
+    // padding rows zeroed, (E) of tile 0
     {
-        double pf0[PF], pf1[PF];
+        double pf0[PF];
         load_x(seg_t0, pf0);
-        if (ntiles > 1) load_x(seg_t0 + T, pf1);
         store_x(lds, pf0, seg_t0);
-        if (ntiles > 1) store_x(lds + XSP, pf1, seg_t0 + T);
+        if constexpr (!X1) {
+            double pf1[PF];
+            if (ntiles > 1) {
+                load_x(seg_t0 + T, pf1);
+                store_x(lds + XSP, pf1, seg_t0 + T);
+            }
+        }
         if constexpr (MODE == MODE_MIX && BSP > W * O) {
             for (int e = threadIdx.x; e < 2 * BSP * kGsRow; e += 64 * W)
                 if ((e % (BSP * kGsRow)) / kGsRow >= W * O) gsb[e] = 0.0;
@@ -551,10 +591,18 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         __syncthreads();
         phase_e(0);
         __syncthreads();
+        if constexpr (X1) {
+            if (ntiles > 1) {
+                double pf1[PF];
+                load_x(seg_t0 + T, pf1);
+                store_x(lds, pf1, seg_t0 + T);
+            }
+            __syncthreads();
+        }
     }
     const bool stager = !kSplit || wave >= NE;
-    double pf[PF2];   // staging registers: x tile it + 2, loaded during iteration it - 1 (kSplit)
-    if (kSplit && stager && ntiles > 2) load_x_loop(seg_t0 + 2 * T, pf);
+    double pf[PF2];   // staging registers: x tile it + 2, loaded during iteration it - 1 (kSplit, X1)
+    if ((kSplit || X1) && stager && ntiles > 2) load_x_loop(seg_t0 + 2 * T, pf);
 
     double st[O];
     double* go_run = MODE == MODE_STATE ? a.gs_out + ((seg_t0 / T) * a.bs_pad + (long)band * O) * 64 + lane : nullptr;
@@ -567,113 +615,134 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
             __builtin_amdgcn_sched_barrier(0);
         }
     };
-    for (int it = 0; it < niter; ++it) {
-        const long t0 = seg_t0 + (long)it * T;
-        stamp(it, 0);
-        const bool stage = it + 2 < ntiles;
-        if constexpr (kSplit) {
+    auto phase_s = [&](int it, long t0) {
+        if (it < ntiles) {
+            // ---- (S) tile it: this wave's band ----
+            const double* z = zb + (it & 1) * BSP * kZRow;
+            double zz[O];
+#pragma unroll
+            for (int k = 0; k < O; ++k) zz[k] = z[(wave * O + k) * kZRow + lane];   // pin z (E operands)
+#define HZ_LTI_SCAN_STEP(CTRL, RM, MAT)                                                               \
+{                                                                                                 \
+    _Pragma("unroll") for (int k = 0; k < O; ++k) nb_[k] = RM == 0xf ? dpp_dm<CTRL, RM>(zz[k])    \
+                                                                   : dpp_dm_old<CTRL, RM>(nb_[k], zz[k]); \
+    _Pragma("unroll") for (int rr = 0; rr < O; ++rr)                                              \
+        _Pragma("unroll") for (int c = 0; c < O; ++c) zz[rr] = fma(MAT[rr * O + c], nb_[c], zz[rr]); \
+}
+            double nb_[O];
+            const double* p1 = r + R::PS;
+            const double* p2 = r + R::PS + O * O;
+            const double* p4 = r + R::PS + 2 * O * O;
+            const double* p8 = r + R::PS + 3 * O * O;
+            if constexpr ((ABL & 2) == 0) {
+            HZ_LTI_SCAN_STEP(kDppRowShr + 1, 0xf, p1)
+            HZ_LTI_SCAN_STEP(kDppRowShr + 2, 0xf, p2)
+            HZ_LTI_SCAN_STEP(kDppRowShr + 4, 0xf, p4)
+            HZ_LTI_SCAN_STEP(kDppRowShr + 8, 0xf, p8)
+            HZ_LTI_SCAN_STEP(kDppRowBcast15, 0xa, qa)
+            HZ_LTI_SCAN_STEP(kDppRowBcast31, 0xc, qb)
+            }
+#undef HZ_LTI_SCAN_STEP
+            double Sn[O];
+#pragma unroll
+            for (int k = 0; k < O; ++k) {
+                double vv = dpp_dm<kDppWaveShr1, 0xf>(zz[k]);  // Z(l-1), 0 at lane 0
+                double sn = readlane_d(zz[k], 63);
+#pragma unroll
+                for (int c = 0; c < O; ++c) {
+                    vv = fma(qc[k * O + c], S[c], vv);
+                    sn = fma(r[R::PS + 4 * O * O + k * O + c], S[c], sn);
+                }
+                st[k] = vv;
+                Sn[k] = sn;
+            }
+#pragma unroll
+            for (int k = 0; k < O; ++k) S[k] = Sn[k];
+            if constexpr (MODE != MODE_SEGEND) {
+                if constexpr (MODE == MODE_MIX) {
+                    double* gs = gsb + (it & 1) * BSP * kGsRow;
+#pragma unroll
+                    for (int k = 0; k < O; ++k) gs[(wave * O + k) * kGsRow + lane] = gb * st[k];
+                } else {   // MODE_STATE: tile-major rows of 64 chunks, row band O + k (dead
+                           // waves write the zero pad rows: gb = 0; every wave has its rows)
+                    double* go = go_run;   // = gs_out + ((t0 / T) bs_pad + band O) 64 + lane
+                    go_run += (long)a.bs_pad * 64;
+#pragma unroll
+                    for (int k = 0; k < O; ++k)
+                        if constexpr ((ABL & 4) == 0)   // unconditional: the x staging waits below
+                            __builtin_nontemporal_store(gb * st[k], go + 64 * k);   // count them exactly
+                }
+                if (last_seg && it == ntiles - 1 && live) {
+                    // end-of-call y history = the start state of the chunk beginning at n
+                    // (n is a multiple of L; chunks past n see zero input)
+                    const int cn = (int)((n - t0) / L);  // in [1, 64]
+                    if (cn < 64) {
+                        if (lane == cn)
+#pragma unroll
+                            for (int k = 0; k < O; ++k) a.ystate_next[(long)band * O + k] = st[k];
+                    } else if (lane == 0) {
+#pragma unroll
+                        for (int k = 0; k < O; ++k) a.ystate_next[(long)band * O + k] = S[k];
+                    }
+                }
+            }
+        }
+    };
+
+    if constexpr (X1) {
+        // chunk 128, one x buffer, two barriers per tile: the E waves run (E) of tile it + 1 while
+        // the others scan tile it; after the first barrier (x buffer free) the E waves scan and the
+        // staging waves store tile it + 2 from registers and load tile it + 3
+        const bool isE = !kSplit || wave < NE;
+        for (int it = 0; it < ntiles; ++it) {
+            const long t0 = seg_t0 + (long)it * T;
+            stamp(it, 0);
+            if (isE) {
+                if (it + 1 < ntiles) phase_e(it + 1);
+            } else {
+                phase_s(it, t0);
+            }
+            stamp(it, 1);
+            __syncthreads();
+            if (isE) phase_s(it, t0);
+            stamp(it, 2);
             if (stager) {
-                if (stage) store_x_loop(lds + (it & 1) * XSP, pf);   // tile it + 2 (its buffer's tile it is done)
+                if (it + 2 < ntiles) store_x_loop(lds, pf);
                 if (it + 3 < ntiles) load_x_loop(t0 + 3 * T, pf);
             }
-        } else {
-            if (stage) load_x_loop(t0 + 2 * T, pf);
+            stamp(it, 3);
+            __syncthreads();
         }
-        // the three phases of an iteration touch disjoint LDS images.  Order E, M, S for every
-        // wave: measured against scan-first orders for the E waves (0.554 vs 0.522 ms per C2
-        // step) and for the mix-only waves (0.581)
-        auto phase_s = [&]() {
-            if (it < ntiles) {
-                // ---- (S) tile it: this wave's band ----
-                const double* z = zb + (it & 1) * BSP * kZRow;
-                double zz[O];
-#pragma unroll
-                for (int k = 0; k < O; ++k) zz[k] = z[(wave * O + k) * kZRow + lane];   // pin z (E operands)
-#define HZ_LTI_SCAN_STEP(CTRL, RM, MAT)                                                               \
-    {                                                                                                 \
-        _Pragma("unroll") for (int k = 0; k < O; ++k) nb_[k] = RM == 0xf ? dpp_dm<CTRL, RM>(zz[k])    \
-                                                                       : dpp_dm_old<CTRL, RM>(nb_[k], zz[k]); \
-        _Pragma("unroll") for (int rr = 0; rr < O; ++rr)                                              \
-            _Pragma("unroll") for (int c = 0; c < O; ++c) zz[rr] = fma(MAT[rr * O + c], nb_[c], zz[rr]); \
-    }
-                double nb_[O];
-                const double* p1 = r + R::PS;
-                const double* p2 = r + R::PS + O * O;
-                const double* p4 = r + R::PS + 2 * O * O;
-                const double* p8 = r + R::PS + 3 * O * O;
-                if constexpr ((ABL & 2) == 0) {
-                HZ_LTI_SCAN_STEP(kDppRowShr + 1, 0xf, p1)
-                HZ_LTI_SCAN_STEP(kDppRowShr + 2, 0xf, p2)
-                HZ_LTI_SCAN_STEP(kDppRowShr + 4, 0xf, p4)
-                HZ_LTI_SCAN_STEP(kDppRowShr + 8, 0xf, p8)
-                HZ_LTI_SCAN_STEP(kDppRowBcast15, 0xa, qa)
-                HZ_LTI_SCAN_STEP(kDppRowBcast31, 0xc, qb)
+    } else {
+        for (int it = 0; it < niter; ++it) {
+            const long t0 = seg_t0 + (long)it * T;
+            stamp(it, 0);
+            const bool stage = it + 2 < ntiles;
+            if constexpr (kSplit) {
+                if (stager) {
+                    if (stage) store_x_loop(lds + (it & 1) * XSP, pf);   // tile it + 2 (its buffer's tile it is done)
+                    if (it + 3 < ntiles) load_x_loop(t0 + 3 * T, pf);
                 }
-#undef HZ_LTI_SCAN_STEP
-                double Sn[O];
-#pragma unroll
-                for (int k = 0; k < O; ++k) {
-                    double vv = dpp_dm<kDppWaveShr1, 0xf>(zz[k]);  // Z(l-1), 0 at lane 0
-                    double sn = readlane_d(zz[k], 63);
-#pragma unroll
-                    for (int c = 0; c < O; ++c) {
-                        vv = fma(qc[k * O + c], S[c], vv);
-                        sn = fma(r[R::PS + 4 * O * O + k * O + c], S[c], sn);
-                    }
-                    st[k] = vv;
-                    Sn[k] = sn;
-                }
-#pragma unroll
-                for (int k = 0; k < O; ++k) S[k] = Sn[k];
-                if constexpr (MODE != MODE_SEGEND) {
-                    if constexpr (MODE == MODE_MIX) {
-                        double* gs = gsb + (it & 1) * BSP * kGsRow;
-#pragma unroll
-                        for (int k = 0; k < O; ++k) gs[(wave * O + k) * kGsRow + lane] = gb * st[k];
-                    } else {   // MODE_STATE: tile-major rows of 64 chunks, row band O + k (dead
-                               // waves write the zero pad rows: gb = 0; every wave has its rows)
-                        double* go = go_run;   // = gs_out + ((t0 / T) bs_pad + band O) 64 + lane
-                        go_run += (long)a.bs_pad * 64;
-#pragma unroll
-                        for (int k = 0; k < O; ++k)
-                            if constexpr ((ABL & 4) == 0)   // unconditional: the x staging waits below
-                                __builtin_nontemporal_store(gb * st[k], go + 64 * k);   // count them exactly
-                    }
-                    if (last_seg && it == ntiles - 1 && live) {
-                        // end-of-call y history = the start state of the chunk beginning at n
-                        // (n is a multiple of L; chunks past n see zero input)
-                        const int cn = (int)((n - t0) / L);  // in [1, 64]
-                        if (cn < 64) {
-                            if (lane == cn)
-#pragma unroll
-                                for (int k = 0; k < O; ++k) a.ystate_next[(long)band * O + k] = st[k];
-                        } else if (lane == 0) {
-#pragma unroll
-                            for (int k = 0; k < O; ++k) a.ystate_next[(long)band * O + k] = S[k];
-                        }
-                    }
-                }
+            } else {
+                if (stage) load_x_loop(t0 + 2 * T, pf);
             }
-        };
-        if (MODE == MODE_STATE && a.scan_first) {
-            phase_s();
-            stamp(it, 1);
-            if (it + 1 < ntiles) phase_e(it + 1);
-            stamp(it, 2);
-        } else {
+            // the three phases of an iteration touch disjoint LDS images.  Order E, M, S for every
+            // wave: measured against scan-first orders for the E waves (0.554 vs 0.522 ms per C2
+            // step) and for the mix-only waves (0.581); scan-first on the state kernel: 0.308 vs
+            // 0.304 ms
             if (it + 1 < ntiles) phase_e(it + 1);
             stamp(it, 1);
             if constexpr (MODE == MODE_MIX) {
                 if (it >= 1) phase_m(it - 1);
             }
-            phase_s();
+            phase_s(it, t0);
             stamp(it, 2);
+            if constexpr (!kSplit) {
+                if (stage) store_x_loop(lds + (it & 1) * XSP, pf);
+            }
+            stamp(it, 3);
+            __syncthreads();
         }
-        if constexpr (!kSplit) {
-            if (stage) store_x_loop(lds + (it & 1) * XSP, pf);
-        }
-        stamp(it, 3);
-        __syncthreads();
     }
 
     if constexpr (MODE == MODE_SEGEND) {
@@ -847,6 +916,54 @@ __global__ __launch_bounds__(128) void fb_lti_reduce_kernel(const double* __rest
 // handful of workgroups, each walking all G slab rows.  Here a workgroup takes 32 samples
 // and splits the G rows over 16 slices (16 x 16 threads), summing the slices in a fixed
 // order through LDS (deterministic; a different order than the long-call kernel).
+// Chunk 128: the slice sum + zero-state term with a quarter of Fmix per workgroup (the whole
+// 128 x 130 matrix would not fit LDS): workgroup (chunk group cg, row block q) covers rows
+// j in [32 q, 32 q + 32) of 8 consecutive chunks, two samples per thread.
+constexpr int kWideRows = 32, kWideChunks = 8;
+template <int O, int L>
+__global__ __launch_bounds__(128) void fb_lti_reduce_wide_kernel(const double* __restrict__ partial, long n_pad,
+                                                                 int G, long n, const double* __restrict__ x,
+                                                                 const double* __restrict__ xhist,
+                                                                 const double* __restrict__ fmix,
+                                                                 double* __restrict__ out) {
+    constexpr int XW = L + O;
+    constexpr int NX = kWideChunks * L + O;
+    __shared__ double fm[kWideRows * XW];
+    __shared__ double xs[NX];
+    const int j0 = blockIdx.y * kWideRows;
+    const long c0 = (long)blockIdx.x * kWideChunks;
+    const long tb = c0 * L;   // first sample of the chunk group
+    for (int e = threadIdx.x; e < kWideRows * XW; e += 128) fm[e] = fmix[(long)j0 * XW + e];
+    for (int e = threadIdx.x; e < NX; e += 128) {
+        const long idx = tb - O + e;
+        xs[e] = idx >= n ? 0.0 : (idx >= 0 || !xhist) ? x[idx] : xhist[-idx - 1];
+    }
+    __syncthreads();
+    const int cc = threadIdx.x >> 4, jj = 2 * (threadIdx.x & 15);
+    const long t = tb + (long)cc * L + j0 + jj;
+    if (t >= n) return;
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    d2 s0 = {0.0, 0.0}, s1 = {0.0, 0.0};
+    const double* col = partial + t;
+    int g = 0;
+    for (; g + 2 <= G; g += 2) {
+        s0 += __builtin_nontemporal_load((const d2*)(col + (long)g * n_pad));
+        s1 += __builtin_nontemporal_load((const d2*)(col + (long)(g + 1) * n_pad));
+    }
+    for (; g < G; ++g) s0 += __builtin_nontemporal_load((const d2*)(col + (long)g * n_pad));
+    d2 acc = s0 + s1;
+    const double* xw = xs + (long)cc * L;   // x[chunk start - O + i] = xw[i]
+    const double* f0 = fm + jj * XW;
+#pragma unroll 2
+    for (int i = 0; i < XW; ++i) {
+        const double xv = xw[i];
+        acc[0] = fma(f0[i], xv, acc[0]);
+        acc[1] = fma(f0[XW + i], xv, acc[1]);
+    }
+    out[t] = acc[0];
+    if (t + 1 < n) out[t + 1] = acc[1];
+}
+
 template <int O, int L>
 __global__ __launch_bounds__(256) void fb_lti_reduce_short_kernel(const double* __restrict__ partial, long n_pad,
                                                                   int G, long n, const double* __restrict__ x,
@@ -897,12 +1014,16 @@ typedef void (*LtiReduceKernel)(const double*, long, int, long, const double*, c
 struct LtiGeom {
     int L, nb, waves;
 };
-static const LtiGeom kLtiGeoms[] = {{16, 1, 16}, {32, 1, 16}, {64, 1, 16}};  // waves: lti_waves(O)
-constexpr int kNumLtiGeoms = 3;
+static const LtiGeom kLtiGeoms[] = {{16, 1, 16}, {32, 1, 16}, {64, 1, 16}, {128, 1, 16}};  // waves: lti_waves(O)
+constexpr int kNumLtiGeoms = 4;
+static_assert(kNumLtiGeoms <= hz_fb::kLtiSets, "one record set per geometry");
 
 template <int O, int L>
 LtiKernel lti_kernel_mode(int mode) {
     static_assert(lti_lds_bytes<O, L>(true) <= 160 * 1024, "LTI kernel LDS over 160 KiB");
+    if constexpr (lti_x1<L>()) {   // chunk 128: state and prepass modes only
+        return mode == MODE_SEGEND ? fb_lti_kernel<O, L, MODE_SEGEND> : fb_lti_kernel<O, L, MODE_STATE>;
+    } else {
     if constexpr (O == 2 && L == 64) {   // diagnostics: ablated state kernels (HZ_FB_LTI_ABL=1..3)
         static const int abl = std::getenv("HZ_FB_LTI_ABL") ? std::atoi(std::getenv("HZ_FB_LTI_ABL")) : 0;
         if (mode == MODE_STATE && abl == 1) return fb_lti_kernel<O, L, MODE_STATE, 1>;
@@ -917,12 +1038,16 @@ LtiKernel lti_kernel_mode(int mode) {
     return mode == MODE_SEGEND ? fb_lti_kernel<O, L, MODE_SEGEND>
          : mode == MODE_STATE  ? fb_lti_kernel<O, L, MODE_STATE>
                                : fb_lti_kernel<O, L, MODE_MIX>;
+    }
 }
 
 template <int O>
 LtiKernel lti_kernel_geom(int geom, int mode) {
     const int L = kLtiGeoms[geom].L;
-    return L == 64 ? lti_kernel_mode<O, 64>(mode) : L == 32 ? lti_kernel_mode<O, 32>(mode) : lti_kernel_mode<O, 16>(mode);
+    return L == 128 ? lti_kernel_mode<O, 128>(mode)
+         : L == 64  ? lti_kernel_mode<O, 64>(mode)
+         : L == 32  ? lti_kernel_mode<O, 32>(mode)
+                    : lti_kernel_mode<O, 16>(mode);
 }
 
 static LtiKernel pick_lti(int O, int geom, int mode) {
@@ -945,19 +1070,28 @@ static size_t lti_lds(int O, int geom, bool mix) {
     }
     if (L == 16) HZ_LTI_LDS(16)
     if (L == 32) HZ_LTI_LDS(32)
+    if (L == 128) HZ_LTI_LDS(128)
     HZ_LTI_LDS(64)
 #undef HZ_LTI_LDS
 }
 
+#define HZ_LTI_O(TEMPLATE, O, LL) \
+    (O == 1 ? TEMPLATE<1, LL> : O == 2 ? TEMPLATE<2, LL> : O == 3 ? TEMPLATE<3, LL> : TEMPLATE<4, LL>)
 #define HZ_LTI_OL(TEMPLATE, O, L)                                                                    \
-    (L == 16 ? (O == 1 ? TEMPLATE<1, 16> : O == 2 ? TEMPLATE<2, 16> : O == 3 ? TEMPLATE<3, 16> : TEMPLATE<4, 16>) \
-     : L == 32 ? (O == 1 ? TEMPLATE<1, 32> : O == 2 ? TEMPLATE<2, 32> : O == 3 ? TEMPLATE<3, 32> : TEMPLATE<4, 32>) \
-               : (O == 1 ? TEMPLATE<1, 64> : O == 2 ? TEMPLATE<2, 64> : O == 3 ? TEMPLATE<3, 64> : TEMPLATE<4, 64>))
-static CarryKernel pick_lti_carry(int O, int L) { return HZ_LTI_OL(fb_lti_seg_carry_kernel, O, L); }
-static FmixKernel pick_fmix(int O, int L) { return HZ_LTI_OL(fb_fmix_kernel, O, L); }
-static LtiReduceKernel pick_lti_reduce(int O, int L) { return HZ_LTI_OL(fb_lti_reduce_kernel, O, L); }
+    (L == 16 ? HZ_LTI_O(TEMPLATE, O, 16) : L == 32 ? HZ_LTI_O(TEMPLATE, O, 32) : HZ_LTI_O(TEMPLATE, O, 64))
+static CarryKernel pick_lti_carry(int O, int L) {
+    return L == 128 ? HZ_LTI_O(fb_lti_seg_carry_kernel, O, 128) : HZ_LTI_OL(fb_lti_seg_carry_kernel, O, L);
+}
+static FmixKernel pick_fmix(int O, int L) {
+    return L == 128 ? HZ_LTI_O(fb_fmix_kernel, O, 128) : HZ_LTI_OL(fb_fmix_kernel, O, L);
+}
+// chunk 128: the quarter-Fmix reduce (grid (chunk groups, L / 32)); the others: one block per 256 samples
+static LtiReduceKernel pick_lti_reduce(int O, int L) {
+    return L == 128 ? HZ_LTI_O(fb_lti_reduce_wide_kernel, O, 128) : HZ_LTI_OL(fb_lti_reduce_kernel, O, L);
+}
 static LtiReduceKernel pick_lti_reduce_short(int O, int L) { return HZ_LTI_OL(fb_lti_reduce_short_kernel, O, L); }
 #undef HZ_LTI_OL
+#undef HZ_LTI_O
 
 }  // namespace
 
@@ -972,9 +1106,13 @@ int fb_lti_geom(const hz_fb* h, long n) {
     static const int env_geom = [] {   // tuning experiments: HZ_FB_LTI_L = 16 / 32 / 64 for long calls
         const char* e = std::getenv("HZ_FB_LTI_L");
         const int v = e ? std::atoi(e) : 0;
-        return v == 16 ? 0 : v == 64 ? 2 : v == 32 ? 1 : -1;
+        return v == 16 ? 0 : v == 64 ? 2 : v == 32 ? 1 : v == 128 ? 3 : -1;
     }();
-    if (n >= 2 * 64L * 32 && env_geom >= 0) return env_geom;
+    if (env_geom >= 0 && n >= 2 * 64L * kLtiGeoms[env_geom].L) return env_geom;
+    // chunk 128 from four of its 8192-sample tiles, for banks that fill the chip without time
+    // segments (C2: 256 groups); shard-sized banks keep chunk 64 (finer tiles for the prepass)
+    const int W = lti_waves(h->order);
+    if (n >= 4 * 64L * 128 && h->order > 0 && (h->N + W - 1) / W >= h->target_groups) return 3;
     if (n >= 2 * 64L * 64) return 2;   // chunk 64 for calls of at least two of its 4096-sample tiles
     if (n >= 2 * 64L * 32) return 1;
     return 0;
@@ -990,7 +1128,7 @@ bool fb_lti_gemm_geom(int geom) {
         const char* e = std::getenv("HZ_FB_LTI_GEMM");
         return e && e[0] == '0';
     }();
-    return kLtiGeoms[geom].L == 64 && !off;
+    return kLtiGeoms[geom].L >= 64 && !off;
 }
 
 // every band's smoothers at their targets (host mirror), relative to the bank's
@@ -1252,8 +1390,6 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         const long nc_pad = ntiles * 64;   // chunks of the launch (GEMM path)
         LtiArgs a;
         a.dbg = nullptr;
-        static const int scan_first = std::getenv("HZ_FB_LTI_ORDER") ? std::atoi(std::getenv("HZ_FB_LTI_ORDER")) : 0;
-        a.scan_first = scan_first;
         a.pin = h->d_pin;
         a.gin = h->d_gin;
         a.ystate = h->d_ystate[h->scur];
@@ -1312,6 +1448,11 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             HZ_TRY_HIP(hipMemsetAsync(d_dbg, 0, sizeof(long long) * 16 * 64 * 4, h->stream));
             a.dbg = d_dbg;
         }
+        if (gemm && bs_pad > lti_group_rows(h->N, O)) {   // GS rows no group writes: zero
+            const int gr = lti_group_rows(h->N, O);
+            HZ_TRY_HIP(hipMemset2DAsync(h->d_partial + (size_t)gr * 64, sizeof(double) * bs_pad * 64, 0,
+                                        sizeof(double) * (bs_pad - gr) * 64, (size_t)ntiles, h->stream));
+        }
         hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * lti_waves(O)), lds, h->stream,
                            (const double*)set.d_rec, a);
         HZ_TRY_HIP(hipGetLastError());
@@ -1345,9 +1486,11 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             double* part = h->d_partial + (size_t)bs_pad * nc_pad;
             if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
             int S = 1;
-            HZ_TRY(fb_lti_gemm_launch(h->d_partial, set.d_kt, bs_pad, part, a.n_pad, (int)ntiles, h->target_groups,
+            HZ_TRY(fb_lti_gemm_launch(h->d_partial, set.d_kt, bs_pad, part, a.n_pad, (int)ntiles, L, h->target_groups,
                                       kMaxSlices, h->stream, &S));
-            hipLaunchKernelGGL(pick_lti_reduce(O, L), dim3((unsigned)((len + 255) / 256)), dim3(128), 0, h->stream,
+            const dim3 rgrid = L == 128 ? dim3((unsigned)((len + kWideChunks * L - 1) / (kWideChunks * L)), L / kWideRows)
+                                        : dim3((unsigned)((len + 255) / 256));
+            hipLaunchKernelGGL(pick_lti_reduce(O, L), rgrid, dim3(128), 0, h->stream,
                                (const double*)part, a.n_pad, S, len, a.x, off == 0 ? xhist_call : nullptr,
                                (const double*)set.d_fmix, d_out + off);
             HZ_TRY_HIP(hipGetLastError());
@@ -1415,7 +1558,8 @@ int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group)
             h->lti_geom = g;
             return HZ_OK;
         }
-    hz::set_error("hz_fb_tune_lti: (chunk, bands/wave, waves) must be one of (16,1,16), (32,1,16), (64,1,16)");
+    hz::set_error("hz_fb_tune_lti: (chunk, bands/wave, waves) must be one of (16,1,16), (32,1,16), (64,1,16), "
+                  "(128,1,16)");
     return HZ_E_INVALID;
 }
 

@@ -963,10 +963,11 @@ int hz_fb_destroy(hz_fb* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (double* p : {h->d_rec, h->d_pin, h->d_gin, h->d_ystate[0], h->d_ystate[1], h->d_pg[0], h->d_pg[1],
                       h->d_xhist[0], h->d_xhist[1],
-                      h->d_partial, h->d_seg, h->d_in, h->d_out, h->lti_set[0].d_rec, h->lti_set[0].d_fmix,
-                      h->lti_set[1].d_rec, h->lti_set[1].d_fmix, h->lti_set[2].d_rec, h->lti_set[2].d_fmix,
-                      h->lti_set[0].d_kt, h->lti_set[1].d_kt, h->lti_set[2].d_kt})
+                      h->d_partial, h->d_seg, h->d_in, h->d_out})
         if (p) (void)hipFree(p);
+    for (auto& st : h->lti_set)
+        for (double* p : {st.d_rec, st.d_fmix, st.d_kt})
+            if (p) (void)hipFree(p);
     if (h->stream_red) (void)hipStreamSynchronize(h->stream_red);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->sync_ev) (void)hipEventDestroy(e);

@@ -174,14 +174,14 @@ class Filterbank:
 
     def tune_lti(self, chunk: int = 0, bands_per_wave: int = 0, waves: int = 0):
         check(self._lib.hz_fb_tune_lti(self._h, chunk, bands_per_wave, waves))
-        self._lti_geom = {16: 0, 32: 1, 64: 2}.get(chunk, 1)
+        self._lti_geom = {16: 0, 32: 1, 64: 2, 128: 3}.get(chunk, 1)
 
     def lti_chunk(self) -> int:
         """Samples per lane chunk of the last LTI launch (hz_fb_lti_last_chunk; the geometry
         is picked by call length unless pinned with tune_lti)."""
         c = C.c_int()
         check(self._lib.hz_fb_lti_last_chunk(self._h, C.byref(c)))
-        return c.value or {0: 16, 1: 32, 2: 64}.get(self._lti_geom, 32)
+        return c.value or {0: 16, 1: 32, 2: 64, 3: 128}.get(self._lti_geom, 32)
 
     def lti_plan(self):
         """-> (time segments, prepass tiles skipped per segment, fine prepass parts) of the

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 TOL = 1e-9
 TOL_STIFF = 1e-7  # Nyquist double pole (see test_filterbank_gpu.py)
-LTI_GEOMS = [(16, 1, 16), (32, 1, 16), (64, 1, 16)]
+LTI_GEOMS = [(16, 1, 16), (32, 1, 16), (64, 1, 16), (128, 1, 16)]
 
 
 def make_pair(order, N, fwd, back, kp=0.001, kg=0.001, boost=None, gains=None):
@@ -78,6 +78,36 @@ def test_c2_recipe_lti(gpu_lib, geom, R, centre):
     g.tune_lti(*geom)
     run_calls(g, o, [700, 4096, 3 * 1024 + 512, 5003, 1024], seed=11,
               tol=TOL_STIFF if centre == 1.0 else TOL)
+
+
+@pytest.mark.parametrize("N,order,groups", [(4096, 2, 256), (203, 2, 256), (300, 1, 16), (100, 3, 8), (77, 4, 64)])
+def test_chunk128_long_calls(gpu_lib, N, order, groups):
+    """Chunk 128 (8192-sample tiles, one x buffer, E operands in LDS, GEMM over 128-sample
+    chunks, quarter-Fmix reduce): multi-tile and ragged calls, with time segments and the
+    prepass for the small banks."""
+    if order == 2:
+        fwd, back = resonant_coefficients(N, 0.999, 0.5)
+        g, o = make_pair(2, N, fwd, back)
+    else:
+        fwd, back = random_bank(order, N, seed=300 + order)
+        rng = np.random.default_rng(order)
+        g, o = make_pair(order, N, fwd, back, boost=rng.uniform(0.2, 2.0, N), gains=rng.uniform(-1, 1, N))
+    g.tune_lti(128, 1, 16)
+    g.set_target_groups(groups)
+    run_calls(g, o, [700, 8192 * 3 + 128 * 5, 40000, 1024, 65536 + 300], seed=40 + order)
+    assert g.lti_chunk() == 128
+
+
+def test_chunk128_picked_for_c2(gpu_lib):
+    """By call length: chunk 128 for a full-chip bank's long calls, chunk 64 for shard-sized
+    banks (time segments), chunk 16 for streaming blocks."""
+    from huygens_amd import Filterbank
+    for N, n, want in ((4096, 480_000, 128), (512, 480_000, 64), (4096, 1024, 16)):
+        fwd, back = resonant_coefficients(N, 0.999, 0.5)
+        g, _ = make_pair(2, N, fwd, back, kp=0.0, kg=0.0)
+        g.process(white_noise_f32(1024, seed=1))
+        g.process(white_noise_f32(n, seed=2))
+        assert g.lti_chunk() == want, (N, n, g.lti_chunk())
 
 
 @pytest.mark.parametrize("order", [1, 2, 3, 4])
