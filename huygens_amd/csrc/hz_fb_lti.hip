@@ -217,6 +217,9 @@ __host__ __device__ constexpr int lti_bsp(int O) { return (lti_waves(O) * O + 15
 // GEMM stages), the rows past the groups' zeroed per call (fb_launch_lti)
 static inline int lti_group_rows(int N, int O) { return (N + lti_waves(O) - 1) / lti_waves(O) * lti_waves(O) * O; }
 static inline int lti_bs_rows(int N, int O) { return (lti_group_rows(N, O) + 31) / 32 * 32; }
+// GEMM path: the bank-wide zero-state term joins the correction GEMM as XW = L + O extra K rows
+// (rounded to 32): GS rows = the chunk's input window x[tc - O + r], K rows = Fmix[j][r]
+static inline int lti_x_rows(int L, int O) { return (L + O + 31) / 32 * 32; }
 constexpr int kZRow = 65;   // z rows [BSP][64 chunks + 1]: E-block writes hit 16 banks apart
 constexpr int kGsRow = 80;  // gs rows [BSP][64 chunks + 16]: mix A-operand reads on disjoint bank halves
 // chunk 64: the mix B operands (K rows) live in LDS instead of registers (the chunk's 17-step E
@@ -916,50 +919,56 @@ __global__ __launch_bounds__(128) void fb_lti_reduce_kernel(const double* __rest
 // handful of workgroups, each walking all G slab rows.  Here a workgroup takes 32 samples
 // and splits the G rows over 16 slices (16 x 16 threads), summing the slices in a fixed
 // order through LDS (deterministic; a different order than the long-call kernel).
-// Chunk 128: the slice sum + zero-state term with a quarter of Fmix per workgroup (the whole
-// 128 x 130 matrix would not fit LDS): workgroup (chunk group cg, row block q) covers rows
-// j in [32 q, 32 q + 32) of 8 consecutive chunks, two samples per thread.
-constexpr int kWideRows = 32, kWideChunks = 8;
+// GEMM path, per launch: GS rows bs_pad + r (r < XR) of every tile hold the chunk input windows
+// x[tc - O + r] (r < L + O; 0 above), so the GEMM's K dimension carries the zero-state term.
+template <int L>
+__global__ __launch_bounds__(256) void fb_lti_xrows_kernel(const double* __restrict__ x,
+                                                           const double* __restrict__ xhist, int O, long n,
+                                                           double* __restrict__ gs, int bs_pad, int bs_tot, int XR,
+                                                           int ntiles) {
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;   // (tile, r, chunk)
+    if (e >= (long)ntiles * XR * 64) return;
+    const int c = (int)(e & 63);
+    const long tr = e >> 6;
+    const int r = (int)(tr % XR);
+    const long tile = tr / XR;
+    double v = 0.0;
+    if (r < L + O) {
+        const long idx = (tile * 64 + c) * L - O + r;
+        v = idx >= n ? 0.0 : (idx >= 0 || !xhist) ? x[idx] : xhist[-idx - 1];
+    }
+    gs[(tile * bs_tot + bs_pad + r) * 64 + c] = v;
+}
+// ... and K rows bs_pad + r = Fmix[j][r] (0 for r >= L + O), written when Fmix changes
 template <int O, int L>
-__global__ __launch_bounds__(128) void fb_lti_reduce_wide_kernel(const double* __restrict__ partial, long n_pad,
-                                                                 int G, long n, const double* __restrict__ x,
-                                                                 const double* __restrict__ xhist,
-                                                                 const double* __restrict__ fmix,
-                                                                 double* __restrict__ out) {
-    constexpr int XW = L + O;
-    constexpr int NX = kWideChunks * L + O;
-    __shared__ double fm[kWideRows * XW];
-    __shared__ double xs[NX];
-    const int j0 = blockIdx.y * kWideRows;
-    const long c0 = (long)blockIdx.x * kWideChunks;
-    const long tb = c0 * L;   // first sample of the chunk group
-    for (int e = threadIdx.x; e < kWideRows * XW; e += 128) fm[e] = fmix[(long)j0 * XW + e];
-    for (int e = threadIdx.x; e < NX; e += 128) {
-        const long idx = tb - O + e;
-        xs[e] = idx >= n ? 0.0 : (idx >= 0 || !xhist) ? x[idx] : xhist[-idx - 1];
-    }
-    __syncthreads();
-    const int cc = threadIdx.x >> 4, jj = 2 * (threadIdx.x & 15);
-    const long t = tb + (long)cc * L + j0 + jj;
-    if (t >= n) return;
+__global__ __launch_bounds__(256) void fb_lti_kt_fmix_kernel(const double* __restrict__ fmix, double* __restrict__ kt,
+                                                             int bs_pad, int XR) {
+    const int e = blockIdx.x * 256 + threadIdx.x;   // (r, j)
+    if (e >= XR * L) return;
+    const int r = e / L, j = e % L;
+    kt[(long)(bs_pad + r) * L + j] = r < L + O ? fmix[j * (L + O) + r] : 0.0;
+}
+// GEMM path: out[t] = sum over the S slices of part[s][t] (fixed order)
+__global__ __launch_bounds__(256) void fb_lti_sum_kernel(const double* __restrict__ part, long n_pad, int S, long n,
+                                                         double* __restrict__ out) {
     typedef double d2 __attribute__((ext_vector_type(2)));
+    const long t = 2 * ((long)blockIdx.x * 256 + threadIdx.x);
+    if (t >= n) return;
+    const double* col = part + t;
     d2 s0 = {0.0, 0.0}, s1 = {0.0, 0.0};
-    const double* col = partial + t;
     int g = 0;
-    for (; g + 2 <= G; g += 2) {
-        s0 += __builtin_nontemporal_load((const d2*)(col + (long)g * n_pad));
-        s1 += __builtin_nontemporal_load((const d2*)(col + (long)(g + 1) * n_pad));
+    for (; g + 8 <= S; g += 8) {
+        d2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load((const d2*)(col + (long)(g + u) * n_pad));
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            s0 += v[u];
+            s1 += v[u + 1];
+        }
     }
-    for (; g < G; ++g) s0 += __builtin_nontemporal_load((const d2*)(col + (long)g * n_pad));
-    d2 acc = s0 + s1;
-    const double* xw = xs + (long)cc * L;   // x[chunk start - O + i] = xw[i]
-    const double* f0 = fm + jj * XW;
-#pragma unroll 2
-    for (int i = 0; i < XW; ++i) {
-        const double xv = xw[i];
-        acc[0] = fma(f0[i], xv, acc[0]);
-        acc[1] = fma(f0[XW + i], xv, acc[1]);
-    }
+    for (; g < S; ++g) s0 += __builtin_nontemporal_load((const d2*)(col + (long)g * n_pad));
+    const d2 acc = s0 + s1;
     out[t] = acc[0];
     if (t + 1 < n) out[t + 1] = acc[1];
 }
@@ -1022,6 +1031,13 @@ template <int O, int L>
 LtiKernel lti_kernel_mode(int mode) {
     static_assert(lti_lds_bytes<O, L>(true) <= 160 * 1024, "LTI kernel LDS over 160 KiB");
     if constexpr (lti_x1<L>()) {   // chunk 128: state and prepass modes only
+        if constexpr (O == 2) {   // diagnostics (HZ_FB_LTI_ABL: 1 no E, 2 no scan, 3 neither, 16 stamps)
+            static const int abl = std::getenv("HZ_FB_LTI_ABL") ? std::atoi(std::getenv("HZ_FB_LTI_ABL")) : 0;
+            if (mode == MODE_STATE && abl == 1) return fb_lti_kernel<O, L, MODE_STATE, 1>;
+            if (mode == MODE_STATE && abl == 2) return fb_lti_kernel<O, L, MODE_STATE, 2>;
+            if (mode == MODE_STATE && abl == 3) return fb_lti_kernel<O, L, MODE_STATE, 3>;
+            if (mode == MODE_STATE && abl == 16) return fb_lti_kernel<O, L, MODE_STATE, 16>;
+        }
         return mode == MODE_SEGEND ? fb_lti_kernel<O, L, MODE_SEGEND> : fb_lti_kernel<O, L, MODE_STATE>;
     } else {
     if constexpr (O == 2 && L == 64) {   // diagnostics: ablated state kernels (HZ_FB_LTI_ABL=1..3)
@@ -1085,11 +1101,15 @@ static CarryKernel pick_lti_carry(int O, int L) {
 static FmixKernel pick_fmix(int O, int L) {
     return L == 128 ? HZ_LTI_O(fb_fmix_kernel, O, 128) : HZ_LTI_OL(fb_fmix_kernel, O, L);
 }
-// chunk 128: the quarter-Fmix reduce (grid (chunk groups, L / 32)); the others: one block per 256 samples
-static LtiReduceKernel pick_lti_reduce(int O, int L) {
-    return L == 128 ? HZ_LTI_O(fb_lti_reduce_wide_kernel, O, 128) : HZ_LTI_OL(fb_lti_reduce_kernel, O, L);
-}
+// (chunk 64 / 128 calls sum the GEMM slices with fb_lti_sum_kernel: the zero-state term is in the GEMM)
+static LtiReduceKernel pick_lti_reduce(int O, int L) { return HZ_LTI_OL(fb_lti_reduce_kernel, O, L); }
 static LtiReduceKernel pick_lti_reduce_short(int O, int L) { return HZ_LTI_OL(fb_lti_reduce_short_kernel, O, L); }
+typedef void (*KtFmixKernel)(const double*, double*, int, int);
+static KtFmixKernel pick_kt_fmix(int O, int L) {
+    return L == 128 ? HZ_LTI_O(fb_lti_kt_fmix_kernel, O, 128) : HZ_LTI_O(fb_lti_kt_fmix_kernel, O, 64);
+}
+typedef void (*XrowsKernel)(const double*, const double*, int, long, double*, int, int, int, int);
+static XrowsKernel pick_xrows(int L) { return L == 128 ? fb_lti_xrows_kernel<128> : fb_lti_xrows_kernel<64>; }
 #undef HZ_LTI_OL
 #undef HZ_LTI_O
 
@@ -1218,18 +1238,19 @@ int fb_prepare_lti(hz_fb* h, int gi) {
         if (!set.d_fmix) HZ_TRY_HIP(hipMalloc(&set.d_fmix, sizeof(double) * L * (L + kMaxOrder)));
         HZ_TRY_HIP(hipMemcpyAsync(set.d_rec, host.data(), sizeof(double) * need, hipMemcpyHostToDevice, h->stream));
         HZ_TRY_HIP(hipStreamSynchronize(h->stream));  // pageable source
-        if (fb_lti_gemm_geom(gi) && O > 0) {   // K rows of every band state, zero-padded to 4
+        if (fb_lti_gemm_geom(gi) && O > 0) {   // K rows of every band state (+ the Fmix rows, below)
             const int bs_pad = lti_bs_rows(h->N, O), ko = lti_k_offset(O, L);
+            const size_t rows = (size_t)bs_pad + lti_x_rows(L, O);
             std::vector<double> kt((size_t)bs_pad * L, 0.0);
             for (int b = 0; b < h->N; ++b)
                 for (int k = 0; k < O; ++k)
                     for (int j = 0; j < L; ++j)
                         kt[((size_t)b * O + k) * L + j] = host[(size_t)b * rs + ko + j * O + k];
-            if (kt.size() > set.kt_cap) {
+            if (rows * L > set.kt_cap) {
                 if (set.d_kt) HZ_TRY_HIP(hipFree(set.d_kt));
                 set.d_kt = nullptr;
-                HZ_TRY_HIP(hipMalloc(&set.d_kt, sizeof(double) * kt.size()));
-                set.kt_cap = kt.size();
+                HZ_TRY_HIP(hipMalloc(&set.d_kt, sizeof(double) * rows * L));
+                set.kt_cap = rows * L;
             }
             HZ_TRY_HIP(hipMemcpyAsync(set.d_kt, kt.data(), sizeof(double) * kt.size(), hipMemcpyHostToDevice,
                                       h->stream));
@@ -1245,6 +1266,12 @@ int fb_prepare_lti(hz_fb* h, int gi) {
                            (const double*)set.d_rec, (const double*)h->d_pin, (const double*)h->d_gin, h->N,
                            set.d_fmix);
         HZ_TRY_HIP(hipGetLastError());
+        if (fb_lti_gemm_geom(gi) && O > 0) {   // the GEMM's zero-state K rows
+            const int XR = lti_x_rows(L, O);
+            hipLaunchKernelGGL(pick_kt_fmix(O, L), dim3((unsigned)((XR * L + 255) / 256)), dim3(256), 0, h->stream,
+                               (const double*)set.d_fmix, set.d_kt, lti_bs_rows(h->N, O), XR);
+            HZ_TRY_HIP(hipGetLastError());
+        }
         set.fmix_valid = true;
     }
     return HZ_OK;
@@ -1281,15 +1308,17 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
     // correction GEMM path: per chunk GS [bs_pad][chunks] + part [S][n_pad] instead of two slabs
     const bool gemm = fb_lti_gemm_geom(gi) && O > 0;
     const int bs_pad = lti_bs_rows(h->N, O);
+    const int XR = gemm ? lti_x_rows(L, O) : 0;
+    const int bs_tot = bs_pad + XR;   // GS rows per tile: band states, then the x-window rows
     long chunk = std::max<long>(T, (((1L << slab_log2) / std::max(1, G)) / T) * T);
-    if (gemm) chunk = std::max<long>(T, (((1L << slab_log2) / bs_pad * L) / T) * T);
+    if (gemm) chunk = std::max<long>(T, (((1L << slab_log2) / bs_tot * L) / T) * T);
     if (!gemm && ntiles_all >= 8 * nsplit) chunk = std::min(chunk, ((ntiles_all + nsplit - 1) / nsplit) * T);
     // (row skews of 32..2050 doubles were measured: no effect on the reduce, which moves the
     // slab plus the mix kernel's dirty write-back at about 5.4 TB/s)
     const long n_pad_max = std::min<long>(ntiles_all * T, chunk);
     const size_t slab = (size_t)G * n_pad_max;
     constexpr int kMaxSlices = 32;   // GEMM band-state slices (rows of part)
-    const size_t need = gemm ? (size_t)bs_pad * (n_pad_max / L) + (size_t)kMaxSlices * n_pad_max : 2 * slab;
+    const size_t need = gemm ? (size_t)bs_tot * (n_pad_max / L) + (size_t)kMaxSlices * n_pad_max : 2 * slab;
     if (need > h->partial_cap) {
         if (h->d_partial) HZ_TRY_HIP(hipFree(h->d_partial));
         h->d_partial = nullptr;
@@ -1401,7 +1430,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         a.xhist_next = h->d_xhist[h->xcur ^ 1];
         a.partial = slab_k;
         a.gs_out = h->d_partial;
-        a.bs_pad = bs_pad;
+        a.bs_pad = bs_tot;
         a.segstate = h->d_seg;
         a.n = len;
         a.n_pad = ntiles * T;
@@ -1450,8 +1479,15 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         }
         if (gemm && bs_pad > lti_group_rows(h->N, O)) {   // GS rows no group writes: zero
             const int gr = lti_group_rows(h->N, O);
-            HZ_TRY_HIP(hipMemset2DAsync(h->d_partial + (size_t)gr * 64, sizeof(double) * bs_pad * 64, 0,
+            HZ_TRY_HIP(hipMemset2DAsync(h->d_partial + (size_t)gr * 64, sizeof(double) * bs_tot * 64, 0,
                                         sizeof(double) * (bs_pad - gr) * 64, (size_t)ntiles, h->stream));
+        }
+        if (gemm) {   // the x-window rows (zero-state term) of every tile
+            const long cnt = ntiles * XR * 64L;
+            hipLaunchKernelGGL(pick_xrows(L), dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, h->stream,
+                               a.x, off == 0 ? xhist_call : nullptr, O, len, h->d_partial, bs_pad, bs_tot, XR,
+                               (int)ntiles);
+            HZ_TRY_HIP(hipGetLastError());
         }
         hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * lti_waves(O)), lds, h->stream,
                            (const double*)set.d_rec, a);
@@ -1483,16 +1519,13 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         if (gemm) {
             // correction GEMM over band-state slices (>= 4 workgroups per CU), then the slice sum
             // + zero-state term in the reduce kernel; one stream, chunks in sequence
-            double* part = h->d_partial + (size_t)bs_pad * nc_pad;
+            double* part = h->d_partial + (size_t)bs_tot * nc_pad;
             if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
             int S = 1;
-            HZ_TRY(fb_lti_gemm_launch(h->d_partial, set.d_kt, bs_pad, part, a.n_pad, (int)ntiles, L, h->target_groups,
+            HZ_TRY(fb_lti_gemm_launch(h->d_partial, set.d_kt, bs_tot, part, a.n_pad, (int)ntiles, L, h->target_groups,
                                       kMaxSlices, h->stream, &S));
-            const dim3 rgrid = L == 128 ? dim3((unsigned)((len + kWideChunks * L - 1) / (kWideChunks * L)), L / kWideRows)
-                                        : dim3((unsigned)((len + 255) / 256));
-            hipLaunchKernelGGL(pick_lti_reduce(O, L), rgrid, dim3(128), 0, h->stream,
-                               (const double*)part, a.n_pad, S, len, a.x, off == 0 ? xhist_call : nullptr,
-                               (const double*)set.d_fmix, d_out + off);
+            hipLaunchKernelGGL(fb_lti_sum_kernel, dim3((unsigned)((len + 511) / 512)), dim3(256), 0, h->stream,
+                               (const double*)part, a.n_pad, S, len, d_out + off);
             HZ_TRY_HIP(hipGetLastError());
             if (e) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
             h->xcur ^= 1;

@@ -7,5 +7,5 @@ OUT=gpurun_out/abl; mkdir -p $OUT
 for v in ${ABLS:-0 1 2 3}; do
   HZ_FB_LTI_ABL=$v timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/p$v -o trace --output-format csv -- \
      python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-traffic --stream-blocks 0 > $OUT/log$v 2>&1 || exit $?
-  echo "ABL=$v"; grep -h "fb_lti_kernel<2, 64, 2" $OUT/p$v/*kernel_stats.csv | cut -d, -f1,3,4 | sed "s/.*fb_lti_kernel/fb_lti_kernel/" | cut -c1-120
+  echo "ABL=$v"; grep -h "fb_lti_kernel<2, 1*[26][48]*, 2" $OUT/p$v/*kernel_stats.csv | cut -d, -f1,3,4 | sed "s/.*fb_lti_kernel/fb_lti_kernel/" | cut -c1-120
 done

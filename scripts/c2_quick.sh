@@ -19,6 +19,6 @@ import csv, glob
 for f in glob.glob("$OUT/prof/*kernel_stats.csv"):
     for r in csv.DictReader(open(f)):
         n = r["Name"]
-        if "fb_lti" in n:
+        if "fb_lti" in n or "sum_kernel" in n or "xrows" in n:
             print("  %-40s %6s calls %8.1f us" % (n[n.find("fb_"):n.find("(", n.find("fb_"))], r["Calls"], float(r["AverageNs"]) / 1e3))
 PY
