@@ -199,13 +199,17 @@ struct LtiArgs {
     long long* dbg;         // diagnostics (ABL bit 4): per-wave phase timestamps of one workgroup
 };
 
-// LDS: x tile x[t0-O .. t0+64L-1] stored at pos(li) = li + li / L (one pad slot per
-// chunk) so lane c's window reads start on distinct banks; double-buffered.
+// LDS: x tile x[t0-O .. t0+64L-1] stored at pos(li) = li + P (li / L), P pad slots per chunk
+// (lane c's window reads start on distinct banks); double-buffered.  Chunk 128 (one buffer,
+// filled by LDS-DMA 1-KiB pieces, one per chunk): P = 2 keeps every chunk 16-B aligned.
+template <int L>
+__host__ __device__ constexpr int lti_xs_padc() { return L >= 128 ? 2 : 1; }
 template <int O, int L>
 __host__ __device__ constexpr int lti_xs_len() { return 64 * L + O; }
 template <int O, int L>
 __host__ __device__ constexpr int lti_xs_pad() {
-    return ((lti_xs_len<O, L>() + lti_xs_len<O, L>() / L + 1) + 1) & ~1;
+    return L >= 128 ? 65 * (L + 2)   // 64 chunks + the O-sample tail piece, whole DMA pieces
+                    : ((lti_xs_len<O, L>() + lti_xs_len<O, L>() / L + 1) + 1) & ~1;
 }
 // Workgroup geometry: one band per wave; 16 waves (bands) per workgroup for O <= 2,
 // 8 for O >= 3 (LDS).  BS = band states of a group, padded to the 16-wide MFMA blocks.
@@ -467,16 +471,17 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
             pf[q] = __builtin_bit_cast(
                 double, __builtin_amdgcn_raw_buffer_load_b64(rs, vq0 + q * 64 * WS * (int)sizeof(double), 0, 0));
     };
-    // LDS position of x[t0x - O + li] is li + li / L; li = tid + q 64 W with 64 W a multiple of L,
-    // so position = (tid + tid / L) + q (64 W + 64 W / L): one base, immediate offsets per q
-    const int xpos0 = (int)threadIdx.x + (int)threadIdx.x / L;
-    const int xposs = sid + sid / L;
+    // LDS position of x[t0x - O + li] is li + P (li / L); li = tid + q 64 W with 64 W a multiple
+    // of L, so position = (tid + P tid / L) + q (64 W + P 64 W / L): one base, immediate offsets
+    constexpr int PC = lti_xs_padc<L>();
+    const int xpos0 = (int)threadIdx.x + PC * ((int)threadIdx.x / L);
+    const int xposs = sid + PC * (sid / L);
     auto store_x_loop = [&](double* xbuf, const double (&pf)[PF2]) {   // in-loop tiles (t0x > 0)
         double* xb = xbuf + xposs;
 #pragma unroll
         for (int q = 0; q < PF2; ++q) {
             const int li = sid + q * 64 * WS;
-            if (li < XS) xb[q * (64 * WS + 64 * WS / L)] = pf[q];
+            if (li < XS) xb[q * (64 * WS + PC * (64 * WS / L))] = pf[q];
         }
     };
     auto store_x = [&](double* xbuf, const double (&pf)[PF], long t0x) {
@@ -485,9 +490,28 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
             const int li = threadIdx.x + q * 64 * W;
-            if (li < XS) xb[q * (64 * W + 64 * W / L)] = pf[q];
+            if (li < XS) xb[q * (64 * W + PC * (64 * W / L))] = pf[q];
         }
         if (t0x == 0 && threadIdx.x < O) xbuf[threadIdx.x] = a.xhist[O - 1 - threadIdx.x];  // x[-O+li]
+    };
+    // chunk 128, in-loop tiles (t0x > 0): the staging waves fill the x buffer by LDS-DMA, one
+    // 1-KiB piece (128 doubles = one chunk, 16 B per lane) per instruction, no registers and no
+    // ds_write; the range check returns 0 past seg_end; __syncthreads() waits for the pieces
+    auto dma_x = [&](double* xbuf, long t0x) {
+        if constexpr (X1) {
+            const unsigned long long xb = (unsigned long long)(a.x + (t0x - O));
+            const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)xb);
+            const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(xb >> 32));
+            const long rem = (seg_end - (t0x - O)) * (long)sizeof(double);
+            const int bytes = __builtin_amdgcn_readfirstlane((int)(rem > 0 ? rem : 0));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(((unsigned long long)hi << 32) | lo), (short)0, bytes, 0x00020000);
+            const int sw = kSplit ? wave - NE : wave;   // staging wave index
+            for (int c = sw; c <= 64; c += WS)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(xbuf + c * (L + 2)), 16,
+                    (c * L + 2 * lane) * (int)sizeof(double), 0, 0, 0);
+        }
     };
 
     // (E) for tile te: this wave's E blocks -> z buffer (te & 1)
@@ -507,7 +531,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                 constexpr int EP = 4;
                 auto xa_at = [&](int q) {
                     const int li = li0 + 4 * q;
-                    return (4 * q + (lane >> 4) < XW) ? xs[li + li / L] : 0.0;
+                    return (4 * q + (lane >> 4) < XW) ? xs[li + PC * (li / L)] : 0.0;
                 };
                 // X1: B = E[tap 4q + (l >> 4)][bs 16 sb + (l & 15)] from LDS, read with A
                 const double* ebl = eb + (lane >> 4) * EBR + 16 * sb + (lane & 15);
@@ -605,7 +629,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     }
     const bool stager = !kSplit || wave >= NE;
     double pf[PF2];   // staging registers: x tile it + 2, loaded during iteration it - 1 (kSplit, X1)
-    if ((kSplit || X1) && stager && ntiles > 2) load_x_loop(seg_t0 + 2 * T, pf);
+    if (kSplit && !X1 && stager && ntiles > 2) load_x_loop(seg_t0 + 2 * T, pf);
 
     double st[O];
     double* go_run = MODE == MODE_STATE ? a.gs_out + ((seg_t0 / T) * a.bs_pad + (long)band * O) * 64 + lane : nullptr;
@@ -695,11 +719,12 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     if constexpr (X1) {
         // chunk 128, one x buffer, two barriers per tile: the E waves run (E) of tile it + 1 while
         // the others scan tile it; after the first barrier (x buffer free) the E waves scan and the
-        // staging waves store tile it + 2 from registers and load tile it + 3
+        // staging waves start the LDS-DMA of tile it + 2
         const bool isE = !kSplit || wave < NE;
         for (int it = 0; it < ntiles; ++it) {
             const long t0 = seg_t0 + (long)it * T;
             stamp(it, 0);
+            // (every wave scanning first, then the E chains: 0.465 vs 0.454 ms per C2 step)
             if (isE) {
                 if (it + 1 < ntiles) phase_e(it + 1);
             } else {
@@ -709,10 +734,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
             __syncthreads();
             if (isE) phase_s(it, t0);
             stamp(it, 2);
-            if (stager) {
-                if (it + 2 < ntiles) store_x_loop(lds, pf);
-                if (it + 3 < ntiles) load_x_loop(t0 + 3 * T, pf);
-            }
+            if (stager && it + 2 < ntiles) dma_x(lds, t0 + 2 * T);
             stamp(it, 3);
             __syncthreads();
         }
