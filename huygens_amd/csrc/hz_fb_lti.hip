@@ -1151,10 +1151,11 @@ int fb_lti_geom(const hz_fb* h, long n) {
         return v == 16 ? 0 : v == 64 ? 2 : v == 32 ? 1 : v == 128 ? 3 : -1;
     }();
     if (env_geom >= 0 && n >= 2 * 64L * kLtiGeoms[env_geom].L) return env_geom;
-    // chunk 128 from four of its 8192-sample tiles, for banks that fill the chip without time
-    // segments (C2: 256 groups); shard-sized banks keep chunk 64 (finer tiles for the prepass)
+    // chunk 128 from four of its 8192-sample tiles, for banks that fill the chip with at most two
+    // time segments (C2: 256 groups; its 2-GPU shard 0.294 -> 0.279 ms); smaller shards keep
+    // chunk 64 (finer tiles for the prepass and the GEMM: 4-GPU shard equal, 8-GPU 0.141 vs 0.164)
     const int W = lti_waves(h->order);
-    if (n >= 4 * 64L * 128 && h->order > 0 && (h->N + W - 1) / W >= h->target_groups) return 3;
+    if (n >= 4 * 64L * 128 && h->order > 0 && 2L * ((h->N + W - 1) / W) >= h->target_groups) return 3;
     if (n >= 2 * 64L * 64) return 2;   // chunk 64 for calls of at least two of its 4096-sample tiles
     if (n >= 2 * 64L * 32) return 1;
     return 0;

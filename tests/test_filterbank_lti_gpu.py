@@ -99,10 +99,10 @@ def test_chunk128_long_calls(gpu_lib, N, order, groups):
 
 
 def test_chunk128_picked_for_c2(gpu_lib):
-    """By call length: chunk 128 for a full-chip bank's long calls, chunk 64 for shard-sized
-    banks (time segments), chunk 16 for streaming blocks."""
+    """By call length: chunk 128 for long calls of banks with at most two time segments, chunk
+    64 for smaller shards, chunk 16 for streaming blocks."""
     from huygens_amd import Filterbank
-    for N, n, want in ((4096, 480_000, 128), (512, 480_000, 64), (4096, 1024, 16)):
+    for N, n, want in ((4096, 480_000, 128), (2048, 240_000, 128), (512, 480_000, 64), (4096, 1024, 16)):
         fwd, back = resonant_coefficients(N, 0.999, 0.5)
         g, _ = make_pair(2, N, fwd, back, kp=0.0, kg=0.0)
         g.process(white_noise_f32(1024, seed=1))
