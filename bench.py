@@ -85,18 +85,20 @@ def cpu_baseline(fwd, back, seconds_target=1.5):
                       f"({nsamp / SR:.2f} s audio), bands split over {threads} threads, {dt:.2f} s wall"}
 
 
-def fb_executed_flops(lti, L=32, O=2):
+def fb_executed_flops(lti, L=32, O=2, N=N_BANDS):
     """FP64 flops the kernel actually issues per band-sample.  LTI engine:
     chunk end states on the matrix cores 2 O ceil((L+O)/4) 4 / L, the correction (group mix,
-    or the bank-wide GEMM at L = 64) 2 O, the 64-lane scan 2 (6 O^2 + 2 O^2) 64 / (64 L) per
-    chunk; general engine ~2 x 10."""
+    or the bank-wide GEMM at L >= 64) 2 O, the 64-lane scan 2 (6 O^2 + 2 O^2) 64 / (64 L) per
+    chunk; at L >= 64 the GEMM also carries the zero-state term as ceil((L+O)/32) 32 extra K rows
+    (2 flops per row and sample, shared by the N bands); general engine ~2 x 10."""
     if not lti:
         return 20.0
     import math
     e = 2.0 * O * 4 * math.ceil((L + O) / 4) / L
     mix = 2.0 * O
     scan = 2.0 * 8 * O * O / L
-    return e + mix + scan
+    zs = 2.0 * math.ceil((L + O) / 32) * 32 / N if L >= 64 else 0.0
+    return e + mix + scan + zs
 
 
 def pmc_traffic(kernels=("fb_mix_kernel",), extra=()):
@@ -283,12 +285,13 @@ def main():
         band_samples_per_launch = cnt * S * args.steps / max(1, launches)
         flops_per_launch = FLOPS_PER_BAND_SAMPLE * band_samples_per_launch
         achieved = flops_per_launch / launch_avg_s / 1e12 if launch_avg_s > 0 else None
-        xflops = fb_executed_flops(lti, chunk)
+        xflops = fb_executed_flops(lti, chunk, N=cnt)
         executed = xflops * band_samples_per_launch / launch_avg_s / 1e12 if launch_avg_s > 0 else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(fwd, back)
-        kernels = (("fb_lti_kernel", "fb_lti_gemm", "fb_lti_reduce", "fb_lti_seg_carry") if lti
+        kernels = (("fb_lti_kernel", "fb_lti_gemm", "fb_lti_reduce", "fb_lti_seg_carry", "fb_lti_sum",
+                    "fb_lti_xrows") if lti
                    else ("fb_mix_kernel", "fb_reduce"))
         traffic, traffic_detail = None, "skipped"
         if not args.no_traffic and world == 1 and S == SAMPLES_PER_STEP:
@@ -311,14 +314,15 @@ def main():
                                    "f_i=0.5(i+1)SR/4096 R=0.999, boost 1 + open, k_p=0.1 k_g=1",
                        "samples_per_step": S, "block": 1024, "bands": N_BANDS,
                        "bands_per_gpu": cnt, "parallelism": f"bands sharded x{world}, RCCL reduce"},
-            "roofline": {"bound": "mfma" if lti else "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
+            "roofline": {"bound": "mfma" if lti else "valu", "achieved": executed, "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": (executed / FP64_PEAK_TFLOPS) if executed else None,
                          "traffic": traffic,
                          "traffic_detail": traffic_detail,
                          "algorithmic_bytes_per_launch": (16 * S + 120 * cnt) * args.steps / max(1, launches),
                          "launches_per_step": launches / max(1, args.steps),
-                         "kernel": (("LTI engine step: fb_lti_kernel<2,64,STATE> + fb_lti_gemm_kernel + "
-                                     "fb_lti_reduce_kernel (+ segment prepass)") if lti and chunk == 64 else
+                         "kernel": (("LTI engine step: fb_lti_kernel<2,%d,STATE> + fb_lti_xrows_kernel + "
+                                     "fb_lti_gemm_pp_kernel<%d> + fb_lti_sum_kernel (+ segment prepass)" % (chunk, chunk))
+                                    if lti and chunk >= 64 else
                                     ("LTI engine step: fb_lti_kernel<2,%d,MIX> + fb_lti_reduce_kernel (+ segment "
                                      "prepass)" % chunk) if lti
                                     else "general engine step: fb_mix_kernel<2,NONE,1,MIX> + fb_reduce_kernel"),
@@ -326,14 +330,18 @@ def main():
                          "components_ms_per_launch": {"segment_prepass": seg_ms / max(1, launches),
                                                       "mix_or_state": mix_ms / max(1, launches),
                                                       "gemm_and_reduce": red_ms / max(1, launches)},
-                         "flops_per_launch": flops_per_launch,
-                         "executed": {"flops_per_band_sample": xflops, "achieved": executed,
-                                      "frac": (executed / FP64_PEAK_TFLOPS) if executed else None},
-                         "note": "achieved = reference-equivalent rate: algorithmic 18 FP64 flops per band-sample "
-                                 "(SURVEY.md 8(d), the reference recurrence) over the whole per-step GPU time of the "
-                                 "engine (kernel_avg_ms = prepass + mix + reduce, HIP events); executed = the FP64 "
-                                 "flops the chunked state-space engine actually issues (DESIGN.md 3.3) over the same "
-                                 "time. peak = FP64 vector = FP64 MFMA peak."},
+                         "flops_per_band_sample": xflops,
+                         "flops_per_launch": xflops * band_samples_per_launch,
+                         "reference_equivalent": {"flops_per_band_sample": FLOPS_PER_BAND_SAMPLE,
+                                                  "achieved": achieved,
+                                                  "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None},
+                         "note": "achieved = the FP64 flops the engine's algorithm performs per band-sample "
+                                 "(chunked state space: chunk end states + 64-lane scan + correction GEMM with the "
+                                 "zero-state rows, DESIGN.md 3.3; PMC-verified in profiles/r2/flops_pmc.txt) over the "
+                                 "whole per-step GPU time of the engine (kernel_avg_ms, HIP events on the handle's "
+                                 "stream). reference_equivalent = the reference recurrence's 18 flops per band-sample "
+                                 "(SURVEY.md 8(d)) over the same time -- it can exceed the peak because the engine "
+                                 "needs fewer than half of them. peak = FP64 vector = FP64 MFMA peak."},
             "streaming": {"band_samples_per_s": stream_rate, "block": 1024,
                           "note": "one process() call per 1024-sample block, device-resident I/O"},
             "cpu_baseline": cpu,

@@ -119,6 +119,7 @@ def run_c3(args, torch, dev, rank=0, world=1, shard_world=None):
         dt = time.perf_counter() - t0
         cpu = {"value": V * O * n / dt, "unit": "partial-samples/s", "cores": 1, "kind": "port",
                "sample": f"oracle/hz_oracle_osc.c Additive, {V}x{O} partials x {n} samples, 1 thread, {dt:.2f} s"}
+    xach = EXEC_C3 * units / kern_s / 1e12 if kern_s > 0 else None
     return {
         "metric": "partial-samples/s for 64-voice x 256-overtone Additive",
         "value": units / elapsed, "unit": "partial-samples/s",
@@ -128,19 +129,19 @@ def run_c3(args, torch, dev, rank=0, world=1, shard_world=None):
                    "samples_per_step": S, "voices": V, "overtones": O, "overtones_per_gpu": oc,
                    "parallelism": f"overtones sharded x{world}, RCCL reduce"},
         "n_gpus": world, "scaling": "strong", "emulated_world": shard_world,
-        "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK if achieved else None, "traffic": None,
+        "roofline": {"bound": "valu", "achieved": xach, "peak": FP64_PEAK, "unit": "TFLOP/s",
+                     "frac": xach / FP64_PEAK if xach else None, "traffic": None,
                      "kernel": "add_mix_kernel (+ add_reduce_kernel, add_advance_kernel)",
                      "kernel_avg_ms": ms / max(1, launches), "launches": launches,
-                     "flops_per_unit": 22,
-                     "executed": {"flops_per_unit": EXEC_C3,
-                                  "achieved": EXEC_C3 * units / kern_s / 1e12 if kern_s > 0 else None,
-                                  "frac": EXEC_C3 * units / kern_s / 1e12 / FP64_PEAK if kern_s > 0 else None,
-                                  "source": "rocprofv3 --pmc SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 on this row "
-                                            "(profiles/r2/flops_pmc.txt)"},
-                     "note": "achieved = reference-equivalent rate: the algorithmic 22 flops (+ 3 transcendentals) "
-                             "of the reference's per-sample update (SURVEY.md 8(d)) over the whole launch (mix + "
-                             "reduce + advance); executed = the FP64 work the closed-form engine issues"},
+                     "flops_per_unit": EXEC_C3,
+                     "flops_source": "rocprofv3 --pmc SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 on this row "
+                                     "(profiles/r2/flops_pmc.txt)",
+                     "reference_equivalent": {"flops_per_unit": 22, "achieved": achieved,
+                                              "frac": achieved / FP64_PEAK if achieved else None},
+                     "note": "achieved = the FP64 work the closed-form engine performs per partial-sample (PMC) "
+                             "over the whole launch (mix + reduce + advance); reference_equivalent = the "
+                             "algorithmic 22 flops (+ 3 transcendentals) of the reference's per-sample update "
+                             "(SURVEY.md 8(d)) over the same time"},
         "cpu_baseline": cpu,
     }
 

@@ -15,7 +15,7 @@ for w in ${ROWS:-c2 c3 c4 c5 c6 c7 c8 c9}; do
   done
 done
 python3 - $OUT <<'PY'
-import csv, os, sys, collections
+import csv, os, re, sys, collections
 out = sys.argv[1]
 for row in sorted(d for d in os.listdir(out) if os.path.isdir(os.path.join(out, d))):
     agg = collections.defaultdict(lambda: collections.defaultdict(float)); disp = collections.defaultdict(set)
@@ -23,7 +23,8 @@ for row in sorted(d for d in os.listdir(out) if os.path.isdir(os.path.join(out, 
         for f in files:
             if f.endswith("counter_collection.csv"):
                 for r in csv.DictReader(open(os.path.join(root, f))):
-                    k = r["Kernel_Name"].split("(")[0][-60:]
+                    m = re.search(r"(\w+)(<[^()]*>)?\(", r["Kernel_Name"])
+                    k = (m.group(1) + (m.group(2) or "")) if m else r["Kernel_Name"][:60]
                     agg[k][r["Counter_Name"]] += float(r["Counter_Value"]); disp[k].add(r["Dispatch_Id"])
     print("==", row)
     for k, c in sorted(agg.items()):
