@@ -120,7 +120,7 @@ int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group)
 /* (diagnostics) plan of the last LTI launch: time segments, segment-prepass tiles skipped
  * at the head of each segment (the horizon prepass; 0 = full prepass), fine prepass parts */
 int hz_fb_lti_plan(hz_fb* h, long* nseg, long* skip_tiles, int* fine_parts);
-/* (diagnostics) chunk length L of the last LTI launch (16, 32 or 64; 0 before any) */
+/* (diagnostics) chunk length L of the last LTI launch (16, 32, 64 or 128; 0 before any) */
 int hz_fb_lti_last_chunk(hz_fb* h, int* chunk);
 
 /* ---- Oscbank<double,N>  (src/oscbank.h:15-97, src/multichannel.h:16-159) -- */
