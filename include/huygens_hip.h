@@ -115,7 +115,9 @@ int hz_fb_set_target_groups(hz_fb* h, int groups);
 int hz_fb_set_path(hz_fb* h, int path);
 int hz_fb_last_path(hz_fb* h, int* path);
 /* LTI engine geometry: (chunk length, bands per wave, waves per group) in
- * {(16,1,16), (32,1,16)}; 0s = default */
+ * {(16,1,16), (32,1,16), (64,1,16), (128,1,16)}; 0s = by call length (default: 128 for calls
+ * of >= 4 x 8192 samples on banks that fill the chip with <= 2 time segments, 64 from
+ * 2 x 4096 samples, 32 from 2 x 2048, else 16) */
 int hz_fb_tune_lti(hz_fb* h, int chunk, int bands_per_wave, int waves_per_group);
 /* (diagnostics) plan of the last LTI launch: time segments, segment-prepass tiles skipped
  * at the head of each segment (the horizon prepass; 0 = full prepass), fine prepass parts */
