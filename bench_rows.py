@@ -53,9 +53,10 @@ def _timed(step, steps, warmup, torch, dev, world=1):
 
 # --------------------------------------------------------------------------- C3
 # FP64 flops the Additive engine executes per partial-sample, measured with PMC counters on the
-# C3 row (profiles/r2/flops_pmc.txt: add_mix_kernel 3.59e11 flops over 5 steps of 7.86e9
-# partial-samples; transcendentals 2e-3 per partial-sample)
-EXEC_C3 = 9.1
+# C3 row (profiles/r2/flops_pmc.txt: add_mix_kernel 1.97e11 flops over 5 steps of 7.86e9
+# partial-samples with the two-term sine recurrence in 32-sample chunks; it was 9.1 with the
+# per-sample complex rotation)
+EXEC_C3 = 5.0
 
 
 def run_c3(args, torch, dev, rank=0, world=1, shard_world=None):

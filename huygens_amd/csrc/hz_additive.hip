@@ -16,8 +16,9 @@
 //     multiplies by the voice envelope amp(t) = act + a^t (amp0 - act) (closed-form seed,
 //     one-pole recurrence inside the chunk);
 //   * chunks where the frequency transient still moves the phase (|D| s^t > 2^-60) are
-//     evaluated per sample (sincospi); all others rotate a seeded phasor by w = e^{2 pi i A}
-//     (seed = z(t0) (w^16)^p (w^256)^r from per-partial tables, z(t0+1024) = z(t0) w^1024);
+//     evaluated per sample (sincospi); all others seed a phasor by w = e^{2 pi i A} per
+//     16-sample chunk (seed = z(t0) (w^16)^p (w^256)^r from per-partial tables,
+//     z(t0+1024) = z(t0) w^1024) and run the two-term sine recurrence inside the chunk;
 //   * time segments need no carry (closed form), so small banks still fill the chip;
 //   * waves' mixes are summed through LDS and a second kernel sums the group rows.
 // PI: the reference's truncated PI enters only through sin(2 PI frac(phi)); using 2 pi
@@ -33,7 +34,8 @@
 
 namespace {
 
-constexpr int kL = 16;
+constexpr int kL = 32;   // samples per lane chunk (16: 1.28 ms per C3 launch; 32 halves the per-chunk
+                         // seed / table / transient-check work per sample)
 constexpr int kTile = 64 * kL;
 constexpr int kWaves = 8;
 constexpr int kMaxPerWave = 64;
@@ -41,7 +43,7 @@ constexpr int kPad = 66;
 
 // per-partial record (depends only on the target frequency and the output weight):
 // A = f_target/SR (cycles/sample), c (output weight), W1 = e^{2 pi i A},
-// T1[p] = W1^(16 p) (p < 16), T2[r] = W1^(256 r) (r < 4), WT = W1^1024
+// T1[p] = W1^(kL p) (p < 16), T2[r] = W1^(16 kL r) (r < 4), WT = W1^(64 kL)
 struct PRec {
     static constexpr int A = 0, C = 1;
     static constexpr int W1 = 2;
@@ -163,15 +165,25 @@ __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __re
                     st *= a.s;
                 }
             } else {
+                // seed z(tc) = z(t0) w^(16 p) w^(256 r); inside the chunk the sines follow the
+                // two-term recurrence sin((k+1) th) = 2 cos th sin(k th) - sin((k-1) th): one
+                // FMA per sample instead of a complex multiply (4), re-seeded every kL samples
+                // (error <= kL eps / |sin th| of the partial's amplitude)
                 double ur, ui, zr, zi;
                 cmul(rr[PRec::T1 + 2 * p16], rr[PRec::T1 + 2 * p16 + 1], rr[PRec::T2 + 2 * r4],
                      rr[PRec::T2 + 2 * r4 + 1], ur, ui);
                 cmul(sr, si, ur, ui, zr, zi);
                 const double w1r = rr[PRec::W1], w1i = rr[PRec::W1 + 1];
+                const double c2 = 2.0 * w1r;
+                double s0 = zi, s1 = fma(zr, w1i, zi * w1r);
+                acc[0] = fma(c, s0, acc[0]);
+                acc[1] = fma(c, s1, acc[1]);
 #pragma unroll
-                for (int j = 0; j < kL; ++j) {
-                    acc[j] = fma(c, zi, acc[j]);
-                    cmul(zr, zi, w1r, w1i, zr, zi);
+                for (int j = 2; j < kL; ++j) {
+                    const double s2 = fma(c2, s1, -s0);
+                    acc[j] = fma(c, s2, acc[j]);
+                    s0 = s1;
+                    s1 = s2;
                 }
             }
         }
@@ -185,7 +197,7 @@ __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __re
         }
         __syncthreads();
         for (int tl = threadIdx.x; tl < kTile; tl += blockDim.x) {
-            const int src = tl >> 4, j = tl & 15;
+            const int src = tl / kL, j = tl % kL;
             double s0 = 0.0;
 #pragma unroll
             for (int w = 0; w < kWaves; ++w) s0 += part[w * (kL * kPad) + j * kPad + src];
@@ -234,15 +246,15 @@ void fill_tables(double A, double* rec) {
     const C w(std::cos(th), std::sin(th));
     rec[PRec::W1] = (double)w.real();
     rec[PRec::W1 + 1] = (double)w.imag();
-    C w16(1, 0);
-    for (int k = 0; k < 16; ++k) w16 *= w;
+    C wl(1, 0);
+    for (int k = 0; k < kL; ++k) wl *= w;
     C acc(1, 0);
     for (int p = 0; p < 16; ++p) {
         rec[PRec::T1 + 2 * p] = (double)acc.real();
         rec[PRec::T1 + 2 * p + 1] = (double)acc.imag();
-        acc *= w16;
+        acc *= wl;
     }
-    const C w256 = acc;
+    const C w256 = acc;   // W1^(16 kL)
     acc = C(1, 0);
     for (int r = 0; r < 4; ++r) {
         rec[PRec::T2 + 2 * r] = (double)acc.real();
