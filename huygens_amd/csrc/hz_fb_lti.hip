@@ -320,7 +320,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     // the E waves (the critical path: MFMA chain, then their scan) never wait on x staging
     constexpr bool X1 = lti_x1<L>();   // chunk 128: one x buffer, E operands in LDS
     static_assert(!X1 || MODE != MODE_MIX, "chunk 128 runs the state / prepass modes only");
-    constexpr bool kSplit = (MODE == MODE_STATE || (X1 && MODE == MODE_SEGEND)) && NE <= W / 2 &&
+    constexpr bool kSplit = (MODE == MODE_STATE || MODE == MODE_SEGEND) && NE <= W / 2 &&
                             (64 * (W - NE)) % L == 0;
     constexpr int WS = kSplit ? W - NE : W;                  // staging waves
     constexpr int PF2 = (XS + 64 * WS - 1) / (64 * WS);      // x values per staging thread
