@@ -159,11 +159,15 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_kernel(const double* __restri
 // multiples of 32), so no load is guarded, and the loop is unrolled by two over ping-pong A
 // registers and B buffers with no exit between the halves (no register copies between stages).
 // L = 64 or 128 samples per chunk (L / 16 accumulator blocks per wave).
-template <int L>
+// PADB: LDS row padding of the B stage (doubles; HZ_FB_GEMM_PADB experiments: C2 GEMM + sum
+// 0.190 / 0.191 / 0.181 / 0.182 / 0.185 ms for 16 / 8 / 4 / 2 / 1).  The staging
+// writes are interleaved (d2 v of a thread at column 2 (t & 15) + 32 v) so that one ds_write_b128
+// covers 256 consecutive bytes of a row.
+template <int L, int PADB = 4>
 __global__ __launch_bounds__(256) void fb_lti_gemm_pp_kernel(const double* __restrict__ gs,
                                                              const double* __restrict__ kt, int kslice, int bs_pad,
                                                              int ntiles, double* __restrict__ part, long n_pad) {
-    constexpr int kD = 4, kRows = 16, JB = L / 16, BR = L + 16, BV = L / 32;   // BV d2 per thread
+    constexpr int kD = 4, kRows = 16, JB = L / 16, BR = L + PADB, BV = L / 32;   // BV d2 per thread
     __shared__ __attribute__((aligned(16))) double bsh[2][kRows * BR];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int tile = blockIdx.x;
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_pp_kernel(const double* __res
 #pragma unroll
     for (int jb = 0; jb < JB; ++jb) acc[jb] = f64x4{0.0, 0.0, 0.0, 0.0};
     const double* ap = gs + ((long)tile * bs_pad + b0 + (lane >> 4)) * 64 + 16 * wave + (lane & 15);
-    const int brow = threadIdx.x >> 4, bcol = 2 * BV * (threadIdx.x & 15);
+    const int brow = threadIdx.x >> 4, bcol = 2 * (threadIdx.x & 15);
     const double* bp = kt + (long)(b0 + brow) * L + bcol;
     typedef double d2 __attribute__((ext_vector_type(2)));
     auto load_a = [&](int st, double (&av)[kD]) {
@@ -183,11 +187,11 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_pp_kernel(const double* __res
     auto load_b = [&](int st, d2 (&bv)[BV]) {
         const double* q = bp + (long)(kRows * st) * L;
 #pragma unroll
-        for (int v = 0; v < BV; ++v) bv[v] = *(const d2*)(q + 2 * v);
+        for (int v = 0; v < BV; ++v) bv[v] = *(const d2*)(q + 32 * v);
     };
     auto store_b = [&](int buf, const d2 (&bv)[BV]) {
 #pragma unroll
-        for (int v = 0; v < BV; ++v) *(d2*)&bsh[buf][brow * BR + bcol + 2 * v] = bv[v];
+        for (int v = 0; v < BV; ++v) *(d2*)&bsh[buf][brow * BR + bcol + 32 * v] = bv[v];
     };
     auto compute = [&](int buf, const double (&av)[kD]) {
         const double* bs = bsh[buf] + (lane >> 4) * BR + (lane & 15);
@@ -287,7 +291,14 @@ int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* p
     if (abl == 1) k = fb_lti_gemm_kernel<1, 4, 1>;
     if (abl == 2) k = fb_lti_gemm_kernel<1, 4, 2>;
     if (abl == 3) k = fb_lti_gemm_kernel<1, 4, 3>;
-    if (full && abl == 0) k = L == 128 ? fb_lti_gemm_pp_kernel<128> : fb_lti_gemm_pp_kernel<64>;
+    static const int padb = std::getenv("HZ_FB_GEMM_PADB") ? std::atoi(std::getenv("HZ_FB_GEMM_PADB")) : 4;
+    if (full && abl == 0) {
+        k = L == 128 ? fb_lti_gemm_pp_kernel<128> : fb_lti_gemm_pp_kernel<64>;
+        if (padb == 16) k = L == 128 ? fb_lti_gemm_pp_kernel<128, 16> : fb_lti_gemm_pp_kernel<64, 16>;
+        if (padb == 8) k = L == 128 ? fb_lti_gemm_pp_kernel<128, 8> : fb_lti_gemm_pp_kernel<64, 8>;
+        if (padb == 2) k = L == 128 ? fb_lti_gemm_pp_kernel<128, 2> : fb_lti_gemm_pp_kernel<64, 2>;
+        if (padb == 1) k = L == 128 ? fb_lti_gemm_pp_kernel<128, 1> : fb_lti_gemm_pp_kernel<64, 1>;
+    }
     hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)S), dim3(256), 0, stream, gs, kt, kslice, bs_pad, ntiles, part,
                        n_pad);
     HZ_TRY_HIP(hipGetLastError());
