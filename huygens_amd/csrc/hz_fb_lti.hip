@@ -237,8 +237,10 @@ __host__ __device__ constexpr int lti_krow() { return L + 16; }
 // tile) and the E operands in LDS ([taps][BSP + 8]) -- their 33 k-steps do not fit registers
 template <int L>
 __host__ __device__ constexpr bool lti_x1() { return L >= 128; }
+// E rows [tap][BSP + 16]: a row stride of 32 banks, so the two taps a half-wave reads (lanes
+// 0-15, 16-31) land on disjoint banks
 template <int O, int L>
-__host__ __device__ constexpr int lti_ebr() { return lti_bsp(O) + 8; }
+__host__ __device__ constexpr int lti_ebr() { return lti_bsp(O) + 16; }
 template <int O, int L>
 __host__ __device__ constexpr size_t lti_lds_bytes(bool mix) {
     if (lti_x1<L>())
