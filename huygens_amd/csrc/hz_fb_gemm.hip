@@ -163,21 +163,29 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_kernel(const double* __restri
 // 0.190 / 0.191 / 0.181 / 0.182 / 0.185 ms for 16 / 8 / 4 / 2 / 1).  The staging
 // writes are interleaved (d2 v of a thread at column 2 (t & 15) + 32 v) so that one ds_write_b128
 // covers 256 consecutive bytes of a row.
-template <int L, int PADB = 4>
-__global__ __launch_bounds__(256) void fb_lti_gemm_pp_kernel(const double* __restrict__ gs,
-                                                             const double* __restrict__ kt, int kslice, int bs_pad,
-                                                             int ntiles, double* __restrict__ part, long n_pad) {
-    constexpr int kD = 4, kRows = 16, JB = L / 16, BR = L + PADB, BV = L / 32;   // BV d2 per thread
+// WJ: sample-column parts per chunk block: the workgroup is 4 WJ waves, wave (cb, jh) = (w & 3,
+// w >> 2) computes chunks 16 cb .. 16 cb + 15 x samples jh L / WJ .. (jh + 1) L / WJ (L / (16 WJ)
+// accumulators): fewer registers per wave (more waves per CU) and one B stage shared by more waves.
+// Measured at C2 (HZ_FB_GEMM_WJ=2, 2 / 3 / 4 workgroups per CU): GEMM + sum 0.234 / 0.193 / 0.190
+// ms against 0.181 for WJ = 1 -- the default stays 1
+template <int L, int PADB = 4, int WJ = 1>
+__global__ __launch_bounds__(256 * WJ) void fb_lti_gemm_pp_kernel(const double* __restrict__ gs,
+                                                                  const double* __restrict__ kt, int kslice,
+                                                                  int bs_pad, int ntiles, double* __restrict__ part,
+                                                                  long n_pad) {
+    constexpr int kD = 4, kRows = 16, JB = L / (16 * WJ), BR = L + PADB;
+    constexpr int TPR = 16 * WJ, BV = L / (2 * TPR);   // threads per B row, d2 per thread
     __shared__ __attribute__((aligned(16))) double bsh[2][kRows * BR];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int cb = wave & 3, j0 = (wave >> 2) * (L / WJ);
     const int tile = blockIdx.x;
     const int b0 = blockIdx.y * kslice;
     const int nst = (min(bs_pad, b0 + kslice) - b0) / kRows;
     f64x4 acc[JB];
 #pragma unroll
     for (int jb = 0; jb < JB; ++jb) acc[jb] = f64x4{0.0, 0.0, 0.0, 0.0};
-    const double* ap = gs + ((long)tile * bs_pad + b0 + (lane >> 4)) * 64 + 16 * wave + (lane & 15);
-    const int brow = threadIdx.x >> 4, bcol = 2 * (threadIdx.x & 15);
+    const double* ap = gs + ((long)tile * bs_pad + b0 + (lane >> 4)) * 64 + 16 * cb + (lane & 15);
+    const int brow = threadIdx.x / TPR, bcol = 2 * (threadIdx.x % TPR);
     const double* bp = kt + (long)(b0 + brow) * L + bcol;
     typedef double d2 __attribute__((ext_vector_type(2)));
     auto load_a = [&](int st, double (&av)[kD]) {
@@ -187,14 +195,14 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_pp_kernel(const double* __res
     auto load_b = [&](int st, d2 (&bv)[BV]) {
         const double* q = bp + (long)(kRows * st) * L;
 #pragma unroll
-        for (int v = 0; v < BV; ++v) bv[v] = *(const d2*)(q + 32 * v);
+        for (int v = 0; v < BV; ++v) bv[v] = *(const d2*)(q + 2 * TPR * v);
     };
     auto store_b = [&](int buf, const d2 (&bv)[BV]) {
 #pragma unroll
-        for (int v = 0; v < BV; ++v) *(d2*)&bsh[buf][brow * BR + bcol + 32 * v] = bv[v];
+        for (int v = 0; v < BV; ++v) *(d2*)&bsh[buf][brow * BR + bcol + 2 * TPR * v] = bv[v];
     };
     auto compute = [&](int buf, const double (&av)[kD]) {
-        const double* bs = bsh[buf] + (lane >> 4) * BR + (lane & 15);
+        const double* bs = bsh[buf] + (lane >> 4) * BR + j0 + (lane & 15);
 #pragma unroll
         for (int u = 0; u < kD; ++u) {
             const double* bu = bs + 4 * u * BR;
@@ -229,8 +237,8 @@ __global__ __launch_bounds__(256) void fb_lti_gemm_pp_kernel(const double* __res
         if (st + 3 < nst) load_b(st + 3, bq);
         __syncthreads();
     }
-    const long c0 = (long)tile * 64 + 16 * wave;
-    double* out = part + (long)blockIdx.y * n_pad + (c0 + (lane >> 4)) * L + (lane & 15);
+    const long c0 = (long)tile * 64 + 16 * cb;
+    double* out = part + (long)blockIdx.y * n_pad + (c0 + (lane >> 4)) * L + j0 + (lane & 15);
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
@@ -292,15 +300,21 @@ int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* p
     if (abl == 2) k = fb_lti_gemm_kernel<1, 4, 2>;
     if (abl == 3) k = fb_lti_gemm_kernel<1, 4, 3>;
     static const int padb = std::getenv("HZ_FB_GEMM_PADB") ? std::atoi(std::getenv("HZ_FB_GEMM_PADB")) : 4;
+    static const int wj = std::getenv("HZ_FB_GEMM_WJ") ? std::atoi(std::getenv("HZ_FB_GEMM_WJ")) : 1;
+    int threads = 256;
     if (full && abl == 0) {
         k = L == 128 ? fb_lti_gemm_pp_kernel<128> : fb_lti_gemm_pp_kernel<64>;
+        if (wj == 2) {
+            k = L == 128 ? fb_lti_gemm_pp_kernel<128, 4, 2> : fb_lti_gemm_pp_kernel<64, 4, 2>;
+            threads = 512;
+        }
         if (padb == 16) k = L == 128 ? fb_lti_gemm_pp_kernel<128, 16> : fb_lti_gemm_pp_kernel<64, 16>;
         if (padb == 8) k = L == 128 ? fb_lti_gemm_pp_kernel<128, 8> : fb_lti_gemm_pp_kernel<64, 8>;
         if (padb == 2) k = L == 128 ? fb_lti_gemm_pp_kernel<128, 2> : fb_lti_gemm_pp_kernel<64, 2>;
         if (padb == 1) k = L == 128 ? fb_lti_gemm_pp_kernel<128, 1> : fb_lti_gemm_pp_kernel<64, 1>;
     }
-    hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)S), dim3(256), 0, stream, gs, kt, kslice, bs_pad, ntiles, part,
-                       n_pad);
+    hipLaunchKernelGGL(k, dim3((unsigned)gx, (unsigned)S), dim3(threads), 0, stream, gs, kt, kslice, bs_pad, ntiles,
+                       part, n_pad);
     HZ_TRY_HIP(hipGetLastError());
     *slices_out = S;
     return HZ_OK;
