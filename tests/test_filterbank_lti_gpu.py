@@ -98,6 +98,35 @@ def test_chunk128_long_calls(gpu_lib, N, order, groups):
     assert g.lti_chunk() == 128
 
 
+@pytest.mark.parametrize("shift", [1, 3])
+def test_chunk128_device_pointers_unaligned(gpu_lib, shift):
+    """hz_fb_process_device on x / out pointers that are only 8-byte aligned (a tensor view
+    starting `shift` doubles in): the chunk-128 LDS-DMA loads 16 B per lane from x + c L + 2 l,
+    which then straddles 16-byte boundaries; results must not change."""
+    torch = pytest.importorskip("torch")
+    N = 1024
+    fwd, back = resonant_coefficients(N, 0.999, 0.5)
+    g, o = make_pair(2, N, fwd, back, kp=0.0, kg=0.0)
+    g.tune_lti(128, 1, 16)
+    rng = np.random.default_rng(70 + shift)
+    for i, n in enumerate([1024, 8192 * 4 + 77, 50000]):
+        x = rng.uniform(-1, 1, n).astype(np.float32).astype(np.float64)
+        buf = torch.zeros(n + 2 * shift, dtype=torch.float64, device="cuda")
+        buf[shift:shift + n] = torch.from_numpy(x).cuda()
+        out = torch.full((n + 2 * shift,), 7.0, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
+        g.process_device(buf[shift:].data_ptr(), out[shift:].data_ptr(), n)
+        g.synchronize()
+        yo = o.process(x)
+        yg = out.cpu().numpy()
+        assert rel_err(yg[shift:shift + n], yo) < TOL, (i, n)
+        assert np.all(yg[:shift] == 7.0) and np.all(yg[shift + n:] == 7.0)
+        if i > 0:
+            assert g.lti_chunk() == 128
+    from huygens_amd._lib import HZ_FB_PATH_LTI
+    assert g.last_path() == HZ_FB_PATH_LTI
+
+
 def test_chunk128_picked_for_c2(gpu_lib):
     """By call length: chunk 128 for long calls of banks with at most two time segments, chunk
     64 for smaller shards, chunk 16 for streaming blocks."""
