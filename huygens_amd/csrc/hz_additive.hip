@@ -394,7 +394,7 @@ struct PhaseBank {
             if (ev_used + 2 > ev.size())
                 for (int q = 0; q < 128; ++q) {
                     hipEvent_t ne;
-                    HZ_TRY_HIP(hipEventCreate(&ne));
+                    HZ_TRY_HIP(hz::prof_event_create(&ne));
                     ev.push_back(ne);
                 }
             e = &ev[ev_used];

@@ -352,7 +352,7 @@ int bowl_launch(hz_bowl* h, void* d_dst, long n, int out_kind) {
         if (h->ev_used + 2 > h->ev.size())
             for (int q = 0; q < 128; ++q) {
                 hipEvent_t ne;
-                HZ_TRY_HIP(hipEventCreate(&ne));
+                HZ_TRY_HIP(hz::prof_event_create(&ne));
                 h->ev.push_back(ne);
             }
         e = &h->ev[h->ev_used];

@@ -24,6 +24,13 @@ void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 // Checks that a gfx950 device is visible and selects it; returns HZ_OK or an error.
 int select_device(int device);
 
+// Timing events of the profile counters: no system-scope fence on record, so a record between
+// two kernels does not write back / invalidate L2 (it cost 5-10 us per record on the C2 step).
+// Only hipEventElapsedTime after a stream synchronize reads them.
+inline hipError_t prof_event_create(hipEvent_t* e) {
+    return hipEventCreateWithFlags(e, hipEventDisableSystemFence);
+}
+
 }  // namespace hz
 
 #define HZ_TRY_HIP(expr)                                                                   \

@@ -285,7 +285,7 @@ int dly_launch_t(hz_dly* h, const void* d_in, void* d_out, long n, int in_per_li
         if (h->ev_used + 2 > h->ev.size())
             for (int q = 0; q < 128; ++q) {
                 hipEvent_t ne;
-                HZ_TRY_HIP(hipEventCreate(&ne));
+                HZ_TRY_HIP(hz::prof_event_create(&ne));
                 h->ev.push_back(ne);
             }
         e = &h->ev[h->ev_used];

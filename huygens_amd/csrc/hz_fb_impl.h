@@ -95,6 +95,9 @@ struct hz_fb {
     bool prof = false;
     std::vector<hipEvent_t> ev;  // quintuplets: start, mix start, mix end, reduce start, reduce end
     size_t ev_used = 0;
+    // per quintuplet: bit 1 = mix start not recorded (same point as start), bit 3 = reduce
+    // start not recorded (same point as mix end); every record costs a few us of GPU time
+    std::vector<unsigned char> ev_skip;
     long prof_launches = 0;
     // converged (LTI) path, hz_fb_lti.hip
     int path_mode = HZ_FB_PATH_AUTO;

@@ -1488,7 +1488,8 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
                                (int)nseg_state, seg_tiles / m);
             HZ_TRY_HIP(hipGetLastError());
         }
-        if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
+        if (e && nseg > 1) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
+        else if (e) h->ev_skip[(e - h->ev.data()) / 5] |= 2;
         static const bool diag_state = std::getenv("HZ_FB_LTI_DIAG_STATE") != nullptr;
         if (diag_state && nseg == 1 && !gemm) {   // (diagnostics) the E + scan work alone, timed by rocprof
             LtiArgs ad = a;
@@ -1545,7 +1546,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             // correction GEMM over band-state slices (>= 4 workgroups per CU), then the slice sum
             // + zero-state term in the reduce kernel; one stream, chunks in sequence
             double* part = h->d_partial + (size_t)bs_tot * nc_pad;
-            if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
+            if (e) h->ev_skip[(e - h->ev.data()) / 5] |= 8;   // reduce start = mix end
             int S = 1;
             HZ_TRY(fb_lti_gemm_launch(h->d_partial, set.d_kt, bs_tot, part, a.n_pad, (int)ntiles, L, h->target_groups,
                                       kMaxSlices, h->stream, &S));

@@ -692,11 +692,13 @@ int fb_prof_events(hz_fb* h, hipEvent_t** e) {
     if (h->ev_used + 5 > h->ev.size()) {
         for (int q = 0; q < 5 * 64; ++q) {
             hipEvent_t ne;
-            HZ_TRY_HIP(hipEventCreate(&ne));
+            HZ_TRY_HIP(hz::prof_event_create(&ne));
             h->ev.push_back(ne);
         }
     }
     *e = &h->ev[h->ev_used];
+    h->ev_skip.resize(h->ev.size() / 5);
+    h->ev_skip[h->ev_used / 5] = 0;
     h->ev_used += 5;
     return HZ_OK;
 }
@@ -1252,9 +1254,12 @@ int hz_fb_profile_read(hz_fb* h, double* segment_ms, double* mix_ms, double* red
     double sg = 0, m = 0, r = 0;
     for (size_t i = 0; i + 5 <= h->ev_used; i += 5) {
         float a = 0, b = 0, c = 0;
-        HZ_TRY_HIP(hipEventElapsedTime(&a, h->ev[i], h->ev[i + 1]));
-        HZ_TRY_HIP(hipEventElapsedTime(&b, h->ev[i + 1], h->ev[i + 2]));
-        HZ_TRY_HIP(hipEventElapsedTime(&c, h->ev[i + 3], h->ev[i + 4]));
+        const unsigned char skip = h->ev_skip[i / 5];
+        const hipEvent_t e1 = (skip & 2) ? h->ev[i] : h->ev[i + 1];
+        const hipEvent_t e3 = (skip & 8) ? h->ev[i + 2] : h->ev[i + 3];
+        if (!(skip & 2)) HZ_TRY_HIP(hipEventElapsedTime(&a, h->ev[i], e1));
+        HZ_TRY_HIP(hipEventElapsedTime(&b, e1, h->ev[i + 2]));
+        HZ_TRY_HIP(hipEventElapsedTime(&c, e3, h->ev[i + 4]));
         sg += a;
         m += b;
         r += c;

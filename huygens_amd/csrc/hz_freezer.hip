@@ -412,7 +412,7 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
             if (h->ev_used + 2 > h->ev.size())
                 for (int q = 0; q < 64; ++q) {
                     hipEvent_t ne;
-                    HZ_TRY_HIP(hipEventCreate(&ne));
+                    HZ_TRY_HIP(hz::prof_event_create(&ne));
                     h->ev.push_back(ne);
                 }
             e = &h->ev[h->ev_used];

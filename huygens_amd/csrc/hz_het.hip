@@ -447,7 +447,7 @@ int het_run(hz_het* h, const double* d_in, double* d_out, long n) {
             if (h->ev_used + 2 > h->ev.size())
                 for (int q = 0; q < 64; ++q) {
                     hipEvent_t ne;
-                    HZ_TRY_HIP(hipEventCreate(&ne));
+                    HZ_TRY_HIP(hz::prof_event_create(&ne));
                     h->ev.push_back(ne);
                 }
             e = &h->ev[h->ev_used];

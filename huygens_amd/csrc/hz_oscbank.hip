@@ -317,7 +317,7 @@ int osc_launch(hz_osc* h, double* d_mix, double* d_per_band, long n) {
         if (h->ev_used + 2 > h->ev.size())
             for (int q = 0; q < 128; ++q) {
                 hipEvent_t ne;
-                HZ_TRY_HIP(hipEventCreate(&ne));
+                HZ_TRY_HIP(hz::prof_event_create(&ne));
                 h->ev.push_back(ne);
             }
         e = &h->ev[h->ev_used];

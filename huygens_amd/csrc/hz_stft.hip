@@ -715,7 +715,7 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
         if (h->ev_used + 3 > h->ev.size())
             for (int q = 0; q < 96; ++q) {
                 hipEvent_t ne;
-                HZ_TRY_HIP(hipEventCreate(&ne));
+                HZ_TRY_HIP(hz::prof_event_create(&ne));
                 h->ev.push_back(ne);
             }
         e = &h->ev[h->ev_used];
