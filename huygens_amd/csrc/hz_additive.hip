@@ -94,6 +94,17 @@ __device__ __forceinline__ double phase_at(double phi0, double A, double D, doub
     return q - floor(q);
 }
 
+// kL samples of one partial in its frequency transient, exact closed form per sample, added to
+// the LDS column `col` (stride kPad); out of line so sinpi's registers stay out of the main loop
+__device__ __attribute__((noinline)) void add_transient(double* col, double phi0, double A, double c, double D,
+                                                        double s, long tc, double st) {
+    for (int j = 0; j < kL; ++j) {
+        const double ph = phase_at(phi0, A, D, s, (double)(tc + j), st);
+        col[j * kPad] = fma(c, sinpi(2.0 * ph), col[j * kPad]);
+        st *= s;
+    }
+}
+
 __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __restrict__ rec, AddArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* part = lds;                           // [W][16][66]
@@ -141,10 +152,11 @@ __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __re
 #pragma unroll
         for (int j = 0; j < kL; ++j) acc[j] = 0.0;
         const double s_tc = pow(a.s, (double)tc);  // transient decay at this chunk
+        bool trans = false;
         for (int q = 0; q < tk.count; ++q) {
             const int pi = tk.first + q;
             const double* rr = rec + (long)pi * PRec::SIZE;
-            const double A = rr[PRec::A], c = rr[PRec::C];
+            const double c = rr[PRec::C];
             const double D = (a.f[pi] - a.ft[pi]) * inv_trans;
             const double sr = myzt[2 * q], si = myzt[2 * q + 1];
             double nr, ni;
@@ -156,14 +168,7 @@ __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __re
             __builtin_amdgcn_wave_barrier();
             if (a.c0 && tc == 0) acc[0] = fma(a.c0[pi] - c, sinpi(2.0 * a.phi[pi]), acc[0]);
             if (fabs(D) * s_tc > 0x1p-60) {
-                // frequency transient: exact closed form per sample (first chunks only)
-                const double phi0 = a.phi[pi];
-                double st = s_tc;
-                for (int j = 0; j < kL; ++j) {
-                    const double ph = phase_at(phi0, A, D, a.s, (double)(tc + j), st);
-                    acc[j] = fma(c, sinpi(2.0 * ph), acc[j]);
-                    st *= a.s;
-                }
+                trans = true;   // frequency transient: the second pass below
             } else {
                 // seed z(tc) = z(t0) w^(16 p) w^(256 r); inside the chunk the sines follow the
                 // two-term recurrence sin((k+1) th) = 2 cos th sin(k th) - sin((k-1) th): one
@@ -190,10 +195,30 @@ __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __re
         // voice envelope amp(t) = act + a^t (amp0 - act), advanced per sample
         double amp = act + (a_lane * a_t) * (amp0 - act);
         double* my = part + wave * (kL * kPad);
+        if (__builtin_amdgcn_ballot_w64(trans) == 0) {
 #pragma unroll
-        for (int j = 0; j < kL; ++j) {
-            my[j * kPad + lane] = amp * acc[j];
-            amp = fma(a.a, amp, (1.0 - a.a) * act);
+            for (int j = 0; j < kL; ++j) {
+                my[j * kPad + lane] = amp * acc[j];
+                amp = fma(a.a, amp, (1.0 - a.a) * act);
+            }
+        } else {
+            // chunks still inside a frequency transient (the first tiles of a retune): the
+            // exact closed form per sample, accumulated through this wave's LDS rows after the
+            // settled partials (the register accumulators are dead here, so sinpi's registers
+            // do not spill the 32 accumulators of the main loop)
+#pragma unroll
+            for (int j = 0; j < kL; ++j) my[j * kPad + lane] = acc[j];
+            for (int q = 0; q < tk.count; ++q) {
+                const int pi = tk.first + q;
+                const double* rr = rec + (long)pi * PRec::SIZE;
+                const double D = (a.f[pi] - a.ft[pi]) * inv_trans;
+                if (fabs(D) * s_tc > 0x1p-60)
+                    add_transient(my + lane, a.phi[pi], rr[PRec::A], rr[PRec::C], D, a.s, tc, s_tc);
+            }
+            for (int j = 0; j < kL; ++j) {
+                my[j * kPad + lane] *= amp;
+                amp = fma(a.a, amp, (1.0 - a.a) * act);
+            }
         }
         __syncthreads();
         for (int tl = threadIdx.x; tl < kTile; tl += blockDim.x) {

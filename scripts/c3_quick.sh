@@ -6,7 +6,7 @@ OUT=gpurun_out/${TAG:-c3q}; mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
     tests/test_additive_gpu.py ${TESTS:-} > $OUT/pytest.log 2>&1
 rc=$?; tail -2 $OUT/pytest.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python bench.py --workload c3 --steps 5 --warmup 1 --no-cpu-baseline > $OUT/bench.log 2>&1
+timeout -k 10 300 python bench.py --workload c3 --steps 100 --warmup 10 --no-cpu-baseline > $OUT/bench.log 2>&1
 rc=$?; [ $rc -ne 0 ] && { tail -5 $OUT/bench.log; exit $rc; }
 python3 -c "
 import json; l=[x for x in open('$OUT/bench.log') if x.startswith('{')][-1]; d=json.loads(l); r=d['roofline']
