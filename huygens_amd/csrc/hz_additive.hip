@@ -153,19 +153,41 @@ __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __re
         for (int j = 0; j < kL; ++j) acc[j] = 0.0;
         const double s_tc = pow(a.s, (double)tc);  // transient decay at this chunk
         bool trans = false;
-        for (int q = 0; q < tk.count; ++q) {
+        // the next partial's record, frequency pair and tile phasor are fetched one iteration
+        // ahead (software pipeline: their global / LDS latency runs under this partial's
+        // recurrence instead of in front of it)
+        struct Fetch {
+            double c, D, wtr, wti, t1r, t1i, t2r, t2i, w1r, w1i, sr, si;
+        };
+        auto fetch = [&](int q, Fetch& p) {
             const int pi = tk.first + q;
             const double* rr = rec + (long)pi * PRec::SIZE;
-            const double c = rr[PRec::C];
-            const double D = (a.f[pi] - a.ft[pi]) * inv_trans;
-            const double sr = myzt[2 * q], si = myzt[2 * q + 1];
+            p.c = rr[PRec::C];
+            p.D = (a.f[pi] - a.ft[pi]) * inv_trans;
+            p.wtr = rr[PRec::WT];
+            p.wti = rr[PRec::WT + 1];
+            p.t1r = rr[PRec::T1 + 2 * p16];
+            p.t1i = rr[PRec::T1 + 2 * p16 + 1];
+            p.t2r = rr[PRec::T2 + 2 * r4];
+            p.t2i = rr[PRec::T2 + 2 * r4 + 1];
+            p.w1r = rr[PRec::W1];
+            p.w1i = rr[PRec::W1 + 1];
+            p.sr = myzt[2 * q];
+            p.si = myzt[2 * q + 1];
+        };
+        Fetch cur;
+        if (tk.count) fetch(0, cur);
+        for (int q = 0; q < tk.count; ++q) {
+            const int pi = tk.first + q;
+            Fetch nxt;
+            if (q + 1 < tk.count) fetch(q + 1, nxt);
+            const double c = cur.c, D = cur.D, sr = cur.sr, si = cur.si;
             double nr, ni;
-            cmul(sr, si, rr[PRec::WT], rr[PRec::WT + 1], nr, ni);
+            cmul(sr, si, cur.wtr, cur.wti, nr, ni);
             if (lane == 0) {
                 myzt[2 * q] = nr;
                 myzt[2 * q + 1] = ni;
             }
-            __builtin_amdgcn_wave_barrier();
             if (a.c0 && tc == 0) acc[0] = fma(a.c0[pi] - c, sinpi(2.0 * a.phi[pi]), acc[0]);
             if (fabs(D) * s_tc > 0x1p-60) {
                 trans = true;   // frequency transient: the second pass below
@@ -175,10 +197,9 @@ __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __re
                 // FMA per sample instead of a complex multiply (4), re-seeded every kL samples
                 // (error <= kL eps / |sin th| of the partial's amplitude)
                 double ur, ui, zr, zi;
-                cmul(rr[PRec::T1 + 2 * p16], rr[PRec::T1 + 2 * p16 + 1], rr[PRec::T2 + 2 * r4],
-                     rr[PRec::T2 + 2 * r4 + 1], ur, ui);
+                cmul(cur.t1r, cur.t1i, cur.t2r, cur.t2i, ur, ui);
                 cmul(sr, si, ur, ui, zr, zi);
-                const double w1r = rr[PRec::W1], w1i = rr[PRec::W1 + 1];
+                const double w1r = cur.w1r, w1i = cur.w1i;
                 const double c2 = 2.0 * w1r;
                 double s0 = zi, s1 = fma(zr, w1i, zi * w1r);
                 acc[0] = fma(c, s0, acc[0]);
@@ -191,7 +212,9 @@ __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __re
                     s1 = s2;
                 }
             }
+            cur = nxt;
         }
+        __builtin_amdgcn_wave_barrier();   // lane 0's phasor updates before the next tile's reads
         // voice envelope amp(t) = act + a^t (amp0 - act), advanced per sample
         double amp = act + (a_lane * a_t) * (amp0 - act);
         double* my = part + wave * (kL * kPad);
