@@ -19,9 +19,12 @@
 // Source ring.  The reference reads slot (origin - c + size) mod 2^32 mod size of a
 // `size`-slot ring whose slot s, at time t, holds the latest sample written at a time
 // tau <= t with tau = t - ((origin_t - s) mod size) (0 if tau < 0).  The device keeps a
-// time-indexed ring of C >= size + kChunk samples (a power of two), so no sample a block
-// still needs is overwritten by the same block: tau >= T0 comes from the block's input,
-// older ones from the ring.  The uint32 index arithmetic is kept verbatim (bit-exact).
+// time-indexed ring of C >= size + kChunk samples (a power of two); a launch's input is
+// copied into it first, so every read is ring[tau mod C]: a read reaches back less than `size`
+// samples, so slot tau mod C still holds x(tau) (its next writer, tau + C, lies past the
+// launch), and a tau < 0 slot is still the ring's initial zero.  The uint32 index arithmetic
+// is kept verbatim (bit-exact) where it can wrap; for 0 <= center < size it reduces to
+// tau = t - center (tau = t - center - 1, or t when center + 1 = size, for the second tap).
 //
 // Layout in HBM: ring [C] doubles; grains [G] x 64 B per block (uploaded once per call).
 #include <algorithm>
@@ -45,12 +48,11 @@ struct alignas(16) GrainDev {
     long t_first, t_end;                      // reads at t_first <= t < t_end
     double offsets, sizes, speeds, gains;     // granulator.h:67-70 (samples, samples, ratio, gain)
     unsigned ticks0, pad0;
-    long pad1;
+    double rsizes;                            // RN(1 / sizes) for a normal finite quotient, else 0
 };
 static_assert(sizeof(GrainDev) == 64, "grain record is one 64 B line");
 
 struct GranArgs {
-    const double* in;     // block input: time T0 + j
     double* out;
     double* ring;         // time-indexed source ring (C = mask + 1 samples)
     const GrainDev* g;    // the call's grains, voice-major
@@ -69,16 +71,12 @@ __device__ __forceinline__ unsigned fastmod(unsigned x, unsigned long fm, unsign
     return (unsigned)__umul64hi(low, (unsigned long)size);
 }
 
-// Address of x(tau) for tau <= t (block input or ring); tau < 0 maps to a valid ring slot
-// and is zeroed by the caller, so the loads need no branch
-__device__ __forceinline__ const double* src_ptr(const GranArgs& a, long tau) {
-    return tau >= a.T0 ? a.in + (tau - a.T0) : a.ring + (tau & a.mask);
-}
-
 constexpr int kUnroll = 4;   // grains in flight per thread: their 2 x 4 gathers issue together
 
 __global__ __launch_bounds__(kThreads) void gran_kernel(GranArgs a) {
 #pragma clang fp contract(off)
+    // the wave's first sample: grains that miss the wave's 64 samples are skipped (scalar branch)
+    const long tw = a.T0 + (long)blockIdx.x * blockDim.x + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63);
     const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= a.n) return;
     const long t = a.T0 + j;
@@ -89,41 +87,57 @@ __global__ __launch_bounds__(kThreads) void gran_kernel(GranArgs a) {
     const int i0 = a.tile_off[k], ng = a.tile_off[k + 1] - i0;
     const int* idx = a.tile_idx + i0;
     for (int e0 = 0; e0 < ng; e0 += kUnroll) {
-        bool act[kUnroll];
+        bool wv[kUnroll], act[kUnroll];
         unsigned ticks[kUnroll];
         double disp[kUnroll], v0[kUnroll], v1[kUnroll];
-        long tau0[kUnroll], tau1[kUnroll];
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {   // phase 1: indices and gathers of kUnroll grains
             const GrainDev g = a.g[idx[e0 + u < ng ? e0 + u : ng - 1]];   // block-uniform: scalar loads
-            act[u] = e0 + u < ng && t >= g.t_first && t < g.t_end;
+            wv[u] = e0 + u < ng && g.t_first < tw + 64 && g.t_end > tw;   // wave-uniform
+            act[u] = wv[u] && t >= g.t_first && t < g.t_end;
+            disp[u] = 0.0;
+            v0[u] = v1[u] = 0.0;
+            ticks[u] = 0u;
+            if (!wv[u]) continue;
             // inactive lanes use ticks 0: their (discarded) cos stays on the short argument path
             ticks[u] = act[u] ? g.ticks0 + (unsigned)(t - g.t_first) : 0u;
             const double position = g.offsets + (1 - g.speeds) * ticks[u];
             // buffer.h:40-47 with its unsigned wrap; the second tap reads center + 1
             const int center = (int)position;
             disp[u] = position - center;
-            const unsigned x0 = origin - (unsigned)center + size;
-            const unsigned s0 = fastmod(x0, a.fm, size);
-            // x1 = x0 - 1 (mod 2^32), so x1 % size follows from s0 unless x0 wrapped to 0
-            const unsigned s1 = x0 == 0u ? a.wrap1 : (s0 == 0u ? size - 1u : s0 - 1u);
-            tau0[u] = t - (long)(origin >= s0 ? origin - s0 : origin + size - s0);
-            tau1[u] = t - (long)(origin >= s1 ? origin - s1 : origin + size - s1);
-            v0[u] = *src_ptr(a, tau0[u]);
-            v1[u] = *src_ptr(a, tau1[u]);
+            long tau0, tau1;
+            if (center >= 0 && (unsigned)center < size) {   // no uint32 wrap: x0 in [1, 2 size)
+                tau0 = t - center;
+                tau1 = (unsigned)center + 1u < size ? tau0 - 1 : t;
+            } else {
+                const unsigned x0 = origin - (unsigned)center + size;
+                const unsigned s0 = fastmod(x0, a.fm, size);
+                // x1 = x0 - 1 (mod 2^32), so x1 % size follows from s0 unless x0 wrapped to 0
+                const unsigned s1 = x0 == 0u ? a.wrap1 : (s0 == 0u ? size - 1u : s0 - 1u);
+                tau0 = t - (long)(origin >= s0 ? origin - s0 : origin + size - s0);
+                tau1 = t - (long)(origin >= s1 ? origin - s1 : origin + size - s1);
+            }
+            v0[u] = a.ring[tau0 & a.mask];
+            v1[u] = a.ring[tau1 & a.mask];
         }
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {   // phase 2: weights, in voice order
+            if (!wv[u]) continue;
             const GrainDev& g = a.g[idx[e0 + u < ng ? e0 + u : ng - 1]];
-            const double x0 = tau0[u] < 0 ? 0.0 : v0[u], x1 = tau1[u] < 0 ? 0.0 : v1[u];
-            const double src = x0 * (1 - disp[u]) + x1 * disp[u];
-            const double phase = (double)ticks[u] / g.sizes;
+            const double src = v0[u] * (1 - disp[u]) + v1[u] * disp[u];
+            const double tk = (double)ticks[u];
+            double phase;
+            if (g.rsizes != 0.0) {   // tk / sizes: reciprocal product + one residual step (within an ulp)
+                const double q0 = tk * g.rsizes;
+                phase = __builtin_fma(__builtin_fma(-q0, g.sizes, tk), g.rsizes, q0);
+            } else {
+                phase = tk / g.sizes;
+            }
             const double term = g.gains * src * (0.5 * (1 - cos(2 * hz::kPI * phase)));   // wave.h:148
             if (act[u]) out += term;
         }
     }
     a.out[j] = out;
-    a.ring[t & a.mask] = a.in[j];   // no thread of this block reads this slot (C >= size + kChunk)
 }
 
 }  // namespace
@@ -182,6 +196,10 @@ int gran_alloc(hz_gran* h, long t, unsigned ticks0, double offset, double size, 
     g.speeds = speed;
     g.gains = gain;
     g.ticks0 = ticks0;
+    {   // RN(1/sizes) when the reciprocal and the quotients stay normal; else the device divides
+        const double r = 1.0 / g.sizes;
+        g.rsizes = (std::isnormal(r) && std::fabs(g.sizes) < 0x1p+900 && std::fabs(g.sizes) > 0x1p-900) ? r : 0.0;
+    }
     g.t_first = t + 1;
     // last read: the first ticks >= ticks0 with (double)ticks >= sizes
     long m;
@@ -276,8 +294,15 @@ int gran_run(hz_gran* h, const double* d_in, double* d_out, long n, const hz_gra
     const char* ds = (const char*)h->d_g;
     for (long c = 0; c < nchunks; ++c) {
         const long T0 = h->T + c * kChunk, m = std::min(n - c * kChunk, kChunk);
+        {   // the launch's input into the time-indexed ring (slots T0 .. T0 + m - 1 mod C)
+            const long C = h->mask + 1, s0 = T0 & h->mask, first = std::min(m, C - s0);
+            HZ_TRY_HIP(hipMemcpyAsync(h->d_ring + s0, d_in + c * kChunk, sizeof(double) * first,
+                                      hipMemcpyDeviceToDevice, h->stream));
+            if (m > first)
+                HZ_TRY_HIP(hipMemcpyAsync(h->d_ring, d_in + c * kChunk + first, sizeof(double) * (m - first),
+                                          hipMemcpyDeviceToDevice, h->stream));
+        }
         GranArgs a;
-        a.in = d_in + c * kChunk;
         a.out = d_out + c * kChunk;
         a.ring = h->d_ring;
         a.g = (const GrainDev*)ds;
