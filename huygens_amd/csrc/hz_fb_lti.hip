@@ -185,7 +185,10 @@ struct LtiArgs {
     double* xhist_next;     // [O]
     double* partial;        // [G][n_pad] (n_pad = row stride)
     double* gs_out;         // MODE_STATE: [tile][bs_pad][64 chunks] gin x chunk start states
-    int bs_pad;             // band-state rows per tile (lti_bs_rows: every wave's O rows; pad rows written 0)
+    int bs_pad;             // GS rows per tile: band-state rows (lti_bs_rows: every wave's O rows; pad rows
+                            // written 0), then the x-window rows
+    int xr0, xr;            // chunk 128, MODE_STATE: the x-window rows xr0 .. xr0 + xr - 1 of every tile,
+                            // written from the LDS x buffer by one workgroup per tile (xr = 0: none)
     double* segstate;       // [N][nseg_state][O] start states of the (prepass-fine) segments
     long n;                 // samples in this launch (multiple of L)
     long n_pad;             // slab row stride (the tile-padded length)
@@ -516,6 +519,41 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         }
     };
 
+    // chunk 128, MODE_STATE: the GEMM's x-window rows of tile itx while the x buffer holds it
+    // (row r, chunk c = x[t0 - O + c L + r] for r < L + O, else 0: piece c slot r, or piece c + 1
+    // slot r - L), by the staging threads of workgroup (global tile) mod G -- the work of
+    // fb_lti_xrows_kernel without its launch or a second read of x
+    // (this workgroup's tiles are tg = blockIdx.x mod G: the next one is tracked, no division)
+    long xr_next = (seg_t0 / T + (long)gridDim.x - 1 - (long)blockIdx.x) / (long)gridDim.x * (long)gridDim.x +
+                   (long)blockIdx.x;   // first tg >= seg_t0 / T with tg mod G = blockIdx.x
+    auto write_xrows = [&](int itx) {
+        if constexpr (X1 && MODE == MODE_STATE) {
+            constexpr int XRC = (L + O + 31) / 32 * 32;   // = lti_x_rows(L, O)
+            constexpr int B = 5;   // LDS reads of a batch issued together, then their stores
+            constexpr int PER = (XRC * 64 + 64 * WS * B - 1) / (64 * WS * B) * B;   // values per staging thread
+            const long tg = seg_t0 / T + itx;
+            if (a.xr == 0 || itx >= ntiles || tg != xr_next) return;
+            xr_next += gridDim.x;
+            double* g = a.gs_out + (tg * a.bs_pad + a.xr0) * 64;
+#pragma unroll
+            for (int q0 = 0; q0 < PER; q0 += B) {
+                double v[B];
+#pragma unroll
+                for (int q = 0; q < B; ++q) {
+                    const int e = sid + (q0 + q) * 64 * WS;
+                    const int r = e >> 6, c = e & 63;
+                    v[q] = 0.0;
+                    if (r < L + O) v[q] = r < L ? lds[c * (L + 2) + r] : lds[(c + 1) * (L + 2) + (r - L)];
+                }
+#pragma unroll
+                for (int q = 0; q < B; ++q) {
+                    const int e = sid + (q0 + q) * 64 * WS;
+                    if (e < XRC * 64) __builtin_nontemporal_store(v[q], g + e);
+                }
+            }
+        }
+    };
+
     // (E) for tile te: this wave's E blocks -> z buffer (te & 1)
     auto phase_e = [&](int te) {
         if constexpr ((ABL & 1) != 0) return;
@@ -618,6 +656,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                 if ((e % (BSP * kGsRow)) / kGsRow >= W * O) gsb[e] = 0.0;
         }
         __syncthreads();
+        if (!kSplit || wave >= NE) write_xrows(0);
         phase_e(0);
         __syncthreads();
         if constexpr (X1) {
@@ -732,6 +771,7 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
             } else {
                 phase_s(it, t0);
             }
+            if (!kSplit || !isE) write_xrows(it + 1);   // the buffer holds tile it + 1 until the barrier
             stamp(it, 1);
             __syncthreads();
             if (isE) phase_s(it, t0);
@@ -1456,6 +1496,8 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         a.partial = slab_k;
         a.gs_out = h->d_partial;
         a.bs_pad = bs_tot;
+        a.xr0 = bs_pad;
+        a.xr = (gemm && L >= 128) ? XR : 0;   // chunk 128: x rows from the state kernel
         a.segstate = h->d_seg;
         a.n = len;
         a.n_pad = ntiles * T;
@@ -1508,7 +1550,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
             HZ_TRY_HIP(hipMemset2DAsync(h->d_partial + (size_t)gr * 64, sizeof(double) * bs_tot * 64, 0,
                                         sizeof(double) * (bs_pad - gr) * 64, (size_t)ntiles, h->stream));
         }
-        if (gemm) {   // the x-window rows (zero-state term) of every tile
+        if (gemm && a.xr == 0) {   // the x-window rows (zero-state term) of every tile
             const long cnt = ntiles * XR * 64L;
             hipLaunchKernelGGL(pick_xrows(L), dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, h->stream,
                                a.x, off == 0 ? xhist_call : nullptr, O, len, h->d_partial, bs_pad, bs_tot, XR,
