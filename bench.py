@@ -322,8 +322,9 @@ def main():
                          "traffic_detail": traffic_detail,
                          "algorithmic_bytes_per_launch": (16 * S + 120 * cnt) * args.steps / max(1, launches),
                          "launches_per_step": launches / max(1, args.steps),
-                         "kernel": (("LTI engine step: fb_lti_kernel<2,%d,STATE> + fb_lti_xrows_kernel + "
-                                     "fb_lti_gemm_pp_kernel<%d> + fb_lti_sum_kernel (+ segment prepass)" % (chunk, chunk))
+                         "kernel": (("LTI engine step: fb_lti_kernel<2,%d,STATE>%s + "
+                                     "fb_lti_gemm_pp_kernel<%d> + fb_lti_sum_kernel (+ segment prepass)"
+                                     % (chunk, " (+ x rows)" if chunk >= 128 else " + fb_lti_xrows_kernel", chunk))
                                     if lti and chunk >= 64 else
                                     ("LTI engine step: fb_lti_kernel<2,%d,MIX> + fb_lti_reduce_kernel (+ segment "
                                      "prepass)" % chunk) if lti
