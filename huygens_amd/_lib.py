@@ -25,6 +25,11 @@ HZ_E_STATE = -7
 HZ_FB_PATH_AUTO = 0
 HZ_FB_PATH_GENERAL = 1
 HZ_FB_PATH_LTI = 2
+HZ_FB_PATH_RESPONSE = 3
+
+HZ_FB_RESP_OFF = 0
+HZ_FB_RESP_EAGER = 1
+HZ_FB_RESP_LAZY = 2
 
 HZ_DIST_NONE = 0
 HZ_DIST_SOFTCLIP = 1
@@ -90,6 +95,10 @@ _SIGS = {
     "hz_fb_tune_lti": (I, [VP, I, I, I]),
     "hz_fb_lti_plan": (I, [VP, C.POINTER(C.c_long), C.POINTER(C.c_long), C.POINTER(C.c_int)]),
     "hz_fb_lti_last_chunk": (I, [VP, C.POINTER(C.c_int)]),
+    "hz_fb_set_response": (I, [VP, I]),
+    "hz_fb_tune_response": (I, [VP, L, L]),
+    "hz_fb_response_info": (I, [VP, C.POINTER(L), C.POINTER(L), C.POINTER(I), C.POINTER(L)]),
+    "hz_fb_get_response": (I, [VP, PD, L]),
     # Oscbank
     "hz_osc_create": (I, [I, D, I, C.POINTER(VP)]),
     "hz_osc_create_shard": (I, [I, I, I, D, I, C.POINTER(VP)]),

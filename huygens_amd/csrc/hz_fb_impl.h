@@ -133,6 +133,35 @@ struct hz_fb {
     bool tv_pending = false;
     int tv_kind = 0;
     double tv_param = 0;
+    // stationary engine (hz_fb_resp.hip): the bank response h of the converged bank and the last
+    // K inputs, from which the band states follow once the bank has been stationary for K samples
+    struct Resp {
+        int mode = HZ_FB_RESP_EAGER;     // HZ_FB_RESP_OFF / _EAGER / _LAZY
+        long K = -2;                     // horizon (samples, multiple of 4096); -1 none; -2 unknown
+        bool h_valid = false;            // d_h / d_H match F, B, pin, gin
+        long run = 0;                    // converged samples in a row written into the history
+        bool implicit = false;           // LAZY: ystate[scur] not yet materialised from the history
+        long calls = 0;                  // stationary calls made
+        long min_call = 0;               // shortest stationary / history-keeping call (0: 16384)
+        long bands_per_sample = -1;      // cost model: stationary when N n >= this (K + n) (-1: 256)
+        double* d_hist[2] = {nullptr, nullptr};   // [K] last K inputs (ping-pong)
+        size_t hist_cap0 = 0, hist_cap1 = 0;
+        int hcur = 0;
+        double* d_h = nullptr;           // [K] aggregate impulse response
+        size_t h_cap = 0;
+        double* d_hpart = nullptr;       // [64-band groups][K]
+        size_t hpart_cap = 0;
+        double* d_coef = nullptr;        // F [N][O+1], B [N][O]
+        size_t coef_cap = 0;
+        double* d_H = nullptr;           // [Q][F] complex partition spectra
+        size_t H_cap = 0;
+        double* d_Z = nullptr;           // [windows][F] complex window spectra
+        size_t Z_cap = 0;
+        double* d_Y = nullptr;           // [D][F] complex output spectra
+        size_t Y_cap = 0;
+        double* d_tw = nullptr;          // complex twiddles of the F-point transform
+        double* d_zero = nullptr;        // kMaxOrder zeros (x history of the zero-start pass)
+    } resp;
 };
 
 namespace hz_fbi {
@@ -155,5 +184,18 @@ int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* p
                        int target_groups, int max_slices, hipStream_t stream, int* slices_out);
 bool fb_converged(hz_fb* h);
 int fb_launch_lti(hz_fb* h, int geom, const double* d_in, double* d_out, long n);
+long fb_horizon(const hz_fb* h);           // samples K with ||M^K|| < 2^-64 for every band (-1: > 2^18)
+// zero-start band states at the end of x[0, len) (len a multiple of 4096; the O samples before
+// x read as xzero) -> h->d_seg[band][1][O] (the LTI state kernel's prepass mode, chunk 64)
+int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xzero);
+int fb_lti_prepare_end(hz_fb* h);          // its records for the current coefficients
+// hz_fb_resp.hip (stationary engine)
+void fb_resp_init(hz_fb* h);
+void fb_resp_invalidate(hz_fb* h, bool coefficients);   // targets / coefficients changed
+bool fb_resp_eligible(hz_fb* h, long n, bool conv);
+int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n);
+int fb_resp_track(hz_fb* h, const double* d_in, long n, bool conv);  // history after any call
+int fb_resp_materialize(hz_fb* h);                                  // LAZY: band states now
+void fb_resp_free(hz_fb* h);
 
 }  // namespace hz_fbi

@@ -1630,6 +1630,55 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
     return HZ_OK;
 }
 
+long fb_horizon(const hz_fb* h) { return fb_lti_horizon(h); }
+
+int fb_lti_prepare_end(hz_fb* h) { return fb_prepare_lti(h, 2); }
+
+// zero-start band states at the end of x[0, len): the state kernel's prepass mode over one
+// segment (chunk 64, 4096-sample tiles), result in d_seg[band][1] (hz_fb_resp.hip)
+int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xzero) {
+    constexpr int gi = 2;   // chunk 64
+    const int O = h->order;
+    if (O == 0 || len <= 0 || len % (64L * kLtiGeoms[gi].L) != 0) {
+        hz::set_error("fb_lti_zero_start_end: order %d, length %ld (a positive multiple of 4096)", O, len);
+        return HZ_E_INVALID;
+    }
+    HZ_TRY(fb_prepare_lti(h, gi));
+    hz_fb::LtiRecSet& set = h->lti_set[gi];
+    const size_t sneed = (size_t)h->N * 2 * O;
+    if (sneed > h->seg_cap) {
+        HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+        if (h->d_seg) HZ_TRY_HIP(hipFree(h->d_seg));
+        h->d_seg = nullptr;
+        HZ_TRY_HIP(hipMalloc(&h->d_seg, sizeof(double) * sneed));
+        h->seg_cap = sneed;
+    }
+    LtiKernel kend = pick_lti(O, gi, MODE_SEGEND);
+    HZ_TRY(fb_set_lds_attr((const void*)kend));
+    LtiArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.pin = h->d_pin;
+    a.gin = h->d_gin;
+    a.ystate = h->d_ystate[h->scur];
+    a.pgstate = h->d_pg[h->scur];
+    a.x = x;
+    a.xhist = xzero;
+    a.segstate = h->d_seg;
+    a.n = len;
+    a.n_pad = len;
+    a.seg_len = len;
+    a.nseg = 2;          // segment 0 is not the last: its end state goes to segstate[band][1]
+    a.nseg_state = 2;
+    a.seg_stride = 1;
+    a.seg_skip = 0;
+    a.nbands = h->N;
+    const int G = (h->N + lti_waves(O) - 1) / lti_waves(O);
+    hipLaunchKernelGGL(kend, dim3(G, 1), dim3(64 * lti_waves(O)), lti_lds(O, gi, false), h->stream,
+                       (const double*)set.d_rec, a);
+    HZ_TRY_HIP(hipGetLastError());
+    return HZ_OK;
+}
+
 }  // namespace hz_fbi
 
 extern "C" {

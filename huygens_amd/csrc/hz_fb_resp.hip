@@ -1,0 +1,534 @@
+// hz_fb_resp.hip -- the stationary Filterbank<double> engine (bank response convolution).
+//
+// Once a bank has run converged (pre = pin, gain = gin: hz_fb_lti.hip) with unchanged
+// coefficients for K samples, K = its horizon (||M^K||_inf < 2^-64 for every band's state
+// transition M, fb_lti_horizon), every band's state is the zero-state response of the last K
+// input samples to 2^-64 of itself, and the bank's mixdown (src/filterbank.h:130,178-179) is ONE
+// linear filter of the input:
+//     out[t] = sum_n gin_n y_n[t] = sum_{tau < K} h[tau] x[t - tau],   h[tau] = sum_n gin_n r_n[tau]
+// with r_n band n's impulse response at pre = pin_n.  A call then runs as a uniformly partitioned
+// overlap-save convolution on FP64 FFTs (P = 2048-sample partitions, 4096-point transforms):
+//   resp_fwd_kernel   one 4096-point FFT per pair of input windows W_i = u[(i-1)P, (i+1)P) of
+//                     u = [last K inputs | call input]: windows i and i + D share a transform
+//                     (real + i imag; h is real, so their products with H stay separable)
+//   resp_mac_kernel   Y_b = sum_{p < Q} H_p Z_{b+Q-1-p} per bin (Q = K / P partition spectra)
+//   resp_inv_kernel   one inverse FFT per output-block pair: Re -> block b, Im -> block b + D
+// Per output sample that is O(Q + log F) work whatever the number of bands; the bands enter once,
+// through h, when coefficients or targets change (resp_h_kernel: each band's response by the
+// reference's own recurrence, summed in a fixed order).
+//
+// The per-band state is kept exact: the last K inputs are the handle's history (updated by every
+// converged long call, whatever engine ran it), and the band states at the call end are their
+// zero-state response over those K samples (the LTI state kernel in its prepass mode,
+// fb_lti_zero_start_end) -- after every call (HZ_FB_RESP_EAGER, default) or only when a later call,
+// get_state or tick needs them (HZ_FB_RESP_LAZY).
+#include <cstdlib>
+
+#include "hz_fb_impl.h"
+#include "hz_fft.h"
+
+namespace {
+
+constexpr int kLgP = 11, kP = 1 << kLgP;       // partition / output block (samples)
+constexpr int kLgF = kLgP + 1, kF = 2 * kP;    // transform size
+constexpr int kRmax = 3;                       // radix-8 passes (hz_fft.h)
+constexpr int kFftThreads = kF >> kRmax;       // 512: one radix-8 group per thread
+constexpr int kMacR = 16;                      // output blocks per MAC thread
+constexpr long kMinCall = 16384;               // shortest call that keeps the history
+
+size_t fft_lds() { return sizeof(double) * 2 * (size_t)hz::padded_len(kF) + sizeof(double2) * hz::twc_len(kLgF); }
+
+// Aggregate impulse response, one wave (64 bands) per workgroup: part[g][tau] = sum over the
+// group's bands of gin_n r_n[tau], r_n = band n's response to a unit impulse with pre = pin_n,
+// by the recurrence of filterbank.h:178-179 (oracle order: ff = F[0] x[t] + ... ; y = ff pre -
+// sum_k B[k] y[t-1-k]); lanes = bands, 64-sample tiles summed through LDS in band order.
+template <int O>
+__global__ __launch_bounds__(64) void resp_h_kernel(const double* __restrict__ F, const double* __restrict__ B,
+                                                    const double* __restrict__ pin, const double* __restrict__ gin,
+                                                    int nbands, long K, double* __restrict__ part) {
+#pragma clang fp contract(off)
+    __shared__ double s[64][65];
+    const int lane = threadIdx.x;
+    const int band = blockIdx.x * 64 + lane;
+    const bool live = band < nbands;
+    double f[O + 1], b[O], y[O];
+#pragma unroll
+    for (int i = 0; i <= O; ++i) f[i] = live ? F[(long)band * (O + 1) + i] : 0.0;
+#pragma unroll
+    for (int k = 0; k < O; ++k) {
+        b[k] = live ? B[(long)band * O + k] : 0.0;
+        y[k] = 0.0;   // y[k] = r[t - 1 - k]
+    }
+    const double p = live ? pin[band] : 0.0, g = live ? gin[band] : 0.0;
+    for (long t0 = 0; t0 < K; t0 += 64) {
+        for (int j = 0; j < 64; ++j) {
+            const long t = t0 + j;
+            double ff = 0.0;   // sum_i F[i] delta[t - i] = F[t] for t <= O
+#pragma unroll
+            for (int i = 0; i <= O; ++i)
+                if (t == i) ff = f[i];
+            double bs = 0.0;
+#pragma unroll
+            for (int k = 0; k < O; ++k) bs += b[k] * y[k];
+            const double yt = ff * p - bs;
+#pragma unroll
+            for (int k = O - 1; k >= 1; --k) y[k] = y[k - 1];
+            y[0] = yt;
+            s[j][lane] = g * yt;
+        }
+        __syncthreads();
+        double acc = 0.0;
+        for (int q = 0; q < 64; ++q) acc += s[lane][q];
+        if (t0 + lane < K) part[(long)blockIdx.x * K + t0 + lane] = acc;
+        __syncthreads();
+    }
+}
+
+// h[tau] = sum_g part[g][tau] (fixed order)
+__global__ __launch_bounds__(256) void resp_hsum_kernel(const double* __restrict__ part, int G, long K,
+                                                        double* __restrict__ h) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= K) return;
+    double acc = 0.0;
+    for (int g = 0; g < G; ++g) acc += part[(long)g * K + t];
+    h[t] = acc;
+}
+
+__device__ __forceinline__ void load_tw(double2* T, const double2* __restrict__ tw) {
+    for (int k = threadIdx.x; k < hz::twc_len(kLgF); k += blockDim.x) T[k] = tw[k];
+}
+
+// Partition spectra H_p = FFT(h[pP, (p+1)P) zero-padded to F) / F (the inverse is unnormalised;
+// 1/F is a power of two), bins in the transforms' storage (bit-reversed) order
+__global__ __launch_bounds__(kFftThreads) void resp_hspec_kernel(const double* __restrict__ h, long K,
+                                                                 const double2* __restrict__ tw,
+                                                                 double2* __restrict__ H) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* re = lds;
+    double* im = lds + hz::padded_len(kF);
+    double2* T = (double2*)(im + hz::padded_len(kF));
+    load_tw(T, tw);
+    const long p0 = (long)blockIdx.x * kP;
+    for (int k = threadIdx.x; k < kF; k += blockDim.x) {
+        re[hz::pad16(k)] = (k < kP && p0 + k < K) ? h[p0 + k] * (1.0 / kF) : 0.0;
+        im[hz::pad16(k)] = 0.0;
+    }
+    __syncthreads();
+    hz::fft_fwd_lead<kRmax>(re, im, kLgF, T, true);
+    double2* o = H + (long)blockIdx.x * kF;
+    for (int q = threadIdx.x; q < kF; q += blockDim.x) o[q] = make_double2(re[hz::pad16(q)], im[hz::pad16(q)]);
+}
+
+struct RespArgs {
+    const double* hist;   // [K] the K inputs before the call
+    const double* x;      // [n] the call's input
+    long K, n;
+    int Q, D;             // partitions; packed output-block pairs
+    const double2* tw;
+    double2* Z;           // [Q + D - 1 (+ pad)][F] packed window spectra
+    const double2* Y;     // [D][F] packed output spectra
+    double* out;          // [n]
+};
+
+// u = [hist | x | 0 ...]
+__device__ __forceinline__ double resp_u(const RespArgs& a, long m) {
+    if (m < a.K) return a.hist[m];
+    m -= a.K;
+    return m < a.n ? a.x[m] : 0.0;
+}
+
+// Z_j = FFT(W_{j+1} + i W_{j+1+D}), W_i = u[(i-1)P, (i+1)P)
+__global__ __launch_bounds__(kFftThreads) void resp_fwd_kernel(RespArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* re = lds;
+    double* im = lds + hz::padded_len(kF);
+    double2* T = (double2*)(im + hz::padded_len(kF));
+    load_tw(T, a.tw);
+    const long j = blockIdx.x;
+    const long m0 = j * kP, m1 = (j + a.D) * kP;
+    for (int k = threadIdx.x; k < kF; k += blockDim.x) {
+        re[hz::pad16(k)] = resp_u(a, m0 + k);
+        im[hz::pad16(k)] = resp_u(a, m1 + k);
+    }
+    __syncthreads();
+    hz::fft_fwd_lead<kRmax>(re, im, kLgF, T, true);
+    double2* z = a.Z + j * kF;
+    for (int q = threadIdx.x; q < kF; q += blockDim.x) z[q] = make_double2(re[hz::pad16(q)], im[hz::pad16(q)]);
+}
+
+// Y_b[q] = sum_{p < Q} H_p[q] Z_{b+Q-1-p}[q] for b in [b0, b0 + R): thread = bin q x R output
+// blocks.  The R Z values of step p sit in a register ring (element r in slot (r - p) mod R): each
+// step loads one new Z value and one H value for R complex FMAs.
+template <int R>
+__global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict__ H, const double2* __restrict__ Z,
+                                                       double2* __restrict__ Y, int Q, int D) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;   // bin (grid.x = F / 256)
+    const int b0 = blockIdx.y * R;
+    double ar[R], ai[R], zr[R], zi[R];
+    const long base = (long)b0 + Q - 1;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        ar[r] = ai[r] = 0.0;
+        const double2 z = Z[(base + r) * kF + q];
+        zr[r] = z.x;
+        zi[r] = z.y;
+    }
+    for (int p0 = 0; p0 < Q; p0 += R) {
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const int p = p0 + u;
+            if (p >= Q) break;
+            const double2 hv = H[(long)p * kF + q];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int sl = ((r - u) % R + R) % R;
+                ar[r] = fma(hv.x, zr[sl], ar[r]);
+                ar[r] = fma(-hv.y, zi[sl], ar[r]);
+                ai[r] = fma(hv.x, zi[sl], ai[r]);
+                ai[r] = fma(hv.y, zr[sl], ai[r]);
+            }
+            if (p + 1 < Q) {   // element 0 of step p + 1: Z[base - p - 1] into the slot element R - 1 leaves
+                const int sl = ((-(u + 1)) % R + R) % R;
+                const double2 z = Z[(base - p - 1) * kF + q];
+                zr[sl] = z.x;
+                zi[sl] = z.y;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (b0 + r < D) Y[(long)(b0 + r) * kF + q] = make_double2(ar[r], ai[r]);
+}
+
+// out[bP + r] = Re IFFT(Y_b)[P + r], out[(b + D)P + r] = Im ...
+__global__ __launch_bounds__(kFftThreads) void resp_inv_kernel(RespArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* re = lds;
+    double* im = lds + hz::padded_len(kF);
+    double2* T = (double2*)(im + hz::padded_len(kF));
+    load_tw(T, a.tw);
+    const long b = blockIdx.x;
+    const double2* y = a.Y + b * kF;
+    for (int q = threadIdx.x; q < kF; q += blockDim.x) {
+        const double2 v = y[q];
+        re[hz::pad16(q)] = v.x;
+        im[hz::pad16(q)] = v.y;
+    }
+    __syncthreads();
+    hz::fft_inv_tail<kRmax>(re, im, kLgF, T, true);
+    for (int r = threadIdx.x; r < kP; r += blockDim.x) {
+        const long t0 = b * kP + r, t1 = (b + a.D) * kP + r;
+        if (t0 < a.n) a.out[t0] = re[hz::pad16(kP + r)];
+        if (t1 < a.n) a.out[t1] = im[hz::pad16(kP + r)];
+    }
+}
+
+// history after a call: the last K samples of [hist | x]
+__global__ __launch_bounds__(256) void resp_hist_kernel(const double* __restrict__ hist, const double* __restrict__ x,
+                                                        long K, long n, double* __restrict__ hist_next) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= K) return;
+    const long m = n + i;
+    hist_next[i] = m < K ? hist[m] : x[m - K];
+}
+
+// end of a stationary call: band states (the zero-start pass over the history, seg[band][1]),
+// the smoothers' closed form, the x history (the last O inputs)
+__global__ __launch_bounds__(256) void resp_finish_kernel(const double* __restrict__ seg, double* __restrict__ ystate,
+                                                          const double* __restrict__ pg, double* __restrict__ pg_next,
+                                                          const double* __restrict__ pin,
+                                                          const double* __restrict__ gin, double sp_n, double sg_n,
+                                                          const double* __restrict__ hist, long K,
+                                                          double* __restrict__ xhist_next, int N, int O, int copy_y) {
+    const int band = blockIdx.x * blockDim.x + threadIdx.x;
+    if (band < N) {
+        if (copy_y)
+            for (int k = 0; k < O; ++k) ystate[(long)band * O + k] = seg[((long)band * 2 + 1) * O + k];
+        if (pg_next) {
+            const double P0 = pg[2 * (long)band], G0 = pg[2 * (long)band + 1];
+            const double pb = pin[band], gb = gin[band];
+            pg_next[2 * (long)band] = pb + sp_n * (P0 - pb);
+            pg_next[2 * (long)band + 1] = gb + sg_n * (G0 - gb);
+        }
+    }
+    if (xhist_next && band < O) xhist_next[band] = hist[K - 1 - band];
+}
+
+typedef void (*RespHKernel)(const double*, const double*, const double*, const double*, int, long, double*);
+RespHKernel pick_h(int O) {
+    switch (O) {
+    case 1: return resp_h_kernel<1>;
+    case 2: return resp_h_kernel<2>;
+    case 3: return resp_h_kernel<3>;
+    default: return resp_h_kernel<4>;
+    }
+}
+
+int resp_alloc(double** p, size_t* cap, size_t need) {
+    if (need <= *cap) return HZ_OK;
+    if (*p) HZ_TRY_HIP(hipFree(*p));
+    *p = nullptr;
+    HZ_TRY_HIP(hipMalloc(p, need * sizeof(double)));
+    *cap = need;
+    return HZ_OK;
+}
+
+// per-bank setup: horizon, history buffers, twiddles
+int resp_setup(hz_fb* h) {
+    hz_fb::Resp& R = h->resp;
+    if (R.K == -2) {
+        R.K = hz_fbi::fb_horizon(h);
+        if (R.K >= 0) R.K = std::max<long>(R.K, kP);   // (a multiple of 4096, so of P)
+        R.h_valid = false;
+        R.run = 0;
+    }
+    if (R.K <= 0) return HZ_OK;
+    HZ_TRY(resp_alloc(&R.d_hist[0], &R.hist_cap0, (size_t)R.K));
+    HZ_TRY(resp_alloc(&R.d_hist[1], &R.hist_cap1, (size_t)R.K));
+    if (!R.d_tw) {
+        std::vector<double2> tw(kF / 2);
+        const long double pi = acosl(-1.0L);
+        for (int k = 0; k < kF / 2; ++k) {
+            const long double ang = -2.0L * pi * k / kF;
+            tw[k] = make_double2((double)cosl(ang), (double)sinl(ang));
+        }
+        HZ_TRY_HIP(hipMalloc((void**)&R.d_tw, sizeof(double2) * tw.size()));
+        HZ_TRY_HIP(hipMemcpy(R.d_tw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice));
+        HZ_TRY_HIP(hipMalloc(&R.d_zero, sizeof(double) * hz_fbi::kMaxOrder));
+        HZ_TRY_HIP(hipMemset(R.d_zero, 0, sizeof(double) * hz_fbi::kMaxOrder));
+        for (const void* k : {(const void*)resp_hspec_kernel, (const void*)resp_fwd_kernel, (const void*)resp_inv_kernel})
+            HZ_TRY(hz_fbi::fb_set_lds_attr(k));
+    }
+    return HZ_OK;
+}
+
+// h and its partition spectra for the current coefficients / targets
+int resp_build_h(hz_fb* h) {
+    hz_fb::Resp& R = h->resp;
+    if (R.h_valid) return HZ_OK;
+    const int O = h->order, N = h->N;
+    const long K = R.K;
+    const int G = (N + 63) / 64;
+    const int Q = (int)(K / kP);
+    HZ_TRY(resp_alloc(&R.d_coef, &R.coef_cap, (size_t)N * (2 * O + 1)));
+    HZ_TRY_HIP(hipMemcpyAsync(R.d_coef, h->F.data(), sizeof(double) * N * (O + 1), hipMemcpyHostToDevice, h->stream));
+    HZ_TRY_HIP(hipMemcpyAsync(R.d_coef + (size_t)N * (O + 1), h->B.data(), sizeof(double) * N * O,
+                              hipMemcpyHostToDevice, h->stream));
+    HZ_TRY(resp_alloc(&R.d_hpart, &R.hpart_cap, (size_t)G * K));
+    HZ_TRY(resp_alloc(&R.d_h, &R.h_cap, (size_t)K));
+    HZ_TRY(resp_alloc(&R.d_H, &R.H_cap, (size_t)2 * Q * kF));
+    hipLaunchKernelGGL(pick_h(O), dim3(G), dim3(64), 0, h->stream, (const double*)R.d_coef,
+                       (const double*)(R.d_coef + (size_t)N * (O + 1)), (const double*)h->d_pin,
+                       (const double*)h->d_gin, N, K, R.d_hpart);
+    HZ_TRY_HIP(hipGetLastError());
+    hipLaunchKernelGGL(resp_hsum_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, h->stream,
+                       (const double*)R.d_hpart, G, K, R.d_h);
+    HZ_TRY_HIP(hipGetLastError());
+    hipLaunchKernelGGL(resp_hspec_kernel, dim3((unsigned)Q), dim3(kFftThreads), fft_lds(), h->stream,
+                       (const double*)R.d_h, K, (const double2*)R.d_tw, (double2*)R.d_H);
+    HZ_TRY_HIP(hipGetLastError());
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));   // pageable coefficient sources
+    R.h_valid = true;
+    return HZ_OK;
+}
+
+// zero-start band states over the history's K samples -> ystate[cur] (LAZY: on demand)
+int resp_states(hz_fb* h, double* ystate, double* pg, double* pg_next, double* xhist_next, long n_adv) {
+    hz_fb::Resp& R = h->resp;
+    const double* hist = R.d_hist[R.hcur];
+    if (ystate) HZ_TRY(hz_fbi::fb_lti_zero_start_end(h, hist, R.K, R.d_zero));
+    const double spn = (double)powl((long double)h->sp, (long double)n_adv);
+    const double sgn = (double)powl((long double)h->sg, (long double)n_adv);
+    hipLaunchKernelGGL(resp_finish_kernel, dim3((unsigned)((std::max(h->N, h->order) + 255) / 256)), dim3(256), 0,
+                       h->stream, (const double*)h->d_seg, ystate, (const double*)pg, pg_next,
+                       (const double*)h->d_pin, (const double*)h->d_gin, spn, sgn, hist, R.K, xhist_next, h->N,
+                       h->order, ystate ? 1 : 0);
+    HZ_TRY_HIP(hipGetLastError());
+    return HZ_OK;
+}
+
+long resp_min_call(const hz_fb* h) { return h->resp.min_call > 0 ? h->resp.min_call : kMinCall; }
+
+int resp_mode_default() {
+    static const int m = [] {
+        const char* e = std::getenv("HZ_FB_RESP");   // 0 off, 1 eager (default), 2 lazy
+        const int v = e ? std::atoi(e) : HZ_FB_RESP_EAGER;
+        return v >= HZ_FB_RESP_OFF && v <= HZ_FB_RESP_LAZY ? v : HZ_FB_RESP_EAGER;
+    }();
+    return m;
+}
+
+}  // namespace
+
+namespace hz_fbi {
+
+void fb_resp_init(hz_fb* h) { h->resp.mode = resp_mode_default(); }
+
+void fb_resp_invalidate(hz_fb* h, bool coefficients) {
+    h->resp.run = 0;
+    h->resp.h_valid = false;
+    if (coefficients) h->resp.K = -2;
+}
+
+bool fb_resp_eligible(hz_fb* h, long n, bool conv) {
+    hz_fb::Resp& R = h->resp;
+    if (R.mode == HZ_FB_RESP_OFF || !conv || h->order == 0 || h->dist_id != HZ_DIST_NONE ||
+        h->path_mode != HZ_FB_PATH_AUTO || n < resp_min_call(h))
+        return false;
+    if (R.K == -2 && resp_setup(h) != HZ_OK) return false;
+    if (R.K <= 0 || R.run < R.K) return false;
+    // the bank engines cost ~N per sample, this one ~(K + n) / n (Q MACs + two FFT passes per
+    // sample): measured crossover near 300 band-equivalents per sample of history + call
+    static const long per_env = std::getenv("HZ_FB_RESP_BANDS") ? std::atol(std::getenv("HZ_FB_RESP_BANDS")) : 256;
+    const long per = R.bands_per_sample >= 0 ? R.bands_per_sample : per_env;
+    return (double)h->N * n >= (double)per * (double)(R.K + n);
+}
+
+int fb_resp_materialize(hz_fb* h) {
+    hz_fb::Resp& R = h->resp;
+    if (!R.implicit) return HZ_OK;
+    HZ_TRY(resp_states(h, h->d_ystate[h->scur], nullptr, nullptr, nullptr, 0));
+    R.implicit = false;
+    return HZ_OK;
+}
+
+// after a call on any engine: the history keeps the last K inputs while the bank stays converged
+int fb_resp_track(hz_fb* h, const double* d_in, long n, bool conv) {
+    hz_fb::Resp& R = h->resp;
+    if (R.mode == HZ_FB_RESP_OFF || !conv || h->order == 0 || n < resp_min_call(h)) {
+        R.run = 0;
+        return HZ_OK;
+    }
+    if (R.K == -2) HZ_TRY(resp_setup(h));
+    if (R.K <= 0) {
+        R.run = 0;
+        return HZ_OK;
+    }
+    HZ_TRY(resp_setup(h));
+    hipLaunchKernelGGL(resp_hist_kernel, dim3((unsigned)((R.K + 255) / 256)), dim3(256), 0, h->stream,
+                       (const double*)R.d_hist[R.hcur], d_in, R.K, n, R.d_hist[R.hcur ^ 1]);
+    HZ_TRY_HIP(hipGetLastError());
+    R.hcur ^= 1;
+    R.run = std::min(R.run + n, 1L << 60);
+    return HZ_OK;
+}
+
+// a stationary call (fb_resp_eligible): output, history, end state
+int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
+    hz_fb::Resp& R = h->resp;
+    HZ_TRY(resp_setup(h));
+    HZ_TRY(resp_build_h(h));
+    const long K = R.K;
+    const int Q = (int)(K / kP);
+    const long B = (n + kP - 1) / kP;
+    const int D = (int)((B + 1) / 2);
+    const int nz = Q + D - 1;
+    const int zrows = (D + kMacR - 1) / kMacR * kMacR + Q;   // the MAC's last register window
+    if ((size_t)zrows * kF * 2 > R.Z_cap) {
+        HZ_TRY(resp_alloc(&R.d_Z, &R.Z_cap, (size_t)zrows * kF * 2));
+        HZ_TRY_HIP(hipMemsetAsync(R.d_Z, 0, sizeof(double2) * (size_t)zrows * kF, h->stream));
+    }
+    HZ_TRY(resp_alloc(&R.d_Y, &R.Y_cap, (size_t)D * kF * 2));
+    hipEvent_t* e = nullptr;
+    if (h->prof) {
+        HZ_TRY(fb_prof_events(h, &e));
+        HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
+        h->ev_skip[(e - h->ev.data()) / 5] |= 2;   // no segment phase
+    }
+    RespArgs a;
+    a.hist = R.d_hist[R.hcur];
+    a.x = d_in;
+    a.K = K;
+    a.n = n;
+    a.Q = Q;
+    a.D = D;
+    a.tw = (const double2*)R.d_tw;
+    a.Z = (double2*)R.d_Z;
+    a.Y = (const double2*)R.d_Y;
+    a.out = d_out;
+    hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kFftThreads), fft_lds(), h->stream, a);
+    HZ_TRY_HIP(hipGetLastError());
+    hipLaunchKernelGGL(resp_mac_kernel<kMacR>, dim3(kF / 256, (unsigned)((D + kMacR - 1) / kMacR)), dim3(256), 0,
+                       h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, D);
+    HZ_TRY_HIP(hipGetLastError());
+    hipLaunchKernelGGL(resp_inv_kernel, dim3((unsigned)D), dim3(kFftThreads), fft_lds(), h->stream, a);
+    HZ_TRY_HIP(hipGetLastError());
+    if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
+    if (e) h->ev_skip[(e - h->ev.data()) / 5] |= 8;
+    HZ_TRY(fb_resp_track(h, d_in, n, true));
+    // end state: bands (EAGER) or marked implicit (LAZY); smoothers and x history always
+    const bool lazy = R.mode == HZ_FB_RESP_LAZY;
+    if (lazy) HZ_TRY(fb_lti_prepare_end(h));   // records of these coefficients for a later materialisation
+    HZ_TRY(resp_states(h, lazy ? nullptr : h->d_ystate[h->scur ^ 1], h->d_pg[h->scur], h->d_pg[h->scur ^ 1],
+                       h->d_xhist[h->xcur ^ 1], n));
+    R.implicit = lazy;
+    if (e) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
+    h->scur ^= 1;
+    h->xcur ^= 1;
+    h->prof_launches += h->prof ? 1 : 0;
+    ++R.calls;
+    fb_mirror_advance(h, n);
+    return HZ_OK;
+}
+
+void fb_resp_free(hz_fb* h) {
+    hz_fb::Resp& R = h->resp;
+    for (double* p : {R.d_hist[0], R.d_hist[1], R.d_h, R.d_hpart, R.d_coef, R.d_zero, R.d_H, R.d_Z, R.d_Y, R.d_tw})
+        if (p) (void)hipFree(p);
+    R = hz_fb::Resp();
+}
+
+}  // namespace hz_fbi
+
+extern "C" {
+
+int hz_fb_set_response(hz_fb* h, int mode) {
+    if (!h || mode < HZ_FB_RESP_OFF || mode > HZ_FB_RESP_LAZY) {
+        hz::set_error("hz_fb_set_response: mode must be HZ_FB_RESP_OFF, _EAGER or _LAZY");
+        return HZ_E_INVALID;
+    }
+    HZ_TRY_HIP(hipSetDevice(h->device));
+    HZ_TRY(hz_fbi::fb_resp_materialize(h));
+    h->resp.mode = mode;
+    if (mode == HZ_FB_RESP_OFF) h->resp.run = 0;
+    return HZ_OK;
+}
+
+int hz_fb_tune_response(hz_fb* h, long min_call, long bands_per_sample) {
+    if (!h || min_call < 0 || bands_per_sample < 0) return HZ_E_INVALID;
+    h->resp.min_call = min_call;                                   // 0: 16384
+    h->resp.bands_per_sample = bands_per_sample ? bands_per_sample : -1;   // 0: 256 (HZ_FB_RESP_BANDS)
+    return HZ_OK;
+}
+
+int hz_fb_response_info(hz_fb* h, long* horizon, long* run, int* implicit_state, long* calls) {
+    if (!h) return HZ_E_INVALID;
+    if (horizon) *horizon = h->resp.K;
+    if (run) *run = h->resp.run;
+    if (implicit_state) *implicit_state = h->resp.implicit ? 1 : 0;
+    if (calls) *calls = h->resp.calls;
+    return HZ_OK;
+}
+
+int hz_fb_get_response(hz_fb* h, double* out, long count) {
+    if (!h || !out || count < 0) return HZ_E_INVALID;
+    HZ_TRY_HIP(hipSetDevice(h->device));
+    HZ_TRY(hz_fbi::fb_upload_staged(h));
+    if (h->order == 0) {
+        hz::set_error("hz_fb_get_response: order 0 bank");
+        return HZ_E_INVALID;
+    }
+    HZ_TRY(resp_setup(h));
+    if (h->resp.K <= 0) {
+        hz::set_error("hz_fb_get_response: no finite horizon (some band needs more than 2^18 samples)");
+        return HZ_E_UNSUPPORTED;
+    }
+    HZ_TRY(resp_build_h(h));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    const long c = std::min(count, h->resp.K);
+    HZ_TRY_HIP(hipMemcpy(out, h->resp.d_h, sizeof(double) * c, hipMemcpyDeviceToHost));
+    for (long i = c; i < count; ++i) out[i] = 0.0;
+    return HZ_OK;
+}
+
+}  // extern "C"

@@ -440,6 +440,8 @@ int hz_fb_process_tv_device(hz_fb* h, const double* d_in, double* d_out, size_t 
     const int up = hz_fbi::fb_upload_staged(h);
     h->dirty_coef = dirty_coef;
     HZ_TRY(up);
+    HZ_TRY(hz_fbi::fb_resp_materialize(h));   // the stream kernel reads the band states
+    hz_fbi::fb_resp_invalidate(h, true);      // and leaves other coefficients behind
     const long N = h->N, G = (N + kThreads - 1) / kThreads;
     const long chunk = std::max(1L, std::min(1L << 20, kPartBytes / (long)sizeof(double) / G));
     const long row = kind == HZ_FB_TV_COEFFS ? (2 * O + 1) * N : N;

@@ -647,6 +647,9 @@ int fb_groups(const hz_fb* h) {
 
 int fb_upload(hz_fb* h) {
     bool uploaded = false;
+    // LAZY band states of a stationary call follow from the coefficients and pre-amps it ran
+    // with: materialise them before new ones reach the device
+    if (h->resp.implicit && (h->dirty_coef || h->dirty_pin || h->tv_pending)) HZ_TRY(hz_fbi::fb_resp_materialize(h));
     HZ_TRY(hz_fbi::fb_tv_materialize(h));
     if (h->dirty_coef) {
         const int O = h->order;
@@ -661,10 +664,13 @@ int fb_upload(hz_fb* h) {
             st.dirty = true;
             st.fmix_valid = false;
         }
+        hz_fbi::fb_resp_invalidate(h, true);
         uploaded = true;
     }
-    if (h->dirty_pin || h->dirty_gin)
+    if (h->dirty_pin || h->dirty_gin) {
         for (auto& st : h->lti_set) st.fmix_valid = false;
+        hz_fbi::fb_resp_invalidate(h, false);
+    }
     if (h->dirty_pin) {
         HZ_TRY_HIP(hipMemcpyAsync(h->d_pin, h->pin.data(), sizeof(double) * h->N, hipMemcpyHostToDevice,
                                   h->stream));
@@ -864,13 +870,23 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
     const int geom = fb_lti_geom(h, n);
     const int L = fb_lti_chunk(geom);
     const long n_lti = n - n % L;
-    if (h->path_mode == HZ_FB_PATH_AUTO && h->order > 0 && h->dist_id == HZ_DIST_NONE && n_lti > 0 &&
-        fb_converged(h)) {
+    // converged for the whole call (the smoothers only get closer): the LTI engine may run, and
+    // the stationary engine's history keeps counting
+    const bool conv = h->order > 0 && n >= 16 && fb_converged(h);
+    if (fb_resp_eligible(h, n, conv)) {
+        HZ_TRY(fb_launch_resp(h, d_in, d_out, n));
+        h->last_path = HZ_FB_PATH_RESPONSE;
+        return HZ_OK;
+    }
+    HZ_TRY(fb_resp_materialize(h));   // LAZY band states of an earlier stationary call
+    if (h->path_mode == HZ_FB_PATH_AUTO && h->dist_id == HZ_DIST_NONE && n_lti > 0 && conv) {
         HZ_TRY(fb_launch_lti(h, geom, d_in, d_out, n_lti));
         h->last_path = HZ_FB_PATH_LTI;
-        return fb_launch_general(h, d_in + n_lti, d_out + n_lti, n - n_lti);
+        HZ_TRY(fb_launch_general(h, d_in + n_lti, d_out + n_lti, n - n_lti));
+    } else {
+        HZ_TRY(fb_launch_general(h, d_in, d_out, n));
     }
-    return fb_launch_general(h, d_in, d_out, n);
+    return fb_resp_track(h, d_in, n, conv);
 }
 
 int fb_check(hz_fb* h) {
@@ -918,6 +934,7 @@ int hz_fb_create_shard(int order, int N_total, int band_begin, int band_count, d
     h->pin.assign(N, 0.0);
     h->gin.assign(N, 0.0);
     h->pg_host.assign(2 * N, 0.0);
+    hz_fbi::fb_resp_init(h);
     // default geometry: 16 waves x 1 band; fewer waves when the bank is small
     h->waves = 16;
     h->bands_per_wave = 1;
@@ -985,6 +1002,7 @@ int hz_fb_destroy(hz_fb* h) {
     if (h->d_xhist_red) (void)hipFree(h->d_xhist_red);
     if (h->tv_row) (void)hipHostFree(h->tv_row);
     if (h->tv_ev) (void)hipEventDestroy(h->tv_ev);
+    hz_fbi::fb_resp_free(h);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return HZ_OK;
@@ -1156,6 +1174,7 @@ int hz_fb_get_state(hz_fb* h, double* buf, size_t count) {
     hz_fb_state_size(h, &need);
     if (!buf || count < need) return HZ_E_INVALID;
     const size_t O = h->order, N = h->N;
+    HZ_TRY(hz_fbi::fb_resp_materialize(h));
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
     if (O) {
         HZ_TRY_HIP(hipMemcpy(buf, h->d_xhist[h->xcur], sizeof(double) * O, hipMemcpyDeviceToHost));
@@ -1181,6 +1200,8 @@ int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
     h->mirror_pending = 0;
     h->converged = false;
     h->spare_ok = false;
+    h->resp.implicit = false;   // overwritten
+    h->resp.run = 0;
     return HZ_OK;
 }
 
@@ -1193,6 +1214,8 @@ int hz_fb_tick(hz_fb* h) {
                       "it would reuse (O+1 samples back) is not kept");
         return HZ_E_STATE;
     }
+    HZ_TRY(hz_fbi::fb_resp_materialize(h));
+    h->resp.run = 0;   // the rotation reuses a stale row: no longer the response of the inputs
     const int N = h->N;
     hipLaunchKernelGGL(fb_tick_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, h->stream,
                        (const double*)h->d_ystate[h->scur], h->d_ystate[h->scur ^ 1], (const double*)h->d_pg[h->scur],

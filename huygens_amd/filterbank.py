@@ -192,3 +192,26 @@ class Filterbank:
 
     def set_target_groups(self, groups: int):
         check(self._lib.hz_fb_set_target_groups(self._h, groups))
+
+    # ---- stationary engine (hz_fb_resp.hip) ---------------------------------
+    def set_response(self, mode: int):
+        """HZ_FB_RESP_OFF (per-band engines only), _EAGER (default: band states computed after
+        every stationary call) or _LAZY (band states computed when next needed)."""
+        check(self._lib.hz_fb_set_response(self._h, int(mode)))
+
+    def tune_response(self, min_call: int = 0, bands_per_sample: int = 0):
+        """(tuning) shortest stationary call and the cost-model threshold (0s = defaults)."""
+        check(self._lib.hz_fb_tune_response(self._h, int(min_call), int(bands_per_sample)))
+
+    def response_info(self):
+        """-> (horizon K, stationary samples so far, band states implicit, stationary calls)"""
+        k, r, i, c = C.c_long(), C.c_long(), C.c_int(), C.c_long()
+        check(self._lib.hz_fb_response_info(self._h, C.byref(k), C.byref(r), C.byref(i), C.byref(c)))
+        return k.value, r.value, bool(i.value), c.value
+
+    def response(self, count: int) -> np.ndarray:
+        """The converged bank's response h[0 .. count): sum_n gin_n (impulse response of band n
+        at pre = pin_n), truncated at the horizon."""
+        out = np.zeros(count)
+        check(self._lib.hz_fb_get_response(self._h, dptr(out), count))
+        return out

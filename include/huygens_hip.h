@@ -112,8 +112,30 @@ int hz_fb_set_target_groups(hz_fb* h, int groups);
 #define HZ_FB_PATH_AUTO 0
 #define HZ_FB_PATH_GENERAL 1
 #define HZ_FB_PATH_LTI 2
+#define HZ_FB_PATH_RESPONSE 3
 int hz_fb_set_path(hz_fb* h, int path);
 int hz_fb_last_path(hz_fb* h, int* path);
+/* Stationary engine (HZ_FB_PATH_RESPONSE, hz_fb_resp.hip).  Once the bank has run converged
+ * (as for the LTI engine) with unchanged coefficients and targets for K samples -- K = its
+ * horizon, the first multiple of 4096 with ||M^K||_inf < 2^-64 for every band's state transition
+ * M (src/filterbank.h:178-179) -- the mixdown of a long call (>= 16384 samples) is one linear
+ * filter of the input, out = h * x with h = sum_n gin_n (band n's impulse response at pre = pin_n),
+ * truncated at K, and runs as a partitioned FFT convolution.  The band states at the call end are
+ * the zero-start response of the last K inputs: computed after every call (HZ_FB_RESP_EAGER,
+ * default) or when a later call / get_state / tick needs them (HZ_FB_RESP_LAZY).
+ * HZ_FB_RESP_OFF keeps the per-band engines.  Env HZ_FB_RESP=0/1/2 sets the default. */
+#define HZ_FB_RESP_OFF 0
+#define HZ_FB_RESP_EAGER 1
+#define HZ_FB_RESP_LAZY 2
+int hz_fb_set_response(hz_fb* h, int mode);
+/* (tuning) shortest call that runs stationary and keeps the history (0: 16384); the engine is
+ * chosen when N n >= bands_per_sample (K + n) (0: 256, env HZ_FB_RESP_BANDS) */
+int hz_fb_tune_response(hz_fb* h, long min_call, long bands_per_sample);
+/* horizon K (-1: none within 2^18 samples, -2: not computed), stationary samples so far,
+ * whether the band states are implicit (LAZY), stationary calls made */
+int hz_fb_response_info(hz_fb* h, long* horizon, long* run, int* implicit_state, long* calls);
+/* the bank response h[0 .. count) (zero past the horizon); HZ_E_UNSUPPORTED without a horizon */
+int hz_fb_get_response(hz_fb* h, double* out, long count);
 /* LTI engine geometry: (chunk length, bands per wave, waves per group) in
  * {(16,1,16), (32,1,16), (64,1,16), (128,1,16)}; 0s = by call length (default: 128 for calls
  * of >= 4 x 8192 samples on banks that fill the chip with <= 2 time segments, 64 from

@@ -24,7 +24,9 @@ LTI_GEOMS = [(16, 1, 16), (32, 1, 16), (64, 1, 16), (128, 1, 16)]
 
 def make_pair(order, N, fwd, back, kp=0.001, kg=0.001, boost=None, gains=None):
     from huygens_amd import Filterbank
+    from huygens_amd._lib import HZ_FB_RESP_OFF
     g = Filterbank(order, N, kp, kg)
+    g.set_response(HZ_FB_RESP_OFF)   # the per-band LTI engine under test (test_filterbank_resp_gpu.py: the other)
     o = OracleFilterbank(order, N, kp, kg)
     for fb in (g, o):
         for n in range(N):
