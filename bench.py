@@ -101,6 +101,23 @@ def fb_executed_flops(lti, L=32, O=2, N=N_BANDS):
     return e + mix + scan + zs
 
 
+def resp_step_flops(K, S, N, O=2):
+    """FP64 flops of one stationary-engine call (hz_fb_resp.hip) of S samples, horizon K:
+    packed window FFTs (Q + D - 1) and output FFTs (D) at 5 F log2 F each, the partition MACs
+    (8 flops per complex MAC, D x F x Q), and the end-state pass (the chunk-64 state kernel in
+    prepass mode over the K history samples: E 2 O 4 ceil((64+O)/4) / 64 + scan 2 8 O^2 / 64
+    flops per band-sample)."""
+    import math
+    P, F, lgF = 2048, 4096, 12
+    Q = K // P
+    B = -(-S // P)
+    D = -(-B // 2)
+    fft = 5.0 * F * lgF
+    conv = (Q + D - 1) * fft + D * F * Q * 8.0 + D * fft
+    state = N * K * (2.0 * O * 4 * math.ceil((64 + O) / 4) / 64 + 2.0 * 8 * O * O / 64)
+    return conv, state
+
+
 def pmc_traffic(kernels=("fb_mix_kernel",), extra=()):
     """HBM bytes per step of the engine's kernels from two separate rocprofv3 --pmc passes
     (FETCH_SIZE, WRITE_SIZE; kernel-trace only), run as child processes on a short bench.
@@ -120,7 +137,7 @@ def pmc_traffic(kernels=("fb_mix_kernel",), extra=()):
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="hz_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
         cmd = [exe, "--pmc", counter, "--kernel-trace", "-d", d, "-o", "pmc", "--output-format", "csv",
-               "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
+               "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "3",
                "--no-cpu-baseline", "--stream-blocks", "0", "--no-traffic", *extra]
         try:
             subprocess.run(cmd, check=True, capture_output=True, timeout=300,
@@ -167,6 +184,10 @@ def main():
     ap.add_argument("--bands-per-wave", type=int, default=0)
     ap.add_argument("--lti", default="", help="LTI engine geometry 'chunk,bands_per_wave,waves' (default engine choice)")
     ap.add_argument("--general", action="store_true", help="force the general engine (no converged fast path)")
+    ap.add_argument("--response", type=int, default=-1,
+                    help="stationary engine: 0 off (per-band engines only), 1 eager (default), 2 lazy")
+    ap.add_argument("--side-steps", type=int, default=50,
+                    help="timed steps of the side figures (per-band engine, lazy stationary engine)")
     ap.add_argument("--target-groups", type=int, default=0, help="(tuning) workgroups wanted per launch")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="(1 GPU, diagnostics) run rank 0's shard of an N-GPU job alone: per-GPU time at N")
@@ -205,6 +226,8 @@ def main():
     if args.general:
         from huygens_amd._lib import HZ_FB_PATH_GENERAL
         fb.set_path(HZ_FB_PATH_GENERAL)
+    if args.response >= 0:
+        fb.set_response(args.response)
     stream = torch.cuda.current_stream(dev)
     fb.set_stream(stream.cuda_stream)
 
@@ -235,10 +258,45 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     seg_ms, mix_ms, red_ms, launches = fb.profile_read()
-    from huygens_amd._lib import HZ_FB_PATH_LTI
-    lti = fb.last_path() == HZ_FB_PATH_LTI
+    from huygens_amd._lib import (HZ_FB_PATH_LTI, HZ_FB_PATH_RESPONSE, HZ_FB_RESP_EAGER, HZ_FB_RESP_LAZY,
+                                  HZ_FB_RESP_OFF)
+    path = fb.last_path()
+    lti = path == HZ_FB_PATH_LTI
+    resp = path == HZ_FB_PATH_RESPONSE
     chunk = fb.lti_chunk()   # the timed steps' chunk (the streaming calls below use a shorter one)
+    horizon = fb.response_info()[0]
     fb.profile(False)
+
+    def side_rate(mode, warm):
+        """ms per step of the same workload with the stationary engine in `mode` (timed like the
+        main loop, fewer steps): the per-band engine's figure and the lazy-state figure"""
+        if args.side_steps <= 0:
+            return None
+        fb.set_response(mode)
+        for _ in range(warm):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        ts = time.perf_counter()
+        for _ in range(args.side_steps):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - ts
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return {"ms_per_step": 1e3 * dt / args.side_steps, "value": N_BANDS * S * args.side_steps / dt,
+                "path": {1: "general", 2: "lti", 3: "response"}.get(fb.last_path(), "?")}
+
+    side = {}
+    if resp:
+        side["per_band_engine"] = side_rate(HZ_FB_RESP_OFF, 3)
+        side["stationary_lazy_states"] = side_rate(HZ_FB_RESP_LAZY, 3)
+        fb.set_response(HZ_FB_RESP_EAGER if args.response < 0 else args.response)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -288,12 +346,17 @@ def main():
         flops_per_launch = FLOPS_PER_BAND_SAMPLE * band_samples_per_launch
         achieved = flops_per_launch / launch_avg_s / 1e12 if launch_avg_s > 0 else None
         xflops = fb_executed_flops(lti, chunk, N=cnt)
+        if resp:   # the stationary engine's flops per call, spread over the call's band-samples
+            conv_f, state_f = resp_step_flops(horizon, S, cnt)
+            xflops = (conv_f + state_f) / (cnt * S)
         executed = xflops * band_samples_per_launch / launch_avg_s / 1e12 if launch_avg_s > 0 else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(fwd, back)
         kernels = (("fb_lti_kernel", "fb_lti_gemm", "fb_lti_reduce", "fb_lti_seg_carry", "fb_lti_sum",
                     "fb_lti_xrows") if lti
+                   else ("resp_fwd_kernel", "resp_mac_kernel", "resp_inv_kernel", "resp_hist_kernel",
+                         "resp_finish_kernel", "fb_lti_kernel<2, 64, 1", "fb_lti_seg_carry") if resp
                    else ("fb_mix_kernel", "fb_reduce"))
         traffic, traffic_detail = None, "skipped"
         if not args.no_traffic and world == 1 and S == SAMPLES_PER_STEP:
@@ -316,13 +379,18 @@ def main():
                                    "f_i=0.5(i+1)SR/4096 R=0.999, boost 1 + open, k_p=0.1 k_g=1",
                        "samples_per_step": S, "block": 1024, "bands": N_BANDS,
                        "bands_per_gpu": cnt, "parallelism": f"bands sharded x{world}, RCCL reduce"},
-            "roofline": {"bound": "mfma" if lti else "valu", "achieved": executed, "peak": FP64_PEAK_TFLOPS,
+            "engine": "stationary (bank response convolution, eager band states)" if resp
+                      else "per-band LTI" if lti else "per-band general",
+            "roofline": {"bound": "mfma" if (lti or resp) else "valu", "achieved": executed, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": (executed / FP64_PEAK_TFLOPS) if executed else None,
                          "traffic": traffic,
                          "traffic_detail": traffic_detail,
                          "algorithmic_bytes_per_launch": (16 * S + 120 * cnt) * args.steps / max(1, launches),
                          "launches_per_step": launches / max(1, args.steps),
-                         "kernel": (("LTI engine step: fb_lti_kernel<2,%d,STATE>%s + "
+                         "kernel": ("stationary engine step: resp_fwd_kernel + resp_mac_kernel<16> + resp_inv_kernel "
+                                    "(partitioned FFT convolution) + resp_hist_kernel + fb_lti_kernel<2,64,SEGEND> "
+                                    "(band states over the %d-sample horizon) + resp_finish_kernel" % horizon) if resp else
+                                   (("LTI engine step: fb_lti_kernel<2,%d,STATE>%s + "
                                      "fb_lti_gemm_pp_kernel<%d> + fb_lti_sum_kernel (+ segment prepass)"
                                      % (chunk, " (+ x rows)" if chunk >= 128 else " + fb_lti_xrows_kernel", chunk))
                                     if lti and chunk >= 64 else
@@ -334,17 +402,27 @@ def main():
                                                       "mix_or_state": mix_ms / max(1, launches),
                                                       "gemm_and_reduce": red_ms / max(1, launches)},
                          "flops_per_band_sample": xflops,
+                         "horizon": horizon if resp else None,
                          "flops_per_launch": xflops * band_samples_per_launch,
                          "reference_equivalent": {"flops_per_band_sample": FLOPS_PER_BAND_SAMPLE,
                                                   "achieved": achieved,
                                                   "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None},
-                         "note": "achieved = the FP64 flops the engine's algorithm performs per band-sample "
+                         "note": ("stationary engine: achieved = the FP64 flops of the call (packed window and output "
+                                  "FFTs at 5 F log2 F, partition MACs, the end-state pass over the horizon; "
+                                  "bench.resp_step_flops) over the engine's whole per-step GPU time (HIP events on the "
+                                  "handle's stream): components mix_or_state = the convolution (fwd + MAC + inv), "
+                                  "gemm_and_reduce = history + band states. reference_equivalent = the reference "
+                                  "recurrence's 18 flops per band-sample over the same time (far above the peak: the "
+                                  "stationary engine's cost does not grow with the bands). peak = FP64 vector = FP64 MFMA "
+                                  "peak.") if resp else
+                                 "achieved = the FP64 flops the engine's algorithm performs per band-sample "
                                  "(chunked state space: chunk end states + 64-lane scan + correction GEMM with the "
                                  "zero-state rows, DESIGN.md 3.3; PMC-verified in profiles/r2/flops_pmc.txt) over the "
                                  "whole per-step GPU time of the engine (kernel_avg_ms, HIP events on the handle's "
                                  "stream). reference_equivalent = the reference recurrence's 18 flops per band-sample "
                                  "(SURVEY.md 8(d)) over the same time -- it can exceed the peak because the engine "
                                  "needs fewer than half of them. peak = FP64 vector = FP64 MFMA peak."},
+            "side": side or None,
             "streaming": {"band_samples_per_s": stream_rate, "block": 1024,
                           "note": "one process() call per 1024-sample block, device-resident I/O"},
             "cpu_baseline": cpu,

@@ -160,7 +160,8 @@ struct hz_fb {
         double* d_Y = nullptr;           // [D][F] complex output spectra
         size_t Y_cap = 0;
         double* d_tw = nullptr;          // complex twiddles of the F-point transform
-        double* d_zero = nullptr;        // kMaxOrder zeros (x history of the zero-start pass)
+        double* d_zero = nullptr;        // N O zeros (x history / start of the zero-start pass)
+        size_t zero_cap = 0;
     } resp;
 };
 
@@ -186,9 +187,10 @@ bool fb_converged(hz_fb* h);
 int fb_launch_lti(hz_fb* h, int geom, const double* d_in, double* d_out, long n);
 long fb_horizon(const hz_fb* h);           // samples K with ||M^K|| < 2^-64 for every band (-1: > 2^18)
 // zero-start band states at the end of x[0, len) (len a multiple of 4096; the O samples before
-// x read as xzero) -> h->d_seg[band][1][O] (the LTI state kernel's prepass mode, chunk 64)
-int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xzero);
-int fb_lti_prepare_end(hz_fb* h);          // its records for the current coefficients
+// x read as xzero) -> out[band][O]; zeros: N O zeros (the carry's start)
+int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xzero, const double* zeros,
+                          double* out);
+int fb_lti_prepare_end(hz_fb* h, long len);   // its records for the current coefficients
 // hz_fb_resp.hip (stationary engine)
 void fb_resp_init(hz_fb* h);
 void fb_resp_invalidate(hz_fb* h, bool coefficients);   // targets / coefficients changed

@@ -1632,26 +1632,36 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
 
 long fb_horizon(const hz_fb* h) { return fb_lti_horizon(h); }
 
-int fb_lti_prepare_end(hz_fb* h) { return fb_prepare_lti(h, 2); }
+int fb_lti_prepare_end(hz_fb* h, long len) { return fb_prepare_lti(h, len % (64L * 128) == 0 ? 3 : 2); }
 
-// zero-start band states at the end of x[0, len): the state kernel's prepass mode over one
-// segment (chunk 64, 4096-sample tiles), result in d_seg[band][1] (hz_fb_resp.hip)
-int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xzero) {
-    constexpr int gi = 2;   // chunk 64
+// zero-start band states at the end of x[0, len) -> out[band][O] (hz_fb_resp.hip): the state
+// kernel's prepass mode, chunk 128 when len is a multiple of its 8192-sample tile (else chunk 64),
+// over m time segments when the bank alone leaves CUs idle (shards), joined by the carry kernel
+int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xzero, const double* zeros,
+                          double* out) {
     const int O = h->order;
-    if (O == 0 || len <= 0 || len % (64L * kLtiGeoms[gi].L) != 0) {
+    const int gi = len % (64L * 128) == 0 ? 3 : 2;
+    const long T = 64L * kLtiGeoms[gi].L;
+    if (O == 0 || len <= 0 || len % T != 0) {
         hz::set_error("fb_lti_zero_start_end: order %d, length %ld (a positive multiple of 4096)", O, len);
         return HZ_E_INVALID;
     }
     HZ_TRY(fb_prepare_lti(h, gi));
     hz_fb::LtiRecSet& set = h->lti_set[gi];
-    const size_t sneed = (size_t)h->N * 2 * O;
-    if (sneed > h->seg_cap) {
-        HZ_TRY_HIP(hipStreamSynchronize(h->stream));
-        if (h->d_seg) HZ_TRY_HIP(hipFree(h->d_seg));
-        h->d_seg = nullptr;
-        HZ_TRY_HIP(hipMalloc(&h->d_seg, sizeof(double) * sneed));
-        h->seg_cap = sneed;
+    const int G = (h->N + lti_waves(O) - 1) / lti_waves(O);
+    const long ntiles = len / T;
+    long m = std::min<long>(ntiles, std::max<long>(1, h->target_groups / G));
+    const long seg_tiles = (ntiles + m - 1) / m;
+    m = (ntiles + seg_tiles - 1) / seg_tiles;
+    if (m > 1) {
+        const size_t sneed = (size_t)h->N * (m + 1) * O;
+        if (sneed > h->seg_cap) {
+            HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+            if (h->d_seg) HZ_TRY_HIP(hipFree(h->d_seg));
+            h->d_seg = nullptr;
+            HZ_TRY_HIP(hipMalloc(&h->d_seg, sizeof(double) * sneed));
+            h->seg_cap = sneed;
+        }
     }
     LtiKernel kend = pick_lti(O, gi, MODE_SEGEND);
     HZ_TRY(fb_set_lds_attr((const void*)kend));
@@ -1659,23 +1669,34 @@ int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xze
     std::memset(&a, 0, sizeof(a));
     a.pin = h->d_pin;
     a.gin = h->d_gin;
-    a.ystate = h->d_ystate[h->scur];
+    a.ystate = zeros;
     a.pgstate = h->d_pg[h->scur];
     a.x = x;
     a.xhist = xzero;
-    a.segstate = h->d_seg;
     a.n = len;
     a.n_pad = len;
-    a.seg_len = len;
-    a.nseg = 2;          // segment 0 is not the last: its end state goes to segstate[band][1]
-    a.nseg_state = 2;
+    a.seg_len = seg_tiles * T;
+    a.nseg = (int)m + 1;   // segment m - 1 is not the last: every segment stores its end state
     a.seg_stride = 1;
     a.seg_skip = 0;
     a.nbands = h->N;
-    const int G = (h->N + lti_waves(O) - 1) / lti_waves(O);
-    hipLaunchKernelGGL(kend, dim3(G, 1), dim3(64 * lti_waves(O)), lti_lds(O, gi, false), h->stream,
+    if (m == 1) {   // slot (band + 1) O of out - O = out[band]
+        a.segstate = out - O;
+        a.nseg_state = 1;
+    } else {
+        a.segstate = h->d_seg;
+        a.nseg_state = (int)m + 1;
+    }
+    hipLaunchKernelGGL(kend, dim3(G, (unsigned)m), dim3(64 * lti_waves(O)), lti_lds(O, gi, false), h->stream,
                        (const double*)set.d_rec, a);
     HZ_TRY_HIP(hipGetLastError());
+    if (m > 1) {
+        hipLaunchKernelGGL(pick_lti_carry(O, kLtiGeoms[gi].L), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0,
+                           h->stream, (const double*)set.d_rec, zeros, h->d_seg, h->N, (int)m + 1, seg_tiles);
+        HZ_TRY_HIP(hipGetLastError());
+        HZ_TRY_HIP(hipMemcpy2DAsync(out, sizeof(double) * O, h->d_seg + (size_t)m * O, sizeof(double) * O * (m + 1),
+                                    sizeof(double) * O, (size_t)h->N, hipMemcpyDeviceToDevice, h->stream));
+    }
     return HZ_OK;
 }
 

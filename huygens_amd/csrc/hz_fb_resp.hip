@@ -33,7 +33,7 @@ constexpr int kLgP = 11, kP = 1 << kLgP;       // partition / output block (samp
 constexpr int kLgF = kLgP + 1, kF = 2 * kP;    // transform size
 constexpr int kRmax = 3;                       // radix-8 passes (hz_fft.h)
 constexpr int kFftThreads = kF >> kRmax;       // 512: one radix-8 group per thread
-constexpr int kMacR = 16;                      // output blocks per MAC thread
+constexpr int kMacR = 8;                       // output blocks per MAC thread (partitions padded to it)
 constexpr long kMinCall = 16384;               // shortest call that keeps the history
 
 size_t fft_lds() { return sizeof(double) * 2 * (size_t)hz::padded_len(kF) + sizeof(double2) * hz::twc_len(kLgF); }
@@ -128,6 +128,14 @@ struct RespArgs {
     double2* Z;           // [Q + D - 1 (+ pad)][F] packed window spectra
     const double2* Y;     // [D][F] packed output spectra
     double* out;          // [n]
+    // state upkeep, done by the inverse kernel's threads: the history after the call (the last K
+    // samples of [hist | x]), the smoothers' closed form, the x history (the last O inputs)
+    double* hist_next;
+    const double *pg, *pin, *gin;
+    double* pg_next;
+    double sp_n, sg_n;
+    double* xhist_next;
+    int N, O;
 };
 
 // u = [hist | x | 0 ...]
@@ -158,10 +166,12 @@ __global__ __launch_bounds__(kFftThreads) void resp_fwd_kernel(RespArgs a) {
 
 // Y_b[q] = sum_{p < Q} H_p[q] Z_{b+Q-1-p}[q] for b in [b0, b0 + R): thread = bin q x R output
 // blocks.  The R Z values of step p sit in a register ring (element r in slot (r - p) mod R): each
-// step loads one new Z value and one H value for R complex FMAs.
+// step brings one new Z value and one H value for R complex MACs.  Partitions are padded to a
+// multiple of R with zero spectra (Qp), so every block of R steps loads unguarded, and the next
+// block's 2R loads are issued before this block's MACs (latency once per call, not per step).
 template <int R>
 __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict__ H, const double2* __restrict__ Z,
-                                                       double2* __restrict__ Y, int Q, int D) {
+                                                       double2* __restrict__ Y, int Q, int Qp, int D) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;   // bin (grid.x = F / 256)
     const int b0 = blockIdx.y * R;
     double ar[R], ai[R], zr[R], zi[R];
@@ -173,26 +183,38 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
         zr[r] = z.x;
         zi[r] = z.y;
     }
-    for (int p0 = 0; p0 < Q; p0 += R) {
+    double2 hb[R], zb[R];
+    auto fetch = [&](int p0) {
 #pragma unroll
         for (int u = 0; u < R; ++u) {
-            const int p = p0 + u;
-            if (p >= Q) break;
-            const double2 hv = H[(long)p * kF + q];
+            hb[u] = H[(long)(p0 + u) * kF + q];
+            const long zi_ = base - (p0 + u) - 1;   // < 0 only past Q (zero H rows)
+            zb[u] = Z[(zi_ > 0 ? zi_ : 0) * kF + q];
+        }
+    };
+    fetch(0);
+    for (int p0 = 0; p0 < Qp; p0 += R) {
+        double2 hc[R], zc[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            hc[u] = hb[u];
+            zc[u] = zb[u];
+        }
+        if (p0 + R < Qp) fetch(p0 + R);
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int sl = ((r - u) % R + R) % R;
-                ar[r] = fma(hv.x, zr[sl], ar[r]);
-                ar[r] = fma(-hv.y, zi[sl], ar[r]);
-                ai[r] = fma(hv.x, zi[sl], ai[r]);
-                ai[r] = fma(hv.y, zr[sl], ai[r]);
+                ar[r] = fma(hc[u].x, zr[sl], ar[r]);
+                ar[r] = fma(-hc[u].y, zi[sl], ar[r]);
+                ai[r] = fma(hc[u].x, zi[sl], ai[r]);
+                ai[r] = fma(hc[u].y, zr[sl], ai[r]);
             }
-            if (p + 1 < Q) {   // element 0 of step p + 1: Z[base - p - 1] into the slot element R - 1 leaves
-                const int sl = ((-(u + 1)) % R + R) % R;
-                const double2 z = Z[(base - p - 1) * kF + q];
-                zr[sl] = z.x;
-                zi[sl] = z.y;
-            }
+            // element 0 of step p + 1 = Z[base - p - 1] into the slot element R - 1 leaves
+            const int sl = ((-(u + 1)) % R + R) % R;
+            zr[sl] = zc[u].x;
+            zi[sl] = zc[u].y;
         }
     }
 #pragma unroll
@@ -221,6 +243,18 @@ __global__ __launch_bounds__(kFftThreads) void resp_inv_kernel(RespArgs a) {
         if (t0 < a.n) a.out[t0] = re[hz::pad16(kP + r)];
         if (t1 < a.n) a.out[t1] = im[hz::pad16(kP + r)];
     }
+    // state upkeep (the forward kernel, the last reader of hist, has finished)
+    const long g = b * blockDim.x + threadIdx.x, stride = (long)gridDim.x * blockDim.x;
+    for (long i = g; i < a.K; i += stride) {
+        const long m = a.n + i;
+        a.hist_next[i] = m < a.K ? a.hist[m] : a.x[m - a.K];
+    }
+    for (long n = g; n < a.N; n += stride) {
+        const double P0 = a.pg[2 * n], G0 = a.pg[2 * n + 1], pb = a.pin[n], gb = a.gin[n];
+        a.pg_next[2 * n] = pb + a.sp_n * (P0 - pb);
+        a.pg_next[2 * n + 1] = gb + a.sg_n * (G0 - gb);
+    }
+    if (g < a.O) a.xhist_next[g] = a.x[a.n - 1 - g];
 }
 
 // history after a call: the last K samples of [hist | x]
@@ -230,28 +264,6 @@ __global__ __launch_bounds__(256) void resp_hist_kernel(const double* __restrict
     if (i >= K) return;
     const long m = n + i;
     hist_next[i] = m < K ? hist[m] : x[m - K];
-}
-
-// end of a stationary call: band states (the zero-start pass over the history, seg[band][1]),
-// the smoothers' closed form, the x history (the last O inputs)
-__global__ __launch_bounds__(256) void resp_finish_kernel(const double* __restrict__ seg, double* __restrict__ ystate,
-                                                          const double* __restrict__ pg, double* __restrict__ pg_next,
-                                                          const double* __restrict__ pin,
-                                                          const double* __restrict__ gin, double sp_n, double sg_n,
-                                                          const double* __restrict__ hist, long K,
-                                                          double* __restrict__ xhist_next, int N, int O, int copy_y) {
-    const int band = blockIdx.x * blockDim.x + threadIdx.x;
-    if (band < N) {
-        if (copy_y)
-            for (int k = 0; k < O; ++k) ystate[(long)band * O + k] = seg[((long)band * 2 + 1) * O + k];
-        if (pg_next) {
-            const double P0 = pg[2 * (long)band], G0 = pg[2 * (long)band + 1];
-            const double pb = pin[band], gb = gin[band];
-            pg_next[2 * (long)band] = pb + sp_n * (P0 - pb);
-            pg_next[2 * (long)band + 1] = gb + sg_n * (G0 - gb);
-        }
-    }
-    if (xhist_next && band < O) xhist_next[band] = hist[K - 1 - band];
 }
 
 typedef void (*RespHKernel)(const double*, const double*, const double*, const double*, int, long, double*);
@@ -278,11 +290,18 @@ int resp_setup(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     if (R.K == -2) {
         R.K = hz_fbi::fb_horizon(h);
-        if (R.K >= 0) R.K = std::max<long>(R.K, kP);   // (a multiple of 4096, so of P)
+        // a whole number of the chunk-128 state kernel's 8192-sample tiles (the end-state pass;
+        // older inputs reach the state below 2^-64 of it)
+        if (R.K >= 0) R.K = std::max<long>(8192, (R.K + 8191) / 8192 * 8192);
         R.h_valid = false;
         R.run = 0;
     }
     if (R.K <= 0) return HZ_OK;
+    const size_t nz = std::max<size_t>((size_t)h->N * h->order, hz_fbi::kMaxOrder);
+    if (nz > R.zero_cap) {
+        HZ_TRY(resp_alloc(&R.d_zero, &R.zero_cap, nz));
+        HZ_TRY_HIP(hipMemset(R.d_zero, 0, sizeof(double) * nz));
+    }
     HZ_TRY(resp_alloc(&R.d_hist[0], &R.hist_cap0, (size_t)R.K));
     HZ_TRY(resp_alloc(&R.d_hist[1], &R.hist_cap1, (size_t)R.K));
     if (!R.d_tw) {
@@ -294,8 +313,6 @@ int resp_setup(hz_fb* h) {
         }
         HZ_TRY_HIP(hipMalloc((void**)&R.d_tw, sizeof(double2) * tw.size()));
         HZ_TRY_HIP(hipMemcpy(R.d_tw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice));
-        HZ_TRY_HIP(hipMalloc(&R.d_zero, sizeof(double) * hz_fbi::kMaxOrder));
-        HZ_TRY_HIP(hipMemset(R.d_zero, 0, sizeof(double) * hz_fbi::kMaxOrder));
         for (const void* k : {(const void*)resp_hspec_kernel, (const void*)resp_fwd_kernel, (const void*)resp_inv_kernel})
             HZ_TRY(hz_fbi::fb_set_lds_attr(k));
     }
@@ -310,13 +327,15 @@ int resp_build_h(hz_fb* h) {
     const long K = R.K;
     const int G = (N + 63) / 64;
     const int Q = (int)(K / kP);
+    const int Qp = (Q + kMacR - 1) / kMacR * kMacR;   // zero spectra past Q (the MAC's unguarded blocks)
     HZ_TRY(resp_alloc(&R.d_coef, &R.coef_cap, (size_t)N * (2 * O + 1)));
     HZ_TRY_HIP(hipMemcpyAsync(R.d_coef, h->F.data(), sizeof(double) * N * (O + 1), hipMemcpyHostToDevice, h->stream));
     HZ_TRY_HIP(hipMemcpyAsync(R.d_coef + (size_t)N * (O + 1), h->B.data(), sizeof(double) * N * O,
                               hipMemcpyHostToDevice, h->stream));
     HZ_TRY(resp_alloc(&R.d_hpart, &R.hpart_cap, (size_t)G * K));
     HZ_TRY(resp_alloc(&R.d_h, &R.h_cap, (size_t)K));
-    HZ_TRY(resp_alloc(&R.d_H, &R.H_cap, (size_t)2 * Q * kF));
+    HZ_TRY(resp_alloc(&R.d_H, &R.H_cap, (size_t)2 * Qp * kF));
+    HZ_TRY_HIP(hipMemsetAsync(R.d_H, 0, sizeof(double2) * (size_t)Qp * kF, h->stream));
     hipLaunchKernelGGL(pick_h(O), dim3(G), dim3(64), 0, h->stream, (const double*)R.d_coef,
                        (const double*)(R.d_coef + (size_t)N * (O + 1)), (const double*)h->d_pin,
                        (const double*)h->d_gin, N, K, R.d_hpart);
@@ -332,19 +351,11 @@ int resp_build_h(hz_fb* h) {
     return HZ_OK;
 }
 
-// zero-start band states over the history's K samples -> ystate[cur] (LAZY: on demand)
-int resp_states(hz_fb* h, double* ystate, double* pg, double* pg_next, double* xhist_next, long n_adv) {
+// zero-start band states over the history's K samples -> ystate (the end state of the last
+// stationary call: after it (EAGER) or when needed (LAZY))
+int resp_states(hz_fb* h, double* ystate) {
     hz_fb::Resp& R = h->resp;
-    const double* hist = R.d_hist[R.hcur];
-    if (ystate) HZ_TRY(hz_fbi::fb_lti_zero_start_end(h, hist, R.K, R.d_zero));
-    const double spn = (double)powl((long double)h->sp, (long double)n_adv);
-    const double sgn = (double)powl((long double)h->sg, (long double)n_adv);
-    hipLaunchKernelGGL(resp_finish_kernel, dim3((unsigned)((std::max(h->N, h->order) + 255) / 256)), dim3(256), 0,
-                       h->stream, (const double*)h->d_seg, ystate, (const double*)pg, pg_next,
-                       (const double*)h->d_pin, (const double*)h->d_gin, spn, sgn, hist, R.K, xhist_next, h->N,
-                       h->order, ystate ? 1 : 0);
-    HZ_TRY_HIP(hipGetLastError());
-    return HZ_OK;
+    return hz_fbi::fb_lti_zero_start_end(h, R.d_hist[R.hcur], R.K, R.d_zero, R.d_zero, ystate);
 }
 
 long resp_min_call(const hz_fb* h) { return h->resp.min_call > 0 ? h->resp.min_call : kMinCall; }
@@ -387,7 +398,7 @@ bool fb_resp_eligible(hz_fb* h, long n, bool conv) {
 int fb_resp_materialize(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     if (!R.implicit) return HZ_OK;
-    HZ_TRY(resp_states(h, h->d_ystate[h->scur], nullptr, nullptr, nullptr, 0));
+    HZ_TRY(resp_states(h, h->d_ystate[h->scur]));
     R.implicit = false;
     return HZ_OK;
 }
@@ -420,6 +431,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     HZ_TRY(resp_build_h(h));
     const long K = R.K;
     const int Q = (int)(K / kP);
+    const int Qp = (Q + kMacR - 1) / kMacR * kMacR;
     const long B = (n + kP - 1) / kP;
     const int D = (int)((B + 1) / 2);
     const int nz = Q + D - 1;
@@ -433,7 +445,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     if (h->prof) {
         HZ_TRY(fb_prof_events(h, &e));
         HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
-        h->ev_skip[(e - h->ev.data()) / 5] |= 2;   // no segment phase
+        h->ev_skip[(e - h->ev.data()) / 5] |= 2 | 8;   // no segment phase; reduce start = mix end
     }
     RespArgs a;
     a.hist = R.d_hist[R.hcur];
@@ -446,22 +458,35 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.Z = (double2*)R.d_Z;
     a.Y = (const double2*)R.d_Y;
     a.out = d_out;
+    a.hist_next = R.d_hist[R.hcur ^ 1];
+    a.pg = h->d_pg[h->scur];
+    a.pg_next = h->d_pg[h->scur ^ 1];
+    a.pin = h->d_pin;
+    a.gin = h->d_gin;
+    a.sp_n = (double)powl((long double)h->sp, (long double)n);
+    a.sg_n = (double)powl((long double)h->sg, (long double)n);
+    a.xhist_next = h->d_xhist[h->xcur ^ 1];
+    a.N = h->N;
+    a.O = h->order;
     hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kFftThreads), fft_lds(), h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     hipLaunchKernelGGL(resp_mac_kernel<kMacR>, dim3(kF / 256, (unsigned)((D + kMacR - 1) / kMacR)), dim3(256), 0,
-                       h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, D);
+                       h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, D);
     HZ_TRY_HIP(hipGetLastError());
     hipLaunchKernelGGL(resp_inv_kernel, dim3((unsigned)D), dim3(kFftThreads), fft_lds(), h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
-    if (e) h->ev_skip[(e - h->ev.data()) / 5] |= 8;
-    HZ_TRY(fb_resp_track(h, d_in, n, true));
-    // end state: bands (EAGER) or marked implicit (LAZY); smoothers and x history always
-    const bool lazy = R.mode == HZ_FB_RESP_LAZY;
-    if (lazy) HZ_TRY(fb_lti_prepare_end(h));   // records of these coefficients for a later materialisation
-    HZ_TRY(resp_states(h, lazy ? nullptr : h->d_ystate[h->scur ^ 1], h->d_pg[h->scur], h->d_pg[h->scur ^ 1],
-                       h->d_xhist[h->xcur ^ 1], n));
-    R.implicit = lazy;
+    R.hcur ^= 1;   // the inverse kernel wrote the history after the call
+    R.run = std::min(R.run + n, 1L << 60);
+    // end state: band states now (EAGER) or when needed (LAZY); smoothers and x history were
+    // written by the inverse kernel
+    if (R.mode == HZ_FB_RESP_LAZY) {
+        HZ_TRY(fb_lti_prepare_end(h, K));   // records of these coefficients for a later materialisation
+        R.implicit = true;
+    } else {
+        HZ_TRY(resp_states(h, h->d_ystate[h->scur ^ 1]));
+        R.implicit = false;
+    }
     if (e) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
     h->scur ^= 1;
     h->xcur ^= 1;
