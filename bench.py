@@ -210,6 +210,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from huygens_amd import Filterbank
+    from huygens_amd._lib import HZ_FB_PATH_RESPONSE
     fwd, back = c2_coefficients()
     b0, cnt = shard_of(rank, world) if not args.emulate_world else shard_of(0, args.emulate_world)
     fb = Filterbank(2, N_BANDS, 0.1, 1.0, device=local, shard=(b0, cnt))
@@ -231,15 +232,71 @@ def main():
     stream = torch.cuda.current_stream(dev)
     fb.set_stream(stream.cuda_stream)
 
+    # N > 1: once stationary, the ranks split the call by TIME (each convolves its share of the
+    # output blocks with the whole bank's response, summed over the band shards by one all-reduce
+    # at setup) and keep their own bands' states; rank 0 gathers the shares
+    tshard = False
+    if world > 1 and not args.general and args.response != 0:
+        from huygens_amd.shard import set_time_shards
+
+        def all_reduce_sum(h):
+            t = torch.from_numpy(h).to(dev)
+            dist.all_reduce(t)
+            return t.cpu().numpy()
+
+        def all_reduce_max(k):
+            t = torch.tensor([k], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return int(t.item())
+        tshard = set_time_shards(fb, rank, world, all_reduce_sum, all_reduce_max)
+    elif args.emulate_world > 1 and not args.general and args.response != 0:
+        # (1 GPU, diagnostics) rank 0 of a time-sharded job: the other shards' handles exist only
+        # to sum the whole bank's response
+        from huygens_amd.shard import set_time_shards
+        others = []
+        for r in range(1, args.emulate_world):
+            ob, oc = shard_of(r, args.emulate_world)
+            o = Filterbank(2, N_BANDS, 0.1, 1.0, device=local, shard=(ob, oc))
+            for n in range(ob, ob + oc):
+                o.coefficients(n, fwd[n], back[n])
+            o.boost(np.ones(N_BANDS))
+            o.open()
+            o.response(8192)
+            others.append(o)
+        k_max = max([o.response_info()[0] for o in others])
+        tshard = set_time_shards(fb, 0, args.emulate_world,
+                                 lambda h: h + sum(o.response(len(h)) for o in others),
+                                 lambda k: max(k, k_max))
+        for o in others:
+            o.close()
+
     S = args.samples
+    gbuf, glist = None, None
     rng = np.random.default_rng(1234)
     x = torch.from_numpy(rng.uniform(-1, 1, S).astype(np.float32).astype(np.float64)).to(dev)
     y = torch.empty_like(x)
 
     def step():
+        nonlocal gbuf, glist
         fb.process_device(x.data_ptr(), y.data_ptr(), S)
         if world > 1:
-            dist.reduce(y, dst=0, op=dist.ReduceOp.SUM)
+            active, first, count = fb.time_shard_info(S) if tshard else (False, 0, S)
+            if active and fb.last_path() == HZ_FB_PATH_RESPONSE:
+                # shares are runs of whole 2048-sample blocks: gather fixed-size slots to rank 0
+                slot = -(-(-(-S // 2048)) // world) * 2048
+                if gbuf is None:
+                    gbuf = torch.zeros(slot, dtype=torch.float64, device=dev)
+                    glist = [torch.empty_like(gbuf) for _ in range(world)] if rank == 0 else None
+                gbuf[:count].copy_(y[first:first + count])
+                dist.gather(gbuf, glist, dst=0)
+                if rank == 0:
+                    B = -(-S // 2048)
+                    for r in range(world):
+                        f = min(S, B * r // world * 2048)
+                        c = min(S, B * (r + 1) // world * 2048) - f
+                        y[f:f + c].copy_(glist[r][:c])
+            else:
+                dist.reduce(y, dst=0, op=dist.ReduceOp.SUM)
 
     for _ in range(args.warmup):
         step()
@@ -378,7 +435,10 @@ def main():
             "config": {"workload": "C2 Filterbank<double>(order 2, 4096 bands), resonant band-pass "
                                    "f_i=0.5(i+1)SR/4096 R=0.999, boost 1 + open, k_p=0.1 k_g=1",
                        "samples_per_step": S, "block": 1024, "bands": N_BANDS,
-                       "bands_per_gpu": cnt, "parallelism": f"bands sharded x{world}, RCCL reduce"},
+                       "bands_per_gpu": cnt,
+                       "parallelism": (f"stationary calls split by time x{world} (whole-bank response, one "
+                                       f"all-reduce at setup), band states sharded x{world}, RCCL gather"
+                                       if tshard and resp else f"bands sharded x{world}, RCCL reduce")},
             "engine": "stationary (bank response convolution, eager band states)" if resp
                       else "per-band LTI" if lti else "per-band general",
             "roofline": {"bound": "mfma" if (lti or resp) else "valu", "achieved": executed, "peak": FP64_PEAK_TFLOPS,

@@ -99,6 +99,9 @@ _SIGS = {
     "hz_fb_tune_response": (I, [VP, L, L]),
     "hz_fb_response_info": (I, [VP, C.POINTER(L), C.POINTER(L), C.POINTER(I), C.POINTER(L)]),
     "hz_fb_get_response": (I, [VP, PD, L]),
+    "hz_fb_set_bank_response": (I, [VP, PD, L]),
+    "hz_fb_set_time_shard": (I, [VP, I, I]),
+    "hz_fb_time_shard_info": (I, [VP, C.POINTER(I), C.POINTER(L), C.POINTER(L), L]),
     # Oscbank
     "hz_osc_create": (I, [I, D, I, C.POINTER(VP)]),
     "hz_osc_create_shard": (I, [I, I, I, D, I, C.POINTER(VP)]),

@@ -144,6 +144,11 @@ struct hz_fb {
         long calls = 0;                  // stationary calls made
         long min_call = 0;               // shortest stationary / history-keeping call (0: 16384)
         long bands_per_sample = -1;      // cost model: stationary when N n >= this (K + n) (-1: 256)
+        // time-range shards (multi-GPU): the whole bank's response, summed over the band shards by
+        // the caller (hz_fb_set_bank_response; cleared by every setter), and this rank's share
+        std::vector<double> h_over;
+        bool over_valid = false;
+        int shard_rank = 0, shard_world = 1;
         double* d_hist[2] = {nullptr, nullptr};   // [K] last K inputs (ping-pong)
         size_t hist_cap0 = 0, hist_cap1 = 0;
         int hcur = 0;
@@ -194,6 +199,7 @@ int fb_lti_prepare_end(hz_fb* h, long len);   // its records for the current coe
 // hz_fb_resp.hip (stationary engine)
 void fb_resp_init(hz_fb* h);
 void fb_resp_invalidate(hz_fb* h, bool coefficients);   // targets / coefficients changed
+void fb_resp_setter(hz_fb* h);   // any setter, also for bands of other shards: the bank response changes
 bool fb_resp_eligible(hz_fb* h, long n, bool conv);
 int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n);
 int fb_resp_track(hz_fb* h, const double* d_in, long n, bool conv);  // history after any call

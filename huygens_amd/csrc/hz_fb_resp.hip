@@ -122,7 +122,8 @@ __global__ __launch_bounds__(kFftThreads) void resp_hspec_kernel(const double* _
 struct RespArgs {
     const double* hist;   // [K] the K inputs before the call
     const double* x;      // [n] the call's input
-    long K, n;
+    long K, n;            // horizon; the call's length
+    long off, n_out;      // outputs of this launch: out[off, off + n_out) (time-range shards)
     int Q, D;             // partitions; packed output-block pairs
     const double2* tw;
     double2* Z;           // [Q + D - 1 (+ pad)][F] packed window spectra
@@ -138,11 +139,12 @@ struct RespArgs {
     int N, O;
 };
 
-// u = [hist | x | 0 ...]
+// u = [hist | x | 0 ...], indexed from the launch's first output block (off)
 __device__ __forceinline__ double resp_u(const RespArgs& a, long m) {
+    m += a.off;
     if (m < a.K) return a.hist[m];
     m -= a.K;
-    return m < a.n ? a.x[m] : 0.0;
+    return m < a.off + a.n_out ? a.x[m] : 0.0;
 }
 
 // Z_j = FFT(W_{j+1} + i W_{j+1+D}), W_i = u[(i-1)P, (i+1)P)
@@ -154,9 +156,20 @@ __global__ __launch_bounds__(kFftThreads) void resp_fwd_kernel(RespArgs a) {
     load_tw(T, a.tw);
     const long j = blockIdx.x;
     const long m0 = j * kP, m1 = (j + a.D) * kP;
-    for (int k = threadIdx.x; k < kF; k += blockDim.x) {
-        re[hz::pad16(k)] = resp_u(a, m0 + k);
-        im[hz::pad16(k)] = resp_u(a, m1 + k);
+    // every load of the thread issued before the first LDS store (one memory latency, not 8)
+    constexpr int PT = kF / kFftThreads;
+    double vr[PT], vi[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+        const int k = threadIdx.x + i * kFftThreads;
+        vr[i] = resp_u(a, m0 + k);
+        vi[i] = resp_u(a, m1 + k);
+    }
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+        const int k = threadIdx.x + i * kFftThreads;
+        re[hz::pad16(k)] = vr[i];
+        im[hz::pad16(k)] = vi[i];
     }
     __syncthreads();
     hz::fft_fwd_lead<kRmax>(re, im, kLgF, T, true);
@@ -231,20 +244,27 @@ __global__ __launch_bounds__(kFftThreads) void resp_inv_kernel(RespArgs a) {
     load_tw(T, a.tw);
     const long b = blockIdx.x;
     const double2* y = a.Y + b * kF;
-    for (int q = threadIdx.x; q < kF; q += blockDim.x) {
-        const double2 v = y[q];
-        re[hz::pad16(q)] = v.x;
-        im[hz::pad16(q)] = v.y;
+    constexpr int PT = kF / kFftThreads;
+    double2 v[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) v[i] = y[threadIdx.x + i * kFftThreads];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+        const int q = threadIdx.x + i * kFftThreads;
+        re[hz::pad16(q)] = v[i].x;
+        im[hz::pad16(q)] = v[i].y;
     }
     __syncthreads();
     hz::fft_inv_tail<kRmax>(re, im, kLgF, T, true);
     for (int r = threadIdx.x; r < kP; r += blockDim.x) {
         const long t0 = b * kP + r, t1 = (b + a.D) * kP + r;
-        if (t0 < a.n) a.out[t0] = re[hz::pad16(kP + r)];
-        if (t1 < a.n) a.out[t1] = im[hz::pad16(kP + r)];
+        if (t0 < a.n_out) a.out[a.off + t0] = re[hz::pad16(kP + r)];
+        if (t1 < a.n_out) a.out[a.off + t1] = im[hz::pad16(kP + r)];
     }
     // state upkeep (the forward kernel, the last reader of hist, has finished)
     const long g = b * blockDim.x + threadIdx.x, stride = (long)gridDim.x * blockDim.x;
+    // a time-range shard leaves zeros outside its range: the ranks' outputs sum to the call's
+    for (long t = g; t < a.n - a.n_out; t += stride) a.out[t < a.off ? t : t + a.n_out] = 0.0;
     for (long i = g; i < a.K; i += stride) {
         const long m = a.n + i;
         a.hist_next[i] = m < a.K ? a.hist[m] : a.x[m - a.K];
@@ -343,6 +363,8 @@ int resp_build_h(hz_fb* h) {
     hipLaunchKernelGGL(resp_hsum_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, h->stream,
                        (const double*)R.d_hpart, G, K, R.d_h);
     HZ_TRY_HIP(hipGetLastError());
+    if (R.over_valid)   // the whole bank's response (time-range shards)
+        HZ_TRY_HIP(hipMemcpyAsync(R.d_h, R.h_over.data(), sizeof(double) * K, hipMemcpyHostToDevice, h->stream));
     hipLaunchKernelGGL(resp_hspec_kernel, dim3((unsigned)Q), dim3(kFftThreads), fft_lds(), h->stream,
                        (const double*)R.d_h, K, (const double2*)R.d_tw, (double2*)R.d_H);
     HZ_TRY_HIP(hipGetLastError());
@@ -378,7 +400,13 @@ void fb_resp_init(hz_fb* h) { h->resp.mode = resp_mode_default(); }
 void fb_resp_invalidate(hz_fb* h, bool coefficients) {
     h->resp.run = 0;
     h->resp.h_valid = false;
+    h->resp.over_valid = false;
     if (coefficients) h->resp.K = -2;
+}
+
+void fb_resp_setter(hz_fb* h) {
+    if (h->resp.over_valid) h->resp.h_valid = false;   // back to this shard's own response
+    h->resp.over_valid = false;
 }
 
 bool fb_resp_eligible(hz_fb* h, long n, bool conv) {
@@ -432,7 +460,16 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     const long K = R.K;
     const int Q = (int)(K / kP);
     const int Qp = (Q + kMacR - 1) / kMacR * kMacR;
-    const long B = (n + kP - 1) / kP;
+    // time-range shard (hz_fb_set_time_shard, with the whole bank's response): this rank's run of
+    // whole output blocks
+    long off = 0, n_out = n;
+    if (R.shard_world > 1 && R.over_valid) {
+        const long Ball = (n + kP - 1) / kP;
+        const long lo = Ball * R.shard_rank / R.shard_world, hi = Ball * (R.shard_rank + 1) / R.shard_world;
+        off = std::min(n, lo * kP);
+        n_out = std::min(n, hi * kP) - off;
+    }
+    const long B = std::max<long>(1, (n_out + kP - 1) / kP);
     const int D = (int)((B + 1) / 2);
     const int nz = Q + D - 1;
     const int zrows = (D + kMacR - 1) / kMacR * kMacR + Q;   // the MAC's last register window
@@ -452,6 +489,8 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.x = d_in;
     a.K = K;
     a.n = n;
+    a.off = off;
+    a.n_out = n_out;
     a.Q = Q;
     a.D = D;
     a.tw = (const double2*)R.d_tw;
@@ -519,10 +558,59 @@ int hz_fb_set_response(hz_fb* h, int mode) {
     return HZ_OK;
 }
 
+int hz_fb_set_bank_response(hz_fb* h, const double* resp, long count) {
+    if (!h || (count > 0 && !resp) || count < 0) return HZ_E_INVALID;
+    HZ_TRY_HIP(hipSetDevice(h->device));
+    HZ_TRY(hz_fbi::fb_upload_staged(h));
+    if (count == 0) {
+        h->resp.over_valid = false;
+        h->resp.h_valid = false;
+        return HZ_OK;
+    }
+    HZ_TRY(resp_setup(h));
+    if (h->resp.K <= 0 || count < h->resp.K || count % 8192 != 0 || count > (1L << 19)) {
+        hz::set_error("hz_fb_set_bank_response: %ld values (a multiple of 8192, at least this shard's "
+                      "horizon %ld)", count, h->resp.K);
+        return HZ_E_INVALID;
+    }
+    if (count > h->resp.K) {   // the bank's horizon (another shard's bands ring longer): a longer history
+        h->resp.K = count;
+        h->resp.run = 0;
+        HZ_TRY(resp_setup(h));
+    }
+    h->resp.h_over.assign(resp, resp + count);
+    h->resp.over_valid = true;
+    h->resp.h_valid = false;
+    return HZ_OK;
+}
+
+int hz_fb_set_time_shard(hz_fb* h, int rank, int world) {
+    if (!h || world < 1 || rank < 0 || rank >= world) return HZ_E_INVALID;
+    h->resp.shard_rank = rank;
+    h->resp.shard_world = world;
+    return HZ_OK;
+}
+
 int hz_fb_tune_response(hz_fb* h, long min_call, long bands_per_sample) {
     if (!h || min_call < 0 || bands_per_sample < 0) return HZ_E_INVALID;
     h->resp.min_call = min_call;                                   // 0: 16384
     h->resp.bands_per_sample = bands_per_sample ? bands_per_sample : -1;   // 0: 256 (HZ_FB_RESP_BANDS)
+    return HZ_OK;
+}
+
+int hz_fb_time_shard_info(hz_fb* h, int* active, long* first, long* count, long n) {
+    if (!h) return HZ_E_INVALID;
+    const hz_fb::Resp& R = h->resp;
+    const bool on = R.shard_world > 1 && R.over_valid;
+    long lo = 0, cnt = n;
+    if (on) {
+        const long Ball = (n + kP - 1) / kP;
+        lo = std::min(n, Ball * R.shard_rank / R.shard_world * kP);
+        cnt = std::min(n, Ball * (R.shard_rank + 1) / R.shard_world * kP) - lo;
+    }
+    if (active) *active = on ? 1 : 0;
+    if (first) *first = lo;
+    if (count) *count = cnt;
     return HZ_OK;
 }
 

@@ -1013,6 +1013,7 @@ int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double*
         hz::set_error("hz_fb_coefficients: invalid arguments");
         return HZ_E_INVALID;
     }
+    hz_fbi::fb_resp_setter(h);
     if (n < 0 || n >= h->N_total) {
         hz::set_error("hz_fb_coefficients: band %d out of range [0,%d)", n, h->N_total);
         return HZ_E_RANGE;
@@ -1029,6 +1030,7 @@ int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double*
 
 int hz_fb_boost(hz_fb* h, int n, double v) {
     if (!h) return HZ_E_INVALID;
+    hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
     if (n < 0 || n >= h->N_total) {
@@ -1045,6 +1047,7 @@ int hz_fb_boost(hz_fb* h, int n, double v) {
 
 int hz_fb_boost_all(hz_fb* h, const double* v, int count) {
     if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
+    hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
     for (int i = 0; i < std::min(h->N_total, count); ++i) {
@@ -1057,6 +1060,7 @@ int hz_fb_boost_all(hz_fb* h, const double* v, int count) {
 
 int hz_fb_mix(hz_fb* h, int n, double v) {
     if (!h) return HZ_E_INVALID;
+    hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
     if (n < 0 || n >= h->N_total) {
@@ -1073,6 +1077,7 @@ int hz_fb_mix(hz_fb* h, int n, double v) {
 
 int hz_fb_mix_all(hz_fb* h, const double* v, int count) {
     if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
+    hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
     for (int i = 0; i < std::min(h->N_total, count); ++i) {
@@ -1085,6 +1090,7 @@ int hz_fb_mix_all(hz_fb* h, const double* v, int count) {
 
 int hz_fb_open(hz_fb* h) {
     if (!h) return HZ_E_INVALID;
+    hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
     std::fill(h->gin.begin(), h->gin.end(), 1.0);

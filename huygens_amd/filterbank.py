@@ -215,3 +215,17 @@ class Filterbank:
         out = np.zeros(count)
         check(self._lib.hz_fb_get_response(self._h, dptr(out), count))
         return out
+
+    def set_bank_response(self, h):
+        """The whole bank's response (sum of the shards' response()) for time-range shards."""
+        v = np.ascontiguousarray(h, dtype=np.float64)
+        check(self._lib.hz_fb_set_bank_response(self._h, dptr(v), len(v)))
+
+    def set_time_shard(self, rank: int, world: int):
+        check(self._lib.hz_fb_set_time_shard(self._h, int(rank), int(world)))
+
+    def time_shard_info(self, n: int):
+        """-> (active, first sample, count) of a stationary call of n samples on this rank"""
+        a, f, c = C.c_int(), C.c_long(), C.c_long()
+        check(self._lib.hz_fb_time_shard_info(self._h, C.byref(a), C.byref(f), C.byref(c), int(n)))
+        return bool(a.value), f.value, c.value

@@ -14,3 +14,22 @@ def shard_of(rank: int, world: int, n_units: int) -> tuple[int, int]:
     base, rem = divmod(n_units, world)
     begin = rank * base + min(rank, rem)
     return begin, base + (1 if rank < rem else 0)
+
+
+def set_time_shards(fb, rank: int, world: int, all_reduce_sum, all_reduce_max) -> bool:
+    """Stationary Filterbank calls split by TIME over the ranks (hz_fb_set_time_shard): the
+    whole bank's response is the sum of the band shards' responses over the largest horizon of
+    the ranks (`all_reduce_sum(array) -> array`, `all_reduce_max(int) -> int`, e.g. RCCL
+    all-reduces), set on every rank; each rank then convolves its run of output blocks and keeps
+    its own bands' states.  Call after the last setter (setters clear it).  Returns False
+    (nothing set) when some shard has no finite horizon."""
+    import numpy as np
+    fb.response(8192)   # computes the shard's horizon
+    K = int(fb.response_info()[0])
+    K_all = int(all_reduce_max(K if K > 0 else 1 << 30))
+    if K_all <= 0 or K_all > (1 << 19):
+        return False
+    full = np.asarray(all_reduce_sum(np.ascontiguousarray(fb.response(K_all))), dtype=np.float64)
+    fb.set_bank_response(full)
+    fb.set_time_shard(rank, world)
+    return True

@@ -136,6 +136,19 @@ int hz_fb_tune_response(hz_fb* h, long min_call, long bands_per_sample);
 int hz_fb_response_info(hz_fb* h, long* horizon, long* run, int* implicit_state, long* calls);
 /* the bank response h[0 .. count) (zero past the horizon); HZ_E_UNSUPPORTED without a horizon */
 int hz_fb_get_response(hz_fb* h, double* out, long count);
+/* Time-range shards of the stationary engine (multi-GPU, one process per GPU): each rank owns a
+ * band shard (hz_fb_create_shard) for the band states, sets the WHOLE bank's response -- the sum
+ * over ranks of hz_fb_get_response(K values), K = the largest horizon of the ranks (a multiple of
+ * 8192; a longer horizon than the shard's own restarts its history), e.g. one RCCL all-reduce -- with
+ * hz_fb_set_bank_response, and its rank / world with hz_fb_set_time_shard.  Its stationary calls
+ * then convolve only rank's run of whole 2048-sample output blocks with that response and write
+ * zeros elsewhere, so the ranks' outputs still sum to the call's mix (or are gathered by range:
+ * hz_fb_time_shard_info).  Every setter (also for bands of other shards) clears the bank
+ * response; count 0 clears it explicitly.  Without it a call outputs all samples of its own bands. */
+int hz_fb_set_bank_response(hz_fb* h, const double* resp, long count);
+int hz_fb_set_time_shard(hz_fb* h, int rank, int world);
+/* for a stationary call of n samples: whether it is time-sharded, and its output range */
+int hz_fb_time_shard_info(hz_fb* h, int* active, long* first, long* count, long n);
 /* LTI engine geometry: (chunk length, bands per wave, waves per group) in
  * {(16,1,16), (32,1,16), (64,1,16), (128,1,16)}; 0s = by call length (default: 128 for calls
  * of >= 4 x 8192 samples on banks that fill the chip with <= 2 time segments, 64 from

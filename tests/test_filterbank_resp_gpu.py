@@ -230,3 +230,54 @@ def test_c2_full_size_against_lti(gpu_lib):
         assert rel_err(yg, yt) < 1e-7, (i, rel_err(yg, yt))   # Nyquist double pole: TOL_STIFF
     assert g.last_path() == L.HZ_FB_PATH_RESPONSE
     assert states_close(g.get_state(), t.get_state(), 1e-7)
+
+
+def test_time_range_shards(gpu_lib):
+    """Multi-GPU layout on one device: three band shards, each given the whole bank's response
+    (sum of the shards' responses) and a time share; their outputs (zeros outside their share)
+    sum to the restatement's mix, calls of any length; a setter clears the bank response and
+    the shards fall back to full-length outputs of their own bands (still summing right)."""
+    from huygens_amd import Filterbank
+    from huygens_amd.shard import set_time_shards
+    L = paths()
+    N = 300
+    fwd, back = resonant_coefficients(N, 0.999, 0.5)
+    _, o = make(2, N, fwd, back, oracle=True)
+    cuts = [(0, 128), (128, 100), (228, 72)]
+    shards = []
+    for b0, cnt in cuts:
+        s = Filterbank(2, N, 0.001, 0.001, shard=(b0, cnt))
+        s.tune_response(0, 1)
+        for n in range(N):
+            s.coefficients(n, fwd[n], back[n])
+        s.boost(np.ones(N))
+        s.open()
+        shards.append(s)
+    # the all-reduces by hand: the largest horizon, every shard's response over it, summed
+    for s in shards:
+        s.response(8192)
+    K_all = max(s.response_info()[0] for s in shards)
+    full = sum(s.response(K_all) for s in shards)
+    for r, s in enumerate(shards):
+        assert set_time_shards(s, r, 3, lambda h, full=full: full, lambda k, K_all=K_all: K_all)
+        assert s.response_info()[0] == K_all
+    rng = np.random.default_rng(11)
+    for n in [1500, 60000, 40000, 17000, 100003]:
+        x = rng.uniform(-1, 1, n)
+        ref = o.process(x)
+        outs = [s.process(x) for s in shards]
+        assert rel_err(sum(outs), ref) < TOL, n
+        if shards[0].last_path() == L.HZ_FB_PATH_RESPONSE:
+            act = [s.time_shard_info(n) for s in shards]
+            assert all(a[0] for a in act)
+            assert sum(a[2] for a in act) == n and act[0][1] == 0
+            for (a, f, c), y in zip(act, outs):   # zeros outside the share
+                assert not np.any(y[:f]) and not np.any(y[f + c:])
+    assert all(s.last_path() == L.HZ_FB_PATH_RESPONSE for s in shards)
+    for fb in shards + [o]:
+        fb.mix(5, 0.25)
+    for n in [3000, 70000, 30000]:
+        x = rng.uniform(-1, 1, n)
+        ref = o.process(x)
+        assert rel_err(sum(s.process(x) for s in shards), ref) < TOL
+    assert not shards[0].time_shard_info(1000)[0]
