@@ -165,6 +165,12 @@ struct hz_fb {
         double* d_Y = nullptr;           // [D][F] complex output spectra
         size_t Y_cap = 0;
         double* d_tw = nullptr;          // complex twiddles of the F-point transform
+        double* d_eg = nullptr;          // end-state GEMM operands (pin E, chunk 128)
+        size_t eg_cap = 0;
+        double* d_epart = nullptr;       // end-state GEMM block sums
+        size_t epart_cap = 0;
+        hipStream_t side = nullptr;      // the end-state GEMM runs beside the convolution
+        hipEvent_t ev_fork = nullptr, ev_join = nullptr;
         double* d_zero = nullptr;        // N O zeros (x history / start of the zero-start pass)
         size_t zero_cap = 0;
     } resp;
@@ -195,7 +201,18 @@ long fb_horizon(const hz_fb* h);           // samples K with ||M^K|| < 2^-64 for
 // x read as xzero) -> out[band][O]; zeros: N O zeros (the carry's start)
 int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xzero, const double* zeros,
                           double* out);
+int fb_lti_zero_start_end_on(hz_fb* h, const double* x, long len, const double* xzero, const double* zeros,
+                             double* out, hipStream_t st);
 int fb_lti_prepare_end(hz_fb* h, long len);   // its records for the current coefficients
+// end-state GEMM (chunk-128 records): operands Eg [fb_end_rows][fb_end_cols] (pin folded in),
+// then the zero-start states after the last K samples of [hist | x] (a call of n samples; n = 0:
+// hist itself) -> out[band][O], on stream st (part: [K / 8192][fb_end_cols] scratch)
+int fb_end_rows(int O);
+int fb_end_cols(int N, int O);
+int fb_end_operands(hz_fb* h, double* Eg);
+int fb_end_state_gemm(hz_fb* h, const double* hist, const double* x, long n, long K, const double* Eg, double* part,
+                      double* out, hipStream_t st);
+size_t fb_end_scratch(int N, int O, long K);
 // hz_fb_resp.hip (stationary engine)
 void fb_resp_init(hz_fb* h);
 void fb_resp_invalidate(hz_fb* h, bool coefficients);   // targets / coefficients changed

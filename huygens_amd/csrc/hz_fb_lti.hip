@@ -1076,6 +1076,162 @@ __global__ __launch_bounds__(256) void fb_lti_reduce_short_kernel(const double* 
     if (t + 1 < n) out[t + 1] = acc[1];
 }
 
+// ---- end-state GEMM (stationary engine, hz_fb_resp.hip) ---------------------------------
+// Zero-start band states at the end of a K-sample window v (K a multiple of 64 chunks of 128):
+//   S = sum_c M^(C-1-c) z_c,  z_c = pin E x_c  (chunk c's zero-state end state, as the state kernel)
+// as one chip-wide GEMM Z[chunk][band state] = X[chunk][tap] Eg[tap][band state] on the FP64
+// matrix cores -- workgroup = 16 bands x 64 chunks, E block in LDS, chunk windows read from L2 --
+// reduced in the workgroup with the chunk powers M^(63-c) (records' QC), then a per-band Horner
+// over the 64-chunk blocks with M^64.  Unlike the state kernel it keeps no prefix scan and no
+// sequential tile loop per band group, so it fills the chip for a short window and leaves most of
+// the LDS free (it runs beside the FFT kernels of the same call).
+constexpr int kEndL = 128;
+
+// Eg[t][bs] = pin_n E_n[k][t] (bs = n O + k), t < 4 ceil((L+O)/4), zero outside the bank
+template <int O>
+__global__ __launch_bounds__(256) void fb_end_eops_kernel(const double* __restrict__ rec, const double* __restrict__ pin,
+                                                          int nbands, int bs_tot, double* __restrict__ Eg) {
+    using R = RecL<O, kEndL>;
+    constexpr int XW = R::XW, KE4 = (XW + 3) / 4 * 4;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)KE4 * bs_tot) return;
+    const int t = (int)(i / bs_tot), bs = (int)(i % bs_tot), n = bs / O, k = bs % O;
+    double v = 0.0;
+    if (n < nbands && t < XW) {
+        const double* rb = rec + (long)n * R::SIZE;
+        v = pin[n] * (t < O ? rb[R::EH + k * O + t] : (t + k < XW ? rb[R::E0 + t + k] : 0.0));
+    }
+    Eg[i] = v;
+}
+
+// v(i) = last K samples of [hist | x] after a call of n samples: hist[n + i] or x[n + i - K]
+__device__ __forceinline__ double end_v(const double* hist, const double* x, long n, long K, long i) {
+    const long m = n + i;
+    return m < K ? hist[m] : x[m - K];
+}
+
+// chunk windows transposed, Xt[t][c] = v(c L - O + t) (0 before the window): the GEMM's A loads
+// then read 16 consecutive chunks of one tap (128 B) instead of 16 chunks 1 KiB apart
+template <int O>
+__global__ __launch_bounds__(256) void fb_end_xt_kernel(const double* __restrict__ hist, const double* __restrict__ x,
+                                                        long n, long K, int C, double* __restrict__ Xt) {
+    constexpr int XW = kEndL + O, KE4 = (XW + 3) / 4 * 4;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)KE4 * C) return;
+    const int t = (int)(i / C), c = (int)(i % C);
+    const long xi = (long)c * kEndL - O + t;
+    Xt[i] = (t < XW && xi >= 0) ? end_v(hist, x, n, K, xi) : 0.0;
+}
+
+// workgroup = BANDS bands (BS = BANDS O band states, BS / 16 column blocks) x 64 chunks (4 waves x
+// 16); the E block lives in LDS and is reused for the z tile after the MFMAs
+template <int O>
+constexpr int end_bands() { return O <= 2 ? 32 : 16; }
+
+template <int O>
+__global__ __launch_bounds__(256) void fb_end_gemm_kernel(const double* __restrict__ rec,
+                                                          const double* __restrict__ Xt, int C,
+                                                          const double* __restrict__ Eg, int bs_tot, int nbands,
+                                                          double* __restrict__ part) {
+    using R = RecL<O, kEndL>;
+    constexpr int XW = R::XW, KE = (XW + 3) / 4, BANDS = end_bands<O>(), BS = BANDS * O, NB = BS / 16;
+    extern __shared__ double end_lds[];   // E block [4 KE][BS + 1], then the z tile [64][BS + 1]
+    double (*eb)[BS + 1] = (double (*)[BS + 1])end_lds;
+    double (*zt)[BS + 1] = (double (*)[BS + 1])end_lds;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = blockIdx.x;
+    const int c0 = blockIdx.y * 64;
+    const int bs0 = g * BS;
+    // A operands (Xt rows, 16 consecutive chunks per tap) and the E block: every load of the
+    // thread issued before its first use
+    double av[KE];
+#pragma unroll
+    for (int q = 0; q < KE; ++q) av[q] = Xt[(long)(4 * q + (lane >> 4)) * C + c0 + 16 * wave + (lane & 15)];
+    constexpr int NEB = 4 * KE * BS, PT = (NEB + 255) / 256;
+    double ev[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+        const int e = threadIdx.x + 256 * i;
+        ev[i] = e < NEB ? Eg[(long)(e / BS) * bs_tot + bs0 + e % BS] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+        const int e = threadIdx.x + 256 * i;
+        if (e < NEB) eb[e / BS][e % BS] = ev[i];
+    }
+    __syncthreads();
+    hz_f64x4 acc[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[nb] = hz_f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < KE; ++q)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+            acc[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], eb[4 * q + (lane >> 4)][16 * nb + (lane & 15)],
+                                                           acc[nb], 0, 0, 0);
+    __syncthreads();   // the z tile overwrites the E block
+    // D: row = chunk 16 wave + (l >> 4) + 4 rr, col = band state 16 nb + (l & 15)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) zt[16 * wave + (lane >> 4) + 4 * rr][16 * nb + (lane & 15)] = acc[nb][rr];
+    __syncthreads();
+    // S_blk = sum_c M^(63 - c) z_c: thread (band b, sub) over chunks sub + SUBS i, then the subs
+    constexpr int SUBS = 256 / BANDS;   // 8 or 16
+    const int b = threadIdx.x / SUBS, sub = threadIdx.x % SUBS;
+    const int band = g * BANDS + b;
+    double S[O];
+#pragma unroll
+    for (int r = 0; r < O; ++r) S[r] = 0.0;
+    if (band < nbands) {
+        const double* rb = rec + (long)band * R::SIZE;
+#pragma unroll
+        for (int i = 0; i < 64 / SUBS; ++i) {
+            const int c = sub + SUBS * i;
+            const double* Qe = rb + R::QC + (63 - c) * O * O;
+#pragma unroll
+            for (int r = 0; r < O; ++r)
+#pragma unroll
+                for (int k = 0; k < O; ++k) S[r] = fma(Qe[r * O + k], zt[c][b * O + k], S[r]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < O; ++r)
+#pragma unroll
+        for (int off = SUBS / 2; off >= 1; off >>= 1) S[r] += __shfl_xor(S[r], off, SUBS);
+    if (sub == 0 && band < nbands)
+#pragma unroll
+        for (int r = 0; r < O; ++r) part[(long)blockIdx.y * bs_tot + (long)band * O + r] = S[r];
+}
+
+// S = sum over blocks in order of M^64 S + S_blk -> out[band][O]
+template <int O>
+__global__ __launch_bounds__(256) void fb_end_combine_kernel(const double* __restrict__ rec,
+                                                             const double* __restrict__ part, int nblk, int bs_tot,
+                                                             int nbands, double* __restrict__ out) {
+    using R = RecL<O, kEndL>;
+    const int band = blockIdx.x * blockDim.x + threadIdx.x;
+    if (band >= nbands) return;
+    const double* M = rec + (long)band * R::SIZE + R::QC + 64 * O * O;
+    double S[O];
+#pragma unroll
+    for (int r = 0; r < O; ++r) S[r] = 0.0;
+    for (int blk = 0; blk < nblk; ++blk) {
+        double T[O];
+#pragma unroll
+        for (int r = 0; r < O; ++r) {
+            double acc = part[(long)blk * bs_tot + (long)band * O + r];
+#pragma unroll
+            for (int k = 0; k < O; ++k) acc = fma(M[r * O + k], S[k], acc);
+            T[r] = acc;
+        }
+#pragma unroll
+        for (int r = 0; r < O; ++r) S[r] = T[r];
+    }
+#pragma unroll
+    for (int r = 0; r < O; ++r) out[(long)band * O + r] = S[r];
+}
+
 // ---- kernel selection -------------------------------------------
 typedef void (*CarryKernel)(const double*, const double*, double*, int, int, long);
 typedef void (*LtiKernel)(const double*, LtiArgs);
@@ -1639,6 +1795,11 @@ int fb_lti_prepare_end(hz_fb* h, long len) { return fb_prepare_lti(h, len % (64L
 // over m time segments when the bank alone leaves CUs idle (shards), joined by the carry kernel
 int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xzero, const double* zeros,
                           double* out) {
+    return fb_lti_zero_start_end_on(h, x, len, xzero, zeros, out, h->stream);
+}
+
+int fb_lti_zero_start_end_on(hz_fb* h, const double* x, long len, const double* xzero, const double* zeros,
+                             double* out, hipStream_t st) {
     const int O = h->order;
     const int gi = len % (64L * 128) == 0 ? 3 : 2;
     const long T = 64L * kLtiGeoms[gi].L;
@@ -1657,6 +1818,7 @@ int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xze
         const size_t sneed = (size_t)h->N * (m + 1) * O;
         if (sneed > h->seg_cap) {
             HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+            HZ_TRY_HIP(hipStreamSynchronize(st));
             if (h->d_seg) HZ_TRY_HIP(hipFree(h->d_seg));
             h->d_seg = nullptr;
             HZ_TRY_HIP(hipMalloc(&h->d_seg, sizeof(double) * sneed));
@@ -1687,17 +1849,72 @@ int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xze
         a.segstate = h->d_seg;
         a.nseg_state = (int)m + 1;
     }
-    hipLaunchKernelGGL(kend, dim3(G, (unsigned)m), dim3(64 * lti_waves(O)), lti_lds(O, gi, false), h->stream,
+    hipLaunchKernelGGL(kend, dim3(G, (unsigned)m), dim3(64 * lti_waves(O)), lti_lds(O, gi, false), st,
                        (const double*)set.d_rec, a);
     HZ_TRY_HIP(hipGetLastError());
     if (m > 1) {
         hipLaunchKernelGGL(pick_lti_carry(O, kLtiGeoms[gi].L), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0,
-                           h->stream, (const double*)set.d_rec, zeros, h->d_seg, h->N, (int)m + 1, seg_tiles);
+                           st, (const double*)set.d_rec, zeros, h->d_seg, h->N, (int)m + 1, seg_tiles);
         HZ_TRY_HIP(hipGetLastError());
         HZ_TRY_HIP(hipMemcpy2DAsync(out, sizeof(double) * O, h->d_seg + (size_t)m * O, sizeof(double) * O * (m + 1),
-                                    sizeof(double) * O, (size_t)h->N, hipMemcpyDeviceToDevice, h->stream));
+                                    sizeof(double) * O, (size_t)h->N, hipMemcpyDeviceToDevice, st));
     }
     return HZ_OK;
+}
+
+// end-state GEMM operands (chunk-128 records + pin) and the GEMM itself (hz_fb_resp.hip)
+int fb_end_rows(int O) { return (O + kEndL + 3) / 4 * 4; }
+int fb_end_cols(int N, int O) { return (N + 31) / 32 * 32 * O; }
+
+int fb_end_operands(hz_fb* h, double* Eg) {
+    const int O = h->order;
+    HZ_TRY(fb_prepare_lti(h, 3));
+    const int bs_tot = fb_end_cols(h->N, O);
+    const long cnt = (long)fb_end_rows(O) * bs_tot;
+    auto k = O == 1 ? fb_end_eops_kernel<1> : O == 2 ? fb_end_eops_kernel<2> : O == 3 ? fb_end_eops_kernel<3>
+                                                                                     : fb_end_eops_kernel<4>;
+    hipLaunchKernelGGL(k, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, h->stream,
+                       (const double*)h->lti_set[3].d_rec, (const double*)h->d_pin, h->N, bs_tot, Eg);
+    HZ_TRY_HIP(hipGetLastError());
+    return HZ_OK;
+}
+
+int fb_end_state_gemm(hz_fb* h, const double* hist, const double* x, long n, long K, const double* Eg, double* part,
+                      double* out, hipStream_t st) {
+    const int O = h->order;
+    if (O == 0 || K <= 0 || K % (64L * kEndL) != 0) {
+        hz::set_error("fb_end_state_gemm: order %d, window %ld (a positive multiple of 8192)", O, K);
+        return HZ_E_INVALID;
+    }
+    const int bs_tot = fb_end_cols(h->N, O);
+    const int nblk = (int)(K / (64L * kEndL));
+    const int C = (int)(K / kEndL);
+    const int bands = O <= 2 ? 32 : 16;
+    double* Xt = part + (size_t)nblk * bs_tot;   // [rows][C] after the block sums
+    auto kx = O == 1 ? fb_end_xt_kernel<1> : O == 2 ? fb_end_xt_kernel<2> : O == 3 ? fb_end_xt_kernel<3>
+                                                                                 : fb_end_xt_kernel<4>;
+    auto kg = O == 1 ? fb_end_gemm_kernel<1> : O == 2 ? fb_end_gemm_kernel<2> : O == 3 ? fb_end_gemm_kernel<3>
+                                                                                     : fb_end_gemm_kernel<4>;
+    auto kc = O == 1 ? fb_end_combine_kernel<1> : O == 2 ? fb_end_combine_kernel<2>
+                                                : O == 3 ? fb_end_combine_kernel<3> : fb_end_combine_kernel<4>;
+    const double* rec = h->lti_set[3].d_rec;
+    const long nxt = (long)fb_end_rows(O) * C;
+    hipLaunchKernelGGL(kx, dim3((unsigned)((nxt + 255) / 256)), dim3(256), 0, st, hist, x, n, K, C, Xt);
+    HZ_TRY_HIP(hipGetLastError());
+    const size_t lds = sizeof(double) * (size_t)fb_end_rows(O) * (bands * O + 1);
+    HZ_TRY(fb_set_lds_attr((const void*)kg));
+    hipLaunchKernelGGL(kg, dim3((unsigned)((h->N + bands - 1) / bands), (unsigned)nblk), dim3(256), lds, st, rec,
+                       (const double*)Xt, C, Eg, bs_tot, h->N, part);
+    HZ_TRY_HIP(hipGetLastError());
+    hipLaunchKernelGGL(kc, dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0, st, rec, (const double*)part, nblk,
+                       bs_tot, h->N, out);
+    HZ_TRY_HIP(hipGetLastError());
+    return HZ_OK;
+}
+
+// scratch doubles of fb_end_state_gemm for a window of K samples
+size_t fb_end_scratch(int N, int O, long K) {
+    return (size_t)(K / (64L * kEndL)) * fb_end_cols(N, O) + (size_t)fb_end_rows(O) * (K / kEndL);
 }
 
 }  // namespace hz_fbi

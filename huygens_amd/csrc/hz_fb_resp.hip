@@ -339,6 +339,14 @@ int resp_setup(hz_fb* h) {
     return HZ_OK;
 }
 
+int resp_state_mode() {
+    // (C2, 200 steps: 2 -> 0.0664 ms/step; 0 -> 0.0730, 1 -> 0.0776, 3 -> 0.0739: beside the
+    // convolution the state work slows the FFT and MAC kernels by as much as it hides)
+    static const int m = std::getenv("HZ_FB_RESP_STATE") ? std::atoi(std::getenv("HZ_FB_RESP_STATE")) : 2;
+    return m >= 0 && m <= 3 ? m : 2;
+}
+bool resp_gemm_states() { return resp_state_mode() == 1 || resp_state_mode() == 3; }
+
 // h and its partition spectra for the current coefficients / targets
 int resp_build_h(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
@@ -368,6 +376,13 @@ int resp_build_h(hz_fb* h) {
     hipLaunchKernelGGL(resp_hspec_kernel, dim3((unsigned)Q), dim3(kFftThreads), fft_lds(), h->stream,
                        (const double*)R.d_h, K, (const double2*)R.d_tw, (double2*)R.d_H);
     HZ_TRY_HIP(hipGetLastError());
+    if (resp_gemm_states()) {   // end-state GEMM operands for these coefficients and pre-amps
+        HZ_TRY(resp_alloc(&R.d_eg, &R.eg_cap, (size_t)hz_fbi::fb_end_rows(O) * hz_fbi::fb_end_cols(N, O)));
+        HZ_TRY(resp_alloc(&R.d_epart, &R.epart_cap, hz_fbi::fb_end_scratch(N, O, K)));
+        HZ_TRY(hz_fbi::fb_end_operands(h, R.d_eg));
+    } else {
+        HZ_TRY(hz_fbi::fb_lti_prepare_end(h, K));   // the state kernel's records, for LAZY too
+    }
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));   // pageable coefficient sources
     R.h_valid = true;
     return HZ_OK;
@@ -377,6 +392,8 @@ int resp_build_h(hz_fb* h) {
 // stationary call: after it (EAGER) or when needed (LAZY))
 int resp_states(hz_fb* h, double* ystate) {
     hz_fb::Resp& R = h->resp;
+    if (resp_gemm_states() && R.d_eg)   // operands of the coefficients the history ran with
+        return hz_fbi::fb_end_state_gemm(h, R.d_hist[R.hcur], nullptr, 0, R.K, R.d_eg, R.d_epart, ystate, h->stream);
     return hz_fbi::fb_lti_zero_start_end(h, R.d_hist[R.hcur], R.K, R.d_zero, R.d_zero, ystate);
 }
 
@@ -507,6 +524,31 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.xhist_next = h->d_xhist[h->xcur ^ 1];
     a.N = h->N;
     a.O = h->order;
+    // EAGER: the band states after this call (the last K samples of [hist | x]) do not depend on
+    // the convolution -- the end-state GEMM runs on a side stream beside it, joined at the end
+    const bool lazy = R.mode == HZ_FB_RESP_LAZY;
+    // where the band states are computed (HZ_FB_RESP_STATE, A/B): 2 (default) the chunk-128 state
+    // kernel in prepass mode after the convolution; 0 that kernel over x's last K samples on a
+    // side stream beside the convolution (calls n >= K; else as 2), 1 the end-state GEMM on the
+    // side stream, 3 the end-state GEMM after the convolution
+    const int smode = resp_state_mode() == 0 && n < K ? 2 : resp_state_mode();
+    const bool side = !lazy && (smode == 0 || smode == 1);
+    if (side) {
+        if (!R.side) {
+            HZ_TRY_HIP(hipStreamCreateWithFlags(&R.side, hipStreamNonBlocking));
+            HZ_TRY_HIP(hipEventCreateWithFlags(&R.ev_fork, hipEventDisableTiming));
+            HZ_TRY_HIP(hipEventCreateWithFlags(&R.ev_join, hipEventDisableTiming));
+        }
+        HZ_TRY_HIP(hipEventRecord(R.ev_fork, h->stream));
+        HZ_TRY_HIP(hipStreamWaitEvent(R.side, R.ev_fork, 0));
+        if (smode == 0)
+            HZ_TRY(hz_fbi::fb_lti_zero_start_end_on(h, d_in + (n - K), K, R.d_zero, R.d_zero,
+                                                    h->d_ystate[h->scur ^ 1], R.side));
+        else
+            HZ_TRY(hz_fbi::fb_end_state_gemm(h, R.d_hist[R.hcur], d_in, n, K, R.d_eg, R.d_epart,
+                                             h->d_ystate[h->scur ^ 1], R.side));
+        HZ_TRY_HIP(hipEventRecord(R.ev_join, R.side));
+    }
     hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kFftThreads), fft_lds(), h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     hipLaunchKernelGGL(resp_mac_kernel<kMacR>, dim3(kF / 256, (unsigned)((D + kMacR - 1) / kMacR)), dim3(256), 0,
@@ -517,11 +559,13 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     R.hcur ^= 1;   // the inverse kernel wrote the history after the call
     R.run = std::min(R.run + n, 1L << 60);
-    // end state: band states now (EAGER) or when needed (LAZY); smoothers and x history were
-    // written by the inverse kernel
-    if (R.mode == HZ_FB_RESP_LAZY) {
-        HZ_TRY(fb_lti_prepare_end(h, K));   // records of these coefficients for a later materialisation
+    // end state: band states joined from the side stream (EAGER) or computed when needed (LAZY);
+    // smoothers and x history were written by the inverse kernel
+    if (lazy) {
         R.implicit = true;
+    } else if (side) {
+        HZ_TRY_HIP(hipStreamWaitEvent(h->stream, R.ev_join, 0));
+        R.implicit = false;
     } else {
         HZ_TRY(resp_states(h, h->d_ystate[h->scur ^ 1]));
         R.implicit = false;
@@ -537,8 +581,13 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
 
 void fb_resp_free(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
-    for (double* p : {R.d_hist[0], R.d_hist[1], R.d_h, R.d_hpart, R.d_coef, R.d_zero, R.d_H, R.d_Z, R.d_Y, R.d_tw})
+    if (R.side) (void)hipStreamSynchronize(R.side);
+    for (double* p : {R.d_hist[0], R.d_hist[1], R.d_h, R.d_hpart, R.d_coef, R.d_zero, R.d_H, R.d_Z, R.d_Y, R.d_tw,
+                      R.d_eg, R.d_epart})
         if (p) (void)hipFree(p);
+    if (R.ev_fork) (void)hipEventDestroy(R.ev_fork);
+    if (R.ev_join) (void)hipEventDestroy(R.ev_join);
+    if (R.side) (void)hipStreamDestroy(R.side);
     R = hz_fb::Resp();
 }
 
