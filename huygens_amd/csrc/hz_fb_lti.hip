@@ -1395,7 +1395,7 @@ bool fb_converged(hz_fb* h) {
 // ||M^K||_inf < 2^-64 (long double, powers of M^4096); -1 if some band needs more than 2^18.
 // Segment start states then depend on the last K samples of input only (to 2^-64 of the
 // state), so the prepass can skip a segment's head.
-static long fb_lti_horizon(const hz_fb* h) {
+static long fb_lti_horizon(const hz_fb* h, long double bound = 0x1p-64L) {
     const int O = h->order;
     if (O == 0) return 0;
     typedef long double ld;
@@ -1429,7 +1429,7 @@ static long fb_lti_horizon(const hz_fb* h) {
                 nrm = std::max(nrm, r);
             }
             if (!(nrm == nrm)) break;   // NaN: unstable
-            if (nrm < 0x1p-64L) {
+            if (nrm < bound) {
                 kb = 4096L * it;
                 break;
             }
@@ -1786,7 +1786,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
     return HZ_OK;
 }
 
-long fb_horizon(const hz_fb* h) { return fb_lti_horizon(h); }
+long fb_horizon(const hz_fb* h, int log2_bound) { return fb_lti_horizon(h, ldexpl(1.0L, log2_bound)); }
 
 int fb_lti_prepare_end(hz_fb* h, long len) { return fb_prepare_lti(h, len % (64L * 128) == 0 ? 3 : 2); }
 
@@ -1811,9 +1811,11 @@ int fb_lti_zero_start_end_on(hz_fb* h, const double* x, long len, const double* 
     hz_fb::LtiRecSet& set = h->lti_set[gi];
     const int G = (h->N + lti_waves(O) - 1) / lti_waves(O);
     const long ntiles = len / T;
+    // equal segments only (the carry powers M by the segment length): the largest m <= the cap
+    // that divides the tile count
     long m = std::min<long>(ntiles, std::max<long>(1, h->target_groups / G));
-    const long seg_tiles = (ntiles + m - 1) / m;
-    m = (ntiles + seg_tiles - 1) / seg_tiles;
+    while (ntiles % m != 0) --m;
+    const long seg_tiles = ntiles / m;
     if (m > 1) {
         const size_t sneed = (size_t)h->N * (m + 1) * O;
         if (sneed > h->seg_cap) {

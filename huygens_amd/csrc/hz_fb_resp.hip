@@ -148,6 +148,8 @@ __device__ __forceinline__ double resp_u(const RespArgs& a, long m) {
 }
 
 // Z_j = FFT(W_{j+1} + i W_{j+1+D}), W_i = u[(i-1)P, (i+1)P)
+// (ABL, diagnostics HZ_FB_RESP_ABL=1: no FFT passes -- wrong results, timed by rocprof)
+template <int ABL = 0>
 __global__ __launch_bounds__(kFftThreads) void resp_fwd_kernel(RespArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* re = lds;
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(kFftThreads) void resp_fwd_kernel(RespArgs a) {
         im[hz::pad16(k)] = vi[i];
     }
     __syncthreads();
-    hz::fft_fwd_lead<kRmax>(re, im, kLgF, T, true);
+    if constexpr (ABL == 0) hz::fft_fwd_lead<kRmax>(re, im, kLgF, T, true);
     double2* z = a.Z + j * kF;
     for (int q = threadIdx.x; q < kF; q += blockDim.x) z[q] = make_double2(re[hz::pad16(q)], im[hz::pad16(q)]);
 }
@@ -236,6 +238,7 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
 }
 
 // out[bP + r] = Re IFFT(Y_b)[P + r], out[(b + D)P + r] = Im ...
+template <int ABL = 0>
 __global__ __launch_bounds__(kFftThreads) void resp_inv_kernel(RespArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* re = lds;
@@ -255,7 +258,7 @@ __global__ __launch_bounds__(kFftThreads) void resp_inv_kernel(RespArgs a) {
         im[hz::pad16(q)] = v[i].y;
     }
     __syncthreads();
-    hz::fft_inv_tail<kRmax>(re, im, kLgF, T, true);
+    if constexpr (ABL == 0) hz::fft_inv_tail<kRmax>(re, im, kLgF, T, true);
     for (int r = threadIdx.x; r < kP; r += blockDim.x) {
         const long t0 = b * kP + r, t1 = (b + a.D) * kP + r;
         if (t0 < a.n_out) a.out[a.off + t0] = re[hz::pad16(kP + r)];
@@ -309,9 +312,12 @@ int resp_alloc(double** p, size_t* cap, size_t need) {
 int resp_setup(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     if (R.K == -2) {
-        R.K = hz_fbi::fb_horizon(h);
-        // a whole number of the chunk-128 state kernel's 8192-sample tiles (the end-state pass;
-        // older inputs reach the state below 2^-64 of it)
+        // ||M^K|| < 2^-53 (env HZ_FB_RESP_HORIZON_LOG2, e.g. -64): older inputs reach a band state
+        // below one unit in the last place of it, and the bank response's tail below 2^-53 of its
+        // l1 norm; then a whole number of the chunk-128 state kernel's 8192-sample tiles
+        static const int lb = std::getenv("HZ_FB_RESP_HORIZON_LOG2") ? std::atoi(std::getenv("HZ_FB_RESP_HORIZON_LOG2"))
+                                                                      : -53;
+        R.K = hz_fbi::fb_horizon(h, lb);
         if (R.K >= 0) R.K = std::max<long>(8192, (R.K + 8191) / 8192 * 8192);
         R.h_valid = false;
         R.run = 0;
@@ -333,7 +339,8 @@ int resp_setup(hz_fb* h) {
         }
         HZ_TRY_HIP(hipMalloc((void**)&R.d_tw, sizeof(double2) * tw.size()));
         HZ_TRY_HIP(hipMemcpy(R.d_tw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice));
-        for (const void* k : {(const void*)resp_hspec_kernel, (const void*)resp_fwd_kernel, (const void*)resp_inv_kernel})
+        for (const void* k : {(const void*)resp_hspec_kernel, (const void*)resp_fwd_kernel<0>, (const void*)resp_inv_kernel<0>,
+                              (const void*)resp_fwd_kernel<1>, (const void*)resp_inv_kernel<1>})
             HZ_TRY(hz_fbi::fb_set_lds_attr(k));
     }
     return HZ_OK;
@@ -549,12 +556,15 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
                                              h->d_ystate[h->scur ^ 1], R.side));
         HZ_TRY_HIP(hipEventRecord(R.ev_join, R.side));
     }
-    hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kFftThreads), fft_lds(), h->stream, a);
+    static const int abl = std::getenv("HZ_FB_RESP_ABL") ? std::atoi(std::getenv("HZ_FB_RESP_ABL")) : 0;
+    hipLaunchKernelGGL(abl == 1 ? resp_fwd_kernel<1> : resp_fwd_kernel<0>, dim3((unsigned)nz), dim3(kFftThreads),
+                       fft_lds(), h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     hipLaunchKernelGGL(resp_mac_kernel<kMacR>, dim3(kF / 256, (unsigned)((D + kMacR - 1) / kMacR)), dim3(256), 0,
                        h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, D);
     HZ_TRY_HIP(hipGetLastError());
-    hipLaunchKernelGGL(resp_inv_kernel, dim3((unsigned)D), dim3(kFftThreads), fft_lds(), h->stream, a);
+    hipLaunchKernelGGL(abl == 1 ? resp_inv_kernel<1> : resp_inv_kernel<0>, dim3((unsigned)D), dim3(kFftThreads),
+                       fft_lds(), h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     R.hcur ^= 1;   // the inverse kernel wrote the history after the call
