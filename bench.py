@@ -271,30 +271,22 @@ def main():
             o.close()
 
     S = args.samples
-    gbuf, glist = None, None
+    gbuf = None   # ShareGather of the time-sharded stationary calls
     rng = np.random.default_rng(1234)
     x = torch.from_numpy(rng.uniform(-1, 1, S).astype(np.float32).astype(np.float64)).to(dev)
     y = torch.empty_like(x)
 
     def step():
-        nonlocal gbuf, glist
+        nonlocal gbuf
         fb.process_device(x.data_ptr(), y.data_ptr(), S)
         if world > 1:
             active, first, count = fb.time_shard_info(S) if tshard else (False, 0, S)
             if active and fb.last_path() == HZ_FB_PATH_RESPONSE:
                 # shares are runs of whole 2048-sample blocks: gather fixed-size slots to rank 0
-                slot = -(-(-(-S // 2048)) // world) * 2048
                 if gbuf is None:
-                    gbuf = torch.zeros(slot, dtype=torch.float64, device=dev)
-                    glist = [torch.empty_like(gbuf) for _ in range(world)] if rank == 0 else None
-                gbuf[:count].copy_(y[first:first + count])
-                dist.gather(gbuf, glist, dst=0)
-                if rank == 0:
-                    B = -(-S // 2048)
-                    for r in range(world):
-                        f = min(S, B * r // world * 2048)
-                        c = min(S, B * (r + 1) // world * 2048) - f
-                        y[f:f + c].copy_(glist[r][:c])
+                    from huygens_amd.shard import ShareGather
+                    gbuf = ShareGather(S, rank, world, y)
+                gbuf(y, dist)
             else:
                 dist.reduce(y, dst=0, op=dist.ReduceOp.SUM)
 

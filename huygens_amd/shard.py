@@ -33,3 +33,36 @@ def set_time_shards(fb, rank: int, world: int, all_reduce_sum, all_reduce_max) -
     fb.set_bank_response(full)
     fb.set_time_shard(rank, world)
     return True
+
+
+def time_share(rank: int, world: int, n: int, block: int = 2048) -> tuple[int, int]:
+    """(first sample, count) of rank's share of a time-sharded stationary call of n samples: a
+    run of whole `block`-sample output blocks (the split of hz_fb_time_shard_info)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("rank must be in [0, world)")
+    nb = -(-n // block)
+    lo = min(n, nb * rank // world * block)
+    hi = min(n, nb * (rank + 1) // world * block)
+    return lo, hi - lo
+
+
+class ShareGather:
+    """Assembles the ranks' time shares of a call's output on rank 0: every rank copies its share
+    into a fixed-size slot (the largest share), one gather moves the slots to rank 0, which copies
+    them into place.  `y` is the call's output buffer on every rank (torch tensor)."""
+
+    def __init__(self, n: int, rank: int, world: int, like, block: int = 2048):
+        import torch
+        self.n, self.rank, self.world = n, rank, world
+        self.shares = [time_share(r, world, n, block) for r in range(world)]
+        self.slot = max(c for _, c in self.shares)
+        self.buf = torch.zeros(self.slot, dtype=like.dtype, device=like.device)
+        self.bufs = [torch.empty_like(self.buf) for _ in range(world)] if rank == 0 else None
+
+    def __call__(self, y, dist):
+        f, c = self.shares[self.rank]
+        self.buf[:c].copy_(y[f:f + c])
+        dist.gather(self.buf, self.bufs, dst=0)
+        if self.rank == 0:
+            for (f, c), b in zip(self.shares, self.bufs):
+                y[f:f + c].copy_(b[:c])

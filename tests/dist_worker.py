@@ -59,6 +59,19 @@ def _delaybank(b0, cnt, N, x):
     return b.process(x).sum(axis=0)   # unscaled line sum; / N after the reduce
 
 
+def _timeshare(rank, world, N, x):
+    """Time-sharded stationary calls: each rank holds the WHOLE bank's output (the oracle stands
+    in for the convolution with the whole-bank response) only on its share, zeros elsewhere; the
+    shares are assembled on rank 0 by the same ShareGather bench.py uses over RCCL."""
+    import torch
+    from huygens_amd.shard import ShareGather, time_share
+    full = _filterbank(0, N, N, x)
+    f, c = time_share(rank, world, len(x), block=256)
+    y = torch.zeros(len(x), dtype=torch.float64)
+    y[f:f + c] = torch.from_numpy(full[f:f + c])
+    return y, full, ShareGather(len(x), rank, world, y, block=256)
+
+
 def main():
     import torch
     import torch.distributed as dist
@@ -66,9 +79,20 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     kind, out_path = sys.argv[1], sys.argv[2]
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    N = {"filterbank": 96, "oscbank": 50, "bowl": 40, "delaybank": 6}[kind]
+    N = {"filterbank": 96, "oscbank": 50, "bowl": 40, "delaybank": 6, "timeshare": 96}[kind]
     n = 3000
     x = np.random.default_rng(1).uniform(-1, 1, n).astype(np.float32).astype(np.float64)
+    if kind == "timeshare":
+        import torch.distributed as dist_
+        y, full, g = _timeshare(rank, world, 96, x)
+        g(y, dist_)
+        if rank == 0:
+            err = float(np.max(np.abs(y.numpy() - full)) / np.max(np.abs(full)))
+            with open(out_path, "w") as fh:
+                json.dump({"err": err, "shares": g.shares}, fh)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     b0, cnt = shard_of(rank, world, N)
     fn = {"filterbank": lambda b, c: _filterbank(b, c, N, x), "oscbank": lambda b, c: _oscbank(b, c, N, n),
           "bowl": lambda b, c: _bowl(b, c, N, n), "delaybank": lambda b, c: _delaybank(b, c, N, x)}[kind]

@@ -49,6 +49,24 @@ def test_world3_uneven(tmp_path):
     assert [c for _, c in res["shards"]] == [32, 32, 32]
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_time_shares_gather(world, tmp_path):
+    """Stationary calls split by time (bench.py at N > 1): the ranks' shares, gathered to rank 0
+    in fixed-size slots, reassemble the whole call (gloo standing in for RCCL)."""
+    res = _run("timeshare", world, tmp_path)
+    assert res["err"] == 0.0
+    shares = res["shares"]
+    assert shares[0][0] == 0 and sum(c for _, c in shares) == 3000
+    assert all(f1 == f0 + c0 for (f0, c0), (f1, _) in zip(shares, shares[1:]))
+
+
+def test_time_share_split():
+    from huygens_amd.shard import time_share
+    assert [time_share(r, 8, 480000) for r in (0, 7)] == [(0, 59392), (419840, 60160)]
+    assert sum(time_share(r, 3, 100003)[1] for r in range(3)) == 100003
+    assert [time_share(r, 3, 100) for r in range(3)] == [(0, 0), (0, 0), (0, 100)]   # one block: the last rank
+
+
 def test_shard_of():
     assert [shard_of(r, 3, 10) for r in range(3)] == [(0, 4), (4, 3), (7, 3)]
     assert [shard_of(r, 8, 4096)[1] for r in range(8)] == [512] * 8

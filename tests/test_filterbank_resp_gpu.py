@@ -238,7 +238,7 @@ def test_time_range_shards(gpu_lib):
     sum to the restatement's mix, calls of any length; a setter clears the bank response and
     the shards fall back to full-length outputs of their own bands (still summing right)."""
     from huygens_amd import Filterbank
-    from huygens_amd.shard import set_time_shards
+    from huygens_amd.shard import set_time_shards, time_share
     L = paths()
     N = 300
     fwd, back = resonant_coefficients(N, 0.999, 0.5)
@@ -270,6 +270,7 @@ def test_time_range_shards(gpu_lib):
         if shards[0].last_path() == L.HZ_FB_PATH_RESPONSE:
             act = [s.time_shard_info(n) for s in shards]
             assert all(a[0] for a in act)
+            assert [(f, c) for _, f, c in act] == [time_share(r, 3, n) for r in range(3)]
             assert sum(a[2] for a in act) == n and act[0][1] == 0
             for (a, f, c), y in zip(act, outs):   # zeros outside the share
                 assert not np.any(y[:f]) and not np.any(y[f + c:])
