@@ -248,7 +248,11 @@ def main():
             t = torch.tensor([k], dtype=torch.int64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             return int(t.item())
-        tshard = set_time_shards(fb, rank, world, all_reduce_sum, all_reduce_max)
+        try:
+            tshard = set_time_shards(fb, rank, world, all_reduce_sum, all_reduce_max)
+        except Exception as e:  # noqa: BLE001 -- fall back to band shards + reduce
+            print(f"rank {rank}: time shards not set ({e}); band shards + reduce", file=sys.stderr)
+            tshard = False
     elif args.emulate_world > 1 and not args.general and args.response != 0:
         # (1 GPU, diagnostics) rank 0 of a time-sharded job: the other shards' handles exist only
         # to sum the whole bank's response

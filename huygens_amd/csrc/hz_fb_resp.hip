@@ -444,7 +444,9 @@ bool fb_resp_eligible(hz_fb* h, long n, bool conv) {
     // sample): measured crossover near 300 band-equivalents per sample of history + call
     static const long per_env = std::getenv("HZ_FB_RESP_BANDS") ? std::atol(std::getenv("HZ_FB_RESP_BANDS")) : 256;
     const long per = R.bands_per_sample >= 0 ? R.bands_per_sample : per_env;
-    return (double)h->N * n >= (double)per * (double)(R.K + n);
+    // time-range shards decide on the whole bank (every rank takes the same engine)
+    const double bands = R.over_valid ? (double)h->N_total : (double)h->N;
+    return bands * n >= (double)per * (double)(R.K + n);
 }
 
 int fb_resp_materialize(hz_fb* h) {
