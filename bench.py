@@ -104,9 +104,9 @@ def fb_executed_flops(lti, L=32, O=2, N=N_BANDS):
 def resp_step_flops(K, S, N, O=2):
     """FP64 flops of one stationary-engine call (hz_fb_resp.hip) of S samples, horizon K:
     packed window FFTs (Q + D - 1) and output FFTs (D) at 5 F log2 F each, the partition MACs
-    (8 flops per complex MAC, D x F x Q), and the end-state pass (the chunk-64 state kernel in
-    prepass mode over the K history samples: E 2 O 4 ceil((64+O)/4) / 64 + scan 2 8 O^2 / 64
-    flops per band-sample)."""
+    (8 flops per complex MAC, D x F x Q), and the end-state pass (the chunk-128 state kernel in
+    prepass mode over the K history samples: E 2 O 4 ceil((128+O)/4) / 128 + the weighted chunk
+    sum 2 (O^2 + 6 O) / 128 flops per band-sample)."""
     import math
     P, F, lgF = 2048, 4096, 12
     Q = K // P
@@ -114,7 +114,7 @@ def resp_step_flops(K, S, N, O=2):
     D = -(-B // 2)
     fft = 5.0 * F * lgF
     conv = (Q + D - 1) * fft + D * F * Q * 8.0 + D * fft
-    state = N * K * (2.0 * O * 4 * math.ceil((64 + O) / 4) / 64 + 2.0 * 8 * O * O / 64)
+    state = N * K * (2.0 * O * 4 * math.ceil((128 + O) / 4) / 128 + 2.0 * (O * O + 6 * O) / 128)
     return conv, state
 
 
@@ -408,8 +408,8 @@ def main():
             cpu = cpu_baseline(fwd, back)
         kernels = (("fb_lti_kernel", "fb_lti_gemm", "fb_lti_reduce", "fb_lti_seg_carry", "fb_lti_sum",
                     "fb_lti_xrows") if lti
-                   else ("resp_fwd_kernel", "resp_mac_kernel", "resp_inv_kernel", "resp_hist_kernel",
-                         "resp_finish_kernel", "fb_lti_kernel<2, 64, 1", "fb_lti_seg_carry") if resp
+                   else ("resp_fwd_kernel", "resp_mac_kernel", "resp_inv_kernel", "fb_lti_kernel<2, 128, 1",
+                         "fb_lti_seg_carry") if resp
                    else ("fb_mix_kernel", "fb_reduce"))
         traffic, traffic_detail = None, "skipped"
         if not args.no_traffic and world == 1 and S == SAMPLES_PER_STEP:
@@ -443,9 +443,10 @@ def main():
                          "traffic_detail": traffic_detail,
                          "algorithmic_bytes_per_launch": (16 * S + 120 * cnt) * args.steps / max(1, launches),
                          "launches_per_step": launches / max(1, args.steps),
-                         "kernel": ("stationary engine step: resp_fwd_kernel + resp_mac_kernel<16> + resp_inv_kernel "
-                                    "(partitioned FFT convolution) + resp_hist_kernel + fb_lti_kernel<2,64,SEGEND> "
-                                    "(band states over the %d-sample horizon) + resp_finish_kernel" % horizon) if resp else
+                         "kernel": ("stationary engine step: resp_fwd_kernel + resp_mac_kernel<8> + resp_inv_kernel "
+                                    "(partitioned FFT convolution, history and smoother upkeep) + "
+                                    "fb_lti_kernel<2,128,SEGEND> (band states over the %d-sample horizon)" % horizon)
+                                   if resp else
                                    (("LTI engine step: fb_lti_kernel<2,%d,STATE>%s + "
                                      "fb_lti_gemm_pp_kernel<%d> + fb_lti_sum_kernel (+ segment prepass)"
                                      % (chunk, " (+ x rows)" if chunk >= 128 else " + fb_lti_xrows_kernel", chunk))

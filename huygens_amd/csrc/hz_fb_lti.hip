@@ -381,6 +381,11 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
             qb[e] = wb ? r[R::QC + eb * O * O + e] : 0.0;
         }
     }
+    // MODE_SEGEND needs only the tile's end state: sum_l M^(63-l) pin z_l (lane l = chunk l), a
+    // weighted wave sum instead of the prefix scan
+    double qr[O * O];
+#pragma unroll
+    for (int e = 0; e < O * O; ++e) qr[e] = MODE == MODE_SEGEND ? r[R::QC + (63 - lane) * O * O + e] : 0.0;
 
     // MFMA B operands of this wave's work items: E items hold E[tap][bs] (tap = 4q + (l >> 4),
     // bs = 16 sb + (l & 15)), mix items K[bs][j] (bs = 4q + (l >> 4), j = 16 jb + (l & 15));
@@ -684,6 +689,40 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         }
     };
     auto phase_s = [&](int it, long t0) {
+        if constexpr (MODE == MODE_SEGEND) {
+            if (it < ntiles) {   // S' = M^64 S + sum_l M^(63-l) pin z_l
+                const double* z = zb + (it & 1) * BSP * kZRow;
+                double zz[O], v[O];
+#pragma unroll
+                for (int k = 0; k < O; ++k) zz[k] = z[(wave * O + k) * kZRow + lane];
+#pragma unroll
+                for (int k = 0; k < O; ++k) {
+                    v[k] = 0.0;
+#pragma unroll
+                    for (int c = 0; c < O; ++c) v[k] = fma(qr[k * O + c], zz[c], v[k]);
+                }
+#pragma unroll
+                for (int k = 0; k < O; ++k) {   // inclusive wave sum: lane 63 holds the total
+                    v[k] += dpp_dm<kDppRowShr + 1, 0xf>(v[k]);
+                    v[k] += dpp_dm<kDppRowShr + 2, 0xf>(v[k]);
+                    v[k] += dpp_dm<kDppRowShr + 4, 0xf>(v[k]);
+                    v[k] += dpp_dm<kDppRowShr + 8, 0xf>(v[k]);
+                    v[k] += dpp_dm<kDppRowBcast15, 0xa>(v[k]);
+                    v[k] += dpp_dm<kDppRowBcast31, 0xc>(v[k]);
+                }
+                double Sn[O];
+#pragma unroll
+                for (int k = 0; k < O; ++k) {
+                    double sn = readlane_d(v[k], 63);
+#pragma unroll
+                    for (int c = 0; c < O; ++c) sn = fma(r[R::PS + 4 * O * O + k * O + c], S[c], sn);
+                    Sn[k] = sn;
+                }
+#pragma unroll
+                for (int k = 0; k < O; ++k) S[k] = Sn[k];
+            }
+            return;
+        }
         if (it < ntiles) {
             // ---- (S) tile it: this wave's band ----
             const double* z = zb + (it & 1) * BSP * kZRow;

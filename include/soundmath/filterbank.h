@@ -70,6 +70,8 @@ public:
         detail::check(hz_fb_process_tv(h_.get(), in, out, n, HZ_FB_TV_RESONANT, freqs, R),
                       "Filterbank::process_resonant");
     }
+    // (new) the stationary engine: HZ_FB_RESP_OFF / _EAGER (default) / _LAZY
+    void response(int mode) { detail::check(hz_fb_set_response(h_.get(), mode), "Filterbank::response"); }
     hz_fb* native() const { return h_.get(); }
 
 private:
