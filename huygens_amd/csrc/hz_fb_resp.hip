@@ -237,6 +237,84 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
         if (b0 + r < D) Y[(long)(b0 + r) * kF + q] = make_double2(ar[r], ai[r]);
 }
 
+// The same MACs with the operands shared through LDS: workgroup = 64 bins x 4 waves, wave w owns
+// output blocks b0 + w R .. + R - 1 of the workgroup's 4 R; the Qp partition spectra and the
+// 4 R + Qp window spectra of the 64 bins are staged once (24 + 57 KB at C2) instead of read by
+// every thread from L2, then each thread runs the register ring of resp_mac_kernel from LDS.
+template <int R>
+__global__ __launch_bounds__(256) void resp_mac_lds_kernel(const double2* __restrict__ H, const double2* __restrict__ Z,
+                                                           double2* __restrict__ Y, int Q, int Qp, int D, int zrows) {
+    extern __shared__ __attribute__((aligned(16))) double mac_lds[];
+    double2* hs = (double2*)mac_lds;   // [Qp][64]
+    double2* zs = hs + Qp * 64;        // [4 R + Qp][64]
+    const int bin = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int q = blockIdx.x * 64 + bin;
+    const int bw = blockIdx.y * 4 * R;            // first output block of the workgroup
+    const int nz = 4 * R + Qp;                    // window rows bw .. bw + nz - 1 (clamped)
+    // staging in batches of 8 loads per thread issued before their stores (few memory latencies)
+    constexpr int SB = 8;
+    for (int i0 = threadIdx.x; i0 < Qp * 64; i0 += SB * 256) {
+        double2 v[SB];
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+            const int i = i0 + k * 256;
+            v[k] = i < Qp * 64 ? H[(long)(i >> 6) * kF + blockIdx.x * 64 + (i & 63)] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int k = 0; k < SB; ++k)
+            if (i0 + k * 256 < Qp * 64) hs[i0 + k * 256] = v[k];
+    }
+    for (int i0 = threadIdx.x; i0 < nz * 64; i0 += SB * 256) {
+        double2 v[SB];
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+            const int i = i0 + k * 256;
+            const int row = min(bw + (i >> 6), zrows - 1);
+            v[k] = i < nz * 64 ? Z[(long)row * kF + blockIdx.x * 64 + (i & 63)] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int k = 0; k < SB; ++k)
+            if (i0 + k * 256 < nz * 64) zs[i0 + k * 256] = v[k];
+    }
+    __syncthreads();
+    // thread's outputs b = bw + w R + r; Y_b = sum_p H_p Z_{b+Q-1-p}: local row w R + r + Q - 1 - p
+    double ar[R], ai[R], zr[R], zi[R];
+    const int base = w * R + Q - 1;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        ar[r] = ai[r] = 0.0;
+        const double2 z = zs[(base + r) * 64 + bin];
+        zr[r] = z.x;
+        zi[r] = z.y;
+    }
+    for (int p0 = 0; p0 < Qp; p0 += R) {
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const int p = p0 + u;
+            const double2 hv = hs[p * 64 + bin];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int sl = ((r - u) % R + R) % R;
+                ar[r] = fma(hv.x, zr[sl], ar[r]);
+                ar[r] = fma(-hv.y, zi[sl], ar[r]);
+                ai[r] = fma(hv.x, zi[sl], ai[r]);
+                ai[r] = fma(hv.y, zr[sl], ai[r]);
+            }
+            const int zrow = base - p - 1;   // < 0 only past Q (zero H rows)
+            const double2 z = zs[(zrow > 0 ? zrow : 0) * 64 + bin];
+            const int sl = ((-(u + 1)) % R + R) % R;
+            zr[sl] = z.x;
+            zi[sl] = z.y;
+        }
+    }
+    (void)q;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int b = bw + w * R + r;
+        if (b < D) Y[(long)b * kF + blockIdx.x * 64 + bin] = make_double2(ar[r], ai[r]);
+    }
+}
+
 // out[bP + r] = Re IFFT(Y_b)[P + r], out[(b + D)P + r] = Im ...
 template <int ABL = 0>
 __global__ __launch_bounds__(kFftThreads) void resp_inv_kernel(RespArgs a) {
@@ -498,7 +576,8 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     const long B = std::max<long>(1, (n_out + kP - 1) / kP);
     const int D = (int)((B + 1) / 2);
     const int nz = Q + D - 1;
-    const int zrows = (D + kMacR - 1) / kMacR * kMacR + Q;   // the MAC's last register window
+    // rows the MACs may read: the last register window (padded to 4 R output blocks, Qp partitions)
+    const int zrows = (D + 4 * kMacR - 1) / (4 * kMacR) * (4 * kMacR) + Qp;
     if ((size_t)zrows * kF * 2 > R.Z_cap) {
         HZ_TRY(resp_alloc(&R.d_Z, &R.Z_cap, (size_t)zrows * kF * 2));
         HZ_TRY_HIP(hipMemsetAsync(R.d_Z, 0, sizeof(double2) * (size_t)zrows * kF, h->stream));
@@ -562,8 +641,19 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     hipLaunchKernelGGL(abl == 1 ? resp_fwd_kernel<1> : resp_fwd_kernel<0>, dim3((unsigned)nz), dim3(kFftThreads),
                        fft_lds(), h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
-    hipLaunchKernelGGL(resp_mac_kernel<kMacR>, dim3(kF / 256, (unsigned)((D + kMacR - 1) / kMacR)), dim3(256), 0,
-                       h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, D);
+    // MAC straight from L2 (default) or through LDS (HZ_FB_RESP_MAC=1; C2: 8.4 vs 8.0 us -- the
+    // L2 reads were not its bound)
+    static const bool mac_lds = std::getenv("HZ_FB_RESP_MAC") && std::getenv("HZ_FB_RESP_MAC")[0] == '1';
+    const size_t mac_bytes = sizeof(double2) * 64 * (size_t)(Qp + 4 * kMacR + Qp);
+    if (mac_lds && mac_bytes <= 160 * 1024) {
+        HZ_TRY(fb_set_lds_attr((const void*)resp_mac_lds_kernel<kMacR>));
+        hipLaunchKernelGGL(resp_mac_lds_kernel<kMacR>, dim3(kF / 64, (unsigned)((D + 4 * kMacR - 1) / (4 * kMacR))),
+                           dim3(256), mac_bytes, h->stream, (const double2*)R.d_H, (const double2*)R.d_Z,
+                           (double2*)R.d_Y, Q, Qp, D, zrows);
+    } else {
+        hipLaunchKernelGGL(resp_mac_kernel<kMacR>, dim3(kF / 256, (unsigned)((D + kMacR - 1) / kMacR)), dim3(256), 0,
+                           h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, D);
+    }
     HZ_TRY_HIP(hipGetLastError());
     hipLaunchKernelGGL(abl == 1 ? resp_inv_kernel<1> : resp_inv_kernel<0>, dim3((unsigned)D), dim3(kFftThreads),
                        fft_lds(), h->stream, a);
