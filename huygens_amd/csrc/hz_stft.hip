@@ -237,20 +237,34 @@ __global__ __launch_bounds__(kFrameThreads) void stft_frame_kernel(StftArgs a) {
     const long f = frame_at(a, fl);
     if constexpr (MODE != 2) {
         const long off = frame_start(f, a.laps, a.stride, N) - a.T0 + (N - 1);
-        for (int k = threadIdx.x; k < N; k += blockDim.x) {
-            const long u = off + k;   // position in [history (N-1) | block input]
-            double vr, vi = 0.0;
-            if (u < N - 1) {
-                vr = a.hr[u];
-                if (a.hi) vi = a.hi[u];
-            } else {
-                vr = a.inr[u - (N - 1)];
-                if (a.hi && a.ini) vi = a.ini[u - (N - 1)];
+        constexpr int PB = 8;   // batches of 8 samples per thread, loads before stores
+        for (int k0 = threadIdx.x; k0 < N; k0 += PB * blockDim.x) {
+            double vr[PB], vi[PB], w[PB];
+#pragma unroll
+            for (int i = 0; i < PB; ++i) {
+                const int k = k0 + i * blockDim.x;
+                const long u = off + k;   // position in [history (N-1) | block input]
+                vr[i] = vi[i] = w[i] = 0.0;
+                if (k < N) {
+                    if (u < N - 1) {
+                        vr[i] = a.hr[u];
+                        if (a.hi) vi[i] = a.hi[u];
+                    } else {
+                        vr[i] = a.inr[u - (N - 1)];
+                        if (a.hi && a.ini) vi[i] = a.ini[u - (N - 1)];
+                    }
+                    w[i] = a.win[k];
+                }
             }
-            const double w = a.win[k];
-            const int e = hz::pad16(k);
-            re[e] = w * vr;   // fourier.h:110-112: window * real, window * imag
-            im[e] = w * vi;
+#pragma unroll
+            for (int i = 0; i < PB; ++i) {
+                const int k = k0 + i * blockDim.x;
+                if (k < N) {
+                    const int e = hz::pad16(k);
+                    re[e] = w[i] * vr[i];   // fourier.h:110-112: window * real, window * imag
+                    im[e] = w[i] * vi[i];
+                }
+            }
         }
     } else {
         const double2* sp = a.spec + (long)fl * N;
@@ -397,14 +411,29 @@ __global__ __launch_bounds__(kFrameThreads) void stft_pair_kernel(StftArgs a, lo
     const long f1 = two ? frame_at(a, 2L * pl + 1) : f0;
     const long off0 = frame_start(f0, a.laps, a.stride, N) - a.T0 + (N - 1);
     const long off1 = two ? frame_start(f1, a.laps, a.stride, N) - a.T0 + (N - 1) : 0;
-    for (int k = threadIdx.x; k < N; k += blockDim.x) {
-        const long u0 = off0 + k, u1 = off1 + k;   // positions in [history (N-1) | block input]
-        const double v0 = u0 < N - 1 ? a.hr[u0] : a.inr[u0 - (N - 1)];
-        const double v1 = two ? (u1 < N - 1 ? a.hr[u1] : a.inr[u1 - (N - 1)]) : 0.0;
-        const double w = a.win[k];
-        const int e = hz::pad16(k);
-        re[e] = w * v0;   // fourier.h:110-112, real input
-        im[e] = w * v1;
+    // batches of 8 samples per thread: every global load of a batch issued before its LDS stores
+    // (one memory latency per batch instead of one per sample; a 4096-point frame is one batch)
+    constexpr int PB = 8;
+    for (int k0 = threadIdx.x; k0 < N; k0 += PB * blockDim.x) {
+        double v0[PB], v1[PB], w[PB];
+#pragma unroll
+        for (int i = 0; i < PB; ++i) {
+            const int k = k0 + i * blockDim.x;
+            const bool ok = k < N;
+            const long u0 = off0 + k, u1 = off1 + k;   // positions in [history (N-1) | block input]
+            v0[i] = ok ? (u0 < N - 1 ? a.hr[u0] : a.inr[u0 - (N - 1)]) : 0.0;
+            v1[i] = ok && two ? (u1 < N - 1 ? a.hr[u1] : a.inr[u1 - (N - 1)]) : 0.0;
+            w[i] = ok ? a.win[k] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < PB; ++i) {
+            const int k = k0 + i * blockDim.x;
+            if (k < N) {
+                const int e = hz::pad16(k);
+                re[e] = w[i] * v0[i];   // fourier.h:110-112, real input
+                im[e] = w[i] * v1[i];
+            }
+        }
     }
     __syncthreads();
     hz::fft_fwd_lead<RMAX>(re, im, lg, T, true);
