@@ -403,8 +403,19 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         }
         return 0.0;
     };
-    if constexpr (X1) {
-        for (int e = threadIdx.x; e < 4 * KE * BSP; e += 64 * W) eb[(e / BSP) * EBR + e % BSP] = e_val(e / BSP, e % BSP);
+    if constexpr (X1) {   // every record / pin load of the thread issued before its LDS stores
+        constexpr int NEF = 4 * KE * BSP, PTE = (NEF + 64 * W - 1) / (64 * W);
+        double ev[PTE];
+#pragma unroll
+        for (int i = 0; i < PTE; ++i) {
+            const int e = (int)threadIdx.x + i * 64 * W;
+            ev[i] = e < NEF ? e_val(e / BSP, e % BSP) : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < PTE; ++i) {
+            const int e = (int)threadIdx.x + i * 64 * W;
+            if (e < NEF) eb[(e / BSP) * EBR + e % BSP] = ev[i];
+        }
     }
 #pragma unroll
     for (int v = 0; v < (X1 ? 0 : IPE); ++v) {
