@@ -149,8 +149,9 @@ __device__ __forceinline__ double resp_u(const RespArgs& a, long m) {
 
 // Z_j = FFT(W_{j+1} + i W_{j+1+D}), W_i = u[(i-1)P, (i+1)P)
 // (ABL, diagnostics HZ_FB_RESP_ABL=1: no FFT passes -- wrong results, timed by rocprof)
-template <int ABL = 0>
-__global__ __launch_bounds__(kFftThreads) void resp_fwd_kernel(RespArgs a) {
+template <int ABL = 0, int RM = kRmax>
+__global__ __launch_bounds__(kF >> RM) void resp_fwd_kernel(RespArgs a) {
+    constexpr int kFftThreads = kF >> RM;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* re = lds;
     double* im = lds + hz::padded_len(kF);
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(kFftThreads) void resp_fwd_kernel(RespArgs a) {
         im[hz::pad16(k)] = vi[i];
     }
     __syncthreads();
-    if constexpr (ABL == 0) hz::fft_fwd_lead<kRmax>(re, im, kLgF, T, true);
+    if constexpr (ABL == 0) hz::fft_fwd_lead<RM>(re, im, kLgF, T, true);
     double2* z = a.Z + j * kF;
     for (int q = threadIdx.x; q < kF; q += blockDim.x) z[q] = make_double2(re[hz::pad16(q)], im[hz::pad16(q)]);
 }
@@ -316,8 +317,9 @@ __global__ __launch_bounds__(256) void resp_mac_lds_kernel(const double2* __rest
 }
 
 // out[bP + r] = Re IFFT(Y_b)[P + r], out[(b + D)P + r] = Im ...
-template <int ABL = 0>
-__global__ __launch_bounds__(kFftThreads) void resp_inv_kernel(RespArgs a) {
+template <int ABL = 0, int RM = kRmax>
+__global__ __launch_bounds__(kF >> RM) void resp_inv_kernel(RespArgs a) {
+    constexpr int kFftThreads = kF >> RM;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* re = lds;
     double* im = lds + hz::padded_len(kF);
@@ -336,7 +338,7 @@ __global__ __launch_bounds__(kFftThreads) void resp_inv_kernel(RespArgs a) {
         im[hz::pad16(q)] = v[i].y;
     }
     __syncthreads();
-    if constexpr (ABL == 0) hz::fft_inv_tail<kRmax>(re, im, kLgF, T, true);
+    if constexpr (ABL == 0) hz::fft_inv_tail<RM>(re, im, kLgF, T, true);
     for (int r = threadIdx.x; r < kP; r += blockDim.x) {
         const long t0 = b * kP + r, t1 = (b + a.D) * kP + r;
         if (t0 < a.n_out) a.out[a.off + t0] = re[hz::pad16(kP + r)];
@@ -638,8 +640,16 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         HZ_TRY_HIP(hipEventRecord(R.ev_join, R.side));
     }
     static const int abl = std::getenv("HZ_FB_RESP_ABL") ? std::atoi(std::getenv("HZ_FB_RESP_ABL")) : 0;
-    hipLaunchKernelGGL(abl == 1 ? resp_fwd_kernel<1> : resp_fwd_kernel<0>, dim3((unsigned)nz), dim3(kFftThreads),
-                       fft_lds(), h->stream, a);
+    // (A/B) HZ_FB_RESP_RADIX=4: radix-4 passes on 1024 threads per transform instead of radix 8 on 512
+    static const bool r4 = std::getenv("HZ_FB_RESP_RADIX") && std::atoi(std::getenv("HZ_FB_RESP_RADIX")) == 4;
+    if (r4) {
+        HZ_TRY(fb_set_lds_attr((const void*)resp_fwd_kernel<0, 2>));
+        HZ_TRY(fb_set_lds_attr((const void*)resp_inv_kernel<0, 2>));
+    }
+    typedef void (*RespFftKernel)(RespArgs);
+    const RespFftKernel kfwd = r4 ? resp_fwd_kernel<0, 2> : abl == 1 ? resp_fwd_kernel<1> : resp_fwd_kernel<0>;
+    const RespFftKernel kinv = r4 ? resp_inv_kernel<0, 2> : abl == 1 ? resp_inv_kernel<1> : resp_inv_kernel<0>;
+    hipLaunchKernelGGL(kfwd, dim3((unsigned)nz), dim3(r4 ? kF >> 2 : kFftThreads), fft_lds(), h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     // MAC straight from L2 (default) or through LDS (HZ_FB_RESP_MAC=1; C2: 8.4 vs 8.0 us -- the
     // L2 reads were not its bound)
@@ -655,8 +665,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
                            h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, D);
     }
     HZ_TRY_HIP(hipGetLastError());
-    hipLaunchKernelGGL(abl == 1 ? resp_inv_kernel<1> : resp_inv_kernel<0>, dim3((unsigned)D), dim3(kFftThreads),
-                       fft_lds(), h->stream, a);
+    hipLaunchKernelGGL(kinv, dim3((unsigned)D), dim3(r4 ? kF >> 2 : kFftThreads), fft_lds(), h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     R.hcur ^= 1;   // the inverse kernel wrote the history after the call
