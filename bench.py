@@ -11,9 +11,13 @@ input already resident in HBM; the result is identical to 469 x {1024-sample blo
 (tests/test_filterbank_gpu.py::test_block_split_and_per_sample).  A streaming figure
 (one call per 1024-sample block) is reported beside it.
 
-Multi-GPU (torchrun, one process per GPU): the 4096 bands are split contiguously
-over ranks (strong scaling: total work fixed); each rank mixes its shard and the
-partial mixes are summed to rank 0 with an RCCL reduce over xGMI every step.
+Multi-GPU (torchrun, one process per GPU): the 4096 bands are split contiguously over ranks
+(each rank keeps its shard's band states).  Once the bank is stationary the
+stream is split by TIME: a step is one call of N x 10 s and every rank outputs its 10 s from the
+shared input with a K-sample halo, convolving with the whole bank's response (summed over the
+band shards by one all-reduce at setup) -- no data-path collective, weak scaling (`--gather`
+collects the shares on rank 0 inside the step).  Per-band calls (before the bank is stationary)
+sum the band shards' partial mixes to rank 0 with an RCCL reduce.
 """
 from __future__ import annotations
 
@@ -186,6 +190,8 @@ def main():
     ap.add_argument("--general", action="store_true", help="force the general engine (no converged fast path)")
     ap.add_argument("--response", type=int, default=-1,
                     help="stationary engine: 0 off (per-band engines only), 1 eager (default), 2 lazy")
+    ap.add_argument("--gather", action="store_true",
+                    help="N > 1, time-sharded stationary calls: gather the shares on rank 0 inside each step")
     ap.add_argument("--side-steps", type=int, default=50,
                     help="timed steps of the side figures (per-band engine, lazy stationary engine)")
     ap.add_argument("--target-groups", type=int, default=0, help="(tuning) workgroups wanted per launch")
@@ -274,8 +280,13 @@ def main():
         for o in others:
             o.close()
 
-    S = args.samples
-    gbuf = None   # ShareGather of the time-sharded stationary calls
+    # Time-sharded stationary calls partition the stream: each rank produces the final output of
+    # its run of blocks from the shared input (a K-sample halo, no exchange), so a step at N > 1 is
+    # a call of N x 10 s with 10 s of output per rank -- weak scaling, no data-path collective
+    # (the per-band warmup calls still sum band shards with one reduce)
+    P_t = (world if world > 1 else max(1, args.emulate_world)) if tshard else 1
+    S = args.samples * P_t
+    gbuf = None   # ShareGather (--gather: collect the shares on rank 0 inside the step)
     rng = np.random.default_rng(1234)
     x = torch.from_numpy(rng.uniform(-1, 1, S).astype(np.float32).astype(np.float64)).to(dev)
     y = torch.empty_like(x)
@@ -286,11 +297,13 @@ def main():
         if world > 1:
             active, first, count = fb.time_shard_info(S) if tshard else (False, 0, S)
             if active and fb.last_path() == HZ_FB_PATH_RESPONSE:
-                # shares are runs of whole 2048-sample blocks: gather fixed-size slots to rank 0
-                if gbuf is None:
-                    from huygens_amd.shard import ShareGather
-                    gbuf = ShareGather(S, rank, world, y)
-                gbuf(y, dist)
+                # every rank holds the final samples of its share: nothing to exchange (--gather
+                # collects them on rank 0 inside the step: fixed-size slots, one gather)
+                if args.gather:
+                    if gbuf is None:
+                        from huygens_amd.shard import ShareGather
+                        gbuf = ShareGather(S, rank, world, y)
+                    gbuf(y, dist)
             else:
                 dist.reduce(y, dst=0, op=dist.ReduceOp.SUM)
 
@@ -396,12 +409,15 @@ def main():
         step_ms = eng_ms_max   # max over ranks
         launch_avg_s = (step_ms / 1e3) / max(1, launches)
         band_samples_per_launch = cnt * S * args.steps / max(1, launches)
+        if resp:   # this GPU's outputs: its time share of the whole bank (all of it at N = 1)
+            band_samples_per_launch = N_BANDS * (S // P_t) * args.steps / max(1, launches)
         flops_per_launch = FLOPS_PER_BAND_SAMPLE * band_samples_per_launch
         achieved = flops_per_launch / launch_avg_s / 1e12 if launch_avg_s > 0 else None
         xflops = fb_executed_flops(lti, chunk, N=cnt)
-        if resp:   # the stationary engine's flops per call, spread over the call's band-samples
-            conv_f, state_f = resp_step_flops(horizon, S, cnt)
-            xflops = (conv_f + state_f) / (cnt * S)
+        if resp:   # the stationary engine's flops per call (its share's convolution, its bands'
+            # states), spread over the share's band-samples
+            conv_f, state_f = resp_step_flops(horizon, S // P_t, cnt)
+            xflops = (conv_f + state_f) / (N_BANDS * (S // P_t))
         executed = xflops * band_samples_per_launch / launch_avg_s / 1e12 if launch_avg_s > 0 else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -424,16 +440,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if P_t > 1 and resp else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic white noise uniform[-1,1) (float32 -> double), seed 1234",
             "config": {"workload": "C2 Filterbank<double>(order 2, 4096 bands), resonant band-pass "
-                                   "f_i=0.5(i+1)SR/4096 R=0.999, boost 1 + open, k_p=0.1 k_g=1",
-                       "samples_per_step": S, "block": 1024, "bands": N_BANDS,
+                                   "f_i=0.5(i+1)SR/4096 R=0.999, boost 1 + open, k_p=0.1 k_g=1"
+                                   + (f", {P_t} x 10 s per step split by time" if P_t > 1 and resp else ""),
+                       "samples_per_step": S, "samples_per_gpu": S // P_t, "block": 1024, "bands": N_BANDS,
                        "bands_per_gpu": cnt,
-                       "parallelism": (f"stationary calls split by time x{world} (whole-bank response, one "
-                                       f"all-reduce at setup), band states sharded x{world}, RCCL gather"
+                       "parallelism": (f"stream split by time x{P_t}: each GPU outputs 10 s of the N x 10 s "
+                                       f"call from the shared input with a {horizon}-sample halo (whole-bank "
+                                       f"response, one all-reduce at setup), band states sharded x{P_t}; no "
+                                       f"data-path collective" + (" (+ gather to rank 0)" if args.gather else "")
                                        if tshard and resp else f"bands sharded x{world}, RCCL reduce")},
             "engine": "stationary (bank response convolution, eager band states)" if resp
                       else "per-band LTI" if lti else "per-band general",
