@@ -173,6 +173,46 @@ def pmc_traffic(kernels=("fb_mix_kernel",), extra=()):
                                      "summed over " + ", ".join(kernels)}
 
 
+class _HostDist:
+    """(rehearsal only, HZ_BENCH_REHEARSAL=1: several ranks on one GPU over gloo) the collectives
+    bench.py issues, run through host copies of the device tensors."""
+
+    def __init__(self, d):
+        self.d = d
+        self.ReduceOp = d.ReduceOp
+
+    def _via(self, fn, t, **kw):
+        c = t.detach().cpu()
+        r = fn(c, **kw)
+        t.copy_(c)
+        return r
+
+    def all_reduce(self, t, op=None):
+        return self._via(self.d.all_reduce, t, op=op or self.d.ReduceOp.SUM)
+
+    def reduce(self, t, dst=0, op=None):
+        return self._via(self.d.reduce, t, dst=dst, op=op or self.d.ReduceOp.SUM)
+
+    def gather(self, t, lst, dst=0):
+        c = t.detach().cpu()
+        lc = [torch_empty_like(c) for _ in lst] if lst is not None else None
+        self.d.gather(c, lc, dst=dst)
+        if lst is not None:
+            for a, b in zip(lst, lc):
+                a.copy_(b)
+
+    def barrier(self):
+        self.d.barrier()
+
+    def destroy_process_group(self):
+        self.d.destroy_process_group()
+
+
+def torch_empty_like(t):
+    import torch
+    return torch.empty_like(t)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -209,7 +249,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and os.environ.get("HZ_BENCH_REHEARSAL") == "1":
+        # (rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, gloo via host copies)
+        local = 0
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+        dist = _HostDist(dist)
+    elif world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
