@@ -98,6 +98,24 @@ __device__ __forceinline__ void load_tw(double2* T, const double2* __restrict__ 
     for (int k = threadIdx.x; k < hz::twc_len(kLgF); k += blockDim.x) T[k] = tw[k];
 }
 
+// the compact twiddle table in two register loads per thread (threads >= twc_len / 2), issued
+// with the data loads and stored with them: one memory latency before the first pass, not two
+template <int NT>
+struct TwRegs {
+    static_assert(2 * NT >= hz::twc_len(kLgF), "two twiddles per thread");
+    double2 a, b;
+    __device__ __forceinline__ void load(const double2* __restrict__ tw) {
+        constexpr int TL = hz::twc_len(kLgF);
+        a = threadIdx.x < TL ? tw[threadIdx.x] : make_double2(0.0, 0.0);
+        b = threadIdx.x + NT < TL ? tw[threadIdx.x + NT] : make_double2(0.0, 0.0);
+    }
+    __device__ __forceinline__ void store(double2* T) const {
+        constexpr int TL = hz::twc_len(kLgF);
+        if (threadIdx.x < TL) T[threadIdx.x] = a;
+        if (threadIdx.x + NT < TL) T[threadIdx.x + NT] = b;
+    }
+};
+
 // Partition spectra H_p = FFT(h[pP, (p+1)P) zero-padded to F) / F (the inverse is unnormalised;
 // 1/F is a power of two), bins in the transforms' storage (bit-reversed) order
 __global__ __launch_bounds__(kFftThreads) void resp_hspec_kernel(const double* __restrict__ h, long K,
@@ -156,11 +174,12 @@ __global__ __launch_bounds__(kF >> RM) void resp_fwd_kernel(RespArgs a) {
     double* re = lds;
     double* im = lds + hz::padded_len(kF);
     double2* T = (double2*)(im + hz::padded_len(kF));
-    load_tw(T, a.tw);
     const long j = blockIdx.x;
     const long m0 = j * kP, m1 = (j + a.D) * kP;
-    // every load of the thread issued before the first LDS store (one memory latency, not 8)
+    // every load of the thread (twiddles included) issued before the first LDS store
     constexpr int PT = kF / kFftThreads;
+    TwRegs<kFftThreads> tr;
+    tr.load(a.tw);
     double vr[PT], vi[PT];
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
@@ -168,6 +187,7 @@ __global__ __launch_bounds__(kF >> RM) void resp_fwd_kernel(RespArgs a) {
         vr[i] = resp_u(a, m0 + k);
         vi[i] = resp_u(a, m1 + k);
     }
+    tr.store(T);
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
         const int k = threadIdx.x + i * kFftThreads;
@@ -324,13 +344,15 @@ __global__ __launch_bounds__(kF >> RM) void resp_inv_kernel(RespArgs a) {
     double* re = lds;
     double* im = lds + hz::padded_len(kF);
     double2* T = (double2*)(im + hz::padded_len(kF));
-    load_tw(T, a.tw);
     const long b = blockIdx.x;
     const double2* y = a.Y + b * kF;
     constexpr int PT = kF / kFftThreads;
+    TwRegs<kFftThreads> tr;
+    tr.load(a.tw);
     double2 v[PT];
 #pragma unroll
     for (int i = 0; i < PT; ++i) v[i] = y[threadIdx.x + i * kFftThreads];
+    tr.store(T);
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
         const int q = threadIdx.x + i * kFftThreads;
