@@ -282,3 +282,38 @@ def test_time_range_shards(gpu_lib):
         ref = o.process(x)
         assert rel_err(sum(s.process(x) for s in shards), ref) < TOL
     assert not shards[0].time_shard_info(1000)[0]
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+def test_stream_and_per_sample_after_stationary(gpu_lib, lazy):
+    """After stationary calls: a per-sample coefficient stream (hz_fb_process_tv reads the band
+    states, then leaves new coefficients), per-sample operator()/tick() and long calls again --
+    every path picks up the exact band states (LAZY: materialised on the way)."""
+    L = paths()
+    N = 256
+    fwd, back = resonant_coefficients(N, 0.999, 0.5)
+    g, o = make(2, N, fwd, back, mode=L.HZ_FB_RESP_LAZY if lazy else L.HZ_FB_RESP_EAGER)
+    rng = np.random.default_rng(21)
+    for n in [2000, 50000, 30000]:
+        x = rng.uniform(-1, 1, n)
+        assert rel_err(g.process(x), o.process(x)) < TOL
+    assert g.last_path() == L.HZ_FB_PATH_RESPONSE
+    assert g.response_info()[2] == lazy
+    # resonant retuning stream over 3000 samples (Subtractive ALLINONE), order 2
+    x = rng.uniform(-1, 1, 3000)
+    fr = np.tile(np.linspace(200.0, 4000.0, N), (3000, 1)) * (1.0 + 0.1 * np.sin(np.arange(3000) / 300.0))[:, None]
+    assert rel_err(g.process_tv(x, 1, fr, 0.999), o.process_tv(x, 1, fr, 0.999)) < TOL
+    assert not g.response_info()[2]
+    # the stream left new coefficients: long calls run per-band, then stationary again
+    for n in [40000, 60000, 20000]:
+        x = rng.uniform(-1, 1, n)
+        assert rel_err(g.process(x), o.process(x)) < TOL
+    assert g.last_path() == L.HZ_FB_PATH_RESPONSE
+    # per-sample operator() / tick() after a stationary call
+    x = rng.uniform(-1, 1, 40)
+    ref = o.process(x)
+    got = []
+    for v in x:
+        got.append(g(v))
+        g.tick()
+    assert rel_err(np.array(got), ref) < TOL
