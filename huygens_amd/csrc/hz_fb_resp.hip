@@ -535,6 +535,16 @@ void fb_resp_setter(hz_fb* h) {
     h->resp.over_valid = false;
 }
 
+// the cost model alone: would a call of n samples run stationary (given the history)?
+static bool resp_worth(const hz_fb* h, long n) {
+    const hz_fb::Resp& R = h->resp;
+    static const long per_env = std::getenv("HZ_FB_RESP_BANDS") ? std::atol(std::getenv("HZ_FB_RESP_BANDS")) : 256;
+    const long per = R.bands_per_sample >= 0 ? R.bands_per_sample : per_env;
+    // time-range shards decide on the whole bank (every rank takes the same engine)
+    const double bands = R.over_valid ? (double)h->N_total : (double)h->N;
+    return bands * n >= (double)per * (double)(R.K + n);
+}
+
 bool fb_resp_eligible(hz_fb* h, long n, bool conv) {
     hz_fb::Resp& R = h->resp;
     if (R.mode == HZ_FB_RESP_OFF || !conv || h->order == 0 || h->dist_id != HZ_DIST_NONE ||
@@ -544,11 +554,7 @@ bool fb_resp_eligible(hz_fb* h, long n, bool conv) {
     if (R.K <= 0 || R.run < R.K) return false;
     // the bank engines cost ~N per sample, this one ~(K + n) / n (Q MACs + two FFT passes per
     // sample): measured crossover near 300 band-equivalents per sample of history + call
-    static const long per_env = std::getenv("HZ_FB_RESP_BANDS") ? std::atol(std::getenv("HZ_FB_RESP_BANDS")) : 256;
-    const long per = R.bands_per_sample >= 0 ? R.bands_per_sample : per_env;
-    // time-range shards decide on the whole bank (every rank takes the same engine)
-    const double bands = R.over_valid ? (double)h->N_total : (double)h->N;
-    return bands * n >= (double)per * (double)(R.K + n);
+    return resp_worth(h, n);
 }
 
 int fb_resp_materialize(hz_fb* h) {
@@ -567,7 +573,9 @@ int fb_resp_track(hz_fb* h, const double* d_in, long n, bool conv) {
         return HZ_OK;
     }
     if (R.K == -2) HZ_TRY(resp_setup(h));
-    if (R.K <= 0) {
+    // no history for banks / call lengths the engine would not take (small banks keep their
+    // per-band calls free of the upkeep launch)
+    if (R.K <= 0 || !resp_worth(h, n)) {
         R.run = 0;
         return HZ_OK;
     }
