@@ -1851,7 +1851,11 @@ int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xze
 int fb_lti_zero_start_end_on(hz_fb* h, const double* x, long len, const double* xzero, const double* zeros,
                              double* out, hipStream_t st) {
     const int O = h->order;
-    const int gi = len % (64L * 128) == 0 ? 3 : 2;
+    // (A/B) HZ_FB_END_L = 32 / 64: chunk of the zero-start pass (default 128 when len allows);
+    // HZ_FB_END_M: time segments per band group (default: fill the CUs)
+    static const int env_l = std::getenv("HZ_FB_END_L") ? std::atoi(std::getenv("HZ_FB_END_L")) : 0;
+    static const int env_m = std::getenv("HZ_FB_END_M") ? std::atoi(std::getenv("HZ_FB_END_M")) : 0;
+    const int gi = env_l == 32 ? 1 : env_l == 64 ? 2 : len % (64L * 128) == 0 ? 3 : 2;
     const long T = 64L * kLtiGeoms[gi].L;
     if (O == 0 || len <= 0 || len % T != 0) {
         hz::set_error("fb_lti_zero_start_end: order %d, length %ld (a positive multiple of 4096)", O, len);
@@ -1863,7 +1867,7 @@ int fb_lti_zero_start_end_on(hz_fb* h, const double* x, long len, const double* 
     const long ntiles = len / T;
     // equal segments only (the carry powers M by the segment length): the largest m <= the cap
     // that divides the tile count
-    long m = std::min<long>(ntiles, std::max<long>(1, h->target_groups / G));
+    long m = std::min<long>(ntiles, std::max<long>(1, env_m > 0 ? env_m : h->target_groups / G));
     while (ntiles % m != 0) --m;
     const long seg_tiles = ntiles / m;
     if (m > 1) {
