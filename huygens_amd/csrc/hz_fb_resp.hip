@@ -1,10 +1,10 @@
 // hz_fb_resp.hip -- the stationary Filterbank<double> engine (bank response convolution).
 //
 // Once a bank has run converged (pre = pin, gain = gin: hz_fb_lti.hip) with unchanged
-// coefficients for K samples, K = its horizon (||M^K||_inf < 2^-64 for every band's state
-// transition M, fb_lti_horizon), every band's state is the zero-state response of the last K
-// input samples to 2^-64 of itself, and the bank's mixdown (src/filterbank.h:130,178-179) is ONE
-// linear filter of the input:
+// coefficients for K samples, K = its horizon (||M^K||_inf < 2^-53 for every band's state
+// transition M, fb_lti_horizon, rounded up to 8192), every band's state is the zero-state response
+// of the last K input samples to below an ulp of itself, and the bank's mixdown
+// (src/filterbank.h:130,178-179) is ONE linear filter of the input:
 //     out[t] = sum_n gin_n y_n[t] = sum_{tau < K} h[tau] x[t - tau],   h[tau] = sum_n gin_n r_n[tau]
 // with r_n band n's impulse response at pre = pin_n.  A call then runs as a uniformly partitioned
 // overlap-save convolution on FP64 FFTs (P = 2048-sample partitions, 4096-point transforms):
@@ -18,10 +18,12 @@
 // reference's own recurrence, summed in a fixed order).
 //
 // The per-band state is kept exact: the last K inputs are the handle's history (updated by every
-// converged long call, whatever engine ran it), and the band states at the call end are their
-// zero-state response over those K samples (the LTI state kernel in its prepass mode,
-// fb_lti_zero_start_end) -- after every call (HZ_FB_RESP_EAGER, default) or only when a later call,
-// get_state or tick needs them (HZ_FB_RESP_LAZY).
+// converged long call the engine could take, whatever engine ran it), and the band states at the
+// call end are their zero-state response over those K samples (the chunk-128 LTI state kernel in
+// its prepass mode, fb_lti_zero_start_end) -- after every call (HZ_FB_RESP_EAGER, default) or only
+// when a later call, get_state, tick or a setter needs them (HZ_FB_RESP_LAZY).
+// Multi-GPU: time-range shards (hz_fb_set_bank_response + hz_fb_set_time_shard) convolve one
+// rank's run of output blocks with the whole bank's response; DESIGN.md 3.6 and 5.
 #include <cstdlib>
 
 #include "hz_fb_impl.h"
