@@ -36,6 +36,14 @@ constexpr int kLgF = kLgP + 1, kF = 2 * kP;    // transform size
 constexpr int kRmax = 3;                       // radix-8 passes (hz_fft.h)
 constexpr int kFftThreads = kF >> kRmax;       // 512: one radix-8 group per thread
 constexpr int kMacR = 8;                       // output blocks per MAC thread (partitions padded to it)
+// (A/B) HZ_FB_RESP_MAC_R = 4 / 8 / 16 output blocks per MAC thread
+int mac_r() {
+    static const int r = [] {
+        const int v = std::getenv("HZ_FB_RESP_MAC_R") ? std::atoi(std::getenv("HZ_FB_RESP_MAC_R")) : kMacR;
+        return v == 4 || v == 16 ? v : kMacR;
+    }();
+    return r;
+}
 constexpr long kMinCall = 16384;               // shortest call that keeps the history
 
 size_t fft_lds() { return sizeof(double) * 2 * (size_t)hz::padded_len(kF) + sizeof(double2) * hz::twc_len(kLgF); }
@@ -466,7 +474,7 @@ int resp_build_h(hz_fb* h) {
     const long K = R.K;
     const int G = (N + 63) / 64;
     const int Q = (int)(K / kP);
-    const int Qp = (Q + kMacR - 1) / kMacR * kMacR;   // zero spectra past Q (the MAC's unguarded blocks)
+    const int Qp = (Q + mac_r() - 1) / mac_r() * mac_r();   // zero spectra past Q (the MAC's unguarded blocks)
     HZ_TRY(resp_alloc(&R.d_coef, &R.coef_cap, (size_t)N * (2 * O + 1)));
     HZ_TRY_HIP(hipMemcpyAsync(R.d_coef, h->F.data(), sizeof(double) * N * (O + 1), hipMemcpyHostToDevice, h->stream));
     HZ_TRY_HIP(hipMemcpyAsync(R.d_coef + (size_t)N * (O + 1), h->B.data(), sizeof(double) * N * O,
@@ -597,7 +605,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     HZ_TRY(resp_build_h(h));
     const long K = R.K;
     const int Q = (int)(K / kP);
-    const int Qp = (Q + kMacR - 1) / kMacR * kMacR;
+    const int Qp = (Q + mac_r() - 1) / mac_r() * mac_r();
     // time-range shard (hz_fb_set_time_shard, with the whole bank's response): this rank's run of
     // whole output blocks
     long off = 0, n_out = n;
@@ -611,7 +619,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     const int D = (int)((B + 1) / 2);
     const int nz = Q + D - 1;
     // rows the MACs may read: the last register window (padded to 4 R output blocks, Qp partitions)
-    const int zrows = (D + 4 * kMacR - 1) / (4 * kMacR) * (4 * kMacR) + Qp;
+    const int zrows = (D + 64 - 1) / 64 * 64 + Qp;   // >= every MAC variant's last window
     if ((size_t)zrows * kF * 2 > R.Z_cap) {
         HZ_TRY(resp_alloc(&R.d_Z, &R.Z_cap, (size_t)zrows * kF * 2));
         HZ_TRY_HIP(hipMemsetAsync(R.d_Z, 0, sizeof(double2) * (size_t)zrows * kF, h->stream));
@@ -693,7 +701,9 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
                            dim3(256), mac_bytes, h->stream, (const double2*)R.d_H, (const double2*)R.d_Z,
                            (double2*)R.d_Y, Q, Qp, D, zrows);
     } else {
-        hipLaunchKernelGGL(resp_mac_kernel<kMacR>, dim3(kF / 256, (unsigned)((D + kMacR - 1) / kMacR)), dim3(256), 0,
+        const int mr = mac_r();
+        auto km = mr == 4 ? resp_mac_kernel<4> : mr == 16 ? resp_mac_kernel<16> : resp_mac_kernel<8>;
+        hipLaunchKernelGGL(km, dim3(kF / 256, (unsigned)((D + mr - 1) / mr)), dim3(256), 0,
                            h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, D);
     }
     HZ_TRY_HIP(hipGetLastError());
