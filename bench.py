@@ -53,40 +53,100 @@ def shard_of(rank, world, N=N_BANDS):
     return _shard_of(rank, world, N)
 
 
-def cpu_baseline(fwd, back, seconds_target=1.5):
-    """The oracle (C restatement, -O2, no FMA contraction) on the host cores: bands
-    split over threads (ctypes releases the GIL), one Filterbank per thread."""
+def cpu_info():
+    """Host CPU model (/proc/cpuinfo), logical CPUs of the machine and of this process."""
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
+
+
+def native_oracle():
+    """The oracle's C sources built -O3 -march=native -ffp-contract=off for THIS host (SURVEY.md
+    8(d)), into a temporary directory; None when gcc is unavailable (then the in-tree -O3
+    generic build is timed and the line says so)."""
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    cc = shutil.which("gcc")
+    if not cc:
+        return None
+    d = tempfile.mkdtemp(prefix="hz_oracle_native_", dir=os.environ.get("TMPDIR", "/tmp"))
+    so = os.path.join(d, "libhz_oracle_native.so")
+    srcs = sorted(glob.glob(os.path.join(ROOT, "oracle", "hz_oracle*.c")))
+    try:
+        subprocess.run([cc, "-O3", "-march=native", "-std=c11", "-fPIC", "-ffp-contract=off", "-shared", "-o", so,
+                        *srcs, "-lm", "-lpthread"], check=True, capture_output=True, timeout=120)
+    except Exception:  # noqa: BLE001
+        return None
+    return so
+
+
+def cpu_baseline(fwd, back, runs=5):
+    """The CPU restatement (oracle/hz_oracle.c, the reference's operation order) timed on this
+    host, SURVEY.md 8(d): (a) ONE thread -- the reference's execution model (one PortAudio
+    callback thread) -- over the whole 4096-band bank for 1 s of audio, and (b) all usable cores
+    (bands split over threads, partial mixes summed) over the full 10 s step; each the median of
+    `runs` runs on fresh banks, built -O3 -march=native -ffp-contract=off.  A restatement of the
+    reference semantics, not the reference (unbuildable here: Eigen / FFTW / PortAudio absent)."""
+    info = cpu_info()
+    so = native_oracle()
+    if so:
+        os.environ["HZ_ORACLE_SO"] = so
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle import OracleFilterbank
-    threads = max(1, min(16, os.cpu_count() or 1))
     N = fwd.shape[0]
     rng = np.random.default_rng(1)
-    nsamp = 480_000
-    x = rng.uniform(-1, 1, nsamp).astype(np.float32).astype(np.float64)
-    banks = []
-    for t in range(threads):
-        b0, cnt = shard_of(t, threads, N)
+    x = rng.uniform(-1, 1, SAMPLES_PER_STEP).astype(np.float32).astype(np.float64)
+
+    def bank(b0, cnt):
         fb = OracleFilterbank(2, cnt)
         for i in range(cnt):
             fb.coefficients(i, fwd[b0 + i], back[b0 + i])
         fb.boost(np.ones(cnt))
         fb.open()
-        banks.append(fb)
-    outs = [None] * threads
+        return fb
 
-    def run(i):
-        outs[i] = banks[i].process(x)
+    def leg(threads, nsamp):
+        xs = x[:nsamp]
+        times = []
+        for _ in range(runs):
+            banks = [bank(*shard_of(t, threads, N)) for t in range(threads)]
+            outs = [None] * threads
 
-    t0 = time.perf_counter()
-    ths = [threading.Thread(target=run, args=(i,)) for i in range(threads)]
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    dt = time.perf_counter() - t0
-    return {"value": N * nsamp / dt, "unit": "band-samples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/hz_oracle.c restatement, {N} bands x {nsamp} samples "
-                      f"({nsamp / SR:.2f} s audio), bands split over {threads} threads, {dt:.2f} s wall"}
+            def run(i):
+                outs[i] = banks[i].process(xs)
+            ths = [threading.Thread(target=run, args=(i,)) for i in range(threads)]
+            t0 = time.perf_counter()
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+            _ = np.sum(outs, axis=0)   # the partial mixes summed, as the reference's one sum
+            times.append(time.perf_counter() - t0)
+        dt = float(np.median(times))
+        return {"value": N * nsamp / dt, "unit": "band-samples/s", "threads": threads, "samples": nsamp,
+                "median_s": dt, "runs_s": times}
+
+    one = leg(1, SR)                                       # 1 s of audio, whole bank, 1 thread
+    cores = max(1, min(16, info["usable_cpus"]))            # the box's CPU share is 16
+    allc = leg(cores, SAMPLES_PER_STEP)
+    build = "-O3 -march=native -ffp-contract=off" if so else "-O3 -ffp-contract=off (in-tree build; gcc unavailable)"
+    return {"value": allc["value"], "unit": "band-samples/s", "cores": cores, "kind": "port",
+            "sample": (f"oracle/hz_oracle.c restatement of src/filterbank.h:170-187, {build}, median of {runs}: "
+                       f"all {N} bands; 1 thread over {SR} samples (1 s), {cores} threads (bands split) over "
+                       f"{SAMPLES_PER_STEP} samples (10 s)"),
+            "threads_1": one, "all_cores": allc, "build": build, **info}
 
 
 def fb_executed_flops(lti, L=32, O=2, N=N_BANDS):
@@ -122,13 +182,15 @@ def resp_step_flops(K, S, N, O=2):
     return conv, state
 
 
-def pmc_traffic(kernels=("fb_mix_kernel",), extra=()):
-    """HBM bytes per step of the engine's kernels from two separate rocprofv3 --pmc passes
-    (FETCH_SIZE, WRITE_SIZE; kernel-trace only), run as child processes on a short bench.
-    Per kernel name (substring) the mean of its two largest launches (the per-step ones) is
-    taken; the kernels are summed.  Correction per MI355X_MICROARCH.md 'HBM': FETCH_SIZE counts
-    wide coalesced streaming reads at 1/2 of their bytes, so it is doubled; WRITE_SIZE is taken
-    as is.  Returns (bytes, detail) or (None, reason)."""
+PMC_FLOP_COUNTERS = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+                     "SQ_INSTS_VALU_MFMA_MOPS_F64")
+
+
+def pmc_pass(counters, kernels, extra=()):
+    """One rocprofv3 --pmc pass (kernel trace only, no other tracing) of a short bench run as a
+    child process: per kernel (name substring) and counter the mean over its two largest
+    dispatches (the per-step launches).  Returns ({kernel: {counter: value}}, None) or
+    (None, reason)."""
     import csv
     import shutil
     import subprocess
@@ -136,41 +198,65 @@ def pmc_traffic(kernels=("fb_mix_kernel",), extra=()):
     exe = shutil.which("rocprofv3")
     if not exe:
         return None, "rocprofv3 not found"
-    vals = {}
-    per_kernel = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = tempfile.mkdtemp(prefix="hz_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-        cmd = [exe, "--pmc", counter, "--kernel-trace", "-d", d, "-o", "pmc", "--output-format", "csv",
-               "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "3",
-               "--no-cpu-baseline", "--stream-blocks", "0", "--no-traffic", *extra]
-        try:
-            subprocess.run(cmd, check=True, capture_output=True, timeout=300,
-                           env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
-        except Exception as e:  # noqa: BLE001
-            return None, f"rocprofv3 --pmc {counter} failed: {e}"
-        rows = []
-        for root, _, files in os.walk(d):
-            for f in files:
-                if f.endswith("counter_collection.csv"):
-                    rows += [r for r in csv.DictReader(open(os.path.join(root, f)))
-                             if r["Counter_Name"] == counter]
+    d = tempfile.mkdtemp(prefix="hz_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    cmd = [exe, "--pmc", *counters, "--kernel-trace", "-d", d, "-o", "pmc", "--output-format", "csv",
+           "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "3",
+           "--no-cpu-baseline", "--stream-blocks", "0", "--no-traffic", "--side-steps", "0", *extra]
+    try:
+        subprocess.run(cmd, check=True, capture_output=True, timeout=300,
+                       env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
+    except Exception as e:  # noqa: BLE001
         shutil.rmtree(d, ignore_errors=True)
-        total = 0.0
-        for k in kernels:
-            v = sorted(float(r["Counter_Value"]) for r in rows if k in r["Kernel_Name"])[-2:]
-            if not v:
-                if k == kernels[0]:
-                    return None, f"no {counter} rows for {k}"
-                continue
-            b = sum(v) / len(v) * 1024.0  # KB -> bytes
-            per_kernel.setdefault(k, {})[counter] = b
-            total += b
-        vals[counter] = total
-    fetch = 2.0 * vals["FETCH_SIZE"]
-    write = vals["WRITE_SIZE"]
-    return fetch + write, {"fetch_bytes": fetch, "write_bytes": write, "per_kernel": per_kernel,
-                           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes; FETCH x2 (gfx950); "
-                                     "summed over " + ", ".join(kernels)}
+        return None, f"rocprofv3 --pmc {' '.join(counters)} failed: {e}"
+    rows = []
+    for root, _, files in os.walk(d):
+        for f in files:
+            if f.endswith("counter_collection.csv"):
+                rows += list(csv.DictReader(open(os.path.join(root, f))))
+    shutil.rmtree(d, ignore_errors=True)
+    out = {}
+    for k in kernels:
+        for c in counters:
+            per = {}
+            for r in rows:
+                if r["Counter_Name"] == c and k in r["Kernel_Name"]:
+                    per[r.get("Dispatch_Id", len(per))] = per.get(r.get("Dispatch_Id", len(per)), 0.0) + \
+                        float(r["Counter_Value"])
+            v = sorted(per.values())[-2:]
+            if v:
+                out.setdefault(k, {})[c] = sum(v) / len(v)
+    if not out:
+        return None, "no counter rows for " + ", ".join(kernels)
+    return out, None
+
+
+def pmc_traffic(kernels, extra=()):
+    """HBM bytes per launch of each kernel from two separate rocprofv3 --pmc passes (FETCH_SIZE,
+    WRITE_SIZE; kernel-trace only).  Correction per MI355X_MICROARCH.md 'HBM': FETCH_SIZE counts
+    wide coalesced streaming reads at 1/2 of their bytes, so it is doubled; WRITE_SIZE is taken as
+    is; both are in KB.  Returns ({kernel: bytes}, detail) or (None, reason)."""
+    per = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        res, err = pmc_pass((counter,), kernels, extra)
+        if res is None:
+            return None, err
+        for k, cv in res.items():
+            per.setdefault(k, {})[counter] = cv.get(counter, 0.0) * 1024.0
+    byk = {k: 2.0 * v.get("FETCH_SIZE", 0.0) + v.get("WRITE_SIZE", 0.0) for k, v in per.items()}
+    return byk, {"per_kernel": per, "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
+                                              "FETCH x2 (gfx950); bytes per launch"}
+
+
+def pmc_flops(kernels, extra=()):
+    """Executed FP64 flops per launch of each kernel: 64 lanes x (2 FMA + MUL + ADD) F64 VALU
+    wave-instructions + 512 per F64 MFMA mop (scripts/flops_pmc.sh), one rocprofv3 --pmc pass."""
+    res, err = pmc_pass(PMC_FLOP_COUNTERS, kernels, extra)
+    if res is None:
+        return None, err
+    fl = {k: 64.0 * (2 * c.get("SQ_INSTS_VALU_FMA_F64", 0) + c.get("SQ_INSTS_VALU_MUL_F64", 0) +
+                     c.get("SQ_INSTS_VALU_ADD_F64", 0)) + 512.0 * c.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0)
+          for k, c in res.items()}
+    return fl, res
 
 
 class _HostDist:
@@ -216,8 +302,7 @@ def torch_empty_like(t):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 200 x 0.38 ms: short runs carry a fixed start-up cost in the timed region (20 steps read
-    # 0.42 ms/step on the same box, 200 steps 0.377, 2000 steps 0.373)
+    # 200 x 0.06 ms: short runs carry a fixed start-up cost in the timed region
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--samples", type=int, default=SAMPLES_PER_STEP)
@@ -233,7 +318,7 @@ def main():
     ap.add_argument("--gather", action="store_true",
                     help="N > 1, time-sharded stationary calls: gather the shares on rank 0 inside each step")
     ap.add_argument("--side-steps", type=int, default=50,
-                    help="timed steps of the side figures (per-band engine, lazy stationary engine)")
+                    help="timed steps of the side figures (per-band engine, lazy states, band partition)")
     ap.add_argument("--target-groups", type=int, default=0, help="(tuning) workgroups wanted per launch")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="(1 GPU, diagnostics) run rank 0's shard of an N-GPU job alone: per-GPU time at N")
@@ -262,7 +347,9 @@ def main():
     dev = torch.device("cuda", local)
 
     from huygens_amd import Filterbank
-    from huygens_amd._lib import HZ_FB_PATH_RESPONSE
+    from huygens_amd._lib import (HZ_FB_PATH_GENERAL, HZ_FB_PATH_LTI, HZ_FB_PATH_RESPONSE, HZ_FB_RESP_EAGER,
+                                  HZ_FB_RESP_LAZY, HZ_FB_RESP_OFF)
+    from huygens_amd.shard import arm_when_ready, set_time_shards
     fwd, back = c2_coefficients()
     b0, cnt = shard_of(rank, world) if not args.emulate_world else shard_of(0, args.emulate_world)
     fb = Filterbank(2, N_BANDS, 0.1, 1.0, device=local, shard=(b0, cnt))
@@ -277,38 +364,33 @@ def main():
     if args.target_groups:
         fb.set_target_groups(args.target_groups)
     if args.general:
-        from huygens_amd._lib import HZ_FB_PATH_GENERAL
         fb.set_path(HZ_FB_PATH_GENERAL)
     if args.response >= 0:
         fb.set_response(args.response)
     stream = torch.cuda.current_stream(dev)
     fb.set_stream(stream.cuda_stream)
 
+    def ar(v, op):   # all-reduce of one host integer / float over the ranks
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=op)
+        return t.item()
+
     # N > 1: once stationary, the ranks split the call by TIME (each convolves its share of the
     # output blocks with the whole bank's response, summed over the band shards by one all-reduce
-    # at setup) and keep their own bands' states; rank 0 gathers the shares
+    # at setup) and keep their own bands' states.  The engine switch is collective: the handles
+    # are armed on every rank in the same call (shard.arm_when_ready, one host all-reduce between
+    # untimed calls), never decided per rank.
     tshard = False
     if world > 1 and not args.general and args.response != 0:
-        from huygens_amd.shard import set_time_shards
-
         def all_reduce_sum(h):
-            t = torch.from_numpy(h).to(dev)
+            t = torch.from_numpy(np.ascontiguousarray(h)).to(dev)
             dist.all_reduce(t)
             return t.cpu().numpy()
-
-        def all_reduce_max(k):
-            t = torch.tensor([k], dtype=torch.int64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            return int(t.item())
-        try:
-            tshard = set_time_shards(fb, rank, world, all_reduce_sum, all_reduce_max)
-        except Exception as e:  # noqa: BLE001 -- fall back to band shards + reduce
-            print(f"rank {rank}: time shards not set ({e}); band shards + reduce", file=sys.stderr)
-            tshard = False
+        tshard = set_time_shards(fb, rank, world, all_reduce_sum, lambda k: int(ar(k, dist.ReduceOp.MAX)))
+        all_reduce_min = lambda k: int(ar(k, dist.ReduceOp.MIN))   # noqa: E731
     elif args.emulate_world > 1 and not args.general and args.response != 0:
         # (1 GPU, diagnostics) rank 0 of a time-sharded job: the other shards' handles exist only
-        # to sum the whole bank's response
-        from huygens_amd.shard import set_time_shards
+        # to sum the whole bank's response; the others are taken to be ready when rank 0 is
         others = []
         for r in range(1, args.emulate_world):
             ob, oc = shard_of(r, args.emulate_world)
@@ -320,19 +402,25 @@ def main():
             o.response(8192)
             others.append(o)
         k_max = max([o.response_info()[0] for o in others])
-        tshard = set_time_shards(fb, 0, args.emulate_world,
-                                 lambda h: h + sum(o.response(len(h)) for o in others),
-                                 lambda k: max(k, k_max))
+        red_calls = [0]
+
+        def emu_max(k):   # 1st call: the horizons; 2nd: the failure flags (the others' are 0)
+            red_calls[0] += 1
+            return max(k, k_max) if red_calls[0] == 1 else k
+        tshard = set_time_shards(fb, 0, args.emulate_world, lambda h: h + sum(o.response(len(h)) for o in others),
+                                 emu_max)
+        all_reduce_min = lambda k: k   # noqa: E731
         for o in others:
             o.close()
 
     # Time-sharded stationary calls partition the stream: each rank produces the final output of
     # its run of blocks from the shared input (a K-sample halo, no exchange), so a step at N > 1 is
     # a call of N x 10 s with 10 s of output per rank -- weak scaling, no data-path collective
-    # (the per-band warmup calls still sum band shards with one reduce)
+    # (before the handles are armed, the per-band calls sum band shards with one reduce)
     P_t = (world if world > 1 else max(1, args.emulate_world)) if tshard else 1
     S = args.samples * P_t
     gbuf = None   # ShareGather (--gather: collect the shares on rank 0 inside the step)
+    armed = False
     rng = np.random.default_rng(1234)
     x = torch.from_numpy(rng.uniform(-1, 1, S).astype(np.float32).astype(np.float64)).to(dev)
     y = torch.empty_like(x)
@@ -341,8 +429,7 @@ def main():
         nonlocal gbuf
         fb.process_device(x.data_ptr(), y.data_ptr(), S)
         if world > 1:
-            active, first, count = fb.time_shard_info(S) if tshard else (False, 0, S)
-            if active and fb.last_path() == HZ_FB_PATH_RESPONSE:
+            if armed:
                 # every rank holds the final samples of its share: nothing to exchange (--gather
                 # collects them on rank 0 inside the step: fixed-size slots, one gather)
                 if args.gather:
@@ -353,29 +440,41 @@ def main():
             else:
                 dist.reduce(y, dst=0, op=dist.ReduceOp.SUM)
 
+    def try_arm():
+        nonlocal armed
+        if tshard and not armed:
+            torch.cuda.synchronize(dev)
+            armed = arm_when_ready(fb, S, all_reduce_min)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    # Priming (untimed, before the W warmup steps): calls until the engine the run settles on is
+    # reached -- the smoothers converge during the first 10 s call (k_g = 1 s), the stationary engine
+    # needs K samples of converged history, and time-sharded ranks must be armed together.
+    for i in range(8):
+        step()
+        try_arm()
+        if (armed if tshard else fb.last_path() == HZ_FB_PATH_RESPONSE) or \
+                (i >= 2 and (args.general or args.response == 0 or not tshard)):
+            break
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    barrier()
     elapsed = time.perf_counter() - t0
     # the engine's GPU time per step (roofline): a separate pass of the same steps with HIP events
     # on the handle's stream (no event records inside the timed region above)
     fb.profile(True)
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    barrier()
     seg_ms, mix_ms, red_ms, launches = fb.profile_read()
-    from huygens_amd._lib import (HZ_FB_PATH_LTI, HZ_FB_PATH_RESPONSE, HZ_FB_RESP_EAGER, HZ_FB_RESP_LAZY,
-                                  HZ_FB_RESP_OFF)
     path = fb.last_path()
     lti = path == HZ_FB_PATH_LTI
     resp = path == HZ_FB_PATH_RESPONSE
@@ -383,104 +482,128 @@ def main():
     horizon = fb.response_info()[0]
     fb.profile(False)
 
-    def side_rate(mode, warm):
-        """ms per step of the same workload with the stationary engine in `mode` (timed like the
-        main loop, fewer steps): the per-band engine's figure and the lazy-state figure"""
-        if args.side_steps <= 0:
-            return None
-        fb.set_response(mode)
+    def timed(fn, warm, steps, n_samples, arm=False):
+        """ms per step and band-samples/s (whole job, max over ranks) of `fn` after `warm` calls"""
         for _ in range(warm):
-            step()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
+            fn()
+            if arm:
+                try_arm()
+        barrier()
         ts = time.perf_counter()
-        for _ in range(args.side_steps):
-            step()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
+        for _ in range(steps):
+            fn()
+        barrier()
         dt = time.perf_counter() - ts
         if world > 1:
-            t = torch.tensor([dt], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        return {"ms_per_step": 1e3 * dt / args.side_steps, "value": N_BANDS * S * args.side_steps / dt,
+            dt = ar(dt, dist.ReduceOp.MAX)
+        return {"ms_per_step": 1e3 * dt / steps, "value": N_BANDS * n_samples * steps / dt,
                 "path": {1: "general", 2: "lti", 3: "response"}.get(fb.last_path(), "?")}
 
     side = {}
-    if resp:
-        side["per_band_engine"] = side_rate(HZ_FB_RESP_OFF, 3)
-        side["stationary_lazy_states"] = side_rate(HZ_FB_RESP_LAZY, 3)
+    if resp and args.side_steps > 0:
+        armed = False
+        fb.set_response(HZ_FB_RESP_OFF)     # disarms: band shards + reduce at N > 1
+        side["per_band_engine"] = timed(step, 3, args.side_steps, S)
+        fb.set_response(HZ_FB_RESP_LAZY)
+        side["stationary_lazy_states"] = timed(step, 3, args.side_steps, S, arm=True)
+        armed = False
         fb.set_response(HZ_FB_RESP_EAGER if args.response < 0 else args.response)
+    if world > 1 and args.side_steps > 0:
+        # north_star's decomposition: the bands partitioned over the GPUs, a FIXED 10 s call per
+        # step (strong scaling), each rank's partial mix summed to rank 0 by an RCCL reduce
+        # (each rank's own engine choice: it outputs all samples of its bands either way)
+        armed = False
+        fb.set_bank_response(np.zeros(0))
+        S1 = args.samples
+
+        def step_bp():
+            fb.process_device(x.data_ptr(), y.data_ptr(), S1)
+            dist.reduce(y[:S1], dst=0, op=dist.ReduceOp.SUM)
+        side["band_partition"] = timed(step_bp, 4, args.side_steps, S1)
+        fb.set_response(HZ_FB_RESP_OFF)
+        side["band_partition_per_band_engine"] = timed(step_bp, 3, args.side_steps, S1)
+        for k in ("band_partition", "band_partition_per_band_engine"):
+            side[k]["note"] = (f"{N_BANDS} bands over {world} GPUs ({cnt} per GPU), one {S1}-sample call per "
+                               "step, partial mixes summed to rank 0 by RCCL reduce (strong scaling)")
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        mm = torch.tensor([seg_ms + mix_ms + red_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(mm, op=dist.ReduceOp.MAX)
-        eng_ms_max = float(mm.item())
+        eng_ms_max = ar(seg_ms + mix_ms + red_ms, dist.ReduceOp.MAX)
+        elapsed = ar(elapsed, dist.ReduceOp.MAX)
     else:
         eng_ms_max = seg_ms + mix_ms + red_ms
 
-    # streaming figure: one process() call per 1024-sample block
+    # streaming figure: one process() call per 1024-sample block (per-band engine: calls below
+    # the stationary minimum; last, since short calls restart the stationary history)
     stream_rate = None
     if args.stream_blocks > 0:
+        armed = False
+        fb.arm_time_shard(False) if tshard else None
         B = 1024
         nb = min(args.stream_blocks, S // B)
         for i in range(min(8, nb)):   # untimed: the short-call geometry's records are built on first use
             fb.process_device(x.data_ptr() + 8 * B * i, y.data_ptr() + 8 * B * i, B)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
+        barrier()
         ts = time.perf_counter()
         for i in range(nb):
             fb.process_device(x.data_ptr() + 8 * B * i, y.data_ptr() + 8 * B * i, B)
             if world > 1:
                 dist.reduce(y[i * B:(i + 1) * B], dst=0, op=dist.ReduceOp.SUM)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
+        barrier()
         tstream = time.perf_counter() - ts
         if world > 1:
-            t = torch.tensor([tstream], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            tstream = float(t.item())
+            tstream = ar(tstream, dist.ReduceOp.MAX)
         stream_rate = N_BANDS * B * nb / tstream
 
     total_band_samples = N_BANDS * S * args.steps
     value = total_band_samples / elapsed
     if rank == 0:
-        # Roofline over the engine's whole per-step GPU time (HIP events on the handle's stream):
-        # the LTI engine = segment prepass (+ carry) + mix kernel + cross-group reduce, the general
-        # engine = its mix + reduce.  One process() call can be several launches (the partial slab
-        # bounds a launch's length).  achieved = algorithmic 18 FP64 flops per band-sample (SURVEY.md
-        # 8(d), the reference recurrence); `executed` = the flops the engine actually issues.
-        step_ms = eng_ms_max   # max over ranks
-        launch_avg_s = (step_ms / 1e3) / max(1, launches)
-        band_samples_per_launch = cnt * S * args.steps / max(1, launches)
-        if resp:   # this GPU's outputs: its time share of the whole bank (all of it at N = 1)
-            band_samples_per_launch = N_BANDS * (S // P_t) * args.steps / max(1, launches)
-        flops_per_launch = FLOPS_PER_BAND_SAMPLE * band_samples_per_launch
-        achieved = flops_per_launch / launch_avg_s / 1e12 if launch_avg_s > 0 else None
-        xflops = fb_executed_flops(lti, chunk, N=cnt)
-        if resp:   # the stationary engine's flops per call (its share's convolution, its bands'
-            # states), spread over the share's band-samples
-            conv_f, state_f = resp_step_flops(horizon, S // P_t, cnt)
-            xflops = (conv_f + state_f) / (N_BANDS * (S // P_t))
-        executed = xflops * band_samples_per_launch / launch_avg_s / 1e12 if launch_avg_s > 0 else None
+        launch_avg_s = (eng_ms_max / 1e3) / max(1, launches)    # whole engine step, per process() call
+        out_samples = S // P_t if resp else S                   # this GPU's outputs per step
+        bs_launch = (N_BANDS if resp else cnt) * out_samples     # band-samples of one call on this GPU
+        # ---- dominant kernel (roofline): the band-state pass of the stationary engine, the state
+        # kernel of the per-band LTI engine, the mix kernel of the general engine; its average
+        # duration from the HIP events around it on the handle's stream
+        if resp:
+            dom = "fb_lti_kernel<2, 128, 1"
+            dom_name = "fb_lti_kernel<2,128,SEGEND> (band states: zero-start pass over the %d-sample history)" % horizon
+            dom_ms = red_ms / max(1, launches)
+            dom_model = resp_step_flops(horizon, out_samples, cnt)[1]
+        elif lti:
+            dom = "fb_lti_kernel<2, %d, 2" % chunk
+            dom_name = "fb_lti_kernel<2,%d,STATE> (chunk end states on MFMA + scan)" % chunk
+            dom_ms = mix_ms / max(1, launches)
+            dom_model = None
+        else:
+            dom = "fb_mix_kernel"
+            dom_name = "fb_mix_kernel<2,NONE,1,MIX>"
+            dom_ms = mix_ms / max(1, launches)
+            dom_model = 20.0 * cnt * S
+        step_kernels = (("fb_lti_kernel", "fb_lti_gemm", "fb_lti_reduce", "fb_lti_seg_carry", "fb_lti_sum",
+                         "fb_lti_xrows") if lti
+                        else ("resp_fwd_kernel", "resp_mac_kernel", "resp_inv_kernel", "fb_lti_kernel<2, 128, 1",
+                              "fb_lti_seg_carry") if resp
+                        else ("fb_mix_kernel", "fb_reduce"))
+        extra = (["--lti", args.lti] if args.lti else []) + (["--general"] if args.general else []) + \
+                (["--response", str(args.response)] if args.response >= 0 else [])
+        traffic = flops = None
+        traffic_detail = flops_detail = "skipped (--no-traffic, N > 1 or a non-default step length)"
+        if not args.no_traffic and world == 1 and S == SAMPLES_PER_STEP:
+            traffic, traffic_detail = pmc_traffic(step_kernels, extra)
+            flops, flops_detail = pmc_flops(step_kernels, extra)
+        dom_flops = flops.get(dom) if flops else None
+        dom_traffic = traffic.get(dom) if traffic else None
+        dom_fl = dom_flops if dom_flops else dom_model
+        achieved = dom_fl / (dom_ms / 1e3) / 1e12 if (dom_fl and dom_ms > 0) else None
+        # ---- the whole step: every kernel of a process() call over its whole GPU time
+        if resp:
+            conv_f, state_f = resp_step_flops(horizon, out_samples, cnt)
+            step_model = conv_f + state_f
+        else:
+            step_model = fb_executed_flops(lti, chunk, N=cnt) * cnt * S
+        step_pmc = sum(flops.values()) if flops else None
+        step_fl = step_pmc or step_model
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(fwd, back)
-        kernels = (("fb_lti_kernel", "fb_lti_gemm", "fb_lti_reduce", "fb_lti_seg_carry", "fb_lti_sum",
-                    "fb_lti_xrows") if lti
-                   else ("resp_fwd_kernel", "resp_mac_kernel", "resp_inv_kernel", "fb_lti_kernel<2, 128, 1",
-                         "fb_lti_seg_carry") if resp
-                   else ("fb_mix_kernel", "fb_reduce"))
-        traffic, traffic_detail = None, "skipped"
-        if not args.no_traffic and world == 1 and S == SAMPLES_PER_STEP:
-            traffic, traffic_detail = pmc_traffic(kernels, extra=(["--lti", args.lti] if args.lti else [])
-                                                  + (["--general"] if args.general else []))
         line = {
             "metric": "band-samples/s (bands x frames/s) for 4096-band Filterbank",
             "value": value,
@@ -493,63 +616,63 @@ def main():
             "scaling": "weak" if P_t > 1 and resp else "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic white noise uniform[-1,1) (float32 -> double), seed 1234",
+            "data": "synthetic white noise uniform[-1,1) (float32 -> double), seed 1234, resident in HBM",
             "config": {"workload": "C2 Filterbank<double>(order 2, 4096 bands), resonant band-pass "
                                    "f_i=0.5(i+1)SR/4096 R=0.999, boost 1 + open, k_p=0.1 k_g=1"
                                    + (f", {P_t} x 10 s per step split by time" if P_t > 1 and resp else ""),
-                       "samples_per_step": S, "samples_per_gpu": S // P_t, "block": 1024, "bands": N_BANDS,
-                       "bands_per_gpu": cnt,
-                       "parallelism": (f"stream split by time x{P_t}: each GPU outputs 10 s of the N x 10 s "
+                       "samples_per_step": S, "samples_per_gpu": out_samples,
+                       "call": f"one process() call of {S} samples per step (== {S // 1024} x 1024-sample "
+                               f"blocks in result; the 1024-block streaming rate is `streaming`)",
+                       "partition": 2048 if resp else None,
+                       "bands": N_BANDS, "bands_per_gpu": cnt,
+                       "parallelism": ("single GPU, all bands, no collective" if world == 1 and P_t == 1 else
+                                       f"stream split by time x{P_t}: each GPU outputs 10 s of the N x 10 s "
                                        f"call from the shared input with a {horizon}-sample halo (whole-bank "
                                        f"response, one all-reduce at setup), band states sharded x{P_t}; no "
                                        f"data-path collective" + (" (+ gather to rank 0)" if args.gather else "")
                                        if tshard and resp else f"bands sharded x{world}, RCCL reduce")},
             "engine": "stationary (bank response convolution, eager band states)" if resp
                       else "per-band LTI" if lti else "per-band general",
-            "roofline": {"bound": "mfma" if (lti or resp) else "valu", "achieved": executed, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": (executed / FP64_PEAK_TFLOPS) if executed else None,
-                         "traffic": traffic,
-                         "traffic_detail": traffic_detail,
-                         "algorithmic_bytes_per_launch": (16 * S + 120 * cnt) * args.steps / max(1, launches),
-                         "launches_per_step": launches / max(1, args.steps),
-                         "kernel": ("stationary engine step: resp_fwd_kernel + resp_mac_kernel<8> + resp_inv_kernel "
-                                    "(partitioned FFT convolution, history and smoother upkeep) + "
-                                    "fb_lti_kernel<2,128,SEGEND> (band states over the %d-sample horizon)" % horizon)
-                                   if resp else
-                                   (("LTI engine step: fb_lti_kernel<2,%d,STATE>%s + "
-                                     "fb_lti_gemm_pp_kernel<%d> + fb_lti_sum_kernel (+ segment prepass)"
-                                     % (chunk, " (+ x rows)" if chunk >= 128 else " + fb_lti_xrows_kernel", chunk))
-                                    if lti and chunk >= 64 else
-                                    ("LTI engine step: fb_lti_kernel<2,%d,MIX> + fb_lti_reduce_kernel (+ segment "
-                                     "prepass)" % chunk) if lti
-                                    else "general engine step: fb_mix_kernel<2,NONE,1,MIX> + fb_reduce_kernel"),
-                         "kernel_avg_ms": 1e3 * launch_avg_s,
-                         "components_ms_per_launch": {"segment_prepass": seg_ms / max(1, launches),
-                                                      "mix_or_state": mix_ms / max(1, launches),
-                                                      "gemm_and_reduce": red_ms / max(1, launches)},
-                         "flops_per_band_sample": xflops,
-                         "horizon": horizon if resp else None,
-                         "flops_per_launch": xflops * band_samples_per_launch,
-                         "reference_equivalent": {"flops_per_band_sample": FLOPS_PER_BAND_SAMPLE,
-                                                  "achieved": achieved,
-                                                  "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None},
-                         "note": ("stationary engine: achieved = the FP64 flops of the call (packed window and output "
-                                  "FFTs at 5 F log2 F, partition MACs, the end-state pass over the horizon; "
-                                  "bench.resp_step_flops) over the engine's whole per-step GPU time (HIP events on the "
-                                  "handle's stream): components mix_or_state = the convolution (fwd + MAC + inv), "
-                                  "gemm_and_reduce = history + band states. reference_equivalent = the reference "
-                                  "recurrence's 18 flops per band-sample over the same time (far above the peak: the "
-                                  "stationary engine's cost does not grow with the bands). peak = FP64 vector = FP64 MFMA "
-                                  "peak.") if resp else
-                                 "achieved = the FP64 flops the engine's algorithm performs per band-sample "
-                                 "(chunked state space: chunk end states + 64-lane scan + correction GEMM with the "
-                                 "zero-state rows, DESIGN.md 3.3; PMC-verified in profiles/r2/flops_pmc.txt) over the "
-                                 "whole per-step GPU time of the engine (kernel_avg_ms, HIP events on the handle's "
-                                 "stream). reference_equivalent = the reference recurrence's 18 flops per band-sample "
-                                 "(SURVEY.md 8(d)) over the same time -- it can exceed the peak because the engine "
-                                 "needs fewer than half of them. peak = FP64 vector = FP64 MFMA peak."},
+            "roofline": {
+                "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
+                "traffic": dom_traffic,
+                "kernel": dom_name,
+                "kernel_avg_ms": dom_ms,
+                "flops_per_launch": dom_fl,
+                "flops_source": "pmc (SQ_INSTS_VALU_{FMA,MUL,ADD}_F64, SQ_INSTS_VALU_MFMA_MOPS_F64)" if dom_flops
+                                else "model (bench.resp_step_flops)",
+                "model_flops_per_launch": dom_model,
+                # state pass: the K history samples in, coefficients + pre-amps (6 doubles) in and
+                # O = 2 states out per band; per-band engines: the block I/O and the band records
+                "algorithmic_bytes_per_launch": (8 * horizon + 64 * cnt) if resp else (16 * out_samples + 120 * cnt),
+                "peak_note": "FP64 MFMA peak = FP64 vector peak on MI355X (78.6 TFLOP/s); the kernel's E phase is "
+                             "v_mfma_f64_16x16x4f64, its scan FP64 VALU on the same pipe",
+                "step": {
+                    "kernels": list(step_kernels),
+                    "ms_per_call": 1e3 * launch_avg_s,
+                    "components_ms_per_call": {"segment_prepass": seg_ms / max(1, launches),
+                                               "convolution_or_state": mix_ms / max(1, launches),
+                                               "states_or_gemm": red_ms / max(1, launches)},
+                    "flops_per_call": step_fl,
+                    "flops_source": "pmc" if step_pmc else "model",
+                    "model_flops_per_call": step_model,
+                    "achieved_tflops": step_fl / launch_avg_s / 1e12 if launch_avg_s > 0 else None,
+                    "frac": step_fl / launch_avg_s / 1e12 / FP64_PEAK_TFLOPS if launch_avg_s > 0 else None,
+                    "traffic_per_call": sum(traffic.values()) if traffic else None,
+                    "traffic_per_kernel": traffic, "flops_per_kernel": flops,
+                    "traffic_detail": traffic_detail if not traffic else traffic_detail.get("method"),
+                    "flops_detail": flops_detail if not flops else "pmc",
+                    "reference_equivalent_tflops": FLOPS_PER_BAND_SAMPLE * bs_launch / launch_avg_s / 1e12
+                                                   if launch_avg_s > 0 else None,
+                    "note": ("reference_equivalent = the reference recurrence's 18 flops per band-sample (SURVEY.md "
+                             "8(d)) over the step's GPU time; the stationary engine's cost does not grow with the "
+                             "bands, so it exceeds the peak"),
+                },
+            },
             "side": side or None,
             "streaming": {"band_samples_per_s": stream_rate, "block": 1024,
+                          "us_per_block": (1e6 * N_BANDS * 1024 / stream_rate) if stream_rate else None,
                           "note": "one process() call per 1024-sample block, device-resident I/O"},
             "cpu_baseline": cpu,
         }

@@ -137,7 +137,7 @@ struct hz_fb {
     // K inputs, from which the band states follow once the bank has been stationary for K samples
     struct Resp {
         int mode = HZ_FB_RESP_EAGER;     // HZ_FB_RESP_OFF / _EAGER / _LAZY
-        long K = -2;                     // horizon (samples, multiple of 4096); -1 none; -2 unknown
+        long K = -2;                     // horizon (samples, multiple of 8192, 2^-53); -1 none; -2 unknown
         bool h_valid = false;            // d_h / d_H match F, B, pin, gin
         long run = 0;                    // converged samples in a row written into the history
         bool implicit = false;           // LAZY: ystate[scur] not yet materialised from the history
@@ -149,6 +149,10 @@ struct hz_fb {
         std::vector<double> h_over;
         bool over_valid = false;
         int shard_rank = 0, shard_world = 1;
+        // a time-sharded handle takes the stationary engine only when the caller has armed it on
+        // every rank (hz_fb_arm_time_shard after an all-reduce of hz_fb_stationary_ready), so all
+        // ranks switch engines in the same call; cleared by every setter
+        bool armed = false;
         double* d_hist[2] = {nullptr, nullptr};   // [K] last K inputs (ping-pong)
         size_t hist_cap0 = 0, hist_cap1 = 0;
         int hcur = 0;
@@ -217,7 +221,8 @@ size_t fb_end_scratch(int N, int O, long K);
 void fb_resp_init(hz_fb* h);
 void fb_resp_invalidate(hz_fb* h, bool coefficients);   // targets / coefficients changed
 void fb_resp_setter(hz_fb* h);   // any setter, also for bands of other shards: the bank response changes
-bool fb_resp_eligible(hz_fb* h, long n, bool conv);
+bool fb_resp_eligible(hz_fb* h, long n, bool conv);   // this handle alone (no arming)
+bool fb_resp_time_sharded(const hz_fb* h);            // the engine choice is the caller's (armed)
 int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n);
 int fb_resp_track(hz_fb* h, const double* d_in, long n, bool conv);  // history after any call
 int fb_resp_materialize(hz_fb* h);                                  // LAZY: band states now

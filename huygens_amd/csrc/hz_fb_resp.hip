@@ -537,20 +537,25 @@ void fb_resp_invalidate(hz_fb* h, bool coefficients) {
     h->resp.run = 0;
     h->resp.h_valid = false;
     h->resp.over_valid = false;
+    h->resp.armed = false;
     if (coefficients) h->resp.K = -2;
 }
 
 void fb_resp_setter(hz_fb* h) {
     if (h->resp.over_valid) h->resp.h_valid = false;   // back to this shard's own response
     h->resp.over_valid = false;
+    h->resp.armed = false;
 }
+
+bool fb_resp_time_sharded(const hz_fb* h) { return h->resp.over_valid && h->resp.shard_world > 1; }
 
 // the cost model alone: would a call of n samples run stationary (given the history)?
 static bool resp_worth(const hz_fb* h, long n) {
     const hz_fb::Resp& R = h->resp;
     static const long per_env = std::getenv("HZ_FB_RESP_BANDS") ? std::atol(std::getenv("HZ_FB_RESP_BANDS")) : 256;
     const long per = R.bands_per_sample >= 0 ? R.bands_per_sample : per_env;
-    // time-range shards decide on the whole bank (every rank takes the same engine)
+    // time-range shards cost the whole bank's convolution (the choice itself is armed by the
+    // caller on every rank, hz_fb_arm_time_shard)
     const double bands = R.over_valid ? (double)h->N_total : (double)h->N;
     return bands * n >= (double)per * (double)(R.K + n);
 }
@@ -578,7 +583,10 @@ int fb_resp_materialize(hz_fb* h) {
 // after a call on any engine: the history keeps the last K inputs while the bank stays converged
 int fb_resp_track(hz_fb* h, const double* d_in, long n, bool conv) {
     hz_fb::Resp& R = h->resp;
-    if (R.mode == HZ_FB_RESP_OFF || !conv || h->order == 0 || n < resp_min_call(h)) {
+    // (handles pinned to the general engine never run stationary: no history upkeep; a
+    // distortion functor keeps it, the engine resumes when the functor is cleared)
+    if (R.mode == HZ_FB_RESP_OFF || !conv || h->order == 0 || n < resp_min_call(h) ||
+        h->path_mode != HZ_FB_PATH_AUTO) {
         R.run = 0;
         return HZ_OK;
     }
@@ -756,6 +764,7 @@ int hz_fb_set_response(hz_fb* h, int mode) {
     HZ_TRY_HIP(hipSetDevice(h->device));
     HZ_TRY(hz_fbi::fb_resp_materialize(h));
     h->resp.mode = mode;
+    h->resp.armed = false;   // a time-sharded handle re-arms (on every rank) for the new mode
     if (mode == HZ_FB_RESP_OFF) h->resp.run = 0;
     return HZ_OK;
 }
@@ -767,6 +776,7 @@ int hz_fb_set_bank_response(hz_fb* h, const double* resp, long count) {
     if (count == 0) {
         h->resp.over_valid = false;
         h->resp.h_valid = false;
+        h->resp.armed = false;
         return HZ_OK;
     }
     HZ_TRY(resp_setup(h));
@@ -777,12 +787,15 @@ int hz_fb_set_bank_response(hz_fb* h, const double* resp, long count) {
     }
     if (count > h->resp.K) {   // the bank's horizon (another shard's bands ring longer): a longer history
         h->resp.K = count;
-        h->resp.run = 0;
         HZ_TRY(resp_setup(h));
     }
+    // every rank restarts its history count here, whatever its own horizon was, so the ranks'
+    // readiness (hz_fb_stationary_ready) evolves alike from this call on
+    h->resp.run = 0;
     h->resp.h_over.assign(resp, resp + count);
     h->resp.over_valid = true;
     h->resp.h_valid = false;
+    h->resp.armed = false;
     return HZ_OK;
 }
 
@@ -790,6 +803,25 @@ int hz_fb_set_time_shard(hz_fb* h, int rank, int world) {
     if (!h || world < 1 || rank < 0 || rank >= world) return HZ_E_INVALID;
     h->resp.shard_rank = rank;
     h->resp.shard_world = world;
+    h->resp.armed = false;
+    return HZ_OK;
+}
+
+int hz_fb_stationary_ready(hz_fb* h, long n, int* ready) {
+    if (!h || !ready || n < 0) return HZ_E_INVALID;
+    HZ_TRY_HIP(hipSetDevice(h->device));
+    const bool conv = h->order > 0 && n >= 16 && hz_fbi::fb_converged(h);
+    *ready = hz_fbi::fb_resp_eligible(h, n, conv) ? 1 : 0;
+    return HZ_OK;
+}
+
+int hz_fb_arm_time_shard(hz_fb* h, int armed) {
+    if (!h) return HZ_E_INVALID;
+    if (armed && !hz_fbi::fb_resp_time_sharded(h)) {
+        hz::set_error("hz_fb_arm_time_shard: no time shard set (hz_fb_set_bank_response + hz_fb_set_time_shard)");
+        return HZ_E_STATE;
+    }
+    h->resp.armed = armed != 0;
     return HZ_OK;
 }
 

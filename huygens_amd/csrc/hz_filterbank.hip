@@ -873,7 +873,17 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
     // converged for the whole call (the smoothers only get closer): the LTI engine may run, and
     // the stationary engine's history keeps counting
     const bool conv = h->order > 0 && n >= 16 && fb_converged(h);
-    if (fb_resp_eligible(h, n, conv)) {
+    // a time-sharded handle (multi-GPU) runs stationary exactly when the caller armed it on
+    // every rank; an armed handle that cannot (its history is short, or a setter or short call
+    // intervened) fails loudly instead of leaving its peers on another engine
+    const bool tshard = fb_resp_time_sharded(h);
+    const bool elig = fb_resp_eligible(h, n, conv);
+    if (tshard && h->resp.armed && !elig) {
+        hz::set_error("hz_fb_process: time-sharded handle armed for the stationary engine, but this call "
+                      "of %ld samples is not stationary here (re-arm after hz_fb_stationary_ready)", n);
+        return HZ_E_STATE;
+    }
+    if (elig && (!tshard || h->resp.armed)) {
         HZ_TRY(fb_launch_resp(h, d_in, d_out, n));
         h->last_path = HZ_FB_PATH_RESPONSE;
         return HZ_OK;

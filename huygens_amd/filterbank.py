@@ -224,6 +224,17 @@ class Filterbank:
     def set_time_shard(self, rank: int, world: int):
         check(self._lib.hz_fb_set_time_shard(self._h, int(rank), int(world)))
 
+    def stationary_ready(self, n: int) -> bool:
+        """Would a call of n samples run stationary on this handle (ignoring arming)?"""
+        r = C.c_int()
+        check(self._lib.hz_fb_stationary_ready(self._h, int(n), C.byref(r)))
+        return bool(r.value)
+
+    def arm_time_shard(self, armed: bool = True):
+        """Time-sharded handles run stationary exactly when armed (set on every rank alike:
+        huygens_amd.shard.arm_when_ready)."""
+        check(self._lib.hz_fb_arm_time_shard(self._h, 1 if armed else 0))
+
     def time_shard_info(self, n: int):
         """-> (active, first sample, count) of a stationary call of n samples on this rank"""
         a, f, c = C.c_int(), C.c_long(), C.c_long()

@@ -21,18 +21,47 @@ def set_time_shards(fb, rank: int, world: int, all_reduce_sum, all_reduce_max) -
     whole bank's response is the sum of the band shards' responses over the largest horizon of
     the ranks (`all_reduce_sum(array) -> array`, `all_reduce_max(int) -> int`, e.g. RCCL
     all-reduces), set on every rank; each rank then convolves its run of output blocks and keeps
-    its own bands' states.  Call after the last setter (setters clear it).  Returns False
-    (nothing set) when some shard has no finite horizon."""
+    its own bands' states.  Call after the last setter (setters clear it), on every rank.
+
+    Collective-safe: every rank takes part in both all-reduces whatever its own shard can do (a
+    shard without a finite horizon -- or whose horizon probe fails -- contributes a sentinel), so
+    the ranks either all set the shards or all return False.  The handles then still need arming
+    (arm_when_ready) before a call runs stationary."""
     import numpy as np
-    fb.response(8192)   # computes the shard's horizon
-    K = int(fb.response_info()[0])
-    K_all = int(all_reduce_max(K if K > 0 else 1 << 30))
+    none = 1 << 30   # no finite horizon on this shard (> the 2^19 the engine supports)
+    try:
+        fb.response(8192)   # computes the shard's horizon
+        K = int(fb.response_info()[0])
+    except Exception:  # noqa: BLE001 -- e.g. HZ_E_UNSUPPORTED: no horizon within 2^18 samples
+        K = -1
+    K_all = int(all_reduce_max(K if K > 0 else none))
     if K_all <= 0 or K_all > (1 << 19):
+        return False   # every rank sees the same K_all: all leave here, no collective pending
+    try:
+        mine = np.ascontiguousarray(fb.response(K_all), dtype=np.float64)
+        ok = True
+    except Exception:  # noqa: BLE001 -- keep the collective matched, then fail together
+        mine = np.zeros(K_all)
+        ok = False
+    full = np.asarray(all_reduce_sum(mine), dtype=np.float64)
+    # agreement on success (a rank that failed after the horizon probe poisons the sum)
+    if int(all_reduce_max(0 if ok else 1)) != 0:
         return False
-    full = np.asarray(all_reduce_sum(np.ascontiguousarray(fb.response(K_all))), dtype=np.float64)
     fb.set_bank_response(full)
     fb.set_time_shard(rank, world)
     return True
+
+
+def arm_when_ready(fb, n: int, all_reduce_min) -> bool:
+    """Arms the time-sharded handles of ALL ranks for the stationary engine in the same call, or
+    none: every rank asks whether a call of n samples would be stationary on its own handle
+    (hz_fb_stationary_ready; it depends on the shard's convergence and history), the flags are
+    all-reduced with MIN (`all_reduce_min(int) -> int`) and the result armed on every rank.
+    Collective: call on every rank between the same two calls.  Returns whether armed."""
+    ready = 1 if fb.stationary_ready(n) else 0
+    armed = int(all_reduce_min(ready)) == 1
+    fb.arm_time_shard(armed)
+    return armed
 
 
 def time_share(rank: int, world: int, n: int, block: int = 2048) -> tuple[int, int]:

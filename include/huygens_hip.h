@@ -117,7 +117,7 @@ int hz_fb_set_path(hz_fb* h, int path);
 int hz_fb_last_path(hz_fb* h, int* path);
 /* Stationary engine (HZ_FB_PATH_RESPONSE, hz_fb_resp.hip).  Once the bank has run converged
  * (as for the LTI engine) with unchanged coefficients and targets for K samples -- K = its
- * horizon, the first multiple of 4096 with ||M^K||_inf < 2^-64 for every band's state transition
+ * horizon, the first multiple of 8192 with ||M^K||_inf < 2^-53 for every band's state transition
  * M (src/filterbank.h:178-179) -- the mixdown of a long call (>= 16384 samples) is one linear
  * filter of the input, out = h * x with h = sum_n gin_n (band n's impulse response at pre = pin_n),
  * truncated at K, and runs as a partitioned FFT convolution.  The band states at the call end are
@@ -147,6 +147,15 @@ int hz_fb_get_response(hz_fb* h, double* out, long count);
  * response; count 0 clears it explicitly.  Without it a call outputs all samples of its own bands. */
 int hz_fb_set_bank_response(hz_fb* h, const double* resp, long count);
 int hz_fb_set_time_shard(hz_fb* h, int rank, int world);
+/* The engine choice of time-sharded handles is collective: such a handle runs its per-band
+ * engines (band-shard partial mixes) until the caller arms it, and runs stationary exactly when
+ * armed -- an armed handle whose call cannot be stationary returns HZ_E_STATE instead of
+ * diverging from its peers.  Protocol (huygens_amd/shard.py arm_when_ready): after a call, every
+ * rank asks hz_fb_stationary_ready(n) (would a call of n samples be stationary on this handle),
+ * all-reduces the flag with MIN and passes the result to hz_fb_arm_time_shard.  Setters,
+ * hz_fb_set_bank_response and hz_fb_set_time_shard disarm. */
+int hz_fb_stationary_ready(hz_fb* h, long n, int* ready);
+int hz_fb_arm_time_shard(hz_fb* h, int armed);
 /* for a stationary call of n samples: whether it is time-sharded, and its output range */
 int hz_fb_time_shard_info(hz_fb* h, int* active, long* first, long* count, long n);
 /* LTI engine geometry: (chunk length, bands per wave, waves per group) in

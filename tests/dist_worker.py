@@ -72,6 +72,96 @@ def _timeshare(rank, world, N, x):
     return y, full, ShareGather(len(x), rank, world, y, block=256)
 
 
+class FakeShardHandle:
+    """Stands in for huygens_amd.Filterbank on a CPU rank (no GPU here): the methods
+    huygens_amd.shard calls, with a horizon, a response and a readiness schedule chosen per rank,
+    so set_time_shards / arm_when_ready / time_share / ShareGather run through their real code."""
+
+    def __init__(self, rank, K, ready_after, fail_probe=False):
+        self.rank, self.K, self.ready_after, self.fail_probe = rank, K, ready_after, fail_probe
+        self.calls = 0
+        self.bank = None
+        self.shard = None
+        self.armed = False
+        self.log = []
+
+    def response(self, count):
+        if self.fail_probe:
+            raise RuntimeError("HZ_E_UNSUPPORTED: no finite horizon")
+        t = np.arange(count, dtype=np.float64)
+        return np.where(t < self.K, (self.rank + 1) * 0.5 ** (t / 4096.0), 0.0)
+
+    def response_info(self):
+        return self.K, 0, False, 0
+
+    def set_bank_response(self, h):
+        self.bank = np.array(h)
+
+    def set_time_shard(self, rank, world):
+        self.shard = (rank, world)
+
+    def stationary_ready(self, n):
+        return self.calls >= self.ready_after
+
+    def arm_time_shard(self, armed=True):
+        self.armed = bool(armed)
+
+    def call(self):
+        self.calls += 1
+        self.log.append(self.armed)
+
+
+def _shard_protocol(rank, world, variant):
+    """set_time_shards + arm_when_ready over gloo with FakeShardHandle ranks."""
+    import torch
+    import torch.distributed as dist
+    from huygens_amd.shard import ShareGather, arm_when_ready, set_time_shards, time_share
+
+    def ar_sum(a):
+        t = torch.from_numpy(np.array(a, dtype=np.float64))
+        dist.all_reduce(t)
+        return t.numpy()
+
+    def ar_max(k):
+        t = torch.tensor([int(k)], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item())
+
+    def ar_min(k):
+        t = torch.tensor([int(k)], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return int(t.item())
+
+    K = 8192 * (rank + 1)                       # the ranks' horizons differ
+    fb = FakeShardHandle(rank, K, ready_after=1 + 2 * rank,
+                         fail_probe=(variant == "no_horizon" and rank == world - 1))
+    ok = set_time_shards(fb, rank, world, ar_sum, ar_max)
+    res = {"ok": ok}
+    if ok:
+        K_all = 8192 * world
+        t = np.arange(K_all, dtype=np.float64)
+        want = sum(np.where(t < 8192 * (r + 1), (r + 1) * 0.5 ** (t / 4096.0), 0.0) for r in range(world))
+        res["bank_err"] = float(np.max(np.abs(fb.bank - want)))
+        res["bank_len"] = len(fb.bank)
+        res["shard"] = list(fb.shard)
+        armed_at = None
+        for c in range(8):                      # calls, with the arming protocol between them
+            fb.call()
+            if not fb.armed and arm_when_ready(fb, 480000, ar_min):
+                armed_at = fb.calls
+        res["armed_at"] = armed_at
+        res["log"] = fb.log
+        # the armed calls' output shares, assembled on rank 0 through ShareGather
+        n = 100000
+        f, c = time_share(rank, world, n)
+        y = torch.zeros(n, dtype=torch.float64)
+        y[f:f + c] = torch.arange(f, f + c, dtype=torch.float64)
+        ShareGather(n, rank, world, y)(y, dist)
+        if rank == 0:
+            res["gather_err"] = float(torch.max(torch.abs(y - torch.arange(n, dtype=torch.float64))).item())
+    return res
+
+
 def main():
     import torch
     import torch.distributed as dist
@@ -79,6 +169,13 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     kind, out_path = sys.argv[1], sys.argv[2]
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if kind.startswith("protocol"):
+        res = _shard_protocol(rank, world, kind.split(":")[1])
+        with open(f"{out_path}.{rank}", "w") as fh:
+            json.dump(res, fh)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     N = {"filterbank": 96, "oscbank": 50, "bowl": 40, "delaybank": 6, "timeshare": 96}[kind]
     n = 3000
     x = np.random.default_rng(1).uniform(-1, 1, n).astype(np.float32).astype(np.float64)

@@ -40,12 +40,16 @@ _lib = None
 
 
 def lib():
+    """The oracle library: oracle/_build/libhz_oracle.so, or HZ_ORACLE_SO (bench.py's
+    cpu_baseline points it at a -O3 -march=native build of the same sources)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(SO):
+        so = os.environ.get("HZ_ORACLE_SO") or SO
+        if not os.path.exists(so):
             import subprocess
             subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-        _lib = C.CDLL(SO)
+            so = SO
+        _lib = C.CDLL(so)
         for name, (res, args) in _SIGS.items():
             fn = getattr(_lib, name)
             fn.restype = res

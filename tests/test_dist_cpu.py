@@ -33,6 +33,8 @@ def _run(kind, world, tmp_path):
     for p in procs:
         o, _ = p.communicate(timeout=240)
         assert p.returncode == 0, o.decode()[-2000:]
+    if kind.startswith("protocol"):
+        return [json.loads((tmp_path / f"{kind}.json.{r}").read_text()) for r in range(world)]
     return json.loads(out.read_text())
 
 
@@ -73,3 +75,27 @@ def test_shard_of():
     assert shard_of(1, 4, 2) == (1, 1) and shard_of(3, 4, 2) == (2, 0)
     with pytest.raises(ValueError):
         shard_of(2, 2, 5)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_time_shard_protocol(world, tmp_path):
+    """huygens_amd.shard.set_time_shards + arm_when_ready through their real code over gloo (a
+    fake handle stands in for the HIP object): the bank response is the sum of the shards' over the
+    largest horizon on every rank, and the ranks -- ready after different numbers of calls -- are
+    armed in the same call, the one after the slowest rank is ready."""
+    res = _run("protocol:normal", world, tmp_path)
+    for r, rr in enumerate(res):
+        assert rr["ok"] is True
+        assert rr["bank_len"] == 8192 * world and rr["bank_err"] < 1e-12
+        assert rr["shard"] == [r, world]
+        assert rr["armed_at"] == 1 + 2 * (world - 1)          # the slowest rank's readiness
+    logs = [rr["log"] for rr in res]
+    assert all(lg == logs[0] for lg in logs)                # every call: same engine on every rank
+    assert res[0]["gather_err"] == 0.0
+
+
+def test_time_shard_protocol_no_horizon(tmp_path):
+    """One shard without a finite horizon: every rank returns False from set_time_shards (no rank
+    left waiting in a collective) -- ADVICE r2."""
+    res = _run("protocol:no_horizon", 2, tmp_path)
+    assert [rr["ok"] for rr in res] == [False, False]
