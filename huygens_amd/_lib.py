@@ -77,6 +77,9 @@ _SIGS = {
     "hz_fb_process": (I, [VP, PD, PD, SZ]),
     "hz_fb_process_device": (I, [VP, VP, VP, SZ]),
     "hz_fb_tick": (I, [VP]),
+    "hz_fb_sample": (I, [VP, D, I, D, PD]),
+    "hz_fb_sample_tick": (I, [VP]),
+    "hz_fb_sample_info": (I, [VP, C.POINTER(I), C.POINTER(C.c_longlong), C.POINTER(I)]),
     "hz_fb_process_tv": (I, [VP, PD, PD, SZ, I, PD, D]),
     "hz_fb_process_tv_device": (I, [VP, VP, VP, SZ, I, VP, D]),
     "hz_fb_set_stream": (I, [VP, VP]),
@@ -165,6 +168,7 @@ _SIGS = {
     "hz_dly_modulate_back": (I, [VP, I, C.c_uint, C.c_uint, D]),
     "hz_dly_process": (I, [VP, VP, VP, SZ, I, I]),
     "hz_dly_process_device": (I, [VP, VP, VP, SZ, I, I]),
+    "hz_dly_tick": (I, [VP, C.c_ulong]),
     "hz_dly_origin": (I, [VP, C.POINTER(C.c_uint)]),
     "hz_dly_info": (I, [VP, C.POINTER(L), C.POINTER(C.c_uint)]),
     "hz_dly_set_split": (I, [VP, I]),
@@ -179,6 +183,11 @@ _SIGS = {
     "hz_stft_process_block": (I, [VP, PD, PD, PD, PD, SZ]),
     "hz_stft_process_block_device": (I, [VP, VP, VP, VP, VP, SZ]),
     "hz_stft_frames": (I, [VP, C.POINTER(L), C.POINTER(L)]),
+    "hz_stft_write": (I, [VP, D, D]),
+    "hz_stft_read": (I, [VP, PD, PD]),
+    "hz_stft_forward": (I, [VP, I]),
+    "hz_stft_backward": (I, [VP, I]),
+    "hz_stft_process_slot": (I, [VP, I]),
     "hz_stft_set_frame_shard": (I, [VP, I, I, C.c_long]),
     "hz_stft_frames_before": (I, [I, I, C.c_long, C.POINTER(C.c_long)]),
     "hz_stft_set_stream": (I, [VP, VP]),

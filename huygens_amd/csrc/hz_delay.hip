@@ -472,6 +472,16 @@ int hz_dly_process(hz_dly* h, const void* in, void* out, size_t n, int in_per_li
     return HZ_OK;
 }
 
+// Buffer::tick of both rings without a sample (delay.h:92-97 after no operator()): the origins
+// move, nothing is written, so the slots keep the samples of `size` ticks earlier -- later reads
+// see exactly those stale values, as in the reference (every read goes through the rings across
+// calls; the rings are committed at each call's end)
+int hz_dly_tick(hz_dly* h, unsigned long count) {
+    HZ_TRY(dly_check(h));
+    h->origin = (unsigned)(((unsigned long)h->origin + count % h->size) % h->size);
+    return HZ_OK;
+}
+
 int hz_dly_origin(hz_dly* h, unsigned* origin) {
     if (!h || !origin) return HZ_E_INVALID;
     *origin = h->origin;

@@ -178,6 +178,25 @@ struct hz_fb {
         double* d_zero = nullptr;        // N O zeros (x history / start of the zero-start pass)
         size_t zero_cap = 0;
     } resp;
+    // per-sample engine (hz_fb_rt.hip): a kernel resident on the stream serving operator() /
+    // tick() through a pinned-host mailbox while per-sample calls continue
+    struct Rt {
+        bool active = false;         // an instance was launched and not stopped by the host
+        bool computed = false;       // the reference's `computed` (filterbank.h:127-128, 168)
+        bool spare_known = false;    // the ring row at origin is known (after any compute)
+        long long seq = 0;           // last request number posted
+        long long epoch = 0;         // instance number
+        long pending_ticks = 0;      // tick() calls since the last served request
+        int groups = 0;              // workgroups of the instance
+        double cached = 0;           // the last served sample
+        int cached_dist = 0;
+        void* mb = nullptr;          // pinned host mailbox (RtReq + RtSlot[])
+        void* dmb = nullptr;         // its device address
+        void* d_ctl = nullptr;       // device control block (request forwarding)
+        double* d_coef = nullptr;    // [N][2O+1]
+        size_t coef_cap = 0;
+        std::vector<double> h_coef;
+    } rt;
 };
 
 namespace hz_fbi {
@@ -227,5 +246,15 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n);
 int fb_resp_track(hz_fb* h, const double* d_in, long n, bool conv);  // history after any call
 int fb_resp_materialize(hz_fb* h);                                  // LAZY: band states now
 void fb_resp_free(hz_fb* h);
+// hz_filterbank.hip: one ring rotation of a tick() without compute (needs spare_ok)
+int fb_tick_rotate(hz_fb* h);
+// hz_fb_rt.hip (per-sample engine)
+bool fb_rt_supported(const hz_fb* h);
+int fb_rt_stop(hz_fb* h);    // the resident kernel leaves (stream-ordered), pending ticks applied
+// a block call after operator() without tick(): the reference's loop returns the cached sample
+// first (re-mixed with the block's distortion) and ticks; -> samples consumed (0 or 1)
+int fb_rt_resolve(hz_fb* h, double* y0);
+double* fb_rt_cached_slot(hz_fb* h);   // pinned host double for an async copy of that sample
+void fb_rt_free(hz_fb* h);
 
 }  // namespace hz_fbi

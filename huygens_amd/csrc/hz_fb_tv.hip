@@ -432,6 +432,20 @@ int hz_fb_process_tv_device(hz_fb* h, const double* d_in, double* d_out, size_t 
         hz::set_error("hz_fb_process_tv: null buffer");
         return HZ_E_INVALID;
     }
+    if (h->rt.computed) {   // after operator() without tick(): the cached sample first (fb_rt_resolve)
+        double y0 = 0;
+        const int k = hz_fbi::fb_rt_resolve(h, &y0);
+        if (k < 0) return k;
+        double* pin0 = hz_fbi::fb_rt_cached_slot(h);
+        *pin0 = y0;
+        HZ_TRY_HIP(hipMemcpyAsync(d_out, pin0, sizeof(double), hipMemcpyHostToDevice, h->stream));
+        const long row0 = kind == HZ_FB_TV_COEFFS ? (2 * O + 1) * (long)h->N : (long)h->N;
+        ++d_in;
+        ++d_out;
+        d_stream += row0;
+        if (--n == 0) return HZ_OK;
+    }
+    HZ_TRY(hz_fbi::fb_rt_stop(h));   // the state back from the per-sample engine
     // pin / gin.  This call's last row supersedes a pending one, and the stream kernel does not
     // read the staged coefficients, so their rebuild waits for the next plain call.
     h->tv_pending = false;

@@ -905,8 +905,10 @@ int fb_check(hz_fb* h) {
         return HZ_E_INVALID;
     }
     HZ_TRY_HIP(hipSetDevice(h->device));
-    return HZ_OK;
+    // every device-side use of the state needs it back from the per-sample engine
+    return hz_fbi::fb_rt_stop(h);
 }
+
 
 // global band index -> local, or -1 when outside this shard
 int fb_local(const hz_fb* h, int n) {
@@ -915,6 +917,28 @@ int fb_local(const hz_fb* h, int n) {
 }
 
 }  // namespace
+
+namespace hz_fbi {
+int fb_tick_rotate(hz_fb* h) {
+    const int O = h->order;
+    if (O == 0) return HZ_OK;   // one-row rings: origin stays 0, nothing moves
+    if (!h->spare_ok) {
+        hz::set_error("hz_fb_tick: tick() without operator() after a block call or set_state: the ring row "
+                      "it would reuse (O+1 samples back) is not kept");
+        return HZ_E_STATE;
+    }
+    HZ_TRY(hz_fbi::fb_resp_materialize(h));
+    h->resp.run = 0;   // the rotation reuses a stale row: no longer the response of the inputs
+    const int N = h->N;
+    hipLaunchKernelGGL(fb_tick_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, h->stream,
+                       (const double*)h->d_ystate[h->scur], h->d_ystate[h->scur ^ 1], (const double*)h->d_pg[h->scur],
+                       h->d_pg[h->scur ^ 1], (const double*)h->d_xhist[h->xcur], h->d_xhist[h->xcur ^ 1], N, O);
+    HZ_TRY_HIP(hipGetLastError());
+    h->scur ^= 1;
+    h->xcur ^= 1;
+    return HZ_OK;
+}
+}  // namespace hz_fbi
 
 extern "C" {
 
@@ -997,7 +1021,10 @@ int hz_fb_create(int order, int N, double k_p, double k_g, int device, hz_fb** o
 int hz_fb_destroy(hz_fb* h) {
     if (!h) return HZ_OK;
     (void)hipSetDevice(h->device);
+    h->rt.pending_ticks = 0;
+    (void)hz_fbi::fb_rt_stop(h);   // the resident per-sample kernel leaves before the buffers go
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    hz_fbi::fb_rt_free(h);
     for (double* p : {h->d_rec, h->d_pin, h->d_gin, h->d_ystate[0], h->d_ystate[1], h->d_pg[0], h->d_pg[1],
                       h->d_xhist[0], h->d_xhist[1],
                       h->d_partial, h->d_seg, h->d_in, h->d_out})
@@ -1119,23 +1146,43 @@ int hz_fb_set_distortion(hz_fb* h, int dist_id, double param) {
 }
 
 int hz_fb_process_device(hz_fb* h, const double* d_in, double* d_out, size_t n) {
-    HZ_TRY(fb_check(h));
     if (n == 0) return HZ_OK;
-    if (!d_in || !d_out) {
-        hz::set_error("hz_fb_process_device: null buffer");
+    if (!h || !d_in || !d_out) {
+        hz::set_error("hz_fb_process_device: null handle or buffer");
         return HZ_E_INVALID;
     }
+    if (h->rt.computed) {   // the cached sample first (fb_rt_resolve), copied from pinned memory
+        HZ_TRY_HIP(hipSetDevice(h->device));
+        double y0 = 0;
+        const int k = hz_fbi::fb_rt_resolve(h, &y0);
+        if (k < 0) return k;
+        double* pin0 = hz_fbi::fb_rt_cached_slot(h);
+        *pin0 = y0;
+        HZ_TRY_HIP(hipMemcpyAsync(d_out, pin0, sizeof(double), hipMemcpyHostToDevice, h->stream));
+        ++d_in;
+        ++d_out;
+        if (--n == 0) return HZ_OK;
+    }
+    HZ_TRY(fb_check(h));
     HZ_TRY(fb_upload(h));
     return fb_launch(h, d_in, d_out, (long)n);
 }
 
 int hz_fb_process(hz_fb* h, const double* in, double* out, size_t n) {
-    HZ_TRY(fb_check(h));
     if (n == 0) return HZ_OK;
-    if (!in || !out) {
-        hz::set_error("hz_fb_process: null buffer");
+    if (!h || !in || !out) {
+        hz::set_error("hz_fb_process: null handle or buffer");
         return HZ_E_INVALID;
     }
+    if (h->rt.computed) {   // the cached sample first (fb_rt_resolve)
+        HZ_TRY_HIP(hipSetDevice(h->device));
+        const int k = hz_fbi::fb_rt_resolve(h, out);
+        if (k < 0) return k;
+        ++in;
+        ++out;
+        if (--n == 0) return HZ_OK;
+    }
+    HZ_TRY(fb_check(h));
     if (n > h->io_cap) {
         if (h->d_in) HZ_TRY_HIP(hipFree(h->d_in));
         if (h->d_out) HZ_TRY_HIP(hipFree(h->d_out));
@@ -1223,24 +1270,9 @@ int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
 
 int hz_fb_tick(hz_fb* h) {
     HZ_TRY(fb_check(h));
-    const int O = h->order;
-    if (O == 0) return HZ_OK;   // one-row rings: origin stays 0, nothing moves
-    if (!h->spare_ok) {
-        hz::set_error("hz_fb_tick: tick() without operator() after a block call or set_state: the ring row "
-                      "it would reuse (O+1 samples back) is not kept");
-        return HZ_E_STATE;
-    }
-    HZ_TRY(hz_fbi::fb_resp_materialize(h));
-    h->resp.run = 0;   // the rotation reuses a stale row: no longer the response of the inputs
-    const int N = h->N;
-    hipLaunchKernelGGL(fb_tick_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, h->stream,
-                       (const double*)h->d_ystate[h->scur], h->d_ystate[h->scur ^ 1], (const double*)h->d_pg[h->scur],
-                       h->d_pg[h->scur ^ 1], (const double*)h->d_xhist[h->xcur], h->d_xhist[h->xcur ^ 1], N, O);
-    HZ_TRY_HIP(hipGetLastError());
-    h->scur ^= 1;
-    h->xcur ^= 1;
-    return HZ_OK;
+    return hz_fbi::fb_tick_rotate(h);
 }
+
 
 int hz_fb_info(hz_fb* h, int* order, int* N_local, int* band_begin, int* N_total) {
     if (!h) return HZ_E_INVALID;

@@ -603,6 +603,71 @@ int ilog2(int N) {
 }
 
 bool pow2(int N) { return N >= 4 && (N & (N - 1)) == 0; }
+// ---- per-sample slot mode (hz_stft_write / read / forward / backward / process_slot) ----------
+// The reference's own state machine runs on the host (fourier.h:102-177: O(2 laps) bookkeeping
+// per sample); the transforms and device processors of a completed slot run here, one
+// workgroup per N-point transform, natural order in and out (FFTW's dft_1d convention,
+// unnormalised): forward = the frame kernel's passes, then the bit-reversal on the way out;
+// inverse = the bit-reversal on the way in, then the inverse passes.
+template <int RMAX, bool INV>
+__global__ __launch_bounds__(kFrameThreads) void slot_fft_kernel(const double2* __restrict__ src, double2* __restrict__ dst,
+                                                                int N, int lg, const double2* __restrict__ tw) {
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* re = lds;
+    double* im = lds + hz::padded_len(N);
+    double2* T = (double2*)(im + hz::padded_len(N) + 2 * (blockDim.x >> 6));
+    for (int k = threadIdx.x; k < hz::twc_len(lg); k += blockDim.x) T[k] = tw[k];
+    for (int p = threadIdx.x; p < N; p += blockDim.x) {
+        const double2 v = src[INV ? hz::bitrev(p, lg) : p];
+        re[hz::pad16(p)] = v.x;
+        im[hz::pad16(p)] = v.y;
+    }
+    __syncthreads();
+    if constexpr (INV) hz::fft_inv_tail<RMAX>(re, im, lg, T, true);
+    else hz::fft_fwd_lead<RMAX>(re, im, lg, T, true);
+    for (int p = threadIdx.x; p < N; p += blockDim.x) {
+        const int e = hz::pad16(p);
+        dst[INV ? p : hz::bitrev(p, lg)] = make_double2(re[e], im[e]);
+    }
+}
+
+// a device processor on one natural-order spectrum: in -> out (out is the slot's persistent
+// output buffer: the gates write every bin of it, as the reference's processors do)
+template <int PROC>
+__global__ __launch_bounds__(kFrameThreads) void slot_proc_kernel(const double2* __restrict__ in, double2* __restrict__ out,
+                                                                  int N, double p0, double p1) {
+#pragma clang fp contract(off)
+    __shared__ double scratch[2 * (kFrameThreads / 64)];
+    if constexpr (PROC == HZ_PROC_STATIC_GATE) {   // staticSTFT.h:99-128
+        const double inv_n = 1.0 / N;
+        double part = 0.0;
+        for (int k = threadIdx.x; k < N; k += blockDim.x) part += sqrt(in[k].x * in[k].x + in[k].y * in[k].y) * inv_n;
+        const double average = block_sum(part, scratch);
+        const double thr = p0 * average * average;
+        for (int k = threadIdx.x; k < N; k += blockDim.x) {
+            const double2 v = in[k];
+            out[k] = v.x * v.x + v.y * v.y < thr ? make_double2(v.x * p1, v.y * p1) : v;
+        }
+    } else if constexpr (PROC == HZ_PROC_GATE_KEEP) {   // tests/spectral.cpp:32-72
+        double hi = 0.0, lo = 0.0;
+        for (int k = threadIdx.x; k < N; k += blockDim.x) hz::dd_add(hi, lo, hypot(in[k].x, in[k].y));
+        block_sum_dd(hi, lo, scratch);
+        const double q = hi / N;
+        const double avg = q + (fma(-q, (double)N, hi) + lo) / N;
+        const double thr = p0 * avg * avg;
+        for (int k = threadIdx.x; k < N; k += blockDim.x) {
+            const double2 v = in[k];
+            out[k] = v.x * v.x + v.y * v.y > thr ? v : make_double2(0.0, 0.0);
+        }
+    } else if constexpr (PROC == HZ_PROC_HILBERT) {   // tests/SFML/hilbert.cpp:37-49: bins k < N/2
+        for (int k = threadIdx.x; k < N; k += blockDim.x) out[k] = k < N / 2 ? in[k] : make_double2(0.0, 0.0);
+    } else {
+        for (int k = threadIdx.x; k < N; k += blockDim.x) out[k] = in[k];
+    }
+}
+
+
 
 std::vector<double2> twiddles(int N) {
     std::vector<double2> tw(N / 2);
@@ -644,6 +709,14 @@ struct hz_stft {
     // time-range shards: frame f is computed here iff (f / sh_block) % sh_world == sh_rank
     long sh_block = 1;
     int sh_world = 1, sh_rank = 0;
+    // per-sample slot mode (fourier.h:102-177 on the host, transforms on the device): the
+    // reference's in / middle / out slot buffers [2 laps][N] and its read / write heads
+    bool slot_mode = false;
+    std::vector<double2> s_in, s_mid, s_out;
+    std::vector<int> s_wp, s_rp;
+    std::vector<char> s_reading, s_writing;
+    std::vector<double> h_win;
+    double2* d_slot = nullptr;   // [2][N] device scratch
 };
 
 namespace {
@@ -895,6 +968,7 @@ int hz_stft_create(int N, int laps, int window, int proc, double p0, double p1, 
         const double hann = 0.5 * (1 - cos(2 * hz::kPI * p));
         win[k] = window == HZ_WIN_HANN ? hann : sqrt(hann);
     }
+    h->h_win = win;
     const std::vector<double2> tw = twiddles(N);
     bool ok = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess;
     ok = ok && hipMalloc(&h->d_win, sizeof(double) * N) == hipSuccess;
@@ -925,6 +999,9 @@ int hz_stft_create(int N, int laps, int window, int proc, double p0, double p1, 
         frame_attr<HZ_PROC_HILBERT, 0>(lds);
         frame_attr<HZ_PROC_IDENTITY, 1>(lds);
         frame_attr<HZ_PROC_IDENTITY, 2>(lds);
+        for (const void* k : {(const void*)slot_fft_kernel<3, false>, (const void*)slot_fft_kernel<3, true>,
+                              (const void*)slot_fft_kernel<4, false>, (const void*)slot_fft_kernel<4, true>})
+            (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         (void)hipFuncSetAttribute((const void*)dct2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         (void)hipFuncSetAttribute((const void*)dct3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr = true;
@@ -938,7 +1015,7 @@ int hz_stft_destroy(hz_stft* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (void* p : {(void*)h->d_win, (void*)h->d_tw, (void*)h->d_fo, (void*)h->d_hist[0], (void*)h->d_hist[1],
-                    (void*)h->d_spec, (void*)h->d_in, (void*)h->d_out})
+                    (void*)h->d_spec, (void*)h->d_in, (void*)h->d_out, (void*)h->d_slot})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -960,6 +1037,11 @@ int hz_stft_process_block_device(hz_stft* h, const double* d_re, const double* d
                                  double* d_out_im, size_t n) {
     HZ_TRY(stft_check(h));
     if (n == 0) return HZ_OK;
+    if (h->slot_mode) {
+        hz::set_error("hz_stft_process_block: this object is driven per sample (write / read); an object runs "
+                      "either per sample or by blocks");
+        return HZ_E_STATE;
+    }
     if (!d_re || !d_out_re) return HZ_E_INVALID;
     if (h->proc == HZ_PROC_HOST && !h->host_proc) {
         hz::set_error("hz_stft: HZ_PROC_HOST without hz_stft_set_processor");
@@ -991,6 +1073,175 @@ int hz_stft_process_block(hz_stft* h, const double* re, const double* im, double
         HZ_TRY_HIP(hipMemcpyAsync(out_im, h->d_out + n, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
     return HZ_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+int slot_enter(hz_stft* h) {
+    if (h->slot_mode) return HZ_OK;
+    if (h->T != 0 || h->sh_world > 1) {
+        hz::set_error("hz_stft: per-sample calls on an object already driven by blocks (or time-sharded); an "
+                      "object runs either per sample or by blocks");
+        return HZ_E_STATE;
+    }
+    const int S = 2 * h->laps, N = h->N;
+    h->s_in.assign((size_t)S * N, make_double2(0.0, 0.0));
+    h->s_mid.assign((size_t)S * N, make_double2(0.0, 0.0));
+    h->s_out.assign((size_t)S * N, make_double2(0.0, 0.0));
+    h->s_wp.assign(S, 0);
+    h->s_rp.assign(S, 0);
+    h->s_reading.assign(S, 0);
+    h->s_writing.assign(S, 1);
+    for (int i = 0; i < S; ++i) h->s_wp[i] = -h->stride * i;   // fourier.h:76-77
+    if (!h->d_slot) HZ_TRY_HIP(hipMalloc(&h->d_slot, sizeof(double2) * 2 * (size_t)N));
+    h->slot_mode = true;
+    return HZ_OK;
+}
+
+int slot_check(hz_stft* h, int i) {
+    HZ_TRY(stft_check(h));
+    HZ_TRY(slot_enter(h));
+    if (i < 0 || i >= 2 * h->laps) {
+        hz::set_error("hz_stft: slot %d out of range [0, %d)", i, 2 * h->laps);
+        return HZ_E_RANGE;
+    }
+    return HZ_OK;
+}
+
+// one N-point transform of a host slot buffer on the device: src -> dst (natural order)
+int slot_transform(hz_stft* h, const double2* src, double2* dst, bool inverse) {
+    const int N = h->N;
+    HZ_TRY_HIP(hipMemcpyAsync(h->d_slot, src, sizeof(double2) * N, hipMemcpyHostToDevice, h->stream));
+    auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(1), dim3(frame_threads(N)), frame_lds(N), h->stream, (const double2*)h->d_slot,
+                           h->d_slot + N, N, h->lg, (const double2*)h->d_tw);
+    };
+    if (frame_rmax(N) == 3) {
+        if (inverse) launch(slot_fft_kernel<3, true>);
+        else launch(slot_fft_kernel<3, false>);
+    } else {
+        if (inverse) launch(slot_fft_kernel<4, true>);
+        else launch(slot_fft_kernel<4, false>);
+    }
+    HZ_TRY_HIP(hipGetLastError());
+    HZ_TRY_HIP(hipMemcpyAsync(dst, h->d_slot + N, sizeof(double2) * N, hipMemcpyDeviceToHost, h->stream));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+// process(i): the processor on middle[i] -> out[i] (fourier.h:141-144; the host callback's
+// return value is ignored there too)
+int slot_process(hz_stft* h, int i) {
+    const int N = h->N;
+    double2* mid = &h->s_mid[(size_t)i * N];
+    double2* out = &h->s_out[(size_t)i * N];
+    if (h->proc == HZ_PROC_HOST) {
+        if (!h->host_proc) {
+            hz::set_error("hz_stft: HZ_PROC_HOST without hz_stft_set_processor");
+            return HZ_E_INVALID;
+        }
+        (void)h->host_proc((const double*)mid, (double*)out);
+        return HZ_OK;
+    }
+    HZ_TRY_HIP(hipMemcpyAsync(h->d_slot, mid, sizeof(double2) * N, hipMemcpyHostToDevice, h->stream));
+    HZ_TRY_HIP(hipMemcpyAsync(h->d_slot + N, out, sizeof(double2) * N, hipMemcpyHostToDevice, h->stream));
+    const double2* a = h->d_slot;
+    double2* b = h->d_slot + N;
+    switch (h->proc) {
+    case HZ_PROC_STATIC_GATE:
+        hipLaunchKernelGGL(slot_proc_kernel<HZ_PROC_STATIC_GATE>, dim3(1), dim3(kFrameThreads), 0, h->stream, a, b, N,
+                           h->p0, h->p1);
+        break;
+    case HZ_PROC_GATE_KEEP:
+        hipLaunchKernelGGL(slot_proc_kernel<HZ_PROC_GATE_KEEP>, dim3(1), dim3(kFrameThreads), 0, h->stream, a, b, N,
+                           h->p0, h->p1);
+        break;
+    case HZ_PROC_HILBERT:
+        hipLaunchKernelGGL(slot_proc_kernel<HZ_PROC_HILBERT>, dim3(1), dim3(kFrameThreads), 0, h->stream, a, b, N,
+                           h->p0, h->p1);
+        break;
+    default:
+        hipLaunchKernelGGL(slot_proc_kernel<HZ_PROC_IDENTITY>, dim3(1), dim3(kFrameThreads), 0, h->stream, a, b, N,
+                           h->p0, h->p1);
+    }
+    HZ_TRY_HIP(hipGetLastError());
+    HZ_TRY_HIP(hipMemcpyAsync(out, b, sizeof(double2) * N, hipMemcpyDeviceToHost, h->stream));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// fourier.h:102-128: the window times the sample into every writing slot; a full slot turns to
+// reading and runs forward(i), process(i), backward(i)
+int hz_stft_write(hz_stft* h, double real, double imag) {
+    HZ_TRY(stft_check(h));
+    HZ_TRY(slot_enter(h));
+    const int N = h->N;
+    for (int i = 0; i < 2 * h->laps; ++i) {
+        if (!h->s_writing[i]) continue;
+        const int wp = h->s_wp[i];
+        if (wp >= 0) {
+            const double window = h->h_win[wp];   // halfhann / hann (wp / (double) N), as created
+            h->s_in[(size_t)i * N + wp] = make_double2(window * real, window * imag);
+        }
+        if (++h->s_wp[i] == N) {
+            h->s_writing[i] = 0;
+            h->s_reading[i] = 1;
+            h->s_rp[i] = 0;
+            HZ_TRY(hz_stft_forward(h, i));
+            HZ_TRY(hz_stft_process_slot(h, i));
+            HZ_TRY(hz_stft_backward(h, i));
+            ++h->frames;
+        }
+    }
+    return HZ_OK;
+}
+
+// fourier.h:147-177: the windowed overlap-add of the reading slots, in long double, divided by
+// the int N * laps / 2; a slot read to its end turns back to writing
+int hz_stft_read(hz_stft* h, double* real, double* imag) {
+    HZ_TRY(stft_check(h));
+    HZ_TRY(slot_enter(h));
+    const int N = h->N;
+    long double ra = 0, ia = 0;
+    for (int i = 0; i < 2 * h->laps; ++i) {
+        if (!h->s_reading[i]) continue;
+        const int rp = h->s_rp[i];
+        const double window = h->h_win[rp];
+        const double2 v = h->s_in[(size_t)i * N + rp];
+        ra += window * v.x;
+        ia += window * v.y;
+        if (++h->s_rp[i] == N) {
+            h->s_writing[i] = 1;
+            h->s_reading[i] = 0;
+            h->s_wp[i] = 0;
+        }
+    }
+    ra /= N * h->laps / 2;
+    ia /= N * h->laps / 2;
+    if (real) *real = (double)ra;
+    if (imag) *imag = (double)ia;
+    return HZ_OK;
+}
+
+int hz_stft_forward(hz_stft* h, int i) {   // fourier.h:130-133: FFT in[i] -> middle[i]
+    HZ_TRY(slot_check(h, i));
+    return slot_transform(h, &h->s_in[(size_t)i * h->N], &h->s_mid[(size_t)i * h->N], false);
+}
+
+int hz_stft_backward(hz_stft* h, int i) {   // fourier.h:135-138: IFFT out[i] -> in[i]
+    HZ_TRY(slot_check(h, i));
+    return slot_transform(h, &h->s_out[(size_t)i * h->N], &h->s_in[(size_t)i * h->N], true);
+}
+
+int hz_stft_process_slot(hz_stft* h, int i) {   // fourier.h:141-144
+    HZ_TRY(slot_check(h, i));
+    return slot_process(h, i);
 }
 
 int hz_stft_set_frame_shard(hz_stft* h, int rank, int world, long block) {

@@ -69,6 +69,11 @@ class Delaybank:
         check(self._lib.hz_dly_process_device(self._h, C.c_void_p(in_ptr), C.c_void_p(out_ptr), n,
                                               1 if per_line else 0, 1 if mix else 0))
 
+    def tick(self, count: int = 1):
+        """tick() without operator() (delay.h:92-97), count times: both rings' origins move and
+        no slot is written (hz_dly_tick)."""
+        check(self._lib.hz_dly_tick(self._h, int(count)))
+
     def origin(self) -> int:
         o = C.c_uint()
         check(self._lib.hz_dly_origin(self._h, C.byref(o)))

@@ -38,8 +38,6 @@ class Filterbank:
         self.N = N
         self.shard = shard
         self._dist = (HZ_DIST_NONE, 0.0)
-        self._computed = False
-        self._cached = 0.0
         self._lti_geom = 1
 
     def close(self):
@@ -91,7 +89,6 @@ class Filterbank:
         out = np.empty_like(xi)
         if len(xi):
             check(self._lib.hz_fb_process(self._h, dptr(xi), dptr(out), len(xi)))
-        self._computed = False
         return out
 
     def process_device(self, x_ptr: int, out_ptr: int, n: int):
@@ -106,7 +103,6 @@ class Filterbank:
         st = np.ascontiguousarray(stream, dtype=np.float64)
         out = np.empty_like(xi)
         check(self._lib.hz_fb_process_tv(self._h, dptr(xi), dptr(out), len(xi), kind, dptr(st), float(param)))
-        self._computed = False
         return out
 
     def process_tv_device(self, x_ptr: int, out_ptr: int, n: int, kind: int, stream_ptr: int, param: float = 0.0):
@@ -114,22 +110,22 @@ class Filterbank:
                                                 C.c_void_p(stream_ptr), float(param)))
 
     def __call__(self, sample: float) -> float:
-        """T operator()(T) (filterbank.h:125-131): cached until tick()."""
-        if not self._computed:
-            xi = np.array([sample], dtype=np.float64)
-            out = np.empty(1)
-            check(self._lib.hz_fb_process(self._h, dptr(xi), dptr(out), 1))
-            self._cached = float(out[0])
-            self._computed = True
-        return self._cached
+        """T operator()(T) / operator()(T, dist) (filterbank.h:125-139) on the GPU's per-sample
+        engine (hz_fb_sample): cached until tick(); the distortion is the one set by distortion()."""
+        y = C.c_double()
+        check(self._lib.hz_fb_sample(self._h, float(sample), int(self._dist[0]), float(self._dist[1]),
+                                     C.byref(y)))
+        return y.value
 
     def tick(self):
-        """tick() (filterbank.h:142-148).  After operator() the GPU state already advanced
-        there; without one, hz_fb_tick moves the ring as the reference does (nothing computed,
-        smoothers still, the row from O+1 samples back becomes the newest history row)."""
-        if not self._computed:
-            check(self._lib.hz_fb_tick(self._h))
-        self._computed = False
+        """tick() (filterbank.h:142-148): recorded, applied with the next sample (or block call)."""
+        check(self._lib.hz_fb_sample_tick(self._h))
+
+    def sample_info(self):
+        """-> (resident kernel serving, requests posted, workgroups)"""
+        a, n, g = C.c_int(), C.c_longlong(), C.c_int()
+        check(self._lib.hz_fb_sample_info(self._h, C.byref(a), C.byref(n), C.byref(g)))
+        return bool(a.value), n.value, g.value
 
     # ---- stream / state ------------------------------------------------------
     def set_stream(self, stream_ptr: int | None):

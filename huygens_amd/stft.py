@@ -74,6 +74,24 @@ class Fourier:
         check(self._lib.hz_stft_frames(self._h, C.byref(f), C.byref(t)))
         return f.value, t.value
 
+    # ---- per-sample operator API (fourier.h:102-177), exact state machine -----------------
+    def write(self, re: float, im: float = 0.0):
+        check(self._lib.hz_stft_write(self._h, float(re), float(im)))
+
+    def read(self):
+        r, i = C.c_double(), C.c_double()
+        check(self._lib.hz_stft_read(self._h, C.byref(r), C.byref(i)))
+        return r.value, i.value
+
+    def forward(self, slot: int):
+        check(self._lib.hz_stft_forward(self._h, int(slot)))
+
+    def backward(self, slot: int):
+        check(self._lib.hz_stft_backward(self._h, int(slot)))
+
+    def process(self, slot: int):
+        check(self._lib.hz_stft_process_slot(self._h, int(slot)))
+
     def set_frame_shard(self, rank: int, world: int, block: int):
         """Time-range shard: compute frame f iff (f // block) % world == rank
         (hz_stft_set_frame_shard); the ranks' outputs sum to the unsharded output."""

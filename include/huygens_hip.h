@@ -85,6 +85,20 @@ int hz_fb_process_device(hz_fb* h, const double* d_in, double* d_out, size_t n);
  * is not kept and hz_fb_tick returns HZ_E_STATE.  (A tick() that follows operator() is
  * already part of every process call.) */
 int hz_fb_tick(hz_fb* h);
+/* Per-sample operator API on the GPU (hz_fb_rt.hip): T operator()(T x) / operator()(T x, dist)
+ * (filterbank.h:125-139) and tick() (142-148) with the reference's exact semantics -- a repeated
+ * operator() before tick() returns the cached row re-mixed (no compute); ticks without operator()
+ * rotate the ring (the row O+1 samples back becomes the newest history row).  Served by a kernel
+ * that stays resident on the handle's stream while per-sample calls continue (pinned-host
+ * mailbox, a few microseconds per sample whatever N); it leaves on the next block call, state
+ * read/write, destroy, or after 100 ms without a call.  hz_fb_sample_tick only records the tick
+ * (no GPU work).  Block calls after an operator() without tick() output the cached sample first,
+ * as the reference's loop does.  HZ_E_UNSUPPORTED above 262,144 bands (orders <= 2; 131,072
+ * above), HZ_E_STATE for a bare tick whose ring row is unknown (see hz_fb_tick). */
+int hz_fb_sample(hz_fb* h, double x, int dist_id, double param, double* y);
+int hz_fb_sample_tick(hz_fb* h);
+/* whether the resident kernel is serving, requests posted so far, its workgroups */
+int hz_fb_sample_info(hz_fb* h, int* active, long long* served, int* groups);
 int hz_fb_set_stream(hz_fb* h, void* hip_stream);
 int hz_fb_get_stream(hz_fb* h, void** hip_stream);
 int hz_fb_synchronize(hz_fb* h);
@@ -275,6 +289,9 @@ int hz_dly_modulate_back(hz_dly* h, int line, unsigned n, unsigned time, double 
  * the mixdown sum_k y_k / N, summed in line order in T (mix 1). */
 int hz_dly_process(hz_dly* h, const void* in, void* out, size_t n, int in_per_line, int mix);
 int hz_dly_process_device(hz_dly* h, const void* d_in, void* d_out, size_t n, int in_per_line, int mix);
+/* tick() without operator() (delay.h:92-97), `count` times: both rings' origins move and no
+ * slot is written (the stale samples stay, as in the reference) */
+int hz_dly_tick(hz_dly* h, unsigned long count);
 int hz_dly_origin(hz_dly* h, unsigned* origin);            /* Buffer::origin after the last call */
 int hz_dly_info(hz_dly* h, long* chunk, unsigned* size);   /* sub-block length (-1: unbounded), ring size */
 int hz_dly_set_split(hz_dly* h, int mode);                 /* 0 auto, 1 workgroup per line, 2 launch per sub-block */
@@ -307,6 +324,19 @@ int hz_stft_process_block(hz_stft* h, const double* re, const double* im, double
 int hz_stft_process_block_device(hz_stft* h, const double* d_re, const double* d_im, double* d_out_re,
                                  double* d_out_im, size_t n);
 int hz_stft_frames(hz_stft* h, long* frames, long* samples);
+/* Per-sample operator API, exactly the reference's state machine: write(re, im) (fourier.h:
+ * 102-128), read(&re, &im) (147-177; long double overlap-add, / the int N*laps/2), in any order
+ * and number, and the slot operations forward(i) (FFT in[i] -> middle[i], 130-133), backward(i)
+ * (IFFT out[i] -> in[i], 135-138) and process(i) (the processor middle[i] -> out[i], 141-144).
+ * The O(2 laps) bookkeeping per sample runs on the host; each slot transform and device
+ * processor runs on the GPU (one workgroup per N-point transform).  An object is driven either
+ * per sample or by blocks (hz_stft_process_block): the first call decides, the other kind then
+ * returns HZ_E_STATE. */
+int hz_stft_write(hz_stft* h, double real, double imag);
+int hz_stft_read(hz_stft* h, double* real, double* imag);
+int hz_stft_forward(hz_stft* h, int slot);
+int hz_stft_backward(hz_stft* h, int slot);
+int hz_stft_process_slot(hz_stft* h, int slot);
 /* Time-range shards (STFT): runs of `block` consecutive frames rotate over
  * `world` ranks; this handle computes frame f iff (f / block) % world == rank.  Its other
  * frames are skipped and add nothing to its overlap-add -- in this call or the later calls a

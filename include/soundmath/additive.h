@@ -15,7 +15,7 @@ class Additive {
 
 public:
     Additive(Wave<T>* form, uint voices, uint overtones, T decay, T harmonicity = 1.0, T k = 0.1, int device = 0) {
-        if (form != &cycle) throw std::runtime_error("Additive: only the cycle waveform runs on the device");
+        if (!form || form->kind != Shape::cycle) throw std::runtime_error("Additive: only the cycle waveform runs on the device");
         hz_add* h = nullptr;
         detail::check(hz_add_create((int)voices, (int)overtones, decay, harmonicity, k, device, &h), "Additive");
         h_ = decltype(h_)(h);

@@ -14,7 +14,7 @@ class Bowl {
 public:
     Bowl(int overtones, const std::vector<T>& f, const std::vector<T>& a, const std::vector<T>& d,
          Wave<T>* form = default_form(), int device = 0) {
-        if (!form || form->shape != Shape::cycle) throw std::runtime_error("Bowl: only sin(2 PI p) runs on the device");
+        if (!form || form->kind != Shape::cycle) throw std::runtime_error("Bowl: only sin(2 PI p) runs on the device");
         const std::vector<double> fd(f.begin(), f.end()), ad(a.begin(), a.end()), dd(d.begin(), d.end());
         const int count = (int)std::min(fd.size(), std::min(ad.size(), dd.size()));
         hz_bowl* h = nullptr;

@@ -55,11 +55,10 @@ public:
         }
         return {out_, (std::size_t)N};
     }
+    // delay.h:92-97: after operator() the engine has advanced already; without one, both rings'
+    // origins move and nothing is written (hz_dly_tick)
     void tick() {
-        if (!computed_) {   // a tick without a sample: zero input
-            T zero[N] = {};
-            detail::check(hz_dly_process(h_.get(), zero, out_, 1, 1, 0), "Delaybank::tick");
-        }
+        if (!computed_) detail::check(hz_dly_tick(h_.get(), 1), "Delaybank::tick");
         computed_ = false;
     }
     // in: mono [n] (per_line false) or [N][n]; out: [N][n] or the mixdown [n]

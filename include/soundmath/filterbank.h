@@ -1,7 +1,9 @@
 // soundmath/filterbank.h -- drop-in Filterbank<T> (src/filterbank.h:16-188) over the HIP
-// engine.  T = double (the engine's arithmetic).  process() is the GPU path; the
-// per-sample operator()/tick() pair is kept with its caching semantics (a repeated
-// operator() before tick() returns the cached sample) and runs one-sample launches.
+// engine.  T = double (the engine's arithmetic).  process() is the block path; the per-sample
+// operator()/tick() pair runs on the GPU's per-sample engine (hz_fb_sample: a kernel resident on
+// the handle's stream, a few microseconds per sample whatever the band count) with the
+// reference's exact semantics -- a repeated operator() before tick() returns the cached row
+// (re-mixed with its functor), a tick() without operator() rotates the ring.
 // operator()(T, T(*)(T)) takes a device functor id instead of a host function pointer
 // (HZ_DIST_SOFTCLIP / SATURATE / LIMITER, see huygens_hip.h).
 #pragma once
@@ -40,14 +42,7 @@ public:
 
     T operator()(T sample) { return sample_with(sample, HZ_DIST_NONE, 0.0); }
     T operator()(T sample, int dist_id, double param = 0.0) { return sample_with(sample, dist_id, param); }
-    // After operator() the engine already advanced.  Without one, the reference's tick() only
-    // moves origin: nothing is computed, the smoothers stand still and the next sample reads the
-    // ring row left from O+1 samples earlier -- hz_fb_tick does exactly that (HZ_E_STATE after
-    // a block process() call, whose last O+1 rows the handle does not keep).
-    void tick() {
-        if (!computed_) detail::check(hz_fb_tick(h_.get()), "Filterbank::tick");
-        computed_ = false;
-    }
+    void tick() { detail::check(hz_fb_sample_tick(h_.get()), "Filterbank::tick"); }
 
     // n x { out[i] = operator()(in[i]); tick(); }
     void process(const T* in, T* out, std::size_t n, int dist_id = HZ_DIST_NONE, double param = 0.0) {
@@ -76,17 +71,12 @@ public:
 
 private:
     T sample_with(T sample, int dist_id, double param) {
-        if (!computed_) {
-            detail::check(hz_fb_set_distortion(h_.get(), dist_id, param), "Filterbank::operator()");
-            detail::check(hz_fb_process(h_.get(), &sample, &last_, 1), "Filterbank::operator()");
-            computed_ = true;
-        }
-        return last_;
+        T y = 0;
+        detail::check(hz_fb_sample(h_.get(), sample, dist_id, param, &y), "Filterbank::operator()");
+        return y;
     }
     handle<hz_fb, hz_fb_destroy> h_;
     int N_, order_;
-    bool computed_ = false;
-    T last_ = 0;
 };
 
 // FFilterbank<T, N, order> (src/filterbank.h:191-319): the fixed-size variant.  The

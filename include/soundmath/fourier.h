@@ -1,12 +1,13 @@
 // soundmath/fourier.h -- drop-in Fourier (src/fourier.h:50-194), StaticSTFT
 // (src/staticSTFT.h:10-177) and Cosine (src/fourier.h:197-234) over the HIP engine.
 //
-// process_block() is the GPU path.  write()/read() keep the reference's per-sample pair
-// for the usual alternation (write(x_t) then read()); each read() processes the pending
-// write as a one-sample block.  forward(i)/backward(i)/process(i) act on slots of the
-// per-sample state machine and have no block counterpart; they are not provided.
-// A processor is the reference's int(*)(const complex<double>*, complex<double>*), run on
-// the host per frame in frame order, or a built-in device processor (HZ_PROC_*).
+// Two ways to drive a Fourier, chosen by the first call:
+//   per sample: write() / read() in any order and number, and the public slot operations
+//     forward(i) / backward(i) / process(i) -- the reference's own state machine (O(2 laps)
+//     bookkeeping per sample on the host), each slot transform and device processor on the GPU;
+//   by blocks: process_block() == n x {write(x_t); read(&y_t)} on the GPU frame engine.
+// A processor is the reference's int(*)(const complex<double>*, complex<double>*), run on the
+// host per frame in frame order, or a built-in device processor (HZ_PROC_*).
 #pragma once
 
 #include "hz.h"
@@ -21,16 +22,11 @@ public:
     // built-in device processor: HZ_PROC_IDENTITY, HZ_PROC_GATE_KEEP (625), HZ_PROC_HILBERT
     Fourier(int builtin, int N, int laps, int device = 0) { init(builtin, N, laps, HZ_WIN_HALFHANN, device, nullptr); }
 
-    void write(double real, double imag = 0) {
-        pre_ = real;
-        pim_ = imag;
-        pending_ = true;
-    }
-    void read(double* real, double* imag) {
-        const double re = pending_ ? pre_ : 0.0, im = pending_ ? pim_ : 0.0;
-        detail::check(hz_stft_process_block(h_.get(), &re, &im, real, imag, 1), "Fourier::read");
-        pending_ = false;
-    }
+    void write(double real, double imag = 0) { detail::check(hz_stft_write(h_.get(), real, imag), "Fourier::write"); }
+    void read(double* real, double* imag) { detail::check(hz_stft_read(h_.get(), real, imag), "Fourier::read"); }
+    void forward(const int i) { detail::check(hz_stft_forward(h_.get(), i), "Fourier::forward"); }
+    void backward(const int i) { detail::check(hz_stft_backward(h_.get(), i), "Fourier::backward"); }
+    void process(const int i) { detail::check(hz_stft_process_slot(h_.get(), i), "Fourier::process"); }
     void process_block(const double* re, const double* im, double* out_re, double* out_im, std::size_t n) {
         detail::check(hz_stft_process_block(h_.get(), re, im, out_re, out_im, n), "Fourier::process_block");
     }
@@ -48,8 +44,6 @@ protected:
             detail::check(hz_stft_set_processor(h, reinterpret_cast<hz_stft_proc>(fn)), "Fourier");
     }
     handle<hz_stft, hz_stft_destroy> h_;
-    double pre_ = 0, pim_ = 0;
-    bool pending_ = false;
 };
 
 class StaticSTFT : public Fourier {

@@ -20,43 +20,10 @@
 #include <type_traits>
 #include <vector>
 
+#include "buffer.h"
 #include "hz.h"
 
 namespace soundmath {
-
-// Circular buffer (src/buffer.h:9-86), host side: unsigned origin/size as the reference,
-// so the interpolated read keeps its mod-2^32 wrap.
-template <typename T>
-class Buffer {
-public:
-    Buffer() = default;
-    explicit Buffer(unsigned size) { initialize(size); }
-    void initialize(unsigned size = 0) {
-        size += (size == 0) ? 1 : 0;   // buffer.h:21
-        size_ = size;
-        origin_ = 0;
-        data_.assign(size, T(0));
-    }
-    void tick() { origin_ = (origin_ + 1) % size_; }
-    T operator()(T position = 0) const {   // buffer.h:40-47 (into the past)
-        const int center = (int)position, before = center + 1;
-        const T disp = position - center;
-        return data_[(origin_ - center + size_) % size_] * (1 - disp) + data_[(origin_ - before + size_) % size_] * disp;
-    }
-    T operator[](T position) const {   // buffer.h:50-57 (static buffers)
-        const int center = (int)position, after = (int)((center + 1) % size_);
-        const T disp = position - center;
-        return data_[(center + size_) % size_] * (1 - disp) + data_[(after + size_) % size_] * disp;
-    }
-    void write(T value) { data_[origin_] = value; }
-    void accum(T value) { data_[origin_] += value; }
-    unsigned get_size() const { return size_; }
-    T current() const { return data_[origin_]; }   // the sample at the write position
-
-private:
-    std::vector<T> data_;
-    unsigned size_ = 1, origin_ = 0;
-};
 
 template <typename T>
 class Granulator {
@@ -66,7 +33,7 @@ public:
     Granulator(Wave<T>* window, Buffer<T>* source, bool realtime = true, unsigned polyphony = 512, int device = 0)
         : source_(source) {
         (void)realtime;   // unused by the reference as well (granulator.h:117)
-        if (!window || window->shape != Shape::hann)
+        if (!window || window->kind != Shape::hann)
             throw std::runtime_error("Granulator: the HIP engine supports the hann window (wave.h:148)");
         hz_gran* h = nullptr;
         detail::check(hz_gran_create(polyphony, source->get_size(), device, &h), "Granulator");

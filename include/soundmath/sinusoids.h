@@ -14,7 +14,7 @@ class Sinusoids {
 public:
     Sinusoids(Wave<T>* form, T fundamental, uint overtones, T decay, T harmonicity = 1, T k = 2.0 / SR,
               int device = 0) {
-        if (form != &cycle) throw std::runtime_error("Sinusoids: only the cycle waveform runs on the device");
+        if (!form || form->kind != Shape::cycle) throw std::runtime_error("Sinusoids: only the cycle waveform runs on the device");
         hz_sin* h = nullptr;
         detail::check(hz_sin_create(fundamental, (int)overtones, decay, harmonicity, k, device, &h), "Sinusoids");
         h_ = decltype(h_)(h);

@@ -107,6 +107,7 @@ void     orc_dly_modulate_forward(orc_dly* b, int line, unsigned n, unsigned t, 
 void     orc_dly_modulate_back(orc_dly* b, int line, unsigned n, unsigned t, double g);
 void     orc_dly_process(orc_dly* b, const void* in, void* out, long n, int in_per_line, int mix);
 unsigned orc_dly_origin(orc_dly* b);
+void orc_dly_tick(orc_dly* b, unsigned long count);
 
 /* ---- Fourier / StaticSTFT / Cosine (src/fourier.h:50-234, src/staticSTFT.h:10-177) ---- */
 #define ORC_PROC_IDENTITY 0
@@ -119,6 +120,9 @@ typedef struct orc_stft orc_stft;
 orc_stft* orc_stft_create(int N, int laps, int window, int proc, double p0, double p1);
 void      orc_stft_set_callback(orc_stft* s, orc_stft_cb cb);
 void      orc_stft_destroy(orc_stft* s);
+void orc_stft_forward(orc_stft* s, int i);
+void orc_stft_backward(orc_stft* s, int i);
+void orc_stft_process_slot(orc_stft* s, int i);
 void      orc_stft_write(orc_stft* s, double re, double im);
 void      orc_stft_read(orc_stft* s, double* re, double* im);
 void      orc_stft_process_block(orc_stft* s, const double* re, const double* im, double* out_re,

@@ -168,4 +168,14 @@ void orc_dly_process(orc_dly* b, const void* in, void* out, long n, int in_per_l
     }
 }
 
+/* tick() without operator() (delay.h:92-97): input.tick(); output.tick() -- the origins move,
+ * nothing is written */
+void orc_dly_tick(orc_dly* b, unsigned long count) {
+    for (unsigned long c = 0; c < count; c++)
+        for (int k = 0; k < b->N; k++) {
+            if (b->is_float) b->lf[k].origin = (b->lf[k].origin + 1) % b->lf[k].size;
+            else b->ld[k].origin = (b->ld[k].origin + 1) % b->ld[k].size;
+        }
+}
+
 unsigned orc_dly_origin(orc_dly* b) { return b->is_float ? b->lf[0].origin : b->ld[0].origin; }

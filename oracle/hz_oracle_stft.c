@@ -177,6 +177,11 @@ static void run_proc(orc_stft* s, const double* in, double* out) {
     }
 }
 
+/* fourier.h:130-144: the slot operations a caller may also invoke directly */
+void orc_stft_forward(orc_stft* s, int i) { dft_ld(s->in + (size_t)2 * s->N * i, s->mid + (size_t)2 * s->N * i, s->N, -1); }
+void orc_stft_backward(orc_stft* s, int i) { dft_ld(s->out + (size_t)2 * s->N * i, s->in + (size_t)2 * s->N * i, s->N, +1); }
+void orc_stft_process_slot(orc_stft* s, int i) { run_proc(s, s->mid + (size_t)2 * s->N * i, s->out + (size_t)2 * s->N * i); }
+
 void orc_stft_write(orc_stft* s, double re, double im) {   /* fourier.h:102-128 */
     const int N = s->N;
     for (int i = 0; i < s->S; i++) {

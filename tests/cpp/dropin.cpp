@@ -2,6 +2,7 @@
 // (tests/resynthesis.cpp, tests/delay.cpp, tests/bowl.cpp, tests/spectral.cpp,
 // tests/fft.cpp).  Writes raw little-endian outputs into argv[1]; tests/test_cpp_gpu.py
 // replays the same scenarios through the oracle.  Build: tests/test_cpp_cpu.py.
+#include <chrono>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -16,6 +17,7 @@
 #include "soundmath/harmbank.h"
 #include "soundmath/oscbank.h"
 #include "soundmath/sinusoids.h"
+#include "soundmath/synth.h"
 
 using namespace soundmath;
 
@@ -63,8 +65,36 @@ int main(int argc, char** argv) {
             fb.tick();
             if (t == 40 || t == 41) fb.tick();   // tick() without operator(): the stale ring row
         }
-        fb.process(x.data() + 100, y.data() + 100, 900);
+        fb.process(x.data() + 100, y.data() + 100, 600);   // block, then per sample again, then block
+        for (int t = 700; t < 800; t++) {
+            y[t] = fb(x[t]);
+            fb.tick();
+        }
+        fb.process(x.data() + 800, y.data() + 800, 200);
         dump("filterbank", y);
+
+        // the per-sample rate of a 4096-band bank (C2's size): operator() + tick() per sample,
+        // the reference's execution model (tests/resynthesis.cpp:35-39)
+        Filterbank<double> big(2, 4096);
+        for (int i = 0; i < 4096; i++) {
+            const double g = 0.001, R = 0.999, th = PI * (i + 0.5) / 4096.0;
+            big.coefficients(i, {g, 0, -g}, {-2 * R * std::cos(th), R * R});
+        }
+        big.boost(std::vector<double>(4096, 1.0));
+        big.open();
+        double acc = 0;
+        for (int t = 0; t < 500; t++) {
+            acc += big(input(t));
+            big.tick();
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int t = 500; t < 20500; t++) {
+            acc += big(input(t));
+            big.tick();
+        }
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("per-sample Filterbank<double>(2, 4096): %.0f samples/s (%.2f us per operator()+tick(), sum %g)\n",
+                    20000 / dt, 1e6 * dt / 20000, acc);
 
         // FFilterbank<double, 16, 2> (tests/filterbank.cpp:184,194 pattern), block form only
         FFilterbank<double, 16, 2> ff;
@@ -98,6 +128,8 @@ int main(int argc, char** argv) {
             y[t] = delay(x[t]);
             delay.tick();
         }
+        delay.tick();   // tick() without operator() (delay.h:92-97): the rings advance, nothing written
+        delay.tick();
         delay.process(x.data() + 10, y.data() + 10, 49990);
         dump("delay", y);
     }
@@ -115,20 +147,52 @@ int main(int argc, char** argv) {
         dump("bowl", y);
     }
     {   // Fourier with a host processor (pointer of the reference's type), StaticSTFT
+        // per sample, tests/spectral.cpp:90-108's loop, with a stretch of two writes per read
+        // (the heads run apart) and one of reads alone (they catch up) -- the reference's own
+        // state machine
         Fourier F(hilbert64, 64, 4);
-        std::vector<double> yr(1000), yi(1000), x(1000), z(1000, 0.0);
+        std::vector<double> yr, yi, x(1000);
         for (int t = 0; t < 1000; t++) x[t] = input(t);
-        for (int t = 0; t < 300; t++) {
-            F.write(x[t]);
-            F.read(&yr[t], &yi[t]);
+        int w = 0;
+        for (int t = 0; t < 900; t++) {
+            F.write(x[w++]);
+            if (t >= 300 && t < 340) F.write(x[w++]);
+            if (t >= 500 && t < 540) continue;   // no read: writes only
+            double r, i;
+            F.read(&r, &i);
+            yr.push_back(r);
+            yi.push_back(i);
+            if (t >= 600 && t < 640) {   // reads alone
+                F.read(&r, &i);
+                yr.push_back(r);
+                yi.push_back(i);
+            }
         }
-        F.process_block(x.data() + 300, z.data() + 300, yr.data() + 300, yi.data() + 300, 700);
         dump("fourier_re", yr);
         dump("fourier_im", yi);
         StaticSTFT S(64, 4);
         std::vector<double> sr(1000), si(1000);
         S.process_block(x.data(), nullptr, sr.data(), si.data(), 1000);
         dump("static_re", sr);
+    }
+    {   // Synth<double> / Oscillator<double>: tests/eigen.cpp:23, tests/fm.cpp:18 (host, as the reference)
+        Synth<double> s(&cycle, 220.0);
+        Oscillator<double> mod(3.0, 0.25, 0.01);
+        std::vector<double> y;
+        for (int t = 0; t < 3000; t++) {
+            if (t == 1000) s.freqmod(330.0);
+            if (t == 2000) s.phasemod(0.5);
+            y.push_back(s());
+            y.push_back(mod());
+            s.tick();
+            mod.tick();
+        }
+        Synth<double> saw_synth(&saw, 100.0, 0.1);
+        for (int t = 0; t < 500; t++) {
+            y.push_back(saw_synth());
+            saw_synth.tick();
+        }
+        dump("synth", y);
     }
     {   // Cosine: tests/fft.cpp (Cosine dct(N, &dct_in, &dct_out))
         double *in, *out;

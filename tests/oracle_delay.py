@@ -16,6 +16,7 @@ _SIGS = {
     "orc_dly_modulate_back": (None, [VP, I, C.c_uint, C.c_uint, D]),
     "orc_dly_process": (None, [VP, VP, VP, L, I, I]),
     "orc_dly_origin": (C.c_uint, [VP]),
+    "orc_dly_tick": (None, [VP, C.c_ulong]),
 }
 
 
@@ -57,6 +58,10 @@ class OracleDelaybank:
 
     def origin(self):
         return self.l.orc_dly_origin(self.h)
+
+    def tick(self, count=1):
+        """tick() without operator() (delay.h:92-97): origins move, nothing written"""
+        self.l.orc_dly_tick(self.h, count)
 
 
 def taps_of(g, line):

@@ -17,6 +17,9 @@ _SIGS = {
     "orc_stft_read": (None, [VP, PD, PD]),
     "orc_stft_process_block": (None, [VP, PD, PD, PD, PD, L]),
     "orc_stft_frames": (L, [VP]),
+    "orc_stft_forward": (None, [VP, I]),
+    "orc_stft_backward": (None, [VP, I]),
+    "orc_stft_process_slot": (None, [VP, I]),
     "orc_dft": (None, [PD, PD, I, I]),
     "orc_dct": (None, [PD, PD, I, I]),
 }
@@ -52,6 +55,23 @@ class OracleSTFT:
 
     def frames(self):
         return self.l.orc_stft_frames(self.h)
+
+    def write(self, re, im=0.0):           # fourier.h:102-128
+        self.l.orc_stft_write(self.h, float(re), float(im))
+
+    def read(self):                          # fourier.h:147-177
+        r, i = C.c_double(), C.c_double()
+        self.l.orc_stft_read(self.h, C.byref(r), C.byref(i))
+        return r.value, i.value
+
+    def forward(self, slot):
+        self.l.orc_stft_forward(self.h, slot)
+
+    def backward(self, slot):
+        self.l.orc_stft_backward(self.h, slot)
+
+    def process(self, slot):
+        self.l.orc_stft_process_slot(self.h, slot)
 
 
 def oracle_dct(x, kind):

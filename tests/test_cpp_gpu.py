@@ -53,7 +53,11 @@ def test_filterbank(outputs):
         o.tick()
         if t in (40, 41):
             o.tick()
-    want[100:] = o.process(x[100:])
+    want[100:700] = o.process(x[100:700])
+    for t in range(700, 800):
+        want[t] = o(x[t])
+        o.tick()
+    want[800:] = o.process(x[800:])
     assert rel_err(outputs("filterbank"), want) < 1e-9
 
 
@@ -79,13 +83,16 @@ def test_subtractive_resonant_stream(outputs):
 
 
 def test_delay_bit_exact(outputs):
+    """Per-sample operator()/tick() for 10 samples, two ticks without operator() (the rings move,
+    nothing is written: delay.h:92-97), then one block."""
     o = OracleDelaybank(1, 10, 2 * 48000)
     o.coefficients(0, [(0, 1.0)], [(20000, 0.5), (10000, 0.5)])
     x = np.zeros(50000)
     x[0] = 1.0
     y = outputs("delay")
-    assert np.array_equal(y, o.process(x)[0])
-    assert list(np.flatnonzero(y)[:3]) == [0, 10000, 20000]
+    want = np.concatenate([o.process(x[:10])[0], (o.tick(2), o.process(x[10:])[0])[1]])
+    assert np.array_equal(y, want)
+    assert list(np.flatnonzero(y)[:3]) == [0, 9998, 19998]
 
 
 def test_bowl_float(outputs):
@@ -97,13 +104,65 @@ def test_bowl_float(outputs):
 
 
 def test_fourier_host_processor_and_static(outputs):
+    """Fourier per sample with the reference's state machine: alternating write/read, a stretch of
+    two writes per read, writes alone, reads alone; a host processor of the reference's type."""
     x = x_input(1000)
     o = OracleSTFT(64, 4, 0, 3)   # the C++ hilbert64 callback == the built-in half-band
-    orr, oi = o.process_block(x, np.zeros(1000))
+    yr, yi = [], []
+    w = 0
+    for t in range(900):
+        o.write(x[w]); w += 1
+        if 300 <= t < 340:
+            o.write(x[w]); w += 1
+        if 500 <= t < 540:
+            continue
+        r, i = o.read(); yr.append(r); yi.append(i)
+        if 600 <= t < 640:
+            r, i = o.read(); yr.append(r); yi.append(i)
+    orr, oi = np.array(yr), np.array(yi)
     assert rel_err(outputs("fourier_re"), orr) < 1e-10
     assert np.max(np.abs(outputs("fourier_im") - oi)) <= 1e-10 * np.max(np.abs(oi))
     s = OracleSTFT(64, 4, 1, 1)
     assert rel_err(outputs("static_re"), s.process_block(x)[0]) < 1e-10
+
+
+def synth_reference(n, f, phi=0.0, k=2.0 / 48000, shape=lambda p: np.sin(2 * PI * p), events=()):
+    """Oscillator<T>::tick (src/oscillator.h:27-38) and Synth::operator() (synth.h:16-17) in plain
+    Python floats, op for op (abs taken as fabs)."""
+    import math
+    s = 0.0 if k == 0 else 2.0 ** (math.log2(2.220446049250313e-16) / (max(0.0, k) * 48000))
+    freq = abs(f); tf = freq; ph = max(0.0, phi); tp = ph
+    out = []
+    ev = dict(events)
+    for t in range(n):
+        if t in ev:
+            kind, v = ev[t]
+            if kind == "f":
+                tf = v
+            else:
+                tp += v; tp -= int(tp); tp += 1; tp -= int(tp)
+        out.append((shape(ph), ph))
+        ph += freq / 48000
+        tp += freq / 48000
+        freq = tf * (1 - s) + freq * s
+        w = (1 - s) * math.sin(2 * PI * (2 * abs(tp - ph) + 0.25))
+        ph = w * tp + (1 - w) * ph
+        ph -= int(ph)
+        tp -= int(tp)
+    return out
+
+
+def test_synth_and_oscillator(outputs):
+    """Synth<double>(&cycle, 220) with freqmod / phasemod, Oscillator<double>(3, 0.25, 0.01) and a
+    saw Synth: the host classes are exact restatements (bit-identical to the Python replay)."""
+    y = outputs("synth")
+    a = synth_reference(3000, 220.0, events={1000: ("f", 330.0), 2000: ("p", 0.5)}.items())
+    m = synth_reference(3000, 3.0, 0.25, 0.01)
+    want = np.array([v for (sa, _), (_, pm) in zip(a, m) for v in (sa, pm)])
+    saw = synth_reference(500, 100.0, 0.1, shape=lambda p: 2 * p - 1)
+    want = np.concatenate([want, [v for v, _ in saw]])
+    assert y.shape == want.shape
+    assert np.max(np.abs(y - want)) <= 1e-15 * 8, np.max(np.abs(y - want))
 
 
 def test_cosine(outputs):

@@ -136,3 +136,24 @@ def test_errors(gpu_lib):
         b.modulate_forward(5, 0, (1, 1.0))
     with pytest.raises(HZError):
         Delaybank(0, 2, 100)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_bare_ticks(gpu_lib, dtype):
+    """tick() without operator() (delay.h:92-97) only moves both rings' origins: the skipped slots
+    keep the samples written `size` ticks earlier and later reads see those stale values, exactly
+    as the reference (round-2 advisor: the drop-in used to run a zero-input sample instead)."""
+    rng = np.random.default_rng(13)
+    g, o = _pair(5, 3, 700, dtype)
+    for k in range(5):
+        fwd, back = [(0, 1.0), (350 + k, 0.5)], [(300 + 7 * k, 0.4), (701, 0.2)]
+        g.coefficients(k, fwd, back)
+        o.coefficients(k, fwd, back)
+    for n, ticks in ((900, 3), (1, 1), (250, 700), (1, 0), (1200, 1401), (64, 5)):
+        x = (0.1 * rng.standard_normal(n)).astype(dtype)
+        assert np.array_equal(g.process(x), o.process(x))
+        g.tick(ticks)
+        o.tick(ticks)
+        assert g.origin() == o.origin()
+    x = (0.1 * rng.standard_normal(2000)).astype(dtype)
+    assert np.array_equal(g.process(x), o.process(x))
