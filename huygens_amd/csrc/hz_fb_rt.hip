@@ -428,7 +428,8 @@ int hz_fb_sample(hz_fb* h, double x, int dist_id, double param, double* y) {
     hz_fb::Rt& T = h->rt;
     const int O = h->order;
     const long ticks = O > 0 ? T.pending_ticks % (O + 1) : 0;
-    if (!T.computed && ticks > 0 && !T.spare_known && !(T.active ? false : h->spare_ok)) {
+    const bool spare_known = T.active ? T.spare_known : h->spare_ok;   // the ring row a bare tick exposes
+    if (!T.computed && ticks > 0 && !spare_known) {
         hz::set_error("hz_fb_sample: tick() without operator() after a block call or set_state: the ring row "
                       "it would reuse (O+1 samples back) is not kept");
         return HZ_E_STATE;

@@ -165,6 +165,21 @@ void orc_fb_tick(orc_fb* fb)
     fb->computed = 0;
 }
 
+/* the state in libhuygens_hip's hz_fb_get_state layout, between tick() and the next sample:
+ * [x history: x[t-1-k], k < O] [y history: band n's y[t-1-k] at n*O + k] [pre, gain per band] --
+ * ring rows origin+1+k of the duplicated rings (filterbank.h:51-52, 175-184) */
+void orc_fb_get_state(const orc_fb* fb, double* buf)
+{
+    const int O = fb->order, N = fb->N, o = fb->origin;
+    for (int k = 0; k < O; k++) buf[k] = fb->xr[o + 1 + k];
+    for (int n = 0; n < N; n++)
+        for (int k = 0; k < O; k++) buf[O + (size_t)n * O + k] = fb->Y[(size_t)(o + 1 + k) * N + n];
+    for (int n = 0; n < N; n++) {
+        buf[O + (size_t)N * O + 2 * (size_t)n] = fb->pout[n];
+        buf[O + (size_t)N * O + 2 * (size_t)n + 1] = fb->gout[n];
+    }
+}
+
 /* the demo block loop (tests/resynthesis.cpp:35-39) */
 void orc_fb_process(orc_fb* fb, const double* in, double* out, long n, int dist_id, double dist_param)
 {

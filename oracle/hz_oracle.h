@@ -41,6 +41,7 @@ void    orc_fb_mix_all(orc_fb* fb, const double* v, int count);
 void    orc_fb_open(orc_fb* fb);
 double  orc_fb_sample(orc_fb* fb, double x, int dist_id, double dist_param);
 void    orc_fb_tick(orc_fb* fb);
+void orc_fb_get_state(const orc_fb* fb, double* buf);
 void    orc_fb_process(orc_fb* fb, const double* in, double* out, long n, int dist_id, double dist_param);
 /* per-sample coefficient streams (kind 0: [n][2O+1][N] coefficients; kind 1: [n][N] resonant
  * frequencies, order 2, R = param); see hz_oracle.c */

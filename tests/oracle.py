@@ -31,6 +31,7 @@ _SIGS = {
     "orc_fb_sample": (D, [VP, D, I, D]),
     "orc_fb_tick": (None, [VP]),
     "orc_fb_process": (None, [VP, PD, PD, L, I, D]),
+    "orc_fb_get_state": (None, [VP, PD]),
     "orc_fb_process_tv": (None, [VP, PD, PD, L, I, PD, D, I, D]),
     "orc_resonant": (D, [D, D]),
     "orc_fb_resonant_coefficients": (None, [D, D, PD, PD]),
@@ -106,6 +107,12 @@ class OracleFilterbank:
         out = np.empty_like(xi)
         self.l.orc_fb_process(self.h, _p(xi), _p(out), len(xi), self.dist[0], self.dist[1])
         return out
+
+    def get_state(self):
+        """[x history (O)] [y history (N O)] [pre, gain (2 N)] -- hz_fb_get_state's layout"""
+        buf = np.zeros(self.order + self.N * self.order + 2 * self.N)
+        self.l.orc_fb_get_state(self.h, _p(buf))
+        return buf
 
     def __call__(self, sample):
         """operator()(T) (filterbank.h:125-131), cached until tick()."""

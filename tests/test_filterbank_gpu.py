@@ -267,8 +267,13 @@ def test_tick_without_operator(gpu_lib, order):
             o.tick()
     err = rel_err(np.array(outs_g), np.array(outs_o))
     assert err < TOL, err
-    # after a block call the spare ring row is not kept
+    # after a block call the spare ring row is not kept: the recorded tick fails at the next
+    # sample (or block call) -- and at once through the direct ABI entry hz_fb_tick
     g.process(white_noise_f32(64, seed=5))
+    g.tick()
     with pytest.raises(HZError) as ei:
-        g.tick()
+        g(0.5)
     assert ei.value.code == HZ_E_STATE
+    g2 = Filterbank(order, N, 0.1, 1.0)
+    g2.process(white_noise_f32(64, seed=5))
+    assert g2._lib.hz_fb_tick(g2._h) == HZ_E_STATE

@@ -259,10 +259,15 @@ def test_time_range_shards(gpu_lib):
     K_all = max(s.response_info()[0] for s in shards)
     full = sum(s.response(K_all) for s in shards)
     for r, s in enumerate(shards):
-        assert set_time_shards(s, r, 3, lambda h, full=full: full, lambda k, K_all=K_all: K_all)
+        # (set_time_shards' second all-reduce is the failure flag: 0 on every rank here)
+        assert set_time_shards(s, r, 3, lambda h, full=full: full, lambda k, K_all=K_all: K_all if k > 1 else k)
         assert s.response_info()[0] == K_all
     rng = np.random.default_rng(11)
     for n in [1500, 60000, 40000, 17000, 100003]:
+        # the collective arming of shard.arm_when_ready, by hand: stationary on every shard or none
+        ready = all(s.stationary_ready(n) for s in shards)
+        for s in shards:
+            s.arm_time_shard(ready)
         x = rng.uniform(-1, 1, n)
         ref = o.process(x)
         outs = [s.process(x) for s in shards]

@@ -25,7 +25,8 @@ def pair(order, N, kp=0.1, kg=1.0, R=0.999, centre=0.5, seed=0):
         rng = np.random.default_rng(seed)
         fwd = rng.uniform(-1, 1, (N, order + 1))
         # stable all-pole parts: poles inside 0.9 of the unit circle (real roots)
-        back = np.array([np.poly(rng.uniform(-0.9, 0.9, order))[1:] for _ in range(N)]).reshape(N, order)
+        back = (np.array([np.poly(rng.uniform(-0.9, 0.9, order))[1:] for _ in range(N)]).reshape(N, order)
+                if order else np.zeros((N, 0)))
     g = Filterbank(order, N, kp, kg)
     o = OracleFilterbank(order, N, kp, kg)
     for fb in (g, o):
