@@ -13,6 +13,7 @@
 namespace hz_fbi {
 
 constexpr int kMaxOrder = 4;
+constexpr int kLtiGeomChunk128 = 3;   // hz_fb_lti.hip kLtiGeoms: chunk 128 (8192-sample tiles)
 
 // MODE_MIX: full pass (mixdown) over one time segment (blockIdx.y) of one band group
 //   (blockIdx.x).
@@ -162,19 +163,17 @@ struct hz_fb {
         size_t hpart_cap = 0;
         double* d_coef = nullptr;        // F [N][O+1], B [N][O]
         size_t coef_cap = 0;
-        double* d_H = nullptr;           // [Q][F] complex partition spectra
+        double* d_H = nullptr;           // [Qp][2048] complex partition spectra, then [Qp] bin 2048
         size_t H_cap = 0;
-        double* d_Z = nullptr;           // [windows][F] complex window spectra
+        double* d_Z = nullptr;           // [rows][2048] complex window spectra, then [rows] bin 2048
         size_t Z_cap = 0;
-        double* d_Y = nullptr;           // [D][F] complex output spectra
+        double* d_Y = nullptr;           // [B][2048] complex output spectra
         size_t Y_cap = 0;
-        double* d_tw = nullptr;          // complex twiddles of the F-point transform
-        double* d_eg = nullptr;          // end-state GEMM operands (pin E, chunk 128)
-        size_t eg_cap = 0;
-        double* d_epart = nullptr;       // end-state GEMM block sums
-        size_t epart_cap = 0;
-        hipStream_t side = nullptr;      // the end-state GEMM runs beside the convolution
-        hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+        double* d_tw = nullptr;          // W_4096^k, k < 2048 (complex)
+        double* d_spart = nullptr;       // band-state pass: segment partials, arrival counters
+        size_t spart_cap = 0;
+        unsigned* d_scount = nullptr;
+        size_t scount_cap = 0;
         double* d_zero = nullptr;        // N O zeros (x history / start of the zero-start pass)
         size_t zero_cap = 0;
     } resp;
@@ -222,20 +221,10 @@ int fb_launch_lti(hz_fb* h, int geom, const double* d_in, double* d_out, long n)
 long fb_horizon(const hz_fb* h, int log2_bound);   // samples K with ||M^K|| < 2^log2_bound for every band (-1: > 2^18)
 // zero-start band states at the end of x[0, len) (len a multiple of 4096; the O samples before
 // x read as xzero) -> out[band][O]; zeros: N O zeros (the carry's start)
-int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xzero, const double* zeros,
-                          double* out);
-int fb_lti_zero_start_end_on(hz_fb* h, const double* x, long len, const double* xzero, const double* zeros,
-                             double* out, hipStream_t st);
+// zero-start band states after the window x[0, len) (len a multiple of 8192) -> out[band][O], on
+// stream st: the stationary engine's band-state pass (hz_fb_state.hip)
+int fb_state_window(hz_fb* h, const double* x, long len, double* out, hipStream_t st);
 int fb_lti_prepare_end(hz_fb* h, long len);   // its records for the current coefficients
-// end-state GEMM (chunk-128 records): operands Eg [fb_end_rows][fb_end_cols] (pin folded in),
-// then the zero-start states after the last K samples of [hist | x] (a call of n samples; n = 0:
-// hist itself) -> out[band][O], on stream st (part: [K / 8192][fb_end_cols] scratch)
-int fb_end_rows(int O);
-int fb_end_cols(int N, int O);
-int fb_end_operands(hz_fb* h, double* Eg);
-int fb_end_state_gemm(hz_fb* h, const double* hist, const double* x, long n, long K, const double* Eg, double* part,
-                      double* out, hipStream_t st);
-size_t fb_end_scratch(int N, int O, long K);
 // hz_fb_resp.hip (stationary engine)
 void fb_resp_init(hz_fb* h);
 void fb_resp_invalidate(hz_fb* h, bool coefficients);   // targets / coefficients changed

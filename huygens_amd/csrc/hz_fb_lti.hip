@@ -30,29 +30,12 @@
 #include <cstdlib>
 
 #include "hz_fb_impl.h"
+#include "hz_fb_rec.h"
 
 
 namespace {
 
 using namespace hz_fbi;
-
-// LTI band record (doubles), built on the host in long double.
-template <int O, int L>
-struct RecL {
-    static constexpr int XW = L + O;            // chunk input window x[tc-O .. tc+L-1]
-    // scalar block, read by the mix kernel every tile (kept small and contiguous so the
-    // 16 bands of a CU stay resident in the scalar cache):
-    static constexpr int E0 = 0;                // E[0][m], m < XW (E[k][i] = E[0][i+k], i >= O)
-    static constexpr int EH = E0 + XW;          // E[k][i], k, i < O (history taps)
-    static constexpr int PS = EH + O * O;       // M^1, M^2, M^4, M^8, M^64
-    static constexpr int SC_END = PS + 5 * O * O;
-    static constexpr int K = SC_END;            // K[j][k]  j<L, k<O  : homogeneous response
-    static constexpr int QC = K + L * O;        // QC[e] = M^e, e <= 64 (M: chunk transition)
-    static constexpr int H = QC + 65 * O * O;   // H[d], d<XW : FIR*IIR impulse response
-    static constexpr int GE = H + XW;           // GE[i][j], i<O, j<L : F[j][i] (history taps)
-    static constexpr int RAW = GE + O * L;
-    static constexpr int SIZE = (RAW + 7) & ~7;
-};
 
 static int lti_rec_size(int O, int L) {
 #define HZ_LTI_RS(LL)                                                           \
@@ -199,7 +182,6 @@ struct LtiArgs {
     int seg_stride;         // segstate index of segment s: s * seg_stride
     int nbands;
     double sp_n, sg_n;      // sp^n, sg^n (closed-form smoother end state)
-    long long* dbg;         // diagnostics (ABL bit 4): per-wave phase timestamps of one workgroup
 };
 
 // LDS: x tile x[t0-O .. t0+64L-1] stored at pos(li) = li + P (li / L), P pad slots per chunk
@@ -293,11 +275,7 @@ constexpr int kDppRowBcast31 = 0x143; // rows 2, 3 <- lane 31 (row_mask 0xc)
 //  (M) the group's correction mix D[chunk][j] = sum_bs gs[bs][chunk] K[bs][j] on the
 //      matrix cores, stored as this group's row of the partial slab.
 // The (E) and (M) blocks are spread over the waves as independent work items.
-// ABL (diagnostics, HZ_FB_LTI_ABL): bit 0 skips the (E) MFMA chains, bit 1 the (S) scan steps,
-// bit 2 the GS stores, bit 3 the x tile loads; bit 4 records s_memtime stamps per wave and
-// iteration for workgroup 100 (loop top, after E, after S, after the x store) --
-// wrong results, timed by rocprof to split the state kernel's time (scripts/abl_state.sh)
-template <int O, int L, int MODE, int ABL = 0>
+template <int O, int L, int MODE>
 __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double* __restrict__ rec, LtiArgs a) {
     using R = RecL<O, L>;
     constexpr int W = lti_waves(O);
@@ -458,11 +436,6 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                                                  0x00020000);
     }();
     auto load_x = [&](long t0x, double (&pf)[PF]) {
-        if constexpr ((ABL & 8) != 0) {
-#pragma unroll
-            for (int q = 0; q < PF; ++q) pf[q] = (double)q;
-            return;
-        }
         const int v0 = (int)((t0x - O) * (long)sizeof(double)) + (int)threadIdx.x * (int)sizeof(double);
 #pragma unroll
         for (int q = 0; q < PF; ++q)
@@ -475,11 +448,6 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     const int sid = kSplit ? (int)threadIdx.x - 64 * NE : (int)threadIdx.x;
     const int vq0 = sid * (int)sizeof(double);
     auto load_x_loop = [&](long t0x, double (&pf)[PF2]) {
-        if constexpr ((ABL & 8) != 0) {
-#pragma unroll
-            for (int q = 0; q < PF2; ++q) pf[q] = (double)q;
-            return;
-        }
         const unsigned long long xb = (unsigned long long)(a.x + (t0x - O));
         const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)xb);
         const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(xb >> 32));
@@ -572,7 +540,6 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
 
     // (E) for tile te: this wave's E blocks -> z buffer (te & 1)
     auto phase_e = [&](int te) {
-        if constexpr ((ABL & 1) != 0) return;
         const double* xs = lds + (X1 ? 0 : (te & 1) * XSP);
         double* z = zb + (te & 1) * BSP * kZRow;
 #pragma unroll
@@ -691,14 +658,6 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
     double st[O];
     double* go_run = MODE == MODE_STATE ? a.gs_out + ((seg_t0 / T) * a.bs_pad + (long)band * O) * 64 + lane : nullptr;
     const int niter = (MODE == MODE_MIX) ? ntiles + 1 : ntiles;
-    auto stamp = [&](int it, int slot) {
-        if constexpr ((ABL & 16) != 0) {
-            __builtin_amdgcn_sched_barrier(0);
-            const long long tt = __builtin_amdgcn_s_memtime();
-            if (blockIdx.x == 100 && lane == 0 && it < 64) a.dbg[((long)wave * 64 + it) * 4 + slot] = tt;
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
     auto phase_s = [&](int it, long t0) {
         if constexpr (MODE == MODE_SEGEND) {
             if (it < ntiles) {   // S' = M^64 S + sum_l M^(63-l) pin z_l
@@ -752,14 +711,12 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
             const double* p2 = r + R::PS + O * O;
             const double* p4 = r + R::PS + 2 * O * O;
             const double* p8 = r + R::PS + 3 * O * O;
-            if constexpr ((ABL & 2) == 0) {
             HZ_LTI_SCAN_STEP(kDppRowShr + 1, 0xf, p1)
             HZ_LTI_SCAN_STEP(kDppRowShr + 2, 0xf, p2)
             HZ_LTI_SCAN_STEP(kDppRowShr + 4, 0xf, p4)
             HZ_LTI_SCAN_STEP(kDppRowShr + 8, 0xf, p8)
             HZ_LTI_SCAN_STEP(kDppRowBcast15, 0xa, qa)
             HZ_LTI_SCAN_STEP(kDppRowBcast31, 0xc, qb)
-            }
 #undef HZ_LTI_SCAN_STEP
             double Sn[O];
 #pragma unroll
@@ -787,8 +744,8 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                     go_run += (long)a.bs_pad * 64;
 #pragma unroll
                     for (int k = 0; k < O; ++k)
-                        if constexpr ((ABL & 4) == 0)   // unconditional: the x staging waits below
-                            __builtin_nontemporal_store(gb * st[k], go + 64 * k);   // count them exactly
+                        // unconditional: the x staging waits below count them exactly
+                        __builtin_nontemporal_store(gb * st[k], go + 64 * k);   // count them exactly
                 }
                 if (last_seg && it == ntiles - 1 && live) {
                     // end-of-call y history = the start state of the chunk beginning at n
@@ -814,7 +771,6 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
         const bool isE = !kSplit || wave < NE;
         for (int it = 0; it < ntiles; ++it) {
             const long t0 = seg_t0 + (long)it * T;
-            stamp(it, 0);
             // (every wave scanning first, then the E chains: 0.465 vs 0.454 ms per C2 step)
             if (isE) {
                 if (it + 1 < ntiles) phase_e(it + 1);
@@ -822,18 +778,14 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                 phase_s(it, t0);
             }
             if (!kSplit || !isE) write_xrows(it + 1);   // the buffer holds tile it + 1 until the barrier
-            stamp(it, 1);
             __syncthreads();
             if (isE) phase_s(it, t0);
-            stamp(it, 2);
             if (stager && it + 2 < ntiles) dma_x(lds, t0 + 2 * T);
-            stamp(it, 3);
             __syncthreads();
         }
     } else {
         for (int it = 0; it < niter; ++it) {
             const long t0 = seg_t0 + (long)it * T;
-            stamp(it, 0);
             const bool stage = it + 2 < ntiles;
             if constexpr (kSplit) {
                 if (stager) {
@@ -848,16 +800,13 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
             // step) and for the mix-only waves (0.581); scan-first on the state kernel: 0.308 vs
             // 0.304 ms
             if (it + 1 < ntiles) phase_e(it + 1);
-            stamp(it, 1);
             if constexpr (MODE == MODE_MIX) {
                 if (it >= 1) phase_m(it - 1);
             }
             phase_s(it, t0);
-            stamp(it, 2);
             if constexpr (!kSplit) {
                 if (stage) store_x_loop(lds + (it & 1) * XSP, pf);
             }
-            stamp(it, 3);
             __syncthreads();
         }
     }
@@ -1126,162 +1075,6 @@ __global__ __launch_bounds__(256) void fb_lti_reduce_short_kernel(const double* 
     if (t + 1 < n) out[t + 1] = acc[1];
 }
 
-// ---- end-state GEMM (stationary engine, hz_fb_resp.hip) ---------------------------------
-// Zero-start band states at the end of a K-sample window v (K a multiple of 64 chunks of 128):
-//   S = sum_c M^(C-1-c) z_c,  z_c = pin E x_c  (chunk c's zero-state end state, as the state kernel)
-// as one chip-wide GEMM Z[chunk][band state] = X[chunk][tap] Eg[tap][band state] on the FP64
-// matrix cores -- workgroup = 16 bands x 64 chunks, E block in LDS, chunk windows read from L2 --
-// reduced in the workgroup with the chunk powers M^(63-c) (records' QC), then a per-band Horner
-// over the 64-chunk blocks with M^64.  Unlike the state kernel it keeps no prefix scan and no
-// sequential tile loop per band group, so it fills the chip for a short window and leaves most of
-// the LDS free (it runs beside the FFT kernels of the same call).
-constexpr int kEndL = 128;
-
-// Eg[t][bs] = pin_n E_n[k][t] (bs = n O + k), t < 4 ceil((L+O)/4), zero outside the bank
-template <int O>
-__global__ __launch_bounds__(256) void fb_end_eops_kernel(const double* __restrict__ rec, const double* __restrict__ pin,
-                                                          int nbands, int bs_tot, double* __restrict__ Eg) {
-    using R = RecL<O, kEndL>;
-    constexpr int XW = R::XW, KE4 = (XW + 3) / 4 * 4;
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (long)KE4 * bs_tot) return;
-    const int t = (int)(i / bs_tot), bs = (int)(i % bs_tot), n = bs / O, k = bs % O;
-    double v = 0.0;
-    if (n < nbands && t < XW) {
-        const double* rb = rec + (long)n * R::SIZE;
-        v = pin[n] * (t < O ? rb[R::EH + k * O + t] : (t + k < XW ? rb[R::E0 + t + k] : 0.0));
-    }
-    Eg[i] = v;
-}
-
-// v(i) = last K samples of [hist | x] after a call of n samples: hist[n + i] or x[n + i - K]
-__device__ __forceinline__ double end_v(const double* hist, const double* x, long n, long K, long i) {
-    const long m = n + i;
-    return m < K ? hist[m] : x[m - K];
-}
-
-// chunk windows transposed, Xt[t][c] = v(c L - O + t) (0 before the window): the GEMM's A loads
-// then read 16 consecutive chunks of one tap (128 B) instead of 16 chunks 1 KiB apart
-template <int O>
-__global__ __launch_bounds__(256) void fb_end_xt_kernel(const double* __restrict__ hist, const double* __restrict__ x,
-                                                        long n, long K, int C, double* __restrict__ Xt) {
-    constexpr int XW = kEndL + O, KE4 = (XW + 3) / 4 * 4;
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (long)KE4 * C) return;
-    const int t = (int)(i / C), c = (int)(i % C);
-    const long xi = (long)c * kEndL - O + t;
-    Xt[i] = (t < XW && xi >= 0) ? end_v(hist, x, n, K, xi) : 0.0;
-}
-
-// workgroup = BANDS bands (BS = BANDS O band states, BS / 16 column blocks) x 64 chunks (4 waves x
-// 16); the E block lives in LDS and is reused for the z tile after the MFMAs
-template <int O>
-constexpr int end_bands() { return O <= 2 ? 32 : 16; }
-
-template <int O>
-__global__ __launch_bounds__(256) void fb_end_gemm_kernel(const double* __restrict__ rec,
-                                                          const double* __restrict__ Xt, int C,
-                                                          const double* __restrict__ Eg, int bs_tot, int nbands,
-                                                          double* __restrict__ part) {
-    using R = RecL<O, kEndL>;
-    constexpr int XW = R::XW, KE = (XW + 3) / 4, BANDS = end_bands<O>(), BS = BANDS * O, NB = BS / 16;
-    extern __shared__ double end_lds[];   // E block [4 KE][BS + 1], then the z tile [64][BS + 1]
-    double (*eb)[BS + 1] = (double (*)[BS + 1])end_lds;
-    double (*zt)[BS + 1] = (double (*)[BS + 1])end_lds;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int g = blockIdx.x;
-    const int c0 = blockIdx.y * 64;
-    const int bs0 = g * BS;
-    // A operands (Xt rows, 16 consecutive chunks per tap) and the E block: every load of the
-    // thread issued before its first use
-    double av[KE];
-#pragma unroll
-    for (int q = 0; q < KE; ++q) av[q] = Xt[(long)(4 * q + (lane >> 4)) * C + c0 + 16 * wave + (lane & 15)];
-    constexpr int NEB = 4 * KE * BS, PT = (NEB + 255) / 256;
-    double ev[PT];
-#pragma unroll
-    for (int i = 0; i < PT; ++i) {
-        const int e = threadIdx.x + 256 * i;
-        ev[i] = e < NEB ? Eg[(long)(e / BS) * bs_tot + bs0 + e % BS] : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < PT; ++i) {
-        const int e = threadIdx.x + 256 * i;
-        if (e < NEB) eb[e / BS][e % BS] = ev[i];
-    }
-    __syncthreads();
-    hz_f64x4 acc[NB];
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[nb] = hz_f64x4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < KE; ++q)
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-            acc[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], eb[4 * q + (lane >> 4)][16 * nb + (lane & 15)],
-                                                           acc[nb], 0, 0, 0);
-    __syncthreads();   // the z tile overwrites the E block
-    // D: row = chunk 16 wave + (l >> 4) + 4 rr, col = band state 16 nb + (l & 15)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) zt[16 * wave + (lane >> 4) + 4 * rr][16 * nb + (lane & 15)] = acc[nb][rr];
-    __syncthreads();
-    // S_blk = sum_c M^(63 - c) z_c: thread (band b, sub) over chunks sub + SUBS i, then the subs
-    constexpr int SUBS = 256 / BANDS;   // 8 or 16
-    const int b = threadIdx.x / SUBS, sub = threadIdx.x % SUBS;
-    const int band = g * BANDS + b;
-    double S[O];
-#pragma unroll
-    for (int r = 0; r < O; ++r) S[r] = 0.0;
-    if (band < nbands) {
-        const double* rb = rec + (long)band * R::SIZE;
-#pragma unroll
-        for (int i = 0; i < 64 / SUBS; ++i) {
-            const int c = sub + SUBS * i;
-            const double* Qe = rb + R::QC + (63 - c) * O * O;
-#pragma unroll
-            for (int r = 0; r < O; ++r)
-#pragma unroll
-                for (int k = 0; k < O; ++k) S[r] = fma(Qe[r * O + k], zt[c][b * O + k], S[r]);
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < O; ++r)
-#pragma unroll
-        for (int off = SUBS / 2; off >= 1; off >>= 1) S[r] += __shfl_xor(S[r], off, SUBS);
-    if (sub == 0 && band < nbands)
-#pragma unroll
-        for (int r = 0; r < O; ++r) part[(long)blockIdx.y * bs_tot + (long)band * O + r] = S[r];
-}
-
-// S = sum over blocks in order of M^64 S + S_blk -> out[band][O]
-template <int O>
-__global__ __launch_bounds__(256) void fb_end_combine_kernel(const double* __restrict__ rec,
-                                                             const double* __restrict__ part, int nblk, int bs_tot,
-                                                             int nbands, double* __restrict__ out) {
-    using R = RecL<O, kEndL>;
-    const int band = blockIdx.x * blockDim.x + threadIdx.x;
-    if (band >= nbands) return;
-    const double* M = rec + (long)band * R::SIZE + R::QC + 64 * O * O;
-    double S[O];
-#pragma unroll
-    for (int r = 0; r < O; ++r) S[r] = 0.0;
-    for (int blk = 0; blk < nblk; ++blk) {
-        double T[O];
-#pragma unroll
-        for (int r = 0; r < O; ++r) {
-            double acc = part[(long)blk * bs_tot + (long)band * O + r];
-#pragma unroll
-            for (int k = 0; k < O; ++k) acc = fma(M[r * O + k], S[k], acc);
-            T[r] = acc;
-        }
-#pragma unroll
-        for (int r = 0; r < O; ++r) S[r] = T[r];
-    }
-#pragma unroll
-    for (int r = 0; r < O; ++r) out[(long)band * O + r] = S[r];
-}
-
 // ---- kernel selection -------------------------------------------
 typedef void (*CarryKernel)(const double*, const double*, double*, int, int, long);
 typedef void (*LtiKernel)(const double*, LtiArgs);
@@ -1294,37 +1087,19 @@ struct LtiGeom {
     int L, nb, waves;
 };
 static const LtiGeom kLtiGeoms[] = {{16, 1, 16}, {32, 1, 16}, {64, 1, 16}, {128, 1, 16}};  // waves: lti_waves(O)
+static_assert(kLtiGeomChunk128 == 3, "kLtiGeoms[3] is chunk 128");
 constexpr int kNumLtiGeoms = 4;
 static_assert(kNumLtiGeoms <= hz_fb::kLtiSets, "one record set per geometry");
 
 template <int O, int L>
 LtiKernel lti_kernel_mode(int mode) {
     static_assert(lti_lds_bytes<O, L>(true) <= 160 * 1024, "LTI kernel LDS over 160 KiB");
-    if constexpr (lti_x1<L>()) {   // chunk 128: state and prepass modes only
-        if constexpr (O == 2) {   // diagnostics (HZ_FB_LTI_ABL: 1 no E, 2 no scan, 3 neither, 16 stamps)
-            static const int abl = std::getenv("HZ_FB_LTI_ABL") ? std::atoi(std::getenv("HZ_FB_LTI_ABL")) : 0;
-            if (mode == MODE_STATE && abl == 1) return fb_lti_kernel<O, L, MODE_STATE, 1>;
-            if (mode == MODE_STATE && abl == 2) return fb_lti_kernel<O, L, MODE_STATE, 2>;
-            if (mode == MODE_STATE && abl == 3) return fb_lti_kernel<O, L, MODE_STATE, 3>;
-            if (mode == MODE_STATE && abl == 16) return fb_lti_kernel<O, L, MODE_STATE, 16>;
-        }
+    if constexpr (lti_x1<L>())   // chunk 128: state and prepass modes only
         return mode == MODE_SEGEND ? fb_lti_kernel<O, L, MODE_SEGEND> : fb_lti_kernel<O, L, MODE_STATE>;
-    } else {
-    if constexpr (O == 2 && L == 64) {   // diagnostics: ablated state kernels (HZ_FB_LTI_ABL=1..3)
-        static const int abl = std::getenv("HZ_FB_LTI_ABL") ? std::atoi(std::getenv("HZ_FB_LTI_ABL")) : 0;
-        if (mode == MODE_STATE && abl == 1) return fb_lti_kernel<O, L, MODE_STATE, 1>;
-        if (mode == MODE_STATE && abl == 2) return fb_lti_kernel<O, L, MODE_STATE, 2>;
-        if (mode == MODE_STATE && abl == 3) return fb_lti_kernel<O, L, MODE_STATE, 3>;
-        if (mode == MODE_STATE && abl == 7) return fb_lti_kernel<O, L, MODE_STATE, 7>;
-        if (mode == MODE_STATE && abl == 11) return fb_lti_kernel<O, L, MODE_STATE, 11>;
-        if (mode == MODE_STATE && abl == 15) return fb_lti_kernel<O, L, MODE_STATE, 15>;
-        if (mode == MODE_STATE && abl == 4) return fb_lti_kernel<O, L, MODE_STATE, 4>;
-        if (mode == MODE_STATE && abl == 16) return fb_lti_kernel<O, L, MODE_STATE, 16>;
-    }
-    return mode == MODE_SEGEND ? fb_lti_kernel<O, L, MODE_SEGEND>
-         : mode == MODE_STATE  ? fb_lti_kernel<O, L, MODE_STATE>
-                               : fb_lti_kernel<O, L, MODE_MIX>;
-    }
+    else
+        return mode == MODE_SEGEND ? fb_lti_kernel<O, L, MODE_SEGEND>
+             : mode == MODE_STATE  ? fb_lti_kernel<O, L, MODE_STATE>
+                                   : fb_lti_kernel<O, L, MODE_MIX>;
 }
 
 template <int O>
@@ -1393,12 +1168,6 @@ namespace hz_fbi {
 // tiles) for the short streaming blocks
 int fb_lti_geom(const hz_fb* h, long n) {
     if (h->lti_geom >= 0) return h->lti_geom;
-    static const int env_geom = [] {   // tuning experiments: HZ_FB_LTI_L = 16 / 32 / 64 for long calls
-        const char* e = std::getenv("HZ_FB_LTI_L");
-        const int v = e ? std::atoi(e) : 0;
-        return v == 16 ? 0 : v == 64 ? 2 : v == 32 ? 1 : v == 128 ? 3 : -1;
-    }();
-    if (env_geom >= 0 && n >= 2 * 64L * kLtiGeoms[env_geom].L) return env_geom;
     // chunk 128 from four of its 8192-sample tiles, for banks that fill the chip with at most two
     // time segments (C2: 256 groups; its 2-GPU shard 0.294 -> 0.279 ms); smaller shards keep
     // chunk 64 (finer tiles for the prepass and the GEMM: 4-GPU shard equal, 8-GPU 0.141 vs 0.164)
@@ -1411,16 +1180,9 @@ int fb_lti_geom(const hz_fb* h, long n) {
 
 int fb_lti_chunk(int geom) { return kLtiGeoms[geom].L; }
 
-// chunk 64 runs the bank-wide correction as a GEMM over all band states (MODE_STATE +
-// fb_lti_gemm_kernel) instead of per-group mixes and the G-row slab; HZ_FB_LTI_GEMM=0 restores
-// the slab path (A/B measurements)
-bool fb_lti_gemm_geom(int geom) {
-    static const bool off = [] {
-        const char* e = std::getenv("HZ_FB_LTI_GEMM");
-        return e && e[0] == '0';
-    }();
-    return kLtiGeoms[geom].L >= 64 && !off;
-}
+// chunk 64 and 128 run the bank-wide correction as a GEMM over all band states (MODE_STATE +
+// the correction GEMM, hz_fb_gemm.hip) instead of per-group mixes and the G-row slab
+bool fb_lti_gemm_geom(int geom) { return kLtiGeoms[geom].L >= 64; }
 
 // every band's smoothers at their targets (host mirror), relative to the bank's
 // largest target: the LTI engine then computes the same outputs to ~2^-60
@@ -1565,16 +1327,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
     // a second stream under the next chunk's mix kernel (FP64-bound).  Measured on MI355X
     // (C2, 480k samples): split 1 0.859 ms, 2 0.868, 3 0.857, 4 0.873 -- the reduce then
     // competes with the mix kernel for CU slots, so the default is 1.
-    static const int slab_log2 = [] {
-        const char* e = std::getenv("HZ_FB_SLAB_LOG2");  // tuning experiments
-        const int v = e ? std::atoi(e) : 27;
-        return v >= 16 && v <= 30 ? v : 27;
-    }();
-    static const int nsplit = [] {
-        const char* e = std::getenv("HZ_FB_LTI_SPLIT");  // tuning experiments
-        const int v = e ? std::atoi(e) : 1;
-        return v >= 1 && v <= 64 ? v : 1;
-    }();
+    constexpr int slab_log2 = 27, nsplit = 1;
     const long ntiles_all = (n + T - 1) / T;
     // correction GEMM path: per chunk GS [bs_pad][chunks] + part [S][n_pad] instead of two slabs
     const bool gemm = fb_lti_gemm_geom(gi) && O > 0;
@@ -1689,7 +1442,6 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         double* slab_k = h->d_partial + (size_t)(k & 1) * slab;
         const long nc_pad = ntiles * 64;   // chunks of the launch (GEMM path)
         LtiArgs a;
-        a.dbg = nullptr;
         a.pin = h->d_pin;
         a.gin = h->d_gin;
         a.ystate = h->d_ystate[h->scur];
@@ -1738,19 +1490,6 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         }
         if (e && nseg > 1) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
         else if (e) h->ev_skip[(e - h->ev.data()) / 5] |= 2;
-        static const bool diag_state = std::getenv("HZ_FB_LTI_DIAG_STATE") != nullptr;
-        if (diag_state && nseg == 1 && !gemm) {   // (diagnostics) the E + scan work alone, timed by rocprof
-            LtiArgs ad = a;
-            hipLaunchKernelGGL(kend, dim3(G, 1), dim3(64 * lti_waves(O)), lds_end, h->stream, (const double*)set.d_rec,
-                               ad);
-        }
-        static const bool stamps = std::getenv("HZ_FB_LTI_ABL") && std::atoi(std::getenv("HZ_FB_LTI_ABL")) == 16;
-        static long long* d_dbg = nullptr;
-        if (stamps && gemm && G > 100) {   // (diagnostics) phase timestamps, printed to stderr
-            if (!d_dbg) HZ_TRY_HIP(hipMalloc(&d_dbg, sizeof(long long) * 16 * 64 * 4));
-            HZ_TRY_HIP(hipMemsetAsync(d_dbg, 0, sizeof(long long) * 16 * 64 * 4, h->stream));
-            a.dbg = d_dbg;
-        }
         if (gemm && bs_pad > lti_group_rows(h->N, O)) {   // GS rows no group writes: zero
             const int gr = lti_group_rows(h->N, O);
             HZ_TRY_HIP(hipMemset2DAsync(h->d_partial + (size_t)gr * 64, sizeof(double) * bs_tot * 64, 0,
@@ -1766,29 +1505,6 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
         hipLaunchKernelGGL(kmix, dim3(G, (unsigned)nseg), dim3(64 * lti_waves(O)), lds, h->stream,
                            (const double*)set.d_rec, a);
         HZ_TRY_HIP(hipGetLastError());
-        if (stamps && a.dbg) {
-            std::vector<long long> hd(16 * 64 * 4);
-            HZ_TRY_HIP(hipMemcpyAsync(hd.data(), d_dbg, sizeof(long long) * hd.size(), hipMemcpyDeviceToHost, h->stream));
-            HZ_TRY_HIP(hipStreamSynchronize(h->stream));
-            for (int w = 0; w < 16; ++w) {
-                double ph[4] = {0, 0, 0, 0};
-                int cnt = 0;
-                for (int it = 8; it < 56; ++it) {
-                    const long long* q = &hd[((size_t)w * 64 + it) * 4];
-                    const long long nx = hd[((size_t)w * 64 + it + 1) * 4];
-                    if (!q[0] || !nx) continue;
-                    ph[0] += q[1] - q[0];
-                    ph[1] += q[2] - q[1];
-                    ph[2] += q[3] - q[2];
-                    ph[3] += nx - q[3];
-                    ++cnt;
-                }
-                if (cnt)
-                    std::fprintf(stderr, "stamps wave %2d: ph1 %7.0f  ph2 %7.0f  xstore %7.0f  barrier %7.0f  (cycles, %d its)\n",
-                                 w, ph[0] / cnt, ph[1] / cnt, ph[2] / cnt, ph[3] / cnt, cnt);
-            }
-            a.dbg = nullptr;
-        }
         if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
         if (gemm) {
             // correction GEMM over band-state slices (>= 4 workgroups per CU), then the slice sum
@@ -1838,140 +1554,7 @@ int fb_launch_lti(hz_fb* h, int gi, const double* d_in, double* d_out, long n) {
 
 long fb_horizon(const hz_fb* h, int log2_bound) { return fb_lti_horizon(h, ldexpl(1.0L, log2_bound)); }
 
-int fb_lti_prepare_end(hz_fb* h, long len) { return fb_prepare_lti(h, len % (64L * 128) == 0 ? 3 : 2); }
-
-// zero-start band states at the end of x[0, len) -> out[band][O] (hz_fb_resp.hip): the state
-// kernel's prepass mode, chunk 128 when len is a multiple of its 8192-sample tile (else chunk 64),
-// over m time segments when the bank alone leaves CUs idle (shards), joined by the carry kernel
-int fb_lti_zero_start_end(hz_fb* h, const double* x, long len, const double* xzero, const double* zeros,
-                          double* out) {
-    return fb_lti_zero_start_end_on(h, x, len, xzero, zeros, out, h->stream);
-}
-
-int fb_lti_zero_start_end_on(hz_fb* h, const double* x, long len, const double* xzero, const double* zeros,
-                             double* out, hipStream_t st) {
-    const int O = h->order;
-    // (A/B) HZ_FB_END_L = 32 / 64: chunk of the zero-start pass (default 128 when len allows);
-    // HZ_FB_END_M: time segments per band group (default: fill the CUs)
-    static const int env_l = std::getenv("HZ_FB_END_L") ? std::atoi(std::getenv("HZ_FB_END_L")) : 0;
-    static const int env_m = std::getenv("HZ_FB_END_M") ? std::atoi(std::getenv("HZ_FB_END_M")) : 0;
-    const int gi = env_l == 32 ? 1 : env_l == 64 ? 2 : len % (64L * 128) == 0 ? 3 : 2;
-    const long T = 64L * kLtiGeoms[gi].L;
-    if (O == 0 || len <= 0 || len % T != 0) {
-        hz::set_error("fb_lti_zero_start_end: order %d, length %ld (a positive multiple of 4096)", O, len);
-        return HZ_E_INVALID;
-    }
-    HZ_TRY(fb_prepare_lti(h, gi));
-    hz_fb::LtiRecSet& set = h->lti_set[gi];
-    const int G = (h->N + lti_waves(O) - 1) / lti_waves(O);
-    const long ntiles = len / T;
-    // equal segments only (the carry powers M by the segment length): the largest m <= the cap
-    // that divides the tile count
-    long m = std::min<long>(ntiles, std::max<long>(1, env_m > 0 ? env_m : h->target_groups / G));
-    while (ntiles % m != 0) --m;
-    const long seg_tiles = ntiles / m;
-    if (m > 1) {
-        const size_t sneed = (size_t)h->N * (m + 1) * O;
-        if (sneed > h->seg_cap) {
-            HZ_TRY_HIP(hipStreamSynchronize(h->stream));
-            HZ_TRY_HIP(hipStreamSynchronize(st));
-            if (h->d_seg) HZ_TRY_HIP(hipFree(h->d_seg));
-            h->d_seg = nullptr;
-            HZ_TRY_HIP(hipMalloc(&h->d_seg, sizeof(double) * sneed));
-            h->seg_cap = sneed;
-        }
-    }
-    LtiKernel kend = pick_lti(O, gi, MODE_SEGEND);
-    HZ_TRY(fb_set_lds_attr((const void*)kend));
-    LtiArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.pin = h->d_pin;
-    a.gin = h->d_gin;
-    a.ystate = zeros;
-    a.pgstate = h->d_pg[h->scur];
-    a.x = x;
-    a.xhist = xzero;
-    a.n = len;
-    a.n_pad = len;
-    a.seg_len = seg_tiles * T;
-    a.nseg = (int)m + 1;   // segment m - 1 is not the last: every segment stores its end state
-    a.seg_stride = 1;
-    a.seg_skip = 0;
-    a.nbands = h->N;
-    if (m == 1) {   // slot (band + 1) O of out - O = out[band]
-        a.segstate = out - O;
-        a.nseg_state = 1;
-    } else {
-        a.segstate = h->d_seg;
-        a.nseg_state = (int)m + 1;
-    }
-    hipLaunchKernelGGL(kend, dim3(G, (unsigned)m), dim3(64 * lti_waves(O)), lti_lds(O, gi, false), st,
-                       (const double*)set.d_rec, a);
-    HZ_TRY_HIP(hipGetLastError());
-    if (m > 1) {
-        hipLaunchKernelGGL(pick_lti_carry(O, kLtiGeoms[gi].L), dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0,
-                           st, (const double*)set.d_rec, zeros, h->d_seg, h->N, (int)m + 1, seg_tiles);
-        HZ_TRY_HIP(hipGetLastError());
-        HZ_TRY_HIP(hipMemcpy2DAsync(out, sizeof(double) * O, h->d_seg + (size_t)m * O, sizeof(double) * O * (m + 1),
-                                    sizeof(double) * O, (size_t)h->N, hipMemcpyDeviceToDevice, st));
-    }
-    return HZ_OK;
-}
-
-// end-state GEMM operands (chunk-128 records + pin) and the GEMM itself (hz_fb_resp.hip)
-int fb_end_rows(int O) { return (O + kEndL + 3) / 4 * 4; }
-int fb_end_cols(int N, int O) { return (N + 31) / 32 * 32 * O; }
-
-int fb_end_operands(hz_fb* h, double* Eg) {
-    const int O = h->order;
-    HZ_TRY(fb_prepare_lti(h, 3));
-    const int bs_tot = fb_end_cols(h->N, O);
-    const long cnt = (long)fb_end_rows(O) * bs_tot;
-    auto k = O == 1 ? fb_end_eops_kernel<1> : O == 2 ? fb_end_eops_kernel<2> : O == 3 ? fb_end_eops_kernel<3>
-                                                                                     : fb_end_eops_kernel<4>;
-    hipLaunchKernelGGL(k, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, h->stream,
-                       (const double*)h->lti_set[3].d_rec, (const double*)h->d_pin, h->N, bs_tot, Eg);
-    HZ_TRY_HIP(hipGetLastError());
-    return HZ_OK;
-}
-
-int fb_end_state_gemm(hz_fb* h, const double* hist, const double* x, long n, long K, const double* Eg, double* part,
-                      double* out, hipStream_t st) {
-    const int O = h->order;
-    if (O == 0 || K <= 0 || K % (64L * kEndL) != 0) {
-        hz::set_error("fb_end_state_gemm: order %d, window %ld (a positive multiple of 8192)", O, K);
-        return HZ_E_INVALID;
-    }
-    const int bs_tot = fb_end_cols(h->N, O);
-    const int nblk = (int)(K / (64L * kEndL));
-    const int C = (int)(K / kEndL);
-    const int bands = O <= 2 ? 32 : 16;
-    double* Xt = part + (size_t)nblk * bs_tot;   // [rows][C] after the block sums
-    auto kx = O == 1 ? fb_end_xt_kernel<1> : O == 2 ? fb_end_xt_kernel<2> : O == 3 ? fb_end_xt_kernel<3>
-                                                                                 : fb_end_xt_kernel<4>;
-    auto kg = O == 1 ? fb_end_gemm_kernel<1> : O == 2 ? fb_end_gemm_kernel<2> : O == 3 ? fb_end_gemm_kernel<3>
-                                                                                     : fb_end_gemm_kernel<4>;
-    auto kc = O == 1 ? fb_end_combine_kernel<1> : O == 2 ? fb_end_combine_kernel<2>
-                                                : O == 3 ? fb_end_combine_kernel<3> : fb_end_combine_kernel<4>;
-    const double* rec = h->lti_set[3].d_rec;
-    const long nxt = (long)fb_end_rows(O) * C;
-    hipLaunchKernelGGL(kx, dim3((unsigned)((nxt + 255) / 256)), dim3(256), 0, st, hist, x, n, K, C, Xt);
-    HZ_TRY_HIP(hipGetLastError());
-    const size_t lds = sizeof(double) * (size_t)fb_end_rows(O) * (bands * O + 1);
-    HZ_TRY(fb_set_lds_attr((const void*)kg));
-    hipLaunchKernelGGL(kg, dim3((unsigned)((h->N + bands - 1) / bands), (unsigned)nblk), dim3(256), lds, st, rec,
-                       (const double*)Xt, C, Eg, bs_tot, h->N, part);
-    HZ_TRY_HIP(hipGetLastError());
-    hipLaunchKernelGGL(kc, dim3((unsigned)((h->N + 255) / 256)), dim3(256), 0, st, rec, (const double*)part, nblk,
-                       bs_tot, h->N, out);
-    HZ_TRY_HIP(hipGetLastError());
-    return HZ_OK;
-}
-
-// scratch doubles of fb_end_state_gemm for a window of K samples
-size_t fb_end_scratch(int N, int O, long K) {
-    return (size_t)(K / (64L * kEndL)) * fb_end_cols(N, O) + (size_t)fb_end_rows(O) * (K / kEndL);
-}
+int fb_lti_prepare_end(hz_fb* h, long len) { return fb_prepare_lti(h, len % (64L * 128) == 0 ? kLtiGeomChunk128 : 2); }
 
 }  // namespace hz_fbi
 

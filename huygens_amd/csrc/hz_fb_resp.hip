@@ -7,20 +7,24 @@
 // (src/filterbank.h:130,178-179) is ONE linear filter of the input:
 //     out[t] = sum_n gin_n y_n[t] = sum_{tau < K} h[tau] x[t - tau],   h[tau] = sum_n gin_n r_n[tau]
 // with r_n band n's impulse response at pre = pin_n.  A call then runs as a uniformly partitioned
-// overlap-save convolution on FP64 FFTs (P = 2048-sample partitions, 4096-point transforms):
-//   resp_fwd_kernel   one 4096-point FFT per pair of input windows W_i = u[(i-1)P, (i+1)P) of
-//                     u = [last K inputs | call input]: windows i and i + D share a transform
-//                     (real + i imag; h is real, so their products with H stay separable)
+// overlap-save convolution on FP64 real transforms (P = 2048-sample partitions / output blocks,
+// F = 4096-sample windows, each a 2048-point complex FFT of its even/odd samples plus a split):
+//   resp_fwd_kernel   one workgroup per window W_j = u[jP, jP + F) of u = [last K inputs | call
+//                     input]: its 2049 bins, stored as 2048 complex (bin 0 = X_0) + X_2048 apart
 //   resp_mac_kernel   Y_b = sum_{p < Q} H_p Z_{b+Q-1-p} per bin (Q = K / P partition spectra)
-//   resp_inv_kernel   one inverse FFT per output-block pair: Re -> block b, Im -> block b + D
+//   resp_inv_kernel   one workgroup per output block: the merge + inverse FFT, out = its last P
+// Every window and every output block is a transform of its own: roundoff in one block scales
+// with that block's own data, never with a louder block elsewhere in the call (the r2 engine's
+// packed complex pairs -- window j in the real part, j + D in the imaginary -- leaked 2^-53 of
+// block j + D into block j: tests/test_c2_pinned_gpu.py::test_impulse_then_silence_horizon_bound).
 // Per output sample that is O(Q + log F) work whatever the number of bands; the bands enter once,
 // through h, when coefficients or targets change (resp_h_kernel: each band's response by the
 // reference's own recurrence, summed in a fixed order).
 //
 // The per-band state is kept exact: the last K inputs are the handle's history (updated by every
 // converged long call the engine could take, whatever engine ran it), and the band states at the
-// call end are their zero-state response over those K samples (the chunk-128 LTI state kernel in
-// its prepass mode, fb_lti_zero_start_end) -- after every call (HZ_FB_RESP_EAGER, default) or only
+// call end are their zero-start response over those K samples (the band-state pass on the FP64
+// matrix cores, hz_fb_state.hip) -- after every call (HZ_FB_RESP_EAGER, default) or only
 // when a later call, get_state, tick or a setter needs them (HZ_FB_RESP_LAZY).
 // Multi-GPU: time-range shards (hz_fb_set_bank_response + hz_fb_set_time_shard) convolve one
 // rank's run of output blocks with the whole bank's response; DESIGN.md 3.6 and 5.
@@ -31,22 +35,17 @@
 
 namespace {
 
-constexpr int kLgP = 11, kP = 1 << kLgP;       // partition / output block (samples)
-constexpr int kLgF = kLgP + 1, kF = 2 * kP;    // transform size
-constexpr int kRmax = 3;                       // radix-8 passes (hz_fft.h)
-constexpr int kFftThreads = kF >> kRmax;       // 512: one radix-8 group per thread
-constexpr int kMacR = 8;                       // output blocks per MAC thread (partitions padded to it)
-// (A/B) HZ_FB_RESP_MAC_R = 4 / 8 / 16 output blocks per MAC thread
-int mac_r() {
-    static const int r = [] {
-        const int v = std::getenv("HZ_FB_RESP_MAC_R") ? std::atoi(std::getenv("HZ_FB_RESP_MAC_R")) : kMacR;
-        return v == 4 || v == 16 ? v : kMacR;
-    }();
-    return r;
-}
-constexpr long kMinCall = 16384;               // shortest call that keeps the history
-
-size_t fft_lds() { return sizeof(double) * 2 * (size_t)hz::padded_len(kF) + sizeof(double2) * hz::twc_len(kLgF); }
+constexpr int kLgP = 11, kP = 1 << kLgP;   // partition / output block (samples)
+constexpr int kF = 2 * kP;                 // window (samples): real transform length
+constexpr int kLgH = kLgP, kH = kP;        // complex transform length = bins stored per row
+constexpr int kThreads = 256;              // per window / output block
+constexpr int kPT = kH / kThreads;         // complex points per thread (8)
+constexpr int kSplit = (kH / 2 + kThreads) / kThreads;   // bin pairs (k, kH - k), k <= kH / 2, per thread
+constexpr int kMacR = 8;                   // output blocks per MAC thread (partitions padded to it)
+constexpr long kMinCall = 16384;           // shortest call that keeps the history
+// cost model: stationary when N n >= kBandsPerSample (K + n) (hz_fb_tune_response overrides it)
+constexpr long kBandsPerSample = 256;
+static_assert(kPT == 8, "radix-8 passes, one group per thread");
 
 // Aggregate impulse response, one wave (64 bands) per workgroup: part[g][tau] = sum over the
 // group's bands of gin_n r_n[tau], r_n = band n's response to a unit impulse with pre = pin_n,
@@ -104,47 +103,79 @@ __global__ __launch_bounds__(256) void resp_hsum_kernel(const double* __restrict
     h[t] = acc;
 }
 
-__device__ __forceinline__ void load_tw(double2* T, const double2* __restrict__ tw) {
-    for (int k = threadIdx.x; k < hz::twc_len(kLgF); k += blockDim.x) T[k] = tw[k];
-}
-
-// the compact twiddle table in two register loads per thread (threads >= twc_len / 2), issued
-// with the data loads and stored with them: one memory latency before the first pass, not two
-template <int NT>
-struct TwRegs {
-    static_assert(2 * NT >= hz::twc_len(kLgF), "two twiddles per thread");
-    double2 a, b;
-    __device__ __forceinline__ void load(const double2* __restrict__ tw) {
-        constexpr int TL = hz::twc_len(kLgF);
-        a = threadIdx.x < TL ? tw[threadIdx.x] : make_double2(0.0, 0.0);
-        b = threadIdx.x + NT < TL ? tw[threadIdx.x + NT] : make_double2(0.0, 0.0);
-    }
-    __device__ __forceinline__ void store(double2* T) const {
-        constexpr int TL = hz::twc_len(kLgF);
-        if (threadIdx.x < TL) T[threadIdx.x] = a;
-        if (threadIdx.x + NT < TL) T[threadIdx.x + NT] = b;
-    }
+// ---- real transforms of one window -----------------------------------------------------------
+// A window of F real samples x[m] is the 2048-point complex sequence z[n] = x[2n] + i x[2n+1];
+// with Zh = FFT(z) (hz_fft.h, bit-reversed out), E = (Zh[k] + conj Zh[kH-k]) / 2 and
+// O = (Zh[k] - conj Zh[kH-k]) / 2i are the even and odd samples' spectra and
+//     X[k] = E + W^k O,   X[kH - k] = conj(E - W^k O),   W = e^{-2 pi i / F},
+// one thread per pair (k, kH - k).  Rows hold X_0 .. X_{kH-1} (X_0 real, imaginary part 0);
+// X_kH (real) is kept apart (nyq), so the MAC is one complex product per stored bin.
+struct FftLds {
+    double re[hz::padded_len(kH)], im[hz::padded_len(kH)];
+    double2 T[hz::twc_len(kLgH)];   // W_kH^k, k <= kH / 8 (tw[2k])
 };
 
-// Partition spectra H_p = FFT(h[pP, (p+1)P) zero-padded to F) / F (the inverse is unnormalised;
-// 1/F is a power of two), bins in the transforms' storage (bit-reversed) order
-__global__ __launch_bounds__(kFftThreads) void resp_hspec_kernel(const double* __restrict__ h, long K,
-                                                                 const double2* __restrict__ tw,
-                                                                 double2* __restrict__ H) {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* re = lds;
-    double* im = lds + hz::padded_len(kF);
-    double2* T = (double2*)(im + hz::padded_len(kF));
-    load_tw(T, tw);
-    const long p0 = (long)blockIdx.x * kP;
-    for (int k = threadIdx.x; k < kF; k += blockDim.x) {
-        re[hz::pad16(k)] = (k < kP && p0 + k < K) ? h[p0 + k] * (1.0 / kF) : 0.0;
-        im[hz::pad16(k)] = 0.0;
+__device__ __forceinline__ void load_tw_compact(double2* T, const double2* __restrict__ tw) {
+    for (int k = threadIdx.x; k < hz::twc_len(kLgH); k += kThreads) T[k] = tw[2 * k];
+}
+
+template <class Load>
+__device__ __forceinline__ void real_window_fwd(FftLds& s, Load load, const double2* __restrict__ tw,
+                                                double2* __restrict__ zrow, double* __restrict__ nyq) {
+    const int t = threadIdx.x;
+    // every global load of the thread before the first LDS store
+    double vr[kPT], vi[kPT];
+#pragma unroll
+    for (int i = 0; i < kPT; ++i) {
+        const int n = t + i * kThreads;
+        vr[i] = load(2 * n);
+        vi[i] = load(2 * n + 1);
+    }
+    double2 w[kSplit];
+#pragma unroll
+    for (int i = 0; i < kSplit; ++i) {
+        const int k = t + i * kThreads;
+        w[i] = k <= kH / 2 ? tw[k] : make_double2(1.0, 0.0);
+    }
+    load_tw_compact(s.T, tw);
+#pragma unroll
+    for (int i = 0; i < kPT; ++i) {
+        const int e = hz::pad16(t + i * kThreads);
+        s.re[e] = vr[i];
+        s.im[e] = vi[i];
     }
     __syncthreads();
-    hz::fft_fwd_lead<kRmax>(re, im, kLgF, T, true);
-    double2* o = H + (long)blockIdx.x * kF;
-    for (int q = threadIdx.x; q < kF; q += blockDim.x) o[q] = make_double2(re[hz::pad16(q)], im[hz::pad16(q)]);
+    hz::fft_fwd_lead<3>(s.re, s.im, kLgH, s.T, true);   // ends with a barrier
+#pragma unroll
+    for (int i = 0; i < kSplit; ++i) {
+        const int k = t + i * kThreads;
+        if (k > kH / 2) break;
+        if (k == 0) {   // E_0 = Re Zh_0, O_0 = Im Zh_0: X_0 = E + O, X_kH = E - O
+            const double zr = s.re[0], zi = s.im[0];
+            zrow[0] = make_double2(zr + zi, 0.0);
+            *nyq = zr - zi;
+            continue;
+        }
+        const int pa = hz::pad16(hz::bitrev(k, kLgH)), pb = hz::pad16(hz::bitrev(kH - k, kLgH));
+        const double ar = s.re[pa], ai = s.im[pa], br = s.re[pb], bi = s.im[pb];
+        const double er = 0.5 * (ar + br), ei = 0.5 * (ai - bi);
+        const double orr = 0.5 * (ai + bi), oi = -0.5 * (ar - br);
+        const double wr = w[i].x * orr - w[i].y * oi, wi = w[i].x * oi + w[i].y * orr;
+        zrow[k] = make_double2(er + wr, ei + wi);
+        if (k != kH / 2) zrow[kH - k] = make_double2(er - wr, wi - ei);
+    }
+}
+
+// Partition spectra H_p = FFT(h[pP, (p+1)P) zero-padded to F) / F (the inverse is unnormalised;
+// 1/F is a power of two)
+__global__ __launch_bounds__(kThreads) void resp_hspec_kernel(const double* __restrict__ h, long K,
+                                                             const double2* __restrict__ tw, double2* __restrict__ H,
+                                                             double* __restrict__ Hn) {
+    __shared__ FftLds s;
+    const long p0 = (long)blockIdx.x * kP;
+    real_window_fwd(
+        s, [&](int m) { return (m < kP && p0 + m < K) ? h[p0 + m] * (1.0 / kF) : 0.0; }, tw,
+        H + (long)blockIdx.x * kH, Hn + blockIdx.x);
 }
 
 struct RespArgs {
@@ -152,10 +183,12 @@ struct RespArgs {
     const double* x;      // [n] the call's input
     long K, n;            // horizon; the call's length
     long off, n_out;      // outputs of this launch: out[off, off + n_out) (time-range shards)
-    int Q, D;             // partitions; packed output-block pairs
-    const double2* tw;
-    double2* Z;           // [Q + D - 1 (+ pad)][F] packed window spectra
-    const double2* Y;     // [D][F] packed output spectra
+    int Q, B;             // partitions; output blocks
+    const double2* tw;    // W_F^k, k < kH
+    double2* Z;           // [Q + B - 1 (+ pad)][kH] window spectra
+    double* Zn;           // [..] their bin kH
+    const double2* Y;     // [B][kH] output spectra (bins < kH)
+    const double* Hn;     // [Q] partition spectra at bin kH
     double* out;          // [n]
     // state upkeep, done by the inverse kernel's threads: the history after the call (the last K
     // samples of [hist | x]), the smoothers' closed form, the x history (the last O inputs)
@@ -175,39 +208,12 @@ __device__ __forceinline__ double resp_u(const RespArgs& a, long m) {
     return m < a.off + a.n_out ? a.x[m] : 0.0;
 }
 
-// Z_j = FFT(W_{j+1} + i W_{j+1+D}), W_i = u[(i-1)P, (i+1)P)
-// (ABL, diagnostics HZ_FB_RESP_ABL=1: no FFT passes -- wrong results, timed by rocprof)
-template <int ABL = 0, int RM = kRmax>
-__global__ __launch_bounds__(kF >> RM) void resp_fwd_kernel(RespArgs a) {
-    constexpr int kFftThreads = kF >> RM;
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* re = lds;
-    double* im = lds + hz::padded_len(kF);
-    double2* T = (double2*)(im + hz::padded_len(kF));
-    const long j = blockIdx.x;
-    const long m0 = j * kP, m1 = (j + a.D) * kP;
-    // every load of the thread (twiddles included) issued before the first LDS store
-    constexpr int PT = kF / kFftThreads;
-    TwRegs<kFftThreads> tr;
-    tr.load(a.tw);
-    double vr[PT], vi[PT];
-#pragma unroll
-    for (int i = 0; i < PT; ++i) {
-        const int k = threadIdx.x + i * kFftThreads;
-        vr[i] = resp_u(a, m0 + k);
-        vi[i] = resp_u(a, m1 + k);
-    }
-    tr.store(T);
-#pragma unroll
-    for (int i = 0; i < PT; ++i) {
-        const int k = threadIdx.x + i * kFftThreads;
-        re[hz::pad16(k)] = vr[i];
-        im[hz::pad16(k)] = vi[i];
-    }
-    __syncthreads();
-    if constexpr (ABL == 0) hz::fft_fwd_lead<RM>(re, im, kLgF, T, true);
-    double2* z = a.Z + j * kF;
-    for (int q = threadIdx.x; q < kF; q += blockDim.x) z[q] = make_double2(re[hz::pad16(q)], im[hz::pad16(q)]);
+// Z_j = the spectrum of W_j = u[jP, jP + F)
+__global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a) {
+    __shared__ FftLds s;
+    const long m0 = (long)blockIdx.x * kP;
+    real_window_fwd(
+        s, [&](int m) { return resp_u(a, m0 + m); }, a.tw, a.Z + (long)blockIdx.x * kH, a.Zn + blockIdx.x);
 }
 
 // Y_b[q] = sum_{p < Q} H_p[q] Z_{b+Q-1-p}[q] for b in [b0, b0 + R): thread = bin q x R output
@@ -217,15 +223,15 @@ __global__ __launch_bounds__(kF >> RM) void resp_fwd_kernel(RespArgs a) {
 // block's 2R loads are issued before this block's MACs (latency once per call, not per step).
 template <int R>
 __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict__ H, const double2* __restrict__ Z,
-                                                       double2* __restrict__ Y, int Q, int Qp, int D) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;   // bin (grid.x = F / 256)
+                                                       double2* __restrict__ Y, int Q, int Qp, int B) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;   // bin (grid.x = kH / 256)
     const int b0 = blockIdx.y * R;
     double ar[R], ai[R], zr[R], zi[R];
     const long base = (long)b0 + Q - 1;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         ar[r] = ai[r] = 0.0;
-        const double2 z = Z[(base + r) * kF + q];
+        const double2 z = Z[(base + r) * kH + q];
         zr[r] = z.x;
         zi[r] = z.y;
     }
@@ -233,9 +239,9 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
     auto fetch = [&](int p0) {
 #pragma unroll
         for (int u = 0; u < R; ++u) {
-            hb[u] = H[(long)(p0 + u) * kF + q];
+            hb[u] = H[(long)(p0 + u) * kH + q];
             const long zi_ = base - (p0 + u) - 1;   // < 0 only past Q (zero H rows)
-            zb[u] = Z[(zi_ > 0 ? zi_ : 0) * kF + q];
+            zb[u] = Z[(zi_ > 0 ? zi_ : 0) * kH + q];
         }
     };
     fetch(0);
@@ -265,121 +271,66 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
     }
 #pragma unroll
     for (int r = 0; r < R; ++r)
-        if (b0 + r < D) Y[(long)(b0 + r) * kF + q] = make_double2(ar[r], ai[r]);
+        if (b0 + r < B) Y[(long)(b0 + r) * kH + q] = make_double2(ar[r], ai[r]);
 }
 
-// The same MACs with the operands shared through LDS: workgroup = 64 bins x 4 waves, wave w owns
-// output blocks b0 + w R .. + R - 1 of the workgroup's 4 R; the Qp partition spectra and the
-// 4 R + Qp window spectra of the 64 bins are staged once (24 + 57 KB at C2) instead of read by
-// every thread from L2, then each thread runs the register ring of resp_mac_kernel from LDS.
-template <int R>
-__global__ __launch_bounds__(256) void resp_mac_lds_kernel(const double2* __restrict__ H, const double2* __restrict__ Z,
-                                                           double2* __restrict__ Y, int Q, int Qp, int D, int zrows) {
-    extern __shared__ __attribute__((aligned(16))) double mac_lds[];
-    double2* hs = (double2*)mac_lds;   // [Qp][64]
-    double2* zs = hs + Qp * 64;        // [4 R + Qp][64]
-    const int bin = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int q = blockIdx.x * 64 + bin;
-    const int bw = blockIdx.y * 4 * R;            // first output block of the workgroup
-    const int nz = 4 * R + Qp;                    // window rows bw .. bw + nz - 1 (clamped)
-    // staging in batches of 8 loads per thread issued before their stores (few memory latencies)
-    constexpr int SB = 8;
-    for (int i0 = threadIdx.x; i0 < Qp * 64; i0 += SB * 256) {
-        double2 v[SB];
-#pragma unroll
-        for (int k = 0; k < SB; ++k) {
-            const int i = i0 + k * 256;
-            v[k] = i < Qp * 64 ? H[(long)(i >> 6) * kF + blockIdx.x * 64 + (i & 63)] : make_double2(0.0, 0.0);
-        }
-#pragma unroll
-        for (int k = 0; k < SB; ++k)
-            if (i0 + k * 256 < Qp * 64) hs[i0 + k * 256] = v[k];
-    }
-    for (int i0 = threadIdx.x; i0 < nz * 64; i0 += SB * 256) {
-        double2 v[SB];
-#pragma unroll
-        for (int k = 0; k < SB; ++k) {
-            const int i = i0 + k * 256;
-            const int row = min(bw + (i >> 6), zrows - 1);
-            v[k] = i < nz * 64 ? Z[(long)row * kF + blockIdx.x * 64 + (i & 63)] : make_double2(0.0, 0.0);
-        }
-#pragma unroll
-        for (int k = 0; k < SB; ++k)
-            if (i0 + k * 256 < nz * 64) zs[i0 + k * 256] = v[k];
-    }
-    __syncthreads();
-    // thread's outputs b = bw + w R + r; Y_b = sum_p H_p Z_{b+Q-1-p}: local row w R + r + Q - 1 - p
-    double ar[R], ai[R], zr[R], zi[R];
-    const int base = w * R + Q - 1;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        ar[r] = ai[r] = 0.0;
-        const double2 z = zs[(base + r) * 64 + bin];
-        zr[r] = z.x;
-        zi[r] = z.y;
-    }
-    for (int p0 = 0; p0 < Qp; p0 += R) {
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-            const int p = p0 + u;
-            const double2 hv = hs[p * 64 + bin];
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int sl = ((r - u) % R + R) % R;
-                ar[r] = fma(hv.x, zr[sl], ar[r]);
-                ar[r] = fma(-hv.y, zi[sl], ar[r]);
-                ai[r] = fma(hv.x, zi[sl], ai[r]);
-                ai[r] = fma(hv.y, zr[sl], ai[r]);
-            }
-            const int zrow = base - p - 1;   // < 0 only past Q (zero H rows)
-            const double2 z = zs[(zrow > 0 ? zrow : 0) * 64 + bin];
-            const int sl = ((-(u + 1)) % R + R) % R;
-            zr[sl] = z.x;
-            zi[sl] = z.y;
-        }
-    }
-    (void)q;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int b = bw + w * R + r;
-        if (b < D) Y[(long)b * kF + blockIdx.x * 64 + bin] = make_double2(ar[r], ai[r]);
-    }
-}
-
-// out[bP + r] = Re IFFT(Y_b)[P + r], out[(b + D)P + r] = Im ...
-template <int ABL = 0, int RM = kRmax>
-__global__ __launch_bounds__(kF >> RM) void resp_inv_kernel(RespArgs a) {
-    constexpr int kFftThreads = kF >> RM;
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* re = lds;
-    double* im = lds + hz::padded_len(kF);
-    double2* T = (double2*)(im + hz::padded_len(kF));
+// output block b: the merge of Y_b into Zh' = E' + i O' (E' = Y[k] + conj Y[kH-k],
+// O' = (Y[k] - conj Y[kH-k]) W^-k), the inverse 2048-point FFT, out[bP + 2r (+1)] = Re (Im)
+// z[kH/2 + r] (the last P samples of the window's circular convolution)
+__global__ __launch_bounds__(kThreads) void resp_inv_kernel(RespArgs a) {
+    __shared__ FftLds s;
+    const int t = threadIdx.x;
     const long b = blockIdx.x;
-    const double2* y = a.Y + b * kF;
-    constexpr int PT = kF / kFftThreads;
-    TwRegs<kFftThreads> tr;
-    tr.load(a.tw);
-    double2 v[PT];
+    const double2* y = a.Y + b * kH;
+    double2 ya[kSplit], yb[kSplit], w[kSplit];
 #pragma unroll
-    for (int i = 0; i < PT; ++i) v[i] = y[threadIdx.x + i * kFftThreads];
-    tr.store(T);
+    for (int i = 0; i < kSplit; ++i) {
+        const int k = t + i * kThreads;
+        const bool on = k <= kH / 2;
+        ya[i] = on ? y[k] : make_double2(0.0, 0.0);
+        yb[i] = on && k ? y[kH - k] : make_double2(0.0, 0.0);
+        w[i] = on ? a.tw[k] : make_double2(1.0, 0.0);
+    }
+    load_tw_compact(s.T, a.tw);
+    // bin kH (real): sum_p Hn[p] Zn[b + Q - 1 - p], wave 0 in a fixed order
+    double yn = 0.0;
+    if (t < 64) {
+        for (int p = t; p < a.Q; p += 64) yn = fma(a.Hn[p], a.Zn[b + a.Q - 1 - p], yn);
 #pragma unroll
-    for (int i = 0; i < PT; ++i) {
-        const int q = threadIdx.x + i * kFftThreads;
-        re[hz::pad16(q)] = v[i].x;
-        im[hz::pad16(q)] = v[i].y;
+        for (int o = 32; o; o >>= 1) yn += __shfl_xor(yn, o);
+    }
+#pragma unroll
+    for (int i = 0; i < kSplit; ++i) {
+        const int k = t + i * kThreads;
+        if (k > kH / 2) break;
+        if (k == 0) {
+            s.re[0] = ya[i].x + yn;
+            s.im[0] = ya[i].x - yn;
+            continue;
+        }
+        const double er = ya[i].x + yb[i].x, ei = ya[i].y - yb[i].y;
+        const double dr = ya[i].x - yb[i].x, di = ya[i].y + yb[i].y;
+        const double orr = dr * w[i].x + di * w[i].y, oi = di * w[i].x - dr * w[i].y;
+        const int pa = hz::pad16(hz::bitrev(k, kLgH)), pb = hz::pad16(hz::bitrev(kH - k, kLgH));
+        s.re[pa] = er - oi;
+        s.im[pa] = ei + orr;
+        if (k != kH / 2) {
+            s.re[pb] = er + oi;
+            s.im[pb] = orr - ei;
+        }
     }
     __syncthreads();
-    if constexpr (ABL == 0) hz::fft_inv_tail<RM>(re, im, kLgF, T, true);
-    for (int r = threadIdx.x; r < kP; r += blockDim.x) {
-        const long t0 = b * kP + r, t1 = (b + a.D) * kP + r;
-        if (t0 < a.n_out) a.out[a.off + t0] = re[hz::pad16(kP + r)];
-        if (t1 < a.n_out) a.out[a.off + t1] = im[hz::pad16(kP + r)];
+    hz::fft_inv_tail<3>(s.re, s.im, kLgH, s.T, true);
+    for (int r = t; r < kH / 2; r += kThreads) {
+        const long t0 = b * kP + 2 * r;
+        const double v0 = s.re[hz::pad16(kH / 2 + r)], v1 = s.im[hz::pad16(kH / 2 + r)];
+        if (t0 < a.n_out) a.out[a.off + t0] = v0;
+        if (t0 + 1 < a.n_out) a.out[a.off + t0 + 1] = v1;
     }
     // state upkeep (the forward kernel, the last reader of hist, has finished)
-    const long g = b * blockDim.x + threadIdx.x, stride = (long)gridDim.x * blockDim.x;
+    const long g = b * blockDim.x + t, stride = (long)gridDim.x * blockDim.x;
     // a time-range shard leaves zeros outside its range: the ranks' outputs sum to the call's
-    for (long t = g; t < a.n - a.n_out; t += stride) a.out[t < a.off ? t : t + a.n_out] = 0.0;
+    for (long i = g; i < a.n - a.n_out; i += stride) a.out[i < a.off ? i : i + a.n_out] = 0.0;
     for (long i = g; i < a.K; i += stride) {
         const long m = a.n + i;
         a.hist_next[i] = m < a.K ? a.hist[m] : a.x[m - a.K];
@@ -420,16 +371,16 @@ int resp_alloc(double** p, size_t* cap, size_t need) {
     return HZ_OK;
 }
 
+int q_padded(int Q) { return (Q + kMacR - 1) / kMacR * kMacR; }
+
 // per-bank setup: horizon, history buffers, twiddles
 int resp_setup(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     if (R.K == -2) {
-        // ||M^K|| < 2^-53 (env HZ_FB_RESP_HORIZON_LOG2, e.g. -64): older inputs reach a band state
-        // below one unit in the last place of it, and the bank response's tail below 2^-53 of its
-        // l1 norm; then a whole number of the chunk-128 state kernel's 8192-sample tiles
-        static const int lb = std::getenv("HZ_FB_RESP_HORIZON_LOG2") ? std::atoi(std::getenv("HZ_FB_RESP_HORIZON_LOG2"))
-                                                                      : -53;
-        R.K = hz_fbi::fb_horizon(h, lb);
+        // ||M^K|| < 2^-53: older inputs reach a band state below one unit in the last place of
+        // it, and the bank response's tail below 2^-53 of its l1 norm; then a whole number of the
+        // chunk-128 state kernel's 8192-sample tiles
+        R.K = hz_fbi::fb_horizon(h, -53);
         if (R.K >= 0) R.K = std::max<long>(8192, (R.K + 8191) / 8192 * 8192);
         R.h_valid = false;
         R.run = 0;
@@ -442,29 +393,18 @@ int resp_setup(hz_fb* h) {
     }
     HZ_TRY(resp_alloc(&R.d_hist[0], &R.hist_cap0, (size_t)R.K));
     HZ_TRY(resp_alloc(&R.d_hist[1], &R.hist_cap1, (size_t)R.K));
-    if (!R.d_tw) {
-        std::vector<double2> tw(kF / 2);
+    if (!R.d_tw) {   // W_F^k, k < kH, in long double
+        std::vector<double2> tw(kH);
         const long double pi = acosl(-1.0L);
-        for (int k = 0; k < kF / 2; ++k) {
+        for (int k = 0; k < kH; ++k) {
             const long double ang = -2.0L * pi * k / kF;
             tw[k] = make_double2((double)cosl(ang), (double)sinl(ang));
         }
         HZ_TRY_HIP(hipMalloc((void**)&R.d_tw, sizeof(double2) * tw.size()));
         HZ_TRY_HIP(hipMemcpy(R.d_tw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice));
-        for (const void* k : {(const void*)resp_hspec_kernel, (const void*)resp_fwd_kernel<0>, (const void*)resp_inv_kernel<0>,
-                              (const void*)resp_fwd_kernel<1>, (const void*)resp_inv_kernel<1>})
-            HZ_TRY(hz_fbi::fb_set_lds_attr(k));
     }
     return HZ_OK;
 }
-
-int resp_state_mode() {
-    // (C2, 200 steps: 2 -> 0.0664 ms/step; 0 -> 0.0730, 1 -> 0.0776, 3 -> 0.0739: beside the
-    // convolution the state work slows the FFT and MAC kernels by as much as it hides)
-    static const int m = std::getenv("HZ_FB_RESP_STATE") ? std::atoi(std::getenv("HZ_FB_RESP_STATE")) : 2;
-    return m >= 0 && m <= 3 ? m : 2;
-}
-bool resp_gemm_states() { return resp_state_mode() == 1 || resp_state_mode() == 3; }
 
 // h and its partition spectra for the current coefficients / targets
 int resp_build_h(hz_fb* h) {
@@ -473,16 +413,15 @@ int resp_build_h(hz_fb* h) {
     const int O = h->order, N = h->N;
     const long K = R.K;
     const int G = (N + 63) / 64;
-    const int Q = (int)(K / kP);
-    const int Qp = (Q + mac_r() - 1) / mac_r() * mac_r();   // zero spectra past Q (the MAC's unguarded blocks)
+    const int Q = (int)(K / kP), Qp = q_padded(Q);   // zero spectra past Q (the MAC's unguarded blocks)
     HZ_TRY(resp_alloc(&R.d_coef, &R.coef_cap, (size_t)N * (2 * O + 1)));
     HZ_TRY_HIP(hipMemcpyAsync(R.d_coef, h->F.data(), sizeof(double) * N * (O + 1), hipMemcpyHostToDevice, h->stream));
     HZ_TRY_HIP(hipMemcpyAsync(R.d_coef + (size_t)N * (O + 1), h->B.data(), sizeof(double) * N * O,
                               hipMemcpyHostToDevice, h->stream));
     HZ_TRY(resp_alloc(&R.d_hpart, &R.hpart_cap, (size_t)G * K));
     HZ_TRY(resp_alloc(&R.d_h, &R.h_cap, (size_t)K));
-    HZ_TRY(resp_alloc(&R.d_H, &R.H_cap, (size_t)2 * Qp * kF));
-    HZ_TRY_HIP(hipMemsetAsync(R.d_H, 0, sizeof(double2) * (size_t)Qp * kF, h->stream));
+    HZ_TRY(resp_alloc(&R.d_H, &R.H_cap, (size_t)Qp * (2 * kH + 1)));   // [Qp][kH] complex, then [Qp] bin kH
+    HZ_TRY_HIP(hipMemsetAsync(R.d_H, 0, sizeof(double) * (size_t)Qp * (2 * kH + 1), h->stream));
     hipLaunchKernelGGL(pick_h(O), dim3(G), dim3(64), 0, h->stream, (const double*)R.d_coef,
                        (const double*)(R.d_coef + (size_t)N * (O + 1)), (const double*)h->d_pin,
                        (const double*)h->d_gin, N, K, R.d_hpart);
@@ -492,16 +431,10 @@ int resp_build_h(hz_fb* h) {
     HZ_TRY_HIP(hipGetLastError());
     if (R.over_valid)   // the whole bank's response (time-range shards)
         HZ_TRY_HIP(hipMemcpyAsync(R.d_h, R.h_over.data(), sizeof(double) * K, hipMemcpyHostToDevice, h->stream));
-    hipLaunchKernelGGL(resp_hspec_kernel, dim3((unsigned)Q), dim3(kFftThreads), fft_lds(), h->stream,
-                       (const double*)R.d_h, K, (const double2*)R.d_tw, (double2*)R.d_H);
+    hipLaunchKernelGGL(resp_hspec_kernel, dim3((unsigned)Q), dim3(kThreads), 0, h->stream, (const double*)R.d_h, K,
+                       (const double2*)R.d_tw, (double2*)R.d_H, R.d_H + (size_t)Qp * 2 * kH);
     HZ_TRY_HIP(hipGetLastError());
-    if (resp_gemm_states()) {   // end-state GEMM operands for these coefficients and pre-amps
-        HZ_TRY(resp_alloc(&R.d_eg, &R.eg_cap, (size_t)hz_fbi::fb_end_rows(O) * hz_fbi::fb_end_cols(N, O)));
-        HZ_TRY(resp_alloc(&R.d_epart, &R.epart_cap, hz_fbi::fb_end_scratch(N, O, K)));
-        HZ_TRY(hz_fbi::fb_end_operands(h, R.d_eg));
-    } else {
-        HZ_TRY(hz_fbi::fb_lti_prepare_end(h, K));   // the state kernel's records, for LAZY too
-    }
+    HZ_TRY(hz_fbi::fb_lti_prepare_end(h, K));   // the state kernel's records, for LAZY too
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));   // pageable coefficient sources
     R.h_valid = true;
     return HZ_OK;
@@ -511,27 +444,16 @@ int resp_build_h(hz_fb* h) {
 // stationary call: after it (EAGER) or when needed (LAZY))
 int resp_states(hz_fb* h, double* ystate) {
     hz_fb::Resp& R = h->resp;
-    if (resp_gemm_states() && R.d_eg)   // operands of the coefficients the history ran with
-        return hz_fbi::fb_end_state_gemm(h, R.d_hist[R.hcur], nullptr, 0, R.K, R.d_eg, R.d_epart, ystate, h->stream);
-    return hz_fbi::fb_lti_zero_start_end(h, R.d_hist[R.hcur], R.K, R.d_zero, R.d_zero, ystate);
+    return hz_fbi::fb_state_window(h, R.d_hist[R.hcur], R.K, ystate, h->stream);
 }
 
 long resp_min_call(const hz_fb* h) { return h->resp.min_call > 0 ? h->resp.min_call : kMinCall; }
-
-int resp_mode_default() {
-    static const int m = [] {
-        const char* e = std::getenv("HZ_FB_RESP");   // 0 off, 1 eager (default), 2 lazy
-        const int v = e ? std::atoi(e) : HZ_FB_RESP_EAGER;
-        return v >= HZ_FB_RESP_OFF && v <= HZ_FB_RESP_LAZY ? v : HZ_FB_RESP_EAGER;
-    }();
-    return m;
-}
 
 }  // namespace
 
 namespace hz_fbi {
 
-void fb_resp_init(hz_fb* h) { h->resp.mode = resp_mode_default(); }
+void fb_resp_init(hz_fb* h) { h->resp.mode = HZ_FB_RESP_EAGER; }
 
 void fb_resp_invalidate(hz_fb* h, bool coefficients) {
     h->resp.run = 0;
@@ -552,8 +474,7 @@ bool fb_resp_time_sharded(const hz_fb* h) { return h->resp.over_valid && h->resp
 // the cost model alone: would a call of n samples run stationary (given the history)?
 static bool resp_worth(const hz_fb* h, long n) {
     const hz_fb::Resp& R = h->resp;
-    static const long per_env = std::getenv("HZ_FB_RESP_BANDS") ? std::atol(std::getenv("HZ_FB_RESP_BANDS")) : 256;
-    const long per = R.bands_per_sample >= 0 ? R.bands_per_sample : per_env;
+    const long per = R.bands_per_sample >= 0 ? R.bands_per_sample : kBandsPerSample;
     // time-range shards cost the whole bank's convolution (the choice itself is armed by the
     // caller on every rank, hz_fb_arm_time_shard)
     const double bands = R.over_valid ? (double)h->N_total : (double)h->N;
@@ -612,8 +533,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     HZ_TRY(resp_setup(h));
     HZ_TRY(resp_build_h(h));
     const long K = R.K;
-    const int Q = (int)(K / kP);
-    const int Qp = (Q + mac_r() - 1) / mac_r() * mac_r();
+    const int Q = (int)(K / kP), Qp = q_padded(Q);
     // time-range shard (hz_fb_set_time_shard, with the whole bank's response): this rank's run of
     // whole output blocks
     long off = 0, n_out = n;
@@ -623,16 +543,17 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         off = std::min(n, lo * kP);
         n_out = std::min(n, hi * kP) - off;
     }
-    const long B = std::max<long>(1, (n_out + kP - 1) / kP);
-    const int D = (int)((B + 1) / 2);
-    const int nz = Q + D - 1;
-    // rows the MACs may read: the last register window (padded to 4 R output blocks, Qp partitions)
-    const int zrows = (D + 64 - 1) / 64 * 64 + Qp;   // >= every MAC variant's last window
-    if ((size_t)zrows * kF * 2 > R.Z_cap) {
-        HZ_TRY(resp_alloc(&R.d_Z, &R.Z_cap, (size_t)zrows * kF * 2));
-        HZ_TRY_HIP(hipMemsetAsync(R.d_Z, 0, sizeof(double2) * (size_t)zrows * kF, h->stream));
+    const int B = (int)std::max<long>(1, (n_out + kP - 1) / kP);
+    const int nz = Q + B - 1;
+    // rows the MAC may read: its last register window (B padded to kMacR output blocks, Qp
+    // partitions); rows past nz are never stored, only multiplied into discarded outputs
+    const int zrows = (B + 64 - 1) / 64 * 64 + Qp;
+    if ((size_t)zrows * (2 * kH + 1) > R.Z_cap) {
+        HZ_TRY(resp_alloc(&R.d_Z, &R.Z_cap, (size_t)zrows * (2 * kH + 1)));
+        HZ_TRY_HIP(hipMemsetAsync(R.d_Z, 0, sizeof(double) * R.Z_cap, h->stream));
     }
-    HZ_TRY(resp_alloc(&R.d_Y, &R.Y_cap, (size_t)D * kF * 2));
+    const size_t zn_at = (size_t)zrows * 2 * kH;   // [zrows] bin kH after the rows
+    HZ_TRY(resp_alloc(&R.d_Y, &R.Y_cap, (size_t)B * kH * 2));
     hipEvent_t* e = nullptr;
     if (h->prof) {
         HZ_TRY(fb_prof_events(h, &e));
@@ -647,10 +568,12 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.off = off;
     a.n_out = n_out;
     a.Q = Q;
-    a.D = D;
+    a.B = B;
     a.tw = (const double2*)R.d_tw;
     a.Z = (double2*)R.d_Z;
+    a.Zn = R.d_Z + zn_at;
     a.Y = (const double2*)R.d_Y;
+    a.Hn = R.d_H + (size_t)Qp * 2 * kH;
     a.out = d_out;
     a.hist_next = R.d_hist[R.hcur ^ 1];
     a.pg = h->d_pg[h->scur];
@@ -662,71 +585,20 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.xhist_next = h->d_xhist[h->xcur ^ 1];
     a.N = h->N;
     a.O = h->order;
-    // EAGER: the band states after this call (the last K samples of [hist | x]) do not depend on
-    // the convolution -- the end-state GEMM runs on a side stream beside it, joined at the end
-    const bool lazy = R.mode == HZ_FB_RESP_LAZY;
-    // where the band states are computed (HZ_FB_RESP_STATE, A/B): 2 (default) the chunk-128 state
-    // kernel in prepass mode after the convolution; 0 that kernel over x's last K samples on a
-    // side stream beside the convolution (calls n >= K; else as 2), 1 the end-state GEMM on the
-    // side stream, 3 the end-state GEMM after the convolution
-    const int smode = resp_state_mode() == 0 && n < K ? 2 : resp_state_mode();
-    const bool side = !lazy && (smode == 0 || smode == 1);
-    if (side) {
-        if (!R.side) {
-            HZ_TRY_HIP(hipStreamCreateWithFlags(&R.side, hipStreamNonBlocking));
-            HZ_TRY_HIP(hipEventCreateWithFlags(&R.ev_fork, hipEventDisableTiming));
-            HZ_TRY_HIP(hipEventCreateWithFlags(&R.ev_join, hipEventDisableTiming));
-        }
-        HZ_TRY_HIP(hipEventRecord(R.ev_fork, h->stream));
-        HZ_TRY_HIP(hipStreamWaitEvent(R.side, R.ev_fork, 0));
-        if (smode == 0)
-            HZ_TRY(hz_fbi::fb_lti_zero_start_end_on(h, d_in + (n - K), K, R.d_zero, R.d_zero,
-                                                    h->d_ystate[h->scur ^ 1], R.side));
-        else
-            HZ_TRY(hz_fbi::fb_end_state_gemm(h, R.d_hist[R.hcur], d_in, n, K, R.d_eg, R.d_epart,
-                                             h->d_ystate[h->scur ^ 1], R.side));
-        HZ_TRY_HIP(hipEventRecord(R.ev_join, R.side));
-    }
-    static const int abl = std::getenv("HZ_FB_RESP_ABL") ? std::atoi(std::getenv("HZ_FB_RESP_ABL")) : 0;
-    // (A/B) HZ_FB_RESP_RADIX=4: radix-4 passes on 1024 threads per transform instead of radix 8 on 512
-    static const bool r4 = std::getenv("HZ_FB_RESP_RADIX") && std::atoi(std::getenv("HZ_FB_RESP_RADIX")) == 4;
-    if (r4) {
-        HZ_TRY(fb_set_lds_attr((const void*)resp_fwd_kernel<0, 2>));
-        HZ_TRY(fb_set_lds_attr((const void*)resp_inv_kernel<0, 2>));
-    }
-    typedef void (*RespFftKernel)(RespArgs);
-    const RespFftKernel kfwd = r4 ? resp_fwd_kernel<0, 2> : abl == 1 ? resp_fwd_kernel<1> : resp_fwd_kernel<0>;
-    const RespFftKernel kinv = r4 ? resp_inv_kernel<0, 2> : abl == 1 ? resp_inv_kernel<1> : resp_inv_kernel<0>;
-    hipLaunchKernelGGL(kfwd, dim3((unsigned)nz), dim3(r4 ? kF >> 2 : kFftThreads), fft_lds(), h->stream, a);
+    hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
-    // MAC straight from L2 (default) or through LDS (HZ_FB_RESP_MAC=1; C2: 8.4 vs 8.0 us -- the
-    // L2 reads were not its bound)
-    static const bool mac_lds = std::getenv("HZ_FB_RESP_MAC") && std::getenv("HZ_FB_RESP_MAC")[0] == '1';
-    const size_t mac_bytes = sizeof(double2) * 64 * (size_t)(Qp + 4 * kMacR + Qp);
-    if (mac_lds && mac_bytes <= 160 * 1024) {
-        HZ_TRY(fb_set_lds_attr((const void*)resp_mac_lds_kernel<kMacR>));
-        hipLaunchKernelGGL(resp_mac_lds_kernel<kMacR>, dim3(kF / 64, (unsigned)((D + 4 * kMacR - 1) / (4 * kMacR))),
-                           dim3(256), mac_bytes, h->stream, (const double2*)R.d_H, (const double2*)R.d_Z,
-                           (double2*)R.d_Y, Q, Qp, D, zrows);
-    } else {
-        const int mr = mac_r();
-        auto km = mr == 4 ? resp_mac_kernel<4> : mr == 16 ? resp_mac_kernel<16> : resp_mac_kernel<8>;
-        hipLaunchKernelGGL(km, dim3(kF / 256, (unsigned)((D + mr - 1) / mr)), dim3(256), 0,
-                           h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, D);
-    }
+    hipLaunchKernelGGL(resp_mac_kernel<kMacR>, dim3(kH / 256, (unsigned)((B + kMacR - 1) / kMacR)), dim3(256), 0,
+                       h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B);
     HZ_TRY_HIP(hipGetLastError());
-    hipLaunchKernelGGL(kinv, dim3((unsigned)D), dim3(r4 ? kF >> 2 : kFftThreads), fft_lds(), h->stream, a);
+    hipLaunchKernelGGL(resp_inv_kernel, dim3((unsigned)B), dim3(kThreads), 0, h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     R.hcur ^= 1;   // the inverse kernel wrote the history after the call
     R.run = std::min(R.run + n, 1L << 60);
-    // end state: band states joined from the side stream (EAGER) or computed when needed (LAZY);
+    // end state: the band states over the new history now (EAGER) or when needed (LAZY); the
     // smoothers and x history were written by the inverse kernel
-    if (lazy) {
+    if (R.mode == HZ_FB_RESP_LAZY) {
         R.implicit = true;
-    } else if (side) {
-        HZ_TRY_HIP(hipStreamWaitEvent(h->stream, R.ev_join, 0));
-        R.implicit = false;
     } else {
         HZ_TRY(resp_states(h, h->d_ystate[h->scur ^ 1]));
         R.implicit = false;
@@ -742,13 +614,10 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
 
 void fb_resp_free(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
-    if (R.side) (void)hipStreamSynchronize(R.side);
     for (double* p : {R.d_hist[0], R.d_hist[1], R.d_h, R.d_hpart, R.d_coef, R.d_zero, R.d_H, R.d_Z, R.d_Y, R.d_tw,
-                      R.d_eg, R.d_epart})
+                      R.d_spart})
         if (p) (void)hipFree(p);
-    if (R.ev_fork) (void)hipEventDestroy(R.ev_fork);
-    if (R.ev_join) (void)hipEventDestroy(R.ev_join);
-    if (R.side) (void)hipStreamDestroy(R.side);
+    if (R.d_scount) (void)hipFree(R.d_scount);
     R = hz_fb::Resp();
 }
 

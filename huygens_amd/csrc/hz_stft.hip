@@ -702,7 +702,7 @@ struct hz_stft {
     bool prof = false;
     long chunk = 0;        // samples per internal block (a frame launch covers one)
     int prof_repeat = 1;   // frame launches per block while profiling (hz_stft_profile)
-    bool pair_ok = true;   // two real frames per transform (stft_pair_kernel); HZ_STFT_PAIR=0 turns it off
+    bool pair_ok = true;   // two real frames per transform (stft_pair_kernel)
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     long launches = 0;
@@ -954,7 +954,6 @@ int hz_stft_create(int N, int laps, int window, int proc, double p0, double p1, 
     h->p0 = p0;
     h->p1 = p1;
     h->device = device;
-    if (const char* e = std::getenv("HZ_STFT_PAIR")) h->pair_ok = std::atoi(e) != 0;
     // frames completing inside one internal block, plus those still being read
     const long P = 2L * N - 1;
     auto ring = [&](long c) { return (c + P - 1) / P * 2 * laps + 2 * laps + 2; };

@@ -1,0 +1,149 @@
+// Probe: where a workgroup of the stationary engine's forward transform (resp_fwd_kernel: one
+// 4096-sample real window = 2048-point complex FFT + split, 256 threads) spends its time --
+// s_memtime stamps after the global loads, the LDS store, each FFT pass and the split, for 258
+// workgroups (the C2 call) and for 24 (the partition spectra).  Same code path as
+// hz_fb_resp.hip's real_window_fwd, instrumented.
+// Build: hipcc --offload-arch=gfx950 -O3 -I huygens_amd/csrc -o scripts/probe/fft_phase_probe scripts/probe/fft_phase_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "hz_fft.h"
+
+constexpr int kLgH = 11, kH = 1 << kLgH, kP = kH, kThreads = 256, kPT = kH / kThreads;
+constexpr int kSplit = (kH / 2 + kThreads) / kThreads;
+constexpr int kStamps = 10;
+
+struct FftLds {
+    double re[hz::padded_len(kH)], im[hz::padded_len(kH)];
+    double2 T[hz::twc_len(kLgH)];
+};
+
+__device__ __forceinline__ long long stamp() {
+    __builtin_amdgcn_sched_barrier(0);
+    const long long t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
+template <int MODE>   // 0: full; 1: loads + stores only (no FFT passes, no split math)
+__global__ __launch_bounds__(kThreads) void fwd_probe(const double* __restrict__ u, const double2* __restrict__ tw,
+                                                     double2* __restrict__ Z, double* __restrict__ Zn,
+                                                     long long* __restrict__ st) {
+    __shared__ FftLds s;
+    long long ts[kStamps];
+    int ns = 0;
+    ts[ns++] = stamp();
+    const int t = threadIdx.x;
+    const long m0 = (long)blockIdx.x * kP;
+    double vr[kPT], vi[kPT];
+#pragma unroll
+    for (int i = 0; i < kPT; ++i) {
+        const int n = t + i * kThreads;
+        vr[i] = u[m0 + 2 * n];
+        vi[i] = u[m0 + 2 * n + 1];
+    }
+    double2 w[kSplit];
+#pragma unroll
+    for (int i = 0; i < kSplit; ++i) {
+        const int k = t + i * kThreads;
+        w[i] = k <= kH / 2 ? tw[k] : make_double2(1.0, 0.0);
+    }
+    for (int k = t; k < hz::twc_len(kLgH); k += kThreads) s.T[k] = tw[2 * k];
+#pragma unroll
+    for (int i = 0; i < kPT; ++i) {
+        const int e = hz::pad16(t + i * kThreads);
+        s.re[e] = vr[i];
+        s.im[e] = vi[i];
+    }
+    ts[ns++] = stamp();   // 1: loads landed (the stores needed them)
+    __syncthreads();
+    ts[ns++] = stamp();   // 2: barrier
+    if constexpr (MODE == 0) {
+        // fft_fwd_lead<3>(lg 11): a radix-4 pass, then three radix-8 passes, stamped
+        hz::fft_pass_r<3, false>(2, s.re, s.im, kLgH, kLgH - 1, s.T);
+        __syncthreads();
+        ts[ns++] = stamp();
+        int lh = kLgH - 1 - 2;
+        for (int p = 0; p < 3; ++p, lh -= 3) {
+            hz::fft_pass_r<3, false>(3, s.re, s.im, kLgH, lh, s.T);
+            __syncthreads();
+            ts[ns++] = stamp();
+        }
+    }
+    double2* zrow = Z + (long)blockIdx.x * kH;
+#pragma unroll
+    for (int i = 0; i < kSplit; ++i) {
+        const int k = t + i * kThreads;
+        if (k > kH / 2) break;
+        if (k == 0) {
+            zrow[0] = make_double2(s.re[0] + s.im[0], 0.0);
+            Zn[blockIdx.x] = s.re[0] - s.im[0];
+            continue;
+        }
+        const int pa = hz::pad16(hz::bitrev(k, kLgH)), pb = hz::pad16(hz::bitrev(kH - k, kLgH));
+        const double ar = s.re[pa], ai = s.im[pa], br = s.re[pb], bi = s.im[pb];
+        const double er = 0.5 * (ar + br), ei = 0.5 * (ai - bi);
+        const double orr = 0.5 * (ai + bi), oi = -0.5 * (ar - br);
+        const double wr = w[i].x * orr - w[i].y * oi, wi = w[i].x * oi + w[i].y * orr;
+        zrow[k] = make_double2(er + wr, ei + wi);
+        if (k != kH / 2) zrow[kH - k] = make_double2(er - wr, wi - ei);
+    }
+    ts[ns++] = stamp();   // split issued
+    __builtin_amdgcn_s_waitcnt(0);   // stores acknowledged
+    ts[ns++] = stamp();
+    if (t == 0)
+        for (int i = 0; i < kStamps; ++i) st[(long)blockIdx.x * kStamps + i] = i < ns ? ts[i] : 0;
+}
+
+int main() {
+    const int maxw = 258;
+    const long nu = (long)(maxw + 1) * kP;
+    double* u;
+    double2 *tw, *Z;
+    double* Zn;
+    long long* st;
+    hipMalloc(&u, nu * sizeof(double));
+    hipMalloc(&tw, kH * sizeof(double2));
+    hipMalloc(&Z, (long)maxw * kH * sizeof(double2));
+    hipMalloc(&Zn, maxw * sizeof(double));
+    hipMalloc(&st, (long)maxw * kStamps * sizeof(long long));
+    std::vector<double> hu(nu);
+    for (long i = 0; i < nu; ++i) hu[i] = std::sin(0.001 * i);
+    hipMemcpy(u, hu.data(), nu * sizeof(double), hipMemcpyHostToDevice);
+    std::vector<double2> htw(kH);
+    for (int k = 0; k < kH; ++k) htw[k] = make_double2(std::cos(-2 * M_PI * k / (2 * kH)), std::sin(-2 * M_PI * k / (2 * kH)));
+    hipMemcpy(tw, htw.data(), kH * sizeof(double2), hipMemcpyHostToDevice);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    for (int mode = 0; mode < 2; ++mode)
+        for (int wg : {24, 258}) {
+            auto k = mode == 0 ? fwd_probe<0> : fwd_probe<1>;
+            for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(k, dim3(wg), dim3(kThreads), 0, 0, u, tw, Z, Zn, st);
+            hipEventRecord(e0);
+            hipLaunchKernelGGL(k, dim3(wg), dim3(kThreads), 0, 0, u, tw, Z, Zn, st);
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms = 0;
+            hipEventElapsedTime(&ms, e0, e1);
+            std::vector<long long> hs((long)wg * kStamps);
+            hipMemcpy(hs.data(), st, hs.size() * sizeof(long long), hipMemcpyDeviceToHost);
+            const int nst = mode == 0 ? 9 : 5;
+            std::vector<double> avg(nst, 0.0);
+            long long first = hs[0], lastend = 0;
+            for (int b = 0; b < wg; ++b) {
+                for (int i = 1; i < nst; ++i) avg[i] += (double)(hs[b * kStamps + i] - hs[b * kStamps + i - 1]) / wg;
+                first = std::min(first, hs[b * kStamps]);
+                lastend = std::max(lastend, hs[b * kStamps + nst - 1]);
+            }
+            std::printf("mode %d (%s), %3d workgroups: event %.2f us; span first start -> last end %.0f ticks; "
+                        "per-WG phase ticks (s_memtime):", mode, mode ? "no FFT" : "full", wg, 1e3 * ms,
+                        (double)(lastend - first));
+            for (int i = 1; i < nst; ++i) std::printf(" %.0f", avg[i]);
+            std::printf("\n");
+        }
+    return 0;
+}
