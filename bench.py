@@ -166,19 +166,20 @@ def fb_executed_flops(lti, L=32, O=2, N=N_BANDS):
 
 
 def resp_step_flops(K, S, N, O=2):
-    """FP64 flops of one stationary-engine call (hz_fb_resp.hip) of S samples, horizon K:
-    packed window FFTs (Q + D - 1) and output FFTs (D) at 5 F log2 F each, the partition MACs
-    (8 flops per complex MAC, D x F x Q), and the end-state pass (the chunk-128 state kernel in
-    prepass mode over the K history samples: E 2 O 4 ceil((128+O)/4) / 128 + the weighted chunk
-    sum 2 (O^2 + 6 O) / 128 flops per band-sample)."""
+    """FP64 flops of one stationary-engine call (hz_fb_resp.hip) of S samples, horizon K: one
+    real 4096-point transform per window (Q + B - 1) and per output block (B), each a 2048-point
+    complex FFT (5 H log2 H, H = 2048) plus its split / merge (~10 flops per bin pair), the
+    partition MACs (8 flops per complex MAC, B x H x Q), and the band-state pass
+    (hz_fb_state.hip: 2 O 4 ceil((128 + O) / 4) / 128 flops per band-sample of the K-sample
+    window on the matrix cores, plus the per-tile M^64 carry 2 O^2 / 128 per band and chunk
+    position)."""
     import math
-    P, F, lgF = 2048, 4096, 12
+    P, H, lgH = 2048, 2048, 11
     Q = K // P
     B = -(-S // P)
-    D = -(-B // 2)
-    fft = 5.0 * F * lgF
-    conv = (Q + D - 1) * fft + D * F * Q * 8.0 + D * fft
-    state = N * K * (2.0 * O * 4 * math.ceil((128 + O) / 4) / 128 + 2.0 * (O * O + 6 * O) / 128)
+    fft = 5.0 * H * lgH + 10.0 * H
+    conv = (Q + B - 1) * fft + B * H * Q * 8.0 + B * fft
+    state = N * K * (2.0 * O * 4 * math.ceil((128 + O) / 4) / 128) + N * 64 * 2.0 * O * O * (K // 8192)
     return conv, state
 
 
@@ -563,8 +564,8 @@ def main():
         # kernel of the per-band LTI engine, the mix kernel of the general engine; its average
         # duration from the HIP events around it on the handle's stream
         if resp:
-            dom = "fb_lti_kernel<2, 128, 1"
-            dom_name = "fb_lti_kernel<2,128,SEGEND> (band states: zero-start pass over the %d-sample history)" % horizon
+            dom = "fb_state_kernel"
+            dom_name = "fb_state_kernel<2> (band states: zero-start pass over the %d-sample history)" % horizon
             dom_ms = red_ms / max(1, launches)
             dom_model = resp_step_flops(horizon, out_samples, cnt)[1]
         elif lti:
@@ -579,8 +580,7 @@ def main():
             dom_model = 20.0 * cnt * S
         step_kernels = (("fb_lti_kernel", "fb_lti_gemm", "fb_lti_reduce", "fb_lti_seg_carry", "fb_lti_sum",
                          "fb_lti_xrows") if lti
-                        else ("resp_fwd_kernel", "resp_mac_kernel", "resp_inv_kernel", "fb_lti_kernel<2, 128, 1",
-                              "fb_lti_seg_carry") if resp
+                        else ("resp_fwd_kernel", "resp_mac_kernel", "resp_inv_kernel", "fb_state_kernel") if resp
                         else ("fb_mix_kernel", "fb_reduce"))
         extra = (["--lti", args.lti] if args.lti else []) + (["--general"] if args.general else []) + \
                 (["--response", str(args.response)] if args.response >= 0 else [])
@@ -646,8 +646,8 @@ def main():
                 # state pass: the K history samples in, coefficients + pre-amps (6 doubles) in and
                 # O = 2 states out per band; per-band engines: the block I/O and the band records
                 "algorithmic_bytes_per_launch": (8 * horizon + 64 * cnt) if resp else (16 * out_samples + 120 * cnt),
-                "peak_note": "FP64 MFMA peak = FP64 vector peak on MI355X (78.6 TFLOP/s); the kernel's E phase is "
-                             "v_mfma_f64_16x16x4f64, its scan FP64 VALU on the same pipe",
+                "peak_note": "FP64 MFMA peak = FP64 vector peak on MI355X (78.6 TFLOP/s); the state pass is "
+                             "v_mfma_f64_16x16x4f64 chains (scripts/probe/mfma_f64_probe.hip: 71-78 TFLOP/s)",
                 "step": {
                     "kernels": list(step_kernels),
                     "ms_per_call": 1e3 * launch_avg_s,

@@ -31,7 +31,7 @@
 #include <cstdlib>
 
 #include "hz_fb_impl.h"
-#include "hz_fft.h"
+#include "hz_fft2k.h"
 
 namespace {
 
@@ -40,12 +40,11 @@ constexpr int kF = 2 * kP;                 // window (samples): real transform l
 constexpr int kLgH = kLgP, kH = kP;        // complex transform length = bins stored per row
 constexpr int kThreads = 256;              // per window / output block
 constexpr int kPT = kH / kThreads;         // complex points per thread (8)
-constexpr int kSplit = (kH / 2 + kThreads) / kThreads;   // bin pairs (k, kH - k), k <= kH / 2, per thread
 constexpr int kMacR = 8;                   // output blocks per MAC thread (partitions padded to it)
 constexpr long kMinCall = 16384;           // shortest call that keeps the history
 // cost model: stationary when N n >= kBandsPerSample (K + n) (hz_fb_tune_response overrides it)
 constexpr long kBandsPerSample = 256;
-static_assert(kPT == 8, "radix-8 passes, one group per thread");
+static_assert(kH == hz2k::kN && kThreads == hz2k::kT, "hz_fft2k.h: 2048 points on 256 threads");
 
 // Aggregate impulse response, one wave (64 bands) per workgroup: part[g][tau] = sum over the
 // group's bands of gin_n r_n[tau], r_n = band n's response to a unit impulse with pre = pin_n,
@@ -105,25 +104,17 @@ __global__ __launch_bounds__(256) void resp_hsum_kernel(const double* __restrict
 
 // ---- real transforms of one window -----------------------------------------------------------
 // A window of F real samples x[m] is the 2048-point complex sequence z[n] = x[2n] + i x[2n+1];
-// with Zh = FFT(z) (hz_fft.h, bit-reversed out), E = (Zh[k] + conj Zh[kH-k]) / 2 and
+// with Zh = FFT(z) (hz_fft2k.h, bit-reversed out), E = (Zh[k] + conj Zh[kH-k]) / 2 and
 // O = (Zh[k] - conj Zh[kH-k]) / 2i are the even and odd samples' spectra and
 //     X[k] = E + W^k O,   X[kH - k] = conj(E - W^k O),   W = e^{-2 pi i / F},
-// one thread per pair (k, kH - k).  Rows hold X_0 .. X_{kH-1} (X_0 real, imaginary part 0);
-// X_kH (real) is kept apart (nyq), so the MAC is one complex product per stored bin.
-struct FftLds {
-    double re[hz::padded_len(kH)], im[hz::padded_len(kH)];
-    double2 T[hz::twc_len(kLgH)];   // W_kH^k, k <= kH / 8 (tw[2k])
-};
-
-__device__ __forceinline__ void load_tw_compact(double2* T, const double2* __restrict__ tw) {
-    for (int k = threadIdx.x; k < hz::twc_len(kLgH); k += kThreads) T[k] = tw[2 * k];
-}
-
+// one thread per pair (k, kH - k), k = t + 256 i (k = 0 pairs with itself: X_0 and X_kH; thread
+// 0 also takes k = kH / 2).  Rows hold X_0 .. X_{kH-1} (X_0 real, imaginary part 0); X_kH (real)
+// is kept apart (nyq), so the MAC is one complex product per stored bin.
 template <class Load>
-__device__ __forceinline__ void real_window_fwd(FftLds& s, Load load, const double2* __restrict__ tw,
+__device__ __forceinline__ void real_window_fwd(hz2k::Lds& s, Load load, const double2* __restrict__ tw,
                                                 double2* __restrict__ zrow, double* __restrict__ nyq) {
     const int t = threadIdx.x;
-    // every global load of the thread before the first LDS store
+    // every global load of the thread (data, pass twiddles, split twiddles) before the first use
     double vr[kPT], vi[kPT];
 #pragma unroll
     for (int i = 0; i < kPT; ++i) {
@@ -131,38 +122,27 @@ __device__ __forceinline__ void real_window_fwd(FftLds& s, Load load, const doub
         vr[i] = load(2 * n);
         vi[i] = load(2 * n + 1);
     }
-    double2 w[kSplit];
+    hz2k::FwdTw ft;
+    ft.load(tw);
+    double2 w[4];
 #pragma unroll
-    for (int i = 0; i < kSplit; ++i) {
-        const int k = t + i * kThreads;
-        w[i] = k <= kH / 2 ? tw[k] : make_double2(1.0, 0.0);
-    }
-    load_tw_compact(s.T, tw);
+    for (int i = 0; i < 4; ++i) w[i] = tw[t + i * kThreads];
+    hz2k::fwd(s, vr, vi, ft);   // ends with a barrier
 #pragma unroll
-    for (int i = 0; i < kPT; ++i) {
-        const int e = hz::pad16(t + i * kThreads);
-        s.re[e] = vr[i];
-        s.im[e] = vi[i];
-    }
-    __syncthreads();
-    hz::fft_fwd_lead<3>(s.re, s.im, kLgH, s.T, true);   // ends with a barrier
-#pragma unroll
-    for (int i = 0; i < kSplit; ++i) {
-        const int k = t + i * kThreads;
-        if (k > kH / 2) break;
-        if (k == 0) {   // E_0 = Re Zh_0, O_0 = Im Zh_0: X_0 = E + O, X_kH = E - O
-            const double zr = s.re[0], zi = s.im[0];
-            zrow[0] = make_double2(zr + zi, 0.0);
-            *nyq = zr - zi;
-            continue;
-        }
-        const int pa = hz::pad16(hz::bitrev(k, kLgH)), pb = hz::pad16(hz::bitrev(kH - k, kLgH));
+    for (int i = 0; i < 4; ++i) {
+        const int k = t + i * kThreads, kb = (kH - k) & (kH - 1);
+        const int pa = hz::pad16(hz::bitrev(k, kLgH)), pb = hz::pad16(hz::bitrev(kb, kLgH));
         const double ar = s.re[pa], ai = s.im[pa], br = s.re[pb], bi = s.im[pb];
         const double er = 0.5 * (ar + br), ei = 0.5 * (ai - bi);
         const double orr = 0.5 * (ai + bi), oi = -0.5 * (ar - br);
         const double wr = w[i].x * orr - w[i].y * oi, wi = w[i].x * oi + w[i].y * orr;
         zrow[k] = make_double2(er + wr, ei + wi);
-        if (k != kH / 2) zrow[kH - k] = make_double2(er - wr, wi - ei);
+        if (k) zrow[kb] = make_double2(er - wr, wi - ei);
+        else *nyq = er - wr;   // X_kH
+    }
+    if (t == 0) {   // X_{kH/2} = conj Zh[kH/2] (bit-reversed position 1)
+        const int pm = hz::pad16(1);
+        zrow[kH / 2] = make_double2(s.re[pm], -s.im[pm]);
     }
 }
 
@@ -171,7 +151,7 @@ __device__ __forceinline__ void real_window_fwd(FftLds& s, Load load, const doub
 __global__ __launch_bounds__(kThreads) void resp_hspec_kernel(const double* __restrict__ h, long K,
                                                              const double2* __restrict__ tw, double2* __restrict__ H,
                                                              double* __restrict__ Hn) {
-    __shared__ FftLds s;
+    __shared__ hz2k::Lds s;
     const long p0 = (long)blockIdx.x * kP;
     real_window_fwd(
         s, [&](int m) { return (m < kP && p0 + m < K) ? h[p0 + m] * (1.0 / kF) : 0.0; }, tw,
@@ -210,7 +190,7 @@ __device__ __forceinline__ double resp_u(const RespArgs& a, long m) {
 
 // Z_j = the spectrum of W_j = u[jP, jP + F)
 __global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a) {
-    __shared__ FftLds s;
+    __shared__ hz2k::Lds s;
     const long m0 = (long)blockIdx.x * kP;
     real_window_fwd(
         s, [&](int m) { return resp_u(a, m0 + m); }, a.tw, a.Z + (long)blockIdx.x * kH, a.Zn + blockIdx.x);
@@ -219,9 +199,11 @@ __global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a) {
 // Y_b[q] = sum_{p < Q} H_p[q] Z_{b+Q-1-p}[q] for b in [b0, b0 + R): thread = bin q x R output
 // blocks.  The R Z values of step p sit in a register ring (element r in slot (r - p) mod R): each
 // step brings one new Z value and one H value for R complex MACs.  Partitions are padded to a
-// multiple of R with zero spectra (Qp), so every block of R steps loads unguarded, and the next
-// block's 2R loads are issued before this block's MACs (latency once per call, not per step).
-template <int R>
+// multiple of R with zero spectra (Qp), so every block of R steps loads unguarded.
+// QP > 0 (Qp == QP, a compile-time count): every H and Z operand of the thread is loaded before
+// the first MAC -- one memory latency per launch (a lone workgroup per CU hides none of it);
+// QP == 0: any Qp, the next block's 2R loads issued before this block's MACs.
+template <int R, int QP>
 __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict__ H, const double2* __restrict__ Z,
                                                        double2* __restrict__ Y, int Q, int Qp, int B) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;   // bin (grid.x = kH / 256)
@@ -235,38 +217,53 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
         zr[r] = z.x;
         zi[r] = z.y;
     }
-    double2 hb[R], zb[R];
-    auto fetch = [&](int p0) {
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-            hb[u] = H[(long)(p0 + u) * kH + q];
-            const long zi_ = base - (p0 + u) - 1;   // < 0 only past Q (zero H rows)
-            zb[u] = Z[(zi_ > 0 ? zi_ : 0) * kH + q];
-        }
+    auto zrow = [&](int p) {   // Z row of step p + 1's new element; < 0 only past Q (zero H rows)
+        const long zi_ = base - p - 1;
+        return (zi_ > 0 ? zi_ : 0) * kH + q;
     };
-    fetch(0);
-    for (int p0 = 0; p0 < Qp; p0 += R) {
-        double2 hc[R], zc[R];
+    auto step = [&](int u, const double2& hc, const double2& zc) {
 #pragma unroll
-        for (int u = 0; u < R; ++u) {
-            hc[u] = hb[u];
-            zc[u] = zb[u];
+        for (int r = 0; r < R; ++r) {
+            const int sl = ((r - u) % R + R) % R;
+            ar[r] = fma(hc.x, zr[sl], ar[r]);
+            ar[r] = fma(-hc.y, zi[sl], ar[r]);
+            ai[r] = fma(hc.x, zi[sl], ai[r]);
+            ai[r] = fma(hc.y, zr[sl], ai[r]);
         }
-        if (p0 + R < Qp) fetch(p0 + R);
+        // element 0 of step p + 1 = Z[base - p - 1] into the slot element R - 1 leaves
+        const int sl = ((-(u + 1)) % R + R) % R;
+        zr[sl] = zc.x;
+        zi[sl] = zc.y;
+    };
+    if constexpr (QP > 0) {
+        double2 hv[QP], zv[QP];
 #pragma unroll
-        for (int u = 0; u < R; ++u) {
+        for (int p = 0; p < QP; ++p) {
+            hv[p] = H[(long)p * kH + q];
+            zv[p] = Z[zrow(p)];
+        }
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int sl = ((r - u) % R + R) % R;
-                ar[r] = fma(hc[u].x, zr[sl], ar[r]);
-                ar[r] = fma(-hc[u].y, zi[sl], ar[r]);
-                ai[r] = fma(hc[u].x, zi[sl], ai[r]);
-                ai[r] = fma(hc[u].y, zr[sl], ai[r]);
+        for (int p = 0; p < QP; ++p) step(p % R, hv[p], zv[p]);
+    } else {
+        double2 hb[R], zb[R];
+        auto fetch = [&](int p0) {
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                hb[u] = H[(long)(p0 + u) * kH + q];
+                zb[u] = Z[zrow(p0 + u)];
             }
-            // element 0 of step p + 1 = Z[base - p - 1] into the slot element R - 1 leaves
-            const int sl = ((-(u + 1)) % R + R) % R;
-            zr[sl] = zc[u].x;
-            zi[sl] = zc[u].y;
+        };
+        fetch(0);
+        for (int p0 = 0; p0 < Qp; p0 += R) {
+            double2 hc[R], zc[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                hc[u] = hb[u];
+                zc[u] = zb[u];
+            }
+            if (p0 + R < Qp) fetch(p0 + R);
+#pragma unroll
+            for (int u = 0; u < R; ++u) step(u, hc[u], zc[u]);
         }
     }
 #pragma unroll
@@ -274,24 +271,36 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
         if (b0 + r < B) Y[(long)(b0 + r) * kH + q] = make_double2(ar[r], ai[r]);
 }
 
+typedef void (*MacKernel)(const double2*, const double2*, double2*, int, int, int);
+MacKernel pick_mac(int Qp) {
+    switch (Qp) {
+    case 8: return resp_mac_kernel<kMacR, 8>;
+    case 16: return resp_mac_kernel<kMacR, 16>;
+    case 24: return resp_mac_kernel<kMacR, 24>;
+    default: return resp_mac_kernel<kMacR, 0>;
+    }
+}
+
 // output block b: the merge of Y_b into Zh' = E' + i O' (E' = Y[k] + conj Y[kH-k],
-// O' = (Y[k] - conj Y[kH-k]) W^-k), the inverse 2048-point FFT, out[bP + 2r (+1)] = Re (Im)
-// z[kH/2 + r] (the last P samples of the window's circular convolution)
+// O' = (Y[k] - conj Y[kH-k]) W^-k; Zh'[kH-k] = conj E' + i conj O'), the inverse 2048-point FFT,
+// out[bP + 2r (+1)] = Re (Im) z[kH/2 + r] (the last P samples of the window's circular
+// convolution) straight from the last pass's registers
 __global__ __launch_bounds__(kThreads) void resp_inv_kernel(RespArgs a) {
-    __shared__ FftLds s;
+    __shared__ hz2k::Lds s;
     const int t = threadIdx.x;
     const long b = blockIdx.x;
     const double2* y = a.Y + b * kH;
-    double2 ya[kSplit], yb[kSplit], w[kSplit];
+    double2 ya[4], yb[4], w[4];
 #pragma unroll
-    for (int i = 0; i < kSplit; ++i) {
+    for (int i = 0; i < 4; ++i) {
         const int k = t + i * kThreads;
-        const bool on = k <= kH / 2;
-        ya[i] = on ? y[k] : make_double2(0.0, 0.0);
-        yb[i] = on && k ? y[kH - k] : make_double2(0.0, 0.0);
-        w[i] = on ? a.tw[k] : make_double2(1.0, 0.0);
+        ya[i] = y[k];
+        yb[i] = y[(kH - k) & (kH - 1)];   // k = 0: replaced by (Y_kH, 0) below
+        w[i] = a.tw[k];
     }
-    load_tw_compact(s.T, a.tw);
+    const double2 ym = y[kH / 2];
+    hz2k::InvTw it;
+    it.load(a.tw);
     // bin kH (real): sum_p Hn[p] Zn[b + Q - 1 - p], wave 0 in a fixed order
     double yn = 0.0;
     if (t < 64) {
@@ -299,33 +308,33 @@ __global__ __launch_bounds__(kThreads) void resp_inv_kernel(RespArgs a) {
 #pragma unroll
         for (int o = 32; o; o >>= 1) yn += __shfl_xor(yn, o);
     }
+    if (t == 0) yb[0] = make_double2(yn, 0.0);
 #pragma unroll
-    for (int i = 0; i < kSplit; ++i) {
-        const int k = t + i * kThreads;
-        if (k > kH / 2) break;
-        if (k == 0) {
-            s.re[0] = ya[i].x + yn;
-            s.im[0] = ya[i].x - yn;
-            continue;
-        }
+    for (int i = 0; i < 4; ++i) {
+        const int k = t + i * kThreads, kb = (kH - k) & (kH - 1);
         const double er = ya[i].x + yb[i].x, ei = ya[i].y - yb[i].y;
         const double dr = ya[i].x - yb[i].x, di = ya[i].y + yb[i].y;
         const double orr = dr * w[i].x + di * w[i].y, oi = di * w[i].x - dr * w[i].y;
-        const int pa = hz::pad16(hz::bitrev(k, kLgH)), pb = hz::pad16(hz::bitrev(kH - k, kLgH));
+        const int pa = hz::pad16(hz::bitrev(k, kLgH)), pb = hz::pad16(hz::bitrev(kb, kLgH));
         s.re[pa] = er - oi;
         s.im[pa] = ei + orr;
-        if (k != kH / 2) {
+        if (k) {
             s.re[pb] = er + oi;
             s.im[pb] = orr - ei;
         }
     }
-    __syncthreads();
-    hz::fft_inv_tail<3>(s.re, s.im, kLgH, s.T, true);
-    for (int r = t; r < kH / 2; r += kThreads) {
-        const long t0 = b * kP + 2 * r;
-        const double v0 = s.re[hz::pad16(kH / 2 + r)], v1 = s.im[hz::pad16(kH / 2 + r)];
-        if (t0 < a.n_out) a.out[a.off + t0] = v0;
-        if (t0 + 1 < a.n_out) a.out[a.off + t0 + 1] = v1;
+    if (t == 0) {   // Zh'[kH/2] = 2 conj Y[kH/2] (bit-reversed position 1)
+        s.re[hz::pad16(1)] = 2.0 * ym.x;
+        s.im[hz::pad16(1)] = -2.0 * ym.y;
+    }
+    double vr[kPT], vi[kPT];
+    hz2k::inv(s, vr, vi, it);
+    // z[kH/2 + r], r = t + 256 (i - 4): output samples bP + 2r, bP + 2r + 1
+#pragma unroll
+    for (int i = kPT / 2; i < kPT; ++i) {
+        const long t0 = b * kP + 2 * (t + (long)(i - kPT / 2) * kThreads);
+        if (t0 < a.n_out) a.out[a.off + t0] = vr[i];
+        if (t0 + 1 < a.n_out) a.out[a.off + t0 + 1] = vi[i];
     }
     // state upkeep (the forward kernel, the last reader of hist, has finished)
     const long g = b * blockDim.x + t, stride = (long)gridDim.x * blockDim.x;
@@ -587,7 +596,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.O = h->order;
     hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
-    hipLaunchKernelGGL(resp_mac_kernel<kMacR>, dim3(kH / 256, (unsigned)((B + kMacR - 1) / kMacR)), dim3(256), 0,
+    hipLaunchKernelGGL(pick_mac(Qp), dim3(kH / 256, (unsigned)((B + kMacR - 1) / kMacR)), dim3(256), 0,
                        h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B);
     HZ_TRY_HIP(hipGetLastError());
     hipLaunchKernelGGL(resp_inv_kernel, dim3((unsigned)B), dim3(kThreads), 0, h->stream, a);
