@@ -170,6 +170,10 @@ struct hz_fb {
         double* d_Y = nullptr;           // [B][2048] complex output spectra
         size_t Y_cap = 0;
         double* d_tw = nullptr;          // W_4096^k, k < 2048 (complex)
+        double* d_sop = nullptr;         // band-state pass: pin E operands (fb_state_prepare)
+        size_t sop_cap = 0;
+        hipStream_t side = nullptr;      // the band-state pass beside the convolution (calls n >= K)
+        hipEvent_t ev_fork = nullptr, ev_join = nullptr;
         double* d_spart = nullptr;       // band-state pass: segment partials, arrival counters
         size_t spart_cap = 0;
         unsigned* d_scount = nullptr;
@@ -224,6 +228,7 @@ long fb_horizon(const hz_fb* h, int log2_bound);   // samples K with ||M^K|| < 2
 // zero-start band states after the window x[0, len) (len a multiple of 8192) -> out[band][O], on
 // stream st: the stationary engine's band-state pass (hz_fb_state.hip)
 int fb_state_window(hz_fb* h, const double* x, long len, double* out, hipStream_t st);
+int fb_state_prepare(hz_fb* h);   // its records and pin E operands (current coefficients, pin), on h->stream
 int fb_lti_prepare_end(hz_fb* h, long len);   // its records for the current coefficients
 // hz_fb_resp.hip (stationary engine)
 void fb_resp_init(hz_fb* h);

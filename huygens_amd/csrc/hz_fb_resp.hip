@@ -44,6 +44,10 @@ constexpr int kMacR = 8;                   // output blocks per MAC thread (part
 constexpr long kMinCall = 16384;           // shortest call that keeps the history
 // cost model: stationary when N n >= kBandsPerSample (K + n) (hz_fb_tune_response overrides it)
 constexpr long kBandsPerSample = 256;
+// the band-state pass on a side stream beside the transforms (calls n >= K).  Measured at C2:
+// 0.0593 ms per step against 0.0524 serial -- the state kernel's 272 VGPRs per wave leave no room
+// for the MAC kernel's waves on a CU, so the two serialise with worse placement (r3k)
+constexpr bool kStatesBeside = false;
 static_assert(kH == hz2k::kN && kThreads == hz2k::kT, "hz_fft2k.h: 2048 points on 256 threads");
 
 // Aggregate impulse response, one wave (64 bands) per workgroup: part[g][tau] = sum over the
@@ -443,7 +447,7 @@ int resp_build_h(hz_fb* h) {
     hipLaunchKernelGGL(resp_hspec_kernel, dim3((unsigned)Q), dim3(kThreads), 0, h->stream, (const double*)R.d_h, K,
                        (const double2*)R.d_tw, (double2*)R.d_H, R.d_H + (size_t)Qp * 2 * kH);
     HZ_TRY_HIP(hipGetLastError());
-    HZ_TRY(hz_fbi::fb_lti_prepare_end(h, K));   // the state kernel's records, for LAZY too
+    HZ_TRY(hz_fbi::fb_state_prepare(h));   // the state pass's records and operands, for LAZY too
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));   // pageable coefficient sources
     R.h_valid = true;
     return HZ_OK;
@@ -567,7 +571,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     if (h->prof) {
         HZ_TRY(fb_prof_events(h, &e));
         HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
-        h->ev_skip[(e - h->ev.data()) / 5] |= 2 | 8;   // no segment phase; reduce start = mix end
+        h->ev_skip[(e - h->ev.data()) / 5] |= 2;   // no segment phase
     }
     RespArgs a;
     a.hist = R.d_hist[R.hcur];
@@ -594,6 +598,24 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.xhist_next = h->d_xhist[h->xcur ^ 1];
     a.N = h->N;
     a.O = h->order;
+    // EAGER, n >= K: the band states after the call are the zero-start states over the call's last
+    // K samples, independent of the convolution -- the state pass (FP64 matrix cores) runs on a
+    // side stream beside the transforms (latency-bound, no MFMA), joined before the call returns
+    const bool lazy = R.mode == HZ_FB_RESP_LAZY;
+    const bool beside = kStatesBeside && !lazy && n >= K;
+    if (beside) {
+        if (!R.side) {
+            HZ_TRY_HIP(hipStreamCreateWithFlags(&R.side, hipStreamNonBlocking));
+            HZ_TRY_HIP(hipEventCreateWithFlags(&R.ev_fork, hipEventDisableTiming));
+            HZ_TRY_HIP(hipEventCreateWithFlags(&R.ev_join, hipEventDisableTiming));
+        }
+        HZ_TRY_HIP(hipEventRecord(R.ev_fork, h->stream));
+        HZ_TRY_HIP(hipStreamWaitEvent(R.side, R.ev_fork, 0));
+        if (e) HZ_TRY_HIP(hipEventRecord(e[3], R.side));
+        HZ_TRY(fb_state_window(h, d_in + (n - K), K, h->d_ystate[h->scur ^ 1], R.side));
+        if (e) HZ_TRY_HIP(hipEventRecord(e[4], R.side));
+        HZ_TRY_HIP(hipEventRecord(R.ev_join, R.side));
+    }
     hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     hipLaunchKernelGGL(pick_mac(Qp), dim3(kH / 256, (unsigned)((B + kMacR - 1) / kMacR)), dim3(256), 0,
@@ -604,15 +626,23 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     R.hcur ^= 1;   // the inverse kernel wrote the history after the call
     R.run = std::min(R.run + n, 1L << 60);
-    // end state: the band states over the new history now (EAGER) or when needed (LAZY); the
-    // smoothers and x history were written by the inverse kernel
-    if (R.mode == HZ_FB_RESP_LAZY) {
+    // end state: the band states over the new history now (EAGER: joined from the side stream,
+    // or after the transforms when n < K) or when needed (LAZY); the smoothers and x history were
+    // written by the inverse kernel
+    // (profiling events 3 / 4 bracket the state pass on the stream it runs on)
+    if (lazy) {
         R.implicit = true;
+        if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
+        if (e) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
+    } else if (beside) {
+        HZ_TRY_HIP(hipStreamWaitEvent(h->stream, R.ev_join, 0));
+        R.implicit = false;
     } else {
+        if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
         HZ_TRY(resp_states(h, h->d_ystate[h->scur ^ 1]));
+        if (e) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
         R.implicit = false;
     }
-    if (e) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
     h->scur ^= 1;
     h->xcur ^= 1;
     h->prof_launches += h->prof ? 1 : 0;
@@ -623,9 +653,13 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
 
 void fb_resp_free(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
+    if (R.side) (void)hipStreamSynchronize(R.side);
     for (double* p : {R.d_hist[0], R.d_hist[1], R.d_h, R.d_hpart, R.d_coef, R.d_zero, R.d_H, R.d_Z, R.d_Y, R.d_tw,
-                      R.d_spart})
+                      R.d_spart, R.d_sop})
         if (p) (void)hipFree(p);
+    if (R.ev_fork) (void)hipEventDestroy(R.ev_fork);
+    if (R.ev_join) (void)hipEventDestroy(R.ev_join);
+    if (R.side) (void)hipStreamDestroy(R.side);
     if (R.d_scount) (void)hipFree(R.d_scount);
     R = hz_fb::Resp();
 }

@@ -75,7 +75,7 @@ __device__ __forceinline__ double mix_cols(const double* w, double v) {
 struct StateArgs {
     const double* rec;     // chunk-128 records [N][rs]
     int rs;                // record size (doubles)
-    const double* pin;     // [N]
+    const double* eop;     // [G][2][KE][64] pin E operands (fb_state_ops_kernel)
     const double* x;       // [len] the window
     long len;
     int nbands;
@@ -87,48 +87,40 @@ struct StateArgs {
 };
 
 template <int O>
-__global__ __launch_bounds__(256) void fb_state_kernel(StateArgs a) {
+__global__ __launch_bounds__(512) void fb_state_kernel(StateArgs a) {
     using R = RecL<O, kL>;
     using Gm = StateGeom<O>;
-    constexpr int OP = Gm::OP, KE = Gm::KE, XW = Gm::XW;
+    constexpr int OP = Gm::OP, KE = Gm::KE;
     const int lane = threadIdx.x & 63;
-    const int m = threadIdx.x >> 6;            // chunk rows 16m .. 16m + 15 of every tile
+    const int w = threadIdx.x >> 6;
+    const int m = w & 3;                       // chunk rows 16m .. 16m + 15 of every tile
+    const int sb = w >> 2;                     // column block 16 sb .. 16 sb + 15
     const int g = blockIdx.x, seg = blockIdx.y;
-    const int col = lane & 15;                 // column within a 16-wide block
+    const int col = lane & 15;                 // column within the block
     const int k = col % OP;                    // state component of the column
-    // this lane's bands in blocks 0 and 1
-    int band[2];
-    bool live[2];
+    const int band = g * Gm::BANDS + (16 * sb + col) / OP;
+    const bool live = band < a.nbands && k < O;
+    // B operands, pin E[tap 4q + (l >> 4)][column] (fb_state_ops_kernel's layout: coalesced)
+    double e[KE];
 #pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-        band[sb] = g * Gm::BANDS + (16 * sb + col) / OP;
-        live[sb] = band[sb] < a.nbands && k < O;
-    }
-    // B operands: pin E[tap 4q + (l >> 4)][column], zero outside the bank / taps / O
-    double e[2][KE];
+    for (int q = 0; q < KE; ++q) e[q] = a.eop[(((long)g * 2 + sb) * KE + q) * 64 + lane];
+    // rows k of the band's M^e (QC[e], e <= 64) as weights of the columns k ^ j: M^64 (the tile
+    // carry), then for the end: M^4 (rows 4 apart in a lane), M^(3 - (l >> 4)) (the lane groups)
+    // and M^(16 (3 - m)) (the row blocks)
+    auto qrow = [&](int ex, double (&wt)[OP]) {
+        const double* rb = a.rec + (long)(live ? band : 0) * a.rs + R::QC + ex * O * O;
 #pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-        const double* rb = a.rec + (long)(live[sb] ? band[sb] : 0) * a.rs;
-        const double p = live[sb] ? a.pin[band[sb]] : 0.0;
-#pragma unroll
-        for (int q = 0; q < KE; ++q) {
-            const int tap = 4 * q + (lane >> 4);
-            double v = 0.0;
-            if (live[sb] && tap < XW) v = tap < O ? rb[R::EH + k * O + tap] : (tap + k < XW ? rb[R::E0 + tap + k] : 0.0);
-            e[sb][q] = p * v;
-        }
-    }
-    // M^64 row k of each band, as weights of the columns k ^ j
-    double m64[2][OP];
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-        const double* rb = a.rec + (long)(live[sb] ? band[sb] : 0) * a.rs + R::QC + 64 * O * O;
-#pragma unroll
-        for (int j = 0; j < OP; ++j) m64[sb][j] = (live[sb] && (k ^ j) < O) ? rb[k * O + (k ^ j)] : 0.0;
-    }
-    // the wave's slab of every tile: x[t0 + it T + 16m L - O + e], e < kSlab (its 16 chunks' taps),
-    // staged global -> registers -> the wave's own LDS slab at pos(e) = e + 2 (e / L) (A reads of 16
-    // chunks x 4 taps hit distinct banks per half-wave); no other wave reads it: no barrier
+        for (int j = 0; j < OP; ++j) wt[j] = (live && (k ^ j) < O) ? rb[k * O + (k ^ j)] : 0.0;
+    };
+    double m64[OP], m4[OP], mg[OP], mw[OP];
+    qrow(64, m64);
+    qrow(4, m4);
+    qrow(3 - (lane >> 4), mg);
+    qrow(16 * (3 - m), mw);
+    // row block m's slab of every tile: x[t0 + it T + 16m L - O + e], e < kSlab (its 16 chunks'
+    // taps), staged global -> registers -> LDS at pos(e) = e + 2 (e / L) (A reads of 16 chunks x
+    // 4 taps hit distinct banks per half-wave); waves m and m + 4 (the two column blocks) share it,
+    // each staging half of it
     const __amdgpu_buffer_rsrc_t xr = [&] {
         const unsigned long long xb = (unsigned long long)a.x;
         const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)xb);
@@ -140,19 +132,21 @@ __global__ __launch_bounds__(256) void fb_state_kernel(StateArgs a) {
     __shared__ double slab_lds[4][kSlabPos];
     double* slab = slab_lds[m];
     const long t0 = (long)seg * a.tps * kTile;
-    const int voff0 = (int)((t0 - O + (long)(16 * m) * kL + lane) * (long)sizeof(double));
-    double st[kStage];
+    constexpr int kHalf = (kStage + 1) / 2;   // staging loads of column block 0's wave (17; block 1: 16)
+    const int i0 = sb * kHalf;
+    const int voff0 = (int)((t0 - O + (long)(16 * m) * kL + lane + 64 * i0) * (long)sizeof(double));
+    double st[kHalf];
     auto load_tile = [&](int it) {
         const int v = voff0 + it * kTile * (int)sizeof(double);
 #pragma unroll
-        for (int i = 0; i < kStage; ++i)
+        for (int i = 0; i < kHalf; ++i)
             st[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, v + 512 * i, 0, 0));
     };
     auto store_tile = [&]() {
 #pragma unroll
-        for (int i = 0; i < kStage; ++i) {
-            const int e = lane + 64 * i;
-            if (i < kStage - 1 || e < kSlab) slab[e + 2 * (e / kL)] = st[i];
+        for (int i = 0; i < kHalf; ++i) {
+            const int e = lane + 64 * (i0 + i);
+            if (e < kSlab) slab[e + 2 * (e / kL)] = st[i];
         }
     };
     // A operand of k-step q: X[chunk c = l & 15][tap t = 4q + (l >> 4)] = slab element 128 c + t
@@ -161,18 +155,15 @@ __global__ __launch_bounds__(256) void fb_state_kernel(StateArgs a) {
         const int t = 4 * q;   // + (l >> 4) < 4: taps 128.. of the last k-step sit after the pad
         return t < kL ? slab[a_pos + t] : slab[a_pos + t + 2];
     };
-    f64x4 acc[2];
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) acc[sb] = f64x4{0.0, 0.0, 0.0, 0.0};
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
     load_tile(0);
     store_tile();
     if (a.tps > 1) load_tile(1);
+    __syncthreads();
     for (int it = 0; it < a.tps; ++it) {
         if (it > 0) {   // acc <- M^64 acc (the previous tiles, one tile further back)
 #pragma unroll
-            for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) acc[sb][rr] = mix_cols<OP>(m64[sb], acc[sb][rr]);
+            for (int rr = 0; rr < 4; ++rr) acc[rr] = mix_cols<OP>(m64, acc[rr]);
         }
         // A operands read EP k-steps ahead of their MFMAs (the LDS latency under the chain; the
         // scheduler would otherwise sink each read to its use)
@@ -186,37 +177,30 @@ __global__ __launch_bounds__(256) void fb_state_kernel(StateArgs a) {
             const double xa = xq[q % EP];
             if (q + EP < KE) xq[q % EP] = a_at(q + EP);
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int sb = 0; sb < 2; ++sb) acc[sb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, e[sb][q], acc[sb], 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, e[q], acc, 0, 0, 0);
         }
-        // the next tile into the slab (the wave's LDS ops run in order: after this tile's reads),
-        // the one after into the staging registers
-        if (it + 1 < a.tps) store_tile();
-        if (it + 2 < a.tps) load_tile(it + 2);
-    }
-    // S = sum_c M^(63-c) A_c: lane rows c = 16m + (l >> 4) + 4 rr
-    double v[2];
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
-        const double* rb = a.rec + (long)(live[sb] ? band[sb] : 0) * a.rs + R::QC;
-        v[sb] = 0.0;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int c = 16 * m + (lane >> 4) + 4 * rr;
-            double w[OP];
-#pragma unroll
-            for (int j = 0; j < OP; ++j) w[j] = (live[sb] && (k ^ j) < O) ? rb[(63 - c) * O * O + k * O + (k ^ j)] : 0.0;
-            v[sb] += mix_cols<OP>(w, acc[sb][rr]);
+        // the next tile into the slab once both waves of the row block have read this one; the
+        // one after into the staging registers
+        if (it + 1 < a.tps) {
+            __syncthreads();
+            store_tile();
+            if (it + 2 < a.tps) load_tile(it + 2);
+            __syncthreads();
         }
-        v[sb] += __shfl_xor(v[sb], 16);
-        v[sb] += __shfl_xor(v[sb], 32);
     }
+    // S = sum_c M^(63-c) A_c, lane rows c = 16m + g + 4 rr (g = l >> 4), by Horner steps: over rr
+    // with M^4 (anchored at row 16m + g + 12), M^(3-g) (row 16m + 15), the sum over g, M^(16(3-m))
+    // (row 63), then the sum over the row blocks
+    double T = acc[0];
+#pragma unroll
+    for (int rr = 1; rr < 4; ++rr) T = mix_cols<OP>(m4, T) + acc[rr];
+    T = mix_cols<OP>(mg, T);
+    T += __shfl_xor(T, 16);
+    T += __shfl_xor(T, 32);
+    const double v = mix_cols<OP>(mw, T);
     __shared__ double red[4][kCols];
     __shared__ int is_last;
-    if (lane < 16) {
-        red[m][lane] = v[0];
-        red[m][16 + lane] = v[1];
-    }
+    if (lane < 16) red[m][16 * sb + lane] = v;
     __syncthreads();
     const int t = threadIdx.x;
     if (t < kCols) {
@@ -226,6 +210,7 @@ __global__ __launch_bounds__(256) void fb_state_kernel(StateArgs a) {
             if (b < a.nbands && kk < O) a.out[(long)b * O + kk] = S;
         } else {
             a.part[((long)g * a.nseg + seg) * kCols + t] = S;
+            __threadfence();   // the partial visible at agent scope before the arrival below
         }
     }
     if (a.nseg == 1) return;
@@ -288,6 +273,42 @@ __global__ __launch_bounds__(256) void fb_state_kernel(StateArgs a) {
     if (t == 0) __hip_atomic_store(a.count + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// pin E in the state kernel's B-operand order, eop[((g 2 + sb) KE + q) 64 + lane] =
+// pin E[tap 4q + (lane >> 4)][column 16 sb + (lane & 15)] of band group g (zero outside the bank,
+// the taps and O): one coalesced load per operand instead of 8 records per load
+template <int O>
+__global__ __launch_bounds__(256) void fb_state_ops_kernel(const double* __restrict__ rec, int rs,
+                                                           const double* __restrict__ pin, int nbands, int G,
+                                                           double* __restrict__ eop) {
+    using R = RecL<O, kL>;
+    using Gm = StateGeom<O>;
+    constexpr int OP = Gm::OP, KE = Gm::KE, XW = Gm::XW;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)G * 2 * KE * 64) return;
+    const int lane = (int)(i & 63), q = (int)((i >> 6) % KE), sb = (int)((i / (64 * KE)) % 2);
+    const int g = (int)(i / (128L * KE));
+    const int col = lane & 15, k = col % OP, tap = 4 * q + (lane >> 4);
+    const int band = g * Gm::BANDS + (16 * sb + col) / OP;
+    double v = 0.0;
+    if (band < nbands && k < O && tap < XW) {
+        const double* rb = rec + (long)band * rs;
+        v = pin[band] * (tap < O ? rb[R::EH + k * O + tap] : (tap + k < XW ? rb[R::E0 + tap + k] : 0.0));
+    }
+    eop[i] = v;
+}
+
+typedef void (*StateOpsKernel)(const double*, int, const double*, int, int, double*);
+StateOpsKernel pick_state_ops(int O) {
+    switch (O) {
+    case 1: return fb_state_ops_kernel<1>;
+    case 2: return fb_state_ops_kernel<2>;
+    case 3: return fb_state_ops_kernel<3>;
+    default: return fb_state_ops_kernel<4>;
+    }
+}
+
+int state_ke(int O) { return (kL + O + 3) / 4; }
+
 typedef void (*StateKernel)(StateArgs);
 StateKernel pick_state(int O) {
     switch (O) {
@@ -304,13 +325,34 @@ int bands_per_group(int O) { return kCols / (O == 3 ? 4 : O); }
 
 namespace hz_fbi {
 
+// the records and the pin E operands for the current coefficients and pre-amp targets, on h->stream
+int fb_state_prepare(hz_fb* h) {
+    const int O = h->order;
+    HZ_TRY(fb_lti_prepare_end(h, kTile));   // the chunk-128 records
+    hz_fb::LtiRecSet& set = h->lti_set[kLtiGeomChunk128];
+    hz_fb::Resp& R = h->resp;
+    const int G = (h->N + bands_per_group(O) - 1) / bands_per_group(O);
+    const size_t need = (size_t)G * 2 * state_ke(O) * 64;
+    if (need > R.sop_cap) {
+        HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+        if (R.d_sop) HZ_TRY_HIP(hipFree(R.d_sop));
+        R.d_sop = nullptr;
+        HZ_TRY_HIP(hipMalloc(&R.d_sop, sizeof(double) * need));
+        R.sop_cap = need;
+    }
+    hipLaunchKernelGGL(pick_state_ops(O), dim3((unsigned)((need + 255) / 256)), dim3(256), 0, h->stream,
+                       (const double*)set.d_rec, set.rs, (const double*)h->d_pin, h->N, G, R.d_sop);
+    HZ_TRY_HIP(hipGetLastError());
+    return HZ_OK;
+}
+
 int fb_state_window(hz_fb* h, const double* x, long len, double* out, hipStream_t st) {
     const int O = h->order;
-    if (O == 0 || len <= 0 || len % kTile != 0 || len > (1L << 27)) {
-        hz::set_error("fb_state_window: order %d, window %ld (a positive multiple of 8192)", O, len);
+    if (O == 0 || len <= 0 || len % kTile != 0 || len > (1L << 27) || !h->resp.d_sop) {
+        hz::set_error("fb_state_window: order %d, window %ld (a positive multiple of 8192), operands %s", O, len,
+                      h->resp.d_sop ? "ready" : "missing");
         return HZ_E_INVALID;
     }
-    HZ_TRY(fb_lti_prepare_end(h, len));   // the chunk-128 records
     hz_fb::LtiRecSet& set = h->lti_set[kLtiGeomChunk128];
     const int G = (h->N + bands_per_group(O) - 1) / bands_per_group(O);
     const int ntiles = (int)(len / kTile);
@@ -340,7 +382,7 @@ int fb_state_window(hz_fb* h, const double* x, long len, double* out, hipStream_
     StateArgs a;
     a.rec = set.d_rec;
     a.rs = set.rs;
-    a.pin = h->d_pin;
+    a.eop = R.d_sop;
     a.x = x;
     a.len = len;
     a.nbands = h->N;
@@ -349,7 +391,7 @@ int fb_state_window(hz_fb* h, const double* x, long len, double* out, hipStream_
     a.part = R.d_spart;
     a.count = R.d_scount;
     a.out = out;
-    hipLaunchKernelGGL(pick_state(O), dim3((unsigned)G, (unsigned)nseg), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(pick_state(O), dim3((unsigned)G, (unsigned)nseg), dim3(512), 0, st, a);
     HZ_TRY_HIP(hipGetLastError());
     return HZ_OK;
 }

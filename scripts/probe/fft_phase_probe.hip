@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "hz_fft.h"
+#include "hz_fft2k.h"
 
 constexpr int kLgH = 11, kH = 1 << kLgH, kP = kH, kThreads = 256, kPT = kH / kThreads;
 constexpr int kSplit = (kH / 2 + kThreads) / kThreads;
@@ -98,6 +99,85 @@ __global__ __launch_bounds__(kThreads) void fwd_probe(const double* __restrict__
         for (int i = 0; i < kStamps; ++i) st[(long)blockIdx.x * kStamps + i] = i < ns ? ts[i] : 0;
 }
 
+// the shipped forward path (hz_fft2k.h + the split of hz_fb_resp.hip's real_window_fwd), stamped:
+// 0 start, 1 loads landed + P1 (registers) + LDS store, 2 barrier, 3-5 LDS passes, 6 split issued,
+// 7 stores acknowledged
+__global__ __launch_bounds__(kThreads) void fwd2k_probe(const double* __restrict__ u, const double2* __restrict__ tw,
+                                                       double2* __restrict__ Z, double* __restrict__ Zn,
+                                                       long long* __restrict__ st) {
+    __shared__ hz2k::Lds s;
+    long long ts[kStamps];
+    int ns = 0;
+    ts[ns++] = stamp();
+    const int t = threadIdx.x;
+    const long m0 = (long)blockIdx.x * kP;
+    double vr[kPT], vi[kPT];
+#pragma unroll
+    for (int i = 0; i < kPT; ++i) {
+        const int n = t + i * kThreads;
+        vr[i] = u[m0 + 2 * n];
+        vi[i] = u[m0 + 2 * n + 1];
+    }
+    hz2k::FwdTw ft;
+    ft.load(tw);
+    double2 w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = tw[t + i * kThreads];
+    // hz2k::fwd, stamped
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        double xr[4], xi[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            xr[j] = vr[g + 2 * j];
+            xi[j] = vi[g + 2 * j];
+        }
+        hz2k::Dif<2, 10>::regs(xr, xi, ft.p1[g]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            vr[g + 2 * j] = xr[j];
+            vi[g + 2 * j] = xi[j];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kPT; ++i) {
+        const int e = hz::pad16(t + kThreads * i);
+        s.re[e] = vr[i];
+        s.im[e] = vi[i];
+    }
+    ts[ns++] = stamp();
+    __syncthreads();
+    ts[ns++] = stamp();
+    hz2k::Dif<3, 8>::lds(s, t, ft.p2);
+    __syncthreads();
+    ts[ns++] = stamp();
+    hz2k::Dif<3, 5>::lds(s, t, ft.p3);
+    __syncthreads();
+    ts[ns++] = stamp();
+    const double2 one[3] = {make_double2(1.0, 0.0), make_double2(1.0, 0.0), make_double2(1.0, 0.0)};
+    hz2k::Dif<3, 2>::lds(s, t, one);
+    __syncthreads();
+    ts[ns++] = stamp();
+    double2* zrow = Z + (long)blockIdx.x * kH;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int k = t + i * kThreads, kb = (kH - k) & (kH - 1);
+        const int pa = hz::pad16(hz::bitrev(k, kLgH)), pb = hz::pad16(hz::bitrev(kb, kLgH));
+        const double ar = s.re[pa], ai = s.im[pa], br = s.re[pb], bi = s.im[pb];
+        const double er = 0.5 * (ar + br), ei = 0.5 * (ai - bi);
+        const double orr = 0.5 * (ai + bi), oi = -0.5 * (ar - br);
+        const double wr = w[i].x * orr - w[i].y * oi, wi = w[i].x * oi + w[i].y * orr;
+        zrow[k] = make_double2(er + wr, ei + wi);
+        if (k) zrow[kb] = make_double2(er - wr, wi - ei);
+        else Zn[blockIdx.x] = er - wr;
+    }
+    ts[ns++] = stamp();
+    __builtin_amdgcn_s_waitcnt(0);
+    ts[ns++] = stamp();
+    if (t == 0)
+        for (int i = 0; i < kStamps; ++i) st[(long)blockIdx.x * kStamps + i] = i < ns ? ts[i] : 0;
+}
+
 int main() {
     const int maxw = 258;
     const long nu = (long)(maxw + 1) * kP;
@@ -119,9 +199,9 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    for (int mode = 0; mode < 2; ++mode)
+    for (int mode = 0; mode < 3; ++mode)
         for (int wg : {24, 258}) {
-            auto k = mode == 0 ? fwd_probe<0> : fwd_probe<1>;
+            auto k = mode == 0 ? fwd_probe<0> : mode == 1 ? fwd_probe<1> : fwd2k_probe;
             for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(k, dim3(wg), dim3(kThreads), 0, 0, u, tw, Z, Zn, st);
             hipEventRecord(e0);
             hipLaunchKernelGGL(k, dim3(wg), dim3(kThreads), 0, 0, u, tw, Z, Zn, st);
@@ -131,7 +211,7 @@ int main() {
             hipEventElapsedTime(&ms, e0, e1);
             std::vector<long long> hs((long)wg * kStamps);
             hipMemcpy(hs.data(), st, hs.size() * sizeof(long long), hipMemcpyDeviceToHost);
-            const int nst = mode == 0 ? 9 : 5;
+            const int nst = mode == 0 ? 9 : mode == 1 ? 5 : 8;
             std::vector<double> avg(nst, 0.0);
             long long first = hs[0], lastend = 0;
             for (int b = 0; b < wg; ++b) {
@@ -140,7 +220,7 @@ int main() {
                 lastend = std::max(lastend, hs[b * kStamps + nst - 1]);
             }
             std::printf("mode %d (%s), %3d workgroups: event %.2f us; span first start -> last end %.0f ticks; "
-                        "per-WG phase ticks (s_memtime):", mode, mode ? "no FFT" : "full", wg, 1e3 * ms,
+                        "per-WG phase ticks (s_memtime):", mode, mode == 2 ? "hz_fft2k" : mode ? "no FFT" : "full", wg, 1e3 * ms,
                         (double)(lastend - first));
             for (int i = 1; i < nst; ++i) std::printf(" %.0f", avg[i]);
             std::printf("\n");

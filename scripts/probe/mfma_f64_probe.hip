@@ -11,7 +11,10 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 template <int CH>
 __global__ void chain_kernel(const double* __restrict__ in, double* __restrict__ out, int iters) {
     const int lane = threadIdx.x & 63;
-    double a = in[lane], b = in[64 + lane];
+    // operands differ per wave and lane (random-looking data: the clock the chip holds under an
+    // FP64 MFMA load depends on the operand bits)
+    const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    double a = in[(lane + 7 * wv) & 127], b = in[(64 + lane + 13 * wv) & 127];
     f64x4 acc[CH];
 #pragma unroll
     for (int c = 0; c < CH; ++c) acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
@@ -69,12 +72,20 @@ static void run(const char* name, K k, int waves_per_cu, int ch, bool mfma, doub
                 (ms * 1e-3 * 2.4e9) / (ops / (256.0 * 4)));
 }
 
-int main() {
+int main(int argc, char**) {
     double *din, *dout;
     hipMalloc(&din, 128 * sizeof(double));
     hipMalloc(&dout, 1 << 24);
     double h[128];
-    for (int i = 0; i < 128; ++i) h[i] = 1.0 + 1e-9 * i;
+    const bool rnd = argc > 1;   // any argument: random operands in [-1, 1)
+    unsigned long long z = 88172645463325252ull;
+    for (int i = 0; i < 128; ++i) {
+        z ^= z << 13;
+        z ^= z >> 7;
+        z ^= z << 17;
+        h[i] = rnd ? (double)(z >> 11) * 0x1p-52 - 1.0 : 1.0 + 1e-9 * i;
+    }
+    std::printf("operands: %s\n", rnd ? "random [-1, 1)" : "1 + 1e-9 i");
     hipMemcpy(din, h, sizeof(h), hipMemcpyHostToDevice);
     for (int w : {4, 8, 16}) {
         run("mfma", chain_kernel<1>, w, 1, true, din, dout);
