@@ -92,6 +92,38 @@ def native_oracle():
     return so
 
 
+def per_sample_rates(device, samples=12000):
+    """The drop-in's per-sample form, `out = F(x); F.tick();` (tests/resynthesis.cpp:35-39), at C1
+    (128 bands) and C2 (4096 bands): operator() + tick() through the C ABI's resident per-sample
+    kernel (hz_fb_sample / hz_fb_sample_tick), called from Python (ctypes) like a demo callback."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from huygens_amd import Filterbank
+    from golden.spec_numpy import resonant_coefficients
+    out = {}
+    for name, N in (("c1_128_bands", 128), ("c2_4096_bands", 4096)):
+        fwd, back = resonant_coefficients(N, 0.999, 1.0)
+        fb = Filterbank(2, N, 0.1, 1.0, device=device)
+        for n in range(N):
+            fb.coefficients(n, fwd[n], back[n])
+        fb.boost(np.ones(N))
+        fb.open()
+        xs = np.random.default_rng(7).uniform(-1, 1, samples + 500)
+        for v in xs[:500]:
+            fb(v)
+            fb.tick()
+        t0 = time.perf_counter()
+        for v in xs[500:]:
+            fb(v)
+            fb.tick()
+        dt = time.perf_counter() - t0
+        out[name] = {"samples_per_s": samples / dt, "us_per_sample": 1e6 * dt / samples,
+                     "real_time_48k": samples / dt >= 48000.0, "resident_kernel": fb.sample_info()[0]}
+        fb.close()
+    out["note"] = ("operator() + tick() per sample through the resident per-sample kernel (pinned-host "
+                   "mailbox), Python ctypes caller, 12,000 samples after 500 of warm-up")
+    return out
+
+
 def cpu_baseline(fwd, back, runs=5):
     """The CPU restatement (oracle/hz_oracle.c, the reference's operation order) timed on this
     host, SURVEY.md 8(d): (a) ONE thread -- the reference's execution model (one PortAudio
@@ -309,6 +341,7 @@ def main():
     ap.add_argument("--samples", type=int, default=SAMPLES_PER_STEP)
     ap.add_argument("--stream-blocks", type=int, default=469, help="1024-sample calls for the streaming figure")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-per-sample", action="store_true", help="skip the per-sample drop-in figure")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 --pmc child passes")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--bands-per-wave", type=int, default=0)
@@ -675,6 +708,7 @@ def main():
                 },
             },
             "side": side or None,
+            "per_sample": per_sample_rates(dev.index or 0) if (world == 1 and not args.no_per_sample) else None,
             "streaming": {"band_samples_per_s": stream_rate, "block": 1024,
                           "us_per_block": (1e6 * N_BANDS * 1024 / stream_rate) if stream_rate else None,
                           "note": "one process() call per 1024-sample block, device-resident I/O"},

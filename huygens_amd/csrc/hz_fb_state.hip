@@ -37,8 +37,9 @@ constexpr int kL = 128;             // chunk (samples)
 constexpr int kTile = 64 * kL;      // 8192 samples per tile
 constexpr int kCols = 32;           // band-state columns per workgroup (two 16-wide MFMA blocks)
 constexpr int kSlab = 16 * kL + 4;  // a wave's x slab per tile: 16 chunks + the last chunk's taps past it
-constexpr int kSlabPos = kSlab + 2 * 16 + 2;   // with 2 pad slots per chunk
-constexpr int kStage = (kSlab + 63) / 64;     // staging loads per lane (33)
+constexpr int kSlabPieces = 17;    // L-sample pieces of a slab (16 chunks + the taps past the last)
+constexpr int kSlabPos = kSlabPieces * (kL + 2);   // with 2 pad slots per piece (16-B aligned pieces)
+constexpr int kStage = (kSlab + 63) / 64;     // register staging loads per lane of tile 0 (33)
 
 template <int O>
 struct StateGeom {
@@ -70,6 +71,47 @@ __device__ __forceinline__ double mix_cols(const double* w, double v) {
         r = fma(w[3], quad_xor<3>(v), r);
     }
     return r;
+}
+
+// One tile of a wave's chain: tile it + 1's pieces of the wave's share of row block m's slab go
+// into `nxt` by LDS-DMA (1 KiB per instruction, 16 B per lane from the x window), then the 33
+// k-steps read their A operands from `cur` (4 ahead of the MFMAs).  `cur` and `nxt` are restrict:
+// inlined here, the compiler knows the DMA does not write what the reads read and issues no wait
+// between them (with one plain pointer it made every read wait for the newest DMA).
+template <int KE, int OP>
+__device__ __forceinline__ void state_tile(const double* __restrict__ cur, double* __restrict__ nxt, bool dma,
+                                           __amdgpu_buffer_rsrc_t xr, int voff, int sb, int a_pos,
+                                           const double (&e)[KE], const double (&m64)[OP], bool carry, f64x4& acc) {
+    if (dma) {
+#pragma unroll
+        for (int i = 0; i < (kSlabPieces + 1) / 2; ++i) {
+            const int p = 2 * i + sb;   // wave-uniform
+            if (p < kSlabPieces)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    xr, (__attribute__((address_space(3))) void*)(nxt + p * (kL + 2)), 16,
+                    voff + p * kL * (int)sizeof(double), 0, 0, 0);
+        }
+    }
+    if (carry) {   // acc <- M^64 acc (the previous tiles, one tile further back)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) acc[rr] = mix_cols<OP>(m64, acc[rr]);
+    }
+    auto a_at = [&](int q) {
+        const int t = 4 * q;   // + (l >> 4) < 4: taps 128.. of the last k-step sit after the pad
+        return t < kL ? cur[a_pos + t] : cur[a_pos + t + 2];
+    };
+    constexpr int EP = 4;
+    double xq[EP];
+#pragma unroll
+    for (int q = 0; q < EP; ++q) xq[q] = a_at(q);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < KE; ++q) {
+        const double xa = xq[q % EP];
+        if (q + EP < KE) xq[q % EP] = a_at(q + EP);
+        __builtin_amdgcn_sched_barrier(0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, e[q], acc, 0, 0, 0);
+    }
 }
 
 struct StateArgs {
@@ -118,9 +160,11 @@ __global__ __launch_bounds__(512) void fb_state_kernel(StateArgs a) {
     qrow(3 - (lane >> 4), mg);
     qrow(16 * (3 - m), mw);
     // row block m's slab of every tile: x[t0 + it T + 16m L - O + e], e < kSlab (its 16 chunks'
-    // taps), staged global -> registers -> LDS at pos(e) = e + 2 (e / L) (A reads of 16 chunks x
-    // 4 taps hit distinct banks per half-wave); waves m and m + 4 (the two column blocks) share it,
-    // each staging half of it
+    // taps) at LDS pos(e) = e + 2 (e / L): 17 pieces of L samples, piece p at p (L + 2) (A reads of
+    // 16 chunks x 4 taps hit distinct banks per half-wave); waves m and m + 4 (the two column
+    // blocks) share it.  Two slab sets: tile it + 1 arrives by LDS-DMA (state_tile) while tile it
+    // is read; one barrier per tile.  Tile 0 of the window (its O taps before the window read as
+    // 0, at any O) is staged through registers.
     const __amdgpu_buffer_rsrc_t xr = [&] {
         const unsigned long long xb = (unsigned long long)a.x;
         const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)xb);
@@ -129,64 +173,42 @@ __global__ __launch_bounds__(512) void fb_state_kernel(StateArgs a) {
         return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, bytes,
                                                  0x00020000);
     }();
-    __shared__ double slab_lds[4][kSlabPos];
-    double* slab = slab_lds[m];
+    __shared__ __attribute__((aligned(16))) double slab_a[4][kSlabPos];
+    __shared__ __attribute__((aligned(16))) double slab_b[4][kSlabPos];
     const long t0 = (long)seg * a.tps * kTile;
-    constexpr int kHalf = (kStage + 1) / 2;   // staging loads of column block 0's wave (17; block 1: 16)
-    const int i0 = sb * kHalf;
-    const int voff0 = (int)((t0 - O + (long)(16 * m) * kL + lane + 64 * i0) * (long)sizeof(double));
-    double st[kHalf];
-    auto load_tile = [&](int it) {
-        const int v = voff0 + it * kTile * (int)sizeof(double);
+    {   // tile 0 through registers (element-wise range check: the taps before the window are 0)
+        constexpr int kHalf = (kStage + 1) / 2;
+        const int i0 = sb * kHalf;
+        const int v = (int)((t0 - O + (long)(16 * m) * kL + lane + 64 * i0) * (long)sizeof(double));
+        double st[kHalf];
 #pragma unroll
         for (int i = 0; i < kHalf; ++i)
             st[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, v + 512 * i, 0, 0));
-    };
-    auto store_tile = [&]() {
 #pragma unroll
         for (int i = 0; i < kHalf; ++i) {
             const int e = lane + 64 * (i0 + i);
-            if (e < kSlab) slab[e + 2 * (e / kL)] = st[i];
+            if (e < kSlab) slab_a[m][e + 2 * (e / kL)] = st[i];
         }
+    }
+    // tile it's DMA offset (16 B per lane: piece p = x[t0 + it T + 16m L - O + p L + 2 lane (+1)])
+    auto voff = [&](int it) {
+        return (int)((t0 + (long)it * kTile - O + (long)(16 * m) * kL + 2 * lane) * (long)sizeof(double));
     };
     // A operand of k-step q: X[chunk c = l & 15][tap t = 4q + (l >> 4)] = slab element 128 c + t
     const int a_pos = (lane & 15) * (kL + 2) + (lane >> 4);
-    auto a_at = [&](int q) {
-        const int t = 4 * q;   // + (l >> 4) < 4: taps 128.. of the last k-step sit after the pad
-        return t < kL ? slab[a_pos + t] : slab[a_pos + t + 2];
-    };
     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-    load_tile(0);
-    store_tile();
-    if (a.tps > 1) load_tile(1);
-    __syncthreads();
-    for (int it = 0; it < a.tps; ++it) {
-        if (it > 0) {   // acc <- M^64 acc (the previous tiles, one tile further back)
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) acc[rr] = mix_cols<OP>(m64, acc[rr]);
-        }
-        // A operands read EP k-steps ahead of their MFMAs (the LDS latency under the chain; the
-        // scheduler would otherwise sink each read to its use)
-        constexpr int EP = 4;
-        double xq[EP];
-#pragma unroll
-        for (int q = 0; q < EP; ++q) xq[q] = a_at(q);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < KE; ++q) {
-            const double xa = xq[q % EP];
-            if (q + EP < KE) xq[q % EP] = a_at(q + EP);
-            __builtin_amdgcn_sched_barrier(0);
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, e[q], acc, 0, 0, 0);
-        }
-        // the next tile into the slab once both waves of the row block have read this one; the
-        // one after into the staging registers
-        if (it + 1 < a.tps) {
-            __syncthreads();
-            store_tile();
-            if (it + 2 < a.tps) load_tile(it + 2);
-            __syncthreads();
-        }
+    __syncthreads();   // tile 0's ds_writes
+    // tile it in slab set it & 1, tile it + 1 arriving in the other; after a tile, this wave's
+    // pieces of the next have landed (vmcnt) and every wave is past this one (barrier)
+    for (int it = 0; it < a.tps; it += 2) {
+        state_tile<KE, OP>(slab_a[m], slab_b[m], it + 1 < a.tps, xr, voff(it + 1), sb, a_pos, e, m64, it > 0, acc);
+        if (it + 1 >= a.tps) break;
+        __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0); expcnt, lgkmcnt at their maxima (no wait)
+        __syncthreads();
+        state_tile<KE, OP>(slab_b[m], slab_a[m], it + 2 < a.tps, xr, voff(it + 2), sb, a_pos, e, m64, true, acc);
+        if (it + 2 >= a.tps) break;
+        __builtin_amdgcn_s_waitcnt(0x0f70);
+        __syncthreads();
     }
     // S = sum_c M^(63-c) A_c, lane rows c = 16m + g + 4 rr (g = l >> 4), by Horner steps: over rr
     // with M^4 (anchored at row 16m + g + 12), M^(3-g) (row 16m + 15), the sum over g, M^(16(3-m))

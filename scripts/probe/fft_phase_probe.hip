@@ -15,7 +15,7 @@
 
 constexpr int kLgH = 11, kH = 1 << kLgH, kP = kH, kThreads = 256, kPT = kH / kThreads;
 constexpr int kSplit = (kH / 2 + kThreads) / kThreads;
-constexpr int kStamps = 10;
+constexpr int kStamps = 12;   // slots 9: hw id, 10 / 11: s_memrealtime at start / end
 
 struct FftLds {
     double re[hz::padded_len(kH)], im[hz::padded_len(kH)];
@@ -107,6 +107,7 @@ __global__ __launch_bounds__(kThreads) void fwd2k_probe(const double* __restrict
                                                        long long* __restrict__ st) {
     __shared__ hz2k::Lds s;
     long long ts[kStamps];
+    const long long rt0 = __builtin_amdgcn_s_memrealtime();
     int ns = 0;
     ts[ns++] = stamp();
     const int t = threadIdx.x;
@@ -174,8 +175,15 @@ __global__ __launch_bounds__(kThreads) void fwd2k_probe(const double* __restrict
     ts[ns++] = stamp();
     __builtin_amdgcn_s_waitcnt(0);
     ts[ns++] = stamp();
-    if (t == 0)
+    // where the workgroup ran: HW_ID (cu [11:8], sh [12], se [15:13]) and XCC_ID
+    const unsigned hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    if (t == 0) {
         for (int i = 0; i < kStamps; ++i) st[(long)blockIdx.x * kStamps + i] = i < ns ? ts[i] : 0;
+        st[(long)blockIdx.x * kStamps + 9] = ((long long)(xcc & 0xf) << 32) | hwid;
+        st[(long)blockIdx.x * kStamps + 10] = rt0;
+        st[(long)blockIdx.x * kStamps + 11] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 int main() {
@@ -199,19 +207,22 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    for (int mode = 0; mode < 3; ++mode)
+    // mode 3: mode 2 with 90 KB of unused dynamic LDS per workgroup, so at most one fits a CU
+    hipFuncSetAttribute((const void*)fwd2k_probe, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    for (int mode = 0; mode < 4; ++mode)
         for (int wg : {24, 258}) {
             auto k = mode == 0 ? fwd_probe<0> : mode == 1 ? fwd_probe<1> : fwd2k_probe;
-            for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(k, dim3(wg), dim3(kThreads), 0, 0, u, tw, Z, Zn, st);
+            const size_t dyn = mode == 3 ? 90 * 1024 : 0;
+            for (int rep = 0; rep < 200; ++rep) hipLaunchKernelGGL(k, dim3(wg), dim3(kThreads), dyn, 0, u, tw, Z, Zn, st);
             hipEventRecord(e0);
-            hipLaunchKernelGGL(k, dim3(wg), dim3(kThreads), 0, 0, u, tw, Z, Zn, st);
+            hipLaunchKernelGGL(k, dim3(wg), dim3(kThreads), dyn, 0, u, tw, Z, Zn, st);
             hipEventRecord(e1);
             hipEventSynchronize(e1);
             float ms = 0;
             hipEventElapsedTime(&ms, e0, e1);
             std::vector<long long> hs((long)wg * kStamps);
             hipMemcpy(hs.data(), st, hs.size() * sizeof(long long), hipMemcpyDeviceToHost);
-            const int nst = mode == 0 ? 9 : mode == 1 ? 5 : 8;
+            const int nst = mode == 0 ? 9 : mode == 1 ? 5 : 8;   // modes 2, 3: the hz_fft2k path
             std::vector<double> avg(nst, 0.0);
             long long first = hs[0], lastend = 0;
             for (int b = 0; b < wg; ++b) {
@@ -220,10 +231,37 @@ int main() {
                 lastend = std::max(lastend, hs[b * kStamps + nst - 1]);
             }
             std::printf("mode %d (%s), %3d workgroups: event %.2f us; span first start -> last end %.0f ticks; "
-                        "per-WG phase ticks (s_memtime):", mode, mode == 2 ? "hz_fft2k" : mode ? "no FFT" : "full", wg, 1e3 * ms,
+                        "per-WG phase ticks (s_memtime):", mode, mode == 3 ? "hz_fft2k, 1/CU" : mode == 2 ? "hz_fft2k" : mode ? "no FFT" : "full", wg, 1e3 * ms,
                         (double)(lastend - first));
             for (int i = 1; i < nst; ++i) std::printf(" %.0f", avg[i]);
             std::printf("\n");
+            if (mode >= 2) {   // workgroups per CU (XCC, SE, SH, CU)
+                std::vector<int> cnt(8 * 8 * 2 * 16, 0);
+                for (int b = 0; b < wg; ++b) {
+                    const long long v = hs[b * kStamps + 9];
+                    const unsigned hw = (unsigned)v, xc = (unsigned)(v >> 32);
+                    const int cu = (hw >> 8) & 15, sh = (hw >> 12) & 1, se = (hw >> 13) & 7;
+                    ++cnt[((xc * 8 + se) * 2 + sh) * 16 + cu];
+                }
+                int used = 0, mx = 0;
+                for (int c : cnt) {
+                    used += c > 0;
+                    mx = std::max(mx, c);
+                }
+                long long r0 = hs[10], r1 = 0, rmax = 0;
+                double rsum = 0;
+                for (int b = 0; b < wg; ++b) {
+                    r0 = std::min(r0, hs[b * kStamps + 10]);
+                    r1 = std::max(r1, hs[b * kStamps + 11]);
+                }
+                for (int b = 0; b < wg; ++b) {
+                    rmax = std::max(rmax, hs[b * kStamps + 10] - r0);
+                    rsum += hs[b * kStamps + 11] - hs[b * kStamps + 10];
+                }
+                std::printf("    %d workgroups on %d distinct CUs, at most %d per CU; real time: first start -> last end "
+                            "%.2f us, last start %.2f us after the first, mean workgroup life %.2f us\n",
+                            wg, used, mx, 0.01 * (r1 - r0), 0.01 * rmax, 0.01 * rsum / wg);
+            }
         }
     return 0;
 }
