@@ -215,6 +215,12 @@ def resp_step_flops(K, S, N, O=2):
     return conv, state
 
 
+def resp_inv_flops(S):
+    """FP64 flops of the inverse transforms of a stationary call's output blocks (as resp_step_flops)."""
+    H, lgH = 2048, 11
+    return -(-S // 2048) * (5.0 * H * lgH + 10.0 * H)
+
+
 PMC_FLOP_COUNTERS = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
                      "SQ_INSTS_VALU_MFMA_MOPS_F64")
 
@@ -559,10 +565,9 @@ def main():
         for k in ("band_partition", "band_partition_per_band_engine"):
             side[k]["note"] = (f"{N_BANDS} bands over {world} GPUs ({cnt} per GPU), one {S1}-sample call per "
                                "step, partial mixes summed to rank 0 by RCCL reduce (strong scaling)")
-    # the engine's GPU time per call: the event sum, except on the stationary path, whose state pass
-    # (red_ms, side stream) runs beside the transforms (mix_ms): there the timed pass's wall time
-    # (one call per step)
-    eng_ms = 1e3 * elapsed if resp else seg_ms + mix_ms + red_ms
+    # the engine's GPU time per call: the event sum (stationary path: forward + MAC kernels, then the
+    # inverse kernel carrying the band-state pass)
+    eng_ms = seg_ms + mix_ms + red_ms
     if world > 1:
         eng_ms_max = ar(eng_ms, dist.ReduceOp.MAX)
         elapsed = ar(elapsed, dist.ReduceOp.MAX)
@@ -597,14 +602,16 @@ def main():
         launch_avg_s = (eng_ms_max / 1e3) / max(1, launches)    # whole engine step, per process() call
         out_samples = S // P_t if resp else S                   # this GPU's outputs per step
         bs_launch = (N_BANDS if resp else cnt) * out_samples     # band-samples of one call on this GPU
-        # ---- dominant kernel (roofline): the band-state pass of the stationary engine, the state
-        # kernel of the per-band LTI engine, the mix kernel of the general engine; its average
-        # duration from the HIP events around it on the handle's stream
+        # ---- dominant kernel (roofline): the stationary engine's inverse kernel, which carries the
+        # band-state pass (hz_fb_state.h: MFMA, ~96% of its flops) beside the output blocks' inverse
+        # transforms; the state kernel of the per-band LTI engine; the mix kernel of the general
+        # engine -- its average duration from the HIP events around it on the handle's stream
         if resp:
-            dom = "fb_state_kernel"
-            dom_name = "fb_state_kernel<2> (band states: zero-start pass over the %d-sample history)" % horizon
+            dom = "resp_inv_kernel"
+            dom_name = ("resp_inv_kernel<2> (inverse transforms of the output blocks + the band-state pass: "
+                        "zero-start pass over the %d-sample history on the FP64 matrix cores)" % horizon)
             dom_ms = red_ms / max(1, launches)
-            dom_model = resp_step_flops(horizon, out_samples, cnt)[1]
+            dom_model = resp_step_flops(horizon, out_samples, cnt)[1] + resp_inv_flops(out_samples)
         elif lti:
             dom = "fb_lti_kernel<2, %d, 2" % chunk
             dom_name = "fb_lti_kernel<2,%d,STATE> (chunk end states on MFMA + scan)" % chunk
@@ -617,7 +624,7 @@ def main():
             dom_model = 20.0 * cnt * S
         step_kernels = (("fb_lti_kernel", "fb_lti_gemm", "fb_lti_reduce", "fb_lti_seg_carry", "fb_lti_sum",
                          "fb_lti_xrows") if lti
-                        else ("resp_fwd_kernel", "resp_mac_kernel", "resp_inv_kernel", "fb_state_kernel") if resp
+                        else ("resp_fwd_kernel", "resp_mac_kernel", "resp_inv_kernel") if resp
                         else ("fb_mix_kernel", "fb_reduce"))
         extra = (["--lti", args.lti] if args.lti else []) + (["--general"] if args.general else []) + \
                 (["--response", str(args.response)] if args.response >= 0 else [])
@@ -680,9 +687,13 @@ def main():
                 "flops_source": "pmc (SQ_INSTS_VALU_{FMA,MUL,ADD}_F64, SQ_INSTS_VALU_MFMA_MOPS_F64)" if dom_flops
                                 else "model (bench.resp_step_flops)",
                 "model_flops_per_launch": dom_model,
-                # state pass: the K history samples in, coefficients + pre-amps (6 doubles) in and
-                # O = 2 states out per band; per-band engines: the block I/O and the band records
-                "algorithmic_bytes_per_launch": (8 * horizon + 64 * cnt) if resp else (16 * out_samples + 120 * cnt),
+                # inverse kernel: the output spectra in, the output out, the next history written;
+                # its state pass: the K history samples in, every band's chunk end-state map E
+                # (O x (128 + O) doubles), carry powers and O states out; per-band engines: the block
+                # I/O and the band records
+                "algorithmic_bytes_per_launch": (16 * 2048 * -(-out_samples // 2048) + 8 * out_samples + 16 * horizon
+                                                 + 8 * cnt * 2 * (130 + 2) + 64 * cnt) if resp
+                                                else (16 * out_samples + 120 * cnt),
                 "peak_note": "FP64 MFMA peak = FP64 vector peak on MI355X (78.6 TFLOP/s); the state pass is "
                              "v_mfma_f64_16x16x4f64 chains (scripts/probe/mfma_f64_probe.hip: 71-78 TFLOP/s)",
                 "step": {

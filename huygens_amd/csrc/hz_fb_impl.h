@@ -172,8 +172,6 @@ struct hz_fb {
         double* d_tw = nullptr;          // W_4096^k, k < 2048 (complex)
         double* d_sop = nullptr;         // band-state pass: pin E operands (fb_state_prepare)
         size_t sop_cap = 0;
-        hipStream_t side = nullptr;      // the band-state pass beside the convolution (calls n >= K)
-        hipEvent_t ev_fork = nullptr, ev_join = nullptr;
         double* d_spart = nullptr;       // band-state pass: segment partials, arrival counters
         size_t spart_cap = 0;
         unsigned* d_scount = nullptr;

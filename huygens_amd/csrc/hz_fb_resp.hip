@@ -31,6 +31,7 @@
 #include <cstdlib>
 
 #include "hz_fb_impl.h"
+#include "hz_fb_state.h"
 #include "hz_fft2k.h"
 
 namespace {
@@ -44,10 +45,15 @@ constexpr int kMacR = 8;                   // output blocks per MAC thread (part
 constexpr long kMinCall = 16384;           // shortest call that keeps the history
 // cost model: stationary when N n >= kBandsPerSample (K + n) (hz_fb_tune_response overrides it)
 constexpr long kBandsPerSample = 256;
-// the band-state pass on a side stream beside the transforms (calls n >= K).  Measured at C2:
-// 0.0593 ms per step against 0.0524 serial -- the state kernel's 272 VGPRs per wave leave no room
-// for the MAC kernel's waves on a CU, so the two serialise with worse placement (r3k)
-constexpr bool kStatesBeside = false;
+// the transform kernels carrying the band-state pieces (bit 0 forward, 1 MAC, 2 inverse).  Measured
+// at C2 (rocprof, per call): every piece pays the pass's prologue (~4.7 us: the 12.6 MB of B operands
+// and the x window arrive at HBM rate) and a CU holds two of these 256-register workgroups, so
+// pieces in all three kernels made them 17.3 + 15.6 + 14.2 us, pieces in the MAC and inverse 9.3 +
+// 17.5 + 16.0, the whole pass in the inverse kernel 9.5 + 9.4 + 21.9 us (the transforms run in the
+// state pass's prologue and beside it), against 9.4 + 9.0 + 8.4 + 19.3 for a separate state kernel,
+// and 51 us per step with that kernel on a second stream (an MFMA chain starves the waves beside it
+// on its SIMD: the older wave issues first, s_setprio changed nothing)
+constexpr int kChainKernels = 4;
 static_assert(kH == hz2k::kN && kThreads == hz2k::kT, "hz_fft2k.h: 2048 points on 256 threads");
 
 // Aggregate impulse response, one wave (64 bands) per workgroup: part[g][tau] = sum over the
@@ -168,6 +174,7 @@ struct RespArgs {
     long K, n;            // horizon; the call's length
     long off, n_out;      // outputs of this launch: out[off, off + n_out) (time-range shards)
     int Q, B;             // partitions; output blocks
+    int nz;               // windows (forward workgroups)
     const double2* tw;    // W_F^k, k < kH
     double2* Z;           // [Q + B - 1 (+ pad)][kH] window spectra
     double* Zn;           // [..] their bin kH
@@ -192,12 +199,29 @@ __device__ __forceinline__ double resp_u(const RespArgs& a, long m) {
     return m < a.off + a.n_out ? a.x[m] : 0.0;
 }
 
+// The transform kernels carry the band-state pass (hz_fb_state.h) as extra workgroups past their
+// own (SO = the bank's order, 0: none): a CU holds one of each (<= 256 registers per wave, LDS the
+// larger of the two), so the MFMA-bound state runs under the latency-bound transforms.
+union RespLds {
+    hz2k::Lds fft;
+    hz_state::StateLds st;
+};
+
+#define HZ_RESP_KERNEL(name) \
+    template <int SO> __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void name
+
 // Z_j = the spectrum of W_j = u[jP, jP + F)
-__global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a) {
-    __shared__ hz2k::Lds s;
+HZ_RESP_KERNEL(resp_fwd_kernel)(RespArgs a, hz_state::StateArgs st) {
+    __shared__ RespLds u;
+    if constexpr (SO > 0) {
+        if ((int)blockIdx.x >= a.nz) {
+            hz_state::state_group<SO>(st, blockIdx.x - a.nz, 0, u.st);
+            return;
+        }
+    }
     const long m0 = (long)blockIdx.x * kP;
     real_window_fwd(
-        s, [&](int m) { return resp_u(a, m0 + m); }, a.tw, a.Z + (long)blockIdx.x * kH, a.Zn + blockIdx.x);
+        u.fft, [&](int m) { return resp_u(a, m0 + m); }, a.tw, a.Z + (long)blockIdx.x * kH, a.Zn + blockIdx.x);
 }
 
 // Y_b[q] = sum_{p < Q} H_p[q] Z_{b+Q-1-p}[q] for b in [b0, b0 + R): thread = bin q x R output
@@ -207,11 +231,22 @@ __global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a) {
 // QP > 0 (Qp == QP, a compile-time count): every H and Z operand of the thread is loaded before
 // the first MAC -- one memory latency per launch (a lone workgroup per CU hides none of it);
 // QP == 0: any Qp, the next block's 2R loads issued before this block's MACs.
-template <int R, int QP>
-__global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict__ H, const double2* __restrict__ Z,
-                                                       double2* __restrict__ Y, int Q, int Qp, int B) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;   // bin (grid.x = kH / 256)
-    const int b0 = blockIdx.y * R;
+// (workgroups past kH / 256 x ceil(B / R): the band-state piece, SO > 0)
+template <int R, int QP, int SO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void resp_mac_kernel(
+    const double2* __restrict__ H, const double2* __restrict__ Z, double2* __restrict__ Y, int Q, int Qp, int B,
+    hz_state::StateArgs st) {
+    constexpr int kBinGroups = kH / 256;
+    const int nmac = kBinGroups * ((B + R - 1) / R);
+    if constexpr (SO > 0) {
+        if ((int)blockIdx.x >= nmac) {
+            __shared__ hz_state::StateLds sl;
+            hz_state::state_group<SO>(st, blockIdx.x - nmac, 0, sl);
+            return;
+        }
+    }
+    const int q = (blockIdx.x % kBinGroups) * blockDim.x + threadIdx.x;   // bin
+    const int b0 = (blockIdx.x / kBinGroups) * R;
     double ar[R], ai[R], zr[R], zi[R];
     const long base = (long)b0 + Q - 1;
 #pragma unroll
@@ -275,22 +310,34 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
         if (b0 + r < B) Y[(long)(b0 + r) * kH + q] = make_double2(ar[r], ai[r]);
 }
 
-typedef void (*MacKernel)(const double2*, const double2*, double2*, int, int, int);
-MacKernel pick_mac(int Qp) {
+typedef void (*MacKernel)(const double2*, const double2*, double2*, int, int, int, hz_state::StateArgs);
+template <int SO>
+MacKernel pick_mac_so(int Qp) {
     switch (Qp) {
-    case 8: return resp_mac_kernel<kMacR, 8>;
-    case 16: return resp_mac_kernel<kMacR, 16>;
-    case 24: return resp_mac_kernel<kMacR, 24>;
-    default: return resp_mac_kernel<kMacR, 0>;
+    case 8: return resp_mac_kernel<kMacR, 8, SO>;
+    case 16: return resp_mac_kernel<kMacR, 16, SO>;
+    case 24: return resp_mac_kernel<kMacR, 24, SO>;
+    default: return resp_mac_kernel<kMacR, 0, SO>;
     }
 }
+MacKernel pick_mac(int Qp, int so) {
+    return so == 1 ? pick_mac_so<1>(Qp) : so == 2 ? pick_mac_so<2>(Qp) : pick_mac_so<0>(Qp);
+}
+typedef void (*RespKernel)(RespArgs, hz_state::StateArgs);
 
 // output block b: the merge of Y_b into Zh' = E' + i O' (E' = Y[k] + conj Y[kH-k],
 // O' = (Y[k] - conj Y[kH-k]) W^-k; Zh'[kH-k] = conj E' + i conj O'), the inverse 2048-point FFT,
 // out[bP + 2r (+1)] = Re (Im) z[kH/2 + r] (the last P samples of the window's circular
 // convolution) straight from the last pass's registers
-__global__ __launch_bounds__(kThreads) void resp_inv_kernel(RespArgs a) {
-    __shared__ hz2k::Lds s;
+HZ_RESP_KERNEL(resp_inv_kernel)(RespArgs a, hz_state::StateArgs st) {
+    __shared__ RespLds u;
+    if constexpr (SO > 0) {
+        if ((int)blockIdx.x >= a.B) {
+            hz_state::state_group<SO>(st, blockIdx.x - a.B, 0, u.st);
+            return;
+        }
+    }
+    hz2k::Lds& s = u.fft;
     const int t = threadIdx.x;
     const long b = blockIdx.x;
     const double2* y = a.Y + b * kH;
@@ -341,7 +388,7 @@ __global__ __launch_bounds__(kThreads) void resp_inv_kernel(RespArgs a) {
         if (t0 + 1 < a.n_out) a.out[a.off + t0 + 1] = vi[i];
     }
     // state upkeep (the forward kernel, the last reader of hist, has finished)
-    const long g = b * blockDim.x + t, stride = (long)gridDim.x * blockDim.x;
+    const long g = b * blockDim.x + t, stride = (long)a.B * blockDim.x;
     // a time-range shard leaves zeros outside its range: the ranks' outputs sum to the call's
     for (long i = g; i < a.n - a.n_out; i += stride) a.out[i < a.off ? i : i + a.n_out] = 0.0;
     for (long i = g; i < a.K; i += stride) {
@@ -598,44 +645,64 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.xhist_next = h->d_xhist[h->xcur ^ 1];
     a.N = h->N;
     a.O = h->order;
+    a.nz = nz;
     // EAGER, n >= K: the band states after the call are the zero-start states over the call's last
-    // K samples, independent of the convolution -- the state pass (FP64 matrix cores) runs on a
-    // side stream beside the transforms (latency-bound, no MFMA), joined before the call returns
+    // K samples, independent of the convolution: the state pass runs as pieces (runs of its tiles)
+    // inside the transform kernels, one piece per kernel of kChainKernels (bit 0 forward, 1 MAC,
+    // 2 inverse), the last piece's workgroups combining the pieces (orders <= 2: 256 registers)
     const bool lazy = R.mode == HZ_FB_RESP_LAZY;
-    const bool beside = kStatesBeside && !lazy && n >= K;
-    if (beside) {
-        if (!R.side) {
-            HZ_TRY_HIP(hipStreamCreateWithFlags(&R.side, hipStreamNonBlocking));
-            HZ_TRY_HIP(hipEventCreateWithFlags(&R.ev_fork, hipEventDisableTiming));
-            HZ_TRY_HIP(hipEventCreateWithFlags(&R.ev_join, hipEventDisableTiming));
-        }
-        HZ_TRY_HIP(hipEventRecord(R.ev_fork, h->stream));
-        HZ_TRY_HIP(hipStreamWaitEvent(R.side, R.ev_fork, 0));
-        if (e) HZ_TRY_HIP(hipEventRecord(e[3], R.side));
-        HZ_TRY(fb_state_window(h, d_in + (n - K), K, h->d_ystate[h->scur ^ 1], R.side));
-        if (e) HZ_TRY_HIP(hipEventRecord(e[4], R.side));
-        HZ_TRY_HIP(hipEventRecord(R.ev_join, R.side));
+    const int mask = kChainKernels;
+    const bool chained = !lazy && n >= K && h->order <= 2 && mask != 0;
+    hz_state::StateArgs st = hz_state::StateArgs();
+    int pieces = 0;
+    if (chained) {
+        pieces = __builtin_popcount(mask);
+        HZ_TRY(fb_state_chained(h, d_in + (n - K), K, h->d_ystate[h->scur ^ 1], pieces, &st));
     }
-    hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, h->stream, a);
+    const int so = chained ? h->order : 0;
+    // kernel k's state workgroups: band groups of piece `next` when bit k is set and pieces remain
+    int next = 0;
+    auto state_wgs = [&](int k, hz_state::StateArgs& sa) {
+        sa = st;
+        if (!chained || !(mask & (1 << k)) || next >= st.nseg) return 0;
+        sa.piece = next++;
+        return st.G;
+    };
+    hz_state::StateArgs sa;
+    int extra = state_wgs(0, sa);
+    RespKernel kf = so == 1 ? resp_fwd_kernel<1> : so == 2 ? resp_fwd_kernel<2> : resp_fwd_kernel<0>;
+    hipLaunchKernelGGL(kf, dim3((unsigned)(nz + extra)), dim3(kThreads), 0, h->stream, a, sa);
     HZ_TRY_HIP(hipGetLastError());
-    hipLaunchKernelGGL(pick_mac(Qp), dim3(kH / 256, (unsigned)((B + kMacR - 1) / kMacR)), dim3(256), 0,
-                       h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B);
+    extra = state_wgs(1, sa);
+    const int nmac = (kH / 256) * ((B + kMacR - 1) / kMacR);
+    hipLaunchKernelGGL(pick_mac(Qp, so), dim3((unsigned)(nmac + extra)), dim3(256), 0, h->stream,
+                       (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B, sa);
     HZ_TRY_HIP(hipGetLastError());
-    hipLaunchKernelGGL(resp_inv_kernel, dim3((unsigned)B), dim3(kThreads), 0, h->stream, a);
+    if (e && chained) {   // profiling: e0..e2 forward + MAC, e2..e4 the inverse kernel with the band states
+        HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
+        h->ev_skip[(e - h->ev.data()) / 5] |= 8;
+    }
+    extra = state_wgs(2, sa);
+    RespKernel ki = so == 1 ? resp_inv_kernel<1> : so == 2 ? resp_inv_kernel<2> : resp_inv_kernel<0>;
+    hipLaunchKernelGGL(ki, dim3((unsigned)(B + extra)), dim3(kThreads), 0, h->stream, a, sa);
     HZ_TRY_HIP(hipGetLastError());
-    if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
+    if (chained && next < st.nseg) {
+        hz::set_error("fb_launch_resp: band-state pieces %d of %d placed", next, st.nseg);
+        return HZ_E_STATE;
+    }
+    if (e && chained) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
+    if (e && !chained) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     R.hcur ^= 1;   // the inverse kernel wrote the history after the call
     R.run = std::min(R.run + n, 1L << 60);
-    // end state: the band states over the new history now (EAGER: joined from the side stream,
-    // or after the transforms when n < K) or when needed (LAZY); the smoothers and x history were
-    // written by the inverse kernel
-    // (profiling events 3 / 4 bracket the state pass on the stream it runs on)
+    // end state: the band states over the new history (EAGER: computed inside the transform
+    // kernels, or after them when n < K / order > 2) or when needed (LAZY); the smoothers and x
+    // history were written by the inverse kernel (profiling events 3 / 4 bracket the state pass;
+    // chained: the three kernels)
     if (lazy) {
         R.implicit = true;
         if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
         if (e) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
-    } else if (beside) {
-        HZ_TRY_HIP(hipStreamWaitEvent(h->stream, R.ev_join, 0));
+    } else if (chained) {
         R.implicit = false;
     } else {
         if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
@@ -653,13 +720,9 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
 
 void fb_resp_free(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
-    if (R.side) (void)hipStreamSynchronize(R.side);
     for (double* p : {R.d_hist[0], R.d_hist[1], R.d_h, R.d_hpart, R.d_coef, R.d_zero, R.d_H, R.d_Z, R.d_Y, R.d_tw,
                       R.d_spart, R.d_sop})
         if (p) (void)hipFree(p);
-    if (R.ev_fork) (void)hipEventDestroy(R.ev_fork);
-    if (R.ev_join) (void)hipEventDestroy(R.ev_join);
-    if (R.side) (void)hipStreamDestroy(R.side);
     if (R.d_scount) (void)hipFree(R.d_scount);
     R = hz_fb::Resp();
 }

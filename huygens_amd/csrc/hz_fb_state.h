@@ -1,0 +1,351 @@
+// hz_fb_state.h -- the band-state pass of the stationary engine as a workgroup-level device
+// function: every band's zero-start state after a window of len samples (len a multiple of 8192),
+//     S_n = sum_c M_n^(C-1-c) pin_n E_n x_c        (c < C = len / 128 chunks of 128 samples)
+// with E_n the chunk's zero-state end-state map over its L + O input taps and M_n the chunk
+// transition (the chunk-128 LTI records, hz_fb_rec.h; the band recurrence of
+// src/filterbank.h:178-179 restated chunk-wise).  That is N O len multiply-adds, ~0.8 GFLOP at
+// C2 (4096 bands, O = 2, len = 49152): the pass is bound by the FP64 matrix cores (78.6 TFLOP/s).
+//
+// Work split: one workgroup = 32 band-state columns (16 bands of O = 2; OP = O padded to a power
+// of two columns per band) x one run of tiles; 4 waves (one per SIMD), wave m owns chunk rows
+// 16m..16m+15 of every 8192-sample tile (64 chunks) and runs two independent chains of 33
+// v_mfma_f64_16x16x4f64 per tile, one per 16-column block, whose accumulators start from M^64
+// applied to the previous tiles' sum, so after the last tile accumulator row c holds
+//     A_c = sum_tiles M^(64 (T-1-t)) z_{t,c},   z_{t,c} = pin E x_{t,c}
+// and S = sum_c M^(63-c) A_c (one weighted reduction at the end, across lanes and waves).
+//   * A operands (the chunk windows) go straight from the L2-resident x window into registers
+//     with no LDS and no barrier: the MFMA's k index is free up to a permutation shared by A and
+//     B, and lane group g (k within the step) of k-step q takes tap
+//         tap(q, g) = 8 (q >> 1) + 2 g + (q & 1)   (q < 32),   128 + g   (q = 32)
+//     so each lane reads its chunk's taps as 16 aligned pairs (buffer_load_dwordx4: 16 chunks x
+//     64 contiguous bytes per instruction) plus one double; each pair is reloaded with the next
+//     tile's taps as soon as its two k-steps have issued (one register set, a tile of latency);
+//   * B operands (pin E in that tap order, fb_state_ops_kernel) reach LDS by LDS-DMA once per
+//     workgroup and then live in registers;
+//   * the O taps before the window are the zero-start history: the window is addressed through
+//     a buffer resource whose range check returns 0 for them (tap pairs never straddle the window
+//     start: odd orders shift the taps by one, s = O & 1, with a zero E row) and for taps past
+//     the window's end (E entries 0 there).
+// At O <= 2 a wave fits 256 registers, so a CU holds a state workgroup beside a transform
+// workgroup: hz_fb_resp.hip runs the pass as extra workgroups of its transform kernels.
+//
+// A window split into runs of tiles ("pieces") combines by Horner steps over the pieces,
+// S = P_last (... (P_1 S_0 + S_1) ...) + S_last, P_s = (M^64)^(tiles of piece s):
+//   * standalone launches (fb_state_kernel, grid.y = pieces of equal length) store the partials
+//     and the last workgroup of a band group to arrive (device-scope counter) combines them;
+//   * pieces run by consecutive kernels (the transform kernels) store theirs, and the last
+//     kernel's workgroups combine: the kernel boundaries order them.
+#pragma once
+
+#include "hz_fb_impl.h"
+#include "hz_fb_rec.h"
+
+namespace hz_state {
+
+constexpr int kL = 128;             // chunk (samples)
+constexpr int kTile = 64 * kL;      // 8192 samples per tile
+constexpr int kCols = 32;           // band-state columns per workgroup (two 16-wide MFMA blocks)
+constexpr int kKE = 33;             // MFMA k-steps per chunk (132 tap slots)
+constexpr int kThreads = 256;       // 4 waves
+// B operands per workgroup: 2 x kKE x 64 doubles, padded to whole 1 KiB pieces per wave
+constexpr int kEop = (2 * kKE * 64 + 2 * kThreads - 1) / (2 * kThreads) * (2 * kThreads);
+// then the M^e weights of every column: W[sb][col][p][j] = row k of M^e(p) at column k ^ j (j < 4),
+// e(p) = 64 (the tile carry), 4, 0..3, 16, 32, 48 (the end's Horner steps); padded to whole 1 KiB
+// pieces per wave
+constexpr int kPows = 9;
+constexpr int kW = (2 * 16 * kPows * 4 + 2 * kThreads - 1) / (2 * kThreads) * (2 * kThreads);
+constexpr int kGrp = kEop + kW;     // doubles per band group (fb_state_ops_kernel)
+__host__ __device__ constexpr int pow_of(int p) { return p == 0 ? 64 : p == 1 ? 4 : p < 6 ? p - 2 : 16 * (p - 5); }
+constexpr int kMaxPieces = 4;
+
+template <int O>
+struct StateGeom {
+    static constexpr int OP = O == 3 ? 4 : O;       // columns per band
+    static constexpr int BANDS = kCols / OP;        // bands per workgroup
+    static constexpr int XW = kL + O;               // chunk input taps
+    static constexpr int S = O & 1;                 // tap shift: tap pairs 16-B aligned in x
+    static_assert(XW + S <= 4 * kKE, "taps fit the k-steps");
+};
+
+inline int bands_per_group(int O) { return kCols / (O == 3 ? 4 : O); }
+
+// tap slot of k-step q for lane group g (the MFMA's k index within the step)
+__host__ __device__ constexpr int tap_slot(int q, int g) { return q < 32 ? 8 * (q >> 1) + 2 * g + (q & 1) : 128 + g; }
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// lane l <- lane (l ^ j) within its quad (DPP quad_perm), j = 1, 2, 3
+template <int J>
+__device__ __forceinline__ double quad_xor(double v) {
+    constexpr int ctrl = J == 1 ? 0xB1 : J == 2 ? 0x4E : 0x1B;
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), ctrl, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), ctrl, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// sum_j w[j] v_(lane ^ j): a band's O x O matrix row k applied to its state columns
+template <int OP>
+__device__ __forceinline__ double mix_cols(const double* w, double v) {
+    double r = w[0] * v;
+    if constexpr (OP >= 2) r = fma(w[1], quad_xor<1>(v), r);
+    if constexpr (OP >= 4) {
+        r = fma(w[2], quad_xor<2>(v), r);
+        r = fma(w[3], quad_xor<3>(v), r);
+    }
+    return r;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t state_rsrc(const double* p, long count) {
+    const unsigned long long b = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane((int)(count * (long)sizeof(double)));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, bytes, 0x00020000);
+}
+
+// a lane's 33 A operands of one tile: x[v / 8 + tap_slot(q, g)], v = the byte offset of its chunk's
+// first slot (16-B aligned; negative = before the window: out of range, 0)
+__device__ __forceinline__ void load_a(__amdgpu_buffer_rsrc_t xr, int v, int g, double (&a)[kKE]) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const u32x4 p = __builtin_amdgcn_raw_buffer_load_b128(xr, v + (int)sizeof(double) * (8 * j + 2 * g), 0, 0);
+        a[2 * j] = __builtin_bit_cast(double, ((unsigned long long)p.y << 32) | p.x);
+        a[2 * j + 1] = __builtin_bit_cast(double, ((unsigned long long)p.w << 32) | p.z);
+    }
+    a[32] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, v + (int)sizeof(double) * (128 + g), 0, 0));
+}
+
+// one tile of both chains: acc_sb <- (M^64 acc_sb if carry) + sum_q A_q B_{sb,q}; each A pair is
+// reloaded with the next tile's taps (byte offset vn) as soon as its two k-steps are issued
+template <int OP>
+__device__ __forceinline__ void state_tile(double (&a)[kKE], const double (&b)[2][kKE], const double (&m64)[2][OP],
+                                           bool carry, __amdgpu_buffer_rsrc_t xr, int vn, int g, f64x4& acc0,
+                                           f64x4& acc1) {
+    if (carry) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            acc0[rr] = mix_cols<OP>(m64[0], acc0[rr]);
+            acc1[rr] = mix_cols<OP>(m64[1], acc1[rr]);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < kKE; ++q) {
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[0][q], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], b[1][q], acc1, 0, 0, 0);
+        if (q & 1) {
+            const u32x4 p = __builtin_amdgcn_raw_buffer_load_b128(xr, vn + (int)sizeof(double) * (8 * (q >> 1) + 2 * g), 0, 0);
+            a[q - 1] = __builtin_bit_cast(double, ((unsigned long long)p.y << 32) | p.x);
+            a[q] = __builtin_bit_cast(double, ((unsigned long long)p.w << 32) | p.z);
+        } else if (q == 32) {
+            a[32] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, vn + (int)sizeof(double) * (128 + g), 0, 0));
+        }
+        __builtin_amdgcn_sched_barrier(0);   // keep each reload beside its k-steps (the scheduler
+                                             // bunched them at the tile's end: a wait per tile)
+    }
+}
+
+struct StateArgs {
+    const double* rec;     // chunk-128 records [N][rs]
+    int rs;                // record size (doubles)
+    const double* eop;     // [G][kGrp] pin E operands [2][kKE][64], M^e weights (fb_state_ops_kernel)
+    const double* x;       // [len] the window
+    long len;
+    int nbands;
+    int G;                 // band groups (workgroups per piece)
+    int tps;               // standalone: tiles per piece (grid.y = pieces)
+    int nseg;              // pieces of the window
+    int piece;             // consecutive-kernel pieces: this launch's piece (-1: standalone)
+    int ptile0[kMaxPieces], ptiles[kMaxPieces];   // consecutive-kernel pieces: first tile, tiles
+    double* part;          // [G][nseg][kCols] piece partials (nseg > 1)
+    unsigned* count;       // [G] arrival counters (standalone, nseg > 1; 0 between launches)
+    double* out;           // [N][O]
+};
+
+struct StateLds {
+    double eb[kGrp];
+    double red[4][kCols];
+    int is_last;
+};
+
+// (M^64)^e by squaring (O x O, row-major)
+template <int O>
+__device__ __forceinline__ void m64_pow(const double* M64, int e, double (&P)[O][O]) {
+    double Pw[O][O], Tm[O][O];
+    for (int i = 0; i < O; ++i)
+        for (int j = 0; j < O; ++j) {
+            Pw[i][j] = M64[i * O + j];
+            P[i][j] = i == j ? 1.0 : 0.0;
+        }
+    for (int ex = e; ex > 0; ex >>= 1) {
+        if (ex & 1) {
+            for (int i = 0; i < O; ++i)
+                for (int j = 0; j < O; ++j) {
+                    double s = 0.0;
+                    for (int q = 0; q < O; ++q) s = fma(P[i][q], Pw[q][j], s);
+                    Tm[i][j] = s;
+                }
+            for (int i = 0; i < O; ++i)
+                for (int j = 0; j < O; ++j) P[i][j] = Tm[i][j];
+        }
+        for (int i = 0; i < O; ++i)
+            for (int j = 0; j < O; ++j) {
+                double s = 0.0;
+                for (int q = 0; q < O; ++q) s = fma(Pw[i][q], Pw[q][j], s);
+                Tm[i][j] = s;
+            }
+        for (int i = 0; i < O; ++i)
+            for (int j = 0; j < O; ++j) Pw[i][j] = Tm[i][j];
+    }
+}
+
+// band b's state from its piece partials p0[s kCols + i]: Horner over the pieces (piece s has
+// uniform tiles, or tiles[s] when uniform is 0)
+template <int O>
+__device__ __forceinline__ void combine_pieces(const StateArgs& a, int b, const double* p0, const int* tiles,
+                                               int uniform) {
+    using R = hz_fbi::RecL<O, kL>;
+    const double* M64 = a.rec + (long)b * a.rs + R::QC + 64 * O * O;
+    double S[O], P[O][O];
+    int pe = -1;
+    for (int i = 0; i < O; ++i) S[i] = p0[i];
+    for (int s = 1; s < a.nseg; ++s) {
+        const int e = uniform > 0 ? uniform : tiles[s];
+        if (e != pe) m64_pow<O>(M64, e, P);
+        pe = e;
+        const double* ps = p0 + (long)s * kCols;
+        double nS[O];
+        for (int i = 0; i < O; ++i) {
+            double acc2 = ps[i];
+            for (int q = 0; q < O; ++q) acc2 = fma(P[i][q], S[q], acc2);
+            nS[i] = acc2;
+        }
+        for (int i = 0; i < O; ++i) S[i] = nS[i];
+    }
+    for (int i = 0; i < O; ++i) a.out[(long)b * O + i] = S[i];
+}
+
+// the workgroup of band group g over piece seg (standalone: tiles [seg tps, (seg + 1) tps);
+// consecutive-kernel pieces: a.piece's tiles); 256 threads
+template <int O>
+__device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, StateLds& L) {
+    using Gm = StateGeom<O>;
+    constexpr int OP = Gm::OP;
+    const int lane = threadIdx.x & 63;
+    const int m = threadIdx.x >> 6;             // chunk rows 16m .. 16m + 15 of every tile
+    const int col = lane & 15;                  // column within a 16-column block
+    const int lg = lane >> 4;                   // lane group: the MFMA's k index
+    const bool chained = a.piece >= 0;
+    const int pc = chained ? a.piece : seg;
+
+    const int ntl = chained ? a.ptiles[pc] : a.tps;
+    const __amdgpu_buffer_rsrc_t xr = state_rsrc(a.x, a.len);
+    // tile it's A offset (bytes) of this lane's chunk 64 it + 16 m + col of the piece
+    const long t0 = (long)(chained ? a.ptile0[pc] : seg * a.tps) * kTile;
+    auto voff = [&](int it) {
+        return (int)((t0 + (long)it * kTile + (long)(16 * m + col) * kL - O - Gm::S) * (long)sizeof(double));
+    };
+    // rows k of the band's M^e as weights of the columns k ^ j, from the LDS copy of the group's
+    // weight block (p: pow_of)
+    auto wrow = [&](int sb, int p, double (&wt)[OP]) {
+        const double* w = L.eb + kEop + ((sb * 16 + col) * kPows + p) * 4;
+#pragma unroll
+        for (int j = 0; j < OP; ++j) wt[j] = w[j];
+    };
+    double xa[kKE];
+    load_a(xr, voff(0), lg, xa);
+    // B operands of both column blocks into LDS by LDS-DMA (1 KiB per wave instruction, no
+    // registers: register-staged fills were serialised by the compiler, one latency per load)
+    {
+        const __amdgpu_buffer_rsrc_t er = state_rsrc(a.eop + (long)g * kGrp, kGrp);
+        constexpr int kPieces = kGrp * (int)sizeof(double) / 1024;
+        static_assert(kPieces % 4 == 0, "whole pieces per wave");
+#pragma unroll
+        for (int r = 0; r < kPieces / 4; ++r) {
+            const int c = m + 4 * r;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(er, (__attribute__((address_space(3))) void*)(L.eb + c * 128), 16,
+                                                     c * 1024 + 16 * lane, 0, 0, 0);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the DMA (and tile 0's x)
+    f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    __syncthreads();
+    double m64[2][OP];
+    wrow(0, 0, m64[0]);
+    wrow(1, 0, m64[1]);
+    double bq[2][kKE];   // B operands in registers for the whole run
+#pragma unroll
+    for (int q = 0; q < kKE; ++q) {
+        bq[0][q] = L.eb[q * 64 + lane];
+        bq[1][q] = L.eb[(kKE + q) * 64 + lane];
+    }
+    // tile it from xa, reloaded with tile it + 1 as it goes (past the last tile: unused loads)
+    for (int it = 0; it < ntl; ++it) state_tile<OP>(xa, bq, m64, it > 0, xr, voff(it + 1), lg, acc0, acc1);
+    // S = sum_c M^(63-c) A_c, lane rows c = 16m + lg + 4 rr, by Horner steps: over rr with M^4
+    // (anchored at row 16m + lg + 12), M^(3-lg) (row 16m + 15), the sum over lg, M^(16(3-m))
+    // (row 63), then the sum over the row blocks (waves)
+    auto finish = [&](int sb, const f64x4& acc) {
+        double m4[OP], mg[OP], mw[OP];
+        wrow(sb, 1, m4);
+        wrow(sb, 2 + (3 - lg), mg);
+        wrow(sb, m == 3 ? 2 : 5 + (3 - m), mw);
+        double T = acc[0];
+#pragma unroll
+        for (int rr = 1; rr < 4; ++rr) T = mix_cols<OP>(m4, T) + acc[rr];
+        T = mix_cols<OP>(mg, T);
+        T += __shfl_xor(T, 16);
+        T += __shfl_xor(T, 32);
+        const double v = mix_cols<OP>(mw, T);
+        if (lane < 16) L.red[m][16 * sb + lane] = v;
+    };
+    finish(0, acc0);
+    finish(1, acc1);
+    __syncthreads();
+    const int t = threadIdx.x;
+    double* prow = a.part + (long)g * a.nseg * kCols;   // this group's piece partials
+    if (t < kCols) {
+        const double S = ((L.red[0][t] + L.red[1][t]) + L.red[2][t]) + L.red[3][t];
+        const int b = g * Gm::BANDS + t / OP, kk = t % OP;
+        if (a.nseg == 1) {
+            if (b < a.nbands && kk < O) a.out[(long)b * O + kk] = S;
+        } else {
+            prow[(long)pc * kCols + t] = S;
+            if (!chained) __threadfence();   // visible at agent scope before the arrival below
+        }
+    }
+    if (a.nseg == 1) return;
+    if (chained) {
+        // consecutive kernels: the earlier pieces' partials are complete; the last combines
+        if (pc != a.nseg - 1) return;
+        __syncthreads();
+        if (t < Gm::BANDS) {
+            const int b = g * Gm::BANDS + t;
+            if (b < a.nbands) combine_pieces<O>(a, b, prow + t * OP, a.ptiles, 0);
+        }
+        return;
+    }
+    // standalone: the last workgroup of this band group to arrive combines the partials
+    __syncthreads();
+    if (t == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(a.count + g, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        L.is_last = prev == (unsigned)(a.nseg - 1);
+    }
+    __syncthreads();
+    if (!L.is_last) return;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    if (t < Gm::BANDS) {
+        const int b = g * Gm::BANDS + t;
+        if (b < a.nbands) combine_pieces<O>(a, b, prow + t * OP, nullptr, a.tps);
+    }
+    if (t == 0) __hip_atomic_store(a.count + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace hz_state
+
+namespace hz_fbi {
+// the band-state pass as `pieces` consecutive runs of tiles (orders <= 2), each run by extra
+// workgroups of a kernel that launches state_group<O>(a, g, 0, lds) with a.piece set to its run;
+// the last run's workgroups combine and write out
+int fb_state_chained(hz_fb* h, const double* x, long len, double* out, int pieces, hz_state::StateArgs* a);
+}  // namespace hz_fbi
