@@ -24,8 +24,9 @@
 // The per-band state is kept exact: the last K inputs are the handle's history (updated by every
 // converged long call the engine could take, whatever engine ran it), and the band states at the
 // call end are their zero-start response over those K samples (the band-state pass on the FP64
-// matrix cores, hz_fb_state.hip) -- after every call (HZ_FB_RESP_EAGER, default) or only
-// when a later call, get_state, tick or a setter needs them (HZ_FB_RESP_LAZY).
+// matrix cores, hz_fb_state.h; for calls n >= K it runs as extra workgroups of resp_inv_kernel)
+// -- after every call (HZ_FB_RESP_EAGER, default) or only when a later call, get_state, tick or a
+// setter needs them (HZ_FB_RESP_LAZY).
 // Multi-GPU: time-range shards (hz_fb_set_bank_response + hz_fb_set_time_shard) convolve one
 // rank's run of output blocks with the whole bank's response; DESIGN.md 3.6 and 5.
 #include <cstdlib>
@@ -45,15 +46,15 @@ constexpr int kMacR = 8;                   // output blocks per MAC thread (part
 constexpr long kMinCall = 16384;           // shortest call that keeps the history
 // cost model: stationary when N n >= kBandsPerSample (K + n) (hz_fb_tune_response overrides it)
 constexpr long kBandsPerSample = 256;
-// the transform kernels carrying the band-state pieces (bit 0 forward, 1 MAC, 2 inverse).  Measured
-// at C2 (rocprof, per call): every piece pays the pass's prologue (~4.7 us: the 12.6 MB of B operands
-// and the x window arrive at HBM rate) and a CU holds two of these 256-register workgroups, so
-// pieces in all three kernels made them 17.3 + 15.6 + 14.2 us, pieces in the MAC and inverse 9.3 +
-// 17.5 + 16.0, the whole pass in the inverse kernel 9.5 + 9.4 + 21.9 us (the transforms run in the
-// state pass's prologue and beside it), against 9.4 + 9.0 + 8.4 + 19.3 for a separate state kernel,
-// and 51 us per step with that kernel on a second stream (an MFMA chain starves the waves beside it
-// on its SIMD: the older wave issues first, s_setprio changed nothing)
-constexpr int kChainKernels = 4;
+// The band-state pass of EAGER calls n >= K runs as extra workgroups of the inverse kernel.  Measured
+// at C2 (rocprof, per call): every piece of the pass pays its prologue (~4.7 us: the 12.6 MB of B
+// operands and the x window arrive at HBM rate) and a CU holds two of these 256-register
+// workgroups, so pieces in all three transform kernels made them 17.3 + 15.6 + 14.2 us, pieces in
+// the MAC and inverse kernels 9.3 + 17.5 + 16.0, the whole pass in the inverse kernel 9.5 + 9.4 +
+// 21.9 us (the transforms run in the state pass's prologue and beside it), against 9.4 + 9.0 + 8.4
+// + 19.3 for a separate state kernel, and 51 us per step with that kernel on a second stream (an
+// MFMA chain starves the waves beside it on its SIMD: the older wave issues first; s_setprio
+// changed nothing)
 static_assert(kH == hz2k::kN && kThreads == hz2k::kT, "hz_fft2k.h: 2048 points on 256 threads");
 
 // Aggregate impulse response, one wave (64 bands) per workgroup: part[g][tau] = sum over the
@@ -199,29 +200,20 @@ __device__ __forceinline__ double resp_u(const RespArgs& a, long m) {
     return m < a.off + a.n_out ? a.x[m] : 0.0;
 }
 
-// The transform kernels carry the band-state pass (hz_fb_state.h) as extra workgroups past their
-// own (SO = the bank's order, 0: none): a CU holds one of each (<= 256 registers per wave, LDS the
-// larger of the two), so the MFMA-bound state runs under the latency-bound transforms.
+// The inverse kernel carries the band-state pass (hz_fb_state.h) as extra workgroups past its own
+// (SO = the bank's order, 0: none): a CU holds one of each (<= 256 registers per wave, LDS the
+// larger of the two), so the latency-bound inverse transforms run beside the state pass.
 union RespLds {
     hz2k::Lds fft;
     hz_state::StateLds st;
 };
 
-#define HZ_RESP_KERNEL(name) \
-    template <int SO> __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void name
-
 // Z_j = the spectrum of W_j = u[jP, jP + F)
-HZ_RESP_KERNEL(resp_fwd_kernel)(RespArgs a, hz_state::StateArgs st) {
-    __shared__ RespLds u;
-    if constexpr (SO > 0) {
-        if ((int)blockIdx.x >= a.nz) {
-            hz_state::state_group<SO>(st, blockIdx.x - a.nz, 0, u.st);
-            return;
-        }
-    }
+__global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a) {
+    __shared__ hz2k::Lds s;
     const long m0 = (long)blockIdx.x * kP;
     real_window_fwd(
-        u.fft, [&](int m) { return resp_u(a, m0 + m); }, a.tw, a.Z + (long)blockIdx.x * kH, a.Zn + blockIdx.x);
+        s, [&](int m) { return resp_u(a, m0 + m); }, a.tw, a.Z + (long)blockIdx.x * kH, a.Zn + blockIdx.x);
 }
 
 // Y_b[q] = sum_{p < Q} H_p[q] Z_{b+Q-1-p}[q] for b in [b0, b0 + R): thread = bin q x R output
@@ -231,20 +223,10 @@ HZ_RESP_KERNEL(resp_fwd_kernel)(RespArgs a, hz_state::StateArgs st) {
 // QP > 0 (Qp == QP, a compile-time count): every H and Z operand of the thread is loaded before
 // the first MAC -- one memory latency per launch (a lone workgroup per CU hides none of it);
 // QP == 0: any Qp, the next block's 2R loads issued before this block's MACs.
-// (workgroups past kH / 256 x ceil(B / R): the band-state piece, SO > 0)
-template <int R, int QP, int SO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void resp_mac_kernel(
-    const double2* __restrict__ H, const double2* __restrict__ Z, double2* __restrict__ Y, int Q, int Qp, int B,
-    hz_state::StateArgs st) {
+template <int R, int QP>
+__global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict__ H, const double2* __restrict__ Z,
+                                                       double2* __restrict__ Y, int Q, int Qp, int B) {
     constexpr int kBinGroups = kH / 256;
-    const int nmac = kBinGroups * ((B + R - 1) / R);
-    if constexpr (SO > 0) {
-        if ((int)blockIdx.x >= nmac) {
-            __shared__ hz_state::StateLds sl;
-            hz_state::state_group<SO>(st, blockIdx.x - nmac, 0, sl);
-            return;
-        }
-    }
     const int q = (blockIdx.x % kBinGroups) * blockDim.x + threadIdx.x;   // bin
     const int b0 = (blockIdx.x / kBinGroups) * R;
     double ar[R], ai[R], zr[R], zi[R];
@@ -310,18 +292,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void r
         if (b0 + r < B) Y[(long)(b0 + r) * kH + q] = make_double2(ar[r], ai[r]);
 }
 
-typedef void (*MacKernel)(const double2*, const double2*, double2*, int, int, int, hz_state::StateArgs);
-template <int SO>
-MacKernel pick_mac_so(int Qp) {
+typedef void (*MacKernel)(const double2*, const double2*, double2*, int, int, int);
+MacKernel pick_mac(int Qp) {
     switch (Qp) {
-    case 8: return resp_mac_kernel<kMacR, 8, SO>;
-    case 16: return resp_mac_kernel<kMacR, 16, SO>;
-    case 24: return resp_mac_kernel<kMacR, 24, SO>;
-    default: return resp_mac_kernel<kMacR, 0, SO>;
+    case 8: return resp_mac_kernel<kMacR, 8>;
+    case 16: return resp_mac_kernel<kMacR, 16>;
+    case 24: return resp_mac_kernel<kMacR, 24>;
+    default: return resp_mac_kernel<kMacR, 0>;
     }
-}
-MacKernel pick_mac(int Qp, int so) {
-    return so == 1 ? pick_mac_so<1>(Qp) : so == 2 ? pick_mac_so<2>(Qp) : pick_mac_so<0>(Qp);
 }
 typedef void (*RespKernel)(RespArgs, hz_state::StateArgs);
 
@@ -329,7 +307,9 @@ typedef void (*RespKernel)(RespArgs, hz_state::StateArgs);
 // O' = (Y[k] - conj Y[kH-k]) W^-k; Zh'[kH-k] = conj E' + i conj O'), the inverse 2048-point FFT,
 // out[bP + 2r (+1)] = Re (Im) z[kH/2 + r] (the last P samples of the window's circular
 // convolution) straight from the last pass's registers
-HZ_RESP_KERNEL(resp_inv_kernel)(RespArgs a, hz_state::StateArgs st) {
+template <int SO>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void resp_inv_kernel(
+    RespArgs a, hz_state::StateArgs st) {
     __shared__ RespLds u;
     if constexpr (SO > 0) {
         if ((int)blockIdx.x >= a.B) {
@@ -647,49 +627,27 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.O = h->order;
     a.nz = nz;
     // EAGER, n >= K: the band states after the call are the zero-start states over the call's last
-    // K samples, independent of the convolution: the state pass runs as pieces (runs of its tiles)
-    // inside the transform kernels, one piece per kernel of kChainKernels (bit 0 forward, 1 MAC,
-    // 2 inverse), the last piece's workgroups combining the pieces (orders <= 2: 256 registers)
+    // K samples, independent of the convolution: the state pass runs as extra workgroups of the
+    // inverse kernel (orders <= 2: 256 registers; prefetching its operands into the XCDs' L2 from the
+    // MAC kernel was measured: no gain)
     const bool lazy = R.mode == HZ_FB_RESP_LAZY;
-    const int mask = kChainKernels;
-    const bool chained = !lazy && n >= K && h->order <= 2 && mask != 0;
+    const bool chained = !lazy && n >= K && h->order <= 2;
     hz_state::StateArgs st = hz_state::StateArgs();
-    int pieces = 0;
-    if (chained) {
-        pieces = __builtin_popcount(mask);
-        HZ_TRY(fb_state_chained(h, d_in + (n - K), K, h->d_ystate[h->scur ^ 1], pieces, &st));
-    }
+    if (chained) HZ_TRY(fb_state_chained(h, d_in + (n - K), K, h->d_ystate[h->scur ^ 1], 1, &st));
     const int so = chained ? h->order : 0;
-    // kernel k's state workgroups: band groups of piece `next` when bit k is set and pieces remain
-    int next = 0;
-    auto state_wgs = [&](int k, hz_state::StateArgs& sa) {
-        sa = st;
-        if (!chained || !(mask & (1 << k)) || next >= st.nseg) return 0;
-        sa.piece = next++;
-        return st.G;
-    };
-    hz_state::StateArgs sa;
-    int extra = state_wgs(0, sa);
-    RespKernel kf = so == 1 ? resp_fwd_kernel<1> : so == 2 ? resp_fwd_kernel<2> : resp_fwd_kernel<0>;
-    hipLaunchKernelGGL(kf, dim3((unsigned)(nz + extra)), dim3(kThreads), 0, h->stream, a, sa);
+    hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
-    extra = state_wgs(1, sa);
     const int nmac = (kH / 256) * ((B + kMacR - 1) / kMacR);
-    hipLaunchKernelGGL(pick_mac(Qp, so), dim3((unsigned)(nmac + extra)), dim3(256), 0, h->stream,
-                       (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B, sa);
+    hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)nmac), dim3(256), 0, h->stream, (const double2*)R.d_H,
+                       (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B);
     HZ_TRY_HIP(hipGetLastError());
     if (e && chained) {   // profiling: e0..e2 forward + MAC, e2..e4 the inverse kernel with the band states
         HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
         h->ev_skip[(e - h->ev.data()) / 5] |= 8;
     }
-    extra = state_wgs(2, sa);
     RespKernel ki = so == 1 ? resp_inv_kernel<1> : so == 2 ? resp_inv_kernel<2> : resp_inv_kernel<0>;
-    hipLaunchKernelGGL(ki, dim3((unsigned)(B + extra)), dim3(kThreads), 0, h->stream, a, sa);
+    hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G : 0))), dim3(kThreads), 0, h->stream, a, st);
     HZ_TRY_HIP(hipGetLastError());
-    if (chained && next < st.nseg) {
-        hz::set_error("fb_launch_resp: band-state pieces %d of %d placed", next, st.nseg);
-        return HZ_E_STATE;
-    }
     if (e && chained) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
     if (e && !chained) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     R.hcur ^= 1;   // the inverse kernel wrote the history after the call
