@@ -20,8 +20,8 @@
 //     so each lane reads its chunk's taps as 16 aligned pairs (buffer_load_dwordx4: 16 chunks x
 //     64 contiguous bytes per instruction) plus one double; each pair is reloaded with the next
 //     tile's taps as soon as its two k-steps have issued (one register set, a tile of latency);
-//   * B operands (pin E in that tap order, fb_state_ops_kernel) reach LDS by LDS-DMA once per
-//     workgroup and then live in registers;
+//   * B operands (pin E in that tap order, fb_state_ops_kernel) live in registers, loaded with
+//     tile 0's A operands in the order the first tile's k-steps use them;
 //   * the O taps before the window are the zero-start history: the window is addressed through
 //     a buffer resource whose range check returns 0 for them (tap pairs never straddle the window
 //     start: odd orders shift the taps by one, s = O & 1, with a zero E row) and for taps past
@@ -164,7 +164,6 @@ struct StateArgs {
 };
 
 struct StateLds {
-    double eb[kGrp];
     double red[4][kCols];
     int is_last;
 };
@@ -246,40 +245,46 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
     auto voff = [&](int it) {
         return (int)((t0 + (long)it * kTile + (long)(16 * m + col) * kL - O - Gm::S) * (long)sizeof(double));
     };
-    // rows k of the band's M^e as weights of the columns k ^ j, from the LDS copy of the group's
-    // weight block (p: pow_of)
+    // rows k of the band's M^e as weights of the columns k ^ j, from the group's weight block
+    // (p: pow_of); buffer loads off the block's resource (32-bit offsets, no address registers)
+    const __amdgpu_buffer_rsrc_t er = state_rsrc(a.eop + (long)g * kGrp, kGrp);
+    auto ld = [&](int i) { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(er, 8 * i, 0, 0)); };
     auto wrow = [&](int sb, int p, double (&wt)[OP]) {
-        const double* w = L.eb + kEop + ((sb * 16 + col) * kPows + p) * 4;
+        const int w = kEop + ((sb * 16 + col) * kPows + p) * 4;
 #pragma unroll
-        for (int j = 0; j < OP; ++j) wt[j] = w[j];
+        for (int j = 0; j < OP; ++j) wt[j] = ld(w + j);
     };
-    double xa[kKE];
-    load_a(xr, voff(0), lg, xa);
-    // B operands of both column blocks into LDS by LDS-DMA (1 KiB per wave instruction, no
-    // registers: register-staged fills were serialised by the compiler, one latency per load)
-    {
-        const __amdgpu_buffer_rsrc_t er = state_rsrc(a.eop + (long)g * kGrp, kGrp);
-        constexpr int kPieces = kGrp * (int)sizeof(double) / 1024;
-        static_assert(kPieces % 4 == 0, "whole pieces per wave");
-#pragma unroll
-        for (int r = 0; r < kPieces / 4; ++r) {
-            const int c = m + 4 * r;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(er, (__attribute__((address_space(3))) void*)(L.eb + c * 128), 16,
-                                                     c * 1024 + 16 * lane, 0, 0, 0);
-        }
-    }
-    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the DMA (and tile 0's x)
-    f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-    __syncthreads();
+    // the carry weights first, then tile 0's A operands and every B operand straight into
+    // registers in the order the first tile's k-steps use them: its MFMAs start as their operands
+    // arrive (a staged LDS copy waited for the whole block behind a barrier: 3.4 us before the
+    // first MFMA)
     double m64[2][OP];
     wrow(0, 0, m64[0]);
     wrow(1, 0, m64[1]);
-    double bq[2][kKE];   // B operands in registers for the whole run
+    double xa[kKE], bq[2][kKE];
+    {
+        const int v = voff(0);
 #pragma unroll
-    for (int q = 0; q < kKE; ++q) {
-        bq[0][q] = L.eb[q * 64 + lane];
-        bq[1][q] = L.eb[(kKE + q) * 64 + lane];
+        for (int j = 0; j < 16; ++j) {
+            const u32x4 pr = __builtin_amdgcn_raw_buffer_load_b128(xr, v + (int)sizeof(double) * (8 * j + 2 * lg), 0, 0);
+            xa[2 * j] = __builtin_bit_cast(double, ((unsigned long long)pr.y << 32) | pr.x);
+            xa[2 * j + 1] = __builtin_bit_cast(double, ((unsigned long long)pr.w << 32) | pr.z);
+#pragma unroll
+            for (int u = 2 * j; u < 2 * j + 2; ++u) {
+                bq[0][u] = ld(u * 64 + lane);
+                bq[1][u] = ld((kKE + u) * 64 + lane);
+            }
+        }
+        xa[32] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, v + (int)sizeof(double) * (128 + lg), 0, 0));
+        bq[0][32] = ld(32 * 64 + lane);
+        bq[1][32] = ld((kKE + 32) * 64 + lane);
     }
+    // the carry weights complete here (the oldest loads): redefined by an empty asm, so the loop's
+    // waits track only the x loads (the compiler otherwise waited for every load in flight before
+    // each carry)
+#pragma unroll
+    for (int j = 0; j < OP; ++j) asm volatile("" : "+v"(m64[0][j]), "+v"(m64[1][j]));
+    f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     // tile it from xa, reloaded with tile it + 1 as it goes (past the last tile: unused loads)
     for (int it = 0; it < ntl; ++it) state_tile<OP>(xa, bq, m64, it > 0, xr, voff(it + 1), lg, acc0, acc1);
     // S = sum_c M^(63-c) A_c, lane rows c = 16m + lg + 4 rr, by Horner steps: over rr with M^4
