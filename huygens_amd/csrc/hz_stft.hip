@@ -440,17 +440,14 @@ __global__ __launch_bounds__(kFrameThreads) void stft_pair_kernel(StftArgs a, lo
     pair_gate<PROC, pair_items<RMAX>()>(re, im, lg, a.p0, a.p1, scratch);
     __syncthreads();
     hz::fft_inv_tail<RMAX>(re, im, lg, T, true);
-    const long plane = (long)a.R * N;
     double* o0 = a.fo + (f0 % a.R) * N;
     double* o1 = a.fo + (f1 % a.R) * N;
+    // the Re planes only: a real frame's Im output is 0, which the overlap-add knows
+    // (hz_stft::im_zero_from) instead of reading 2 N zeros per pair back from the ring
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
         const int e = hz::pad16(k);
         o0[k] = re[e];
-        o0[plane + k] = 0.0;
-        if (two) {
-            o1[k] = im[e];
-            o1[plane + k] = 0.0;
-        }
+        if (two) o1[k] = im[e];
     }
 }
 
@@ -472,6 +469,7 @@ struct OlaArgs {
     long sh_block;
     int sh_world, sh_rank;
     double sh_inv;   // 1 / sh_block
+    long im_zero_from;   // frames from here on: Im part 0, not in the ring (hz_stft::im_zero_from)
 };
 
 __device__ __forceinline__ bool frame_owned(long f, long block, int world, int rank, double inv) {
@@ -535,7 +533,7 @@ __global__ __launch_bounds__(256) void stft_ola_kernel(OlaArgs a) {
             const long q = (long)row * a.N + r;
             const double w = a.win[r];
             hz::dd_add(rh, rl, w * a.fo[q]);
-            if (a.out_im) hz::dd_add(ih, il, w * a.fo[plane + q]);
+            if (a.out_im && c * 2 * a.laps + i < a.im_zero_from) hz::dd_add(ih, il, w * a.fo[plane + q]);
         }
     }
     const double D = (double)(a.N * a.laps / 2);   // int expression, fourier.h:174-175
@@ -692,6 +690,9 @@ struct hz_stft {
     double* d_fo = nullptr;                    // planar frame ring: Re [R][N], Im [R][N]
     double* d_hist[2] = {nullptr, nullptr};    // last N-1 input samples, [Re | Im] (ping-pong)
     long last_cplx = -1;                       // last sample index that came with an imaginary part
+    // frames >= im_zero_from came from the pair kernel, whose Im plane (all zeros) is not written:
+    // the overlap-add reads no Im part for them (LONG_MAX: none since the last other launch)
+    long im_zero_from = LONG_MAX;
     int hcur = 0;
     size_t spec_cap = 0;
     double *d_in = nullptr, *d_out = nullptr;
@@ -777,11 +778,13 @@ void launch_pairs(hz_stft* h, const StftArgs& a, long nf) {
                            frame_lds(h->N), h->stream, a, nf);
 }
 
+// real input and a magnitude gate: two frames per transform (stft_pair_kernel)
+bool pair_launch(const hz_stft* h, const StftArgs& a) {
+    return h->pair_ok && !a.hi && h->N >= 16 && (h->proc == HZ_PROC_STATIC_GATE || h->proc == HZ_PROC_GATE_KEEP);
+}
+
 int frames_fused(hz_stft* h, const StftArgs& a, long nf) {
-    // real input and a magnitude gate: two frames per transform (stft_pair_kernel)
-    const bool pair = h->pair_ok && !a.hi && h->N >= 16 &&
-                      (h->proc == HZ_PROC_STATIC_GATE || h->proc == HZ_PROC_GATE_KEEP);
-    if (pair) {
+    if (pair_launch(h, a)) {
         if (h->proc == HZ_PROC_STATIC_GATE) launch_pairs<HZ_PROC_STATIC_GATE>(h, a, nf);
         else launch_pairs<HZ_PROC_GATE_KEEP>(h, a, nf);
         HZ_TRY_HIP(hipGetLastError());
@@ -865,6 +868,18 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
         // frames start in increasing order: the first one decides whether any reads an Im part
         a.hi = (nf > 0 && frame_start(f_lo, h->laps, h->stride, N) <= h->last_cplx) ? hc + (N - 1) : nullptr;
         if (nf > 0) {
+            // Im planes: a pair launch leaves them unwritten (0); any other launch writes them, so
+            // the last 2 laps pair frames before it, which the overlap-add still reads, get
+            // explicit zeros first
+            const bool pair = h->proc != HZ_PROC_HOST && pair_launch(h, a);
+            if (pair) {
+                if (h->im_zero_from == LONG_MAX) h->im_zero_from = f_lo;
+            } else if (h->im_zero_from != LONG_MAX) {
+                for (long f = std::max(h->im_zero_from, f_lo - 2L * h->laps); f < f_lo; ++f)
+                    HZ_TRY_HIP(hipMemsetAsync(h->d_fo + (size_t)h->R * N + (size_t)(f % h->R) * N, 0,
+                                              sizeof(double) * N, h->stream));
+                h->im_zero_from = LONG_MAX;
+            }
             if (h->proc != HZ_PROC_HOST) {
                 // profiling may repeat the (idempotent) frame launch so the event pair brackets
                 // several back-to-back launches: per-launch time without the event overhead
@@ -912,6 +927,7 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
     o.sh_world = h->sh_world;
     o.sh_rank = h->sh_rank;
     o.sh_inv = 1.0 / (double)h->sh_block;
+    o.im_zero_from = h->im_zero_from;
     const long threads = std::max(n, (long)N - 1);
     hipLaunchKernelGGL(stft_ola_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, o);
     HZ_TRY_HIP(hipGetLastError());

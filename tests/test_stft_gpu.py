@@ -79,6 +79,30 @@ def test_real_then_complex_calls(gpu_lib, N, laps):
     assert g.frames()[0] == o.frames()
 
 
+@pytest.mark.parametrize("N,laps,proc", [(64, 4, 2), (4096, 4, 2), (512, 4, 1)])
+def test_gate_real_then_complex_calls(gpu_lib, N, laps, proc):
+    """Gated frames of real calls run two per transform (stft_pair_kernel), whose frames leave the
+    ring's Im plane unwritten (the overlap-add takes their Im part as 0); complex calls in
+    between run one frame per transform and write it -- the Im output must match the
+    restatement across every switch, including switches closer together than 2 laps frames."""
+    g, o = make(N, laps, 0, proc)
+    rng = np.random.default_rng(11)
+    T = 0
+    seq = ((3 * N + 1, False), (N // 2 + 3, True), (5, False), (4 * N, False), (N + 9, True), (3 * N, False),
+           (2 * N + 7, True), (N // 4, False), (3, True), (5 * N, False))
+    for n, cplx in seq:
+        t = np.arange(T, T + n)
+        z = 0.5 * np.exp(2j * np.pi * 3 * t / N) + 0.05 * rng.standard_normal(n)
+        re = z.real.copy()
+        im = z.imag.copy() if cplx else None
+        T += n
+        gr, gi = g.process_block(re, im)
+        orr, oi = o.process_block(re, im)
+        scale = max(np.max(np.abs(orr)), np.max(np.abs(oi)), 1e-300)
+        assert np.max(np.abs(gr - orr)) < TOL * scale and np.max(np.abs(gi - oi)) < TOL * scale
+    assert g.frames()[0] == o.frames()
+
+
 @pytest.mark.parametrize("N,laps", [(4096, 4), (8192, 4), (512, 4), (8192, 32)])
 def test_static_stft_c4(gpu_lib, N, laps):
     from huygens_amd import StaticSTFT
