@@ -1052,9 +1052,19 @@ __global__ __launch_bounds__(256) void fb_lti_reduce_short_kernel(const double* 
     const long t = 2 * ((long)blockIdx.x * 16 + pr);
     d2 s = {0.0, 0.0};
     if (t < n) {
+        // every slice row's load issued before the first add (the rolled loop waited for each
+        // batch of 4 in turn); rows past 16 per slice (banks over 4096 bands) in a second pass
         const double* col = partial + t;
-#pragma unroll 4
-        for (int g = sl; g < G; g += SL) s += *(const d2*)(col + (long)g * n_pad);
+        constexpr int R = 16;
+        d2 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int g = sl + r * SL;
+            v[r] = g < G ? *(const d2*)(col + (long)g * n_pad) : d2{0.0, 0.0};
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) s += v[r];
+        for (int g = sl + R * SL; g < G; g += SL) s += *(const d2*)(col + (long)g * n_pad);
     }
     part[sl][pr] = s;
     __syncthreads();
