@@ -313,7 +313,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     __shared__ RespLds u;
     if constexpr (SO > 0) {
         if ((int)blockIdx.x >= a.B) {
-            hz_state::state_group<SO>(st, blockIdx.x - a.B, 0, u.st);
+            const int i = blockIdx.x - a.B;
+            hz_state::state_group<SO>(st, i % st.G, i / st.G, u.st);
             return;
         }
     }
@@ -633,7 +634,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     const bool lazy = R.mode == HZ_FB_RESP_LAZY;
     const bool chained = !lazy && n >= K && h->order <= 2;
     hz_state::StateArgs st = hz_state::StateArgs();
-    if (chained) HZ_TRY(fb_state_chained(h, d_in + (n - K), K, h->d_ystate[h->scur ^ 1], 1, &st));
+    if (chained) HZ_TRY(fb_state_chained(h, d_in + (n - K), K, h->d_ystate[h->scur ^ 1], &st));
     const int so = chained ? h->order : 0;
     hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
@@ -646,7 +647,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         h->ev_skip[(e - h->ev.data()) / 5] |= 8;
     }
     RespKernel ki = so == 1 ? resp_inv_kernel<1> : so == 2 ? resp_inv_kernel<2> : resp_inv_kernel<0>;
-    hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G : 0))), dim3(kThreads), 0, h->stream, a, st);
+    hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0))), dim3(kThreads), 0, h->stream, a, st);
     HZ_TRY_HIP(hipGetLastError());
     if (e && chained) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
     if (e && !chained) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));

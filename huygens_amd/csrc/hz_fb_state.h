@@ -29,12 +29,10 @@
 // At O <= 2 a wave fits 256 registers, so a CU holds a state workgroup beside a transform
 // workgroup: hz_fb_resp.hip runs the pass as extra workgroups of its transform kernels.
 //
-// A window split into runs of tiles ("pieces") combines by Horner steps over the pieces,
-// S = P_last (... (P_1 S_0 + S_1) ...) + S_last, P_s = (M^64)^(tiles of piece s):
-//   * standalone launches (fb_state_kernel, grid.y = pieces of equal length) store the partials
-//     and the last workgroup of a band group to arrive (device-scope counter) combines them;
-//   * pieces run by consecutive kernels (the transform kernels) store theirs, and the last
-//     kernel's workgroups combine: the kernel boundaries order them.
+// Banks with fewer band groups than CUs split the window into equal runs of tiles ("pieces", one
+// workgroup each); they store their partials and the last workgroup of a band group to arrive
+// (device-scope counter) combines them by Horner steps, S = P (... (P S_0 + S_1) ...) + S_last,
+// P = (M^64)^(tiles per piece), and re-arms the counter.
 #pragma once
 
 #include "hz_fb_impl.h"
@@ -56,7 +54,6 @@ constexpr int kPows = 9;
 constexpr int kW = (2 * 16 * kPows * 4 + 2 * kThreads - 1) / (2 * kThreads) * (2 * kThreads);
 constexpr int kGrp = kEop + kW;     // doubles per band group (fb_state_ops_kernel)
 __host__ __device__ constexpr int pow_of(int p) { return p == 0 ? 64 : p == 1 ? 4 : p < 6 ? p - 2 : 16 * (p - 5); }
-constexpr int kMaxPieces = 4;
 
 template <int O>
 struct StateGeom {
@@ -154,12 +151,10 @@ struct StateArgs {
     long len;
     int nbands;
     int G;                 // band groups (workgroups per piece)
-    int tps;               // standalone: tiles per piece (grid.y = pieces)
-    int nseg;              // pieces of the window
-    int piece;             // consecutive-kernel pieces: this launch's piece (-1: standalone)
-    int ptile0[kMaxPieces], ptiles[kMaxPieces];   // consecutive-kernel pieces: first tile, tiles
+    int tps;               // tiles per piece
+    int nseg;              // pieces of the window (equal runs of tps tiles)
     double* part;          // [G][nseg][kCols] piece partials (nseg > 1)
-    unsigned* count;       // [G] arrival counters (standalone, nseg > 1; 0 between launches)
+    unsigned* count;       // [G] arrival counters (nseg > 1; 0 between launches)
     double* out;           // [N][O]
 };
 
@@ -199,20 +194,15 @@ __device__ __forceinline__ void m64_pow(const double* M64, int e, double (&P)[O]
     }
 }
 
-// band b's state from its piece partials p0[s kCols + i]: Horner over the pieces (piece s has
-// uniform tiles, or tiles[s] when uniform is 0)
+// band b's state from its piece partials p0[s kCols + i]: Horner over the pieces of `tiles` tiles
 template <int O>
-__device__ __forceinline__ void combine_pieces(const StateArgs& a, int b, const double* p0, const int* tiles,
-                                               int uniform) {
+__device__ __forceinline__ void combine_pieces(const StateArgs& a, int b, const double* p0, int tiles) {
     using R = hz_fbi::RecL<O, kL>;
     const double* M64 = a.rec + (long)b * a.rs + R::QC + 64 * O * O;
     double S[O], P[O][O];
-    int pe = -1;
+    m64_pow<O>(M64, tiles, P);
     for (int i = 0; i < O; ++i) S[i] = p0[i];
     for (int s = 1; s < a.nseg; ++s) {
-        const int e = uniform > 0 ? uniform : tiles[s];
-        if (e != pe) m64_pow<O>(M64, e, P);
-        pe = e;
         const double* ps = p0 + (long)s * kCols;
         double nS[O];
         for (int i = 0; i < O; ++i) {
@@ -225,8 +215,7 @@ __device__ __forceinline__ void combine_pieces(const StateArgs& a, int b, const 
     for (int i = 0; i < O; ++i) a.out[(long)b * O + i] = S[i];
 }
 
-// the workgroup of band group g over piece seg (standalone: tiles [seg tps, (seg + 1) tps);
-// consecutive-kernel pieces: a.piece's tiles); 256 threads
+// the workgroup of band group g over piece seg (tiles [seg tps, (seg + 1) tps)); 256 threads
 template <int O>
 __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, StateLds& L) {
     using Gm = StateGeom<O>;
@@ -235,13 +224,10 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
     const int m = threadIdx.x >> 6;             // chunk rows 16m .. 16m + 15 of every tile
     const int col = lane & 15;                  // column within a 16-column block
     const int lg = lane >> 4;                   // lane group: the MFMA's k index
-    const bool chained = a.piece >= 0;
-    const int pc = chained ? a.piece : seg;
-
-    const int ntl = chained ? a.ptiles[pc] : a.tps;
+    const int pc = seg, ntl = a.tps;
     const __amdgpu_buffer_rsrc_t xr = state_rsrc(a.x, a.len);
     // tile it's A offset (bytes) of this lane's chunk 64 it + 16 m + col of the piece
-    const long t0 = (long)(chained ? a.ptile0[pc] : seg * a.tps) * kTile;
+    const long t0 = (long)seg * a.tps * kTile;
     auto voff = [&](int it) {
         return (int)((t0 + (long)it * kTile + (long)(16 * m + col) * kL - O - Gm::S) * (long)sizeof(double));
     };
@@ -316,21 +302,11 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
             if (b < a.nbands && kk < O) a.out[(long)b * O + kk] = S;
         } else {
             prow[(long)pc * kCols + t] = S;
-            if (!chained) __threadfence();   // visible at agent scope before the arrival below
+            __threadfence();   // visible at agent scope before the arrival below
         }
     }
     if (a.nseg == 1) return;
-    if (chained) {
-        // consecutive kernels: the earlier pieces' partials are complete; the last combines
-        if (pc != a.nseg - 1) return;
-        __syncthreads();
-        if (t < Gm::BANDS) {
-            const int b = g * Gm::BANDS + t;
-            if (b < a.nbands) combine_pieces<O>(a, b, prow + t * OP, a.ptiles, 0);
-        }
-        return;
-    }
-    // standalone: the last workgroup of this band group to arrive combines the partials
+    // the last workgroup of this band group to arrive combines the partials
     __syncthreads();
     if (t == 0) {
         const unsigned prev = __hip_atomic_fetch_add(a.count + g, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -341,7 +317,7 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     if (t < Gm::BANDS) {
         const int b = g * Gm::BANDS + t;
-        if (b < a.nbands) combine_pieces<O>(a, b, prow + t * OP, nullptr, a.tps);
+        if (b < a.nbands) combine_pieces<O>(a, b, prow + t * OP, a.tps);
     }
     if (t == 0) __hip_atomic_store(a.count + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -349,8 +325,7 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
 }  // namespace hz_state
 
 namespace hz_fbi {
-// the band-state pass as `pieces` consecutive runs of tiles (orders <= 2), each run by extra
-// workgroups of a kernel that launches state_group<O>(a, g, 0, lds) with a.piece set to its run;
-// the last run's workgroups combine and write out
-int fb_state_chained(hz_fb* h, const double* x, long len, double* out, int pieces, hz_state::StateArgs* a);
+// the band-state pass's arguments for a launch inside another kernel (orders <= 2): G nseg extra
+// workgroups, workgroup i running state_group<O>(a, i % G, i / G, lds)
+int fb_state_chained(hz_fb* h, const double* x, long len, double* out, hz_state::StateArgs* a);
 }  // namespace hz_fbi

@@ -100,9 +100,9 @@ int fb_state_prepare(hz_fb* h) {
     return HZ_OK;
 }
 
-// the standalone launch's arguments and piece count (time pieces while the band groups leave CUs
-// idle: the largest m <= target / G dividing the tile count)
-static int state_args(hz_fb* h, const double* x, long len, double* out, int npieces_chained, StateArgs* a) {
+// the pass's arguments and piece count (time pieces while the band groups leave CUs idle: the
+// largest m <= target / G dividing the tile count)
+static int state_args(hz_fb* h, const double* x, long len, double* out, StateArgs* a) {
     const int O = h->order;
     if (O == 0 || len <= 0 || len % kTile != 0 || len > (1L << 27) || !h->resp.d_sop) {
         hz::set_error("fb_state_window: order %d, window %ld (a positive multiple of 8192), operands %s", O, len,
@@ -112,13 +112,8 @@ static int state_args(hz_fb* h, const double* x, long len, double* out, int npie
     hz_fb::LtiRecSet& set = h->lti_set[kLtiGeomChunk128];
     const int G = (h->N + bands_per_group(O) - 1) / bands_per_group(O);
     const int ntiles = (int)(len / kTile);
-    int nseg;
-    if (npieces_chained > 0) {
-        nseg = std::min(npieces_chained, ntiles);
-    } else {
-        nseg = std::max(1, std::min(ntiles, h->target_groups / G));
-        while (ntiles % nseg != 0) --nseg;
-    }
+    int nseg = std::max(1, std::min(ntiles, h->target_groups / G));
+    while (ntiles % nseg != 0) --nseg;
     hz_fb::Resp& R = h->resp;
     if (nseg > 1) {
         const size_t need = (size_t)G * nseg * kCols;
@@ -129,7 +124,7 @@ static int state_args(hz_fb* h, const double* x, long len, double* out, int npie
             HZ_TRY_HIP(hipMalloc(&R.d_spart, sizeof(double) * need));
             R.spart_cap = need;
         }
-        if (npieces_chained == 0 && (size_t)G > R.scount_cap) {
+        if ((size_t)G > R.scount_cap) {
             HZ_TRY_HIP(hipDeviceSynchronize());
             if (R.d_scount) HZ_TRY_HIP(hipFree(R.d_scount));
             R.d_scount = nullptr;
@@ -148,13 +143,6 @@ static int state_args(hz_fb* h, const double* x, long len, double* out, int npie
     a->G = G;
     a->tps = ntiles / nseg;
     a->nseg = nseg;
-    a->piece = npieces_chained > 0 ? 0 : -1;
-    for (int s = 0, t0 = 0; s < nseg; ++s) {   // chained pieces: the tiles split as evenly as they go
-        const int nt = ntiles * (s + 1) / nseg - ntiles * s / nseg;
-        a->ptile0[s] = t0;
-        a->ptiles[s] = nt;
-        t0 += nt;
-    }
     a->part = R.d_spart;
     a->count = R.d_scount;
     a->out = out;
@@ -163,18 +151,18 @@ static int state_args(hz_fb* h, const double* x, long len, double* out, int npie
 
 int fb_state_window(hz_fb* h, const double* x, long len, double* out, hipStream_t st) {
     StateArgs a;
-    HZ_TRY(state_args(h, x, len, out, 0, &a));
+    HZ_TRY(state_args(h, x, len, out, &a));
     hipLaunchKernelGGL(pick_state(h->order), dim3((unsigned)a.G, (unsigned)a.nseg), dim3(kThreads), 0, st, a);
     HZ_TRY_HIP(hipGetLastError());
     return HZ_OK;
 }
 
-int fb_state_chained(hz_fb* h, const double* x, long len, double* out, int pieces, hz_state::StateArgs* a) {
-    if (pieces < 1 || pieces > kMaxPieces || h->order > 2) {
-        hz::set_error("fb_state_chained: %d pieces at order %d", pieces, h->order);
+int fb_state_chained(hz_fb* h, const double* x, long len, double* out, hz_state::StateArgs* a) {
+    if (h->order > 2) {
+        hz::set_error("fb_state_chained: order %d (at most 2 fit beside another kernel)", h->order);
         return HZ_E_INVALID;
     }
-    return state_args(h, x, len, out, pieces, a);
+    return state_args(h, x, len, out, a);
 }
 
 }  // namespace hz_fbi
