@@ -649,6 +649,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     RespKernel ki = so == 1 ? resp_inv_kernel<1> : so == 2 ? resp_inv_kernel<2> : resp_inv_kernel<0>;
     hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0))), dim3(kThreads), 0, h->stream, a, st);
     HZ_TRY_HIP(hipGetLastError());
+    if (chained) HZ_TRY(fb_state_combine(h, st, h->stream));   // pieces of a small bank
     if (e && chained) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
     if (e && !chained) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     R.hcur ^= 1;   // the inverse kernel wrote the history after the call

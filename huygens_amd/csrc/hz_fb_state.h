@@ -30,9 +30,9 @@
 // workgroup: hz_fb_resp.hip runs the pass as extra workgroups of its transform kernels.
 //
 // Banks with fewer band groups than CUs split the window into equal runs of tiles ("pieces", one
-// workgroup each); they store their partials and the last workgroup of a band group to arrive
-// (device-scope counter) combines them by Horner steps, S = P (... (P S_0 + S_1) ...) + S_last,
-// P = (M^64)^(tiles per piece), and re-arms the counter.
+// workgroup each); they store their partials, combined by Horner steps, S = P (... (P S_0 + S_1)
+// ...) + S_last, P = (M^64)^(tiles per piece): standalone, by the last workgroup of a band group to
+// arrive (device-scope counter, re-armed); inside the inverse kernel, by a small kernel after it.
 #pragma once
 
 #include "hz_fb_impl.h"
@@ -45,14 +45,23 @@ constexpr int kTile = 64 * kL;      // 8192 samples per tile
 constexpr int kCols = 32;           // band-state columns per workgroup (two 16-wide MFMA blocks)
 constexpr int kKE = 33;             // MFMA k-steps per chunk (132 tap slots)
 constexpr int kThreads = 256;       // 4 waves
-// B operands per workgroup: 2 x kKE x 64 doubles, padded to whole 1 KiB pieces per wave
-constexpr int kEop = (2 * kKE * 64 + 2 * kThreads - 1) / (2 * kThreads) * (2 * kThreads);
-// then the M^e weights of every column: W[sb][col][p][j] = row k of M^e(p) at column k ^ j (j < 4),
-// e(p) = 64 (the tile carry), 4, 0..3, 16, 32, 48 (the end's Horner steps); padded to whole 1 KiB
-// pieces per wave
+// A band group's operand block (fb_state_ops_kernel): per band kEs doubles -- pin E_0[i] for
+// i < XW (the end-state map's first row: its row k is E_0 shifted by k taps past the O history
+// taps), zeros up to kEh, then the history taps pin E_H[k O + i] -- followed by the M^e weights of
+// every column: W[sb][col][p][j] = row k of M^e(p) at column k ^ j (j < 4), e(p) = 64 (the tile
+// carry), 4, 0..3, 16, 32, 48 (the end's Horner steps).  A lane gathers its 66 B operands from
+// its band's row (the two state columns of a band share it: 31 KB per group at O = 2 instead of
+// the 48 KB of operands laid out per lane)
+constexpr int kEh = 136, kEs = 152;
 constexpr int kPows = 9;
-constexpr int kW = (2 * 16 * kPows * 4 + 2 * kThreads - 1) / (2 * kThreads) * (2 * kThreads);
-constexpr int kGrp = kEop + kW;     // doubles per band group (fb_state_ops_kernel)
+constexpr int kW = 2 * 16 * kPows * 4;
+template <int O>
+constexpr int grp_e() { return (kCols / (O == 3 ? 4 : O)) * kEs; }
+template <int O>
+constexpr int grp_doubles() { return grp_e<O>() + kW; }
+inline int grp_doubles(int O) {
+    return O == 1 ? grp_doubles<1>() : O == 2 ? grp_doubles<2>() : O == 3 ? grp_doubles<3>() : grp_doubles<4>();
+}
 __host__ __device__ constexpr int pow_of(int p) { return p == 0 ? 64 : p == 1 ? 4 : p < 6 ? p - 2 : 16 * (p - 5); }
 
 template <int O>
@@ -62,6 +71,7 @@ struct StateGeom {
     static constexpr int XW = kL + O;               // chunk input taps
     static constexpr int S = O & 1;                 // tap shift: tap pairs 16-B aligned in x
     static_assert(XW + S <= 4 * kKE, "taps fit the k-steps");
+    static_assert(4 * kKE - 1 - S + (O - 1) < kEh && kEh + O * O <= kEs, "band row layout");
 };
 
 inline int bands_per_group(int O) { return kCols / (O == 3 ? 4 : O); }
@@ -146,7 +156,7 @@ __device__ __forceinline__ void state_tile(double (&a)[kKE], const double (&b)[2
 struct StateArgs {
     const double* rec;     // chunk-128 records [N][rs]
     int rs;                // record size (doubles)
-    const double* eop;     // [G][kGrp] pin E operands [2][kKE][64], M^e weights (fb_state_ops_kernel)
+    const double* eop;     // [G][grp_doubles<O>] band rows of pin E, M^e weights (fb_state_ops_kernel)
     const double* x;       // [len] the window
     long len;
     int nbands;
@@ -155,6 +165,9 @@ struct StateArgs {
     int nseg;              // pieces of the window (equal runs of tps tiles)
     double* part;          // [G][nseg][kCols] piece partials (nseg > 1)
     unsigned* count;       // [G] arrival counters (nseg > 1; 0 between launches)
+    int deferred;          // nseg > 1 inside another kernel: partials only, combined by a kernel of
+                           // its own after it (fb_state_combine_kernel: the agent-scope fences of
+                           // the last-arrival combine cost 8 us beside the inverse transforms)
     double* out;           // [N][O]
 };
 
@@ -233,10 +246,11 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
     };
     // rows k of the band's M^e as weights of the columns k ^ j, from the group's weight block
     // (p: pow_of); buffer loads off the block's resource (32-bit offsets, no address registers)
-    const __amdgpu_buffer_rsrc_t er = state_rsrc(a.eop + (long)g * kGrp, kGrp);
+    constexpr int kGrpO = grp_doubles<O>(), kEO = grp_e<O>();
+    const __amdgpu_buffer_rsrc_t er = state_rsrc(a.eop + (long)g * kGrpO, kGrpO);
     auto ld = [&](int i) { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(er, 8 * i, 0, 0)); };
     auto wrow = [&](int sb, int p, double (&wt)[OP]) {
-        const int w = kEop + ((sb * 16 + col) * kPows + p) * 4;
+        const int w = kEO + ((sb * 16 + col) * kPows + p) * 4;
 #pragma unroll
         for (int j = 0; j < OP; ++j) wt[j] = ld(w + j);
     };
@@ -247,6 +261,16 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
     double m64[2][OP];
     wrow(0, 0, m64[0]);
     wrow(1, 0, m64[1]);
+    // B operand (sb, q) of this lane: pin E[k][tap], tap = tap_slot(q, lg) - S, from its band's row
+    // (tap >= O: E_0[tap + k]; tap < O: E_H[k O + tap]; columns k >= O and taps < 0: 0)
+    const int k = col % OP;
+    const double kmask = k < O ? 1.0 : 0.0;
+    auto b_idx = [&](int sb, int q) {
+        const int row = ((16 * sb + col) / OP) * kEs;
+        const int tap = tap_slot(q, lg) - Gm::S;
+        if (q >= 2) return row + tap + k;   // tap >= 7 >= O
+        return tap < 0 ? row + kEh - 1 : tap < O ? row + kEh + (k < O ? k : 0) * O + tap : row + tap + k;
+    };
     double xa[kKE], bq[2][kKE];
     {
         const int v = voff(0);
@@ -257,13 +281,13 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
             xa[2 * j + 1] = __builtin_bit_cast(double, ((unsigned long long)pr.w << 32) | pr.z);
 #pragma unroll
             for (int u = 2 * j; u < 2 * j + 2; ++u) {
-                bq[0][u] = ld(u * 64 + lane);
-                bq[1][u] = ld((kKE + u) * 64 + lane);
+                bq[0][u] = ld(b_idx(0, u)) * kmask;
+                bq[1][u] = ld(b_idx(1, u)) * kmask;
             }
         }
         xa[32] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, v + (int)sizeof(double) * (128 + lg), 0, 0));
-        bq[0][32] = ld(32 * 64 + lane);
-        bq[1][32] = ld((kKE + 32) * 64 + lane);
+        bq[0][32] = ld(b_idx(0, 32)) * kmask;
+        bq[1][32] = ld(b_idx(1, 32)) * kmask;
     }
     // the carry weights complete here (the oldest loads): redefined by an empty asm, so the loop's
     // waits track only the x loads (the compiler otherwise waited for every load in flight before
@@ -302,10 +326,10 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
             if (b < a.nbands && kk < O) a.out[(long)b * O + kk] = S;
         } else {
             prow[(long)pc * kCols + t] = S;
-            __threadfence();   // visible at agent scope before the arrival below
+            if (!a.deferred) __threadfence();   // visible at agent scope before the arrival below
         }
     }
-    if (a.nseg == 1) return;
+    if (a.nseg == 1 || a.deferred) return;
     // the last workgroup of this band group to arrive combines the partials
     __syncthreads();
     if (t == 0) {
@@ -328,4 +352,5 @@ namespace hz_fbi {
 // the band-state pass's arguments for a launch inside another kernel (orders <= 2): G nseg extra
 // workgroups, workgroup i running state_group<O>(a, i % G, i / G, lds)
 int fb_state_chained(hz_fb* h, const double* x, long len, double* out, hz_state::StateArgs* a);
+int fb_state_combine(hz_fb* h, const hz_state::StateArgs& a, hipStream_t st);   // after it, when a.nseg > 1
 }  // namespace hz_fbi

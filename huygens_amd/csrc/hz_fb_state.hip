@@ -15,38 +15,47 @@ __global__ __launch_bounds__(kThreads) void fb_state_kernel(StateArgs a) {
 }
 
 // orders <= 2 within 256 registers: two waves per SIMD, room for other kernels' waves beside it
+// the pieces' partials of a pass run inside another kernel, combined per band
+template <int O>
+__global__ __launch_bounds__(256) void fb_state_combine_kernel(StateArgs a) {
+    using Gm = StateGeom<O>;
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.nbands) return;
+    const int g = b / Gm::BANDS, t = b % Gm::BANDS;
+    combine_pieces<O>(a, b, a.part + (long)g * a.nseg * kCols + t * Gm::OP, a.tps);
+}
+
 template <int O>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void fb_state_kernel_w2(StateArgs a) {
     __shared__ StateLds L;
     state_group<O>(a, blockIdx.x, blockIdx.y, L);
 }
 
-// a band group's block for the state pass: eop[g kGrp + (sb kKE + q) 64 + lane] =
-// pin E[tap_slot(q, lane >> 4) - s][column 16 sb + (lane & 15)] (zero outside the bank, the taps
-// and O), then eop[g kGrp + kEop + ((sb 16 + col) kPows + p) 4 + j] = row k of M^pow_of(p) at
-// column k ^ j (the chunk-128 records' QC powers; zero where k ^ j >= O): one LDS-DMA per
-// workgroup instead of record gathers from HBM at its start and end
+// a band group's block for the state pass (hz_fb_state.h, grp_doubles<O>): per band its row --
+// pin E_0[i] (i < XW; zeros to kEh), pin E_H[k O + i] (k, i < O) -- then the M^e weights
+// W[sb][col][p][j] = row k of M^pow_of(p) at column k ^ j (the chunk-128 records' QC powers;
+// zero where k ^ j >= O or past the bank): one coalesced block per workgroup instead of record
+// gathers from HBM at its start and end
 template <int O>
 __global__ __launch_bounds__(256) void fb_state_ops_kernel(const double* __restrict__ rec, int rs,
                                                            const double* __restrict__ pin, int nbands, int G,
                                                            double* __restrict__ eop) {
     using R = RecL<O, kL>;
     using Gm = StateGeom<O>;
-    constexpr int OP = Gm::OP, XW = Gm::XW;
+    constexpr int OP = Gm::OP, XW = Gm::XW, kGrpO = grp_doubles<O>(), kEO = grp_e<O>();
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (long)G * kGrp) return;
-    const int g = (int)(i / kGrp), r = (int)(i % kGrp);
+    if (i >= (long)G * kGrpO) return;
+    const int g = (int)(i / kGrpO), r = (int)(i % kGrpO);
     double v = 0.0;
-    if (r < kEop) {
-        const int lane = r & 63, q = (r >> 6) % kKE, sb = r / (64 * kKE);   // sb == 2: padding
-        const int col = lane & 15, k = col % OP, tap = tap_slot(q, lane >> 4) - Gm::S;
-        const int band = g * Gm::BANDS + (16 * sb + col) / OP;
-        if (sb < 2 && band < nbands && k < O && tap >= 0 && tap < XW) {
+    if (r < kEO) {
+        const int band = g * Gm::BANDS + r / kEs, e = r % kEs;
+        if (band < nbands) {
             const double* rb = rec + (long)band * rs;
-            v = pin[band] * (tap < O ? rb[R::EH + k * O + tap] : (tap + k < XW ? rb[R::E0 + tap + k] : 0.0));
+            if (e < XW) v = pin[band] * rb[R::E0 + e];
+            else if (e >= kEh && e - kEh < O * O) v = pin[band] * rb[R::EH + (e - kEh)];
         }
     } else {
-        const int w = r - kEop, j = w & 3, p = (w >> 2) % kPows, sc = w / (4 * kPows);   // sc = sb 16 + col
+        const int w = r - kEO, j = w & 3, p = (w >> 2) % kPows, sc = w / (4 * kPows);   // sc = sb 16 + col
         const int sb = sc / 16, col = sc % 16, k = col % OP;
         const int band = g * Gm::BANDS + (16 * sb + col) / OP;
         if (sb < 2 && j < OP && band < nbands && k < O && (k ^ j) < O)
@@ -86,7 +95,7 @@ int fb_state_prepare(hz_fb* h) {
     hz_fb::LtiRecSet& set = h->lti_set[kLtiGeomChunk128];
     hz_fb::Resp& R = h->resp;
     const int G = (h->N + bands_per_group(O) - 1) / bands_per_group(O);
-    const size_t need = (size_t)G * kGrp;
+    const size_t need = (size_t)G * grp_doubles(O);
     if (need > R.sop_cap) {
         HZ_TRY_HIP(hipDeviceSynchronize());
         if (R.d_sop) HZ_TRY_HIP(hipFree(R.d_sop));
@@ -146,6 +155,7 @@ static int state_args(hz_fb* h, const double* x, long len, double* out, StateArg
     a->part = R.d_spart;
     a->count = R.d_scount;
     a->out = out;
+    a->deferred = 0;
     return HZ_OK;
 }
 
@@ -162,7 +172,23 @@ int fb_state_chained(hz_fb* h, const double* x, long len, double* out, hz_state:
         hz::set_error("fb_state_chained: order %d (at most 2 fit beside another kernel)", h->order);
         return HZ_E_INVALID;
     }
-    return state_args(h, x, len, out, a);
+    HZ_TRY(state_args(h, x, len, out, a));
+    a->deferred = a->nseg > 1 ? 1 : 0;
+    return HZ_OK;
+}
+
+int fb_state_combine(hz_fb* h, const hz_state::StateArgs& a, hipStream_t st) {
+    if (a.nseg <= 1) return HZ_OK;
+    const unsigned grid = (unsigned)((h->N + 255) / 256);
+    switch (h->order) {
+    case 1: hipLaunchKernelGGL(fb_state_combine_kernel<1>, dim3(grid), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(fb_state_combine_kernel<2>, dim3(grid), dim3(256), 0, st, a); break;
+    default:
+        hz::set_error("fb_state_combine: order %d", h->order);
+        return HZ_E_INVALID;
+    }
+    HZ_TRY_HIP(hipGetLastError());
+    return HZ_OK;
 }
 
 }  // namespace hz_fbi
