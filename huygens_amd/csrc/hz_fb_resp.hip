@@ -321,6 +321,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     hz2k::Lds& s = u.fft;
     const int t = threadIdx.x;
     const long b = blockIdx.x;
+#ifdef HZ_DIAG_STAMPS
+    long long* stp = SO > 0 && st.stamps ? st.stamps + ((long)st.G * st.nseg + b) * 4 : nullptr;
+    if (stp && t == 0) {
+        stp[0] = __builtin_amdgcn_s_memrealtime();
+        stp[3] = ((long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) | __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    }
+#endif
     const double2* y = a.Y + b * kH;
     double2 ya[4], yb[4], w[4];
 #pragma unroll
@@ -382,6 +389,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         a.pg_next[2 * n + 1] = gb + a.sg_n * (G0 - gb);
     }
     if (g < a.O) a.xhist_next[g] = a.x[a.n - 1 - g];
+#ifdef HZ_DIAG_STAMPS
+    if (stp && t == 0) stp[1] = stp[2] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // history after a call: the last K samples of [hist | x]
@@ -650,6 +660,9 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0))), dim3(kThreads), 0, h->stream, a, st);
     HZ_TRY_HIP(hipGetLastError());
     if (chained) HZ_TRY(fb_state_combine(h, st, h->stream));   // pieces of a small bank
+#ifdef HZ_DIAG_STAMPS
+    if (chained && R.calls == 30) fb_state_stamps_dump(st, B, R.calls);
+#endif
     if (e && chained) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
     if (e && !chained) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     R.hcur ^= 1;   // the inverse kernel wrote the history after the call

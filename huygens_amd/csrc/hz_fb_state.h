@@ -169,6 +169,7 @@ struct StateArgs {
                            // its own after it (fb_state_combine_kernel: the agent-scope fences of
                            // the last-arrival combine cost 8 us beside the inverse transforms)
     double* out;           // [N][O]
+    long long* stamps;     // (diagnostic builds, -DHZ_DIAG_STAMPS) [pieces][G][4] per-workgroup stamps
 };
 
 struct StateLds {
@@ -239,6 +240,13 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
     const int lg = lane >> 4;                   // lane group: the MFMA's k index
     const int pc = seg, ntl = a.tps;
     const __amdgpu_buffer_rsrc_t xr = state_rsrc(a.x, a.len);
+#ifdef HZ_DIAG_STAMPS
+    long long* stp = a.stamps ? a.stamps + ((long)seg * a.G + g) * 4 : nullptr;
+    if (stp && threadIdx.x == 0) {
+        stp[0] = __builtin_amdgcn_s_memrealtime();
+        stp[3] = ((long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) | __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    }
+#endif
     // tile it's A offset (bytes) of this lane's chunk 64 it + 16 m + col of the piece
     const long t0 = (long)seg * a.tps * kTile;
     auto voff = [&](int it) {
@@ -279,10 +287,21 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
             const u32x4 pr = __builtin_amdgcn_raw_buffer_load_b128(xr, v + (int)sizeof(double) * (8 * j + 2 * lg), 0, 0);
             xa[2 * j] = __builtin_bit_cast(double, ((unsigned long long)pr.y << 32) | pr.x);
             xa[2 * j + 1] = __builtin_bit_cast(double, ((unsigned long long)pr.w << 32) | pr.z);
+            if (j == 0) {
 #pragma unroll
-            for (int u = 2 * j; u < 2 * j + 2; ++u) {
-                bq[0][u] = ld(b_idx(0, u)) * kmask;
-                bq[1][u] = ld(b_idx(1, u)) * kmask;
+                for (int u = 0; u < 2; ++u) {
+                    bq[0][u] = ld(b_idx(0, u)) * kmask;
+                    bq[1][u] = ld(b_idx(1, u)) * kmask;
+                }
+            } else {
+                // k-steps 2j, 2j + 1 read adjacent row entries: one 16-B load (8-B aligned) per
+                // pair keeps the prologue's loads under the 63 a wave can have in flight
+#pragma unroll
+                for (int sb = 0; sb < 2; ++sb) {
+                    const u32x4 pb = __builtin_amdgcn_raw_buffer_load_b128(er, 8 * b_idx(sb, 2 * j), 0, 0);
+                    bq[sb][2 * j] = __builtin_bit_cast(double, ((unsigned long long)pb.y << 32) | pb.x) * kmask;
+                    bq[sb][2 * j + 1] = __builtin_bit_cast(double, ((unsigned long long)pb.w << 32) | pb.z) * kmask;
+                }
             }
         }
         xa[32] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, v + (int)sizeof(double) * (128 + lg), 0, 0));
@@ -296,7 +315,13 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
     for (int j = 0; j < OP; ++j) asm volatile("" : "+v"(m64[0][j]), "+v"(m64[1][j]));
     f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     // tile it from xa, reloaded with tile it + 1 as it goes (past the last tile: unused loads)
+#ifdef HZ_DIAG_STAMPS
+    if (stp && threadIdx.x == 0) stp[1] = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int it = 0; it < ntl; ++it) state_tile<OP>(xa, bq, m64, it > 0, xr, voff(it + 1), lg, acc0, acc1);
+#ifdef HZ_DIAG_STAMPS
+    if (stp && threadIdx.x == 0) stp[2] = __builtin_amdgcn_s_memrealtime();
+#endif
     // S = sum_c M^(63-c) A_c, lane rows c = 16m + lg + 4 rr, by Horner steps: over rr with M^4
     // (anchored at row 16m + lg + 12), M^(3-lg) (row 16m + 15), the sum over lg, M^(16(3-m))
     // (row 63), then the sum over the row blocks (waves)
@@ -353,4 +378,7 @@ namespace hz_fbi {
 // workgroups, workgroup i running state_group<O>(a, i % G, i / G, lds)
 int fb_state_chained(hz_fb* h, const double* x, long len, double* out, hz_state::StateArgs* a);
 int fb_state_combine(hz_fb* h, const hz_state::StateArgs& a, hipStream_t st);   // after it, when a.nseg > 1
+#ifdef HZ_DIAG_STAMPS
+void fb_state_stamps_dump(const hz_state::StateArgs& a, int nfft, long call);
+#endif
 }  // namespace hz_fbi

@@ -3,6 +3,11 @@
 // the host side of both launch forms (standalone, or pieces inside the transform kernels).
 #include "hz_fb_state.h"
 
+#ifdef HZ_DIAG_STAMPS
+#include <cstdio>
+#include <map>
+#endif
+
 namespace {
 
 using namespace hz_fbi;
@@ -156,8 +161,64 @@ static int state_args(hz_fb* h, const double* x, long len, double* out, StateArg
     a->count = R.d_scount;
     a->out = out;
     a->deferred = 0;
+    a->stamps = nullptr;
+#ifdef HZ_DIAG_STAMPS
+    static long long* d_st = nullptr;
+    if (!d_st) HZ_TRY_HIP(hipMalloc(&d_st, sizeof(long long) * 4 * 64 * 8192));
+    a->stamps = d_st;
+#endif
     return HZ_OK;
 }
+
+#ifdef HZ_DIAG_STAMPS
+// (diagnostic builds) the last launch's workgroup stamps: state workgroups [0, G nseg) (start,
+// loop start, loop end, HW id), then the inverse kernel's nfft transform workgroups (start, end, end,
+// HW id); which of them shared a CU while running
+void fb_state_stamps_dump(const StateArgs& a, int nfft, long call) {
+    const int n = a.G * a.nseg, nt = n + nfft;
+    std::vector<long long> v((size_t)nt * 4);
+    if (hipDeviceSynchronize() != hipSuccess) return;
+    if (hipMemcpy(v.data(), a.stamps, sizeof(long long) * v.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
+    long long t0 = v[0];
+    for (int i = 0; i < nt; ++i) t0 = std::min(t0, v[(size_t)i * 4]);
+    // CU key: XCC, SE, SH, CU (HW_ID bits 15:8)
+    auto cu = [&](int i) { const long long hw = v[(size_t)i * 4 + 3]; return ((hw >> 32) & 0xf) << 8 | ((hw >> 8) & 0xff); };
+    auto overlap = [&](int i, int j) { return v[(size_t)i * 4] < v[(size_t)j * 4 + 2] && v[(size_t)j * 4] < v[(size_t)i * 4 + 2]; };
+    std::map<long long, int> scu, fcu;
+    int ss = 0, sf = 0, ff = 0;
+    for (int i = 0; i < nt; ++i) (i < n ? scu : fcu)[cu(i)]++;
+    for (int i = 0; i < n; ++i) {
+        bool s2 = false, f2 = false;
+        for (int j = 0; j < nt; ++j)
+            if (j != i && cu(j) == cu(i) && overlap(i, j)) (j < n ? s2 : f2) = true;
+        ss += s2;
+        sf += f2;
+    }
+    for (int i = n; i < nt; ++i)
+        for (int j = n; j < nt; ++j)
+            if (j != i && cu(j) == cu(i) && overlap(i, j)) { ++ff; break; }
+    double pro = 0, loop = 0, st_max = 0, loop_max = 0, fs_max = 0, fe_max = 0, fdur = 0;
+    for (int i = 0; i < n; ++i) {
+        const long long* s = &v[(size_t)i * 4];
+        pro += (s[1] - s[0]) * 0.01;
+        loop += (s[2] - s[1]) * 0.01;
+        st_max = std::max(st_max, (s[0] - t0) * 0.01);
+        loop_max = std::max(loop_max, (s[2] - t0) * 0.01);
+    }
+    for (int i = n; i < nt; ++i) {
+        const long long* s = &v[(size_t)i * 4];
+        fs_max = std::max(fs_max, (s[0] - t0) * 0.01);
+        fe_max = std::max(fe_max, (s[2] - t0) * 0.01);
+        fdur += (s[2] - s[0]) * 0.01;
+    }
+    std::fprintf(stderr, "[state stamps call %ld] %d state workgroups (%d pieces x %d groups, %d tiles each) on %zu CUs; "
+                 "%d overlapped another state workgroup on their CU, %d a transform workgroup; mean prologue %.2f us, "
+                 "loop %.2f us; starts up to %.2f us, last loop end %.2f us | %d transform workgroups on %zu CUs, %d "
+                 "beside another; mean %.2f us, starts up to %.2f us, last end %.2f us\n", call, n, a.nseg, a.G,
+                 a.tps, scu.size(), ss, sf, pro / n, loop / n, st_max, loop_max, nfft, fcu.size(), ff,
+                 nfft ? fdur / nfft : 0.0, fs_max, fe_max);
+}
+#endif
 
 int fb_state_window(hz_fb* h, const double* x, long len, double* out, hipStream_t st) {
     StateArgs a;
