@@ -29,6 +29,7 @@
 // setter needs them (HZ_FB_RESP_LAZY).
 // Multi-GPU: time-range shards (hz_fb_set_bank_response + hz_fb_set_time_shard) convolve one
 // rank's run of output blocks with the whole bank's response; DESIGN.md 3.6 and 5.
+#include <cstdio>
 #include <cstdlib>
 
 #include "hz_fb_impl.h"
@@ -56,6 +57,18 @@ constexpr long kBandsPerSample = 256;
 // MFMA chain starves the waves beside it on its SIMD: the older wave issues first; s_setprio
 // changed nothing)
 static_assert(kH == hz2k::kN && kThreads == hz2k::kT, "hz_fft2k.h: 2048 points on 256 threads");
+
+#ifdef HZ_DIAG_STAMPS
+// (diagnostic builds) per-workgroup stamps of the forward [0] and MAC [1] kernels: start, operands
+// arrived, transform / MACs done, end
+__device__ long long g_diag[2][1024][4];
+__device__ __forceinline__ void diag_stamp(int k, int i) {
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_diag[k][blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();
+}
+#define HZ_DIAG_AT(k, i) diag_stamp(k, i)
+#else
+#define HZ_DIAG_AT(k, i) ((void)0)
+#endif
 
 // Aggregate impulse response, one wave (64 bands) per workgroup: part[g][tau] = sum over the
 // group's bands of gin_n r_n[tau], r_n = band n's response to a unit impulse with pre = pin_n,
@@ -123,8 +136,10 @@ __global__ __launch_bounds__(256) void resp_hsum_kernel(const double* __restrict
 // is kept apart (nyq), so the MAC is one complex product per stored bin.
 template <class Load>
 __device__ __forceinline__ void real_window_fwd(hz2k::Lds& s, Load load, const double2* __restrict__ tw,
-                                                double2* __restrict__ zrow, double* __restrict__ nyq) {
+                                                double2* __restrict__ zrow, double* __restrict__ nyq,
+                                                bool stamps = false) {
     const int t = threadIdx.x;
+    if (stamps) HZ_DIAG_AT(0, 0);
     // every global load of the thread (data, pass twiddles, split twiddles) before the first use
     double vr[kPT], vi[kPT];
 #pragma unroll
@@ -138,7 +153,14 @@ __device__ __forceinline__ void real_window_fwd(hz2k::Lds& s, Load load, const d
     double2 w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] = tw[t + i * kThreads];
+#ifdef HZ_DIAG_STAMPS
+    if (stamps) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        HZ_DIAG_AT(0, 1);
+    }
+#endif
     hz2k::fwd(s, vr, vi, ft);   // ends with a barrier
+    if (stamps) HZ_DIAG_AT(0, 2);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int k = t + i * kThreads, kb = (kH - k) & (kH - 1);
@@ -155,6 +177,7 @@ __device__ __forceinline__ void real_window_fwd(hz2k::Lds& s, Load load, const d
         const int pm = hz::pad16(1);
         zrow[kH / 2] = make_double2(s.re[pm], -s.im[pm]);
     }
+    if (stamps) HZ_DIAG_AT(0, 3);
 }
 
 // Partition spectra H_p = FFT(h[pP, (p+1)P) zero-padded to F) / F (the inverse is unnormalised;
@@ -208,12 +231,13 @@ union RespLds {
     hz_state::StateLds st;
 };
 
+
 // Z_j = the spectrum of W_j = u[jP, jP + F)
 __global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a) {
     __shared__ hz2k::Lds s;
     const long m0 = (long)blockIdx.x * kP;
     real_window_fwd(
-        s, [&](int m) { return resp_u(a, m0 + m); }, a.tw, a.Z + (long)blockIdx.x * kH, a.Zn + blockIdx.x);
+        s, [&](int m) { return resp_u(a, m0 + m); }, a.tw, a.Z + (long)blockIdx.x * kH, a.Zn + blockIdx.x, true);
 }
 
 // Y_b[q] = sum_{p < Q} H_p[q] Z_{b+Q-1-p}[q] for b in [b0, b0 + R): thread = bin q x R output
@@ -229,6 +253,7 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
     constexpr int kBinGroups = kH / 256;
     const int q = (blockIdx.x % kBinGroups) * blockDim.x + threadIdx.x;   // bin
     const int b0 = (blockIdx.x / kBinGroups) * R;
+    HZ_DIAG_AT(1, 0);
     double ar[R], ai[R], zr[R], zi[R];
     const long base = (long)b0 + Q - 1;
 #pragma unroll
@@ -263,8 +288,13 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
             hv[p] = H[(long)p * kH + q];
             zv[p] = Z[zrow(p)];
         }
+#ifdef HZ_DIAG_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        HZ_DIAG_AT(1, 1);
+#endif
 #pragma unroll
         for (int p = 0; p < QP; ++p) step(p % R, hv[p], zv[p]);
+        HZ_DIAG_AT(1, 2);
     } else {
         double2 hb[R], zb[R];
         auto fetch = [&](int p0) {
@@ -290,6 +320,7 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
 #pragma unroll
     for (int r = 0; r < R; ++r)
         if (b0 + r < B) Y[(long)(b0 + r) * kH + q] = make_double2(ar[r], ai[r]);
+    HZ_DIAG_AT(1, 3);
 }
 
 typedef void (*MacKernel)(const double2*, const double2*, double2*, int, int, int);
@@ -661,7 +692,26 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     HZ_TRY_HIP(hipGetLastError());
     if (chained) HZ_TRY(fb_state_combine(h, st, h->stream));   // pieces of a small bank
 #ifdef HZ_DIAG_STAMPS
-    if (chained && R.calls == 30) fb_state_stamps_dump(st, B, R.calls);
+    if (chained && R.calls == 30) {
+        fb_state_stamps_dump(st, B, R.calls);
+        static long long hv[2][1024][4];
+        if (hipMemcpyFromSymbol(hv, HIP_SYMBOL(g_diag), sizeof(hv)) == hipSuccess) {
+            const int cnt[2] = {std::min((int)nz, 1024), std::min(nmac, 1024)};
+            for (int k = 0; k < 2; ++k) {
+                long long t0 = hv[k][0][0];
+                double ph[3] = {0, 0, 0}, smax = 0, emax = 0;
+                for (int i = 0; i < cnt[k]; ++i) t0 = std::min(t0, hv[k][i][0]);
+                for (int i = 0; i < cnt[k]; ++i) {
+                    for (int j = 0; j < 3; ++j) ph[j] += (hv[k][i][j + 1] - hv[k][i][j]) * 0.01 / cnt[k];
+                    smax = std::max(smax, (hv[k][i][0] - t0) * 0.01);
+                    emax = std::max(emax, (hv[k][i][3] - t0) * 0.01);
+                }
+                std::fprintf(stderr, "[%s stamps] %d workgroups: mean operands %.2f us, compute %.2f us, stores %.2f us; "
+                             "starts up to %.2f us, last end %.2f us\n", k ? "mac" : "fwd", cnt[k], ph[0], ph[1], ph[2],
+                             smax, emax);
+            }
+        }
+    }
 #endif
     if (e && chained) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
     if (e && !chained) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
