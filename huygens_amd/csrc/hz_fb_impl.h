@@ -221,8 +221,6 @@ int fb_lti_gemm_launch(const double* gs, const double* kt, int bs_pad, double* p
 bool fb_converged(hz_fb* h);
 int fb_launch_lti(hz_fb* h, int geom, const double* d_in, double* d_out, long n);
 long fb_horizon(const hz_fb* h, int log2_bound);   // samples K with ||M^K|| < 2^log2_bound for every band (-1: > 2^18)
-// zero-start band states at the end of x[0, len) (len a multiple of 4096; the O samples before
-// x read as xzero) -> out[band][O]; zeros: N O zeros (the carry's start)
 // zero-start band states after the window x[0, len) (len a multiple of 8192) -> out[band][O], on
 // stream st: the stationary engine's band-state pass (hz_fb_state.hip)
 int fb_state_window(hz_fb* h, const double* x, long len, double* out, hipStream_t st);
