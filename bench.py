@@ -576,7 +576,7 @@ def main():
 
     # streaming figure: one process() call per 1024-sample block (per-band engine: calls below
     # the stationary minimum; last, since short calls restart the stationary history)
-    stream_rate = None
+    stream_rate, stream_detail = None, {}
     if args.stream_blocks > 0:
         armed = False
         fb.arm_time_shard(False) if tshard else None
@@ -595,6 +595,36 @@ def main():
         if world > 1:
             tstream = ar(tstream, dist.ReduceOp.MAX)
         stream_rate = N_BANDS * B * nb / tstream
+        # the same blocks again with HIP events on the handle's stream: the GPU's share of a block
+        # (the rest of the wall time per block is the host's call and launch latency)
+        fb.profile(True)
+        for i in range(nb):
+            fb.process_device(x.data_ptr() + 8 * B * i, y.data_ptr() + 8 * B * i, B)
+            if world > 1:
+                dist.reduce(y[i * B:(i + 1) * B], dst=0, op=dist.ReduceOp.SUM)
+        barrier()
+        s_seg, s_mix, s_red, s_calls = fb.profile_read()
+        s_path, s_chunk = fb.last_path(), fb.lti_chunk()
+        fb.profile(False)
+        gpu_us = 1e3 * (s_seg + s_mix + s_red) / max(1, s_calls)
+        wall_us = 1e6 * N_BANDS * B / stream_rate
+        stream_detail = {
+            "path": {HZ_FB_PATH_LTI: "lti"}.get(s_path, str(s_path)), "chunk": s_chunk,
+            "kernels": ([f"fb_lti_kernel<2, {s_chunk}, *>", f"fb_lti_reduce_short_kernel<2, {s_chunk}>"]
+                        if s_path == HZ_FB_PATH_LTI else None),
+            # event-bracketed (5 records per call, each adding its own latency: the sum exceeds
+            # the un-instrumented wall time per block); the split says where a block's time goes
+            "profiled_us_per_block": gpu_us,
+            "profiled_components_us": {"state_or_mix": 1e3 * s_mix / max(1, s_calls),
+                                       "reduce": 1e3 * s_red / max(1, s_calls)},
+            "roofline": {"bound": "latency: 2 dependent kernel launches per block",
+                         "reference_equivalent_tflops": FLOPS_PER_BAND_SAMPLE * N_BANDS * B / (wall_us * 1e-6) / 1e12
+                         if wall_us > 0 else None,
+                         "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": FLOPS_PER_BAND_SAMPLE * N_BANDS * B / (wall_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS
+                         if wall_us > 0 else None,
+                         "note": "reference recurrence's 18 flops per band-sample over the wall time per block"},
+        }
 
     total_band_samples = N_BANDS * S * args.steps
     value = total_band_samples / elapsed
@@ -722,7 +752,8 @@ def main():
             "per_sample": per_sample_rates(dev.index or 0) if (world == 1 and not args.no_per_sample) else None,
             "streaming": {"band_samples_per_s": stream_rate, "block": 1024,
                           "us_per_block": (1e6 * N_BANDS * 1024 / stream_rate) if stream_rate else None,
-                          "note": "one process() call per 1024-sample block, device-resident I/O"},
+                          "note": "one process() call per 1024-sample block, device-resident I/O",
+                          **stream_detail},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
