@@ -53,8 +53,41 @@ def shard_of(rank, world, N=N_BANDS):
     return _shard_of(rank, world, N)
 
 
+def cpu_quota():
+    """CPUs this process may use: min(affinity, cgroup CPU quota); without a cgroup quota, the
+    pool's per-GPU share when it is exported as OMP_NUM_THREADS (the GPU box sets it), else the
+    affinity.  -> (cpus, source)"""
+    import math
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):                       # cgroup v2: "<quota|max> <period>"
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = (float(q) / float(per), f"cgroup v2 {path} = {q}/{per}")
+        except (OSError, ValueError):
+            pass
+    if quota is None:                                                # cgroup v1
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = (q / per, f"cgroup v1 cpu.cfs_quota_us/cfs_period_us = {q}/{per}")
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        return max(1, min(aff, int(math.floor(quota[0] + 1e-9)))), quota[1] + f", affinity {aff}"
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        return min(aff, int(omp)), f"no cgroup CPU quota; OMP_NUM_THREADS={omp} (the pool's per-GPU CPU share), affinity {aff}"
+    return aff, f"no cgroup CPU quota, no OMP_NUM_THREADS: sched_getaffinity = {aff}"
+
+
 def cpu_info():
-    """Host CPU model (/proc/cpuinfo), logical CPUs of the machine and of this process."""
+    """Host CPU model (/proc/cpuinfo), logical CPUs of the machine, of this process, and its quota."""
     model = "unknown"
     try:
         for ln in open("/proc/cpuinfo"):
@@ -67,7 +100,8 @@ def cpu_info():
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count() or 1
-    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
+    q, src = cpu_quota()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable, "cpu_quota": q, "quota_source": src}
 
 
 def native_oracle():
@@ -170,15 +204,30 @@ def cpu_baseline(fwd, back, runs=5):
         return {"value": N * nsamp / dt, "unit": "band-samples/s", "threads": threads, "samples": nsamp,
                 "median_s": dt, "runs_s": times}
 
+    def stream_leg(nblocks, B=1024):
+        """the reference's execution model: ONE thread, one call per 1024-sample block"""
+        times = []
+        for _ in range(3):
+            fb = bank(0, N)
+            t0 = time.perf_counter()
+            for b in range(nblocks):
+                fb.process(x[b * B:(b + 1) * B])
+            times.append(time.perf_counter() - t0)
+        dt = float(np.median(times))
+        return {"value": N * B * nblocks / dt, "unit": "band-samples/s", "threads": 1, "blocks": nblocks,
+                "block": B, "us_per_block": 1e6 * dt / nblocks, "median_s": dt, "runs_s": times}
+
     one = leg(1, SR)                                       # 1 s of audio, whole bank, 1 thread
-    cores = max(1, min(16, info["usable_cpus"]))            # the box's CPU share is 16
+    cores = info["cpu_quota"]                               # cgroup quota / the pool's share / affinity
     allc = leg(cores, SAMPLES_PER_STEP)
+    streaming = stream_leg(94)                              # 2 s of audio in 1024-sample calls
     build = "-O3 -march=native -ffp-contract=off" if so else "-O3 -ffp-contract=off (in-tree build; gcc unavailable)"
     return {"value": allc["value"], "unit": "band-samples/s", "cores": cores, "kind": "port",
             "sample": (f"oracle/hz_oracle.c restatement of src/filterbank.h:170-187, {build}, median of {runs}: "
                        f"all {N} bands; 1 thread over {SR} samples (1 s), {cores} threads (bands split) over "
-                       f"{SAMPLES_PER_STEP} samples (10 s)"),
-            "threads_1": one, "all_cores": allc, "build": build, **info}
+                       f"{SAMPLES_PER_STEP} samples (10 s); streaming: 1 thread, 94 calls of 1024 samples "
+                       f"(median of 3)"),
+            "threads_1": one, "all_cores": allc, "streaming_1_thread": streaming, "build": build, **info}
 
 
 def fb_executed_flops(lti, L=32, O=2, N=N_BANDS):
@@ -213,6 +262,15 @@ def resp_step_flops(K, S, N, O=2):
     conv = (Q + B - 1) * fft + B * H * Q * 8.0 + B * fft
     state = N * K * (2.0 * O * 4 * math.ceil((128 + O) / 4) / 128) + N * 64 * 2.0 * O * O * (K // 8192)
     return conv, state
+
+
+def stream_block_flops(K, P=1024):
+    """FP64 flops of one streaming block (hz_fb_stream.hip): per column (33) the forward's stage 1
+    (2048 real x complex MACs, 4 flops each) and stage 3 (32 x 32 complex MACs after a twiddle, 8
+    flops each + 6), the partition MAC (K / P complex MACs per bin, 32 bins), the inverse column
+    (as stage 3); the last workgroup's combine (1024 outputs x 31 columns x 4 flops)."""
+    col = 2048 * 4 + 32 * (32 * 8 + 6) + (K // P) * 32 * 8 + 32 * (32 * 8 + 6)
+    return 33.0 * col + 1024 * 31 * 4.0
 
 
 def resp_inv_flops(S):
@@ -387,8 +445,8 @@ def main():
     dev = torch.device("cuda", local)
 
     from huygens_amd import Filterbank
-    from huygens_amd._lib import (HZ_FB_PATH_GENERAL, HZ_FB_PATH_LTI, HZ_FB_PATH_RESPONSE, HZ_FB_RESP_EAGER,
-                                  HZ_FB_RESP_LAZY, HZ_FB_RESP_OFF)
+    from huygens_amd._lib import (HZ_FB_PATH_GENERAL, HZ_FB_PATH_LTI, HZ_FB_PATH_RESPONSE, HZ_FB_PATH_STREAM,
+                                  HZ_FB_RESP_EAGER, HZ_FB_RESP_LAZY, HZ_FB_RESP_OFF)
     from huygens_amd.shard import arm_when_ready, set_time_shards
     fwd, back = c2_coefficients()
     b0, cnt = shard_of(rank, world) if not args.emulate_world else shard_of(0, args.emulate_world)
@@ -574,56 +632,99 @@ def main():
     else:
         eng_ms_max = eng_ms
 
-    # streaming figure: one process() call per 1024-sample block (per-band engine: calls below
-    # the stationary minimum; last, since short calls restart the stationary history)
+    # streaming figure: one process() call per 1024-sample block -- the reference's audio callback
+    # (tests/resynthesis.cpp:33-42).  On the stationary bank these calls take the streaming engine
+    # (hz_fb_stream.hip: one launch per block); the per-band engine's rate is measured beside it
     stream_rate, stream_detail = None, {}
     if args.stream_blocks > 0:
         armed = False
-        fb.arm_time_shard(False) if tshard else None
+        if tshard:   # band shards stream their own bands' response; the mixes are reduced per block
+            fb.arm_time_shard(False)
+            fb.set_bank_response(np.zeros(0))
         B = 1024
         nb = min(args.stream_blocks, S // B)
-        for i in range(min(8, nb)):   # untimed: the short-call geometry's records are built on first use
-            fb.process_device(x.data_ptr() + 8 * B * i, y.data_ptr() + 8 * B * i, B)
-        barrier()
-        ts = time.perf_counter()
-        for i in range(nb):
-            fb.process_device(x.data_ptr() + 8 * B * i, y.data_ptr() + 8 * B * i, B)
+
+        def stream_blocks(n_blocks):
+            for i in range(n_blocks):
+                fb.process_device(x.data_ptr() + 8 * B * i, y.data_ptr() + 8 * B * i, B)
+                if world > 1:
+                    dist.reduce(y[i * B:(i + 1) * B], dst=0, op=dist.ReduceOp.SUM)
+
+        def stream_figure():
+            stream_blocks(min(8, nb))   # untimed: the engine's spectra / records are built on first use
+            barrier()
+            ts = time.perf_counter()
+            stream_blocks(nb)
+            barrier()
+            tst = time.perf_counter() - ts
             if world > 1:
-                dist.reduce(y[i * B:(i + 1) * B], dst=0, op=dist.ReduceOp.SUM)
-        barrier()
-        tstream = time.perf_counter() - ts
-        if world > 1:
-            tstream = ar(tstream, dist.ReduceOp.MAX)
+                tst = ar(tst, dist.ReduceOp.MAX)
+            s_path_ = fb.last_path()
+            # the same blocks with HIP events on the handle's stream: the GPU's share of a block
+            fb.profile(True)
+            stream_blocks(nb)
+            barrier()
+            s_seg, s_mix, s_red, s_calls = fb.profile_read()
+            s_chunk = fb.lti_chunk()
+            fb.profile(False)
+            return tst, s_path_, s_chunk, 1e3 * (s_seg + s_mix + s_red) / max(1, s_calls), \
+                1e3 * s_mix / max(1, s_calls), 1e3 * s_red / max(1, s_calls)
+
+        def e2e_figure():
+            """host buffers (pinned), one synchronous call per block: H2D + engine + D2H"""
+            hx = torch.empty(nb * B, dtype=torch.float64).pin_memory()
+            hy = torch.empty(nb * B, dtype=torch.float64).pin_memory()
+            hx.copy_(x[:nb * B].cpu())
+            for i in range(min(8, nb)):
+                fb.process_host(hx.data_ptr() + 8 * B * i, hy.data_ptr() + 8 * B * i, B)
+            ts = time.perf_counter()
+            for i in range(nb):
+                fb.process_host(hx.data_ptr() + 8 * B * i, hy.data_ptr() + 8 * B * i, B)
+            dt = time.perf_counter() - ts
+            return {"us_per_block": 1e6 * dt / nb, "band_samples_per_s": N_BANDS * B * nb / dt, "path": name_of(fb.last_path()),
+                    "note": "hz_fb_process on pinned host buffers: H2D copy + engine + D2H copy + stream synchronize "
+                            "per 1024-sample call (the reference's callback shape, host I/O included)"}
+
+        def name_of(p):
+            return {HZ_FB_PATH_GENERAL: "general", HZ_FB_PATH_LTI: "lti", HZ_FB_PATH_RESPONSE: "response",
+                    HZ_FB_PATH_STREAM: "stream"}.get(p, str(p))
+
+        tstream, s_path, s_chunk, gpu_us, mix_us, red_us = stream_figure()
         stream_rate = N_BANDS * B * nb / tstream
-        # the same blocks again with HIP events on the handle's stream: the GPU's share of a block
-        # (the rest of the wall time per block is the host's call and launch latency)
-        fb.profile(True)
-        for i in range(nb):
-            fb.process_device(x.data_ptr() + 8 * B * i, y.data_ptr() + 8 * B * i, B)
-            if world > 1:
-                dist.reduce(y[i * B:(i + 1) * B], dst=0, op=dist.ReduceOp.SUM)
-        barrier()
-        s_seg, s_mix, s_red, s_calls = fb.profile_read()
-        s_path, s_chunk = fb.last_path(), fb.lti_chunk()
-        fb.profile(False)
-        gpu_us = 1e3 * (s_seg + s_mix + s_red) / max(1, s_calls)
         wall_us = 1e6 * N_BANDS * B / stream_rate
+        e2e = e2e_figure() if world == 1 else None
+        # the per-band engine on the same 1024-sample calls (streaming engine off)
+        fb.tune_stream(False)
+        pb_t, pb_path, pb_chunk, pb_gpu_us, pb_mix, pb_red = stream_figure()
+        fb.tune_stream(True)
+        per_band = {"us_per_block": 1e6 * pb_t / nb, "band_samples_per_s": N_BANDS * B * nb / pb_t,
+                    "path": name_of(pb_path), "chunk": pb_chunk, "profiled_us_per_block": pb_gpu_us,
+                    "profiled_components_us": {"state_or_mix": pb_mix, "reduce": pb_red},
+                    "kernels": [f"fb_lti_kernel<2, {pb_chunk}, *>", f"fb_lti_reduce_short_kernel<2, {pb_chunk}>"]
+                    if pb_path == HZ_FB_PATH_LTI else None}
+        stream_flops = stream_block_flops(horizon)
         stream_detail = {
-            "path": {HZ_FB_PATH_LTI: "lti"}.get(s_path, str(s_path)), "chunk": s_chunk,
-            "kernels": ([f"fb_lti_kernel<2, {s_chunk}, *>", f"fb_lti_reduce_short_kernel<2, {s_chunk}>"]
-                        if s_path == HZ_FB_PATH_LTI else None),
-            # event-bracketed (5 records per call, each adding its own latency: the sum exceeds
-            # the un-instrumented wall time per block); the split says where a block's time goes
+            "path": name_of(s_path),
+            "kernels": (["stream_block_kernel<%d>" % (horizon // 8192)] if s_path == HZ_FB_PATH_STREAM else
+                        [f"fb_lti_kernel<2, {s_chunk}, *>", f"fb_lti_reduce_short_kernel<2, {s_chunk}>"]),
+            "launches_per_block": 1 if s_path == HZ_FB_PATH_STREAM else 2,
+            # event-bracketed (records add their own latency: the sum can exceed the un-instrumented
+            # wall time per block)
             "profiled_us_per_block": gpu_us,
-            "profiled_components_us": {"state_or_mix": 1e3 * s_mix / max(1, s_calls),
-                                       "reduce": 1e3 * s_red / max(1, s_calls)},
-            "roofline": {"bound": "latency: 2 dependent kernel launches per block",
+            "end_to_end_host_buffers": e2e,
+            "per_band_engine": per_band,
+            "roofline": {"bound": "latency: %s per block" % ("1 kernel launch" if s_path == HZ_FB_PATH_STREAM
+                                                             else "2 dependent kernel launches"),
+                         "achieved_tflops": stream_flops / (wall_us * 1e-6) / 1e12 if wall_us > 0 else None,
+                         "flops_per_block": stream_flops,
                          "reference_equivalent_tflops": FLOPS_PER_BAND_SAMPLE * N_BANDS * B / (wall_us * 1e-6) / 1e12
                          if wall_us > 0 else None,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": FLOPS_PER_BAND_SAMPLE * N_BANDS * B / (wall_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS
                          if wall_us > 0 else None,
-                         "note": "reference recurrence's 18 flops per band-sample over the wall time per block"},
+                         "note": "frac = the reference recurrence's 18 flops per band-sample over the wall time per "
+                                 "block (reference-equivalent); achieved = the streaming engine's own FP64 work "
+                                 "(bench.stream_block_flops) over the same time"},
         }
 
     total_band_samples = N_BANDS * S * args.steps
@@ -752,7 +853,8 @@ def main():
             "per_sample": per_sample_rates(dev.index or 0) if (world == 1 and not args.no_per_sample) else None,
             "streaming": {"band_samples_per_s": stream_rate, "block": 1024,
                           "us_per_block": (1e6 * N_BANDS * 1024 / stream_rate) if stream_rate else None,
-                          "note": "one process() call per 1024-sample block, device-resident I/O",
+                          "note": "one process() call per 1024-sample block, device-resident I/O, calls issued "
+                                  "back to back (end_to_end_host_buffers: host I/O, synchronous per block)",
                           **stream_detail},
             "cpu_baseline": cpu,
         }

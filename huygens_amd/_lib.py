@@ -26,6 +26,7 @@ HZ_FB_PATH_AUTO = 0
 HZ_FB_PATH_GENERAL = 1
 HZ_FB_PATH_LTI = 2
 HZ_FB_PATH_RESPONSE = 3
+HZ_FB_PATH_STREAM = 4
 
 HZ_FB_RESP_OFF = 0
 HZ_FB_RESP_EAGER = 1
@@ -107,6 +108,8 @@ _SIGS = {
     "hz_fb_time_shard_info": (I, [VP, C.POINTER(I), C.POINTER(L), C.POINTER(L), L]),
     "hz_fb_stationary_ready": (I, [VP, L, C.POINTER(I)]),
     "hz_fb_arm_time_shard": (I, [VP, I]),
+    "hz_fb_tune_stream": (I, [VP, I]),
+    "hz_fb_stream_info": (I, [VP, C.POINTER(I), C.POINTER(L), C.POINTER(L), C.POINTER(I)]),
     # Oscbank
     "hz_osc_create": (I, [I, D, I, C.POINTER(VP)]),
     "hz_osc_create_shard": (I, [I, I, I, D, I, C.POINTER(VP)]),

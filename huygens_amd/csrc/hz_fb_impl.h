@@ -14,6 +14,7 @@ namespace hz_fbi {
 
 constexpr int kMaxOrder = 4;
 constexpr int kLtiGeomChunk128 = 3;   // hz_fb_lti.hip kLtiGeoms: chunk 128 (8192-sample tiles)
+constexpr int kStreamBlock = 1024;    // hz_fb_stream.hip: the streaming engine's call length
 
 // MODE_MIX: full pass (mixdown) over one time segment (blockIdx.y) of one band group
 //   (blockIdx.x).
@@ -178,6 +179,27 @@ struct hz_fb {
         size_t scount_cap = 0;
         double* d_zero = nullptr;        // N O zeros (x history / start of the zero-start pass)
         size_t zero_cap = 0;
+        long h_gen = 0;                  // d_h rebuilds (the streaming spectra follow it)
+        // streaming calls (hz_fb_stream.hip): 1024-sample blocks of a stationary bank, one launch
+        // each, through a frequency-domain delay line; the history in a mirrored ring
+        struct Stream {
+            bool on = true;              // engine enabled (hz_fb_tune_stream)
+            long R = 0;                  // ring length (K + 2048); the ring holds 2 R doubles
+            double* d_line = nullptr;    // [2 R]: sample of position i at i mod R and i mod R + R
+            size_t line_cap = 0;
+            long pos = 0;                // samples written; the history is positions [pos - K, pos)
+            bool line_hist = false;      // the history lives in the ring (not resp.d_hist)
+            bool fdl_valid = false;      // d_ZS holds the spectra of the windows ending at pos
+            long hs_gen = -1;            // h_gen the partition spectra were built from
+            int head = 0;                // slot of the next call's window
+            double *d_ZS = nullptr, *d_HS = nullptr;   // [K/1024][33][32] complex
+            size_t zs_cap = 0, hs_cap = 0;
+            double* d_xch = nullptr;     // [33][32] complex: published inverse columns
+            unsigned* d_count = nullptr; // arrival counter
+            double* d_tw = nullptr;      // twiddles (W_64, W_32, W_2048)
+            long pend = 0;               // streamed samples not yet applied to the smoothers / x history
+            long calls = 0;
+        } st;
     } resp;
     // per-sample engine (hz_fb_rt.hip): a kernel resident on the stream serving operator() /
     // tick() through a pinned-host mailbox while per-sample calls continue
@@ -236,6 +258,17 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n);
 int fb_resp_track(hz_fb* h, const double* d_in, long n, bool conv);  // history after any call
 int fb_resp_materialize(hz_fb* h);                                  // LAZY: band states now
 void fb_resp_free(hz_fb* h);
+int fb_resp_setup(hz_fb* h);   // horizon and history buffers
+int fb_resp_build(hz_fb* h);   // + h, its spectra and the band-state operands for the current bank
+// hz_fb_stream.hip (streaming calls of a stationary bank)
+bool fb_stream_trackable(hz_fb* h, long n, bool conv);   // a call the ring keeps the history of
+bool fb_stream_eligible(hz_fb* h, long n, bool conv);    // ... and that streams (history >= K)
+int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n);
+int fb_stream_track(hz_fb* h, const double* d_in, long n, bool conv);   // a short per-band call
+int fb_stream_materialize(hz_fb* h);   // band states, smoothers, x history from the ring
+int fb_stream_to_hist(hz_fb* h);       // the ring's history back to resp.d_hist (long calls)
+void fb_stream_reset(hz_fb* h);        // state overwritten (set_state, tick)
+void fb_stream_free(hz_fb* h);
 // hz_filterbank.hip: one ring rotation of a tick() without compute (needs spare_ok)
 int fb_tick_rotate(hz_fb* h);
 // hz_fb_rt.hip (per-sample engine)

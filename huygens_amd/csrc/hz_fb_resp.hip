@@ -519,6 +519,7 @@ int resp_build_h(hz_fb* h) {
     HZ_TRY(hz_fbi::fb_state_prepare(h));   // the state pass's records and operands, for LAZY too
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));   // pageable coefficient sources
     R.h_valid = true;
+    ++R.h_gen;
     return HZ_OK;
 }
 
@@ -575,10 +576,20 @@ bool fb_resp_eligible(hz_fb* h, long n, bool conv) {
     return resp_worth(h, n);
 }
 
+int fb_resp_setup(hz_fb* h) { return resp_setup(h); }
+
+int fb_resp_build(hz_fb* h) {
+    HZ_TRY(resp_setup(h));
+    return resp_build_h(h);
+}
+
 int fb_resp_materialize(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     if (!R.implicit) return HZ_OK;
-    HZ_TRY(resp_states(h, h->d_ystate[h->scur]));
+    if (R.st.line_hist)   // streamed calls: the history is in the ring
+        HZ_TRY(fb_stream_materialize(h));
+    else
+        HZ_TRY(resp_states(h, h->d_ystate[h->scur]));
     R.implicit = false;
     return HZ_OK;
 }
@@ -586,13 +597,17 @@ int fb_resp_materialize(hz_fb* h) {
 // after a call on any engine: the history keeps the last K inputs while the bank stays converged
 int fb_resp_track(hz_fb* h, const double* d_in, long n, bool conv) {
     hz_fb::Resp& R = h->resp;
+    // short calls: 1024-sample blocks the streaming engine could take keep the history in its
+    // ring (hz_fb_stream.hip); any other short call restarts the count
+    if (n < resp_min_call(h)) return fb_stream_track(h, d_in, n, conv);
     // (handles pinned to the general engine never run stationary: no history upkeep; a
     // distortion functor keeps it, the engine resumes when the functor is cleared)
-    if (R.mode == HZ_FB_RESP_OFF || !conv || h->order == 0 || n < resp_min_call(h) ||
-        h->path_mode != HZ_FB_PATH_AUTO) {
+    if (R.mode == HZ_FB_RESP_OFF || !conv || h->order == 0 || h->path_mode != HZ_FB_PATH_AUTO) {
         R.run = 0;
+        R.st.fdl_valid = false;
         return HZ_OK;
     }
+    HZ_TRY(fb_stream_to_hist(h));   // after streamed calls
     if (R.K == -2) HZ_TRY(resp_setup(h));
     // no history for banks / call lengths the engine would not take (small banks keep their
     // per-band calls free of the upkeep launch)
@@ -613,6 +628,7 @@ int fb_resp_track(hz_fb* h, const double* d_in, long n, bool conv) {
 int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     hz_fb::Resp& R = h->resp;
     HZ_TRY(resp_setup(h));
+    HZ_TRY(fb_stream_to_hist(h));   // after streamed calls: the history back in d_hist
     HZ_TRY(resp_build_h(h));
     const long K = R.K;
     const int Q = (int)(K / kP), Qp = q_padded(Q);
@@ -747,6 +763,7 @@ void fb_resp_free(hz_fb* h) {
                       R.d_spart, R.d_sop})
         if (p) (void)hipFree(p);
     if (R.d_scount) (void)hipFree(R.d_scount);
+    fb_stream_free(h);
     R = hz_fb::Resp();
 }
 

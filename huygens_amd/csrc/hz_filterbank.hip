@@ -877,6 +877,12 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
     // every rank; an armed handle that cannot (its history is short, or a setter or short call
     // intervened) fails loudly instead of leaving its peers on another engine
     const bool tshard = fb_resp_time_sharded(h);
+    // 1024-sample blocks of a stationary bank: one launch each (hz_fb_stream.hip)
+    if (!tshard && fb_stream_eligible(h, n, conv)) {
+        HZ_TRY(fb_launch_stream(h, d_in, d_out, n));
+        h->last_path = HZ_FB_PATH_STREAM;
+        return HZ_OK;
+    }
     const bool elig = fb_resp_eligible(h, n, conv);
     if (tshard && h->resp.armed && !elig) {
         hz::set_error("hz_fb_process: time-sharded handle armed for the stationary engine, but this call "
@@ -929,6 +935,7 @@ int fb_tick_rotate(hz_fb* h) {
     }
     HZ_TRY(hz_fbi::fb_resp_materialize(h));
     h->resp.run = 0;   // the rotation reuses a stale row: no longer the response of the inputs
+    hz_fbi::fb_stream_reset(h);
     const int N = h->N;
     hipLaunchKernelGGL(fb_tick_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, h->stream,
                        (const double*)h->d_ystate[h->scur], h->d_ystate[h->scur ^ 1], (const double*)h->d_pg[h->scur],
@@ -1265,6 +1272,7 @@ int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
     h->spare_ok = false;
     h->resp.implicit = false;   // overwritten
     h->resp.run = 0;
+    hz_fbi::fb_stream_reset(h);
     return HZ_OK;
 }
 

@@ -12,7 +12,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import HZ_DIST_NONE, check, dptr, load
+from ._lib import HZ_DIST_NONE, PD, check, dptr, load
 
 
 TV_COEFFS, TV_RESONANT = 0, 1   # HZ_FB_TV_*
@@ -90,6 +90,10 @@ class Filterbank:
         if len(xi):
             check(self._lib.hz_fb_process(self._h, dptr(xi), dptr(out), len(xi)))
         return out
+
+    def process_host(self, x_ptr: int, out_ptr: int, n: int):
+        """Host pointers (e.g. pinned buffers), synchronous: H2D + engine + D2H (hz_fb_process)."""
+        check(self._lib.hz_fb_process(self._h, C.cast(C.c_void_p(x_ptr), PD), C.cast(C.c_void_p(out_ptr), PD), n))
 
     def process_device(self, x_ptr: int, out_ptr: int, n: int):
         """Device pointers, asynchronous on the handle's stream."""
@@ -236,3 +240,13 @@ class Filterbank:
         a, f, c = C.c_int(), C.c_long(), C.c_long()
         check(self._lib.hz_fb_time_shard_info(self._h, C.byref(a), C.byref(f), C.byref(c), int(n)))
         return bool(a.value), f.value, c.value
+
+    def tune_stream(self, enable: bool = True):
+        """Streaming engine for 1024-sample calls of a stationary bank (hz_fb_stream.hip) on / off."""
+        check(self._lib.hz_fb_tune_stream(self._h, 1 if enable else 0))
+
+    def stream_info(self):
+        """-> (enabled, call length, streamed calls, history in the ring)"""
+        e, b, c, r = C.c_int(), C.c_long(), C.c_long(), C.c_int()
+        check(self._lib.hz_fb_stream_info(self._h, C.byref(e), C.byref(b), C.byref(c), C.byref(r)))
+        return bool(e.value), b.value, c.value, bool(r.value)

@@ -127,6 +127,7 @@ int hz_fb_set_target_groups(hz_fb* h, int groups);
 #define HZ_FB_PATH_GENERAL 1
 #define HZ_FB_PATH_LTI 2
 #define HZ_FB_PATH_RESPONSE 3
+#define HZ_FB_PATH_STREAM 4
 int hz_fb_set_path(hz_fb* h, int path);
 int hz_fb_last_path(hz_fb* h, int* path);
 /* Stationary engine (HZ_FB_PATH_RESPONSE, hz_fb_resp.hip).  Once the bank has run converged
@@ -172,6 +173,17 @@ int hz_fb_stationary_ready(hz_fb* h, long n, int* ready);
 int hz_fb_arm_time_shard(hz_fb* h, int armed);
 /* for a stationary call of n samples: whether it is time-sharded, and its output range */
 int hz_fb_time_shard_info(hz_fb* h, int* active, long* first, long* count, long n);
+/* Streaming calls (HZ_FB_PATH_STREAM, hz_fb_stream.hip) -- the reference's 1024-sample audio
+ * callback (tests/resynthesis.cpp:33-42 over src/filterbank.h:125-148).  A call of exactly 1024
+ * samples on a stationary bank (as above: converged, unchanged for K samples, K <= 2^17, no
+ * distortion, no time shard) runs as ONE kernel launch: a partitioned overlap-save convolution
+ * with 1024-sample partitions whose window spectra stay on the device between calls.  1024-sample
+ * calls on the per-band engines keep the history for it; band states stay implicit after a
+ * streamed call (in every response mode) until a later call, get_state, tick or a setter needs
+ * them.  hz_fb_tune_stream(h, 0) keeps such calls on the per-band engines (default 1). */
+int hz_fb_tune_stream(hz_fb* h, int enable);
+/* engine enabled, its call length (1024), streamed calls made, history currently in its ring */
+int hz_fb_stream_info(hz_fb* h, int* enabled, long* block, long* calls, int* history_in_ring);
 /* LTI engine geometry: (chunk length, bands per wave, waves per group) in
  * {(16,1,16), (32,1,16), (64,1,16), (128,1,16)}; 0s = by call length (default: 128 for calls
  * of >= 4 x 8192 samples on banks that fill the chip with <= 2 time segments, 64 from

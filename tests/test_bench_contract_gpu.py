@@ -33,3 +33,7 @@ def test_bench_line_contract():
     st = d["streaming"]
     assert st["block"] == 1024 and st["us_per_block"] > 0
     assert st["kernels"] and st["roofline"]["bound"].startswith("latency")
+    # 1024-sample calls of the stationary C2 bank take the streaming engine: one launch per block
+    assert st["path"] == "stream" and st["launches_per_block"] == 1, st
+    assert st["end_to_end_host_buffers"]["us_per_block"] > 0
+    assert st["per_band_engine"]["path"] == "lti"
