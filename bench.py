@@ -127,34 +127,94 @@ def native_oracle():
 
 
 def per_sample_rates(device, samples=12000):
-    """The drop-in's per-sample form, `out = F(x); F.tick();` (tests/resynthesis.cpp:35-39), at C1
-    (128 bands) and C2 (4096 bands): operator() + tick() through the C ABI's resident per-sample
-    kernel (hz_fb_sample / hz_fb_sample_tick), called from Python (ctypes) like a demo callback."""
+    """The drop-ins' per-sample form -- `out = bank(x); bank.tick();` once per sample, as every
+    reference demo's audio callback does -- called from Python (ctypes) like a demo callback, for
+    every bank: Filterbank at C1 (128 bands) and C2 (4096), eight 864-band Filterbanks interleaved
+    (tests/filterbanks.cpp), Delay(10, 2 SR) (tests/delay.cpp), Granulator with 512 voices and
+    grain requests (tests/granny.cpp), Additive 10 x 7 (tests/additive.cpp) and 64 x 256 (C3),
+    Sinusoids, Oscbank<72> operator() + mixdown() + tick() (tests/oscbank.cpp) and Bowl<303>
+    (tests/bowl.cpp).  Input-driven banks go through the per-sample server (hz_rt.hip), generator
+    banks through speculative blocks (huygens_hip.h, hz_add_fill)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from huygens_amd import Filterbank
+    from huygens_amd import Additive, Bowl, Delay, Filterbank, Granulator, Oscbank, Sinusoids, rt_info
     from golden.spec_numpy import resonant_coefficients
     out = {}
-    for name, N in (("c1_128_bands", 128), ("c2_4096_bands", 4096)):
+    rng = np.random.default_rng(7)
+    xs = rng.uniform(-1, 1, samples + 500)
+
+    def timed(name, step, n=samples, warm=500, frames=1, **extra):
+        for i in range(warm):
+            step(i)
+        t0 = time.perf_counter()
+        for i in range(n):
+            step(warm + i)
+        dt = time.perf_counter() - t0
+        rate = n / dt
+        out[name] = {"samples_per_s": rate, "us_per_sample": 1e6 * dt / n, "real_time_48k": rate >= 48000.0,
+                     "calls_per_sample": frames, **extra}
+
+    def fb_bank(N, boost=1.0):
         fwd, back = resonant_coefficients(N, 0.999, 1.0)
         fb = Filterbank(2, N, 0.1, 1.0, device=device)
         for n in range(N):
             fb.coefficients(n, fwd[n], back[n])
-        fb.boost(np.ones(N))
+        fb.boost(np.full(N, boost))
         fb.open()
-        xs = np.random.default_rng(7).uniform(-1, 1, samples + 500)
-        for v in xs[:500]:
-            fb(v)
+        return fb
+
+    for name, N in (("filterbank_c1_128_bands", 128), ("filterbank_c2_4096_bands", 4096)):
+        fb = fb_bank(N)
+
+        def st(i, fb=fb):
+            fb(xs[i % len(xs)])
             fb.tick()
-        t0 = time.perf_counter()
-        for v in xs[500:]:
-            fb(v)
-            fb.tick()
-        dt = time.perf_counter() - t0
-        out[name] = {"samples_per_s": samples / dt, "us_per_sample": 1e6 * dt / samples,
-                     "real_time_48k": samples / dt >= 48000.0, "resident_kernel": fb.sample_info()[0]}
+        timed(name, st, path="per-sample server (hz_rt.hip OP_FB)")
         fb.close()
-    out["note"] = ("operator() + tick() per sample through the resident per-sample kernel (pinned-host "
-                   "mailbox), Python ctypes caller, 12,000 samples after 500 of warm-up")
+    fbs = [fb_bank(864, 1.0 + 0.1 * k) for k in range(8)]
+
+    def st8(i):
+        for fb in fbs:
+            fb(xs[i % len(xs)])
+            fb.tick()
+    timed("filterbank_8x864_interleaved", st8, n=samples // 4, frames=8, path="per-sample server, 8 handles")
+    for fb in fbs:
+        fb.close()
+    d = Delay(10, 2 * 48000, device=device)
+    d.coefficients([(0, 1.0)], [(20000, 0.5), (10000, 0.5)])
+    timed("delay_10_taps_2s", lambda i: d(xs[i % len(xs)]), path="per-sample server (OP_DLY)")
+    g = Granulator(3 * 48000, 512, device=device)
+
+    def gran(i):
+        g.sample(xs[i % len(xs)])
+        if i % 2400 == 0:
+            g.request(0.0, 0.15, 1.0 + 0.1 * ((i // 2400) % 5), 0.5, ticked=True)
+    timed("granulator_512_voices", gran, path="per-sample server (OP_GRAN)")
+    for name, (V, O) in (("additive_10x7_demo", (10, 7)), ("additive_64x256_c3", (64, 256))):
+        a = Additive(V, O, 0.75, 1.0, device=device)
+        for v in range(V):
+            a.makenote(36 + v, 1.0)
+        timed(name, lambda i, a=a: a.fill(1), path="speculative blocks (1024 samples)")
+        a.close()
+    sn = Sinusoids(220.0, 12, 0.8, 1.0, device=device)
+    timed("sinusoids_12", lambda i: sn.fill(1), path="speculative blocks")
+    ob = Oscbank(72, device=device)
+    for k in range(72):
+        ob.freqmod(k, 55.0 * 2 ** (k / 12))
+    ob.open()
+
+    def osc(i):
+        ob.phases()
+        ob.mixdown()
+        ob.tick()
+    timed("oscbank_72_operator_mixdown_tick", osc, path="speculative blocks")
+    frng = np.random.default_rng(5)
+    f = np.exp(frng.uniform(np.log(20), np.log(16000), 303))
+    bw = Bowl(303, f, frng.uniform(1e-4, 5e-2, 303), frng.uniform(0.05, 15, 303), device=device)
+    bw.trigger()
+    timed("bowl_303_modes", lambda i: bw.render(1), path="speculative blocks")
+    req, launches, _ = rt_info(device)
+    out["note"] = ("one call per sample (operator() + tick(); Oscbank: operator() + mixdown() + tick()) from a Python "
+                   "ctypes caller, after 500 warm-up samples; per-sample server requests %d, launches %d" % (req, launches))
     return out
 
 

@@ -4,7 +4,7 @@ The product is libhuygens_hip.so (C ABI: include/huygens_hip.h) with the C++
 drop-in headers in include/soundmath/.  This package is the Python mirror of
 that ABI used by tests/ and bench.py.
 """
-from ._lib import HZError, load, header_symbols  # noqa: F401
+from ._lib import HZError, load, header_symbols, rt_info  # noqa: F401
 from .filterbank import Filterbank  # noqa: F401
 from .oscbank import Oscbank  # noqa: F401
 from .additive import Additive, Sinusoids  # noqa: F401

@@ -109,6 +109,11 @@ _SIGS = {
     "hz_fb_stationary_ready": (I, [VP, L, C.POINTER(I)]),
     "hz_fb_arm_time_shard": (I, [VP, I]),
     "hz_fb_tune_stream": (I, [VP, I]),
+    "hz_fb_setter_seq": (I, [VP, C.POINTER(C.c_longlong)]),
+    "hz_dly_sample": (I, [VP, VP, VP, I]),
+    "hz_gran_sample": (I, [VP, D, PD]),
+    "hz_rt_info": (I, [I, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong), C.POINTER(I)]),
+    "hz_add_lookahead_info": (I, [VP, C.POINTER(L), C.POINTER(L), C.POINTER(L)]),
     "hz_fb_stream_info": (I, [VP, C.POINTER(I), C.POINTER(L), C.POINTER(L), C.POINTER(I)]),
     # Oscbank
     "hz_osc_create": (I, [I, D, I, C.POINTER(VP)]),
@@ -284,3 +289,11 @@ def check(code: int):
 def dptr(a):
     """ctypes double* of a C-contiguous float64 numpy array."""
     return a.ctypes.data_as(PD)
+
+
+def rt_info(device: int = 0):
+    """The per-sample server (hz_rt.hip) of a device: (requests served, kernel launches, resident)."""
+    lib = load()
+    r, n, a = C.c_longlong(), C.c_longlong(), C.c_int()
+    check(lib.hz_rt_info(device, C.byref(r), C.byref(n), C.byref(a)))
+    return r.value, n.value, bool(a.value)

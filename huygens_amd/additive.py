@@ -110,3 +110,10 @@ class Sinusoids:
         if n:
             check(self._lib.hz_sin_fill(self._h, dptr(out), n))
         return out
+
+
+def lookahead_info(bank) -> tuple[int, int, int]:
+    """(speculative blocks rendered, rollbacks, block length) of an Additive's per-sample service."""
+    b, r, L = C.c_long(), C.c_long(), C.c_long()
+    check(bank._lib.hz_add_lookahead_info(bank._h, C.byref(b), C.byref(r), C.byref(L)))
+    return b.value, r.value, L.value

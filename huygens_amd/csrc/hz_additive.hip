@@ -346,6 +346,19 @@ struct PhaseBank {
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     long launches = 0;
+    // Per-sample calls (operator() / tick(): fills shorter than kLookMin) are served from a
+    // speculative block: the next kLook samples rendered at once from a snapshot of the state
+    // (the outputs need no input: src/additive.h:38-62, src/sinusoids.h:34-57), consumed one by
+    // one; a setter or a longer fill first rolls the engine back to the consumed position
+    // (snapshot restored, exactly that many samples re-rendered), so every sample is the one the
+    // per-sample sequence produces.
+    static constexpr long kLook = 1024, kLookMin = 64;
+    double* la_buf = nullptr;          // pinned [kLook] rendered outputs
+    long la_n = 0, la_pos = 0;         // rendered / consumed samples of the speculative block
+    double *d_phi_snap = nullptr, *d_f_snap = nullptr;
+    std::vector<double> amp_snap, c_first_snap;
+    std::vector<char> alive_snap;
+    long la_blocks = 0, la_rollbacks = 0;
 
     int init(int V_, int O_, int o0_, int OL_, double s_, double a_, int dev) {
         V = V_;
@@ -385,8 +398,10 @@ struct PhaseBank {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         for (void* p : {(void*)d_rec, (void*)d_phi, (void*)d_f, (void*)d_ft, (void*)d_amp, (void*)d_act,
-                        (void*)d_partial, (void*)d_out, (void*)d_tasks, (void*)d_c0})
+                        (void*)d_partial, (void*)d_out, (void*)d_tasks, (void*)d_c0, (void*)d_phi_snap,
+                        (void*)d_f_snap})
             if (p) (void)hipFree(p);
+        if (la_buf) (void)hipHostFree(la_buf);
         for (hipEvent_t e : ev) (void)hipEventDestroy(e);
         if (own_stream && stream) (void)hipStreamDestroy(stream);
     }
@@ -513,8 +528,72 @@ struct PhaseBank {
         return HZ_OK;
     }
 
+    // roll the engine back to the consumed position of the speculative block (before any setter,
+    // any longer fill or a device fill)
+    int settle() {
+        if (la_pos < la_n) {
+            const size_t P = (size_t)V * OL;
+            HZ_TRY_HIP(hipMemcpyAsync(d_phi, d_phi_snap, sizeof(double) * P, hipMemcpyDeviceToDevice, stream));
+            HZ_TRY_HIP(hipMemcpyAsync(d_f, d_f_snap, sizeof(double) * P, hipMemcpyDeviceToDevice, stream));
+            amp = amp_snap;
+            alive = alive_snap;
+            c_first = c_first_snap;
+            const long m = la_pos;
+            la_n = la_pos = 0;
+            ++la_rollbacks;
+            if (m > 0) HZ_TRY(render_scratch(m));
+        }
+        la_n = la_pos = 0;
+        return HZ_OK;
+    }
+
+    int ensure_out(long n) {
+        if ((size_t)n <= out_cap) return HZ_OK;
+        if (d_out) HZ_TRY_HIP(hipFree(d_out));
+        d_out = nullptr;
+        HZ_TRY_HIP(hipMalloc(&d_out, sizeof(double) * n));
+        out_cap = n;
+        return HZ_OK;
+    }
+
+    int render_scratch(long n) {
+        HZ_TRY(ensure_out(n));
+        return render(d_out, n);
+    }
+
+    // a new speculative block: snapshot, render kLook samples, outputs to pinned memory
+    int look_ahead() {
+        const size_t P = (size_t)V * OL;
+        if (!la_buf) {
+            HZ_TRY_HIP(hipHostMalloc((void**)&la_buf, sizeof(double) * kLook));
+            HZ_TRY_HIP(hipMalloc(&d_phi_snap, sizeof(double) * P));
+            HZ_TRY_HIP(hipMalloc(&d_f_snap, sizeof(double) * P));
+        }
+        HZ_TRY_HIP(hipMemcpyAsync(d_phi_snap, d_phi, sizeof(double) * P, hipMemcpyDeviceToDevice, stream));
+        HZ_TRY_HIP(hipMemcpyAsync(d_f_snap, d_f, sizeof(double) * P, hipMemcpyDeviceToDevice, stream));
+        amp_snap = amp;
+        alive_snap = alive;
+        c_first_snap = c_first;
+        HZ_TRY(ensure_out(kLook));
+        HZ_TRY(render(d_out, kLook));
+        HZ_TRY_HIP(hipMemcpyAsync(la_buf, d_out, sizeof(double) * kLook, hipMemcpyDeviceToHost, stream));
+        HZ_TRY_HIP(hipStreamSynchronize(stream));
+        la_n = kLook;
+        la_pos = 0;
+        ++la_blocks;
+        return HZ_OK;
+    }
+
     int fill_host(double* out, long n) {
         if (n <= 0) return HZ_OK;
+        if (n < kLookMin) {   // per-sample calls: from the speculative block
+            for (long i = 0; i < n; ++i) {
+                if (la_pos == la_n) HZ_TRY(look_ahead());
+                out[i] = la_buf[la_pos++];
+            }
+            return HZ_OK;
+        }
+        HZ_TRY(settle());
         if ((size_t)n > out_cap) {
             if (d_out) HZ_TRY_HIP(hipFree(d_out));
             d_out = nullptr;
@@ -616,6 +695,8 @@ int hz_add_destroy(hz_add* h) {
 // particle positions stay where request() puts them.
 int hz_add_request(hz_add* h, double fundamental, double amplitude, int* voice_out) {
     if (!h) return HZ_E_INVALID;
+    HZ_TRY(add_check(h));
+    HZ_TRY(h->bank.settle());   // a speculative block rolls back to the consumed sample first
     int voice = -1;
     for (int i = 0; i < h->V; ++i)
         if (!h->active[i]) {
@@ -652,6 +733,8 @@ int hz_add_request(hz_add* h, double fundamental, double amplitude, int* voice_o
 // release(voice) minimizer.h:161-172 (voice < 0: all)
 int hz_add_release(hz_add* h, int voice) {
     if (!h) return HZ_E_INVALID;
+    HZ_TRY(add_check(h));
+    HZ_TRY(h->bank.settle());
     for (int i = 0; i < h->V; ++i)
         if (voice < 0 || i == voice) {
             h->active[i] = 0;
@@ -686,11 +769,22 @@ int hz_add_fill(hz_add* h, double* out, size_t n) {
 int hz_add_fill_device(hz_add* h, double* d_out, size_t n) {
     HZ_TRY(add_check(h));
     if (n && !d_out) return HZ_E_INVALID;
+    HZ_TRY(h->bank.settle());
     return h->bank.render(d_out, (long)n);
+}
+
+// per-sample service statistics: speculative blocks rendered, rollbacks (setters inside a block)
+int hz_add_lookahead_info(hz_add* h, long* blocks, long* rollbacks, long* block_len) {
+    if (!h) return HZ_E_INVALID;
+    if (blocks) *blocks = h->bank.la_blocks;
+    if (rollbacks) *rollbacks = h->bank.la_rollbacks;
+    if (block_len) *block_len = PhaseBank::kLook;
+    return HZ_OK;
 }
 
 int hz_add_set_stream(hz_add* h, void* s) {
     HZ_TRY(add_check(h));
+    HZ_TRY(h->bank.settle());
     HZ_TRY_HIP(hipStreamSynchronize(h->bank.stream));
     if (h->bank.own_stream) HZ_TRY_HIP(hipStreamDestroy(h->bank.stream));
     if (s) {
@@ -804,6 +898,8 @@ int hz_sin_destroy(hz_sin* h) {
 
 int hz_sin_fundmod(hz_sin* h, double target) {   // sinusoids.h:67-68
     if (!h) return HZ_E_INVALID;
+    HZ_TRY_HIP(hipSetDevice(h->bank.device));
+    HZ_TRY(h->bank.settle());
     h->fundamental = target;
     sin_retarget(h);
     return HZ_OK;
@@ -811,6 +907,8 @@ int hz_sin_fundmod(hz_sin* h, double target) {   // sinusoids.h:67-68
 
 int hz_sin_decaymod(hz_sin* h, double target) {   // sinusoids.h:61-62
     if (!h) return HZ_E_INVALID;
+    HZ_TRY_HIP(hipSetDevice(h->bank.device));
+    HZ_TRY(h->bank.settle());
     h->decay = target;
     sin_retarget(h);
     return HZ_OK;
@@ -818,6 +916,8 @@ int hz_sin_decaymod(hz_sin* h, double target) {   // sinusoids.h:61-62
 
 int hz_sin_harmmod(hz_sin* h, double target) {    // sinusoids.h:64-65
     if (!h) return HZ_E_INVALID;
+    HZ_TRY_HIP(hipSetDevice(h->bank.device));
+    HZ_TRY(h->bank.settle());
     h->harmonicity = target;
     sin_retarget(h);
     return HZ_OK;
@@ -835,6 +935,7 @@ int hz_sin_fill_device(hz_sin* h, double* d_out, size_t n) {
     if (!h) return HZ_E_INVALID;
     HZ_TRY_HIP(hipSetDevice(h->bank.device));
     if (n && !d_out) return HZ_E_INVALID;
+    HZ_TRY(h->bank.settle());
     return h->bank.render(d_out, (long)n);
 }
 

@@ -305,6 +305,13 @@ struct hz_bowl {
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     long launches = 0;
+    // per-sample calls (renders shorter than kLookMin: the drop-in's operator() / tick()) come
+    // from a speculative block of kLook samples rendered at once; the state is the phase counter
+    // alone, so a rollback sets it to the consumed sample (huygens_hip.h, hz_add_fill)
+    static constexpr long kLook = 1024, kLookMin = 64;
+    double* la_buf = nullptr;
+    long la_n = 0, la_pos = 0;
+    double n0_snap = 0;
 };
 
 namespace {
@@ -396,6 +403,26 @@ int bowl_launch(hz_bowl* h, void* d_dst, long n, int out_kind) {
     return HZ_OK;
 }
 
+// roll a speculative block back to its consumed sample (the counter saturates as bowl_launch's)
+void bowl_settle(hz_bowl* h) {
+    if (h->la_pos < h->la_n) {
+        h->n0 = h->n0_snap + (double)h->la_pos;
+        if (h->is_float && h->n0 > 16777216.0) h->n0 = 16777216.0;
+    }
+    h->la_n = h->la_pos = 0;
+}
+
+int bowl_host(hz_bowl* h, void* out, size_t elem, long n, int kind);
+
+int bowl_look_ahead(hz_bowl* h) {
+    if (!h->la_buf) HZ_TRY_HIP(hipHostMalloc((void**)&h->la_buf, sizeof(double) * hz_bowl::kLook));
+    h->n0_snap = h->n0;
+    HZ_TRY(bowl_host(h, h->la_buf, sizeof(double), hz_bowl::kLook, 1));
+    h->la_n = hz_bowl::kLook;
+    h->la_pos = 0;
+    return HZ_OK;
+}
+
 int bowl_host(hz_bowl* h, void* out, size_t elem, long n, int kind) {
     if (n <= 0) return HZ_OK;
     if ((size_t)n * elem > h->out_cap) {
@@ -461,6 +488,7 @@ int hz_bowl_destroy(hz_bowl* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (void* p : {(void*)h->d_rec, (void*)h->d_partial, h->d_out})
         if (p) (void)hipFree(p);
+    if (h->la_buf) (void)hipHostFree(h->la_buf);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -469,6 +497,7 @@ int hz_bowl_destroy(hz_bowl* h) {
 
 int hz_bowl_trigger(hz_bowl* h) {   // bowl.h:25-28
     if (!h) return HZ_E_INVALID;
+    bowl_settle(h);
     h->n0 = 0;
     return HZ_OK;
 }
@@ -476,12 +505,14 @@ int hz_bowl_trigger(hz_bowl* h) {   // bowl.h:25-28
 int hz_bowl_fill(hz_bowl* h, float* buffer, size_t bsize) {   // bowl.h:50-63
     HZ_TRY(bowl_check(h));
     if (bsize && !buffer) return HZ_E_INVALID;
+    bowl_settle(h);
     return bowl_host(h, buffer, sizeof(float), (long)bsize, 0);
 }
 
 int hz_bowl_fill_device(hz_bowl* h, float* d_buffer, size_t bsize) {
     HZ_TRY(bowl_check(h));
     if (bsize && !d_buffer) return HZ_E_INVALID;
+    bowl_settle(h);
     return bowl_launch(h, d_buffer, (long)bsize, 0);
 }
 
@@ -489,17 +520,27 @@ int hz_bowl_fill_device(hz_bowl* h, float* d_buffer, size_t bsize) {
 int hz_bowl_render(hz_bowl* h, double* out, size_t n) {
     HZ_TRY(bowl_check(h));
     if (n && !out) return HZ_E_INVALID;
+    if ((long)n < hz_bowl::kLookMin) {   // per-sample calls: from the speculative block
+        for (size_t i = 0; i < n; ++i) {
+            if (h->la_pos == h->la_n) HZ_TRY(bowl_look_ahead(h));
+            out[i] = h->la_buf[h->la_pos++];
+        }
+        return HZ_OK;
+    }
+    bowl_settle(h);
     return bowl_host(h, out, sizeof(double), (long)n, 1);
 }
 
 int hz_bowl_render_device(hz_bowl* h, double* d_out, size_t n) {
     HZ_TRY(bowl_check(h));
     if (n && !d_out) return HZ_E_INVALID;
+    bowl_settle(h);
     return bowl_launch(h, d_out, (long)n, 1);
 }
 
 int hz_bowl_phase(hz_bowl* h, double* phase) {
     if (!h || !phase) return HZ_E_INVALID;
+    bowl_settle(h);
     *phase = h->n0;
     return HZ_OK;
 }

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "hz_common.h"
+#include "hz_rt.h"
 
 namespace {
 
@@ -185,6 +186,7 @@ struct hz_dly {
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     long launches = 0;
+    bool pending = false;           // block work queued on the stream since the last synchronisation
     size_t elem() const { return is_float ? sizeof(float) : sizeof(double); }
 };
 
@@ -335,6 +337,7 @@ int dly_launch_t(hz_dly* h, const void* d_in, void* d_out, long n, int in_per_li
     }
     h->origin = (unsigned)(((unsigned long)h->origin + (unsigned long)n) % h->size);
     h->launches += h->prof ? 1 : 0;
+    h->pending = true;
     return HZ_OK;
 }
 
@@ -469,6 +472,51 @@ int hz_dly_process(hz_dly* h, const void* in, void* out, size_t n, int in_per_li
     HZ_TRY(dly_launch(h, h->d_in, h->d_out, (long)n, in_per_line, mix));
     HZ_TRY_HIP(hipMemcpyAsync(out, h->d_out, out_bytes, hipMemcpyDeviceToHost, h->stream));
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+// one sample of every line through the device's per-sample server (hz_rt.hip OP_DLY): the
+// reference's `y = D(x); D.tick();` (tests/delay.cpp:20-28) without a launch per sample; in: one
+// T (mono) or N T (per line); out: N T
+int hz_dly_sample(hz_dly* h, const void* in, void* out, int in_per_line) {
+    HZ_TRY(dly_check(h));
+    if (!in || !out) return HZ_E_INVALID;
+    HZ_TRY(dly_upload(h));
+    if (h->pending) {   // block calls' ring updates land before the server reads the rings
+        HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+        h->pending = false;
+    }
+    hz_rt::Server* srv = hz_rt::server(h->device);
+    if (!srv) return HZ_E_NODEV;
+    std::lock_guard<std::recursive_mutex> lk(hz_rt::lock(srv));
+    const int N = h->N;
+    double* res = hz_rt::result(srv, N);
+    double* pay = in_per_line ? hz_rt::payload(srv, N) : nullptr;
+    if (!res || (in_per_line && !pay)) return HZ_E_ALLOC;
+    hz_rt::DlyArgs a{};
+    a.rx = h->d_rx;
+    a.ry = h->d_ry;
+    a.taps = h->d_taps;
+    a.gains = h->d_gains;
+    if (in_per_line) {
+        for (int l = 0; l < N; ++l) pay[l] = h->is_float ? (double)((const float*)in)[l] : ((const double*)in)[l];
+        a.xin = (const double*)hz_rt::dev(srv, pay);
+    } else {
+        a.x = h->is_float ? (double)*(const float*)in : *(const double*)in;
+    }
+    a.out = (double*)hz_rt::dev(srv, res);
+    a.N = N;
+    a.S = h->S;
+    a.is_float = h->is_float;
+    a.size = h->size;
+    a.o = h->origin;
+    const int groups = std::max(1, std::min(hz_rt::kGroups, (N + hz_rt::kThreads - 1) / hz_rt::kThreads));
+    HZ_TRY(hz_rt::call(srv, hz_rt::OP_DLY, &a, sizeof(a), groups, nullptr));
+    for (int l = 0; l < N; ++l) {
+        if (h->is_float) ((float*)out)[l] = (float)res[l];
+        else ((double*)out)[l] = res[l];
+    }
+    h->origin = (unsigned)(((unsigned long)h->origin + 1ul) % h->size);
     return HZ_OK;
 }
 

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "hz_common.h"
@@ -55,10 +56,17 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 
 }  // namespace hz_fbi
 
+constexpr int kMaxOrderRt = 4;   // (= hz_fbi::kMaxOrder)
+
 // ---------------------------------------------------------------------------
 // handle (the opaque hz_fb of include/huygens_hip.h)
 // ---------------------------------------------------------------------------
 struct hz_fb {
+    // entry points that touch the staged parameters or the state hold it (setters may come from
+    // another thread while samples run: tests/filterbank.cpp:217-252 vs 200-210)
+    std::recursive_mutex mu;
+    long pg_gen = 0, coef_gen = 0;   // generations of the staged targets / coefficients
+    long long setter_seq = 0;        // per-sample calls served when the last setter ran
     int order = 2, N = 0, N_total = 0, band_begin = 0, device = 0;
     double sp = 0, sg = 0;
     int rec = 8;
@@ -194,29 +202,26 @@ struct hz_fb {
             int head = 0;                // slot of the next call's window
             double *d_ZS = nullptr, *d_HS = nullptr;   // [K/1024][33][32] complex
             size_t zs_cap = 0, hs_cap = 0;
-            double* d_xch = nullptr;     // [33][32] complex: published inverse columns
-            unsigned* d_count = nullptr; // arrival counter
+            double* d_CR = nullptr;      // [2][33][32] tail columns C, then [2][33][32] MAC sums R (complex)
+            long blk = 0;                // streamed blocks since the ring was primed (parity of C / R)
             double* d_tw = nullptr;      // twiddles (W_64, W_32, W_2048)
             long pend = 0;               // streamed samples not yet applied to the smoothers / x history
             long calls = 0;
         } st;
     } resp;
-    // per-sample engine (hz_fb_rt.hip): a kernel resident on the stream serving operator() /
-    // tick() through a pinned-host mailbox while per-sample calls continue
+    // per-sample path (hz_fb_rt.hip): OP_FB requests to the device's per-sample server (hz_rt.hip)
     struct Rt {
-        bool active = false;         // an instance was launched and not stopped by the host
+        bool active = false;         // the state is in the per-sample layout (ring rows)
         bool computed = false;       // the reference's `computed` (filterbank.h:127-128, 168)
         bool spare_known = false;    // the ring row at origin is known (after any compute)
-        long long seq = 0;           // last request number posted
-        long long epoch = 0;         // instance number
+        long long seq = 0;           // samples served
         long pending_ticks = 0;      // tick() calls since the last served request
-        int groups = 0;              // workgroups of the instance
         double cached = 0;           // the last served sample
         int cached_dist = 0;
-        void* mb = nullptr;          // pinned host mailbox (RtReq + RtSlot[])
-        void* dmb = nullptr;         // its device address
-        void* d_ctl = nullptr;       // device control block (request forwarding)
-        double* d_coef = nullptr;    // [N][2O+1]
+        double xr[kMaxOrderRt + 1] = {};   // input ring (ring order), host mirror
+        long pg_gen = 0, coef_gen = 0;     // generations the server's arrays hold
+        double* pin1 = nullptr;      // pinned staging (x history, a cached sample)
+        double* d_coef = nullptr;    // [N][2O+1] coefficients, then [N][O+1] ring rows
         size_t coef_cap = 0;
         std::vector<double> h_coef;
     } rt;

@@ -5,17 +5,20 @@
 // (tests/resynthesis.cpp:33-42 -> src/filterbank.h:125-148).  Once the bank is stationary
 // (hz_fb_resp.hip: converged for its horizon K), the block's mixdown is
 //     out[t] = sum_{tau < K} h[tau] x[t - tau]
-// and a block call runs here as ONE kernel launch: a uniformly partitioned overlap-save
-// convolution with P = 1024-sample partitions (the call length) and F = 2048-point real
-// transforms, whose frequency-domain delay line -- the spectra of the last Q = K / P windows --
-// stays on the device between calls.  Each transform is split column-wise (four-step,
-// n = 32 n1 + n2, k = k1 + 64 k2): workgroup c (c = 0..32) computes, straight from the samples,
-// its 32 bins X[c + 64 k2] of the new window's spectrum, its 32 bins of the partition MAC
-// Y = sum_p H_p Z_{b-p}, and its column of the inverse transform; it publishes that column
-// (512 B, write-through stores) and adds to an arrival counter; the workgroup whose add comes
-// last combines the 33 columns (Hermitian symmetry gives the other 31) into the block's 1024
-// outputs.  tests/stream_model.py restates this algebra and is checked against a direct
-// convolution on the CPU.
+// and a block call runs here as ONE kernel launch of a uniformly partitioned overlap-save
+// convolution with P = 1024-sample partitions (the call length) and F = 2048-point real transforms,
+// whose frequency-domain delay line -- the spectra Z of the last Q = K / P windows -- stays on the
+// device between calls.  Each transform is split column-wise (four-step, n = 32 n1 + n2,
+// k = k1 + 64 k2), so workgroup c (c = 0..32) computes its 32 bins straight from the samples and
+// Hermitian symmetry gives columns 33..63.  The launch has three roles that share no data, so no
+// workgroup waits for another (an in-launch exchange of the inverse columns measured 10 us per
+// block: its write-through, arrival and reload round trips are the block's latency):
+//   outputs    y_b = head_b + tail_b: head = the partition-0 term h[0..1023] * x, direct in time;
+//              tail = the Hermitian combine of 33 inverse columns C_b the PREVIOUS launch wrote
+//   transform  Z_b into the ring; Y_{b+1} = H_1 Z_b + H_2 Z_{b-1} + R_{b+1}; C_{b+1} = its inverse
+//              columns (the next block's tail)
+//   MAC        R_{b+2} = sum_{p >= 3} H_p Z_{b+2-p} over the ring (Z_{b-1} and older)
+// tests/stream_model.py restates this schedule and is checked against a direct convolution.
 //
 // Band states stay implicit (every mode): they are the zero-start response of the last K inputs,
 // which the engine keeps in a mirrored device ring (every sample written at i and i + R, so any K
@@ -141,13 +144,36 @@ struct StreamArgs {
     long R;
     long wpos;            // write position of the call's first sample (pos mod R, a multiple of 1024)
     long prev;            // ring index of the previous block's first sample ((pos - 1024) mod R)
-    const double2* HS;    // [Q][33][32]
+    const double2* HS;    // [Q + 8][33][32] (rows past Q zero)
     double2* ZS;          // [Q][33][32] window spectra ring
-    int Q, head;          // partitions; slot of this call's window (older windows: head - p mod Q)
+    int Q, head;          // partitions; slot of this call's window Z_b (Z_{b-p}: head - p mod Q)
     const double2* tw;
-    double* xch;          // [33][32] complex: the published columns
-    unsigned* count;      // arrival counter (0 between launches)
+    const double* h;      // [K] the bank response (head taps 0 .. 1023)
+    const double2* Cin;   // [33][32] inverse columns of this block's tail (previous launch)
+    double2* Cout;        // [33][32] ... of the next block's tail
+    const double2* Rin;   // [33][32] R_{b+1} = sum_{p >= 3} H_p Z_{b+1-p} (previous launch)
+    double2* Rout;        // [33][32] R_{b+2}
 };
+
+__device__ __forceinline__ int ring_slot(int head, int back, int Q) {
+    int s = head - back;
+    while (s < 0) s += Q;
+    return s;
+}
+
+// inverse column (s.y holds the column's 32 bins Y[k2]): C[n2] = W_2048^(-n2 c) sum_k2 W_32^(-n2 k2)
+// Y[k2] -> dst[n2] (n2 < 32); the thread sums k2 = 4 g + q with the forward's stage-3 twiddles
+// conjugated (index (4g+q) j mod 32 either way)
+__device__ __forceinline__ void col_inverse_store(ColLds& s, const ColTw& ct, double2 tcol, double2* __restrict__ dst) {
+    const int t = threadIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
+    double2 cp = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cp = cadd(cp, cmulc(ct.t32[q], s.y[4 * g + q]));
+    cp = half_sum(cp);
+    if (l < 32) s.c[w][j] = cp;
+    __syncthreads();
+    if (t < 32) dst[t] = cmulc(tcol, cadd(cadd(s.c[0][t], s.c[1][t]), cadd(s.c[2][t], s.c[3][t])));
+}
 
 // The ring's windows b - p (p = 1 .. Q - 1) from the history: slot (head - p) mod Q <- the window
 // [pos - P (p + 1), pos - P (p - 1)), grid (33, Q - 1)
@@ -157,136 +183,219 @@ __global__ __launch_bounds__(kT) void stream_prime_kernel(StreamArgs a) {
     long ws = a.wpos - (long)kSP * (p + 1);
     if (ws < 0) ws += a.R;
     const double* src = a.line + ws;   // contiguous: ws < R, ws + 2048 <= 2 R
-    int slot = a.head - p;
-    if (slot < 0) slot += a.Q;
-    col_forward(s, a.tw, c, [&](int n) { return src[n]; }, a.ZS + ((long)slot * kCols + c) * 32);
+    col_forward(s, a.tw, c, [&](int n) { return src[n]; }, a.ZS + ((long)ring_slot(a.head, p, a.Q) * kCols + c) * 32);
 }
 
-// One 1024-sample block (see the file comment).  QI = Q / 8 partitions per thread.
+// after stream_prime_kernel, per column: the first block's tail columns C_b (Y_b = sum_{p >= 1}
+// H_p Z_{b-p}) into Cout and R_{b+1} = sum_{p >= 3} H_p Z_{b+1-p} into Rout
 template <int QI>
-__global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
+__global__ __launch_bounds__(kT) void stream_prime2_kernel(StreamArgs a) {
     __shared__ ColLds s;
     const int t = threadIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
     const int c = blockIdx.x;
-    // ---- every operand of the column in flight at once: the window (previous block from the
-    // ring, this block from the caller), the partition spectra and the older windows' spectra of
-    // the thread's partitions p = g + 8 i, the twiddles
-    double v[8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = a.line[a.prev + 32 * (g + 8 * i) + j];
-#pragma unroll
-    for (int i = 4; i < 8; ++i) v[i] = a.x[32 * (g + 8 * i - 32) + j];
-    double2 hv[QI], zv[QI];
+    double2 y = make_double2(0.0, 0.0), r = make_double2(0.0, 0.0);
 #pragma unroll
     for (int i = 0; i < QI; ++i) {
-        const int p = g + 8 * i;
-        hv[i] = a.HS[((long)p * kCols + c) * 32 + j];
-        int slot = a.head - p;
-        if (slot < 0) slot += a.Q;
-        // p = 0 is this call's window (computed below); its slot holds a stale spectrum
-        zv[i] = a.ZS[((long)slot * kCols + c) * 32 + j];
+        const int p = 1 + g + 8 * i;   // <= Q: row Q of HS is zero
+        y = cadd(y, cmul(a.HS[((long)p * kCols + c) * 32 + j], a.ZS[((long)ring_slot(a.head, p, a.Q) * kCols + c) * 32 + j]));
+        const int p3 = 3 + g + 8 * i;  // < Q + 8
+        r = cadd(r, cmul(a.HS[((long)p3 * kCols + c) * 32 + j],
+                         a.ZS[((long)ring_slot(a.head, p3 - 1, a.Q) * kCols + c) * 32 + j]));
     }
     ColTw ct;
     ct.load(a.tw, c, j, g);
-    const double2 tcol = a.tw[kTw2k + j * c];   // W_2048^(n2 c), n2 = j (inverse column twiddle)
-    // the block's samples into the ring (both mirror positions) for the next calls
-    if (c == 0) {
-#pragma unroll
-        for (int i = 4; i < 8; ++i) {
-            const long k = a.wpos + 32 * (g + 8 * i - 32) + j;
-            a.line[k] = v[i];
-            a.line[k + a.R] = v[i];
-        }
-    }
-    // ---- forward stage 1 + the MAC partial over the thread's older windows
-    const double2 a1 = stage1(v, ct.t64);
-    double2 mp = make_double2(0.0, 0.0);
-#pragma unroll
-    for (int i = 0; i < QI; ++i) {
-        if (i == 0 && g == 0) continue;   // p = 0: the new window, added below
-        mp = cadd(mp, cmul(hv[i], zv[i]));
-    }
-    mp = half_sum(mp);
+    const double2 tcol = a.tw[kTw2k + j * c];
+    y = half_sum(y);
+    r = half_sum(r);
     if (l < 32) {
-        s.a[w][j] = a1;
-        s.m[w][j] = mp;
+        s.m[w][j] = y;
+        s.x[w][j] = r;
     }
-    __syncthreads();
-    // ---- forward stage 3 -> X (this window's bins), Y = H_0 X + sum of the MAC partials
-    const double2 xp = stage3(s, g, ct.t2k, ct.t32);
-    if (l < 32) s.x[w][j] = xp;
     __syncthreads();
     if (t < 32) {
-        const double2 X = cadd(cadd(s.x[0][t], s.x[1][t]), cadd(s.x[2][t], s.x[3][t]));
-        a.ZS[((long)a.head * kCols + c) * 32 + t] = X;
-        const double2 M = cadd(cadd(s.m[0][t], s.m[1][t]), cadd(s.m[2][t], s.m[3][t]));
-        s.y[t] = cadd(M, cmul(hv[0], X));   // thread t < 32: g = 0, hv[0] = H_0
+        s.y[t] = cadd(cadd(s.m[0][t], s.m[1][t]), cadd(s.m[2][t], s.m[3][t]));
+        a.Rout[c * 32 + t] = cadd(cadd(s.x[0][t], s.x[1][t]), cadd(s.x[2][t], s.x[3][t]));
     }
     __syncthreads();
-    // ---- inverse column: C[n2] = W_2048^(-n2 c) sum_k2 W_32^(-n2 k2) Y[k2]; the thread sums
-    // k2 = 4 g + q (the forward's stage-3 twiddles, conjugated)
-    double2 cp = make_double2(0.0, 0.0);
+    col_inverse_store(s, ct, tcol, a.Cout + c * 32);
+}
+
+struct OutLds {
+    double sx[1088];          // x[t0 - 1023 .. t0 + 64]
+    double sh[kSP];           // h[0 .. 1023]
+    double2 col[kCols][32];   // the tail's inverse columns
+    double2 tw[64];
+    double part[32][65];      // head partials [tap group][output]
+    double tpart[4][64];      // tail partials [column group][output]
+};
+union StreamLds {
+    ColLds col;
+    OutLds out;
+};
+
+// One 1024-sample block, three roles with no data shared inside the launch (tests/stream_model.py):
+//   blocks [0, 33)  transform column c: Z_b's bins from the window, into the ring; Y_{b+1} = H_1 Z_b
+//                   + H_2 Z_{b-1} + R_{b+1}; its inverse column -> Cout (the next block's tail)
+//   blocks [33, 66) MAC column c: R_{b+2} = sum_{p >= 3} H_p Z_{b+2-p} over the ring -> Rout
+//   blocks [66, 82) 64 outputs each: head (h[0..1023] direct, the partition-0 term of overlap-save)
+//                   + tail (the 33 columns Cin of the previous launch, Hermitian-combined)
+// QI = Q / 8: partitions per MAC thread.
+template <int QI>
+__global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
+    __shared__ StreamLds u;
+    const int t = threadIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
+    const int blk = blockIdx.x;
+    if (blk < kCols) {
+        // ---------------- transform column
+        ColLds& s = u.col;
+        const int c = blk;
+        double v[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) cp = cadd(cp, cmulc(ct.t32[q], s.y[4 * g + q]));
-    cp = half_sum(cp);
-    if (l < 32) s.c[w][j] = cp;
-    __syncthreads();
-    if (w == 0) {
-        if (l < 32) {
-            const double2 C = cmulc(tcol, cadd(cadd(s.c[0][l], s.c[1][l]), cadd(s.c[2][l], s.c[3][l])));
-            // write-through (sc1) stores: the last workgroup reads them with sc1 loads, no fences
-            double* dst = a.xch + 2 * (c * 32 + l);
-            st_sc1(dst, C.x);
-            st_sc1(dst + 1, C.y);
+        for (int i = 0; i < 4; ++i) v[i] = a.line[a.prev + 32 * (g + 8 * i) + j];
+#pragma unroll
+        for (int i = 4; i < 8; ++i) v[i] = a.x[32 * (g + 8 * i - 32) + j];
+        double2 h1 = make_double2(0.0, 0.0), h2 = h1, z1 = h1, rn = h1;
+        if (t < 32) {
+            h1 = a.HS[((long)1 * kCols + c) * 32 + t];
+            h2 = a.HS[((long)2 * kCols + c) * 32 + t];
+            z1 = a.ZS[((long)ring_slot(a.head, 1, a.Q) * kCols + c) * 32 + t];
+            rn = a.Rin[c * 32 + t];
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this (only) storing wave
-        if (l == 0) {
-            const unsigned prev = __hip_atomic_fetch_add(a.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s.last = prev == kCols - 1;
+        ColTw ct;
+        ct.load(a.tw, c, j, g);
+        const double2 tcol = a.tw[kTw2k + j * c];
+        const double2 a1 = stage1(v, ct.t64);
+        if (l < 32) s.a[w][j] = a1;
+        __syncthreads();
+        const double2 xp = stage3(s, g, ct.t2k, ct.t32);
+        if (l < 32) s.x[w][j] = xp;
+        __syncthreads();
+        if (t < 32) {
+            const double2 X = cadd(cadd(s.x[0][t], s.x[1][t]), cadd(s.x[2][t], s.x[3][t]));
+            a.ZS[((long)a.head * kCols + c) * 32 + t] = X;
+            s.y[t] = cadd(cadd(cmul(h1, X), cmul(h2, z1)), rn);
         }
-    }
-    __syncthreads();
-    if (!s.last) return;
-    // ---- last workgroup: the 33 columns (sc1 loads) and W_64 into LDS, then the outputs
-    // out[32 m + n2] = C0 + (-1)^n1 C32 + 2 Re sum_{k1=1}^{31} W_64^(-n1 k1) C[k1], n1 = 32 + m
-    {
-        double* cl = &s.col[0][0].x;
-        for (int i = t; i < kCols * 64; i += kT)
-            cl[i] = ld_sc1(a.xch + i);
-        if (t < 64) s.tw[t] = a.tw[kTw64 + t];
-    }
-    __syncthreads();
-    if (t == 0) __hip_atomic_store(a.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const double c0 = s.col[0][j].x, c32 = s.col[32][j].x;
-    double acc[4];
+        __syncthreads();
+        col_inverse_store(s, ct, tcol, a.Cout + c * 32);
+    } else if (blk < 2 * kCols) {
+        // ---------------- MAC column: R_{b+2}
+        ColLds& s = u.col;
+        const int c = blk - kCols;
+        double2 hv[QI], zv[QI];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] = 0.0;
-#pragma unroll
-    for (int k1 = 1; k1 < 32; ++k1) {
-        const double2 C = s.col[k1][j];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int n1 = 32 + g + 8 * r;
-            const double2 wv = s.tw[(n1 * k1) & 63];
-            acc[r] = fma(wv.x, C.x, fma(wv.y, C.y, acc[r]));
+        for (int i = 0; i < QI; ++i) {
+            const int p = 3 + g + 8 * i;   // < Q + 8: rows past Q are zero
+            hv[i] = a.HS[((long)p * kCols + c) * 32 + j];
+            zv[i] = a.ZS[((long)ring_slot(a.head, p - 2, a.Q) * kCols + c) * 32 + j];
         }
-    }
+        double2 r = make_double2(0.0, 0.0);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int m = g + 8 * r;
-        const double sgn = (m & 1) ? -c32 : c32;   // (-1)^n1, n1 = 32 + m
-        a.out[32 * m + j] = c0 + sgn + 2.0 * acc[r];
+        for (int i = 0; i < QI; ++i) r = cadd(r, cmul(hv[i], zv[i]));
+        r = half_sum(r);
+        if (l < 32) s.m[w][j] = r;
+        __syncthreads();
+        if (t < 32) a.Rout[c * 32 + t] = cadd(cadd(s.m[0][t], s.m[1][t]), cadd(s.m[2][t], s.m[3][t]));
+    } else {
+        // ---------------- 64 outputs: head + tail
+        OutLds& s = u.out;
+        const int k = blk - 2 * kCols;
+        const int t0 = 64 * k;
+        // every global load of the thread in flight before the first LDS store (a load -> store
+        // chain per loop iteration waited one memory latency each): window positions 64k + 1 ..
+        // 64k + 1087 (2048-sample window: previous block | this block), h[0..1023], the columns
+        double xv[5], hv[4];
+        double2 cv[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const int i = min(t + q * kT, 1086);
+            const int wp = t0 + 1 + i;
+            xv[q] = wp < kSP ? a.line[a.prev + wp] : a.x[wp - kSP];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) hv[q] = a.h[t + q * kT];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) cv[q] = a.Cin[min(t + q * kT, kCols * 32 - 1)];
+        const double2 twv = a.tw[kTw64 + (t & 63)];
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            if (t + q * kT < 1087) s.sx[t + q * kT] = xv[q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s.sh[t + q * kT] = hv[q];
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            if (t + q * kT < kCols * 32) (&s.col[0][0])[t + q * kT] = cv[q];
+        if (t < 64) s.tw[t] = twv;
+        __syncthreads();
+        // the block's samples into the ring (both mirror positions), for the next calls
+        if (t < 64) {
+            const double xv = s.sx[1023 + t];
+            const long kk = a.wpos + t0 + t;
+            a.line[kk] = xv;
+            a.line[kk + a.R] = xv;
+        }
+        // head: thread = 8 outputs (o8) x 32 taps (q): y[j] += h[tau] x[t0 + j - tau]
+        {
+            const int o8 = t & 7, q = t >> 3;
+            const int j0 = 8 * o8, tau0 = 32 * q;
+            double xs[39], hs[32], acc[8];
+#pragma unroll
+            for (int i = 0; i < 39; ++i) xs[i] = s.sx[1023 + j0 - tau0 - 31 + i];   // x[t0 + j0 - tau0 - 31 + i]
+#pragma unroll
+            for (int i = 0; i < 32; ++i) hs[i] = s.sh[tau0 + i];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) acc[r] = 0.0;
+#pragma unroll
+            for (int i = 0; i < 32; ++i)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) acc[r] = fma(hs[i], xs[31 + r - i], acc[r]);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) s.part[q][j0 + r] = acc[r];
+        }
+        // tail partials: output o (t & 63), columns c = 1 + cg + 4 i (cg = t >> 6)
+        {
+            const int o = t & 63, cg = t >> 6;
+            const int n = t0 + o, m = n >> 5, n2 = n & 31, n1 = 32 + m;
+            double acc = 0.0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int c = 1 + cg + 4 * i;
+                if (c < 32) {
+                    const double2 C = s.col[c][n2], wv = s.tw[(n1 * c) & 63];
+                    acc = fma(wv.x, C.x, fma(wv.y, C.y, acc));
+                }
+            }
+            acc *= 2.0;
+            if (cg == 0) acc += s.col[0][n2].x + ((n1 & 1) ? -s.col[32][n2].x : s.col[32][n2].x);
+            s.tpart[cg][o] = acc;
+        }
+        __syncthreads();
+        if (t < 64) {
+            double y = 0.0;
+#pragma unroll
+            for (int q = 0; q < 32; ++q) y += s.part[q][t];
+            const double tail = (s.tpart[0][t] + s.tpart[1][t]) + (s.tpart[2][t] + s.tpart[3][t]);
+            a.out[t0 + t] = y + tail;
+        }
     }
 }
 
 typedef void (*BlockKernel)(StreamArgs);
-template <int... I>
-BlockKernel pick_block_impl(int qi, std::integer_sequence<int, I...>) {
+template <template <int> class K, int... I>
+BlockKernel pick_impl(int qi, std::integer_sequence<int, I...>) {
     BlockKernel k = nullptr;
-    ((qi == I + 1 ? (k = stream_block_kernel<I + 1>, 0) : 0), ...);
+    ((qi == I + 1 ? (k = K<I + 1>::fn, 0) : 0), ...);
     return k;
 }
-BlockKernel pick_block(int qi) { return pick_block_impl(qi, std::make_integer_sequence<int, 16>()); }
+template <int QI>
+struct BlockK {
+    static constexpr BlockKernel fn = stream_block_kernel<QI>;
+};
+template <int QI>
+struct Prime2K {
+    static constexpr BlockKernel fn = stream_prime2_kernel<QI>;
+};
+BlockKernel pick_block(int qi) { return pick_impl<BlockK>(qi, std::make_integer_sequence<int, 16>()); }
+BlockKernel pick_prime2(int qi) { return pick_impl<Prime2K>(qi, std::make_integer_sequence<int, 16>()); }
 
 // line[i] = line[i + R] = src[i], i < n, from write position wpos
 __global__ __launch_bounds__(256) void stream_put_kernel(const double* __restrict__ src, long n, double* __restrict__ line,
@@ -344,13 +453,16 @@ int stream_setup(hz_fb* h) {
         S.head = 0;
     }
     HZ_TRY(s_alloc(&S.d_line, &S.line_cap, (size_t)(2 * ring)));
-    const size_t spec = (size_t)(K / kSP) * kCols * 32 * 2;
-    HZ_TRY(s_alloc(&S.d_ZS, &S.zs_cap, spec));
-    HZ_TRY(s_alloc(&S.d_HS, &S.hs_cap, spec));
-    if (!S.d_xch) HZ_TRY_HIP(hipMalloc(&S.d_xch, sizeof(double) * kCols * 64));
-    if (!S.d_count) {
-        HZ_TRY_HIP(hipMalloc(&S.d_count, sizeof(unsigned) * 64));
-        HZ_TRY_HIP(hipMemset(S.d_count, 0, sizeof(unsigned) * 64));
+    const size_t col = (size_t)kCols * 32 * 2;   // doubles per spectrum (33 columns x 32 bins)
+    const size_t zcap = S.zs_cap, hcap = S.hs_cap;
+    HZ_TRY(s_alloc(&S.d_ZS, &S.zs_cap, (size_t)(K / kSP) * col));
+    HZ_TRY(s_alloc(&S.d_HS, &S.hs_cap, (size_t)(K / kSP + 8) * col));   // 8 zero rows past Q
+    // zero rows (and never-written slots) must be exact zeros: the MAC multiplies them
+    if (S.zs_cap != zcap) HZ_TRY_HIP(hipMemset(S.d_ZS, 0, sizeof(double) * S.zs_cap));
+    if (S.hs_cap != hcap) HZ_TRY_HIP(hipMemset(S.d_HS, 0, sizeof(double) * S.hs_cap));
+    if (!S.d_CR) {   // tail columns C and MAC sums R, two parities each
+        HZ_TRY_HIP(hipMalloc(&S.d_CR, sizeof(double) * 4 * col));
+        HZ_TRY_HIP(hipMemset(S.d_CR, 0, sizeof(double) * 4 * col));
     }
     if (!S.d_tw) {   // in long double
         std::vector<double2> tw(kTwN);
@@ -399,8 +511,17 @@ StreamArgs stream_args(hz_fb* h) {
     a.Q = (int)(h->resp.K / kSP);
     a.head = S.head;
     a.tw = (const double2*)S.d_tw;
-    a.xch = S.d_xch;
-    a.count = S.d_count;
+    a.h = h->resp.d_h;
+    // C_b in parity b, R_b in parity b (block counter blk): this launch reads C_b, R_{b+1} and
+    // writes C_{b+1}, R_{b+2}
+    const size_t col = (size_t)kCols * 32;
+    double2* C = (double2*)S.d_CR;
+    double2* Rb = C + 2 * col;
+    const int b = (int)(S.blk & 1);
+    a.Cin = C + b * col;
+    a.Cout = C + (b ^ 1) * col;
+    a.Rin = Rb + (b ^ 1) * col;
+    a.Rout = Rb + b * col;
     return a;
 }
 
@@ -435,9 +556,13 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
         S.hs_gen = R.h_gen;
     }
     if (!S.line_hist) HZ_TRY(hist_to_line(h));
-    if (!S.fdl_valid) {
+    if (!S.fdl_valid) {   // the ring of window spectra, the first block's tail columns and R
         hipLaunchKernelGGL(stream_prime_kernel, dim3(kCols, (unsigned)(Q - 1)), dim3(kT), 0, h->stream, stream_args(h));
         HZ_TRY_HIP(hipGetLastError());
+        S.blk = 1;   // prime2 writes as the launch before block 0 would: C_0 -> parity 0, R_1 -> parity 1
+        hipLaunchKernelGGL(pick_prime2(Q / 8), dim3(kCols), dim3(kT), 0, h->stream, stream_args(h));
+        HZ_TRY_HIP(hipGetLastError());
+        S.blk = 0;
         S.fdl_valid = true;
     }
     StreamArgs a = stream_args(h);
@@ -449,7 +574,7 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
         HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
         h->ev_skip[(e - h->ev.data()) / 5] |= 2 | 8;
     }
-    hipLaunchKernelGGL(pick_block(Q / 8), dim3(kCols), dim3(kT), 0, h->stream, a);
+    hipLaunchKernelGGL(pick_block(Q / 8), dim3(2 * kCols + kSP / 64), dim3(kT), 0, h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     if (e) {
         HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
@@ -458,6 +583,7 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
     }
     S.pos += n;
     S.head = (S.head + 1) % Q;
+    ++S.blk;
     S.pend += n;
     ++S.calls;
     R.implicit = true;
@@ -543,10 +669,8 @@ void fb_stream_reset(hz_fb* h) {
 
 void fb_stream_free(hz_fb* h) {
     hz_fb::Resp::Stream& S = h->resp.st;
-    for (double* p : {S.d_line, S.d_ZS, S.d_HS, S.d_xch})
+    for (double* p : {S.d_line, S.d_ZS, S.d_HS, S.d_CR, S.d_tw})
         if (p) (void)hipFree(p);
-    if (S.d_tw) (void)hipFree(S.d_tw);
-    if (S.d_count) (void)hipFree(S.d_count);
     const bool on = S.on;
     S = hz_fb::Resp::Stream();
     S.on = on;

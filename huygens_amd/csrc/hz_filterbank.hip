@@ -1057,6 +1057,9 @@ int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double*
         hz::set_error("hz_fb_coefficients: invalid arguments");
         return HZ_E_INVALID;
     }
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    ++h->coef_gen;
+    h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
     if (n < 0 || n >= h->N_total) {
         hz::set_error("hz_fb_coefficients: band %d out of range [0,%d)", n, h->N_total);
@@ -1074,6 +1077,9 @@ int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double*
 
 int hz_fb_boost(hz_fb* h, int n, double v) {
     if (!h) return HZ_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    ++h->pg_gen;
+    h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
@@ -1091,6 +1097,9 @@ int hz_fb_boost(hz_fb* h, int n, double v) {
 
 int hz_fb_boost_all(hz_fb* h, const double* v, int count) {
     if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    ++h->pg_gen;
+    h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
@@ -1104,6 +1113,9 @@ int hz_fb_boost_all(hz_fb* h, const double* v, int count) {
 
 int hz_fb_mix(hz_fb* h, int n, double v) {
     if (!h) return HZ_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    ++h->pg_gen;
+    h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
@@ -1121,6 +1133,9 @@ int hz_fb_mix(hz_fb* h, int n, double v) {
 
 int hz_fb_mix_all(hz_fb* h, const double* v, int count) {
     if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    ++h->pg_gen;
+    h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
@@ -1134,6 +1149,9 @@ int hz_fb_mix_all(hz_fb* h, const double* v, int count) {
 
 int hz_fb_open(hz_fb* h) {
     if (!h) return HZ_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    ++h->pg_gen;
+    h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
@@ -1147,6 +1165,7 @@ int hz_fb_set_distortion(hz_fb* h, int dist_id, double param) {
         hz::set_error("hz_fb_set_distortion: unknown functor %d", dist_id);
         return HZ_E_INVALID;
     }
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
     h->dist_id = dist_id;
     h->dist_param = param;
     return HZ_OK;
@@ -1158,6 +1177,7 @@ int hz_fb_process_device(hz_fb* h, const double* d_in, double* d_out, size_t n) 
         hz::set_error("hz_fb_process_device: null handle or buffer");
         return HZ_E_INVALID;
     }
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
     if (h->rt.computed) {   // the cached sample first (fb_rt_resolve), copied from pinned memory
         HZ_TRY_HIP(hipSetDevice(h->device));
         double y0 = 0;
@@ -1181,6 +1201,7 @@ int hz_fb_process(hz_fb* h, const double* in, double* out, size_t n) {
         hz::set_error("hz_fb_process: null handle or buffer");
         return HZ_E_INVALID;
     }
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
     if (h->rt.computed) {   // the cached sample first (fb_rt_resolve)
         HZ_TRY_HIP(hipSetDevice(h->device));
         const int k = hz_fbi::fb_rt_resolve(h, out);
@@ -1239,6 +1260,8 @@ int hz_fb_state_size(hz_fb* h, size_t* count) {
 }
 
 int hz_fb_get_state(hz_fb* h, double* buf, size_t count) {
+    if (!h) return HZ_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
     HZ_TRY(fb_check(h));
     size_t need;
     hz_fb_state_size(h, &need);
@@ -1255,6 +1278,8 @@ int hz_fb_get_state(hz_fb* h, double* buf, size_t count) {
 }
 
 int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
+    if (!h) return HZ_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
     HZ_TRY(fb_check(h));
     size_t need;
     hz_fb_state_size(h, &need);
@@ -1277,10 +1302,19 @@ int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
 }
 
 int hz_fb_tick(hz_fb* h) {
+    if (!h) return HZ_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
     HZ_TRY(fb_check(h));
     return hz_fbi::fb_tick_rotate(h);
 }
 
+
+int hz_fb_setter_seq(hz_fb* h, long long* seq) {
+    if (!h || !seq) return HZ_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    *seq = h->setter_seq;
+    return HZ_OK;
+}
 
 int hz_fb_info(hz_fb* h, int* order, int* N_local, int* band_begin, int* N_total) {
     if (!h) return HZ_E_INVALID;

@@ -28,6 +28,7 @@
 //
 // Layout in HBM: ring [C] doubles; grains [G] x 64 B per block (uploaded once per call).
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <deque>
@@ -36,6 +37,7 @@
 #include <vector>
 
 #include "hz_common.h"
+#include "hz_rt.h"
 
 namespace {
 
@@ -44,13 +46,7 @@ constexpr long kChunk = 1L << 18;             // samples per launch
 constexpr long kTile = 4096;                  // samples sharing one grain list (multiple of kThreads)
 constexpr long kNever = 1L << 62;             // t_end of a grain that never finishes (NaN/inf size)
 
-struct alignas(16) GrainDev {
-    long t_first, t_end;                      // reads at t_first <= t < t_end
-    double offsets, sizes, speeds, gains;     // granulator.h:67-70 (samples, samples, ratio, gain)
-    unsigned ticks0, pad0;
-    double rsizes;                            // RN(1 / sizes) for a normal finite quotient, else 0
-};
-static_assert(sizeof(GrainDev) == 64, "grain record is one 64 B line");
+typedef hz_rt::Grain GrainDev;   // one 64-B line (shared with the per-sample server)
 
 struct GranArgs {
     double* out;
@@ -143,6 +139,7 @@ __global__ __launch_bounds__(kThreads) void gran_kernel(GranArgs a) {
 }  // namespace
 
 struct hz_gran {
+    long uid = 0;                     // unique per handle (the per-sample server's grain-cache key)
     unsigned polyphony = 0, size = 0;
     int device = 0;
     long T = 0;                       // samples processed
@@ -166,6 +163,14 @@ struct hz_gran {
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     long launches = 0, grain_samples = 0;
+    bool pending = false;             // block work queued on the stream since the last synchronisation
+    // per-sample calls (hz_gran_sample): the grains that may still read, in voice order, in pinned
+    // memory for the server (which caches them by version)
+    GrainDev* h_list = nullptr;
+    size_t list_cap = 0;
+    int list_count = 0;
+    long list_version = 0, list_min_end = 0;
+    bool list_dirty = true;
 };
 
 namespace {
@@ -208,6 +213,7 @@ int gran_alloc(hz_gran* h, long t, unsigned ticks0, double offset, double size, 
     else m = (long)std::ceil(g.sizes) - ticks0 + 1;
     g.t_end = m >= kNever - g.t_first ? kNever : g.t_first + m;
     h->busy_until[voice] = g.t_end;
+    h->list_dirty = true;
     h->tree[node] = g.t_end;
     for (unsigned q = node >> 1; q >= 1; q >>= 1) h->tree[q] = std::min(h->tree[2 * q], h->tree[2 * q + 1]);
     h->vg[voice].push_back(g);
@@ -339,6 +345,8 @@ int gran_run(hz_gran* h, const double* d_in, double* d_out, long n, const hz_gra
         }
     }
     h->T += n;
+    h->pending = true;
+    h->list_dirty = true;
     return HZ_OK;
 }
 
@@ -355,6 +363,8 @@ int hz_gran_create(unsigned polyphony, unsigned buffer_size, int device, hz_gran
     HZ_TRY(hz::select_device(device));
     hz_gran* h = new (std::nothrow) hz_gran();
     if (!h) return HZ_E_ALLOC;
+    static std::atomic<long> next_uid{1};
+    h->uid = next_uid++;
     h->polyphony = polyphony;
     h->size = buffer_size + (buffer_size == 0 ? 1u : 0u);   // buffer.h:21 (size zero disallowed)
     h->device = device;
@@ -391,6 +401,7 @@ int hz_gran_destroy(hz_gran* h) {
     for (void* p : {(void*)h->d_ring, (void*)h->d_g, (void*)h->d_in, (void*)h->d_out})
         if (p) (void)hipFree(p);
     if (h->h_g) (void)hipHostFree(h->h_g);
+    if (h->h_list) (void)hipHostFree(h->h_list);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     if (h->up_ev) (void)hipEventDestroy(h->up_ev);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -428,6 +439,63 @@ int hz_gran_process(hz_gran* h, const double* in, double* out, size_t n, const h
     HZ_TRY(gran_run(h, h->d_in, h->d_out, (long)n, reqs, nreq, voices));
     HZ_TRY_HIP(hipMemcpyAsync(out, h->d_out, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    return HZ_OK;
+}
+
+// one sample through the device's per-sample server (hz_rt.hip OP_GRAN): the reference's
+// `source.write(x); y = granny(); granny.tick();` (tests/granny.cpp:36-56) without a launch per sample
+int hz_gran_sample(hz_gran* h, double x, double* y) {
+    HZ_TRY(gran_check(h));
+    if (!y) return HZ_E_INVALID;
+    if (h->pending) {   // the ring's block-call writes land before the server reads it
+        HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+        h->pending = false;
+    }
+    for (auto& q : h->vg)
+        while (!q.empty() && q.front().t_end <= h->T) q.pop_front();
+    if (h->list_dirty || h->list_min_end <= h->T) {   // grains started or ended: a new list version
+        size_t cnt = 0;
+        for (const auto& q : h->vg) cnt += q.size();
+        if (cnt > (size_t)hz_rt::kMaxGrains) {
+            hz::set_error("hz_gran_sample: %zu grains pending (the per-sample server holds %d)", cnt, hz_rt::kMaxGrains);
+            return HZ_E_UNSUPPORTED;
+        }
+        if (cnt > h->list_cap || !h->h_list) {
+            if (h->h_list) HZ_TRY_HIP(hipHostFree(h->h_list));
+            h->h_list = nullptr;
+            h->list_cap = std::max<size_t>(cnt, 64);
+            HZ_TRY_HIP(hipHostMalloc((void**)&h->h_list, sizeof(GrainDev) * h->list_cap,
+                                     hipHostMallocCoherent | hipHostMallocMapped));
+        }
+        long mn = kNever;
+        int k = 0;
+        for (const auto& q : h->vg)   // voice order (the reference's summation order)
+            for (const GrainDev& g : q) {
+                h->h_list[k++] = g;
+                mn = std::min(mn, g.t_end);
+            }
+        h->list_count = k;
+        h->list_min_end = mn;
+        ++h->list_version;
+        h->list_dirty = false;
+    }
+    hz_rt::Server* srv = hz_rt::server(h->device);
+    if (!srv) return HZ_E_NODEV;
+    hz_rt::GranArgs a{};
+    a.ring = h->d_ring;
+    a.grains = (const hz_rt::Grain*)hz_rt::dev(srv, h->h_list);
+    a.mask = h->mask;
+    a.t = h->T;
+    a.key = h->uid;
+    a.version = h->list_version;
+    a.x = x;
+    a.fm = h->size == 1u ? 0ul : ~0ul / h->size + 1ul;
+    a.count = h->list_count;
+    a.size = h->size;
+    a.origin = (unsigned)(h->T % (long)h->size);
+    a.wrap1 = 0xffffffffu % h->size;
+    HZ_TRY(hz_rt::call(srv, hz_rt::OP_GRAN, &a, sizeof(a), 1, y));
+    h->T += 1;
     return HZ_OK;
 }
 

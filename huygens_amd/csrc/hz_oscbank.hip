@@ -269,6 +269,14 @@ struct hz_osc {
     std::vector<hipEvent_t> ev;
     size_t ev_used = 0;
     long launches = 0;
+    // per-sample calls (operator() / mixdown() / tick() of the drop-in) are served from a
+    // speculative block: the phasors and mixes of the next la_L samples rendered at once from a
+    // snapshot (an Oscbank has no input); setters roll the phasors back to the consumed sample
+    // (huygens_hip.h, hz_add_fill)
+    long la_L = 0, la_n = 0, la_pos = 0;
+    double *d_la_pb = nullptr, *d_la_mix = nullptr, *d_z_snap = nullptr;
+    double* la_mix = nullptr;          // pinned [la_L][2]
+    double* la_pb = nullptr;           // pinned [la_L][N][2] per-band rows (small banks: N la_L <= 2^18)
 };
 
 namespace {
@@ -381,6 +389,40 @@ int osc_launch(hz_osc* h, double* d_mix, double* d_per_band, long n) {
     return HZ_OK;
 }
 
+int osc_settle(hz_osc* h) {
+    if (h->la_pos < h->la_n) {
+        HZ_TRY_HIP(hipMemcpyAsync(h->d_z, h->d_z_snap, sizeof(double) * 2 * h->N, hipMemcpyDeviceToDevice, h->stream));
+        const long m = h->la_pos;
+        h->la_n = h->la_pos = 0;
+        if (m > 0) HZ_TRY(osc_launch(h, nullptr, nullptr, m));   // the consumed ticks again
+    }
+    h->la_n = h->la_pos = 0;
+    return HZ_OK;
+}
+
+int osc_look_ahead(hz_osc* h) {
+    if (!h->la_L) {
+        h->la_L = std::min<long>(1024, std::max<long>(16, (1L << 21) / std::max(1, h->N)));
+        HZ_TRY_HIP(hipMalloc(&h->d_la_pb, sizeof(double) * 2 * h->la_L * h->N));
+        HZ_TRY_HIP(hipMalloc(&h->d_la_mix, sizeof(double) * 2 * h->la_L));
+        HZ_TRY_HIP(hipMalloc(&h->d_z_snap, sizeof(double) * 2 * h->N));
+        HZ_TRY_HIP(hipHostMalloc((void**)&h->la_mix, sizeof(double) * 2 * h->la_L));
+        if ((long)h->N * h->la_L <= (1L << 18))   // small banks: operator() reads host memory
+            HZ_TRY_HIP(hipHostMalloc((void**)&h->la_pb, sizeof(double) * 2 * h->la_L * h->N));
+    }
+    HZ_TRY(osc_upload(h));
+    HZ_TRY_HIP(hipMemcpyAsync(h->d_z_snap, h->d_z, sizeof(double) * 2 * h->N, hipMemcpyDeviceToDevice, h->stream));
+    HZ_TRY(osc_launch(h, h->d_la_mix, h->d_la_pb, h->la_L));
+    HZ_TRY_HIP(hipMemcpyAsync(h->la_mix, h->d_la_mix, sizeof(double) * 2 * h->la_L, hipMemcpyDeviceToHost, h->stream));
+    if (h->la_pb)
+        HZ_TRY_HIP(hipMemcpyAsync(h->la_pb, h->d_la_pb, sizeof(double) * 2 * h->la_L * h->N, hipMemcpyDeviceToHost,
+                                  h->stream));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+    h->la_n = h->la_L;
+    h->la_pos = 0;
+    return HZ_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -433,8 +475,10 @@ int hz_osc_destroy(hz_osc* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (void* p : {(void*)h->d_rec, (void*)h->d_z, (void*)h->d_partial, (void*)h->d_mix, (void*)h->d_pb,
-                    (void*)h->d_act, (void*)h->d_active})
+                    (void*)h->d_act, (void*)h->d_active, (void*)h->d_la_pb, (void*)h->d_la_mix, (void*)h->d_z_snap})
         if (p) (void)hipFree(p);
+    if (h->la_mix) (void)hipHostFree(h->la_mix);
+    if (h->la_pb) (void)hipHostFree(h->la_pb);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -443,6 +487,8 @@ int hz_osc_destroy(hz_osc* h) {
 
 int hz_osc_freqmod(hz_osc* h, int index, double hz) {
     if (!h) return HZ_E_INVALID;
+    HZ_TRY(osc_check(h));
+    HZ_TRY(osc_settle(h));
     const int l = osc_local(h, index);  // out of range: ignored, as oscbank.h:51
     if (l < 0) return HZ_OK;
     h->wr[l] = std::cos(2 * hz::kPI * hz / hz::kSR);
@@ -453,6 +499,8 @@ int hz_osc_freqmod(hz_osc* h, int index, double hz) {
 
 int hz_osc_activate(hz_osc* h, const int* idx, int count) {
     if (!h || (count > 0 && !idx) || count < 0) return HZ_E_INVALID;
+    HZ_TRY(osc_check(h));
+    HZ_TRY(osc_settle(h));
     for (int c = 0; c < count; ++c) {
         const int l = osc_local(h, idx[c]);  // out of range: ignored (multichannel.h:90)
         if (l >= 0 && !h->active[l]) {
@@ -465,6 +513,8 @@ int hz_osc_activate(hz_osc* h, const int* idx, int count) {
 
 int hz_osc_deactivate(hz_osc* h, const int* idx, int count) {
     if (!h || (count > 0 && !idx) || count < 0) return HZ_E_INVALID;
+    HZ_TRY(osc_check(h));
+    HZ_TRY(osc_settle(h));
     for (int c = 0; c < count; ++c) {
         const int l = osc_local(h, idx[c]);
         if (l >= 0 && h->active[l]) {
@@ -477,6 +527,8 @@ int hz_osc_deactivate(hz_osc* h, const int* idx, int count) {
 
 int hz_osc_open(hz_osc* h) {
     if (!h) return HZ_E_INVALID;
+    HZ_TRY(osc_check(h));
+    HZ_TRY(osc_settle(h));
     std::fill(h->active.begin(), h->active.end(), 1);
     h->dirty_act = true;
     return HZ_OK;
@@ -484,6 +536,8 @@ int hz_osc_open(hz_osc* h) {
 
 int hz_osc_close(hz_osc* h) {
     if (!h) return HZ_E_INVALID;
+    HZ_TRY(osc_check(h));
+    HZ_TRY(osc_settle(h));
     std::fill(h->active.begin(), h->active.end(), 0);
     h->dirty_act = true;
     return HZ_OK;
@@ -500,6 +554,7 @@ int hz_osc_active_count(hz_osc* h, int* count) {
 int hz_osc_fill_device(hz_osc* h, double* d_mix, double* d_per_band, size_t n) {
     HZ_TRY(osc_check(h));
     if (n == 0) return HZ_OK;
+    HZ_TRY(osc_settle(h));
     HZ_TRY(osc_upload(h));
     return osc_launch(h, d_mix, d_per_band, (long)n);
 }
@@ -507,6 +562,12 @@ int hz_osc_fill_device(hz_osc* h, double* d_mix, double* d_per_band, size_t n) {
 int hz_osc_fill(hz_osc* h, double* mix, double* per_band, size_t n) {
     HZ_TRY(osc_check(h));
     if (n == 0) return HZ_OK;
+    if (n == 1 && !mix && !per_band) {   // tick(): from the speculative block
+        if (h->la_pos == h->la_n) HZ_TRY(osc_look_ahead(h));
+        ++h->la_pos;
+        return HZ_OK;
+    }
+    HZ_TRY(osc_settle(h));
     if (mix && 2 * n > h->mix_cap) {
         if (h->d_mix) HZ_TRY_HIP(hipFree(h->d_mix));
         h->d_mix = nullptr;
@@ -532,6 +593,17 @@ int hz_osc_fill(hz_osc* h, double* mix, double* per_band, size_t n) {
 int hz_osc_phases(hz_osc* h, double* z) {
     HZ_TRY(osc_check(h));
     if (!z) return HZ_E_INVALID;
+    if (h->la_L) {   // per-sample use: the row of the speculative block
+        if (h->la_pos == h->la_n) HZ_TRY(osc_look_ahead(h));
+        if (h->la_pb) {
+            std::memcpy(z, h->la_pb + 2 * (size_t)h->la_pos * h->N, sizeof(double) * 2 * h->N);
+            return HZ_OK;
+        }
+        HZ_TRY_HIP(hipMemcpyAsync(z, h->d_la_pb + 2 * (size_t)h->la_pos * h->N, sizeof(double) * 2 * h->N,
+                                  hipMemcpyDeviceToHost, h->stream));
+        HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+        return HZ_OK;
+    }
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
     HZ_TRY_HIP(hipMemcpy(z, h->d_z, sizeof(double) * 2 * h->N, hipMemcpyDeviceToHost));
     return HZ_OK;
@@ -540,6 +612,12 @@ int hz_osc_phases(hz_osc* h, double* z) {
 int hz_osc_mixdown(hz_osc* h, double* mix) {   // oscbank.h:81-90, without advancing
     HZ_TRY(osc_check(h));
     if (!mix) return HZ_E_INVALID;
+    if (h->la_L) {   // per-sample use: the speculative block's mix (the engine's summation order)
+        if (h->la_pos == h->la_n) HZ_TRY(osc_look_ahead(h));
+        mix[0] = h->la_mix[2 * h->la_pos];
+        mix[1] = h->la_mix[2 * h->la_pos + 1];
+        return HZ_OK;
+    }
     std::vector<double> z(2 * (size_t)h->N);
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
     HZ_TRY_HIP(hipMemcpy(z.data(), h->d_z, sizeof(double) * z.size(), hipMemcpyDeviceToHost));
@@ -557,6 +635,7 @@ int hz_osc_mixdown(hz_osc* h, double* mix) {   // oscbank.h:81-90, without advan
 int hz_osc_set_phases(hz_osc* h, const double* z) {
     HZ_TRY(osc_check(h));
     if (!z) return HZ_E_INVALID;
+    HZ_TRY(osc_settle(h));
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
     HZ_TRY_HIP(hipMemcpy(h->d_z, z, sizeof(double) * 2 * h->N, hipMemcpyHostToDevice));
     return HZ_OK;

@@ -1,0 +1,109 @@
+// hz_rt.h -- the per-sample server (hz_rt.hip): one resident kernel per device that serves the
+// per-sample operator calls of every input-driven bank -- Filterbank operator()/tick()
+// (src/filterbank.h:125-148), Delay/Delaybank operator()/tick() (src/delay.h:71-97) and
+// Granulator operator()/tick() with its source Buffer (src/granulator.h:81-104) -- through a
+// mailbox in pinned host memory.  The reference calls these once per sample inside the audio
+// callback (tests/resynthesis.cpp:35-39, tests/delay.cpp:20-28, tests/granny.cpp:32-56), and a
+// caller may feed an output back into the next input, so a sample cannot wait for a block.
+//
+// One server for all handles (instead of a resident kernel per handle): with GPU_MAX_HW_QUEUES
+// hardware queues per process, a resident kernel per handle occupied one queue each and every
+// other stream mapped onto that queue waited for its idle exit.  The server runs on a stream of
+// the highest priority (its own hardware queue) and leaves after kIdleNs without a request.
+#pragma once
+
+#include <mutex>
+
+#include "hz_common.h"
+
+namespace hz_rt {
+
+constexpr int kGroups = 8;      // workgroups of the resident kernel (each polls the mailbox)
+constexpr int kThreads = 512;   // threads per workgroup (units per workgroup per pass)
+constexpr int kMaxGrains = 1024;
+
+enum : int { OP_NONE = 0, OP_FB = 1, OP_DLY = 2, OP_GRAN = 3, OP_STOP = 4 };
+
+// Granulator grain record (hz_granulator.hip: the block engine's layout, one 64-B line)
+struct alignas(16) Grain {
+    long t_first, t_end;                      // reads at t_first <= t < t_end
+    double offsets, sizes, speeds, gains;     // granulator.h:67-70 (samples, samples, ratio, gain)
+    unsigned ticks0, pad0;
+    double rsizes;                            // RN(1 / sizes) for a normal finite quotient, else 0
+};
+static_assert(sizeof(Grain) == 64, "grain record is one 64 B line");
+
+// ---- op arguments (copied into the request line; <= kArgWords 8-byte words) ------------------
+// Filterbank sample: ring rows R [N][O+1] in ring order (R[0..O-1] = y[t-1 .. t-O], R[O] = the
+// row at origin), smoothers pg [N][2], coefficients [N][2O+1], targets pin / gin [N].
+struct FbArgs {
+    double* R;
+    double* pg;
+    const double* coef;
+    double* pin;
+    double* gin;
+    const double* reload;   // (device address of pinned payload) [N] pin then [N] gin, or null
+    const double* reload_coef;   // (pinned payload) [N][2O+1] new coefficients, or null
+    double x, param, sp, sg;
+    double xr[5];           // input ring (ring order) after the ticks, before this compute
+    int N, O;
+    int ticks, compute, dist, pad;
+};
+// Delaybank sample (hz_delay.hip layout): rings [N][size], taps [N][2S] {thr, age_nowrap,
+// age_wrap, 0}, gains [N][2S] T; every line reads x (mono) or xin[line]; y[line] -> out
+struct DlyArgs {
+    void* rx;
+    void* ry;
+    const int4* taps;
+    const void* gains;
+    const double* xin;      // (pinned payload) per-line inputs, or null: mono x
+    double* out;            // (pinned result) [N] line outputs (in T's precision, widened)
+    double x;
+    int N, S, is_float, pad;
+    unsigned size, o;
+};
+// Granulator sample at time t: x into the time-indexed ring, then the sum over the active grains
+// (voice order); the grain list is cached in the serving workgroup's LDS by (key, version)
+struct GranArgs {
+    double* ring;
+    const Grain* grains;    // (pinned payload) the handle's grains that may still read, voice order
+    long mask, t, key, version;
+    double x;
+    unsigned long fm;
+    int count, pad;
+    unsigned size, origin, wrap1, pad2;
+};
+
+constexpr int kArgWords = 30;
+struct alignas(64) Req {
+    long long req;          // request number, written last (release)
+    int op, groups;         // op; workgroups that take part (the others only acknowledge)
+    long long w[kArgWords]; // op arguments
+};
+static_assert(sizeof(FbArgs) <= sizeof(long long) * kArgWords && sizeof(DlyArgs) <= sizeof(long long) * kArgWords &&
+                  sizeof(GranArgs) <= sizeof(long long) * kArgWords,
+              "op arguments fit the request line");
+struct alignas(64) Slot {   // per workgroup
+    double y, y2;           // partial mix
+    long long done;         // last request served (written after y)
+    long long exited;       // epoch of the instance whose workgroup left
+    long long pad[4];
+};
+
+// ---- host side ------------------------------------------------------------------------------
+struct Server;
+// the device's server (created on first use; lives for the process)
+Server* server(int device);
+// pinned staging shared by the server's requests (host pointer; device address via dev())
+double* payload(Server* s, size_t doubles);   // grows (only between requests)
+double* result(Server* s, size_t doubles);
+const void* dev(Server* s, const void* host_ptr);
+// one request: args copied into the line, every workgroup acknowledges; -> sum of the taking-part
+// workgroups' partials (y, y2) in workgroup order.  Serialised per device (the caller holds
+// lock(s) across a multi-request sequence when the order matters).
+int call(Server* s, int op, const void* args, size_t bytes, int groups, double* y, double* y2 = nullptr);
+std::recursive_mutex& lock(Server* s);
+// statistics: requests served, launches of the resident kernel
+void info(Server* s, long long* requests, long long* launches, int* active);
+
+}  // namespace hz_rt

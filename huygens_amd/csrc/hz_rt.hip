@@ -1,0 +1,521 @@
+// hz_rt.hip -- the per-sample server (hz_rt.h): one resident kernel per device, serving the
+// per-sample operator calls of the input-driven banks through a pinned-host mailbox.
+//
+//   host:   op arguments -> the request line, then the request number (release store)
+//   device: every workgroup polls the request number (system-scope acquire), loads the line's
+//           arguments (system scope), runs its share of the op's units (bands, lines, grains)
+//           and writes its partial and the request number to its own 64-byte response line
+//   host:   waits for every workgroup's response, sums the partials in workgroup order
+// State stays in device memory in the block engines' layouts (rings, smoothers, coefficients),
+// so per-sample and block calls interleave; every request ends with a system-scope release (the
+// response) and starts with an acquire (the poll), and the host orders block work before and
+// after requests by stream synchronisation.
+//
+// Exactly-once service: the host writes a request line only after every workgroup acknowledged
+// the previous one; a workgroup resumes from its own last acknowledged request when the kernel is
+// relaunched after an idle exit (workgroup 0 decides it after kIdleNs without a request and the
+// others follow through a device-memory flag), so a request is served once by each workgroup even
+// when it arrives while the instance leaves.
+#include <chrono>
+#include <cstring>
+#include <vector>
+
+#include "hz_rt.h"
+
+namespace hz_rt {
+
+constexpr long long kIdleTicks = 200000;   // 2 ms of the 100 MHz real-time counter without a request
+constexpr long long kQuit = -1;
+
+struct ServerArgs {
+    Req* req;
+    Slot* slot;
+    long long* ctl;   // device memory: workgroup 0's idle-exit decision
+    long long epoch;
+};
+
+namespace {
+
+__device__ __forceinline__ long long ld_acq(const long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ long long ld_sys(const long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ double ldd_sys(const double* p) {
+    return __longlong_as_double(ld_sys((const long long*)p));
+}
+__device__ __forceinline__ void st_sys(long long* p, long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void std_sys(double* p, double v) { st_sys((long long*)p, __double_as_longlong(v)); }
+__device__ __forceinline__ void st_rel(long long* p, long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+struct SrvLds {
+    long long w[kArgWords + 1];
+    long long req;
+    double part[kThreads / 64];
+    // OP_GRAN (one workgroup): the handle's grain list and this sample's terms
+    long long gkey, gver;
+    int gcount;
+    Grain gr[kMaxGrains];
+    double term[kMaxGrains];
+};
+
+// ---------------------------------------------------------------------------------------------
+// OP_FB: Filterbank operator() / tick() (src/filterbank.h:125-148, 170-187) for the bands of this
+// workgroup, in the restatement's operation order without FMA contraction (every band's output
+// and state bit-identical to it; the mixdown's order is thread, wave tree, waves, workgroups)
+template <int O>
+__device__ double op_fb(const FbArgs& a, int g, int groups) {
+#pragma clang fp contract(off)
+    constexpr int R1 = O + 1;
+    double v = 0.0;
+    for (int b = g * kThreads + (int)threadIdx.x; b < a.N; b += groups * kThreads) {
+        const double* c = a.coef + (long)b * (2 * O + 1);
+        double f[R1], bk[O > 0 ? O : 1], R[R1];
+#pragma unroll
+        for (int i = 0; i <= O; ++i) R[i] = a.R[(long)b * R1 + i];
+        if (a.reload_coef) {   // coefficients() since the last sample: from the payload
+            const double* rc = a.reload_coef + (long)b * (2 * O + 1);
+            double* cw = const_cast<double*>(c);
+#pragma unroll
+            for (int i = 0; i <= 2 * O; ++i) {
+                const double cv = ldd_sys(rc + i);
+                cw[i] = cv;
+                if (i <= O) f[i] = cv;
+                else bk[i - O - 1] = cv;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i <= O; ++i) f[i] = c[i];
+#pragma unroll
+            for (int k = 0; k < O; ++k) bk[k] = c[O + 1 + k];
+        }
+        double pre = a.pg[2 * b], gain = a.pg[2 * b + 1];
+        double pi, gi;
+        if (a.reload) {   // setters since the last sample: the targets from the payload
+            pi = ldd_sys(a.reload + b);
+            gi = ldd_sys(a.reload + a.N + b);
+            a.pin[b] = pi;
+            a.gin[b] = gi;
+        } else {
+            pi = a.pin[b];
+            gi = a.gin[b];
+        }
+        // bare ticks: the ring rotates right (tick() moves origin back; hz_fb_rt.hip)
+        for (int q = 0; q < a.ticks; ++q) {
+            const double t0 = R[O];
+#pragma unroll
+            for (int k = O; k >= 1; --k) R[k] = R[k - 1];
+            R[0] = t0;
+        }
+        if (a.compute) {
+            pre = (1 - a.sp) * pi + a.sp * pre;
+            gain = (1 - a.sg) * gi + a.sg * gain;
+            double ff = f[0] * a.x;
+#pragma unroll
+            for (int i = 1; i <= O; ++i) ff += f[i] * a.xr[i - 1];
+            double bsum = 0;
+#pragma unroll
+            for (int k = 0; k < O; ++k) bsum += bk[k] * R[k];
+            R[O] = ff * pre - bsum;
+        }
+#pragma unroll
+        for (int i = 0; i <= O; ++i) a.R[(long)b * R1 + i] = R[i];
+        a.pg[2 * b] = pre;
+        a.pg[2 * b + 1] = gain;
+        const double yg = R[O] * gain;
+        double d = yg;
+        if (a.dist == HZ_DIST_SOFTCLIP) d = hz::dist_apply<HZ_DIST_SOFTCLIP>(yg, a.param);
+        else if (a.dist == HZ_DIST_SATURATE) d = hz::dist_apply<HZ_DIST_SATURATE>(yg, a.param);
+        else if (a.dist == HZ_DIST_LIMITER) d = hz::dist_apply<HZ_DIST_LIMITER>(yg, a.param);
+        v += d;
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// OP_DLY: one sample of every line (src/delay.h:71-89 over src/buffer.h:40-47), the block
+// kernel's arithmetic (hz_delay.hip dly_line_kernel) for a 1-sample call: a tap of age 0 reads
+// this sample's input (forward) or the partial sum (feedback); the rings take x and y at origin
+template <typename T>
+__device__ void op_dly(const DlyArgs& a, int g, int groups) {
+#pragma clang fp contract(off)
+    const unsigned size = a.size, o = a.o;
+    for (int l = g * kThreads + (int)threadIdx.x; l < a.N; l += groups * kThreads) {
+        const int4* tp = a.taps + (long)l * 2 * a.S;
+        const T* gn = (const T*)a.gains + (long)l * 2 * a.S;
+        T* rx = (T*)a.rx + (long)l * size;
+        T* ry = (T*)a.ry + (long)l * size;
+        const T x = (T)(a.xin ? ldd_sys(a.xin + l) : a.x);
+        T acc = (T)0;
+        for (int i = 0; i < a.S; ++i) {
+            const int4 qf = tp[i];
+            const T f = gn[i];
+            const T b = gn[a.S + i];
+            const unsigned af = ((int)o < qf.x) ? (unsigned)qf.z : (unsigned)qf.y;
+            const T xv = af == 0 ? x : rx[o >= af ? o - af : o + size - af];
+            T yv = (T)0;
+            if (b != (T)0) {
+                const int4 qb = tp[a.S + i];
+                const unsigned ab = ((int)o < qb.x) ? (unsigned)qb.z : (unsigned)qb.y;
+                yv = ab == 0 ? acc : ry[o >= ab ? o - ab : o + size - ab];
+            }
+            const T fx = f * xv;
+            const T by = b * yv;
+            acc = acc + (fx - by);
+        }
+        rx[o] = x;
+        ry[o] = acc;
+        std_sys(a.out + l, (double)acc);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// OP_GRAN (workgroup 0): the sample at time t of src/granulator.h:88-104 over the source ring,
+// the block kernel's per-grain arithmetic (hz_granulator.hip gran_kernel), terms summed in voice
+// order by one thread (the block kernel's order)
+__device__ __forceinline__ unsigned fastmod(unsigned x, unsigned long fm, unsigned size) {
+    const unsigned long low = fm * (unsigned long)x;
+    return (unsigned)__umul64hi(low, (unsigned long)size);
+}
+
+__device__ double op_gran(const GranArgs& a, SrvLds& s) {
+#pragma clang fp contract(off)
+    const int tid = threadIdx.x;
+    if (s.gkey != a.key || s.gver != a.version) {   // the handle's grain list changed: reload
+        __syncthreads();
+        const long long* src = (const long long*)a.grains;
+        long long* dst = (long long*)s.gr;
+        for (int i = tid; i < a.count * 8; i += kThreads) dst[i] = ld_sys(src + i);
+        __syncthreads();
+        if (tid == 0) {
+            s.gkey = a.key;
+            s.gver = a.version;
+            s.gcount = a.count;
+        }
+        __syncthreads();
+    }
+    const long t = a.t;
+    const unsigned size = a.size, origin = a.origin;
+    for (int e = tid; e < a.count; e += kThreads) {
+        const Grain& gr = s.gr[e];
+        double term = 0.0;
+        if (t >= gr.t_first && t < gr.t_end) {
+            const unsigned ticks = gr.ticks0 + (unsigned)(t - gr.t_first);
+            const double position = gr.offsets + (1 - gr.speeds) * ticks;
+            const int center = (int)position;
+            const double disp = position - center;
+            long tau0, tau1;
+            if (center >= 0 && (unsigned)center < size) {
+                tau0 = t - center;
+                tau1 = (unsigned)center + 1u < size ? tau0 - 1 : t;
+            } else {
+                const unsigned x0 = origin - (unsigned)center + size;
+                const unsigned s0 = fastmod(x0, a.fm, size);
+                const unsigned s1 = x0 == 0u ? a.wrap1 : (s0 == 0u ? size - 1u : s0 - 1u);
+                tau0 = t - (long)(origin >= s0 ? origin - s0 : origin + size - s0);
+                tau1 = t - (long)(origin >= s1 ? origin - s1 : origin + size - s1);
+            }
+            // this sample's input is the argument (the ring takes it below)
+            const double v0 = tau0 == t ? a.x : a.ring[tau0 & a.mask];
+            const double v1 = tau1 == t ? a.x : a.ring[tau1 & a.mask];
+            const double src = v0 * (1 - disp) + v1 * disp;
+            const double tk = (double)ticks;
+            double phase;
+            if (gr.rsizes != 0.0) {
+                const double q0 = tk * gr.rsizes;
+                phase = __builtin_fma(__builtin_fma(-q0, gr.sizes, tk), gr.rsizes, q0);
+            } else {
+                phase = tk / gr.sizes;
+            }
+            term = gr.gains * src * (0.5 * (1 - cos(2 * hz::kPI * phase)));   // wave.h:148
+        }
+        s.term[e] = term;
+    }
+    __syncthreads();
+    double out = 0.0;
+    if (tid == 0) {
+        for (int e = 0; e < a.count; ++e) {
+            const Grain& gr = s.gr[e];
+            if (t >= gr.t_first && t < gr.t_end) out += s.term[e];
+        }
+        a.ring[t & a.mask] = a.x;
+    }
+    return out;
+}
+
+__global__ __launch_bounds__(kThreads) void rt_server_kernel(ServerArgs a) {
+    __shared__ SrvLds s;
+    const int tid = threadIdx.x;
+    const int g = blockIdx.x;
+    if (tid == 0) s.gkey = -1;
+    long long seen = ld_sys(&a.slot[g].done);   // resume after this workgroup's last served request
+    long long last = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (tid == 0) {
+            long long r;
+            for (;;) {
+                r = ld_acq(&a.req->req);
+                if (r != seen) break;
+                if (g == 0) {
+                    if (__builtin_amdgcn_s_memrealtime() - last > kIdleTicks) {
+                        __hip_atomic_store(a.ctl, kQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        r = kQuit;
+                        break;
+                    }
+                } else if (__hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kQuit) {
+                    r = kQuit;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            s.req = r;
+        }
+        __syncthreads();
+        const long long r = s.req;
+        if (r == kQuit) break;
+        if (tid <= kArgWords) s.w[tid] = ld_sys((const long long*)&a.req->op + tid);   // op|groups, args
+        __syncthreads();
+        const int op = (int)(unsigned)(s.w[0] & 0xffffffffu), groups = (int)(s.w[0] >> 32);
+        if (op == OP_STOP) {
+            seen = r;
+            break;
+        }
+        double y = 0.0;
+        if (g < groups) {
+            if (op == OP_FB) {
+                FbArgs fa;
+                __builtin_memcpy(&fa, &s.w[1], sizeof(fa));
+                switch (fa.O) {
+                case 0: y = op_fb<0>(fa, g, groups); break;
+                case 1: y = op_fb<1>(fa, g, groups); break;
+                case 2: y = op_fb<2>(fa, g, groups); break;
+                case 3: y = op_fb<3>(fa, g, groups); break;
+                default: y = op_fb<4>(fa, g, groups); break;
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) y += __shfl_xor(y, o);
+                if ((tid & 63) == 0) s.part[tid >> 6] = y;
+                __syncthreads();
+                y = 0.0;
+#pragma unroll
+                for (int w = 0; w < kThreads / 64; ++w) y += s.part[w];   // waves in order
+            } else if (op == OP_DLY) {
+                DlyArgs da;
+                __builtin_memcpy(&da, &s.w[1], sizeof(da));
+                if (da.is_float) op_dly<float>(da, g, groups);
+                else op_dly<double>(da, g, groups);
+            } else if (op == OP_GRAN) {
+                GranArgs ga;
+                __builtin_memcpy(&ga, &s.w[1], sizeof(ga));
+                y = op_gran(ga, s);
+            }
+        }
+        // every storing wave drains, then one lane answers with a system-scope release
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            std_sys(&a.slot[g].y, y);
+            st_rel(&a.slot[g].done, r);
+        }
+        seen = r;
+        last = __builtin_amdgcn_s_memrealtime();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        st_sys(&a.slot[g].done, seen);
+        st_rel(&a.slot[g].exited, a.epoch);
+    }
+}
+
+long long host_load(const long long* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+
+}  // namespace
+
+struct Server {
+    int device = 0;
+    std::recursive_mutex mu;
+    hipStream_t stream = nullptr;
+    void* mb = nullptr;          // pinned: Req, then kGroups Slots
+    long long* d_ctl = nullptr;
+    long long seq = 0, epoch = 0, requests = 0, launches = 0;
+    bool active = false;
+    double* pay = nullptr;       // pinned payload / result
+    size_t pay_cap = 0;
+    double* res = nullptr;
+    size_t res_cap = 0;
+    Req* req() { return (Req*)mb; }
+    Slot* slot() { return (Slot*)((char*)mb + sizeof(Req)); }
+};
+
+namespace {
+
+Server* g_servers[64] = {};
+std::mutex g_servers_mu;
+
+int srv_init(Server* s) {
+    HZ_TRY_HIP(hipSetDevice(s->device));
+    int least = 0, greatest = 0;
+    HZ_TRY_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    // the highest priority: a hardware queue of its own (normal streams keep theirs)
+    HZ_TRY_HIP(hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, greatest));
+    const size_t bytes = sizeof(Req) + sizeof(Slot) * kGroups;
+    HZ_TRY_HIP(hipHostMalloc(&s->mb, bytes, hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(s->mb, 0, bytes);
+    HZ_TRY_HIP(hipMalloc(&s->d_ctl, 64));
+    return HZ_OK;
+}
+
+bool srv_left(Server* s) { return host_load(&s->slot()[0].exited) == s->epoch; }
+
+int srv_launch(Server* s) {
+    HZ_TRY_HIP(hipMemsetAsync(s->d_ctl, 0, 64, s->stream));
+    ServerArgs a;
+    void* dmb = nullptr;
+    HZ_TRY_HIP(hipHostGetDevicePointer(&dmb, s->mb, 0));
+    a.req = (Req*)dmb;
+    a.slot = (Slot*)((char*)dmb + sizeof(Req));
+    a.ctl = s->d_ctl;
+    a.epoch = ++s->epoch;
+    hipLaunchKernelGGL(rt_server_kernel, dim3(kGroups), dim3(kThreads), 0, s->stream, a);
+    HZ_TRY_HIP(hipGetLastError());
+    s->active = true;
+    ++s->launches;
+    return HZ_OK;
+}
+
+void srv_shutdown() {
+    // process exit: every resident instance leaves (a STOP request), so no wave outlives the host
+    for (Server* s : g_servers) {
+        if (!s || !s->active || srv_left(s)) continue;
+        std::lock_guard<std::recursive_mutex> lk(s->mu);
+        Req* q = s->req();
+        q->op = OP_STOP;
+        q->groups = 0;
+        __atomic_store_n(&q->req, ++s->seq, __ATOMIC_RELEASE);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!srv_left(s) && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
+        }
+        (void)hipStreamSynchronize(s->stream);
+        s->active = false;
+    }
+}
+
+}  // namespace
+
+Server* server(int device) {
+    std::lock_guard<std::mutex> lk(g_servers_mu);
+    if (device < 0 || device >= 64) return nullptr;
+    if (!g_servers[device]) {
+        Server* s = new Server();
+        s->device = device;
+        if (srv_init(s) != HZ_OK) {
+            delete s;
+            return nullptr;
+        }
+        static bool registered = false;
+        if (!registered) {
+            std::atexit(srv_shutdown);
+            registered = true;
+        }
+        g_servers[device] = s;
+    }
+    return g_servers[device];
+}
+
+std::recursive_mutex& lock(Server* s) { return s->mu; }
+
+static double* grow(double** p, size_t* cap, size_t n) {
+    if (n <= *cap) return *p;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t c = std::max<size_t>(n, 4096);
+    if (hipHostMalloc((void**)p, c * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+        return nullptr;
+    *cap = c;
+    return *p;
+}
+
+double* payload(Server* s, size_t n) { return grow(&s->pay, &s->pay_cap, n); }
+double* result(Server* s, size_t n) { return grow(&s->res, &s->res_cap, n); }
+
+const void* dev(Server* s, const void* host_ptr) {
+    (void)s;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, const_cast<void*>(host_ptr), 0) != hipSuccess) return nullptr;
+    return d;
+}
+
+int call(Server* s, int op, const void* args, size_t bytes, int groups, double* y, double* y2) {
+    std::lock_guard<std::recursive_mutex> lk(s->mu);
+    HZ_TRY_HIP(hipSetDevice(s->device));
+    if (bytes > sizeof(long long) * kArgWords || groups < 1 || groups > kGroups) {
+        hz::set_error("hz_rt::call: op arguments %zu bytes, %d workgroups", bytes, groups);
+        return HZ_E_INVALID;
+    }
+    if (!s->active || srv_left(s)) {
+        s->active = false;
+        HZ_TRY(srv_launch(s));
+    }
+    Req* q = s->req();
+    Slot* slot = s->slot();
+    q->op = op;
+    q->groups = groups;
+    std::memcpy(q->w, args, bytes);
+    const long long want = ++s->seq;
+    __atomic_store_n(&q->req, want, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    int relaunched = 0;
+    for (;;) {
+        bool all = true;
+        for (int g = 0; g < kGroups && all; ++g) all = host_load(&slot[g].done) >= want;
+        if (all) break;
+        if (srv_left(s)) {
+            // the instance left (idle) as the request arrived: the workgroups that had not served it
+            // serve it after the relaunch (each resumes from its own response line)
+            if (relaunched++ > 3) {
+                hz::set_error("hz_rt: the per-sample server left repeatedly without serving");
+                return HZ_E_HIP;
+            }
+            HZ_TRY(srv_launch(s));
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+            hz::set_error("hz_rt: the per-sample server did not answer within 5 s");
+            return HZ_E_HIP;
+        }
+    }
+    double a = 0.0, b = 0.0;
+    for (int g = 0; g < groups; ++g) {
+        a += slot[g].y;
+        b += slot[g].y2;
+    }
+    if (y) *y = a;
+    if (y2) *y2 = b;
+    ++s->requests;
+    return HZ_OK;
+}
+
+void info(Server* s, long long* requests, long long* launches, int* active) {
+    if (requests) *requests = s->requests;
+    if (launches) *launches = s->launches;
+    if (active) *active = (s->active && !srv_left(s)) ? 1 : 0;
+}
+
+}  // namespace hz_rt
+
+extern "C" {
+
+int hz_rt_info(int device, long long* requests, long long* launches, int* active) {
+    hz_rt::Server* s = hz_rt::server(device);
+    if (!s) return HZ_E_NODEV;
+    hz_rt::info(s, requests, launches, active);
+    return HZ_OK;
+}
+
+}  // extern "C"

@@ -65,6 +65,18 @@ class Delaybank:
                                            1 if per_line else 0, 1 if mix else 0))
         return out
 
+    def sample(self, x) -> np.ndarray:
+        """One sample of every line, `y_k = line_k(x); tick();` (delay.h:71-97), through the
+        per-sample server (hz_dly_sample): x a scalar (mono) or [lines] (T); -> [lines]."""
+        xa = np.ascontiguousarray(np.atleast_1d(x), dtype=self.dtype)
+        if xa.size not in (1, self.lines):
+            raise ValueError("sample: one input or one per line")
+        per_line = xa.size == self.lines and self.lines > 1
+        out = np.zeros(self.lines, dtype=self.dtype)
+        check(self._lib.hz_dly_sample(self._h, C.c_void_p(xa.ctypes.data), C.c_void_p(out.ctypes.data),
+                                      1 if per_line else 0))
+        return out
+
     def process_device(self, in_ptr: int, out_ptr: int, n: int, per_line: bool = False, mix: bool = False):
         check(self._lib.hz_dly_process_device(self._h, C.c_void_p(in_ptr), C.c_void_p(out_ptr), n,
                                               1 if per_line else 0, 1 if mix else 0))
@@ -122,3 +134,7 @@ class Delay(Delaybank):
 
     def process(self, x) -> np.ndarray:  # noqa: D102
         return super().process(np.asarray(x).reshape(-1))[0]
+
+    def __call__(self, x) -> float:
+        """`y = delay(x); delay.tick();` (tests/delay.cpp:22-27) through the per-sample server"""
+        return float(self.sample(x)[0])

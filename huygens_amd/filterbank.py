@@ -125,8 +125,14 @@ class Filterbank:
         """tick() (filterbank.h:142-148): recorded, applied with the next sample (or block call)."""
         check(self._lib.hz_fb_sample_tick(self._h))
 
+    def setter_seq(self) -> int:
+        """per-sample calls served when the last setter ran (it applies from that call on)"""
+        v = C.c_longlong()
+        check(self._lib.hz_fb_setter_seq(self._h, C.byref(v)))
+        return v.value
+
     def sample_info(self):
-        """-> (resident kernel serving, requests posted, workgroups)"""
+        """-> (in per-sample mode, samples served, server workgroups taking part)"""
         a, n, g = C.c_int(), C.c_longlong(), C.c_int()
         check(self._lib.hz_fb_sample_info(self._h, C.byref(a), C.byref(n), C.byref(g)))
         return bool(a.value), n.value, g.value

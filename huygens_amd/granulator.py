@@ -55,6 +55,13 @@ class Granulator:
                                         1 if ticked else 0, C.byref(v)))
         return v.value
 
+    def sample(self, x: float) -> float:
+        """`source.write(x); y = granny(); granny.tick();` (tests/granny.cpp:36-56) for one sample,
+        through the per-sample server (hz_gran_sample)"""
+        y = C.c_double()
+        check(self._lib.hz_gran_sample(self._h, float(x), C.byref(y)))
+        return y.value
+
     def process(self, x, requests=None):
         x = np.ascontiguousarray(x, dtype=np.float64)
         r = _reqs(requests)

@@ -98,3 +98,14 @@ class Oscbank:
         ms, c = C.c_double(), C.c_long()
         check(self._lib.hz_osc_profile_read(self._h, C.byref(ms), C.byref(c)))
         return ms.value, c.value
+
+    # ---- per-sample operator API (src/oscbank.h:59-90): served from a speculative block ----
+    def mixdown(self) -> complex:
+        """mixdown() of the current phasors (no tick)."""
+        m = np.zeros(2)
+        check(self._lib.hz_osc_mixdown(self._h, dptr(m)))
+        return complex(m[0], m[1])
+
+    def tick(self):
+        """tick(): one sample."""
+        check(self._lib.hz_osc_fill(self._h, None, None, 1))

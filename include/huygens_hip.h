@@ -88,16 +88,22 @@ int hz_fb_tick(hz_fb* h);
 /* Per-sample operator API on the GPU (hz_fb_rt.hip): T operator()(T x) / operator()(T x, dist)
  * (filterbank.h:125-139) and tick() (142-148) with the reference's exact semantics -- a repeated
  * operator() before tick() returns the cached row re-mixed (no compute); ticks without operator()
- * rotate the ring (the row O+1 samples back becomes the newest history row).  Served by a kernel
- * that stays resident on the handle's stream while per-sample calls continue (pinned-host
- * mailbox, a few microseconds per sample whatever N); it leaves on the next block call, state
- * read/write, destroy, or after 100 ms without a call.  hz_fb_sample_tick only records the tick
+ * rotate the ring (the row O+1 samples back becomes the newest history row).  Served by the
+ * device's per-sample server (hz_rt_info: one resident kernel for every handle, pinned-host
+ * mailbox, a few microseconds per sample) over the handle's state in device memory; the state is
+ * converted back on the next block call, state read/write or destroy.  Setters between samples
+ * reach the next request as a payload (no restart).  hz_fb_sample_tick only records the tick
  * (no GPU work).  Block calls after an operator() without tick() output the cached sample first,
- * as the reference's loop does.  HZ_E_UNSUPPORTED above 262,144 bands (orders <= 2; 131,072
- * above), HZ_E_STATE for a bare tick whose ring row is unknown (see hz_fb_tick). */
+ * as the reference's loop does.  HZ_E_STATE for a bare tick whose ring row is unknown (see
+ * hz_fb_tick). */
 int hz_fb_sample(hz_fb* h, double x, int dist_id, double param, double* y);
 int hz_fb_sample_tick(hz_fb* h);
-/* whether the resident kernel is serving, requests posted so far, its workgroups */
+/* the number of per-sample calls served when the last setter (coefficients / boost / mix / open)
+ * ran: the setter applies from that call on (setters may come from another thread while samples
+ * run -- every entry point holds the handle's lock; the reference's MIDI thread,
+ * tests/filterbank.cpp:217-252) */
+int hz_fb_setter_seq(hz_fb* h, long long* seq);
+/* whether the handle is in per-sample mode, samples served, server workgroups taking part */
 int hz_fb_sample_info(hz_fb* h, int* active, long long* served, int* groups);
 int hz_fb_set_stream(hz_fb* h, void* hip_stream);
 int hz_fb_get_stream(hz_fb* h, void** hip_stream);
@@ -195,6 +201,13 @@ int hz_fb_lti_plan(hz_fb* h, long* nseg, long* skip_tiles, int* fine_parts);
 /* (diagnostics) chunk length L of the last LTI launch (16, 32, 64 or 128; 0 before any) */
 int hz_fb_lti_last_chunk(hz_fb* h, int* chunk);
 
+/* ---- the per-sample server (hz_rt.hip) ----------------------------------------
+ * One resident kernel per device serves the per-sample calls of Filterbank (hz_fb_sample),
+ * Delay / Delaybank (hz_dly_sample) and Granulator (hz_gran_sample) through a pinned-host
+ * mailbox, on a stream of the highest priority; it leaves after 2 ms without a request and is
+ * relaunched on demand.  Statistics: requests served, launches, currently resident. */
+int hz_rt_info(int device, long long* requests, long long* launches, int* active);
+
 /* ---- Oscbank<double,N>  (src/oscbank.h:15-97, src/multichannel.h:16-159) -- */
 typedef struct hz_osc hz_osc;
 
@@ -240,8 +253,16 @@ int hz_add_request(hz_add* h, double fundamental, double amplitude, int* voice);
 int hz_add_release(hz_add* h, int voice);                                          /* 161-172, -1 = all */
 int hz_add_makenote(hz_add* h, double pitch, double amplitude, int* voice);        /* 174-179 */
 int hz_add_endnote(hz_add* h, double pitch);                                       /* 182-187 */
-/* n x { out[t] = operator()(); tick(); }  additive.h:38-62 (tests/additive.cpp:27-37) */
+/* n x { out[t] = operator()(); tick(); }  additive.h:38-62 (tests/additive.cpp:27-37).
+ * Per-sample calls (n < 64: the drop-in's operator() / tick()) are served from a speculative
+ * block: the next 1024 samples rendered at once from a snapshot of the state (the output needs no
+ * input); a setter, a longer fill or a device fill first rolls the engine back to the consumed
+ * sample (snapshot restored, that many samples re-rendered), so the samples are exactly those of
+ * the per-sample sequence.  The same holds for Sinusoids (hz_sin_fill), Bowl (hz_bowl_render /
+ * hz_bowl_fill) and Oscbank (hz_osc_fill with n = 1, hz_osc_phases, hz_osc_mixdown). */
 int hz_add_fill(hz_add* h, double* out, size_t n);
+/* speculative blocks rendered, rollbacks (a setter inside a block), block length */
+int hz_add_lookahead_info(hz_add* h, long* blocks, long* rollbacks, long* block_len);
 int hz_add_fill_device(hz_add* h, double* d_out, size_t n);
 int hz_add_set_stream(hz_add* h, void* hip_stream);
 int hz_add_set_target_groups(hz_add* h, int groups);
@@ -301,6 +322,10 @@ int hz_dly_modulate_back(hz_dly* h, int line, unsigned n, unsigned time, double 
  * the mixdown sum_k y_k / N, summed in line order in T (mix 1). */
 int hz_dly_process(hz_dly* h, const void* in, void* out, size_t n, int in_per_line, int mix);
 int hz_dly_process_device(hz_dly* h, const void* d_in, void* d_out, size_t n, int in_per_line, int mix);
+/* one sample of every line, `y_k = line_k(x); tick();` (delay.h:71-97), through the device's
+ * per-sample server (a resident kernel shared by every handle of the process; no launch per
+ * sample): in = one T (in_per_line 0) or N T, out = N T.  Bit-identical to hz_dly_process(n = 1). */
+int hz_dly_sample(hz_dly* h, const void* in, void* out, int in_per_line);
 /* tick() without operator() (delay.h:92-97), `count` times: both rings' origins move and no
  * slot is written (the stale samples stay, as in the reference) */
 int hz_dly_tick(hz_dly* h, unsigned long count);
@@ -407,6 +432,9 @@ int hz_gran_process(hz_gran* h, const double* in, double* out, size_t n, const h
 /* device in/out, asynchronous on the handle's stream (requests and voices stay on the host) */
 int hz_gran_process_device(hz_gran* h, const double* d_in, double* d_out, size_t n, const hz_grain_req* reqs,
                            int nreq, int* voices);
+/* one sample, `source.write(x); y = granny(); granny.tick();` (tests/granny.cpp:36-56), through
+ * the device's per-sample server (no launch per sample); the same arithmetic as hz_gran_process */
+int hz_gran_sample(hz_gran* h, double x, double* y);
 int hz_gran_activity(hz_gran* h, unsigned* activity);   /* active voices; idle() 106-109 is == 0 */
 int hz_gran_set_stream(hz_gran* h, void* hip_stream);
 int hz_gran_synchronize(hz_gran* h);

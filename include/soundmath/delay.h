@@ -50,7 +50,7 @@ public:
     // one sample of every line; in: N per-line samples
     cspan<T> operator()(const T* in) {
         if (!computed_) {
-            detail::check(hz_dly_process(h_.get(), in, out_, 1, 1, 0), "Delaybank::operator()");
+            detail::check(hz_dly_sample(h_.get(), in, out_, 1), "Delaybank::operator()");   // per-sample server
             computed_ = true;
         }
         return {out_, (std::size_t)N};

@@ -58,7 +58,7 @@ public:
     T operator()() {
         if (read_pending_) return last_;   // repeated read before tick(): same value
         const T x = source_->current();
-        detail::check(hz_gran_process(h_.get(), &x, &last_, 1, nullptr, 0, nullptr), "Granulator::operator()");
+        detail::check(hz_gran_sample(h_.get(), x, &last_), "Granulator::operator()");   // per-sample server
         read_pending_ = true;
         return last_;
     }

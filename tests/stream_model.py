@@ -58,12 +58,18 @@ def final_stage(Cs):
 
 
 class StreamModel:
-    """The engine's state: partition spectra HS[p][c] (with 1 / F), the window spectra ring
-    ZS[slot][c], the last block's samples; `prime` builds the ring from a history."""
+    """The engine's state and its pipelined schedule (hz_fb_stream.hip): launch b outputs
+        y_b = head_b + tail_b,   head_b[t] = sum_{tau < P} h[tau] x[t - tau]  (direct),
+        tail_b = last P samples of IFFT(Y_b),  Y_b = sum_{p >= 1} H_p Z_{b-p},
+    where the tail's inverse columns C_b were computed by launch b - 1:
+        Y_{b+1} = H_1 Z_b + H_2 Z_{b-1} + R_{b+1},   R_{b+2} = sum_{p >= 3} H_p Z_{b+2-p}
+    (R computed one launch ahead from the ring of window spectra).  Within a launch the three
+    roles (outputs, transform columns, MAC columns) share no data."""
 
     def __init__(self, h):
         h = np.asarray(h, dtype=np.float64)
         assert len(h) % (8 * P) == 0
+        self.h = h
         self.K = len(h)
         self.Q = self.K // P
         self.HS = np.zeros((self.Q, COLS, 32), dtype=np.complex128)
@@ -73,11 +79,18 @@ class StreamModel:
             for c in range(COLS):
                 self.HS[p, c] = col_forward(win, c)
         self.ZS = np.zeros((self.Q, COLS, 32), dtype=np.complex128)
-        self.head = 0
+        self.head = 0            # slot of the next window spectrum Z_b
         self.prev = np.zeros(P)
+        self.C = None            # inverse columns of the next block's tail
+        self.R = None            # R_{b+1}
+
+    def _z(self, p):
+        """Z_{b-p} (p >= 1) from the ring, b = the next block"""
+        return self.ZS[(self.head - p) % self.Q]
 
     def prime(self, hist):
-        """hist = the last K inputs: windows b - p (p = 1 .. Q - 1) into slots head - p."""
+        """hist = the last K inputs: windows b - p (p = 1 .. Q - 1) into slots head - p, then the
+        first block's tail columns C_b and R_{b+1}."""
         hist = np.asarray(hist, dtype=np.float64)
         assert len(hist) == self.K
         for p in range(1, self.Q):
@@ -87,19 +100,27 @@ class StreamModel:
             for c in range(COLS):
                 self.ZS[slot, c] = col_forward(win, c)
         self.prev = hist[-P:].copy()
+        Y = sum(self.HS[p] * self._z(p) for p in range(1, self.Q))
+        self.C = [col_inverse(Y[c], c) for c in range(COLS)]
+        # R_{b+1} = sum_{p >= 3} H_p Z_{b+1-p}: Z_{b+1-p} = ring entry p - 1 back
+        self.R = sum(self.HS[p] * self._z(p - 1) for p in range(3, self.Q))
 
     def block(self, x):
         x = np.asarray(x, dtype=np.float64)
         assert len(x) == P
-        win = np.concatenate([self.prev, x])
-        Cs = []
-        for c in range(COLS):
-            X = col_forward(win, c)
-            self.ZS[self.head, c] = X
-            Y = np.zeros(32, dtype=np.complex128)
-            for p in range(self.Q):
-                Y += self.HS[p, c] * self.ZS[(self.head - p) % self.Q, c]
-            Cs.append(col_inverse(Y, c))
+        # outputs: head (direct, taps 0 .. P-1) + tail (columns from the previous launch)
+        full = np.concatenate([self.prev, x])
+        head = np.array([np.dot(self.h[:P], full[P + i - P + 1:P + i + 1][::-1]) for i in range(P)])
+        y = head + final_stage(self.C)
+        # transform columns: Z_b, then C_{b+1} from Y_{b+1} = H_1 Z_b + H_2 Z_{b-1} + R_{b+1}
+        Zb = np.array([col_forward(full, c) for c in range(COLS)])
+        Zb1 = self._z(1).copy()
+        Y1 = self.HS[1] * Zb + self.HS[2] * Zb1 + self.R
+        C1 = [col_inverse(Y1[c], c) for c in range(COLS)]
+        # MAC columns: R_{b+2} = sum_{p >= 3} H_p Z_{b+2-p} (Z_{b-1} and older)
+        R2 = sum(self.HS[p] * self._z(p - 2) for p in range(3, self.Q))
+        self.ZS[self.head] = Zb
         self.head = (self.head + 1) % self.Q
+        self.C, self.R = C1, R2
         self.prev = x.copy()
-        return final_stage(Cs)
+        return y

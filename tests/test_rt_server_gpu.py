@@ -1,0 +1,197 @@
+"""The per-sample server (hz_rt.hip): one resident kernel per device serving the per-sample
+operator calls of Filterbank, Delay / Delaybank and Granulator (the reference's audio-callback
+loops: tests/resynthesis.cpp:35-39, tests/delay.cpp:20-28, tests/granny.cpp:32-56), interleaved
+with block calls, several handles at once, setters from another thread, and a block call on another
+stream while the server is resident."""
+import os
+import subprocess
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from golden.spec_numpy import resonant_coefficients, white_noise_f32
+from oracle import OracleFilterbank
+from oracle_delay import OracleDelaybank
+from oracle_gran import OracleGranulator
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOL = 1e-9
+SR = 48000
+
+
+def test_delay_per_sample_bit_exact(gpu_lib):
+    """Delay<double>(10, 2 SR) with the taps of tests/delay.cpp:41, per sample (the server) and in
+    blocks, against the restatement: bit-exact."""
+    from huygens_amd import Delay
+    g, o = Delay(10, 2 * SR), OracleDelaybank(1, 10, 2 * SR)
+    fwd, back = [(0, 1.0)], [(20000, 0.5), (10000, 0.5)]
+    g.coefficients(fwd, back)
+    o.coefficients(0, fwd, back)
+    x = white_noise_f32(45000, seed=3)
+    yg = np.concatenate([np.array([g(v) for v in x[:12000]]), g.process(x[12000:30000]),
+                         np.array([g(v) for v in x[30000:]])])
+    yo = o.process(x)[0]
+    assert np.array_equal(yg, yo)
+    assert g.origin() == o.origin()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_delaybank_per_line_inputs(gpu_lib, dtype):
+    from huygens_amd import Delaybank
+    L, S, time_ = 64, 3, 3000
+    g, o = Delaybank(L, S, time_, dtype=dtype), OracleDelaybank(L, S, time_, dtype=dtype)
+    rng = np.random.default_rng(4)
+    for line in range(L):
+        fwd = [(0, 1.0), (int(rng.integers(1, 900)), float(rng.uniform(-0.5, 0.5)))]
+        back = [(int(rng.integers(1, 2999)), float(rng.uniform(-0.5, 0.5))), (int(rng.integers(1, 5)), 0.25)]
+        g.coefficients(line, fwd, back)
+        o.coefficients(line, fwd, back)
+    x = rng.uniform(-1, 1, (L, 5000)).astype(dtype)
+    yg = np.zeros_like(x)
+    for t in range(0, 1500):
+        yg[:, t] = g.sample(x[:, t])
+    yg[:, 1500:3500] = g.process(x[:, 1500:3500])
+    for t in range(3500, 5000):
+        yg[:, t] = g.sample(x[:, t])
+    yo = o.process(x)
+    assert np.array_equal(yg, yo)
+
+
+def test_granulator_per_sample(gpu_lib):
+    """tests/granny.cpp:32-56: per-sample calls with grain requests, against a block-driven twin
+    (same arithmetic: bit-identical) and the restatement (<= 1e-12 of peak)."""
+    from huygens_amd import Granulator
+    size = 3 * SR
+    g, twin, o = Granulator(size, 512), Granulator(size, 512), OracleGranulator(size, 512)
+    rng = np.random.default_rng(8)
+    x = np.sin(np.arange(30000) * 0.01) + 0.2 * rng.standard_normal(30000)
+    reqs = sorted(rng.choice(np.arange(1, 29000), 60, replace=False).tolist())
+    params = {t: (float(rng.uniform(0, 0.5)), float(rng.uniform(0.01, 0.2)), float(rng.uniform(0.5, 2.0)),
+                  float(rng.uniform(0.1, 1.0))) for t in reqs}
+    yg, yo = np.zeros(len(x)), np.zeros(len(x))
+    for t in range(len(x)):
+        yg[t] = g.sample(x[t])
+        o.write(x[t])
+        yo[t] = o.sample()
+        if t in params:
+            off, sz, sp, gn = params[t]
+            g.request(off, sz, sp, gn, ticked=True)
+            o.request(off, sz, sp, gn)
+        o.tick()
+    # the block twin: the same requests at the same samples
+    from huygens_amd import GRAIN_REQ
+    r = np.array([(t, *params[t], 0.0) for t in reqs], dtype=GRAIN_REQ)
+    yt, _ = twin.process(x, r)
+    assert np.array_equal(yg, yt)
+    assert np.max(np.abs(yg - yo)) <= 1e-12 * np.max(np.abs(yo))
+
+
+def test_interleaved_filterbank_handles(gpu_lib):
+    """tests/filterbanks.cpp's shape: several Filterbanks (864 bands, FFilterbank<double,864,2>)
+    called per sample, interleaved; one server serves them all (no per-handle resident kernel, no
+    hardware-queue stalls)."""
+    from huygens_amd import Filterbank
+    H, N = 8, 864
+    fwd, back = resonant_coefficients(N, 0.999, 1.0)
+    gs, os_ = [], []
+    for k in range(H):
+        g, o = Filterbank(2, N), OracleFilterbank(2, N)
+        for fb in (g, o):
+            for n in range(N):
+                fb.coefficients(n, fwd[n], back[n])
+            fb.boost(np.full(N, 1.0 + 0.1 * k))
+            fb.open()
+        gs.append(g)
+        os_.append(o)
+    x = white_noise_f32(600, seed=12)
+    worst, lat = 0.0, []
+    for t in range(len(x)):
+        for k in range(H):
+            t0 = time.perf_counter()
+            yg = gs[k](x[t] * (k + 1))
+            gs[k].tick()
+            lat.append(time.perf_counter() - t0)
+            yo = os_[k](x[t] * (k + 1))
+            os_[k].tick()
+            worst = max(worst, abs(yg - yo) / max(1e-30, abs(yo)))
+    assert worst < 1e-8, worst
+    lat = np.array(lat[8 * H:])
+    print(f"{H} interleaved handles: mean {1e6 * lat.mean():.1f} us, max {1e6 * lat.max():.1f} us per call")
+    assert lat.mean() < 50e-6 and lat.max() < 5e-3, (lat.mean(), lat.max())
+
+
+def test_block_call_beside_resident_server(gpu_lib):
+    """A block call on another stream while the server is resident does not wait for the server's
+    idle exit (the server's stream has a hardware queue of its own)."""
+    from huygens_amd import Filterbank, rt_info
+    g, _ = Filterbank(2, 256), None
+    g2 = Filterbank(2, 256)
+    fwd, back = resonant_coefficients(256, 0.99, 1.0)
+    for fb in (g, g2):
+        for n in range(256):
+            fb.coefficients(n, fwd[n], back[n])
+        fb.boost(np.ones(256))
+        fb.open()
+    x = white_noise_f32(4096, seed=2)
+    g2.process(x)   # warm
+    g(0.1)
+    g.tick()
+    launches0 = rt_info(0)[1]
+    times = []
+    for i in range(20):
+        g(0.1)
+        g.tick()
+        assert rt_info(0)[2]            # resident
+        t0 = time.perf_counter()
+        g2.process(x)                   # 4096 samples on another handle's stream
+        times.append(time.perf_counter() - t0)
+    relaunched = rt_info(0)[1] - launches0
+    print("block call beside the resident server (ms):", " ".join(f"{1e3 * t:.3f}" for t in times),
+          f"; server relaunches {relaunched}")
+    # a block call queued behind the resident kernel would wait for its 2 ms idle exit, and the
+    # server would then be relaunched by the next sample
+    assert np.median(times) < 0.5e-3 and relaunched == 0, (times, relaunched)
+
+
+def test_setters_from_another_thread(gpu_lib, tmp_path):
+    """tests/filterbank.cpp:194-252: a MIDI thread changes boost / mix at ~2 kHz while the audio
+    thread runs F(x); F.tick() on 4096 bands (C++ drop-in, tests/cpp/rt_midi.cpp).  Replayed through
+    the restatement with every setter at the sample it applied from; the worst per-sample latency is
+    reported (48 kHz budget: 20.8 us)."""
+    exe = os.path.join(ROOT, "tests", "cpp", "rt_midi")
+    lib = os.path.join(ROOT, "huygens_amd", "lib")
+    r = subprocess.run(["g++", "-std=c++17", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "cpp", "rt_midi.cpp"), "-o", exe, "-L", lib, "-lhuygens_hip",
+                        f"-Wl,-rpath,{lib}", "-Wl,-rpath-link,/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    N, S = 4096, 6000
+    p = subprocess.run([exe, str(tmp_path), str(N), str(S), "500"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "rt_midi ok" in p.stdout, p.stdout + p.stderr
+    coef = np.fromfile(tmp_path / "coef.bin").reshape(N, 5)
+    xin = np.fromfile(tmp_path / "in.bin")
+    yg = np.fromfile(tmp_path / "out.bin")
+    lat = np.fromfile(tmp_path / "lat.bin", dtype=np.int64)
+    log = np.fromfile(tmp_path / "log.bin").reshape(-1, 4)
+    assert len(log) > 20
+    o = OracleFilterbank(2, N, 0.1, 1.0)
+    for n in range(N):
+        o.coefficients(n, coef[n, :3], coef[n, 3:])
+    o.boost(np.ones(N))
+    o.open()
+    yo = np.zeros(S)
+    k = 0
+    for t in range(S):
+        while k < len(log) and log[k, 0] <= t:
+            seq, kind, band, v = log[k]
+            (o.boost if kind == 0 else o.mix)(int(band), float(v))
+            k += 1
+        yo[t] = o(xin[t])
+        o.tick()
+    assert np.max(np.abs(yg - yo)) <= 1e-9 * np.max(np.abs(yo))
+    steady = lat[200:] * 1e-3
+    print(f"{len(log)} setters; per-sample latency: median {np.median(steady):.2f} us, p99 "
+          f"{np.percentile(steady, 99):.2f} us, worst {steady.max():.2f} us")
