@@ -4,6 +4,7 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -65,6 +66,9 @@ struct hz_fb {
     // entry points that touch the staged parameters or the state hold it (setters may come from
     // another thread while samples run: tests/filterbank.cpp:217-252 vs 200-210)
     std::recursive_mutex mu;
+    // setters waiting for `mu`: a per-sample call lets them in first (a thread calling operator()
+    // in a tight loop would otherwise re-take the lock before a waiting setter is scheduled)
+    std::atomic<int> setter_wait{0};
     long pg_gen = 0, coef_gen = 0;   // generations of the staged targets / coefficients
     long long setter_seq = 0;        // per-sample calls served when the last setter ran
     int order = 2, N = 0, N_total = 0, band_begin = 0, device = 0;
@@ -228,6 +232,17 @@ struct hz_fb {
 };
 
 namespace hz_fbi {
+
+// a setter's hold on the handle (announced, so per-sample calls let it in: hz_fb::setter_wait)
+struct SetterLock {
+    hz_fb* h;
+    explicit SetterLock(hz_fb* h_) : h(h_) {
+        h->setter_wait.fetch_add(1);
+        h->mu.lock();
+        h->setter_wait.fetch_sub(1);
+    }
+    ~SetterLock() { h->mu.unlock(); }
+};
 
 // hz_filterbank.hip
 int fb_set_lds_attr(const void* kernel);

@@ -26,6 +26,7 @@
 // documented application point.
 #include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "hz_fb_impl.h"
 #include "hz_rt.h"
@@ -162,6 +163,8 @@ int hz_fb_sample(hz_fb* h, double x, int dist_id, double param, double* y) {
         hz::set_error("hz_fb_sample: invalid arguments");
         return HZ_E_INVALID;
     }
+    for (int spin = 0; h->setter_wait.load(std::memory_order_relaxed) > 0 && spin < (1 << 20); ++spin)
+        std::this_thread::yield();   // a setter from another thread goes first (the next sample sees it)
     std::lock_guard<std::recursive_mutex> lk(h->mu);
     HZ_TRY_HIP(hipSetDevice(h->device));
     hz_fb::Rt& T = h->rt;

@@ -1057,7 +1057,7 @@ int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double*
         hz::set_error("hz_fb_coefficients: invalid arguments");
         return HZ_E_INVALID;
     }
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::SetterLock lk(h);
     ++h->coef_gen;
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
@@ -1077,7 +1077,7 @@ int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double*
 
 int hz_fb_boost(hz_fb* h, int n, double v) {
     if (!h) return HZ_E_INVALID;
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::SetterLock lk(h);
     ++h->pg_gen;
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
@@ -1097,7 +1097,7 @@ int hz_fb_boost(hz_fb* h, int n, double v) {
 
 int hz_fb_boost_all(hz_fb* h, const double* v, int count) {
     if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::SetterLock lk(h);
     ++h->pg_gen;
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
@@ -1113,7 +1113,7 @@ int hz_fb_boost_all(hz_fb* h, const double* v, int count) {
 
 int hz_fb_mix(hz_fb* h, int n, double v) {
     if (!h) return HZ_E_INVALID;
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::SetterLock lk(h);
     ++h->pg_gen;
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
@@ -1133,7 +1133,7 @@ int hz_fb_mix(hz_fb* h, int n, double v) {
 
 int hz_fb_mix_all(hz_fb* h, const double* v, int count) {
     if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::SetterLock lk(h);
     ++h->pg_gen;
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
@@ -1149,7 +1149,7 @@ int hz_fb_mix_all(hz_fb* h, const double* v, int count) {
 
 int hz_fb_open(hz_fb* h) {
     if (!h) return HZ_E_INVALID;
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::SetterLock lk(h);
     ++h->pg_gen;
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);

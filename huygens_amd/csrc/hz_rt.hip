@@ -17,6 +17,7 @@
 // others follow through a device-memory flag), so a request is served once by each workgroup even
 // when it arrives while the instance leaves.
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -25,6 +26,7 @@
 namespace hz_rt {
 
 constexpr long long kIdleTicks = 200000;   // 2 ms of the 100 MHz real-time counter without a request
+                                           // (env HZ_RT_IDLE_US overrides it at each launch)
 constexpr long long kQuit = -1;
 
 struct ServerArgs {
@@ -32,6 +34,7 @@ struct ServerArgs {
     Slot* slot;
     long long* ctl;   // device memory: workgroup 0's idle-exit decision
     long long epoch;
+    long long idle;   // real-time ticks without a request before leaving
 };
 
 namespace {
@@ -262,7 +265,7 @@ __global__ __launch_bounds__(kThreads) void rt_server_kernel(ServerArgs a) {
                 r = ld_acq(&a.req->req);
                 if (r != seen) break;
                 if (g == 0) {
-                    if (__builtin_amdgcn_s_memrealtime() - last > kIdleTicks) {
+                    if (__builtin_amdgcn_s_memrealtime() - last > a.idle) {
                         __hip_atomic_store(a.ctl, kQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         r = kQuit;
                         break;
@@ -382,6 +385,11 @@ int srv_launch(Server* s) {
     a.slot = (Slot*)((char*)dmb + sizeof(Req));
     a.ctl = s->d_ctl;
     a.epoch = ++s->epoch;
+    a.idle = kIdleTicks;
+    if (const char* e = std::getenv("HZ_RT_IDLE_US")) {
+        const long long us = std::atoll(e);
+        if (us > 0 && us <= 10000000) a.idle = us * 100;
+    }
     hipLaunchKernelGGL(rt_server_kernel, dim3(kGroups), dim3(kThreads), 0, s->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     s->active = true;

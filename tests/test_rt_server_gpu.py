@@ -124,11 +124,13 @@ def test_interleaved_filterbank_handles(gpu_lib):
 
 
 def test_block_call_beside_resident_server(gpu_lib):
-    """A block call on another stream while the server is resident does not wait for the server's
-    idle exit (the server's stream has a hardware queue of its own)."""
+    """A block call on another stream while the server is resident does not wait for the server to
+    leave (the server's stream has a hardware queue of its own: rocprofv3 shows it on a queue of its
+    own, scripts/probe/rt_beside.py).  The server is launched with a
+    20 ms idle exit here, so a block call queued behind it would take >= 20 ms."""
     from huygens_amd import Filterbank, rt_info
-    g, _ = Filterbank(2, 256), None
-    g2 = Filterbank(2, 256)
+    g = Filterbank(2, 256)
+    g2 = Filterbank(2, 256, 0.001, 0.001)
     fwd, back = resonant_coefficients(256, 0.99, 1.0)
     for fb in (g, g2):
         for n in range(256):
@@ -136,24 +138,25 @@ def test_block_call_beside_resident_server(gpu_lib):
         fb.boost(np.ones(256))
         fb.open()
     x = white_noise_f32(4096, seed=2)
-    g2.process(x)   # warm
-    g(0.1)
-    g.tick()
-    launches0 = rt_info(0)[1]
-    times = []
-    for i in range(20):
-        g(0.1)
-        g.tick()
-        assert rt_info(0)[2]            # resident
-        t0 = time.perf_counter()
-        g2.process(x)                   # 4096 samples on another handle's stream
-        times.append(time.perf_counter() - t0)
-    relaunched = rt_info(0)[1] - launches0
-    print("block call beside the resident server (ms):", " ".join(f"{1e3 * t:.3f}" for t in times),
-          f"; server relaunches {relaunched}")
-    # a block call queued behind the resident kernel would wait for its 2 ms idle exit, and the
-    # server would then be relaunched by the next sample
-    assert np.median(times) < 0.5e-3 and relaunched == 0, (times, relaunched)
+    for _ in range(4):   # warm: converged, the LTI records built (host work on first use)
+        g2.process(x)
+    os.environ["HZ_RT_IDLE_US"] = "20000"
+    try:
+        time.sleep(0.05)
+        assert not rt_info(0)[2]        # the 2 ms instance has left; the next one waits 20 ms
+        times = []
+        for i in range(30):
+            g(0.1)
+            g.tick()
+            t0 = time.perf_counter()
+            g2.process(x)               # 4096 samples on another handle's stream
+            times.append(time.perf_counter() - t0)
+            assert rt_info(0)[2]
+    finally:
+        del os.environ["HZ_RT_IDLE_US"]
+    time.sleep(0.05)                    # the 20 ms instance leaves; later tests get the default
+    print("block call beside the resident server (ms):", " ".join(f"{1e3 * t:.3f}" for t in times))
+    assert max(times) < 10e-3 and np.median(times) < 0.5e-3, times
 
 
 def test_setters_from_another_thread(gpu_lib, tmp_path):
