@@ -333,6 +333,23 @@ def stream_block_flops(K, P=1024):
     return 33.0 * col + 1024 * 31 * 4.0
 
 
+def resp_alg_bytes(K, S, N, O=2, Qp=24):
+    """Algorithmic HBM bytes of one stationary call (no engine intermediates: the window spectra Z
+    and output spectra Y live only between the engine's own kernels).  Returns (dominant kernel,
+    whole call):
+      * inverse kernel + band-state pass: the output (8 S), the state window's K inputs (8 K, read
+        once), the history after the call (8 K), the pass's per-band operand rows (pin E_0, pin E_H
+        and the carry / Horner weights: 2432 + 1152 doubles per group of 16 bands at O = 2,
+        hz_fb_state.h grp_doubles), the states out (8 N O) and the smoothers (16 N in, 16 N out);
+      * the whole call adds the input read by the forward transforms (8 S + 8 K history) and the
+        response's partition spectra (Qp x 2049 complex, read by the MAC)."""
+    groups = -(-N // (32 // O))
+    ops = groups * ((32 // O) * 152 + 2 * 16 * 9 * 4) * 8
+    dom = 8 * S + 8 * K + 8 * K + ops + 8 * N * O + 32 * N
+    call = dom + 8 * S + 8 * K + Qp * (2 * 2048 + 1) * 8
+    return dom, call
+
+
 def resp_inv_flops(S):
     """FP64 flops of the inverse transforms of a stationary call's output blocks (as resp_step_flops)."""
     H, lgH = 2048, 11
@@ -866,6 +883,22 @@ def main():
                                        f"response, one all-reduce at setup), band states sharded x{P_t}; no "
                                        f"data-path collective" + (" (+ gather to rank 0)" if args.gather else "")
                                        if tshard and resp else f"bands sharded x{world}, RCCL reduce")},
+            "rehearsal": (f"{world} ranks on one GPU, collectives over gloo through host copies "
+                          "(HZ_BENCH_REHEARSAL=1): the N > 1 code path, not an N-GPU figure")
+                         if world > 1 and os.environ.get("HZ_BENCH_REHEARSAL") == "1" else None,
+            # N > 1: which decomposition `value` is, and north_star's beside it
+            "decomposition": None if world == 1 else {
+                "value": (f"WEAK scaling: a step is one {world} x 10 s call split by time, each GPU outputs "
+                          f"its own 10 s of all {N_BANDS} bands (the work per GPU is fixed, the job grows with N)"
+                          if P_t > 1 and resp else
+                          f"STRONG scaling: a fixed 10 s call per step, bands sharded x{world}, RCCL reduce"),
+                "north_star_band_partition": dict(side.get("band_partition") or {},
+                                                  scaling="strong",
+                                                  what=(f"north_star's decomposition: a FIXED 10 s call per step, "
+                                                        f"{N_BANDS} bands partitioned over {world} GPUs, partial "
+                                                        "mixes summed to rank 0 by an RCCL reduce"))
+                if side.get("band_partition") else "not measured (--side-steps 0)",
+            },
             "engine": "stationary (bank response convolution, eager band states)" if resp
                       else "per-band LTI" if lti else "per-band general",
             "roofline": {
@@ -878,13 +911,14 @@ def main():
                 "flops_source": "pmc (SQ_INSTS_VALU_{FMA,MUL,ADD}_F64, SQ_INSTS_VALU_MFMA_MOPS_F64)" if dom_flops
                                 else "model (bench.resp_step_flops)",
                 "model_flops_per_launch": dom_model,
-                # inverse kernel: the output spectra in, the output out, the next history written;
-                # its state pass: the K history samples in, every band's chunk end-state map E
-                # (O x (128 + O) doubles), carry powers and O states out; per-band engines: the block
-                # I/O and the band records
-                "algorithmic_bytes_per_launch": (16 * 2048 * -(-out_samples // 2048) + 8 * out_samples + 16 * horizon
-                                                 + 8 * cnt * 2 * (130 + 2) + 64 * cnt) if resp
+                # inverse kernel + state pass: bench.resp_alg_bytes (the output, the state window,
+                # the history written, the pass's operand rows, the states and smoothers -- not the
+                # Y spectra, an engine intermediate); per-band engines: the block I/O and the band
+                # records
+                "algorithmic_bytes_per_launch": resp_alg_bytes(horizon, out_samples, cnt)[0] if resp
                                                 else (16 * out_samples + 120 * cnt),
+                "traffic_over_algorithmic": (dom_traffic / resp_alg_bytes(horizon, out_samples, cnt)[0])
+                                            if (resp and dom_traffic) else None,
                 "peak_note": "FP64 MFMA peak = FP64 vector peak on MI355X (78.6 TFLOP/s); the state pass is "
                              "v_mfma_f64_16x16x4f64 chains (scripts/probe/mfma_f64_probe.hip: 71-78 TFLOP/s)",
                 "step": {
@@ -899,6 +933,10 @@ def main():
                     "achieved_tflops": step_fl / launch_avg_s / 1e12 if launch_avg_s > 0 else None,
                     "frac": step_fl / launch_avg_s / 1e12 / FP64_PEAK_TFLOPS if launch_avg_s > 0 else None,
                     "traffic_per_call": sum(traffic.values()) if traffic else None,
+                    "algorithmic_bytes_per_call": resp_alg_bytes(horizon, out_samples, cnt)[1] if resp
+                                                  else (16 * out_samples + 120 * cnt),
+                    "traffic_over_algorithmic": (sum(traffic.values()) / resp_alg_bytes(horizon, out_samples, cnt)[1])
+                                                if (resp and traffic) else None,
                     "traffic_per_kernel": traffic, "flops_per_kernel": flops,
                     "traffic_detail": traffic_detail if not traffic else traffic_detail.get("method"),
                     "flops_detail": flops_detail if not flops else "pmc",
@@ -933,13 +971,23 @@ def run_row(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and args.workload not in ("c3", "c4"):
         raise SystemExit("--workload c5..c9 are single-GPU configs (SURVEY.md 8(d)); c3 and c4 shard")
+    rehearsal = world > 1 and os.environ.get("HZ_BENCH_REHEARSAL") == "1"
+    if rehearsal:   # (one-GPU box: every rank on cuda:0, the reduces through host copies over gloo)
+        local = 0
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group("gloo")
+            bench_rows.COLL = _HostDist(dist)
+        else:
+            os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            dist.init_process_group("nccl", device_id=dev)
         body = (bench_rows.run_c3 if args.workload == "c3" else bench_rows.run_c4)(args, torch, dev, rank, world)
+        if rehearsal:
+            body["rehearsal"] = (f"{world} ranks on one GPU, reduces over gloo through host copies "
+                                 "(HZ_BENCH_REHEARSAL=1): the N > 1 code path, not an N-GPU figure")
     elif args.workload in ("c3", "c4") and args.emulate_world:
         body = (bench_rows.run_c3 if args.workload == "c3" else bench_rows.run_c4)(args, torch, dev, 0, 1,
                                                                                   args.emulate_world)

@@ -27,20 +27,40 @@ def _tests_path():
         sys.path.insert(0, p)
 
 
+# the collectives of a multi-rank row: torch.distributed over RCCL, or (HZ_BENCH_REHEARSAL=1,
+# several ranks on one GPU) bench._HostDist over gloo; set by bench.run_row
+COLL = None
+
+
+def _coll():
+    if COLL is None:
+        import torch.distributed as dist
+        return dist
+    return COLL
+
+
+def _sync(torch, dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _stream_handle(torch, dev):
+    return torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
+
+
 def _timed(step, steps, warmup, torch, dev, world=1):
     """Wall time of `steps` steps after `warmup`, barrier + synchronize on both sides; the
     max over ranks when world > 1."""
-    if world > 1:
-        import torch.distributed as dist
+    dist = _coll() if world > 1 else None
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize(dev)
+    _sync(torch, dev)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-    torch.cuda.synchronize(dev)
+    _sync(torch, dev)
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
@@ -59,11 +79,12 @@ def _timed(step, steps, warmup, torch, dev, world=1):
 EXEC_C3 = 5.0
 
 
-def run_c3(args, torch, dev, rank=0, world=1, shard_world=None):
+def run_c3(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
     """Additive<double>(&cycle, 64, 256, 0.75, 1.0), all voices via makenote(36+v, 1),
     voices 0-7 released at sample 24,000; one step = 480,000 samples.  With world > 1 (the
     BASELINE config: 8 GPUs) each rank owns a contiguous overtone range (huygens_amd.shard,
-    hz_add_create_shard) and the partial mixes are summed to rank 0 by an RCCL reduce."""
+    hz_add_create_shard) and the partial mixes are summed to rank 0 by an RCCL reduce.  `probe`
+    (tests) is called with the last step's output after the timed steps."""
     from huygens_amd import Additive
     from huygens_amd.shard import shard_of
     V, O, S = 64, 256, args.samples
@@ -72,8 +93,7 @@ def run_c3(args, torch, dev, rank=0, world=1, shard_world=None):
     add = Additive(V, O, 0.75, 1.0, device=dev.index or 0, shard=(o0, oc) if sw > 1 else None)
     for v in range(V):
         add.makenote(36 + v, 1.0)
-    stream = torch.cuda.current_stream(dev)
-    add.set_stream(stream.cuda_stream)
+    add.set_stream(_stream_handle(torch, dev))
     y = torch.empty(S, dtype=torch.float64, device=dev)
     rel = min(24000, S)
 
@@ -85,20 +105,12 @@ def run_c3(args, torch, dev, rank=0, world=1, shard_world=None):
         if world > 1:
             dist.reduce(y, dst=0, op=dist.ReduceOp.SUM)
 
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
+    dist = _coll() if world > 1 else None
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = _timed(step, args.steps, 0, torch, dev)
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = _timed(step, args.steps, 0, torch, dev, world)
+    if probe is not None:
+        probe(y)
     add.profile(True)   # kernel times: a separate profiled pass (no events in the timed region)
     _timed(step, args.steps, 0, torch, dev)
     ms, launches = add.profile_read()
@@ -157,7 +169,7 @@ def c4_signal(n, seed=3):
     return x
 
 
-def run_c4(args, torch, dev, rank=0, world=1, shard_world=None):
+def run_c4(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
     """StaticSTFT(4096, 4) with its built-in gate over 480,000 samples (C4 (i)); the
     Fourier(gate625) variant (ii) is timed beside it.  Under torchrun (world > 1) every rank
     streams the whole input but computes only its runs of frames (runs of ceil(frames per
@@ -169,10 +181,9 @@ def run_c4(args, torch, dev, rank=0, world=1, shard_world=None):
     x = torch.from_numpy(c4_signal(S)).to(dev)
     yr = torch.empty_like(x)
     yi = torch.empty_like(x)
-    stream = torch.cuda.current_stream(dev)
     out = {}
     for name, eng in (("static", StaticSTFT(N, laps)), ("gate625", Fourier(2, N, laps))):
-        eng.set_stream(stream.cuda_stream)
+        eng.set_stream(_stream_handle(torch, dev))
         sw = shard_world or world   # --emulate-world: rank 0's share of an sw-GPU job, no reduce
         if sw > 1:
             eng.set_frame_shard(rank, sw, -(-frames_before(N, laps, S) // sw))
@@ -180,14 +191,16 @@ def run_c4(args, torch, dev, rank=0, world=1, shard_world=None):
         def step():
             eng.process_block_device(x.data_ptr(), 0, yr.data_ptr(), yi.data_ptr(), S)
             if world > 1:
-                import torch.distributed as dist
+                dist = _coll()
                 dist.reduce(yr, dst=0, op=dist.ReduceOp.SUM)
 
         for _ in range(args.warmup):
             step()
-        torch.cuda.synchronize(dev)
+        _sync(torch, dev)
         f0 = eng.frames()[0]
         elapsed = _timed(step, args.steps, 0, torch, dev, world)
+        if probe is not None and name == "static":
+            probe(yr)
         frames = eng.frames()[0] - f0
         # kernel times from a separate profiled pass: each block's frame launch repeated 8x
         # between one event pair (an event pair costs about as much as one ~20 us launch)

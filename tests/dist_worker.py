@@ -162,6 +162,100 @@ def _shard_protocol(rank, world, variant):
     return res
 
 
+class FakeAdditive:
+    """Stands in for huygens_amd.Additive in bench_rows.run_c3 on a CPU device: fill_device writes
+    the shard's partial mix y[t] = sum over its overtones o of cos(1e-3 (o + 1) t), t the handle's
+    running sample count, into the (CPU) buffer at the pointer."""
+
+    def __init__(self, V, O, k_p, k_g, device=0, shard=None):
+        self.o0, self.oc = shard if shard is not None else (0, O)
+        self.t = 0
+
+    def makenote(self, *a):
+        pass
+
+    def release(self, v):
+        pass
+
+    def set_stream(self, s):
+        pass
+
+    def fill_device(self, ptr, n):
+        import ctypes
+        t = np.arange(self.t, self.t + n, dtype=np.float64)
+        o = np.arange(self.o0, self.o0 + self.oc, dtype=np.float64)[:, None]
+        y = np.ascontiguousarray(np.cos(1e-3 * (o + 1) * t).sum(axis=0) if self.oc else np.zeros(n))
+        ctypes.memmove(ptr, y.ctypes.data, 8 * n)
+        self.t += n
+
+    def profile(self, on):
+        pass
+
+    def profile_read(self):
+        return 1.0, 1
+
+
+class FakeSTFT:
+    """Stands in for StaticSTFT / Fourier in bench_rows.run_c4 on a CPU device: process_block_device
+    writes x[t] for the samples of this rank's frame runs (runs of `per` 1024-sample hops rotating
+    over the ranks) and 0 elsewhere, so the reduced output is x."""
+
+    def __init__(self, *a):
+        self.rank, self.world, self.per, self.f = 0, 1, 1, 0
+
+    def set_stream(self, s):
+        pass
+
+    def set_frame_shard(self, rank, world, per):
+        self.rank, self.world, self.per = rank, world, per
+
+    def process_block_device(self, xp, _, yrp, yip, n):
+        import ctypes
+        x = np.ctypeslib.as_array((ctypes.c_double * n).from_address(xp)).copy()
+        run = (np.arange(n) // 1024) // max(1, self.per)
+        y = np.where(run % self.world == self.rank, x, 0.0)
+        ctypes.memmove(yrp, np.ascontiguousarray(y).ctypes.data, 8 * n)
+        ctypes.memmove(yip, np.zeros(n).ctypes.data, 8 * n)
+        self.f += n // 1024
+
+    def frames(self):
+        return (self.f, 0)
+
+    def profile(self, on, repeat=1):
+        pass
+
+    def profile_read(self):
+        return 1.0, 1.0, 1
+
+
+def _row(kind, rank, world, dist):
+    """bench_rows.run_c3 / run_c4 through their real multi-rank code (the reduce to rank 0, the
+    max-over-ranks timing) over gloo, fake handles standing in for the HIP objects."""
+    import argparse
+    import torch
+    import bench_rows
+    import huygens_amd
+    bench_rows.COLL = dist
+    args = argparse.Namespace(samples=4800, warmup=1, steps=2, no_cpu_baseline=True, no_traffic=True)
+    got = {}
+    if kind == "c3":
+        huygens_amd.Additive = FakeAdditive
+        body = bench_rows.run_c3(args, torch, torch.device("cpu"), rank, world,
+                                 probe=lambda y: got.setdefault("y", y.clone()))
+        t = np.arange((args.warmup + args.steps - 1) * args.samples, (args.warmup + args.steps) * args.samples)
+        full = np.cos(1e-3 * (np.arange(256)[:, None] + 1) * t).sum(axis=0)
+    else:
+        huygens_amd.StaticSTFT = FakeSTFT
+        huygens_amd.Fourier = FakeSTFT
+        body = bench_rows.run_c4(args, torch, torch.device("cpu"), rank, world,
+                                 probe=lambda y: got.setdefault("y", y.clone()))
+        full = bench_rows.c4_signal(args.samples)
+    res = {"n_gpus": body["n_gpus"], "value": body["value"], "ms": body["ms_per_step"]}
+    if rank == 0 and got.get("y") is not None:
+        res["err"] = float(np.max(np.abs(got["y"].numpy() - full)) / np.max(np.abs(full)))
+    return res
+
+
 def main():
     import torch
     import torch.distributed as dist
@@ -169,6 +263,13 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     kind, out_path = sys.argv[1], sys.argv[2]
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if kind.startswith("row:"):
+        res = _row(kind.split(":")[1], rank, world, dist)
+        with open(f"{out_path}.{rank}", "w") as fh:
+            json.dump(res, fh)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     if kind.startswith("protocol"):
         res = _shard_protocol(rank, world, kind.split(":")[1])
         with open(f"{out_path}.{rank}", "w") as fh:

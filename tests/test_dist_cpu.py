@@ -33,7 +33,7 @@ def _run(kind, world, tmp_path):
     for p in procs:
         o, _ = p.communicate(timeout=240)
         assert p.returncode == 0, o.decode()[-2000:]
-    if kind.startswith("protocol"):
+    if kind.startswith(("protocol", "row:")):
         return [json.loads((tmp_path / f"{kind}.json.{r}").read_text()) for r in range(world)]
     return json.loads(out.read_text())
 
@@ -99,3 +99,14 @@ def test_time_shard_protocol_no_horizon(tmp_path):
     left waiting in a collective) -- ADVICE r2."""
     res = _run("protocol:no_horizon", 2, tmp_path)
     assert [rr["ok"] for rr in res] == [False, False]
+
+@pytest.mark.parametrize("row", ["c3", "c4"])
+def test_bench_row_reduce_world2(row, tmp_path):
+    """bench_rows.run_c3 / run_c4 at world 2 through their real multi-rank code -- shard
+    construction, the per-step reduce to rank 0, max-over-ranks timing -- over gloo, with fake
+    handles on a CPU device (tests/dist_worker.py FakeAdditive / FakeSTFT): rank 0's reduced output
+    is the whole job's (C3's N > 1 path had never executed)."""
+    res = _run(f"row:{row}", 2, tmp_path)
+    assert [r["n_gpus"] for r in res] == [2, 2]
+    assert res[0]["ms"] == res[1]["ms"]          # max over ranks on both
+    assert res[0]["err"] < 1e-12
