@@ -277,26 +277,38 @@ def run_c5(args, torch, dev):
     bank = Delaybank(L, 3, 2 * SR, np.float32)
     for k in range(L):
         bank.coefficients(k, [(0, 1.0)], [(10000 + 37 * k, 0.5), (20000 + 53 * k, 0.5)])
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)   # one stream for both handles (the fused call requires it)
     bowl.set_stream(stream.cuda_stream)
     bank.set_stream(stream.cuda_stream)
     buf = torch.empty(nb * B, dtype=torch.float32, device=dev)
     mix = torch.empty(nb * B, dtype=torch.float32, device=dev)
 
-    def step():
+    def step_calls():   # the reference's two calls per block: fill, then process (4 launches)
         bowl.trigger()
         for i in range(nb):
             bowl.fill_device(buf.data_ptr() + 4 * B * i, B)
             bank.process_device(buf.data_ptr() + 4 * B * i, mix.data_ptr() + 4 * B * i, B, False, True)
 
+    def step():   # the same two calls as one launch per block (hz_bowl_fill_delaybank)
+        bowl.trigger()
+        for i in range(nb):
+            bowl.fill_delaybank(bank, buf.data_ptr() + 4 * B * i, mix.data_ptr() + 4 * B * i, B, True)
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     elapsed = _timed(step, args.steps, 0, torch, dev)   # no event records in the timed region
-    # kernel times of the streamed blocks: a separate profiled pass
+    elapsed_calls = _timed(step_calls, args.steps, 1, torch, dev)
+    # kernel times of the streamed blocks: a separate profiled pass (the fused launch is the bowl's)
     bowl.profile(True)
     bank.profile(True)
     _timed(step, args.steps, 0, torch, dev)
+    fms, fl = bowl.profile_read()
+    bowl.profile(False)
+    bank.profile(False)
+    bowl.profile(True)
+    bank.profile(True)
+    _timed(step_calls, args.steps, 0, torch, dev)
     bms, bl = bowl.profile_read()
     dms, dl = bank.profile_read()
     bowl.profile(False)
@@ -362,6 +374,14 @@ def run_c5(args, torch, dev):
                                "line_samples_per_s_kernel": dly_rate, "bytes_per_unit": 20,
                                "whole_signal_ms_by_split": split_ms},
         "streamed_kernel_ms_per_step": {"bowl": bms / args.steps, "delaybank": dms / args.steps},
+        "block": {"us_per_block": 1e6 * elapsed / args.steps / nb, "launches_per_block": 1,
+                  "kernel": "bowl_dly_chain_kernel (hz_bowl_fill_delaybank: the block's Bowl samples, "
+                            "every line, the ring commit and the mixdown in one launch)",
+                  "kernel_us_per_block": 1e3 * fms / max(1, fl),
+                  "two_calls_per_block": {"us_per_block": 1e6 * elapsed_calls / args.steps / nb,
+                                          "launches_per_block": 4,
+                                          "value": M * n * args.steps / elapsed_calls,
+                                          "kernel_us_per_block": 1e3 * (bms + dms) / args.steps / nb}},
         "cpu_baseline": cpu,
     }
 

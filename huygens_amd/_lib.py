@@ -169,6 +169,7 @@ _SIGS = {
     "hz_bowl_set_target_groups": (I, [VP, I]),
     "hz_bowl_profile": (I, [VP, I]),
     "hz_bowl_profile_read": (I, [VP, PD, C.POINTER(L)]),
+    "hz_bowl_fill_delaybank": (I, [VP, VP, VP, VP, SZ, I]),
     "hz_dly_create": (I, [I, C.c_uint, C.c_uint, I, I, C.POINTER(VP)]),
     "hz_dly_destroy": (I, [VP]),
     "hz_dly_coefficients": (I, [VP, I, C.POINTER(C.c_uint), PD, I, C.POINTER(C.c_uint), PD, I]),

@@ -45,6 +45,12 @@ class Bowl:
     def fill_device(self, ptr: int, n: int):
         check(self._lib.hz_bowl_fill_device(self._h, C.c_void_p(ptr), n))
 
+    def fill_delaybank(self, bank, buf_ptr: int, out_ptr: int, n: int, mix: bool = True):
+        """`fill(buf, n); bank.process(buf, out, n)` on device buffers in one launch when the bank's
+        taps allow it (hz_bowl_fill_delaybank), else the two block calls; both on one stream."""
+        check(self._lib.hz_bowl_fill_delaybank(self._h, C.c_void_p(buf_ptr), bank._h, C.c_void_p(out_ptr), n,
+                                               1 if mix else 0))
+
     def render(self, n: int) -> np.ndarray:
         out = np.zeros(n)
         if n:

@@ -27,6 +27,7 @@
 #include <new>
 #include <vector>
 
+#include "hz_chain.h"
 #include "hz_common.h"
 
 namespace {
@@ -256,6 +257,146 @@ __global__ __launch_bounds__(64 * kShortSlices) void bowl_reduce_short_kernel(co
     }
 }
 
+// ---- Bowl<float>::fill into a Delaybank<float> in one launch (hz_chain.h) ----------------------
+// A workgroup owns kChainSpw consecutive samples: the float modal model of every mode for them
+// (bowl_mix_kernel's per-sample arithmetic, the decay seeded at the workgroup's first sample), the
+// mode sum in double rounded to float (the fill buffer), then every line of the bank for those
+// samples (dly_line_kernel's tap arithmetic: age-0 reads take the new sample, all others ring
+// slots no sample of the block writes -- loaded before the modal sums, so their latency hides
+// under them), the ring commit and the mixdown in line order / N.  Modes come from a compact
+// table (float f, d, a + the double decay step), one coalesced load per mode and thread.
+constexpr int kChainSpw = 4;
+constexpr int kChainThreads = 512;
+constexpr int kChainMaxLines = kChainThreads / kChainSpw;   // one (line, sample) per thread
+constexpr long kChainMaxN = 8192;
+
+struct ChainArgs {
+    const float4* fda;     // [M] {f, d, a, 0} (Bowl<float>'s float coefficients)
+    const double* rstep;   // [M] E^{-d/SR} (BRec::R)
+    int M;
+    double n0;
+    long n;
+    float* buf;            // the fill buffer [n]
+    hz_chain::DlyBlock d;
+    float* out;            // mix: [n] (line sum / N); else [N][n] line outputs
+    int mix;
+};
+
+__global__ __launch_bounds__(kChainThreads) void bowl_dly_chain_kernel(ChainArgs a) {
+    constexpr int kW = kChainThreads / 64;
+    __shared__ double wsum[kW][kChainSpw];
+    __shared__ float xs[kChainSpw];
+    __shared__ float ly[kChainMaxLines * kChainSpw];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long t0 = (long)blockIdx.x * kChainSpw;
+    const hz_chain::DlyBlock& d = a.d;
+    const int S = d.S;
+    // ---- the bank's ring reads for this thread's (line, sample), issued first
+    const int l = tid / kChainSpw, sl = tid % kChainSpw;
+    const long j = t0 + sl;
+    const bool live = l < d.N && j < a.n;
+    const unsigned o = live ? (unsigned)((d.o0 + (unsigned long)j) % d.size) : 0u;
+    float rxv[hz_chain::kMaxTaps], ryv[hz_chain::kMaxTaps], fg[hz_chain::kMaxTaps], bg[hz_chain::kMaxTaps];
+    unsigned af_[hz_chain::kMaxTaps], ab_[hz_chain::kMaxTaps];
+#pragma unroll
+    for (int i = 0; i < hz_chain::kMaxTaps; ++i) {
+        rxv[i] = ryv[i] = fg[i] = bg[i] = 0.0f;
+        af_[i] = ab_[i] = 0u;
+        if (live && i < S) {
+            const int4* tp = d.taps + (long)l * 2 * S;
+            const float* gn = d.gains + (long)l * 2 * S;
+            const int4 qf = tp[i], qb = tp[S + i];
+            fg[i] = gn[i];
+            bg[i] = gn[S + i];
+            af_[i] = ((int)o < qf.x) ? (unsigned)qf.z : (unsigned)qf.y;
+            ab_[i] = ((int)o < qb.x) ? (unsigned)qb.z : (unsigned)qb.y;
+            if (af_[i] != 0u) rxv[i] = d.rx[(long)l * d.size + (o >= af_[i] ? o - af_[i] : o + d.size - af_[i])];
+            if (bg[i] != 0.0f && ab_[i] != 0u)
+                ryv[i] = d.ry[(long)l * d.size + (o >= ab_[i] ? o - ab_[i] : o + d.size - ab_[i])];
+        }
+    }
+    // ---- generator: acc[s] = sum over this thread's modes
+    float ph[kChainSpw];
+#pragma unroll
+    for (int s = 0; s < kChainSpw; ++s) ph[s] = phase_f(a.n0, t0 + s);
+    double acc[kChainSpw];
+#pragma unroll
+    for (int s = 0; s < kChainSpw; ++s) acc[s] = 0.0;
+    // kPre modes per thread per pass, their table entries loaded together (a mode past M is
+    // all zeros: amplitude 0 adds an exact 0)
+    constexpr int kPre = 4;
+    for (int m0 = tid; m0 < a.M; m0 += kPre * kChainThreads) {
+        float4 q[kPre];
+        double rs[kPre];
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) {
+            const int m = m0 + u * kChainThreads;
+            q[u] = m < a.M ? a.fda[m] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            rs[u] = m < a.M ? a.rstep[m] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) {
+            const float x0 = div_sr(-q[u].y * ph[0]);
+            double amag = (double)q[u].z * exp((double)x0);
+#pragma unroll
+            for (int s = 0; s < kChainSpw; ++s) {
+                const float p = div_sr(q[u].x * ph[s]);
+                const float wv = (float)sin2pi_ref(p);
+                acc[s] = fma(amag, (double)wv, acc[s]);
+                amag *= rs[u];
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < kChainSpw; ++s) {
+        double v = acc[s];
+#pragma unroll
+        for (int w = 32; w; w >>= 1) v += __shfl_xor(v, w);
+        if (lane == 0) wsum[wave][s] = v;
+    }
+    __syncthreads();
+    if (tid < kChainSpw) {
+        double v = wsum[0][tid];
+#pragma unroll
+        for (int w = 1; w < kW; ++w) v += wsum[w][tid];
+        const float x = (float)v;
+        xs[tid] = x;
+        if (t0 + tid < a.n) a.buf[t0 + tid] = x;
+    }
+    __syncthreads();
+    // ---- the bank (fp contraction off: every product and sum rounds as the reference's)
+    {
+#pragma clang fp contract(off)
+        if (live) {
+            const float x = xs[sl];
+            float accd = 0.0f;
+#pragma unroll
+            for (int i = 0; i < hz_chain::kMaxTaps; ++i) {
+                if (i < S) {
+                    const float xv = af_[i] == 0u ? x : rxv[i];
+                    const float yv = bg[i] != 0.0f ? (ab_[i] == 0u ? accd : ryv[i]) : 0.0f;
+                    const float fx = fg[i] * xv;
+                    const float by = bg[i] * yv;
+                    accd = accd + (fx - by);
+                }
+            }
+            d.rx[(long)l * d.size + o] = x;
+            d.ry[(long)l * d.size + o] = accd;
+            if (a.mix) ly[l * kChainSpw + sl] = accd;
+            else a.out[(long)l * a.n + j] = accd;
+        }
+        if (a.mix) {
+            __syncthreads();
+            if (tid < kChainSpw && t0 + tid < a.n) {
+                float m = 0.0f;   // line order; the LDS reads of 16 lines issue together
+#pragma unroll 16
+                for (int k = 0; k < d.N; ++k) m = m + ly[k * kChainSpw + tid];
+                a.out[t0 + tid] = m / (float)d.N;
+            }
+        }
+    }
+}
+
 void build_brec(double f, double amp, double d, bool is_float, double* rec) {
     using C = std::complex<long double>;
     std::memset(rec, 0, sizeof(double) * BRec::SIZE);
@@ -296,6 +437,7 @@ struct hz_bowl {
     int M = 0, device = 0, is_float = 0;
     double n0 = 0;  // phase counter (T) at the next call
     double *d_rec = nullptr, *d_partial = nullptr;
+    void* d_chain = nullptr;   // (float Bowls) [M] float4 {f, d, a, 0} then [M] double decay steps
     void* d_out = nullptr;
     size_t partial_cap = 0, out_cap = 0;
     int target_groups = 256;
@@ -478,6 +620,26 @@ int hz_bowl_create(int overtones, const double* f, const double* a, const double
         return HZ_E_ALLOC;
     }
     h->own_stream = true;
+    if (h->is_float) {   // the fused block's compact mode table (hz_bowl_fill_delaybank)
+        std::vector<float> fda((size_t)overtones * 4, 0.0f);
+        std::vector<double> rs((size_t)overtones);
+        for (int i = 0; i < overtones; ++i) {
+            const double* r = &rec[(size_t)i * BRec::SIZE];
+            fda[4 * (size_t)i] = (float)r[BRec::F];
+            fda[4 * (size_t)i + 1] = (float)r[BRec::D];
+            fda[4 * (size_t)i + 2] = (float)r[BRec::AMP];
+            rs[i] = r[BRec::R];
+        }
+        const size_t fb = sizeof(float) * fda.size();
+        if (hipMalloc(&h->d_chain, fb + sizeof(double) * rs.size()) != hipSuccess ||
+            hipMemcpy(h->d_chain, fda.data(), fb, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy((char*)h->d_chain + fb, rs.data(), sizeof(double) * rs.size(), hipMemcpyHostToDevice) !=
+                hipSuccess) {
+            hz::set_error("hz_bowl_create: device allocation failed");
+            (void)hz_bowl_destroy(h);
+            return HZ_E_ALLOC;
+        }
+    }
     *out = h;
     return HZ_OK;
 }
@@ -486,7 +648,7 @@ int hz_bowl_destroy(hz_bowl* h) {
     if (!h) return HZ_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (void* p : {(void*)h->d_rec, (void*)h->d_partial, h->d_out})
+    for (void* p : {(void*)h->d_rec, (void*)h->d_partial, h->d_out, h->d_chain})
         if (p) (void)hipFree(p);
     if (h->la_buf) (void)hipHostFree(h->la_buf);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
@@ -585,6 +747,60 @@ int hz_bowl_profile_read(hz_bowl* h, double* ms, long* launches) {
     }
     if (ms) *ms = m;
     if (launches) *launches = h->launches;
+    return HZ_OK;
+}
+
+// Bowl<float>::fill(buf, n) then Delaybank<float>::process(buf, out, n, mix) (bowl.h:50-63,
+// delay.h:71-97) as one launch when the bank's taps allow it (hz_chain.h), else
+// the two block calls.  Both objects on one stream.
+int hz_bowl_fill_delaybank(hz_bowl* h, float* d_buf, hz_dly* bank, void* d_out, size_t bsize, int mix) {
+    HZ_TRY(bowl_check(h));
+    if (!bank || (bsize && (!d_buf || !d_out))) return HZ_E_INVALID;
+    bowl_settle(h);
+    const long n = (long)bsize;
+    hz_chain::DlyBlock d;
+    bool fusable = false;
+    HZ_TRY(hz_chain::dly_block_begin(bank, n, &d, &fusable));
+    HZ_TRY(bowl_check(h));
+    if (d.stream != h->stream) {
+        hz::set_error("hz_bowl_fill_delaybank: the bowl and the bank run on different streams (set_stream both)");
+        return HZ_E_INVALID;
+    }
+    if (n == 0) return HZ_OK;
+    if (!fusable || !h->is_float || !h->d_chain || n > kChainMaxN || d.N > kChainMaxLines) {
+        HZ_TRY(bowl_launch(h, d_buf, n, 0));
+        return hz_dly_process_device(bank, d_buf, d_out, bsize, 0, mix);
+    }
+    hipEvent_t* e = nullptr;
+    if (h->prof) {
+        if (h->ev_used + 2 > h->ev.size())
+            for (int q = 0; q < 128; ++q) {
+                hipEvent_t ne;
+                HZ_TRY_HIP(hz::prof_event_create(&ne));
+                h->ev.push_back(ne);
+            }
+        e = &h->ev[h->ev_used];
+        h->ev_used += 2;
+        HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
+    }
+    ChainArgs a;
+    a.fda = (const float4*)h->d_chain;
+    a.rstep = (const double*)((const char*)h->d_chain + sizeof(float4) * h->M);
+    a.M = h->M;
+    a.n0 = h->n0;
+    a.n = n;
+    a.buf = d_buf;
+    a.d = d;
+    a.out = (float*)d_out;
+    a.mix = mix ? 1 : 0;
+    hipLaunchKernelGGL(bowl_dly_chain_kernel, dim3((unsigned)((n + kChainSpw - 1) / kChainSpw)), dim3(kChainThreads),
+                       0, h->stream, a);
+    HZ_TRY_HIP(hipGetLastError());
+    if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
+    h->n0 += (double)n;
+    if (h->n0 > 16777216.0) h->n0 = 16777216.0;
+    h->launches += h->prof ? 1 : 0;
+    hz_chain::dly_block_end(bank, n);
     return HZ_OK;
 }
 

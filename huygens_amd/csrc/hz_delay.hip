@@ -33,6 +33,7 @@
 #include <new>
 #include <vector>
 
+#include "hz_chain.h"
 #include "hz_common.h"
 #include "hz_rt.h"
 
@@ -368,6 +369,44 @@ int set_tap(hz_dly* h, int line, int back, unsigned i, unsigned t, double g) {
 }
 
 }  // namespace
+
+namespace hz_chain {
+
+int dly_block_begin(hz_dly* h, long n, DlyBlock* b, bool* fusable) {
+    *fusable = false;
+    HZ_TRY(dly_check(h));
+    HZ_TRY(dly_upload(h));
+    b->taps = h->d_taps;
+    b->gains = (const float*)h->d_gains;
+    b->rx = (float*)h->d_rx;
+    b->ry = (float*)h->d_ry;
+    b->size = h->size;
+    b->o0 = h->origin;
+    b->N = h->N;
+    b->S = h->S;
+    b->stream = h->stream;
+    if (!h->is_float || h->S > kMaxTaps || n <= 0 || 2 * n > (long)h->size) return HZ_OK;
+    // every read of the block: the current sample, or a ring slot written before the call that no
+    // sample of the call overwrites (a read at age a from sample j hits slot o0 + j - a)
+    auto ok = [&](long a) { return a == 0 || (a >= n && a <= (long)h->size - n); };
+    for (int l = 0; l < h->N; ++l)
+        for (int i = 0; i < h->S; ++i)
+            for (int back = 0; back < 2; ++back) {
+                const size_t ti = (size_t)l * h->S + i;
+                if (back && h->bg[ti] == 0.0) continue;   // the kernel skips zero feedback gains
+                const int4 q = resolve_tap(h, back ? h->bt[ti] : h->ft[ti]);
+                if (!ok(q.y) || (q.x > 0 && !ok(q.z))) return HZ_OK;
+            }
+    *fusable = true;
+    return HZ_OK;
+}
+
+void dly_block_end(hz_dly* h, long n) {
+    h->origin = (unsigned)(((unsigned long)h->origin + (unsigned long)n) % h->size);
+    h->pending = true;
+}
+
+}  // namespace hz_chain
 
 extern "C" {
 

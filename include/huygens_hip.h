@@ -338,6 +338,14 @@ int hz_dly_set_target_groups(hz_dly* h, int groups);
 int hz_dly_profile(hz_dly* h, int enable);
 int hz_dly_profile_read(hz_dly* h, double* ms, long* launches);
 
+/* ---- a Bowl block into a Delaybank (`bowl.fill(buf, n);
+ * bank.process(buf, out, n);`, bowl.h:50-63 + delay.h:71-97) in one launch: every output equal to
+ * the two calls' (the fill buffer written too) when the Bowl is float, the bank is float with
+ * <= 128 lines of <= 8 taps, n <= 8192, 2 n <= the ring size and every live tap reads the current sample
+ * (time 0) or one at least n and at most size - n samples old (no sample of the block depends on
+ * another); otherwise the two block calls.  Both handles on one stream (set_stream). */
+int hz_bowl_fill_delaybank(hz_bowl* bowl, float* d_buffer, hz_dly* bank, void* d_out, size_t bsize, int mix);
+
 /* ---- Fourier / StaticSTFT (src/fourier.h:50-194, src/staticSTFT.h:10-177) ----
  * Fourier(int (*processor)(const complex<double>*, complex<double>*), int N, int laps):
  *   window HZ_WIN_HALFHANN; StaticSTFT(int N, int laps): window HZ_WIN_HANN with
