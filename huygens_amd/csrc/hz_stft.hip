@@ -64,6 +64,11 @@ struct StftArgs {
     // first run (index sh_q0) entered sh_off frames in; sh_world <= 1: f_lo, f_lo + 1, ...
     long sh_q0, sh_block;
     int sh_off, sh_world;
+    // unsharded launches (stft_pair4096_kernel): frame f_lo + i starts at position
+    // u0 + c (2N - 1) + stride r, (c, r) = (i0 + i) divmod 2 laps, and fills ring row (r0 + i) mod R
+    // -- the 64-bit divides of frame_at / frame_start / f % R done once on the host
+    long u0;
+    int i0, r0;
 };
 
 // the launch's i-th frame (one 64-bit divide per workgroup when sharded)
@@ -451,6 +456,333 @@ __global__ __launch_bounds__(kFrameThreads) void stft_pair_kernel(StftArgs a, lo
     }
 }
 
+// ---- N = 4096 pair frames (StaticSTFT's default size; C4), specialised ---------------------------
+// stft_pair_kernel<PROC, 3> at lg = 12 with the pass plan fixed at compile time: the same stage
+// arithmetic (hz::dif_regs / dit_regs order, the same twiddle values, so the same bits), with
+//   * the twiddles expanded once per workgroup from the compact table into a full half-table in
+//     LDS (one lookup per stage instead of the symmetry selects of hz::twc),
+//   * the frame in LDS at e ^ ((e >> 3) & 31): every pass of the plan conflict-free
+//     (scripts/probe/stft_layout.py; the pad16 layout cost 62 % of the LDS cycles in bank
+//     conflicts, rocprofv3 SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE on the C4 step),
+//   * the window product straight into the first pass's registers and the last inverse pass
+//     straight to the ring (two LDS round trips fewer),
+//   * the pair gate walking spectrum POSITIONS: bin k = bitrev(q) pairs with bin N - k at
+//     q ^ (hibit(q) - 1), the mirror of q within its power-of-two octave, so both reads of a
+//     pair run over contiguous positions.
+namespace p4 {
+constexpr int kLg = 12, kN = 1 << kLg, kH = kN / 2, kT = kN / 8;
+__device__ __forceinline__ int lx(int e) { return e ^ ((e >> 3) & 31); }
+inline size_t lds_bytes() { return sizeof(double) * 2 * kN + sizeof(double) * 32; }
+
+// (x + iy) *= w (conj: w̄): contracted (FMA); the FFT passes of this kernel need no op-by-op
+// agreement with the generic kernel, only the tolerance of the parity tests
+__device__ __forceinline__ void cmul_fma(double& r, double& i, double2 w, bool conj) {
+    const double wi = conj ? -w.y : w.y;
+    const double nr = fma(r, w.x, -i * wi);
+    const double ni = fma(r, wi, i * w.x);
+    r = nr;
+    i = ni;
+}
+
+// stage twiddles per pass (host-built after the N/2 table, hz_stft_create), contiguous in p:
+// A[k][p] = W^(p << k), p < 512 (forward lh 11, inverse lh 9 as A[2 - k]); B[k][p] = W^(p << (3 + k)),
+// p < 64 (lh 8 / 6); C[k][p] = W^(p << (6 + k)), p < 8 (lh 5 / 3); lh 2 / 0 have p = 0 (unit
+// twiddles, skipped).  A thread's nine twiddles (the inverse reuses the forward's) load once.
+constexpr int kTwA = 0, kTwB = 3 * 512, kTwC = kTwB + 3 * 64, kTwLen = kTwC + 3 * 8;
+
+// radix-8 DIF group (hz::dif_regs<3, true> stage order), twiddles tw[k * stride + p]
+template <bool UNIT>
+__device__ __forceinline__ void dif8(double (&xr)[8], double (&xi)[8], const double2 (&tw)[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int S = 8 >> (k + 1);
+        const double2 w = UNIT ? make_double2(1.0, 0.0) : tw[k];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j & S) continue;
+            const double ar = xr[j], ai = xi[j], cr = xr[j + S], ci = xi[j + S];
+            double dr = ar - cr, di = ai - ci;
+            if (!UNIT) cmul_fma(dr, di, w, false);
+            hz::mul_root16(dr, di, (j & (S - 1)) << (1 + k), false);
+            xr[j] = ar + cr;
+            xi[j] = ai + ci;
+            xr[j + S] = dr;
+            xi[j + S] = di;
+        }
+    }
+}
+
+// radix-8 DIT group (hz::dit_regs<3, true> stage order), conjugate twiddles tw[(2 - k) stride + p]
+template <bool UNIT>
+__device__ __forceinline__ void dit8(double (&xr)[8], double (&xi)[8], const double2 (&tw)[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int S = 1 << k;
+        const double2 w = UNIT ? make_double2(1.0, 0.0) : tw[2 - k];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j & S) continue;
+            double cr = xr[j + S], ci = xi[j + S];
+            if (!UNIT) cmul_fma(cr, ci, w, true);
+            hz::mul_root16(cr, ci, (j & (S - 1)) << (3 - k), true);
+            const double ar = xr[j], ai = xi[j];
+            xr[j] = ar + cr;
+            xi[j] = ai + ci;
+            xr[j + S] = ar - cr;
+            xi[j + S] = ai - ci;
+        }
+    }
+}
+
+template <int LD>   // a DIF pass's group (fft_fwd_lead: lh = LD + 2): base, stride 2^LD
+__device__ __forceinline__ int dif_base(int b) { return ((b >> LD) << (LD + 3)) + (b & ((1 << LD) - 1)); }
+template <int LH>   // a DIT pass's group (fft_inv_tail): base, stride 2^LH
+__device__ __forceinline__ int dit_base(int b) { return ((b >> LH) << (LH + 3)) + (b & ((1 << LH) - 1)); }
+
+// the frame as interleaved complex: one ds_read_b128 / ds_write_b128 per element (b128 reads reach
+// the LDS rate at one wave per SIMD, b64 reads need about four)
+template <int STRIDE>
+__device__ __forceinline__ void lds_get(const double2* z, int base, double (&xr)[8], double (&xi)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const double2 v = z[lx(base + j * STRIDE)];
+        xr[j] = v.x;
+        xi[j] = v.y;
+    }
+}
+template <int STRIDE>
+__device__ __forceinline__ void lds_put(double2* z, int base, const double (&xr)[8], const double (&xi)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[lx(base + j * STRIDE)] = make_double2(xr[j], xi[j]);
+}
+
+__device__ __forceinline__ int hibit(int x) { return 1 << (31 - __builtin_clz(x)); }
+
+// After the first forward pass the 4096-point DIF splits into eight 512-point transforms, and the
+// groups of forward lh 8, 5, 2 and inverse lh 0, 3, 6 of wave w all lie in [512 w, 512 w + 512):
+// between those passes a wave waits only for its own LDS writes (a wave's LDS operations complete
+// in order), not for the workgroup
+__device__ __forceinline__ void wave_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// pair_gate over positions (see above); c = 2 for a pair, 1 for bins 0 and N/2
+template <int PROC>
+__device__ __forceinline__ void gate(double2* zf, double p0, double p1, double* scratch) {
+#pragma clang fp contract(off)
+    constexpr int kItems = 5;   // 2047 pairs + the two self-paired bins (u = 2047, 2048) over 512 threads
+    const int b = threadIdx.x;
+    double ar[kItems], ai[kItems], br[kItems], bi[kItems];
+    int ek[kItems], em[kItems];
+    bool live[kItems], self[kItems];
+    double pa = 0.0, pb = 0.0, la = 0.0, lb = 0.0;
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const int u = b + kT * i;
+        int q, qq;
+        if (u < kH - 1) {
+            q = (u + 1) + hibit(u + 1);
+            qq = q ^ (hibit(q) - 1);
+        } else {   // u = 2047: bin 0 (position 0); u = 2048..: bin N/2 (position 1) on u = 2048 only
+            q = qq = u == kH - 1 ? 0 : 1;
+        }
+        live[i] = u <= kH;
+        self[i] = q == qq;
+        // k <= N/2 is the pair's first bin (pair_gate's k), m = N - k its partner
+        const int kq = hz::bitrev(q, kLg), kqq = hz::bitrev(qq, kLg);
+        const int qk = kq <= kqq ? q : qq, qm = kq <= kqq ? qq : q;
+        ek[i] = lx(qk);
+        em[i] = lx(qm);
+        ar[i] = ai[i] = br[i] = bi[i] = 0.0;
+        if (live[i]) {
+            const double2 zv = zf[ek[i]], wv = zf[em[i]];
+            const double zr = zv.x, zi = zv.y, wr = wv.x, wi = wv.y;
+            ar[i] = (zr + wr) * 0.5;   // X_f
+            ai[i] = (zi - wi) * 0.5;
+            br[i] = (zi + wi) * 0.5;   // X_{f+1}
+            bi[i] = (wr - zr) * 0.5;
+            const double c = self[i] ? 1.0 : 2.0;
+            if constexpr (PROC == HZ_PROC_STATIC_GATE) {
+                pa += c * (sqrt(ar[i] * ar[i] + ai[i] * ai[i]) / kN);
+                pb += c * (sqrt(br[i] * br[i] + bi[i] * bi[i]) / kN);
+            } else {
+                const double ha = hypot(ar[i], ai[i]), hb = hypot(br[i], bi[i]);
+                hz::dd_add(pa, la, ha);
+                hz::dd_add(pb, lb, hb);
+                if (c == 2.0) {
+                    hz::dd_add(pa, la, ha);
+                    hz::dd_add(pb, lb, hb);
+                }
+            }
+        }
+    }
+    double thra, thrb;
+    // both frames' sums in one reduction (block_sum / block_sum_dd's order for each)
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if constexpr (PROC == HZ_PROC_STATIC_GATE) {   // staticSTFT.h:99-128
+        for (int o = 32; o > 0; o >>= 1) {
+            pa += __shfl_xor(pa, o, 64);
+            pb += __shfl_xor(pb, o, 64);
+        }
+        if (lane == 0) {
+            scratch[2 * wave] = pa;
+            scratch[2 * wave + 1] = pb;
+        }
+        __syncthreads();
+        double avga = 0.0, avgb = 0.0;
+        for (int w = 0; w < kT / 64; ++w) {
+            avga += scratch[2 * w];
+            avgb += scratch[2 * w + 1];
+        }
+        thra = p0 * avga * avga;
+        thrb = p0 * avgb * avgb;
+    } else {   // tests/spectral.cpp:32-72 (sum / N in long double)
+        for (int o = 32; o > 0; o >>= 1) {
+            const double ah = __shfl_xor(pa, o, 64), al = __shfl_xor(la, o, 64);
+            const double bh = __shfl_xor(pb, o, 64), bl = __shfl_xor(lb, o, 64);
+            hz::dd_add(pa, la, ah);
+            hz::dd_add(pa, la, al);
+            hz::dd_add(pb, lb, bh);
+            hz::dd_add(pb, lb, bl);
+        }
+        if (lane == 0) {
+            scratch[4 * wave] = pa;
+            scratch[4 * wave + 1] = la;
+            scratch[4 * wave + 2] = pb;
+            scratch[4 * wave + 3] = lb;
+        }
+        __syncthreads();
+        pa = la = pb = lb = 0.0;
+        for (int w = 0; w < kT / 64; ++w) {
+            hz::dd_add(pa, la, scratch[4 * w]);
+            hz::dd_add(pa, la, scratch[4 * w + 1]);
+            hz::dd_add(pb, lb, scratch[4 * w + 2]);
+            hz::dd_add(pb, lb, scratch[4 * w + 3]);
+        }
+        const double qa = pa / kN, qb = pb / kN;
+        const double avga = qa + (fma(-qa, (double)kN, pa) + la) / kN;
+        const double avgb = qb + (fma(-qb, (double)kN, pb) + lb) / kN;
+        thra = p0 * avga * avga;
+        thrb = p0 * avgb * avgb;
+    }
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        if (!live[i]) continue;
+        double xr = ar[i], xi = ai[i], yr = br[i], yi = bi[i];
+        if constexpr (PROC == HZ_PROC_STATIC_GATE) {
+            if (xr * xr + xi * xi < thra) {
+                xr = xr * p1;
+                xi = xi * p1;
+            }
+            if (yr * yr + yi * yi < thrb) {
+                yr = yr * p1;
+                yi = yi * p1;
+            }
+        } else {
+            if (!(xr * xr + xi * xi > thra)) xr = xi = 0.0;
+            if (!(yr * yr + yi * yi > thrb)) yr = yi = 0.0;
+        }
+        // Y_k = X_f + i X_{f+1};  Y_{N-k} = conj X_f + i conj X_{f+1}
+        zf[ek[i]] = make_double2(xr - yi, xi + yr);
+        if (!self[i]) zf[em[i]] = make_double2(xr + yi, yr - xi);
+    }
+}
+}  // namespace p4
+
+template <int PROC>
+__global__ __launch_bounds__(p4::kT) void stft_pair4096_kernel(StftArgs a, long nf) {
+#pragma clang fp contract(off)
+    using namespace p4;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double2* z = (double2*)lds;
+    double* scratch = lds + 2 * kN;
+    const int b = threadIdx.x;
+    const double2* ptw = a.tw + kH;   // the pass tables
+    double2 twA[3], twB[3], twC[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        twA[k] = ptw[kTwA + 512 * k + b];
+        twB[k] = ptw[kTwB + 64 * k + (b & 63)];
+        twC[k] = ptw[kTwC + 8 * k + (b & 7)];
+    }
+    const int pl = frame_of_block(blockIdx.x, gridDim.x);   // frame pair within the launch
+    const bool two = 2L * pl + 1 < nf;
+    long off0, off1 = 0, row0, row1;
+    if (a.sh_world <= 1) {   // 32-bit arithmetic from the host's per-launch terms
+        const int tl = 2 * a.laps;
+        const int j0 = a.i0 + 2 * pl, j1 = j0 + (two ? 1 : 0);
+        const int c0 = j0 / tl, c1 = j1 / tl;
+        off0 = a.u0 + (long)c0 * (2 * kN - 1) + (long)a.stride * (j0 - c0 * tl);
+        off1 = two ? a.u0 + (long)c1 * (2 * kN - 1) + (long)a.stride * (j1 - c1 * tl) : 0;
+        row0 = (a.r0 + 2 * pl) % a.R;
+        row1 = (a.r0 + 2 * pl + (two ? 1 : 0)) % a.R;
+    } else {
+        const long f0 = frame_at(a, 2L * pl);
+        const long f1 = two ? frame_at(a, 2L * pl + 1) : f0;
+        off0 = frame_start(f0, a.laps, a.stride, kN) - a.T0 + (kN - 1);
+        off1 = two ? frame_start(f1, a.laps, a.stride, kN) - a.T0 + (kN - 1) : 0;
+        row0 = f0 % a.R;
+        row1 = f1 % a.R;
+    }
+    double xr[8], xi[8];
+    {   // the first forward pass's group {b + 512 j}: window x real input (fourier.h:110-112)
+        double v0[8], v1[8], w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = b + kT * j;
+            const long u0 = off0 + k, u1 = off1 + k;   // positions in [history (N-1) | block input]
+            v0[j] = u0 < kN - 1 ? a.hr[u0] : a.inr[u0 - (kN - 1)];
+            v1[j] = two ? (u1 < kN - 1 ? a.hr[u1] : a.inr[u1 - (kN - 1)]) : 0.0;
+            w[j] = a.win[k];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            xr[j] = w[j] * v0[j];
+            xi[j] = w[j] * v1[j];
+        }
+    }
+    dif8<false>(xr, xi, twA);   // lh 11
+    lds_put<512>(z, dif_base<9>(b), xr, xi);
+    __syncthreads();
+    lds_get<64>(z, dif_base<6>(b), xr, xi);
+    dif8<false>(xr, xi, twB);   // lh 8
+    lds_put<64>(z, dif_base<6>(b), xr, xi);
+    wave_sync();
+    lds_get<8>(z, dif_base<3>(b), xr, xi);
+    dif8<false>(xr, xi, twC);   // lh 5
+    lds_put<8>(z, dif_base<3>(b), xr, xi);
+    wave_sync();
+    lds_get<1>(z, dif_base<0>(b), xr, xi);
+    dif8<true>(xr, xi, twC);   // lh 2
+    lds_put<1>(z, dif_base<0>(b), xr, xi);
+    __syncthreads();
+    gate<PROC>(z, a.p0, a.p1, scratch);
+    __syncthreads();
+    lds_get<1>(z, dit_base<0>(b), xr, xi);
+    dit8<true>(xr, xi, twC);   // lh 0
+    lds_put<1>(z, dit_base<0>(b), xr, xi);
+    wave_sync();
+    lds_get<8>(z, dit_base<3>(b), xr, xi);
+    dit8<false>(xr, xi, twC);   // lh 3
+    lds_put<8>(z, dit_base<3>(b), xr, xi);
+    wave_sync();
+    lds_get<64>(z, dit_base<6>(b), xr, xi);
+    dit8<false>(xr, xi, twB);   // lh 6
+    lds_put<64>(z, dit_base<6>(b), xr, xi);
+    __syncthreads();
+    lds_get<512>(z, dit_base<9>(b), xr, xi);
+    dit8<false>(xr, xi, twA);   // lh 9
+    // natural order {b + 512 j}: straight to the ring (the Re planes only, as stft_pair_kernel)
+    double* o0 = a.fo + row0 * kN;
+    double* o1 = a.fo + row1 * kN;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        o0[b + kT * j] = xr[j];
+        if (two) o1[b + kT * j] = xi[j];
+    }
+}
+
 struct OlaArgs {
     const double* fo;   // planar ring (Re plane, then Im plane of R*N)
     const double* win;
@@ -770,7 +1102,17 @@ void launch_pairs(hz_stft* h, const StftArgs& a, long nf) {
                                   (int)frame_lds(kMaxN));
         attr = true;
     }
-    if (frame_rmax(h->N) == 3)
+    static const bool generic = std::getenv("HZ_STFT_GENERIC_PAIR") != nullptr;   // (A/B measurements)
+    if (h->N == p4::kN && !generic) {
+        static bool attr4 = false;
+        if (!attr4) {
+            (void)hipFuncSetAttribute((const void*)stft_pair4096_kernel<PROC>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)p4::lds_bytes());
+            attr4 = true;
+        }
+        hipLaunchKernelGGL((stft_pair4096_kernel<PROC>), dim3((unsigned)((nf + 1) / 2)), dim3(p4::kT),
+                           p4::lds_bytes(), h->stream, a, nf);
+    } else if (frame_rmax(h->N) == 3)
         hipLaunchKernelGGL((stft_pair_kernel<PROC, 3>), dim3((unsigned)((nf + 1) / 2)), dim3(frame_threads(h->N)),
                            frame_lds(h->N), h->stream, a, nf);
     else
@@ -865,6 +1207,9 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
     {
         const long f_hi = f_lo + nf;   // (unsharded: host-processor frames are f_lo .. f_hi - 1)
         a.f_lo = f_lo;
+        a.i0 = (int)(f_lo % (2L * h->laps));
+        a.u0 = (f_lo / (2L * h->laps)) * (2L * N - 1) - a.T0 + (N - 1);
+        a.r0 = (int)(f_lo % h->R);
         // frames start in increasing order: the first one decides whether any reads an Im part
         a.hi = (nf > 0 && frame_start(f_lo, h->laps, h->stride, N) <= h->last_cplx) ? hc + (N - 1) : nullptr;
         if (nf > 0) {
@@ -987,14 +1332,26 @@ int hz_stft_create(int N, int laps, int window, int proc, double p0, double p1, 
     const std::vector<double2> tw = twiddles(N);
     bool ok = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess;
     ok = ok && hipMalloc(&h->d_win, sizeof(double) * N) == hipSuccess;
-    ok = ok && hipMalloc(&h->d_tw, sizeof(double2) * (N / 2)) == hipSuccess;
+    // N = 4096: the specialised pair kernel's pass tables after the N/2 table (p4::kTwLen)
+    std::vector<double2> twx = tw;
+    if (N == p4::kN) {
+        twx.resize(N / 2 + p4::kTwLen);
+        for (int i = 0; i < p4::kTwLen; ++i) {
+            int k, p, sh;
+            if (i < p4::kTwB) k = i / 512, p = i % 512, sh = k;
+            else if (i < p4::kTwC) k = (i - p4::kTwB) / 64, p = (i - p4::kTwB) % 64, sh = 3 + k;
+            else k = (i - p4::kTwC) / 8, p = (i - p4::kTwC) % 8, sh = 6 + k;
+            twx[N / 2 + i] = tw[p << sh];
+        }
+    }
+    ok = ok && hipMalloc(&h->d_tw, sizeof(double2) * twx.size()) == hipSuccess;
     ok = ok && hipMalloc(&h->d_fo, sizeof(double2) * (size_t)h->R * N) == hipSuccess;
     for (double*& p : h->d_hist) {
         ok = ok && hipMalloc(&p, 2 * sizeof(double) * (N - 1)) == hipSuccess;
         ok = ok && hipMemset(p, 0, 2 * sizeof(double) * (N - 1)) == hipSuccess;
     }
     ok = ok && hipMemcpy(h->d_win, win.data(), sizeof(double) * N, hipMemcpyHostToDevice) == hipSuccess;
-    ok = ok && hipMemcpy(h->d_tw, tw.data(), sizeof(double2) * (N / 2), hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMemcpy(h->d_tw, twx.data(), sizeof(double2) * twx.size(), hipMemcpyHostToDevice) == hipSuccess;
     ok = ok && hipMemset(h->d_fo, 0, sizeof(double2) * (size_t)h->R * N) == hipSuccess;
     if (!ok) {
         hz::set_error("hz_stft_create: device allocation failed");
