@@ -1,7 +1,10 @@
 """GPU parity of the stationary Filterbank engine (huygens_amd/csrc/hz_fb_resp.hip).
 
 Once a converged bank (pre = pin, gain = gin) has kept its coefficients for K samples -- K its
-horizon, ||M^K|| < 2^-64 for every band -- long calls run as ONE partitioned FFT convolution of
+horizon, ||M^K||_inf < 2^-53 for every band, rounded up to a multiple of 8192 (49,152 samples at
+C2; inputs older than K reach an output below 2^-53 of their own scale, the bound
+tests/test_c2_pinned_gpu.py::test_impulse_then_silence_horizon_bound asserts as 2^-50 of the
+peak) -- long calls run as ONE partitioned FFT convolution of
 the input with the bank response h = sum_n gin_n r_n (src/filterbank.h:130,178-179 summed over
 bands), and the band states at the call end are the zero-start response of the last K inputs.
 Every test drives the GPU object and the CPU restatement (oracle/hz_oracle.c) through the same
