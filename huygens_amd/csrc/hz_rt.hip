@@ -348,6 +348,7 @@ struct Server {
     long long* d_ctl = nullptr;
     long long seq = 0, epoch = 0, requests = 0, launches = 0;
     bool active = false;
+    bool broken = false;         // a request went unanswered: later calls fail (no double service)
     double* pay = nullptr;       // pinned payload / result
     size_t pay_cap = 0;
     double* res = nullptr;
@@ -467,6 +468,10 @@ int call(Server* s, int op, const void* args, size_t bytes, int groups, double* 
         hz::set_error("hz_rt::call: op arguments %zu bytes, %d workgroups", bytes, groups);
         return HZ_E_INVALID;
     }
+    if (s->broken) {
+        hz::set_error("hz_rt: the per-sample server stopped answering earlier; per-sample calls are off");
+        return HZ_E_HIP;
+    }
     if (!s->active || srv_left(s)) {
         s->active = false;
         HZ_TRY(srv_launch(s));
@@ -488,12 +493,16 @@ int call(Server* s, int op, const void* args, size_t bytes, int groups, double* 
             // the instance left (idle) as the request arrived: the workgroups that had not served it
             // serve it after the relaunch (each resumes from its own response line)
             if (relaunched++ > 3) {
+                s->broken = true;
                 hz::set_error("hz_rt: the per-sample server left repeatedly without serving");
                 return HZ_E_HIP;
             }
             HZ_TRY(srv_launch(s));
         }
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+            // the request stays posted: a late answer would advance a state the caller was told
+            // did not move, so no later request may follow it
+            s->broken = true;
             hz::set_error("hz_rt: the per-sample server did not answer within 5 s");
             return HZ_E_HIP;
         }

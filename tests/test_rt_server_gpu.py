@@ -198,3 +198,49 @@ def test_setters_from_another_thread(gpu_lib, tmp_path):
     steady = lat[200:] * 1e-3
     print(f"{len(log)} setters; per-sample latency: median {np.median(steady):.2f} us, p99 "
           f"{np.percentile(steady, 99):.2f} us, worst {steady.max():.2f} us")
+
+
+def test_idle_exit_races(gpu_lib):
+    """The server leaving on its idle timer while requests arrive: with a 20 us idle
+    time it exits between many samples, some requests land while an instance is leaving; every
+    workgroup must still serve every request exactly once -- Filterbank and Delay outputs equal
+    the restatement sample by sample and many relaunches happened."""
+    import os
+    import time as _t
+    from huygens_amd import Delay, Filterbank, rt_info
+    from oracle import OracleFilterbank
+    from oracle_delay import OracleDelaybank
+    fwd, back = resonant_coefficients(96, 0.99, 1.0)
+    g, o = Filterbank(2, 96), OracleFilterbank(2, 96)
+    for fb in (g, o):
+        for n in range(96):
+            fb.coefficients(n, fwd[n], back[n])
+        fb.boost(np.ones(96))
+        fb.open()
+    d = Delay(4, 3000)
+    od = OracleDelaybank(1, 4, 3000)
+    d.coefficients([(0, 1.0), (17, 0.5)], [(40, 0.3), (1500, 0.2)])
+    od.coefficients(0, [(0, 1.0), (17, 0.5)], [(40, 0.3), (1500, 0.2)])
+    x = white_noise_f32(1500, seed=21)
+    launches0 = rt_info(0)[1]
+    os.environ["HZ_RT_IDLE_US"] = "20"
+    try:
+        rng = np.random.default_rng(3)
+        yg, yo, dg = [], [], []
+        for t, v in enumerate(x):
+            pause = rng.uniform(0.0, 60e-6)   # around the idle time: some requests meet a leaving instance
+            t0 = _t.perf_counter()
+            while _t.perf_counter() - t0 < pause:
+                pass
+            yg.append(g(v)); g.tick()
+            yo.append(o(v)); o.tick()
+            dg.append(d(v))
+        yd = od.process(np.asarray(x, dtype=np.float64))[0]
+    finally:
+        del os.environ["HZ_RT_IDLE_US"]
+    yg, yo = np.array(yg), np.array(yo)
+    assert np.max(np.abs(yg - yo)) <= 1e-11 * np.max(np.abs(yo))
+    assert np.array_equal(np.array(dg), yd)
+    relaunches = rt_info(0)[1] - launches0
+    print(f"relaunches: {relaunches}")
+    assert relaunches > 50
