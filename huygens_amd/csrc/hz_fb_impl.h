@@ -102,6 +102,10 @@ struct hz_fb {
     int target_groups = 256;  // workgroups wanted per launch (CU count)
     double *d_in = nullptr, *d_out = nullptr;
     size_t io_cap = 0;       // doubles
+    // host-buffer calls that take the streaming engine: pinned, device-mapped staging the kernel
+    // reads and writes directly ([kStreamBlock] in, then [kStreamBlock] out)
+    double* pin_io = nullptr;   // + 128 completion flags (long long) after the in/out blocks
+    long long pin_seq = 0;
     std::vector<double> h_rec;
     hipStream_t stream = nullptr;
     bool own_stream = false;
@@ -211,6 +215,8 @@ struct hz_fb {
             double* d_tw = nullptr;      // twiddles (W_64, W_32, W_2048)
             long pend = 0;               // streamed samples not yet applied to the smoothers / x history
             long calls = 0;
+            long long* flags_dev = nullptr;   // completion flags of a host-buffer call (hz_fb_process)
+            long long flags_seq = 0;
         } st;
     } resp;
     // per-sample path (hz_fb_rt.hip): OP_FB requests to the device's per-sample server (hz_rt.hip)
@@ -284,6 +290,7 @@ int fb_resp_build(hz_fb* h);   // + h, its spectra and the band-state operands f
 bool fb_stream_trackable(hz_fb* h, long n, bool conv);   // a call the ring keeps the history of
 bool fb_stream_eligible(hz_fb* h, long n, bool conv);    // ... and that streams (history >= K)
 int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n);
+int fb_stream_workgroups();   // workgroups of one streaming launch (completion flags)
 int fb_stream_track(hz_fb* h, const double* d_in, long n, bool conv);   // a short per-band call
 int fb_stream_materialize(hz_fb* h);   // band states, smoothers, x history from the ring
 int fb_stream_to_hist(hz_fb* h);       // the ring's history back to resp.d_hist (long calls)

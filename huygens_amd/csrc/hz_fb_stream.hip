@@ -153,7 +153,21 @@ struct StreamArgs {
     double2* Cout;        // [33][32] ... of the next block's tail
     const double2* Rin;   // [33][32] R_{b+1} = sum_{p >= 3} H_p Z_{b+1-p} (previous launch)
     double2* Rout;        // [33][32] R_{b+2}
+    // host-buffer calls (hz_fb_process): every workgroup posts `seq` to flags[blockIdx] in pinned
+    // host memory once its reads of x and writes of out are done, so the host returns without a
+    // stream synchronisation (null: device-buffer calls)
+    long long* flags;
+    long long seq;
 };
+
+// all of this workgroup's stores complete, then one system-scope release of the flag
+__device__ __forceinline__ void post_done(const StreamArgs& a) {
+    if (!a.flags) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(a.flags + blockIdx.x, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __device__ __forceinline__ int ring_slot(int head, int back, int Q) {
     int s = head - back;
@@ -277,6 +291,7 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
         }
         __syncthreads();
         col_inverse_store(s, ct, tcol, a.Cout + c * 32);
+        post_done(a);
     } else if (blk < 2 * kCols) {
         // ---------------- MAC column: R_{b+2}
         ColLds& s = u.col;
@@ -295,6 +310,7 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
         if (l < 32) s.m[w][j] = r;
         __syncthreads();
         if (t < 32) a.Rout[c * 32 + t] = cadd(cadd(s.m[0][t], s.m[1][t]), cadd(s.m[2][t], s.m[3][t]));
+        post_done(a);
     } else {
         // ---------------- 64 outputs: head + tail
         OutLds& s = u.out;
@@ -376,6 +392,7 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
             const double tail = (s.tpart[0][t] + s.tpart[1][t]) + (s.tpart[2][t] + s.tpart[3][t]);
             a.out[t0 + t] = y + tail;
         }
+        post_done(a);
     }
 }
 
@@ -522,12 +539,16 @@ StreamArgs stream_args(hz_fb* h) {
     a.Cout = C + (b ^ 1) * col;
     a.Rin = Rb + (b ^ 1) * col;
     a.Rout = Rb + b * col;
+    a.flags = nullptr;
+    a.seq = 0;
     return a;
 }
 
 }  // namespace
 
 namespace hz_fbi {
+
+int fb_stream_workgroups() { return 2 * kCols + kSP / 64; }
 
 bool fb_stream_trackable(hz_fb* h, long n, bool conv) {
     hz_fb::Resp& R = h->resp;
@@ -568,6 +589,8 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
     StreamArgs a = stream_args(h);
     a.x = d_in;
     a.out = d_out;
+    a.flags = S.flags_dev;   // set by hz_fb_process for its zero-copy call only
+    a.seq = S.flags_seq;
     hipEvent_t* e = nullptr;
     if (h->prof) {
         HZ_TRY(fb_prof_events(h, &e));
