@@ -28,6 +28,7 @@
 //
 // Layout in HBM: ring [C] doubles; grains [G] x 64 B per block (uploaded once per call).
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <cmath>
 #include <cstring>
@@ -59,6 +60,7 @@ struct GranArgs {
     unsigned size, o0;    // Buffer size and origin at time T0
     unsigned long fm;     // fastmod multiplier for `size`: 2^64 / size rounded up (0 for size 1)
     unsigned wrap1;       // (2^32 - 1) % size: the second tap's slot when the first index is 0 mod 2^32
+    int fastcos;          // cos_0_2pi for the window (HZ_GRAN_LIBCOS=1: the library cos, A/B)
 };
 
 // x mod size for any uint32 x, without a divide (Lemire, Kaser & Kurz 2019, "fastmod")
@@ -129,7 +131,9 @@ __global__ __launch_bounds__(kThreads) void gran_kernel(GranArgs a) {
             } else {
                 phase = tk / g.sizes;
             }
-            const double term = g.gains * src * (0.5 * (1 - cos(2 * hz::kPI * phase)));   // wave.h:148
+            const double arg = 2 * hz::kPI * phase;
+            const double cv = hz_rt::hann_cos(arg, a.fastcos != 0);
+            const double term = g.gains * src * (0.5 * (1 - cv));   // wave.h:148
             if (act[u]) out += term;
         }
     }
@@ -322,6 +326,8 @@ int gran_run(hz_gran* h, const double* d_in, double* d_out, long n, const hz_gra
         a.o0 = (unsigned)(T0 % (long)h->size);
         a.fm = h->size == 1u ? 0ul : ~0ul / h->size + 1ul;
         a.wrap1 = 0xffffffffu % h->size;
+        static const bool libcos = std::getenv("HZ_GRAN_LIBCOS") != nullptr;
+        a.fastcos = libcos ? 0 : 1;
         hipEvent_t* e = nullptr;
         if (h->prof) {
             if (h->ev_used + 2 > h->ev.size())

@@ -33,6 +33,47 @@ struct alignas(16) Grain {
 };
 static_assert(sizeof(Grain) == 64, "grain record is one 64 B line");
 
+// cos(x) for 0 <= x <= 2 PI + 1e-9 (the hann argument 2 PI phase, phase in [0, 1]): k = rint(x 2/pi)
+// in 0..4, r = x - k pi/2 in a two-part Cody-Waite split (k pio2_1 exact: 33-bit head), then
+// fdlibm's __kernel_sin / __kernel_cos polynomials on |r| <= pi/4 (< 1 ulp each) -- against the
+// library cos's general argument reduction
+__device__ __forceinline__ double cos_0_2pi(double x) {
+    constexpr double kInvPio2 = 6.36619772367581382433e-01;
+    constexpr double kPio2_1 = 1.57079632673412561417e+00, kPio2_1t = 6.07710050650619224932e-11;
+    const double kf = __builtin_rint(x * kInvPio2);
+    const int k = (int)kf;
+    const double r = (x - kf * kPio2_1) - kf * kPio2_1t;
+    const double z = r * r;
+    // __kernel_sin(r): r + r^3 (S1 + z (S2 + ...))
+    double ps = 1.58969099521155010221e-10;
+    ps = __builtin_fma(ps, z, -2.50507602534068634195e-08);
+    ps = __builtin_fma(ps, z, 2.75573137070700676789e-06);
+    ps = __builtin_fma(ps, z, -1.98412698298579493134e-04);
+    ps = __builtin_fma(ps, z, 8.33333333332248946124e-03);
+    ps = __builtin_fma(ps, z, -1.66666666666666324348e-01);
+    const double sn = __builtin_fma(r * z, ps, r);
+    // __kernel_cos(r): 1 - z/2 + z^2 (C1 + z (C2 + ...)), the 1 - z/2 part compensated
+    double pc = -1.13596475577881948265e-11;
+    pc = __builtin_fma(pc, z, 2.08757232129817482790e-09);
+    pc = __builtin_fma(pc, z, -2.75573143513906633035e-07);
+    pc = __builtin_fma(pc, z, 2.48015872894767294178e-05);
+    pc = __builtin_fma(pc, z, -1.38888888888741095749e-03);
+    pc = __builtin_fma(pc, z, 4.16666666666666019037e-02);
+    const double hz_ = 0.5 * z, w = 1.0 - hz_;
+    const double cs = w + (((1.0 - w) - hz_) + z * z * pc);
+    switch (k & 3) {
+    case 0: return cs;
+    case 1: return -sn;
+    case 2: return -cs;
+    default: return sn;
+    }
+}
+
+// the Granulator's window term's cosine, block kernel and per-sample server alike (bit-identical)
+__device__ __forceinline__ double hann_cos(double arg, bool fast) {
+    return (fast && arg >= 0.0 && arg <= 6.2831853072) ? cos_0_2pi(arg) : cos(arg);
+}
+
 // ---- op arguments (copied into the request line; <= kArgWords 8-byte words) ------------------
 // Filterbank sample: ring rows R [N][O+1] in ring order (R[0..O-1] = y[t-1 .. t-O], R[O] = the
 // row at origin), smoothers pg [N][2], coefficients [N][2O+1], targets pin / gin [N].

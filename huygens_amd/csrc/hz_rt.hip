@@ -235,7 +235,7 @@ __device__ double op_gran(const GranArgs& a, SrvLds& s) {
             } else {
                 phase = tk / gr.sizes;
             }
-            term = gr.gains * src * (0.5 * (1 - cos(2 * hz::kPI * phase)));   // wave.h:148
+            term = gr.gains * src * (0.5 * (1 - hann_cos(2 * hz::kPI * phase, true)));   // wave.h:148
         }
         s.term[e] = term;
     }
