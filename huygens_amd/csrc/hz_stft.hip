@@ -484,19 +484,24 @@ __device__ __forceinline__ void cmul_fma(double& r, double& i, double2 w, bool c
     i = ni;
 }
 
-// stage twiddles per pass (host-built after the N/2 table, hz_stft_create), contiguous in p:
-// A[k][p] = W^(p << k), p < 512 (forward lh 11, inverse lh 9 as A[2 - k]); B[k][p] = W^(p << (3 + k)),
-// p < 64 (lh 8 / 6); C[k][p] = W^(p << (6 + k)), p < 8 (lh 5 / 3); lh 2 / 0 have p = 0 (unit
-// twiddles, skipped).  A thread's nine twiddles (the inverse reuses the forward's) load once.
-constexpr int kTwA = 0, kTwB = 3 * 512, kTwC = kTwB + 3 * 64, kTwLen = kTwC + 3 * 8;
+// Twiddles once per element (an A/B alternative; the stage-wise form below is the default): a radix-8 DIF group {base + j d} (p its offset in the span) is the
+// 8-point DFT of its elements followed by W_N^(e r) on output j, r = bitrev3(j), e = p 2^(lg-1-lh);
+// the DIT group mirrors it (conj W_N^(e r) on input j, e = p 2^(lg-3-lh), then the butterflies).
+// The stage-by-stage form (hz::dif_regs / dit_regs) multiplied every stage's differences: 12
+// complex products per group and pass against 7 here.  Host-built tables after the N/2 table
+// (hz_stft_create), contiguous in p: A[r-1][p] = W^(p r), p < 512 (forward lh 11, inverse lh 9);
+// B[r-1][p] = W^(8 p r), p < 64 (lh 8 / 6); C[r-1][p] = W^(64 p r), p < 8 (lh 5 / 3); lh 2 / 0 have
+// p = 0 (no twiddles).  A thread's 21 twiddles load once.
+constexpr int kTwA = 0, kTwB = 7 * 512, kTwC = kTwB + 7 * 64, kTwLen = kTwC + 7 * 8;
+constexpr int kBr3[8] = {0, 4, 2, 6, 1, 5, 3, 7};
 
-// radix-8 DIF group (hz::dif_regs<3, true> stage order), twiddles tw[k * stride + p]
+// the stage-by-stage form (hz::dif_regs<3, true> order: stage k's differences times W^(e 2^k))
 template <bool UNIT>
-__device__ __forceinline__ void dif8(double (&xr)[8], double (&xi)[8], const double2 (&tw)[3]) {
+__device__ __forceinline__ void dif8s(double (&xr)[8], double (&xi)[8], const double2 (&tw)[7]) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int S = 8 >> (k + 1);
-        const double2 w = UNIT ? make_double2(1.0, 0.0) : tw[k];
+        const double2 w = tw[(1 << k) - 1];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             if (j & S) continue;
@@ -512,18 +517,66 @@ __device__ __forceinline__ void dif8(double (&xr)[8], double (&xi)[8], const dou
     }
 }
 
-// radix-8 DIT group (hz::dit_regs<3, true> stage order), conjugate twiddles tw[(2 - k) stride + p]
+// hz::dit_regs<3, true> order: stage k's second inputs times conj W^(e 2^(2-k))
 template <bool UNIT>
-__device__ __forceinline__ void dit8(double (&xr)[8], double (&xi)[8], const double2 (&tw)[3]) {
+__device__ __forceinline__ void dit8s(double (&xr)[8], double (&xi)[8], const double2 (&tw)[7]) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int S = 1 << k;
-        const double2 w = UNIT ? make_double2(1.0, 0.0) : tw[2 - k];
+        const double2 w = tw[(1 << (2 - k)) - 1];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             if (j & S) continue;
             double cr = xr[j + S], ci = xi[j + S];
             if (!UNIT) cmul_fma(cr, ci, w, true);
+            hz::mul_root16(cr, ci, (j & (S - 1)) << (3 - k), true);
+            const double ar = xr[j], ai = xi[j];
+            xr[j] = ar + cr;
+            xi[j] = ai + ci;
+            xr[j + S] = ar - cr;
+            xi[j + S] = ai - ci;
+        }
+    }
+}
+
+// radix-8 DIF group: butterflies with the pass-internal roots, then the output twiddles
+template <bool UNIT>
+__device__ __forceinline__ void dif8(double (&xr)[8], double (&xi)[8], const double2 (&tw)[7]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int S = 8 >> (k + 1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j & S) continue;
+            const double ar = xr[j], ai = xi[j], cr = xr[j + S], ci = xi[j + S];
+            double dr = ar - cr, di = ai - ci;
+            hz::mul_root16(dr, di, (j & (S - 1)) << (1 + k), false);
+            xr[j] = ar + cr;
+            xi[j] = ai + ci;
+            xr[j + S] = dr;
+            xi[j + S] = di;
+        }
+    }
+    if (!UNIT) {
+#pragma unroll
+        for (int j = 1; j < 8; ++j) cmul_fma(xr[j], xi[j], tw[kBr3[j] - 1], false);
+    }
+}
+
+// radix-8 DIT group: the input twiddles (conjugate), then the butterflies with the internal roots
+template <bool UNIT>
+__device__ __forceinline__ void dit8(double (&xr)[8], double (&xi)[8], const double2 (&tw)[7]) {
+    if (!UNIT) {
+#pragma unroll
+        for (int j = 1; j < 8; ++j) cmul_fma(xr[j], xi[j], tw[kBr3[j] - 1], true);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int S = 1 << k;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j & S) continue;
+            double cr = xr[j + S], ci = xi[j + S];
             hz::mul_root16(cr, ci, (j & (S - 1)) << (3 - k), true);
             const double ar = xr[j], ai = xi[j];
             xr[j] = ar + cr;
@@ -690,7 +743,7 @@ __device__ __forceinline__ void gate(double2* zf, double p0, double p1, double* 
 }
 }  // namespace p4
 
-template <int PROC>
+template <int PROC, bool ONCE>
 __global__ __launch_bounds__(p4::kT) void stft_pair4096_kernel(StftArgs a, long nf) {
 #pragma clang fp contract(off)
     using namespace p4;
@@ -699,12 +752,12 @@ __global__ __launch_bounds__(p4::kT) void stft_pair4096_kernel(StftArgs a, long 
     double* scratch = lds + 2 * kN;
     const int b = threadIdx.x;
     const double2* ptw = a.tw + kH;   // the pass tables
-    double2 twA[3], twB[3], twC[3];
+    double2 twA[7], twB[7], twC[7];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        twA[k] = ptw[kTwA + 512 * k + b];
-        twB[k] = ptw[kTwB + 64 * k + (b & 63)];
-        twC[k] = ptw[kTwC + 8 * k + (b & 7)];
+    for (int r = 0; r < 7; ++r) {
+        twA[r] = ptw[kTwA + 512 * r + b];
+        twB[r] = ptw[kTwB + 64 * r + (b & 63)];
+        twC[r] = ptw[kTwC + 8 * r + (b & 7)];
     }
     const int pl = frame_of_block(blockIdx.x, gridDim.x);   // frame pair within the launch
     const bool two = 2L * pl + 1 < nf;
@@ -742,37 +795,37 @@ __global__ __launch_bounds__(p4::kT) void stft_pair4096_kernel(StftArgs a, long 
             xi[j] = w[j] * v1[j];
         }
     }
-    dif8<false>(xr, xi, twA);   // lh 11
+    if constexpr (ONCE) dif8<false>(xr, xi, twA); else dif8s<false>(xr, xi, twA);   // lh 11
     lds_put<512>(z, dif_base<9>(b), xr, xi);
     __syncthreads();
     lds_get<64>(z, dif_base<6>(b), xr, xi);
-    dif8<false>(xr, xi, twB);   // lh 8
+    if constexpr (ONCE) dif8<false>(xr, xi, twB); else dif8s<false>(xr, xi, twB);   // lh 8
     lds_put<64>(z, dif_base<6>(b), xr, xi);
     wave_sync();
     lds_get<8>(z, dif_base<3>(b), xr, xi);
-    dif8<false>(xr, xi, twC);   // lh 5
+    if constexpr (ONCE) dif8<false>(xr, xi, twC); else dif8s<false>(xr, xi, twC);   // lh 5
     lds_put<8>(z, dif_base<3>(b), xr, xi);
     wave_sync();
     lds_get<1>(z, dif_base<0>(b), xr, xi);
-    dif8<true>(xr, xi, twC);   // lh 2
+    if constexpr (ONCE) dif8<true>(xr, xi, twC); else dif8s<true>(xr, xi, twC);   // lh 2
     lds_put<1>(z, dif_base<0>(b), xr, xi);
     __syncthreads();
     gate<PROC>(z, a.p0, a.p1, scratch);
     __syncthreads();
     lds_get<1>(z, dit_base<0>(b), xr, xi);
-    dit8<true>(xr, xi, twC);   // lh 0
+    if constexpr (ONCE) dit8<true>(xr, xi, twC); else dit8s<true>(xr, xi, twC);   // lh 0
     lds_put<1>(z, dit_base<0>(b), xr, xi);
     wave_sync();
     lds_get<8>(z, dit_base<3>(b), xr, xi);
-    dit8<false>(xr, xi, twC);   // lh 3
+    if constexpr (ONCE) dit8<false>(xr, xi, twC); else dit8s<false>(xr, xi, twC);   // lh 3
     lds_put<8>(z, dit_base<3>(b), xr, xi);
     wave_sync();
     lds_get<64>(z, dit_base<6>(b), xr, xi);
-    dit8<false>(xr, xi, twB);   // lh 6
+    if constexpr (ONCE) dit8<false>(xr, xi, twB); else dit8s<false>(xr, xi, twB);   // lh 6
     lds_put<64>(z, dit_base<6>(b), xr, xi);
     __syncthreads();
     lds_get<512>(z, dit_base<9>(b), xr, xi);
-    dit8<false>(xr, xi, twA);   // lh 9
+    if constexpr (ONCE) dit8<false>(xr, xi, twA); else dit8s<false>(xr, xi, twA);   // lh 9
     // natural order {b + 512 j}: straight to the ring (the Re planes only, as stft_pair_kernel)
     double* o0 = a.fo + row0 * kN;
     double* o1 = a.fo + row1 * kN;
@@ -1103,15 +1156,23 @@ void launch_pairs(hz_stft* h, const StftArgs& a, long nf) {
         attr = true;
     }
     static const bool generic = std::getenv("HZ_STFT_GENERIC_PAIR") != nullptr;   // (A/B measurements)
+    // twiddles once per element (7 products per group and pass) measured slower on one box than the
+    // stage-wise form (12): 15.1 vs 14.6 us per C4 step, alternating runs (profiles/r4/rows/c4/ab.log);
+    // HZ_STFT_TWIDDLE_ONCE=1 selects it for such A/B runs
+    static const bool stagewise = std::getenv("HZ_STFT_TWIDDLE_ONCE") == nullptr;
     if (h->N == p4::kN && !generic) {
         static bool attr4 = false;
         if (!attr4) {
-            (void)hipFuncSetAttribute((const void*)stft_pair4096_kernel<PROC>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)p4::lds_bytes());
+            for (const void* k : {(const void*)stft_pair4096_kernel<PROC, true>, (const void*)stft_pair4096_kernel<PROC, false>})
+                (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p4::lds_bytes());
             attr4 = true;
         }
-        hipLaunchKernelGGL((stft_pair4096_kernel<PROC>), dim3((unsigned)((nf + 1) / 2)), dim3(p4::kT),
-                           p4::lds_bytes(), h->stream, a, nf);
+        if (stagewise)
+            hipLaunchKernelGGL((stft_pair4096_kernel<PROC, false>), dim3((unsigned)((nf + 1) / 2)), dim3(p4::kT),
+                               p4::lds_bytes(), h->stream, a, nf);
+        else
+            hipLaunchKernelGGL((stft_pair4096_kernel<PROC, true>), dim3((unsigned)((nf + 1) / 2)), dim3(p4::kT),
+                               p4::lds_bytes(), h->stream, a, nf);
     } else if (frame_rmax(h->N) == 3)
         hipLaunchKernelGGL((stft_pair_kernel<PROC, 3>), dim3((unsigned)((nf + 1) / 2)), dim3(frame_threads(h->N)),
                            frame_lds(h->N), h->stream, a, nf);
@@ -1334,14 +1395,17 @@ int hz_stft_create(int N, int laps, int window, int proc, double p0, double p1, 
     ok = ok && hipMalloc(&h->d_win, sizeof(double) * N) == hipSuccess;
     // N = 4096: the specialised pair kernel's pass tables after the N/2 table (p4::kTwLen)
     std::vector<double2> twx = tw;
-    if (N == p4::kN) {
+    if (N == p4::kN) {   // W^((p << s) r) mod N, r = 1..7, in long double
         twx.resize(N / 2 + p4::kTwLen);
+        const long double pi = acosl(-1.0L);
         for (int i = 0; i < p4::kTwLen; ++i) {
-            int k, p, sh;
-            if (i < p4::kTwB) k = i / 512, p = i % 512, sh = k;
-            else if (i < p4::kTwC) k = (i - p4::kTwB) / 64, p = (i - p4::kTwB) % 64, sh = 3 + k;
-            else k = (i - p4::kTwC) / 8, p = (i - p4::kTwC) % 8, sh = 6 + k;
-            twx[N / 2 + i] = tw[p << sh];
+            int r, p, sh;
+            if (i < p4::kTwB) r = i / 512 + 1, p = i % 512, sh = 0;
+            else if (i < p4::kTwC) r = (i - p4::kTwB) / 64 + 1, p = (i - p4::kTwB) % 64, sh = 3;
+            else r = (i - p4::kTwC) / 8 + 1, p = (i - p4::kTwC) % 8, sh = 6;
+            const long k = ((long)(p << sh) * r) % N;
+            const long double ang = -2.0L * pi * k / N;
+            twx[N / 2 + i] = make_double2((double)cosl(ang), (double)sinl(ang));
         }
     }
     ok = ok && hipMalloc(&h->d_tw, sizeof(double2) * twx.size()) == hipSuccess;
