@@ -117,8 +117,8 @@ struct GranArgs {
 
 constexpr int kArgWords = 30;
 struct alignas(64) Req {
-    long long req;          // request number, written last (release)
-    int op, groups;         // op; workgroups that take part (the others only acknowledge)
+    long long req;          // request number << 4 | participating workgroups, written last (release)
+    int op, groups;         // op; workgroups that take part (the others skip the request)
     long long w[kArgWords]; // op arguments
 };
 static_assert(sizeof(FbArgs) <= sizeof(long long) * kArgWords && sizeof(DlyArgs) <= sizeof(long long) * kArgWords &&
@@ -139,7 +139,7 @@ Server* server(int device);
 double* payload(Server* s, size_t doubles);   // grows (only between requests)
 double* result(Server* s, size_t doubles);
 const void* dev(Server* s, const void* host_ptr);
-// one request: args copied into the line, every workgroup acknowledges; -> sum of the taking-part
+// one request: args copied into the line, the participating workgroups answer; -> sum of the taking-part
 // workgroups' partials (y, y2) in workgroup order.  Serialised per device (the caller holds
 // lock(s) across a multi-request sequence when the order matters).
 int call(Server* s, int op, const void* args, size_t bytes, int groups, double* y, double* y2 = nullptr);

@@ -11,9 +11,9 @@
 // response) and starts with an acquire (the poll), and the host orders block work before and
 // after requests by stream synchronisation.
 //
-// Exactly-once service: the host writes a request line only after every workgroup acknowledged
-// the previous one; a workgroup resumes from its own last acknowledged request when the kernel is
-// relaunched after an idle exit (workgroup 0 decides it after kIdleNs without a request and the
+// Exactly-once service: the host writes a request line only after every participating workgroup
+// (named in the request word itself) acknowledged the previous one; a workgroup resumes from its
+// own last acknowledged request when the kernel is relaunched after an idle exit (workgroup 0 decides it after kIdleNs without a request and the
 // others follow through a device-memory flag), so a request is served once by each workgroup even
 // when it arrives while the instance leaves.
 #include <chrono>
@@ -59,6 +59,7 @@ __device__ __forceinline__ void st_rel(long long* p, long long v) {
 struct SrvLds {
     long long w[kArgWords + 1];
     long long req;
+    int grp;
     double part[kThreads / 64];
     // OP_GRAN (one workgroup): the handle's grain list and this sample's terms
     long long gkey, gver;
@@ -261,8 +262,14 @@ __global__ __launch_bounds__(kThreads) void rt_server_kernel(ServerArgs a) {
     for (;;) {
         if (tid == 0) {
             long long r;
+            int grp = 0;
             for (;;) {
-                r = ld_acq(&a.req->req);
+                // the request word carries the participating workgroups (low 4 bits): a workgroup
+                // decides from this one 64-bit load, and only participants -- whom the host waits
+                // for before it rewrites the line -- read the arguments
+                const long long wd = ld_acq(&a.req->req);
+                r = wd >> 4;
+                grp = (int)(wd & 15);
                 if (r != seen) break;
                 if (g == 0) {
                     if (__builtin_amdgcn_s_memrealtime() - last > a.idle) {
@@ -277,13 +284,20 @@ __global__ __launch_bounds__(kThreads) void rt_server_kernel(ServerArgs a) {
                 __builtin_amdgcn_s_sleep(1);
             }
             s.req = r;
+            s.grp = grp;
         }
         __syncthreads();
         const long long r = s.req;
         if (r == kQuit) break;
+        const int groups = s.grp;
+        if (g >= groups) {   // not taking part: no answer (the host waits for the participants only)
+            seen = r;
+            last = __builtin_amdgcn_s_memrealtime();
+            continue;
+        }
         if (tid <= kArgWords) s.w[tid] = ld_sys((const long long*)&a.req->op + tid);   // op|groups, args
         __syncthreads();
-        const int op = (int)(unsigned)(s.w[0] & 0xffffffffu), groups = (int)(s.w[0] >> 32);
+        const int op = (int)(unsigned)(s.w[0] & 0xffffffffu);
         if (op == OP_STOP) {
             seen = r;
             break;
@@ -405,8 +419,8 @@ void srv_shutdown() {
         std::lock_guard<std::recursive_mutex> lk(s->mu);
         Req* q = s->req();
         q->op = OP_STOP;
-        q->groups = 0;
-        __atomic_store_n(&q->req, ++s->seq, __ATOMIC_RELEASE);
+        q->groups = kGroups;
+        __atomic_store_n(&q->req, (++s->seq << 4) | kGroups, __ATOMIC_RELEASE);
         const auto t0 = std::chrono::steady_clock::now();
         while (!srv_left(s) && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
         }
@@ -482,12 +496,12 @@ int call(Server* s, int op, const void* args, size_t bytes, int groups, double* 
     q->groups = groups;
     std::memcpy(q->w, args, bytes);
     const long long want = ++s->seq;
-    __atomic_store_n(&q->req, want, __ATOMIC_RELEASE);
+    __atomic_store_n(&q->req, (want << 4) | groups, __ATOMIC_RELEASE);
     const auto t0 = std::chrono::steady_clock::now();
     int relaunched = 0;
     for (;;) {
         bool all = true;
-        for (int g = 0; g < kGroups && all; ++g) all = host_load(&slot[g].done) >= want;
+        for (int g = 0; g < groups && all; ++g) all = host_load(&slot[g].done) >= want;
         if (all) break;
         if (srv_left(s)) {
             // the instance left (idle) as the request arrived: the workgroups that had not served it
