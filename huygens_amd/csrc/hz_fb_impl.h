@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -136,7 +137,8 @@ struct hz_fb {
     static constexpr int kLtiSets = 4;   // chunks 16, 32, 64, 128
     LtiRecSet lti_set[kLtiSets];
     std::vector<double> pg_host;     // host mirror of the smoother state [N][2] (pre, gain)
-    long mirror_pending = 0;         // samples processed since pg_host was last brought up to date
+    long mirror_clock = 0;           // samples processed (the closed form is applied lazily)
+    std::vector<long> mirror_at;     // [N] mirror_clock at which pg_host[b] was last brought current
     bool converged = false;          // pg_host at the targets; cleared by every setter
     // LTI launches are split in chunks whose cross-group reduce runs on a second stream,
     // overlapped with the next chunk's mix kernel (double-buffered partial slab)
@@ -230,6 +232,12 @@ struct hz_fb {
         int cached_dist = 0;
         double xr[kMaxOrderRt + 1] = {};   // input ring (ring order), host mirror
         long pg_gen = 0, coef_gen = 0;     // generations the server's arrays hold
+        // one-band target setters since the server's copy (generation sp_base .. sp_gen): the next
+        // sample sends (band, pin, gin) triples instead of both [N] arrays while the list covers
+        // every target change since (sp_base == pg_gen, sp_gen == the handle's pg_gen)
+        std::vector<int> dirty;
+        std::vector<unsigned char> mark;   // [N] band in `dirty`
+        long sp_base = 0, sp_gen = 0;
         double* pin1 = nullptr;      // pinned staging (x history, a cached sample)
         double* d_coef = nullptr;    // [N][2O+1] coefficients, then [N][O+1] ring rows
         size_t coef_cap = 0;
@@ -239,15 +247,63 @@ struct hz_fb {
 
 namespace hz_fbi {
 
-// a setter's hold on the handle (announced, so per-sample calls let it in: hz_fb::setter_wait)
-struct SetterLock {
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+// bounded spins before a blocking wait: a thread put to sleep on the mutex costs the other side a
+// scheduler wake-up (5-10 us) per hand-off, a quarter of a sample period at 48 kHz
+constexpr int kSpinSetter = 1 << 16;    // ~ a few ms of pause instructions
+constexpr int kSpinSample = 1 << 20;
+
+// the hold of a setter or any other entry point but operator() / tick() (SampleLock), announced
+// from before it locks until after it unlocks, so a per-sample call neither takes the lock ahead
+// of it (an audio thread spinning on the lock would otherwise starve a blocked waiter) nor blocks
+// behind it (hz_fb::setter_wait); it spins for the lock while a sample is being served
+struct HandleLock {
     hz_fb* h;
-    explicit SetterLock(hz_fb* h_) : h(h_) {
+    explicit HandleLock(hz_fb* h_) : h(h_) {
         h->setter_wait.fetch_add(1);
-        h->mu.lock();
+        int spin = 0;
+        while (!h->mu.try_lock()) {
+            if (++spin == kSpinSetter) {
+                h->mu.lock();
+                break;
+            }
+            cpu_relax();
+        }
+    }
+    ~HandleLock() {
+        h->mu.unlock();
         h->setter_wait.fetch_sub(1);
     }
-    ~SetterLock() { h->mu.unlock(); }
+};
+
+// a per-sample call's hold (operator() / tick()): announced setters go first (this sample sees
+// them) for at most kAnnounceWaitNs -- a setter thread descheduled between its announcement and
+// the lock must not stall the audio thread for a scheduler slice -- then the lock, spinning
+// rather than sleeping on the mutex
+constexpr long long kAnnounceWaitNs = 20000;
+struct SampleLock {
+    hz_fb* h;
+    explicit SampleLock(hz_fb* h_) : h(h_) {
+        if (h->setter_wait.load(std::memory_order_acquire) > 0) {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int spin = 1; h->setter_wait.load(std::memory_order_acquire) > 0; ++spin) {
+                if ((spin & 63) == 0 && std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                            std::chrono::steady_clock::now() - t0).count() > kAnnounceWaitNs)
+                    break;
+                cpu_relax();
+            }
+        }
+        int spin = 0;
+        while (!h->mu.try_lock()) {
+            if (++spin == kSpinSample) {
+                h->mu.lock();
+                break;
+            }
+            cpu_relax();
+        }
+    }
+    ~SampleLock() { h->mu.unlock(); }
 };
 
 // hz_filterbank.hip
@@ -255,6 +311,10 @@ int fb_set_lds_attr(const void* kernel);
 int fb_prof_events(hz_fb* h, hipEvent_t** e);
 void fb_mirror_advance(hz_fb* h, long len);  // O(1): the closed form is applied lazily
 void fb_mirror_sync(hz_fb* h);               // bring pg_host up to date (before a setter)
+void fb_mirror_sync_band(hz_fb* h, int l);   // band l only (before a one-band setter)
+// a target setter advances pg_gen: l = its local band, -1 = a band of another shard, kAllBands = all
+constexpr int kAllBands = -2;
+void fb_rt_target_setter(hz_fb* h, int l);
 int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n);
 int fb_upload_staged(hz_fb* h);              // staged setters -> device
 int fb_tv_materialize(hz_fb* h);             // pending stream row -> F/B (hz_fb_tv.hip)

@@ -58,6 +58,29 @@ namespace hz_fbi {
 
 bool fb_rt_supported(const hz_fb*) { return true; }   // the server loops over any number of bands
 
+// sparse reloads: at most this many triples (beyond it both arrays are cheaper to send)
+static size_t sparse_cap(int N) { return std::max<size_t>(16, (size_t)N / 8); }
+
+static void sparse_clear(hz_fb* h) {
+    hz_fb::Rt& T = h->rt;
+    for (int l : T.dirty) T.mark[l] = 0;
+    T.dirty.clear();
+    T.sp_base = T.sp_gen = h->pg_gen;
+}
+
+void fb_rt_target_setter(hz_fb* h, int l) {
+    hz_fb::Rt& T = h->rt;
+    const bool track = l != kAllBands && T.sp_gen == h->pg_gen;
+    ++h->pg_gen;
+    if (!track) return;
+    if (l >= 0 && !T.mark[l]) {
+        if (T.dirty.size() >= sparse_cap(h->N)) return;   // the list stops covering: both arrays
+        T.mark[l] = 1;
+        T.dirty.push_back(l);
+    }
+    T.sp_gen = h->pg_gen;
+}
+
 // the state into ring rows, the coefficients into the op's layout, the input ring to the host
 static int rt_enter(hz_fb* h) {
     hz_fb::Rt& T = h->rt;
@@ -99,6 +122,7 @@ static int rt_enter(hz_fb* h) {
     T.xr[O] = (O > 0 && spare) ? xo[O - 1] : 0.0;
     T.pg_gen = h->pg_gen;
     T.coef_gen = h->coef_gen;
+    sparse_clear(h);
     T.active = true;
     T.spare_known = h->spare_ok;
     // per-sample calls own the state from here; the stationary history no longer follows it
@@ -135,10 +159,13 @@ int fb_rt_stop(hz_fb* h) {
     return HZ_OK;
 }
 
+static int sample_locked(hz_fb* h, double x, int dist_id, double param, double* y);
+static void tick_locked(hz_fb* h);
+
 int fb_rt_resolve(hz_fb* h, double* y0) {
     if (!h->rt.computed) return 0;
-    HZ_TRY(hz_fb_sample(h, 0.0, h->dist_id, h->dist_param, y0));
-    HZ_TRY(hz_fb_sample_tick(h));
+    HZ_TRY(sample_locked(h, 0.0, h->dist_id, h->dist_param, y0));   // (the caller holds the handle)
+    tick_locked(h);
     HZ_TRY(fb_rt_stop(h));
     return 1;
 }
@@ -154,18 +181,8 @@ void fb_rt_free(hz_fb* h) {
     T.active = false;
 }
 
-}  // namespace hz_fbi
-
-extern "C" {
-
-int hz_fb_sample(hz_fb* h, double x, int dist_id, double param, double* y) {
-    if (!h || !y || dist_id < HZ_DIST_NONE || dist_id > HZ_DIST_LIMITER) {
-        hz::set_error("hz_fb_sample: invalid arguments");
-        return HZ_E_INVALID;
-    }
-    for (int spin = 0; h->setter_wait.load(std::memory_order_relaxed) > 0 && spin < (1 << 20); ++spin)
-        std::this_thread::yield();   // a setter from another thread goes first (the next sample sees it)
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+// operator() with the handle held (the entry point below, or a block call resolving a cached sample)
+static int sample_locked(hz_fb* h, double x, int dist_id, double param, double* y) {
     HZ_TRY_HIP(hipSetDevice(h->device));
     hz_fb::Rt& T = h->rt;
     const int O = h->order, N = h->N;
@@ -199,20 +216,34 @@ int hz_fb_sample(hz_fb* h, double x, int dist_id, double param, double* y) {
     a.gin = h->d_gin;
     a.reload = nullptr;
     a.reload_coef = nullptr;
+    a.sparse = nullptr;
+    a.nsparse = 0;
     std::lock_guard<std::recursive_mutex> slk(hz_rt::lock(srv));
     if (T.pg_gen != h->pg_gen || T.coef_gen != h->coef_gen) {
         // setters since the last sample: the new targets / coefficients ride in the payload and the
         // server writes them into the device arrays (block calls upload them again: dirty flags stay)
         const bool tg = T.pg_gen != h->pg_gen, cf = T.coef_gen != h->coef_gen;
-        double* p = hz_rt::payload(srv, (tg ? 2 * (size_t)N : 0) + (cf ? nc : 0));
+        // one-band setters only (the list covers every change since the server's copy): triples
+        const bool sparse = tg && T.sp_base == T.pg_gen && T.sp_gen == h->pg_gen;
+        const size_t nt = !tg ? 0 : sparse ? 3 * T.dirty.size() : 2 * (size_t)N;
+        double* p = hz_rt::payload(srv, std::max<size_t>(1, nt + (cf ? nc : 0)));
         if (!p) return HZ_E_ALLOC;
-        size_t at = 0;
-        if (tg) {
+        const size_t at = nt;
+        if (sparse) {
+            for (size_t j = 0; j < T.dirty.size(); ++j) {
+                const int l = T.dirty[j];
+                p[3 * j] = (double)l;
+                p[3 * j + 1] = h->pin[l];
+                p[3 * j + 2] = h->gin[l];
+            }
+            a.sparse = (const double*)hz_rt::dev(srv, p);
+            a.nsparse = (int)T.dirty.size();
+        } else if (tg) {
             std::memcpy(p, h->pin.data(), sizeof(double) * N);
             std::memcpy(p + N, h->gin.data(), sizeof(double) * N);
             a.reload = (const double*)hz_rt::dev(srv, p);
-            at = 2 * (size_t)N;
         }
+        if (tg) hz_fbi::sparse_clear(h);
         if (cf) {
             HZ_TRY(hz_fbi::fb_tv_materialize(h));
             for (int n = 0; n < N; ++n) {
@@ -258,17 +289,34 @@ int hz_fb_sample(hz_fb* h, double x, int dist_id, double param, double* y) {
     return HZ_OK;
 }
 
-int hz_fb_sample_tick(hz_fb* h) {
-    if (!h) return HZ_E_INVALID;
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+static void tick_locked(hz_fb* h) {
     ++h->rt.pending_ticks;
     h->rt.computed = false;
+}
+
+}  // namespace hz_fbi
+
+extern "C" {
+
+int hz_fb_sample(hz_fb* h, double x, int dist_id, double param, double* y) {
+    if (!h || !y || dist_id < HZ_DIST_NONE || dist_id > HZ_DIST_LIMITER) {
+        hz::set_error("hz_fb_sample: invalid arguments");
+        return HZ_E_INVALID;
+    }
+    hz_fbi::SampleLock lk(h);   // a setter from another thread goes first (this sample sees it)
+    return hz_fbi::sample_locked(h, x, dist_id, param, y);
+}
+
+int hz_fb_sample_tick(hz_fb* h) {
+    if (!h) return HZ_E_INVALID;
+    hz_fbi::SampleLock lk(h);
+    hz_fbi::tick_locked(h);
     return HZ_OK;
 }
 
 int hz_fb_sample_info(hz_fb* h, int* active, long long* served, int* groups) {
     if (!h) return HZ_E_INVALID;
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::HandleLock lk(h);
     if (active) *active = h->rt.active ? 1 : 0;
     if (served) *served = h->rt.seq;
     if (groups) *groups = groups_for(h->N);

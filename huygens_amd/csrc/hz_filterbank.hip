@@ -731,19 +731,37 @@ int fb_upload_staged(hz_fb* h) { return fb_upload(h); }
 
 // host mirror of the closed-form smoother end state written by every launch
 // (pgstate_next = pin + sp^n (pre - pin), likewise for the gains)
-void fb_mirror_advance(hz_fb* h, long len) { h->mirror_pending += len; }
+void fb_mirror_advance(hz_fb* h, long len) { h->mirror_clock += len; }
+
+// pg_host[b] after the d samples since band b was last brought current (its targets unchanged since)
+static inline void mirror_apply(hz_fb* h, int b, double spn, double sgn) {
+    double& P = h->pg_host[2 * (size_t)b];
+    double& G = h->pg_host[2 * (size_t)b + 1];
+    P = h->pin[b] + spn * (P - h->pin[b]);
+    G = h->gin[b] + sgn * (G - h->gin[b]);
+    h->mirror_at[b] = h->mirror_clock;
+}
 
 void fb_mirror_sync(hz_fb* h) {
-    if (h->mirror_pending == 0) return;
-    const double spn = (double)powl((long double)h->sp, (long double)h->mirror_pending);
-    const double sgn = (double)powl((long double)h->sg, (long double)h->mirror_pending);
+    long last = 0;   // bands synced by one-band setters lag by other counts: powers per distinct lag
+    double spn = 1, sgn = 1;
     for (int b = 0; b < h->N; ++b) {
-        double& P = h->pg_host[2 * (size_t)b];
-        double& G = h->pg_host[2 * (size_t)b + 1];
-        P = h->pin[b] + spn * (P - h->pin[b]);
-        G = h->gin[b] + sgn * (G - h->gin[b]);
+        const long d = h->mirror_clock - h->mirror_at[b];
+        if (d == 0) continue;
+        if (d != last) {
+            spn = (double)powl((long double)h->sp, (long double)d);
+            sgn = (double)powl((long double)h->sg, (long double)d);
+            last = d;
+        }
+        mirror_apply(h, b, spn, sgn);
     }
-    h->mirror_pending = 0;
+}
+
+void fb_mirror_sync_band(hz_fb* h, int l) {
+    if (l < 0) return;
+    const long d = h->mirror_clock - h->mirror_at[l];
+    if (d == 0) return;
+    mirror_apply(h, l, (double)powl((long double)h->sp, (long double)d), (double)powl((long double)h->sg, (long double)d));
 }
 
 int fb_launch_general(hz_fb* h, const double* d_in, double* d_out, long n) {
@@ -976,6 +994,8 @@ int hz_fb_create_shard(int order, int N_total, int band_begin, int band_count, d
     h->pin.assign(N, 0.0);
     h->gin.assign(N, 0.0);
     h->pg_host.assign(2 * N, 0.0);
+    h->mirror_at.assign(N, 0);
+    h->rt.mark.assign(N, 0);
     hz_fbi::fb_resp_init(h);
     // default geometry: 16 waves x 1 band; fewer waves when the bank is small
     h->waves = 16;
@@ -1059,7 +1079,7 @@ int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double*
         hz::set_error("hz_fb_coefficients: invalid arguments");
         return HZ_E_INVALID;
     }
-    hz_fbi::SetterLock lk(h);
+    hz_fbi::HandleLock lk(h);
     ++h->coef_gen;
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
@@ -1079,17 +1099,17 @@ int hz_fb_coefficients(hz_fb* h, int n, const double* fwd, int nf, const double*
 
 int hz_fb_boost(hz_fb* h, int n, double v) {
     if (!h) return HZ_E_INVALID;
-    hz_fbi::SetterLock lk(h);
-    ++h->pg_gen;
+    hz_fbi::HandleLock lk(h);
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
-    fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
     if (n < 0 || n >= h->N_total) {
         hz::set_error("hz_fb_boost: band %d out of range [0,%d)", n, h->N_total);
         return HZ_E_RANGE;
     }
     const int l = fb_local(h, n);
+    hz_fbi::fb_mirror_sync_band(h, l);   // band l's device smoothers ran on its old targets until now
+    hz_fbi::fb_rt_target_setter(h, l);
     if (l >= 0) {
         h->pin[l] = v;
         h->dirty_pin = true;
@@ -1099,8 +1119,8 @@ int hz_fb_boost(hz_fb* h, int n, double v) {
 
 int hz_fb_boost_all(hz_fb* h, const double* v, int count) {
     if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
-    hz_fbi::SetterLock lk(h);
-    ++h->pg_gen;
+    hz_fbi::HandleLock lk(h);
+    hz_fbi::fb_rt_target_setter(h, hz_fbi::kAllBands);
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
@@ -1115,17 +1135,17 @@ int hz_fb_boost_all(hz_fb* h, const double* v, int count) {
 
 int hz_fb_mix(hz_fb* h, int n, double v) {
     if (!h) return HZ_E_INVALID;
-    hz_fbi::SetterLock lk(h);
-    ++h->pg_gen;
+    hz_fbi::HandleLock lk(h);
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
-    fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
     h->converged = false;
     if (n < 0 || n >= h->N_total) {
         hz::set_error("hz_fb_mix: band %d out of range [0,%d)", n, h->N_total);
         return HZ_E_RANGE;
     }
     const int l = fb_local(h, n);
+    hz_fbi::fb_mirror_sync_band(h, l);   // band l's device smoothers ran on its old targets until now
+    hz_fbi::fb_rt_target_setter(h, l);
     if (l >= 0) {
         h->gin[l] = v;
         h->dirty_gin = true;
@@ -1135,8 +1155,8 @@ int hz_fb_mix(hz_fb* h, int n, double v) {
 
 int hz_fb_mix_all(hz_fb* h, const double* v, int count) {
     if (!h || (count > 0 && !v) || count < 0) return HZ_E_INVALID;
-    hz_fbi::SetterLock lk(h);
-    ++h->pg_gen;
+    hz_fbi::HandleLock lk(h);
+    hz_fbi::fb_rt_target_setter(h, hz_fbi::kAllBands);
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
@@ -1151,8 +1171,8 @@ int hz_fb_mix_all(hz_fb* h, const double* v, int count) {
 
 int hz_fb_open(hz_fb* h) {
     if (!h) return HZ_E_INVALID;
-    hz_fbi::SetterLock lk(h);
-    ++h->pg_gen;
+    hz_fbi::HandleLock lk(h);
+    hz_fbi::fb_rt_target_setter(h, hz_fbi::kAllBands);
     h->setter_seq = h->rt.seq;
     hz_fbi::fb_resp_setter(h);
     fb_mirror_sync(h);  // the device smoothers ran on the old targets until now
@@ -1167,7 +1187,7 @@ int hz_fb_set_distortion(hz_fb* h, int dist_id, double param) {
         hz::set_error("hz_fb_set_distortion: unknown functor %d", dist_id);
         return HZ_E_INVALID;
     }
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::HandleLock lk(h);
     h->dist_id = dist_id;
     h->dist_param = param;
     return HZ_OK;
@@ -1179,7 +1199,7 @@ int hz_fb_process_device(hz_fb* h, const double* d_in, double* d_out, size_t n) 
         hz::set_error("hz_fb_process_device: null handle or buffer");
         return HZ_E_INVALID;
     }
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::HandleLock lk(h);
     if (h->rt.computed) {   // the cached sample first (fb_rt_resolve), copied from pinned memory
         HZ_TRY_HIP(hipSetDevice(h->device));
         double y0 = 0;
@@ -1203,7 +1223,7 @@ int hz_fb_process(hz_fb* h, const double* in, double* out, size_t n) {
         hz::set_error("hz_fb_process: null handle or buffer");
         return HZ_E_INVALID;
     }
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::HandleLock lk(h);
     if (h->rt.computed) {   // the cached sample first (fb_rt_resolve)
         HZ_TRY_HIP(hipSetDevice(h->device));
         const int k = hz_fbi::fb_rt_resolve(h, out);
@@ -1303,7 +1323,7 @@ int hz_fb_state_size(hz_fb* h, size_t* count) {
 
 int hz_fb_get_state(hz_fb* h, double* buf, size_t count) {
     if (!h) return HZ_E_INVALID;
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::HandleLock lk(h);
     HZ_TRY(fb_check(h));
     size_t need;
     hz_fb_state_size(h, &need);
@@ -1321,7 +1341,7 @@ int hz_fb_get_state(hz_fb* h, double* buf, size_t count) {
 
 int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
     if (!h) return HZ_E_INVALID;
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::HandleLock lk(h);
     HZ_TRY(fb_check(h));
     size_t need;
     hz_fb_state_size(h, &need);
@@ -1334,7 +1354,7 @@ int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
     }
     HZ_TRY_HIP(hipMemcpy(h->d_pg[h->scur], buf + O + N * O, sizeof(double) * N * 2, hipMemcpyHostToDevice));
     std::memcpy(h->pg_host.data(), buf + O + N * O, sizeof(double) * N * 2);
-    h->mirror_pending = 0;
+    std::fill(h->mirror_at.begin(), h->mirror_at.end(), h->mirror_clock);
     h->converged = false;
     h->spare_ok = false;
     h->resp.implicit = false;   // overwritten
@@ -1345,7 +1365,7 @@ int hz_fb_set_state(hz_fb* h, const double* buf, size_t count) {
 
 int hz_fb_tick(hz_fb* h) {
     if (!h) return HZ_E_INVALID;
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::HandleLock lk(h);
     HZ_TRY(fb_check(h));
     return hz_fbi::fb_tick_rotate(h);
 }
@@ -1353,7 +1373,7 @@ int hz_fb_tick(hz_fb* h) {
 
 int hz_fb_setter_seq(hz_fb* h, long long* seq) {
     if (!h || !seq) return HZ_E_INVALID;
-    std::lock_guard<std::recursive_mutex> lk(h->mu);
+    hz_fbi::HandleLock lk(h);
     *seq = h->setter_seq;
     return HZ_OK;
 }

@@ -85,10 +85,11 @@ struct FbArgs {
     double* gin;
     const double* reload;   // (device address of pinned payload) [N] pin then [N] gin, or null
     const double* reload_coef;   // (pinned payload) [N][2O+1] new coefficients, or null
+    const double* sparse;   // (pinned payload) [nsparse] (band, pin, gin) triples, or null
     double x, param, sp, sg;
     double xr[5];           // input ring (ring order) after the ticks, before this compute
     int N, O;
-    int ticks, compute, dist, pad;
+    int ticks, compute, dist, nsparse;
 };
 // Delaybank sample (hz_delay.hip layout): rings [N][size], taps [N][2S] {thr, age_nowrap,
 // age_wrap, 0}, gains [N][2S] T; every line reads x (mono) or xin[line]; y[line] -> out

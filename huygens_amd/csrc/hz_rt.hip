@@ -76,6 +76,16 @@ template <int O>
 __device__ double op_fb(const FbArgs& a, int g, int groups) {
 #pragma clang fp contract(off)
     constexpr int R1 = O + 1;
+    if (a.nsparse > 0) {   // one-band setters since the last sample: the owners write the targets
+        for (int j = (int)threadIdx.x; j < a.nsparse; j += kThreads) {
+            const int b = (int)ldd_sys(a.sparse + 3 * j);
+            if ((b / kThreads) % groups == g) {
+                a.pin[b] = ldd_sys(a.sparse + 3 * j + 1);
+                a.gin[b] = ldd_sys(a.sparse + 3 * j + 2);
+            }
+        }
+        __syncthreads();   // (the band loop below reads them from another thread of the workgroup)
+    }
     double v = 0.0;
     for (int b = g * kThreads + (int)threadIdx.x; b < a.N; b += groups * kThreads) {
         const double* c = a.coef + (long)b * (2 * O + 1);

@@ -142,6 +142,38 @@ def test_setters_block_calls_and_state(gpu_lib):
     assert st.shape[0] == 2 + N * 2 + N * 2
 
 
+def test_one_band_setter_reloads(gpu_lib):
+    """One-band boost / mix between samples reach the server as (band, pin, gin) triples written by
+    the band's owning workgroup; a burst over N/8 bands, an all-band setter in between, or a band
+    set twice fall back to / stay consistent with both arrays.  8 workgroups own the bands; a
+    block call afterwards checks the host mirror of the smoothers (converged test, LTI path)."""
+    N = 5000
+    g, o = pair(2, N, centre=0.41)
+    rng = np.random.default_rng(11)
+    x = white_noise_f32(3000, seed=12)
+    errs, i = [], 0
+
+    def both(fn):
+        fn(g)
+        fn(o)
+    for rnd in range(12):
+        k = (1, 3, 700)[rnd % 3]          # 700 > N/8: the list stops covering, both arrays go
+        for b in rng.integers(0, N, k):
+            v = float(rng.uniform(0.2, 3.0))
+            both(lambda fb: fb.boost(int(b), v) if rnd % 2 else fb.mix(int(b), v))
+        if rnd == 4:
+            both(lambda fb: fb.boost(7, 1.5))
+            both(lambda fb: fb.boost(7, 0.25))   # the same band twice: the last value
+        if rnd == 7:
+            both(lambda fb: fb.open())           # all bands, then one band on top
+            both(lambda fb: fb.mix(4999, 0.125))
+        errs.append(run_lockstep(g, o, x[i:i + 40], ["st"] * 40)); i += 40
+    yg = g.process(x[i:i + 2000])
+    yo = o.process(x[i:i + 2000])
+    errs.append(float(np.max(np.abs(yg - yo)) / np.max(np.abs(yo))))
+    assert max(errs) < 1e-9, errs
+
+
 def test_feedback_through_caller(gpu_lib):
     """tests/spectral.cpp:94-104 shape: each input depends on the previous output, which only a
     synchronous per-sample path can serve."""

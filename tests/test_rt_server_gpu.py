@@ -196,8 +196,16 @@ def test_setters_from_another_thread(gpu_lib, tmp_path):
         o.tick()
     assert np.max(np.abs(yg - yo)) <= 1e-9 * np.max(np.abs(yo))
     steady = lat[200:] * 1e-3
+    at = np.zeros(S, dtype=bool)
+    at[np.clip(log[:, 0].astype(np.int64), 0, S - 1)] = True
+    at = at[200:]
     print(f"{len(log)} setters; per-sample latency: median {np.median(steady):.2f} us, p99 "
-          f"{np.percentile(steady, 99):.2f} us, worst {steady.max():.2f} us")
+          f"{np.percentile(steady, 99):.2f} us, p99.9 {np.percentile(steady, 99.9):.2f} us, worst "
+          f"{steady.max():.2f} us, {int((steady > 20.8).sum())} of {len(steady)} over 20.8 us; samples a "
+          f"setter applies at: median {np.median(steady[at]):.2f} us, worst {steady[at].max():.2f} us")
+    # a setter costs the sample it applies at its one-band reload, not a thread wake-up (both sides
+    # spin: hz_fbi::SetterLock / SampleLock); the median is robust to the box's rare host hiccups
+    assert np.median(steady[at]) < 20.8
 
 
 def test_idle_exit_races(gpu_lib):
