@@ -17,6 +17,7 @@
 // others follow through a device-memory flag), so a request is served once by each workgroup even
 // when it arrives while the instance leaves.
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -35,6 +36,9 @@ struct ServerArgs {
     long long* ctl;   // device memory: workgroup 0's idle-exit decision
     long long epoch;
     long long idle;   // real-time ticks without a request before leaving
+    // (tests) workgroup 0 holds its answer to request stall_req back by stall ticks: an unanswered
+    // request as the host sees it (env HZ_RT_DEBUG_STALL = "request:microseconds")
+    long long stall_req, stall;
 };
 
 namespace {
@@ -346,6 +350,10 @@ __global__ __launch_bounds__(kThreads) void rt_server_kernel(ServerArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
+            if (a.stall > 0 && g == 0 && r == a.stall_req) {   // (tests) a late answer, bounded
+                const long long t0 = __builtin_amdgcn_s_memrealtime();
+                while (__builtin_amdgcn_s_memrealtime() - t0 < a.stall) __builtin_amdgcn_s_sleep(100);
+            }
             std_sys(&a.slot[g].y, y);
             st_rel(&a.slot[g].done, r);
         }
@@ -373,6 +381,7 @@ struct Server {
     long long seq = 0, epoch = 0, requests = 0, launches = 0;
     bool active = false;
     bool broken = false;         // a request went unanswered: later calls fail (no double service)
+    long long answer_ms = 5000;  // the host's wait for an answer
     double* pay = nullptr;       // pinned payload / result
     size_t pay_cap = 0;
     double* res = nullptr;
@@ -414,6 +423,19 @@ int srv_launch(Server* s) {
     if (const char* e = std::getenv("HZ_RT_IDLE_US")) {
         const long long us = std::atoll(e);
         if (us > 0 && us <= 10000000) a.idle = us * 100;
+    }
+    a.stall_req = a.stall = 0;
+    if (const char* e = std::getenv("HZ_RT_DEBUG_STALL")) {   // (tests) "request:microseconds", <= 2 s
+        long long rq = 0, us = 0;
+        if (std::sscanf(e, "%lld:%lld", &rq, &us) == 2 && rq > 0 && us > 0 && us <= 2000000) {
+            a.stall_req = rq;
+            a.stall = us * 100;
+        }
+    }
+    s->answer_ms = 5000;
+    if (const char* e = std::getenv("HZ_RT_ANSWER_TIMEOUT_MS")) {   // (tests) the host's wait
+        const long long ms = std::atoll(e);
+        if (ms > 0 && ms <= 5000) s->answer_ms = ms;
     }
     hipLaunchKernelGGL(rt_server_kernel, dim3(kGroups), dim3(kThreads), 0, s->stream, a);
     HZ_TRY_HIP(hipGetLastError());
@@ -523,11 +545,11 @@ int call(Server* s, int op, const void* args, size_t bytes, int groups, double* 
             }
             HZ_TRY(srv_launch(s));
         }
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(s->answer_ms)) {
             // the request stays posted: a late answer would advance a state the caller was told
             // did not move, so no later request may follow it
             s->broken = true;
-            hz::set_error("hz_rt: the per-sample server did not answer within 5 s");
+            hz::set_error("hz_rt: the per-sample server did not answer within %lld ms", s->answer_ms);
             return HZ_E_HIP;
         }
     }

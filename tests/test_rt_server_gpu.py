@@ -5,6 +5,7 @@ with block calls, several handles at once, setters from another thread, and a bl
 stream while the server is resident."""
 import os
 import subprocess
+import sys
 import threading
 import time
 
@@ -252,3 +253,44 @@ def test_idle_exit_races(gpu_lib):
     relaunches = rt_info(0)[1] - launches0
     print(f"relaunches: {relaunches}")
     assert relaunches > 50
+
+
+_STALL_SCRIPT = r"""
+import time
+from huygens_amd import Filterbank
+from huygens_amd._lib import HZError, HZ_E_HIP
+g = Filterbank(2, 64, 0.1, 1.0)
+for n in range(64):
+    g.coefficients(n, [1.0, 0.0, -1.0], [-1.9, 0.95])
+g.boost([1.0] * 64)
+g.open()
+ys = [g(0.5), g(0.25)]                   # requests 1, 2 answered
+t0 = time.perf_counter()
+try:
+    g(0.125)                             # request 3: answered 400 ms late
+    raise SystemExit("unanswered request returned")
+except HZError as e:
+    assert e.code == HZ_E_HIP and "did not answer" in str(e), e
+waited = time.perf_counter() - t0
+time.sleep(0.5)                          # the late answer lands
+try:
+    g(0.0)                               # no request may follow an unanswered one
+    raise SystemExit("a request followed the unanswered one")
+except HZError as e:
+    assert e.code == HZ_E_HIP and "stopped answering" in str(e), e
+print(f"stall ok: waited {1e3 * waited:.1f} ms")
+"""
+
+
+def test_unanswered_request_disables_server(gpu_lib):
+    """A request the server does not answer within the host's wait (a wedged instance, simulated by
+    a test hook holding workgroup 0's answer back): the call fails, every later per-sample call is
+    refused instead of posting behind it (a late answer must not advance the state twice), and the
+    process still exits cleanly (the exit STOP is served after the late answer).  Runs in a child
+    process: the server stays disabled for the process's life."""
+    env = dict(os.environ, HZ_RT_DEBUG_STALL="3:400000", HZ_RT_ANSWER_TIMEOUT_MS="50")
+    p = subprocess.run([sys.executable, "-c", _STALL_SCRIPT], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=60)
+    assert p.returncode == 0 and "stall ok" in p.stdout, p.stdout + p.stderr
+    waited = float(p.stdout.split("waited")[1].split("ms")[0])
+    assert 50 <= waited < 300, waited
