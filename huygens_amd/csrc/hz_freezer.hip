@@ -21,7 +21,8 @@
 // reads x(t - N) or the Delay ring as it stood when the current unfrozen stretch began.
 //
 // Layout in HBM: input history ring [H]; window [N]; per freeze norms/phases [M][N]
-// (bit-reversed bins) and IFrames [M][N] (Re only: the output takes the real part);
+// (bit-reversed bins) and IFrames [M][N] (Re only: the output takes the real part; stored times
+// the output window);
 // IFrame state [M][N]; Delay ring snapshots [S][N+1]; runs and slot maps per call.
 #include <algorithm>
 #include <cmath>
@@ -37,7 +38,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxN = 8192;
-constexpr long kChunk = 1L << 18;
+constexpr long kChunk = 1L << 20;   // samples per chunk: a 10 s call at 48 kHz is one output launch
 
 struct FrzRun {
     long t0;        // first sample of the run (absolute)
@@ -97,7 +98,8 @@ __global__ __launch_bounds__(kThreads) void frz_frame_kernel(const double* in, l
 // 503-505).  Then the IFrame IFFT(polar(sqrt(dnorm), fmod(dphase, 2 PI))), Re part.
 __global__ __launch_bounds__(kThreads) void frz_iframe_kernel(const double* norm, const double* phase,
                                                               double* dnorm, double* dphase, const double2* tw,
-                                                              int N, int lg, int M, int excluded, double* ifr) {
+                                                              const double* win, int N, int lg, int M, int excluded,
+                                                              double* ifr) {
 #pragma clang fp contract(off)
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* re = lds;
@@ -123,7 +125,9 @@ __global__ __launch_bounds__(kThreads) void frz_iframe_kernel(const double* norm
     }
     __syncthreads();
     hz::lds_fft_inv(re, im, N, lg, tw);
-    for (int k = threadIdx.x; k < N; k += blockDim.x) ifr[(long)d * N + k] = re[k];
+    // stored times the output window: the output's product Re(IFrame[spot]) * halfhann(spot)
+    // (fourier.h:516), one rounding as there, made once per frame instead of per sample and slot
+    for (int k = threadIdx.x; k < N; k += blockDim.x) ifr[(long)d * N + k] = re[k] * win[k];
 }
 
 // Delay ring snapshots: snap[q+1] = snap[q] after the writes of dry stretch q = [a_q, b_q)
@@ -148,13 +152,13 @@ struct OutArgs {
     double* ring;
     long mask, T0, n;
     const FrzRun* runs;
+    const int* blk_run;      // [workgroups + 1] the run holding each workgroup's first sample
     int nruns;
     const SlotSrc* maps;
     const double* ifstate;   // [M][N]
     const double* ifopen;    // [M][N]
     const double* ifnew;     // [P][M][N]
     const double* snaps;     // [S][N+1]
-    const double* win;
     int N, M, stride, readsize;
 };
 
@@ -163,7 +167,9 @@ __global__ __launch_bounds__(kThreads) void frz_out_kernel(OutArgs a) {
     const long j = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= a.n) return;
     const long t = a.T0 + j;
-    int lo = 0, hi = a.nruns - 1;   // last run with t0 <= t
+    // last run with t0 <= t, within this workgroup's runs (host table: one dependent load or two
+    // instead of a search over the chunk's ~2 runs per stride)
+    int lo = a.blk_run[blockIdx.x], hi = a.blk_run[blockIdx.x + 1];
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (a.runs[mid].t0 <= t) lo = mid;
@@ -173,17 +179,21 @@ __global__ __launch_bounds__(kThreads) void frz_out_kernel(OutArgs a) {
     const int N = a.N;
     double output = 0;
     if (r.frozen) {
-        const int rh = (int)((r.rh0 + (t - r.t0)) % a.readsize);
+        // frozen runs end at the next populate point (<= stride samples), so rh0 + (t - t0) and
+        // rh - i stride stay within one readsize of [0, readsize): a compare instead of a division
+        const long d = t - r.t0;
+        int rh = d < a.readsize ? r.rh0 + (int)d : (int)((r.rh0 + d) % a.readsize);
+        if (rh >= a.readsize) rh -= a.readsize;
         const SlotSrc* map = a.maps + (long)r.map * a.M;
         for (int i = 0; i < a.M; ++i) {   // fourier.h:493-521, slot order
-            const int spot = (rh - i * a.stride + a.readsize) % a.readsize;
+            int spot = rh - i * a.stride;   // (rh - i stride + readsize) mod readsize, i stride < readsize
+            if (spot < 0) spot += a.readsize;
             if (spot < N) {
                 const SlotSrc m = map[i];
                 const double* f = m.src < 0    ? a.ifstate
                                   : m.src == 0 ? a.ifopen
                                                : a.ifnew + (long)(m.src - 1) * a.M * N;
-                const double v = f[(long)m.k * N + spot];
-                output += v * a.win[spot];
+                output += f[(long)m.k * N + spot];   // (IFrames stored windowed: frz_iframe_kernel)
             }
         }
         output /= N;
@@ -193,7 +203,18 @@ __global__ __launch_bounds__(kThreads) void frz_out_kernel(OutArgs a) {
         output = 0.0 + v;
     }
     a.out[j] = output;
-    a.ring[t & a.mask] = a.in[j];   // the history ring is >= 2 size + 2 N + kChunk: no reader of this slot
+    a.ring[t & a.mask] = a.in[j];   // the history ring is >= 2 size + 2 N + chunk: no reader of this slot
+}
+
+// IFrame state <- the latest content of each frame (src[q]: -1 unchanged, 0 the open period's
+// frames, p >= 1 the p-th freeze of the chunk), one launch for all M frames
+__global__ __launch_bounds__(256) void frz_carry_kernel(double* ifstate, const double* ifopen, const double* ifnew,
+                                                         const int* src, int M, int N) {
+    const int q = blockIdx.y, e = blockIdx.x * blockDim.x + threadIdx.x;
+    const int sq = src[q];
+    if (sq < 0 || e >= N) return;
+    const double* f = sq == 0 ? ifopen : ifnew + (size_t)(sq - 1) * M * N;
+    ifstate[(size_t)q * N + e] = f[(size_t)q * N + e];
 }
 
 int ilog2(int N) {
@@ -212,6 +233,7 @@ struct hz_frz {
     std::vector<int> iqueue;
     long u0 = 0;                  // start of the current unfrozen stretch (the Delay ring snapshot is at u0)
     long mask = 0;
+    long chunk = 0;               // samples per chunk (kChunk; env HZ_FRZ_CHUNK at create, tests)
     double *d_ring = nullptr, *d_win = nullptr, *d_norm = nullptr, *d_phase = nullptr, *d_ifstate = nullptr;
     double* d_ifopen = nullptr;   // [M][N] IFrames of the freeze period open at chunk start
     double *d_dnorm = nullptr, *d_dphase = nullptr;   // [M][N] DFrame state (persists across freezes)
@@ -298,6 +320,7 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
         }
     };
 
+    std::vector<SlotSrc> before(M);
     int k = 0;
     long t = T0;
     const long T1 = T0 + n;
@@ -316,7 +339,6 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
             if (rh % h->stride == 0 && rh / h->stride < M) {   // slot i = rh / stride at spot 0
                 const int i = rh / h->stride;
                 // before the populate: slots <= i; after: slots > i
-                std::vector<SlotSrc> before(M);
                 for (int q = 0; q < M; ++q) before[q] = {h->iqueue[q], last_src[h->iqueue[q]]};
                 int next = std::rand() % (M - 2);   // fourier.h:503-509
                 if (next >= h->excluded) next += 2;
@@ -356,19 +378,31 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
                            period_tf[q], h->d_norm, h->d_phase);
         HZ_TRY_HIP(hipGetLastError());
         hipLaunchKernelGGL(frz_iframe_kernel, dim3(M), dim3(ft), lds, h->stream, (const double*)h->d_norm,
-                           (const double*)h->d_phase, h->d_dnorm, h->d_dphase, (const double2*)h->d_tw, N, h->lg, M,
+                           (const double*)h->d_phase, h->d_dnorm, h->d_dphase, (const double2*)h->d_tw,
+                           (const double*)h->d_win, N, h->lg, M,
                            period_excl[q], h->d_ifnew + (size_t)q * M * N);
         HZ_TRY_HIP(hipGetLastError());
     }
-    // tables: runs, maps, stretches
+    // tables: runs, maps, stretches, each output workgroup's first run, the carry sources
     const size_t b_runs = runs.size() * sizeof(FrzRun), b_maps = std::max<size_t>(1, maps.size()) * sizeof(SlotSrc);
     const size_t b_st = std::max<size_t>(2, stretch.size()) * sizeof(long);
     const size_t nsnap = stretch.size() / 2 + 1;
-    HZ_TRY(grow(&h->d_tab, &h->tab_cap, b_runs + b_maps + b_st + 64, h->stream));
-    std::vector<char> hb(b_runs + b_maps + b_st);
+    const long nb = (n + kThreads - 1) / kThreads;
+    const size_t b_blk = sizeof(int) * (size_t)(nb + 1), b_src = sizeof(int) * (size_t)M;
+    HZ_TRY(grow(&h->d_tab, &h->tab_cap, b_runs + b_maps + b_st + b_blk + b_src + 64, h->stream));
+    std::vector<char> hb(b_runs + b_maps + b_st + b_blk + b_src);
     std::memcpy(hb.data(), runs.data(), b_runs);
     if (!maps.empty()) std::memcpy(hb.data() + b_runs, maps.data(), maps.size() * sizeof(SlotSrc));
     if (!stretch.empty()) std::memcpy(hb.data() + b_runs + b_maps, stretch.data(), stretch.size() * sizeof(long));
+    int* blk = (int*)(hb.data() + b_runs + b_maps + b_st);
+    for (long b = 0, r = 0; b < nb; ++b) {   // runs ascend in t0: the run at each workgroup start
+        const long tb = T0 + b * kThreads;
+        while (r + 1 < (long)runs.size() && runs[r + 1].t0 <= tb) ++r;
+        blk[b] = (int)r;
+    }
+    // a workgroup's runs lie in [blk[b], blk[b + 1]] (the run at the next workgroup's start)
+    blk[nb] = runs.empty() ? 0 : (int)runs.size() - 1;
+    std::memcpy(hb.data() + b_runs + b_maps + b_st + b_blk, last_src.data(), b_src);
     HZ_TRY_HIP(hipMemcpyAsync(h->d_tab, hb.data(), hb.size(), hipMemcpyHostToDevice, h->stream));
     const char* tab = (const char*)h->d_tab;
     // Delay ring snapshots after each dry stretch that ended here
@@ -395,13 +429,13 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
     a.T0 = T0;
     a.n = n;
     a.runs = (const FrzRun*)tab;
+    a.blk_run = (const int*)(tab + b_runs + b_maps + b_st);
     a.nruns = (int)runs.size();
     a.maps = (const SlotSrc*)(tab + b_runs);
     a.ifstate = h->d_ifstate;
     a.ifopen = h->d_ifopen;
     a.ifnew = h->d_ifnew;
     a.snaps = h->d_snap;
-    a.win = h->d_win;
     a.N = N;
     a.M = M;
     a.stride = h->stride;
@@ -428,12 +462,12 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
         }
     }
     // carry: IFrame state <- latest content (before the open period's frames are replaced)
-    for (int q = 0; q < M; ++q)
-        if (last_src[q] >= 0) {
-            const double* src = last_src[q] == 0 ? h->d_ifopen : h->d_ifnew + (size_t)(last_src[q] - 1) * M * N;
-            HZ_TRY_HIP(hipMemcpyAsync(h->d_ifstate + (size_t)q * N, src + (size_t)q * N, sizeof(double) * N,
-                                      hipMemcpyDeviceToDevice, h->stream));
-        }
+    if (std::any_of(last_src.begin(), last_src.end(), [](int v) { return v >= 0; })) {
+        hipLaunchKernelGGL(frz_carry_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)M), dim3(256), 0, h->stream,
+                           h->d_ifstate, (const double*)h->d_ifopen, (const double*)h->d_ifnew,
+                           (const int*)(tab + b_runs + b_maps + b_st + b_blk), M, N);
+        HZ_TRY_HIP(hipGetLastError());
+    }
     // a period still open at the chunk end: its frames for later chunks
     if (h->frozen && P > 0)
         HZ_TRY_HIP(hipMemcpyAsync(h->d_ifopen, h->d_ifnew + (size_t)(P - 1) * M * N, sizeof(double) * M * N,
@@ -476,7 +510,12 @@ int hz_frz_create(int N, int laps, double width, int device, hz_frz** out) {
         return HZ_E_INVALID;
     }
     long H = 1;
-    while (H < 2L * h->size + 2L * N + kChunk + 2) H <<= 1;
+    h->chunk = kChunk;
+    if (const char* e = std::getenv("HZ_FRZ_CHUNK")) {   // (tests: the launch split at a shorter length)
+        const long c = std::atol(e);
+        if (c >= 4096 && c <= kChunk) h->chunk = c;
+    }
+    while (H < 2L * h->size + 2L * N + h->chunk + 2) H <<= 1;
     h->mask = H - 1;
     std::vector<double> win(N);
     for (int k = 0; k < N; ++k) win[k] = std::sqrt(0.5 * (1 - std::cos(2 * hz::kPI * (k / (double)N))));   // halfhann
@@ -589,7 +628,7 @@ int hz_frz_process_device(hz_frz* h, const double* d_in, double* d_out, size_t n
     long done = 0;
     int k0 = 0;
     do {
-        const long m = std::min<long>((long)n - done, kChunk);
+        const long m = std::min<long>((long)n - done, h->chunk);
         int k1 = k0;
         while (k1 < nev && (ev[k1].at < done + m || (done + m == (long)n && ev[k1].at <= done + m))) ++k1;
         std::vector<hz_frz_event> local(ev + k0, ev + k1);

@@ -46,8 +46,10 @@ def test_freeze_cycles_vs_oracle(gpu_lib, N, laps, width):
     assert np.array_equal(gy[:3000], oy[:3000])   # the dry path before any freeze: exact
 
 
-def test_freeze_spanning_calls_and_launches(gpu_lib):
-    """A frozen period across calls and across the 2^18-sample launch split."""
+def test_freeze_spanning_calls_and_launches(gpu_lib, monkeypatch):
+    """A frozen period across calls and across a launch split (chunks of 2^18 samples here; the
+    default 2^20 makes a 10 s call one launch)."""
+    monkeypatch.setenv("HZ_FRZ_CHUNK", str(1 << 18))
     N, laps = 512, 4
     x = np.random.default_rng(1).standard_normal(300000 + 20000)
     blocks = [(20000, [(15000, 1)]), (300000, [(290000, 0)])]
