@@ -208,9 +208,14 @@ __global__ __launch_bounds__(kThreads) void frz_out_kernel(OutArgs a) {
 
 // IFrame state <- the latest content of each frame (src[q]: -1 unchanged, 0 the open period's
 // frames, p >= 1 the p-th freeze of the chunk), one launch for all M frames
+// (row M: Delay ring snapshot 0 <- the last one, when the chunk ended dry stretches)
 __global__ __launch_bounds__(256) void frz_carry_kernel(double* ifstate, const double* ifopen, const double* ifnew,
-                                                         const int* src, int M, int N) {
+                                                         const int* src, int M, int N, double* snap, int nsnap) {
     const int q = blockIdx.y, e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q == M) {
+        if (nsnap > 1 && e <= N) snap[e] = snap[(size_t)(nsnap - 1) * (N + 1) + e];
+        return;
+    }
     const int sq = src[q];
     if (sq < 0 || e >= N) return;
     const double* f = sq == 0 ? ifopen : ifnew + (size_t)(sq - 1) * M * N;
@@ -243,6 +248,12 @@ struct hz_frz {
     size_t snap_cap = 0;
     double2* d_tw = nullptr;
     void* d_tab = nullptr;        // runs + maps + stretches of one chunk
+    // host side of the chunk tables, kept across chunks (capacity reused: no regrowth copies); the
+    // upload goes from pinned staging (an async DMA, no bounce copy)
+    std::vector<FrzRun> v_runs;
+    std::vector<SlotSrc> v_maps;
+    char* h_tab = nullptr;        // pinned
+    size_t h_tab_cap = 0;
     size_t tab_cap = 0;
     double *d_in = nullptr, *d_out = nullptr;
     size_t in_cap = 0, out_cap = 0;
@@ -279,8 +290,10 @@ int grow(void** p, size_t* cap, size_t bytes, hipStream_t st) {
 int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz_event* ev, int nev) {
     const int N = h->N, M = h->M;
     const long T0 = h->T;
-    std::vector<FrzRun> runs;
-    std::vector<SlotSrc> maps;
+    std::vector<FrzRun>& runs = h->v_runs;
+    std::vector<SlotSrc>& maps = h->v_maps;
+    runs.clear();
+    maps.clear();
     std::vector<long> stretch;         // dry stretches ended in this chunk: [a, b) pairs
     std::vector<long> period_tf;       // freeze transitions in this chunk
     std::vector<int> period_excl;
@@ -319,6 +332,40 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
             h->frozen = false;
         }
     };
+
+    // the freeze transitions depend on the events alone (fourier.h:468-479): their frame / DFrame /
+    // IFrame passes are launched first and run on the device while the host builds the runs below
+    std::vector<long> pre_tf;
+    std::vector<int> pre_excl;
+    {
+        bool fz = h->frozen;
+        for (int e = 0; e < nev; ++e) {
+            const long te = T0 + ev[e].at;
+            if (ev[e].kind == HZ_FRZ_FREEZE) {
+                if (!fz) {
+                    pre_tf.push_back(te);
+                    pre_excl.push_back((int)((te % h->size) / h->stride));
+                }
+                fz = true;
+            } else {
+                fz = false;
+            }
+        }
+    }
+    const int P = (int)pre_tf.size();
+    HZ_TRY(grow((void**)&h->d_ifnew, &h->ifnew_cap, sizeof(double) * (size_t)std::max(1, P) * M * N, h->stream));
+    const size_t lds = sizeof(double) * 2 * N;
+    const int ft = std::min(kThreads, std::max(64, N / 4));   // within the kernels' launch bounds
+    for (int q = 0; q < P; ++q) {   // new period q is source q + 1
+        hipLaunchKernelGGL(frz_frame_kernel, dim3(M), dim3(ft), lds, h->stream, d_in, T0, (const double*)h->d_ring,
+                           h->mask, (const double*)h->d_win, (const double2*)h->d_tw, N, h->lg, h->stride, M, h->size,
+                           pre_tf[q], h->d_norm, h->d_phase);
+        HZ_TRY_HIP(hipGetLastError());
+        hipLaunchKernelGGL(frz_iframe_kernel, dim3(M), dim3(ft), lds, h->stream, (const double*)h->d_norm,
+                           (const double*)h->d_phase, h->d_dnorm, h->d_dphase, (const double2*)h->d_tw,
+                           (const double*)h->d_win, N, h->lg, M, pre_excl[q], h->d_ifnew + (size_t)q * M * N);
+        HZ_TRY_HIP(hipGetLastError());
+    }
 
     std::vector<SlotSrc> before(M);
     int k = 0;
@@ -367,21 +414,9 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
     }
     for (; k < nev; ++k) apply(ev[k], T1);   // events at the chunk end (at == n)
 
-    const int P = (int)period_tf.size();
-    // device work: per new period, frames -> DFrames -> IFrames
-    HZ_TRY(grow((void**)&h->d_ifnew, &h->ifnew_cap, sizeof(double) * (size_t)std::max(1, P) * M * N, h->stream));
-    const size_t lds = sizeof(double) * 2 * N;
-    const int ft = std::min(kThreads, std::max(64, N / 4));   // within the kernels' launch bounds
-    for (int q = 0; q < P; ++q) {   // new period q is source q + 1
-        hipLaunchKernelGGL(frz_frame_kernel, dim3(M), dim3(ft), lds, h->stream, d_in, T0, (const double*)h->d_ring,
-                           h->mask, (const double*)h->d_win, (const double2*)h->d_tw, N, h->lg, h->stride, M, h->size,
-                           period_tf[q], h->d_norm, h->d_phase);
-        HZ_TRY_HIP(hipGetLastError());
-        hipLaunchKernelGGL(frz_iframe_kernel, dim3(M), dim3(ft), lds, h->stream, (const double*)h->d_norm,
-                           (const double*)h->d_phase, h->d_dnorm, h->d_dphase, (const double2*)h->d_tw,
-                           (const double*)h->d_win, N, h->lg, M,
-                           period_excl[q], h->d_ifnew + (size_t)q * M * N);
-        HZ_TRY_HIP(hipGetLastError());
+    if (period_tf != pre_tf || period_excl != pre_excl) {   // (the pre-pass restates apply())
+        hz::set_error("hz_frz: freeze transitions disagree with the pre-pass");
+        return HZ_E_STATE;
     }
     // tables: runs, maps, stretches, each output workgroup's first run, the carry sources
     const size_t b_runs = runs.size() * sizeof(FrzRun), b_maps = std::max<size_t>(1, maps.size()) * sizeof(SlotSrc);
@@ -390,11 +425,19 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
     const long nb = (n + kThreads - 1) / kThreads;
     const size_t b_blk = sizeof(int) * (size_t)(nb + 1), b_src = sizeof(int) * (size_t)M;
     HZ_TRY(grow(&h->d_tab, &h->tab_cap, b_runs + b_maps + b_st + b_blk + b_src + 64, h->stream));
-    std::vector<char> hb(b_runs + b_maps + b_st + b_blk + b_src);
-    std::memcpy(hb.data(), runs.data(), b_runs);
-    if (!maps.empty()) std::memcpy(hb.data() + b_runs, maps.data(), maps.size() * sizeof(SlotSrc));
-    if (!stretch.empty()) std::memcpy(hb.data() + b_runs + b_maps, stretch.data(), stretch.size() * sizeof(long));
-    int* blk = (int*)(hb.data() + b_runs + b_maps + b_st);
+    const size_t b_tab = b_runs + b_maps + b_st + b_blk + b_src;
+    if (b_tab > h->h_tab_cap) {   // (the previous chunk's upload finished: every chunk ends synchronised)
+        if (h->h_tab) HZ_TRY_HIP(hipHostFree(h->h_tab));
+        h->h_tab = nullptr;
+        h->h_tab_cap = 0;
+        HZ_TRY_HIP(hipHostMalloc((void**)&h->h_tab, b_tab * 2));
+        h->h_tab_cap = b_tab * 2;
+    }
+    char* hb = h->h_tab;
+    std::memcpy(hb, runs.data(), b_runs);
+    if (!maps.empty()) std::memcpy(hb + b_runs, maps.data(), maps.size() * sizeof(SlotSrc));
+    if (!stretch.empty()) std::memcpy(hb + b_runs + b_maps, stretch.data(), stretch.size() * sizeof(long));
+    int* blk = (int*)(hb + b_runs + b_maps + b_st);
     for (long b = 0, r = 0; b < nb; ++b) {   // runs ascend in t0: the run at each workgroup start
         const long tb = T0 + b * kThreads;
         while (r + 1 < (long)runs.size() && runs[r + 1].t0 <= tb) ++r;
@@ -402,8 +445,8 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
     }
     // a workgroup's runs lie in [blk[b], blk[b + 1]] (the run at the next workgroup's start)
     blk[nb] = runs.empty() ? 0 : (int)runs.size() - 1;
-    std::memcpy(hb.data() + b_runs + b_maps + b_st + b_blk, last_src.data(), b_src);
-    HZ_TRY_HIP(hipMemcpyAsync(h->d_tab, hb.data(), hb.size(), hipMemcpyHostToDevice, h->stream));
+    std::memcpy(hb + b_runs + b_maps + b_st + b_blk, last_src.data(), b_src);
+    HZ_TRY_HIP(hipMemcpyAsync(h->d_tab, hb, b_tab, hipMemcpyHostToDevice, h->stream));
     const char* tab = (const char*)h->d_tab;
     // Delay ring snapshots after each dry stretch that ended here
     if (nsnap > h->snap_cap / (sizeof(double) * (N + 1))) {
@@ -462,21 +505,18 @@ int frz_chunk(hz_frz* h, const double* d_in, double* d_out, long n, const hz_frz
         }
     }
     // carry: IFrame state <- latest content (before the open period's frames are replaced)
-    if (std::any_of(last_src.begin(), last_src.end(), [](int v) { return v >= 0; })) {
-        hipLaunchKernelGGL(frz_carry_kernel, dim3((unsigned)((N + 255) / 256), (unsigned)M), dim3(256), 0, h->stream,
-                           h->d_ifstate, (const double*)h->d_ifopen, (const double*)h->d_ifnew,
-                           (const int*)(tab + b_runs + b_maps + b_st + b_blk), M, N);
+    // (and snapshot 0 <- the Delay ring at the start of the current or next dry stretch: row M)
+    if (nsnap > 1 || std::any_of(last_src.begin(), last_src.end(), [](int v) { return v >= 0; })) {
+        hipLaunchKernelGGL(frz_carry_kernel, dim3((unsigned)((N + 1 + 255) / 256), (unsigned)M + 1), dim3(256), 0,
+                           h->stream, h->d_ifstate, (const double*)h->d_ifopen, (const double*)h->d_ifnew,
+                           (const int*)(tab + b_runs + b_maps + b_st + b_blk), M, N, h->d_snap, (int)nsnap);
         HZ_TRY_HIP(hipGetLastError());
     }
     // a period still open at the chunk end: its frames for later chunks
     if (h->frozen && P > 0)
         HZ_TRY_HIP(hipMemcpyAsync(h->d_ifopen, h->d_ifnew + (size_t)(P - 1) * M * N, sizeof(double) * M * N,
                                   hipMemcpyDeviceToDevice, h->stream));
-    // snapshot 0 <- the Delay ring at the start of the current (or next) dry stretch
-    if (nsnap > 1)
-        HZ_TRY_HIP(hipMemcpyAsync(h->d_snap, h->d_snap + (nsnap - 1) * (N + 1), sizeof(double) * (N + 1),
-                                  hipMemcpyDeviceToDevice, h->stream));
-    HZ_TRY_HIP(hipStreamSynchronize(h->stream));   // hb (pageable) must outlive the copy
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));   // the pinned tables are rewritten by the next chunk
     h->T += n;
     return HZ_OK;
 }
@@ -579,6 +619,7 @@ int hz_frz_destroy(hz_frz* h) {
                     (void*)h->d_ifnew, (void*)h->d_snap, h->d_tab, (void*)h->d_in,
                     (void*)h->d_out})
         if (p) (void)hipFree(p);
+    if (h->h_tab) (void)hipHostFree(h->h_tab);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
