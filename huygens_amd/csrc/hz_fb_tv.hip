@@ -18,10 +18,12 @@
 // Algorithmic HBM traffic per band-sample: COEFFS 8 (2O+1) B (40 B at order 2); RESONANT 8 B.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
 #include "hz_fb_impl.h"
+#include "hz_rt.h"
 
 // per-band arithmetic in the restatement's order, without FMA contraction
 #pragma clang fp contract(off)
@@ -54,6 +56,7 @@ struct TvArgs {
     long n, pstride, stream_row;   // stream_row: doubles per sample row
     int N;
     double sp, sg, param, dist_param;
+    int fasttrig;          // bounded-range sin / cos for 0 <= arg <= 2 PI (hz_rt.h); 0: libm (env HZ_FB_TV_LIBM=1)
 };
 
 // libgcc's __divdc3 (Smith's algorithm) for (a + ib) / (c + id)
@@ -97,9 +100,19 @@ __device__ __forceinline__ void cdiv_one(double c, double d, double& x, double& 
 }
 
 // subtractive.h:240-249
-__device__ __forceinline__ double resonant(double frequency, double Q) {
+// cos / sincos of an angle: the bounded-range kernels (< 1 ulp, hz_rt.h) for 0 <= x <= 2 PI -- every
+// audio frequency's 2 PI f / SR and 4 PI f / SR -- else libm
+__device__ __forceinline__ double tv_cos(double x, bool fast) {
+    return (fast && x >= 0.0 && x <= 6.2831853072) ? hz_rt::cos_0_2pi(x) : cos(x);
+}
+__device__ __forceinline__ void tv_sincos(double x, double* s, double* c, bool fast) {
+    if (fast && x >= 0.0 && x <= 6.2831853072) hz_rt::sincos_0_2pi(x, s, c);
+    else sincos(x, s, c);
+}
+
+__device__ __forceinline__ double resonant(double frequency, double Q, bool fast = false) {
     double s2, c2;
-    sincos(div_sr(4 * hz::kPI * frequency), &s2, &c2);
+    tv_sincos(div_sr(4 * hz::kPI * frequency), &s2, &c2, fast);
     const double ir = 0.0 * s2 - 1.0 * 0.0, ii = 0.0 * 0.0 + 1.0 * s2;   // 1.0i * sine2
     const double dr = (Q - c2) - ir, di = -0.0 - ii;
     double qr, qi;
@@ -143,8 +156,8 @@ __global__ __launch_bounds__(kThreads) void fb_tv_kernel(TvArgs a) {
             } else {   // HZ_FB_TV_RESONANT, O == 2
                 const double fr = srow[t * a.stream_row];
                 const double R = a.param;
-                const double cosine = cos(2 * hz::kPI * fr / hz::kSR);
-                const double g = resonant(fr, R);
+                const double cosine = tv_cos(2 * hz::kPI * fr / hz::kSR, a.fasttrig != 0);
+                const double g = resonant(fr, R, a.fasttrig != 0);
                 f[0] = g;
                 f[1] = 0;
                 f[2] = -g;
@@ -275,8 +288,8 @@ __global__ __launch_bounds__(kResThreads) void fb_tv_res_kernel(TvArgs a) {
 #pragma unroll
                 for (int i = 0; i < kResPer; ++i) {
                     const int j = pw * kResPer + i;
-                    const double cosine = cos(div_sr(2 * hz::kPI * fr[i]));
-                    const double g = resonant(fr[i], R);
+                    const double cosine = tv_cos(div_sr(2 * hz::kPI * fr[i]), a.fasttrig != 0);
+                    const double g = resonant(fr[i], R, a.fasttrig != 0);
                     gb[c][j][lane] = g;
                     bb[c][j][lane] = -2 * R * cosine;
                 }
@@ -486,6 +499,7 @@ int hz_fb_process_tv_device(hz_fb* h, const double* d_in, double* d_out, size_t 
         a.pstride = pstride;
         a.stream_row = row;
         a.N = (int)N;
+        a.fasttrig = std::getenv("HZ_FB_TV_LIBM") ? 0 : 1;
         a.sp = h->sp;
         a.sg = h->sg;
         a.param = param;

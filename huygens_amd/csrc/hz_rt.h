@@ -69,6 +69,38 @@ __device__ __forceinline__ double cos_0_2pi(double x) {
     }
 }
 
+// sin and cos of 0 <= x <= 2 PI + 1e-9, the reduction and polynomials of cos_0_2pi (its cosine is
+// bit-identical to cos_0_2pi's)
+__device__ __forceinline__ void sincos_0_2pi(double x, double* sn_out, double* cs_out) {
+    constexpr double kInvPio2 = 6.36619772367581382433e-01;
+    constexpr double kPio2_1 = 1.57079632673412561417e+00, kPio2_1t = 6.07710050650619224932e-11;
+    const double kf = __builtin_rint(x * kInvPio2);
+    const int k = (int)kf;
+    const double r = (x - kf * kPio2_1) - kf * kPio2_1t;
+    const double z = r * r;
+    double ps = 1.58969099521155010221e-10;
+    ps = __builtin_fma(ps, z, -2.50507602534068634195e-08);
+    ps = __builtin_fma(ps, z, 2.75573137070700676789e-06);
+    ps = __builtin_fma(ps, z, -1.98412698298579493134e-04);
+    ps = __builtin_fma(ps, z, 8.33333333332248946124e-03);
+    ps = __builtin_fma(ps, z, -1.66666666666666324348e-01);
+    const double sn = __builtin_fma(r * z, ps, r);
+    double pc = -1.13596475577881948265e-11;
+    pc = __builtin_fma(pc, z, 2.08757232129817482790e-09);
+    pc = __builtin_fma(pc, z, -2.75573143513906633035e-07);
+    pc = __builtin_fma(pc, z, 2.48015872894767294178e-05);
+    pc = __builtin_fma(pc, z, -1.38888888888741095749e-03);
+    pc = __builtin_fma(pc, z, 4.16666666666666019037e-02);
+    const double hz_ = 0.5 * z, w = 1.0 - hz_;
+    const double cs = w + (((1.0 - w) - hz_) + z * z * pc);
+    switch (k & 3) {
+    case 0: *sn_out = sn; *cs_out = cs; break;
+    case 1: *sn_out = cs; *cs_out = -sn; break;
+    case 2: *sn_out = -sn; *cs_out = -cs; break;
+    default: *sn_out = -cs; *cs_out = sn; break;
+    }
+}
+
 // the Granulator's window term's cosine, block kernel and per-sample server alike (bit-identical)
 __device__ __forceinline__ double hann_cos(double arg, bool fast) {
     return (fast && arg >= 0.0 && arg <= 6.2831853072) ? cos_0_2pi(arg) : cos(arg);
