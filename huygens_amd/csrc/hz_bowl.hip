@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -282,17 +283,18 @@ struct ChainArgs {
     int mix;
 };
 
+template <int SPW>
 __global__ __launch_bounds__(kChainThreads) void bowl_dly_chain_kernel(ChainArgs a) {
     constexpr int kW = kChainThreads / 64;
-    __shared__ double wsum[kW][kChainSpw];
-    __shared__ float xs[kChainSpw];
-    __shared__ float ly[kChainMaxLines * kChainSpw];
+    __shared__ double wsum[kW][SPW];
+    __shared__ float xs[SPW];
+    __shared__ float ly[(kChainThreads / SPW) * SPW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const long t0 = (long)blockIdx.x * kChainSpw;
+    const long t0 = (long)blockIdx.x * SPW;
     const hz_chain::DlyBlock& d = a.d;
     const int S = d.S;
     // ---- the bank's ring reads for this thread's (line, sample), issued first
-    const int l = tid / kChainSpw, sl = tid % kChainSpw;
+    const int l = tid / SPW, sl = tid % SPW;
     const long j = t0 + sl;
     const bool live = l < d.N && j < a.n;
     const unsigned o = live ? (unsigned)((d.o0 + (unsigned long)j) % d.size) : 0u;
@@ -316,12 +318,12 @@ __global__ __launch_bounds__(kChainThreads) void bowl_dly_chain_kernel(ChainArgs
         }
     }
     // ---- generator: acc[s] = sum over this thread's modes
-    float ph[kChainSpw];
+    float ph[SPW];
 #pragma unroll
-    for (int s = 0; s < kChainSpw; ++s) ph[s] = phase_f(a.n0, t0 + s);
-    double acc[kChainSpw];
+    for (int s = 0; s < SPW; ++s) ph[s] = phase_f(a.n0, t0 + s);
+    double acc[SPW];
 #pragma unroll
-    for (int s = 0; s < kChainSpw; ++s) acc[s] = 0.0;
+    for (int s = 0; s < SPW; ++s) acc[s] = 0.0;
     // kPre modes per thread per pass, their table entries loaded together (a mode past M is
     // all zeros: amplitude 0 adds an exact 0)
     constexpr int kPre = 4;
@@ -339,7 +341,7 @@ __global__ __launch_bounds__(kChainThreads) void bowl_dly_chain_kernel(ChainArgs
             const float x0 = div_sr(-q[u].y * ph[0]);
             double amag = (double)q[u].z * exp((double)x0);
 #pragma unroll
-            for (int s = 0; s < kChainSpw; ++s) {
+            for (int s = 0; s < SPW; ++s) {
                 const float p = div_sr(q[u].x * ph[s]);
                 const float wv = (float)sin2pi_ref(p);
                 acc[s] = fma(amag, (double)wv, acc[s]);
@@ -348,14 +350,14 @@ __global__ __launch_bounds__(kChainThreads) void bowl_dly_chain_kernel(ChainArgs
         }
     }
 #pragma unroll
-    for (int s = 0; s < kChainSpw; ++s) {
+    for (int s = 0; s < SPW; ++s) {
         double v = acc[s];
 #pragma unroll
         for (int w = 32; w; w >>= 1) v += __shfl_xor(v, w);
         if (lane == 0) wsum[wave][s] = v;
     }
     __syncthreads();
-    if (tid < kChainSpw) {
+    if (tid < SPW) {
         double v = wsum[0][tid];
 #pragma unroll
         for (int w = 1; w < kW; ++w) v += wsum[w][tid];
@@ -382,15 +384,15 @@ __global__ __launch_bounds__(kChainThreads) void bowl_dly_chain_kernel(ChainArgs
             }
             d.rx[(long)l * d.size + o] = x;
             d.ry[(long)l * d.size + o] = accd;
-            if (a.mix) ly[l * kChainSpw + sl] = accd;
+            if (a.mix) ly[l * SPW + sl] = accd;
             else a.out[(long)l * a.n + j] = accd;
         }
         if (a.mix) {
             __syncthreads();
-            if (tid < kChainSpw && t0 + tid < a.n) {
+            if (tid < SPW && t0 + tid < a.n) {
                 float m = 0.0f;   // line order; the LDS reads of 16 lines issue together
 #pragma unroll 16
-                for (int k = 0; k < d.N; ++k) m = m + ly[k * kChainSpw + tid];
+                for (int k = 0; k < d.N; ++k) m = m + ly[k * SPW + tid];
                 a.out[t0 + tid] = m / (float)d.N;
             }
         }
@@ -793,8 +795,16 @@ int hz_bowl_fill_delaybank(hz_bowl* h, float* d_buf, hz_dly* bank, void* d_out, 
     a.d = d;
     a.out = (float*)d_out;
     a.mix = mix ? 1 : 0;
-    hipLaunchKernelGGL(bowl_dly_chain_kernel, dim3((unsigned)((n + kChainSpw - 1) / kChainSpw)), dim3(kChainThreads),
-                       0, h->stream, a);
+    // samples per workgroup (env HZ_CHAIN_SPW = 2 / 4 / 8 for A/B; lines must fit kChainThreads / SPW)
+    int spw = kChainSpw;
+    if (const char* e = std::getenv("HZ_CHAIN_SPW")) {
+        const int v = std::atoi(e);
+        if ((v == 2 || v == 4 || v == 8) && d.N <= kChainThreads / v) spw = v;
+    }
+    const unsigned grid = (unsigned)((n + spw - 1) / spw);
+    if (spw == 2) hipLaunchKernelGGL(bowl_dly_chain_kernel<2>, dim3(grid), dim3(kChainThreads), 0, h->stream, a);
+    else if (spw == 8) hipLaunchKernelGGL(bowl_dly_chain_kernel<8>, dim3(grid), dim3(kChainThreads), 0, h->stream, a);
+    else hipLaunchKernelGGL(bowl_dly_chain_kernel<kChainSpw>, dim3(grid), dim3(kChainThreads), 0, h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
     if (e) HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
     h->n0 += (double)n;
