@@ -194,6 +194,66 @@ __device__ void op_dly(const DlyArgs& a, int g, int groups) {
     }
 }
 
+// OP_DLY with a line's taps across lanes (S <= 64, SP = S rounded up to a power of two, so a line's
+// lanes share a wave): every lane loads its tap's records and ring values at once -- instead of
+// one thread walking the taps, a tap record then a ring read per tap -- and the line's first lane
+// accumulates in tap order through shuffles (a zero-age feedback tap reads the running sum, as
+// op_dly does), so every product and sum is op_dly's, bit for bit
+template <class T>
+__device__ void op_dly_lanes(const DlyArgs& a, int g, int groups) {
+#pragma clang fp contract(off)
+    const unsigned size = a.size, o = a.o;
+    const int S = a.S;
+    int SP = 1;
+    while (SP < S) SP <<= 1;
+    const int per = kThreads / SP;                   // lines per workgroup pass
+    const int i = (int)threadIdx.x % SP, base = (int)threadIdx.x - i;
+    const int lanebase = base & 63;
+    for (int l0 = g * per; l0 < a.N; l0 += groups * per) {   // uniform across the workgroup
+        const int l = l0 + (int)threadIdx.x / SP;
+        const bool live = l < a.N && i < S;
+        const long lc = live ? l : 0;
+        T fx = (T)0, by = (T)0, b = (T)0;
+        int zero_age = 0;
+        T x = (T)0;
+        if (l < a.N) x = (T)(a.xin ? ldd_sys(a.xin + l) : a.x);
+        if (live) {
+            const int4* tp = a.taps + lc * 2 * S;
+            const T* gn = (const T*)a.gains + lc * 2 * S;
+            const T* rx = (const T*)a.rx + lc * size;
+            const T* ry = (const T*)a.ry + lc * size;
+            const int4 qf = tp[i];
+            const T f = gn[i];
+            b = gn[S + i];
+            const unsigned af = ((int)o < qf.x) ? (unsigned)qf.z : (unsigned)qf.y;
+            const T xv = af == 0 ? x : rx[o >= af ? o - af : o + size - af];
+            fx = f * xv;
+            if (b != (T)0) {
+                const int4 qb = tp[S + i];
+                const unsigned ab = ((int)o < qb.x) ? (unsigned)qb.z : (unsigned)qb.y;
+                if (ab == 0) zero_age = 1;
+                else by = b * ry[o >= ab ? o - ab : o + size - ab];
+            }
+        }
+        T acc = (T)0;
+        for (int k = 0; k < S; ++k) {   // every lane shuffles; the line's lane 0 keeps the sum
+            const T fk = __shfl(fx, lanebase + k);
+            T bk = __shfl(by, lanebase + k);
+            const T gk = __shfl(b, lanebase + k);
+            const int zk = __shfl(zero_age, lanebase + k);
+            if (zk) bk = gk * acc;
+            acc = acc + (fk - bk);
+        }
+        if (i == 0 && l < a.N) {
+            T* rx = (T*)a.rx + (long)l * size;
+            T* ry = (T*)a.ry + (long)l * size;
+            rx[o] = x;
+            ry[o] = acc;
+            std_sys(a.out + l, (double)acc);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // OP_GRAN (workgroup 0): the sample at time t of src/granulator.h:88-104 over the source ring,
 // the block kernel's per-grain arithmetic (hz_granulator.hip gran_kernel), terms summed in voice
@@ -340,8 +400,14 @@ __global__ __launch_bounds__(kThreads) void rt_server_kernel(ServerArgs a) {
             } else if (op == OP_DLY) {
                 DlyArgs da;
                 __builtin_memcpy(&da, &s.w[1], sizeof(da));
-                if (da.is_float) op_dly<float>(da, g, groups);
-                else op_dly<double>(da, g, groups);
+                if (da.S <= 64) {
+                    if (da.is_float) op_dly_lanes<float>(da, g, groups);
+                    else op_dly_lanes<double>(da, g, groups);
+                } else if (da.is_float) {
+                    op_dly<float>(da, g, groups);
+                } else {
+                    op_dly<double>(da, g, groups);
+                }
             } else if (op == OP_GRAN) {
                 GranArgs ga;
                 __builtin_memcpy(&ga, &s.w[1], sizeof(ga));
