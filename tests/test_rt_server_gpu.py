@@ -294,3 +294,47 @@ def test_unanswered_request_disables_server(gpu_lib):
     assert p.returncode == 0 and "stall ok" in p.stdout, p.stdout + p.stderr
     waited = float(p.stdout.split("waited")[1].split("ms")[0])
     assert 50 <= waited < 300, waited
+
+
+_HOST_LINE_SCRIPT = r"""
+import numpy as np
+import sys
+sys.path.insert(0, "tests")
+from golden.spec_numpy import resonant_coefficients, white_noise_f32
+from oracle import OracleFilterbank
+from oracle_delay import OracleDelaybank
+from huygens_amd import Delay, Filterbank
+N = 600
+g, o = Filterbank(2, N), OracleFilterbank(2, N)
+fwd, back = resonant_coefficients(N, 0.999, 0.5)
+for fb in (g, o):
+    for n in range(N):
+        fb.coefficients(n, fwd[n], back[n])
+    fb.boost(np.ones(N))
+    fb.open()
+x = white_noise_f32(300, seed=21)
+yg, yo = [], []
+for t, v in enumerate(x):
+    if t == 150:
+        g.boost(3, 2.0); o.boost(3, 2.0)
+    yg.append(g(v)); g.tick()
+    yo.append(o(v)); o.tick()
+yg, yo = np.array(yg), np.array(yo)
+assert np.max(np.abs(yg - yo)) <= 1e-11 * np.max(np.abs(yo)), np.max(np.abs(yg - yo))
+d, od = Delay(10, 96000), OracleDelaybank(1, 10, 96000)
+d.coefficients([(0, 1.0)], [(20, 0.5), (7, 0.25)])
+od.coefficients(0, [(0, 1.0)], [(20, 0.5), (7, 0.25)])
+dg = np.array([d(v) for v in x])
+assert np.array_equal(dg, od.process(x)[0])
+print("host line ok")
+"""
+
+
+def test_pinned_host_request_line(gpu_lib):
+    """The request line in pinned host memory (devices without a large BAR; HZ_RT_HOST_MAILBOX=1
+    forces it): per-sample Filterbank with a setter and a bit-exact Delay against the restatement
+    in a child process (the line is chosen when the process creates its server)."""
+    env = dict(os.environ, HZ_RT_HOST_MAILBOX="1")
+    p = subprocess.run([sys.executable, "-c", _HOST_LINE_SCRIPT], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0 and "host line ok" in p.stdout, p.stdout + p.stderr
