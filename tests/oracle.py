@@ -172,9 +172,12 @@ def golden_names(prefix):
 
 
 def rel_err(got, ref):
-    """norm-wise parity metric of SURVEY.md 8(d): ||got-ref||_inf / ||ref||_inf."""
-    got = np.asarray(got, dtype=np.float64)
-    ref = np.asarray(ref, dtype=np.float64)
+    """norm-wise parity metric of SURVEY.md 8(d): ||got-ref||_inf / ||ref||_inf (complex values
+    compare as complex: both parts count)."""
+    got, ref = np.asarray(got), np.asarray(ref)
+    dt = np.complex128 if np.iscomplexobj(got) or np.iscomplexobj(ref) else np.float64
+    got = got.astype(dt)
+    ref = ref.astype(dt)
     den = np.max(np.abs(ref)) if ref.size else 0.0
     if den == 0.0:
         return float(np.max(np.abs(got))) if got.size else 0.0
