@@ -27,6 +27,15 @@ struct Lds {
     double re[hz::padded_len(kN)], im[hz::padded_len(kN)];
 };
 
+// forward passes 2-4 and inverse passes 1-3 touch only the 512-point block of the group's wave
+// (group b = thread t: block b >> 6 = t >> 6), so between them a wave's own LDS writes need only
+// land -- the workgroup barrier stays where data crosses waves (after the register pass, before
+// the caller's reads)
+__device__ __forceinline__ void wave_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // W_2048^m from the W_4096 table (tw[k] = e^{-2 pi i k / 4096}, k < 2048)
 __device__ __forceinline__ double2 w2k(const double2* __restrict__ tw, int m) { return tw[2 * m]; }
 
@@ -117,9 +126,9 @@ __device__ __forceinline__ void fwd(Lds& s, double (&vr)[kPT], double (&vi)[kPT]
     }
     __syncthreads();
     Dif<3, 8>::lds(s, t, w.p2);
-    __syncthreads();
+    wave_sync();
     Dif<3, 5>::lds(s, t, w.p3);
-    __syncthreads();
+    wave_sync();
     const double2 one[3] = {make_double2(1.0, 0.0), make_double2(1.0, 0.0), make_double2(1.0, 0.0)};
     Dif<3, 2>::lds(s, t, one);
     __syncthreads();
@@ -190,9 +199,9 @@ __device__ __forceinline__ void inv(Lds& s, double (&vr)[kPT], double (&vi)[kPT]
     __syncthreads();
     const double2 one[3] = {make_double2(1.0, 0.0), make_double2(1.0, 0.0), make_double2(1.0, 0.0)};
     Dit<3, 0>::lds(s, t, one);
-    __syncthreads();
+    wave_sync();
     Dit<3, 3>::lds(s, t, w.p2);
-    __syncthreads();
+    wave_sync();
     Dit<3, 6>::lds(s, t, w.p3);
     __syncthreads();
     // pass 4 (R 2, LH 9) on registers: group t = t + 512 j, group t + 256 = t + 256 + 512 j
