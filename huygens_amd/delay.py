@@ -122,6 +122,10 @@ class Delay(Delaybank):
 
     def __init__(self, sparsity: int, time: int, dtype=np.float64, device: int = 0):
         super().__init__(1, sparsity, time, dtype, device)
+        # operator()'s input and output as preallocated C scalars (no arrays per sample)
+        ct = C.c_float if self.dtype == np.float32 else C.c_double
+        self._cx, self._cy = ct(), ct()
+        self._px, self._py = C.c_void_p(C.addressof(self._cx)), C.c_void_p(C.addressof(self._cy))
 
     def coefficients(self, forward, back):  # noqa: D102
         super().coefficients(0, forward, back)
@@ -137,4 +141,6 @@ class Delay(Delaybank):
 
     def __call__(self, x) -> float:
         """`y = delay(x); delay.tick();` (tests/delay.cpp:22-27) through the per-sample server"""
-        return float(self.sample(x)[0])
+        self._cx.value = x   # (c_float: rounded to T as the array path's cast)
+        check(self._lib.hz_dly_sample(self._h, self._px, self._py, 0))
+        return float(self._cy.value)
