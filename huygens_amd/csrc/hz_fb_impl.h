@@ -353,6 +353,7 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n);
 int fb_stream_workgroups();   // workgroups of one streaming launch (completion flags)
 int fb_stream_track(hz_fb* h, const double* d_in, long n, bool conv);   // a short per-band call
 int fb_stream_materialize(hz_fb* h);   // band states, smoothers, x history from the ring
+int fb_stream_upkeep(hz_fb* h);        // smoothers and x history over the streamed samples
 int fb_stream_to_hist(hz_fb* h);       // the ring's history back to resp.d_hist (long calls)
 void fb_stream_reset(hz_fb* h);        // state overwritten (set_state, tick)
 void fb_stream_free(hz_fb* h);

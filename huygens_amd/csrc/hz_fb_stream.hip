@@ -299,9 +299,11 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
         double2 hv[QI], zv[QI];
 #pragma unroll
         for (int i = 0; i < QI; ++i) {
-            const int p = 3 + g + 8 * i;   // < Q + 8: rows past Q are zero
-            hv[i] = a.HS[((long)p * kCols + c) * 32 + j];
-            zv[i] = a.ZS[((long)ring_slot(a.head, p - 2, a.Q) * kCols + c) * 32 + j];
+            const int p = 3 + g + 8 * i;   // < Q + 3; partitions past Q - 1 contribute nothing
+            // (masked: slot ring_slot(head, Q) is the one this launch's transform role writes)
+            const bool live = p < a.Q;
+            hv[i] = live ? a.HS[((long)p * kCols + c) * 32 + j] : make_double2(0.0, 0.0);
+            zv[i] = live ? a.ZS[((long)ring_slot(a.head, p - 2, a.Q) * kCols + c) * 32 + j] : make_double2(0.0, 0.0);
         }
         double2 r = make_double2(0.0, 0.0);
 #pragma unroll
@@ -571,6 +573,10 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
     HZ_TRY(stream_setup(h));
     const int Q = (int)(R.K / kSP);
     if (S.hs_gen != R.h_gen) {   // partition spectra of the current h
+        // rows Q .. Q + 7 are read by the MAC roles and must be exact zeros; a shorter horizon than
+        // the buffer was sized for leaves an older response's spectra there
+        const size_t col = (size_t)kCols * 32 * 2;
+        HZ_TRY_HIP(hipMemsetAsync(S.d_HS + (size_t)Q * col, 0, sizeof(double) * 8 * col, h->stream));
         hipLaunchKernelGGL(stream_hs_kernel, dim3(kCols, (unsigned)Q), dim3(kT), 0, h->stream, (const double*)R.d_h,
                            (const double2*)S.d_tw, (double2*)S.d_HS);
         HZ_TRY_HIP(hipGetLastError());
@@ -641,8 +647,9 @@ int fb_stream_track(hz_fb* h, const double* d_in, long n, bool conv) {
     return HZ_OK;
 }
 
-// the smoothers and x history after the streamed samples (pend), in place
-static int stream_upkeep(hz_fb* h) {
+// the smoothers and x history after the streamed samples (pend), in place, toward the targets
+// (d_pin / d_gin) the samples ran with: fb_upload calls it before new targets are uploaded
+int fb_stream_upkeep(hz_fb* h) {
     hz_fb::Resp::Stream& S = h->resp.st;
     if (S.pend == 0) return HZ_OK;
     const double spm = (double)powl((long double)h->sp, (long double)S.pend);
@@ -660,7 +667,7 @@ static int stream_upkeep(hz_fb* h) {
 int fb_stream_materialize(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     hz_fb::Resp::Stream& S = R.st;
-    HZ_TRY(stream_upkeep(h));
+    HZ_TRY(fb_stream_upkeep(h));
     HZ_TRY(fb_resp_build(h));
     return fb_state_window(h, S.d_line + ring_index(S, S.pos - R.K), R.K, h->d_ystate[h->scur], h->stream);
 }
@@ -671,7 +678,7 @@ int fb_stream_to_hist(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     hz_fb::Resp::Stream& S = R.st;
     if (!S.line_hist) return HZ_OK;
-    HZ_TRY(stream_upkeep(h));
+    HZ_TRY(fb_stream_upkeep(h));
     if (R.run > 0) {
         HZ_TRY(fb_resp_setup(h));
         hipLaunchKernelGGL(stream_get_kernel, dim3((unsigned)((R.K + 255) / 256)), dim3(256), 0, h->stream,

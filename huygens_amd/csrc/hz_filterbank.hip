@@ -651,6 +651,9 @@ int fb_upload(hz_fb* h) {
     // LAZY band states of a stationary call follow from the coefficients and pre-amps it ran
     // with: materialise them before new ones reach the device
     if (h->resp.implicit && (h->dirty_coef || h->dirty_pin || h->tv_pending)) HZ_TRY(hz_fbi::fb_resp_materialize(h));
+    // streamed samples bring the smoothers up to date lazily, toward the targets they ran with:
+    // apply them before new targets (mix / boost) reach the device
+    if (h->dirty_pin || h->dirty_gin) HZ_TRY(hz_fbi::fb_stream_upkeep(h));
     HZ_TRY(hz_fbi::fb_tv_materialize(h));
     if (h->dirty_coef) {
         const int O = h->order;

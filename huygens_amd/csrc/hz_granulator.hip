@@ -462,10 +462,9 @@ int hz_gran_sample(hz_gran* h, double x, double* y) {
     if (h->list_dirty || h->list_min_end <= h->T) {   // grains started or ended: a new list version
         size_t cnt = 0;
         for (const auto& q : h->vg) cnt += q.size();
-        if (cnt > (size_t)hz_rt::kMaxGrains) {
-            hz::set_error("hz_gran_sample: %zu grains pending (the per-sample server holds %d)", cnt, hz_rt::kMaxGrains);
-            return HZ_E_UNSUPPORTED;
-        }
+        // the server caches the grain list in LDS (kMaxGrains); a denser texture takes the
+        // one-sample block call, which has no such cap (the list stays dirty until it fits)
+        if (cnt > (size_t)hz_rt::kMaxGrains) return hz_gran_process(h, &x, y, 1, nullptr, 0, nullptr);
         if (cnt > h->list_cap || !h->h_list) {
             if (h->h_list) HZ_TRY_HIP(hipHostFree(h->h_list));
             h->h_list = nullptr;

@@ -512,15 +512,19 @@ int srv_launch(Server* s) {
         if (us > 0 && us <= 10000000) a.idle = us * 100;
     }
     a.stall_req = a.stall = 0;
-    if (const char* e = std::getenv("HZ_RT_DEBUG_STALL")) {   // (tests) "request:microseconds", <= 2 s
+    s->answer_ms = 5000;
+    // test hooks, honoured only with HZ_RT_TEST_HOOKS=1 (a stray variable in production must not
+    // stall the server or shorten the host's wait): INTEGRATION.md section 4
+    const char* hooks = std::getenv("HZ_RT_TEST_HOOKS");
+    const bool test_hooks = hooks && hooks[0] == '1' && hooks[1] == 0;
+    if (const char* e = test_hooks ? std::getenv("HZ_RT_DEBUG_STALL") : nullptr) {   // (tests) "request:microseconds", <= 2 s
         long long rq = 0, us = 0;
         if (std::sscanf(e, "%lld:%lld", &rq, &us) == 2 && rq > 0 && us > 0 && us <= 2000000) {
             a.stall_req = rq;
             a.stall = us * 100;
         }
     }
-    s->answer_ms = 5000;
-    if (const char* e = std::getenv("HZ_RT_ANSWER_TIMEOUT_MS")) {   // (tests) the host's wait
+    if (const char* e = test_hooks ? std::getenv("HZ_RT_ANSWER_TIMEOUT_MS") : nullptr) {   // (tests) the host's wait
         const long long ms = std::atoll(e);
         if (ms > 0 && ms <= 5000) s->answer_ms = ms;
     }

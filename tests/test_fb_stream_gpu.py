@@ -181,3 +181,67 @@ def test_stream_c2_exact_config_per_block(gpu_lib):
 
 def sh_count(o):
     return o.N
+
+
+def test_stream_horizon_shrinks_after_coefficients(gpu_lib):
+    """ a bank streamed with a long horizon, then coefficients with a shorter one: the
+    partition-spectra rows past the new Q must be zeros again (they held the old response's
+    spectra), so every streamed block after the change still matches the restatement."""
+    from huygens_amd._lib import HZ_FB_PATH_STREAM
+    N = 128
+    g, o = _bank(N, R=0.999, k_p=0.01, k_g=0.01)
+    rng = np.random.default_rng(11)
+
+    def run():
+        x = rng.uniform(-1, 1, B).astype(np.float32).astype(np.float64)
+        _check(g.process(x), o.process(x))
+        return g.last_path()
+
+    K1 = None
+    for _ in range(120):
+        if run() == HZ_FB_PATH_STREAM:
+            K1 = g.response_info()[0]
+            break
+    assert K1 is not None
+    for _ in range(8):
+        assert run() == HZ_FB_PATH_STREAM
+    fwd, back = resonant_coefficients(N, 0.99, 1.0)
+    for fb in (g, o):
+        for n in range(N):
+            fb.coefficients(n, fwd[n], back[n])
+    paths = [run() for _ in range(40)]
+    K2 = g.response_info()[0]
+    assert 0 < K2 < K1, (K1, K2)
+    assert paths[-1] == HZ_FB_PATH_STREAM, paths
+    assert sum(p == HZ_FB_PATH_STREAM for p in paths) >= 10, paths
+    g.close()
+
+
+def test_stream_mix_mid_stream(gpu_lib):
+    """ mix() after streamed blocks: the gain smoothers glide from the gains the
+    streamed samples ran with (their lazy upkeep is applied before the new targets are
+    uploaded), per block against the restatement; the same for a one-band mix(n, v)."""
+    from huygens_amd._lib import HZ_FB_PATH_STREAM
+    N = 128
+    g, o = _bank(N, R=0.99, k_p=0.01, k_g=0.001)
+    rng = np.random.default_rng(12)
+
+    def run():
+        x = rng.uniform(-1, 1, B).astype(np.float32).astype(np.float64)
+        _check(g.process(x), o.process(x))
+        return g.last_path()
+
+    paths = [run() for _ in range(60)]
+    assert paths[-1] == HZ_FB_PATH_STREAM, paths
+    gains = rng.uniform(0.2, 1.5, N)
+    g.mix(gains)
+    o.mix(gains)
+    for _ in range(6):
+        run()
+    for _ in range(20):
+        run()
+    g.mix(5, 0.1)
+    o.mix(5, 0.1)
+    for _ in range(6):
+        run()
+    g.close()

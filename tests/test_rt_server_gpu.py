@@ -288,7 +288,7 @@ def test_unanswered_request_disables_server(gpu_lib):
     refused instead of posting behind it (a late answer must not advance the state twice), and the
     process still exits cleanly (the exit STOP is served after the late answer).  Runs in a child
     process: the server stays disabled for the process's life."""
-    env = dict(os.environ, HZ_RT_DEBUG_STALL="3:400000", HZ_RT_ANSWER_TIMEOUT_MS="50")
+    env = dict(os.environ, HZ_RT_TEST_HOOKS="1", HZ_RT_DEBUG_STALL="3:400000", HZ_RT_ANSWER_TIMEOUT_MS="50")
     p = subprocess.run([sys.executable, "-c", _STALL_SCRIPT], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=60)
     assert p.returncode == 0 and "stall ok" in p.stdout, p.stdout + p.stderr
@@ -338,3 +338,29 @@ def test_pinned_host_request_line(gpu_lib):
     p = subprocess.run([sys.executable, "-c", _HOST_LINE_SCRIPT], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=120)
     assert p.returncode == 0 and "host line ok" in p.stdout, p.stdout + p.stderr
+
+
+def test_granulator_per_sample_beyond_server_grain_cap(gpu_lib):
+    """ more grains pending than the server's LDS list holds (1,024): operator() falls
+    back to a one-sample block call instead of failing, and returns to the server once the list
+    fits again; outputs against the restatement."""
+    from huygens_amd import Granulator
+    size, P = SR, 1400
+    g, o = Granulator(size, P), OracleGranulator(size, P)
+    rng = np.random.default_rng(9)
+    x = np.sin(np.arange(4000) * 0.013) + 0.1 * rng.standard_normal(4000)
+    yg, yo = np.zeros(len(x)), np.zeros(len(x))
+    for t in range(len(x)):
+        yg[t] = g.sample(x[t])
+        o.write(x[t])
+        yo[t] = o.sample()
+        if t == 5:   # 1,200 grains of 40-60 ms at once: > 1,024 alive for ~2,000 samples
+            for k in range(1200):
+                par = (float(rng.uniform(0, 0.3)), float(rng.uniform(0.04, 0.06)), float(rng.uniform(0.5, 2.0)),
+                       float(rng.uniform(0.0, 0.01)))
+                assert g.request(*par, ticked=True) == o.request(*par)
+        o.tick()
+        if t == 500:
+            assert g.activity() == o.activity() == 1200
+    assert g.activity() == o.activity() == 0
+    assert np.max(np.abs(yg - yo)) <= 1e-12 * np.max(np.abs(yo))
