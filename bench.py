@@ -11,13 +11,15 @@ input already resident in HBM; the result is identical to 469 x {1024-sample blo
 (tests/test_filterbank_gpu.py::test_block_split_and_per_sample).  A streaming figure
 (one call per 1024-sample block) is reported beside it.
 
-Multi-GPU (torchrun, one process per GPU): the 4096 bands are split contiguously over ranks
-(each rank keeps its shard's band states).  Once the bank is stationary the
-stream is split by TIME: a step is one call of N x 10 s and every rank outputs its 10 s from the
-shared input with a K-sample halo, convolving with the whole bank's response (summed over the
-band shards by one all-reduce at setup) -- no data-path collective, weak scaling (`--gather`
-collects the shares on rank 0 inside the step).  Per-band calls (before the bank is stationary)
-sum the band shards' partial mixes to rank 0 with an RCCL reduce.
+Multi-GPU (one process per GPU): `bench.py --gpus N` outside a launcher reruns itself under
+`torch.distributed.run --nproc-per-node N` as a child process before any torch / HIP import and
+forwards rank 0's JSON line; under a launcher WORLD_SIZE must equal --gpus (else exit 2).  At
+N > 1 `value` is north_star's decomposition, STRONG scaling: a fixed 10 s call per step with the
+4096 bands partitioned over the ranks (each rank's engine on its own band shard) and the partial
+mixes summed to rank 0 by an RCCL reduce, src/filterbank.h:130's mixdown sum sharded (the reduce
+of one step overlaps the next step's compute, double-buffered).  The time-split stationary call
+(N x 10 s per step, each rank outputs its 10 s from the shared input with a K-sample halo; weak
+scaling, no data-path collective) is reported beside it as side.time_split_weak.
 """
 from __future__ import annotations
 
@@ -473,6 +475,65 @@ def torch_empty_like(t):
     return torch.empty_like(t)
 
 
+def launch_plan(gpus: int, env) -> tuple[str, str | None]:
+    """What `bench.py --gpus N` does in this environment (no torch / HIP import before it):
+    'run' (world matches), 'relaunch' (N > 1 and no launcher: rerun under torch.distributed.run),
+    or 'mismatch' (a launcher's WORLD_SIZE disagrees with --gpus: refuse, exit non-zero)."""
+    if gpus < 1:
+        return "mismatch", f"--gpus {gpus}: at least one GPU"
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return ("relaunch" if gpus > 1 else "run"), None
+    try:
+        world = int(ws)
+    except ValueError:
+        return "mismatch", f"WORLD_SIZE={ws!r} is not an integer"
+    if world != gpus:
+        return "mismatch", f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks"
+    return "run", None
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def relaunch_cmd(gpus: int, argv, port: int):
+    """one process per GPU on this node, rendezvous on 127.0.0.1"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def forward_child(cmd, env=None) -> int:
+    """Run `cmd` as a CHILD process (this process never touched the GPU, and nothing is exec'd over
+    it), echo its output to stderr as it arrives, and print its JSON result line(s) -- rank 0's
+    bench line -- on stdout.  Returns the child's exit status."""
+    import subprocess
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    for ln in p.stdout:
+        t = ln.strip()
+        if t.startswith("{") and '"metric"' in t:
+            print(t, flush=True)
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    return p.wait()
+
+
+def launcher(args) -> int | None:
+    """--gpus N: None = run here; otherwise the exit status to return (relaunched or refused)."""
+    plan, why = launch_plan(args.gpus, os.environ)
+    if plan == "run":
+        return None
+    if plan == "mismatch":
+        sys.stderr.write(f"bench.py: {why}\n")
+        return 2
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return forward_child(relaunch_cmd(args.gpus, sys.argv[1:], free_port()), env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -500,6 +561,14 @@ def main():
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "c6", "c7", "c8", "c9"], default="c2",
                     help="c2 = the BASELINE.json metric (default); c3/c4/c5 = the other SURVEY.md 8(d) rows; c6 = Granulator, c7 = Freezer, c8 = heterodyne chain, c9 = per-sample coefficient streams (8(f) rows 1-4)")
     args = ap.parse_args()
+    rc = launcher(args)   # --gpus N > 1 without a launcher: N ranks under torch.distributed.run
+    if rc is not None:
+        return rc
+    if os.environ.get("HZ_BENCH_DRY") == "1":   # (tests/test_bench_launcher_cpu.py) the launch alone
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps({"metric": "dry launch", "n_gpus": int(os.environ.get("WORLD_SIZE", "1")),
+                              "gpus_arg": args.gpus}), flush=True)
+        return 0
     if args.workload != "c2":
         return run_row(args)
 
@@ -550,90 +619,57 @@ def main():
         dist.all_reduce(t, op=op)
         return t.item()
 
-    # N > 1: once stationary, the ranks split the call by TIME (each convolves its share of the
-    # output blocks with the whole bank's response, summed over the band shards by one all-reduce
-    # at setup) and keep their own bands' states.  The engine switch is collective: the handles
-    # are armed on every rank in the same call (shard.arm_when_ready, one host all-reduce between
-    # untimed calls), never decided per rank.
+    # N > 1 (north_star's decomposition, `value`): a FIXED 10 s call per step, the 4096 bands
+    # partitioned over the ranks, each rank's partial mix summed to rank 0 by an RCCL reduce
+    # (src/filterbank.h:130's mixdown sum, sharded).  The reduce of step i runs on the collective
+    # stream while step i + 1 computes into the other output buffer (double-buffered: a buffer is
+    # reused only after its reduce completed, stream-ordered).  The time-split stationary call
+    # (weak scaling) is measured beside it (side.time_split_weak).
     tshard = False
-    if world > 1 and not args.general and args.response != 0:
-        def all_reduce_sum(h):
-            t = torch.from_numpy(np.ascontiguousarray(h)).to(dev)
-            dist.all_reduce(t)
-            return t.cpu().numpy()
-        tshard = set_time_shards(fb, rank, world, all_reduce_sum, lambda k: int(ar(k, dist.ReduceOp.MAX)))
-        all_reduce_min = lambda k: int(ar(k, dist.ReduceOp.MIN))   # noqa: E731
-    elif args.emulate_world > 1 and not args.general and args.response != 0:
-        # (1 GPU, diagnostics) rank 0 of a time-sharded job: the other shards' handles exist only
-        # to sum the whole bank's response; the others are taken to be ready when rank 0 is
-        others = []
-        for r in range(1, args.emulate_world):
-            ob, oc = shard_of(r, args.emulate_world)
-            o = Filterbank(2, N_BANDS, 0.1, 1.0, device=local, shard=(ob, oc))
-            for n in range(ob, ob + oc):
-                o.coefficients(n, fwd[n], back[n])
-            o.boost(np.ones(N_BANDS))
-            o.open()
-            o.response(8192)
-            others.append(o)
-        k_max = max([o.response_info()[0] for o in others])
-        red_calls = [0]
-
-        def emu_max(k):   # 1st call: the horizons; 2nd: the failure flags (the others' are 0)
-            red_calls[0] += 1
-            return max(k, k_max) if red_calls[0] == 1 else k
-        tshard = set_time_shards(fb, 0, args.emulate_world, lambda h: h + sum(o.response(len(h)) for o in others),
-                                 emu_max)
-        all_reduce_min = lambda k: k   # noqa: E731
-        for o in others:
-            o.close()
-
-    # Time-sharded stationary calls partition the stream: each rank produces the final output of
-    # its run of blocks from the shared input (a K-sample halo, no exchange), so a step at N > 1 is
-    # a call of N x 10 s with 10 s of output per rank -- weak scaling, no data-path collective
-    # (before the handles are armed, the per-band calls sum band shards with one reduce)
-    P_t = (world if world > 1 else max(1, args.emulate_world)) if tshard else 1
-    S = args.samples * P_t
-    gbuf = None   # ShareGather (--gather: collect the shares on rank 0 inside the step)
+    gbuf = None   # ShareGather (--gather: collect the time shares on rank 0 inside the step)
     armed = False
+    S = args.samples
     rng = np.random.default_rng(1234)
     x = torch.from_numpy(rng.uniform(-1, 1, S).astype(np.float32).astype(np.float64)).to(dev)
-    y = torch.empty_like(x)
+    ys = [torch.empty_like(x), torch.empty_like(x)]
+    y = ys[0]
+    works = [None, None]
+    nstep = [0]
+
+    def reduce_async(t):
+        if isinstance(dist, _HostDist):
+            dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+            return None
+        return dist.reduce(t, dst=0, op=dist.ReduceOp.SUM, async_op=True)
 
     def step():
-        nonlocal gbuf
-        fb.process_device(x.data_ptr(), y.data_ptr(), S)
+        k = nstep[0] & 1
+        nstep[0] += 1
+        if works[k] is not None:   # the reduce that last read this buffer (stream-ordered wait)
+            works[k].wait()
+            works[k] = None
+        fb.process_device(x.data_ptr(), ys[k].data_ptr(), S)
         if world > 1:
-            if armed:
-                # every rank holds the final samples of its share: nothing to exchange (--gather
-                # collects them on rank 0 inside the step: fixed-size slots, one gather)
-                if args.gather:
-                    if gbuf is None:
-                        from huygens_amd.shard import ShareGather
-                        gbuf = ShareGather(S, rank, world, y)
-                    gbuf(y, dist)
-            else:
-                dist.reduce(y, dst=0, op=dist.ReduceOp.SUM)
+            works[k] = reduce_async(ys[k])
 
-    def try_arm():
-        nonlocal armed
-        if tshard and not armed:
-            torch.cuda.synchronize(dev)
-            armed = arm_when_ready(fb, S, all_reduce_min)
+    def drain():
+        for k in (0, 1):
+            if works[k] is not None:
+                works[k].wait()
+                works[k] = None
 
     def barrier():
+        drain()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
 
     # Priming (untimed, before the W warmup steps): calls until the engine the run settles on is
-    # reached -- the smoothers converge during the first 10 s call (k_g = 1 s), the stationary engine
-    # needs K samples of converged history, and time-sharded ranks must be armed together.
+    # reached -- the smoothers converge during the first 10 s call (k_g = 1 s) and the stationary
+    # engine needs K samples of converged history (each rank decides for its own band shard).
     for i in range(8):
         step()
-        try_arm()
-        if (armed if tshard else fb.last_path() == HZ_FB_PATH_RESPONSE) or \
-                (i >= 2 and (args.general or args.response == 0 or not tshard)):
+        if fb.last_path() == HZ_FB_PATH_RESPONSE or (i >= 2 and (args.general or args.response == 0)):
             break
     for _ in range(args.warmup):
         step()
@@ -657,12 +693,12 @@ def main():
     horizon = fb.response_info()[0]
     fb.profile(False)
 
-    def timed(fn, warm, steps, n_samples, arm=False):
+    def timed(fn, warm, steps, n_samples, arm=None):
         """ms per step and band-samples/s (whole job, max over ranks) of `fn` after `warm` calls"""
         for _ in range(warm):
             fn()
             if arm:
-                try_arm()
+                arm()
         barrier()
         ts = time.perf_counter()
         for _ in range(steps):
@@ -676,30 +712,64 @@ def main():
 
     side = {}
     if resp and args.side_steps > 0:
-        armed = False
-        fb.set_response(HZ_FB_RESP_OFF)     # disarms: band shards + reduce at N > 1
-        side["per_band_engine"] = timed(step, 3, args.side_steps, S)
-        fb.set_response(HZ_FB_RESP_LAZY)
-        side["stationary_lazy_states"] = timed(step, 3, args.side_steps, S, arm=True)
-        armed = False
-        fb.set_response(HZ_FB_RESP_EAGER if args.response < 0 else args.response)
-    if world > 1 and args.side_steps > 0:
-        # north_star's decomposition: the bands partitioned over the GPUs, a FIXED 10 s call per
-        # step (strong scaling), each rank's partial mix summed to rank 0 by an RCCL reduce
-        # (each rank's own engine choice: it outputs all samples of its bands either way)
-        armed = False
-        fb.set_bank_response(np.zeros(0))
-        S1 = args.samples
-
-        def step_bp():
-            fb.process_device(x.data_ptr(), y.data_ptr(), S1)
-            dist.reduce(y[:S1], dst=0, op=dist.ReduceOp.SUM)
-        side["band_partition"] = timed(step_bp, 4, args.side_steps, S1)
         fb.set_response(HZ_FB_RESP_OFF)
-        side["band_partition_per_band_engine"] = timed(step_bp, 3, args.side_steps, S1)
-        for k in ("band_partition", "band_partition_per_band_engine"):
-            side[k]["note"] = (f"{N_BANDS} bands over {world} GPUs ({cnt} per GPU), one {S1}-sample call per "
-                               "step, partial mixes summed to rank 0 by RCCL reduce (strong scaling)")
+        side["per_band_engine"] = timed(step, 3, args.side_steps, S)
+        if world > 1:
+            side["per_band_engine"]["note"] = (f"{N_BANDS} bands over {world} GPUs ({cnt} per GPU), per-band "
+                                               "engines, partial mixes reduced to rank 0 (strong scaling)")
+        fb.set_response(HZ_FB_RESP_LAZY)
+        side["stationary_lazy_states"] = timed(step, 3, args.side_steps, S)
+        fb.set_response(HZ_FB_RESP_EAGER if args.response < 0 else args.response)
+        drain()
+    if world > 1 and args.side_steps > 0 and not args.general and args.response != 0:
+        # weak-scaling figure: once stationary, a step is ONE call of N x 10 s split by TIME -- each
+        # rank convolves its run of output blocks with the whole bank's response (the band shards'
+        # responses summed by one all-reduce at setup) from the shared input with a K-sample halo,
+        # and keeps its own bands' states; no data-path collective (--gather collects the shares)
+        def all_reduce_sum(hv):
+            t = torch.from_numpy(np.ascontiguousarray(hv)).to(dev)
+            dist.all_reduce(t)
+            return t.cpu().numpy()
+        barrier()
+        tshard = set_time_shards(fb, rank, world, all_reduce_sum, lambda k: int(ar(k, dist.ReduceOp.MAX)))
+        if tshard:
+            St = S * world
+            xt = torch.from_numpy(np.random.default_rng(4321).uniform(-1, 1, St).astype(np.float32)
+                                  .astype(np.float64)).to(dev)
+            yt = torch.empty_like(xt)
+
+            def step_ts():
+                nonlocal gbuf
+                fb.process_device(xt.data_ptr(), yt.data_ptr(), St)
+                if armed and args.gather:
+                    if gbuf is None:
+                        from huygens_amd.shard import ShareGather
+                        gbuf = ShareGather(St, rank, world, yt)
+                    gbuf(yt, dist)
+                elif not armed:   # (before arming: band shards, partial mixes reduced)
+                    dist.reduce(yt, dst=0, op=dist.ReduceOp.SUM)
+
+            def try_arm():
+                nonlocal armed
+                if not armed:
+                    torch.cuda.synchronize(dev)
+                    armed = arm_when_ready(fb, St, lambda k: int(ar(k, dist.ReduceOp.MIN)))
+            for _ in range(8):
+                step_ts()
+                try_arm()
+                if armed:
+                    break
+            tw = timed(step_ts, 3, args.side_steps, St, arm=try_arm)
+            tw.update(scaling="weak", armed=armed, samples_per_step=St, samples_per_gpu=S,
+                      note=(f"one {world} x 10 s call per step split by time: each GPU outputs its own 10 s of "
+                            f"all {N_BANDS} bands (whole-bank response, K-sample halo), band states sharded; "
+                            "no data-path collective" + (" (+ gather to rank 0)" if args.gather else "")))
+            side["time_split_weak"] = tw
+            armed = False
+            fb.arm_time_shard(False)
+            fb.set_bank_response(np.zeros(0))
+            del xt, yt
+        barrier()
     # the engine's GPU time per call: the event sum (stationary path: forward + MAC kernels, then the
     # inverse kernel carrying the band-state pass)
     eng_ms = seg_ms + mix_ms + red_ms
@@ -714,11 +784,7 @@ def main():
     # (hz_fb_stream.hip: one launch per block); the per-band engine's rate is measured beside it
     stream_rate, stream_detail = None, {}
     if args.stream_blocks > 0:
-        armed = False
-        if tshard:   # band shards stream their own bands' response; the mixes are reduced per block
-            fb.arm_time_shard(False)
-            fb.set_bank_response(np.zeros(0))
-        B = 1024
+        B = 1024   # (N > 1: band shards stream their own bands' response; the mixes are reduced per block)
         nb = min(args.stream_blocks, S // B)
 
         def stream_blocks(n_blocks):
@@ -810,8 +876,8 @@ def main():
     value = total_band_samples / elapsed
     if rank == 0:
         launch_avg_s = (eng_ms_max / 1e3) / max(1, launches)    # whole engine step, per process() call
-        out_samples = S // P_t if resp else S                   # this GPU's outputs per step
-        bs_launch = (N_BANDS if resp else cnt) * out_samples     # band-samples of one call on this GPU
+        out_samples = S                                         # this GPU's outputs per step (its bands)
+        bs_launch = cnt * out_samples                           # band-samples of one call on this GPU
         # ---- dominant kernel (roofline): the stationary engine's inverse kernel, which carries the
         # band-state pass (hz_fb_state.h: MFMA, ~96% of its flops) beside the output blocks' inverse
         # transforms; the state kernel of the per-band LTI engine; the mix kernel of the general
@@ -856,7 +922,7 @@ def main():
         step_pmc = sum(flops.values()) if flops else None
         step_fl = step_pmc or step_model
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:   # rank 0's host cores, at every N (the other ranks wait)
             cpu = cpu_baseline(fwd, back)
         line = {
             "metric": "band-samples/s (bands x frames/s) for 4096-band Filterbank",
@@ -867,39 +933,29 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak" if P_t > 1 and resp else "strong",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic white noise uniform[-1,1) (float32 -> double), seed 1234, resident in HBM",
             "config": {"workload": "C2 Filterbank<double>(order 2, 4096 bands), resonant band-pass "
-                                   "f_i=0.5(i+1)SR/4096 R=0.999, boost 1 + open, k_p=0.1 k_g=1"
-                                   + (f", {P_t} x 10 s per step split by time" if P_t > 1 and resp else ""),
+                                   "f_i=0.5(i+1)SR/4096 R=0.999, boost 1 + open, k_p=0.1 k_g=1",
                        "samples_per_step": S, "samples_per_gpu": out_samples,
                        "call": f"one process() call of {S} samples per step (== {S // 1024} x 1024-sample "
                                f"blocks in result; the 1024-block streaming rate is `streaming`)",
                        "partition": 2048 if resp else None,
                        "bands": N_BANDS, "bands_per_gpu": cnt,
-                       "parallelism": ("single GPU, all bands, no collective" if world == 1 and P_t == 1 else
-                                       f"stream split by time x{P_t}: each GPU outputs 10 s of the N x 10 s "
-                                       f"call from the shared input with a {horizon}-sample halo (whole-bank "
-                                       f"response, one all-reduce at setup), band states sharded x{P_t}; no "
-                                       f"data-path collective" + (" (+ gather to rank 0)" if args.gather else "")
-                                       if tshard and resp else f"bands sharded x{world}, RCCL reduce")},
+                       "parallelism": ("single GPU, all bands, no collective" if world == 1 else
+                                       f"bands partitioned x{world} ({cnt} per GPU), partial mixes summed to "
+                                       "rank 0 by an RCCL reduce per step (overlapped with the next step's "
+                                       "compute, double-buffered)")},
             "rehearsal": (f"{world} ranks on one GPU, collectives over gloo through host copies "
                           "(HZ_BENCH_REHEARSAL=1): the N > 1 code path, not an N-GPU figure")
                          if world > 1 and os.environ.get("HZ_BENCH_REHEARSAL") == "1" else None,
-            # N > 1: which decomposition `value` is, and north_star's beside it
             "decomposition": None if world == 1 else {
-                "value": (f"WEAK scaling: a step is one {world} x 10 s call split by time, each GPU outputs "
-                          f"its own 10 s of all {N_BANDS} bands (the work per GPU is fixed, the job grows with N)"
-                          if P_t > 1 and resp else
-                          f"STRONG scaling: a fixed 10 s call per step, bands sharded x{world}, RCCL reduce"),
-                "north_star_band_partition": dict(side.get("band_partition") or {},
-                                                  scaling="strong",
-                                                  what=(f"north_star's decomposition: a FIXED 10 s call per step, "
-                                                        f"{N_BANDS} bands partitioned over {world} GPUs, partial "
-                                                        "mixes summed to rank 0 by an RCCL reduce"))
-                if side.get("band_partition") else "not measured (--side-steps 0)",
+                "value": (f"STRONG scaling (north_star's decomposition): a FIXED 10 s call per step, "
+                          f"{N_BANDS} bands partitioned over {world} GPUs, each rank's partial mix summed "
+                          "to rank 0 by an RCCL reduce (src/filterbank.h:130's mixdown, sharded)"),
+                "time_split_weak": side.get("time_split_weak") or "not measured (--side-steps 0)",
             },
             "engine": "stationary (bank response convolution, eager band states)" if resp
                       else "per-band LTI" if lti else "per-band general",
@@ -1011,4 +1067,4 @@ def run_row(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)
