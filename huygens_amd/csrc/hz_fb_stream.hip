@@ -630,6 +630,9 @@ int fb_stream_track(hz_fb* h, const double* d_in, long n, bool conv) {
         R.run = 0;
         return HZ_OK;
     }
+    // a new horizon (coefficients changed: R.run restarted at 0) re-lays the ring out for it; the
+    // samples tracked into the old layout are no longer history
+    if (S.line_hist) HZ_TRY(stream_setup(h));
     if (!S.line_hist) {
         if (R.run > 0) {
             HZ_TRY(hist_to_line(h));

@@ -95,6 +95,7 @@ orc_bowl* orc_bowl_create(int overtones, const double* f, const double* a, const
                           int is_float);
 void      orc_bowl_destroy(orc_bowl* b);
 void      orc_bowl_trigger(orc_bowl* b);
+void      orc_bowl_seek(orc_bowl* b, long ticks);
 int       orc_bowl_fill(orc_bowl* b, float* buffer, long bsize);
 void      orc_bowl_render(orc_bowl* b, double* out, long n);
 

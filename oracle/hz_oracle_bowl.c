@@ -55,6 +55,15 @@ void orc_bowl_destroy(orc_bowl* b)
 
 void orc_bowl_trigger(orc_bowl* b) { b->phase = 0; b->phasef = 0; }   /* bowl.h:25-28 */
 
+/* the state after trigger() and `ticks` samples: the phase counter alone (bowl.h:42-47, 61:
+ * phase++ from 0, exact in float below 2^24), so time segments of one signal can be restated
+ * independently (tests/test_fullsize_gpu.py) */
+void orc_bowl_seek(orc_bowl* b, long ticks) {
+    b->phase = 0; b->phasef = 0;
+    if (ticks < (1L << 24)) { b->phase = (double)ticks; b->phasef = (float)ticks; return; }
+    for (long j = 0; j < ticks; j++) { b->phase++; b->phasef++; }
+}
+
 /* bowl.h:35-36 / 55-56, T = double, form = cycle (wave.h:147) */
 static double sample_d(orc_bowl* b)
 {

@@ -11,6 +11,7 @@ _SIGS = {
     "orc_bowl_create": (VP, [I, PD, PD, PD, I, I]),
     "orc_bowl_destroy": (None, [VP]),
     "orc_bowl_trigger": (None, [VP]),
+    "orc_bowl_seek": (None, [VP, L]),
     "orc_bowl_fill": (I, [VP, C.POINTER(C.c_float), L]),
     "orc_bowl_render": (None, [VP, PD, L]),
 }
@@ -32,6 +33,10 @@ class OracleBowl:
 
     def trigger(self):
         self.l.orc_bowl_trigger(self.h)
+
+    def seek(self, ticks):
+        """the state after trigger() and `ticks` samples (the phase counter)"""
+        self.l.orc_bowl_seek(self.h, int(ticks))
 
     def fill(self, n):
         out = np.zeros(n, dtype=np.float32)

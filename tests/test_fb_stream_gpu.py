@@ -209,7 +209,13 @@ def test_stream_horizon_shrinks_after_coefficients(gpu_lib):
     for fb in (g, o):
         for n in range(N):
             fb.coefficients(n, fwd[n], back[n])
-    paths = [run() for _ in range(40)]
+    log = []
+    for _ in range(40):
+        x = rng.uniform(-1, 1, B).astype(np.float32).astype(np.float64)
+        err, _ = block_errors(g.process(x), o.process(x))
+        log.append((g.last_path(), float(err.max())))
+    assert max(e for _, e in log) <= TIGHT, log
+    paths = [p for p, _ in log]
     K2 = g.response_info()[0]
     assert 0 < K2 < K1, (K1, K2)
     assert paths[-1] == HZ_FB_PATH_STREAM, paths
