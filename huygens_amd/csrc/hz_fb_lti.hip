@@ -1241,8 +1241,9 @@ static long fb_lti_horizon(const hz_fb* h, long double bound = 0x1p-64L) {
         for (int s = 0; s < 12; ++s) mul(P, P, P);   // M^4096
         for (int i = 0; i < O; ++i)
             for (int j = 0; j < O; ++j) Q[i][j] = (i == j);
+        // up to 2^21 samples: R = 0.9999 resonators (tests/eigen.cpp:26) forget in ~0.5 M
         long kb = -1;
-        for (int it = 1; it <= 64; ++it) {
+        for (int it = 1; it <= 512; ++it) {
             mul(Q, P, Q);
             ld nrm = 0;
             for (int i = 0; i < O; ++i) {
