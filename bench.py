@@ -551,6 +551,8 @@ def main():
     ap.add_argument("--general", action="store_true", help="force the general engine (no converged fast path)")
     ap.add_argument("--response", type=int, default=-1,
                     help="stationary engine: 0 off (per-band engines only), 1 eager (default), 2 lazy")
+    ap.add_argument("--resp-engine", type=int, default=-1,
+                    help="(A/B) stationary long calls: 1 column-split (default), 0 three-kernel path")
     ap.add_argument("--gather", action="store_true",
                     help="N > 1, time-sharded stationary calls: gather the shares on rank 0 inside each step")
     ap.add_argument("--side-steps", type=int, default=50,
@@ -611,6 +613,8 @@ def main():
         fb.set_path(HZ_FB_PATH_GENERAL)
     if args.response >= 0:
         fb.set_response(args.response)
+    if args.resp_engine >= 0:
+        fb.tune_response_engine(bool(args.resp_engine))
     stream = torch.cuda.current_stream(dev)
     fb.set_stream(stream.cuda_stream)
 

@@ -101,6 +101,8 @@ _SIGS = {
     "hz_fb_lti_last_chunk": (I, [VP, C.POINTER(C.c_int)]),
     "hz_fb_set_response": (I, [VP, I]),
     "hz_fb_tune_response": (I, [VP, L, L]),
+    "hz_fb_tune_response_engine": (I, [VP, I]),
+    "hz_fb_response_engine": (I, [VP, C.POINTER(I), C.POINTER(I)]),
     "hz_fb_response_info": (I, [VP, C.POINTER(L), C.POINTER(L), C.POINTER(I), C.POINTER(L)]),
     "hz_fb_get_response": (I, [VP, PD, L]),
     "hz_fb_set_bank_response": (I, [VP, PD, L]),

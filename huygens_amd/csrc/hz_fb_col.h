@@ -1,0 +1,277 @@
+// hz_fb_col.h -- the stationary engine's column-split convolution (included by hz_fb_resp.hip).
+//
+// The same overlap-save convolution as the three-kernel path (P = 2048-sample partitions, F =
+// 4096-point real transforms; hz_fb_resp.hip), with every transform split four-step, F = 64 x 64,
+// so that the window spectra never leave the workgroup that computes them
+// (tests/resp_col_model.py restates this schedule and checks it against a direct convolution):
+//
+//   resp_col_kernel   workgroup = (unit, range of kWB output blocks).  A unit is four columns
+//                     c0 + 16 i (bins k = c + 64 k2) sharing one pass over the samples:
+//                       stage 1  D_s^c[n2] = sum_{m<32} u[sP + 64 m + n2] W64^(mc) for the segments
+//                                s of the range and its Q-partition halo (a radix-4 step over m
+//                                gives the four columns from one set of loads), into LDS;
+//                       stage 3  Z_j = FFT64_n2(W4096^(n2 c) (D_j + (-1)^c D_{j+1})) per window,
+//                                across the wave's lanes, in place in LDS (wave i = column i);
+//                       MAC      Y_b = sum_p H_p Z_{b+Q-1-p} per bin (lane), Z in a register ring;
+//                       inverse  T_b^c[n1] = W4096^(-n1 c) IFFT64_k2(Y_b) -> HBM, [b][slot][n1].
+//   resp_comb_kernel  one workgroup per output block: x[n1 + 64 n2] = sum_c W64^(-n2 c) T^c[n1]
+//                     (T^(64-c) = conj T^c), the block's samples n2 >= 32; its threads also do
+//                     the history / smoother / x-history upkeep, and the band-state pass rides in
+//                     it as extra workgroups (as in resp_inv_kernel).
+// Units: c0 = 1..7 hold columns c0, c0+16, c0+32 (= conj of 32-c0), c0+48 (= conj of 16-c0);
+// c0 = 0 holds 0, 16, 32 and c0 = 8 holds 8, 24: the 33 columns 0..32 up to conjugation.
+#pragma once
+
+namespace hz_col {
+
+constexpr int kP = 2048;
+constexpr int kUnits = 9;
+constexpr int kSlots = 4 * kUnits;   // H / T slots: 4u + i (unused slots of units 7, 8 never read)
+constexpr int kWB = 10;              // output blocks per range (B = 235 -> 24 ranges, 3 per XCD)
+
+__host__ __device__ constexpr int unit_c0(int u) { return u < 7 ? u + 1 : (u == 7 ? 0 : 8); }
+__host__ __device__ constexpr int unit_ncol(int u) { return u < 7 ? 4 : (u == 7 ? 3 : 2); }
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 cmulc(double2 a, double2 b) {   // conj(a) b
+    return make_double2(a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 shfl_xor2(double2 v, int m) {
+    return make_double2(__shfl_xor(v.x, m), __shfl_xor(v.y, m));
+}
+__device__ __forceinline__ int brev6(int l) { return (int)(__builtin_bitreverse32((unsigned)l) >> 26); }
+
+// 64-point transforms across a wave's lanes.  tw4k = W4096^k (k < 4096, long double on the host).
+struct Fft64 {
+    double2 w[6];   // stage q (span s = 32 >> q): W64^((l & (s-1)) 32 / s)
+    __device__ __forceinline__ void init(const double2* __restrict__ tw4k, int l) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            const int s = 32 >> q;
+            w[q] = tw4k[64 * ((l & (s - 1)) * (32 / s))];
+        }
+    }
+    // forward (W64 = e^{-2 pi i / 64}), decimation in frequency: lane n in, lane l out holds X[brev6(l)]
+    __device__ __forceinline__ double2 fwd(double2 v, int l) const {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            const int s = 32 >> q;
+            const double2 o = shfl_xor2(v, s);
+            v = (l & s) ? cmul(csub(o, v), w[q]) : cadd(v, o);
+        }
+        return v;
+    }
+    // inverse (unnormalised), decimation in time: lane l holds Y[brev6(l)] in, lane n out
+    __device__ __forceinline__ double2 inv(double2 v, int l) const {
+#pragma unroll
+        for (int q = 5; q >= 0; --q) {
+            const int s = 32 >> q;
+            const double2 o = shfl_xor2(v, s);
+            v = (l & s) ? csub(o, cmulc(w[q], v)) : cadd(v, cmulc(w[q], o));
+        }
+        return v;
+    }
+};
+
+struct ColArgs {
+    const double* hist;   // [K] the K inputs before the call
+    const double* x;      // [n]
+    long K, off, n_out;   // horizon; the launch's first output sample and count (time shards)
+    int Q, B, NR;         // partitions, output blocks, ranges of kWB blocks
+    const double2* tw4k;  // [4096] W4096^k
+    const double2* Hc;    // [kSlots][Q][64] H_p at bin c + 64 brev6(l) (lane order), / F
+    double2* T;           // [B][kSlots][64] inverse columns
+};
+
+template <int QP>
+struct ColLds {
+    double2 z[4][kWB + QP][64];   // D of the segments, then Z of the windows, per column
+};
+
+// u = [hist | x | 0 ...] indexed from the launch's first output sample: one segment's source
+__device__ __forceinline__ const double* col_segment(const ColArgs& a, long s, long* lim) {
+    const long m0 = s * kP + a.off;
+    if (m0 < a.K) {   // K and off are multiples of P: the segment lies in the history
+        *lim = kP;
+        return a.hist + m0;
+    }
+    *lim = a.off + a.n_out - (m0 - a.K);
+    return a.x + (m0 - a.K);
+}
+
+template <int QP>
+__device__ __forceinline__ void col_group(const ColArgs& a, int u, int r, ColLds<QP>& L) {
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int c0 = unit_c0(u), ncol = unit_ncol(u);
+    const int b0 = r * kWB;
+    // stage-1 twiddles (lane-uniform): W16^(q c0) (rows m = 4q + rr, q < 8) and W64^(rr c0)
+    double2 t16[8], t64[4];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t16[q] = a.tw4k[256 * ((q * c0) & 15)];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) t64[rr] = a.tw4k[64 * ((rr * c0) & 63)];
+    // ---- stage 1: segments s_l = w, w + 4, ... of [0, kWB + QP), next segment's loads in flight
+    constexpr int NS = kWB + QP;
+    double cur[32], nxt[32];
+    auto load = [&](int sl, double (&v)[32]) {
+        long lim;
+        const double* src = col_segment(a, (long)b0 + sl, &lim);
+#pragma unroll
+        for (int m = 0; m < 32; ++m) {
+            const int i = 64 * m + l;
+            v[m] = i < lim ? src[i] : 0.0;
+        }
+    };
+    if (w < NS) load(w, nxt);
+    for (int sl = w; sl < NS; sl += 4) {
+#pragma unroll
+        for (int m = 0; m < 32; ++m) cur[m] = nxt[m];
+        if (sl + 4 < NS) load(sl + 4, nxt);
+        double2 P[4];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            double2 acc = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                acc.x = fma(cur[4 * q + rr], t16[q].x, acc.x);
+                acc.y = fma(cur[4 * q + rr], t16[q].y, acc.y);
+            }
+            P[rr] = cmul(acc, t64[rr]);
+        }
+        // D^{c0 + 16 i} = sum_rr W4^(rr i) P_rr, W4 = -i
+        const double2 s02 = cadd(P[0], P[2]), d02 = csub(P[0], P[2]);
+        const double2 s13 = cadd(P[1], P[3]), d13 = csub(P[1], P[3]);
+        L.z[0][sl][l] = cadd(s02, s13);
+        L.z[1][sl][l] = make_double2(d02.x + d13.y, d02.y - d13.x);   // d02 - i d13
+        L.z[2][sl][l] = csub(s02, s13);
+        if (ncol > 3) L.z[3][sl][l] = make_double2(d02.x - d13.y, d02.y + d13.x);   // d02 + i d13
+    }
+    __syncthreads();
+    if (w >= ncol) return;   // (units 7, 8: fewer columns than waves)
+    const int c = c0 + 16 * w;
+    Fft64 f;
+    f.init(a.tw4k, l);
+    // ---- stage 3, in place: window j_l = segments j_l, j_l + 1
+    {
+        const double2 tn = a.tw4k[l * c];   // W4096^(n2 c), n2 = l
+        const double sg = (c0 & 1) ? -1.0 : 1.0;
+        double2 dn = L.z[w][0][l];
+        for (int j = 0; j < NS - 1; ++j) {
+            const double2 d0 = dn;
+            dn = L.z[w][j + 1][l];
+            const double2 A = make_double2(fma(sg, dn.x, d0.x), fma(sg, dn.y, d0.y));
+            L.z[w][j][l] = f.fwd(cmul(A, tn), l);   // lane l: bin k2 = brev6(l)
+        }
+    }
+    // ---- MAC: Y_b = sum_p H_p Z_{b+Q-1-p} for the range's kWB blocks (the wave's own LDS rows:
+    // no barrier), window b + t in ring slot (b + t) % kWB at step t = Q - 1 - p
+    const double2* hc = a.Hc + ((long)(4 * u + w) * a.Q) * 64 + l;
+    double2 Y[kWB], ring[kWB];
+#pragma unroll
+    for (int b = 0; b < kWB; ++b) {
+        Y[b] = make_double2(0.0, 0.0);
+        ring[b] = L.z[w][b][l];
+    }
+    double2 hv[QP];
+#pragma unroll
+    for (int p = 0; p < QP; ++p) hv[p] = hc[(long)p * 64];
+#pragma unroll
+    for (int ts = 0; ts < QP; ++ts) {
+        const double2 h = hv[QP - 1 - ts];
+#pragma unroll
+        for (int b = 0; b < kWB; ++b) {
+            const double2 z = ring[(b + ts) % kWB];
+            Y[b].x = fma(h.x, z.x, fma(-h.y, z.y, Y[b].x));
+            Y[b].y = fma(h.x, z.y, fma(h.y, z.x, Y[b].y));
+        }
+        if (ts + 1 < QP) ring[ts % kWB] = L.z[w][kWB + ts][l];
+    }
+    // ---- inverse columns of the range's blocks -> T[b][slot][n1]
+    const double2 tn1 = a.tw4k[l * c];   // W4096^(n1 c), n1 = l (conjugated below)
+#pragma unroll
+    for (int b = 0; b < kWB; ++b) {
+        const int bg = b0 + b;
+        const double2 v = cmulc(tn1, f.inv(Y[b], l));
+        if (bg < a.B) a.T[((long)bg * kSlots + 4 * u + w) * 64 + l] = v;
+    }
+}
+
+// bin c + 64 brev6(l) of the full-spectrum partition spectra from the three-kernel layout
+// (H [Qp][2048] complex, Hn [Qp] bin 2048): Hc [kSlots][Q][64]; grid (kSlots, Q), 64 threads
+__global__ __launch_bounds__(64) void resp_hcol_kernel(const double2* __restrict__ H, const double* __restrict__ Hn,
+                                                      int Q, double2* __restrict__ Hc) {
+    const int slot = blockIdx.x, p = blockIdx.y, l = threadIdx.x;
+    const int u = slot / 4, i = slot % 4;
+    if (i >= unit_ncol(u)) return;
+    const int k = unit_c0(u) + 16 * i + 64 * brev6(l);
+    double2 v;
+    if (k < kP) v = H[(long)p * kP + k];
+    else if (k == kP) v = make_double2(Hn[p], 0.0);
+    else {
+        const double2 m = H[(long)p * kP + (2 * kP - k)];
+        v = make_double2(m.x, -m.y);
+    }
+    Hc[((long)slot * Q + p) * 64 + l] = v;
+}
+
+// the combine's column table: for c < 64 the slot holding T^c (bit 7 set: conj of that slot's
+// T^(64-c)); built on the host
+inline void col_map(unsigned char (&m)[64]) {
+    for (int c = 0; c < 64; ++c) m[c] = 0xff;
+    for (int u = 0; u < kUnits; ++u)
+        for (int i = 0; i < unit_ncol(u); ++i) m[unit_c0(u) + 16 * i] = (unsigned char)(4 * u + i);
+    for (int c = 1; c < 64; ++c)
+        if (m[c] == 0xff) m[c] = (unsigned char)(m[64 - c] | 0x80);
+}
+
+struct CombLds {
+    double2 ts[kSlots][64];   // the block's inverse columns
+    double out[kP];           // its samples, [n2 - 32][n1]
+};
+
+// one output block: x[n1 + 64 n2] = sum_c W64^(-n2 c) V^c[n1] for n2 >= 32, two n1 per transform
+// (V^c[q] + i V^c[q + 32]: both outputs real); columns 0 and 32 are real (imaginary roundoff
+// dropped)
+__device__ __forceinline__ void comb_block(const double2* __restrict__ T, const unsigned char* __restrict__ cmap,
+                                           const double2* __restrict__ tw4k, long b, CombLds& L,
+                                           double* __restrict__ out, long n_out) {
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const double2* src = T + b * kSlots * 64;
+#pragma unroll
+    for (int i = 0; i < kSlots * 64 / 256; ++i) (&L.ts[0][0])[t + 256 * i] = src[t + 256 * i];
+    const int e = cmap[l];
+    const int slot = e & 0x7f;
+    const bool cj = (e & 0x80) != 0, re_only = (l & 31) == 0;
+    Fft64 f;
+    f.init(tw4k, l);
+    __syncthreads();
+    for (int q = 8 * w; q < 8 * w + 8; ++q) {
+        double2 va = L.ts[slot][q], vb = L.ts[slot][q + 32];
+        if (cj) {
+            va.y = -va.y;
+            vb.y = -vb.y;
+        }
+        if (re_only) va.y = vb.y = 0.0;
+        // IDFT(V) = conj(DFT(conj V)), V = va + i vb
+        const double2 cv = make_double2(va.x - vb.y, -(va.y + vb.x));
+        const double2 xv = f.fwd(cv, l);   // lane l: n2 = brev6(l)
+        const int n2 = brev6(l);
+        if (n2 >= 32) {
+            L.out[(n2 - 32) * 64 + q] = xv.x;          // Re: n1 = q
+            L.out[(n2 - 32) * 64 + q + 32] = -xv.y;    // Im (conjugated back): n1 = q + 32
+        }
+    }
+    __syncthreads();
+    const long t0 = b * kP;
+#pragma unroll
+    for (int i = 0; i < kP / 256; ++i) {
+        const long k = t + 256 * i;
+        if (t0 + k < n_out) out[t0 + k] = L.out[k];
+    }
+}
+
+}  // namespace hz_col

@@ -189,6 +189,16 @@ struct hz_fb {
         double* d_Y = nullptr;           // [B][2048] complex output spectra
         size_t Y_cap = 0;
         double* d_tw = nullptr;          // W_4096^k, k < 2048 (complex)
+        // column-split path (hz_fb_col.h): W_4096^k for k < 4096, H in column layout, the inverse
+        // columns T of a call, the combine's column map
+        bool col_on = true;              // hz_fb_tune_response_engine
+        int last_engine = 0;             // 0 three-kernel, 1 column-split (last stationary call)
+        double* d_tw4k = nullptr;
+        double* d_Hc = nullptr;
+        size_t Hc_cap = 0;
+        double* d_T = nullptr;
+        size_t T_cap = 0;
+        unsigned char* d_cmap = nullptr;
         double* d_sop = nullptr;         // band-state pass: pin E operands (fb_state_prepare)
         size_t sop_cap = 0;
         double* d_spart = nullptr;       // band-state pass: segment partials, arrival counters

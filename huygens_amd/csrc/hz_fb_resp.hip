@@ -35,6 +35,7 @@
 #include "hz_fb_impl.h"
 #include "hz_fb_state.h"
 #include "hz_fft2k.h"
+#include "hz_fb_col.h"
 
 namespace {
 
@@ -334,6 +335,25 @@ MacKernel pick_mac(int Qp) {
 }
 typedef void (*RespKernel)(RespArgs, hz_state::StateArgs);
 
+// history after the call, smoothers' closed form, x history; a time-range shard's zeros outside
+// its range (threads of the B output-block workgroups)
+__device__ __forceinline__ void resp_upkeep(const RespArgs& a, long b) {
+    const int t = threadIdx.x;
+    const long g = b * blockDim.x + t, stride = (long)a.B * blockDim.x;
+    // a time-range shard leaves zeros outside its range: the ranks' outputs sum to the call's
+    for (long i = g; i < a.n - a.n_out; i += stride) a.out[i < a.off ? i : i + a.n_out] = 0.0;
+    for (long i = g; i < a.K; i += stride) {
+        const long m = a.n + i;
+        a.hist_next[i] = m < a.K ? a.hist[m] : a.x[m - a.K];
+    }
+    for (long n = g; n < a.N; n += stride) {
+        const double P0 = a.pg[2 * n], G0 = a.pg[2 * n + 1], pb = a.pin[n], gb = a.gin[n];
+        a.pg_next[2 * n] = pb + a.sp_n * (P0 - pb);
+        a.pg_next[2 * n + 1] = gb + a.sg_n * (G0 - gb);
+    }
+    if (g < a.O) a.xhist_next[g] = a.x[a.n - 1 - g];
+}
+
 // output block b: the merge of Y_b into Zh' = E' + i O' (E' = Y[k] + conj Y[kH-k],
 // O' = (Y[k] - conj Y[kH-k]) W^-k; Zh'[kH-k] = conj E' + i conj O'), the inverse 2048-point FFT,
 // out[bP + 2r (+1)] = Re (Im) z[kH/2 + r] (the last P samples of the window's circular
@@ -406,24 +426,46 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         if (t0 < a.n_out) a.out[a.off + t0] = vr[i];
         if (t0 + 1 < a.n_out) a.out[a.off + t0 + 1] = vi[i];
     }
-    // state upkeep (the forward kernel, the last reader of hist, has finished)
-    const long g = b * blockDim.x + t, stride = (long)a.B * blockDim.x;
-    // a time-range shard leaves zeros outside its range: the ranks' outputs sum to the call's
-    for (long i = g; i < a.n - a.n_out; i += stride) a.out[i < a.off ? i : i + a.n_out] = 0.0;
-    for (long i = g; i < a.K; i += stride) {
-        const long m = a.n + i;
-        a.hist_next[i] = m < a.K ? a.hist[m] : a.x[m - a.K];
-    }
-    for (long n = g; n < a.N; n += stride) {
-        const double P0 = a.pg[2 * n], G0 = a.pg[2 * n + 1], pb = a.pin[n], gb = a.gin[n];
-        a.pg_next[2 * n] = pb + a.sp_n * (P0 - pb);
-        a.pg_next[2 * n + 1] = gb + a.sg_n * (G0 - gb);
-    }
-    if (g < a.O) a.xhist_next[g] = a.x[a.n - 1 - g];
+    resp_upkeep(a, b);
 #ifdef HZ_DIAG_STAMPS
     if (stp && t == 0) stp[1] = stp[2] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
+
+// column-split path: the inverse columns of the range's blocks (hz_fb_col.h).  (The band-state
+// pass stays in the combine kernel: this kernel's 136 KB of LDS would leave no room beside it.)
+template <int QP>
+__global__ __launch_bounds__(kThreads) void resp_col_kernel(hz_col::ColArgs a) {
+    __shared__ hz_col::ColLds<QP> u;
+    // ranges of the same unit index spread over the XCDs, all units of a range on one XCD (NR a
+    // multiple of 8): a range's samples are read into one L2
+    hz_col::col_group<QP>(a, (int)blockIdx.x / a.NR, (int)blockIdx.x % a.NR, u);
+}
+
+union CombLdsU {
+    hz_col::CombLds c;
+    hz_state::StateLds st;
+};
+
+// column-split path: one workgroup per output block (the combine + the upkeep), the band-state
+// pass as extra workgroups past them (SO = the bank's order, 0: none)
+template <int SO>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void resp_comb_kernel(
+    RespArgs a, const double2* __restrict__ T, const unsigned char* __restrict__ cmap, const double2* __restrict__ tw4k,
+    hz_state::StateArgs st) {
+    __shared__ CombLdsU u;
+    if constexpr (SO > 0) {
+        if ((int)blockIdx.x >= a.B) {
+            const int i = blockIdx.x - a.B;
+            hz_state::state_group<SO>(st, i % st.G, i / st.G, u.st);
+            return;
+        }
+    }
+    const long b = blockIdx.x;
+    hz_col::comb_block(T, cmap, tw4k, b, u.c, a.out + a.off, a.n_out);
+    resp_upkeep(a, b);
+}
+
 
 // history after a call: the last K samples of [hist | x]
 __global__ __launch_bounds__(256) void resp_hist_kernel(const double* __restrict__ hist, const double* __restrict__ x,
@@ -455,6 +497,14 @@ int resp_alloc(double** p, size_t* cap, size_t need) {
 
 int q_padded(int Q) { return (Q + kMacR - 1) / kMacR * kMacR; }
 
+// partition counts the column-split kernel is built for (its LDS holds kWB + Q window rows of four
+// columns: Q <= 24 is 136 KB)
+bool col_q_ok(int Q) { return Q == 8 || Q == 16 || Q == 24; }
+typedef void (*ColKernel)(hz_col::ColArgs);
+ColKernel pick_col(int Q) {
+    return Q == 8 ? resp_col_kernel<8> : Q == 16 ? resp_col_kernel<16> : resp_col_kernel<24>;
+}
+
 // per-bank setup: horizon, history buffers, twiddles
 int resp_setup(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
@@ -475,6 +525,20 @@ int resp_setup(hz_fb* h) {
     }
     HZ_TRY(resp_alloc(&R.d_hist[0], &R.hist_cap0, (size_t)R.K));
     HZ_TRY(resp_alloc(&R.d_hist[1], &R.hist_cap1, (size_t)R.K));
+    if (!R.d_tw4k) {   // column path: W_4096^k, k < 4096, in long double; the combine's column map
+        std::vector<double2> tw(kF);
+        const long double pi = acosl(-1.0L);
+        for (int k = 0; k < kF; ++k) {
+            const long double ang = -2.0L * pi * k / kF;
+            tw[k] = make_double2((double)cosl(ang), (double)sinl(ang));
+        }
+        HZ_TRY_HIP(hipMalloc((void**)&R.d_tw4k, sizeof(double2) * kF));
+        HZ_TRY_HIP(hipMemcpy(R.d_tw4k, tw.data(), sizeof(double2) * kF, hipMemcpyHostToDevice));
+        unsigned char cm[64];
+        hz_col::col_map(cm);
+        HZ_TRY_HIP(hipMalloc((void**)&R.d_cmap, sizeof(cm)));
+        HZ_TRY_HIP(hipMemcpy(R.d_cmap, cm, sizeof(cm), hipMemcpyHostToDevice));
+    }
     if (!R.d_tw) {   // W_F^k, k < kH, in long double
         std::vector<double2> tw(kH);
         const long double pi = acosl(-1.0L);
@@ -516,6 +580,12 @@ int resp_build_h(hz_fb* h) {
     hipLaunchKernelGGL(resp_hspec_kernel, dim3((unsigned)Q), dim3(kThreads), 0, h->stream, (const double*)R.d_h, K,
                        (const double2*)R.d_tw, (double2*)R.d_H, R.d_H + (size_t)Qp * 2 * kH);
     HZ_TRY_HIP(hipGetLastError());
+    if (col_q_ok(Q)) {   // the column path's partition spectra, lane order
+        HZ_TRY(resp_alloc(&R.d_Hc, &R.Hc_cap, (size_t)hz_col::kSlots * Q * 64 * 2));
+        hipLaunchKernelGGL(hz_col::resp_hcol_kernel, dim3(hz_col::kSlots, (unsigned)Q), dim3(64), 0, h->stream,
+                           (const double2*)R.d_H, (const double*)(R.d_H + (size_t)Qp * 2 * kH), Q, (double2*)R.d_Hc);
+        HZ_TRY_HIP(hipGetLastError());
+    }
     HZ_TRY(hz_fbi::fb_state_prepare(h));   // the state pass's records and operands, for LAZY too
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));   // pageable coefficient sources
     R.h_valid = true;
@@ -693,19 +763,51 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     hz_state::StateArgs st = hz_state::StateArgs();
     if (chained) HZ_TRY(fb_state_chained(h, d_in + (n - K), K, h->d_ystate[h->scur ^ 1], &st));
     const int so = chained ? h->order : 0;
-    hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, h->stream, a);
-    HZ_TRY_HIP(hipGetLastError());
+    const bool col = R.col_on && col_q_ok(Q);
     const int nmac = (kH / 256) * ((B + kMacR - 1) / kMacR);
-    hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)nmac), dim3(256), 0, h->stream, (const double2*)R.d_H,
-                       (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B);
-    HZ_TRY_HIP(hipGetLastError());
-    if (e && chained) {   // profiling: e0..e2 forward + MAC, e2..e4 the inverse kernel with the band states
-        HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
-        h->ev_skip[(e - h->ev.data()) / 5] |= 8;
+    R.last_engine = col ? 1 : 0;
+    if (col) {
+        // column-split path (hz_fb_col.h): window spectra never leave the column kernel; the
+        // combine kernel carries the band-state pass
+        const int NR = (B + hz_col::kWB - 1) / hz_col::kWB;
+        HZ_TRY(resp_alloc(&R.d_T, &R.T_cap, (size_t)B * hz_col::kSlots * 64 * 2));
+        hz_col::ColArgs ca;
+        ca.hist = a.hist;
+        ca.x = a.x;
+        ca.K = K;
+        ca.off = off;
+        ca.n_out = n_out;
+        ca.Q = Q;
+        ca.B = B;
+        ca.NR = NR;
+        ca.tw4k = (const double2*)R.d_tw4k;
+        ca.Hc = (const double2*)R.d_Hc;
+        ca.T = (double2*)R.d_T;
+        hipLaunchKernelGGL(pick_col(Q), dim3((unsigned)(hz_col::kUnits * NR)), dim3(kThreads), 0, h->stream, ca);
+        HZ_TRY_HIP(hipGetLastError());
+        if (e && chained) {
+            HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
+            h->ev_skip[(e - h->ev.data()) / 5] |= 8;
+        }
+        auto kc = so == 1 ? resp_comb_kernel<1> : so == 2 ? resp_comb_kernel<2> : resp_comb_kernel<0>;
+        hipLaunchKernelGGL(kc, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0))), dim3(kThreads), 0, h->stream, a,
+                           (const double2*)R.d_T, (const unsigned char*)R.d_cmap, (const double2*)R.d_tw4k, st);
+        HZ_TRY_HIP(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, h->stream, a);
+        HZ_TRY_HIP(hipGetLastError());
+        hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)nmac), dim3(256), 0, h->stream, (const double2*)R.d_H,
+                           (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B);
+        HZ_TRY_HIP(hipGetLastError());
+        if (e && chained) {   // profiling: e0..e2 forward + MAC, e2..e4 the inverse kernel with the band states
+            HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
+            h->ev_skip[(e - h->ev.data()) / 5] |= 8;
+        }
+        RespKernel ki = so == 1 ? resp_inv_kernel<1> : so == 2 ? resp_inv_kernel<2> : resp_inv_kernel<0>;
+        hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0))), dim3(kThreads), 0, h->stream, a,
+                           st);
+        HZ_TRY_HIP(hipGetLastError());
     }
-    RespKernel ki = so == 1 ? resp_inv_kernel<1> : so == 2 ? resp_inv_kernel<2> : resp_inv_kernel<0>;
-    hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0))), dim3(kThreads), 0, h->stream, a, st);
-    HZ_TRY_HIP(hipGetLastError());
     if (chained) HZ_TRY(fb_state_combine(h, st, h->stream));   // pieces of a small bank
 #ifdef HZ_DIAG_STAMPS
     if (chained && R.calls == 30) {
@@ -760,11 +862,14 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
 void fb_resp_free(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     for (double* p : {R.d_hist[0], R.d_hist[1], R.d_h, R.d_hpart, R.d_coef, R.d_zero, R.d_H, R.d_Z, R.d_Y, R.d_tw,
-                      R.d_spart, R.d_sop})
+                      R.d_spart, R.d_sop, R.d_tw4k, R.d_Hc, R.d_T})
         if (p) (void)hipFree(p);
+    if (R.d_cmap) (void)hipFree(R.d_cmap);
     if (R.d_scount) (void)hipFree(R.d_scount);
     fb_stream_free(h);
+    const bool col_on = R.col_on;
     R = hz_fb::Resp();
+    R.col_on = col_on;
 }
 
 }  // namespace hz_fbi
@@ -837,6 +942,20 @@ int hz_fb_arm_time_shard(hz_fb* h, int armed) {
         return HZ_E_STATE;
     }
     h->resp.armed = armed != 0;
+    return HZ_OK;
+}
+
+int hz_fb_tune_response_engine(hz_fb* h, int column_split) {
+    if (!h) return HZ_E_INVALID;
+    const bool on = column_split != 0;
+    h->resp.col_on = on;
+    return HZ_OK;
+}
+
+int hz_fb_response_engine(hz_fb* h, int* column_split_on, int* last_call_column_split) {
+    if (!h) return HZ_E_INVALID;
+    if (column_split_on) *column_split_on = h->resp.col_on ? 1 : 0;
+    if (last_call_column_split) *last_call_column_split = h->resp.last_engine;
     return HZ_OK;
 }
 

@@ -209,6 +209,16 @@ class Filterbank:
         """(tuning) shortest stationary call and the cost-model threshold (0s = defaults)."""
         check(self._lib.hz_fb_tune_response(self._h, int(min_call), int(bands_per_sample)))
 
+    def tune_response_engine(self, column_split: bool = True):
+        """(A/B) 1 = column-split long calls (default), 0 = the three-kernel path"""
+        check(self._lib.hz_fb_tune_response_engine(self._h, 1 if column_split else 0))
+
+    def response_engine(self):
+        """-> (column split enabled, last stationary call ran it)"""
+        a, b = C.c_int(), C.c_int()
+        check(self._lib.hz_fb_response_engine(self._h, C.byref(a), C.byref(b)))
+        return bool(a.value), bool(b.value)
+
     def response_info(self):
         """-> (horizon K, stationary samples so far, band states implicit, stationary calls)"""
         k, r, i, c = C.c_long(), C.c_long(), C.c_int(), C.c_long()

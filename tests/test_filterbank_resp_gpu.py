@@ -325,3 +325,38 @@ def test_stream_and_per_sample_after_stationary(gpu_lib, lazy):
         got.append(g(v))
         g.tick()
     assert rel_err(np.array(got), ref) < TOL
+
+
+@pytest.mark.parametrize("R,centre,order", [(0.999, 1.0, 2), (0.9985, 0.5, 2), (0.997, 0.5, 2), (0.999, 0.5, 4)])
+def test_column_split_vs_three_kernel(gpu_lib, R, centre, order):
+    """The long-call convolution's two structures (hz_fb_col.h column split, default; the
+    three-kernel path, hz_fb_tune_response_engine(h, 0)) on the same calls: both against the
+    restatement, ragged lengths, band states equal; horizons of 8 / 16 / 24 partitions take the
+    column split."""
+    from test_filterbank_lti_gpu import random_bank
+    L = paths()
+    N = 512
+    if order == 2:
+        fwd, back = resonant_coefficients(N, R, centre)
+    else:
+        fwd, back = random_bank(order, N, seed=77, radius=(0.5, R))
+    g, o = make(order, N, fwd, back)
+    t, _ = make(order, N, fwd, back, oracle=False)
+    t.tune_response_engine(False)
+    rng = np.random.default_rng(21)
+    col_calls = 0
+    for i, n in enumerate([3000, 60000, 60000, 50001, 2048 * 30, 100000, 16384, 99999]):
+        x = rng.uniform(-1, 1, n)
+        yg, yt, yo = g.process(x), t.process(x), o.process(x)
+        tol = 1e-7 if centre == 1.0 else TOL
+        assert rel_err(yg, yo) < tol, (i, n, rel_err(yg, yo))
+        assert rel_err(yt, yo) < tol, (i, n)
+        assert g.last_path() == t.last_path()
+        if g.last_path() == L.HZ_FB_PATH_RESPONSE:
+            assert not t.response_engine()[1]
+            col_calls += g.response_engine()[1]
+            assert states_close(g.get_state(), t.get_state(), 1e-9)
+    K = g.response_info()[0]
+    if K // 2048 in (8, 16, 24):
+        assert col_calls >= 3, (K, col_calls)
+    print("horizon", K, "column-split calls", col_calls)
