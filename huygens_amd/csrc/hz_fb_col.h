@@ -40,12 +40,41 @@ __device__ __forceinline__ double2 cmulc(double2 a, double2 b) {   // conj(a) b
 }
 __device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ double2 shfl_xor2(double2 v, int m) {
-    return make_double2(__shfl_xor(v.x, m), __shfl_xor(v.y, m));
-}
 __device__ __forceinline__ int brev6(int l) { return (int)(__builtin_bitreverse32((unsigned)l) >> 26); }
 
-// 64-point transforms across a wave's lanes.  tw4k = W4096^k (k < 4096, long double on the host).
+// The value of lane l ^ S, without LDS: DPP within 16-lane rows (S = 1, 2: quad_perm; 4: two
+// row rotations; 8: row_ror 8), v_permlane16/32_swap across rows (gfx950)
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, true);
+}
+template <int S>
+__device__ __forceinline__ unsigned xor_u(unsigned v, int l) {
+    if constexpr (S == 1) return dpp_u<0xB1>(v);                      // quad_perm [1,0,3,2]
+    else if constexpr (S == 2) return dpp_u<0x4E>(v);                 // quad_perm [2,3,0,1]
+    else if constexpr (S == 4) return (l & 4) ? dpp_u<0x124>(v) : dpp_u<0x12C>(v);   // row_ror 4 / 12
+    else if constexpr (S == 8) return dpp_u<0x128>(v);                // row_ror 8
+    else if constexpr (S == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (l & 16) ? r[0] : r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (l & 32) ? r[0] : r[1];
+    }
+}
+template <int S>
+__device__ __forceinline__ double xor_d(double v, int l) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = xor_u<S>((unsigned)b, l), hi = xor_u<S>((unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <int S>
+__device__ __forceinline__ double2 xor2(double2 v, int l) {
+    return make_double2(xor_d<S>(v.x, l), xor_d<S>(v.y, l));
+}
+
+// 64-point transforms across a wave's lanes, G independent transforms in lockstep (their
+// exchanges and FP64 chains interleave).  tw4k = W4096^k (k < 4096, long double on the host).
 struct Fft64 {
     double2 w[6];   // stage q (span s = 32 >> q): W64^((l & (s-1)) 32 / s)
     __device__ __forceinline__ void init(const double2* __restrict__ tw4k, int l) {
@@ -55,25 +84,41 @@ struct Fft64 {
             w[q] = tw4k[64 * ((l & (s - 1)) * (32 / s))];
         }
     }
-    // forward (W64 = e^{-2 pi i / 64}), decimation in frequency: lane n in, lane l out holds X[brev6(l)]
-    __device__ __forceinline__ double2 fwd(double2 v, int l) const {
+    template <int S, int G>
+    __device__ __forceinline__ void fwd_stage(double2 (&v)[G], int l, const double2& wq) const {
 #pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            const int s = 32 >> q;
-            const double2 o = shfl_xor2(v, s);
-            v = (l & s) ? cmul(csub(o, v), w[q]) : cadd(v, o);
+        for (int g = 0; g < G; ++g) {
+            const double2 o = xor2<S>(v[g], l);
+            v[g] = (l & S) ? cmul(csub(o, v[g]), wq) : cadd(v[g], o);
         }
-        return v;
+    }
+    template <int S, int G>
+    __device__ __forceinline__ void inv_stage(double2 (&v)[G], int l, const double2& wq) const {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const double2 o = xor2<S>(v[g], l);
+            v[g] = (l & S) ? csub(o, cmulc(wq, v[g])) : cadd(v[g], cmulc(wq, o));
+        }
+    }
+    // forward (W64 = e^{-2 pi i / 64}), decimation in frequency: lane n in, lane l out holds X[brev6(l)]
+    template <int G>
+    __device__ __forceinline__ void fwd(double2 (&v)[G], int l) const {
+        fwd_stage<32>(v, l, w[0]);
+        fwd_stage<16>(v, l, w[1]);
+        fwd_stage<8>(v, l, w[2]);
+        fwd_stage<4>(v, l, w[3]);
+        fwd_stage<2>(v, l, w[4]);
+        fwd_stage<1>(v, l, w[5]);
     }
     // inverse (unnormalised), decimation in time: lane l holds Y[brev6(l)] in, lane n out
-    __device__ __forceinline__ double2 inv(double2 v, int l) const {
-#pragma unroll
-        for (int q = 5; q >= 0; --q) {
-            const int s = 32 >> q;
-            const double2 o = shfl_xor2(v, s);
-            v = (l & s) ? csub(o, cmulc(w[q], v)) : cadd(v, cmulc(w[q], o));
-        }
-        return v;
+    template <int G>
+    __device__ __forceinline__ void inv(double2 (&v)[G], int l) const {
+        inv_stage<1>(v, l, w[5]);
+        inv_stage<2>(v, l, w[4]);
+        inv_stage<4>(v, l, w[3]);
+        inv_stage<8>(v, l, w[2]);
+        inv_stage<16>(v, l, w[1]);
+        inv_stage<32>(v, l, w[0]);
     }
 };
 
@@ -103,9 +148,21 @@ __device__ __forceinline__ const double* col_segment(const ColArgs& a, long s, l
     return a.x + (m0 - a.K);
 }
 
+#ifdef HZ_DIAG_STAMPS
+// (diagnostic builds) per column workgroup, wave 0: start, stage 1 done, stage 3 done, MACs done, end
+__device__ long long g_cdiag[1024][5];
+#define HZ_COL_STAMP(i)                                                                                   \
+    do {                                                                                                  \
+        if (t == 0 && blockIdx.x < 1024) g_cdiag[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();       \
+    } while (0)
+#else
+#define HZ_COL_STAMP(i) ((void)0)
+#endif
+
 template <int QP>
 __device__ __forceinline__ void col_group(const ColArgs& a, int u, int r, ColLds<QP>& L) {
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    HZ_COL_STAMP(0);
     const int c0 = unit_c0(u), ncol = unit_ncol(u);
     const int b0 = r * kWB;
     // stage-1 twiddles (lane-uniform): W16^(q c0) (rows m = 4q + rr, q < 8) and W64^(rr c0)
@@ -151,22 +208,32 @@ __device__ __forceinline__ void col_group(const ColArgs& a, int u, int r, ColLds
         if (ncol > 3) L.z[3][sl][l] = make_double2(d02.x - d13.y, d02.y + d13.x);   // d02 + i d13
     }
     __syncthreads();
+    HZ_COL_STAMP(1);
     if (w >= ncol) return;   // (units 7, 8: fewer columns than waves)
     const int c = c0 + 16 * w;
     Fft64 f;
     f.init(a.tw4k, l);
-    // ---- stage 3, in place: window j_l = segments j_l, j_l + 1
+    // ---- stage 3, in place: window j = segments j, j + 1; four windows' transforms in lockstep
     {
         const double2 tn = a.tw4k[l * c];   // W4096^(n2 c), n2 = l
         const double sg = (c0 & 1) ? -1.0 : 1.0;
-        double2 dn = L.z[w][0][l];
-        for (int j = 0; j < NS - 1; ++j) {
-            const double2 d0 = dn;
-            dn = L.z[w][j + 1][l];
-            const double2 A = make_double2(fma(sg, dn.x, d0.x), fma(sg, dn.y, d0.y));
-            L.z[w][j][l] = f.fwd(cmul(A, tn), l);   // lane l: bin k2 = brev6(l)
+        constexpr int NW = NS - 1, G = 4;
+        for (int j0 = 0; j0 < NW; j0 += G) {
+            double2 v[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int j = min(j0 + g, NW - 1);   // (a tail group repeats its last window)
+                const double2 d0 = L.z[w][j][l], d1 = L.z[w][j + 1][l];
+                v[g] = cmul(make_double2(fma(sg, d1.x, d0.x), fma(sg, d1.y, d0.y)), tn);
+            }
+            f.fwd(v, l);   // lane l: bin k2 = brev6(l)
+            // (the group's reads are done before its writes: slot j0 + G is read again by the next group)
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                if (j0 + g < NW) L.z[w][j0 + g][l] = v[g];
         }
     }
+    HZ_COL_STAMP(2);
     // ---- MAC: Y_b = sum_p H_p Z_{b+Q-1-p} for the range's kWB blocks (the wave's own LDS rows:
     // no barrier), window b + t in ring slot (b + t) % kWB at step t = Q - 1 - p
     const double2* hc = a.Hc + ((long)(4 * u + w) * a.Q) * 64 + l;
@@ -190,14 +257,16 @@ __device__ __forceinline__ void col_group(const ColArgs& a, int u, int r, ColLds
         }
         if (ts + 1 < QP) ring[ts % kWB] = L.z[w][kWB + ts][l];
     }
+    HZ_COL_STAMP(3);
     // ---- inverse columns of the range's blocks -> T[b][slot][n1]
     const double2 tn1 = a.tw4k[l * c];   // W4096^(n1 c), n1 = l (conjugated below)
+    f.inv(Y, l);
 #pragma unroll
     for (int b = 0; b < kWB; ++b) {
         const int bg = b0 + b;
-        const double2 v = cmulc(tn1, f.inv(Y[b], l));
-        if (bg < a.B) a.T[((long)bg * kSlots + 4 * u + w) * 64 + l] = v;
+        if (bg < a.B) a.T[((long)bg * kSlots + 4 * u + w) * 64 + l] = cmulc(tn1, Y[b]);
     }
+    HZ_COL_STAMP(4);
 }
 
 // bin c + 64 brev6(l) of the full-spectrum partition spectra from the three-kernel layout
@@ -257,8 +326,9 @@ __device__ __forceinline__ void comb_block(const double2* __restrict__ T, const 
         }
         if (re_only) va.y = vb.y = 0.0;
         // IDFT(V) = conj(DFT(conj V)), V = va + i vb
-        const double2 cv = make_double2(va.x - vb.y, -(va.y + vb.x));
-        const double2 xv = f.fwd(cv, l);   // lane l: n2 = brev6(l)
+        double2 xa[1] = {make_double2(va.x - vb.y, -(va.y + vb.x))};
+        f.fwd(xa, l);   // lane l: n2 = brev6(l)
+        const double2 xv = xa[0];
         const int n2 = brev6(l);
         if (n2 >= 32) {
             L.out[(n2 - 32) * 64 + q] = xv.x;          // Re: n1 = q

@@ -810,6 +810,28 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     }
     if (chained) HZ_TRY(fb_state_combine(h, st, h->stream));   // pieces of a small bank
 #ifdef HZ_DIAG_STAMPS
+    if (col && R.calls == 30) {
+        static long long cv[1024][5];
+        HZ_TRY_HIP(hipStreamSynchronize(h->stream));
+        if (hipMemcpyFromSymbol(cv, HIP_SYMBOL(hz_col::g_cdiag), sizeof(cv)) == hipSuccess) {
+            const int n = std::min(1024, hz_col::kUnits * ((B + hz_col::kWB - 1) / hz_col::kWB));
+            long long t0 = cv[0][0];
+            for (int i = 0; i < n; ++i) t0 = std::min(t0, cv[i][0]);
+            double ph[4] = {0, 0, 0, 0}, smax = 0, emax = 0;
+            int full = 0;
+            for (int i = 0; i < n; ++i) {
+                smax = std::max(smax, (cv[i][0] - t0) * 0.01);
+                emax = std::max(emax, (cv[i][4] - t0) * 0.01);
+                if (cv[i][4] > cv[i][0]) {
+                    ++full;
+                    for (int j = 0; j < 4; ++j) ph[j] += (cv[i][j + 1] - cv[i][j]) * 0.01;
+                }
+            }
+            std::fprintf(stderr, "[col stamps] %d workgroups: mean stage1 %.2f us, stage3 %.2f us, MAC %.2f us, "
+                         "inverse %.2f us; starts up to %.2f us, last end %.2f us\n", n, ph[0] / full, ph[1] / full,
+                         ph[2] / full, ph[3] / full, smax, emax);
+        }
+    }
     if (chained && R.calls == 30) {
         fb_state_stamps_dump(st, B, R.calls);
         static long long hv[2][1024][4];
