@@ -52,7 +52,12 @@ template <int S>
 __device__ __forceinline__ unsigned xor_u(unsigned v, int l) {
     if constexpr (S == 1) return dpp_u<0xB1>(v);                      // quad_perm [1,0,3,2]
     else if constexpr (S == 2) return dpp_u<0x4E>(v);                 // quad_perm [2,3,0,1]
-    else if constexpr (S == 4) return (l & 4) ? dpp_u<0x124>(v) : dpp_u<0x12C>(v);   // row_ror 4 / 12
+    else if constexpr (S == 4) {   // row_ror 4 / 12, both for every lane (a DPP read of a lane
+        // a branch has switched off returns 0), then a bitwise select
+        const unsigned lo = dpp_u<0x124>(v), hi = dpp_u<0x12C>(v);
+        const unsigned m = 0u - (unsigned)((l >> 2) & 1);
+        return (lo & m) | (hi & ~m);
+    }
     else if constexpr (S == 8) return dpp_u<0x128>(v);                // row_ror 8
     else if constexpr (S == 16) {
         const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
