@@ -11,9 +11,11 @@
 //                                s of the range and its Q-partition halo (a radix-4 step over m
 //                                gives the four columns from one set of loads), into LDS;
 //                       stage 3  Z_j = FFT64_n2(W4096^(n2 c) (D_j + (-1)^c D_{j+1})) per window,
-//                                across the wave's lanes, in place in LDS (wave i = column i);
+//                                8 x 8 points (radix-8 in registers, transposed through the
+//                                window's own LDS row), eight windows per wave (wave i = column i);
 //                       MAC      Y_b = sum_p H_p Z_{b+Q-1-p} per bin (lane), Z in a register ring;
-//                       inverse  T_b^c[n1] = W4096^(-n1 c) IFFT64_k2(Y_b) -> HBM, [b][slot][n1].
+//                       inverse  T_b^c[n1] = W4096^(-n1 c) IFFT64_k2(Y_b) -> HBM, [b][slot][n1]
+//                                (the same 8 x 8 scheme, eight blocks per wave).
 //   resp_comb_kernel  one workgroup per output block: x[n1 + 64 n2] = sum_c W64^(-n2 c) T^c[n1]
 //                     (T^(64-c) = conj T^c), the block's samples n2 >= 32; its threads also do
 //                     the history / smoother / x-history upkeep, and the band-state pass rides in
@@ -133,14 +135,54 @@ struct ColArgs {
     long K, off, n_out;   // horizon; the launch's first output sample and count (time shards)
     int Q, B, NR;         // partitions, output blocks, ranges of kWB blocks
     const double2* tw4k;  // [4096] W4096^k
-    const double2* Hc;    // [kSlots][Q][64] H_p at bin c + 64 brev6(l) (lane order), / F
+    const double2* Hc;    // [kSlots][Q][64] H_p at bin c + 64 l, / F
     double2* T;           // [B][kSlots][64] inverse columns
 };
 
+// Rows are padded to kRow complex so that the transposed accesses of the radix-8 transforms
+// spread over the LDS banks
+constexpr int kRow = 65;
 template <int QP>
 struct ColLds {
-    double2 z[4][kWB + QP][64];   // D of the segments, then Z of the windows, per column
+    double2 z[4][kWB + QP][kRow];   // D of the segments, then Z of the windows, per column
 };
+
+// 8-point DFT in registers, natural order in and out (radix-2 decimation in time); INV: W8 -> conj
+template <bool INV>
+__device__ __forceinline__ void dft8(double2 (&x)[8]) {
+    constexpr double h = 0.70710678118654752440;
+    double2 a[8] = {x[0], x[4], x[2], x[6], x[1], x[5], x[3], x[7]};
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        const double2 p = a[i], q = a[i + 1];
+        a[i] = cadd(p, q);
+        a[i + 1] = csub(p, q);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i += 4) {
+        // span 2: twiddles 1, W4 (= -i forward, +i inverse)
+        double2 p = a[i], q = a[i + 2];
+        a[i] = cadd(p, q);
+        a[i + 2] = csub(p, q);
+        p = a[i + 1];
+        q = INV ? make_double2(-a[i + 3].y, a[i + 3].x) : make_double2(a[i + 3].y, -a[i + 3].x);
+        a[i + 1] = cadd(p, q);
+        a[i + 3] = csub(p, q);
+    }
+    // span 4: twiddles W8^i, i < 4
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double2 q = a[i + 4];
+        if (i == 1) q = INV ? make_double2(h * (q.x - q.y), h * (q.x + q.y)) : make_double2(h * (q.x + q.y), h * (q.y - q.x));
+        if (i == 2) q = INV ? make_double2(-q.y, q.x) : make_double2(q.y, -q.x);
+        if (i == 3) q = INV ? make_double2(-h * (q.x + q.y), h * (q.x - q.y)) : make_double2(h * (q.y - q.x), -h * (q.x + q.y));
+        const double2 p = a[i];
+        a[i] = cadd(p, q);
+        a[i + 4] = csub(p, q);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = a[i];
+}
 
 // u = [hist | x | 0 ...] indexed from the launch's first output sample: one segment's source
 __device__ __forceinline__ const double* col_segment(const ColArgs& a, long s, long* lim) {
@@ -164,6 +206,33 @@ __device__ long long g_cdiag[1024][5];
 #define HZ_COL_STAMP(i) ((void)0)
 #endif
 
+// A 64-point transform of eight rows of one column at once, in place (rows row0 .. row0 + 7, the
+// last `valid` of them kept): lane (g, r) = (l >> 3, l & 7) holds the row g + row0's points r + 8 m
+// (m < 8, already loaded and twiddled) -> 8-point DFT over m -> x W64^(+-r k1) -> transpose through
+// the rows themselves -> 8-point DFT over r; out[k1 + 8 k2] for lane (g, k1), k2 < 8 (natural order)
+template <bool INV>
+__device__ __forceinline__ void col_fft8x8(double2 (&v)[8], double2 (*rows)[kRow], int row0, int valid, int l,
+                                           const double2* __restrict__ tw4k) {
+    const int g = l >> 3, r = l & 7;
+    dft8<INV>(v);
+#pragma unroll
+    for (int k1 = 1; k1 < 8; ++k1) {
+        const double2 w = tw4k[64 * r * k1];   // W64^(r k1)
+        v[k1] = INV ? cmulc(w, v[k1]) : cmul(v[k1], w);
+    }
+    const bool live = g < valid;
+    if (live) {
+#pragma unroll
+        for (int k1 = 0; k1 < 8; ++k1) rows[row0 + g][8 * r + k1] = v[k1];
+    }
+    // (the wave's own LDS writes land before its reads: LDS instructions of a wave run in order)
+    if (live) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = rows[row0 + g][8 * q + r];   // lane (g, k1 = r)
+    }
+    dft8<INV>(v);
+}
+
 template <int QP>
 __device__ __forceinline__ void col_group(const ColArgs& a, int u, int r, ColLds<QP>& L) {
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
@@ -176,112 +245,147 @@ __device__ __forceinline__ void col_group(const ColArgs& a, int u, int r, ColLds
     for (int q = 0; q < 8; ++q) t16[q] = a.tw4k[256 * ((q * c0) & 15)];
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) t64[rr] = a.tw4k[64 * ((rr * c0) & 63)];
-    // ---- stage 1: segments s_l = w, w + 4, ... of [0, kWB + QP), next segment's loads in flight
+    // ---- stage 1: the wave's segments s_l = w, w + 4, ... of [0, kWB + QP) in halves of 16 rows,
+    // two halves in flight beside the one being summed
     constexpr int NS = kWB + QP;
-    double cur[32], nxt[32];
-    auto load = [&](int sl, double (&v)[32]) {
+    const int nseg = (NS - w + 3) / 4, nit = 2 * nseg;
+    double b0v[16], b1v[16], b2v[16];
+    auto load = [&](int it, double (&v)[16]) {
+        if (it >= nit) return;
         long lim;
-        const double* src = col_segment(a, (long)b0 + sl, &lim);
+        const double* src = col_segment(a, (long)b0 + w + 4 * (it >> 1), &lim);
+        const int m0 = 16 * (it & 1);
 #pragma unroll
-        for (int m = 0; m < 32; ++m) {
-            const int i = 64 * m + l;
+        for (int m = 0; m < 16; ++m) {
+            const int i = 64 * (m0 + m) + l;
             v[m] = i < lim ? src[i] : 0.0;
         }
     };
-    if (w < NS) load(w, nxt);
-    for (int sl = w; sl < NS; sl += 4) {
+    double2 acc[4];
+    auto step = [&](int it, double (&v)[16]) {
+        if (it >= nit) return;
+        const int h = it & 1;
+        if (!h) {
 #pragma unroll
-        for (int m = 0; m < 32; ++m) cur[m] = nxt[m];
-        if (sl + 4 < NS) load(sl + 4, nxt);
-        double2 P[4];
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            double2 acc = make_double2(0.0, 0.0);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                acc.x = fma(cur[4 * q + rr], t16[q].x, acc.x);
-                acc.y = fma(cur[4 * q + rr], t16[q].y, acc.y);
-            }
-            P[rr] = cmul(acc, t64[rr]);
+            for (int rr = 0; rr < 4; ++rr) acc[rr] = make_double2(0.0, 0.0);
         }
-        // D^{c0 + 16 i} = sum_rr W4^(rr i) P_rr, W4 = -i
-        const double2 s02 = cadd(P[0], P[2]), d02 = csub(P[0], P[2]);
-        const double2 s13 = cadd(P[1], P[3]), d13 = csub(P[1], P[3]);
-        L.z[0][sl][l] = cadd(s02, s13);
-        L.z[1][sl][l] = make_double2(d02.x + d13.y, d02.y - d13.x);   // d02 - i d13
-        L.z[2][sl][l] = csub(s02, s13);
-        if (ncol > 3) L.z[3][sl][l] = make_double2(d02.x - d13.y, d02.y + d13.x);   // d02 + i d13
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                const double2 tq = t16[4 * h + qq];
+                acc[rr].x = fma(v[4 * qq + rr], tq.x, acc[rr].x);
+                acc[rr].y = fma(v[4 * qq + rr], tq.y, acc[rr].y);
+            }
+        load(it + 3, v);   // this buffer's next item
+        if (h) {
+            double2 P[4];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) P[rr] = cmul(acc[rr], t64[rr]);
+            // D^{c0 + 16 i} = sum_rr W4^(rr i) P_rr, W4 = -i
+            const double2 s02 = cadd(P[0], P[2]), d02 = csub(P[0], P[2]);
+            const double2 s13 = cadd(P[1], P[3]), d13 = csub(P[1], P[3]);
+            const int sl = w + 4 * (it >> 1);
+            L.z[0][sl][l] = cadd(s02, s13);
+            L.z[1][sl][l] = make_double2(d02.x + d13.y, d02.y - d13.x);   // d02 - i d13
+            L.z[2][sl][l] = csub(s02, s13);
+            if (ncol > 3) L.z[3][sl][l] = make_double2(d02.x - d13.y, d02.y + d13.x);   // d02 + i d13
+        }
+    };
+    load(0, b0v);
+    load(1, b1v);
+    load(2, b2v);
+    for (int it = 0; it < nit; it += 3) {
+        step(it, b0v);
+        step(it + 1, b1v);
+        step(it + 2, b2v);
     }
     __syncthreads();
     HZ_COL_STAMP(1);
     if (w >= ncol) return;   // (units 7, 8: fewer columns than waves)
     const int c = c0 + 16 * w;
-    Fft64 f;
-    f.init(a.tw4k, l);
-    // ---- stage 3, in place: window j = segments j, j + 1; four windows' transforms in lockstep
+    double2(*rows)[kRow] = L.z[w];
+    // ---- stage 3, in place: window j = segments j, j + 1; eight windows per transform
     {
-        const double2 tn = a.tw4k[l * c];   // W4096^(n2 c), n2 = l
+        constexpr int NW = NS - 1;
+        const int g = l >> 3, rr = l & 7;
         const double sg = (c0 & 1) ? -1.0 : 1.0;
-        constexpr int NW = NS - 1, G = 4;
-        for (int j0 = 0; j0 < NW; j0 += G) {
-            double2 v[G];
+        double2 tn[8];   // W4096^(n2 c), n2 = rr + 8 m
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const int j = min(j0 + g, NW - 1);   // (a tail group repeats its last window)
-                const double2 d0 = L.z[w][j][l], d1 = L.z[w][j + 1][l];
-                v[g] = cmul(make_double2(fma(sg, d1.x, d0.x), fma(sg, d1.y, d0.y)), tn);
+        for (int m = 0; m < 8; ++m) tn[m] = a.tw4k[(rr + 8 * m) * c];
+        for (int j0 = 0; j0 < NW; j0 += 8) {
+            const int j = min(j0 + g, NW - 1);
+            double2 v[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const double2 d0 = rows[j][rr + 8 * m], d1 = rows[j + 1][rr + 8 * m];
+                v[m] = cmul(make_double2(fma(sg, d1.x, d0.x), fma(sg, d1.y, d0.y)), tn[m]);
             }
-            f.fwd(v, l);   // lane l: bin k2 = brev6(l)
-            // (the group's reads are done before its writes: slot j0 + G is read again by the next group)
+            const int valid = min(8, NW - j0);
+            col_fft8x8<false>(v, rows, j0, valid, l, a.tw4k);
+            if (g < valid) {
 #pragma unroll
-            for (int g = 0; g < G; ++g)
-                if (j0 + g < NW) L.z[w][j0 + g][l] = v[g];
+                for (int k2 = 0; k2 < 8; ++k2) rows[j0 + g][rr + 8 * k2] = v[k2];   // bin rr + 8 k2
+            }
         }
     }
     HZ_COL_STAMP(2);
-    // ---- MAC: Y_b = sum_p H_p Z_{b+Q-1-p} for the range's kWB blocks (the wave's own LDS rows:
-    // no barrier), window b + t in ring slot (b + t) % kWB at step t = Q - 1 - p
+    // ---- MAC: Y_b = sum_p H_p Z_{b+Q-1-p} for the range's kWB blocks (lane = bin, the wave's own
+    // LDS rows), window b + t in ring slot (b + t) % kWB at step t = Q - 1 - p
     const double2* hc = a.Hc + ((long)(4 * u + w) * a.Q) * 64 + l;
     double2 Y[kWB], ring[kWB];
 #pragma unroll
     for (int b = 0; b < kWB; ++b) {
         Y[b] = make_double2(0.0, 0.0);
-        ring[b] = L.z[w][b][l];
+        ring[b] = rows[b][l];
     }
-    double2 hv[QP];
-#pragma unroll
-    for (int p = 0; p < QP; ++p) hv[p] = hc[(long)p * 64];
 #pragma unroll
     for (int ts = 0; ts < QP; ++ts) {
-        const double2 h = hv[QP - 1 - ts];
+        const double2 h = hc[(long)(QP - 1 - ts) * 64];
 #pragma unroll
         for (int b = 0; b < kWB; ++b) {
             const double2 z = ring[(b + ts) % kWB];
             Y[b].x = fma(h.x, z.x, fma(-h.y, z.y, Y[b].x));
             Y[b].y = fma(h.x, z.y, fma(h.y, z.x, Y[b].y));
         }
-        if (ts + 1 < QP) ring[ts % kWB] = L.z[w][kWB + ts][l];
+        if (ts + 1 < QP) ring[ts % kWB] = rows[kWB + ts][l];
     }
     HZ_COL_STAMP(3);
-    // ---- inverse columns of the range's blocks -> T[b][slot][n1]
-    const double2 tn1 = a.tw4k[l * c];   // W4096^(n1 c), n1 = l (conjugated below)
-    f.inv(Y, l);
+    // ---- inverse columns of the range's blocks -> T[b][slot][n1]: Y into rows 0 .. kWB - 1
+    // (every MAC read of the wave is done), eight blocks per transform
 #pragma unroll
-    for (int b = 0; b < kWB; ++b) {
-        const int bg = b0 + b;
-        if (bg < a.B) a.T[((long)bg * kSlots + 4 * u + w) * 64 + l] = cmulc(tn1, Y[b]);
+    for (int b = 0; b < kWB; ++b) rows[b][l] = Y[b];
+    {
+        const int g = l >> 3, rr = l & 7;
+        for (int bl0 = 0; bl0 < kWB; bl0 += 8) {
+            const int bl = min(bl0 + g, kWB - 1);
+            double2 v[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) v[m] = rows[bl][rr + 8 * m];
+            const int valid = min(8, kWB - bl0);
+            col_fft8x8<true>(v, rows, bl0, valid, l, a.tw4k);
+            const int bg = b0 + bl0 + g;
+            if (g < valid && bg < a.B) {
+                double2* dst = a.T + ((long)bg * kSlots + 4 * u + w) * 64;
+#pragma unroll
+                for (int n1b = 0; n1b < 8; ++n1b) {
+                    const int n1 = rr + 8 * n1b;
+                    dst[n1] = cmulc(a.tw4k[n1 * c], v[n1b]);   // x W4096^(-n1 c)
+                }
+            }
+        }
     }
     HZ_COL_STAMP(4);
 }
 
-// bin c + 64 brev6(l) of the full-spectrum partition spectra from the three-kernel layout
-// (H [Qp][2048] complex, Hn [Qp] bin 2048): Hc [kSlots][Q][64]; grid (kSlots, Q), 64 threads
+// bin c + 64 l of the full-spectrum partition spectra from the three-kernel layout (H [Qp][2048]
+// complex, Hn [Qp] bin 2048): Hc [kSlots][Q][64]; grid (kSlots, Q), 64 threads
 __global__ __launch_bounds__(64) void resp_hcol_kernel(const double2* __restrict__ H, const double* __restrict__ Hn,
                                                       int Q, double2* __restrict__ Hc) {
     const int slot = blockIdx.x, p = blockIdx.y, l = threadIdx.x;
     const int u = slot / 4, i = slot % 4;
     if (i >= unit_ncol(u)) return;
-    const int k = unit_c0(u) + 16 * i + 64 * brev6(l);
+    const int k = unit_c0(u) + 16 * i + 64 * l;
     double2 v;
     if (k < kP) v = H[(long)p * kP + k];
     else if (k == kP) v = make_double2(Hn[p], 0.0);
