@@ -145,6 +145,8 @@ constexpr int kRow = 65;
 template <int QP>
 struct ColLds {
     double2 z[4][kWB + QP][kRow];   // D of the segments, then Z of the windows, per column
+    double2 tn[4][64];              // W4096^(n c), n < 64, per column
+    double2 w64[64];                // W64^(r k), [8 r + k]
 };
 
 // 8-point DFT in registers, natural order in and out (radix-2 decimation in time); INV: W8 -> conj
@@ -212,12 +214,12 @@ __device__ long long g_cdiag[1024][5];
 // the rows themselves -> 8-point DFT over r; out[k1 + 8 k2] for lane (g, k1), k2 < 8 (natural order)
 template <bool INV>
 __device__ __forceinline__ void col_fft8x8(double2 (&v)[8], double2 (*rows)[kRow], int row0, int valid, int l,
-                                           const double2* __restrict__ tw4k) {
+                                           const double2* __restrict__ w64) {
     const int g = l >> 3, r = l & 7;
     dft8<INV>(v);
 #pragma unroll
     for (int k1 = 1; k1 < 8; ++k1) {
-        const double2 w = tw4k[64 * r * k1];   // W64^(r k1)
+        const double2 w = w64[8 * r + k1];   // W64^(r k1)
         v[k1] = INV ? cmulc(w, v[k1]) : cmul(v[k1], w);
     }
     const bool live = g < valid;
@@ -233,145 +235,132 @@ __device__ __forceinline__ void col_fft8x8(double2 (&v)[8], double2 (*rows)[kRow
     dft8<INV>(v);
 }
 
+// kColThreads threads = 8 waves: stage 1 on all eight (more loads in flight), stage 3 and the
+// inverse on waves w and w + 4 of column w (alternate groups of eight rows), the MAC on waves 0-3
+constexpr int kColThreads = 512;
+
 template <int QP>
 __device__ __forceinline__ void col_group(const ColArgs& a, int u, int r, ColLds<QP>& L) {
-    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int t = threadIdx.x, l = t & 63, wv = t >> 6;
     HZ_COL_STAMP(0);
     const int c0 = unit_c0(u), ncol = unit_ncol(u);
     const int b0 = r * kWB;
-    // stage-1 twiddles (lane-uniform): W16^(q c0) (rows m = 4q + rr, q < 8) and W64^(rr c0)
+    const int w = wv & 3, half = wv >> 2;   // column, and which of its two waves
+    const int g8 = l >> 3, r8 = l & 7;
+    // stage-1 twiddles (lane-uniform): W16^(q c0) (rows m = 4q + rr, q < 8) and W64^(rr c0); the
+    // later phases' tables into LDS now (visible after stage 1's barrier)
     double2 t16[8], t64[4];
 #pragma unroll
     for (int q = 0; q < 8; ++q) t16[q] = a.tw4k[256 * ((q * c0) & 15)];
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) t64[rr] = a.tw4k[64 * ((rr * c0) & 63)];
-    // ---- stage 1: the wave's segments s_l = w, w + 4, ... of [0, kWB + QP) in halves of 16 rows,
-    // two halves in flight beside the one being summed
+    if (t < 256) L.tn[t >> 6][l] = a.tw4k[l * (c0 + 16 * (t >> 6))];
+    else if (t < 320) L.w64[t - 256] = a.tw4k[64 * ((t - 256) >> 3) * ((t - 256) & 7)];
+    // ---- stage 1: segments s_l = wv, wv + 8, ... of [0, kWB + QP), the next one's loads in flight
     constexpr int NS = kWB + QP;
-    const int nseg = (NS - w + 3) / 4, nit = 2 * nseg;
-    double b0v[16], b1v[16], b2v[16];
-    auto load = [&](int it, double (&v)[16]) {
-        if (it >= nit) return;
+    double cur[32], nxt[32];
+    auto load = [&](int sl, double (&v)[32]) {
         long lim;
-        const double* src = col_segment(a, (long)b0 + w + 4 * (it >> 1), &lim);
-        const int m0 = 16 * (it & 1);
+        const double* src = col_segment(a, (long)b0 + sl, &lim);
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            const int i = 64 * (m0 + m) + l;
+        for (int m = 0; m < 32; ++m) {
+            const int i = 64 * m + l;
             v[m] = i < lim ? src[i] : 0.0;
         }
     };
-    double2 acc[4];
-    auto step = [&](int it, double (&v)[16]) {
-        if (it >= nit) return;
-        const int h = it & 1;
-        if (!h) {
+    if (wv < NS) load(wv, nxt);
+    for (int sl = wv; sl < NS; sl += 8) {
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) acc[rr] = make_double2(0.0, 0.0);
-        }
+        for (int m = 0; m < 32; ++m) cur[m] = nxt[m];
+        if (sl + 8 < NS) load(sl + 8, nxt);
+        double2 P[4];
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
+        for (int rr = 0; rr < 4; ++rr) {
+            double2 acc = make_double2(0.0, 0.0);
 #pragma unroll
-            for (int qq = 0; qq < 4; ++qq) {
-                const double2 tq = t16[4 * h + qq];
-                acc[rr].x = fma(v[4 * qq + rr], tq.x, acc[rr].x);
-                acc[rr].y = fma(v[4 * qq + rr], tq.y, acc[rr].y);
+            for (int q = 0; q < 8; ++q) {
+                acc.x = fma(cur[4 * q + rr], t16[q].x, acc.x);
+                acc.y = fma(cur[4 * q + rr], t16[q].y, acc.y);
             }
-        load(it + 3, v);   // this buffer's next item
-        if (h) {
-            double2 P[4];
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) P[rr] = cmul(acc[rr], t64[rr]);
-            // D^{c0 + 16 i} = sum_rr W4^(rr i) P_rr, W4 = -i
-            const double2 s02 = cadd(P[0], P[2]), d02 = csub(P[0], P[2]);
-            const double2 s13 = cadd(P[1], P[3]), d13 = csub(P[1], P[3]);
-            const int sl = w + 4 * (it >> 1);
-            L.z[0][sl][l] = cadd(s02, s13);
-            L.z[1][sl][l] = make_double2(d02.x + d13.y, d02.y - d13.x);   // d02 - i d13
-            L.z[2][sl][l] = csub(s02, s13);
-            if (ncol > 3) L.z[3][sl][l] = make_double2(d02.x - d13.y, d02.y + d13.x);   // d02 + i d13
+            P[rr] = cmul(acc, t64[rr]);
         }
-    };
-    load(0, b0v);
-    load(1, b1v);
-    load(2, b2v);
-    for (int it = 0; it < nit; it += 3) {
-        step(it, b0v);
-        step(it + 1, b1v);
-        step(it + 2, b2v);
+        // D^{c0 + 16 i} = sum_rr W4^(rr i) P_rr, W4 = -i
+        const double2 s02 = cadd(P[0], P[2]), d02 = csub(P[0], P[2]);
+        const double2 s13 = cadd(P[1], P[3]), d13 = csub(P[1], P[3]);
+        L.z[0][sl][l] = cadd(s02, s13);
+        L.z[1][sl][l] = make_double2(d02.x + d13.y, d02.y - d13.x);   // d02 - i d13
+        L.z[2][sl][l] = csub(s02, s13);
+        if (ncol > 3) L.z[3][sl][l] = make_double2(d02.x - d13.y, d02.y + d13.x);   // d02 + i d13
     }
     __syncthreads();
     HZ_COL_STAMP(1);
-    if (w >= ncol) return;   // (units 7, 8: fewer columns than waves)
-    const int c = c0 + 16 * w;
+    const bool colw = w < ncol;   // (units 7, 8: fewer columns than waves)
     double2(*rows)[kRow] = L.z[w];
-    // ---- stage 3, in place: window j = segments j, j + 1; eight windows per transform
-    {
+    // ---- stage 3, in place: window j = segments j, j + 1; eight windows per transform, the
+    // column's groups alternating between its two waves (a group writes only its own eight rows
+    // and reads the next group's first row, which no group writes)
+    if (colw) {
         constexpr int NW = NS - 1;
-        const int g = l >> 3, rr = l & 7;
         const double sg = (c0 & 1) ? -1.0 : 1.0;
-        double2 tn[8];   // W4096^(n2 c), n2 = rr + 8 m
-#pragma unroll
-        for (int m = 0; m < 8; ++m) tn[m] = a.tw4k[(rr + 8 * m) * c];
-        for (int j0 = 0; j0 < NW; j0 += 8) {
-            const int j = min(j0 + g, NW - 1);
+        for (int j0 = 8 * half; j0 < NW; j0 += 16) {
+            const int j = min(j0 + g8, NW - 1);
             double2 v[8];
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
-                const double2 d0 = rows[j][rr + 8 * m], d1 = rows[j + 1][rr + 8 * m];
-                v[m] = cmul(make_double2(fma(sg, d1.x, d0.x), fma(sg, d1.y, d0.y)), tn[m]);
+                const double2 d0 = rows[j][r8 + 8 * m], d1 = rows[j + 1][r8 + 8 * m];
+                v[m] = cmul(make_double2(fma(sg, d1.x, d0.x), fma(sg, d1.y, d0.y)), L.tn[w][r8 + 8 * m]);
             }
             const int valid = min(8, NW - j0);
-            col_fft8x8<false>(v, rows, j0, valid, l, a.tw4k);
-            if (g < valid) {
+            col_fft8x8<false>(v, rows, j0, valid, l, L.w64);
+            if (g8 < valid) {
 #pragma unroll
-                for (int k2 = 0; k2 < 8; ++k2) rows[j0 + g][rr + 8 * k2] = v[k2];   // bin rr + 8 k2
+                for (int k2 = 0; k2 < 8; ++k2) rows[j0 + g8][r8 + 8 * k2] = v[k2];   // bin r + 8 k2
             }
         }
     }
+    __syncthreads();
     HZ_COL_STAMP(2);
-    // ---- MAC: Y_b = sum_p H_p Z_{b+Q-1-p} for the range's kWB blocks (lane = bin, the wave's own
-    // LDS rows), window b + t in ring slot (b + t) % kWB at step t = Q - 1 - p
-    const double2* hc = a.Hc + ((long)(4 * u + w) * a.Q) * 64 + l;
-    double2 Y[kWB], ring[kWB];
-#pragma unroll
-    for (int b = 0; b < kWB; ++b) {
-        Y[b] = make_double2(0.0, 0.0);
-        ring[b] = rows[b][l];
-    }
-#pragma unroll
-    for (int ts = 0; ts < QP; ++ts) {
-        const double2 h = hc[(long)(QP - 1 - ts) * 64];
+    // ---- MAC (waves 0-3): Y_b = sum_p H_p Z_{b+Q-1-p} for the range's kWB blocks (lane = bin),
+    // window b + t in ring slot (b + t) % kWB at step t = Q - 1 - p; Y into rows 0 .. kWB - 1
+    if (colw && half == 0) {
+        const double2* hc = a.Hc + ((long)(4 * u + w) * a.Q) * 64 + l;
+        double2 Y[kWB], ring[kWB];
 #pragma unroll
         for (int b = 0; b < kWB; ++b) {
-            const double2 z = ring[(b + ts) % kWB];
-            Y[b].x = fma(h.x, z.x, fma(-h.y, z.y, Y[b].x));
-            Y[b].y = fma(h.x, z.y, fma(h.y, z.x, Y[b].y));
+            Y[b] = make_double2(0.0, 0.0);
+            ring[b] = rows[b][l];
         }
-        if (ts + 1 < QP) ring[ts % kWB] = rows[kWB + ts][l];
-    }
-    HZ_COL_STAMP(3);
-    // ---- inverse columns of the range's blocks -> T[b][slot][n1]: Y into rows 0 .. kWB - 1
-    // (every MAC read of the wave is done), eight blocks per transform
 #pragma unroll
-    for (int b = 0; b < kWB; ++b) rows[b][l] = Y[b];
-    {
-        const int g = l >> 3, rr = l & 7;
-        for (int bl0 = 0; bl0 < kWB; bl0 += 8) {
-            const int bl = min(bl0 + g, kWB - 1);
+        for (int ts = 0; ts < QP; ++ts) {
+            const double2 h = hc[(long)(QP - 1 - ts) * 64];
+#pragma unroll
+            for (int b = 0; b < kWB; ++b) {
+                const double2 z = ring[(b + ts) % kWB];
+                Y[b].x = fma(h.x, z.x, fma(-h.y, z.y, Y[b].x));
+                Y[b].y = fma(h.x, z.y, fma(h.y, z.x, Y[b].y));
+            }
+            if (ts + 1 < QP) ring[ts % kWB] = rows[kWB + ts][l];
+        }
+#pragma unroll
+        for (int b = 0; b < kWB; ++b) rows[b][l] = Y[b];   // (every MAC read of the wave is done)
+    }
+    __syncthreads();
+    HZ_COL_STAMP(3);
+    // ---- inverse columns -> T[b][slot][n1], eight blocks per transform, groups alternating
+    if (colw) {
+        for (int bl0 = 8 * half; bl0 < kWB; bl0 += 16) {
+            const int bl = min(bl0 + g8, kWB - 1);
             double2 v[8];
 #pragma unroll
-            for (int m = 0; m < 8; ++m) v[m] = rows[bl][rr + 8 * m];
+            for (int m = 0; m < 8; ++m) v[m] = rows[bl][r8 + 8 * m];
             const int valid = min(8, kWB - bl0);
-            col_fft8x8<true>(v, rows, bl0, valid, l, a.tw4k);
-            const int bg = b0 + bl0 + g;
-            if (g < valid && bg < a.B) {
+            col_fft8x8<true>(v, rows, bl0, valid, l, L.w64);
+            const int bg = b0 + bl0 + g8;
+            if (g8 < valid && bg < a.B) {
                 double2* dst = a.T + ((long)bg * kSlots + 4 * u + w) * 64;
 #pragma unroll
-                for (int n1b = 0; n1b < 8; ++n1b) {
-                    const int n1 = rr + 8 * n1b;
-                    dst[n1] = cmulc(a.tw4k[n1 * c], v[n1b]);   // x W4096^(-n1 c)
-                }
+                for (int n1b = 0; n1b < 8; ++n1b)   // x W4096^(-n1 c)
+                    dst[r8 + 8 * n1b] = cmulc(L.tn[w][r8 + 8 * n1b], v[n1b]);
             }
         }
     }

@@ -435,7 +435,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
 // column-split path: the inverse columns of the range's blocks (hz_fb_col.h).  (The band-state
 // pass stays in the combine kernel: this kernel's 136 KB of LDS would leave no room beside it.)
 template <int QP>
-__global__ __launch_bounds__(kThreads) void resp_col_kernel(hz_col::ColArgs a) {
+__global__ __launch_bounds__(hz_col::kColThreads) void resp_col_kernel(hz_col::ColArgs a) {
     __shared__ hz_col::ColLds<QP> u;
     // ranges of the same unit index spread over the XCDs, all units of a range on one XCD (NR a
     // multiple of 8): a range's samples are read into one L2
@@ -783,7 +783,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         ca.tw4k = (const double2*)R.d_tw4k;
         ca.Hc = (const double2*)R.d_Hc;
         ca.T = (double2*)R.d_T;
-        hipLaunchKernelGGL(pick_col(Q), dim3((unsigned)(hz_col::kUnits * NR)), dim3(kThreads), 0, h->stream, ca);
+        hipLaunchKernelGGL(pick_col(Q), dim3((unsigned)(hz_col::kUnits * NR)), dim3(hz_col::kColThreads), 0, h->stream, ca);
         HZ_TRY_HIP(hipGetLastError());
         if (e && chained) {
             HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
