@@ -78,6 +78,46 @@ def _timed(step, steps, warmup, torch, dev, world=1):
 # per-sample complex rotation)
 EXEC_C3 = 5.0
 
+# rocprofv3 --pmc counter sets (one pass each: <= 8 SQ counters)
+PMC_VALU = ("SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_TRANS_F32",
+            "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")
+PMC_F64_MFMA = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+                "SQ_INSTS_VALU_MFMA_MOPS_F64", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES")
+
+
+def pmc_counts(kernel, workload, counters):
+    """one rocprofv3 --pmc pass over a short run of this row (bench.pmc_pass: kernel trace only, a
+    child process): per-launch counts of `kernel` and the flops / lane-ops they imply"""
+    import bench
+    res, err = bench.pmc_pass(counters, (kernel,), extra=("--workload", workload))
+    if res is None:
+        return {"error": err}
+    c = res.get(kernel, {})
+    out = {"counters": c, "counters_per": "launch (mean of the two largest dispatches)"}
+    lanes = 64.0
+    out["f32_flops"] = lanes * (2 * c.get("SQ_INSTS_VALU_FMA_F32", 0) + c.get("SQ_INSTS_VALU_MUL_F32", 0) +
+                                c.get("SQ_INSTS_VALU_ADD_F32", 0))
+    out["f64_flops"] = lanes * (2 * c.get("SQ_INSTS_VALU_FMA_F64", 0) + c.get("SQ_INSTS_VALU_MUL_F64", 0) +
+                                c.get("SQ_INSTS_VALU_ADD_F64", 0)) + 512.0 * c.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0)
+    out["trans_ops"] = lanes * (c.get("SQ_INSTS_VALU_TRANS_F32", 0) + c.get("SQ_INSTS_VALU_TRANS_F64", 0))
+    if c.get("SQ_BUSY_CYCLES"):
+        out["mfma_busy_frac"] = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / c["SQ_BUSY_CYCLES"]
+    return out
+
+
+def pipe_fracs(counts, seconds):
+    """each pipe's executed rate over the kernel's time against that pipe's peak"""
+    if not counts or "error" in counts or not seconds:
+        return counts
+    f32 = counts["f32_flops"] / seconds / 1e12
+    f64 = counts["f64_flops"] / seconds / 1e12
+    tr = counts["trans_ops"] / seconds / 1e12
+    fr = {"fp32_valu": f32 / FP32_PEAK, "fp64_valu": f64 / FP64_PEAK, "transcendental": tr / (FP32_PEAK / 8)}
+    return dict(counts, seconds_per_launch=seconds, tflops_fp32=f32, tflops_fp64=f64, trans_tops=tr, fracs=fr,
+                binding_pipe=max(fr, key=fr.get),
+                trans_peak_note="transcendental peak taken as a quarter of the FP32 FMA lane rate: FP32_PEAK / 8 "
+                                "lane-ops/s")
+
 
 def run_c3(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
     """Additive<double>(&cycle, 64, 256, 0.75, 1.0), all voices via makenote(36+v, 1),
@@ -146,6 +186,10 @@ def run_c3(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
                      "frac": xach / FP64_PEAK if xach else None, "traffic": None,
                      "kernel": "add_mix_kernel (+ add_reduce_kernel, add_advance_kernel)",
                      "kernel_avg_ms": ms / max(1, launches), "launches": launches,
+                     "kernel_ms_per_step": ms / args.steps, "launches_per_step": launches / max(1, args.steps),
+                     "launch_note": "two add_mix launches per step (24,000 then 456,000 samples, the release "
+                                    "between): kernel_avg_ms is their mean; a rocprofv3 summary of this row "
+                                    "reproduces kernel_ms_per_step as TotalDurationNs / steps",
                      "flops_per_unit": EXEC_C3,
                      "flops_source": "rocprofv3 --pmc SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 on this row "
                                      "(profiles/r2/flops_pmc.txt)",
@@ -229,10 +273,13 @@ def run_c4(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
                          f"long double radix-2 FFT, 1 thread, {dt:.2f} s"}
     e2, f2, o2, b2, fr2 = out["gate625"]
     traffic, tdetail = None, "not collected (--no-traffic)"
+    pmc = None
+    kname = "stft_pair4096_kernel"   # StaticSTFT(4096)'s gate kernel (hz_stft.hip)
     if not args.no_traffic and sw == 1:
         import bench
-        tb, tdetail = bench.pmc_traffic(("stft_pair_kernel<1,",), extra=("--workload", "c4"))
-        traffic = tb   # HBM bytes per frame launch (one launch per step here)
+        tb, tdetail = bench.pmc_traffic((kname, "stft_ola_kernel"), extra=("--workload", "c4"))
+        traffic = tb   # HBM bytes per launch (one frame launch + one overlap-add launch per step)
+        pmc = pmc_counts(kname, "c4", PMC_F64_MFMA)
     return {
         "metric": "STFT frames/s, StaticSTFT 4096-pt / 75% overlap spectral gate",
         "value": frames / elapsed, "unit": "frames/s",
@@ -245,11 +292,19 @@ def run_c4(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
         "n_gpus": world, "scaling": "strong", "emulated_world": shard_world,
         "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK if achieved else None,
-                     "traffic": traffic, "traffic_detail": tdetail,
-                     "kernel": "stft_pair_kernel<STATIC_GATE,3> (two real frames per transform: window, "
-                               "FFT, split + gate + merge, IFFT in LDS)",
+                     "traffic": (traffic or {}).get(kname), "traffic_ola": (traffic or {}).get("stft_ola_kernel"),
+                     "traffic_detail": tdetail,
+                     "kernel": "stft_pair4096_kernel<STATIC_GATE> (two real frames per transform: window, "
+                               "radix-8 FFT, split + gate + merge, IFFT in LDS)",
                      "kernel_ms_per_step": fms / args.steps, "ola_ms_per_step": oms / args.steps,
-                     "flops_per_frame": 491520},
+                     "flops_per_frame": 491520,
+                     "pmc": pmc,
+                     "executed_flops_per_launch": (pmc or {}).get("f64_flops"),
+                     "mfma_utilisation": (pmc or {}).get("mfma_busy_frac"),
+                     "mfma_note": "0 by design: the DFT runs as a radix-8 FFT on the FP64 VALU. An FP64 MFMA DFT "
+                                  "(v_mfma_f64_16x16x4f64, 64 x 64 factorisation) does 17x the FFT's flops at the "
+                                  "same FP64 rate (FP64 MFMA and VALU share the pipe on MI355X) and measured 2.63x "
+                                  "slower (DESIGN.md 4.1)"},
         "variant_fourier_gate625": {"frames_per_s": fr2 / e2, "kernel_ms_per_step": f2 / args.steps,
                                     "ola_ms_per_step": o2 / args.steps},
         "cpu_baseline": cpu,
@@ -342,6 +397,14 @@ def run_c5(args, torch, dev):
     bowl_rate = M * n * bl_w / (bms_w / 1e3) if bms_w > 0 else None
     dly_rate = L * n * dl_w / (dms_w / 1e3) if dms_w > 0 else None
     achieved = bowl_rate * 8 / 1e12 if bowl_rate else None
+    pipes = chain_pipes = chain_traffic = None
+    if not args.no_traffic:
+        import bench
+        kb = bms_w / max(1, bl_w) / 1e3                         # whole-signal bowl_mix_kernel, s
+        kc = fms / max(1, fl) / 1e3                              # fused block kernel, s
+        pipes = pipe_fracs(pmc_counts("bowl_mix_kernel", "c5", PMC_VALU), kb)
+        chain_pipes = pipe_fracs(pmc_counts("bowl_dly_chain_kernel", "c5", PMC_VALU), kc)
+        chain_traffic, _ = bench.pmc_traffic(("bowl_dly_chain_kernel",), extra=("--workload", "c5"))
     cpu = None
     if not args.no_cpu_baseline:
         _tests_path()
@@ -366,7 +429,11 @@ def run_c5(args, torch, dev):
                      "kernel": "bowl_mix_kernel (float phase model)",
                      "kernel_ms_whole_signal": bms_w / max(1, bl_w), "flops_per_unit": 8,
                      "mode_samples_per_s_kernel": bowl_rate,
-                     "note": "8 flops per mode-sample (+ exp + sin), FP32 vector peak (SURVEY.md 8(d) C5)"},
+                     "executed_pipes": pipes,
+                     "note": "frac: the model's 8 flops per mode-sample over the FP32 vector peak (SURVEY.md 8(d) "
+                             "C5); executed_pipes: PMC-counted FP32 / FP64 flops and transcendental lane-ops of the "
+                             "same kernel over its time, each against its own pipe's peak -- the largest fraction "
+                             "names the binding pipe"},
         "roofline_delaybank": {"bound": "hbm", "achieved": dly_rate * 20 / 1e9 if dly_rate else None,
                                "peak": HBM_PEAK, "unit": "GB/s",
                                "frac": dly_rate * 20 / 1e9 / HBM_PEAK if dly_rate else None,
@@ -378,6 +445,8 @@ def run_c5(args, torch, dev):
                   "kernel": "bowl_dly_chain_kernel (hz_bowl_fill_delaybank: the block's Bowl samples, "
                             "every line, the ring commit and the mixdown in one launch)",
                   "kernel_us_per_block": 1e3 * fms / max(1, fl),
+                  "executed_pipes": chain_pipes,
+                  "traffic_per_launch": (chain_traffic or {}).get("bowl_dly_chain_kernel"),
                   "two_calls_per_block": {"us_per_block": 1e6 * elapsed_calls / args.steps / nb,
                                           "launches_per_block": 4,
                                           "value": M * n * args.steps / elapsed_calls,

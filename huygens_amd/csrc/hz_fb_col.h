@@ -296,25 +296,33 @@ __device__ __forceinline__ void col_group(const ColArgs& a, int u, int r, ColLds
     HZ_COL_STAMP(1);
     const bool colw = w < ncol;   // (units 7, 8: fewer columns than waves)
     double2(*rows)[kRow] = L.z[w];
-    // ---- stage 3, in place: window j = segments j, j + 1; eight windows per transform, the
-    // column's groups alternating between its two waves (a group writes only its own eight rows
-    // and reads the next group's first row, which no group writes)
-    if (colw) {
-        constexpr int NW = NS - 1;
+    // ---- stage 3, in place: window j = segments j, j + 1; eight windows per transform, rounds of
+    // two groups (wave w: group 2k, wave w + 4: group 2k + 1).  A group reads its eight rows and the
+    // next group's first row and then writes its own eight rows: the round's reads all precede its
+    // writes (a barrier between), and the next round's reads touch no row this round writes.
+    {
+        constexpr int NW = NS - 1, NG = (NW + 7) / 8;
         const double sg = (c0 & 1) ? -1.0 : 1.0;
-        for (int j0 = 8 * half; j0 < NW; j0 += 16) {
-            const int j = min(j0 + g8, NW - 1);
+        for (int k = 0; k < (NG + 1) / 2; ++k) {
+            const int j0 = 8 * (2 * k + half);
+            const bool act = colw && j0 < NW;
+            const int valid = act ? min(8, NW - j0) : 0;
             double2 v[8];
+            if (act) {
+                const int j = min(j0 + g8, NW - 1);
 #pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const double2 d0 = rows[j][r8 + 8 * m], d1 = rows[j + 1][r8 + 8 * m];
-                v[m] = cmul(make_double2(fma(sg, d1.x, d0.x), fma(sg, d1.y, d0.y)), L.tn[w][r8 + 8 * m]);
+                for (int m = 0; m < 8; ++m) {
+                    const double2 d0 = rows[j][r8 + 8 * m], d1 = rows[j + 1][r8 + 8 * m];
+                    v[m] = cmul(make_double2(fma(sg, d1.x, d0.x), fma(sg, d1.y, d0.y)), L.tn[w][r8 + 8 * m]);
+                }
             }
-            const int valid = min(8, NW - j0);
-            col_fft8x8<false>(v, rows, j0, valid, l, L.w64);
-            if (g8 < valid) {
+            __syncthreads();
+            if (act) {
+                col_fft8x8<false>(v, rows, j0, valid, l, L.w64);
+                if (g8 < valid) {
 #pragma unroll
-                for (int k2 = 0; k2 < 8; ++k2) rows[j0 + g8][r8 + 8 * k2] = v[k2];   // bin r + 8 k2
+                    for (int k2 = 0; k2 < 8; ++k2) rows[j0 + g8][r8 + 8 * k2] = v[k2];   // bin r + 8 k2
+                }
             }
         }
     }
