@@ -552,7 +552,7 @@ def main():
     ap.add_argument("--response", type=int, default=-1,
                     help="stationary engine: 0 off (per-band engines only), 1 eager (default), 2 lazy")
     ap.add_argument("--resp-engine", type=int, default=-1,
-                    help="(A/B) stationary long calls: 1 column-split (default), 0 three-kernel path")
+                    help="(A/B) stationary long calls: 1 column-split, 0 three-kernel path (default)")
     ap.add_argument("--gather", action="store_true",
                     help="N > 1, time-sharded stationary calls: gather the shares on rank 0 inside each step")
     ap.add_argument("--side-steps", type=int, default=50,

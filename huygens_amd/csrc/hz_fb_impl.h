@@ -191,7 +191,7 @@ struct hz_fb {
         double* d_tw = nullptr;          // W_4096^k, k < 2048 (complex)
         // column-split path (hz_fb_col.h): W_4096^k for k < 4096, H in column layout, the inverse
         // columns T of a call, the combine's column map
-        bool col_on = true;              // hz_fb_tune_response_engine
+        bool col_on = false;             // hz_fb_tune_response_engine (column split: opt-in)
         int last_engine = 0;             // 0 three-kernel, 1 column-split (last stationary call)
         double* d_tw4k = nullptr;
         double* d_Hc = nullptr;

@@ -210,7 +210,7 @@ class Filterbank:
         check(self._lib.hz_fb_tune_response(self._h, int(min_call), int(bands_per_sample)))
 
     def tune_response_engine(self, column_split: bool = True):
-        """(A/B) 1 = column-split long calls (default), 0 = the three-kernel path"""
+        """(A/B) 1 = column-split long calls, 0 = the three-kernel path (default)"""
         check(self._lib.hz_fb_tune_response_engine(self._h, 1 if column_split else 0))
 
     def response_engine(self):

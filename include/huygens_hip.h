@@ -152,11 +152,12 @@ int hz_fb_set_response(hz_fb* h, int mode);
 /* (tuning) shortest call that runs stationary and keeps the history (0: 16384); the engine is
  * chosen when N n >= bands_per_sample (K + n) (0: 256, env HZ_FB_RESP_BANDS) */
 int hz_fb_tune_response(hz_fb* h, long min_call, long bands_per_sample);
-/* (tuning / A-B) the long-call convolution's structure: 1 (default) = column-split, two kernels
- * per call (hz_fb_col.h: forward transforms, partition MACs and inverse columns in one kernel that
- * keeps the window spectra on chip, then the output combine with the band-state pass) for banks
- * whose horizon is 8, 16 or 24 partitions of 2048; 0 = the three-kernel path (forward transforms,
- * MACs, inverse transforms) for every horizon.  Results agree to rounding. */
+/* (tuning / A-B) the long-call convolution's structure: 0 (default) = the three-kernel path
+ * (forward transforms, partition MACs, inverse transforms + band-state pass); 1 = column-split, two
+ * kernels per call (hz_fb_col.h: forward transforms, partition MACs and inverse columns in one
+ * kernel that keeps the window spectra on chip, then the output combine with the band-state pass)
+ * for banks whose horizon is 8, 16 or 24 partitions of 2048 -- measured slower on MI355X (C2: 0.048
+ * against 0.0405 ms per step).  Results agree to rounding. */
 int hz_fb_tune_response_engine(hz_fb* h, int column_split);
 /* the setting above, and whether the last stationary call ran the column-split path */
 int hz_fb_response_engine(hz_fb* h, int* column_split_on, int* last_call_column_split);

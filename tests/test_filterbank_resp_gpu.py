@@ -329,8 +329,8 @@ def test_stream_and_per_sample_after_stationary(gpu_lib, lazy):
 
 @pytest.mark.parametrize("R,centre,order", [(0.999, 1.0, 2), (0.9985, 0.5, 2), (0.997, 0.5, 2), (0.999, 0.5, 4)])
 def test_column_split_vs_three_kernel(gpu_lib, R, centre, order):
-    """The long-call convolution's two structures (hz_fb_col.h column split, default; the
-    three-kernel path, hz_fb_tune_response_engine(h, 0)) on the same calls: both against the
+    """The long-call convolution's two structures (hz_fb_col.h column split, opt-in; the
+    three-kernel path, the default) on the same calls: both against the
     restatement, ragged lengths, band states equal; horizons of 8 / 16 / 24 partitions take the
     column split."""
     from test_filterbank_lti_gpu import random_bank
@@ -341,6 +341,7 @@ def test_column_split_vs_three_kernel(gpu_lib, R, centre, order):
     else:
         fwd, back = random_bank(order, N, seed=77, radius=(0.5, R))
     g, o = make(order, N, fwd, back)
+    g.tune_response_engine(True)
     t, _ = make(order, N, fwd, back, oracle=False)
     t.tune_response_engine(False)
     rng = np.random.default_rng(21)
