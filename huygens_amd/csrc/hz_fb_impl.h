@@ -252,6 +252,7 @@ struct hz_fb {
         double* d_coef = nullptr;    // [N][2O+1] coefficients, then [N][O+1] ring rows
         size_t coef_cap = 0;
         std::vector<double> h_coef;
+        bool many = false;           // the server last served these rows through OP_FB_MANY
     } rt;
 };
 

@@ -24,7 +24,10 @@
 // coefficients() call reaches the next sample's request as a payload the server copies into the
 // device arrays (no conversion, no restart), so it applies from the next operator() on -- the
 // documented application point.
+#include <algorithm>
 #include <chrono>
+#include <memory>
+#include <mutex>
 #include <cstring>
 #include <thread>
 
@@ -198,6 +201,10 @@ static int sample_locked(hz_fb* h, double x, int dist_id, double param, double* 
         hz::set_error("hz_fb_sample: no per-sample server on device %d", h->device);
         return HZ_E_NODEV;
     }
+    if (T.many) {   // the rows were served by other workgroups (OP_FB_MANY): a fresh instance
+        hz_rt::quiesce(srv);
+        T.many = false;
+    }
     if (!T.active || h->tv_pending) {
         if (T.active) {   // a coefficient stream call left a row staged: convert back and in again
             const long keep = T.pending_ticks;
@@ -294,6 +301,181 @@ static void tick_locked(hz_fb* h) {
     h->rt.computed = false;
 }
 
+// ---- several handles per request (OP_FB_MANY) ------------------------------------------------
+// The chunk table of the last group served on each device (rebuilt when a member's arrays move)
+struct ManyCache {
+    std::vector<hz_fb*> hs;
+    std::vector<hz_rt::ManyChunk> chunks;
+    hz_rt::ManyChunk* d = nullptr;
+    size_t cap = 0;
+};
+static ManyCache g_many[64];
+static std::mutex g_many_mu;
+
+static int many_table(int device, hz_fb* const* hs, int H, int* nchunks, const hz_rt::ManyChunk** d) {
+    std::vector<hz_rt::ManyChunk> ch;
+    for (int m = 0; m < H; ++m) {
+        hz_fb* h = hs[m];
+        const int O = h->order, N = h->N;
+        const size_t nc = (size_t)N * (2 * O + 1);
+        double* R = h->rt.d_coef + nc;
+        for (int b0 = 0; b0 < N; b0 += 64) {
+            hz_rt::ManyChunk c{};
+            c.R = R + (size_t)b0 * (O + 1);
+            c.pg = h->d_pg[h->scur] + 2 * (size_t)b0;
+            c.coef = h->rt.d_coef + (size_t)b0 * (2 * O + 1);
+            c.pin = h->d_pin + b0;
+            c.gin = h->d_gin + b0;
+            c.n = std::min(64, N - b0);
+            c.m = m;
+            c.sp = h->sp;
+            c.sg = h->sg;
+            ch.push_back(c);
+        }
+    }
+    ManyCache& C = g_many[device];
+    const bool same = C.hs.size() == (size_t)H && std::equal(C.hs.begin(), C.hs.end(), hs) &&
+                      C.chunks.size() == ch.size() &&
+                      std::memcmp(C.chunks.data(), ch.data(), sizeof(hz_rt::ManyChunk) * ch.size()) == 0;
+    if (!same) {
+        if (ch.size() > C.cap) {
+            if (C.d) HZ_TRY_HIP(hipFree(C.d));
+            C.d = nullptr;
+            HZ_TRY_HIP(hipMalloc(&C.d, sizeof(hz_rt::ManyChunk) * ch.size()));
+            C.cap = ch.size();
+        }
+        HZ_TRY_HIP(hipMemcpy(C.d, ch.data(), sizeof(hz_rt::ManyChunk) * ch.size(), hipMemcpyHostToDevice));
+        C.hs.assign(hs, hs + H);
+        C.chunks = std::move(ch);
+    }
+    *nchunks = (int)C.chunks.size();
+    *d = C.d;
+    return HZ_OK;
+}
+
+// setters staged on a member since the server's copy: with the server out, straight into the
+// device arrays (targets, and the per-sample layout's coefficients)
+static int many_apply_setters(hz_fb* h) {
+    hz_fb::Rt& T = h->rt;
+    if (T.pg_gen == h->pg_gen && T.coef_gen == h->coef_gen) return HZ_OK;
+    const int O = h->order, N = h->N;
+    if (T.pg_gen != h->pg_gen) {
+        HZ_TRY_HIP(hipMemcpy(h->d_pin, h->pin.data(), sizeof(double) * N, hipMemcpyHostToDevice));
+        HZ_TRY_HIP(hipMemcpy(h->d_gin, h->gin.data(), sizeof(double) * N, hipMemcpyHostToDevice));
+        sparse_clear(h);
+    }
+    if (T.coef_gen != h->coef_gen) {
+        HZ_TRY(fb_tv_materialize(h));
+        const size_t nc = (size_t)N * (2 * O + 1);
+        T.h_coef.resize(nc);
+        for (int n = 0; n < N; ++n) {
+            for (int i = 0; i <= O; ++i) T.h_coef[(size_t)n * (2 * O + 1) + i] = h->F[(size_t)n * (O + 1) + i];
+            for (int k = 0; k < O; ++k) T.h_coef[(size_t)n * (2 * O + 1) + O + 1 + k] = h->B[(size_t)n * O + k];
+        }
+        HZ_TRY_HIP(hipMemcpy(T.d_coef, T.h_coef.data(), sizeof(double) * nc, hipMemcpyHostToDevice));
+    }
+    T.pg_gen = h->pg_gen;
+    T.coef_gen = h->coef_gen;
+    return HZ_OK;
+}
+
+static int sample_many_locked(hz_fb* const* hs, int H, const double* x, int dist_id, double param, double* y) {
+    const int O = hs[0]->order, dev = hs[0]->device;
+    HZ_TRY_HIP(hipSetDevice(dev));
+    hz_rt::Server* srv = hz_rt::server(dev);
+    if (!srv) {
+        hz::set_error("hz_fb_sample_many: no per-sample server on device %d", dev);
+        return HZ_E_NODEV;
+    }
+    std::lock_guard<std::recursive_mutex> slk(hz_rt::lock(srv));
+    // members entering the per-sample layout, members last served one by one (other workgroups),
+    // members with staged setters: all handled with the resident instance out
+    bool fresh = false;
+    for (int m = 0; m < H; ++m) {
+        hz_fb::Rt& T = hs[m]->rt;
+        const long ticks = O > 0 ? T.pending_ticks % (O + 1) : 0;
+        const bool spare_known = T.active ? T.spare_known : hs[m]->spare_ok;
+        if (!T.computed && ticks > 0 && !spare_known) {
+            hz::set_error("hz_fb_sample_many: tick() without operator() after a block call or set_state (member %d)", m);
+            return HZ_E_STATE;
+        }
+        if (!T.active || hs[m]->tv_pending || !T.many || T.pg_gen != hs[m]->pg_gen || T.coef_gen != hs[m]->coef_gen)
+            fresh = true;
+    }
+    if (fresh) {
+        hz_rt::quiesce(srv);
+        for (int m = 0; m < H; ++m) {
+            hz_fb* h = hs[m];
+            hz_fb::Rt& T = h->rt;
+            if (!T.active || h->tv_pending) {
+                if (T.active) {
+                    const long keep = T.pending_ticks;
+                    T.pending_ticks = 0;
+                    HZ_TRY(fb_rt_stop(h));
+                    T.pending_ticks = keep;
+                }
+                HZ_TRY(rt_enter(h));
+            }
+            HZ_TRY(many_apply_setters(h));
+            T.many = true;
+        }
+    }
+    int nch = 0;
+    const hz_rt::ManyChunk* d = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_many_mu);
+        HZ_TRY(many_table(dev, hs, H, &nch, &d));
+    }
+    const int groups = std::max(1, std::min(hz_rt::kGroups, (nch + hz_rt::kThreads / 64 - 1) / (hz_rt::kThreads / 64)));
+    double* res = hz_rt::result(srv, (size_t)hz_rt::kGroups * hz_rt::kMaxMany);
+    if (!res) return HZ_E_ALLOC;
+    long long w[hz_rt::kArgWords] = {};
+    hz_rt::ManyArgs* a = (hz_rt::ManyArgs*)w;
+    a->chunks = d;
+    a->out = (double*)hz_rt::dev(srv, res);
+    a->param = param;
+    a->H = H;
+    a->nchunks = nch;
+    a->O = O;
+    a->dist = dist_id;
+    a->meta = 0;
+    double* xv = (double*)(w + hz_rt::kManyHeader);
+    for (int m = 0; m < H; ++m) {
+        hz_fb::Rt& T = hs[m]->rt;
+        const long ticks = O > 0 ? T.pending_ticks % (O + 1) : 0;
+        for (long q = 0; q < ticks; ++q) {   // the input ring after the bare ticks
+            const double t0 = T.xr[O];
+            for (int k = O; k >= 1; --k) T.xr[k] = T.xr[k - 1];
+            T.xr[0] = t0;
+        }
+        const bool compute = !T.computed;
+        a->meta |= (unsigned long long)(ticks | (compute ? 8 : 0)) << (4 * m);
+        xv[m * (O + 2)] = x[m];
+        for (int k = 0; k <= O; ++k) xv[m * (O + 2) + 1 + k] = T.xr[k];
+    }
+    const size_t bytes = sizeof(long long) * (hz_rt::kManyHeader + (size_t)H * (O + 2));
+    HZ_TRY(hz_rt::call(srv, hz_rt::OP_FB_MANY, w, bytes, groups, nullptr));
+    for (int m = 0; m < H; ++m) {
+        double v = 0.0;
+        for (int g = 0; g < groups; ++g) v += res[g * H + m];   // workgroups in order
+        hz_fb* h = hs[m];
+        hz_fb::Rt& T = h->rt;
+        const bool compute = ((a->meta >> (4 * m)) & 8) != 0;
+        if (compute) {
+            T.xr[O] = x[m];
+            T.computed = true;
+            T.spare_known = true;
+            T.cached = v;
+            fb_mirror_advance(h, 1);
+        }
+        T.pending_ticks = 0;
+        T.cached_dist = dist_id;
+        ++T.seq;
+        y[m] = v;
+    }
+    return HZ_OK;
+}
+
 }  // namespace hz_fbi
 
 extern "C" {
@@ -305,6 +487,36 @@ int hz_fb_sample(hz_fb* h, double x, int dist_id, double param, double* y) {
     }
     hz_fbi::SampleLock lk(h);   // a setter from another thread goes first (this sample sees it)
     return hz_fbi::sample_locked(h, x, dist_id, param, y);
+}
+
+int hz_fb_sample_many(hz_fb* const* handles, int count, const double* x, int dist_id, double param, double* y) {
+    if (!handles || !x || !y || count < 1 || count > hz_rt::kMaxMany || dist_id < HZ_DIST_NONE ||
+        dist_id > HZ_DIST_LIMITER) {
+        hz::set_error("hz_fb_sample_many: invalid arguments (1 <= count <= %d)", hz_rt::kMaxMany);
+        return HZ_E_INVALID;
+    }
+    std::vector<hz_fb*> order(handles, handles + count);
+    for (int m = 0; m < count; ++m) {
+        if (!handles[m] || handles[m]->device != handles[0]->device || handles[m]->order != handles[0]->order) {
+            hz::set_error("hz_fb_sample_many: the handles must share a device and an order");
+            return HZ_E_INVALID;
+        }
+    }
+    const int O = handles[0]->order;
+    if (hz_rt::kManyHeader + count * (O + 2) > hz_rt::kArgWords) {
+        hz::set_error("hz_fb_sample_many: at most %d handles of order %d per request",
+                      (hz_rt::kArgWords - hz_rt::kManyHeader) / (O + 2), O);
+        return HZ_E_INVALID;
+    }
+    std::sort(order.begin(), order.end());
+    if (std::adjacent_find(order.begin(), order.end()) != order.end()) {
+        hz::set_error("hz_fb_sample_many: a handle appears twice");
+        return HZ_E_INVALID;
+    }
+    // every member held (in address order: no lock-order inversion between callers)
+    std::vector<std::unique_ptr<hz_fbi::SampleLock>> locks;
+    for (hz_fb* h : order) locks.emplace_back(new hz_fbi::SampleLock(h));
+    return hz_fbi::sample_many_locked(handles, count, x, dist_id, param, y);
 }
 
 int hz_fb_sample_tick(hz_fb* h) {

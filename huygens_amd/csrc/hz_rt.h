@@ -12,6 +12,7 @@
 // the highest priority (its own hardware queue) and leaves after kIdleNs without a request.
 #pragma once
 
+#include <cstddef>
 #include <mutex>
 
 #include "hz_common.h"
@@ -22,7 +23,7 @@ constexpr int kGroups = 8;      // workgroups of the resident kernel (each polls
 constexpr int kThreads = 512;   // threads per workgroup (units per workgroup per pass)
 constexpr int kMaxGrains = 1024;
 
-enum : int { OP_NONE = 0, OP_FB = 1, OP_DLY = 2, OP_GRAN = 3, OP_STOP = 4 };
+enum : int { OP_NONE = 0, OP_FB = 1, OP_DLY = 2, OP_GRAN = 3, OP_STOP = 4, OP_FB_MANY = 5 };
 
 // Granulator grain record (hz_granulator.hip: the block engine's layout, one 64-B line)
 struct alignas(16) Grain {
@@ -148,7 +149,32 @@ struct GranArgs {
     unsigned size, origin, wrap1, pad2;
 };
 
-constexpr int kArgWords = 30;
+// OP_FB_MANY: one sample of several Filterbanks in one request (the per-channel banks of
+// tests/filterbanks.cpp:191-211).  The static part is a device table of 64-band chunks (each with
+// its member's arrays offset to the chunk's first band); the request line carries each member's
+// input and input ring.
+constexpr int kMaxMany = 12;
+struct alignas(64) ManyChunk {
+    double* R;              // ring rows [n][O+1] from the chunk's first band
+    double* pg;             // smoothers [n][2]
+    const double* coef;     // [n][2O+1]
+    const double* pin;
+    const double* gin;
+    int n, m;               // bands in the chunk (<= 64), member
+    double sp, sg;
+};
+struct ManyArgs {
+    const ManyChunk* chunks;
+    double* out;            // (pinned result) [groups][H] partial mixdowns
+    double param;
+    int H, nchunks;
+    int O, dist;
+    unsigned long long meta;   // per member 4 bits: ticks (0..O) | compute << 3
+    double xv[1];           // per member x, then its input ring xr[0..O] (O + 2 words each)
+};
+constexpr int kManyHeader = 6;   // words before xv
+
+constexpr int kArgWords = 62;
 struct alignas(64) Req {
     long long req;          // request number << 4 | participating workgroups, written last (release)
     int op, groups;         // op; workgroups that take part (the others skip the request)
@@ -157,6 +183,7 @@ struct alignas(64) Req {
 static_assert(sizeof(FbArgs) <= sizeof(long long) * kArgWords && sizeof(DlyArgs) <= sizeof(long long) * kArgWords &&
                   sizeof(GranArgs) <= sizeof(long long) * kArgWords,
               "op arguments fit the request line");
+static_assert(offsetof(ManyArgs, xv) == 8 * kManyHeader, "OP_FB_MANY header");
 struct alignas(64) Slot {   // per workgroup
     double y, y2;           // partial mix
     long long done;         // last request served (written after y)
@@ -177,6 +204,9 @@ const void* dev(Server* s, const void* host_ptr);
 // lock(s) across a multi-request sequence when the order matters).
 int call(Server* s, int op, const void* args, size_t bytes, int groups, double* y, double* y2 = nullptr);
 std::recursive_mutex& lock(Server* s);
+// the resident instance leaves now (the next request relaunches it): a handle whose bands change
+// workgroups (OP_FB <-> OP_FB_MANY) must not read rows another XCD's L2 wrote
+void quiesce(Server* s);
 // statistics: requests served, launches of the resident kernel
 void info(Server* s, long long* requests, long long* launches, int* active);
 

@@ -67,6 +67,7 @@ struct SrvLds {
     long long req;
     int grp;
     double part[kThreads / 64];
+    double mpart[kThreads / 64][kMaxMany];   // OP_FB_MANY: per wave and member
     // OP_GRAN (one workgroup): the handle's grain list and this sample's terms
     long long gkey, gver;
     int gcount;
@@ -155,6 +156,78 @@ __device__ double op_fb(const FbArgs& a, int g, int groups) {
         v += d;
     }
     return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// OP_FB_MANY: operator() of several Filterbanks (one order O) for one sample each -- op_fb's band
+// arithmetic, op for op -- over the descriptor's 64-band chunks: wave w of workgroup g takes chunks
+// (g * waves + w) + k * (groups * waves); each chunk's mixdown is a wave tree, added per member in
+// chunk order into the wave's LDS slot, then summed over the waves in order into out[g][member]
+template <int O>
+__device__ void op_fb_many(const ManyArgs& a, const long long* xvw, int g, int groups, SrvLds& s) {
+#pragma clang fp contract(off)
+    constexpr int R1 = O + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int kWaves = kThreads / 64;
+    const int H = a.H;
+    if (lane < kMaxMany) s.mpart[wave][lane] = 0.0;
+    for (int c = g * kWaves + wave; c < a.nchunks; c += groups * kWaves) {
+        const ManyChunk& ck = a.chunks[c];
+        const int m = ck.m, b = lane;
+        const int sh = 4 * m;
+        const int ticks = (int)((a.meta >> sh) & 7), compute = (int)((a.meta >> (sh + 3)) & 1);
+        const double* xm = (const double*)xvw + m * (O + 2);   // x, xr[0..O]
+        double v = 0.0;
+        if (b < ck.n) {
+            const double* cf = ck.coef + (long)b * (2 * O + 1);
+            double f[R1], bk[O > 0 ? O : 1], R[R1];
+#pragma unroll
+            for (int i = 0; i <= O; ++i) {
+                R[i] = ck.R[(long)b * R1 + i];
+                f[i] = cf[i];
+            }
+#pragma unroll
+            for (int k = 0; k < O; ++k) bk[k] = cf[O + 1 + k];
+            double pre = ck.pg[2 * b], gain = ck.pg[2 * b + 1];
+            const double pi = ck.pin[b], gi = ck.gin[b];
+            for (int q = 0; q < ticks; ++q) {   // bare ticks: the ring rotates right
+                const double t0 = R[O];
+#pragma unroll
+                for (int k = O; k >= 1; --k) R[k] = R[k - 1];
+                R[0] = t0;
+            }
+            if (compute) {
+                pre = (1 - ck.sp) * pi + ck.sp * pre;
+                gain = (1 - ck.sg) * gi + ck.sg * gain;
+                double ff = f[0] * xm[0];
+#pragma unroll
+                for (int i = 1; i <= O; ++i) ff += f[i] * xm[i];   // xr[i - 1]
+                double bsum = 0;
+#pragma unroll
+                for (int k = 0; k < O; ++k) bsum += bk[k] * R[k];
+                R[O] = ff * pre - bsum;
+            }
+#pragma unroll
+            for (int i = 0; i <= O; ++i) ck.R[(long)b * R1 + i] = R[i];
+            ck.pg[2 * b] = pre;
+            ck.pg[2 * b + 1] = gain;
+            const double yg = R[O] * gain;
+            v = yg;
+            if (a.dist == HZ_DIST_SOFTCLIP) v = hz::dist_apply<HZ_DIST_SOFTCLIP>(yg, a.param);
+            else if (a.dist == HZ_DIST_SATURATE) v = hz::dist_apply<HZ_DIST_SATURATE>(yg, a.param);
+            else if (a.dist == HZ_DIST_LIMITER) v = hz::dist_apply<HZ_DIST_LIMITER>(yg, a.param);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) s.mpart[wave][m] += v;
+    }
+    __syncthreads();
+    if (tid < H) {
+        double y = 0.0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) y += s.mpart[w][tid];   // waves in order
+        std_sys(a.out + (long)g * H + tid, y);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -408,6 +481,17 @@ __global__ __launch_bounds__(kThreads) void rt_server_kernel(ServerArgs a) {
                 } else {
                     op_dly<double>(da, g, groups);
                 }
+            } else if (op == OP_FB_MANY) {
+                ManyArgs ma;
+                __builtin_memcpy(&ma, &s.w[1], sizeof(ManyArgs) - sizeof(double));
+                const long long* xvw = &s.w[1 + kManyHeader];
+                switch (ma.O) {
+                case 0: op_fb_many<0>(ma, xvw, g, groups, s); break;
+                case 1: op_fb_many<1>(ma, xvw, g, groups, s); break;
+                case 2: op_fb_many<2>(ma, xvw, g, groups, s); break;
+                case 3: op_fb_many<3>(ma, xvw, g, groups, s); break;
+                default: op_fb_many<4>(ma, xvw, g, groups, s); break;
+                }
             } else if (op == OP_GRAN) {
                 GranArgs ga;
                 __builtin_memcpy(&ga, &s.w[1], sizeof(ga));
@@ -535,6 +619,26 @@ int srv_launch(Server* s) {
     return HZ_OK;
 }
 
+// one server's resident instance leaves (a STOP request) and the call waits for it: the next
+// request relaunches it with every XCD's L2 written back and invalidated by the kernel boundary
+void srv_quiesce(Server* s) {
+    if (!s->active || srv_left(s)) {
+        s->active = false;
+        return;
+    }
+    Req* q = s->req();
+    q->op = OP_STOP;
+    q->groups = kGroups;
+    s->wc_fence();
+    __atomic_store_n(&q->req, (++s->seq << 4) | kGroups, __ATOMIC_RELEASE);
+    s->wc_fence();
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!srv_left(s) && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
+    }
+    (void)hipStreamSynchronize(s->stream);
+    s->active = false;
+}
+
 void srv_shutdown() {
     // process exit: every resident instance leaves (a STOP request), so no wave outlives the host
     for (Server* s : g_servers) {
@@ -577,6 +681,11 @@ Server* server(int device) {
 }
 
 std::recursive_mutex& lock(Server* s) { return s->mu; }
+
+void quiesce(Server* s) {
+    std::lock_guard<std::recursive_mutex> lk(s->mu);
+    srv_quiesce(s);
+}
 
 static double* grow(double** p, size_t* cap, size_t n) {
     if (n <= *cap) return *p;

@@ -266,3 +266,15 @@ class Filterbank:
         e, b, c, r = C.c_int(), C.c_long(), C.c_long(), C.c_int()
         check(self._lib.hz_fb_stream_info(self._h, C.byref(e), C.byref(b), C.byref(c), C.byref(r)))
         return bool(e.value), b.value, c.value, bool(r.value)
+
+
+def sample_many(banks, x, dist: int = HZ_DIST_NONE, param: float = 0.0) -> np.ndarray:
+    """One sample of several Filterbanks in one per-sample server request (hz_fb_sample_many):
+    y[i] = banks[i](x[i], dist) -- each bank's tick() stays separate (tests/filterbanks.cpp:191-211)."""
+    n = len(banks)
+    lib = banks[0]._lib
+    hs = (C.c_void_p * n)(*[b._h for b in banks])
+    xs = np.ascontiguousarray(x, dtype=np.float64)
+    ys = np.empty(n)
+    check(lib.hz_fb_sample_many(hs, n, xs.ctypes.data_as(PD), int(dist), float(param), ys.ctypes.data_as(PD)))
+    return ys

@@ -98,6 +98,14 @@ int hz_fb_tick(hz_fb* h);
  * hz_fb_tick). */
 int hz_fb_sample(hz_fb* h, double x, int dist_id, double param, double* y);
 int hz_fb_sample_tick(hz_fb* h);
+/* One sample of several Filterbanks in ONE per-sample server request -- the per-channel banks of
+ * tests/filterbanks.cpp:191-211 (CHANELS FFilterbank<double,864,2> ticked per sample, &softclip):
+ * y[i] = operator()(x[i], dist) of handles[i] for every i, each with its own pending tick()s, as
+ * count separate hz_fb_sample calls would give (the mixdown summed in another fixed order: equal to
+ * rounding).  The handles share a device and an order, each appears once; count <= 12 and
+ * 6 + count (order + 2) <= 62.  Setters on a member since its last sample, and switching a handle
+ * between this call and hz_fb_sample, relaunch the server (tens of microseconds once). */
+int hz_fb_sample_many(hz_fb* const* handles, int count, const double* x, int dist_id, double param, double* y);
 /* the number of per-sample calls served when the last setter (coefficients / boost / mix / open)
  * ran: the setter applies from that call on (setters may come from another thread while samples
  * run -- every entry point holds the handle's lock; the reference's MIDI thread,

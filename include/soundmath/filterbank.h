@@ -91,4 +91,19 @@ public:
     void print() = delete;
 };
 
+// (new) one sample of several banks in ONE per-sample request: out[j] = (*F[j])(in[j], dist_id, param)
+// for every j (each with its own pending tick()s) -- the multi-channel loop of tests/filterbanks.cpp:
+// 191-211 keeps its per-channel tick() calls and changes one line, the channels' operator() calls
+// into one call per sample:
+//     double ys[CHANELS];   // xs[j] = each channel's filterbank input
+//     soundmath::sample_many(Fs, CHANELS, xs, ys, HZ_DIST_SOFTCLIP);
+template <typename Bank>
+void sample_many(Bank* const* banks, int count, const double* in, double* out, int dist_id = HZ_DIST_NONE,
+                 double param = 0.0) {
+    hz_fb* hs[12];
+    if (count > 12) detail::check(HZ_E_INVALID, "sample_many: at most 12 banks");
+    for (int j = 0; j < count; ++j) hs[j] = banks[j]->native();
+    detail::check(hz_fb_sample_many(hs, count, in, dist_id, param, out), "sample_many");
+}
+
 }  // namespace soundmath

@@ -364,3 +364,64 @@ def test_granulator_per_sample_beyond_server_grain_cap(gpu_lib):
             assert g.activity() == o.activity() == 1200
     assert g.activity() == o.activity() == 0
     assert np.max(np.abs(yg - yo)) <= 1e-12 * np.max(np.abs(yo))
+
+
+def test_sample_many_multichannel(gpu_lib):
+    """tests/filterbanks.cpp:191-211: CHANELS FFilterbank<double,864,2> per sample with &softclip,
+    each channel its own input, served by ONE request per sample (hz_fb_sample_many), against the
+    restatement per channel; a setter on one channel, single-handle calls and a block call in
+    between (the server relaunches on those switches), and the per-frame latency."""
+    from huygens_amd import Filterbank, sample_many
+    from huygens_amd._lib import HZ_DIST_SOFTCLIP
+    H, N = 8, 864
+    fwd, back = resonant_coefficients(N, 0.999, 1.0)
+    gs, os_ = [], []
+    for k in range(H):
+        g, o = Filterbank(2, N), OracleFilterbank(2, N)
+        for fb in (g, o):
+            for n in range(N):
+                fb.coefficients(n, fwd[n], back[n])
+            fb.boost(np.full(N, 1.0 + 0.1 * k))
+            fb.open()
+        o.distortion(HZ_DIST_SOFTCLIP, 0.0)
+        gs.append(g)
+        os_.append(o)
+    rng = np.random.default_rng(13)
+    T = 1500
+    x = rng.uniform(-1, 1, (T, H))
+    worst, lat = 0.0, []
+    for t in range(T):
+        if t == 600:   # a MIDI-thread setter on one channel
+            gs[3].boost(np.full(N, 0.5))
+            os_[3].boost(np.full(N, 0.5))
+        if 900 <= t < 905:   # the same channels one by one for a few samples
+            for k in range(H):
+                gs[k].distortion(HZ_DIST_SOFTCLIP, 0.0)
+            yg = np.array([gs[k](x[t, k]) for k in range(H)])
+        else:
+            t0 = time.perf_counter()
+            yg = sample_many(gs, x[t], HZ_DIST_SOFTCLIP, 0.0)
+            lat.append(time.perf_counter() - t0)
+        yo = np.array([os_[k](x[t, k]) for k in range(H)])
+        for k in range(H):
+            gs[k].tick()
+            os_[k].tick()
+        worst = max(worst, float(np.max(np.abs(yg - yo) / np.maximum(1e-30, np.abs(yo)))))
+    assert worst < 1e-8, worst
+    # a block call on one channel after the per-sample calls, then per-sample again
+    xb = rng.uniform(-1, 1, 2048)
+    yb = gs[0].process(xb)
+    os_[0].distortion(HZ_DIST_SOFTCLIP, 0.0)
+    yob = os_[0].process(xb)
+    assert np.max(np.abs(yb - yob)) <= 1e-8 * np.max(np.abs(yob))
+    for t in range(50):
+        v = rng.uniform(-1, 1, H)
+        yg = sample_many(gs, v, HZ_DIST_SOFTCLIP, 0.0)
+        yo = np.array([os_[k](v[k]) for k in range(H)])
+        for k in range(H):
+            gs[k].tick()
+            os_[k].tick()
+        assert np.max(np.abs(yg - yo) / np.maximum(1e-30, np.abs(yo))) < 1e-8
+    lat = np.sort(np.array(lat[100:]))
+    print(f"sample_many {H}x{N}: median {1e6 * np.median(lat):.1f} us per frame, p99 {1e6 * lat[int(0.99 * len(lat))]:.1f}")
+    assert np.median(lat) < 20.8e-6, np.median(lat)
