@@ -425,3 +425,39 @@ def test_sample_many_multichannel(gpu_lib):
     lat = np.sort(np.array(lat[100:]))
     print(f"sample_many {H}x{N}: median {1e6 * np.median(lat):.1f} us per frame, p99 {1e6 * lat[int(0.99 * len(lat))]:.1f}")
     assert np.median(lat) < 20.8e-6, np.median(lat)
+
+
+def test_sample_many_cpp_multichannel(gpu_lib, tmp_path):
+    """The C++ drop-in (tests/cpp/multichannel.cpp): 8 x FFilterbank<double,864,2> with softclip,
+    one soundmath::sample_many call per frame (the one-line change to tests/filterbanks.cpp's loop);
+    outputs against the restatement per channel, and the per-frame time of a C++ caller."""
+    from huygens_amd._lib import HZ_DIST_SOFTCLIP
+    H, N, T = 8, 864, 4000
+    fwd, back = resonant_coefficients(N, 0.999, 1.0)
+    np.concatenate([np.asarray(fwd)[:, :3], np.asarray(back)[:, :2]], axis=1).astype(np.float64).tofile(tmp_path / "coef.bin")
+    x = np.random.default_rng(21).uniform(-1, 1, (T, H))
+    x.tofile(tmp_path / "x.bin")
+    lib = os.path.join(ROOT, "huygens_amd", "lib")
+    exe = str(tmp_path / "multichannel")
+    r = subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "cpp", "multichannel.cpp"), "-o", exe, "-L", lib, "-lhuygens_hip",
+                        f"-Wl,-rpath,{lib}", "-Wl,-rpath-link,/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    p = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "multichannel ok" in p.stdout, p.stdout + p.stderr
+    y = np.fromfile(tmp_path / "y.bin").reshape(T, H)
+    lat = np.fromfile(tmp_path / "lat.bin")
+    for k in range(H):
+        o = OracleFilterbank(2, N)
+        for n in range(N):
+            o.coefficients(n, fwd[n], back[n])
+        o.boost(np.full(N, 1.0 + 0.1 * k))
+        o.open()
+        o.distortion(HZ_DIST_SOFTCLIP, 0.0)
+        yo = np.array([(o(v), o.tick())[0] for v in x[:, k]])
+        assert np.max(np.abs(y[:, k] - yo) / np.maximum(1e-30, np.abs(yo))) < 1e-8, k
+    lat = np.sort(lat[200:])
+    med, p99 = float(np.median(lat)), float(lat[int(0.99 * len(lat))])
+    print(f"C++ sample_many 8x864 softclip: median {1e6 * med:.2f} us per frame, p99 {1e6 * p99:.2f} us")
+    assert med < 20.8e-6, med
