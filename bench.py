@@ -179,6 +179,16 @@ def per_sample_rates(device, samples=12000):
             fb(xs[i % len(xs)])
             fb.tick()
     timed("filterbank_8x864_interleaved", st8, n=samples // 4, frames=8, path="per-sample server, 8 handles")
+    from huygens_amd import sample_many
+    from huygens_amd._lib import HZ_DIST_SOFTCLIP
+    xs8 = rng.uniform(-1, 1, (samples // 4 + 500, 8))
+
+    def stm(i):   # tests/filterbanks.cpp:191-211: 8 channels, &softclip, one request per frame
+        sample_many(fbs, xs8[i % len(xs8)], HZ_DIST_SOFTCLIP, 0.0)
+        for fb in fbs:
+            fb.tick()
+    timed("filterbank_8x864_sample_many_softclip", stm, n=samples // 4, frames=1,
+          path="per-sample server, OP_FB_MANY: one request per frame for the 8 handles (hz_fb_sample_many)")
     for fb in fbs:
         fb.close()
     d = Delay(10, 2 * 48000, device=device)
