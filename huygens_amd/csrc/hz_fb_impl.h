@@ -229,6 +229,22 @@ struct hz_fb {
             long calls = 0;
             long long* flags_dev = nullptr;   // completion flags of a host-buffer call (hz_fb_process)
             long long flags_seq = 0;
+            // horizons past the head (K > 2^17, e.g. R = 0.9999): the response's tail h[K1, K) is
+            // convolved per 16384-sample epoch ahead of time, on a side stream, by the long-call
+            // engine's kernels (hz_fb_resp.hip fb_resp_tail_conv); blocks add tail_out
+            bool tail = false;
+            long K1 = 0;                 // head horizon (<= 2^17)
+            int tQ = 0;                  // tail partitions of 2048
+            double* d_tH = nullptr;      // [tQp][2048] complex tail partition spectra, then [tQp] bin 2048
+            size_t tH_cap = 0;
+            double *d_tZ = nullptr, *d_tY = nullptr;   // the tail convolution's window / output spectra
+            size_t tZ_cap = 0, tY_cap = 0;
+            double* d_tout = nullptr;    // [2][16384] tail outputs of epochs e (slot e & 1)
+            size_t tout_cap = 0;
+            long tail_launched = -1;     // last epoch whose tail convolution was issued
+            bool tail_async[2] = {false, false};   // that slot's convolution ran on the side stream
+            hipStream_t side = nullptr;
+            hipEvent_t ev_main = nullptr, ev_tail[2] = {nullptr, nullptr};
         } st;
     } resp;
     // per-sample path (hz_fb_rt.hip): OP_FB requests to the device's per-sample server (hz_rt.hip)
@@ -368,6 +384,10 @@ int fb_stream_upkeep(hz_fb* h);        // smoothers and x history over the strea
 int fb_stream_to_hist(hz_fb* h);       // the ring's history back to resp.d_hist (long calls)
 void fb_stream_reset(hz_fb* h);        // state overwritten (set_state, tick)
 void fb_stream_free(hz_fb* h);
+// the streaming engine's response tail (hz_fb_resp.hip): partition spectra of h[K1, K), and the
+// convolution out[i] = sum_{tau < Kt} h[K1 + tau] u[Kt + i - tau], i < n, of a contiguous u
+int fb_resp_tail_spectra(hz_fb* h, long K1);
+int fb_resp_tail_conv(hz_fb* h, const double* u, long n, double* out, hipStream_t st);
 // hz_filterbank.hip: one ring rotation of a tick() without compute (needs spare_ok)
 int fb_tick_rotate(hz_fb* h);
 // hz_fb_rt.hip (per-sample engine)

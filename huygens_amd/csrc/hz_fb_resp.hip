@@ -214,6 +214,7 @@ struct RespArgs {
     double sp_n, sg_n;
     double* xhist_next;
     int N, O;
+    int upkeep;           // 0: a plain convolution (the streaming engine's response tail)
 };
 
 // u = [hist | x | 0 ...], indexed from the launch's first output block (off)
@@ -426,7 +427,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         if (t0 < a.n_out) a.out[a.off + t0] = vr[i];
         if (t0 + 1 < a.n_out) a.out[a.off + t0 + 1] = vi[i];
     }
-    resp_upkeep(a, b);
+    if (a.upkeep) resp_upkeep(a, b);
 #ifdef HZ_DIAG_STAMPS
     if (stp && t == 0) stp[1] = stp[2] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -754,6 +755,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.N = h->N;
     a.O = h->order;
     a.nz = nz;
+    a.upkeep = 1;
     // EAGER, n >= K: the band states after the call are the zero-start states over the call's last
     // K samples, independent of the convolution: the state pass runs as extra workgroups of the
     // inverse kernel (orders <= 2: 256 registers; prefetching its operands into the XCDs' L2 from the
@@ -878,6 +880,60 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     h->prof_launches += h->prof ? 1 : 0;
     ++R.calls;
     fb_mirror_advance(h, n);
+    return HZ_OK;
+}
+
+int fb_resp_tail_spectra(hz_fb* h, long K1) {
+    hz_fb::Resp& R = h->resp;
+    hz_fb::Resp::Stream& S = R.st;
+    const long Kt = R.K - K1;
+    const int Q = (int)(Kt / kP), Qp = q_padded(Q);
+    HZ_TRY(resp_alloc(&S.d_tH, &S.tH_cap, (size_t)Qp * (2 * kH + 1)));
+    HZ_TRY_HIP(hipMemsetAsync(S.d_tH, 0, sizeof(double) * (size_t)Qp * (2 * kH + 1), h->stream));
+    hipLaunchKernelGGL(resp_hspec_kernel, dim3((unsigned)Q), dim3(kThreads), 0, h->stream, (const double*)(R.d_h + K1),
+                       Kt, (const double2*)R.d_tw, (double2*)S.d_tH, S.d_tH + (size_t)Qp * 2 * kH);
+    HZ_TRY_HIP(hipGetLastError());
+    S.tQ = Q;
+    return HZ_OK;
+}
+
+int fb_resp_tail_conv(hz_fb* h, const double* u, long n, double* out, hipStream_t st) {
+    hz_fb::Resp& R = h->resp;
+    hz_fb::Resp::Stream& S = R.st;
+    const int Q = S.tQ, Qp = q_padded(Q);
+    const long Kt = (long)Q * kP;
+    const int B = (int)((n + kP - 1) / kP), nz = Q + B - 1;
+    const int zrows = (B + 64 - 1) / 64 * 64 + Qp;
+    if ((size_t)zrows * (2 * kH + 1) > S.tZ_cap) {
+        HZ_TRY(resp_alloc(&S.d_tZ, &S.tZ_cap, (size_t)zrows * (2 * kH + 1)));
+        HZ_TRY_HIP(hipMemsetAsync(S.d_tZ, 0, sizeof(double) * S.tZ_cap, st));
+    }
+    HZ_TRY(resp_alloc(&S.d_tY, &S.tY_cap, (size_t)B * kH * 2));
+    RespArgs a{};
+    a.hist = u;
+    a.x = u + Kt;
+    a.K = Kt;
+    a.n = n;
+    a.off = 0;
+    a.n_out = n;
+    a.Q = Q;
+    a.B = B;
+    a.nz = nz;
+    a.tw = (const double2*)R.d_tw;
+    a.Z = (double2*)S.d_tZ;
+    a.Zn = S.d_tZ + (size_t)zrows * 2 * kH;
+    a.Y = (const double2*)S.d_tY;
+    a.Hn = S.d_tH + (size_t)Qp * 2 * kH;
+    a.out = out;
+    a.upkeep = 0;
+    hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, st, a);
+    HZ_TRY_HIP(hipGetLastError());
+    const int nmac = (kH / 256) * ((B + kMacR - 1) / kMacR);
+    hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)nmac), dim3(256), 0, st, (const double2*)S.d_tH,
+                       (const double2*)S.d_tZ, (double2*)S.d_tY, Q, Qp, B);
+    HZ_TRY_HIP(hipGetLastError());
+    hipLaunchKernelGGL(resp_inv_kernel<0>, dim3((unsigned)B), dim3(kThreads), 0, st, a, hz_state::StateArgs());
+    HZ_TRY_HIP(hipGetLastError());
     return HZ_OK;
 }
 

@@ -35,7 +35,9 @@ constexpr int kSP = hz_fbi::kStreamBlock;   // partition = call length
 constexpr int kSF = 2 * kSP;                // real transform length
 constexpr int kCols = 33;                   // stored columns k1 = 0..32
 constexpr int kT = 256;                     // threads per column workgroup
-constexpr long kMaxK = 1L << 17;            // longest horizon streamed (Q <= 128 partitions)
+constexpr long kMaxK = 1L << 17;            // longest head streamed (Q <= 128 partitions of 1024)
+constexpr long kMaxTailK = 1L << 21;        // longest horizon streamed with a response tail
+constexpr long kE = 16384;                  // tail epoch: h[K1, K) convolved per 16384 outputs
 // twiddle table (double2): W_64^m (m < 64), W_32^m (m < 32), W_2048^m (m < 1024)
 constexpr int kTw64 = 0, kTw32 = 64, kTw2k = 96, kTwN = 96 + 1024;
 
@@ -158,6 +160,7 @@ struct StreamArgs {
     // stream synchronisation (null: device-buffer calls)
     long long* flags;
     long long seq;
+    const double* tail2;  // [1024] the response tail's contribution to this block (null: none)
 };
 
 // all of this workgroup's stores complete, then one system-scope release of the flag
@@ -392,7 +395,7 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
 #pragma unroll
             for (int q = 0; q < 32; ++q) y += s.part[q][t];
             const double tail = (s.tpart[0][t] + s.tpart[1][t]) + (s.tpart[2][t] + s.tpart[3][t]);
-            a.out[t0 + t] = y + tail;
+            a.out[t0 + t] = a.tail2 ? (y + tail) + a.tail2[t0 + t] : y + tail;
         }
         post_done(a);
     }
@@ -458,24 +461,51 @@ int s_alloc(double** p, size_t* cap, size_t need) {
     return HZ_OK;
 }
 
+// the side stream's work on the ring done (before anything else reuses or rewrites it)
+int tail_quiet(hz_fb::Resp::Stream& S) {
+    if (S.side) HZ_TRY_HIP(hipStreamSynchronize(S.side));
+    S.tail_async[0] = S.tail_async[1] = false;
+    return HZ_OK;
+}
+
 // buffers for the current horizon
 int stream_setup(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     hz_fb::Resp::Stream& S = R.st;
     const long K = R.K;
-    const long ring = K + 2 * kSP;
+    const bool tail = K > kMaxK;
+    const long K1 = tail ? kMaxK : K;
+    // with a tail the ring also keeps the epoch before the oldest input a tail convolution reads
+    const long ring = K + 2 * kSP + (tail ? kE : 0);
     if (S.R != ring) {   // a new horizon: the ring's contents no longer hold the history
+        HZ_TRY(tail_quiet(S));
         S.R = ring;
         S.line_hist = false;
         S.fdl_valid = false;
         S.hs_gen = -1;
         S.head = 0;
+        S.tail_launched = -1;
     }
+    S.tail = tail;
+    S.K1 = K1;
+    const size_t lcap = S.line_cap;
     HZ_TRY(s_alloc(&S.d_line, &S.line_cap, (size_t)(2 * ring)));
+    // never-written positions are zeros: a tail convolution's windows reach back past the history
+    // (into outputs nobody reads), and a stale NaN there would spread through the window's FFT
+    if (S.line_cap != lcap) HZ_TRY_HIP(hipMemset(S.d_line, 0, sizeof(double) * S.line_cap));
+    if (tail) {
+        HZ_TRY(s_alloc(&S.d_tout, &S.tout_cap, (size_t)(2 * kE)));
+        if (!S.side) {
+            HZ_TRY_HIP(hipStreamCreateWithFlags(&S.side, hipStreamNonBlocking));
+            HZ_TRY_HIP(hipEventCreateWithFlags(&S.ev_main, hipEventDisableTiming));
+            HZ_TRY_HIP(hipEventCreateWithFlags(&S.ev_tail[0], hipEventDisableTiming));
+            HZ_TRY_HIP(hipEventCreateWithFlags(&S.ev_tail[1], hipEventDisableTiming));
+        }
+    }
     const size_t col = (size_t)kCols * 32 * 2;   // doubles per spectrum (33 columns x 32 bins)
     const size_t zcap = S.zs_cap, hcap = S.hs_cap;
-    HZ_TRY(s_alloc(&S.d_ZS, &S.zs_cap, (size_t)(K / kSP) * col));
-    HZ_TRY(s_alloc(&S.d_HS, &S.hs_cap, (size_t)(K / kSP + 8) * col));   // 8 zero rows past Q
+    HZ_TRY(s_alloc(&S.d_ZS, &S.zs_cap, (size_t)(K1 / kSP) * col));
+    HZ_TRY(s_alloc(&S.d_HS, &S.hs_cap, (size_t)(K1 / kSP + 8) * col));   // 8 zero rows past Q
     // zero rows (and never-written slots) must be exact zeros: the MAC multiplies them
     if (S.zs_cap != zcap) HZ_TRY_HIP(hipMemset(S.d_ZS, 0, sizeof(double) * S.zs_cap));
     if (S.hs_cap != hcap) HZ_TRY_HIP(hipMemset(S.d_HS, 0, sizeof(double) * S.hs_cap));
@@ -527,7 +557,7 @@ StreamArgs stream_args(hz_fb* h) {
     a.prev = ring_index(S, S.pos - kSP);
     a.HS = (const double2*)S.d_HS;
     a.ZS = (double2*)S.d_ZS;
-    a.Q = (int)(h->resp.K / kSP);
+    a.Q = (int)(S.K1 / kSP);
     a.head = S.head;
     a.tw = (const double2*)S.d_tw;
     a.h = h->resp.d_h;
@@ -543,7 +573,42 @@ StreamArgs stream_args(hz_fb* h) {
     a.Rout = Rb + b * col;
     a.flags = nullptr;
     a.seq = 0;
+    a.tail2 = nullptr;
     return a;
+}
+
+// the tail's contribution to the outputs of epoch e, out[i] = sum_{tau >= K1} h[tau] x[eE + i - tau]
+// (i < kE), into slot e & 1: the long-call engine's convolution of the ring from position eE - K
+int tail_issue(hz_fb* h, long e, hipStream_t st) {
+    hz_fb::Resp::Stream& S = h->resp.st;
+    const long p0 = e * kE - h->resp.K;
+    return hz_fbi::fb_resp_tail_conv(h, S.d_line + ring_index(S, p0), kE, S.d_tout + (e & 1) * kE, st);
+}
+
+// before a block at position pos: the tail of its epoch is ready on the handle's stream, and the
+// next epoch's convolution is issued on the side stream (its inputs are all older than K1 - kE
+// samples before the epoch: written long ago; the main stream waits for it at the next epoch)
+int tail_schedule(hz_fb* h) {
+    hz_fb::Resp::Stream& S = h->resp.st;
+    const long e = S.pos / kE;
+    if (S.tail_launched < e) {   // (prime: this epoch's tail on the handle's stream)
+        HZ_TRY(tail_issue(h, e, h->stream));
+        S.tail_async[e & 1] = false;
+        S.tail_launched = e;
+    }
+    if (S.tail_async[e & 1]) {
+        HZ_TRY_HIP(hipStreamWaitEvent(h->stream, S.ev_tail[e & 1], 0));
+        S.tail_async[e & 1] = false;
+    }
+    if (S.tail_launched < e + 1) {
+        HZ_TRY_HIP(hipEventRecord(S.ev_main, h->stream));   // the ring's writes so far
+        HZ_TRY_HIP(hipStreamWaitEvent(S.side, S.ev_main, 0));
+        HZ_TRY(tail_issue(h, e + 1, S.side));
+        HZ_TRY_HIP(hipEventRecord(S.ev_tail[(e + 1) & 1], S.side));
+        S.tail_async[(e + 1) & 1] = true;
+        S.tail_launched = e + 1;
+    }
+    return HZ_OK;
 }
 
 }  // namespace
@@ -559,7 +624,7 @@ bool fb_stream_trackable(hz_fb* h, long n, bool conv) {
         return false;
     // the horizon (hz_fb_resp.hip resp_setup): computed once per coefficient set
     if (R.K == -2 && fb_resp_setup(h) != HZ_OK) return false;
-    return R.K > 0 && R.K <= kMaxK;
+    return R.K > 0 && R.K <= kMaxTailK;
 }
 
 bool fb_stream_eligible(hz_fb* h, long n, bool conv) {
@@ -571,7 +636,7 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
     hz_fb::Resp::Stream& S = R.st;
     HZ_TRY(fb_resp_build(h));   // h (and the band-state operands) for the current bank
     HZ_TRY(stream_setup(h));
-    const int Q = (int)(R.K / kSP);
+    const int Q = (int)(S.K1 / kSP);
     if (S.hs_gen != R.h_gen) {   // partition spectra of the current h
         // rows Q .. Q + 7 are read by the MAC roles and must be exact zeros; a shorter horizon than
         // the buffer was sized for leaves an older response's spectra there
@@ -580,6 +645,11 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
         hipLaunchKernelGGL(stream_hs_kernel, dim3(kCols, (unsigned)Q), dim3(kT), 0, h->stream, (const double*)R.d_h,
                            (const double2*)S.d_tw, (double2*)S.d_HS);
         HZ_TRY_HIP(hipGetLastError());
+        if (S.tail) {
+            HZ_TRY(tail_quiet(S));
+            HZ_TRY(fb_resp_tail_spectra(h, S.K1));
+            S.tail_launched = -1;
+        }
         S.hs_gen = R.h_gen;
     }
     if (!S.line_hist) HZ_TRY(hist_to_line(h));
@@ -592,9 +662,11 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
         S.blk = 0;
         S.fdl_valid = true;
     }
+    if (S.tail) HZ_TRY(tail_schedule(h));
     StreamArgs a = stream_args(h);
     a.x = d_in;
     a.out = d_out;
+    if (S.tail) a.tail2 = S.d_tout + ((S.pos / kE) & 1) * kE + (S.pos % kE);
     a.flags = S.flags_dev;   // set by hz_fb_process for its zero-copy call only
     a.seq = S.flags_seq;
     hipEvent_t* e = nullptr;
@@ -626,6 +698,10 @@ int fb_stream_track(hz_fb* h, const double* d_in, long n, bool conv) {
     hz_fb::Resp& R = h->resp;
     hz_fb::Resp::Stream& S = R.st;
     S.fdl_valid = false;
+    if (S.tail_launched >= 0) {   // streaming stops: its tail convolutions finish before the ring moves on
+        HZ_TRY(tail_quiet(S));
+        S.tail_launched = -1;
+    }
     if (!fb_stream_trackable(h, n, conv)) {
         R.run = 0;
         return HZ_OK;
@@ -681,6 +757,8 @@ int fb_stream_to_hist(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     hz_fb::Resp::Stream& S = R.st;
     if (!S.line_hist) return HZ_OK;
+    HZ_TRY(tail_quiet(S));
+    S.tail_launched = -1;
     HZ_TRY(fb_stream_upkeep(h));
     if (R.run > 0) {
         HZ_TRY(fb_resp_setup(h));
@@ -695,6 +773,8 @@ int fb_stream_to_hist(hz_fb* h) {
 
 void fb_stream_reset(hz_fb* h) {
     hz_fb::Resp::Stream& S = h->resp.st;
+    (void)tail_quiet(S);
+    S.tail_launched = -1;
     S.pend = 0;
     S.line_hist = false;
     S.fdl_valid = false;
@@ -702,8 +782,12 @@ void fb_stream_reset(hz_fb* h) {
 
 void fb_stream_free(hz_fb* h) {
     hz_fb::Resp::Stream& S = h->resp.st;
-    for (double* p : {S.d_line, S.d_ZS, S.d_HS, S.d_CR, S.d_tw})
+    (void)tail_quiet(S);
+    for (double* p : {S.d_line, S.d_ZS, S.d_HS, S.d_CR, S.d_tw, S.d_tH, S.d_tZ, S.d_tY, S.d_tout})
         if (p) (void)hipFree(p);
+    for (hipEvent_t e : {S.ev_main, S.ev_tail[0], S.ev_tail[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (S.side) (void)hipStreamDestroy(S.side);
     const bool on = S.on;
     S = hz_fb::Resp::Stream();
     S.on = on;

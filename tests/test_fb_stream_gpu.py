@@ -251,3 +251,36 @@ def test_stream_mix_mid_stream(gpu_lib):
     for _ in range(6):
         run()
     g.close()
+
+
+def test_stream_high_q_tail(gpu_lib):
+    """ a horizon past the head's 2^17 samples (R = 0.9999: K ~ 0.4-0.5 M): the
+    1024-sample calls stream in one launch each, the response tail h[K1, K) added from per-epoch
+    (16384-sample) convolutions issued ahead on a side stream -- per block against the restatement
+    over several epochs, through a long call, a setter and get_state."""
+    from huygens_amd._lib import HZ_FB_PATH_RESPONSE, HZ_FB_PATH_STREAM
+    N = 64
+    g, o = _bank(N, R=0.9999, k_p=0.01, k_g=0.01)
+    rng = np.random.default_rng(31)
+
+    def run(n, tol=1e-6):
+        x = rng.uniform(-1, 1, n).astype(np.float32).astype(np.float64)
+        yg, yc = g.process(x), o.process(x)
+        err, _ = block_errors(yg, yc)
+        assert err.max() <= tol, (n, g.last_path(), err.max())
+        return g.last_path()
+
+    # long calls until stationary (the horizon needs K converged samples)
+    paths = [run(200_000) for _ in range(6)]
+    K = g.response_info()[0]
+    assert K > 1 << 17, K
+    assert paths[-1] == HZ_FB_PATH_RESPONSE, paths
+    bp = [run(B) for _ in range(70)]   # > 4 epochs of 16 blocks
+    assert all(p == HZ_FB_PATH_STREAM for p in bp), bp
+    st_g, st_c = g.get_state(), o.get_state()
+    sc = np.max(np.abs(st_c[2:2 + 2 * N]))
+    assert np.max(np.abs(st_g[2:2 + 2 * N] - st_c[2:2 + 2 * N])) <= 1e-6 * sc
+    assert [run(B) for _ in range(20)] == [HZ_FB_PATH_STREAM] * 20
+    assert run(50_000) == HZ_FB_PATH_RESPONSE
+    assert [run(B) for _ in range(40)] == [HZ_FB_PATH_STREAM] * 40
+    g.close()

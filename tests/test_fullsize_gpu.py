@@ -234,6 +234,8 @@ def test_c2_high_q_stationary_and_blocks(gpu_lib, c2_high_q):
         bpaths.append(g.last_path())
         assert e <= TIGHT_HQ, (len(bpaths), bpaths[-1], e)
     print("R = 0.9999 1024-sample calls: worst", wb, "paths", sorted(set(bpaths)))
+    from huygens_amd._lib import HZ_FB_PATH_STREAM
+    assert bpaths[-1] == HZ_FB_PATH_STREAM, bpaths   # the streaming engine with its response tail
 
 
 def test_c2_high_q_impulse_horizon(gpu_lib, c2_high_q):
