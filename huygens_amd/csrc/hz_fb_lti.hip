@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "hz_dd.h"
 #include "hz_fb_impl.h"
 #include "hz_fb_rec.h"
 
@@ -100,39 +101,38 @@ void build_record_lti(const double* b, const double* av, double* rec) {
         for (int m = 0; m < XW; ++m) rec[R::E0 + m] = (double)F(L - 1, m);
         for (int k = 0; k < O; ++k)
             for (int i = 0; i < O; ++i) rec[R::EH + k * O + i] = (double)F(L - 1 - k, i);
-        // homogeneous responses: y[-1-k] = 1, zero input
-        long double Kh[L][O];
+        // homogeneous responses: y[-1-k] = 1, zero input; they and the chunk transition's powers
+        // in double-double, M^64 keeping its low word (the tile and segment carries apply it many
+        // times: hz_dd.h)
+        using hz_dd::dd;
+        dd Kh[L][O];
         for (int k = 0; k < O; ++k) {
-            long double yh[O];
-            for (int q = 0; q < O; ++q) yh[q] = (q == k) ? 1.0L : 0.0L;
+            dd yh[O];
+            for (int q = 0; q < O; ++q) yh[q] = {q == k ? 1.0 : 0.0, 0.0};
             for (int j = 0; j < L; ++j) {
-                long double y = 0;
-                for (int q = 0; q < O; ++q) y -= (long double)av[q] * yh[q];
+                dd y{0.0, 0.0};
+                for (int q = 0; q < O; ++q) y = hz_dd::add(y, hz_dd::mul(yh[q], -av[q]));
                 for (int q = O - 1; q > 0; --q) yh[q] = yh[q - 1];
                 yh[0] = y;
                 Kh[j][k] = y;
-                rec[R::K + j * O + k] = (double)y;
+                rec[R::K + j * O + k] = y.hi;
             }
         }
-        long double M[O][O], T[O][O], Qp[O][O];
+        dd M[O][O], T[O][O], Qp[O][O];
         for (int r = 0; r < O; ++r)
             for (int c = 0; c < O; ++c) {
                 M[r][c] = Kh[L - 1 - r][c];
-                Qp[r][c] = (r == c) ? 1.0L : 0.0L;
+                Qp[r][c] = {r == c ? 1.0 : 0.0, 0.0};
             }
         for (int e = 0; e <= 64; ++e) {
             const int ps = e == 1 ? 0 : e == 2 ? 1 : e == 4 ? 2 : e == 8 ? 3 : e == 64 ? 4 : -1;
             for (int r = 0; r < O; ++r)
                 for (int c = 0; c < O; ++c) {
-                    rec[R::QC + e * O * O + r * O + c] = (double)Qp[r][c];
-                    if (ps >= 0) rec[R::PS + ps * O * O + r * O + c] = (double)Qp[r][c];
+                    rec[R::QC + e * O * O + r * O + c] = Qp[r][c].hi;
+                    if (ps >= 0) rec[R::PS + ps * O * O + r * O + c] = Qp[r][c].hi;
+                    if (e == 64) rec[R::PSL + r * O + c] = Qp[r][c].lo;
                 }
-            for (int r = 0; r < O; ++r)
-                for (int c = 0; c < O; ++c) {
-                    long double acc = 0;
-                    for (int q = 0; q < O; ++q) acc += Qp[r][q] * M[q][c];
-                    T[r][c] = acc;
-                }
+            hz_dd::mat_mul<O>(Qp, M, T);
             std::memcpy(Qp, T, sizeof(Qp));
         }
     }
@@ -685,6 +685,8 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
                 for (int k = 0; k < O; ++k) {
                     double sn = readlane_d(v[k], 63);
 #pragma unroll
+                    for (int c = 0; c < O; ++c) sn = fma(r[R::PSL + k * O + c], S[c], sn);
+#pragma unroll
                     for (int c = 0; c < O; ++c) sn = fma(r[R::PS + 4 * O * O + k * O + c], S[c], sn);
                     Sn[k] = sn;
                 }
@@ -723,6 +725,8 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
             for (int k = 0; k < O; ++k) {
                 double vv = dpp_dm<kDppWaveShr1, 0xf>(zz[k]);  // Z(l-1), 0 at lane 0
                 double sn = readlane_d(zz[k], 63);
+#pragma unroll
+                for (int c = 0; c < O; ++c) sn = fma(r[R::PSL + k * O + c], S[c], sn);
 #pragma unroll
                 for (int c = 0; c < O; ++c) {
                     vv = fma(qc[k * O + c], S[c], vv);
@@ -831,7 +835,8 @@ __global__ __launch_bounds__(64 * lti_waves(O)) void fb_lti_kernel(const double*
 }
 
 // Sequential carry over time segments (one thread per band), LTI records:
-//   start(s+1) = M_tile^seg_tiles start(s) + zsr_end(s), M_tile = M^64 = QC[64].
+//   start(s+1) = M_tile^seg_tiles start(s) + zsr_end(s), M_tile = M^64 = QC[64]; the power in
+//   double-double, applied as hi S + lo S (hz_dd.h).
 template <int O, int L>
 __global__ __launch_bounds__(256) void fb_lti_seg_carry_kernel(const double* __restrict__ rec,
                                                                const double* __restrict__ ystate,
@@ -841,33 +846,16 @@ __global__ __launch_bounds__(256) void fb_lti_seg_carry_kernel(const double* __r
     const int band = blockIdx.x * blockDim.x + threadIdx.x;
     if (band >= nbands) return;
     const double* r = rec + (long)band * R::SIZE;
-    double M[O][O], Pw[O][O], Tm[O][O];
-#pragma unroll
-    for (int i = 0; i < O; ++i)
-#pragma unroll
-        for (int j = 0; j < O; ++j) {
-            Pw[i][j] = r[R::QC + 64 * O * O + i * O + j];
-            M[i][j] = (i == j) ? 1.0 : 0.0;
-        }
-    for (long e = seg_tiles; e > 0; e >>= 1) {
-        if (e & 1) {
-            for (int i = 0; i < O; ++i)
-                for (int j = 0; j < O; ++j) {
-                    double acc = 0;
-                    for (int q = 0; q < O; ++q) acc = fma(M[i][q], Pw[q][j], acc);
-                    Tm[i][j] = acc;
-                }
-            for (int i = 0; i < O; ++i)
-                for (int j = 0; j < O; ++j) M[i][j] = Tm[i][j];
-        }
+    double M[O][O], Ml[O][O];
+    {
+        hz_dd::dd B[O][O], Cp[O][O];
+        hz_dd::load<O>(r + R::QC + 64 * O * O, r + R::PSL, B);
+        hz_dd::mat_pow<O>(B, seg_tiles, Cp);
         for (int i = 0; i < O; ++i)
             for (int j = 0; j < O; ++j) {
-                double acc = 0;
-                for (int q = 0; q < O; ++q) acc = fma(Pw[i][q], Pw[q][j], acc);
-                Tm[i][j] = acc;
+                M[i][j] = Cp[i][j].hi;
+                Ml[i][j] = Cp[i][j].lo;
             }
-        for (int i = 0; i < O; ++i)
-            for (int j = 0; j < O; ++j) Pw[i][j] = Tm[i][j];
     }
     double Sv[O];
 #pragma unroll
@@ -878,6 +866,8 @@ __global__ __launch_bounds__(256) void fb_lti_seg_carry_kernel(const double* __r
 #pragma unroll
         for (int i = 0; i < O; ++i) {
             double acc = slot[i];
+#pragma unroll
+            for (int q = 0; q < O; ++q) acc = fma(Ml[i][q], Sv[q], acc);
 #pragma unroll
             for (int q = 0; q < O; ++q) acc = fma(M[i][q], Sv[q], acc);
             nS[i] = acc;

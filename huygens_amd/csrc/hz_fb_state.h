@@ -35,6 +35,7 @@
 // arrive (device-scope counter, re-armed); inside the inverse kernel, by a small kernel after it.
 #pragma once
 
+#include "hz_dd.h"
 #include "hz_fb_impl.h"
 #include "hz_fb_rec.h"
 
@@ -177,50 +178,35 @@ struct StateLds {
     int is_last;
 };
 
-// (M^64)^e by squaring (O x O, row-major)
+// (M^64)^e by squaring in double-double (O x O, row-major; hz_dd.h): the Horner over the pieces
+// applies it nseg - 1 times
 template <int O>
-__device__ __forceinline__ void m64_pow(const double* M64, int e, double (&P)[O][O]) {
-    double Pw[O][O], Tm[O][O];
+__device__ __forceinline__ void m64_pow(const double* M64, const double* M64l, int e, double (&P)[O][O],
+                                        double (&Pl)[O][O]) {
+    hz_dd::dd B[O][O], Cp[O][O];
+    hz_dd::load<O>(M64, M64l, B);
+    hz_dd::mat_pow<O>(B, e, Cp);
     for (int i = 0; i < O; ++i)
         for (int j = 0; j < O; ++j) {
-            Pw[i][j] = M64[i * O + j];
-            P[i][j] = i == j ? 1.0 : 0.0;
+            P[i][j] = Cp[i][j].hi;
+            Pl[i][j] = Cp[i][j].lo;
         }
-    for (int ex = e; ex > 0; ex >>= 1) {
-        if (ex & 1) {
-            for (int i = 0; i < O; ++i)
-                for (int j = 0; j < O; ++j) {
-                    double s = 0.0;
-                    for (int q = 0; q < O; ++q) s = fma(P[i][q], Pw[q][j], s);
-                    Tm[i][j] = s;
-                }
-            for (int i = 0; i < O; ++i)
-                for (int j = 0; j < O; ++j) P[i][j] = Tm[i][j];
-        }
-        for (int i = 0; i < O; ++i)
-            for (int j = 0; j < O; ++j) {
-                double s = 0.0;
-                for (int q = 0; q < O; ++q) s = fma(Pw[i][q], Pw[q][j], s);
-                Tm[i][j] = s;
-            }
-        for (int i = 0; i < O; ++i)
-            for (int j = 0; j < O; ++j) Pw[i][j] = Tm[i][j];
-    }
 }
 
 // band b's state from its piece partials p0[s kCols + i]: Horner over the pieces of `tiles` tiles
 template <int O>
 __device__ __forceinline__ void combine_pieces(const StateArgs& a, int b, const double* p0, int tiles) {
     using R = hz_fbi::RecL<O, kL>;
-    const double* M64 = a.rec + (long)b * a.rs + R::QC + 64 * O * O;
-    double S[O], P[O][O];
-    m64_pow<O>(M64, tiles, P);
+    const double* rb = a.rec + (long)b * a.rs;
+    double S[O], P[O][O], Pl[O][O];
+    m64_pow<O>(rb + R::QC + 64 * O * O, rb + R::PSL, tiles, P, Pl);
     for (int i = 0; i < O; ++i) S[i] = p0[i];
     for (int s = 1; s < a.nseg; ++s) {
         const double* ps = p0 + (long)s * kCols;
         double nS[O];
         for (int i = 0; i < O; ++i) {
             double acc2 = ps[i];
+            for (int q = 0; q < O; ++q) acc2 = fma(Pl[i][q], S[q], acc2);
             for (int q = 0; q < O; ++q) acc2 = fma(P[i][q], S[q], acc2);
             nS[i] = acc2;
         }

@@ -29,6 +29,7 @@
 #include <new>
 #include <vector>
 
+#include "hz_dd.h"
 #include "hz_fb_impl.h"
 
 namespace {
@@ -46,7 +47,8 @@ struct Rec {
     static constexpr int H = 2 * O + 1;          // h[k][j] k<O j<16  homogeneous responses
     static constexpr int P = H + kL * O;         // P[s][r][c] s<6    (M16)^(2^s)
     static constexpr int Q = P + 6 * O * O;      // Q[p][r][c] p<16   (M16)^p
-    static constexpr int RAW = Q + kL * O * O;
+    static constexpr int PL = Q + kL * O * O;    // PL[s-4][r][c]     low words of P[4], P[5] (hz_dd.h)
+    static constexpr int RAW = PL + 2 * O * O;
     static constexpr int SIZE = (RAW + 7) & ~7;  // 64-B aligned records
 };
 
@@ -291,6 +293,8 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
                     for (int i = 0; i < O; ++i) {
                         double acc = readlane_d(z[i], 16 * rw + 15);
 #pragma unroll
+                        for (int q = 0; q < O; ++q) acc = fma(r[R::PL + i * O + q], C[rw][q], acc);
+#pragma unroll
                         for (int q = 0; q < O; ++q) acc = fma(r[R::P + 4 * O * O + i * O + q], C[rw][q], acc);
                         C[rw + 1][i] = acc;
                     }
@@ -449,47 +453,29 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
 
 // Sequential carry over time segments, one thread per band:
 //   start(s+1) = C^seg_len start(s) + zsr_end(s),  start(0) = ystate.
-// C^seg_len = (M16^64)^(seg_len/1024) by binary powering of the record's P[5]^2.
+// C^seg_len = (M16^64)^(seg_len/1024) by binary powering of the record's P[5]^2, in double-double
+// and applied as hi S + lo S (hz_dd.h: the same rounded power is applied nseg - 1 times).
 template <int O>
 __global__ __launch_bounds__(256) void fb_seg_carry_kernel(const double* __restrict__ rec,
                                                            const double* __restrict__ ystate,
                                                            double* __restrict__ segstate, int nbands,
                                                            int nseg, long seg_tiles) {
     using R = Rec<O>;
+    using hz_dd::dd;
     const int band = blockIdx.x * blockDim.x + threadIdx.x;
     if (band >= nbands) return;
     const double* r = rec + (long)band * R::SIZE;
-    double M[O][O], Pw[O][O], T[O][O];
-    // M1024 = P[5] * P[5]
-#pragma unroll
-    for (int i = 0; i < O; ++i)
-#pragma unroll
-        for (int j = 0; j < O; ++j) {
-            double acc = 0;
-#pragma unroll
-            for (int q = 0; q < O; ++q) acc = fma(r[R::P + 5 * O * O + i * O + q], r[R::P + 5 * O * O + q * O + j], acc);
-            Pw[i][j] = acc;
-            M[i][j] = (i == j) ? 1.0 : 0.0;
-        }
-    for (long e = seg_tiles; e > 0; e >>= 1) {
-        if (e & 1) {
-            for (int i = 0; i < O; ++i)
-                for (int j = 0; j < O; ++j) {
-                    double acc = 0;
-                    for (int q = 0; q < O; ++q) acc = fma(M[i][q], Pw[q][j], acc);
-                    T[i][j] = acc;
-                }
-            for (int i = 0; i < O; ++i)
-                for (int j = 0; j < O; ++j) M[i][j] = T[i][j];
-        }
+    double M[O][O], Ml[O][O];
+    {
+        dd P5[O][O], M1024[O][O], Cp[O][O];
+        hz_dd::load<O>(r + R::P + 5 * O * O, r + R::PL + O * O, P5);
+        hz_dd::mat_mul<O>(P5, P5, M1024);
+        hz_dd::mat_pow<O>(M1024, seg_tiles, Cp);
         for (int i = 0; i < O; ++i)
             for (int j = 0; j < O; ++j) {
-                double acc = 0;
-                for (int q = 0; q < O; ++q) acc = fma(Pw[i][q], Pw[q][j], acc);
-                T[i][j] = acc;
+                M[i][j] = Cp[i][j].hi;
+                Ml[i][j] = Cp[i][j].lo;
             }
-        for (int i = 0; i < O; ++i)
-            for (int j = 0; j < O; ++j) Pw[i][j] = T[i][j];
     }
     double S[O];
 #pragma unroll
@@ -500,6 +486,8 @@ __global__ __launch_bounds__(256) void fb_seg_carry_kernel(const double* __restr
 #pragma unroll
         for (int i = 0; i < O; ++i) {
             double acc = slot[i];
+#pragma unroll
+            for (int q = 0; q < O; ++q) acc = fma(Ml[i][q], S[q], acc);
 #pragma unroll
             for (int q = 0; q < O; ++q) acc = fma(M[i][q], S[q], acc);
             nS[i] = acc;
@@ -527,54 +515,49 @@ __global__ __launch_bounds__(256) void fb_reduce_kernel(const double* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// host-side precompute of a band record (long double)
+// host-side precompute of a band record, in double-double (hz_dd.h): the homogeneous responses
+// h[k][j], M16, its powers; P[4] and P[5] keep their low words (the carries apply them many times)
 // ---------------------------------------------------------------------------
 template <int O>
 void build_record(const double* b, const double* av, double* rec) {
     using R = Rec<O>;
+    using hz_dd::dd;
     std::memset(rec, 0, sizeof(double) * R::SIZE);
     for (int i = 0; i <= O; ++i) rec[R::B + i] = b[i];
     if constexpr (O > 0) {
         for (int k = 0; k < O; ++k) rec[R::A + k] = av[k];
-        long double h[O][kL];
+        dd h[O][kL];
         for (int k = 0; k < O; ++k) {
-            long double yh[O];
-            for (int q = 0; q < O; ++q) yh[q] = (q == k) ? 1.0L : 0.0L;
+            dd yh[O];
+            for (int q = 0; q < O; ++q) yh[q] = {q == k ? 1.0 : 0.0, 0.0};
             for (int j = 0; j < kL; ++j) {
-                long double y = 0;
-                for (int q = 0; q < O; ++q) y -= (long double)av[q] * yh[q];
+                dd y{0.0, 0.0};
+                for (int q = 0; q < O; ++q) y = hz_dd::add(y, hz_dd::mul(yh[q], -av[q]));
                 for (int q = O - 1; q > 0; --q) yh[q] = yh[q - 1];
                 yh[0] = y;
                 h[k][j] = y;
-                rec[R::H + k * kL + j] = (double)y;
+                rec[R::H + k * kL + j] = y.hi;
             }
         }
-        long double M[O][O], T[O][O], Qp[O][O];
+        dd M[O][O], T[O][O], Qp[O][O];
         for (int rr = 0; rr < O; ++rr)
             for (int c = 0; c < O; ++c) {
                 M[rr][c] = h[c][kL - 1 - rr];
-                Qp[rr][c] = (rr == c) ? 1.0L : 0.0L;
+                Qp[rr][c] = {rr == c ? 1.0 : 0.0, 0.0};
             }
         for (int p = 0; p < kL; ++p) {
             for (int rr = 0; rr < O; ++rr)
-                for (int c = 0; c < O; ++c) rec[R::Q + p * O * O + rr * O + c] = (double)Qp[rr][c];
-            for (int rr = 0; rr < O; ++rr)
-                for (int c = 0; c < O; ++c) {
-                    long double acc = 0;
-                    for (int q = 0; q < O; ++q) acc += Qp[rr][q] * M[q][c];
-                    T[rr][c] = acc;
-                }
+                for (int c = 0; c < O; ++c) rec[R::Q + p * O * O + rr * O + c] = Qp[rr][c].hi;
+            hz_dd::mat_mul<O>(Qp, M, T);
             std::memcpy(Qp, T, sizeof(Qp));
         }
         for (int s = 0; s < 6; ++s) {
             for (int rr = 0; rr < O; ++rr)
-                for (int c = 0; c < O; ++c) rec[R::P + s * O * O + rr * O + c] = (double)M[rr][c];
-            for (int rr = 0; rr < O; ++rr)
                 for (int c = 0; c < O; ++c) {
-                    long double acc = 0;
-                    for (int q = 0; q < O; ++q) acc += M[rr][q] * M[q][c];
-                    T[rr][c] = acc;
+                    rec[R::P + s * O * O + rr * O + c] = M[rr][c].hi;
+                    if (s >= 4) rec[R::PL + (s - 4) * O * O + rr * O + c] = M[rr][c].lo;
                 }
+            hz_dd::mat_mul<O>(M, M, T);
             std::memcpy(M, T, sizeof(M));
         }
     }
