@@ -50,11 +50,12 @@ constexpr int kThreads = 256;       // 4 waves
 // i < XW (the end-state map's first row: its row k is E_0 shifted by k taps past the O history
 // taps), zeros up to kEh, then the history taps pin E_H[k O + i] -- followed by the M^e weights of
 // every column: W[sb][col][p][j] = row k of M^e(p) at column k ^ j (j < 4), e(p) = 64 (the tile
-// carry), 4, 0..3, 16, 32, 48 (the end's Horner steps).  A lane gathers its 66 B operands from
+// carry), 4, 0..3, 16, 32, 48 (the end's Horner steps), then the low word of M^64 (p = 9: the
+// tile carry applies hi + lo, hz_dd.h).  A lane gathers its 66 B operands from
 // its band's row (the two state columns of a band share it: 31 KB per group at O = 2 instead of
 // the 48 KB of operands laid out per lane)
 constexpr int kEh = 136, kEs = 152;
-constexpr int kPows = 9;
+constexpr int kPows = 10;
 constexpr int kW = 2 * 16 * kPows * 4;
 template <int O>
 constexpr int grp_e() { return (kCols / (O == 3 ? 4 : O)) * kEs; }
@@ -105,6 +106,24 @@ __device__ __forceinline__ double mix_cols(const double* w, double v) {
     return r;
 }
 
+// the same with a double-double row (w + wl): the tile carry, applied once per tile
+template <int OP>
+__device__ __forceinline__ double mix_cols2(const double* w, const double* wl, double v) {
+    double x[OP];
+    x[0] = v;
+    if constexpr (OP >= 2) x[1] = quad_xor<1>(v);
+    if constexpr (OP >= 4) {
+        x[2] = quad_xor<2>(v);
+        x[3] = quad_xor<3>(v);
+    }
+    double r = wl[0] * x[0];
+#pragma unroll
+    for (int j = 1; j < OP; ++j) r = fma(wl[j], x[j], r);
+#pragma unroll
+    for (int j = 0; j < OP; ++j) r = fma(w[j], x[j], r);
+    return r;
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t state_rsrc(const double* p, long count) {
     const unsigned long long b = (unsigned long long)p;
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
@@ -129,13 +148,13 @@ __device__ __forceinline__ void load_a(__amdgpu_buffer_rsrc_t xr, int v, int g, 
 // reloaded with the next tile's taps (byte offset vn) as soon as its two k-steps are issued
 template <int OP>
 __device__ __forceinline__ void state_tile(double (&a)[kKE], const double (&b)[2][kKE], const double (&m64)[2][OP],
-                                           bool carry, __amdgpu_buffer_rsrc_t xr, int vn, int g, f64x4& acc0,
+                                           const double (&m64l)[2][OP], bool carry, __amdgpu_buffer_rsrc_t xr, int vn, int g, f64x4& acc0,
                                            f64x4& acc1) {
     if (carry) {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-            acc0[rr] = mix_cols<OP>(m64[0], acc0[rr]);
-            acc1[rr] = mix_cols<OP>(m64[1], acc1[rr]);
+            acc0[rr] = mix_cols2<OP>(m64[0], m64l[0], acc0[rr]);
+            acc1[rr] = mix_cols2<OP>(m64[1], m64l[1], acc1[rr]);
         }
     }
 #pragma unroll
@@ -252,9 +271,11 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
     // registers in the order the first tile's k-steps use them: its MFMAs start as their operands
     // arrive (a staged LDS copy waited for the whole block behind a barrier: 3.4 us before the
     // first MFMA)
-    double m64[2][OP];
+    double m64[2][OP], m64l[2][OP];
     wrow(0, 0, m64[0]);
     wrow(1, 0, m64[1]);
+    wrow(0, 9, m64l[0]);
+    wrow(1, 9, m64l[1]);
     // B operand (sb, q) of this lane: pin E[k][tap], tap = tap_slot(q, lg) - S, from its band's row
     // (tap >= O: E_0[tap + k]; tap < O: E_H[k O + tap]; columns k >= O and taps < 0: 0)
     const int k = col % OP;
@@ -298,13 +319,14 @@ __device__ __forceinline__ void state_group(const StateArgs& a, int g, int seg, 
     // waits track only the x loads (the compiler otherwise waited for every load in flight before
     // each carry)
 #pragma unroll
-    for (int j = 0; j < OP; ++j) asm volatile("" : "+v"(m64[0][j]), "+v"(m64[1][j]));
+    for (int j = 0; j < OP; ++j)
+        asm volatile("" : "+v"(m64[0][j]), "+v"(m64[1][j]), "+v"(m64l[0][j]), "+v"(m64l[1][j]));
     f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     // tile it from xa, reloaded with tile it + 1 as it goes (past the last tile: unused loads)
 #ifdef HZ_DIAG_STAMPS
     if (stp && threadIdx.x == 0) stp[1] = __builtin_amdgcn_s_memrealtime();
 #endif
-    for (int it = 0; it < ntl; ++it) state_tile<OP>(xa, bq, m64, it > 0, xr, voff(it + 1), lg, acc0, acc1);
+    for (int it = 0; it < ntl; ++it) state_tile<OP>(xa, bq, m64, m64l, it > 0, xr, voff(it + 1), lg, acc0, acc1);
 #ifdef HZ_DIAG_STAMPS
     if (stp && threadIdx.x == 0) stp[2] = __builtin_amdgcn_s_memrealtime();
 #endif

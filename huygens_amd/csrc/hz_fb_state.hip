@@ -64,7 +64,8 @@ __global__ __launch_bounds__(256) void fb_state_ops_kernel(const double* __restr
         const int sb = sc / 16, col = sc % 16, k = col % OP;
         const int band = g * Gm::BANDS + (16 * sb + col) / OP;
         if (sb < 2 && j < OP && band < nbands && k < O && (k ^ j) < O)
-            v = rec[(long)band * rs + R::QC + pow_of(p) * O * O + k * O + (k ^ j)];
+            v = p == 9 ? rec[(long)band * rs + R::PSL + k * O + (k ^ j)]
+                       : rec[(long)band * rs + R::QC + pow_of(p) * O * O + k * O + (k ^ j)];
     }
     eop[i] = v;
 }

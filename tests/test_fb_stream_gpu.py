@@ -261,6 +261,7 @@ def test_stream_high_q_tail(gpu_lib):
     from huygens_amd._lib import HZ_FB_PATH_RESPONSE, HZ_FB_PATH_STREAM
     N = 64
     g, o = _bank(N, R=0.9999, k_p=0.01, k_g=0.01)
+    g.tune_response(bands_per_sample=1)   # a 64-band bank: let the cost model pick the engines
     rng = np.random.default_rng(31)
 
     def run(n, tol=1e-6):
