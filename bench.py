@@ -886,6 +886,55 @@ def main():
                                  "(bench.stream_block_flops) over the same time"},
         }
 
+    # the high-Q variant of C2 (tests/eigen.cpp:26's r = 0.9999): the same
+    # recipe at R = 0.9999, whose horizon (~0.4 M samples) is past the streaming head's 2^17 -- the
+    # 1024-sample calls add the response tail from per-epoch convolutions on a side stream
+    # (hz_fb_stream.hip); parity: tests/test_fullsize_gpu.py::test_c2_high_q_*,
+    # tests/test_fb_stream_gpu.py::test_stream_high_q_tail
+    if world == 1 and args.side_steps > 0 and args.stream_blocks > 0 and not args.general and args.response != 0:
+        fq, bq = c2_coefficients(R=0.9999)
+        hq = Filterbank(2, N_BANDS, 0.1, 1.0, device=local)
+        for n in range(N_BANDS):
+            hq.coefficients(n, fq[n], bq[n])
+        hq.boost(np.ones(N_BANDS))
+        hq.open()
+        hq.set_stream(stream.cuda_stream)
+        yq = ys[1]
+
+        def hq_long():
+            hq.process_device(x.data_ptr(), yq.data_ptr(), S)
+
+        for _ in range(6):   # priming: smoothers, then K samples of converged history
+            hq_long()
+            if hq.last_path() == HZ_FB_PATH_RESPONSE:
+                break
+        long_t = timed(hq_long, 3, min(args.side_steps, 20), S)
+        long_t["path"] = {1: "general", 2: "lti", 3: "response"}.get(hq.last_path(), "?")
+        B = 1024
+        nbq = min(args.stream_blocks, S // B)
+
+        def hq_blocks(n_blocks):
+            for i in range(n_blocks):
+                hq.process_device(x.data_ptr() + 8 * B * i, yq.data_ptr() + 8 * B * i, B)
+
+        hq_blocks(min(32, nbq))   # untimed: ring, head and tail spectra, first epochs
+        barrier()
+        ts = time.perf_counter()
+        hq_blocks(nbq)
+        barrier()
+        tq = time.perf_counter() - ts
+        side["high_q"] = {
+            "R": 0.9999, "horizon": hq.response_info()[0],
+            "long_calls": long_t,
+            "streaming": {"us_per_block": 1e6 * tq / nbq, "band_samples_per_s": N_BANDS * B * nbq / tq,
+                          "blocks": nbq, "path": {3: "response", 4: "stream"}.get(hq.last_path(), str(hq.last_path())),
+                          "note": "one process() call per 1024-sample block; past the head's 2^17 samples the "
+                                  "response tail is convolved per 16384-sample epoch ahead of time on a side "
+                                  "stream and added by the block kernel (still one launch per block on the "
+                                  "handle's stream)"},
+        }
+        hq.close()
+
     total_band_samples = N_BANDS * S * args.steps
     value = total_band_samples / elapsed
     if rank == 0:
