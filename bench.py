@@ -563,6 +563,8 @@ def main():
                     help="stationary engine: 0 off (per-band engines only), 1 eager (default), 2 lazy")
     ap.add_argument("--resp-engine", type=int, default=-1,
                     help="(A/B) stationary long calls: 1 column-split, 0 three-kernel path (default)")
+    ap.add_argument("--modal", type=int, default=-1,
+                    help="(A/B) stationary band states: 1 modal (default where the bank qualifies), 0 matrix-core pass")
     ap.add_argument("--gather", action="store_true",
                     help="N > 1, time-sharded stationary calls: gather the shares on rank 0 inside each step")
     ap.add_argument("--side-steps", type=int, default=50,
@@ -625,6 +627,8 @@ def main():
         fb.set_response(args.response)
     if args.resp_engine >= 0:
         fb.tune_response_engine(bool(args.resp_engine))
+    if args.modal >= 0:
+        fb.tune_modal(bool(args.modal))
     stream = torch.cuda.current_stream(dev)
     fb.set_stream(stream.cuda_stream)
 

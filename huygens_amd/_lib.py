@@ -104,6 +104,8 @@ _SIGS = {
     "hz_fb_tune_response_engine": (I, [VP, I]),
     "hz_fb_sample_many": (I, [C.POINTER(VP), I, PD, I, D, PD]),
     "hz_fb_response_engine": (I, [VP, C.POINTER(I), C.POINTER(I)]),
+    "hz_fb_tune_modal": (I, [VP, I]),
+    "hz_fb_modal_info": (I, [VP, C.POINTER(I), C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
     "hz_fb_response_info": (I, [VP, C.POINTER(L), C.POINTER(L), C.POINTER(I), C.POINTER(L)]),
     "hz_fb_get_response": (I, [VP, PD, L]),
     "hz_fb_set_bank_response": (I, [VP, PD, L]),

@@ -207,6 +207,22 @@ struct hz_fb {
         size_t scount_cap = 0;
         double* d_zero = nullptr;        // N O zeros (x history / start of the zero-start pass)
         size_t zero_cap = 0;
+        // modal band states (hz_fb_modal.h): banks whose poles sit on one circle on the 2 pi / 8192
+        // grid get their states from a fold and one DFT instead of the MFMA pass
+        bool modal_on = true;            // hz_fb_tune_modal
+        bool modal_ok = false;           // the current bank qualifies (built with d_h)
+        bool modal_last = false;         // the last stationary call used it
+        double* d_mpar = nullptr;        // BandPar [N]
+        size_t mpar_cap = 0;
+        double* d_mtab = nullptr;        // R_g^r [8192], R_g^(8192 s) [S], e^(2 pi i q / 8192) [8192]
+        size_t mtab_cap = 0;
+        double* d_mA = nullptr;          // [2][64][128] complex (phase 1 -> phase 2)
+        size_t mA_cap = 0;
+        double* d_mexc = nullptr;        // exceptional responses [nexc][K + 1], then their partials
+        size_t mexc_cap = 0;
+        int* d_mint = nullptr;           // csr_ptr [65], csr (band, k2) [N], exceptional bands [8]
+        size_t mint_cap = 0;
+        int mexc_n = 0, mexc_chunks = 0, mS = 0;
         long h_gen = 0;                  // d_h rebuilds (the streaming spectra follow it)
         // streaming calls (hz_fb_stream.hip): 1024-sample blocks of a stationary bank, one launch
         // each, through a frequency-domain delay line; the history in a mirrored ring

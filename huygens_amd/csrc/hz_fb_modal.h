@@ -1,0 +1,199 @@
+// hz_fb_modal.h -- modal band states for the stationary engine (hz_fb_resp.hip): the band states
+// after a stationary call, for banks whose poles sit on one circle at angles on the 2 pi / 8192
+// grid (the reference's own resonator recipe: f_i = 0.5 (i + 1) SR / N, R shared,
+// tests/resynthesis.cpp:48-54), from one fold of the call's last K inputs and one 8192-point DFT
+// instead of the N O K multiply-adds of the MFMA pass (hz_fb_state.h).
+//
+// A second-order band y = pin (b0 x[t] + b1 x[t-1] + b2 x[t-2]) / (1 + a1 z^-1 + a2 z^-2)
+// (src/filterbank.h:178-179 at pre = pin) with poles p, conj p has g[tau] = (p^(tau+1) -
+// conj p^(tau+1)) / (p - conj p), so over the window of the last K inputs (the MFMA pass's zero-start
+// semantics)
+//     y[t] = Im(p U(t)) / Im p,   U(t) = pin (b0 Z(t) + b1 Z(t-1) + b2 Z(t-2)),
+//     Z(t) = sum_{tau < K} p^tau x[t - tau],   Z(t-1) = (Z(t) - x[t]) / p.
+// With p = p_g e^c, p_g = R_g e^(2 pi i m / L) on the grid (c: the coefficients' own rounding off
+// it, |c| K <= 1e-6, checked on the host in long double):
+//     Z(T-1) = G0[m] + c G1[m]  (+ O((c K)^2) <= 5e-13),
+//     G_j[m] = sum_{r < L} e^(2 pi i m r / L) F_j[r],  F_j[r] = sum_{tau = r mod L} tau^j R_g^tau x[T-1-tau].
+// The DFT is four-step, L = 8192 = 64 x 128 (r = r1 + 128 r2, m = k1 + 64 k2, W = e^(2 pi i / L)):
+//   phase 1 (workgroup r1, extra workgroups of the forward kernel):
+//     A_j[k1][r1] = W^(r1 k1) sum_{r2 < 64} F_j[r1 + 128 r2] W64^(r2 k1)  -- the fold included;
+//   phase 2 (workgroup k1, extra workgroups of the inverse kernel, two launches later):
+//     G_j[k1 + 64 k2] = sum_{r1 < 128} W128^(r1 k2) A_j[k1][r1], then the states of the bands whose
+//     m = k1 (mod 64).
+// Bands whose poles (nearly) coincide -- the recipe's Nyquist band is a double pole at -R -- are
+// exceptional: a direct dot product of the window with their own response (host, long double),
+// accumulated in double-double per 16384-sample chunk (phase 1) and summed in phase 2.
+// numpy model and CPU checks: tests/modal_model.py, tests/test_modal_model_cpu.py.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "hz_dd.h"
+
+namespace hz_modal {
+
+constexpr int kL = 8192;           // grid / DFT length
+constexpr int kR1 = 128, kR2 = 64; // r = r1 + 128 r2; k = k1 + 64 k2
+constexpr int kMaxExc = 8;         // exceptional bands handled by direct dot products
+constexpr long kExcChunk = 16384;  // samples per exceptional partial
+constexpr int kThreads = 256;
+constexpr int kPhase1 = kR1;       // phase-1 workgroups (one per r1)
+constexpr int kPhase2 = kR2;       // phase-2 workgroups (one per k1), + 1 for the exceptional sums
+
+struct BandPar {                   // regular band n
+    double pr, pi;                 // pole p = (-a1 / 2, sqrt(a2 - a1^2 / 4))
+    double cr, ci;                 // c = log(p / p_g)
+    double inv_im;                 // 1 / Im p
+    double b0, b1, b2;             // pin * fwd
+};
+
+struct ModalArgs {
+    int on;                        // 0: no modal work in this launch
+    const double* xw;              // the window: xw[i] = x[T - K + i], i < K
+    long K;
+    int S;                         // K / kL
+    const double* wR;              // [kL] R_g^r
+    const double* RL;              // [S] R_g^(kL s)
+    const double2* tw;             // [kL] e^(2 pi i q / kL)
+    double2* A;                    // [2][64][128]
+    const BandPar* par;            // [N]
+    const int* csr_ptr;            // [65] bands of residue k1 = m mod 64: csr[csr_ptr[k1] .. csr_ptr[k1 + 1])
+    const int2* csr;               // (band, k2)
+    int nexc;
+    const int* exc_band;           // [nexc]
+    const double* exc_r;           // [nexc][K + 1] responses (pin included)
+    double* exc_part;              // [nexc][chunks][4] (hi, lo) of both components
+    int exc_chunks;
+    double* out;                   // [N][2]: y[T-1], y[T-2]
+};
+
+struct Lds1 {
+    double red[4][64][2];
+    double F[2][64];
+};
+struct Lds2 {
+    double2 a[2][kR1];
+    double2 g[2][kR1];
+    hz_dd::dd part[kThreads][2];
+};
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// phase 1, workgroup r1 < 128: the fold of residues r1 + 128 r2 (r2 < 64) and their 64-point DFTs
+__device__ __forceinline__ void phase1(const ModalArgs& a, int r1, Lds1& L) {
+    const int t = threadIdx.x, r2 = t & 63, g = t >> 6;
+    const int r = r1 + kR1 * r2;
+    const double w0 = a.wR[r];
+    double f0 = 0.0, f1 = 0.0;
+    for (int s = g; s < a.S; s += 4) {
+        const long tau = r + (long)kL * s;
+        const double v = w0 * a.RL[s] * a.xw[a.K - 1 - tau];
+        f0 += v;
+        f1 = fma((double)tau, v, f1);
+    }
+    L.red[g][r2][0] = f0;
+    L.red[g][r2][1] = f1;
+    __syncthreads();
+    if (t < 128) {
+        const int j = t >> 6, q = t & 63;
+        L.F[j][q] = ((L.red[0][q][j] + L.red[1][q][j]) + L.red[2][q][j]) + L.red[3][q][j];
+    }
+    __syncthreads();
+    if (t < 128) {
+        const int j = t >> 6, k1 = t & 63;
+        double re = 0.0, im = 0.0;
+#pragma unroll 8
+        for (int q = 0; q < kR2; ++q) {
+            const double2 w = a.tw[kR1 * ((q * k1) & 63)];   // W64^(q k1)
+            const double f = L.F[j][q];
+            re = fma(f, w.x, re);
+            im = fma(f, w.y, im);
+        }
+        const double2 v = cmul(make_double2(re, im), a.tw[(r1 * k1) & (kL - 1)]);
+        a.A[((long)j * kR2 + k1) * kR1 + r1] = v;
+    }
+}
+
+// phase 1, exceptional band e, chunk q: both components' partial dot products in double-double
+__device__ __forceinline__ void exc_partial(const ModalArgs& a, int e, int q, Lds2& L) {
+    using hz_dd::dd;
+    const int t = threadIdx.x;
+    const double* r = a.exc_r + (long)e * (a.K + 1);
+    const long t0 = (long)q * kExcChunk, t1 = min(t0 + kExcChunk, a.K);
+    dd s0{0.0, 0.0}, s1{0.0, 0.0};
+    for (long tau = t0 + t; tau < t1; tau += kThreads) {
+        const double rv = r[tau];
+        s0 = hz_dd::add(s0, hz_dd::two_prod(rv, a.xw[a.K - 1 - tau]));
+        if (tau < a.K - 1) s1 = hz_dd::add(s1, hz_dd::two_prod(rv, a.xw[a.K - 2 - tau]));
+    }
+    L.part[t][0] = s0;
+    L.part[t][1] = s1;
+    __syncthreads();
+    if (t < 2) {
+        dd acc{0.0, 0.0};
+        for (int i = 0; i < kThreads; ++i) acc = hz_dd::add(acc, L.part[i][t]);
+        double* o = a.exc_part + ((long)e * a.exc_chunks + q) * 4 + 2 * t;
+        o[0] = acc.hi;
+        o[1] = acc.lo;
+    }
+}
+
+// phase 2, workgroup k1 < 64: G_j[k1 + 64 k2] and the states of the bands of residue k1
+__device__ __forceinline__ void phase2(const ModalArgs& a, int k1, Lds2& L) {
+    const int t = threadIdx.x;
+    {
+        const int j = t >> 7, r1 = t & 127;
+        L.a[j][r1] = a.A[((long)j * kR2 + k1) * kR1 + r1];
+    }
+    __syncthreads();
+    {
+        const int j = t >> 7, k2 = t & 127;
+        double re = 0.0, im = 0.0;
+#pragma unroll 8
+        for (int r1 = 0; r1 < kR1; ++r1) {
+            const double2 w = a.tw[kR2 * ((r1 * k2) & 127)];   // W128^(r1 k2)
+            const double2 v = L.a[j][r1];
+            re = fma(v.x, w.x, re);
+            re = fma(-v.y, w.y, re);
+            im = fma(v.x, w.y, im);
+            im = fma(v.y, w.x, im);
+        }
+        L.g[j][k2] = make_double2(re, im);
+    }
+    __syncthreads();
+    const double x1 = a.xw[a.K - 1], x2 = a.xw[a.K - 2], x3 = a.xw[a.K - 3];
+    for (int i = a.csr_ptr[k1] + t; i < a.csr_ptr[k1 + 1]; i += kThreads) {
+        const int2 bk = a.csr[i];
+        const BandPar P = a.par[bk.x];
+        const double2 g0 = L.g[0][bk.y], g1 = L.g[1][bk.y];
+        // Z1 = G0 + c G1; Z(t-1) = (Z(t) - x[t]) / p = (Z(t) - x[t]) conj(p) / |p|^2
+        double2 z1 = make_double2(g0.x + (P.cr * g1.x - P.ci * g1.y), g0.y + (P.cr * g1.y + P.ci * g1.x));
+        const double in2 = 1.0 / (P.pr * P.pr + P.pi * P.pi);
+        const double2 pc = make_double2(P.pr * in2, -P.pi * in2);
+        const double2 z2 = cmul(make_double2(z1.x - x1, z1.y), pc);
+        const double2 z3 = cmul(make_double2(z2.x - x2, z2.y), pc);
+        const double2 z4 = cmul(make_double2(z3.x - x3, z3.y), pc);
+        const double2 u1 = make_double2(P.b0 * z1.x + P.b1 * z2.x + P.b2 * z3.x, P.b0 * z1.y + P.b1 * z2.y + P.b2 * z3.y);
+        const double2 u2 = make_double2(P.b0 * z2.x + P.b1 * z3.x + P.b2 * z4.x, P.b0 * z2.y + P.b1 * z3.y + P.b2 * z4.y);
+        // Im(p u) / Im p
+        a.out[2L * bk.x] = (P.pr * u1.y + P.pi * u1.x) * P.inv_im;
+        a.out[2L * bk.x + 1] = (P.pr * u2.y + P.pi * u2.x) * P.inv_im;
+    }
+}
+
+// phase 2, the extra workgroup: the exceptional bands' partials summed in chunk order
+__device__ __forceinline__ void exc_sum(const ModalArgs& a) {
+    const int t = threadIdx.x;
+    if (t >= 2 * a.nexc) return;
+    const int e = t >> 1, c = t & 1;
+    hz_dd::dd acc{0.0, 0.0};
+    for (int q = 0; q < a.exc_chunks; ++q) {
+        const double* p = a.exc_part + ((long)e * a.exc_chunks + q) * 4 + 2 * c;
+        acc = hz_dd::add(acc, hz_dd::dd{p[0], p[1]});
+    }
+    a.out[2L * a.exc_band[e] + c] = acc.hi + acc.lo;
+}
+
+}  // namespace hz_modal

@@ -36,6 +36,7 @@
 #include "hz_fb_state.h"
 #include "hz_fft2k.h"
 #include "hz_fb_col.h"
+#include "hz_fb_modal.h"
 
 namespace {
 
@@ -231,12 +232,26 @@ __device__ __forceinline__ double resp_u(const RespArgs& a, long m) {
 union RespLds {
     hz2k::Lds fft;
     hz_state::StateLds st;
+    hz_modal::Lds2 md;
+};
+union RespFwdLds {
+    hz2k::Lds fft;
+    hz_modal::Lds1 m1;
+    hz_modal::Lds2 m2;
 };
 
 
 // Z_j = the spectrum of W_j = u[jP, jP + F)
-__global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a) {
-    __shared__ hz2k::Lds s;
+// (modal band states, hz_fb_modal.h: phase 1 and the exceptional partials as workgroups past nz)
+__global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a, hz_modal::ModalArgs md) {
+    __shared__ RespFwdLds u;
+    if (md.on && (int)blockIdx.x >= a.nz) {
+        const int i = blockIdx.x - a.nz;
+        if (i < hz_modal::kPhase1) hz_modal::phase1(md, i, u.m1);
+        else hz_modal::exc_partial(md, (i - hz_modal::kPhase1) / md.exc_chunks, (i - hz_modal::kPhase1) % md.exc_chunks, u.m2);
+        return;
+    }
+    hz2k::Lds& s = u.fft;
     const long m0 = (long)blockIdx.x * kP;
     real_window_fwd(
         s, [&](int m) { return resp_u(a, m0 + m); }, a.tw, a.Z + (long)blockIdx.x * kH, a.Zn + blockIdx.x, true);
@@ -334,7 +349,7 @@ MacKernel pick_mac(int Qp) {
     default: return resp_mac_kernel<kMacR, 0>;
     }
 }
-typedef void (*RespKernel)(RespArgs, hz_state::StateArgs);
+typedef void (*RespKernel)(RespArgs, hz_state::StateArgs, hz_modal::ModalArgs);
 
 // history after the call, smoothers' closed form, x history; a time-range shard's zeros outside
 // its range (threads of the B output-block workgroups)
@@ -361,8 +376,16 @@ __device__ __forceinline__ void resp_upkeep(const RespArgs& a, long b) {
 // convolution) straight from the last pass's registers
 template <int SO>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void resp_inv_kernel(
-    RespArgs a, hz_state::StateArgs st) {
+    RespArgs a, hz_state::StateArgs st, hz_modal::ModalArgs md) {
     __shared__ RespLds u;
+    if constexpr (SO == 0) {   // modal band states, phase 2 (hz_fb_modal.h)
+        if (md.on && (int)blockIdx.x >= a.B) {
+            const int i = blockIdx.x - a.B;
+            if (i < hz_modal::kPhase2) hz_modal::phase2(md, i, u.md);
+            else hz_modal::exc_sum(md);
+            return;
+        }
+    }
     if constexpr (SO > 0) {
         if ((int)blockIdx.x >= a.B) {
             const int i = blockIdx.x - a.B;
@@ -554,6 +577,8 @@ int resp_setup(hz_fb* h) {
 }
 
 // h and its partition spectra for the current coefficients / targets
+int modal_prepare(hz_fb* h);
+
 int resp_build_h(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     if (R.h_valid) return HZ_OK;
@@ -588,6 +613,7 @@ int resp_build_h(hz_fb* h) {
         HZ_TRY_HIP(hipGetLastError());
     }
     HZ_TRY(hz_fbi::fb_state_prepare(h));   // the state pass's records and operands, for LAZY too
+    HZ_TRY(modal_prepare(h));               // banks on one pole circle (hz_fb_modal.h)
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));   // pageable coefficient sources
     R.h_valid = true;
     ++R.h_gen;
@@ -599,6 +625,140 @@ int resp_build_h(hz_fb* h) {
 int resp_states(hz_fb* h, double* ystate) {
     hz_fb::Resp& R = h->resp;
     return hz_fbi::fb_state_window(h, R.d_hist[R.hcur], R.K, ystate, h->stream);
+}
+
+// ---- modal band states (hz_fb_modal.h) -----------------------------------------------------
+// Does the bank qualify, and its tables (with h, per coefficient / target change): order 2, every
+// band's poles complex on one circle at angles on the 2 pi / 8192 grid up to |c| K <= 1e-6 (c =
+// log(p / p_g), long double), at most kMaxExc bands with (nearly) coincident poles -- those get their
+// long-double responses for the direct sums.
+int modal_prepare(hz_fb* h) {
+    using namespace hz_modal;
+    hz_fb::Resp& R = h->resp;
+    R.modal_ok = false;
+    const long K = R.K;
+    const int N = h->N;
+    if (h->order != 2 || K < kL || K % kL != 0 || N <= 0 || R.over_valid) return HZ_OK;
+    const long double pi = 3.141592653589793238462643383279502884L;
+    std::vector<BandPar> par((size_t)N);
+    std::vector<int> exc;
+    std::vector<long> mm((size_t)N, -1);
+    std::vector<long double> Rn((size_t)N), ph((size_t)N);
+    long double Rg = -1;
+    for (int n = 0; n < N; ++n) {
+        const long double a1 = h->B[2 * (size_t)n], a2 = h->B[2 * (size_t)n + 1];
+        const long double disc = a2 - a1 * a1 / 4;   // Im(p)^2
+        const long double im = disc > 0 ? sqrtl(disc) : 0.0L;
+        if (a2 <= 0 || im <= 1e-6L * sqrtl(a2)) {
+            exc.push_back(n);
+            continue;
+        }
+        Rn[n] = sqrtl(a2);
+        ph[n] = atan2l(im, -a1 / 2);
+        if (Rg < 0) Rg = Rn[n];
+        const double pin = h->pin[n];
+        BandPar& P = par[n];
+        P.pr = (double)(-a1 / 2);
+        P.pi = (double)im;
+        P.inv_im = (double)(1.0L / im);
+        P.b0 = pin * h->F[3 * (size_t)n];
+        P.b1 = pin * h->F[3 * (size_t)n + 1];
+        P.b2 = pin * h->F[3 * (size_t)n + 2];
+    }
+    if ((int)exc.size() > kMaxExc || Rg < 0) return HZ_OK;
+    std::vector<int> ints(65 + 2 * (size_t)N + kMaxExc, 0);
+    std::vector<std::vector<std::pair<int, int>>> bucket(64);
+    for (int n = 0; n < N; ++n) {
+        if (Rn[n] == 0) continue;   // exceptional
+        const long m = std::lround((double)(ph[n] * kL / (2 * pi)));
+        if (m <= 0 || m >= kL / 2) return HZ_OK;
+        const long double cr = logl(Rn[n] / Rg), ci = ph[n] - 2 * pi * m / kL;
+        if (sqrtl(cr * cr + ci * ci) * K > 1e-6L) return HZ_OK;
+        par[n].cr = (double)cr;
+        par[n].ci = (double)ci;
+        bucket[m & 63].push_back({n, (int)(m >> 6)});
+    }
+    int at = 0;
+    for (int k1 = 0; k1 < 64; ++k1) {
+        ints[k1] = at;
+        for (auto& bk : bucket[k1]) {
+            ints[65 + 2 * at] = bk.first;
+            ints[65 + 2 * at + 1] = bk.second;
+            ++at;
+        }
+    }
+    ints[64] = at;
+    for (size_t e = 0; e < exc.size(); ++e) ints[65 + 2 * (size_t)N + e] = exc[e];
+    // tables: R_g^r, R_g^(L s), e^(2 pi i q / L)
+    const int S = (int)(K / kL);
+    std::vector<double> tab((size_t)kL + S + 2 * (size_t)kL);
+    for (int r = 0; r < kL; ++r) tab[r] = (double)powl(Rg, (long double)r);
+    for (int q = 0; q < S; ++q) tab[kL + q] = (double)powl(Rg, (long double)kL * q);
+    for (int q = 0; q < kL; ++q) {
+        tab[kL + S + 2 * (size_t)q] = (double)cosl(2 * pi * q / kL);
+        tab[kL + S + 2 * (size_t)q + 1] = (double)sinl(2 * pi * q / kL);
+    }
+    // exceptional bands: their zero-start responses r[tau], tau <= K (pin included), long double
+    const int chunks = (int)((K + kExcChunk - 1) / kExcChunk);
+    std::vector<double> er(exc.size() * (size_t)(K + 1));
+    for (size_t e = 0; e < exc.size(); ++e) {
+        const int n = exc[e];
+        const long double f0 = h->F[3 * (size_t)n], f1 = h->F[3 * (size_t)n + 1], f2 = h->F[3 * (size_t)n + 2];
+        const long double a1 = h->B[2 * (size_t)n], a2 = h->B[2 * (size_t)n + 1], pin = h->pin[n];
+        long double y1 = 0, y2 = 0;
+        for (long t = 0; t <= K; ++t) {
+            const long double ff = t == 0 ? f0 : t == 1 ? f1 : t == 2 ? f2 : 0.0L;
+            const long double y = pin * ff - (a1 * y1 + a2 * y2);
+            y2 = y1;
+            y1 = y;
+            er[e * (size_t)(K + 1) + t] = (double)y;
+        }
+    }
+    HZ_TRY(resp_alloc(&R.d_mpar, &R.mpar_cap, (size_t)N * sizeof(BandPar) / sizeof(double)));
+    HZ_TRY(resp_alloc(&R.d_mtab, &R.mtab_cap, tab.size()));
+    HZ_TRY(resp_alloc(&R.d_mA, &R.mA_cap, 2 * 2 * (size_t)kR2 * kR1));
+    HZ_TRY(resp_alloc(&R.d_mexc, &R.mexc_cap, er.size() + exc.size() * (size_t)chunks * 4 + 1));
+    if (ints.size() > R.mint_cap) {
+        if (R.d_mint) HZ_TRY_HIP(hipFree(R.d_mint));
+        R.d_mint = nullptr;
+        HZ_TRY_HIP(hipMalloc(&R.d_mint, sizeof(int) * ints.size()));
+        R.mint_cap = ints.size();
+    }
+    HZ_TRY_HIP(hipMemcpyAsync(R.d_mpar, par.data(), sizeof(BandPar) * N, hipMemcpyHostToDevice, h->stream));
+    HZ_TRY_HIP(hipMemcpyAsync(R.d_mtab, tab.data(), sizeof(double) * tab.size(), hipMemcpyHostToDevice, h->stream));
+    if (!er.empty())
+        HZ_TRY_HIP(hipMemcpyAsync(R.d_mexc, er.data(), sizeof(double) * er.size(), hipMemcpyHostToDevice, h->stream));
+    HZ_TRY_HIP(hipMemcpyAsync(R.d_mint, ints.data(), sizeof(int) * ints.size(), hipMemcpyHostToDevice, h->stream));
+    HZ_TRY_HIP(hipStreamSynchronize(h->stream));   // the host tables above are locals
+    R.mexc_n = (int)exc.size();
+    R.mexc_chunks = chunks;
+    R.mS = S;
+    R.modal_ok = true;
+    return HZ_OK;
+}
+
+void modal_args(hz_fb* h, const double* xw, double* out, hz_modal::ModalArgs* a) {
+    using namespace hz_modal;
+    hz_fb::Resp& R = h->resp;
+    const long K = R.K;
+    *a = ModalArgs();
+    a->on = 1;
+    a->xw = xw;
+    a->K = K;
+    a->S = R.mS;
+    a->wR = R.d_mtab;
+    a->RL = R.d_mtab + kL;
+    a->tw = (const double2*)(R.d_mtab + kL + R.mS);
+    a->A = (double2*)R.d_mA;
+    a->par = (const BandPar*)R.d_mpar;
+    a->csr_ptr = R.d_mint;
+    a->csr = (const int2*)(R.d_mint + 65);
+    a->nexc = R.mexc_n;
+    a->exc_band = R.d_mint + 65 + 2 * (size_t)h->N;
+    a->exc_r = R.d_mexc;
+    a->exc_part = R.d_mexc + (size_t)R.mexc_n * (K + 1);
+    a->exc_chunks = R.mexc_chunks;
+    a->out = out;
 }
 
 long resp_min_call(const hz_fb* h) { return h->resp.min_call > 0 ? h->resp.min_call : kMinCall; }
@@ -761,13 +921,20 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     // inverse kernel (orders <= 2: 256 registers; prefetching its operands into the XCDs' L2 from the
     // MAC kernel was measured: no gain)
     const bool lazy = R.mode == HZ_FB_RESP_LAZY;
-    const bool chained = !lazy && n >= K && h->order <= 2;
+    const bool col = R.col_on && col_q_ok(Q);
+    // banks on one pole circle: the modal states (hz_fb_modal.h) instead of the MFMA pass, phase 1
+    // in the forward kernel, phase 2 in the inverse kernel
+    const bool modal = !lazy && n >= K && R.modal_on && R.modal_ok && !col;
+    const bool chained = !lazy && n >= K && h->order <= 2 && !modal;
+    const bool inside = chained || modal;   // the states come out of the transform kernels
     hz_state::StateArgs st = hz_state::StateArgs();
     if (chained) HZ_TRY(fb_state_chained(h, d_in + (n - K), K, h->d_ystate[h->scur ^ 1], &st));
+    hz_modal::ModalArgs md = hz_modal::ModalArgs();
+    if (modal) modal_args(h, d_in + (n - K), h->d_ystate[h->scur ^ 1], &md);
     const int so = chained ? h->order : 0;
-    const bool col = R.col_on && col_q_ok(Q);
     const int nmac = (kH / 256) * ((B + kMacR - 1) / kMacR);
-    R.last_engine = col ? 1 : 0;
+    R.last_engine = col ? 1 : modal ? 2 : 0;
+    R.modal_last = modal;
     if (col) {
         // column-split path (hz_fb_col.h): window spectra never leave the column kernel; the
         // combine kernel carries the band-state pass
@@ -787,7 +954,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         ca.T = (double2*)R.d_T;
         hipLaunchKernelGGL(pick_col(Q), dim3((unsigned)(hz_col::kUnits * NR)), dim3(hz_col::kColThreads), 0, h->stream, ca);
         HZ_TRY_HIP(hipGetLastError());
-        if (e && chained) {
+        if (e && inside) {
             HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
             h->ev_skip[(e - h->ev.data()) / 5] |= 8;
         }
@@ -796,18 +963,20 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
                            (const double2*)R.d_T, (const unsigned char*)R.d_cmap, (const double2*)R.d_tw4k, st);
         HZ_TRY_HIP(hipGetLastError());
     } else {
-        hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, h->stream, a);
+        const int nm1 = modal ? hz_modal::kPhase1 + md.nexc * md.exc_chunks : 0;
+        hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)(nz + nm1)), dim3(kThreads), 0, h->stream, a, md);
         HZ_TRY_HIP(hipGetLastError());
         hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)nmac), dim3(256), 0, h->stream, (const double2*)R.d_H,
                            (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B);
         HZ_TRY_HIP(hipGetLastError());
-        if (e && chained) {   // profiling: e0..e2 forward + MAC, e2..e4 the inverse kernel with the band states
+        if (e && inside) {   // profiling: e0..e2 forward + MAC, e2..e4 the inverse kernel with the band states
             HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
             h->ev_skip[(e - h->ev.data()) / 5] |= 8;
         }
         RespKernel ki = so == 1 ? resp_inv_kernel<1> : so == 2 ? resp_inv_kernel<2> : resp_inv_kernel<0>;
-        hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0))), dim3(kThreads), 0, h->stream, a,
-                           st);
+        const int nm2 = modal ? hz_modal::kPhase2 + (md.nexc ? 1 : 0) : 0;
+        hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0) + nm2)), dim3(kThreads), 0,
+                           h->stream, a, st, md);
         HZ_TRY_HIP(hipGetLastError());
     }
     if (chained) HZ_TRY(fb_state_combine(h, st, h->stream));   // pieces of a small bank
@@ -855,8 +1024,8 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         }
     }
 #endif
-    if (e && chained) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
-    if (e && !chained) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
+    if (e && inside) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
+    if (e && !inside) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     R.hcur ^= 1;   // the inverse kernel wrote the history after the call
     R.run = std::min(R.run + n, 1L << 60);
     // end state: the band states over the new history (EAGER: computed inside the transform
@@ -867,7 +1036,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         R.implicit = true;
         if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
         if (e) HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
-    } else if (chained) {
+    } else if (inside) {
         R.implicit = false;
     } else {
         if (e) HZ_TRY_HIP(hipEventRecord(e[3], h->stream));
@@ -926,13 +1095,14 @@ int fb_resp_tail_conv(hz_fb* h, const double* u, long n, double* out, hipStream_
     a.Hn = S.d_tH + (size_t)Qp * 2 * kH;
     a.out = out;
     a.upkeep = 0;
-    hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, st, a, hz_modal::ModalArgs());
     HZ_TRY_HIP(hipGetLastError());
     const int nmac = (kH / 256) * ((B + kMacR - 1) / kMacR);
     hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)nmac), dim3(256), 0, st, (const double2*)S.d_tH,
                        (const double2*)S.d_tZ, (double2*)S.d_tY, Q, Qp, B);
     HZ_TRY_HIP(hipGetLastError());
-    hipLaunchKernelGGL(resp_inv_kernel<0>, dim3((unsigned)B), dim3(kThreads), 0, st, a, hz_state::StateArgs());
+    hipLaunchKernelGGL(resp_inv_kernel<0>, dim3((unsigned)B), dim3(kThreads), 0, st, a, hz_state::StateArgs(),
+                       hz_modal::ModalArgs());
     HZ_TRY_HIP(hipGetLastError());
     return HZ_OK;
 }
@@ -940,14 +1110,16 @@ int fb_resp_tail_conv(hz_fb* h, const double* u, long n, double* out, hipStream_
 void fb_resp_free(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     for (double* p : {R.d_hist[0], R.d_hist[1], R.d_h, R.d_hpart, R.d_coef, R.d_zero, R.d_H, R.d_Z, R.d_Y, R.d_tw,
-                      R.d_spart, R.d_sop, R.d_tw4k, R.d_Hc, R.d_T})
+                      R.d_spart, R.d_sop, R.d_tw4k, R.d_Hc, R.d_T, R.d_mpar, R.d_mtab, R.d_mA, R.d_mexc})
         if (p) (void)hipFree(p);
     if (R.d_cmap) (void)hipFree(R.d_cmap);
     if (R.d_scount) (void)hipFree(R.d_scount);
+    if (R.d_mint) (void)hipFree(R.d_mint);
     fb_stream_free(h);
-    const bool col_on = R.col_on;
+    const bool col_on = R.col_on, modal_on = R.modal_on;
     R = hz_fb::Resp();
     R.col_on = col_on;
+    R.modal_on = modal_on;
 }
 
 }  // namespace hz_fbi
@@ -1027,6 +1199,21 @@ int hz_fb_tune_response_engine(hz_fb* h, int column_split) {
     if (!h) return HZ_E_INVALID;
     const bool on = column_split != 0;
     h->resp.col_on = on;
+    return HZ_OK;
+}
+
+int hz_fb_tune_modal(hz_fb* h, int on) {
+    if (!h) return HZ_E_INVALID;
+    h->resp.modal_on = on != 0;
+    return HZ_OK;
+}
+
+int hz_fb_modal_info(hz_fb* h, int* on, int* qualifies, int* exceptional, int* last_call) {
+    if (!h) return HZ_E_INVALID;
+    if (on) *on = h->resp.modal_on ? 1 : 0;
+    if (qualifies) *qualifies = h->resp.modal_ok ? 1 : 0;
+    if (exceptional) *exceptional = h->resp.modal_ok ? h->resp.mexc_n : -1;
+    if (last_call) *last_call = h->resp.modal_last ? 1 : 0;
     return HZ_OK;
 }
 

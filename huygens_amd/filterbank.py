@@ -217,7 +217,18 @@ class Filterbank:
         """-> (column split enabled, last stationary call ran it)"""
         a, b = C.c_int(), C.c_int()
         check(self._lib.hz_fb_response_engine(self._h, C.byref(a), C.byref(b)))
-        return bool(a.value), bool(b.value)
+        return bool(a.value), b.value == 1
+
+    def tune_modal(self, on: bool = True):
+        """modal band states for banks on one pole circle (default on; off: the matrix-core pass)"""
+        check(self._lib.hz_fb_tune_modal(self._h, 1 if on else 0))
+
+    def modal_info(self):
+        """-> (enabled, the bank qualifies, exceptional bands (-1: does not qualify), last stationary
+        call used it)"""
+        v = [C.c_int() for _ in range(4)]
+        check(self._lib.hz_fb_modal_info(self._h, *[C.byref(x) for x in v]))
+        return bool(v[0].value), bool(v[1].value), v[2].value, bool(v[3].value)
 
     def response_info(self):
         """-> (horizon K, stationary samples so far, band states implicit, stationary calls)"""

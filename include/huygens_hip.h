@@ -167,8 +167,19 @@ int hz_fb_tune_response(hz_fb* h, long min_call, long bands_per_sample);
  * for banks whose horizon is 8, 16 or 24 partitions of 2048 -- measured slower on MI355X (C2: 0.048
  * against 0.0405 ms per step).  Results agree to rounding. */
 int hz_fb_tune_response_engine(hz_fb* h, int column_split);
-/* the setting above, and whether the last stationary call ran the column-split path */
+/* the setting above, and the last stationary call's path: 1 column-split, 2 three-kernel with
+ * modal band states (hz_fb_tune_modal), 0 three-kernel with the matrix-core state pass */
 int hz_fb_response_engine(hz_fb* h, int* column_split_on, int* last_call_column_split);
+/* Modal band states (default on): a stationary call's band states for banks whose poles sit on one
+ * circle at angles on the 2 pi / 8192 grid (e.g. the resonator recipe f_i = 0.5 (i + 1) SR / N,
+ * N <= 4096, one R; tests/resynthesis.cpp:48-54) come from a fold of the call's last K inputs and
+ * one 8192-point DFT instead of the N O K multiply-adds of the matrix-core pass; up to 8 bands with
+ * (nearly) coincident poles take direct sums.  Results agree with the matrix-core pass to rounding
+ * (DESIGN.md 3.6).  on = 0: always the matrix-core pass. */
+int hz_fb_tune_modal(hz_fb* h, int on);
+/* the setting, whether the current bank qualifies (its states computed by the modal pass), its
+ * exceptional (direct-sum) bands (-1: does not qualify) and whether the last stationary call used it */
+int hz_fb_modal_info(hz_fb* h, int* on, int* qualifies, int* exceptional, int* last_call);
 /* horizon K (-1: none within 2^21 samples, -2: not computed), stationary samples so far,
  * whether the band states are implicit (LAZY), stationary calls made */
 int hz_fb_response_info(hz_fb* h, long* horizon, long* run, int* implicit_state, long* calls);
