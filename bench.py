@@ -362,6 +362,32 @@ def resp_alg_bytes(K, S, N, O=2, Qp=24):
     return dom, call
 
 
+def modal_kernels(K, S, N, nexc=1):
+    """Per-kernel (flops, algorithmic bytes) of a stationary call with MODAL band states
+    (hz_fb_modal.h), for the three launches:
+      * resp_fwd_kernel: the window transforms (Q + B - 1 real 4096-point) + phase 1 (the fold, 2
+        flops per window sample and map, and 2 x 128 x 64 x 64 real x complex MACs) + the
+        exceptional direct sums (2 dot products of K in double-double, ~20 flops per term);
+        bytes: the call's input and the K history (8 (S + K)), the window spectra out
+        ((Q + B - 1) rows of 2049 complex) and phase 1's A (2 x 64 x 128 complex);
+      * resp_mac_kernel: B x 2048 x Q complex MACs; bytes: Z and H in, Y out;
+      * resp_inv_kernel: the output blocks' inverse transforms + phase 2 (2 x 64 x 128 x 128
+        complex MACs + ~60 flops per band); bytes: Y and A in, the output, the history after the
+        call, the per-band parameters (64 B) and states (16 B) and the smoothers (32 B per band)."""
+    H, lgH, P = 2048, 11, 2048
+    Q, B = K // P, -(-S // P)
+    fft = 5.0 * H * lgH + 10.0 * H
+    row = 16 * (H + 1)
+    a_bytes = 2 * 64 * 128 * 16
+    fwd_f = (Q + B - 1) * fft + 4.0 * K + 2 * 128 * 64 * 64 * 4 + nexc * 2 * K * 20.0
+    fwd_b = 8 * (S + K) + (Q + B - 1) * row + a_bytes + nexc * 8 * (K + 1)
+    mac_f = B * H * Q * 8.0
+    mac_b = (Q + B - 1) * row + Q * row + B * row
+    inv_f = B * fft + 2 * 64 * 128 * 128 * 8.0 + 60.0 * N
+    inv_b = B * row + a_bytes + 8 * S + 8 * K + N * (64 + 16 + 32)
+    return {"resp_fwd_kernel": (fwd_f, fwd_b), "resp_mac_kernel": (mac_f, mac_b), "resp_inv_kernel": (inv_f, inv_b)}
+
+
 def resp_inv_flops(S):
     """FP64 flops of the inverse transforms of a stationary call's output blocks (as resp_step_flops)."""
     H, lgH = 2048, 11
@@ -709,6 +735,7 @@ def main():
     resp = path == HZ_FB_PATH_RESPONSE
     chunk = fb.lti_chunk()   # the timed steps' chunk (the streaming calls below use a shorter one)
     horizon = fb.response_info()[0]
+    modal = bool(resp and fb.modal_info()[3])   # band states by the modal pass (hz_fb_modal.h)
     fb.profile(False)
 
     def timed(fn, warm, steps, n_samples, arm=None):
@@ -738,6 +765,10 @@ def main():
         fb.set_response(HZ_FB_RESP_LAZY)
         side["stationary_lazy_states"] = timed(step, 3, args.side_steps, S)
         fb.set_response(HZ_FB_RESP_EAGER if args.response < 0 else args.response)
+        if fb.modal_info()[3]:   # the same eager states by the matrix-core pass (hz_fb_state.h)
+            fb.tune_modal(False)
+            side["matrix_core_states"] = timed(step, 3, args.side_steps, S)
+            fb.tune_modal(True)
         drain()
     if world > 1 and args.side_steps > 0 and not args.general and args.response != 0:
         # weak-scaling figure: once stationary, a step is ONE call of N x 10 s split by TIME -- each
@@ -949,7 +980,20 @@ def main():
         # band-state pass (hz_fb_state.h: MFMA, ~96% of its flops) beside the output blocks' inverse
         # transforms; the state kernel of the per-band LTI engine; the mix kernel of the general
         # engine -- its average duration from the HIP events around it on the handle's stream
-        if resp:
+        mk = modal_kernels(horizon, out_samples, cnt) if modal else None
+        if modal:
+            # the three launches are each one wave of workgroups (latency-bound, intensity 2-5
+            # flop/B, under the 9.8 flop/B ridge): the longest one by the events, against HBM
+            per_k = {"resp_fwd_kernel": seg_ms, "resp_mac_kernel": mix_ms, "resp_inv_kernel": red_ms}
+            dom = max(per_k, key=per_k.get)
+            dom_name = {"resp_fwd_kernel": "resp_fwd_kernel (window transforms + modal phase 1: the fold and "
+                                           "64-point DFTs of the band states)",
+                        "resp_mac_kernel": "resp_mac_kernel<8,%d> (partition MACs)" % (horizon // 2048),
+                        "resp_inv_kernel": "resp_inv_kernel<0> (inverse transforms of the output blocks + modal "
+                                           "phase 2: 128-point DFTs and the band states)"}[dom]
+            dom_ms = per_k[dom] / max(1, launches)
+            dom_model = mk[dom][0]
+        elif resp:
             dom = "resp_inv_kernel"
             dom_name = ("resp_inv_kernel<2> (inverse transforms of the output blocks + the band-state pass: "
                         "zero-start pass over the %d-sample history on the FP64 matrix cores)" % horizon)
@@ -970,7 +1014,8 @@ def main():
                         else ("resp_fwd_kernel", "resp_mac_kernel", "resp_inv_kernel") if resp
                         else ("fb_mix_kernel", "fb_reduce"))
         extra = (["--lti", args.lti] if args.lti else []) + (["--general"] if args.general else []) + \
-                (["--response", str(args.response)] if args.response >= 0 else [])
+                (["--response", str(args.response)] if args.response >= 0 else []) + \
+                (["--modal", str(args.modal)] if args.modal >= 0 else [])
         traffic = flops = None
         traffic_detail = flops_detail = "skipped (--no-traffic, N > 1 or a non-default step length)"
         if not args.no_traffic and world == 1 and S == SAMPLES_PER_STEP:
@@ -981,11 +1026,23 @@ def main():
         dom_fl = dom_flops if dom_flops else dom_model
         achieved = dom_fl / (dom_ms / 1e3) / 1e12 if (dom_fl and dom_ms > 0) else None
         # ---- the whole step: every kernel of a process() call over its whole GPU time
-        if resp:
+        if modal:
+            step_model = sum(v[0] for v in mk.values())
+        elif resp:
             conv_f, state_f = resp_step_flops(horizon, out_samples, cnt)
             step_model = conv_f + state_f
         else:
             step_model = fb_executed_flops(lti, chunk, N=cnt) * cnt * S
+        # algorithmic bytes of the whole call: the input and history in, the output and the history
+        # out, the partition spectra, the per-band rows (modal: parameters, states, smoothers; the
+        # matrix-core pass: its operand rows) -- not the engine's Z / Y / A intermediates
+        if modal:
+            call_bytes = (8 * (out_samples + horizon) + 8 * out_samples + 8 * horizon
+                          + (horizon // 2048) * 16 * 2049 + cnt * (64 + 16 + 32))
+        elif resp:
+            call_bytes = resp_alg_bytes(horizon, out_samples, cnt)[1]
+        else:
+            call_bytes = 16 * out_samples + 120 * cnt
         step_pmc = sum(flops.values()) if flops else None
         step_fl = step_pmc or step_model
         cpu = None
@@ -1024,11 +1081,24 @@ def main():
                           "to rank 0 by an RCCL reduce (src/filterbank.h:130's mixdown, sharded)"),
                 "time_split_weak": side.get("time_split_weak") or "not measured (--side-steps 0)",
             },
-            "engine": "stationary (bank response convolution, eager band states)" if resp
+            "engine": "stationary (bank response convolution, eager band states: %s)" % (
+                "modal pass, hz_fb_modal.h" if modal else "matrix-core pass, hz_fb_state.h") if resp
                       else "per-band LTI" if lti else "per-band general",
             "roofline": {
-                "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
+                **({"bound": "hbm", "achieved": mk[dom][1] / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else None,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": mk[dom][1] / (dom_ms / 1e3) / 1e9 / HBM_PEAK_GBS if dom_ms > 0 else None,
+                    "algorithmic_bytes_source": "bench.modal_kernels (the kernel's own inputs and outputs)",
+                    "achieved_tflops": achieved,
+                    "kernels_ms_per_call": {"resp_fwd_kernel": seg_ms / max(1, launches),
+                                            "resp_mac_kernel": mix_ms / max(1, launches),
+                                            "resp_inv_kernel": red_ms / max(1, launches)},
+                    "modal_note": "band states by the modal pass (hz_fb_modal.h, DESIGN.md 3.11): the 0.83 GFLOP "
+                                  "matrix-core pass is gone; each of the three launches is one wave of workgroups "
+                                  "at 2-5 flop/B (FP64 ridge 9.8), so the dominant one is quoted against HBM"}
+                   if modal else
+                   {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None}),
                 "traffic": dom_traffic,
                 "kernel": dom_name,
                 "kernel_avg_ms": dom_ms,
@@ -1040,28 +1110,31 @@ def main():
                 # the history written, the pass's operand rows, the states and smoothers -- not the
                 # Y spectra, an engine intermediate); per-band engines: the block I/O and the band
                 # records
-                "algorithmic_bytes_per_launch": resp_alg_bytes(horizon, out_samples, cnt)[0] if resp
+                "algorithmic_bytes_per_launch": mk[dom][1] if modal else
+                                                resp_alg_bytes(horizon, out_samples, cnt)[0] if resp
                                                 else (16 * out_samples + 120 * cnt),
-                "traffic_over_algorithmic": (dom_traffic / resp_alg_bytes(horizon, out_samples, cnt)[0])
+                "traffic_over_algorithmic": (dom_traffic / (mk[dom][1] if modal else
+                                                            resp_alg_bytes(horizon, out_samples, cnt)[0]))
                                             if (resp and dom_traffic) else None,
                 "peak_note": "FP64 MFMA peak = FP64 vector peak on MI355X (78.6 TFLOP/s); the state pass is "
                              "v_mfma_f64_16x16x4f64 chains (scripts/probe/mfma_f64_probe.hip: 71-78 TFLOP/s)",
                 "step": {
                     "kernels": list(step_kernels),
                     "ms_per_call": 1e3 * launch_avg_s,
-                    "components_ms_per_call": {"segment_prepass": seg_ms / max(1, launches),
-                                               "convolution_or_state": mix_ms / max(1, launches),
-                                               "states_or_gemm": red_ms / max(1, launches)},
+                    "components_ms_per_call": ({"forward": seg_ms / max(1, launches),
+                                                "mac": mix_ms / max(1, launches),
+                                                "inverse_and_states": red_ms / max(1, launches)} if resp else
+                                               {"segment_prepass": seg_ms / max(1, launches),
+                                                "convolution_or_state": mix_ms / max(1, launches),
+                                                "states_or_gemm": red_ms / max(1, launches)}),
                     "flops_per_call": step_fl,
                     "flops_source": "pmc" if step_pmc else "model",
                     "model_flops_per_call": step_model,
                     "achieved_tflops": step_fl / launch_avg_s / 1e12 if launch_avg_s > 0 else None,
                     "frac": step_fl / launch_avg_s / 1e12 / FP64_PEAK_TFLOPS if launch_avg_s > 0 else None,
                     "traffic_per_call": sum(traffic.values()) if traffic else None,
-                    "algorithmic_bytes_per_call": resp_alg_bytes(horizon, out_samples, cnt)[1] if resp
-                                                  else (16 * out_samples + 120 * cnt),
-                    "traffic_over_algorithmic": (sum(traffic.values()) / resp_alg_bytes(horizon, out_samples, cnt)[1])
-                                                if (resp and traffic) else None,
+                    "algorithmic_bytes_per_call": call_bytes,
+                    "traffic_over_algorithmic": (sum(traffic.values()) / call_bytes) if (resp and traffic) else None,
                     "traffic_per_kernel": traffic, "flops_per_kernel": flops,
                     "traffic_detail": traffic_detail if not traffic else traffic_detail.get("method"),
                     "flops_detail": flops_detail if not flops else "pmc",

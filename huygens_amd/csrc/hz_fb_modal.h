@@ -35,7 +35,7 @@ namespace hz_modal {
 constexpr int kL = 8192;           // grid / DFT length
 constexpr int kR1 = 128, kR2 = 64; // r = r1 + 128 r2; k = k1 + 64 k2
 constexpr int kMaxExc = 8;         // exceptional bands handled by direct dot products
-constexpr long kExcChunk = 16384;  // samples per exceptional partial
+constexpr long kExcChunk = 4096;   // samples per exceptional partial (16 per thread, loaded at once)
 constexpr int kThreads = 256;
 constexpr int kPhase1 = kR1;       // phase-1 workgroups (one per r1)
 constexpr int kPhase2 = kR2;       // phase-2 workgroups (one per k1), + 1 for the exceptional sums
@@ -64,16 +64,23 @@ struct ModalArgs {
     const double* exc_r;           // [nexc][K + 1] responses (pin included)
     double* exc_part;              // [nexc][chunks][4] (hi, lo) of both components
     int exc_chunks;
+    int first2, n2;                // the launch's phase-2 workgroups: blockIdx.x in [first2, first2 + n2)
+    int per1, per2;                // residues r1 per phase-1 workgroup, k1 per phase-2 workgroup
+    int n1, n2p;                   // phase-1 workgroups (128 / per1), phase-2 DFT workgroups (64 / per2)
     double* out;                   // [N][2]: y[T-1], y[T-2]
 };
 
+// (the DFT twiddles are staged in LDS: a global table read inside the MAC loops cost one L2
+// latency per unrolled batch -- phase 2 took ~19 us that way)
 struct Lds1 {
     double red[4][64][2];
     double F[2][64];
+    double2 w64[kR2];
 };
 struct Lds2 {
     double2 a[2][kR1];
     double2 g[2][kR1];
+    double2 w128[kR1];
     hz_dd::dd part[kThreads][2];
 };
 
@@ -85,8 +92,11 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
 __device__ __forceinline__ void phase1(const ModalArgs& a, int r1, Lds1& L) {
     const int t = threadIdx.x, r2 = t & 63, g = t >> 6;
     const int r = r1 + kR1 * r2;
+    if (t < kR2) L.w64[t] = a.tw[kR1 * t];   // W64^t
+    const double2 wr = a.tw[(r1 * (t & 63)) & (kL - 1)];   // W^(r1 k1) of this thread's output
     const double w0 = a.wR[r];
     double f0 = 0.0, f1 = 0.0;
+#pragma unroll 4
     for (int s = g; s < a.S; s += 4) {
         const long tau = r + (long)kL * s;
         const double v = w0 * a.RL[s] * a.xw[a.K - 1 - tau];
@@ -106,12 +116,12 @@ __device__ __forceinline__ void phase1(const ModalArgs& a, int r1, Lds1& L) {
         double re = 0.0, im = 0.0;
 #pragma unroll 8
         for (int q = 0; q < kR2; ++q) {
-            const double2 w = a.tw[kR1 * ((q * k1) & 63)];   // W64^(q k1)
+            const double2 w = L.w64[(q * k1) & 63];   // W64^(q k1)
             const double f = L.F[j][q];
             re = fma(f, w.x, re);
             im = fma(f, w.y, im);
         }
-        const double2 v = cmul(make_double2(re, im), a.tw[(r1 * k1) & (kL - 1)]);
+        const double2 v = cmul(make_double2(re, im), wr);
         a.A[((long)j * kR2 + k1) * kR1 + r1] = v;
     }
 }
@@ -122,30 +132,58 @@ __device__ __forceinline__ void exc_partial(const ModalArgs& a, int e, int q, Ld
     const int t = threadIdx.x;
     const double* r = a.exc_r + (long)e * (a.K + 1);
     const long t0 = (long)q * kExcChunk, t1 = min(t0 + kExcChunk, a.K);
+    constexpr int kPer = (int)(kExcChunk / kThreads);
+    double rv[kPer], xa[kPer], xb[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {   // every load of the thread first
+        const long tau = t0 + t + (long)i * kThreads;
+        const bool ok = tau < t1;
+        rv[i] = ok ? r[tau] : 0.0;
+        xa[i] = ok ? a.xw[a.K - 1 - tau] : 0.0;
+        xb[i] = (ok && tau < a.K - 1) ? a.xw[a.K - 2 - tau] : 0.0;
+    }
     dd s0{0.0, 0.0}, s1{0.0, 0.0};
-    for (long tau = t0 + t; tau < t1; tau += kThreads) {
-        const double rv = r[tau];
-        s0 = hz_dd::add(s0, hz_dd::two_prod(rv, a.xw[a.K - 1 - tau]));
-        if (tau < a.K - 1) s1 = hz_dd::add(s1, hz_dd::two_prod(rv, a.xw[a.K - 2 - tau]));
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        s0 = hz_dd::add(s0, hz_dd::two_prod(rv[i], xa[i]));
+        s1 = hz_dd::add(s1, hz_dd::two_prod(rv[i], xb[i]));
     }
     L.part[t][0] = s0;
     L.part[t][1] = s1;
     __syncthreads();
+    for (int w = kThreads / 2; w > 0; w >>= 1) {   // tree in a fixed order (a serial walk: ~3 us)
+        if (t < w) {
+            L.part[t][0] = hz_dd::add(L.part[t][0], L.part[t + w][0]);
+            L.part[t][1] = hz_dd::add(L.part[t][1], L.part[t + w][1]);
+        }
+        __syncthreads();
+    }
     if (t < 2) {
-        dd acc{0.0, 0.0};
-        for (int i = 0; i < kThreads; ++i) acc = hz_dd::add(acc, L.part[i][t]);
         double* o = a.exc_part + ((long)e * a.exc_chunks + q) * 4 + 2 * t;
-        o[0] = acc.hi;
-        o[1] = acc.lo;
+        o[0] = L.part[0][t].hi;
+        o[1] = L.part[0][t].lo;
     }
 }
 
 // phase 2, workgroup k1 < 64: G_j[k1 + 64 k2] and the states of the bands of residue k1
 __device__ __forceinline__ void phase2(const ModalArgs& a, int k1, Lds2& L) {
     const int t = threadIdx.x;
+    // every global operand of the workgroup is requested before the first barrier: A, the
+    // twiddles, this thread's first band (csr entry, then its parameters) and the last inputs
+    // (a band chain loaded after the DFT cost ~2 us of dependent latencies)
+    const int i0 = a.csr_ptr[k1], i1 = a.csr_ptr[k1 + 1];
+    const bool has = i0 + t < i1;
+    int2 bk0 = make_int2(0, 0);
+    BandPar P0 = BandPar();
+    if (has) {
+        bk0 = a.csr[i0 + t];
+        P0 = a.par[bk0.x];
+    }
+    const double x1 = a.xw[a.K - 1], x2 = a.xw[a.K - 2], x3 = a.xw[a.K - 3];
     {
         const int j = t >> 7, r1 = t & 127;
         L.a[j][r1] = a.A[((long)j * kR2 + k1) * kR1 + r1];
+        if (t < kR1) L.w128[t] = a.tw[kR2 * t];   // W128^t
     }
     __syncthreads();
     {
@@ -153,7 +191,7 @@ __device__ __forceinline__ void phase2(const ModalArgs& a, int k1, Lds2& L) {
         double re = 0.0, im = 0.0;
 #pragma unroll 8
         for (int r1 = 0; r1 < kR1; ++r1) {
-            const double2 w = a.tw[kR2 * ((r1 * k2) & 127)];   // W128^(r1 k2)
+            const double2 w = L.w128[(r1 * k2) & 127];   // W128^(r1 k2)
             const double2 v = L.a[j][r1];
             re = fma(v.x, w.x, re);
             re = fma(-v.y, w.y, re);
@@ -163,13 +201,10 @@ __device__ __forceinline__ void phase2(const ModalArgs& a, int k1, Lds2& L) {
         L.g[j][k2] = make_double2(re, im);
     }
     __syncthreads();
-    const double x1 = a.xw[a.K - 1], x2 = a.xw[a.K - 2], x3 = a.xw[a.K - 3];
-    for (int i = a.csr_ptr[k1] + t; i < a.csr_ptr[k1 + 1]; i += kThreads) {
-        const int2 bk = a.csr[i];
-        const BandPar P = a.par[bk.x];
+    auto state = [&](const int2 bk, const BandPar& P) {
         const double2 g0 = L.g[0][bk.y], g1 = L.g[1][bk.y];
         // Z1 = G0 + c G1; Z(t-1) = (Z(t) - x[t]) / p = (Z(t) - x[t]) conj(p) / |p|^2
-        double2 z1 = make_double2(g0.x + (P.cr * g1.x - P.ci * g1.y), g0.y + (P.cr * g1.y + P.ci * g1.x));
+        const double2 z1 = make_double2(g0.x + (P.cr * g1.x - P.ci * g1.y), g0.y + (P.cr * g1.y + P.ci * g1.x));
         const double in2 = 1.0 / (P.pr * P.pr + P.pi * P.pi);
         const double2 pc = make_double2(P.pr * in2, -P.pi * in2);
         const double2 z2 = cmul(make_double2(z1.x - x1, z1.y), pc);
@@ -180,6 +215,22 @@ __device__ __forceinline__ void phase2(const ModalArgs& a, int k1, Lds2& L) {
         // Im(p u) / Im p
         a.out[2L * bk.x] = (P.pr * u1.y + P.pi * u1.x) * P.inv_im;
         a.out[2L * bk.x + 1] = (P.pr * u2.y + P.pi * u2.x) * P.inv_im;
+    };
+    if (has) state(bk0, P0);
+    for (int i = i0 + t + kThreads; i < i1; i += kThreads) state(a.csr[i], a.par[a.csr[i].x]);
+}
+
+// per1 residues / per2 columns per workgroup, one after the other
+__device__ __forceinline__ void phase1_group(const ModalArgs& a, int w, Lds1& L) {
+    for (int i = 0; i < a.per1; ++i) {
+        phase1(a, w * a.per1 + i, L);
+        __syncthreads();
+    }
+}
+__device__ __forceinline__ void phase2_group(const ModalArgs& a, int w, Lds2& L) {
+    for (int i = 0; i < a.per2; ++i) {
+        phase2(a, w * a.per2 + i, L);
+        __syncthreads();
     }
 }
 

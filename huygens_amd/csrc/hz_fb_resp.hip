@@ -31,6 +31,7 @@
 // rank's run of output blocks with the whole bank's response; DESIGN.md 3.6 and 5.
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #include "hz_fb_impl.h"
 #include "hz_fb_state.h"
@@ -247,8 +248,8 @@ __global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a, hz_modal
     __shared__ RespFwdLds u;
     if (md.on && (int)blockIdx.x >= a.nz) {
         const int i = blockIdx.x - a.nz;
-        if (i < hz_modal::kPhase1) hz_modal::phase1(md, i, u.m1);
-        else hz_modal::exc_partial(md, (i - hz_modal::kPhase1) / md.exc_chunks, (i - hz_modal::kPhase1) % md.exc_chunks, u.m2);
+        if (i < md.n1) hz_modal::phase1_group(md, i, u.m1);
+        else hz_modal::exc_partial(md, (i - md.n1) / md.exc_chunks, (i - md.n1) % md.exc_chunks, u.m2);
         return;
     }
     hz2k::Lds& s = u.fft;
@@ -266,8 +267,16 @@ __global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a, hz_modal
 // QP == 0: any Qp, the next block's 2R loads issued before this block's MACs.
 template <int R, int QP>
 __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict__ H, const double2* __restrict__ Z,
-                                                       double2* __restrict__ Y, int Q, int Qp, int B) {
+                                                       double2* __restrict__ Y, int Q, int Qp, int B,
+                                                       hz_modal::ModalArgs md) {
     constexpr int kBinGroups = kH / 256;
+    if (md.on && (int)blockIdx.x >= md.first2) {   // modal band states, phase 2 (hz_fb_modal.h)
+        __shared__ hz_modal::Lds2 l2;
+        const int i = blockIdx.x - md.first2;
+        if (i < md.n2p) hz_modal::phase2_group(md, i, l2);
+        else hz_modal::exc_sum(md);
+        return;
+    }
     const int q = (blockIdx.x % kBinGroups) * blockDim.x + threadIdx.x;   // bin
     const int b0 = (blockIdx.x / kBinGroups) * R;
     HZ_DIAG_AT(1, 0);
@@ -340,7 +349,7 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
     HZ_DIAG_AT(1, 3);
 }
 
-typedef void (*MacKernel)(const double2*, const double2*, double2*, int, int, int);
+typedef void (*MacKernel)(const double2*, const double2*, double2*, int, int, int, hz_modal::ModalArgs);
 MacKernel pick_mac(int Qp) {
     switch (Qp) {
     case 8: return resp_mac_kernel<kMacR, 8>;
@@ -378,10 +387,10 @@ template <int SO>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void resp_inv_kernel(
     RespArgs a, hz_state::StateArgs st, hz_modal::ModalArgs md) {
     __shared__ RespLds u;
-    if constexpr (SO == 0) {   // modal band states, phase 2 (hz_fb_modal.h)
-        if (md.on && (int)blockIdx.x >= a.B) {
-            const int i = blockIdx.x - a.B;
-            if (i < hz_modal::kPhase2) hz_modal::phase2(md, i, u.md);
+    if constexpr (SO == 0) {   // modal band states, phase 2 (hz_fb_modal.h): workgroups [first2, first2 + n2)
+        const int i = (int)blockIdx.x - md.first2;
+        if (md.on && i >= 0 && i < md.n2) {
+            if (i < md.n2p) hz_modal::phase2_group(md, i, u.md);
             else hz_modal::exc_sum(md);
             return;
         }
@@ -395,7 +404,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     }
     hz2k::Lds& s = u.fft;
     const int t = threadIdx.x;
-    const long b = blockIdx.x;
+    const long b = (long)blockIdx.x - ((SO == 0 && md.on && md.first2 == 0) ? md.n2 : 0);
 #ifdef HZ_DIAG_STAMPS
     long long* stp = SO > 0 && st.stamps ? st.stamps + ((long)st.G * st.nseg + b) * 4 : nullptr;
     if (stp && t == 0) {
@@ -759,6 +768,13 @@ void modal_args(hz_fb* h, const double* xw, double* out, hz_modal::ModalArgs* a)
     a->exc_part = R.d_mexc + (size_t)R.mexc_n * (K + 1);
     a->exc_chunks = R.mexc_chunks;
     a->out = out;
+    // (A/B) residues per phase-1 workgroup, columns per phase-2 workgroup
+    static const int per1 = std::getenv("HZ_MODAL_R1PER") ? std::atoi(std::getenv("HZ_MODAL_R1PER")) : 1;
+    static const int per2 = std::getenv("HZ_MODAL_K1PER") ? std::atoi(std::getenv("HZ_MODAL_K1PER")) : 1;
+    a->per1 = (per1 > 0 && kR1 % per1 == 0) ? per1 : 1;
+    a->per2 = (per2 > 0 && kR2 % per2 == 0) ? per2 : 1;
+    a->n1 = kR1 / a->per1;
+    a->n2p = kR2 / a->per2;
 }
 
 long resp_min_call(const hz_fb* h) { return h->resp.min_call > 0 ? h->resp.min_call : kMinCall; }
@@ -963,20 +979,38 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
                            (const double2*)R.d_T, (const unsigned char*)R.d_cmap, (const double2*)R.d_tw4k, st);
         HZ_TRY_HIP(hipGetLastError());
     } else {
-        const int nm1 = modal ? hz_modal::kPhase1 + md.nexc * md.exc_chunks : 0;
+        // (HZ_MODAL_DIAG, timing diagnostics only -- wrong states: 1 no phase-1 / exceptional
+        // workgroups, 2 no phase 2, 3 no exceptional partials)
+        static const int diag = std::getenv("HZ_MODAL_DIAG") ? std::atoi(std::getenv("HZ_MODAL_DIAG")) : 0;
+        const int nm1 = !modal || diag == 1 ? 0 : diag == 3 ? md.n1 : md.n1 + md.nexc * md.exc_chunks;
         hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)(nz + nm1)), dim3(kThreads), 0, h->stream, a, md);
         HZ_TRY_HIP(hipGetLastError());
-        hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)nmac), dim3(256), 0, h->stream, (const double2*)R.d_H,
-                           (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B);
+        if (e && inside) {   // profiling: e0..e1 forward, e1..e2 MAC, e2..e4 inverse with the band states
+            HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
+            h->ev_skip[(e - h->ev.data()) / 5] &= (unsigned char)~2;
+        }
+        // phase 2: extra workgroups of the inverse kernel after its transforms (HZ_MODAL_P2 =
+        // inv_first: before them; mac: beside the MAC -- A/B)
+        static const char* p2env = std::getenv("HZ_MODAL_P2");
+        static const int p2 = !p2env ? 1 : std::string(p2env) == "mac" ? 0 : std::string(p2env) == "inv_first" ? 2 : 1;
+        const int nm2 = !modal || diag == 2 ? 0 : md.n2p + (md.nexc ? 1 : 0);
+        hz_modal::ModalArgs mdm = md, mdi = md;
+        mdm.on = modal && p2 == 0;
+        mdm.first2 = nmac;
+        mdm.n2 = nm2;
+        mdi.on = modal && p2 != 0;
+        mdi.first2 = p2 == 2 ? 0 : B;
+        mdi.n2 = nm2;
+        hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)(nmac + (mdm.on ? nm2 : 0))), dim3(256), 0, h->stream,
+                           (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B, mdm);
         HZ_TRY_HIP(hipGetLastError());
-        if (e && inside) {   // profiling: e0..e2 forward + MAC, e2..e4 the inverse kernel with the band states
+        if (e && inside) {
             HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
             h->ev_skip[(e - h->ev.data()) / 5] |= 8;
         }
         RespKernel ki = so == 1 ? resp_inv_kernel<1> : so == 2 ? resp_inv_kernel<2> : resp_inv_kernel<0>;
-        const int nm2 = modal ? hz_modal::kPhase2 + (md.nexc ? 1 : 0) : 0;
-        hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0) + nm2)), dim3(kThreads), 0,
-                           h->stream, a, st, md);
+        hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0) + (mdi.on ? nm2 : 0))),
+                           dim3(kThreads), 0, h->stream, a, st, mdi);
         HZ_TRY_HIP(hipGetLastError());
     }
     if (chained) HZ_TRY(fb_state_combine(h, st, h->stream));   // pieces of a small bank
@@ -1099,7 +1133,7 @@ int fb_resp_tail_conv(hz_fb* h, const double* u, long n, double* out, hipStream_
     HZ_TRY_HIP(hipGetLastError());
     const int nmac = (kH / 256) * ((B + kMacR - 1) / kMacR);
     hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)nmac), dim3(256), 0, st, (const double2*)S.d_tH,
-                       (const double2*)S.d_tZ, (double2*)S.d_tY, Q, Qp, B);
+                       (const double2*)S.d_tZ, (double2*)S.d_tY, Q, Qp, B, hz_modal::ModalArgs());
     HZ_TRY_HIP(hipGetLastError());
     hipLaunchKernelGGL(resp_inv_kernel<0>, dim3((unsigned)B), dim3(kThreads), 0, st, a, hz_state::StateArgs(),
                        hz_modal::ModalArgs());

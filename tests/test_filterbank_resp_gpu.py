@@ -344,6 +344,7 @@ def test_column_split_vs_three_kernel(gpu_lib, R, centre, order):
     g.tune_response_engine(True)
     t, _ = make(order, N, fwd, back, oracle=False)
     t.tune_response_engine(False)
+    t.tune_modal(False)   # the same (matrix-core) band-state pass on both: this compares the convolutions
     rng = np.random.default_rng(21)
     col_calls = 0
     for i, n in enumerate([3000, 60000, 60000, 50001, 2048 * 30, 100000, 16384, 99999]):
