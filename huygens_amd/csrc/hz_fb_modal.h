@@ -38,7 +38,8 @@ constexpr int kMaxExc = 8;         // exceptional bands handled by direct dot pr
 constexpr long kExcChunk = 4096;   // samples per exceptional partial (16 per thread, loaded at once)
 constexpr int kThreads = 256;
 constexpr int kPhase1 = kR1;       // phase-1 workgroups (one per r1)
-constexpr int kPhase2 = kR2;       // phase-2 workgroups (one per k1), + 1 for the exceptional sums
+constexpr int kParts = 4;          // phase-2 workgroups per k1 (16 bins k2 < 64 each)
+constexpr int kPhase2 = kR2 * kParts;   // phase-2 workgroups, + 1 for the exceptional sums
 
 struct BandPar {                   // regular band n
     double pr, pi;                 // pole p = (-a1 / 2, sqrt(a2 - a1^2 / 4))
@@ -57,7 +58,7 @@ struct ModalArgs {
     const double2* tw;             // [kL] e^(2 pi i q / kL)
     double2* A;                    // [2][64][128]
     const BandPar* par;            // [N]
-    const int* csr_ptr;            // [65] bands of residue k1 = m mod 64: csr[csr_ptr[k1] .. csr_ptr[k1 + 1])
+    const int* csr_ptr;            // [257] bands of bin group w = 4 k1 + k2 / 16 (k1 = m mod 64, k2 = m / 64)
     const int2* csr;               // (band, k2)
     int nexc;
     const int* exc_band;           // [nexc]
@@ -93,7 +94,7 @@ __device__ __forceinline__ void phase1(const ModalArgs& a, int r1, Lds1& L) {
     const int t = threadIdx.x, r2 = t & 63, g = t >> 6;
     const int r = r1 + kR1 * r2;
     if (t < kR2) L.w64[t] = a.tw[kR1 * t];   // W64^t
-    const double2 wr = a.tw[(r1 * (t & 63)) & (kL - 1)];   // W^(r1 k1) of this thread's output
+    const double2 wr = a.tw[(r1 * ((t >> 1) & 63)) & (kL - 1)];   // W^(r1 k1) of this thread's output
     const double w0 = a.wR[r];
     double f0 = 0.0, f1 = 0.0;
 #pragma unroll 4
@@ -111,18 +112,19 @@ __device__ __forceinline__ void phase1(const ModalArgs& a, int r1, Lds1& L) {
         L.F[j][q] = ((L.red[0][q][j] + L.red[1][q][j]) + L.red[2][q][j]) + L.red[3][q][j];
     }
     __syncthreads();
-    if (t < 128) {
-        const int j = t >> 6, k1 = t & 63;
+    {   // output (j, k1) by two threads, q halves, summed through a lane exchange
+        const int j = t >> 7, k1 = (t >> 1) & 63, h = t & 1;
         double re = 0.0, im = 0.0;
 #pragma unroll 8
-        for (int q = 0; q < kR2; ++q) {
+        for (int q = 32 * h; q < 32 * h + 32; ++q) {
             const double2 w = L.w64[(q * k1) & 63];   // W64^(q k1)
             const double f = L.F[j][q];
             re = fma(f, w.x, re);
             im = fma(f, w.y, im);
         }
-        const double2 v = cmul(make_double2(re, im), wr);
-        a.A[((long)j * kR2 + k1) * kR1 + r1] = v;
+        re += __shfl_xor(re, 1);
+        im += __shfl_xor(im, 1);
+        if (!h) a.A[((long)j * kR2 + k1) * kR1 + r1] = cmul(make_double2(re, im), wr);
     }
 }
 
@@ -166,12 +168,14 @@ __device__ __forceinline__ void exc_partial(const ModalArgs& a, int e, int q, Ld
 }
 
 // phase 2, workgroup k1 < 64: G_j[k1 + 64 k2] and the states of the bands of residue k1
-__device__ __forceinline__ void phase2(const ModalArgs& a, int k1, Lds2& L) {
-    const int t = threadIdx.x;
-    // every global operand of the workgroup is requested before the first barrier: A, the
-    // twiddles, this thread's first band (csr entry, then its parameters) and the last inputs
-    // (a band chain loaded after the DFT cost ~2 us of dependent latencies)
-    const int i0 = a.csr_ptr[k1], i1 = a.csr_ptr[k1 + 1];
+// phase 2, workgroup w = 4 k1 + part (part < 4): G_j[k1 + 64 k2] for k2 in [16 part, 16 part + 16)
+// (32 outputs, eight threads each over r1 eighths; bands use m < L / 2, i.e. k2 < 64) and the
+// states of the bands in that bin range
+__device__ __forceinline__ void phase2(const ModalArgs& a, int w, Lds2& L) {
+    const int t = threadIdx.x, k1 = w >> 2, part = w & 3;
+    // every global operand is requested before the first barrier: A, the twiddles, this thread's
+    // first band (csr entry, then its parameters) and the last inputs
+    const int i0 = a.csr_ptr[w], i1 = a.csr_ptr[w + 1];
     const bool has = i0 + t < i1;
     int2 bk0 = make_int2(0, 0);
     BandPar P0 = BandPar();
@@ -187,18 +191,25 @@ __device__ __forceinline__ void phase2(const ModalArgs& a, int k1, Lds2& L) {
     }
     __syncthreads();
     {
-        const int j = t >> 7, k2 = t & 127;
+        const int o = t >> 3, qq = t & 7;          // output o = (j, k2 - 16 part), r1 eighth qq
+        const int j = o >> 4, k2 = 16 * part + (o & 15);
         double re = 0.0, im = 0.0;
 #pragma unroll 8
-        for (int r1 = 0; r1 < kR1; ++r1) {
-            const double2 w = L.w128[(r1 * k2) & 127];   // W128^(r1 k2)
+        for (int r1 = 16 * qq; r1 < 16 * qq + 16; ++r1) {
+            const double2 wv = L.w128[(r1 * k2) & 127];   // W128^(r1 k2)
             const double2 v = L.a[j][r1];
-            re = fma(v.x, w.x, re);
-            re = fma(-v.y, w.y, re);
-            im = fma(v.x, w.y, im);
-            im = fma(v.y, w.x, im);
+            re = fma(v.x, wv.x, re);
+            re = fma(-v.y, wv.y, re);
+            im = fma(v.x, wv.y, im);
+            im = fma(v.y, wv.x, im);
         }
-        L.g[j][k2] = make_double2(re, im);
+        re += __shfl_xor(re, 1);
+        im += __shfl_xor(im, 1);
+        re += __shfl_xor(re, 2);
+        im += __shfl_xor(im, 2);
+        re += __shfl_xor(re, 4);
+        im += __shfl_xor(im, 4);
+        if (!qq) L.g[j][k2] = make_double2(re, im);
     }
     __syncthreads();
     auto state = [&](const int2 bk, const BandPar& P) {

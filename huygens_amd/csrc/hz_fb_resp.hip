@@ -675,8 +675,9 @@ int modal_prepare(hz_fb* h) {
         P.b2 = pin * h->F[3 * (size_t)n + 2];
     }
     if ((int)exc.size() > kMaxExc || Rg < 0) return HZ_OK;
-    std::vector<int> ints(65 + 2 * (size_t)N + kMaxExc, 0);
-    std::vector<std::vector<std::pair<int, int>>> bucket(64);
+    constexpr int kW2 = kPhase2;   // phase-2 bin groups: w = 4 k1 + k2 / 16 (k2 < 64: m < L / 2)
+    std::vector<int> ints(kW2 + 1 + 2 * (size_t)N + kMaxExc, 0);
+    std::vector<std::vector<std::pair<int, int>>> bucket(kW2);
     for (int n = 0; n < N; ++n) {
         if (Rn[n] == 0) continue;   // exceptional
         const long m = std::lround((double)(ph[n] * kL / (2 * pi)));
@@ -685,19 +686,19 @@ int modal_prepare(hz_fb* h) {
         if (sqrtl(cr * cr + ci * ci) * K > 1e-6L) return HZ_OK;
         par[n].cr = (double)cr;
         par[n].ci = (double)ci;
-        bucket[m & 63].push_back({n, (int)(m >> 6)});
+        bucket[(m & 63) * kParts + (int)((m >> 6) / 16)].push_back({n, (int)(m >> 6)});
     }
     int at = 0;
-    for (int k1 = 0; k1 < 64; ++k1) {
-        ints[k1] = at;
-        for (auto& bk : bucket[k1]) {
-            ints[65 + 2 * at] = bk.first;
-            ints[65 + 2 * at + 1] = bk.second;
+    for (int w = 0; w < kW2; ++w) {
+        ints[w] = at;
+        for (auto& bk : bucket[w]) {
+            ints[kW2 + 1 + 2 * at] = bk.first;
+            ints[kW2 + 1 + 2 * at + 1] = bk.second;
             ++at;
         }
     }
-    ints[64] = at;
-    for (size_t e = 0; e < exc.size(); ++e) ints[65 + 2 * (size_t)N + e] = exc[e];
+    ints[kW2] = at;
+    for (size_t e = 0; e < exc.size(); ++e) ints[kW2 + 1 + 2 * (size_t)N + e] = exc[e];
     // tables: R_g^r, R_g^(L s), e^(2 pi i q / L)
     const int S = (int)(K / kL);
     std::vector<double> tab((size_t)kL + S + 2 * (size_t)kL);
@@ -761,9 +762,9 @@ void modal_args(hz_fb* h, const double* xw, double* out, hz_modal::ModalArgs* a)
     a->A = (double2*)R.d_mA;
     a->par = (const BandPar*)R.d_mpar;
     a->csr_ptr = R.d_mint;
-    a->csr = (const int2*)(R.d_mint + 65);
+    a->csr = (const int2*)(R.d_mint + kPhase2 + 1);
     a->nexc = R.mexc_n;
-    a->exc_band = R.d_mint + 65 + 2 * (size_t)h->N;
+    a->exc_band = R.d_mint + kPhase2 + 1 + 2 * (size_t)h->N;
     a->exc_r = R.d_mexc;
     a->exc_part = R.d_mexc + (size_t)R.mexc_n * (K + 1);
     a->exc_chunks = R.mexc_chunks;
@@ -772,9 +773,9 @@ void modal_args(hz_fb* h, const double* xw, double* out, hz_modal::ModalArgs* a)
     static const int per1 = std::getenv("HZ_MODAL_R1PER") ? std::atoi(std::getenv("HZ_MODAL_R1PER")) : 1;
     static const int per2 = std::getenv("HZ_MODAL_K1PER") ? std::atoi(std::getenv("HZ_MODAL_K1PER")) : 1;
     a->per1 = (per1 > 0 && kR1 % per1 == 0) ? per1 : 1;
-    a->per2 = (per2 > 0 && kR2 % per2 == 0) ? per2 : 1;
+    a->per2 = (per2 > 0 && kPhase2 % per2 == 0) ? per2 : 1;
     a->n1 = kR1 / a->per1;
-    a->n2p = kR2 / a->per2;
+    a->n2p = kPhase2 / a->per2;
 }
 
 long resp_min_call(const hz_fb* h) { return h->resp.min_call > 0 ? h->resp.min_call : kMinCall; }
