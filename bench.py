@@ -765,7 +765,7 @@ def main():
         fb.set_response(HZ_FB_RESP_LAZY)
         side["stationary_lazy_states"] = timed(step, 3, args.side_steps, S)
         fb.set_response(HZ_FB_RESP_EAGER if args.response < 0 else args.response)
-        if fb.modal_info()[3]:   # the same eager states by the matrix-core pass (hz_fb_state.h)
+        if modal:   # the same eager states by the matrix-core pass (hz_fb_state.h)
             fb.tune_modal(False)
             side["matrix_core_states"] = timed(step, 3, args.side_steps, S)
             fb.tune_modal(True)
