@@ -398,7 +398,7 @@ PMC_FLOP_COUNTERS = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS
                      "SQ_INSTS_VALU_MFMA_MOPS_F64")
 
 
-def pmc_pass(counters, kernels, extra=()):
+def pmc_pass(counters, kernels, extra=(), per_step=None):
     """One rocprofv3 --pmc pass (kernel trace only, no other tracing) of a short bench run as a
     child process: per kernel (name substring) and counter the mean over its two largest
     dispatches (the per-step launches).  Returns ({kernel: {counter: value}}, None) or
@@ -434,6 +434,10 @@ def pmc_pass(counters, kernels, extra=()):
                 if r["Counter_Name"] == c and k in r["Kernel_Name"]:
                     per[r.get("Dispatch_Id", len(per))] = per.get(r.get("Dispatch_Id", len(per)), 0.0) + \
                         float(r["Counter_Value"])
+            if per_step:   # several launches per step: all dispatches' sum per step
+                if per:
+                    out.setdefault(k, {})[c] = sum(per.values()) * per_step / len(per)
+                continue
             v = sorted(per.values())[-2:]
             if v:
                 out.setdefault(k, {})[c] = sum(v) / len(v)
@@ -442,14 +446,14 @@ def pmc_pass(counters, kernels, extra=()):
     return out, None
 
 
-def pmc_traffic(kernels, extra=()):
+def pmc_traffic(kernels, extra=(), per_step=None):
     """HBM bytes per launch of each kernel from two separate rocprofv3 --pmc passes (FETCH_SIZE,
     WRITE_SIZE; kernel-trace only).  Correction per MI355X_MICROARCH.md 'HBM': FETCH_SIZE counts
     wide coalesced streaming reads at 1/2 of their bytes, so it is doubled; WRITE_SIZE is taken as
     is; both are in KB.  Returns ({kernel: bytes}, detail) or (None, reason)."""
     per = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        res, err = pmc_pass((counter,), kernels, extra)
+        res, err = pmc_pass((counter,), kernels, extra, per_step=per_step)
         if res is None:
             return None, err
         for k, cv in res.items():

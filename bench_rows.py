@@ -105,6 +105,46 @@ def pmc_counts(kernel, workload, counters):
     return out
 
 
+def row_evidence(kernel, workload, seconds_per_unit, counters=PMC_VALU, per_step=None, alg_bytes=None):
+    """PMC evidence for a row's dominant kernel: HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, separate
+    passes) and executed FP32 / FP64 flops and transcendental lane-ops, each over
+    `seconds_per_unit` (the kernel's HIP-event time per launch, or per step when `per_step` = the
+    launches per step: then the counts are summed over all dispatches and divided by
+    dispatches / per_step) against its pipe's peak.  The binding pipe is the largest fraction."""
+    import bench
+    mode = "launch" if per_step is None else f"step ({per_step} launches)"
+    res, err = bench.pmc_pass(counters, (kernel,), extra=("--workload", workload), per_step=per_step)
+    if res is None:
+        return {"error": err}
+    c = res.get(kernel, {})
+    tr, terr = bench.pmc_traffic((kernel,), extra=("--workload", workload), per_step=per_step)
+    lanes = 64.0
+    f32 = lanes * (2 * c.get("SQ_INSTS_VALU_FMA_F32", 0) + c.get("SQ_INSTS_VALU_MUL_F32", 0) +
+                   c.get("SQ_INSTS_VALU_ADD_F32", 0))
+    f64 = lanes * (2 * c.get("SQ_INSTS_VALU_FMA_F64", 0) + c.get("SQ_INSTS_VALU_MUL_F64", 0) +
+                   c.get("SQ_INSTS_VALU_ADD_F64", 0)) + 512.0 * c.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0)
+    trans = lanes * (c.get("SQ_INSTS_VALU_TRANS_F32", 0) + c.get("SQ_INSTS_VALU_TRANS_F64", 0))
+    traffic = (tr or {}).get(kernel)
+    out = {"kernel": kernel, "per": mode, "counters": c, "f32_flops": f32, "f64_flops": f64, "trans_ops": trans,
+           "traffic_bytes": traffic, "traffic_error": terr if tr is None else None,
+           "algorithmic_bytes": alg_bytes, "seconds": seconds_per_unit}
+    if seconds_per_unit:
+        fr = {"fp32_valu": f32 / seconds_per_unit / 1e12 / FP32_PEAK,
+              "fp64_valu": f64 / seconds_per_unit / 1e12 / FP64_PEAK,
+              "transcendental": trans / seconds_per_unit / 1e12 / (FP32_PEAK / 8)}
+        if traffic:
+            fr["hbm"] = traffic / seconds_per_unit / 1e9 / HBM_PEAK
+        out.update(tflops_fp64=f64 / seconds_per_unit / 1e12, tflops_fp32=f32 / seconds_per_unit / 1e12,
+                   gbs=traffic / seconds_per_unit / 1e9 if traffic else None, fracs=fr,
+                   binding_pipe=max(fr, key=fr.get))
+        if traffic and alg_bytes:
+            out["traffic_over_algorithmic"] = traffic / alg_bytes
+    out["note"] = ("counts from rocprofv3 --pmc passes of this row (kernel trace only); seconds from HIP events "
+                   "on the engine's stream; the row's rocprofv3 kernel-trace summary (profiles/r5/rows/*_kernel_"
+                   "stats*.csv) reproduces the time")
+    return out
+
+
 def pipe_fracs(counts, seconds):
     """each pipe's executed rate over the kernel's time against that pipe's peak"""
     if not counts or "error" in counts or not seconds:
@@ -173,6 +213,10 @@ def run_c3(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
         cpu = {"value": V * O * n / dt, "unit": "partial-samples/s", "cores": 1, "kind": "port",
                "sample": f"oracle/hz_oracle_osc.c Additive, {V}x{O} partials x {n} samples, 1 thread, {dt:.2f} s"}
     xach = EXEC_C3 * units / kern_s / 1e12 if kern_s > 0 else None
+    ev = None
+    if not getattr(args, "no_traffic", True) and sw == 1:
+        ev = row_evidence("add_mix_kernel", "c3", kern_s / args.steps, per_step=2,
+                          alg_bytes=8.0 * S)   # the mix's output; partial state stays on chip
     return {
         "metric": "partial-samples/s for 64-voice x 256-overtone Additive",
         "value": units / elapsed, "unit": "partial-samples/s",
@@ -183,7 +227,8 @@ def run_c3(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
                    "parallelism": f"overtones sharded x{world}, RCCL reduce"},
         "n_gpus": world, "scaling": "strong", "emulated_world": shard_world,
         "roofline": {"bound": "valu", "achieved": xach, "peak": FP64_PEAK, "unit": "TFLOP/s",
-                     "frac": xach / FP64_PEAK if xach else None, "traffic": None,
+                     "frac": xach / FP64_PEAK if xach else None,
+                     "traffic": (ev or {}).get("traffic_bytes"), "pmc_evidence": ev,
                      "kernel": "add_mix_kernel (+ add_reduce_kernel, add_advance_kernel)",
                      "kernel_avg_ms": ms / max(1, launches), "launches": launches,
                      "kernel_ms_per_step": ms / args.steps, "launches_per_step": launches / max(1, args.steps),
@@ -405,6 +450,13 @@ def run_c5(args, torch, dev):
         pipes = pipe_fracs(pmc_counts("bowl_mix_kernel", "c5", PMC_VALU), kb)
         chain_pipes = pipe_fracs(pmc_counts("bowl_dly_chain_kernel", "c5", PMC_VALU), kc)
         chain_traffic, _ = bench.pmc_traffic(("bowl_dly_chain_kernel",), extra=("--workload", "c5"))
+        mix_traffic, _ = bench.pmc_traffic(("bowl_mix_kernel",), extra=("--workload", "c5"))
+        if pipes and "error" not in pipes:
+            pipes["traffic_bytes"] = (mix_traffic or {}).get("bowl_mix_kernel")
+            pipes["algorithmic_bytes"] = 12.0 * M + 8.0 * n   # mode table in, f64 mix out
+            if pipes["traffic_bytes"]:
+                pipes["gbs"] = pipes["traffic_bytes"] / kb / 1e9
+                pipes["fracs"]["hbm"] = pipes["gbs"] / HBM_PEAK
     cpu = None
     if not args.no_cpu_baseline:
         _tests_path()
@@ -425,7 +477,8 @@ def run_c5(args, torch, dev):
         "config": {"workload": "C5 Bowl<float>(2048) fill x 469 blocks + Delaybank<float,64>(3, 2SR), mix /64",
                    "samples_per_step": n, "block": B, "modes": M, "lines": L},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": FP32_PEAK, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_PEAK if achieved else None, "traffic": None,
+                     "frac": achieved / FP32_PEAK if achieved else None,
+                     "traffic": (pipes or {}).get("traffic_bytes"),
                      "kernel": "bowl_mix_kernel (float phase model)",
                      "kernel_ms_whole_signal": bms_w / max(1, bl_w), "flops_per_unit": 8,
                      "mode_samples_per_s_kernel": bowl_rate,
@@ -496,6 +549,11 @@ def run_c6(args, torch, dev):
     g.profile(False)
     flops = 16.0 * gs   # per grain-sample: 16 FP64 flops + 1 cos + 1 divide
     achieved = flops / (ms / 1e3) / 1e12 if ms > 0 else None
+    ev = None
+    if not getattr(args, "no_traffic", True) and launches:
+        per = max(1, round(launches / args.steps))
+        ev = row_evidence("gran_kernel", "c6", ms / 1e3 / args.steps, per_step=per,
+                          alg_bytes=16.0 * S + 16.0 * gs / args.steps)   # in/out + two ring reads per grain-sample
     cpu = None
     if not args.no_cpu_baseline:
         _tests_path()
@@ -520,7 +578,8 @@ def run_c6(args, torch, dev):
         "config": {"workload": "C6 Granulator<double>(&hann, Buffer(3*SR), 512) (SURVEY.md 8(f) row 1)",
                    "samples_per_step": S, "requests_per_step": int(reqs.size), "polyphony": P},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK if achieved else None, "traffic": None,
+                     "frac": achieved / FP64_PEAK if achieved else None,
+                     "traffic": (ev or {}).get("traffic_bytes"), "pmc_evidence": ev,
                      "kernel": "gran_kernel", "kernel_ms_per_step": ms / args.steps, "launches": launches,
                      "grain_samples_per_step": gs / args.steps, "flops_per_unit": 16,
                      "note": "16 FP64 flops + cos + divide per grain-sample; transcendental-bound"},
@@ -568,6 +627,10 @@ def run_c7(args, torch, dev):
     # GB/s of the dominant kernel: 8 B in + 8 B out per sample over its launches' mean duration
     kern_s = kms / 1e3 / max(1, klaunch)
     achieved = 16.0 * S * args.steps / max(1, klaunch) / kern_s / 1e9 if kern_s > 0 else None
+    ev = None
+    if not getattr(args, "no_traffic", True) and klaunch:
+        per = max(1, round(klaunch / args.steps))
+        ev = row_evidence("frz_out_kernel", "c7", kms / 1e3 / args.steps, per_step=per, alg_bytes=16.0 * S)
     return {
         "metric": "samples/s, Freezer<2048>(8, 1) spectral freeze",
         "value": S * args.steps / elapsed, "unit": "samples/s",
@@ -575,7 +638,8 @@ def run_c7(args, torch, dev):
         "data": "synthetic: 0.3 sin(2 pi 440 t) + 0.05 N(0,1) seed 8; freeze at 2 s, unfreeze at 8 s",
         "config": {"workload": "C7 Freezer<2048>(laps 8, width 1) (SURVEY.md 8(f) row 2)", "samples_per_step": S},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK if achieved else None, "traffic": None, "kernel": "frz_out_kernel",
+                     "frac": achieved / HBM_PEAK if achieved else None,
+                     "traffic": (ev or {}).get("traffic_bytes"), "pmc_evidence": ev, "kernel": "frz_out_kernel",
                      "kernel_avg_ms": 1e3 * kern_s, "launches_per_step": klaunch / max(1, args.steps),
                      "whole_step_gbs": 16.0 * S * args.steps / elapsed / 1e9,
                      "note": "16 B per sample over the output kernel's HIP-event time; the step also holds "

@@ -932,6 +932,122 @@ __global__ __launch_bounds__(256) void stft_ola_kernel(OlaArgs a) {
     }
 }
 
+// Overlap-add by segments (fourier.h:153-172, LAPS-specialised). In period c (2N - 1 positions,
+// 2 LAPS slots) the positions r in segment k = [stride k, stride (k + 1)) all read the same slots:
+// slot i <= k from this period's frame at offset r - stride i (live iff k - i < LAPS), slot i > k
+// from the previous period's frame at r + P - stride i (live iff i > k + LAPS, and i = k + LAPS at
+// r = stride k only). So a workgroup owns one segment: the slot list (rows, offsets, shard and Im
+// flags) is decided once, and each thread issues all its samples' loads before the dd sums, which
+// run in the reference's slot order (ascending i). The last N - 1 inputs are carried into the
+// next call's history by the first `aux` workgroups, which also write the zeros before the first
+// frame completes.
+template <int LAPS>
+__global__ __launch_bounds__(256) void stft_ola_seg_kernel(OlaArgs a, long g0, long u_lo, long u_hi, int aux) {
+    constexpr int S = 2 * LAPS;
+    constexpr int SPT = 16 / LAPS;   // samples per thread per round, loads issued together
+    const int N = a.N, stride = a.stride;
+    const long P = 2L * N - 1;
+    const long tb = (long)blockIdx.x;
+    if (tb < aux) {
+        const int N1 = N - 1;
+        const long zp = a.T0 < N1 ? std::min((long)N1, a.T0 + a.n) - a.T0 : 0;   // outputs before any frame
+        for (long j = tb * 256 + threadIdx.x; j < std::max((long)N1, zp); j += (long)aux * 256) {
+            if (j < N1) {
+                const long s = j + a.n;
+                if (s < N1) {
+                    a.hist_new[j] = a.hist_old[s];
+                    a.hist_new[N1 + j] = a.hist_old[N1 + s];
+                } else {
+                    a.hist_new[j] = a.in_re[s - N1];
+                    a.hist_new[N1 + j] = a.in_im ? a.in_im[s - N1] : 0.0;
+                }
+            }
+            if (j < zp) {
+                a.out_re[j] = 0.0;
+                if (a.out_im) a.out_im[j] = 0.0;
+            }
+        }
+        return;
+    }
+    const long g = g0 + (tb - aux);
+    const long c = g / S;
+    const int k = (int)(g - c * S);
+    const long ubase = c * P + (long)stride * k;   // position of the segment's first sample
+    const int seglen = (int)std::min((long)stride, P - (long)stride * k);
+    const int j_lo = (int)std::max(0L, u_lo - ubase);
+    const int j_hi = (int)std::min((long)seglen, u_hi - ubase + 1);
+    // the LAPS live slots for r > stride k, ascending: this period's i = k - ncur + 1 .. k, then the
+    // previous period's i = k + LAPS + 1 .. S - 1
+    const int ncur = k < LAPS - 1 ? k + 1 : LAPS;
+    const long cur0 = (c * S) % a.R, prv0 = c > 0 ? ((c - 1) * S) % a.R : 0;
+    const long plane = (long)a.R * N;
+    long roff[LAPS];
+    int dl[LAPS];
+    bool live[LAPS], imv[LAPS];
+#pragma unroll
+    for (int m = 0; m < LAPS; ++m) {
+        const bool cur = m < ncur;
+        const int i = cur ? k - ncur + 1 + m : k + LAPS + 1 + (m - ncur);
+        const long f = cur ? c * S + i : (c - 1) * S + i;
+        long row = (cur ? cur0 : prv0) + i;
+        if (row >= a.R) row -= a.R;
+        roff[m] = row * N;
+        dl[m] = cur ? stride * (k - i) : (int)(P - (long)stride * (i - k));
+        live[m] = (cur || c > 0) && frame_owned(f, a.sh_block, a.sh_world, a.sh_rank, a.sh_inv);
+        imv[m] = a.out_im != nullptr && f < a.im_zero_from;
+    }
+    const double D = (double)(N * LAPS / 2);   // int expression, fourier.h:174-175
+    const long o0 = ubase + (N - 1) - a.T0;   // output index of the segment's first sample
+    for (int jb = j_lo + (int)threadIdx.x; jb < j_hi; jb += 256 * SPT) {
+        double fr[SPT][LAPS], fi[SPT][LAPS], w[SPT][LAPS];
+#pragma unroll
+        for (int s = 0; s < SPT; ++s) {
+            const int j = jb + 256 * s;
+#pragma unroll
+            for (int m = 0; m < LAPS; ++m) {
+                const bool ok = live[m] && j < j_hi;
+                const int q = j + dl[m];
+                w[s][m] = ok ? a.win[q] : 0.0;
+                fr[s][m] = ok ? a.fo[roff[m] + q] : 0.0;
+                fi[s][m] = ok && imv[m] ? a.fo[plane + roff[m] + q] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < SPT; ++s) {
+            const int j = jb + 256 * s;
+            if (j >= j_hi) break;
+            double rh = 0.0, rl = 0.0, ih = 0.0, il = 0.0;
+#pragma unroll
+            for (int m = 0; m <= LAPS; ++m) {
+                if (j == 0 && m == ncur && k + LAPS < S && c > 0) {
+                    // r = stride k: the previous period's slot k + LAPS at offset N - 1 comes first
+                    const int i = k + LAPS;
+                    const long f = (c - 1) * S + i;
+                    if (frame_owned(f, a.sh_block, a.sh_world, a.sh_rank, a.sh_inv)) {
+                        long row = prv0 + i;
+                        if (row >= a.R) row -= a.R;
+                        const double wv = a.win[N - 1];
+                        hz::dd_add(rh, rl, wv * a.fo[row * N + (N - 1)]);
+                        if (a.out_im && f < a.im_zero_from) hz::dd_add(ih, il, wv * a.fo[plane + row * N + (N - 1)]);
+                    }
+                }
+                if (m < LAPS && live[m]) {
+                    hz::dd_add(rh, rl, w[s][m] * fr[s][m]);
+                    if (imv[m]) hz::dd_add(ih, il, w[s][m] * fi[s][m]);
+                }
+            }
+            double q = rh / D;
+            q += (fma(-q, D, rh) + rl) / D;
+            a.out_re[o0 + j] = q;
+            if (a.out_im) {
+                double qi = ih / D;
+                qi += (fma(-qi, D, ih) + il) / D;
+                a.out_im[o0 + j] = qi;
+            }
+        }
+    }
+}
+
 // ---- Cosine: REDFT10 / REDFT01 via a length-N complex FFT (one workgroup per transform)
 __global__ __launch_bounds__(kThreads) void dct2_kernel(const double* __restrict__ x, double* __restrict__ y, int N,
                                                         int lg, const double2* __restrict__ tw,
@@ -1334,8 +1450,30 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
     o.sh_rank = h->sh_rank;
     o.sh_inv = 1.0 / (double)h->sh_block;
     o.im_zero_from = h->im_zero_from;
-    const long threads = std::max(n, (long)N - 1);
-    hipLaunchKernelGGL(stft_ola_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, o);
+    static const bool ola_flat = std::getenv("HZ_STFT_OLA_FLAT") != nullptr;   // (A/B measurements)
+    if (!ola_flat && (h->laps == 2 || h->laps == 4 || h->laps == 8) && h->stride * h->laps == N) {
+        // segment overlap-add: one workgroup per stride-long segment of the period grid
+        const long P = 2L * N - 1, S = 2L * h->laps;
+        const long u_lo = std::max(h->T - (N - 1), 0L), u_hi = h->T + n - 1 - (N - 1);
+        auto seg = [&](long u) {
+            const long c = u / P;
+            return c * S + (u - c * P) / h->stride;
+        };
+        const long g0 = u_hi >= u_lo ? seg(u_lo) : 0;
+        const long nseg = u_hi >= u_lo ? seg(u_hi) - g0 + 1 : 0;
+        const long zp = h->T < N - 1 ? std::min((long)N - 1, h->T + n) - h->T : 0;
+        const int aux = (int)((std::max((long)N - 1, zp) + 255) / 256);
+        const dim3 grid((unsigned)(aux + nseg));
+        if (h->laps == 2)
+            hipLaunchKernelGGL(stft_ola_seg_kernel<2>, grid, dim3(256), 0, h->stream, o, g0, u_lo, u_hi, aux);
+        else if (h->laps == 4)
+            hipLaunchKernelGGL(stft_ola_seg_kernel<4>, grid, dim3(256), 0, h->stream, o, g0, u_lo, u_hi, aux);
+        else
+            hipLaunchKernelGGL(stft_ola_seg_kernel<8>, grid, dim3(256), 0, h->stream, o, g0, u_lo, u_hi, aux);
+    } else {
+        const long threads = std::max(n, (long)N - 1);
+        hipLaunchKernelGGL(stft_ola_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, o);
+    }
     HZ_TRY_HIP(hipGetLastError());
     if (e) HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
     h->hcur ^= 1;   // the overlap-add launch wrote the next block's history
