@@ -729,7 +729,7 @@ def main():
     elapsed = time.perf_counter() - t0
     # the engine's GPU time per step (roofline): a separate pass of the same steps with HIP events
     # on the handle's stream (no event records inside the timed region above)
-    fb.profile(True)
+    fb.profile(True, repeat=8)   # (modal path: each kernel 8x between its events, per-launch times)
     for _ in range(args.steps):
         step()
     barrier()

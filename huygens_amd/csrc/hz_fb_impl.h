@@ -117,6 +117,11 @@ struct hz_fb {
     // per quintuplet: bit 1 = mix start not recorded (same point as start), bit 3 = reduce
     // start not recorded (same point as mix end); every record costs a few us of GPU time
     std::vector<unsigned char> ev_skip;
+    // per quintuplet: launches per timed kernel between its events (hz_fb_profile(h, rep > 1): the
+    // stationary engine's idempotent kernels repeated back to back, so one event pair's own
+    // latency is spread over rep launches)
+    std::vector<unsigned char> ev_rep;
+    int prof_rep = 1;
     long prof_launches = 0;
     // converged (LTI) path, hz_fb_lti.hip
     int path_mode = HZ_FB_PATH_AUTO;

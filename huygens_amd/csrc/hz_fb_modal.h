@@ -69,6 +69,8 @@ struct ModalArgs {
     int per1, per2;                // residues r1 per phase-1 workgroup, k1 per phase-2 workgroup
     int n1, n2p;                   // phase-1 workgroups (128 / per1), phase-2 DFT workgroups (64 / per2)
     double* out;                   // [N][2]: y[T-1], y[T-2]
+    int first1, n1l;               // the launch's phase-1 (+ exceptional partial) workgroups when they
+                                   // ride in the MAC launch: blockIdx.x in [first1, first1 + n1l)
 };
 
 // (the DFT twiddles are staged in LDS: a global table read inside the MAC loops cost one L2

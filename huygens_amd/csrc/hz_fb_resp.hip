@@ -235,6 +235,10 @@ union RespLds {
     hz_state::StateLds st;
     hz_modal::Lds2 md;
 };
+union ModalLds {
+    hz_modal::Lds1 m1;
+    hz_modal::Lds2 m2;
+};
 union RespFwdLds {
     hz2k::Lds fft;
     hz_modal::Lds1 m1;
@@ -270,12 +274,20 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
                                                        double2* __restrict__ Y, int Q, int Qp, int B,
                                                        hz_modal::ModalArgs md) {
     constexpr int kBinGroups = kH / 256;
-    if (md.on && (int)blockIdx.x >= md.first2) {   // modal band states, phase 2 (hz_fb_modal.h)
-        __shared__ hz_modal::Lds2 l2;
-        const int i = blockIdx.x - md.first2;
-        if (i < md.n2p) hz_modal::phase2_group(md, i, l2);
-        else hz_modal::exc_sum(md);
-        return;
+    if (md.on) {   // modal band states (hz_fb_modal.h): phase 1 and / or phase 2 as extra workgroups
+        __shared__ ModalLds ml;
+        const int i1 = (int)blockIdx.x - md.first1;
+        if (md.n1l && i1 >= 0 && i1 < md.n1l) {
+            if (i1 < md.n1) hz_modal::phase1_group(md, i1, ml.m1);
+            else hz_modal::exc_partial(md, (i1 - md.n1) / md.exc_chunks, (i1 - md.n1) % md.exc_chunks, ml.m2);
+            return;
+        }
+        const int i2 = (int)blockIdx.x - md.first2;
+        if (md.n2 && i2 >= 0 && i2 < md.n2) {
+            if (i2 < md.n2p) hz_modal::phase2_group(md, i2, ml.m2);
+            else hz_modal::exc_sum(md);
+            return;
+        }
     }
     const int q = (blockIdx.x % kBinGroups) * blockDim.x + threadIdx.x;   // bin
     const int b0 = (blockIdx.x / kBinGroups) * R;
@@ -984,7 +996,16 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         // workgroups, 2 no phase 2, 3 no exceptional partials)
         static const int diag = std::getenv("HZ_MODAL_DIAG") ? std::atoi(std::getenv("HZ_MODAL_DIAG")) : 0;
         const int nm1 = !modal || diag == 1 ? 0 : diag == 3 ? md.n1 : md.n1 + md.nexc * md.exc_chunks;
-        hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)(nz + nm1)), dim3(kThreads), 0, h->stream, a, md);
+        // phase 1: extra workgroups of the forward kernel (HZ_MODAL_P1=mac: of the MAC kernel -- A/B)
+        static const char* p1env = std::getenv("HZ_MODAL_P1");
+        static const bool p1mac = p1env && std::string(p1env) == "mac";
+        // profiling with hz_fb_profile(h, rep > 1): each (idempotent) kernel of the modal path launched rep
+        // times between its events
+        const int rep = e && modal ? h->prof_rep : 1;
+        if (e) h->ev_rep[(e - h->ev.data()) / 5] = (unsigned char)rep;
+        for (int r = 0; r < rep; ++r)
+            hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)(nz + (p1mac ? 0 : nm1))), dim3(kThreads), 0,
+                               h->stream, a, md);
         HZ_TRY_HIP(hipGetLastError());
         if (e && inside) {   // profiling: e0..e1 forward, e1..e2 MAC, e2..e4 inverse with the band states
             HZ_TRY_HIP(hipEventRecord(e[1], h->stream));
@@ -996,22 +1017,26 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         static const int p2 = !p2env ? 1 : std::string(p2env) == "mac" ? 0 : std::string(p2env) == "inv_first" ? 2 : 1;
         const int nm2 = !modal || diag == 2 ? 0 : md.n2p + (md.nexc ? 1 : 0);
         hz_modal::ModalArgs mdm = md, mdi = md;
-        mdm.on = modal && p2 == 0;
+        mdm.on = modal && (p2 == 0 || p1mac);
         mdm.first2 = nmac;
-        mdm.n2 = nm2;
+        mdm.n2 = p2 == 0 ? nm2 : 0;
+        mdm.first1 = nmac + mdm.n2;
+        mdm.n1l = modal && p1mac ? nm1 : 0;
         mdi.on = modal && p2 != 0;
         mdi.first2 = p2 == 2 ? 0 : B;
         mdi.n2 = nm2;
-        hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)(nmac + (mdm.on ? nm2 : 0))), dim3(256), 0, h->stream,
-                           (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B, mdm);
+        for (int r = 0; r < rep; ++r)
+            hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)(nmac + (mdm.on ? mdm.n2 + mdm.n1l : 0))), dim3(256), 0,
+                               h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B, mdm);
         HZ_TRY_HIP(hipGetLastError());
         if (e && inside) {
             HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
             h->ev_skip[(e - h->ev.data()) / 5] |= 8;
         }
         RespKernel ki = so == 1 ? resp_inv_kernel<1> : so == 2 ? resp_inv_kernel<2> : resp_inv_kernel<0>;
-        hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0) + (mdi.on ? nm2 : 0))),
-                           dim3(kThreads), 0, h->stream, a, st, mdi);
+        for (int r = 0; r < rep; ++r)
+            hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0) + (mdi.on ? nm2 : 0))),
+                               dim3(kThreads), 0, h->stream, a, st, mdi);
         HZ_TRY_HIP(hipGetLastError());
     }
     if (chained) HZ_TRY(fb_state_combine(h, st, h->stream));   // pieces of a small bank

@@ -700,6 +700,8 @@ int fb_prof_events(hz_fb* h, hipEvent_t** e) {
     *e = &h->ev[h->ev_used];
     h->ev_skip.resize(h->ev.size() / 5);
     h->ev_skip[h->ev_used / 5] = 0;
+    h->ev_rep.resize(h->ev.size() / 5);
+    h->ev_rep[h->ev_used / 5] = 1;
     h->ev_used += 5;
     return HZ_OK;
 }
@@ -1411,6 +1413,7 @@ int hz_fb_profile(hz_fb* h, int enable) {
     HZ_TRY(fb_check(h));
     HZ_TRY_HIP(hipStreamSynchronize(h->stream));
     h->prof = enable != 0;
+    h->prof_rep = enable > 1 ? std::min(enable, 64) : 1;
     h->ev_used = 0;
     h->prof_launches = 0;
     return HZ_OK;
@@ -1429,9 +1432,10 @@ int hz_fb_profile_read(hz_fb* h, double* segment_ms, double* mix_ms, double* red
         if (!(skip & 2)) HZ_TRY_HIP(hipEventElapsedTime(&a, h->ev[i], e1));
         HZ_TRY_HIP(hipEventElapsedTime(&b, e1, h->ev[i + 2]));
         HZ_TRY_HIP(hipEventElapsedTime(&c, e3, h->ev[i + 4]));
-        sg += a;
-        m += b;
-        r += c;
+        const double rep = h->ev_rep.size() > i / 5 ? (double)h->ev_rep[i / 5] : 1.0;
+        sg += a / rep;
+        m += b / rep;
+        r += c / rep;
     }
     if (segment_ms) *segment_ms = sg;
     if (mix_ms) *mix_ms = m;

@@ -160,8 +160,10 @@ class Filterbank:
         b = np.ascontiguousarray(buf, dtype=np.float64)
         check(self._lib.hz_fb_set_state(self._h, dptr(b), len(b)))
 
-    def profile(self, enable: bool):
-        check(self._lib.hz_fb_profile(self._h, 1 if enable else 0))
+    def profile(self, enable: bool, repeat: int = 1):
+        """HIP-event kernel timing; repeat > 1: the stationary engine's modal-path kernels run
+        `repeat` times back to back between their events (times are per launch)"""
+        check(self._lib.hz_fb_profile(self._h, max(1, int(repeat)) if enable else 0))
 
     def profile_read(self):
         """-> (segment pre-pass ms, mix kernel ms, reduce kernel ms, launches)"""

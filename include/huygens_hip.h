@@ -126,7 +126,9 @@ int hz_fb_tune(hz_fb* h, int waves_per_group, int bands_per_wave);
 /* HIP-event timing of the launches of subsequent process calls, on the handle's
  * stream: total ms of the time-segment pre-pass (segment end states + carry;
  * 0 when the bank fills the GPU with bands alone), of the IIR/mixdown kernel,
- * of the cross-group reduce kernel, and the number of process launches. */
+ * of the cross-group reduce kernel, and the number of process launches.
+ * enable > 1 (at most 64): the stationary engine's modal-path kernels run `enable`
+ * times back to back between their events and the times read are per launch. */
 int hz_fb_profile(hz_fb* h, int enable);
 int hz_fb_profile_read(hz_fb* h, double* segment_ms, double* mix_ms, double* reduce_ms, long* launches);
 /* workgroups wanted per launch before time segmentation kicks in (default: CU count) */

@@ -3,7 +3,7 @@
 # kernel) and their kernel-trace summaries, overall and per launch size.  Stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
-OUT=gpurun_out/r5/${TAG:-rows2}
+OUT=gpurun_out/r5/${TAG:-rows2}/rows
 mkdir -p "$OUT"
 for w in ${ROWS:-c3 c4 c5 c6 c7 c8 c9}; do
   echo "== row $w"; date
