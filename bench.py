@@ -725,6 +725,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    t_enq = time.perf_counter() - t0   # host time to issue the steps (launch-bound if ~ elapsed)
     barrier()
     elapsed = time.perf_counter() - t0
     # the engine's GPU time per step (roofline): a separate pass of the same steps with HIP events
@@ -1060,6 +1061,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
+            "host_issue_ms_per_step": 1e3 * t_enq / args.steps,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
