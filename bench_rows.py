@@ -323,10 +323,12 @@ def run_c4(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
     e2, f2, o2, b2, fr2 = out["gate625"]
     traffic, tdetail = None, "not collected (--no-traffic)"
     pmc = None
-    kname = "stft_pair4096_kernel"   # StaticSTFT(4096)'s gate kernel (hz_stft.hip)
+    # StaticSTFT(4096)'s gate kernel (hz_stft.hip): HZ_STFT_FRAME=half (one frame per workgroup) or pair
+    pair = os.environ.get("HZ_STFT_FRAME", "pair") != "half"
+    kname = "stft_pair4096_kernel" if pair else "stft_half4096_kernel"
     if not args.no_traffic and sw == 1:
         import bench
-        tb, tdetail = bench.pmc_traffic((kname, "stft_ola_kernel"), extra=("--workload", "c4"))
+        tb, tdetail = bench.pmc_traffic((kname, "stft_ola_seg_kernel"), extra=("--workload", "c4"))
         traffic = tb   # HBM bytes per launch (one frame launch + one overlap-add launch per step)
         pmc = pmc_counts(kname, "c4", PMC_F64_MFMA)
     return {
@@ -341,10 +343,12 @@ def run_c4(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
         "n_gpus": world, "scaling": "strong", "emulated_world": shard_world,
         "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK if achieved else None,
-                     "traffic": (traffic or {}).get(kname), "traffic_ola": (traffic or {}).get("stft_ola_kernel"),
+                     "traffic": (traffic or {}).get(kname), "traffic_ola": (traffic or {}).get("stft_ola_seg_kernel"),
                      "traffic_detail": tdetail,
-                     "kernel": "stft_pair4096_kernel<STATIC_GATE> (two real frames per transform: window, "
-                               "radix-8 FFT, split + gate + merge, IFFT in LDS)",
+                     "kernel": ("stft_pair4096_kernel<STATIC_GATE> (two real frames per transform: window, "
+                                "radix-8 FFT, split + gate + merge, IFFT in LDS)") if pair else
+                               ("stft_half4096_kernel<STATIC_GATE> (one real frame per workgroup as a 2048-point "
+                                "even/odd transform: window, radix-8/4 FFT, split + gate + merge, IFFT in LDS)"),
                      "kernel_ms_per_step": fms / args.steps, "ola_ms_per_step": oms / args.steps,
                      "flops_per_frame": 491520,
                      "pmc": pmc,

@@ -836,6 +836,310 @@ __global__ __launch_bounds__(p4::kT) void stft_pair4096_kernel(StftArgs a, long 
     }
 }
 
+// ---- N = 4096, one real frame per workgroup (StaticSTFT's gate on real input; C4) ------------------
+// The frame's 4096 real samples as 2048 complex ones, z[n] = w x[2n] + i w x[2n+1] (fourier.h:110-112
+// windowing), so the transform is a 2048-point one on 256 threads (4 waves, 32 KB of LDS): twice the
+// workgroups of the pair kernel at half the size, two or more resident per CU, where the pair kernel
+// ran one 8-wave workgroup per CU and exposed every pass's barrier and LDS round trip.
+//   forward: Z = DFT_M(z), M = N/2; per bin pair (k, M - k): E = (Z_k + conj Z_{M-k}) / 2,
+//            O = (Z_k - conj Z_{M-k}) / 2i, t = W_N^k O, X_k = E + t, X_{M-k} = conj(E - t)
+//            (bins N - k are conj X_k; bin 0 and M from Z_0, bin M/2 = conj Z_{M/2})
+//   gate:    the reference's per-bin test on |X_k|^2 against p0 avg^2 (staticSTFT.h:99-128, or the
+//            gate625 callback), avg over all N bins
+//   inverse: Z''_k = S + V, Z''_{M-k} = conj(S - V), S = X'_k + conj X'_{M-k}, V = i conj(W_N^k)
+//            (X'_k - conj X'_{M-k}); z'' = IDFT_M(Z''), y[2n] + i y[2n+1] = z''[n] (unnormalised, as
+//            FFTW's backward transform; the overlap-add divides)
+// Pass plan: DIF lh 10-9-8 (stride 256), 7-6-5 (32), 4-3-2 (4), 1-0 (radix 4, contiguous); the
+// inverse mirrored. Twiddles W_{8s}^{p r} of a stride-s pass are W_N^{(N/8s) p r} of the N/2 table.
+// The layout p4::lx is conflict-free for every pass (scripts/probe/stft_layout_half.py).
+namespace h4 {
+constexpr int kM = 2048, kLgM = 11, kT = 256, kN = 4096;
+inline size_t lds_bytes() { return sizeof(double2) * kM + sizeof(double) * 16; }
+
+// the last forward pass: stages lh 1, 0 on two radix-4 groups of contiguous elements
+__device__ __forceinline__ void dif4x2(double (&xr)[8], double (&xi)[8]) {
+#pragma unroll
+    for (int g = 0; g < 8; g += 4) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {   // h = 2: the difference times W_4^e
+            const double ar = xr[g + e], ai = xi[g + e], cr = xr[g + e + 2], ci = xi[g + e + 2];
+            const double dr = ar - cr, di = ai - ci;
+            xr[g + e] = ar + cr;
+            xi[g + e] = ai + ci;
+            if (e == 0) {
+                xr[g + 2] = dr;
+                xi[g + 2] = di;
+            } else {   // (dr + i di)(-i)
+                xr[g + 3] = di;
+                xi[g + 3] = -dr;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {   // h = 1
+            const double ar = xr[g + e], ai = xi[g + e], cr = xr[g + e + 1], ci = xi[g + e + 1];
+            xr[g + e] = ar + cr;
+            xi[g + e] = ai + ci;
+            xr[g + e + 1] = ar - cr;
+            xi[g + e + 1] = ai - ci;
+        }
+    }
+}
+
+// the first inverse pass: stages lh 0, 1 (DIT: the second input times conj W_4^e)
+__device__ __forceinline__ void dit4x2(double (&xr)[8], double (&xi)[8]) {
+#pragma unroll
+    for (int g = 0; g < 8; g += 4) {
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {   // h = 1
+            const double ar = xr[g + e], ai = xi[g + e], cr = xr[g + e + 1], ci = xi[g + e + 1];
+            xr[g + e] = ar + cr;
+            xi[g + e] = ai + ci;
+            xr[g + e + 1] = ar - cr;
+            xi[g + e + 1] = ai - ci;
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {   // h = 2
+            double cr = xr[g + e + 2], ci = xi[g + e + 2];
+            if (e == 1) {   // (cr + i ci) i
+                const double t = cr;
+                cr = -ci;
+                ci = t;
+            }
+            const double ar = xr[g + e], ai = xi[g + e];
+            xr[g + e] = ar + cr;
+            xi[g + e] = ai + ci;
+            xr[g + e + 2] = ar - cr;
+            xi[g + e + 2] = ai - ci;
+        }
+    }
+}
+
+// a stride-s pass's stage twiddles for dif8s / dit8s (entries 0, 1, 3 = W_{8s}^{p}, ^{2p}, ^{4p})
+template <int F>   // F = N / (8 s)
+__device__ __forceinline__ void pass_tw(const double2* __restrict__ tw, int p, double2 (&t)[7]) {
+    t[0] = tw[F * p];
+    t[1] = tw[2 * F * p];
+    t[3] = tw[4 * F * p];
+    t[2] = t[4] = t[5] = t[6] = make_double2(1.0, 0.0);
+}
+
+// split, gate and merge over spectrum positions (p4::gate's walk at lg = 11)
+template <int PROC>
+__device__ __forceinline__ void gate(double2* zf, const double2* __restrict__ tw, double p0, double p1,
+                                     double* scratch) {
+#pragma clang fp contract(off)
+    constexpr int kItems = 5;   // 1023 pairs, then u = 1023 (bins 0 and M) and u = 1024 (bin M/2)
+    const int b = threadIdx.x;
+    double er[kItems], ei[kItems], tr[kItems], ti[kItems], wr[kItems], wi[kItems];
+    int ek[kItems], em[kItems], kind[kItems];   // kind 0 pair, 1 bins 0 / M, 2 bin M/2, 3 none
+    double pa = 0.0, la = 0.0;
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        const int u = b + kT * i;
+        kind[i] = u < kM / 2 - 1 ? 0 : u == kM / 2 - 1 ? 1 : u == kM / 2 ? 2 : 3;
+        er[i] = ei[i] = tr[i] = ti[i] = wr[i] = wi[i] = 0.0;
+        ek[i] = em[i] = 0;
+        if (kind[i] == 3) continue;
+        double xa_r, xa_i, xb_r = 0.0, xb_i = 0.0, ca, cb;   // the item's bins and their counts
+        if (kind[i] == 0) {
+            const int q = (u + 1) + p4::hibit(u + 1), qq = q ^ (p4::hibit(q) - 1);
+            const int kq = hz::bitrev(q, kLgM), kqq = hz::bitrev(qq, kLgM);
+            const int k = kq < kqq ? kq : kqq;
+            ek[i] = p4::lx(kq < kqq ? q : qq);
+            em[i] = p4::lx(kq < kqq ? qq : q);
+            const double2 zk = zf[ek[i]], zm = zf[em[i]], w = tw[k];
+            wr[i] = w.x;
+            wi[i] = w.y;
+            er[i] = (zk.x + zm.x) * 0.5;
+            ei[i] = (zk.y - zm.y) * 0.5;
+            const double orr = (zk.y + zm.y) * 0.5, oi = (zm.x - zk.x) * 0.5;
+            tr[i] = w.x * orr - w.y * oi;   // t = W^k O
+            ti[i] = w.x * oi + w.y * orr;
+            xa_r = er[i] + tr[i];   // X_k
+            xa_i = ei[i] + ti[i];
+            xb_r = er[i] - tr[i];   // X_{M-k} = conj(E - t)
+            xb_i = -(ei[i] - ti[i]);
+            ca = cb = 2.0;
+        } else if (kind[i] == 1) {
+            ek[i] = p4::lx(0);
+            const double2 z0 = zf[ek[i]];
+            er[i] = z0.x;   // E_0, O_0
+            tr[i] = z0.y;
+            xa_r = z0.x + z0.y;   // X_0
+            xa_i = 0.0;
+            xb_r = z0.x - z0.y;   // X_M
+            ca = cb = 1.0;
+        } else {
+            ek[i] = p4::lx(1);
+            const double2 zh = zf[ek[i]];
+            xa_r = zh.x;   // X_{M/2} = conj Z_{M/2}
+            xa_i = -zh.y;
+            ca = 2.0;
+            cb = 0.0;
+        }
+        er[i] = kind[i] == 0 ? er[i] : xa_r;   // kinds 1, 2 keep the bins themselves
+        ei[i] = kind[i] == 0 ? ei[i] : xa_i;
+        tr[i] = kind[i] == 0 ? tr[i] : xb_r;
+        ti[i] = kind[i] == 0 ? ti[i] : xb_i;
+        if constexpr (PROC == HZ_PROC_STATIC_GATE) {
+            pa += ca * (sqrt(xa_r * xa_r + xa_i * xa_i) / kN);
+            if (cb != 0.0) pa += cb * (sqrt(xb_r * xb_r + xb_i * xb_i) / kN);
+        } else {
+            const double ha = hypot(xa_r, xa_i), hb = hypot(xb_r, xb_i);
+            hz::dd_add(pa, la, ha);
+            if (ca == 2.0) hz::dd_add(pa, la, ha);
+            if (cb != 0.0) hz::dd_add(pa, la, hb);
+            if (cb == 2.0) hz::dd_add(pa, la, hb);
+        }
+    }
+    double thr;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if constexpr (PROC == HZ_PROC_STATIC_GATE) {   // staticSTFT.h:99-128
+        for (int o = 32; o > 0; o >>= 1) pa += __shfl_xor(pa, o, 64);
+        if (lane == 0) scratch[wave] = pa;
+        __syncthreads();
+        double avg = 0.0;
+        for (int w = 0; w < kT / 64; ++w) avg += scratch[w];
+        thr = p0 * avg * avg;
+    } else {   // tests/spectral.cpp:32-72 (sum / N in long double)
+        for (int o = 32; o > 0; o >>= 1) {
+            const double ah = __shfl_xor(pa, o, 64), al = __shfl_xor(la, o, 64);
+            hz::dd_add(pa, la, ah);
+            hz::dd_add(pa, la, al);
+        }
+        if (lane == 0) {
+            scratch[2 * wave] = pa;
+            scratch[2 * wave + 1] = la;
+        }
+        __syncthreads();
+        pa = la = 0.0;
+        for (int w = 0; w < kT / 64; ++w) {
+            hz::dd_add(pa, la, scratch[2 * w]);
+            hz::dd_add(pa, la, scratch[2 * w + 1]);
+        }
+        const double qa = pa / kN;
+        const double avg = qa + (fma(-qa, (double)kN, pa) + la) / kN;
+        thr = p0 * avg * avg;
+    }
+    auto gated = [&](double& xr, double& xi) {
+        if constexpr (PROC == HZ_PROC_STATIC_GATE) {
+            if (xr * xr + xi * xi < thr) {
+                xr = xr * p1;
+                xi = xi * p1;
+            }
+        } else {
+            if (!(xr * xr + xi * xi > thr)) xr = xi = 0.0;
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < kItems; ++i) {
+        if (kind[i] == 3) continue;
+        if (kind[i] == 0) {
+            double ar = er[i] + tr[i], ai = ei[i] + ti[i];      // X_k
+            double br = er[i] - tr[i], bi = -(ei[i] - ti[i]);   // X_{M-k}
+            gated(ar, ai);
+            gated(br, bi);
+            // S = X'_k + conj X'_{M-k}, D = X'_k - conj X'_{M-k}, V = i conj(W^k) D
+            const double sr = ar + br, si = ai - bi, dr = ar - br, di = ai + bi;
+            const double cr = wr[i] * dr + wi[i] * di, ci = wr[i] * di - wi[i] * dr;   // conj(W^k) D
+            const double vr = -ci, vi = cr;
+            zf[ek[i]] = make_double2(sr + vr, si + vi);
+            zf[em[i]] = make_double2(sr - vr, -(si - vi));
+        } else if (kind[i] == 1) {
+            double ar = er[i], ai = 0.0, br = tr[i], bi = 0.0;
+            gated(ar, ai);
+            gated(br, bi);
+            zf[ek[i]] = make_double2(ar + br, ar - br);
+        } else {
+            double ar = er[i], ai = ei[i];
+            gated(ar, ai);
+            zf[ek[i]] = make_double2(2.0 * ar, -2.0 * ai);
+        }
+    }
+}
+}  // namespace h4
+
+template <int PROC>
+__global__ __launch_bounds__(h4::kT) void stft_half4096_kernel(StftArgs a, long nf) {
+#pragma clang fp contract(off)
+    using namespace h4;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double2* z = (double2*)lds;
+    double* scratch = lds + 2 * kM;
+    const int b = threadIdx.x;
+    double2 twA[7], twB[7], twC[7];
+    pass_tw<2>(a.tw, b, twA);          // stride 256
+    pass_tw<16>(a.tw, b & 31, twB);    // stride 32
+    pass_tw<128>(a.tw, b & 3, twC);    // stride 4
+    const int fl = frame_of_block(blockIdx.x, gridDim.x);
+    long off, row;
+    if (a.sh_world <= 1) {
+        const int tl = 2 * a.laps;
+        const int j0 = a.i0 + fl;
+        const int c0 = j0 / tl;
+        off = a.u0 + (long)c0 * (2 * kN - 1) + (long)a.stride * (j0 - c0 * tl);
+        row = (a.r0 + fl) % a.R;
+    } else {
+        const long f = frame_at(a, fl);
+        off = frame_start(f, a.laps, a.stride, kN) - a.T0 + (kN - 1);
+        row = f % a.R;
+    }
+    (void)nf;
+    double xr[8], xi[8];
+    {   // z[n] = w x[2n] + i w x[2n+1], n = b + 256 j (fourier.h:110-112)
+        double v0[8], v1[8];
+        double2 w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int n = b + kT * j;
+            const long u = off + 2 * n;   // position in [history (N-1) | block input]
+            v0[j] = u < kN - 1 ? a.hr[u] : a.inr[u - (kN - 1)];
+            v1[j] = u + 1 < kN - 1 ? a.hr[u + 1] : a.inr[u + 1 - (kN - 1)];
+            w[j] = ((const double2*)a.win)[n];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            xr[j] = w[j].x * v0[j];
+            xi[j] = w[j].y * v1[j];
+        }
+    }
+    p4::dif8s<false>(xr, xi, twA);   // lh 10, 9, 8
+    p4::lds_put<256>(z, b, xr, xi);
+    __syncthreads();
+    p4::lds_get<32>(z, p4::dif_base<5>(b), xr, xi);
+    p4::dif8s<false>(xr, xi, twB);   // lh 7, 6, 5
+    p4::lds_put<32>(z, p4::dif_base<5>(b), xr, xi);
+    p4::wave_sync();
+    p4::lds_get<4>(z, p4::dif_base<2>(b), xr, xi);
+    p4::dif8s<false>(xr, xi, twC);   // lh 4, 3, 2
+    p4::lds_put<4>(z, p4::dif_base<2>(b), xr, xi);
+    p4::wave_sync();
+    p4::lds_get<1>(z, 8 * b, xr, xi);
+    dif4x2(xr, xi);                  // lh 1, 0
+    p4::lds_put<1>(z, 8 * b, xr, xi);
+    __syncthreads();
+    gate<PROC>(z, a.tw, a.p0, a.p1, scratch);
+    __syncthreads();
+    p4::lds_get<1>(z, 8 * b, xr, xi);
+    dit4x2(xr, xi);                  // lh 0, 1
+    p4::lds_put<1>(z, 8 * b, xr, xi);
+    p4::wave_sync();
+    p4::lds_get<4>(z, p4::dit_base<2>(b), xr, xi);
+    p4::dit8s<false>(xr, xi, twC);   // lh 2, 3, 4
+    p4::lds_put<4>(z, p4::dit_base<2>(b), xr, xi);
+    p4::wave_sync();
+    p4::lds_get<32>(z, p4::dit_base<5>(b), xr, xi);
+    p4::dit8s<false>(xr, xi, twB);   // lh 5, 6, 7
+    p4::lds_put<32>(z, p4::dit_base<5>(b), xr, xi);
+    __syncthreads();
+    p4::lds_get<256>(z, b, xr, xi);
+    p4::dit8s<false>(xr, xi, twA);   // lh 8, 9, 10
+    // natural order z''[b + 256 j] = y[2n] + i y[2n + 1]: straight to the ring's Re plane
+    double2* o = (double2*)(a.fo + row * kN);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[b + kT * j] = make_double2(xr[j], xi[j]);
+}
+
 struct OlaArgs {
     const double* fo;   // planar ring (Re plane, then Im plane of R*N)
     const double* win;
@@ -855,6 +1159,9 @@ struct OlaArgs {
     int sh_world, sh_rank;
     double sh_inv;   // 1 / sh_block
     long im_zero_from;   // frames from here on: Im part 0, not in the ring (hz_stft::im_zero_from)
+    // stft_ola_seg_kernel: the launch's first period and its first ring row, (c_first 2 laps) mod R
+    long c_first;
+    int row_first;
 };
 
 __device__ __forceinline__ bool frame_owned(long f, long block, int world, int rank, double inv) {
@@ -977,11 +1284,15 @@ __global__ __launch_bounds__(256) void stft_ola_seg_kernel(OlaArgs a, long g0, l
     const int j_lo = (int)std::max(0L, u_lo - ubase);
     const int j_hi = (int)std::min((long)seglen, u_hi - ubase + 1);
     // the LAPS live slots for r > stride k, ascending: this period's i = k - ncur + 1 .. k, then the
-    // previous period's i = k + LAPS + 1 .. S - 1
+    // previous period's i = k + LAPS + 1 .. S - 1. Ring rows in 32 bits from the launch's first
+    // period (row_first = (c_first S) mod R on the host; a launch spans < 2^20 / P periods), so no
+    // 64-bit divide runs on the device
     const int ncur = k < LAPS - 1 ? k + 1 : LAPS;
-    const long cur0 = (c * S) % a.R, prv0 = c > 0 ? ((c - 1) * S) % a.R : 0;
-    const long plane = (long)a.R * N;
-    long roff[LAPS];
+    const unsigned R = (unsigned)a.R;
+    const unsigned cur0 = ((unsigned)a.row_first + (unsigned)(c - a.c_first) * S) % R;
+    const unsigned prv0 = cur0 >= (unsigned)S ? cur0 - S : cur0 + R - S;
+    const unsigned plane = R * (unsigned)N;
+    unsigned roff[LAPS];
     int dl[LAPS];
     bool live[LAPS], imv[LAPS];
 #pragma unroll
@@ -989,15 +1300,21 @@ __global__ __launch_bounds__(256) void stft_ola_seg_kernel(OlaArgs a, long g0, l
         const bool cur = m < ncur;
         const int i = cur ? k - ncur + 1 + m : k + LAPS + 1 + (m - ncur);
         const long f = cur ? c * S + i : (c - 1) * S + i;
-        long row = (cur ? cur0 : prv0) + i;
-        if (row >= a.R) row -= a.R;
-        roff[m] = row * N;
+        unsigned row = (cur ? cur0 : prv0) + i;
+        if (row >= R) row -= R;
+        roff[m] = row * (unsigned)N;
         dl[m] = cur ? stride * (k - i) : (int)(P - (long)stride * (i - k));
         live[m] = (cur || c > 0) && frame_owned(f, a.sh_block, a.sh_world, a.sh_rank, a.sh_inv);
         imv[m] = a.out_im != nullptr && f < a.im_zero_from;
     }
-    const double D = (double)(N * LAPS / 2);   // int expression, fourier.h:174-175
+    // D = N LAPS / 2 (an int expression, fourier.h:174-175) is a power of two (N = 2^lg): the
+    // quotients below are the products by 1 / D, bit for bit
+    const double D = (double)(N * LAPS / 2), invD = 1.0 / D;
     const long o0 = ubase + (N - 1) - a.T0;   // output index of the segment's first sample
+    double* __restrict__ ore = a.out_re + o0;
+    double* __restrict__ oim = a.out_im ? a.out_im + o0 : nullptr;
+    const double* __restrict__ fo = a.fo;
+    const double* __restrict__ win = a.win;
     for (int jb = j_lo + (int)threadIdx.x; jb < j_hi; jb += 256 * SPT) {
         double fr[SPT][LAPS], fi[SPT][LAPS], w[SPT][LAPS];
 #pragma unroll
@@ -1006,10 +1323,10 @@ __global__ __launch_bounds__(256) void stft_ola_seg_kernel(OlaArgs a, long g0, l
 #pragma unroll
             for (int m = 0; m < LAPS; ++m) {
                 const bool ok = live[m] && j < j_hi;
-                const int q = j + dl[m];
-                w[s][m] = ok ? a.win[q] : 0.0;
-                fr[s][m] = ok ? a.fo[roff[m] + q] : 0.0;
-                fi[s][m] = ok && imv[m] ? a.fo[plane + roff[m] + q] : 0.0;
+                const unsigned q = (unsigned)(j + dl[m]);
+                w[s][m] = ok ? win[q] : 0.0;
+                fr[s][m] = ok ? fo[roff[m] + q] : 0.0;
+                fi[s][m] = ok && imv[m] ? fo[plane + roff[m] + q] : 0.0;
             }
         }
 #pragma unroll
@@ -1024,11 +1341,11 @@ __global__ __launch_bounds__(256) void stft_ola_seg_kernel(OlaArgs a, long g0, l
                     const int i = k + LAPS;
                     const long f = (c - 1) * S + i;
                     if (frame_owned(f, a.sh_block, a.sh_world, a.sh_rank, a.sh_inv)) {
-                        long row = prv0 + i;
-                        if (row >= a.R) row -= a.R;
-                        const double wv = a.win[N - 1];
-                        hz::dd_add(rh, rl, wv * a.fo[row * N + (N - 1)]);
-                        if (a.out_im && f < a.im_zero_from) hz::dd_add(ih, il, wv * a.fo[plane + row * N + (N - 1)]);
+                        unsigned row = prv0 + i;
+                        if (row >= R) row -= R;
+                        const double wv = win[N - 1];
+                        hz::dd_add(rh, rl, wv * fo[row * (unsigned)N + (N - 1)]);
+                        if (a.out_im && f < a.im_zero_from) hz::dd_add(ih, il, wv * fo[plane + row * (unsigned)N + (N - 1)]);
                     }
                 }
                 if (m < LAPS && live[m]) {
@@ -1036,13 +1353,13 @@ __global__ __launch_bounds__(256) void stft_ola_seg_kernel(OlaArgs a, long g0, l
                     if (imv[m]) hz::dd_add(ih, il, w[s][m] * fi[s][m]);
                 }
             }
-            double q = rh / D;
-            q += (fma(-q, D, rh) + rl) / D;
-            a.out_re[o0 + j] = q;
-            if (a.out_im) {
-                double qi = ih / D;
-                qi += (fma(-qi, D, ih) + il) / D;
-                a.out_im[o0 + j] = qi;
+            double q = rh * invD;
+            q += (fma(-q, D, rh) + rl) * invD;
+            ore[j] = q;
+            if (oim) {
+                double qi = ih * invD;
+                qi += (fma(-qi, D, ih) + il) * invD;
+                oim[j] = qi;
             }
         }
     }
@@ -1276,7 +1593,16 @@ void launch_pairs(hz_stft* h, const StftArgs& a, long nf) {
     // stage-wise form (12): 15.1 vs 14.6 us per C4 step, alternating runs (profiles/r4/rows/c4/ab.log);
     // HZ_STFT_TWIDDLE_ONCE=1 selects it for such A/B runs
     static const bool stagewise = std::getenv("HZ_STFT_TWIDDLE_ONCE") == nullptr;
-    if (h->N == p4::kN && !generic) {
+    // HZ_STFT_FRAME=half: one frame per workgroup (2048-point even/odd transform); pair (default):
+    // two frames per 4096-point transform -- for A/B runs
+    static const bool pair4096 = [] {
+        const char* v = std::getenv("HZ_STFT_FRAME");
+        return !(v && std::strcmp(v, "half") == 0);
+    }();
+    if (h->N == h4::kN && !generic && !pair4096) {
+        hipLaunchKernelGGL((stft_half4096_kernel<PROC>), dim3((unsigned)nf), dim3(h4::kT), h4::lds_bytes(),
+                           h->stream, a, nf);
+    } else if (h->N == p4::kN && !generic) {
         static bool attr4 = false;
         if (!attr4) {
             for (const void* k : {(const void*)stft_pair4096_kernel<PROC, true>, (const void*)stft_pair4096_kernel<PROC, false>})
@@ -1460,10 +1786,19 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
             return c * S + (u - c * P) / h->stride;
         };
         const long g0 = u_hi >= u_lo ? seg(u_lo) : 0;
+        o.c_first = g0 / S;
+        o.row_first = (int)((o.c_first * S) % h->R);
         const long nseg = u_hi >= u_lo ? seg(u_hi) - g0 + 1 : 0;
         const long zp = h->T < N - 1 ? std::min((long)N - 1, h->T + n) - h->T : 0;
         const int aux = (int)((std::max((long)N - 1, zp) + 255) / 256);
         const dim3 grid((unsigned)(aux + nseg));
+        // (diagnostics) HZ_STFT_OLA_REPEAT=r launches the idempotent overlap-add r times: the later
+        // launches show its time with the ring already in the L2s
+        static const int ola_rep = std::max(1, std::getenv("HZ_STFT_OLA_REPEAT") ? std::atoi(std::getenv("HZ_STFT_OLA_REPEAT")) : 1);
+        for (int rep = 1; rep < ola_rep; ++rep) {
+            if (h->laps == 4)
+                hipLaunchKernelGGL(stft_ola_seg_kernel<4>, grid, dim3(256), 0, h->stream, o, g0, u_lo, u_hi, aux);
+        }
         if (h->laps == 2)
             hipLaunchKernelGGL(stft_ola_seg_kernel<2>, grid, dim3(256), 0, h->stream, o, g0, u_lo, u_hi, aux);
         else if (h->laps == 4)
