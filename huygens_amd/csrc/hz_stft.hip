@@ -1248,10 +1248,10 @@ __global__ __launch_bounds__(256) void stft_ola_kernel(OlaArgs a) {
 // run in the reference's slot order (ascending i). The last N - 1 inputs are carried into the
 // next call's history by the first `aux` workgroups, which also write the zeros before the first
 // frame completes.
-template <int LAPS>
+template <int LAPS, int SPLIT>   // SPLIT workgroups per segment
 __global__ __launch_bounds__(256) void stft_ola_seg_kernel(OlaArgs a, long g0, long u_lo, long u_hi, int aux) {
     constexpr int S = 2 * LAPS;
-    constexpr int SPT = 16 / LAPS;   // samples per thread per round, loads issued together
+    constexpr int SPT = 16 / LAPS / SPLIT > 0 ? 16 / LAPS / SPLIT : 1;   // samples per thread per round
     const int N = a.N, stride = a.stride;
     const long P = 2L * N - 1;
     const long tb = (long)blockIdx.x;
@@ -1276,13 +1276,15 @@ __global__ __launch_bounds__(256) void stft_ola_seg_kernel(OlaArgs a, long g0, l
         }
         return;
     }
-    const long g = g0 + (tb - aux);
+    const long g = g0 + (tb - aux) / SPLIT;
+    const int part = (int)((tb - aux) % SPLIT);
     const long c = g / S;
     const int k = (int)(g - c * S);
     const long ubase = c * P + (long)stride * k;   // position of the segment's first sample
     const int seglen = (int)std::min((long)stride, P - (long)stride * k);
-    const int j_lo = (int)std::max(0L, u_lo - ubase);
-    const int j_hi = (int)std::min((long)seglen, u_hi - ubase + 1);
+    const int piece = stride / SPLIT;
+    const int j_lo = (int)std::max((long)part * piece, u_lo - ubase);
+    const int j_hi = (int)std::min((long)(part == SPLIT - 1 ? seglen : (part + 1) * piece), u_hi - ubase + 1);
     // the LAPS live slots for r > stride k, ascending: this period's i = k - ncur + 1 .. k, then the
     // previous period's i = k + LAPS + 1 .. S - 1. Ring rows in 32 bits from the launch's first
     // period (row_first = (c_first S) mod R on the host; a launch spans < 2^20 / P periods), so no
@@ -1791,20 +1793,23 @@ int stft_block(hz_stft* h, const double* d_re, const double* d_im, double* d_ore
         const long nseg = u_hi >= u_lo ? seg(u_hi) - g0 + 1 : 0;
         const long zp = h->T < N - 1 ? std::min((long)N - 1, h->T + n) - h->T : 0;
         const int aux = (int)((std::max((long)N - 1, zp) + 255) / 256);
-        const dim3 grid((unsigned)(aux + nseg));
         // (diagnostics) HZ_STFT_OLA_REPEAT=r launches the idempotent overlap-add r times: the later
         // launches show its time with the ring already in the L2s
         static const int ola_rep = std::max(1, std::getenv("HZ_STFT_OLA_REPEAT") ? std::atoi(std::getenv("HZ_STFT_OLA_REPEAT")) : 1);
-        for (int rep = 1; rep < ola_rep; ++rep) {
-            if (h->laps == 4)
-                hipLaunchKernelGGL(stft_ola_seg_kernel<4>, grid, dim3(256), 0, h->stream, o, g0, u_lo, u_hi, aux);
+        // two workgroups per segment by default (7.4 against 7.8 us per C4 launch, alternating runs,
+        // profiles/r5/c4_half/olasplit.txt); HZ_STFT_OLA_SPLIT=1|2|4 for A/B runs
+        static const int split = [] {
+            const char* v = std::getenv("HZ_STFT_OLA_SPLIT");
+            const int x = v ? std::atoi(v) : 2;
+            return x == 1 || x == 4 ? x : 2;
+        }();
+        const dim3 gridS((unsigned)(aux + split * nseg));
+        for (int rep = 0; rep < ola_rep; ++rep) {
+            auto go = [&](auto kern) { hipLaunchKernelGGL(kern, gridS, dim3(256), 0, h->stream, o, g0, u_lo, u_hi, aux); };
+            if (h->laps == 2) split == 1 ? go(stft_ola_seg_kernel<2, 1>) : split == 2 ? go(stft_ola_seg_kernel<2, 2>) : go(stft_ola_seg_kernel<2, 4>);
+            else if (h->laps == 4) split == 1 ? go(stft_ola_seg_kernel<4, 1>) : split == 2 ? go(stft_ola_seg_kernel<4, 2>) : go(stft_ola_seg_kernel<4, 4>);
+            else split == 1 ? go(stft_ola_seg_kernel<8, 1>) : split == 2 ? go(stft_ola_seg_kernel<8, 2>) : go(stft_ola_seg_kernel<8, 4>);
         }
-        if (h->laps == 2)
-            hipLaunchKernelGGL(stft_ola_seg_kernel<2>, grid, dim3(256), 0, h->stream, o, g0, u_lo, u_hi, aux);
-        else if (h->laps == 4)
-            hipLaunchKernelGGL(stft_ola_seg_kernel<4>, grid, dim3(256), 0, h->stream, o, g0, u_lo, u_hi, aux);
-        else
-            hipLaunchKernelGGL(stft_ola_seg_kernel<8>, grid, dim3(256), 0, h->stream, o, g0, u_lo, u_hi, aux);
     } else {
         const long threads = std::max(n, (long)N - 1);
         hipLaunchKernelGGL(stft_ola_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, h->stream, o);
