@@ -167,8 +167,8 @@ __device__ __forceinline__ void real_window_fwd(hz2k::Lds& s, Load load, const d
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int k = t + i * kThreads, kb = (kH - k) & (kH - 1);
-        const int pa = hz::pad16(hz::bitrev(k, kLgH)), pb = hz::pad16(hz::bitrev(kb, kLgH));
-        const double ar = s.re[pa], ai = s.im[pa], br = s.re[pb], bi = s.im[pb];
+        const double2 za = s.z[hz2k::ix(hz::bitrev(k, kLgH))], zb = s.z[hz2k::ix(hz::bitrev(kb, kLgH))];
+        const double ar = za.x, ai = za.y, br = zb.x, bi = zb.y;
         const double er = 0.5 * (ar + br), ei = 0.5 * (ai - bi);
         const double orr = 0.5 * (ai + bi), oi = -0.5 * (ar - br);
         const double wr = w[i].x * orr - w[i].y * oi, wi = w[i].x * oi + w[i].y * orr;
@@ -177,8 +177,8 @@ __device__ __forceinline__ void real_window_fwd(hz2k::Lds& s, Load load, const d
         else *nyq = er - wr;   // X_kH
     }
     if (t == 0) {   // X_{kH/2} = conj Zh[kH/2] (bit-reversed position 1)
-        const int pm = hz::pad16(1);
-        zrow[kH / 2] = make_double2(s.re[pm], -s.im[pm]);
+        const double2 zm = s.z[hz2k::ix(1)];
+        zrow[kH / 2] = make_double2(zm.x, -zm.y);
     }
     if (stamps) HZ_DIAG_AT(0, 3);
 }
@@ -450,17 +450,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         const double er = ya[i].x + yb[i].x, ei = ya[i].y - yb[i].y;
         const double dr = ya[i].x - yb[i].x, di = ya[i].y + yb[i].y;
         const double orr = dr * w[i].x + di * w[i].y, oi = di * w[i].x - dr * w[i].y;
-        const int pa = hz::pad16(hz::bitrev(k, kLgH)), pb = hz::pad16(hz::bitrev(kb, kLgH));
-        s.re[pa] = er - oi;
-        s.im[pa] = ei + orr;
-        if (k) {
-            s.re[pb] = er + oi;
-            s.im[pb] = orr - ei;
-        }
+        s.z[hz2k::ix(hz::bitrev(k, kLgH))] = make_double2(er - oi, ei + orr);
+        if (k) s.z[hz2k::ix(hz::bitrev(kb, kLgH))] = make_double2(er + oi, orr - ei);
     }
     if (t == 0) {   // Zh'[kH/2] = 2 conj Y[kH/2] (bit-reversed position 1)
-        s.re[hz::pad16(1)] = 2.0 * ym.x;
-        s.im[hz::pad16(1)] = -2.0 * ym.y;
+        s.z[hz2k::ix(1)] = make_double2(2.0 * ym.x, -2.0 * ym.y);
     }
     double vr[kPT], vi[kPT];
     hz2k::inv(s, vr, vi, it);

@@ -23,9 +23,16 @@ namespace hz2k {
 
 constexpr int kLg = 11, kN = 1 << kLg, kT = 256, kPT = kN / kT;
 
+// The transform sits in LDS as interleaved complex (one ds_read_b128 / ds_write_b128 per point) at
+// ix(e) = e ^ ((e >> 3) & 31) ^ ((e >> 8) & 31): conflict-free for every pass of the plan and for
+// the register pass's stride-256 stores, and at most two-way for the caller's split / merge reads
+// at bit-reversed positions (scripts/probe/fft2k_layout.py; the planar layout with one pad per 16
+// it replaces cost ~550 LDS bank-conflict cycles per wave in each of the forward and inverse
+// kernels, rocprofv3 SQ_LDS_BANK_CONFLICT, profiles/r5/c2_sq)
 struct Lds {
-    double re[hz::padded_len(kN)], im[hz::padded_len(kN)];
+    double2 z[kN];
 };
+__device__ __forceinline__ int ix(int e) { return e ^ ((e >> 3) & 31) ^ ((e >> 8) & 31); }
 
 // forward passes 2-4 and inverse passes 1-3 touch only the 512-point block of the group's wave
 // (group b = thread t: block b >> 6 = t >> 6), so between them a wave's own LDS writes need only
@@ -72,16 +79,14 @@ struct Dif {
         double xr[M], xi[M];
 #pragma unroll
         for (int j = 0; j < M; ++j) {
-            const int e = hz::pad16(base + (j << LD));
-            xr[j] = s.re[e];
-            xi[j] = s.im[e];
+            const double2 v = s.z[ix(base + (j << LD))];
+            xr[j] = v.x;
+            xi[j] = v.y;
         }
         regs(xr, xi, w);
 #pragma unroll
         for (int j = 0; j < M; ++j) {
-            const int e = hz::pad16(base + (j << LD));
-            s.re[e] = xr[j];
-            s.im[e] = xi[j];
+            s.z[ix(base + (j << LD))] = make_double2(xr[j], xi[j]);
         }
     }
 };
@@ -120,9 +125,7 @@ __device__ __forceinline__ void fwd(Lds& s, double (&vr)[kPT], double (&vi)[kPT]
     }
 #pragma unroll
     for (int i = 0; i < kPT; ++i) {
-        const int e = hz::pad16(t + kT * i);
-        s.re[e] = vr[i];
-        s.im[e] = vi[i];
+        s.z[ix(t + kT * i)] = make_double2(vr[i], vi[i]);
     }
     __syncthreads();
     Dif<3, 8>::lds(s, t, w.p2);
@@ -167,16 +170,14 @@ struct Dit {
         double xr[M], xi[M];
 #pragma unroll
         for (int j = 0; j < M; ++j) {
-            const int e = hz::pad16(base + (j << LH));
-            xr[j] = s.re[e];
-            xi[j] = s.im[e];
+            const double2 v = s.z[ix(base + (j << LH))];
+            xr[j] = v.x;
+            xi[j] = v.y;
         }
         regs(xr, xi, w);
 #pragma unroll
         for (int j = 0; j < M; ++j) {
-            const int e = hz::pad16(base + (j << LH));
-            s.re[e] = xr[j];
-            s.im[e] = xi[j];
+            s.z[ix(base + (j << LH))] = make_double2(xr[j], xi[j]);
         }
     }
 };
@@ -207,9 +208,9 @@ __device__ __forceinline__ void inv(Lds& s, double (&vr)[kPT], double (&vi)[kPT]
     // pass 4 (R 2, LH 9) on registers: group t = t + 512 j, group t + 256 = t + 256 + 512 j
 #pragma unroll
     for (int i = 0; i < kPT; ++i) {
-        const int e = hz::pad16(t + kT * i);
-        vr[i] = s.re[e];
-        vi[i] = s.im[e];
+        const double2 v = s.z[ix(t + kT * i)];
+        vr[i] = v.x;
+        vi[i] = v.y;
     }
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
