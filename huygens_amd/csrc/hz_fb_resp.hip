@@ -31,6 +31,7 @@
 // rank's run of output blocks with the whole bank's response; DESIGN.md 3.6 and 5.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "hz_fb_impl.h"
@@ -64,7 +65,7 @@ static_assert(kH == hz2k::kN && kThreads == hz2k::kT, "hz_fft2k.h: 2048 points o
 #ifdef HZ_DIAG_STAMPS
 // (diagnostic builds) per-workgroup stamps of the forward [0] and MAC [1] kernels: start, operands
 // arrived, transform / MACs done, end
-__device__ long long g_diag[2][1024][4];
+__device__ long long g_diag[3][1024][4];   // forward, MAC, inverse
 __device__ __forceinline__ void diag_stamp(int k, int i) {
     if (threadIdx.x == 0 && blockIdx.x < 1024) g_diag[k][blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();
 }
@@ -251,9 +252,13 @@ union RespFwdLds {
 __global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a, hz_modal::ModalArgs md) {
     __shared__ RespFwdLds u;
     if (md.on && (int)blockIdx.x >= a.nz) {
+        HZ_DIAG_AT(0, 0);
         const int i = blockIdx.x - a.nz;
         if (i < md.n1) hz_modal::phase1_group(md, i, u.m1);
         else hz_modal::exc_partial(md, (i - md.n1) / md.exc_chunks, (i - md.n1) % md.exc_chunks, u.m2);
+        HZ_DIAG_AT(0, 1);
+        HZ_DIAG_AT(0, 2);
+        HZ_DIAG_AT(0, 3);
         return;
     }
     hz2k::Lds& s = u.fft;
@@ -361,6 +366,103 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
     HZ_DIAG_AT(1, 3);
 }
 
+// The MAC with its operands staged in LDS: a workgroup owns 64 bins x 32 output blocks (a wave per
+// 8 blocks), loads the QP partition spectra and the 32 + QP - 1 window-spectrum rows those blocks
+// read once (80 KB at QP = 24), and each thread runs resp_mac_kernel's register ring (the same
+// FMAs in the same order, so the same bits) from LDS.  The register-only kernel loads every H row
+// once per 8 blocks and every Z row about four times: 55 MB through the L2s per C2 call, which its
+// operand phase waits 3.4 us for (stamps, profiles/r5/diag); here 20 MB.
+constexpr int kMacBins = 64, kMacBlk = 32;
+template <int QP>
+constexpr size_t mac_lds_bytes() { return sizeof(double2) * kMacBins * (QP + kMacBlk + QP - 1); }
+
+template <int QP>
+__global__ __launch_bounds__(256) void resp_mac_lds_kernel(const double2* __restrict__ H, const double2* __restrict__ Z,
+                                                           double2* __restrict__ Y, int Q, int B) {
+    constexpr int kZr = kMacBlk + QP - 1, kHL = QP / 4, kZL = (kZr + 3) / 4;
+    extern __shared__ double2 mac_lds[];
+    double2(*hs)[kMacBins] = (double2(*)[kMacBins])mac_lds;
+    double2(*zs)[kMacBins] = (double2(*)[kMacBins])(mac_lds + QP * kMacBins);
+    const int t = threadIdx.x, lq = t & (kMacBins - 1), sl = t >> 6;
+    const int q = (blockIdx.x % (kH / kMacBins)) * kMacBins + lq;
+    const int b0 = (blockIdx.x / (kH / kMacBins)) * kMacBlk;
+    // Z row of block b, partition p: b + Q - 1 - p = row_lo + (b - b0) + QP - 1 - p; rows < 0 only
+    // for p >= Q (zero H rows), read as row 0
+    const long row_lo = (long)b0 + Q - QP;
+    double2 hv[kHL], zv[kZL];
+#pragma unroll
+    for (int k = 0; k < kHL; ++k) hv[k] = H[(long)(sl + 4 * k) * kH + q];
+#pragma unroll
+    for (int k = 0; k < kZL; ++k) {
+        const int r = sl + 4 * k;
+        const long row = row_lo + r;
+        zv[k] = r < kZr ? Z[(row > 0 ? row : 0) * kH + q] : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int k = 0; k < kHL; ++k) hs[sl + 4 * k][lq] = hv[k];
+#pragma unroll
+    for (int k = 0; k < kZL; ++k)
+        if (sl + 4 * k < kZr) zs[sl + 4 * k][lq] = zv[k];
+    __syncthreads();
+    double ar[8], ai[8], zr[8], zi[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        ar[r] = ai[r] = 0.0;
+        const double2 z = zs[8 * sl + r + QP - 1][lq];
+        zr[r] = z.x;
+        zi[r] = z.y;
+    }
+#pragma unroll
+    for (int p = 0; p < QP; ++p) {
+        const double2 hc = hs[p][lq];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {   // resp_mac_kernel's step: the same FMA order
+            ar[r] = fma(hc.x, zr[r], ar[r]);
+            ar[r] = fma(-hc.y, zi[r], ar[r]);
+            ai[r] = fma(hc.x, zi[r], ai[r]);
+            ai[r] = fma(hc.y, zr[r], ai[r]);
+        }
+        if (p + 1 < QP) {   // step p + 1 reads step p's rows one block down, and one new row
+#pragma unroll
+            for (int r = 7; r > 0; --r) {
+                zr[r] = zr[r - 1];
+                zi[r] = zi[r - 1];
+            }
+            const double2 z = zs[8 * sl + QP - 2 - p][lq];
+            zr[0] = z.x;
+            zi[0] = z.y;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const int b = b0 + 8 * sl + r;
+        if (b < B) Y[(long)b * kH + q] = make_double2(ar[r], ai[r]);
+    }
+}
+
+// HZ_MAC=lds selects the LDS-staged MAC (Qp = 8, 16, 24, no modal phase in the MAC launch);
+// reg (default): the register-only kernel
+bool mac_lds_ok(int Qp, bool modal_in_mac) {
+    static const bool reg = [] {
+        const char* v = std::getenv("HZ_MAC");
+        return !(v && std::strcmp(v, "lds") == 0);
+    }();
+    return !reg && !modal_in_mac && (Qp == 8 || Qp == 16 || Qp == 24);
+}
+void launch_mac_lds(int Qp, int B, const double2* H, const double2* Z, double2* Y, int Q, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)resp_mac_lds_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<8>());
+        (void)hipFuncSetAttribute((const void*)resp_mac_lds_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<16>());
+        (void)hipFuncSetAttribute((const void*)resp_mac_lds_kernel<24>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<24>());
+        attr = true;
+    }
+    const dim3 grid((unsigned)((kH / kMacBins) * ((B + kMacBlk - 1) / kMacBlk)));
+    if (Qp == 8) hipLaunchKernelGGL(resp_mac_lds_kernel<8>, grid, dim3(256), mac_lds_bytes<8>(), s, H, Z, Y, Q, B);
+    else if (Qp == 16) hipLaunchKernelGGL(resp_mac_lds_kernel<16>, grid, dim3(256), mac_lds_bytes<16>(), s, H, Z, Y, Q, B);
+    else hipLaunchKernelGGL(resp_mac_lds_kernel<24>, grid, dim3(256), mac_lds_bytes<24>(), s, H, Z, Y, Q, B);
+}
+
 typedef void (*MacKernel)(const double2*, const double2*, double2*, int, int, int, hz_modal::ModalArgs);
 MacKernel pick_mac(int Qp) {
     switch (Qp) {
@@ -402,8 +504,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     if constexpr (SO == 0) {   // modal band states, phase 2 (hz_fb_modal.h): workgroups [first2, first2 + n2)
         const int i = (int)blockIdx.x - md.first2;
         if (md.on && i >= 0 && i < md.n2) {
+            HZ_DIAG_AT(2, 0);
             if (i < md.n2p) hz_modal::phase2_group(md, i, u.md);
             else hz_modal::exc_sum(md);
+            HZ_DIAG_AT(2, 1);
+            HZ_DIAG_AT(2, 2);
+            HZ_DIAG_AT(2, 3);
             return;
         }
     }
@@ -417,6 +523,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     hz2k::Lds& s = u.fft;
     const int t = threadIdx.x;
     const long b = (long)blockIdx.x - ((SO == 0 && md.on && md.first2 == 0) ? md.n2 : 0);
+    if (SO == 0) HZ_DIAG_AT(2, 0);
 #ifdef HZ_DIAG_STAMPS
     long long* stp = SO > 0 && st.stamps ? st.stamps + ((long)st.G * st.nseg + b) * 4 : nullptr;
     if (stp && t == 0) {
@@ -457,7 +564,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         s.z[hz2k::ix(1)] = make_double2(2.0 * ym.x, -2.0 * ym.y);
     }
     double vr[kPT], vi[kPT];
+    if (SO == 0) HZ_DIAG_AT(2, 1);
     hz2k::inv(s, vr, vi, it);
+    if (SO == 0) HZ_DIAG_AT(2, 2);
     // z[kH/2 + r], r = t + 256 (i - 4): output samples bP + 2r, bP + 2r + 1
 #pragma unroll
     for (int i = kPT / 2; i < kPT; ++i) {
@@ -466,6 +575,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         if (t0 + 1 < a.n_out) a.out[a.off + t0 + 1] = vi[i];
     }
     if (a.upkeep) resp_upkeep(a, b);
+    if (SO == 0) HZ_DIAG_AT(2, 3);
 #ifdef HZ_DIAG_STAMPS
     if (stp && t == 0) stp[1] = stp[2] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -956,6 +1066,8 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     if (modal) modal_args(h, d_in + (n - K), h->d_ystate[h->scur ^ 1], &md);
     const int so = chained ? h->order : 0;
     const int nmac = (kH / 256) * ((B + kMacR - 1) / kMacR);
+    int dg_fx = 0, dg_ix = 0, dg_i0 = 0;   // (diagnostic stamps) modal workgroups per launch
+    (void)dg_fx; (void)dg_ix; (void)dg_i0;
     R.last_engine = col ? 1 : modal ? 2 : 0;
     R.modal_last = modal;
     if (col) {
@@ -1019,14 +1131,21 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         mdi.on = modal && p2 != 0;
         mdi.first2 = p2 == 2 ? 0 : B;
         mdi.n2 = nm2;
-        for (int r = 0; r < rep; ++r)
-            hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)(nmac + (mdm.on ? mdm.n2 + mdm.n1l : 0))), dim3(256), 0,
-                               h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B, mdm);
+        for (int r = 0; r < rep; ++r) {
+            if (mac_lds_ok(Qp, mdm.on))
+                launch_mac_lds(Qp, B, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, h->stream);
+            else
+                hipLaunchKernelGGL(pick_mac(Qp), dim3((unsigned)(nmac + (mdm.on ? mdm.n2 + mdm.n1l : 0))), dim3(256), 0,
+                                   h->stream, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, Qp, B, mdm);
+        }
         HZ_TRY_HIP(hipGetLastError());
         if (e && inside) {
             HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
             h->ev_skip[(e - h->ev.data()) / 5] |= 8;
         }
+        dg_fx = p1mac ? 0 : nm1;
+        dg_ix = mdi.on ? nm2 : 0;
+        dg_i0 = mdi.first2;
         RespKernel ki = so == 1 ? resp_inv_kernel<1> : so == 2 ? resp_inv_kernel<2> : resp_inv_kernel<0>;
         for (int r = 0; r < rep; ++r)
             hipLaunchKernelGGL(ki, dim3((unsigned)(B + (chained ? st.G * st.nseg : 0) + (mdi.on ? nm2 : 0))),
@@ -1057,23 +1176,34 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
                          ph[2] / full, ph[3] / full, smax, emax);
         }
     }
-    if (chained && R.calls == 30) {
-        fb_state_stamps_dump(st, B, R.calls);
-        static long long hv[2][1024][4];
+    if ((chained || modal) && R.calls == 30) {
+        if (chained) fb_state_stamps_dump(st, B, R.calls);
+        static long long hv[3][1024][4];
         if (hipMemcpyFromSymbol(hv, HIP_SYMBOL(g_diag), sizeof(hv)) == hipSuccess) {
-            const int cnt[2] = {std::min((int)nz, 1024), std::min(nmac, 1024)};
-            for (int k = 0; k < 2; ++k) {
+            // workgroups [0, main) run the kernel's own part, the rest (up to 1024) the modal phases
+            const int tot[3] = {std::min((int)nz + dg_fx, 1024), std::min(nmac, 1024), std::min((int)B + dg_ix, 1024)};
+            for (int k = 0; k < 3; ++k) {
                 long long t0 = hv[k][0][0];
-                double ph[3] = {0, 0, 0}, smax = 0, emax = 0;
-                for (int i = 0; i < cnt[k]; ++i) t0 = std::min(t0, hv[k][i][0]);
-                for (int i = 0; i < cnt[k]; ++i) {
-                    for (int j = 0; j < 3; ++j) ph[j] += (hv[k][i][j + 1] - hv[k][i][j]) * 0.01 / cnt[k];
+                for (int i = 0; i < tot[k]; ++i) t0 = std::min(t0, hv[k][i][0]);
+                double ph[3] = {0, 0, 0}, emain = 0, eextra = 0, smax = 0;
+                int nmain = 0, nextra = 0;
+                for (int i = 0; i < tot[k]; ++i) {
+                    const bool extra = k == 0 ? i >= nz : k == 2 ? (dg_i0 == 0 ? i < dg_ix : i >= B) : false;
+                    const double e = (hv[k][i][3] - t0) * 0.01;
                     smax = std::max(smax, (hv[k][i][0] - t0) * 0.01);
-                    emax = std::max(emax, (hv[k][i][3] - t0) * 0.01);
+                    if (extra) {
+                        ++nextra;
+                        eextra = std::max(eextra, e);
+                    } else {
+                        ++nmain;
+                        emain = std::max(emain, e);
+                        for (int j = 0; j < 3; ++j) ph[j] += (hv[k][i][j + 1] - hv[k][i][j]) * 0.01;
+                    }
                 }
                 std::fprintf(stderr, "[%s stamps] %d workgroups: mean operands %.2f us, compute %.2f us, stores %.2f us; "
-                             "starts up to %.2f us, last end %.2f us\n", k ? "mac" : "fwd", cnt[k], ph[0], ph[1], ph[2],
-                             smax, emax);
+                             "starts up to %.2f us, last end %.2f us; %d modal workgroups, last end %.2f us\n",
+                             k == 0 ? "fwd" : k == 1 ? "mac" : "inv", nmain, ph[0] / std::max(nmain, 1),
+                             ph[1] / std::max(nmain, 1), ph[2] / std::max(nmain, 1), smax, emain, nextra, eextra);
             }
         }
     }
