@@ -440,12 +440,13 @@ __global__ __launch_bounds__(256) void resp_mac_lds_kernel(const double2* __rest
     }
 }
 
-// HZ_MAC=lds selects the LDS-staged MAC (Qp = 8, 16, 24, no modal phase in the MAC launch);
-// reg (default): the register-only kernel
+// the LDS-staged MAC for Qp = 8, 16, 24 when no modal phase rides in the MAC launch (C2: 6.1
+// against 7.4 us per launch, step 29.4 against 30.6 us, alternating runs on one box,
+// profiles/r5/mac/summary.txt); HZ_MAC=reg selects the register-only kernel (A/B)
 bool mac_lds_ok(int Qp, bool modal_in_mac) {
     static const bool reg = [] {
         const char* v = std::getenv("HZ_MAC");
-        return !(v && std::strcmp(v, "lds") == 0);
+        return v && std::strcmp(v, "reg") == 0;
     }();
     return !reg && !modal_in_mac && (Qp == 8 || Qp == 16 || Qp == 24);
 }
