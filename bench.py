@@ -993,7 +993,7 @@ def main():
             dom = max(per_k, key=per_k.get)
             dom_name = {"resp_fwd_kernel": "resp_fwd_kernel (window transforms + modal phase 1: the fold and "
                                            "64-point DFTs of the band states)",
-                        "resp_mac_kernel": "resp_mac_kernel<8,%d> (partition MACs)" % (horizon // 2048),
+                        "resp_mac_kernel": "resp_mac_kernel_lds<%d> (partition MACs, operands staged in LDS)" % (horizon // 2048),
                         "resp_inv_kernel": "resp_inv_kernel<0> (inverse transforms of the output blocks + modal "
                                            "phase 2: 128-point DFTs and the band states)"}[dom]
             dom_ms = per_k[dom] / max(1, launches)

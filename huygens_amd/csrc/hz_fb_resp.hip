@@ -377,7 +377,7 @@ template <int QP>
 constexpr size_t mac_lds_bytes() { return sizeof(double2) * kMacBins * (QP + kMacBlk + QP - 1); }
 
 template <int QP>
-__global__ __launch_bounds__(256) void resp_mac_lds_kernel(const double2* __restrict__ H, const double2* __restrict__ Z,
+__global__ __launch_bounds__(256) void resp_mac_kernel_lds(const double2* __restrict__ H, const double2* __restrict__ Z,
                                                            double2* __restrict__ Y, int Q, int B) {
     constexpr int kZr = kMacBlk + QP - 1, kHL = QP / 4, kZL = (kZr + 3) / 4;
     extern __shared__ double2 mac_lds[];
@@ -453,15 +453,15 @@ bool mac_lds_ok(int Qp, bool modal_in_mac) {
 void launch_mac_lds(int Qp, int B, const double2* H, const double2* Z, double2* Y, int Q, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)resp_mac_lds_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<8>());
-        (void)hipFuncSetAttribute((const void*)resp_mac_lds_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<16>());
-        (void)hipFuncSetAttribute((const void*)resp_mac_lds_kernel<24>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<24>());
+        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<8>());
+        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<16>());
+        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<24>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<24>());
         attr = true;
     }
     const dim3 grid((unsigned)((kH / kMacBins) * ((B + kMacBlk - 1) / kMacBlk)));
-    if (Qp == 8) hipLaunchKernelGGL(resp_mac_lds_kernel<8>, grid, dim3(256), mac_lds_bytes<8>(), s, H, Z, Y, Q, B);
-    else if (Qp == 16) hipLaunchKernelGGL(resp_mac_lds_kernel<16>, grid, dim3(256), mac_lds_bytes<16>(), s, H, Z, Y, Q, B);
-    else hipLaunchKernelGGL(resp_mac_lds_kernel<24>, grid, dim3(256), mac_lds_bytes<24>(), s, H, Z, Y, Q, B);
+    if (Qp == 8) hipLaunchKernelGGL(resp_mac_kernel_lds<8>, grid, dim3(256), mac_lds_bytes<8>(), s, H, Z, Y, Q, B);
+    else if (Qp == 16) hipLaunchKernelGGL(resp_mac_kernel_lds<16>, grid, dim3(256), mac_lds_bytes<16>(), s, H, Z, Y, Q, B);
+    else hipLaunchKernelGGL(resp_mac_kernel_lds<24>, grid, dim3(256), mac_lds_bytes<24>(), s, H, Z, Y, Q, B);
 }
 
 typedef void (*MacKernel)(const double2*, const double2*, double2*, int, int, int, hz_modal::ModalArgs);
@@ -1067,8 +1067,8 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     if (modal) modal_args(h, d_in + (n - K), h->d_ystate[h->scur ^ 1], &md);
     const int so = chained ? h->order : 0;
     const int nmac = (kH / 256) * ((B + kMacR - 1) / kMacR);
-    int dg_fx = 0, dg_ix = 0, dg_i0 = 0;   // (diagnostic stamps) modal workgroups per launch
-    (void)dg_fx; (void)dg_ix; (void)dg_i0;
+    int dg_fx = 0, dg_ix = 0, dg_i0 = 0, dg_n1 = 0;   // (diagnostic stamps) modal workgroups per launch
+    (void)dg_fx; (void)dg_ix; (void)dg_i0; (void)dg_n1;
     R.last_engine = col ? 1 : modal ? 2 : 0;
     R.modal_last = modal;
     if (col) {
@@ -1145,6 +1145,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
             h->ev_skip[(e - h->ev.data()) / 5] |= 8;
         }
         dg_fx = p1mac ? 0 : nm1;
+        dg_n1 = md.n1;
         dg_ix = mdi.on ? nm2 : 0;
         dg_i0 = mdi.first2;
         RespKernel ki = so == 1 ? resp_inv_kernel<1> : so == 2 ? resp_inv_kernel<2> : resp_inv_kernel<0>;
@@ -1200,6 +1201,16 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
                         emain = std::max(emain, e);
                         for (int j = 0; j < 3; ++j) ph[j] += (hv[k][i][j + 1] - hv[k][i][j]) * 0.01;
                     }
+                }
+                if (k == 0 && dg_fx > dg_n1) {   // phase-1 residues vs the exceptional bands' partials
+                    double e1 = 0, ex = 0;
+                    for (int i = nz; i < tot[0]; ++i) {
+                        const double e = (hv[0][i][3] - t0) * 0.01;
+                        if (i < nz + dg_n1) e1 = std::max(e1, e);
+                        else ex = std::max(ex, e);
+                    }
+                    std::fprintf(stderr, "[fwd stamps] phase-1 workgroups (%d) last end %.2f us, exceptional partials (%d) last end %.2f us\n",
+                                 dg_n1, e1, dg_fx - dg_n1, ex);
                 }
                 std::fprintf(stderr, "[%s stamps] %d workgroups: mean operands %.2f us, compute %.2f us, stores %.2f us; "
                              "starts up to %.2f us, last end %.2f us; %d modal workgroups, last end %.2f us\n",
