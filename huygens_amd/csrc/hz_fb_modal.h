@@ -35,7 +35,7 @@ namespace hz_modal {
 constexpr int kL = 8192;           // grid / DFT length
 constexpr int kR1 = 128, kR2 = 64; // r = r1 + 128 r2; k = k1 + 64 k2
 constexpr int kMaxExc = 8;         // exceptional bands handled by direct dot products
-constexpr long kExcChunk = 4096;   // samples per exceptional partial (16 per thread, loaded at once)
+constexpr long kExcChunk = 2048;   // samples per exceptional partial (8 per thread, loaded at once)
 constexpr int kThreads = 256;
 constexpr int kPhase1 = kR1;       // phase-1 workgroups (one per r1)
 constexpr int kParts = 4;          // phase-2 workgroups per k1 (16 bins k2 < 64 each)
@@ -152,20 +152,25 @@ __device__ __forceinline__ void exc_partial(const ModalArgs& a, int e, int q, Ld
         s0 = hz_dd::add(s0, hz_dd::two_prod(rv[i], xa[i]));
         s1 = hz_dd::add(s1, hz_dd::two_prod(rv[i], xb[i]));
     }
-    L.part[t][0] = s0;
-    L.part[t][1] = s1;
-    __syncthreads();
-    for (int w = kThreads / 2; w > 0; w >>= 1) {   // tree in a fixed order (a serial walk: ~3 us)
-        if (t < w) {
-            L.part[t][0] = hz_dd::add(L.part[t][0], L.part[t + w][0]);
-            L.part[t][1] = hz_dd::add(L.part[t][1], L.part[t + w][1]);
-        }
-        __syncthreads();
+    // the wave's partials by an xor-shuffle tree, then the four waves in order (lane 0's order is
+    // fixed; the LDS tree this replaces spent eight barriers and left the forward launch's last
+    // workgroups 1.2 us behind its transforms, stamps in profiles/r5/final/stamps.txt)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 = hz_dd::add(s0, dd{__shfl_xor(s0.hi, o, 64), __shfl_xor(s0.lo, o, 64)});
+        s1 = hz_dd::add(s1, dd{__shfl_xor(s1.hi, o, 64), __shfl_xor(s1.lo, o, 64)});
     }
+    if ((t & 63) == 0) {
+        L.part[t >> 6][0] = s0;
+        L.part[t >> 6][1] = s1;
+    }
+    __syncthreads();
     if (t < 2) {
+        dd acc = L.part[0][t];
+        for (int w = 1; w < kThreads / 64; ++w) acc = hz_dd::add(acc, L.part[w][t]);
         double* o = a.exc_part + ((long)e * a.exc_chunks + q) * 4 + 2 * t;
-        o[0] = L.part[0][t].hi;
-        o[1] = L.part[0][t].lo;
+        o[0] = acc.hi;
+        o[1] = acc.lo;
     }
 }
 
