@@ -476,22 +476,48 @@ MacKernel pick_mac(int Qp) {
 typedef void (*RespKernel)(RespArgs, hz_state::StateArgs, hz_modal::ModalArgs);
 
 // history after the call, smoothers' closed form, x history; a time-range shard's zeros outside
-// its range (threads of the B output-block workgroups)
-__device__ __forceinline__ void resp_upkeep(const RespArgs& a, long b) {
+// its range (threads of the B output-block workgroups).  A thread's first element of each is
+// loaded with the transform's operands (UpkeepPre) and stored after the transform, so the tail of
+// the launch waits on no load (stamps: the store phase was 1.3 us with the loads issued there)
+struct UpkeepPre {
+    double h = 0.0, p0 = 0.0, g0 = 0.0, pb = 0.0, gb = 0.0, xh = 0.0;
+};
+__device__ __forceinline__ UpkeepPre resp_upkeep_pre(const RespArgs& a, long b) {
+    UpkeepPre u;
+    const long g = b * blockDim.x + threadIdx.x;
+    if (g < a.K) {
+        const long m = a.n + g;
+        u.h = m < a.K ? a.hist[m] : a.x[m - a.K];
+    }
+    if (g < a.N) {
+        u.p0 = a.pg[2 * g];
+        u.g0 = a.pg[2 * g + 1];
+        u.pb = a.pin[g];
+        u.gb = a.gin[g];
+    }
+    if (g < a.O) u.xh = a.x[a.n - 1 - g];
+    return u;
+}
+__device__ __forceinline__ void resp_upkeep(const RespArgs& a, long b, const UpkeepPre& u) {
     const int t = threadIdx.x;
     const long g = b * blockDim.x + t, stride = (long)a.B * blockDim.x;
     // a time-range shard leaves zeros outside its range: the ranks' outputs sum to the call's
     for (long i = g; i < a.n - a.n_out; i += stride) a.out[i < a.off ? i : i + a.n_out] = 0.0;
-    for (long i = g; i < a.K; i += stride) {
+    if (g < a.K) a.hist_next[g] = u.h;
+    for (long i = g + stride; i < a.K; i += stride) {
         const long m = a.n + i;
         a.hist_next[i] = m < a.K ? a.hist[m] : a.x[m - a.K];
     }
-    for (long n = g; n < a.N; n += stride) {
+    if (g < a.N) {
+        a.pg_next[2 * g] = u.pb + a.sp_n * (u.p0 - u.pb);
+        a.pg_next[2 * g + 1] = u.gb + a.sg_n * (u.g0 - u.gb);
+    }
+    for (long n = g + stride; n < a.N; n += stride) {
         const double P0 = a.pg[2 * n], G0 = a.pg[2 * n + 1], pb = a.pin[n], gb = a.gin[n];
         a.pg_next[2 * n] = pb + a.sp_n * (P0 - pb);
         a.pg_next[2 * n + 1] = gb + a.sg_n * (G0 - gb);
     }
-    if (g < a.O) a.xhist_next[g] = a.x[a.n - 1 - g];
+    if (g < a.O) a.xhist_next[g] = u.xh;
 }
 
 // output block b: the merge of Y_b into Zh' = E' + i O' (E' = Y[k] + conj Y[kH-k],
@@ -544,6 +570,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     const double2 ym = y[kH / 2];
     hz2k::InvTw it;
     it.load(a.tw);
+    const UpkeepPre up = a.upkeep ? resp_upkeep_pre(a, b) : UpkeepPre();
     // bin kH (real): sum_p Hn[p] Zn[b + Q - 1 - p], wave 0 in a fixed order
     double yn = 0.0;
     if (t < 64) {
@@ -575,7 +602,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         if (t0 < a.n_out) a.out[a.off + t0] = vr[i];
         if (t0 + 1 < a.n_out) a.out[a.off + t0 + 1] = vi[i];
     }
-    if (a.upkeep) resp_upkeep(a, b);
+    if (a.upkeep) resp_upkeep(a, b, up);
     if (SO == 0) HZ_DIAG_AT(2, 3);
 #ifdef HZ_DIAG_STAMPS
     if (stp && t == 0) stp[1] = stp[2] = __builtin_amdgcn_s_memrealtime();
@@ -612,8 +639,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         }
     }
     const long b = blockIdx.x;
+    const UpkeepPre up = resp_upkeep_pre(a, b);
     hz_col::comb_block(T, cmap, tw4k, b, u.c, a.out + a.off, a.n_out);
-    resp_upkeep(a, b);
+    resp_upkeep(a, b, up);
 }
 
 
