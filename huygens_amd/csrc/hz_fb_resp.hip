@@ -31,6 +31,7 @@
 // rank's run of output blocks with the whole bank's response; DESIGN.md 3.6 and 5.
 #include <cstdio>
 #include <cstdlib>
+#include <cstdint>
 #include <cstring>
 #include <string>
 
@@ -149,8 +150,9 @@ __device__ __forceinline__ void real_window_fwd(hz2k::Lds& s, Load load, const d
 #pragma unroll
     for (int i = 0; i < kPT; ++i) {
         const int n = t + i * kThreads;
-        vr[i] = load(2 * n);
-        vi[i] = load(2 * n + 1);
+        const double2 v = load(2 * n);   // samples 2n, 2n + 1
+        vr[i] = v.x;
+        vi[i] = v.y;
     }
     hz2k::FwdTw ft;
     ft.load(tw);
@@ -192,7 +194,12 @@ __global__ __launch_bounds__(kThreads) void resp_hspec_kernel(const double* __re
     __shared__ hz2k::Lds s;
     const long p0 = (long)blockIdx.x * kP;
     real_window_fwd(
-        s, [&](int m) { return (m < kP && p0 + m < K) ? h[p0 + m] * (1.0 / kF) : 0.0; }, tw,
+        s,
+        [&](int m) {
+            auto g = [&](int k) { return (k < kP && p0 + k < K) ? h[p0 + k] * (1.0 / kF) : 0.0; };
+            return make_double2(g(m), g(m + 1));
+        },
+        tw,
         H + (long)blockIdx.x * kH, Hn + blockIdx.x);
 }
 
@@ -263,8 +270,20 @@ __global__ __launch_bounds__(kThreads) void resp_fwd_kernel(RespArgs a, hz_modal
     }
     hz2k::Lds& s = u.fft;
     const long m0 = (long)blockIdx.x * kP;
+    // the pair (m, m + 1), m even, lies in one of hist / x (K and off are even): one 16-byte load
+    // when that buffer is 16-byte aligned and the pair is inside the call
+    const bool al = ((reinterpret_cast<uintptr_t>(a.hist) | reinterpret_cast<uintptr_t>(a.x)) & 15) == 0;
     real_window_fwd(
-        s, [&](int m) { return resp_u(a, m0 + m); }, a.tw, a.Z + (long)blockIdx.x * kH, a.Zn + blockIdx.x, true);
+        s,
+        [&](int mm) {
+            const long m = m0 + mm + a.off;
+            if (al) {
+                if (m + 1 < a.K) return *reinterpret_cast<const double2*>(a.hist + m);
+                if (m >= a.K && m + 1 - a.K < a.off + a.n_out) return *reinterpret_cast<const double2*>(a.x + (m - a.K));
+            }
+            return make_double2(resp_u(a, m0 + mm), resp_u(a, m0 + mm + 1));
+        },
+        a.tw, a.Z + (long)blockIdx.x * kH, a.Zn + blockIdx.x, true);
 }
 
 // Y_b[q] = sum_{p < Q} H_p[q] Z_{b+Q-1-p}[q] for b in [b0, b0 + R): thread = bin q x R output
@@ -595,12 +614,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     if (SO == 0) HZ_DIAG_AT(2, 1);
     hz2k::inv(s, vr, vi, it);
     if (SO == 0) HZ_DIAG_AT(2, 2);
-    // z[kH/2 + r], r = t + 256 (i - 4): output samples bP + 2r, bP + 2r + 1
+    // z[kH/2 + r], r = t + 256 (i - 4): output samples bP + 2r, bP + 2r + 1 (one 16-byte store
+    // when the output is 16-byte aligned)
+    const bool oal = (reinterpret_cast<uintptr_t>(a.out + a.off) & 15) == 0;
 #pragma unroll
     for (int i = kPT / 2; i < kPT; ++i) {
         const long t0 = b * kP + 2 * (t + (long)(i - kPT / 2) * kThreads);
-        if (t0 < a.n_out) a.out[a.off + t0] = vr[i];
-        if (t0 + 1 < a.n_out) a.out[a.off + t0 + 1] = vi[i];
+        if (oal && t0 + 1 < a.n_out) {
+            *reinterpret_cast<double2*>(a.out + a.off + t0) = make_double2(vr[i], vi[i]);
+        } else {
+            if (t0 < a.n_out) a.out[a.off + t0] = vr[i];
+            if (t0 + 1 < a.n_out) a.out[a.off + t0 + 1] = vi[i];
+        }
     }
     if (a.upkeep) resp_upkeep(a, b, up);
     if (SO == 0) HZ_DIAG_AT(2, 3);
