@@ -391,14 +391,15 @@ __global__ __launch_bounds__(256) void resp_mac_kernel(const double2* __restrict
 // FMAs in the same order, so the same bits) from LDS.  The register-only kernel loads every H row
 // once per 8 blocks and every Z row about four times: 55 MB through the L2s per C2 call, which its
 // operand phase waits 3.4 us for (stamps, profiles/r5/diag); here 20 MB.
-constexpr int kMacBins = 64, kMacBlk = 32;
-template <int QP>
-constexpr size_t mac_lds_bytes() { return sizeof(double2) * kMacBins * (QP + kMacBlk + QP - 1); }
+constexpr int kMacBins = 64;
+// BPW output blocks per wave, 4 waves: 4 BPW blocks per workgroup
+template <int QP, int BPW>
+constexpr size_t mac_lds_bytes() { return sizeof(double2) * kMacBins * (QP + 4 * BPW + QP - 1); }
 
-template <int QP>
+template <int QP, int BPW>
 __global__ __launch_bounds__(256) void resp_mac_kernel_lds(const double2* __restrict__ H, const double2* __restrict__ Z,
                                                            double2* __restrict__ Y, int Q, int B) {
-    constexpr int kZr = kMacBlk + QP - 1, kHL = QP / 4, kZL = (kZr + 3) / 4;
+    constexpr int kMacBlk = 4 * BPW, kZr = kMacBlk + QP - 1, kHL = QP / 4, kZL = (kZr + 3) / 4;
     extern __shared__ double2 mac_lds[];
     double2(*hs)[kMacBins] = (double2(*)[kMacBins])mac_lds;
     double2(*zs)[kMacBins] = (double2(*)[kMacBins])(mac_lds + QP * kMacBins);
@@ -423,11 +424,11 @@ __global__ __launch_bounds__(256) void resp_mac_kernel_lds(const double2* __rest
     for (int k = 0; k < kZL; ++k)
         if (sl + 4 * k < kZr) zs[sl + 4 * k][lq] = zv[k];
     __syncthreads();
-    double ar[8], ai[8], zr[8], zi[8];
+    double ar[BPW], ai[BPW], zr[BPW], zi[BPW];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < BPW; ++r) {
         ar[r] = ai[r] = 0.0;
-        const double2 z = zs[8 * sl + r + QP - 1][lq];
+        const double2 z = zs[BPW * sl + r + QP - 1][lq];
         zr[r] = z.x;
         zi[r] = z.y;
     }
@@ -435,7 +436,7 @@ __global__ __launch_bounds__(256) void resp_mac_kernel_lds(const double2* __rest
     for (int p = 0; p < QP; ++p) {
         const double2 hc = hs[p][lq];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {   // resp_mac_kernel's step: the same FMA order
+        for (int r = 0; r < BPW; ++r) {   // resp_mac_kernel's step: the same FMA order
             ar[r] = fma(hc.x, zr[r], ar[r]);
             ar[r] = fma(-hc.y, zi[r], ar[r]);
             ai[r] = fma(hc.x, zi[r], ai[r]);
@@ -443,18 +444,18 @@ __global__ __launch_bounds__(256) void resp_mac_kernel_lds(const double2* __rest
         }
         if (p + 1 < QP) {   // step p + 1 reads step p's rows one block down, and one new row
 #pragma unroll
-            for (int r = 7; r > 0; --r) {
+            for (int r = BPW - 1; r > 0; --r) {
                 zr[r] = zr[r - 1];
                 zi[r] = zi[r - 1];
             }
-            const double2 z = zs[8 * sl + QP - 2 - p][lq];
+            const double2 z = zs[BPW * sl + QP - 2 - p][lq];
             zr[0] = z.x;
             zi[0] = z.y;
         }
     }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const int b = b0 + 8 * sl + r;
+    for (int r = 0; r < BPW; ++r) {
+        const int b = b0 + BPW * sl + r;
         if (b < B) Y[(long)b * kH + q] = make_double2(ar[r], ai[r]);
     }
 }
@@ -469,18 +470,26 @@ bool mac_lds_ok(int Qp, bool modal_in_mac) {
     }();
     return !reg && !modal_in_mac && (Qp == 8 || Qp == 16 || Qp == 24);
 }
-void launch_mac_lds(int Qp, int B, const double2* H, const double2* Z, double2* Y, int Q, hipStream_t s) {
+template <int BPW>
+void launch_mac_lds_t(int Qp, int B, const double2* H, const double2* Z, double2* Y, int Q, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<8>());
-        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<16>());
-        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<24>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<24>());
+        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<8, BPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<8, BPW>());
+        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<16, BPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<16, BPW>());
+        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<24, BPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<24, BPW>());
         attr = true;
     }
-    const dim3 grid((unsigned)((kH / kMacBins) * ((B + kMacBlk - 1) / kMacBlk)));
-    if (Qp == 8) hipLaunchKernelGGL(resp_mac_kernel_lds<8>, grid, dim3(256), mac_lds_bytes<8>(), s, H, Z, Y, Q, B);
-    else if (Qp == 16) hipLaunchKernelGGL(resp_mac_kernel_lds<16>, grid, dim3(256), mac_lds_bytes<16>(), s, H, Z, Y, Q, B);
-    else hipLaunchKernelGGL(resp_mac_kernel_lds<24>, grid, dim3(256), mac_lds_bytes<24>(), s, H, Z, Y, Q, B);
+    const dim3 grid((unsigned)((kH / kMacBins) * ((B + 4 * BPW - 1) / (4 * BPW))));
+    if (Qp == 8) hipLaunchKernelGGL((resp_mac_kernel_lds<8, BPW>), grid, dim3(256), (mac_lds_bytes<8, BPW>()), s, H, Z, Y, Q, B);
+    else if (Qp == 16) hipLaunchKernelGGL((resp_mac_kernel_lds<16, BPW>), grid, dim3(256), (mac_lds_bytes<16, BPW>()), s, H, Z, Y, Q, B);
+    else hipLaunchKernelGGL((resp_mac_kernel_lds<24, BPW>), grid, dim3(256), (mac_lds_bytes<24, BPW>()), s, H, Z, Y, Q, B);
+}
+// HZ_MAC_BPW=4: 4 blocks per wave (16 per workgroup, twice the workgroups) -- A/B; measured
+// slower: 8.25 against 6.07 us per C2 launch (profiles/r5/bpw/summary.txt)
+void launch_mac_lds(int Qp, int B, const double2* H, const double2* Z, double2* Y, int Q, hipStream_t s) {
+    static const int bpw = std::getenv("HZ_MAC_BPW") && std::atoi(std::getenv("HZ_MAC_BPW")) == 4 ? 4 : 8;
+    if (bpw == 4) launch_mac_lds_t<4>(Qp, B, H, Z, Y, Q, s);
+    else launch_mac_lds_t<8>(Qp, B, H, Z, Y, Q, s);
 }
 
 typedef void (*MacKernel)(const double2*, const double2*, double2*, int, int, int, hz_modal::ModalArgs);
