@@ -362,30 +362,42 @@ def resp_alg_bytes(K, S, N, O=2, Qp=24):
     return dom, call
 
 
-def modal_kernels(K, S, N, nexc=1):
+def modal_kernels(K, S, N, nexc=1, n_call=None, first=0):
     """Per-kernel (flops, algorithmic bytes) of a stationary call with MODAL band states
-    (hz_fb_modal.h), for the three launches:
+    (hz_fb_modal.h), for the three launches, over a share of S output samples starting at `first`
+    of a call of n_call samples (the whole call at N = 1; a rank's time share at N > 1).  The bytes
+    are SURVEY.md 8(d)'s: the kernel's own inputs and outputs that are NOT engine intermediates --
+    the window spectra Z (forward -> MAC), the output spectra Y (MAC -> inverse) and phase 1's A
+    (forward -> inverse) live only between the engine's own kernels and are not counted:
       * resp_fwd_kernel: the window transforms (Q + B - 1 real 4096-point) + phase 1 (the fold, 2
         flops per window sample and map, and 2 x 128 x 64 x 64 real x complex MACs) + the
-        exceptional direct sums (2 dot products of K in double-double, ~20 flops per term);
-        bytes: the call's input and the K history (8 (S + K)), the window spectra out
-        ((Q + B - 1) rows of 2049 complex) and phase 1's A (2 x 64 x 128 complex);
-      * resp_mac_kernel: B x 2048 x Q complex MACs; bytes: Z and H in, Y out;
+        exceptional direct sums (2 dot products of K in double-double, ~20 flops per term); bytes:
+        the distinct input samples read (the share's windows [first - K, first + S) of [history |
+        call] and phase 1's window, the call's last K inputs) and the exceptional bands' responses;
+      * resp_mac_kernel: B x 2048 x Q complex MACs; bytes: the Q partition spectra H;
       * resp_inv_kernel: the output blocks' inverse transforms + phase 2 (2 x 64 x 128 x 128
-        complex MACs + ~60 flops per band); bytes: Y and A in, the output, the history after the
-        call, the per-band parameters (64 B) and states (16 B) and the smoothers (32 B per band)."""
+        complex MACs + ~60 flops per band); bytes: the output share, the history after the call
+        (the call's last K inputs read, written), the per-band parameters (64 B), states (16 B) and
+        smoothers (32 B per band).
+    Returns {kernel: (flops, bytes)} and, under "call", the whole call's (flops, bytes) with the
+    history's K inputs counted once."""
     H, lgH, P = 2048, 11, 2048
+    n_call = S if n_call is None else n_call
     Q, B = K // P, -(-S // P)
     fft = 5.0 * H * lgH + 10.0 * H
     row = 16 * (H + 1)
-    a_bytes = 2 * 64 * 128 * 16
+    a_lo, a_hi = first - K, first + S               # the share's windows, in call coordinates
+    b_lo, b_hi = n_call - K, n_call                 # phase 1's window
+    inp = (a_hi - a_lo) + (b_hi - b_lo) - max(0, min(a_hi, b_hi) - max(a_lo, b_lo))
     fwd_f = (Q + B - 1) * fft + 4.0 * K + 2 * 128 * 64 * 64 * 4 + nexc * 2 * K * 20.0
-    fwd_b = 8 * (S + K) + (Q + B - 1) * row + a_bytes + nexc * 8 * (K + 1)
+    fwd_b = 8 * inp + nexc * 8 * (K + 1)
     mac_f = B * H * Q * 8.0
-    mac_b = (Q + B - 1) * row + Q * row + B * row
+    mac_b = Q * row
     inv_f = B * fft + 2 * 64 * 128 * 128 * 8.0 + 60.0 * N
-    inv_b = B * row + a_bytes + 8 * S + 8 * K + N * (64 + 16 + 32)
-    return {"resp_fwd_kernel": (fwd_f, fwd_b), "resp_mac_kernel": (mac_f, mac_b), "resp_inv_kernel": (inv_f, inv_b)}
+    inv_b = 8 * S + 8 * K + 8 * K + N * (64 + 16 + 32)
+    out = {"resp_fwd_kernel": (fwd_f, fwd_b), "resp_mac_kernel": (mac_f, mac_b), "resp_inv_kernel": (inv_f, inv_b)}
+    out["call"] = (fwd_f + mac_f + inv_f, fwd_b + mac_b + inv_b - 8 * K)
+    return out
 
 
 def resp_inv_flops(S):
@@ -515,6 +527,58 @@ def torch_empty_like(t):
     return torch.empty_like(t)
 
 
+def emulated_collectives(Filterbank, fwd, back, device):
+    """(--emulate-world P on one GPU) the three host all-reduces of the time split as one process
+    sees them at world P: the sum of the band shards' responses is the whole bank's response (a
+    whole-bank handle's), the max of the shards' horizons the whole bank's horizon (the protocol's
+    0/1 failure flag passes through), the min of the readiness flags this rank's own flag."""
+    full = Filterbank(2, N_BANDS, 0.1, 1.0, device=device)
+    for n in range(N_BANDS):
+        full.coefficients(n, fwd[n], back[n])
+    full.boost(np.ones(N_BANDS))
+    full.open()
+    full.response(8192)
+    K_full = int(full.response_info()[0])
+    h_full = full.response(K_full)
+    full.close()
+    return ((lambda hv: h_full[:len(hv)].copy() if len(hv) <= K_full else np.concatenate([h_full, np.zeros(len(hv) - K_full)])),
+            (lambda k: max(int(k), K_full) if k > 1 else int(k)),
+            (lambda k: int(k)))
+
+
+def c2_setup_time_split(fb, rank, world, coll) -> bool:
+    """Time-split stationary calls (huygens_amd.shard.set_time_shards: the whole bank's response
+    on every rank, this rank's share of the output blocks), with disjoint share-only outputs
+    (hz_fb_set_time_shard_fill(h, 0)).  coll = (all_reduce_sum, all_reduce_max, all_reduce_min)."""
+    from huygens_amd.shard import set_time_shards
+    ok = set_time_shards(fb, rank, world, coll[0], coll[1])
+    if ok:
+        fb.set_time_shard_fill(False)
+    return ok
+
+
+def c2_prime(fb, step, n, tsplit, all_reduce_min, path_response, stop_early=False, armed=None, max_calls=8):
+    """Untimed calls until the engine the run settles on, every decision agreed over the ranks:
+    time split -- after each call every rank asks whether the next call of n samples would be
+    stationary and the handles of ALL ranks are armed in the same call (huygens_amd.shard.
+    arm_when_ready, all-reduce MIN); otherwise -- stop once every rank's last call was stationary
+    (all-reduce MIN of the flag), or after 3 calls for the per-band runs.  `armed` ([bool]) is set
+    when the time split is armed.  Returns the number of priming calls."""
+    from huygens_amd.shard import arm_when_ready
+    for i in range(max_calls):
+        step()
+        if tsplit:
+            if arm_when_ready(fb, n, all_reduce_min):
+                if armed is not None:
+                    armed[0] = True
+                return i + 1
+            continue
+        done = fb.last_path() == path_response or (stop_early and i >= 2)
+        if int(all_reduce_min(1 if done else 0)) == 1:
+            return i + 1
+    return max_calls
+
+
 def launch_plan(gpus: int, env) -> tuple[str, str | None]:
     """What `bench.py --gpus N` does in this environment (no torch / HIP import before it):
     'run' (world matches), 'relaunch' (N > 1 and no launcher: rerun under torch.distributed.run),
@@ -601,7 +665,12 @@ def main():
                     help="timed steps of the side figures (per-band engine, lazy states, band partition)")
     ap.add_argument("--target-groups", type=int, default=0, help="(tuning) workgroups wanted per launch")
     ap.add_argument("--emulate-world", type=int, default=0,
-                    help="(1 GPU, diagnostics) run rank 0's shard of an N-GPU job alone: per-GPU time at N")
+                    help="(1 GPU, diagnostics) run one rank's share of an N-GPU job alone: per-GPU time at N")
+    ap.add_argument("--emulate-rank", type=int, default=-1,
+                    help="(with --emulate-world P) the rank to run (default P - 1: the shard with the "
+                         "exceptional Nyquist band, the heaviest)")
+    ap.add_argument("--band-partition", action="store_true",
+                    help="N > 1: the value path on band shards + RCCL sum-reduce instead of the time split")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "c6", "c7", "c8", "c9"], default="c2",
                     help="c2 = the BASELINE.json metric (default); c3/c4/c5 = the other SURVEY.md 8(d) rows; c6 = Granulator, c7 = Freezer, c8 = heterodyne chain, c9 = per-sample coefficient streams (8(f) rows 1-4)")
     args = ap.parse_args()
@@ -637,9 +706,14 @@ def main():
     from huygens_amd import Filterbank
     from huygens_amd._lib import (HZ_FB_PATH_GENERAL, HZ_FB_PATH_LTI, HZ_FB_PATH_RESPONSE, HZ_FB_PATH_STREAM,
                                   HZ_FB_RESP_EAGER, HZ_FB_RESP_LAZY, HZ_FB_RESP_OFF)
-    from huygens_amd.shard import arm_when_ready, set_time_shards
     fwd, back = c2_coefficients()
-    b0, cnt = shard_of(rank, world) if not args.emulate_world else shard_of(0, args.emulate_world)
+    # the time split's ranks: the real world at N > 1, or (--emulate-world P, one GPU) rank
+    # --emulate-rank of P alone -- its per-rank step time at N = P
+    P = world if world > 1 else max(1, args.emulate_world)
+    r_split = rank if world > 1 else (args.emulate_rank if args.emulate_rank >= 0 else P - 1)
+    if not 0 <= r_split < P:
+        raise SystemExit(f"--emulate-rank {r_split} outside [0, {P})")
+    b0, cnt = shard_of(r_split, P)
     fb = Filterbank(2, N_BANDS, 0.1, 1.0, device=local, shard=(b0, cnt))
     for n in range(b0, b0 + cnt):
         fb.coefficients(n, fwd[n], back[n])
@@ -663,24 +737,48 @@ def main():
     fb.set_stream(stream.cuda_stream)
 
     def ar(v, op):   # all-reduce of one host integer / float over the ranks
+        if world == 1:
+            return v
         t = torch.tensor([v], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=op)
         return t.item()
 
-    # N > 1 (north_star's decomposition, `value`): a FIXED 10 s call per step, the 4096 bands
-    # partitioned over the ranks, each rank's partial mix summed to rank 0 by an RCCL reduce
-    # (src/filterbank.h:130's mixdown sum, sharded).  The reduce of step i runs on the collective
-    # stream while step i + 1 computes into the other output buffer (double-buffered: a buffer is
-    # reused only after its reduce completed, stream-ordered).  The time-split stationary call
-    # (weak scaling) is measured beside it (side.time_split_weak).
-    tshard = False
-    gbuf = None   # ShareGather (--gather: collect the time shares on rank 0 inside the step)
-    armed = False
     S = args.samples
     rng = np.random.default_rng(1234)
     x = torch.from_numpy(rng.uniform(-1, 1, S).astype(np.float32).astype(np.float64)).to(dev)
     ys = [torch.empty_like(x), torch.empty_like(x)]
     y = ys[0]
+
+    # N > 1 (`value`): the FIXED 10 s call of N = 1 split by TIME over the ranks (STRONG scaling).
+    # Once stationary, a call's output depends only on its input and the K inputs before it, so
+    # rank r convolves its run of whole 2048-sample output blocks with the WHOLE bank's response
+    # (the band shards' responses summed by one all-reduce at setup) from the shared input, and
+    # computes its own band shard's states over the call's last K inputs (modal pass).  The shares
+    # are disjoint and final (hz_fb_set_time_shard_fill(h, 0)): no data-path collective in the
+    # step.  side.gather_to_rank0 adds one RCCL gather of the shares per step (1/N of the output
+    # per rank); side.band_partition_* are the band-sharded decompositions with the 3.84 MB RCCL
+    # sum-reduce of the partial mixes (src/filterbank.h:130's mixdown, sharded).
+    if world > 1:
+        def ar_sum(hv):
+            t = torch.from_numpy(np.ascontiguousarray(hv)).to(dev)
+            dist.all_reduce(t)
+            return t.cpu().numpy()
+
+        def ar_max(k):
+            return int(ar(k, dist.ReduceOp.MAX))
+
+        def ar_min(k):
+            return int(ar(k, dist.ReduceOp.MIN))
+        coll = (ar_sum, ar_max, ar_min)
+    elif P > 1:
+        coll = emulated_collectives(Filterbank, fwd, back, local)
+    else:
+        coll = None
+    tsplit = False
+    if coll is not None and not args.general and args.response != 0 and not args.band_partition:
+        tsplit = c2_setup_time_split(fb, r_split, P, coll)
+    share_first, share_count = (fb.time_shard_info(S)[1:] if tsplit else (0, S))
+
     works = [None, None]
     nstep = [0]
 
@@ -691,13 +789,16 @@ def main():
         return dist.reduce(t, dst=0, op=dist.ReduceOp.SUM, async_op=True)
 
     def step():
+        """one step of the value path: time split (no collective) -- or, when the bank cannot run
+        stationary (--general, --response 0, --band-partition), band shards whose partial mixes are
+        summed to rank 0 (double-buffered: a buffer is reused after its reduce completed)"""
         k = nstep[0] & 1
         nstep[0] += 1
-        if works[k] is not None:   # the reduce that last read this buffer (stream-ordered wait)
+        if works[k] is not None:
             works[k].wait()
             works[k] = None
         fb.process_device(x.data_ptr(), ys[k].data_ptr(), S)
-        if world > 1:
+        if world > 1 and not armed[0]:
             works[k] = reduce_async(ys[k])
 
     def drain():
@@ -712,13 +813,14 @@ def main():
         if world > 1:
             dist.barrier()
 
-    # Priming (untimed, before the W warmup steps): calls until the engine the run settles on is
-    # reached -- the smoothers converge during the first 10 s call (k_g = 1 s) and the stationary
-    # engine needs K samples of converged history (each rank decides for its own band shard).
-    for i in range(8):
-        step()
-        if fb.last_path() == HZ_FB_PATH_RESPONSE or (i >= 2 and (args.general or args.response == 0)):
-            break
+    # Priming (untimed, before the W warmup steps): calls until the engine the run settles on --
+    # the smoothers converge during the first 10 s call (k_g = 1 s), the stationary engine needs K
+    # samples of converged history.  Every decision is agreed over the ranks (all-reduce MIN), so
+    # every rank issues the same calls and collectives.
+    armed = [False]
+    primed = c2_prime(fb, step, S, tsplit, coll[2] if coll else (lambda k: k), HZ_FB_PATH_RESPONSE,
+                      stop_early=args.general or args.response == 0, armed=armed)
+    value_split = tsplit and armed[0]   # the value path is the time split (its shares only)
     for _ in range(args.warmup):
         step()
     barrier()
@@ -741,14 +843,13 @@ def main():
     chunk = fb.lti_chunk()   # the timed steps' chunk (the streaming calls below use a shorter one)
     horizon = fb.response_info()[0]
     modal = bool(resp and fb.modal_info()[3])   # band states by the modal pass (hz_fb_modal.h)
+    nexc = max(0, fb.modal_info()[2]) if modal else 0
     fb.profile(False)
 
-    def timed(fn, warm, steps, n_samples, arm=None):
+    def timed(fn, warm, steps, n_samples):
         """ms per step and band-samples/s (whole job, max over ranks) of `fn` after `warm` calls"""
         for _ in range(warm):
             fn()
-            if arm:
-                arm()
         barrier()
         ts = time.perf_counter()
         for _ in range(steps):
@@ -761,69 +862,65 @@ def main():
                 "path": {1: "general", 2: "lti", 3: "response"}.get(fb.last_path(), "?")}
 
     side = {}
+    if tsplit and args.side_steps > 0 and world > 1:
+        # the value path + one gather of the shares to rank 0 per step (1/N of the output per rank,
+        # fixed-size slots; double-buffered: step i + 2 reuses step i's buffer after its gather)
+        from huygens_amd.shard import ShareGather
+        gathers = [ShareGather(S, rank, world, ys[k]) for k in (0, 1)]
+        gworks = [None, None]
+
+        def step_gather():
+            k = nstep[0] & 1
+            nstep[0] += 1
+            if gworks[k] is not None:
+                gworks[k].wait()
+                gathers[k].finish(ys[k])
+                gworks[k] = None
+            fb.process_device(x.data_ptr(), ys[k].data_ptr(), S)
+            w = gathers[k].start(ys[k], dist, async_op=not isinstance(dist, _HostDist))
+            if w is None:   # (rehearsal: the gather ran synchronously through host copies)
+                gathers[k].finish(ys[k])
+            gworks[k] = w
+
+        tg = timed(step_gather, 3, args.side_steps, S)
+        for k in (0, 1):
+            if gworks[k] is not None:
+                gworks[k].wait()
+                gathers[k].finish(ys[k])
+                gworks[k] = None
+        tg["note"] = (f"the value path plus one RCCL gather per step of the {world} disjoint time shares to "
+                      f"rank 0 ({8 * max(c for _, c in gathers[0].shares)} B per rank), overlapped with the next "
+                      "step (double-buffered)")
+        side["gather_to_rank0"] = tg
+    if tsplit and args.side_steps > 0:
+        # the band-partitioned decompositions (north_star's wording; round 5's N > 1 value): every
+        # rank runs its band shard's own engine over the whole call and the partial mixes are summed
+        # to rank 0 (3.84 MB per step)
+        armed[0] = False
+        fb.arm_time_shard(False)
+        fb.set_bank_response(np.zeros(0))   # back to this shard's own response
+        for _ in range(4):
+            step()
+        bp = timed(step, 3, args.side_steps, S)
+        bp["note"] = (f"{cnt} bands per rank through the shard's own stationary engine (its response alone), "
+                      "partial mixes summed to rank 0 by an RCCL reduce per step: every rank redoes the "
+                      "whole convolution")
+        side["band_partition_stationary"] = bp
+        tsplit = False
     if resp and args.side_steps > 0:
         fb.set_response(HZ_FB_RESP_OFF)
         side["per_band_engine"] = timed(step, 3, args.side_steps, S)
-        if world > 1:
-            side["per_band_engine"]["note"] = (f"{N_BANDS} bands over {world} GPUs ({cnt} per GPU), per-band "
+        if P > 1:
+            side["per_band_engine"]["note"] = (f"{N_BANDS} bands over {P} GPUs ({cnt} per GPU), per-band "
                                                "engines, partial mixes reduced to rank 0 (strong scaling)")
         fb.set_response(HZ_FB_RESP_LAZY)
         side["stationary_lazy_states"] = timed(step, 3, args.side_steps, S)
         fb.set_response(HZ_FB_RESP_EAGER if args.response < 0 else args.response)
-        if modal:   # the same eager states by the matrix-core pass (hz_fb_state.h)
+        if modal and P == 1:   # the same eager states by the matrix-core pass (hz_fb_state.h)
             fb.tune_modal(False)
             side["matrix_core_states"] = timed(step, 3, args.side_steps, S)
             fb.tune_modal(True)
         drain()
-    if world > 1 and args.side_steps > 0 and not args.general and args.response != 0:
-        # weak-scaling figure: once stationary, a step is ONE call of N x 10 s split by TIME -- each
-        # rank convolves its run of output blocks with the whole bank's response (the band shards'
-        # responses summed by one all-reduce at setup) from the shared input with a K-sample halo,
-        # and keeps its own bands' states; no data-path collective (--gather collects the shares)
-        def all_reduce_sum(hv):
-            t = torch.from_numpy(np.ascontiguousarray(hv)).to(dev)
-            dist.all_reduce(t)
-            return t.cpu().numpy()
-        barrier()
-        tshard = set_time_shards(fb, rank, world, all_reduce_sum, lambda k: int(ar(k, dist.ReduceOp.MAX)))
-        if tshard:
-            St = S * world
-            xt = torch.from_numpy(np.random.default_rng(4321).uniform(-1, 1, St).astype(np.float32)
-                                  .astype(np.float64)).to(dev)
-            yt = torch.empty_like(xt)
-
-            def step_ts():
-                nonlocal gbuf
-                fb.process_device(xt.data_ptr(), yt.data_ptr(), St)
-                if armed and args.gather:
-                    if gbuf is None:
-                        from huygens_amd.shard import ShareGather
-                        gbuf = ShareGather(St, rank, world, yt)
-                    gbuf(yt, dist)
-                elif not armed:   # (before arming: band shards, partial mixes reduced)
-                    dist.reduce(yt, dst=0, op=dist.ReduceOp.SUM)
-
-            def try_arm():
-                nonlocal armed
-                if not armed:
-                    torch.cuda.synchronize(dev)
-                    armed = arm_when_ready(fb, St, lambda k: int(ar(k, dist.ReduceOp.MIN)))
-            for _ in range(8):
-                step_ts()
-                try_arm()
-                if armed:
-                    break
-            tw = timed(step_ts, 3, args.side_steps, St, arm=try_arm)
-            tw.update(scaling="weak", armed=armed, samples_per_step=St, samples_per_gpu=S,
-                      note=(f"one {world} x 10 s call per step split by time: each GPU outputs its own 10 s of "
-                            f"all {N_BANDS} bands (whole-bank response, K-sample halo), band states sharded; "
-                            "no data-path collective" + (" (+ gather to rank 0)" if args.gather else "")))
-            side["time_split_weak"] = tw
-            armed = False
-            fb.arm_time_shard(False)
-            fb.set_bank_response(np.zeros(0))
-            del xt, yt
-        barrier()
     # the engine's GPU time per call: the event sum (stationary path: forward + MAC kernels, then the
     # inverse kernel carrying the band-state pass)
     eng_ms = seg_ms + mix_ms + red_ms
@@ -979,13 +1076,16 @@ def main():
     value = total_band_samples / elapsed
     if rank == 0:
         launch_avg_s = (eng_ms_max / 1e3) / max(1, launches)    # whole engine step, per process() call
-        out_samples = S                                         # this GPU's outputs per step (its bands)
-        bs_launch = cnt * out_samples                           # band-samples of one call on this GPU
+        # this GPU's outputs per step: its time share (N > 1 / emulated) or the whole call
+        out_samples = share_count if value_split else S
+        # band-samples of one call on this GPU: all bands over its share, or its bands over the call
+        bs_launch = (N_BANDS if value_split else cnt) * out_samples
         # ---- dominant kernel (roofline): the stationary engine's inverse kernel, which carries the
         # band-state pass (hz_fb_state.h: MFMA, ~96% of its flops) beside the output blocks' inverse
         # transforms; the state kernel of the per-band LTI engine; the mix kernel of the general
         # engine -- its average duration from the HIP events around it on the handle's stream
-        mk = modal_kernels(horizon, out_samples, cnt) if modal else None
+        mk = modal_kernels(horizon, out_samples, cnt, nexc=nexc, n_call=S,
+                           first=share_first if value_split else 0) if modal else None
         if modal:
             # the three launches are each one wave of workgroups (latency-bound, intensity 2-5
             # flop/B, under the 9.8 flop/B ridge): the longest one by the events, against HBM
@@ -1032,7 +1132,7 @@ def main():
         achieved = dom_fl / (dom_ms / 1e3) / 1e12 if (dom_fl and dom_ms > 0) else None
         # ---- the whole step: every kernel of a process() call over its whole GPU time
         if modal:
-            step_model = sum(v[0] for v in mk.values())
+            step_model = mk["call"][0]
         elif resp:
             conv_f, state_f = resp_step_flops(horizon, out_samples, cnt)
             step_model = conv_f + state_f
@@ -1042,8 +1142,7 @@ def main():
         # out, the partition spectra, the per-band rows (modal: parameters, states, smoothers; the
         # matrix-core pass: its operand rows) -- not the engine's Z / Y / A intermediates
         if modal:
-            call_bytes = (8 * (out_samples + horizon) + 8 * out_samples + 8 * horizon
-                          + (horizon // 2048) * 16 * 2049 + cnt * (64 + 16 + 32))
+            call_bytes = mk["call"][1]
         elif resp:
             call_bytes = resp_alg_bytes(horizon, out_samples, cnt)[1]
         else:
@@ -1075,18 +1174,35 @@ def main():
                        "partition": 2048 if resp else None,
                        "bands": N_BANDS, "bands_per_gpu": cnt,
                        "parallelism": ("single GPU, all bands, no collective" if world == 1 else
+                                       f"time split x{world}: rank r outputs its run of whole 2048-sample blocks "
+                                       f"of the call ({out_samples} samples on rank 0) for all {N_BANDS} bands from "
+                                       f"the shared input with a {horizon}-sample halo (whole-bank response, one "
+                                       f"all-reduce at setup) and its own {cnt} bands' states; disjoint shares, "
+                                       "no data-path collective" if value_split else
                                        f"bands partitioned x{world} ({cnt} per GPU), partial mixes summed to "
                                        "rank 0 by an RCCL reduce per step (overlapped with the next step's "
                                        "compute, double-buffered)")},
             "rehearsal": (f"{world} ranks on one GPU, collectives over gloo through host copies "
                           "(HZ_BENCH_REHEARSAL=1): the N > 1 code path, not an N-GPU figure")
                          if world > 1 and os.environ.get("HZ_BENCH_REHEARSAL") == "1" else None,
-            "decomposition": None if world == 1 else {
-                "value": (f"STRONG scaling (north_star's decomposition): a FIXED 10 s call per step, "
-                          f"{N_BANDS} bands partitioned over {world} GPUs, each rank's partial mix summed "
-                          "to rank 0 by an RCCL reduce (src/filterbank.h:130's mixdown, sharded)"),
-                "time_split_weak": side.get("time_split_weak") or "not measured (--side-steps 0)",
+            "decomposition": None if P == 1 else {
+                "value": (f"STRONG scaling: the FIXED 10 s call of N = 1 split by time over {P} GPUs; each rank "
+                          "convolves its share of the output blocks with the whole bank's response (a stationary "
+                          "call's output depends only on its input and the K inputs before it) and keeps its band "
+                          "shard's states; shares disjoint and final, no collective in the step" if value_split else
+                          f"STRONG scaling: a FIXED 10 s call per step, {N_BANDS} bands partitioned over {P} GPUs, "
+                          "each rank's partial mix summed to rank 0 by an RCCL reduce (src/filterbank.h:130's "
+                          "mixdown, sharded)"),
+                "gather_to_rank0": side.get("gather_to_rank0"),
+                "band_partition_stationary": side.get("band_partition_stationary"),
+                "latency_floor": ("each rank's step is three dependent launches of one workgroup wave each; at "
+                                  "N = 8 a share is 30 output blocks, so a launch is set by its latency, not its "
+                                  "work: strong scaling is latency-floored near 3 launch latencies (DESIGN.md 5)"),
             },
+            "emulated": ({"world": P, "rank": r_split, "note": (
+                f"ONE GPU running rank {r_split} of {P} alone (--emulate-world): value = the whole job's "
+                "band-samples over THIS rank's step time, i.e. the N-GPU figure if every rank took as long "
+                "(no collective involved)")} if world == 1 and P > 1 else None),
             "engine": "stationary (bank response convolution, eager band states: %s)" % (
                 "modal pass, hz_fb_modal.h" if modal else "matrix-core pass, hz_fb_state.h") if resp
                       else "per-band LTI" if lti else "per-band general",

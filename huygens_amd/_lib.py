@@ -110,6 +110,7 @@ _SIGS = {
     "hz_fb_get_response": (I, [VP, PD, L]),
     "hz_fb_set_bank_response": (I, [VP, PD, L]),
     "hz_fb_set_time_shard": (I, [VP, I, I]),
+    "hz_fb_set_time_shard_fill": (I, [VP, I]),
     "hz_fb_time_shard_info": (I, [VP, C.POINTER(I), C.POINTER(L), C.POINTER(L), L]),
     "hz_fb_stationary_ready": (I, [VP, L, C.POINTER(I)]),
     "hz_fb_arm_time_shard": (I, [VP, I]),

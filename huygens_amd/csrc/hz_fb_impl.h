@@ -174,6 +174,9 @@ struct hz_fb {
         std::vector<double> h_over;
         bool over_valid = false;
         int shard_rank = 0, shard_world = 1;
+        // outside its share a time-sharded call writes zeros (1, default: the ranks' outputs sum to
+        // the call's mix) or leaves the output untouched (0: disjoint shares, nothing to reduce)
+        bool shard_zero = true;
         // a time-sharded handle takes the stationary engine only when the caller has armed it on
         // every rank (hz_fb_arm_time_shard after an all-reduce of hz_fb_stationary_ready), so all
         // ranks switch engines in the same call; cleared by every setter

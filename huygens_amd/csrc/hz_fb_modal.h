@@ -183,6 +183,9 @@ __device__ __forceinline__ void phase2(const ModalArgs& a, int w, Lds2& L) {
     // every global operand is requested before the first barrier: A, the twiddles, this thread's
     // first band (csr entry, then its parameters) and the last inputs
     const int i0 = a.csr_ptr[w], i1 = a.csr_ptr[w + 1];
+    // no band of this shard in the bin range (band shards of a time-sharded bank): nothing to do
+    // (uniform over the workgroup, before its first barrier)
+    if (i0 == i1) return;
     const bool has = i0 + t < i1;
     int2 bk0 = make_int2(0, 0);
     BandPar P0 = BandPar();

@@ -225,6 +225,7 @@ struct RespArgs {
     double* xhist_next;
     int N, O;
     int upkeep;           // 0: a plain convolution (the streaming engine's response tail)
+    int zero_outside;     // time-range shard: zeros outside [off, off + n_out) (hz_fb_set_time_shard_fill)
 };
 
 // u = [hist | x | 0 ...], indexed from the launch's first output block (off)
@@ -529,8 +530,10 @@ __device__ __forceinline__ UpkeepPre resp_upkeep_pre(const RespArgs& a, long b) 
 __device__ __forceinline__ void resp_upkeep(const RespArgs& a, long b, const UpkeepPre& u) {
     const int t = threadIdx.x;
     const long g = b * blockDim.x + t, stride = (long)a.B * blockDim.x;
-    // a time-range shard leaves zeros outside its range: the ranks' outputs sum to the call's
-    for (long i = g; i < a.n - a.n_out; i += stride) a.out[i < a.off ? i : i + a.n_out] = 0.0;
+    // a time-range shard leaves zeros outside its range (the ranks' outputs sum to the call's), or
+    // nothing there (disjoint shares)
+    if (a.zero_outside)
+        for (long i = g; i < a.n - a.n_out; i += stride) a.out[i < a.off ? i : i + a.n_out] = 0.0;
     if (g < a.K) a.hist_next[g] = u.h;
     for (long i = g + stride; i < a.K; i += stride) {
         const long m = a.n + i;
@@ -826,7 +829,9 @@ int modal_prepare(hz_fb* h) {
     R.modal_ok = false;
     const long K = R.K;
     const int N = h->N;
-    if (h->order != 2 || K < kL || K % kL != 0 || N <= 0 || R.over_valid) return HZ_OK;
+    // (time-range shards qualify too: every rank has the whole call's input, so its own bands'
+    // states over the call's last K inputs come out of the same fold and DFT)
+    if (h->order != 2 || K < kL || K % kL != 0 || N <= 0) return HZ_OK;
     const long double pi = 3.141592653589793238462643383279502884L;
     std::vector<BandPar> par((size_t)N);
     std::vector<int> exc;
@@ -1112,6 +1117,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.O = h->order;
     a.nz = nz;
     a.upkeep = 1;
+    a.zero_outside = R.shard_zero ? 1 : 0;
     // EAGER, n >= K: the band states after the call are the zero-start states over the call's last
     // K samples, independent of the convolution: the state pass runs as extra workgroups of the
     // inverse kernel (orders <= 2: 256 registers; prefetching its operands into the XCDs' L2 from the
@@ -1353,6 +1359,7 @@ int fb_resp_tail_conv(hz_fb* h, const double* u, long n, double* out, hipStream_
     a.Hn = S.d_tH + (size_t)Qp * 2 * kH;
     a.out = out;
     a.upkeep = 0;
+    a.zero_outside = 0;
     hipLaunchKernelGGL(resp_fwd_kernel, dim3((unsigned)nz), dim3(kThreads), 0, st, a, hz_modal::ModalArgs());
     HZ_TRY_HIP(hipGetLastError());
     const int nmac = (kH / 256) * ((B + kMacR - 1) / kMacR);
@@ -1432,6 +1439,12 @@ int hz_fb_set_time_shard(hz_fb* h, int rank, int world) {
     h->resp.shard_rank = rank;
     h->resp.shard_world = world;
     h->resp.armed = false;
+    return HZ_OK;
+}
+
+int hz_fb_set_time_shard_fill(hz_fb* h, int zero_outside) {
+    if (!h) return HZ_E_INVALID;
+    h->resp.shard_zero = zero_outside != 0;
     return HZ_OK;
 }
 

@@ -253,6 +253,11 @@ class Filterbank:
     def set_time_shard(self, rank: int, world: int):
         check(self._lib.hz_fb_set_time_shard(self._h, int(rank), int(world)))
 
+    def set_time_shard_fill(self, zero_outside: bool = True):
+        """zero_outside: zeros outside this rank's share (the ranks' outputs sum to the mix);
+        False: the share only, the rest of the output untouched (disjoint shares)."""
+        check(self._lib.hz_fb_set_time_shard_fill(self._h, 1 if zero_outside else 0))
+
     def stationary_ready(self, n: int) -> bool:
         """Would a call of n samples run stationary on this handle (ignoring arming)?"""
         r = C.c_int()
@@ -288,6 +293,8 @@ def sample_many(banks, x, dist: int = HZ_DIST_NONE, param: float = 0.0) -> np.nd
     lib = banks[0]._lib
     hs = (C.c_void_p * n)(*[b._h for b in banks])
     xs = np.ascontiguousarray(x, dtype=np.float64)
+    if xs.shape != (n,):
+        raise ValueError(f"sample_many: x must hold one value per bank ({n}), got shape {xs.shape}")
     ys = np.empty(n)
     check(lib.hz_fb_sample_many(hs, n, xs.ctypes.data_as(PD), int(dist), float(param), ys.ctypes.data_as(PD)))
     return ys

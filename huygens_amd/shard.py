@@ -89,9 +89,19 @@ class ShareGather:
         self.bufs = [torch.empty_like(self.buf) for _ in range(world)] if rank == 0 else None
 
     def __call__(self, y, dist):
+        self.start(y, dist)
+        self.finish(y)
+
+    def start(self, y, dist, async_op=False):
+        """copy this rank's share into the slot and issue the gather (async_op: returns its work
+        handle; call finish(y) after it completed)"""
         f, c = self.shares[self.rank]
         self.buf[:c].copy_(y[f:f + c])
-        dist.gather(self.buf, self.bufs, dst=0)
+        return dist.gather(self.buf, self.bufs, dst=0, async_op=async_op) if async_op else \
+            dist.gather(self.buf, self.bufs, dst=0)
+
+    def finish(self, y):
+        """(rank 0) the gathered slots into place in y"""
         if self.rank == 0:
             for (f, c), b in zip(self.shares, self.bufs):
                 y[f:f + c].copy_(b[:c])

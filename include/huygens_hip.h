@@ -198,6 +198,11 @@ int hz_fb_get_response(hz_fb* h, double* out, long count);
  * response; count 0 clears it explicitly.  Without it a call outputs all samples of its own bands. */
 int hz_fb_set_bank_response(hz_fb* h, const double* resp, long count);
 int hz_fb_set_time_shard(hz_fb* h, int rank, int world);
+/* zero_outside = 1 (default): a time-sharded stationary call writes zeros outside its share, so the
+ * ranks' outputs sum (one reduce) to the call's mix; 0: it leaves the rest of the output untouched --
+ * the shares are disjoint and final, nothing to reduce (bench.py N > 1: no data-path collective;
+ * huygens_amd.shard.ShareGather collects them on one rank with 1/world of the output per rank). */
+int hz_fb_set_time_shard_fill(hz_fb* h, int zero_outside);
 /* The engine choice of time-sharded handles is collective: such a handle runs its per-band
  * engines (band-shard partial mixes) until the caller arms it, and runs stationary exactly when
  * armed -- an armed handle whose call cannot be stationary returns HZ_E_STATE instead of

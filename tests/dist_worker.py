@@ -162,6 +162,98 @@ def _shard_protocol(rank, world, variant):
     return res
 
 
+class FakeC2Handle(FakeShardHandle):
+    """Stands in for the C2 Filterbank shard in bench.py's N > 1 value path (bench.c2_setup_time_split,
+    bench.c2_prime, the share-only step): before arming, a call writes its own bands' partial mix over
+    the whole call (here (rank + 1) x); once armed, the WHOLE bank's output (here sum over ranks of
+    (r + 1) x) on this rank's time share only, leaving the rest of the buffer untouched."""
+
+    def __init__(self, rank, world, K, ready_after):
+        super().__init__(rank, K, ready_after)
+        self.world, self.fill = world, True
+
+    def set_time_shard_fill(self, zero_outside=True):
+        self.fill = bool(zero_outside)
+
+    def time_shard_info(self, n):
+        from huygens_amd.shard import time_share
+        f, c = time_share(self.shard[0], self.shard[1], n)
+        return True, f, c
+
+    def process_device(self, xp, yp, n):
+        import ctypes
+        x = np.ctypeslib.as_array((ctypes.c_double * n).from_address(xp)).copy()
+        y = np.ctypeslib.as_array((ctypes.c_double * n).from_address(yp))
+        self.call()
+        if self.armed:
+            _, f, c = self.time_shard_info(n)
+            whole = sum(r + 1 for r in range(self.world)) * x
+            if self.fill:
+                y[:] = 0.0
+            y[f:f + c] = whole[f:f + c]
+        else:
+            y[:] = (self.rank + 1) * x
+
+    def last_path(self):
+        return 3 if self.armed else 2
+
+
+def _c2_split(rank, world):
+    """bench.py's N > 1 C2 value path through its real helpers over gloo: c2_setup_time_split (the
+    whole-bank response and the share-only fill on every rank), c2_prime (ranks ready after
+    different numbers of calls are armed in the same call), the share-only steps (no collective),
+    and ShareGather.start / finish (side.gather_to_rank0) assembling the whole call on rank 0."""
+    import torch
+    import torch.distributed as dist
+    import bench
+    from huygens_amd.shard import ShareGather
+
+    def ar_sum(a):
+        t = torch.from_numpy(np.array(a, dtype=np.float64))
+        dist.all_reduce(t)
+        return t.numpy()
+
+    def ar_op(op):
+        def f(k):
+            t = torch.tensor([int(k)], dtype=torch.int64)
+            dist.all_reduce(t, op=op)
+            return int(t.item())
+        return f
+    coll = (ar_sum, ar_op(dist.ReduceOp.MAX), ar_op(dist.ReduceOp.MIN))
+    fb = FakeC2Handle(rank, world, 8192 * (rank + 1), ready_after=1 + 2 * rank)
+    ok = bench.c2_setup_time_split(fb, rank, world, coll)
+    n = 100000
+    x = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, n))
+    y = torch.full((n,), 7.0, dtype=torch.float64)
+    armed = [False]
+    reduces = [0]
+
+    def step():
+        fb.process_device(x.data_ptr(), y.data_ptr(), n)
+        if not armed[0]:   # (band shards before arming: partial mixes reduced, as bench.step)
+            t = y.clone()
+            dist.reduce(t, dst=0)
+            reduces[0] += 1
+    calls = bench.c2_prime(fb, step, n, ok, coll[2], 3, armed=armed)
+    before = y.clone()
+    y.fill_(7.0)
+    step()                                   # an armed (timed) step: the share only, no collective
+    _, f, c = fb.time_shard_info(n)
+    whole = sum(r + 1 for r in range(world)) * x
+    res = {"ok": ok, "fill": fb.fill, "armed": armed[0], "calls": calls, "reduces": reduces[0],
+           "log": fb.log, "share": [f, c],
+           "share_err": float(torch.max(torch.abs(y[f:f + c] - whole[f:f + c])).item()),
+           "outside_untouched": bool(torch.all(torch.cat([y[:f], y[f + c:]]) == 7.0).item()),
+           "before_armed_partial": float(torch.max(torch.abs(before - (rank + 1) * x)).item())}
+    g = ShareGather(n, rank, world, y)
+    w = g.start(y, dist, async_op=True)
+    w.wait()
+    g.finish(y)
+    if rank == 0:
+        res["gather_err"] = float(torch.max(torch.abs(y - whole)).item())
+    return res
+
+
 class FakeAdditive:
     """Stands in for huygens_amd.Additive in bench_rows.run_c3 on a CPU device: fill_device writes
     the shard's partial mix y[t] = sum over its overtones o of cos(1e-3 (o + 1) t), t the handle's
@@ -265,6 +357,13 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     if kind.startswith("row:"):
         res = _row(kind.split(":")[1], rank, world, dist)
+        with open(f"{out_path}.{rank}", "w") as fh:
+            json.dump(res, fh)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    if kind == "c2split":
+        res = _c2_split(rank, world)
         with open(f"{out_path}.{rank}", "w") as fh:
             json.dump(res, fh)
         dist.barrier()

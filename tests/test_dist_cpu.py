@@ -33,7 +33,7 @@ def _run(kind, world, tmp_path):
     for p in procs:
         o, _ = p.communicate(timeout=240)
         assert p.returncode == 0, o.decode()[-2000:]
-    if kind.startswith(("protocol", "row:")):
+    if kind.startswith(("protocol", "row:", "c2split")):
         return [json.loads((tmp_path / f"{kind}.json.{r}").read_text()) for r in range(world)]
     return json.loads(out.read_text())
 
@@ -110,3 +110,24 @@ def test_bench_row_reduce_world2(row, tmp_path):
     assert [r["n_gpus"] for r in res] == [2, 2]
     assert res[0]["ms"] == res[1]["ms"]          # max over ranks on both
     assert res[0]["err"] < 1e-12
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c2_time_split_value_path(world, tmp_path):
+    """bench.py's N > 1 C2 value path through its real helpers over gloo:
+    every rank arms in the same call although the ranks are ready after different numbers of
+    calls (the priming decision agrees across ranks), every rank issues the same
+    number of reduces before arming and none after, an armed step writes the whole bank's output
+    on the rank's share only (share-only fill, the rest untouched: no collective), and the shares
+    gathered to rank 0 (side.gather_to_rank0) are the whole call."""
+    res = _run("c2split", world, tmp_path)
+    for r, rr in enumerate(res):
+        assert rr["ok"] is True and rr["fill"] is False and rr["armed"] is True
+        assert rr["calls"] == 1 + 2 * (world - 1)          # the slowest rank's readiness
+        assert rr["reduces"] == rr["calls"]                # same collectives on every rank
+        assert rr["share_err"] == 0.0 and rr["outside_untouched"]
+        assert rr["before_armed_partial"] == 0.0
+    assert all(rr["log"] == res[0]["log"] for rr in res)
+    shares = [rr["share"] for rr in res]
+    assert shares[0][0] == 0 and sum(c for _, c in shares) == 100000
+    assert res[0]["gather_err"] == 0.0

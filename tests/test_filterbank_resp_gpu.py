@@ -362,3 +362,74 @@ def test_column_split_vs_three_kernel(gpu_lib, R, centre, order):
     if K // 2048 in (8, 16, 24):
         assert col_calls >= 3, (K, col_calls)
     print("horizon", K, "column-split calls", col_calls)
+
+
+@pytest.mark.parametrize("fill", [True, False])
+def test_time_range_shards_modal(gpu_lib, fill):
+    """The N > 1 value path of bench.py on one device: band shards of a bank
+    on one pole circle at grid angles (the C2 recipe with N = 512: m = 8 (i + 1), the last band the
+    Nyquist double pole) time-split with the whole bank's response.  Their band states come from
+    the MODAL pass (hz_fb_modal.h, now allowed under time shards: every rank holds the whole call's
+    input), equal to the restatement's; fill=True: zeros outside each share, outputs summing to the
+    mix; fill=False (hz_fb_set_time_shard_fill(h, 0)): each share written, the rest untouched, the
+    shares assembled by range equal to the mix.  The shard without any band in a phase-2 bin range
+    skips it (early exit): states still exact."""
+    import torch
+    from huygens_amd import Filterbank
+    from huygens_amd.shard import set_time_shards
+    L = paths()
+    N, O = 512, 2
+    fwd, back = resonant_coefficients(N, 0.999, 1.0)
+    _, o = make(2, N, fwd, back, oracle=True)
+    cuts = [(0, 200), (200, 256), (456, 56)]
+    shards = []
+    for b0, cnt in cuts:
+        s = Filterbank(2, N, 0.001, 0.001, shard=(b0, cnt))
+        s.tune_response(0, 1)
+        for n in range(N):
+            s.coefficients(n, fwd[n], back[n])
+        s.boost(np.ones(N))
+        s.open()
+        shards.append(s)
+    for s in shards:
+        s.response(8192)
+    K_all = max(s.response_info()[0] for s in shards)
+    full = sum(s.response(K_all) for s in shards)
+    for r, s in enumerate(shards):
+        assert set_time_shards(s, r, 3, lambda h, full=full: full, lambda k, K_all=K_all: K_all if k > 1 else k)
+        s.set_time_shard_fill(fill)
+    rng = np.random.default_rng(12)
+    modal_calls = 0
+    for n in [60000, 60000, 70001, 52000, 100003]:
+        ready = all(s.stationary_ready(n) for s in shards)
+        for s in shards:
+            s.arm_time_shard(ready)
+        x = rng.uniform(-1, 1, n)
+        ref = o.process(x)
+        outs = []
+        xd = torch.from_numpy(x).cuda()
+        for s in shards:   # device buffers (process_device): the untouched samples are observable
+            yd = torch.full((n,), 7.0, dtype=torch.float64, device="cuda")
+            s.process_device(xd.data_ptr(), yd.data_ptr(), n)
+            s.synchronize()
+            outs.append(yd.cpu().numpy())
+        if shards[0].last_path() == L.HZ_FB_PATH_RESPONSE:
+            assert all(s.modal_info()[3] for s in shards), [s.modal_info() for s in shards]
+            modal_calls += 1
+            if fill:
+                got = sum(outs)
+            else:
+                got = np.zeros(n)
+                for s, y in zip(shards, outs):
+                    _, f, c = s.time_shard_info(n)
+                    assert np.all(y[:f] == 7.0) and np.all(y[f + c:] == 7.0)   # outside: untouched
+                    got[f:f + c] = y[f:f + c]
+        else:
+            got = sum(outs)
+        assert rel_err(got, ref) < TOL, n
+        st = o.get_state()
+        for (b0, cnt), s in zip(cuts, shards):
+            gs = s.get_state()
+            assert states_close(gs[O:O + cnt * O], st[O + b0 * O:O + (b0 + cnt) * O]), (n, b0)
+    assert modal_calls >= 2
+    assert shards[2].modal_info()[2] == 1 and shards[0].modal_info()[2] == 0   # the Nyquist band: shard 2
