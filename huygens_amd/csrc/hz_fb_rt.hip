@@ -312,7 +312,9 @@ struct ManyCache {
 static ManyCache g_many[64];
 static std::mutex g_many_mu;
 
-static int many_table(int device, hz_fb* const* hs, int H, int* nchunks, const hz_rt::ManyChunk** d) {
+// *changed: the table differs from the last group's -- a member's chunks move to other workgroups
+// (the chunk -> workgroup map follows the group's order and size), so the caller quiesces the server
+static int many_table(int device, hz_fb* const* hs, int H, int* nchunks, const hz_rt::ManyChunk** d, bool* changed) {
     std::vector<hz_rt::ManyChunk> ch;
     for (int m = 0; m < H; ++m) {
         hz_fb* h = hs[m];
@@ -350,6 +352,7 @@ static int many_table(int device, hz_fb* const* hs, int H, int* nchunks, const h
     }
     *nchunks = (int)C.chunks.size();
     *d = C.d;
+    *changed = !same;
     return HZ_OK;
 }
 
@@ -422,10 +425,14 @@ static int sample_many_locked(hz_fb* const* hs, int H, const double* x, int dist
     }
     int nch = 0;
     const hz_rt::ManyChunk* d = nullptr;
+    bool changed = false;
     {
         std::lock_guard<std::mutex> lk(g_many_mu);
-        HZ_TRY(many_table(dev, hs, H, &nch, &d));
+        HZ_TRY(many_table(dev, hs, H, &nch, &d, &changed));
     }
+    // another group (other members, order or size) than the last request's: its band rows were
+    // served by other workgroups, possibly on another XCD -- a kernel boundary first
+    if (changed && !fresh) hz_rt::quiesce(srv);
     const int groups = std::max(1, std::min(hz_rt::kGroups, (nch + hz_rt::kThreads / 64 - 1) / (hz_rt::kThreads / 64)));
     double* res = hz_rt::result(srv, (size_t)hz_rt::kGroups * hz_rt::kMaxMany);
     if (!res) return HZ_E_ALLOC;

@@ -427,6 +427,43 @@ def test_sample_many_multichannel(gpu_lib):
     assert np.median(lat) < 20.8e-6, np.median(lat)
 
 
+def test_sample_many_changing_groups(gpu_lib):
+    """OP_FB_MANY maps a member's 64-band chunks onto workgroups by the group's order
+    and size, so alternating groups of different sizes and orders over the same handles moves a
+    handle's band rows between workgroups (and XCDs); the server is quiesced whenever the chunk
+    table changes.  Every sample against the restatement per handle; a short x is refused."""
+    from huygens_amd import Filterbank, sample_many
+    from huygens_amd._lib import HZ_DIST_SOFTCLIP
+    H, N = 6, 200
+    fwd, back = resonant_coefficients(N, 0.999, 1.0)
+    gs, os_ = [], []
+    for k in range(H):
+        g, o = Filterbank(2, N), OracleFilterbank(2, N)
+        for fb in (g, o):
+            for n in range(N):
+                fb.coefficients(n, fwd[n], back[n])
+            fb.boost(np.full(N, 1.0 + 0.2 * k))
+            fb.open()
+        o.distortion(HZ_DIST_SOFTCLIP, 0.0)
+        gs.append(g)
+        os_.append(o)
+    rng = np.random.default_rng(29)
+    groups = [list(range(6)), [0, 1, 2, 3], [5, 4, 3, 2, 1, 0], [2], [1, 3, 5], list(range(6)), [4, 0]]
+    worst = 0.0
+    for t in range(700):
+        grp = groups[(t // 7) % len(groups)] if t < 350 else groups[t % len(groups)]
+        v = rng.uniform(-1, 1, len(grp))
+        yg = sample_many([gs[k] for k in grp], v, HZ_DIST_SOFTCLIP, 0.0)
+        yo = np.array([os_[k](v[i]) for i, k in enumerate(grp)])
+        for k in grp:
+            gs[k].tick()
+            os_[k].tick()
+        worst = max(worst, float(np.max(np.abs(yg - yo) / np.maximum(1e-30, np.abs(yo)))))
+    assert worst < 1e-8, worst
+    with pytest.raises(ValueError):
+        sample_many(gs[:3], np.zeros(2), HZ_DIST_SOFTCLIP, 0.0)
+
+
 def test_sample_many_cpp_multichannel(gpu_lib, tmp_path):
     """The C++ drop-in (tests/cpp/multichannel.cpp): 8 x FFilterbank<double,864,2> with softclip,
     one soundmath::sample_many call per frame (the one-line change to tests/filterbanks.cpp's loop);
