@@ -184,7 +184,7 @@ def per_sample_rates(device, samples=12000):
     xs8 = rng.uniform(-1, 1, (samples // 4 + 500, 8))
 
     def stm(i):   # tests/filterbanks.cpp:191-211: 8 channels, &softclip, one request per frame
-        sample_many(fbs, xs8[i % len(xs8)], HZ_DIST_SOFTCLIP, 0.0)
+        sample_many(fbs, xs8[i % len(xs8)], HZ_DIST_SOFTCLIP)   # &softclip: width 0.125
         for fb in fbs:
             fb.tick()
     timed("filterbank_8x864_sample_many_softclip", stm, n=samples // 4, frames=1,
@@ -425,7 +425,8 @@ def pmc_pass(counters, kernels, extra=(), per_step=None):
     d = tempfile.mkdtemp(prefix="hz_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     cmd = [exe, "--pmc", *counters, "--kernel-trace", "-d", d, "-o", "pmc", "--output-format", "csv",
            "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "3",
-           "--no-cpu-baseline", "--stream-blocks", "0", "--no-traffic", "--side-steps", "0", *extra]
+           "--no-cpu-baseline", "--stream-blocks", "0", "--no-traffic", "--side-steps", "0", "--no-per-sample",
+           "--no-general-side", *extra]
     try:
         subprocess.run(cmd, check=True, capture_output=True, timeout=300,
                        env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
@@ -579,6 +580,82 @@ def c2_prime(fb, step, n, tsplit, all_reduce_min, path_response, stop_early=Fals
     return max_calls
 
 
+def general_softclip_figures(Filterbank, device, stream, x, y, S, traffic=True, steps=10):
+    """The general engine (hz_filterbank.hip fb_mix_kernel) on the reference demos' own calls:
+    F(x, &softclip) with the one-argument softclip (width 0.125, tests/filterbank.cpp:158-171,
+    200-215) -- a distortion functor keeps every call off the converged engines.  4096 bands (the
+    C2 bank, k_p = 0.1, k_g = 1) and the demo's FFilterbank<double, 864, 2> (k_p = 0.001, k_g = 1,
+    tests/filterbank.cpp:191), each on 480,000-sample calls and 1024-sample calls.  frac = the
+    reference recurrence's 18 flops per band-sample over the mix kernel's event
+    time, against the FP64 peak; PMC executed flops and HBM bytes of fb_mix_kernel from child
+    rocprofv3 passes (bench.py --dist softclip)."""
+    import torch
+    from huygens_amd._lib import HZ_DIST_SOFTCLIP
+    out = {}
+    B = 1024
+    for N, kp, name in ((N_BANDS, 0.1, "c2_4096_bands"), (864, 0.001, "ffilterbank_864_bands")):
+        fwd, back = c2_coefficients(N=N)
+        fb = Filterbank(2, N, kp, 1.0, device=device)
+        for n in range(N):
+            fb.coefficients(n, fwd[n], back[n])
+        fb.boost(np.ones(N))
+        fb.open()
+        fb.distortion(HZ_DIST_SOFTCLIP)
+        fb.set_stream(stream.cuda_stream)
+
+        def long_call():
+            fb.process_device(x.data_ptr(), y.data_ptr(), S)
+        for _ in range(2):
+            long_call()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            long_call()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        fb.profile(True)
+        for _ in range(steps):
+            long_call()
+        torch.cuda.synchronize()
+        seg_ms, mix_ms, red_ms, launches = fb.profile_read()
+        fb.profile(False)
+        mix_avg = mix_ms / max(1, launches) / 1e3
+        ref_fl = FLOPS_PER_BAND_SAMPLE * N * S
+        rec = {"long_calls": {"ms_per_call": 1e3 * dt, "band_samples_per_s": N * S / dt,
+                              "mix_kernel_ms": 1e3 * mix_avg, "reduce_kernel_ms": red_ms / max(1, launches),
+                              "frac_18_flops": ref_fl / mix_avg / 1e12 / FP64_PEAK_TFLOPS if mix_avg > 0 else None,
+                              "path": {1: "general"}.get(fb.last_path(), str(fb.last_path()))}}
+        nb = min(469, S // B)
+
+        def blocks(k):
+            for i in range(k):
+                fb.process_device(x.data_ptr() + 8 * B * i, y.data_ptr() + 8 * B * i, B)
+        blocks(16)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        blocks(nb)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        rec["blocks_1024"] = {"us_per_block": 1e6 * dt / nb, "band_samples_per_s": N * B * nb / dt,
+                              "path": {1: "general"}.get(fb.last_path(), str(fb.last_path()))}
+        fb.close()
+        out[name] = rec
+    if traffic:
+        tr, _ = pmc_traffic(("fb_mix_kernel", "fb_reduce"), ["--dist", "softclip"])
+        fl, _ = pmc_flops(("fb_mix_kernel",), ["--dist", "softclip"])
+        mix_ms = out["c2_4096_bands"]["long_calls"]["mix_kernel_ms"]
+        out["pmc_c2_4096"] = {
+            "fb_mix_kernel_bytes": tr.get("fb_mix_kernel") if tr else None,
+            "fb_reduce_bytes": tr.get("fb_reduce") if tr else None,
+            "fb_mix_kernel_flops": fl.get("fb_mix_kernel") if fl else None,
+            "executed_tflops": (fl["fb_mix_kernel"] / (mix_ms / 1e3) / 1e12) if (fl and mix_ms) else None,
+            "executed_frac": (fl["fb_mix_kernel"] / (mix_ms / 1e3) / 1e12 / FP64_PEAK_TFLOPS) if (fl and mix_ms) else None,
+            "hbm_frac": (tr["fb_mix_kernel"] / (mix_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if (tr and mix_ms) else None}
+    out["note"] = ("F(x, &softclip) per band (filterbank.h:133-139), width 0.125; the distortion keeps the calls on "
+                   "the general engine (smoothers and functor per band-sample)")
+    return out
+
+
 def launch_plan(gpus: int, env) -> tuple[str, str | None]:
     """What `bench.py --gpus N` does in this environment (no torch / HIP import before it):
     'run' (world matches), 'relaunch' (N > 1 and no launcher: rerun under torch.distributed.run),
@@ -648,6 +725,10 @@ def main():
     ap.add_argument("--stream-blocks", type=int, default=469, help="1024-sample calls for the streaming figure")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-sample", action="store_true", help="skip the per-sample drop-in figure")
+    ap.add_argument("--dist", choices=["none", "softclip"], default="none",
+                    help="C2 with the reference demos' &softclip on every band (the general engine)")
+    ap.add_argument("--no-general-side", action="store_true",
+                    help="skip side.general_softclip (the general engine on the reference demos' softclip calls)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 --pmc child passes")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--bands-per-wave", type=int, default=0)
@@ -733,6 +814,9 @@ def main():
         fb.tune_response_engine(bool(args.resp_engine))
     if args.modal >= 0:
         fb.tune_modal(bool(args.modal))
+    if args.dist == "softclip":   # F(x, &softclip): width 0.125 (tests/filterbank.cpp:168-171)
+        from huygens_amd._lib import HZ_DIST_SOFTCLIP
+        fb.distortion(HZ_DIST_SOFTCLIP)
     stream = torch.cuda.current_stream(dev)
     fb.set_stream(stream.cuda_stream)
 
@@ -819,7 +903,7 @@ def main():
     # every rank issues the same calls and collectives.
     armed = [False]
     primed = c2_prime(fb, step, S, tsplit, coll[2] if coll else (lambda k: k), HZ_FB_PATH_RESPONSE,
-                      stop_early=args.general or args.response == 0, armed=armed)
+                      stop_early=args.general or args.response == 0 or args.dist != "none", armed=armed)
     value_split = tsplit and armed[0]   # the value path is the time split (its shares only)
     for _ in range(args.warmup):
         step()
@@ -1071,6 +1155,10 @@ def main():
                                   "handle's stream)"},
         }
         hq.close()
+
+    if world == 1 and P == 1 and args.side_steps > 0 and not args.no_general_side and args.dist == "none":
+        side["general_softclip"] = general_softclip_figures(Filterbank, local, stream, x, ys[1], S,
+                                                            traffic=not args.no_traffic and S == SAMPLES_PER_STEP)
 
     total_band_samples = N_BANDS * S * args.steps
     value = total_band_samples / elapsed

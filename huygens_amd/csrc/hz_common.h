@@ -56,15 +56,25 @@ namespace hz {
 
 // Distortion functors (replacing the host function pointer of
 // Filterbank::operator()(T, T(*)(T)), src/filterbank.h:133-139).
+// softclip's tail (|v| >= width): out of line, so the engines' unrolled per-sample loops keep one
+// call site per sample instead of 16 inlined atan sequences -- inline, the general engine's mix
+// kernel spilled its recurrence registers (244 B per lane of scratch, 23.8 GB of scratch traffic
+// per C2 call, rocprofv3 PMC round 6); the identity branch, the common one at the reference's width
+// 0.125, stays inline
+__device__ __noinline__ double softclip_tail(double v, double width);
+__device__ __noinline__ inline double softclip_tail(double v, double width) {
+    const double sign = (v > 0.0) ? 1.0 : ((v < 0.0) ? -1.0 : 0.0);
+    const double gap = v - sign * width;
+    return sign * width + (1 - width) * 2.0 / kPI * atan(kPI * gap / (2 * (1 - width)));
+}
+
 template <int DIST>
 __device__ __forceinline__ double dist_apply(double v, double param) {
     if constexpr (DIST == HZ_DIST_SOFTCLIP) {
         // tests/filterbank.cpp:158-166 (abs taken as fabs)
         const double width = param;
         if (fabs(v) < width) return v;
-        const double sign = (v > 0.0) ? 1.0 : ((v < 0.0) ? -1.0 : 0.0);
-        const double gap = v - sign * width;
-        return sign * width + (1 - width) * 2.0 / kPI * atan(kPI * gap / (2 * (1 - width)));
+        return softclip_tail(v, width);
     } else if constexpr (DIST == HZ_DIST_SATURATE) {
         return 2.0 / kPI * atan(2 * kPI * v / 2.0);  // tests/filterbank.cpp:173-176
     } else if constexpr (DIST == HZ_DIST_LIMITER) {

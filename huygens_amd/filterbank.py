@@ -12,7 +12,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import HZ_DIST_NONE, PD, check, dptr, load
+from ._lib import HZ_DIST_NONE, HZ_DIST_SOFTCLIP, PD, check, dptr, load
 
 
 TV_COEFFS, TV_RESONANT = 0, 1   # HZ_FB_TV_*
@@ -74,8 +74,11 @@ class Filterbank:
     def open(self):
         check(self._lib.hz_fb_open(self._h))
 
-    def distortion(self, dist_id: int, param: float = 0.0):
-        """Select the per-band T(*)(T) of operator()(T, T(*)(T)) (filterbank.h:133)."""
+    def distortion(self, dist_id: int, param: float | None = None):
+        """Select the per-band T(*)(T) of operator()(T, T(*)(T)) (filterbank.h:133); param None: the
+        reference's default (softclip: the one-argument overload's width 0.125, the one &softclip
+        names in tests/filterbank.cpp:168-171)."""
+        param = dist_default_param(dist_id) if param is None else param
         check(self._lib.hz_fb_set_distortion(self._h, dist_id, param))
         self._dist = (dist_id, param)
 
@@ -286,7 +289,12 @@ class Filterbank:
         return bool(e.value), b.value, c.value, bool(r.value)
 
 
-def sample_many(banks, x, dist: int = HZ_DIST_NONE, param: float = 0.0) -> np.ndarray:
+def dist_default_param(dist_id: int) -> float:
+    """HZ_DIST_DEFAULT_PARAM: softclip's width 0.125 (tests/filterbank.cpp:168-171), else 0"""
+    return 0.125 if dist_id == HZ_DIST_SOFTCLIP else 0.0
+
+
+def sample_many(banks, x, dist: int = HZ_DIST_NONE, param: float | None = None) -> np.ndarray:
     """One sample of several Filterbanks in one per-sample server request (hz_fb_sample_many):
     y[i] = banks[i](x[i], dist) -- each bank's tick() stays separate (tests/filterbanks.cpp:191-211)."""
     n = len(banks)
@@ -296,5 +304,6 @@ def sample_many(banks, x, dist: int = HZ_DIST_NONE, param: float = 0.0) -> np.nd
     if xs.shape != (n,):
         raise ValueError(f"sample_many: x must hold one value per bank ({n}), got shape {xs.shape}")
     ys = np.empty(n)
+    param = dist_default_param(dist) if param is None else param
     check(lib.hz_fb_sample_many(hs, n, xs.ctypes.data_as(PD), int(dist), float(param), ys.ctypes.data_as(PD)))
     return ys

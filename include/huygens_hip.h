@@ -46,6 +46,11 @@ extern "C" {
 #define HZ_DIST_SOFTCLIP 1 /* tests/filterbank.cpp:158-166, param = width      */
 #define HZ_DIST_SATURATE 2 /* tests/filterbank.cpp:173-176                     */
 #define HZ_DIST_LIMITER 3  /* src/wave.h:150 limiter, FUNCTIONAL: 2/PI atan(x) */
+/* The reference's demos pass &softclip, which resolves to the one-argument overload
+ * softclip(sample) = softclip(sample, 0.125) (tests/filterbank.cpp:168-171): the width a drop-in
+ * F(x, HZ_DIST_SOFTCLIP) uses when none is given. */
+#define HZ_SOFTCLIP_WIDTH 0.125
+#define HZ_DIST_DEFAULT_PARAM(dist_id) ((dist_id) == HZ_DIST_SOFTCLIP ? HZ_SOFTCLIP_WIDTH : 0.0)
 
 /* ---- library ---------------------------------------------------------- */
 const char* hz_last_error(void);

@@ -41,11 +41,14 @@ public:
     void print() { std::printf("Filterbank<double>(order %d, %d bands) on HIP\n", order_, N_); }
 
     T operator()(T sample) { return sample_with(sample, HZ_DIST_NONE, 0.0); }
-    T operator()(T sample, int dist_id, double param = 0.0) { return sample_with(sample, dist_id, param); }
+    // F(x, &softclip) -> F(x, HZ_DIST_SOFTCLIP): the one-argument softclip's width 0.125 by default
+    T operator()(T sample, int dist_id) { return sample_with(sample, dist_id, HZ_DIST_DEFAULT_PARAM(dist_id)); }
+    T operator()(T sample, int dist_id, double param) { return sample_with(sample, dist_id, param); }
     void tick() { detail::check(hz_fb_sample_tick(h_.get()), "Filterbank::tick"); }
 
     // n x { out[i] = operator()(in[i]); tick(); }
-    void process(const T* in, T* out, std::size_t n, int dist_id = HZ_DIST_NONE, double param = 0.0) {
+    void process(const T* in, T* out, std::size_t n, int dist_id = HZ_DIST_NONE, double param = -1.0) {
+        if (param < 0.0) param = HZ_DIST_DEFAULT_PARAM(dist_id);
         detail::check(hz_fb_set_distortion(h_.get(), dist_id, param), "Filterbank::process");
         detail::check(hz_fb_process(h_.get(), in, out, n), "Filterbank::process");
     }
@@ -53,14 +56,16 @@ public:
     // the Subtractive ALLINONE / ONEPERVOICE pattern (src/subtractive.h:215-228, 300-317) as one
     // call.  coeffs: [n][2*order+1][N] (forward then back, band-minor).  The last row stays set.
     void process_stream(const T* in, T* out, std::size_t n, const T* coeffs, int dist_id = HZ_DIST_NONE,
-                        double param = 0.0) {
+                        double param = -1.0) {
+        if (param < 0.0) param = HZ_DIST_DEFAULT_PARAM(dist_id);
         detail::check(hz_fb_set_distortion(h_.get(), dist_id, param), "Filterbank::process_stream");
         detail::check(hz_fb_process_tv(h_.get(), in, out, n, HZ_FB_TV_COEFFS, coeffs, 0.0),
                       "Filterbank::process_stream");
     }
     // the same with every band retuned to resonant(freqs[t][b], R) (order 2, subtractive.h:240-264)
     void process_resonant(const T* in, T* out, std::size_t n, const T* freqs, double R,
-                          int dist_id = HZ_DIST_NONE, double param = 0.0) {
+                          int dist_id = HZ_DIST_NONE, double param = -1.0) {
+        if (param < 0.0) param = HZ_DIST_DEFAULT_PARAM(dist_id);
         detail::check(hz_fb_set_distortion(h_.get(), dist_id, param), "Filterbank::process_resonant");
         detail::check(hz_fb_process_tv(h_.get(), in, out, n, HZ_FB_TV_RESONANT, freqs, R),
                       "Filterbank::process_resonant");
@@ -99,7 +104,8 @@ public:
 //     soundmath::sample_many(Fs, CHANELS, xs, ys, HZ_DIST_SOFTCLIP);
 template <typename Bank>
 void sample_many(Bank* const* banks, int count, const double* in, double* out, int dist_id = HZ_DIST_NONE,
-                 double param = 0.0) {
+                 double param = -1.0) {
+    if (param < 0.0) param = HZ_DIST_DEFAULT_PARAM(dist_id);   // &softclip: width 0.125
     hz_fb* hs[12];
     if (count > 12) detail::check(HZ_E_INVALID, "sample_many: at most 12 banks");
     for (int j = 0; j < count; ++j) hs[j] = banks[j]->native();

@@ -99,8 +99,9 @@ class OracleFilterbank:
     def open(self):
         self.l.orc_fb_open(self.h)
 
-    def distortion(self, dist_id, param=0.0):
-        self.dist = (dist_id, param)
+    def distortion(self, dist_id, param=None):
+        # param None: the reference's default (softclip: width 0.125, tests/filterbank.cpp:168-171)
+        self.dist = (dist_id, (0.125 if dist_id == 1 else 0.0) if param is None else param)
 
     def process(self, x):
         xi = np.ascontiguousarray(x, dtype=np.float64)

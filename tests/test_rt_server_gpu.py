@@ -491,7 +491,7 @@ def test_sample_many_cpp_multichannel(gpu_lib, tmp_path):
             o.coefficients(n, fwd[n], back[n])
         o.boost(np.full(N, 1.0 + 0.1 * k))
         o.open()
-        o.distortion(HZ_DIST_SOFTCLIP, 0.0)
+        o.distortion(HZ_DIST_SOFTCLIP)   # &softclip: the one-argument overload, width 0.125 (the drop-in's default)
         yo = np.array([(o(v), o.tick())[0] for v in x[:, k]])
         assert np.max(np.abs(y[:, k] - yo) / np.maximum(1e-30, np.abs(yo))) < 1e-8, k
     lat = np.sort(lat[200:])
