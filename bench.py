@@ -752,7 +752,7 @@ def main():
                          "exceptional Nyquist band, the heaviest)")
     ap.add_argument("--band-partition", action="store_true",
                     help="N > 1: the value path on band shards + RCCL sum-reduce instead of the time split")
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "c6", "c7", "c8", "c9"], default="c2",
+    ap.add_argument("--workload", choices=["c2", "c3", "c3osc", "c4", "c5", "c6", "c7", "c8", "c9"], default="c2",
                     help="c2 = the BASELINE.json metric (default); c3/c4/c5 = the other SURVEY.md 8(d) rows; c6 = Granulator, c7 = Freezer, c8 = heterodyne chain, c9 = per-sample coefficient streams (8(f) rows 1-4)")
     args = ap.parse_args()
     rc = launcher(args)   # --gpus N > 1 without a launcher: N ranks under torch.distributed.run
@@ -1377,8 +1377,9 @@ def run_row(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and args.workload not in ("c3", "c4"):
-        raise SystemExit("--workload c5..c9 are single-GPU configs (SURVEY.md 8(d)); c3 and c4 shard")
+    if world > 1 and args.workload not in ("c3", "c3osc", "c4"):
+        raise SystemExit("--workload c5..c9 are single-GPU configs (SURVEY.md 8(d)); c3, c3osc and c4 shard")
+    shard_runs = {"c3": bench_rows.run_c3, "c3osc": bench_rows.run_c3osc, "c4": bench_rows.run_c4}
     rehearsal = world > 1 and os.environ.get("HZ_BENCH_REHEARSAL") == "1"
     if rehearsal:   # (one-GPU box: every rank on cuda:0, the reduces through host copies over gloo)
         local = 0
@@ -1392,15 +1393,14 @@ def run_row(args):
         else:
             os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
             dist.init_process_group("nccl", device_id=dev)
-        body = (bench_rows.run_c3 if args.workload == "c3" else bench_rows.run_c4)(args, torch, dev, rank, world)
+        body = shard_runs[args.workload](args, torch, dev, rank, world)
         if rehearsal:
             body["rehearsal"] = (f"{world} ranks on one GPU, reduces over gloo through host copies "
                                  "(HZ_BENCH_REHEARSAL=1): the N > 1 code path, not an N-GPU figure")
-    elif args.workload in ("c3", "c4") and args.emulate_world:
-        body = (bench_rows.run_c3 if args.workload == "c3" else bench_rows.run_c4)(args, torch, dev, 0, 1,
-                                                                                  args.emulate_world)
+    elif args.workload in shard_runs and args.emulate_world:
+        body = shard_runs[args.workload](args, torch, dev, 0, 1, args.emulate_world)
     else:
-        fn = {"c3": bench_rows.run_c3, "c4": bench_rows.run_c4, "c5": bench_rows.run_c5,
+        fn = {"c3": bench_rows.run_c3, "c3osc": bench_rows.run_c3osc, "c4": bench_rows.run_c4, "c5": bench_rows.run_c5,
               "c6": bench_rows.run_c6, "c7": bench_rows.run_c7, "c8": bench_rows.run_c8,
               "c9": bench_rows.run_c9}[args.workload]
         body = fn(args, torch, dev)

@@ -252,6 +252,96 @@ def run_c3(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
     }
 
 
+# ------------------------------------------------------------------ C3 (Oscbank variant)
+def c3_frequencies(V=64, O=256):
+    """The C3 partials' target frequencies as Additive::request sets them (src/additive.h:91-110,
+    harm = 1): f_vj = mtof(ftom(f0_v (1 + j))), f0_v = mtof(36 + v) (src/includes.h mtof / ftom)"""
+    import math
+
+    def mtof(m):
+        return 440.0 * 2.0 ** ((m - 69) / 12)
+
+    def ftom(f):
+        return 69 + math.log2(f / 440.0) * 12
+    return np.array([mtof(ftom(mtof(36 + v) * (1 + j))) for v in range(V) for j in range(O)])
+
+
+def run_c3osc(args, torch, dev, rank=0, world=1, shard_world=None, probe=None):
+    """C3's secondary variant (SURVEY.md 8(d) C3): Oscbank<double, 16384> with the C3 partials'
+    frequencies (c3_frequencies), every partial active (open()), and the complex Mixer mixdown
+    (src/oscbank.h:59-90, src/mixer.h:9) over 480,000 samples per step.  world > 1: partials sharded
+    (hz_osc_create_shard), the complex mixes (2 x 480,000 doubles) summed to rank 0 by an RCCL reduce."""
+    from huygens_amd import Oscbank
+    from huygens_amd.shard import shard_of
+    N, S = 16384, args.samples
+    f = c3_frequencies()
+    sw = shard_world or world
+    p0, pc = shard_of(rank, sw, N)
+    ob = Oscbank(N, device=dev.index or 0, shard=(p0, pc) if sw > 1 else None)
+    for i in range(p0, p0 + pc):
+        ob.freqmod(i, f[i])
+    ob.open()
+    ob.set_stream(_stream_handle(torch, dev))
+    mix = torch.empty(2 * S, dtype=torch.float64, device=dev)
+
+    def step():
+        ob.fill_device(mix.data_ptr(), None, S)
+        if world > 1:
+            dist.reduce(mix, dst=0, op=dist.ReduceOp.SUM)
+
+    dist = _coll() if world > 1 else None
+    for _ in range(args.warmup):
+        step()
+    elapsed = _timed(step, args.steps, 0, torch, dev, world)
+    if probe is not None:
+        probe(mix)
+    ob.profile(True)
+    _timed(step, args.steps, 0, torch, dev)
+    ms, launches = ob.profile_read()
+    ob.profile(False)
+    units = N * S * args.steps if shard_world is None else pc * sw * S * args.steps
+    kern_s = ms / 1e3
+    ref_fl = 15.0 * pc * S * args.steps   # SURVEY.md 8(d) C3 Oscbank: 15 FP64 flops per partial-sample
+    achieved = ref_fl / kern_s / 1e12 if kern_s > 0 else None
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        _tests_path()
+        from oracle import OracleOscbank
+        o = OracleOscbank(N)
+        for i in range(N):
+            o.freqmod(i, f[i])
+        o.open()
+        n = 2000
+        t0 = time.perf_counter()
+        o.fill(n)
+        dt = time.perf_counter() - t0
+        cpu = {"value": N * n / dt, "unit": "partial-samples/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/hz_oracle_osc.c Oscbank, {N} partials x {n} samples, 1 thread, {dt:.2f} s"}
+    ev = None
+    if not getattr(args, "no_traffic", True) and sw == 1:
+        ev = row_evidence("osc_mix_kernel", "c3osc", kern_s / max(1, launches), alg_bytes=16.0 * S)
+    return {
+        "metric": "partial-samples/s for Oscbank<double,16384> + complex mixdown (C3 variant)",
+        "value": units / elapsed, "unit": "partial-samples/s",
+        "ms_per_step": 1e3 * elapsed / args.steps, "dtype": "f64",
+        "data": "synthetic: the C3 partials' frequencies (64 voices x 256 overtones of mtof(36 + v)), all active",
+        "config": {"workload": "C3 variant: Oscbank<double,16384> + Mixer, 480,000 samples per step",
+                   "samples_per_step": S, "partials": N, "partials_per_gpu": pc,
+                   "parallelism": f"partials sharded x{world}, RCCL reduce of the complex mix"},
+        "n_gpus": world, "scaling": "strong", "emulated_world": shard_world,
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK if achieved else None,
+                     "traffic": (ev or {}).get("traffic_bytes"), "pmc_evidence": ev,
+                     "kernel": "osc_mix_kernel (+ osc_reduce_kernel, osc_advance_kernel)",
+                     "kernel_avg_ms": ms / max(1, launches), "launches": launches,
+                     "flops_per_unit": 15,
+                     "note": "achieved = SURVEY.md 8(d)'s 15 FP64 flops per partial-sample of the reference's "
+                             "renormalised phasor recurrence over the whole launch (mix + reduce + advance); the "
+                             "engine evaluates z0 w^t in closed form (pmc_evidence: its executed work)"},
+        "cpu_baseline": cpu,
+    }
+
+
 # --------------------------------------------------------------------------- C4
 def c4_signal(n, seed=3):
     rng = np.random.default_rng(seed)

@@ -26,7 +26,6 @@
 #include <cmath>
 #include <chrono>
 #include <cstring>
-#include <cstdlib>
 #include <new>
 #include <vector>
 
@@ -38,11 +37,6 @@ namespace {
 using namespace hz_fbi;
 
 constexpr int kL = 16;            // samples per lane chunk
-// MODE_MIXR: MODE_MIX that RECOMPUTES the recurrence from each chunk's start state in its mix pass
-// instead of keeping the 16 zero-state outputs per band in registers for a fix-up: 2-4 more FP64
-// ops per band-sample, 32 fewer VGPRs per band -- the 16-wave workgroup's 128-VGPR budget then
-// holds the kernel without scratch spills (round 6; HZ_FB_FIXUP=1 selects MODE_MIX for A/B)
-constexpr int MODE_MIXR = 3;
 constexpr int kTile = 64 * kL;    // samples per wave tile (= reference BSIZE 1024)
 
 // Per-band record (doubles), O-dependent layout.
@@ -123,9 +117,11 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
     // rec is passed as its own __restrict__ argument so the compiler can prove the
     // kernel's stores never clobber it: wave-uniform record reads become s_load.
     using R = Rec<O>;
-    constexpr bool kRecomp = MODE == MODE_MIXR;
-    constexpr bool kMixing = MODE == MODE_MIX || kRecomp;
     constexpr bool kDistRow = NB == 1 && (DIST == HZ_DIST_SATURATE || DIST == HZ_DIST_LIMITER);
+    // softclip with one band per wave: the identity branch (|gy| < width, the common case at the
+    // reference's width 0.125) costs one max per sample; only a wave whose tile reaches the width
+    // runs the tail over its LDS row (inline, the per-sample branch cost 2.5 ms per C2 call)
+    constexpr bool kClipRow = NB == 1 && DIST == HZ_DIST_SOFTCLIP;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* part = lds + 2 * kXsPad;  // xs double buffer: lds[0..kXsPad), lds[kXsPad..2 kXsPad)
     const int lane = threadIdx.x & 63;
@@ -214,8 +210,7 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
             pfast = pfast && (sp_t * fabs(P0[b] - pin[b]) <= 0x1p-60 * fabs(pin[b]));
             gfast = gfast && (sg_t * fabs(G0[b] - gin[b]) <= 0x1p-60 * fabs(gin[b]));
         }
-        double zsr[NB][kRecomp ? 1 : kL];
-        double zend[NB][O > 0 ? O : 1];   // (MODE_MIXR) the lane's zero-state end state
+        double zsr[NB][kL];
         auto zsr_pass = [&](auto fast_tag) {
             constexpr bool FAST = decltype(fast_tag)::value;
             double xw[O + 1];  // x[t], x[t-1], ... sliding window
@@ -251,15 +246,11 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
 #pragma unroll
                     for (int k = O - 1; k > 0; --k) yh[b][k] = yh[b][k - 1];
                     if constexpr (O > 0) yh[b][0] = y;
-                    if constexpr (!kRecomp) zsr[b][j] = y;
+                    zsr[b][j] = y;
                 }
 #pragma unroll
                 for (int k = O; k > 0; --k) xw[k] = xw[k - 1];
             }
-#pragma unroll
-            for (int b = 0; b < NB; ++b)
-#pragma unroll
-                for (int k = 0; k < O; ++k) zend[b][k] = yh[b][k];
         };
         if (pfast) zsr_pass(std::true_type{});
         else zsr_pass(std::false_type{});
@@ -282,7 +273,7 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
                 for (int e = 0; e < O * O; ++e) qm[e] = r[R::Q + p * O * O + e];
                 double z[O];
 #pragma unroll
-                for (int k = 0; k < O; ++k) z[k] = kRecomp ? zend[b][k] : zsr[b][kRecomp ? 0 : kL - 1 - k];
+                for (int k = 0; k < O; ++k) z[k] = zsr[b][kL - 1 - k];
 #define HZ_ROW_STEP(SIDX, D)                                                                 \
     {                                                                                        \
         double nb_[O];                                                                       \
@@ -330,97 +321,12 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
             }
         }
 
-        if constexpr (kRecomp) {
-            // ---- the recurrence again from the chunk start state st (y[tc-1-k]), then gain
-            // smoothing, distortion and mixdown; on the call's last tile the lanes holding its last
-            // O samples capture them (the y history of the next call)
-            auto mix_pass = [&](auto fast_tag, auto cap_tag) {
-                constexpr bool FAST = decltype(fast_tag)::value;   // pre and gain converged
-                constexpr bool CAP = decltype(cap_tag)::value;
-                double xw[O + 1];
-#pragma unroll
-                for (int k = 1; k <= O; ++k) xw[k] = xs[17 * lane + 16 - k];
-                double pre[NB], g[NB], bp[NB][O + 1];
-                double yh[NB][O > 0 ? O : 1];
-                double ycap[NB][O > 0 ? O : 1];
-                int jj[O > 0 ? O : 1];
-#pragma unroll
-                for (int k = 0; k < O; ++k) jj[k] = CAP ? (int)(n - 1 - k - tc) : -1;   // in [0, 16) on its lane
-#pragma unroll
-                for (int b = 0; b < NB; ++b) {
-                    const double* r = rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
-                    pre[b] = pin[b] + (sp_lane * sp_t) * (P0[b] - pin[b]);
-                    g[b] = FAST ? gin[b] : gin[b] + (sg_lane * sg_t) * (G0[b] - gin[b]);
-#pragma unroll
-                    for (int i = 0; i <= O; ++i) bp[b][i] = FAST ? pin[b] * r[R::B + i] : r[R::B + i];
-#pragma unroll
-                    for (int k = 0; k < O; ++k) {
-                        yh[b][k] = st[b][k];
-                        ycap[b][k] = 0.0;
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < kL; ++j) {
-                    xw[0] = xs[17 * lane + 17 + j];
-                    double v = 0.0;
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) {
-                        const double* r = rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
-                        double ff = bp[b][0] * xw[0];
-#pragma unroll
-                        for (int i = 1; i <= O; ++i) ff = fma(bp[b][i], xw[i], ff);
-                        double y = ff;
-                        if constexpr (!FAST) {
-                            pre[b] = fma(a.sp, pre[b], (1.0 - a.sp) * pin[b]);
-                            y = ff * pre[b];
-                        }
-#pragma unroll
-                        for (int k = 0; k < O; ++k) y = fma(-r[R::A + k], yh[b][k], y);
-#pragma unroll
-                        for (int k = O - 1; k > 0; --k) yh[b][k] = yh[b][k - 1];
-                        if constexpr (O > 0) yh[b][0] = y;
-                        if constexpr (CAP) {
-#pragma unroll
-                            for (int k = 0; k < O; ++k) ycap[b][k] = (j == jj[k]) ? y : ycap[b][k];
-                        }
-                        if constexpr (!FAST) g[b] = fma(a.sg, g[b], (1.0 - a.sg) * gin[b]);
-                        double gy = g[b] * y;
-                        if constexpr (DIST != HZ_DIST_NONE && !kDistRow) gy = hz::dist_apply<DIST>(gy, a.dist_param);
-                        if constexpr (NB == 1) v = gy;
-                        else v += live[b] ? gy : 0.0;
-                    }
-                    my[j * kPartPad + lane] = v;
-#pragma unroll
-                    for (int k = O; k > 0; --k) xw[k] = xw[k - 1];
-                }
-                if constexpr (CAP && O > 0) {
-#pragma unroll
-                    for (int k = 0; k < O; ++k) {
-                        if (jj[k] < 0 || jj[k] >= kL) continue;
-#pragma unroll
-                        for (int b = 0; b < NB; ++b)
-                            if (live[b]) a.ystate_next[(long)(band0 + b) * O + k] = ycap[b][k];
-                    }
-                }
-            };
-            const bool fast = pfast && gfast;
-            if (last_tile) {
-                if (fast) mix_pass(std::true_type{}, std::true_type{});
-                else mix_pass(std::false_type{}, std::true_type{});
-            } else {
-                if (fast) mix_pass(std::true_type{}, std::false_type{});
-                else mix_pass(std::false_type{}, std::false_type{});
-            }
-            if (NB == 1 && !live[0]) {  // wave-uniform: padding wave past the last band
-#pragma unroll
-                for (int j = 0; j < kL; ++j) my[j * kPartPad + lane] = 0.0;
-            }
-        }
         if constexpr (MODE == MODE_MIX) {
             // ---- fix-up, gain smoothing and mixdown (bands summed in registers) ---
             // correction c = y - zsr obeys the homogeneous recurrence seeded with the
             // chunk start state: c_j = -sum_k a_k c_{j-1-k}, c_{-1-k} = st[k].
             // Gain fast path once the gain smoother has converged (as for pre).
+            double gmax = 0.0;   // (kClipRow) the wave-lane's largest |gy| of the tile
             auto fix_pass = [&](auto fast_tag) {
                 constexpr bool FAST = decltype(fast_tag)::value;
                 double g[NB], cr[NB][O > 0 ? O : 1];
@@ -436,7 +342,7 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
 #pragma unroll
                     for (int b = 0; b < NB; ++b) {
                         const double* r = rec + (long)(live[b] ? band0 + b : 0) * R::SIZE;
-                        double y = zsr[b][kRecomp ? 0 : j];
+                        double y = zsr[b][j];
                         if constexpr (O > 0) {
                             double c = -r[R::A] * cr[b][0];
 #pragma unroll
@@ -448,13 +354,14 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
                         }
                         if constexpr (!FAST) g[b] = fma(a.sg, g[b], (1.0 - a.sg) * gin[b]);
                         double gy = g[b] * y;
-                        // (MODE_MIX: saturate / limiter with one band per wave: on the LDS row below, after the
+                        // (saturate / limiter with one band per wave: on the LDS row below, after the
                         // recurrence registers are dead -- inline here they spilled them: C2 bank
                         // 7.7 -> 4.9 ms per 10 s; softclip's branch runs better inline, 5.4 vs 11.9)
-                        if constexpr (DIST != HZ_DIST_NONE && !kDistRow) gy = hz::dist_apply<DIST>(gy, a.dist_param);
+                        if constexpr (kClipRow) gmax = fmax(gmax, fabs(gy));
+                        else if constexpr (DIST != HZ_DIST_NONE && !kDistRow) gy = hz::dist_apply<DIST>(gy, a.dist_param);
                         if constexpr (NB == 1) v = gy;  // a dead wave's row is zeroed below
                         else v += live[b] ? gy : 0.0;
-                        zsr[b][kRecomp ? 0 : j] = y;  // keep y for the end-of-signal state capture
+                        zsr[b][j] = y;  // keep y for the end-of-signal state capture
                     }
                     my[j * kPartPad + lane] = v;
                 }
@@ -476,14 +383,12 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
                             if (!live[b]) continue;
                             double y = 0.0;
 #pragma unroll
-                            for (int j = 0; j < kL; ++j) y = (j == jj) ? zsr[b][kRecomp ? 0 : j] : y;
+                            for (int j = 0; j < kL; ++j) y = (j == jj) ? zsr[b][j] : y;
                             a.ystate_next[(long)(band0 + b) * O + k] = y;
                         }
                     }
                 }
             }
-        }
-        if constexpr (kMixing) {
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
                 if (!last_tile || lane != 0 || !live[b]) continue;
@@ -502,6 +407,14 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
                 a.pgstate_next[2 * band + 1] = gin[b] + a.sg_n * (G0[b] - gin[b]);
             }
 
+            if constexpr (kClipRow) {   // softclip's tail where some sample of the wave reaches the width
+                if (__builtin_amdgcn_ballot_w64(gmax >= a.dist_param) != 0 && live[0]) {
+                    for (int j = 0; j < kL; ++j) {
+                        const double v = my[j * kPartPad + lane];
+                        if (fabs(v) >= a.dist_param) my[j * kPartPad + lane] = hz::softclip_tail(v, a.dist_param);
+                    }
+                }
+            }
             if constexpr (kDistRow) {   // the same T(*)(T) per sample, from LDS
                 for (int j = 0; j < kL; ++j) my[j * kPartPad + lane] = hz::dist_apply<DIST>(my[j * kPartPad + lane], a.dist_param);
             }
@@ -677,27 +590,9 @@ static void build_record_any(int O, const double* b, const double* a, double* re
 typedef void (*MixKernel)(const double*, MixArgs);
 typedef void (*CarryKernel)(const double*, const double*, double*, int, int, long);
 
-// (A/B) HZ_FB_FIXUP=1: the mix pass keeps the zero-state outputs and adds the homogeneous fix-up
-// (MODE_MIX, rounds 1-5) instead of recomputing the recurrence (MODE_MIXR)
-static bool fb_fixup_mode() {
-    static const bool on = [] {
-        const char* v = std::getenv("HZ_FB_FIXUP");
-        return v && v[0] == '1';
-    }();
-    return on;
-}
-
 template <int O, int PF, int NB>
 MixKernel pick_dist(int dist, int mode) {
     if (mode == MODE_SEGEND) return fb_mix_kernel<O, HZ_DIST_NONE, NB, MODE_SEGEND, PF>;
-    if (!fb_fixup_mode()) {
-        switch (dist) {
-        case HZ_DIST_SOFTCLIP: return fb_mix_kernel<O, HZ_DIST_SOFTCLIP, NB, MODE_MIXR, PF>;
-        case HZ_DIST_SATURATE: return fb_mix_kernel<O, HZ_DIST_SATURATE, NB, MODE_MIXR, PF>;
-        case HZ_DIST_LIMITER: return fb_mix_kernel<O, HZ_DIST_LIMITER, NB, MODE_MIXR, PF>;
-        default: return fb_mix_kernel<O, HZ_DIST_NONE, NB, MODE_MIXR, PF>;
-        }
-    }
     switch (dist) {
     case HZ_DIST_SOFTCLIP: return fb_mix_kernel<O, HZ_DIST_SOFTCLIP, NB, MODE_MIX, PF>;
     case HZ_DIST_SATURATE: return fb_mix_kernel<O, HZ_DIST_SATURATE, NB, MODE_MIX, PF>;

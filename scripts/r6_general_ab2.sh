@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 COMMON="--steps 20 --warmup 3 --no-cpu-baseline --no-traffic --no-per-sample --stream-blocks 0 --side-steps 0 --no-general-side"
 for rep in 1 2; do
 for mode in "--general" "--dist softclip"; do
-  for fix in 0 1; do
+  for fix in ${FIXES:-0 1}; do
     tag="$(echo $mode | tr -d ' -')_fix${fix}_$rep"
     HZ_FB_FIXUP=$fix timeout -k 10 120 python3 -u bench.py $COMMON $mode > $OUT/$tag.json 2> $OUT/$tag.err || { echo "$tag failed"; tail -3 $OUT/$tag.err; exit 1; }
     python3 - $OUT/$tag.json $tag <<'PY'

@@ -115,6 +115,47 @@ def test_c3_full_length(gpu_lib):
     assert last <= 1e-9, last
 
 
+def test_c3osc_full_length(gpu_lib):
+    """C3's Oscbank variant (bench.py --workload c3osc): Oscbank<double,16384>
+    with the C3 partials' frequencies, all active, the complex mixdown over 480,000 samples.  The
+    engine's closed-form phasors z0 w^t against the reference's renormalised recurrence
+    (src/oscbank.h:59-63) over the bench's whole length: two 256-partial shards (the lowest and
+    the highest voice) against the restatement, per 1024-sample block and in the final phasors;
+    the whole bank's mix against the sum of four 4096-partial shards (the N > 1 decomposition)."""
+    import bench_rows
+    from huygens_amd import Oscbank
+    from oracle import OracleOscbank
+    N, S = 16384, 480000
+    f = bench_rows.c3_frequencies()
+    for p0 in (0, N - 256):
+        g, o = Oscbank(N, shard=(p0, 256)), OracleOscbank(256)
+        for i in range(256):
+            g.freqmod(p0 + i, f[p0 + i])
+            o.freqmod(i, f[p0 + i])
+        g.open()
+        o.open()
+        mg, mo = g.fill(S), o.fill(S)
+        errs = [np.max(np.abs(mg[b:b + 1024] - mo[b:b + 1024])) / max(1e-300, np.max(np.abs(mo[b:b + 1024])))
+                for b in range(0, S, 1024)]
+        assert max(errs) < 1e-9, (p0, max(errs))
+        assert np.max(np.abs(g.phases() - o.phases())) < 1e-9
+        g.close()
+    full = Oscbank(N)
+    for i in range(N):
+        full.freqmod(i, f[i])
+    full.open()
+    mf = full.fill(S)
+    parts = []
+    for r in range(4):
+        sh = Oscbank(N, shard=(r * 4096, 4096))
+        for i in range(r * 4096, (r + 1) * 4096):
+            sh.freqmod(i, f[i])
+        sh.open()
+        parts.append(sh.fill(S))
+        sh.close()
+    assert np.max(np.abs(mf - sum(parts))) <= 1e-12 * np.max(np.abs(mf))
+
+
 def test_c5_full_length_chain(gpu_lib):
     import torch
     from huygens_amd import Bowl, Delaybank
