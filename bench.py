@@ -1131,6 +1131,15 @@ def main():
                 break
         long_t = timed(hq_long, 3, min(args.side_steps, 20), S)
         long_t["path"] = {1: "general", 2: "lti", 3: "response"}.get(hq.last_path(), "?")
+        hq.profile(True)   # the three launches' event times (forward, MAC, inverse + states)
+        for _ in range(5):
+            hq_long()
+        barrier()
+        f_ms, m_ms, i_ms, nl = hq.profile_read()
+        hq.profile(False)
+        long_t["kernels_ms_per_call"] = {"resp_fwd_kernel": f_ms / max(1, nl), "resp_mac_kernel": m_ms / max(1, nl),
+                                         "resp_inv_kernel": i_ms / max(1, nl)}
+        long_t["partitions"] = hq.response_info()[0] // 2048
         B = 1024
         nbq = min(args.stream_blocks, S // B)
 

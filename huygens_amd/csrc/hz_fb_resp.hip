@@ -461,6 +461,85 @@ __global__ __launch_bounds__(256) void resp_mac_kernel_lds(const double2* __rest
     }
 }
 
+// The LDS-staged MAC for long horizons (Qp > 24 partitions, e.g. R = 0.9999: K = 507,904, Q = 248):
+// the partitions in chunks of 24 -- per chunk the 24 H rows and the 24 + 31 Z rows of the
+// workgroup's 32 blocks go through LDS as in resp_mac_kernel_lds<24> (the next chunk's operands
+// loaded into registers while this chunk's MACs run), the accumulators carried across chunks.  The
+// partitions are visited in order with the same FMAs, so the result is the register kernel's bit
+// for bit.  The register kernel it replaces pulled every H row once per 8 blocks and every Z row
+// ~4 times through the L2s: ~0.5 GB per R = 0.9999 call.
+constexpr int kMacChunk = 24;
+template <int BPW>
+__global__ __launch_bounds__(256) void resp_mac_kernel_ldsc(const double2* __restrict__ H, const double2* __restrict__ Z,
+                                                            double2* __restrict__ Y, int Q, int B, int nch) {
+    constexpr int QP = kMacChunk, kMacBlk = 4 * BPW, kZr = kMacBlk + QP - 1, kHL = QP / 4, kZL = (kZr + 3) / 4;
+    extern __shared__ double2 mac_lds[];
+    double2(*hs)[kMacBins] = (double2(*)[kMacBins])mac_lds;
+    double2(*zs)[kMacBins] = (double2(*)[kMacBins])(mac_lds + QP * kMacBins);
+    const int t = threadIdx.x, lq = t & (kMacBins - 1), sl = t >> 6;
+    const int q = (blockIdx.x % (kH / kMacBins)) * kMacBins + lq;
+    const int b0 = (blockIdx.x / (kH / kMacBins)) * kMacBlk;
+    double2 hv[kHL], zv[kZL];
+    auto fetch = [&](int c) {   // chunk c: partitions [24 c, 24 c + 24)
+#pragma unroll
+        for (int k = 0; k < kHL; ++k) hv[k] = H[(long)(QP * c + sl + 4 * k) * kH + q];
+        const long row_lo = (long)b0 + Q - (long)QP * (c + 1);
+#pragma unroll
+        for (int k = 0; k < kZL; ++k) {
+            const int r = sl + 4 * k;
+            const long row = row_lo + r;
+            zv[k] = r < kZr ? Z[(row > 0 ? row : 0) * kH + q] : make_double2(0.0, 0.0);
+        }
+    };
+    double ar[BPW], ai[BPW];
+#pragma unroll
+    for (int r = 0; r < BPW; ++r) ar[r] = ai[r] = 0.0;
+    fetch(0);
+    for (int c = 0; c < nch; ++c) {
+#pragma unroll
+        for (int k = 0; k < kHL; ++k) hs[sl + 4 * k][lq] = hv[k];
+#pragma unroll
+        for (int k = 0; k < kZL; ++k)
+            if (sl + 4 * k < kZr) zs[sl + 4 * k][lq] = zv[k];
+        __syncthreads();
+        if (c + 1 < nch) fetch(c + 1);   // in flight under this chunk's MACs
+        double zr[BPW], zi[BPW];
+#pragma unroll
+        for (int r = 0; r < BPW; ++r) {
+            const double2 z = zs[BPW * sl + r + QP - 1][lq];
+            zr[r] = z.x;
+            zi[r] = z.y;
+        }
+#pragma unroll
+        for (int p = 0; p < QP; ++p) {
+            const double2 hc = hs[p][lq];
+#pragma unroll
+            for (int r = 0; r < BPW; ++r) {
+                ar[r] = fma(hc.x, zr[r], ar[r]);
+                ar[r] = fma(-hc.y, zi[r], ar[r]);
+                ai[r] = fma(hc.x, zi[r], ai[r]);
+                ai[r] = fma(hc.y, zr[r], ai[r]);
+            }
+            if (p + 1 < QP) {
+#pragma unroll
+                for (int r = BPW - 1; r > 0; --r) {
+                    zr[r] = zr[r - 1];
+                    zi[r] = zi[r - 1];
+                }
+                const double2 z = zs[BPW * sl + QP - 2 - p][lq];
+                zr[0] = z.x;
+                zi[0] = z.y;
+            }
+        }
+        __syncthreads();   // the next chunk's stores overwrite hs / zs
+    }
+#pragma unroll
+    for (int r = 0; r < BPW; ++r) {
+        const int b = b0 + BPW * sl + r;
+        if (b < B) Y[(long)b * kH + q] = make_double2(ar[r], ai[r]);
+    }
+}
+
 // the LDS-staged MAC for Qp = 8, 16, 24 when no modal phase rides in the MAC launch (C2: 6.1
 // against 7.4 us per launch, step 29.4 against 30.6 us, alternating runs on one box,
 // profiles/r5/mac/summary.txt); HZ_MAC=reg selects the register-only kernel (A/B)
@@ -469,7 +548,7 @@ bool mac_lds_ok(int Qp, bool modal_in_mac) {
         const char* v = std::getenv("HZ_MAC");
         return v && std::strcmp(v, "reg") == 0;
     }();
-    return !reg && !modal_in_mac && (Qp == 8 || Qp == 16 || Qp == 24);
+    return !reg && !modal_in_mac && (Qp == 8 || Qp == 16 || Qp == 24 || Qp % kMacChunk == 0);
 }
 template <int BPW>
 void launch_mac_lds_t(int Qp, int B, const double2* H, const double2* Z, double2* Y, int Q, hipStream_t s) {
@@ -478,9 +557,15 @@ void launch_mac_lds_t(int Qp, int B, const double2* H, const double2* Z, double2
         (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<8, BPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<8, BPW>());
         (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<16, BPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<16, BPW>());
         (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<24, BPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<24, BPW>());
+        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_ldsc<BPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<24, BPW>());
         attr = true;
     }
     const dim3 grid((unsigned)((kH / kMacBins) * ((B + 4 * BPW - 1) / (4 * BPW))));
+    if (Qp > kMacChunk) {   // long horizons: partitions in chunks of 24
+        hipLaunchKernelGGL((resp_mac_kernel_ldsc<BPW>), grid, dim3(256), (mac_lds_bytes<24, BPW>()), s, H, Z, Y, Q, B,
+                           Qp / kMacChunk);
+        return;
+    }
     if (Qp == 8) hipLaunchKernelGGL((resp_mac_kernel_lds<8, BPW>), grid, dim3(256), (mac_lds_bytes<8, BPW>()), s, H, Z, Y, Q, B);
     else if (Qp == 16) hipLaunchKernelGGL((resp_mac_kernel_lds<16, BPW>), grid, dim3(256), (mac_lds_bytes<16, BPW>()), s, H, Z, Y, Q, B);
     else hipLaunchKernelGGL((resp_mac_kernel_lds<24, BPW>), grid, dim3(256), (mac_lds_bytes<24, BPW>()), s, H, Z, Y, Q, B);
@@ -710,7 +795,9 @@ int resp_alloc(double** p, size_t* cap, size_t need) {
     return HZ_OK;
 }
 
-int q_padded(int Q) { return (Q + kMacR - 1) / kMacR * kMacR; }
+// partitions padded with zero spectra: to the MAC's register window (8), or to whole chunks of the
+// chunked LDS MAC (24) past 24
+int q_padded(int Q) { return Q > 24 ? (Q + 23) / 24 * 24 : (Q + kMacR - 1) / kMacR * kMacR; }
 
 // partition counts the column-split kernel is built for (its LDS holds kWB + Q window rows of four
 // columns: Q <= 24 is 136 KB)

@@ -118,10 +118,11 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
     // kernel's stores never clobber it: wave-uniform record reads become s_load.
     using R = Rec<O>;
     constexpr bool kDistRow = NB == 1 && (DIST == HZ_DIST_SATURATE || DIST == HZ_DIST_LIMITER);
-    // softclip with one band per wave: the identity branch (|gy| < width, the common case at the
-    // reference's width 0.125) costs one max per sample; only a wave whose tile reaches the width
-    // runs the tail over its LDS row (inline, the per-sample branch cost 2.5 ms per C2 call)
-    constexpr bool kClipRow = NB == 1 && DIST == HZ_DIST_SOFTCLIP;
+    // (softclip: dist_apply's identity branch inline, its atan tail out of line -- inline, the tail
+    // spilled the recurrence registers of every sample: 244 B of scratch per lane, 23.8 GB of
+    // scratch traffic per C2 call, 5.9 ms; out of line 80 B, 4.57 ms.  A per-wave max with the tail
+    // on the LDS row measured 5.1 ms (its call site, or inlined atan, raised the scratch to 128 /
+    // 224 B): profiles/r6/general)
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* part = lds + 2 * kXsPad;  // xs double buffer: lds[0..kXsPad), lds[kXsPad..2 kXsPad)
     const int lane = threadIdx.x & 63;
@@ -326,7 +327,6 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
             // correction c = y - zsr obeys the homogeneous recurrence seeded with the
             // chunk start state: c_j = -sum_k a_k c_{j-1-k}, c_{-1-k} = st[k].
             // Gain fast path once the gain smoother has converged (as for pre).
-            double gmax = 0.0;   // (kClipRow) the wave-lane's largest |gy| of the tile
             auto fix_pass = [&](auto fast_tag) {
                 constexpr bool FAST = decltype(fast_tag)::value;
                 double g[NB], cr[NB][O > 0 ? O : 1];
@@ -357,8 +357,7 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
                         // (saturate / limiter with one band per wave: on the LDS row below, after the
                         // recurrence registers are dead -- inline here they spilled them: C2 bank
                         // 7.7 -> 4.9 ms per 10 s; softclip's branch runs better inline, 5.4 vs 11.9)
-                        if constexpr (kClipRow) gmax = fmax(gmax, fabs(gy));
-                        else if constexpr (DIST != HZ_DIST_NONE && !kDistRow) gy = hz::dist_apply<DIST>(gy, a.dist_param);
+                        if constexpr (DIST != HZ_DIST_NONE && !kDistRow) gy = hz::dist_apply<DIST>(gy, a.dist_param);
                         if constexpr (NB == 1) v = gy;  // a dead wave's row is zeroed below
                         else v += live[b] ? gy : 0.0;
                         zsr[b][j] = y;  // keep y for the end-of-signal state capture
@@ -407,14 +406,6 @@ __global__ __launch_bounds__(wg_threads(PF)) void fb_mix_kernel(const double* __
                 a.pgstate_next[2 * band + 1] = gin[b] + a.sg_n * (G0[b] - gin[b]);
             }
 
-            if constexpr (kClipRow) {   // softclip's tail where some sample of the wave reaches the width
-                if (__builtin_amdgcn_ballot_w64(gmax >= a.dist_param) != 0 && live[0]) {
-                    for (int j = 0; j < kL; ++j) {
-                        const double v = my[j * kPartPad + lane];
-                        if (fabs(v) >= a.dist_param) my[j * kPartPad + lane] = hz::softclip_tail(v, a.dist_param);
-                    }
-                }
-            }
             if constexpr (kDistRow) {   // the same T(*)(T) per sample, from LDS
                 for (int j = 0; j < kL; ++j) my[j * kPartPad + lane] = hz::dist_apply<DIST>(my[j * kPartPad + lane], a.dist_param);
             }
