@@ -50,7 +50,11 @@ struct BandPar {                   // regular band n
 
 struct ModalArgs {
     int on;                        // 0: no modal work in this launch
-    const double* xw;              // the window: xw[i] = x[T - K + i], i < K
+    // the window w[i] = x[T - K + i], i < K, in two pieces: w[i] = xw[i] for i < split (the history
+    // before a call shorter than K), xw2[i - split] after (the call's input)
+    const double* xw;
+    const double* xw2;
+    long split;
     long K;
     int S;                         // K / kL
     const double* wR;              // [kL] R_g^r
@@ -91,6 +95,8 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
+__device__ __forceinline__ double win(const ModalArgs& a, long i) { return i < a.split ? a.xw[i] : a.xw2[i - a.split]; }
+
 // phase 1, workgroup r1 < 128: the fold of residues r1 + 128 r2 (r2 < 64) and their 64-point DFTs
 __device__ __forceinline__ void phase1(const ModalArgs& a, int r1, Lds1& L) {
     const int t = threadIdx.x, r2 = t & 63, g = t >> 6;
@@ -102,7 +108,7 @@ __device__ __forceinline__ void phase1(const ModalArgs& a, int r1, Lds1& L) {
 #pragma unroll 4
     for (int s = g; s < a.S; s += 4) {
         const long tau = r + (long)kL * s;
-        const double v = w0 * a.RL[s] * a.xw[a.K - 1 - tau];
+        const double v = w0 * a.RL[s] * win(a, a.K - 1 - tau);
         f0 += v;
         f1 = fma((double)tau, v, f1);
     }
@@ -143,8 +149,8 @@ __device__ __forceinline__ void exc_partial(const ModalArgs& a, int e, int q, Ld
         const long tau = t0 + t + (long)i * kThreads;
         const bool ok = tau < t1;
         rv[i] = ok ? r[tau] : 0.0;
-        xa[i] = ok ? a.xw[a.K - 1 - tau] : 0.0;
-        xb[i] = (ok && tau < a.K - 1) ? a.xw[a.K - 2 - tau] : 0.0;
+        xa[i] = ok ? win(a, a.K - 1 - tau) : 0.0;
+        xb[i] = (ok && tau < a.K - 1) ? win(a, a.K - 2 - tau) : 0.0;
     }
     dd s0{0.0, 0.0}, s1{0.0, 0.0};
 #pragma unroll
@@ -193,7 +199,7 @@ __device__ __forceinline__ void phase2(const ModalArgs& a, int w, Lds2& L) {
         bk0 = a.csr[i0 + t];
         P0 = a.par[bk0.x];
     }
-    const double x1 = a.xw[a.K - 1], x2 = a.xw[a.K - 2], x3 = a.xw[a.K - 3];
+    const double x1 = win(a, a.K - 1), x2 = win(a, a.K - 2), x3 = win(a, a.K - 3);
     {
         const int j = t >> 7, r1 = t & 127;
         L.a[j][r1] = a.A[((long)j * kR2 + k1) * kR1 + r1];
@@ -255,17 +261,22 @@ __device__ __forceinline__ void phase2_group(const ModalArgs& a, int w, Lds2& L)
     }
 }
 
-// phase 2, the extra workgroup: the exceptional bands' partials summed in chunk order
+// phase 2, the extra workgroup: the exceptional bands' partials summed in double-double, 16 lanes
+// per (band, component) series -- lane l takes chunks l, l + 16, ..., then a fixed xor-shuffle tree
+// (one lane walking all chunks was a dependent chain of K / 2048 double-double adds: ~17 us at
+// R = 0.9999's 248 chunks, the inverse launch's last workgroup)
 __device__ __forceinline__ void exc_sum(const ModalArgs& a) {
-    const int t = threadIdx.x;
-    if (t >= 2 * a.nexc) return;
-    const int e = t >> 1, c = t & 1;
+    const int t = threadIdx.x, ser = t >> 4, sub = t & 15;
+    if (ser >= 2 * a.nexc) return;   // whole 16-lane groups: the shuffles below stay inside a group
+    const int e = ser >> 1, c = ser & 1;
     hz_dd::dd acc{0.0, 0.0};
-    for (int q = 0; q < a.exc_chunks; ++q) {
+    for (int q = sub; q < a.exc_chunks; q += 16) {
         const double* p = a.exc_part + ((long)e * a.exc_chunks + q) * 4 + 2 * c;
         acc = hz_dd::add(acc, hz_dd::dd{p[0], p[1]});
     }
-    a.out[2L * a.exc_band[e] + c] = acc.hi + acc.lo;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) acc = hz_dd::add(acc, hz_dd::dd{__shfl_xor(acc.hi, o, 64), __shfl_xor(acc.lo, o, 64)});
+    if (sub == 0) a.out[2L * a.exc_band[e] + c] = acc.hi + acc.lo;
 }
 
 }  // namespace hz_modal

@@ -469,24 +469,31 @@ __global__ __launch_bounds__(256) void resp_mac_kernel_lds(const double2* __rest
 // for bit.  The register kernel it replaces pulled every H row once per 8 blocks and every Z row
 // ~4 times through the L2s: ~0.5 GB per R = 0.9999 call.
 constexpr int kMacChunk = 24;
-template <int BPW>
+// BINS bins x (256 / BINS) slices of BPW blocks per workgroup: 64 x 4 x 8 = 32 blocks (the C2
+// kernel's tile), 32 x 8 x 8 = 64 or 16 x 16 x 8 = 128 blocks (the default: the H rows re-read by
+// 2 instead of 8 block rows, the Z rows re-read less per block; HZ_MACC_BINS=32 / 64 for A/B)
+template <int BINS, int BPW>
+constexpr size_t macc_lds_bytes() { return sizeof(double2) * BINS * (kMacChunk + (256 / BINS) * BPW + kMacChunk - 1); }
+template <int BINS, int BPW>
 __global__ __launch_bounds__(256) void resp_mac_kernel_ldsc(const double2* __restrict__ H, const double2* __restrict__ Z,
                                                             double2* __restrict__ Y, int Q, int B, int nch) {
-    constexpr int QP = kMacChunk, kMacBlk = 4 * BPW, kZr = kMacBlk + QP - 1, kHL = QP / 4, kZL = (kZr + 3) / 4;
+    constexpr int QP = kMacChunk, SL = 256 / BINS, kMacBlk = SL * BPW, kZr = kMacBlk + QP - 1;
+    constexpr int kHL = (QP + SL - 1) / SL, kZL = (kZr + SL - 1) / SL;
     extern __shared__ double2 mac_lds[];
-    double2(*hs)[kMacBins] = (double2(*)[kMacBins])mac_lds;
-    double2(*zs)[kMacBins] = (double2(*)[kMacBins])(mac_lds + QP * kMacBins);
-    const int t = threadIdx.x, lq = t & (kMacBins - 1), sl = t >> 6;
-    const int q = (blockIdx.x % (kH / kMacBins)) * kMacBins + lq;
-    const int b0 = (blockIdx.x / (kH / kMacBins)) * kMacBlk;
+    double2(*hs)[BINS] = (double2(*)[BINS])mac_lds;
+    double2(*zs)[BINS] = (double2(*)[BINS])(mac_lds + QP * BINS);
+    const int t = threadIdx.x, lq = t & (BINS - 1), sl = t / BINS;
+    const int q = (blockIdx.x % (kH / BINS)) * BINS + lq;
+    const int b0 = (blockIdx.x / (kH / BINS)) * kMacBlk;
     double2 hv[kHL], zv[kZL];
     auto fetch = [&](int c) {   // chunk c: partitions [24 c, 24 c + 24)
 #pragma unroll
-        for (int k = 0; k < kHL; ++k) hv[k] = H[(long)(QP * c + sl + 4 * k) * kH + q];
+        for (int k = 0; k < kHL; ++k)
+            hv[k] = sl + SL * k < QP ? H[(long)(QP * c + sl + SL * k) * kH + q] : make_double2(0.0, 0.0);
         const long row_lo = (long)b0 + Q - (long)QP * (c + 1);
 #pragma unroll
         for (int k = 0; k < kZL; ++k) {
-            const int r = sl + 4 * k;
+            const int r = sl + SL * k;
             const long row = row_lo + r;
             zv[k] = r < kZr ? Z[(row > 0 ? row : 0) * kH + q] : make_double2(0.0, 0.0);
         }
@@ -497,10 +504,11 @@ __global__ __launch_bounds__(256) void resp_mac_kernel_ldsc(const double2* __res
     fetch(0);
     for (int c = 0; c < nch; ++c) {
 #pragma unroll
-        for (int k = 0; k < kHL; ++k) hs[sl + 4 * k][lq] = hv[k];
+        for (int k = 0; k < kHL; ++k)
+            if (sl + SL * k < QP) hs[sl + SL * k][lq] = hv[k];
 #pragma unroll
         for (int k = 0; k < kZL; ++k)
-            if (sl + 4 * k < kZr) zs[sl + 4 * k][lq] = zv[k];
+            if (sl + SL * k < kZr) zs[sl + SL * k][lq] = zv[k];
         __syncthreads();
         if (c + 1 < nch) fetch(c + 1);   // in flight under this chunk's MACs
         double zr[BPW], zi[BPW];
@@ -539,6 +547,19 @@ __global__ __launch_bounds__(256) void resp_mac_kernel_ldsc(const double2* __res
         if (b < B) Y[(long)b * kH + q] = make_double2(ar[r], ai[r]);
     }
 }
+template <int BINS>
+void launch_macc(int Qp, int B, const double2* H, const double2* Z, double2* Y, int Q, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_ldsc<BINS, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)macc_lds_bytes<BINS, 8>());
+        attr = true;
+    }
+    constexpr int blk = (256 / BINS) * 8;
+    const dim3 grid((unsigned)((kH / BINS) * ((B + blk - 1) / blk)));
+    hipLaunchKernelGGL((resp_mac_kernel_ldsc<BINS, 8>), grid, dim3(256), (macc_lds_bytes<BINS, 8>()), s, H, Z, Y, Q, B,
+                       Qp / kMacChunk);
+}
 
 // the LDS-staged MAC for Qp = 8, 16, 24 when no modal phase rides in the MAC launch (C2: 6.1
 // against 7.4 us per launch, step 29.4 against 30.6 us, alternating runs on one box,
@@ -557,13 +578,16 @@ void launch_mac_lds_t(int Qp, int B, const double2* H, const double2* Z, double2
         (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<8, BPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<8, BPW>());
         (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<16, BPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<16, BPW>());
         (void)hipFuncSetAttribute((const void*)resp_mac_kernel_lds<24, BPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<24, BPW>());
-        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_ldsc<BPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mac_lds_bytes<24, BPW>());
         attr = true;
     }
     const dim3 grid((unsigned)((kH / kMacBins) * ((B + 4 * BPW - 1) / (4 * BPW))));
     if (Qp > kMacChunk) {   // long horizons: partitions in chunks of 24
-        hipLaunchKernelGGL((resp_mac_kernel_ldsc<BPW>), grid, dim3(256), (mac_lds_bytes<24, BPW>()), s, H, Z, Y, Q, B,
-                           Qp / kMacChunk);
+        // 16 bins x 128 blocks: 35.5 us per R = 0.9999 call against 37.4 (32 x 64) and 46.2 (64 x 32),
+        // alternating on one box (profiles/r6/highq)
+        static const int bins = std::getenv("HZ_MACC_BINS") ? std::atoi(std::getenv("HZ_MACC_BINS")) : 16;
+        if (bins == 64) launch_macc<64>(Qp, B, H, Z, Y, Q, s);
+        else if (bins == 16) launch_macc<16>(Qp, B, H, Z, Y, Q, s);
+        else launch_macc<32>(Qp, B, H, Z, Y, Q, s);
         return;
     }
     if (Qp == 8) hipLaunchKernelGGL((resp_mac_kernel_lds<8, BPW>), grid, dim3(256), (mac_lds_bytes<8, BPW>()), s, H, Z, Y, Q, B);
@@ -1018,13 +1042,22 @@ int modal_prepare(hz_fb* h) {
     return HZ_OK;
 }
 
-void modal_args(hz_fb* h, const double* xw, double* out, hz_modal::ModalArgs* a) {
+// the window of the call's last K inputs: [history n.. | call] for calls n < K, else the call's tail
+void modal_args(hz_fb* h, const double* hist, const double* x, long n, double* out, hz_modal::ModalArgs* a) {
     using namespace hz_modal;
     hz_fb::Resp& R = h->resp;
     const long K = R.K;
     *a = ModalArgs();
     a->on = 1;
-    a->xw = xw;
+    if (n >= K) {
+        a->xw = x + (n - K);
+        a->xw2 = x + (n - K);
+        a->split = 0;
+    } else {
+        a->xw = hist + n;
+        a->xw2 = x;
+        a->split = K - n;
+    }
     a->K = K;
     a->S = R.mS;
     a->wR = R.d_mtab;
@@ -1213,13 +1246,14 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     const bool col = R.col_on && col_q_ok(Q);
     // banks on one pole circle: the modal states (hz_fb_modal.h) instead of the MFMA pass, phase 1
     // in the forward kernel, phase 2 in the inverse kernel
-    const bool modal = !lazy && n >= K && R.modal_on && R.modal_ok && !col;
+    // (calls shorter than K too: the window is the history's tail and the call, hz_fb_modal.h win())
+    const bool modal = !lazy && n >= 3 && R.modal_on && R.modal_ok && !col;
     const bool chained = !lazy && n >= K && h->order <= 2 && !modal;
     const bool inside = chained || modal;   // the states come out of the transform kernels
     hz_state::StateArgs st = hz_state::StateArgs();
     if (chained) HZ_TRY(fb_state_chained(h, d_in + (n - K), K, h->d_ystate[h->scur ^ 1], &st));
     hz_modal::ModalArgs md = hz_modal::ModalArgs();
-    if (modal) modal_args(h, d_in + (n - K), h->d_ystate[h->scur ^ 1], &md);
+    if (modal) modal_args(h, R.d_hist[R.hcur], d_in, n, h->d_ystate[h->scur ^ 1], &md);
     const int so = chained ? h->order : 0;
     const int nmac = (kH / 256) * ((B + kMacR - 1) / kMacR);
     int dg_fx = 0, dg_ix = 0, dg_i0 = 0, dg_n1 = 0;   // (diagnostic stamps) modal workgroups per launch

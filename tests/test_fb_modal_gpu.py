@@ -60,7 +60,10 @@ def test_modal_plan_flags(gpu_lib):
 
 
 @pytest.mark.parametrize("N,R,centre,n", [(4096, 0.999, 1.0, 200_000), (2048, 0.999, 0.5, 200_000),
-                                          (4096, 0.9999, 1.0, 600_000)])
+                                          (4096, 0.9999, 1.0, 600_000),
+                                          # calls shorter than the horizon (K = 507,904): the modal
+                                          # window is the history's tail plus the call (round 6)
+                                          (4096, 0.9999, 1.0, 480_000), (1024, 0.999, 1.0, 30_000)])
 def test_modal_matches_matrix_core_pass(gpu_lib, N, R, centre, n):
     fwd, back = resonant_coefficients(N, R, centre)
     gm, gc = _bank(N, fwd, back, modal=True), _bank(N, fwd, back, modal=False)
@@ -78,7 +81,9 @@ def test_modal_matches_matrix_core_pass(gpu_lib, N, R, centre, n):
     # both against the numpy model of the modal pass (itself within 3e-13 of the restatement:
     # tests/test_modal_model_cpu.py) over the call's last K inputs
     K = gm.response_info()[0]
-    ref, _ = mm.states(xs[-1][-K:], fwd, back, np.ones(N), exc_direct=False)
+    win = np.concatenate(xs)[-K:]   # the last K inputs (across calls when the call is shorter)
+    assert len(win) == K
+    ref, _ = mm.states(win, fwd, back, np.ones(N), exc_direct=False)
     ref = ref.reshape(-1)
     em = np.max(np.abs(sm[reg] - ref[reg])) / scale
     ec = np.max(np.abs(sc[reg] - ref[reg])) / scale
@@ -86,7 +91,7 @@ def test_modal_matches_matrix_core_pass(gpu_lib, N, R, centre, n):
     assert ec <= 1e-8, (em, ec)   # the matrix-core pass: its FP64 MFMA chains over the window
     if exc.any():   # the direct sums against the model's (long-double response, numpy dot)
         e = np.repeat(exc, 2)
-        dref = mm.direct(xs[-1][-K:], fwd[-1], back[-1], 1.0)
+        dref = mm.direct(win, fwd[-1], back[-1], 1.0)
         es = np.max(np.abs(sm[e] - dref)) / np.max(np.abs(dref))
         ecx = np.max(np.abs(sc[e] - dref)) / np.max(np.abs(dref))
         assert es <= 1e-10, (es, ecx)
