@@ -656,6 +656,57 @@ def general_softclip_figures(Filterbank, device, stream, x, y, S, traffic=True, 
     return out
 
 
+def setter_churn_figure(fb, x, y, nb, stream_rate, B=1024, every=4800, nbands=9):
+    """1024-sample calls with mix() on `nbands` random bands every `every` samples: device-resident
+    calls issued back to back (against `streaming`), then host buffers per call (against
+    streaming.end_to_end_host_buffers); the path of every call and the setters applied as
+    transients"""
+    import torch
+    from huygens_amd._lib import HZ_FB_PATH_STREAM
+    rng = np.random.default_rng(17)
+    N = fb.N
+
+    def setters(i):
+        if (i * B) // every != ((i - 1) * B) // every:
+            for b, v in zip(rng.choice(N, nbands, replace=False), rng.uniform(0.5, 1.5, nbands)):
+                fb.mix(int(b), float(v))
+            return 1
+        return 0
+
+    def run(k, host=None):
+        n_set = streamed = 0
+        for i in range(k):
+            n_set += setters(i)
+            if host is None:
+                fb.process_device(x.data_ptr() + 8 * B * i, y.data_ptr() + 8 * B * i, B)
+            else:
+                fb.process_host(host[0].data_ptr() + 8 * B * i, host[1].data_ptr() + 8 * B * i, B)
+            streamed += fb.last_path() == HZ_FB_PATH_STREAM
+        return n_set, streamed
+
+    run(16)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n_set, streamed = run(nb)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    hx = torch.empty(nb * B, dtype=torch.float64).pin_memory()
+    hy = torch.empty(nb * B, dtype=torch.float64).pin_memory()
+    hx.copy_(x[:nb * B].cpu())
+    t1 = time.perf_counter()
+    h_set, h_streamed = run(nb, (hx, hy))
+    dth = time.perf_counter() - t1
+    us = 1e6 * dt / nb
+    stat_us = 1e6 * N * B / stream_rate
+    return {"us_per_block": us, "band_samples_per_s": N * B * nb / dt, "blocks": nb, "setters": n_set,
+            "bands_per_setter": nbands, "setter_every_samples": every, "blocks_streamed": streamed,
+            "vs_converged_streaming": us / stat_us,
+            "host_buffers": {"us_per_block": 1e6 * dth / nb, "setters": h_set, "blocks_streamed": h_streamed},
+            "note": "mix() on 9 random bands every 4800 samples between 1024-sample process() calls; the bank keeps "
+                    "streaming with the gain transient as a second convolution (hz_fb_stream.hip); "
+                    "vs_converged_streaming = us_per_block over `streaming`'s converged figure"}
+
+
 def launch_plan(gpus: int, env) -> tuple[str, str | None]:
     """What `bench.py --gpus N` does in this environment (no torch / HIP import before it):
     'run' (world matches), 'relaunch' (N > 1 and no launcher: rerun under torch.distributed.run),
@@ -1106,6 +1157,13 @@ def main():
                                  "block (reference-equivalent); achieved = the streaming engine's own FP64 work "
                                  "(bench.stream_block_flops) over the same time"},
         }
+
+    # setter churn: the reference demos retarget mix() on every MIDI note
+    # (tests/filterbank.cpp:217-252) -- here 9 random bands every 4800 samples (100 ms) over the
+    # 1024-sample calls; the streaming engine keeps running with a transient term (hz_fb_stream.hip
+    # fb_stream_gain_setter).  Last figure on the main handle: its gains change.
+    if world == 1 and args.stream_blocks > 0 and stream_rate and args.side_steps > 0:
+        side["setter_churn"] = setter_churn_figure(fb, x, y, min(args.stream_blocks, S // 1024), stream_rate)
 
     # the high-Q variant of C2 (tests/eigen.cpp:26's r = 0.9999): the same
     # recipe at R = 0.9999, whose horizon (~0.4 M samples) is past the streaming head's 2^17 -- the

@@ -269,6 +269,31 @@ struct hz_fb {
             bool tail_async[2] = {false, false};   // that slot's convolution ran on the side stream
             hipStream_t side = nullptr;
             hipEvent_t ev_main = nullptr, ev_tail[2] = {nullptr, nullptr};
+            // gain transients (round 6): mix() while streaming keeps the engine.  The gain smoothers
+            // share s_g, so g_n(t) = gin_n + s_g^(t - dref) D_n and the mix is
+            //     out(t) = conv(h, x)(t) + s_g^(t - dref) conv(h_D, x)(t),  h_D = sum_n D_n r_n,
+            // both responses updated per setter from the per-band responses r_n (resident in HBM,
+            // [K][N]); a second launch per block (the D pass) adds the transient term
+            bool dmode = false;
+            long dref = 0;               // stream position the D term is referred to
+            double dmax = 0;             // bound on max |D_n| at dref (decay check)
+            long dsetters = 0;           // setters applied as transients
+            double* d_hD = nullptr;      // [K1] h_D
+            size_t hD_cap = 0;
+            double* d_HSD = nullptr;     // [K1/1024 + 8][33][32] its spectra
+            size_t hsd_cap = 0;
+            double* d_CRD = nullptr;     // its C / R parities
+            double* d_rband = nullptr;   // [K1][N] r_n (pre = pin, no gain)
+            size_t rband_cap = 0;
+            bool rband_valid = false;
+            double* d_sgpow = nullptr;   // s_g^j, j < 1024
+            double sgpow_of = -1;        // the s_g it holds
+            double* d_delta = nullptr;   // a setter's (band, delta) list
+            size_t delta_cap = 0;
+            std::vector<double> h_delta;
+            std::vector<double> gin_base;   // the gins d_h is built with
+            bool prime_main = false;     // C / R of the main pass to recompute (h changed, ring valid)
+            bool prime_d = false;        // ... of the D pass
         } st;
     } resp;
     // per-sample path (hz_fb_rt.hip): OP_FB requests to the device's per-sample server (hz_rt.hip)
@@ -408,6 +433,9 @@ int fb_stream_upkeep(hz_fb* h);        // smoothers and x history over the strea
 int fb_stream_to_hist(hz_fb* h);       // the ring's history back to resp.d_hist (long calls)
 void fb_stream_reset(hz_fb* h);        // state overwritten (set_state, tick)
 void fb_stream_free(hz_fb* h);
+bool fb_stream_gain_setter(hz_fb* h);     // a gin-only setter applied as a streaming transient
+bool fb_stream_dmode(const hz_fb* h);     // a gain transient is streaming (gains still moving)
+void fb_stream_dclear(hz_fb* h);          // leave the transient mode (the response is rebuilt)
 // the streaming engine's response tail (hz_fb_resp.hip): partition spectra of h[K1, K), and the
 // convolution out[i] = sum_{tau < Kt} h[K1 + tau] u[Kt + i - tau], i < n, of a contiguous u
 int fb_resp_tail_spectra(hz_fb* h, long K1);

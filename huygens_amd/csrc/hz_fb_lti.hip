@@ -1188,6 +1188,7 @@ bool fb_lti_gemm_geom(int geom) { return kLtiGeoms[geom].L >= 64; }
 // largest target: the LTI engine then computes the same outputs to ~2^-60
 bool fb_converged(hz_fb* h) {
     if (h->converged) return true;  // targets unchanged since: the smoothers only get closer
+    if (h->resp.st.dmode) return false;   // a streaming gain transient: gains moving (O(1) decay check there)
     fb_mirror_sync(h);
     double pmax = 0, gmax = 0;
     for (int b = 0; b < h->N; ++b) {

@@ -1091,6 +1091,8 @@ namespace hz_fbi {
 void fb_resp_init(hz_fb* h) { h->resp.mode = HZ_FB_RESP_EAGER; }
 
 void fb_resp_invalidate(hz_fb* h, bool coefficients) {
+    fb_stream_dclear(h);
+    if (coefficients) h->resp.st.rband_valid = false;
     h->resp.run = 0;
     h->resp.h_valid = false;
     h->resp.over_valid = false;
@@ -1157,6 +1159,7 @@ int fb_resp_track(hz_fb* h, const double* d_in, long n, bool conv) {
     if (R.mode == HZ_FB_RESP_OFF || !conv || h->order == 0 || h->path_mode != HZ_FB_PATH_AUTO) {
         R.run = 0;
         R.st.fdl_valid = false;
+        fb_stream_dclear(h);
         return HZ_OK;
     }
     HZ_TRY(fb_stream_to_hist(h));   // after streamed calls

@@ -161,6 +161,9 @@ struct StreamArgs {
     long long* flags;
     long long seq;
     const double* tail2;  // [1024] the response tail's contribution to this block (null: none)
+    // (D pass: a gain transient's term, added to out) s_g^(pos - dref) and s_g^j (j < 1024)
+    double dscale;
+    const double* sgpow;
 };
 
 // all of this workgroup's stores complete, then one system-scope release of the flag
@@ -257,7 +260,12 @@ union StreamLds {
 //   blocks [66, 82) 64 outputs each: head (h[0..1023] direct, the partition-0 term of overlap-save)
 //                   + tail (the 33 columns Cin of the previous launch, Hermitian-combined)
 // QI = Q / 8: partitions per MAC thread.
-template <int QI>
+// DP (the D pass of a gain transient, mix() while streaming): the same three roles for the transient
+// response h_D (HS = its spectra, h = its taps, C / R its own parities) over the SAME window spectra
+// -- the transform role reads this block's Z_b from the ring (the main pass of this block wrote it)
+// instead of transforming the window, nothing goes into the ring, and the output role ADDS
+// s_g^(t - dref) (head + tail) to the main pass's outputs.
+template <int QI, bool DP>
 __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
     __shared__ StreamLds u;
     const int t = threadIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
@@ -266,30 +274,33 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
         // ---------------- transform column
         ColLds& s = u.col;
         const int c = blk;
-        double v[8];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = a.line[a.prev + 32 * (g + 8 * i) + j];
-#pragma unroll
-        for (int i = 4; i < 8; ++i) v[i] = a.x[32 * (g + 8 * i - 32) + j];
-        double2 h1 = make_double2(0.0, 0.0), h2 = h1, z1 = h1, rn = h1;
+        double2 h1 = make_double2(0.0, 0.0), h2 = h1, z1 = h1, rn = h1, x0 = h1;
         if (t < 32) {
             h1 = a.HS[((long)1 * kCols + c) * 32 + t];
             h2 = a.HS[((long)2 * kCols + c) * 32 + t];
             z1 = a.ZS[((long)ring_slot(a.head, 1, a.Q) * kCols + c) * 32 + t];
             rn = a.Rin[c * 32 + t];
+            if (DP) x0 = a.ZS[((long)a.head * kCols + c) * 32 + t];   // Z_b, from this block's main pass
         }
         ColTw ct;
         ct.load(a.tw, c, j, g);
         const double2 tcol = a.tw[kTw2k + j * c];
-        const double2 a1 = stage1(v, ct.t64);
-        if (l < 32) s.a[w][j] = a1;
-        __syncthreads();
-        const double2 xp = stage3(s, g, ct.t2k, ct.t32);
-        if (l < 32) s.x[w][j] = xp;
-        __syncthreads();
+        if constexpr (!DP) {
+            double v[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = a.line[a.prev + 32 * (g + 8 * i) + j];
+#pragma unroll
+            for (int i = 4; i < 8; ++i) v[i] = a.x[32 * (g + 8 * i - 32) + j];
+            const double2 a1 = stage1(v, ct.t64);
+            if (l < 32) s.a[w][j] = a1;
+            __syncthreads();
+            const double2 xp = stage3(s, g, ct.t2k, ct.t32);
+            if (l < 32) s.x[w][j] = xp;
+            __syncthreads();
+        }
         if (t < 32) {
-            const double2 X = cadd(cadd(s.x[0][t], s.x[1][t]), cadd(s.x[2][t], s.x[3][t]));
-            a.ZS[((long)a.head * kCols + c) * 32 + t] = X;
+            const double2 X = DP ? x0 : cadd(cadd(s.x[0][t], s.x[1][t]), cadd(s.x[2][t], s.x[3][t]));
+            if (!DP) a.ZS[((long)a.head * kCols + c) * 32 + t] = X;
             s.y[t] = cadd(cadd(cmul(h1, X), cmul(h2, z1)), rn);
         }
         __syncthreads();
@@ -348,7 +359,7 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
         if (t < 64) s.tw[t] = twv;
         __syncthreads();
         // the block's samples into the ring (both mirror positions), for the next calls
-        if (t < 64) {
+        if (!DP && t < 64) {
             const double xv = s.sx[1023 + t];
             const long kk = a.wpos + t0 + t;
             a.line[kk] = xv;
@@ -395,7 +406,10 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
 #pragma unroll
             for (int q = 0; q < 32; ++q) y += s.part[q][t];
             const double tail = (s.tpart[0][t] + s.tpart[1][t]) + (s.tpart[2][t] + s.tpart[3][t]);
-            a.out[t0 + t] = a.tail2 ? (y + tail) + a.tail2[t0 + t] : y + tail;
+            if (DP)
+                a.out[t0 + t] += (a.dscale * a.sgpow[t0 + t]) * (y + tail);
+            else
+                a.out[t0 + t] = a.tail2 ? (y + tail) + a.tail2[t0 + t] : y + tail;
         }
         post_done(a);
     }
@@ -410,14 +424,69 @@ BlockKernel pick_impl(int qi, std::integer_sequence<int, I...>) {
 }
 template <int QI>
 struct BlockK {
-    static constexpr BlockKernel fn = stream_block_kernel<QI>;
+    static constexpr BlockKernel fn = stream_block_kernel<QI, false>;
+};
+template <int QI>
+struct BlockKD {
+    static constexpr BlockKernel fn = stream_block_kernel<QI, true>;
 };
 template <int QI>
 struct Prime2K {
     static constexpr BlockKernel fn = stream_prime2_kernel<QI>;
 };
 BlockKernel pick_block(int qi) { return pick_impl<BlockK>(qi, std::make_integer_sequence<int, 16>()); }
+BlockKernel pick_block_d(int qi) { return pick_impl<BlockKD>(qi, std::make_integer_sequence<int, 16>()); }
 BlockKernel pick_prime2(int qi) { return pick_impl<Prime2K>(qi, std::make_integer_sequence<int, 16>()); }
+
+// Per-band responses r[tau][n] (tau < K, time-major so a wave's stores are coalesced over its 64
+// bands): band n's impulse response at pre = pin_n by the reference recurrence in the oracle's
+// operation order (filterbank.h:178-179, as resp_h_kernel), no gain.  Once per coefficient / pre-amp
+// set, when the first gain transient streams.
+template <int O>
+__global__ __launch_bounds__(64) void stream_rband_kernel(const double* __restrict__ F, const double* __restrict__ B,
+                                                          const double* __restrict__ pin, int nbands, long K,
+                                                          double* __restrict__ r) {
+#pragma clang fp contract(off)
+    const int band = blockIdx.x * 64 + threadIdx.x;
+    if (band >= nbands) return;
+    double f[O + 1], b[O], y[O];
+#pragma unroll
+    for (int i = 0; i <= O; ++i) f[i] = F[(long)band * (O + 1) + i];
+#pragma unroll
+    for (int k = 0; k < O; ++k) {
+        b[k] = B[(long)band * O + k];
+        y[k] = 0.0;
+    }
+    const double p = pin[band];
+    for (long t = 0; t < K; ++t) {
+        double ff = 0.0;
+#pragma unroll
+        for (int i = 0; i <= O; ++i)
+            if (t == i) ff = f[i];
+        double bs = 0.0;
+#pragma unroll
+        for (int k = 0; k < O; ++k) bs += b[k] * y[k];
+        const double yt = ff * p - bs;
+#pragma unroll
+        for (int k = O - 1; k >= 1; --k) y[k] = y[k - 1];
+        y[0] = yt;
+        r[t * nbands + band] = yt;
+    }
+}
+
+// A gain setter as a transient: d[tau] = sum_i delta_i r[tau][band_i] (the setter's bands in list
+// order), h += d (the new targets), h_D = rebase h_D - d (D_n = g_n(t) - gin_n loses delta_n)
+__global__ __launch_bounds__(256) void stream_churn_kernel(const double* __restrict__ r, int nbands, long K,
+                                                           const double* __restrict__ delta, int m, double rebase,
+                                                           double* __restrict__ h, double* __restrict__ hD) {
+    const long tau = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tau >= K) return;
+    const double* row = r + tau * nbands;
+    double d = 0.0;
+    for (int i = 0; i < m; ++i) d = fma(delta[2 * i + 1], row[(int)delta[2 * i]], d);
+    h[tau] += d;
+    hD[tau] = rebase * hD[tau] - d;
+}
 
 // line[i] = line[i + R] = src[i], i < n, from write position wpos
 __global__ __launch_bounds__(256) void stream_put_kernel(const double* __restrict__ src, long n, double* __restrict__ line,
@@ -574,7 +643,25 @@ StreamArgs stream_args(hz_fb* h) {
     a.flags = nullptr;
     a.seq = 0;
     a.tail2 = nullptr;
+    a.dscale = 0.0;
+    a.sgpow = nullptr;
     return a;
+}
+
+// the D pass's operands: h_D's spectra and taps, its own C / R parities (same parity scheme)
+void d_args(hz_fb* h, StreamArgs* a) {
+    hz_fb::Resp::Stream& S = h->resp.st;
+    const size_t col = (size_t)kCols * 32;
+    double2* C = (double2*)S.d_CRD;
+    double2* Rb = C + 2 * col;
+    const int b = (int)(S.blk & 1);
+    a->HS = (const double2*)S.d_HSD;
+    a->h = S.d_hD;
+    a->Cin = C + b * col;
+    a->Cout = C + (b ^ 1) * col;
+    a->Rin = Rb + (b ^ 1) * col;
+    a->Rout = Rb + b * col;
+    a->sgpow = S.d_sgpow;
 }
 
 // the tail's contribution to the outputs of epoch e, out[i] = sum_{tau >= K1} h[tau] x[eE + i - tau]
@@ -634,6 +721,15 @@ bool fb_stream_eligible(hz_fb* h, long n, bool conv) {
 int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
     hz_fb::Resp& R = h->resp;
     hz_fb::Resp::Stream& S = R.st;
+    if (S.dmode) {   // the transient has decayed below 2^-60 of the targets: plain streaming from here
+        double gmax = 0;
+        for (double g : h->gin) gmax = std::max(gmax, std::fabs(g));
+        const double sd = (double)powl((long double)h->sg, (long double)(S.pos - S.dref));
+        if (sd * S.dmax <= 0x1p-60 * gmax) {
+            fb_stream_dclear(h);   // the response is rebuilt for the long-call engine's spectra too
+            h->converged = true;   // pre-amps converged at the first setter, gains now
+        }
+    }
     HZ_TRY(fb_resp_build(h));   // h (and the band-state operands) for the current bank
     HZ_TRY(stream_setup(h));
     const int Q = (int)(S.K1 / kSP);
@@ -651,6 +747,8 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
             S.tail_launched = -1;
         }
         S.hs_gen = R.h_gen;
+        S.gin_base = h->gin;   // the targets this h was built with (gain transients start from them)
+        if (S.fdl_valid) S.prime_main = true;   // a rebuilt h with the ring still valid
     }
     if (!S.line_hist) HZ_TRY(hist_to_line(h));
     if (!S.fdl_valid) {   // the ring of window spectra, the first block's tail columns and R
@@ -661,6 +759,26 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
         HZ_TRY_HIP(hipGetLastError());
         S.blk = 0;
         S.fdl_valid = true;
+        S.prime_main = false;
+        S.prime_d = S.dmode;
+    }
+    if (S.prime_main) {   // h changed (a gain transient) with the ring still valid: C_b and R_{b+1} again
+        const long blk = S.blk;
+        S.blk = blk - 1;   // as the launch before this block writes them
+        hipLaunchKernelGGL(pick_prime2(Q / 8), dim3(kCols), dim3(kT), 0, h->stream, stream_args(h));
+        HZ_TRY_HIP(hipGetLastError());
+        S.blk = blk;
+        S.prime_main = false;
+    }
+    if (S.dmode && S.prime_d) {   // the D pass's C_b and R_{b+1} from the ring and h_D's spectra
+        const long blk = S.blk;
+        S.blk = blk - 1;
+        StreamArgs ad = stream_args(h);
+        S.blk = blk;
+        d_args(h, &ad);
+        hipLaunchKernelGGL(pick_prime2(Q / 8), dim3(kCols), dim3(kT), 0, h->stream, ad);
+        HZ_TRY_HIP(hipGetLastError());
+        S.prime_d = false;
     }
     if (S.tail) HZ_TRY(tail_schedule(h));
     StreamArgs a = stream_args(h);
@@ -677,6 +795,17 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
     }
     hipLaunchKernelGGL(pick_block(Q / 8), dim3(2 * kCols + kSP / 64), dim3(kT), 0, h->stream, a);
     HZ_TRY_HIP(hipGetLastError());
+    if (S.dmode) {   // the transient term: s_g^(t - dref) conv(h_D, x), added to the block's outputs
+        StreamArgs ad = a;
+        d_args(h, &ad);
+        ad.flags = nullptr;
+        ad.tail2 = nullptr;
+        // (compute() smooths before the sample's output, filterbank.h:172-173: D is g(dref - 1) -
+        // gin, so sample t carries s_g^(t - dref + 1))
+        ad.dscale = (double)powl((long double)h->sg, (long double)(S.pos - S.dref + 1));
+        hipLaunchKernelGGL(pick_block_d(Q / 8), dim3(2 * kCols + kSP / 64), dim3(kT), 0, h->stream, ad);
+        HZ_TRY_HIP(hipGetLastError());
+    }
     if (e) {
         HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
         HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
@@ -704,6 +833,7 @@ int fb_stream_track(hz_fb* h, const double* d_in, long n, bool conv) {
     }
     if (!fb_stream_trackable(h, n, conv)) {
         R.run = 0;
+        fb_stream_dclear(h);
         return HZ_OK;
     }
     // a new horizon (coefficients changed: R.run restarted at 0) re-lays the ring out for it; the
@@ -772,6 +902,7 @@ int fb_stream_to_hist(hz_fb* h) {
 }
 
 void fb_stream_reset(hz_fb* h) {
+    fb_stream_dclear(h);
     hz_fb::Resp::Stream& S = h->resp.st;
     (void)tail_quiet(S);
     S.tail_launched = -1;
@@ -780,10 +911,115 @@ void fb_stream_reset(hz_fb* h) {
     S.fdl_valid = false;
 }
 
+bool fb_stream_dmode(const hz_fb* h) { return h->resp.st.dmode; }
+
+// leave the transient mode where the history stops (a call the ring does not stream, a reset): d_h
+// still equals sum_n gin_n r_n up to roundoff, but the long-call engine's spectra were built before
+// the setters -- rebuilt with the response when next needed
+void fb_stream_dclear(hz_fb* h) {
+    hz_fb::Resp::Stream& S = h->resp.st;
+    if (!S.dmode && S.dsetters == 0) return;
+    if (S.dmode || S.dsetters) h->resp.h_valid = false;
+    S.dmode = false;
+    S.dsetters = 0;
+    S.prime_main = S.prime_d = false;
+}
+
+// A setter that changed only gains (mix / open) while the bank streams stationary: keep streaming.
+// h += sum_n (gin'_n - gin_n) r_n, h_D = s_g^(pos - dref) h_D - (the same sum), dref = pos; both
+// responses' spectra again; the next block re-primes both passes' C / R from the (valid) ring.
+// false: not applicable here (the caller invalidates the response as before).
+bool fb_stream_gain_setter(hz_fb* h) {
+    hz_fb::Resp& R = h->resp;
+    hz_fb::Resp::Stream& S = R.st;
+    const int N = h->N, O = h->order;
+    if (!S.on || !S.line_hist || !S.fdl_valid || !R.h_valid || S.hs_gen != R.h_gen || R.run < R.K || R.over_valid ||
+        S.tail || R.mode == HZ_FB_RESP_OFF || h->dist_id != HZ_DIST_NONE || h->path_mode != HZ_FB_PATH_AUTO || O == 0 ||
+        (int)S.gin_base.size() != N)
+        return false;
+    const long K = S.K1;
+    if ((double)K * N * 8.0 > 8.0 * (1L << 30)) return false;   // the per-band responses stay <= 8 GiB
+    // pre-amps converged (boost() invalidates instead); gains converged to gin_base unless a transient
+    // already streams (then g_n(t) - gin_base_n = s_g^(t - dref) D_n by construction)
+    fb_mirror_sync(h);
+    double pmax = 0, gmax = 0;
+    for (int b = 0; b < N; ++b) {
+        pmax = std::max(pmax, std::fabs(h->pin[b]));
+        gmax = std::max(gmax, std::fabs(S.gin_base[b]));
+    }
+    for (int b = 0; b < N; ++b) {
+        if (!(std::fabs(h->pg_host[2 * (size_t)b] - h->pin[b]) <= 0x1p-60 * pmax)) return false;
+        if (!S.dmode && !(std::fabs(h->pg_host[2 * (size_t)b + 1] - S.gin_base[b]) <= 0x1p-60 * gmax)) return false;
+    }
+    // the setter's bands
+    S.h_delta.clear();
+    double dmx = 0;
+    for (int b = 0; b < N; ++b) {
+        const double d = h->gin[b] - S.gin_base[b];
+        if (d != 0.0) {
+            S.h_delta.push_back((double)b);
+            S.h_delta.push_back(d);
+            dmx = std::max(dmx, std::fabs(d));
+        }
+    }
+    const int m = (int)(S.h_delta.size() / 2);
+    if (m == 0) return true;
+    auto alloc = [](double** p, size_t* cap, size_t need) -> int { return s_alloc(p, cap, need); };
+    const size_t col = (size_t)kCols * 32 * 2;
+    const int Q = (int)(K / kSP);
+    if (alloc(&S.d_rband, &S.rband_cap, (size_t)K * N) != HZ_OK || alloc(&S.d_hD, &S.hD_cap, (size_t)K) != HZ_OK ||
+        alloc(&S.d_delta, &S.delta_cap, S.h_delta.size()) != HZ_OK)
+        return false;
+    const size_t hcap = S.hsd_cap;
+    if (alloc(&S.d_HSD, &S.hsd_cap, (size_t)(Q + 8) * col) != HZ_OK) return false;
+    if (S.hsd_cap != hcap && hipMemset(S.d_HSD, 0, sizeof(double) * S.hsd_cap) != hipSuccess) return false;
+    if (!S.d_CRD && hipMalloc(&S.d_CRD, sizeof(double) * 4 * col) != hipSuccess) return false;
+    if (S.sgpow_of != h->sg) {
+        std::vector<double> sp(kSP);
+        for (int j = 0; j < kSP; ++j) sp[j] = (double)powl((long double)h->sg, (long double)j);
+        if (!S.d_sgpow && hipMalloc(&S.d_sgpow, sizeof(double) * kSP) != hipSuccess) return false;
+        if (hipMemcpy(S.d_sgpow, sp.data(), sizeof(double) * kSP, hipMemcpyHostToDevice) != hipSuccess) return false;
+        S.sgpow_of = h->sg;
+    }
+    if (!S.rband_valid) {   // r_n at the current coefficients and pre-amps (R.d_coef: resp_build_h)
+        const double* F = R.d_coef;
+        const double* Bc = R.d_coef + (size_t)N * (O + 1);
+        const unsigned g = (unsigned)((N + 63) / 64);
+        switch (O) {
+        case 1: hipLaunchKernelGGL(stream_rband_kernel<1>, dim3(g), dim3(64), 0, h->stream, F, Bc, (const double*)h->d_pin, N, K, S.d_rband); break;
+        case 2: hipLaunchKernelGGL(stream_rband_kernel<2>, dim3(g), dim3(64), 0, h->stream, F, Bc, (const double*)h->d_pin, N, K, S.d_rband); break;
+        case 3: hipLaunchKernelGGL(stream_rband_kernel<3>, dim3(g), dim3(64), 0, h->stream, F, Bc, (const double*)h->d_pin, N, K, S.d_rband); break;
+        default: hipLaunchKernelGGL(stream_rband_kernel<4>, dim3(g), dim3(64), 0, h->stream, F, Bc, (const double*)h->d_pin, N, K, S.d_rband); break;
+        }
+        if (hipGetLastError() != hipSuccess) return false;
+        S.rband_valid = true;
+    }
+    if (!S.dmode && hipMemsetAsync(S.d_hD, 0, sizeof(double) * K, h->stream) != hipSuccess) return false;
+    const double rebase = S.dmode ? (double)powl((long double)h->sg, (long double)(S.pos - S.dref)) : 0.0;
+    if (hipMemcpyAsync(S.d_delta, S.h_delta.data(), sizeof(double) * S.h_delta.size(), hipMemcpyHostToDevice,
+                       h->stream) != hipSuccess)
+        return false;
+    hipLaunchKernelGGL(stream_churn_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, h->stream,
+                       (const double*)S.d_rband, N, K, (const double*)S.d_delta, m, rebase, R.d_h, S.d_hD);
+    hipLaunchKernelGGL(stream_hs_kernel, dim3(kCols, (unsigned)Q), dim3(kT), 0, h->stream, (const double*)R.d_h,
+                       (const double2*)S.d_tw, (double2*)S.d_HS);
+    hipLaunchKernelGGL(stream_hs_kernel, dim3(kCols, (unsigned)Q), dim3(kT), 0, h->stream, (const double*)S.d_hD,
+                       (const double2*)S.d_tw, (double2*)S.d_HSD);
+    if (hipGetLastError() != hipSuccess) return false;
+    S.dmax = rebase * S.dmax + dmx;
+    S.dref = S.pos;
+    S.dmode = true;
+    S.prime_main = S.prime_d = true;
+    ++S.dsetters;
+    S.gin_base = h->gin;
+    return true;
+}
+
 void fb_stream_free(hz_fb* h) {
     hz_fb::Resp::Stream& S = h->resp.st;
     (void)tail_quiet(S);
-    for (double* p : {S.d_line, S.d_ZS, S.d_HS, S.d_CR, S.d_tw, S.d_tH, S.d_tZ, S.d_tY, S.d_tout})
+    for (double* p : {S.d_line, S.d_ZS, S.d_HS, S.d_CR, S.d_tw, S.d_tH, S.d_tZ, S.d_tY, S.d_tout, S.d_hD, S.d_HSD,
+                      S.d_CRD, S.d_rband, S.d_sgpow, S.d_delta})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : {S.ev_main, S.ev_tail[0], S.ev_tail[1]})
         if (e) (void)hipEventDestroy(e);

@@ -659,9 +659,14 @@ int fb_upload(hz_fb* h) {
         hz_fbi::fb_resp_invalidate(h, true);
         uploaded = true;
     }
+    if (h->dirty_pin) h->resp.st.rband_valid = false;   // r_n are at pre = pin
+    // gains only, while the bank streams stationary: a transient of the streaming engine instead of
+    // a new response and K samples of history (hz_fb_stream.hip fb_stream_gain_setter)
+    const bool transient = h->dirty_gin && !h->dirty_pin && !uploaded && !h->tv_pending &&
+                           hz_fbi::fb_stream_gain_setter(h);
     if (h->dirty_pin || h->dirty_gin) {
         for (auto& st : h->lti_set) st.fmix_valid = false;
-        hz_fbi::fb_resp_invalidate(h, false);
+        if (!transient) hz_fbi::fb_resp_invalidate(h, false);
     }
     if (h->dirty_pin) {
         HZ_TRY_HIP(hipMemcpyAsync(h->d_pin, h->pin.data(), sizeof(double) * h->N, hipMemcpyHostToDevice,
@@ -885,12 +890,14 @@ int fb_launch(hz_fb* h, const double* d_in, double* d_out, long n) {
     // converged for the whole call (the smoothers only get closer): the LTI engine may run, and
     // the stationary engine's history keeps counting
     const bool conv = h->order > 0 && n >= 16 && fb_converged(h);
+    // a gain transient streams with the gains still moving (hz_fb_stream.hip)
+    const bool sconv = conv || (h->order > 0 && fb_stream_dmode(h));
     // a time-sharded handle (multi-GPU) runs stationary exactly when the caller armed it on
     // every rank; an armed handle that cannot (its history is short, or a setter or short call
     // intervened) fails loudly instead of leaving its peers on another engine
     const bool tshard = fb_resp_time_sharded(h);
     // 1024-sample blocks of a stationary bank: one launch each (hz_fb_stream.hip)
-    if (!tshard && fb_stream_eligible(h, n, conv)) {
+    if (!tshard && fb_stream_eligible(h, n, sconv)) {
         HZ_TRY(fb_launch_stream(h, d_in, d_out, n));
         h->last_path = HZ_FB_PATH_STREAM;
         return HZ_OK;
