@@ -774,8 +774,8 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
         const long blk = S.blk;
         S.blk = blk - 1;
         StreamArgs ad = stream_args(h);
+        d_args(h, &ad);   // (its parities from blk - 1 too)
         S.blk = blk;
-        d_args(h, &ad);
         hipLaunchKernelGGL(pick_prime2(Q / 8), dim3(kCols), dim3(kT), 0, h->stream, ad);
         HZ_TRY_HIP(hipGetLastError());
         S.prime_d = false;
