@@ -656,6 +656,32 @@ def general_softclip_figures(Filterbank, device, stream, x, y, S, traffic=True, 
     return out
 
 
+def churn_cpp(x):
+    """tests/cpp/churn.cpp (the reference's language, C ABI on device buffers): the same churn from a
+    C++ caller, against its own converged calls; None when the compiler is unavailable"""
+    import shutil
+    import subprocess
+    import tempfile
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    d = tempfile.mkdtemp(prefix="hz_churn_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        fwd, back = c2_coefficients()
+        np.concatenate([np.asarray(fwd)[:, :3], np.asarray(back)[:, :2]], axis=1).astype(np.float64).tofile(
+            os.path.join(d, "coef.bin"))
+        np.ascontiguousarray(x, dtype=np.float64).tofile(os.path.join(d, "x.bin"))
+        lib = os.path.join(ROOT, "huygens_amd", "lib")
+        exe = os.path.join(d, "churn")
+        subprocess.run([hipcc, "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "cpp", "churn.cpp"), "-o", exe, "-L", lib, "-lhuygens_hip",
+                        f"-Wl,-rpath,{lib}"], check=True, capture_output=True, timeout=180)
+        r = subprocess.run([exe, d], check=True, capture_output=True, text=True, timeout=120)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # noqa: BLE001
+        return {"error": str(e)[:300]}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def setter_churn_figure(fb, x, y, nb, stream_rate, B=1024, every=4800, nbands=9):
     """1024-sample calls with mix() on `nbands` random bands every `every` samples: device-resident
     calls issued back to back (against `streaming`), then host buffers per call (against
@@ -684,7 +710,11 @@ def setter_churn_figure(fb, x, y, nb, stream_rate, B=1024, every=4800, nbands=9)
             streamed += fb.last_path() == HZ_FB_PATH_STREAM
         return n_set, streamed
 
-    run(16)
+    # untimed: the bank back to streaming first (the figures before may have reset its history):
+    # K samples of converged calls, without setters
+    warm = -(-fb.response_info()[0] // B) + 8
+    for i in range(warm):
+        fb.process_device(x.data_ptr() + 8 * B * (i % nb), y.data_ptr() + 8 * B * (i % nb), B)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     n_set, streamed = run(nb)
@@ -698,7 +728,9 @@ def setter_churn_figure(fb, x, y, nb, stream_rate, B=1024, every=4800, nbands=9)
     dth = time.perf_counter() - t1
     us = 1e6 * dt / nb
     stat_us = 1e6 * N * B / stream_rate
+    cpp = churn_cpp(x[:nb * B].cpu().numpy())
     return {"us_per_block": us, "band_samples_per_s": N * B * nb / dt, "blocks": nb, "setters": n_set,
+            "cpp_caller": cpp,
             "bands_per_setter": nbands, "setter_every_samples": every, "blocks_streamed": streamed,
             "vs_converged_streaming": us / stat_us,
             "host_buffers": {"us_per_block": 1e6 * dth / nb, "setters": h_set, "blocks_streamed": h_streamed},

@@ -277,13 +277,16 @@ struct hz_fb {
             bool dmode = false;
             long dref = 0;               // stream position the D term is referred to
             double dmax = 0;             // bound on max |D_n| at dref (decay check)
+            double gin_max = 0;          // max |gin_n| (the decay check's scale)
             long dsetters = 0;           // setters applied as transients
             double* d_hD = nullptr;      // [K1] h_D
             size_t hD_cap = 0;
             double* d_HSD = nullptr;     // [K1/1024 + 8][33][32] its spectra
             size_t hsd_cap = 0;
             double* d_CRD = nullptr;     // its C / R parities
-            double* d_rband = nullptr;   // [K1][N] r_n (pre = pin, no gain)
+            double* d_rband = nullptr;   // [N][K1] r_n (pre = pin, no gain)
+            double* d_dv = nullptr;      // [K1] a setter's update sum_n delta_n r_n
+            size_t dv_cap = 0;
             size_t rband_cap = 0;
             bool rband_valid = false;
             double* d_sgpow = nullptr;   // s_g^j, j < 1024
@@ -433,7 +436,8 @@ int fb_stream_upkeep(hz_fb* h);        // smoothers and x history over the strea
 int fb_stream_to_hist(hz_fb* h);       // the ring's history back to resp.d_hist (long calls)
 void fb_stream_reset(hz_fb* h);        // state overwritten (set_state, tick)
 void fb_stream_free(hz_fb* h);
-bool fb_stream_gain_setter(hz_fb* h);     // a gin-only setter applied as a streaming transient
+int fb_stream_gain_setter(hz_fb* h);      // a gin-only setter as a streaming transient (0: not applied,
+                                          // 1: applied, d_gin written; 2: applied, upload d_gin)
 bool fb_stream_dmode(const hz_fb* h);     // a gain transient is streaming (gains still moving)
 void fb_stream_dclear(hz_fb* h);          // leave the transient mode (the response is rebuilt)
 // the streaming engine's response tail (hz_fb_resp.hip): partition spectra of h[K1, K), and the

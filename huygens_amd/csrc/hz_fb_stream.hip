@@ -25,6 +25,7 @@
 // consecutive samples are contiguous), and are computed by the band-state pass
 // (hz_fb_state.hip) only when a later call, get_state, tick or a setter needs them.
 #include <cstdio>
+#include <type_traits>
 #include <utility>
 
 #include "hz_fb_impl.h"
@@ -139,6 +140,24 @@ __global__ __launch_bounds__(kT) void stream_hs_kernel(const double* __restrict_
                 HS + ((long)p * kCols + c) * 32);
 }
 
+// a gain transient's spectra by linearity: dS = the partition spectra of the update d (the same
+// column transform as stream_hs_kernel), HS += dS, HS_D = rebase HS_D - dS
+__global__ __launch_bounds__(kT) void stream_hsd_kernel(const double* __restrict__ d, const double2* __restrict__ tw,
+                                                        double rebase, double2* __restrict__ HS, double2* __restrict__ HSD) {
+    __shared__ ColLds s;
+    __shared__ double2 dS[32];
+    const int c = blockIdx.x, p = blockIdx.y;
+    const double* dp = d + (long)p * kSP;
+    col_forward(s, tw, c, [&](int n) { return n < kSP ? dp[n] * (1.0 / kSF) : 0.0; }, dS);
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        const long at = ((long)p * kCols + c) * 32 + threadIdx.x;
+        const double2 v = dS[threadIdx.x], a = HS[at], b = HSD[at];
+        HS[at] = make_double2(a.x + v.x, a.y + v.y);
+        HSD[at] = make_double2(rebase * b.x - v.x, rebase * b.y - v.y);
+    }
+}
+
 struct StreamArgs {
     const double* x;      // [1024] the call's input
     double* out;          // [1024]
@@ -161,7 +180,13 @@ struct StreamArgs {
     long long* flags;
     long long seq;
     const double* tail2;  // [1024] the response tail's contribution to this block (null: none)
-    // (D pass: a gain transient's term, added to out) s_g^(pos - dref) and s_g^j (j < 1024)
+    // (a gain transient, DUAL) h_D's spectra, taps and C / R parities; s_g^(pos - dref + 1), s_g^j
+    const double2* HSD;
+    const double* hD;
+    const double2* CDin;
+    double2* CDout;
+    const double2* RDin;
+    double2* RDout;
     double dscale;
     const double* sgpow;
 };
@@ -248,171 +273,230 @@ struct OutLds {
     double part[32][65];      // head partials [tap group][output]
     double tpart[4][64];      // tail partials [column group][output]
 };
+// (a gain transient, FUSED) the same for h_D
+struct OutLdsD {
+    OutLds m;
+    double shD[kSP];
+    double2 colD[kCols][32];
+    double partD[32][65];
+    double tpartD[4][64];
+};
 union StreamLds {
     ColLds col;
     OutLds out;
 };
+union StreamLdsD {
+    ColLds col;
+    OutLdsD out;
+};
+
+// ---- the three roles of a block launch (tests/stream_model.py) -------------------------------
+// transform column c: Z_b's bins from the window (WRITEZ: into the ring); Y_{b+1} = H_1 Z_b +
+// H_2 Z_{b-1} + R_{b+1}; its inverse column -> Cout (the next block's tail)
+template <bool WRITEZ>
+__device__ __forceinline__ void role_transform(const StreamArgs& a, const double2* __restrict__ HS,
+                                               const double2* __restrict__ Rin, double2* __restrict__ Cout,
+                                               ColLds& s, int c) {
+    const int t = threadIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = a.line[a.prev + 32 * (g + 8 * i) + j];
+#pragma unroll
+    for (int i = 4; i < 8; ++i) v[i] = a.x[32 * (g + 8 * i - 32) + j];
+    double2 h1 = make_double2(0.0, 0.0), h2 = h1, z1 = h1, rn = h1;
+    if (t < 32) {
+        h1 = HS[((long)1 * kCols + c) * 32 + t];
+        h2 = HS[((long)2 * kCols + c) * 32 + t];
+        z1 = a.ZS[((long)ring_slot(a.head, 1, a.Q) * kCols + c) * 32 + t];
+        rn = Rin[c * 32 + t];
+    }
+    ColTw ct;
+    ct.load(a.tw, c, j, g);
+    const double2 tcol = a.tw[kTw2k + j * c];
+    const double2 a1 = stage1(v, ct.t64);
+    if (l < 32) s.a[w][j] = a1;
+    __syncthreads();
+    const double2 xp = stage3(s, g, ct.t2k, ct.t32);
+    if (l < 32) s.x[w][j] = xp;
+    __syncthreads();
+    if (t < 32) {
+        const double2 X = cadd(cadd(s.x[0][t], s.x[1][t]), cadd(s.x[2][t], s.x[3][t]));
+        if (WRITEZ) a.ZS[((long)a.head * kCols + c) * 32 + t] = X;
+        s.y[t] = cadd(cadd(cmul(h1, X), cmul(h2, z1)), rn);
+    }
+    __syncthreads();
+    col_inverse_store(s, ct, tcol, Cout + c * 32);
+}
+
+// MAC column c: R_{b+2} = sum_{p >= 3} H_p Z_{b+2-p} over the ring -> Rout
+template <int QI>
+__device__ __forceinline__ void role_mac(const StreamArgs& a, const double2* __restrict__ HS, double2* __restrict__ Rout,
+                                         ColLds& s, int c) {
+    const int t = threadIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
+    double2 hv[QI], zv[QI];
+#pragma unroll
+    for (int i = 0; i < QI; ++i) {
+        const int p = 3 + g + 8 * i;   // < Q + 3; partitions past Q - 1 contribute nothing
+        // (masked: slot ring_slot(head, Q) is the one this launch's transform role writes)
+        const bool live = p < a.Q;
+        hv[i] = live ? HS[((long)p * kCols + c) * 32 + j] : make_double2(0.0, 0.0);
+        zv[i] = live ? a.ZS[((long)ring_slot(a.head, p - 2, a.Q) * kCols + c) * 32 + j] : make_double2(0.0, 0.0);
+    }
+    double2 r = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int i = 0; i < QI; ++i) r = cadd(r, cmul(hv[i], zv[i]));
+    r = half_sum(r);
+    if (l < 32) s.m[w][j] = r;
+    __syncthreads();
+    if (t < 32) Rout[c * 32 + t] = cadd(cadd(s.m[0][t], s.m[1][t]), cadd(s.m[2][t], s.m[3][t]));
+}
+
+// head: thread = 8 outputs (o8) x 32 taps (q): y[j] += h[tau] x[t0 + j - tau], partials into part
+__device__ __forceinline__ void head_partials(const double* __restrict__ sx, const double* __restrict__ sh,
+                                              double (*part)[65]) {
+    const int t = threadIdx.x, o8 = t & 7, q = t >> 3;
+    const int j0 = 8 * o8, tau0 = 32 * q;
+    double xs[39], hs[32], acc[8];
+#pragma unroll
+    for (int i = 0; i < 39; ++i) xs[i] = sx[1023 + j0 - tau0 - 31 + i];   // x[t0 + j0 - tau0 - 31 + i]
+#pragma unroll
+    for (int i = 0; i < 32; ++i) hs[i] = sh[tau0 + i];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc[r] = fma(hs[i], xs[31 + r - i], acc[r]);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) part[q][j0 + r] = acc[r];
+}
+
+// tail partials: output o (t & 63), columns c = 1 + cg + 4 i (cg = t >> 6)
+__device__ __forceinline__ void tail_partials(const double2 (*col)[32], const double2* __restrict__ tw, int t0,
+                                              double (*tpart)[64]) {
+    const int t = threadIdx.x, o = t & 63, cg = t >> 6;
+    const int n = t0 + o, m = n >> 5, n2 = n & 31, n1 = 32 + m;
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int c = 1 + cg + 4 * i;
+        if (c < 32) {
+            const double2 C = col[c][n2], wv = tw[(n1 * c) & 63];
+            acc = fma(wv.x, C.x, fma(wv.y, C.y, acc));
+        }
+    }
+    acc *= 2.0;
+    if (cg == 0) acc += col[0][n2].x + ((n1 & 1) ? -col[32][n2].x : col[32][n2].x);
+    tpart[cg][o] = acc;
+}
+
+// 64 outputs: head (h[0..1023] direct, the partition-0 term of overlap-save) + tail (the 33 columns
+// Cin of the previous launch, Hermitian-combined); DUAL (a gain transient): + s_g^(t - dref + 1) x
+// the same for h_D (its taps and columns)
+template <bool DUAL, class L>
+__device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
+    OutLds& s = [&]() -> OutLds& {
+        if constexpr (DUAL) return u.m;
+        else return u;
+    }();
+    const int t = threadIdx.x;
+    const int t0 = 64 * k;
+    // every global load of the thread in flight before the first LDS store (a load -> store
+    // chain per loop iteration waited one memory latency each): window positions 64k + 1 ..
+    // 64k + 1087 (2048-sample window: previous block | this block), h[0..1023], the columns
+    double xv[5], hv[4], hvD[4];
+    double2 cv[5], cvD[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const int i = min(t + q * kT, 1086);
+        const int wp = t0 + 1 + i;
+        xv[q] = wp < kSP ? a.line[a.prev + wp] : a.x[wp - kSP];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        hv[q] = a.h[t + q * kT];
+        if (DUAL) hvD[q] = a.hD[t + q * kT];
+    }
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        cv[q] = a.Cin[min(t + q * kT, kCols * 32 - 1)];
+        if (DUAL) cvD[q] = a.CDin[min(t + q * kT, kCols * 32 - 1)];
+    }
+    const double2 twv = a.tw[kTw64 + (t & 63)];
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+        if (t + q * kT < 1087) s.sx[t + q * kT] = xv[q];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s.sh[t + q * kT] = hv[q];
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+        if (t + q * kT < kCols * 32) (&s.col[0][0])[t + q * kT] = cv[q];
+    if constexpr (DUAL) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) u.shD[t + q * kT] = hvD[q];
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            if (t + q * kT < kCols * 32) (&u.colD[0][0])[t + q * kT] = cvD[q];
+    }
+    if (t < 64) s.tw[t] = twv;
+    __syncthreads();
+    // the block's samples into the ring (both mirror positions), for the next calls
+    if (t < 64) {
+        const double xw = s.sx[1023 + t];
+        const long kk = a.wpos + t0 + t;
+        a.line[kk] = xw;
+        a.line[kk + a.R] = xw;
+    }
+    head_partials(s.sx, s.sh, s.part);
+    tail_partials(s.col, s.tw, t0, s.tpart);
+    if constexpr (DUAL) {
+        head_partials(s.sx, u.shD, u.partD);
+        tail_partials(u.colD, s.tw, t0, u.tpartD);
+    }
+    __syncthreads();
+    if (t < 64) {
+        double y = 0.0;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) y += s.part[q][t];
+        const double tail = (s.tpart[0][t] + s.tpart[1][t]) + (s.tpart[2][t] + s.tpart[3][t]);
+        double o = a.tail2 ? (y + tail) + a.tail2[t0 + t] : y + tail;
+        if constexpr (DUAL) {
+            double yd = 0.0;
+#pragma unroll
+            for (int q = 0; q < 32; ++q) yd += u.partD[q][t];
+            const double taild = (u.tpartD[0][t] + u.tpartD[1][t]) + (u.tpartD[2][t] + u.tpartD[3][t]);
+            o += (a.dscale * a.sgpow[t0 + t]) * (yd + taild);
+        }
+        a.out[t0 + t] = o;
+    }
+}
 
 // One 1024-sample block, three roles with no data shared inside the launch (tests/stream_model.py):
-//   blocks [0, 33)  transform column c: Z_b's bins from the window, into the ring; Y_{b+1} = H_1 Z_b
-//                   + H_2 Z_{b-1} + R_{b+1}; its inverse column -> Cout (the next block's tail)
-//   blocks [33, 66) MAC column c: R_{b+2} = sum_{p >= 3} H_p Z_{b+2-p} over the ring -> Rout
-//   blocks [66, 82) 64 outputs each: head (h[0..1023] direct, the partition-0 term of overlap-save)
-//                   + tail (the 33 columns Cin of the previous launch, Hermitian-combined)
+//   blocks [0, 33)  transform column c
+//   blocks [33, 66) MAC column c
+//   blocks [66, 82) 64 outputs each: head + tail
+// DUAL (a gain transient, hz_fb_stream fb_stream_gain_setter): the transient response's roles in
+// the same launch -- its own transform columns (Z_b transformed again: no dependence on the main
+// transform role), its MAC columns (h_D's spectra, its C / R parities), and the output role adds
+// s_g^(t - dref + 1) (head_D + tail_D).  [82, 115) D transform, [115, 148) D MAC.
 // QI = Q / 8: partitions per MAC thread.
-// DP (the D pass of a gain transient, mix() while streaming): the same three roles for the transient
-// response h_D (HS = its spectra, h = its taps, C / R its own parities) over the SAME window spectra
-// -- the transform role reads this block's Z_b from the ring (the main pass of this block wrote it)
-// instead of transforming the window, nothing goes into the ring, and the output role ADDS
-// s_g^(t - dref) (head + tail) to the main pass's outputs.
-template <int QI, bool DP>
+template <int QI, bool DUAL>
 __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
-    __shared__ StreamLds u;
-    const int t = threadIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
+    using Lds = typename std::conditional<DUAL, StreamLdsD, StreamLds>::type;
+    __shared__ Lds u;
     const int blk = blockIdx.x;
+    constexpr int kOut0 = 2 * kCols, kOut1 = 2 * kCols + kSP / 64;
     if (blk < kCols) {
-        // ---------------- transform column
-        ColLds& s = u.col;
-        const int c = blk;
-        double2 h1 = make_double2(0.0, 0.0), h2 = h1, z1 = h1, rn = h1, x0 = h1;
-        if (t < 32) {
-            h1 = a.HS[((long)1 * kCols + c) * 32 + t];
-            h2 = a.HS[((long)2 * kCols + c) * 32 + t];
-            z1 = a.ZS[((long)ring_slot(a.head, 1, a.Q) * kCols + c) * 32 + t];
-            rn = a.Rin[c * 32 + t];
-            if (DP) x0 = a.ZS[((long)a.head * kCols + c) * 32 + t];   // Z_b, from this block's main pass
-        }
-        ColTw ct;
-        ct.load(a.tw, c, j, g);
-        const double2 tcol = a.tw[kTw2k + j * c];
-        if constexpr (!DP) {
-            double v[8];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = a.line[a.prev + 32 * (g + 8 * i) + j];
-#pragma unroll
-            for (int i = 4; i < 8; ++i) v[i] = a.x[32 * (g + 8 * i - 32) + j];
-            const double2 a1 = stage1(v, ct.t64);
-            if (l < 32) s.a[w][j] = a1;
-            __syncthreads();
-            const double2 xp = stage3(s, g, ct.t2k, ct.t32);
-            if (l < 32) s.x[w][j] = xp;
-            __syncthreads();
-        }
-        if (t < 32) {
-            const double2 X = DP ? x0 : cadd(cadd(s.x[0][t], s.x[1][t]), cadd(s.x[2][t], s.x[3][t]));
-            if (!DP) a.ZS[((long)a.head * kCols + c) * 32 + t] = X;
-            s.y[t] = cadd(cadd(cmul(h1, X), cmul(h2, z1)), rn);
-        }
-        __syncthreads();
-        col_inverse_store(s, ct, tcol, a.Cout + c * 32);
-        post_done(a);
+        role_transform<true>(a, a.HS, a.Rin, a.Cout, u.col, blk);
     } else if (blk < 2 * kCols) {
-        // ---------------- MAC column: R_{b+2}
-        ColLds& s = u.col;
-        const int c = blk - kCols;
-        double2 hv[QI], zv[QI];
-#pragma unroll
-        for (int i = 0; i < QI; ++i) {
-            const int p = 3 + g + 8 * i;   // < Q + 3; partitions past Q - 1 contribute nothing
-            // (masked: slot ring_slot(head, Q) is the one this launch's transform role writes)
-            const bool live = p < a.Q;
-            hv[i] = live ? a.HS[((long)p * kCols + c) * 32 + j] : make_double2(0.0, 0.0);
-            zv[i] = live ? a.ZS[((long)ring_slot(a.head, p - 2, a.Q) * kCols + c) * 32 + j] : make_double2(0.0, 0.0);
-        }
-        double2 r = make_double2(0.0, 0.0);
-#pragma unroll
-        for (int i = 0; i < QI; ++i) r = cadd(r, cmul(hv[i], zv[i]));
-        r = half_sum(r);
-        if (l < 32) s.m[w][j] = r;
-        __syncthreads();
-        if (t < 32) a.Rout[c * 32 + t] = cadd(cadd(s.m[0][t], s.m[1][t]), cadd(s.m[2][t], s.m[3][t]));
-        post_done(a);
-    } else {
-        // ---------------- 64 outputs: head + tail
-        OutLds& s = u.out;
-        const int k = blk - 2 * kCols;
-        const int t0 = 64 * k;
-        // every global load of the thread in flight before the first LDS store (a load -> store
-        // chain per loop iteration waited one memory latency each): window positions 64k + 1 ..
-        // 64k + 1087 (2048-sample window: previous block | this block), h[0..1023], the columns
-        double xv[5], hv[4];
-        double2 cv[5];
-#pragma unroll
-        for (int q = 0; q < 5; ++q) {
-            const int i = min(t + q * kT, 1086);
-            const int wp = t0 + 1 + i;
-            xv[q] = wp < kSP ? a.line[a.prev + wp] : a.x[wp - kSP];
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) hv[q] = a.h[t + q * kT];
-#pragma unroll
-        for (int q = 0; q < 5; ++q) cv[q] = a.Cin[min(t + q * kT, kCols * 32 - 1)];
-        const double2 twv = a.tw[kTw64 + (t & 63)];
-#pragma unroll
-        for (int q = 0; q < 5; ++q)
-            if (t + q * kT < 1087) s.sx[t + q * kT] = xv[q];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s.sh[t + q * kT] = hv[q];
-#pragma unroll
-        for (int q = 0; q < 5; ++q)
-            if (t + q * kT < kCols * 32) (&s.col[0][0])[t + q * kT] = cv[q];
-        if (t < 64) s.tw[t] = twv;
-        __syncthreads();
-        // the block's samples into the ring (both mirror positions), for the next calls
-        if (!DP && t < 64) {
-            const double xv = s.sx[1023 + t];
-            const long kk = a.wpos + t0 + t;
-            a.line[kk] = xv;
-            a.line[kk + a.R] = xv;
-        }
-        // head: thread = 8 outputs (o8) x 32 taps (q): y[j] += h[tau] x[t0 + j - tau]
-        {
-            const int o8 = t & 7, q = t >> 3;
-            const int j0 = 8 * o8, tau0 = 32 * q;
-            double xs[39], hs[32], acc[8];
-#pragma unroll
-            for (int i = 0; i < 39; ++i) xs[i] = s.sx[1023 + j0 - tau0 - 31 + i];   // x[t0 + j0 - tau0 - 31 + i]
-#pragma unroll
-            for (int i = 0; i < 32; ++i) hs[i] = s.sh[tau0 + i];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) acc[r] = 0.0;
-#pragma unroll
-            for (int i = 0; i < 32; ++i)
-#pragma unroll
-                for (int r = 0; r < 8; ++r) acc[r] = fma(hs[i], xs[31 + r - i], acc[r]);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) s.part[q][j0 + r] = acc[r];
-        }
-        // tail partials: output o (t & 63), columns c = 1 + cg + 4 i (cg = t >> 6)
-        {
-            const int o = t & 63, cg = t >> 6;
-            const int n = t0 + o, m = n >> 5, n2 = n & 31, n1 = 32 + m;
-            double acc = 0.0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int c = 1 + cg + 4 * i;
-                if (c < 32) {
-                    const double2 C = s.col[c][n2], wv = s.tw[(n1 * c) & 63];
-                    acc = fma(wv.x, C.x, fma(wv.y, C.y, acc));
-                }
-            }
-            acc *= 2.0;
-            if (cg == 0) acc += s.col[0][n2].x + ((n1 & 1) ? -s.col[32][n2].x : s.col[32][n2].x);
-            s.tpart[cg][o] = acc;
-        }
-        __syncthreads();
-        if (t < 64) {
-            double y = 0.0;
-#pragma unroll
-            for (int q = 0; q < 32; ++q) y += s.part[q][t];
-            const double tail = (s.tpart[0][t] + s.tpart[1][t]) + (s.tpart[2][t] + s.tpart[3][t]);
-            if (DP)
-                a.out[t0 + t] += (a.dscale * a.sgpow[t0 + t]) * (y + tail);
-            else
-                a.out[t0 + t] = a.tail2 ? (y + tail) + a.tail2[t0 + t] : y + tail;
-        }
-        post_done(a);
+        role_mac<QI>(a, a.HS, a.Rout, u.col, blk - kCols);
+    } else if (blk < kOut1) {
+        role_out<DUAL>(a, u.out, blk - kOut0);
+    } else if constexpr (DUAL) {
+        if (blk < kOut1 + kCols) role_transform<false>(a, a.HSD, a.RDin, a.CDout, u.col, blk - kOut1);
+        else role_mac<QI>(a, a.HSD, a.RDout, u.col, blk - kOut1 - kCols);
     }
+    post_done(a);
 }
 
 typedef void (*BlockKernel)(StreamArgs);
@@ -430,6 +514,7 @@ template <int QI>
 struct BlockKD {
     static constexpr BlockKernel fn = stream_block_kernel<QI, true>;
 };
+constexpr int kBlockWG = 2 * kCols + kSP / 64, kBlockWGD = 4 * kCols + kSP / 64;
 template <int QI>
 struct Prime2K {
     static constexpr BlockKernel fn = stream_prime2_kernel<QI>;
@@ -438,54 +523,81 @@ BlockKernel pick_block(int qi) { return pick_impl<BlockK>(qi, std::make_integer_
 BlockKernel pick_block_d(int qi) { return pick_impl<BlockKD>(qi, std::make_integer_sequence<int, 16>()); }
 BlockKernel pick_prime2(int qi) { return pick_impl<Prime2K>(qi, std::make_integer_sequence<int, 16>()); }
 
-// Per-band responses r[tau][n] (tau < K, time-major so a wave's stores are coalesced over its 64
-// bands): band n's impulse response at pre = pin_n by the reference recurrence in the oracle's
-// operation order (filterbank.h:178-179, as resp_h_kernel), no gain.  Once per coefficient / pre-amp
-// set, when the first gain transient streams.
+// Per-band responses r[n][tau] (tau < K): band n's impulse response at pre = pin_n by the reference
+// recurrence in the oracle's operation order (filterbank.h:178-179, as resp_h_kernel), no gain.  Lanes
+// are bands; each 64-sample tile goes through LDS so a band's row is stored as contiguous 512-byte
+// runs (a setter's update then reads its bands' rows coalesced).  Once per coefficient / pre-amp set,
+// when the first gain transient streams.
 template <int O>
 __global__ __launch_bounds__(64) void stream_rband_kernel(const double* __restrict__ F, const double* __restrict__ B,
                                                           const double* __restrict__ pin, int nbands, long K,
                                                           double* __restrict__ r) {
 #pragma clang fp contract(off)
-    const int band = blockIdx.x * 64 + threadIdx.x;
-    if (band >= nbands) return;
+    __shared__ double tile[64][65];
+    const int lane = threadIdx.x, band = blockIdx.x * 64 + lane;
+    const bool live = band < nbands;
     double f[O + 1], b[O], y[O];
 #pragma unroll
-    for (int i = 0; i <= O; ++i) f[i] = F[(long)band * (O + 1) + i];
+    for (int i = 0; i <= O; ++i) f[i] = live ? F[(long)band * (O + 1) + i] : 0.0;
 #pragma unroll
     for (int k = 0; k < O; ++k) {
-        b[k] = B[(long)band * O + k];
+        b[k] = live ? B[(long)band * O + k] : 0.0;
         y[k] = 0.0;
     }
-    const double p = pin[band];
-    for (long t = 0; t < K; ++t) {
-        double ff = 0.0;
+    const double p = live ? pin[band] : 0.0;
+    for (long t0 = 0; t0 < K; t0 += 64) {
+        for (int jj = 0; jj < 64; ++jj) {
+            const long t = t0 + jj;
+            double ff = 0.0;
 #pragma unroll
-        for (int i = 0; i <= O; ++i)
-            if (t == i) ff = f[i];
-        double bs = 0.0;
+            for (int i = 0; i <= O; ++i)
+                if (t == i) ff = f[i];
+            double bs = 0.0;
 #pragma unroll
-        for (int k = 0; k < O; ++k) bs += b[k] * y[k];
-        const double yt = ff * p - bs;
+            for (int k = 0; k < O; ++k) bs += b[k] * y[k];
+            const double yt = ff * p - bs;
 #pragma unroll
-        for (int k = O - 1; k >= 1; --k) y[k] = y[k - 1];
-        y[0] = yt;
-        r[t * nbands + band] = yt;
+            for (int k = O - 1; k >= 1; --k) y[k] = y[k - 1];
+            y[0] = yt;
+            tile[lane][jj] = yt;
+        }
+        __syncthreads();
+        for (int q = 0; q < 64; ++q) {   // band blockIdx.x * 64 + q: 64 consecutive samples
+            const int bq = blockIdx.x * 64 + q;
+            if (bq < nbands && t0 + lane < K) r[(long)bq * K + t0 + lane] = tile[q][lane];
+        }
+        __syncthreads();
     }
 }
 
 // A gain setter as a transient: d[tau] = sum_i delta_i r[tau][band_i] (the setter's bands in list
-// order), h += d (the new targets), h_D = rebase h_D - d (D_n = g_n(t) - gin_n loses delta_n)
+// order), h += d (the new targets), h_D = rebase h_D - d (D_n = g_n(t) - gin_n loses delta_n).
+// Up to kChurnArg bands travel in the kernel arguments, with their new targets for d_gin (no host
+// copy, no stream synchronisation); longer lists come from device memory (gin uploaded by the caller)
+constexpr int kChurnArg = 24;
+struct ChurnList {
+    int m;
+    int band[kChurnArg];
+    double delta[kChurnArg];
+    double gin[kChurnArg];
+};
 __global__ __launch_bounds__(256) void stream_churn_kernel(const double* __restrict__ r, int nbands, long K,
-                                                           const double* __restrict__ delta, int m, double rebase,
-                                                           double* __restrict__ h, double* __restrict__ hD) {
+                                                           ChurnList L, const double* __restrict__ dlist, int m,
+                                                           double rebase, double* __restrict__ h,
+                                                           double* __restrict__ hD, double* __restrict__ dv,
+                                                           double* __restrict__ gin) {
     const long tau = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && (int)threadIdx.x < L.m) gin[L.band[threadIdx.x]] = L.gin[threadIdx.x];
     if (tau >= K) return;
-    const double* row = r + tau * nbands;
     double d = 0.0;
-    for (int i = 0; i < m; ++i) d = fma(delta[2 * i + 1], row[(int)delta[2 * i]], d);
+    if (L.m) {
+        for (int i = 0; i < L.m; ++i) d = fma(L.delta[i], r[(long)L.band[i] * K + tau], d);
+    } else {
+        for (int i = 0; i < m; ++i) d = fma(dlist[2 * i + 1], r[(long)dlist[2 * i] * K + tau], d);
+    }
     h[tau] += d;
     hD[tau] = rebase * hD[tau] - d;
+    dv[tau] = d;
 }
 
 // line[i] = line[i + R] = src[i], i < n, from write position wpos
@@ -643,6 +755,10 @@ StreamArgs stream_args(hz_fb* h) {
     a.flags = nullptr;
     a.seq = 0;
     a.tail2 = nullptr;
+    a.HSD = nullptr;
+    a.hD = nullptr;
+    a.CDin = a.RDin = nullptr;
+    a.CDout = a.RDout = nullptr;
     a.dscale = 0.0;
     a.sgpow = nullptr;
     return a;
@@ -655,13 +771,24 @@ void d_args(hz_fb* h, StreamArgs* a) {
     double2* C = (double2*)S.d_CRD;
     double2* Rb = C + 2 * col;
     const int b = (int)(S.blk & 1);
-    a->HS = (const double2*)S.d_HSD;
-    a->h = S.d_hD;
-    a->Cin = C + b * col;
-    a->Cout = C + (b ^ 1) * col;
-    a->Rin = Rb + (b ^ 1) * col;
-    a->Rout = Rb + b * col;
+    a->HSD = (const double2*)S.d_HSD;
+    a->hD = S.d_hD;
+    a->CDin = C + b * col;
+    a->CDout = C + (b ^ 1) * col;
+    a->RDin = Rb + (b ^ 1) * col;
+    a->RDout = Rb + b * col;
     a->sgpow = S.d_sgpow;
+}
+// prime2 over h_D: the D fields in the main slots
+StreamArgs d_as_main(const StreamArgs& a) {
+    StreamArgs d = a;
+    d.HS = a.HSD;
+    d.h = a.hD;
+    d.Cin = a.CDin;
+    d.Cout = a.CDout;
+    d.Rin = a.RDin;
+    d.Rout = a.RDout;
+    return d;
 }
 
 // the tail's contribution to the outputs of epoch e, out[i] = sum_{tau >= K1} h[tau] x[eE + i - tau]
@@ -722,10 +849,8 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
     hz_fb::Resp& R = h->resp;
     hz_fb::Resp::Stream& S = R.st;
     if (S.dmode) {   // the transient has decayed below 2^-60 of the targets: plain streaming from here
-        double gmax = 0;
-        for (double g : h->gin) gmax = std::max(gmax, std::fabs(g));
         const double sd = (double)powl((long double)h->sg, (long double)(S.pos - S.dref));
-        if (sd * S.dmax <= 0x1p-60 * gmax) {
+        if (sd * S.dmax <= 0x1p-60 * S.gin_max) {
             fb_stream_dclear(h);   // the response is rebuilt for the long-call engine's spectra too
             h->converged = true;   // pre-amps converged at the first setter, gains now
         }
@@ -776,7 +901,7 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
         StreamArgs ad = stream_args(h);
         d_args(h, &ad);   // (its parities from blk - 1 too)
         S.blk = blk;
-        hipLaunchKernelGGL(pick_prime2(Q / 8), dim3(kCols), dim3(kT), 0, h->stream, ad);
+        hipLaunchKernelGGL(pick_prime2(Q / 8), dim3(kCols), dim3(kT), 0, h->stream, d_as_main(ad));
         HZ_TRY_HIP(hipGetLastError());
         S.prime_d = false;
     }
@@ -793,19 +918,16 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
         HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
         h->ev_skip[(e - h->ev.data()) / 5] |= 2 | 8;
     }
-    hipLaunchKernelGGL(pick_block(Q / 8), dim3(2 * kCols + kSP / 64), dim3(kT), 0, h->stream, a);
-    HZ_TRY_HIP(hipGetLastError());
-    if (S.dmode) {   // the transient term: s_g^(t - dref) conv(h_D, x), added to the block's outputs
-        StreamArgs ad = a;
-        d_args(h, &ad);
-        ad.flags = nullptr;
-        ad.tail2 = nullptr;
+    if (S.dmode) {   // a gain transient: + s_g^(t - dref + 1) conv(h_D, x), its roles in the same launch
+        d_args(h, &a);
         // (compute() smooths before the sample's output, filterbank.h:172-173: D is g(dref - 1) -
         // gin, so sample t carries s_g^(t - dref + 1))
-        ad.dscale = (double)powl((long double)h->sg, (long double)(S.pos - S.dref + 1));
-        hipLaunchKernelGGL(pick_block_d(Q / 8), dim3(2 * kCols + kSP / 64), dim3(kT), 0, h->stream, ad);
-        HZ_TRY_HIP(hipGetLastError());
+        a.dscale = (double)powl((long double)h->sg, (long double)(S.pos - S.dref + 1));
+        hipLaunchKernelGGL(pick_block_d(Q / 8), dim3(kBlockWGD), dim3(kT), 0, h->stream, a);
+    } else {
+        hipLaunchKernelGGL(pick_block(Q / 8), dim3(kBlockWG), dim3(kT), 0, h->stream, a);
     }
+    HZ_TRY_HIP(hipGetLastError());
     if (e) {
         HZ_TRY_HIP(hipEventRecord(e[2], h->stream));
         HZ_TRY_HIP(hipEventRecord(e[4], h->stream));
@@ -928,57 +1050,71 @@ void fb_stream_dclear(hz_fb* h) {
 // A setter that changed only gains (mix / open) while the bank streams stationary: keep streaming.
 // h += sum_n (gin'_n - gin_n) r_n, h_D = s_g^(pos - dref) h_D - (the same sum), dref = pos; both
 // responses' spectra again; the next block re-primes both passes' C / R from the (valid) ring.
-// false: not applicable here (the caller invalidates the response as before).
-bool fb_stream_gain_setter(hz_fb* h) {
+// Returns 0: not applicable here (the caller invalidates the response as before); 1: applied, d_gin
+// written by the update kernel (a short list: no host copy, no synchronisation); 2: applied, the
+// caller uploads d_gin.
+int fb_stream_gain_setter(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     hz_fb::Resp::Stream& S = R.st;
     const int N = h->N, O = h->order;
     if (!S.on || !S.line_hist || !S.fdl_valid || !R.h_valid || S.hs_gen != R.h_gen || R.run < R.K || R.over_valid ||
         S.tail || R.mode == HZ_FB_RESP_OFF || h->dist_id != HZ_DIST_NONE || h->path_mode != HZ_FB_PATH_AUTO || O == 0 ||
         (int)S.gin_base.size() != N)
-        return false;
+        return 0;
     const long K = S.K1;
-    if ((double)K * N * 8.0 > 8.0 * (1L << 30)) return false;   // the per-band responses stay <= 8 GiB
-    // pre-amps converged (boost() invalidates instead); gains converged to gin_base unless a transient
-    // already streams (then g_n(t) - gin_base_n = s_g^(t - dref) D_n by construction)
-    fb_mirror_sync(h);
-    double pmax = 0, gmax = 0;
-    for (int b = 0; b < N; ++b) {
-        pmax = std::max(pmax, std::fabs(h->pin[b]));
-        gmax = std::max(gmax, std::fabs(S.gin_base[b]));
-    }
-    for (int b = 0; b < N; ++b) {
-        if (!(std::fabs(h->pg_host[2 * (size_t)b] - h->pin[b]) <= 0x1p-60 * pmax)) return false;
-        if (!S.dmode && !(std::fabs(h->pg_host[2 * (size_t)b + 1] - S.gin_base[b]) <= 0x1p-60 * gmax)) return false;
+    if ((double)K * N * 8.0 > 8.0 * (1L << 30)) return 0;   // the per-band responses stay <= 8 GiB
+    if (!S.dmode) {
+        // the first transient: pre-amps converged (boost() invalidates instead, so this holds until
+        // the transient ends) and gains converged to gin_base (later setters: g_n(t) - gin_base_n =
+        // s_g^(t - dref) D_n by construction)
+        fb_mirror_sync(h);
+        double pmax = 0, gmax = 0;
+        for (int b = 0; b < N; ++b) {
+            pmax = std::max(pmax, std::fabs(h->pin[b]));
+            gmax = std::max(gmax, std::fabs(S.gin_base[b]));
+        }
+        for (int b = 0; b < N; ++b) {
+            if (!(std::fabs(h->pg_host[2 * (size_t)b] - h->pin[b]) <= 0x1p-60 * pmax)) return 0;
+            if (!(std::fabs(h->pg_host[2 * (size_t)b + 1] - S.gin_base[b]) <= 0x1p-60 * gmax)) return 0;
+        }
     }
     // the setter's bands
+    ChurnList L{};
     S.h_delta.clear();
     double dmx = 0;
     for (int b = 0; b < N; ++b) {
         const double d = h->gin[b] - S.gin_base[b];
         if (d != 0.0) {
+            if (L.m < kChurnArg) {
+                L.band[L.m] = b;
+                L.delta[L.m] = d;
+                L.gin[L.m] = h->gin[b];
+            }
+            ++L.m;
             S.h_delta.push_back((double)b);
             S.h_delta.push_back(d);
             dmx = std::max(dmx, std::fabs(d));
         }
     }
     const int m = (int)(S.h_delta.size() / 2);
-    if (m == 0) return true;
-    auto alloc = [](double** p, size_t* cap, size_t need) -> int { return s_alloc(p, cap, need); };
+    if (m == 0) return 1;
+    const bool by_value = m <= kChurnArg;
+    if (!by_value) L.m = 0;
     const size_t col = (size_t)kCols * 32 * 2;
     const int Q = (int)(K / kSP);
-    if (alloc(&S.d_rband, &S.rband_cap, (size_t)K * N) != HZ_OK || alloc(&S.d_hD, &S.hD_cap, (size_t)K) != HZ_OK ||
-        alloc(&S.d_delta, &S.delta_cap, S.h_delta.size()) != HZ_OK)
-        return false;
+    if (s_alloc(&S.d_rband, &S.rband_cap, (size_t)K * N) != HZ_OK || s_alloc(&S.d_hD, &S.hD_cap, (size_t)K) != HZ_OK ||
+        s_alloc(&S.d_dv, &S.dv_cap, (size_t)K) != HZ_OK ||
+        s_alloc(&S.d_delta, &S.delta_cap, S.h_delta.size()) != HZ_OK)
+        return 0;
     const size_t hcap = S.hsd_cap;
-    if (alloc(&S.d_HSD, &S.hsd_cap, (size_t)(Q + 8) * col) != HZ_OK) return false;
-    if (S.hsd_cap != hcap && hipMemset(S.d_HSD, 0, sizeof(double) * S.hsd_cap) != hipSuccess) return false;
-    if (!S.d_CRD && hipMalloc(&S.d_CRD, sizeof(double) * 4 * col) != hipSuccess) return false;
+    if (s_alloc(&S.d_HSD, &S.hsd_cap, (size_t)(Q + 8) * col) != HZ_OK) return 0;
+    if (S.hsd_cap != hcap && hipMemset(S.d_HSD, 0, sizeof(double) * S.hsd_cap) != hipSuccess) return 0;
+    if (!S.d_CRD && hipMalloc(&S.d_CRD, sizeof(double) * 4 * col) != hipSuccess) return 0;
     if (S.sgpow_of != h->sg) {
         std::vector<double> sp(kSP);
         for (int j = 0; j < kSP; ++j) sp[j] = (double)powl((long double)h->sg, (long double)j);
-        if (!S.d_sgpow && hipMalloc(&S.d_sgpow, sizeof(double) * kSP) != hipSuccess) return false;
-        if (hipMemcpy(S.d_sgpow, sp.data(), sizeof(double) * kSP, hipMemcpyHostToDevice) != hipSuccess) return false;
+        if (!S.d_sgpow && hipMalloc(&S.d_sgpow, sizeof(double) * kSP) != hipSuccess) return 0;
+        if (hipMemcpy(S.d_sgpow, sp.data(), sizeof(double) * kSP, hipMemcpyHostToDevice) != hipSuccess) return 0;
         S.sgpow_of = h->sg;
     }
     if (!S.rband_valid) {   // r_n at the current coefficients and pre-amps (R.d_coef: resp_build_h)
@@ -991,35 +1127,40 @@ bool fb_stream_gain_setter(hz_fb* h) {
         case 3: hipLaunchKernelGGL(stream_rband_kernel<3>, dim3(g), dim3(64), 0, h->stream, F, Bc, (const double*)h->d_pin, N, K, S.d_rband); break;
         default: hipLaunchKernelGGL(stream_rband_kernel<4>, dim3(g), dim3(64), 0, h->stream, F, Bc, (const double*)h->d_pin, N, K, S.d_rband); break;
         }
-        if (hipGetLastError() != hipSuccess) return false;
+        if (hipGetLastError() != hipSuccess) return 0;
         S.rband_valid = true;
     }
-    if (!S.dmode && hipMemsetAsync(S.d_hD, 0, sizeof(double) * K, h->stream) != hipSuccess) return false;
+    if (!S.dmode && (hipMemsetAsync(S.d_hD, 0, sizeof(double) * K, h->stream) != hipSuccess ||
+                     hipMemsetAsync(S.d_HSD, 0, sizeof(double) * (size_t)Q * col, h->stream) != hipSuccess))
+        return 0;
     const double rebase = S.dmode ? (double)powl((long double)h->sg, (long double)(S.pos - S.dref)) : 0.0;
-    if (hipMemcpyAsync(S.d_delta, S.h_delta.data(), sizeof(double) * S.h_delta.size(), hipMemcpyHostToDevice,
-                       h->stream) != hipSuccess)
-        return false;
+    // (a long list from device memory: the caller's upload synchronises the stream before h_delta
+    // changes again)
+    if (!by_value && hipMemcpyAsync(S.d_delta, S.h_delta.data(), sizeof(double) * S.h_delta.size(),
+                                    hipMemcpyHostToDevice, h->stream) != hipSuccess)
+        return 0;
     hipLaunchKernelGGL(stream_churn_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, h->stream,
-                       (const double*)S.d_rband, N, K, (const double*)S.d_delta, m, rebase, R.d_h, S.d_hD);
-    hipLaunchKernelGGL(stream_hs_kernel, dim3(kCols, (unsigned)Q), dim3(kT), 0, h->stream, (const double*)R.d_h,
-                       (const double2*)S.d_tw, (double2*)S.d_HS);
-    hipLaunchKernelGGL(stream_hs_kernel, dim3(kCols, (unsigned)Q), dim3(kT), 0, h->stream, (const double*)S.d_hD,
-                       (const double2*)S.d_tw, (double2*)S.d_HSD);
-    if (hipGetLastError() != hipSuccess) return false;
+                       (const double*)S.d_rband, N, K, L, (const double*)S.d_delta, m, rebase, R.d_h, S.d_hD, S.d_dv,
+                       h->d_gin);
+    hipLaunchKernelGGL(stream_hsd_kernel, dim3(kCols, (unsigned)Q), dim3(kT), 0, h->stream, (const double*)S.d_dv,
+                       (const double2*)S.d_tw, rebase, (double2*)S.d_HS, (double2*)S.d_HSD);
+    if (hipGetLastError() != hipSuccess) return 0;
     S.dmax = rebase * S.dmax + dmx;
     S.dref = S.pos;
     S.dmode = true;
     S.prime_main = S.prime_d = true;
     ++S.dsetters;
-    S.gin_base = h->gin;
-    return true;
+    for (size_t i = 0; i < S.h_delta.size(); i += 2) S.gin_base[(size_t)S.h_delta[i]] = h->gin[(size_t)S.h_delta[i]];
+    S.gin_max = 0;
+    for (double v : S.gin_base) S.gin_max = std::max(S.gin_max, std::fabs(v));
+    return by_value ? 1 : 2;
 }
 
 void fb_stream_free(hz_fb* h) {
     hz_fb::Resp::Stream& S = h->resp.st;
     (void)tail_quiet(S);
     for (double* p : {S.d_line, S.d_ZS, S.d_HS, S.d_CR, S.d_tw, S.d_tH, S.d_tZ, S.d_tY, S.d_tout, S.d_hD, S.d_HSD,
-                      S.d_CRD, S.d_rband, S.d_sgpow, S.d_delta})
+                      S.d_CRD, S.d_rband, S.d_sgpow, S.d_delta, S.d_dv})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : {S.ev_main, S.ev_tail[0], S.ev_tail[1]})
         if (e) (void)hipEventDestroy(e);

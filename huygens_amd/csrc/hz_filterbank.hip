@@ -662,12 +662,12 @@ int fb_upload(hz_fb* h) {
     if (h->dirty_pin) h->resp.st.rband_valid = false;   // r_n are at pre = pin
     // gains only, while the bank streams stationary: a transient of the streaming engine instead of
     // a new response and K samples of history (hz_fb_stream.hip fb_stream_gain_setter)
-    const bool transient = h->dirty_gin && !h->dirty_pin && !uploaded && !h->tv_pending &&
-                           hz_fbi::fb_stream_gain_setter(h);
+    const int transient = (h->dirty_gin && !h->dirty_pin && !uploaded && !h->tv_pending) ? hz_fbi::fb_stream_gain_setter(h) : 0;
     if (h->dirty_pin || h->dirty_gin) {
         for (auto& st : h->lti_set) st.fmix_valid = false;
         if (!transient) hz_fbi::fb_resp_invalidate(h, false);
     }
+    if (transient == 1) h->dirty_gin = false;   // the update kernel wrote d_gin: no upload, no synchronisation
     if (h->dirty_pin) {
         HZ_TRY_HIP(hipMemcpyAsync(h->d_pin, h->pin.data(), sizeof(double) * h->N, hipMemcpyHostToDevice,
                                   h->stream));
