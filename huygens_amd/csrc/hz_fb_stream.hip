@@ -234,17 +234,22 @@ __global__ __launch_bounds__(kT) void stream_prime_kernel(StreamArgs a) {
 // after stream_prime_kernel, per column: the first block's tail columns C_b (Y_b = sum_{p >= 1}
 // H_p Z_{b-p}) into Cout and R_{b+1} = sum_{p >= 3} H_p Z_{b+1-p} into Rout
 template <int QI>
+// (blockIdx.y = 1: the same for a gain transient's h_D -- its spectra and C / R parities -- in the
+// same launch)
 __global__ __launch_bounds__(kT) void stream_prime2_kernel(StreamArgs a) {
     __shared__ ColLds s;
     const int t = threadIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
     const int c = blockIdx.x;
+    const double2* __restrict__ HS = blockIdx.y ? a.HSD : a.HS;
+    double2* Rout = blockIdx.y ? a.RDout : a.Rout;
+    double2* Cout = blockIdx.y ? a.CDout : a.Cout;
     double2 y = make_double2(0.0, 0.0), r = make_double2(0.0, 0.0);
 #pragma unroll
     for (int i = 0; i < QI; ++i) {
         const int p = 1 + g + 8 * i;   // <= Q: row Q of HS is zero
-        y = cadd(y, cmul(a.HS[((long)p * kCols + c) * 32 + j], a.ZS[((long)ring_slot(a.head, p, a.Q) * kCols + c) * 32 + j]));
+        y = cadd(y, cmul(HS[((long)p * kCols + c) * 32 + j], a.ZS[((long)ring_slot(a.head, p, a.Q) * kCols + c) * 32 + j]));
         const int p3 = 3 + g + 8 * i;  // < Q + 8
-        r = cadd(r, cmul(a.HS[((long)p3 * kCols + c) * 32 + j],
+        r = cadd(r, cmul(HS[((long)p3 * kCols + c) * 32 + j],
                          a.ZS[((long)ring_slot(a.head, p3 - 1, a.Q) * kCols + c) * 32 + j]));
     }
     ColTw ct;
@@ -259,10 +264,10 @@ __global__ __launch_bounds__(kT) void stream_prime2_kernel(StreamArgs a) {
     __syncthreads();
     if (t < 32) {
         s.y[t] = cadd(cadd(s.m[0][t], s.m[1][t]), cadd(s.m[2][t], s.m[3][t]));
-        a.Rout[c * 32 + t] = cadd(cadd(s.x[0][t], s.x[1][t]), cadd(s.x[2][t], s.x[3][t]));
+        Rout[c * 32 + t] = cadd(cadd(s.x[0][t], s.x[1][t]), cadd(s.x[2][t], s.x[3][t]));
     }
     __syncthreads();
-    col_inverse_store(s, ct, tcol, a.Cout + c * 32);
+    col_inverse_store(s, ct, tcol, Cout + c * 32);
 }
 
 struct OutLds {
@@ -887,23 +892,19 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
         S.prime_main = false;
         S.prime_d = S.dmode;
     }
-    if (S.prime_main) {   // h changed (a gain transient) with the ring still valid: C_b and R_{b+1} again
-        const long blk = S.blk;
-        S.blk = blk - 1;   // as the launch before this block writes them
-        hipLaunchKernelGGL(pick_prime2(Q / 8), dim3(kCols), dim3(kT), 0, h->stream, stream_args(h));
-        HZ_TRY_HIP(hipGetLastError());
-        S.blk = blk;
-        S.prime_main = false;
-    }
-    if (S.dmode && S.prime_d) {   // the D pass's C_b and R_{b+1} from the ring and h_D's spectra
+    // h changed (a gain transient, or a rebuild) with the ring still valid: C_b and R_{b+1} again, as
+    // the launch before this block writes them; h_D's in the same launch (grid y = 2)
+    const bool pm = S.prime_main, pd = S.dmode && S.prime_d;
+    if (pm || pd) {
         const long blk = S.blk;
         S.blk = blk - 1;
-        StreamArgs ad = stream_args(h);
-        d_args(h, &ad);   // (its parities from blk - 1 too)
+        StreamArgs ap = stream_args(h);
+        if (pd) d_args(h, &ap);   // (its parities from blk - 1 too)
         S.blk = blk;
-        hipLaunchKernelGGL(pick_prime2(Q / 8), dim3(kCols), dim3(kT), 0, h->stream, d_as_main(ad));
+        hipLaunchKernelGGL(pick_prime2(Q / 8), dim3(kCols, pm && pd ? 2 : 1), dim3(kT), 0, h->stream,
+                           pm ? ap : d_as_main(ap));
         HZ_TRY_HIP(hipGetLastError());
-        S.prime_d = false;
+        S.prime_main = S.prime_d = false;
     }
     if (S.tail) HZ_TRY(tail_schedule(h));
     StreamArgs a = stream_args(h);
