@@ -284,16 +284,17 @@ struct hz_fb {
             double* d_HSD = nullptr;     // [K1/1024 + 8][33][32] its spectra
             size_t hsd_cap = 0;
             double* d_CRD = nullptr;     // its C / R parities
-            double* d_rband = nullptr;   // [N][K1] r_n (pre = pin, no gain)
-            double* d_dv = nullptr;      // [K1] a setter's update sum_n delta_n r_n
-            size_t dv_cap = 0;
-            size_t rband_cap = 0;
+            // r_n (pre = pin, no gain) in partition form (hz_fb_stream.hip stream_rbasis_kernel)
+            double* d_r0 = nullptr;      // [N][1024] partition 0
+            double* d_phi = nullptr;     // [N][O][1024] homogeneous basis responses
+            double* d_st = nullptr;      // [N][Q][O] states at the partition starts
+            double* d_rsp = nullptr;     // [N][O + 1][33][32] double2: spectra of r0, phi
+            size_t r0_cap = 0, phi_cap = 0, st_cap = 0, rsp_cap = 0;
             bool rband_valid = false;
             double* d_sgpow = nullptr;   // s_g^j, j < 1024
             double sgpow_of = -1;        // the s_g it holds
-            double* d_delta = nullptr;   // a setter's (band, delta) list
-            size_t delta_cap = 0;
-            std::vector<double> h_delta;
+            std::vector<double> h_delta;   // the last setter's bands
+            unsigned long long* d_stamps = nullptr;   // (diagnostic) setter launch phase stamps
             std::vector<double> gin_base;   // the gins d_h is built with
             bool prime_main = false;     // C / R of the main pass to recompute (h changed, ring valid)
             bool prime_d = false;        // ... of the D pass
@@ -437,7 +438,7 @@ int fb_stream_to_hist(hz_fb* h);       // the ring's history back to resp.d_hist
 void fb_stream_reset(hz_fb* h);        // state overwritten (set_state, tick)
 void fb_stream_free(hz_fb* h);
 int fb_stream_gain_setter(hz_fb* h);      // a gin-only setter as a streaming transient (0: not applied,
-                                          // 1: applied, d_gin written; 2: applied, upload d_gin)
+                                          // 1: applied, d_gin written by its launch)
 bool fb_stream_dmode(const hz_fb* h);     // a gain transient is streaming (gains still moving)
 void fb_stream_dclear(hz_fb* h);          // leave the transient mode (the response is rebuilt)
 // the streaming engine's response tail (hz_fb_resp.hip): partition spectra of h[K1, K), and the

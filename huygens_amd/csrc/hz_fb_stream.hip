@@ -28,6 +28,7 @@
 #include <type_traits>
 #include <utility>
 
+#include "hz_dd.h"
 #include "hz_fb_impl.h"
 
 namespace {
@@ -112,13 +113,10 @@ struct ColTw {   // the thread's twiddles for column c
 };
 
 // One column's bins of a window's spectrum into dst[k2] (k2 < 32): prime / partition spectra.
-template <class Load>
-__device__ __forceinline__ void col_forward(ColLds& s, const double2* __restrict__ tw, int c, Load load,
-                                            double2* __restrict__ dst) {
+// (v[i] = the window at 32 (g + 8 i) + j)
+__device__ __forceinline__ void col_forward_v(ColLds& s, const double2* __restrict__ tw, int c, const double (&v)[8],
+                                              double2* __restrict__ dst) {
     const int t = threadIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
-    double v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = load(32 * (g + 8 * i) + j);
     ColTw ct;
     ct.load(tw, c, j, g);
     const double2 a = stage1(v, ct.t64);
@@ -129,6 +127,15 @@ __device__ __forceinline__ void col_forward(ColLds& s, const double2* __restrict
     __syncthreads();
     if (t < 32) dst[t] = cadd(cadd(s.x[0][t], s.x[1][t]), cadd(s.x[2][t], s.x[3][t]));
 }
+template <class Load>
+__device__ __forceinline__ void col_forward(ColLds& s, const double2* __restrict__ tw, int c, Load load,
+                                            double2* __restrict__ dst) {
+    const int t = threadIdx.x, l = t & 63, g = 2 * (t >> 6) + (l >> 5), j = l & 31;
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = load(32 * (g + 8 * i) + j);
+    col_forward_v(s, tw, c, v, dst);
+}
 
 // Partition spectra HS[p][c][k2] = DFT_2048(h[pP, (p+1)P) zero-padded) / F, grid (33, Q)
 __global__ __launch_bounds__(kT) void stream_hs_kernel(const double* __restrict__ h, const double2* __restrict__ tw,
@@ -138,24 +145,6 @@ __global__ __launch_bounds__(kT) void stream_hs_kernel(const double* __restrict_
     const double* hp = h + (long)p * kSP;
     col_forward(s, tw, c, [&](int n) { return n < kSP ? hp[n] * (1.0 / kSF) : 0.0; },
                 HS + ((long)p * kCols + c) * 32);
-}
-
-// a gain transient's spectra by linearity: dS = the partition spectra of the update d (the same
-// column transform as stream_hs_kernel), HS += dS, HS_D = rebase HS_D - dS
-__global__ __launch_bounds__(kT) void stream_hsd_kernel(const double* __restrict__ d, const double2* __restrict__ tw,
-                                                        double rebase, double2* __restrict__ HS, double2* __restrict__ HSD) {
-    __shared__ ColLds s;
-    __shared__ double2 dS[32];
-    const int c = blockIdx.x, p = blockIdx.y;
-    const double* dp = d + (long)p * kSP;
-    col_forward(s, tw, c, [&](int n) { return n < kSP ? dp[n] * (1.0 / kSF) : 0.0; }, dS);
-    __syncthreads();
-    if (threadIdx.x < 32) {
-        const long at = ((long)p * kCols + c) * 32 + threadIdx.x;
-        const double2 v = dS[threadIdx.x], a = HS[at], b = HSD[at];
-        HS[at] = make_double2(a.x + v.x, a.y + v.y);
-        HSD[at] = make_double2(rebase * b.x - v.x, rebase * b.y - v.y);
-    }
 }
 
 struct StreamArgs {
@@ -189,6 +178,7 @@ struct StreamArgs {
     double2* RDout;
     double dscale;
     const double* sgpow;
+    unsigned long long* wst;   // (diagnostic, HZ_SETTER_STAMPS) [2][160]: every workgroup's start and end
 };
 
 // all of this workgroup's stores complete, then one system-scope release of the flag
@@ -490,6 +480,7 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
     using Lds = typename std::conditional<DUAL, StreamLdsD, StreamLds>::type;
     __shared__ Lds u;
     const int blk = blockIdx.x;
+    if (a.wst && threadIdx.x == 0) a.wst[blk] = __builtin_amdgcn_s_memrealtime();
     constexpr int kOut0 = 2 * kCols, kOut1 = 2 * kCols + kSP / 64;
     if (blk < kCols) {
         role_transform<true>(a, a.HS, a.Rin, a.Cout, u.col, blk);
@@ -502,6 +493,10 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
         else role_mac<QI>(a, a.HSD, a.RDout, u.col, blk - kOut1 - kCols);
     }
     post_done(a);
+    if (a.wst) {
+        __syncthreads();
+        if (threadIdx.x == 0) a.wst[160 + blk] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 typedef void (*BlockKernel)(StreamArgs);
@@ -528,57 +523,94 @@ BlockKernel pick_block(int qi) { return pick_impl<BlockK>(qi, std::make_integer_
 BlockKernel pick_block_d(int qi) { return pick_impl<BlockKD>(qi, std::make_integer_sequence<int, 16>()); }
 BlockKernel pick_prime2(int qi) { return pick_impl<Prime2K>(qi, std::make_integer_sequence<int, 16>()); }
 
-// Per-band responses r[n][tau] (tau < K): band n's impulse response at pre = pin_n by the reference
-// recurrence in the oracle's operation order (filterbank.h:178-179, as resp_h_kernel), no gain.  Lanes
-// are bands; each 64-sample tile goes through LDS so a band's row is stored as contiguous 512-byte
-// runs (a setter's update then reads its bands' rows coalesced).  Once per coefficient / pre-amp set,
-// when the first gain transient streams.
+
+// Per-band responses r_n (band n's impulse response at pre = pin_n, no gain: the reference recurrence
+// in the oracle's operation order, filterbank.h:178-179, as resp_h_kernel) in partition form, once per
+// coefficient / pre-amp set when the first gain transient streams.  Past its first O + 1 samples r_n is
+// homogeneous, so on partition p > 0 it is the zero-input response of its state there:
+//     r_n[1024 p + j] = sum_k S_np[k] phi_nk[j],   phi_nk = the response from the unit state e_k,
+// and the partition spectra are the same combination of phi_nk's spectra.  Stored per band:
+//     r0 [N][1024]       partition 0 of r_n
+//     phi[N][O][1024]    the homogeneous basis responses
+//     st [N][Q][O]       S_np (state before sample 1024 p: y[1024 p - 1 - k]; row 0 unused)
+//     sp [N][O + 1][33][32]  the column spectra of r0 and phi_nk (as stream_hs_kernel: / 2048)
+// S_np is the state after the impulse's taps advanced by M^(1024 p - O - 1), the companion matrix's
+// power in double-double (hz_dd.h).  Grid (N, 2): y = 0 runs r0 and the phi_nk (lanes 0 .. O), y = 1
+// the states (lane p - 1).
 template <int O>
-__global__ __launch_bounds__(64) void stream_rband_kernel(const double* __restrict__ F, const double* __restrict__ B,
-                                                          const double* __restrict__ pin, int nbands, long K,
-                                                          double* __restrict__ r) {
+__global__ __launch_bounds__(128) void stream_rbasis_kernel(const double* __restrict__ F, const double* __restrict__ B,
+                                                            const double* __restrict__ pin, int Q,
+                                                            double* __restrict__ r0, double* __restrict__ phi,
+                                                            double* __restrict__ st) {
 #pragma clang fp contract(off)
-    __shared__ double tile[64][65];
-    const int lane = threadIdx.x, band = blockIdx.x * 64 + lane;
-    const bool live = band < nbands;
+    using hz_dd::dd;
+    const int t = threadIdx.x, band = blockIdx.x;
     double f[O + 1], b[O], y[O];
 #pragma unroll
-    for (int i = 0; i <= O; ++i) f[i] = live ? F[(long)band * (O + 1) + i] : 0.0;
+    for (int i = 0; i <= O; ++i) f[i] = F[(long)band * (O + 1) + i];
 #pragma unroll
     for (int k = 0; k < O; ++k) {
-        b[k] = live ? B[(long)band * O + k] : 0.0;
+        b[k] = B[(long)band * O + k];
         y[k] = 0.0;
     }
-    const double p = live ? pin[band] : 0.0;
-    for (long t0 = 0; t0 < K; t0 += 64) {
-        for (int jj = 0; jj < 64; ++jj) {
-            const long t = t0 + jj;
-            double ff = 0.0;
+    const double pv = pin[band];
+    auto step = [&](long tt, bool input) {
+        double ff = 0.0;
+        if (input) {
 #pragma unroll
             for (int i = 0; i <= O; ++i)
-                if (t == i) ff = f[i];
-            double bs = 0.0;
-#pragma unroll
-            for (int k = 0; k < O; ++k) bs += b[k] * y[k];
-            const double yt = ff * p - bs;
-#pragma unroll
-            for (int k = O - 1; k >= 1; --k) y[k] = y[k - 1];
-            y[0] = yt;
-            tile[lane][jj] = yt;
+                if (tt == i) ff = f[i];
         }
-        __syncthreads();
-        for (int q = 0; q < 64; ++q) {   // band blockIdx.x * 64 + q: 64 consecutive samples
-            const int bq = blockIdx.x * 64 + q;
-            if (bq < nbands && t0 + lane < K) r[(long)bq * K + t0 + lane] = tile[q][lane];
+        double bs = 0.0;
+#pragma unroll
+        for (int k = 0; k < O; ++k) bs += b[k] * y[k];
+        const double yt = ff * pv - bs;
+#pragma unroll
+        for (int k = O - 1; k >= 1; --k) y[k] = y[k - 1];
+        y[0] = yt;
+        return yt;
+    };
+    if (blockIdx.y == 0) {
+        if (t > O) return;
+        double* dst = t == 0 ? r0 + (long)band * kSP : phi + ((long)band * O + (t - 1)) * kSP;
+        if (t > 0) {
+#pragma unroll
+            for (int k = 0; k < O; ++k) y[k] = k == t - 1 ? 1.0 : 0.0;
         }
-        __syncthreads();
+        for (int j = 0; j < kSP; ++j) dst[j] = step(j, t == 0);
+        return;
+    }
+    const int p = t + 1;
+    if (p >= Q) return;
+    for (long tt = 0; tt <= O; ++tt) (void)step(tt, true);
+    dd M[O][O], P[O][O];
+#pragma unroll
+    for (int i = 0; i < O; ++i)
+#pragma unroll
+        for (int j = 0; j < O; ++j) M[i][j] = {i == 0 ? -b[j] : (j == i - 1 ? 1.0 : 0.0), 0.0};
+    hz_dd::mat_pow<O>(M, (long)p * kSP - O - 1, P);
+#pragma unroll
+    for (int i = 0; i < O; ++i) {
+        dd acc{0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < O; ++j) acc = hz_dd::add(acc, hz_dd::mul(P[i][j], y[j]));
+        st[((long)band * Q + p) * O + i] = acc.hi;
     }
 }
 
-// A gain setter as a transient: d[tau] = sum_i delta_i r[tau][band_i] (the setter's bands in list
-// order), h += d (the new targets), h_D = rebase h_D - d (D_n = g_n(t) - gin_n loses delta_n).
-// Up to kChurnArg bands travel in the kernel arguments, with their new targets for d_gin (no host
-// copy, no stream synchronisation); longer lists come from device memory (gin uploaded by the caller)
+// sp[n][s][c][k2]: column c of series s of band n (s = 0: r0, s = 1 + k: phi_nk), grid (33, O + 1, N)
+__global__ __launch_bounds__(kT) void stream_rspec_kernel(const double* __restrict__ r0, const double* __restrict__ phi,
+                                                          int O, const double2* __restrict__ tw,
+                                                          double2* __restrict__ sp) {
+    __shared__ ColLds s;
+    const int c = blockIdx.x, sr = blockIdx.y, band = blockIdx.z;
+    const double* src = sr == 0 ? r0 + (long)band * kSP : phi + ((long)band * O + (sr - 1)) * kSP;
+    col_forward(s, tw, c, [&](int n) { return n < kSP ? src[n] * (1.0 / kSF) : 0.0; },
+                sp + (((long)band * (O + 1) + sr) * kCols + c) * 32);
+}
+
+// A gain setter's bands, in the kernel arguments with their new targets for d_gin (no host copy, no
+// stream synchronisation); kChurnArg per launch
 constexpr int kChurnArg = 24;
 struct ChurnList {
     int m;
@@ -586,24 +618,283 @@ struct ChurnList {
     double delta[kChurnArg];
     double gin[kChurnArg];
 };
-__global__ __launch_bounds__(256) void stream_churn_kernel(const double* __restrict__ r, int nbands, long K,
-                                                           ChurnList L, const double* __restrict__ dlist, int m,
-                                                           double rebase, double* __restrict__ h,
-                                                           double* __restrict__ hD, double* __restrict__ dv,
-                                                           double* __restrict__ gin) {
-    const long tau = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (blockIdx.x == 0 && (int)threadIdx.x < L.m) gin[L.band[threadIdx.x]] = L.gin[threadIdx.x];
-    if (tau >= K) return;
-    double d = 0.0;
-    if (L.m) {
-        for (int i = 0; i < L.m; ++i) d = fma(L.delta[i], r[(long)L.band[i] * K + tau], d);
-    } else {
-        for (int i = 0; i < m; ++i) d = fma(dlist[2 * i + 1], r[(long)dlist[2 * i] * K + tau], d);
+struct SetterArgs {
+    // the per-band responses in partition form (stream_rbasis_kernel)
+    const double* r0;
+    const double* phi;
+    const double* st;
+    const double2* sp;
+    long K;
+    int Q, O;
+    ChurnList L;          // the setter's bands (a longer list: one launch per kChurnArg bands)
+    double rebase;        // s_g^(pos - dref): h_D's decay since the previous setter
+    int dfirst;           // the first transient: h_D, its spectra and parities start from zero
+    double* h;            // [K] the bank response
+    double* hD;           // [K] the transient response
+    double2* HS;          // [Q + 8][33][32] their partition spectra
+    double2* HSD;
+    const double2* ZS;    // the window spectra ring, slot of Z_{b-p}: ring_slot(head, p, Q)
+    int head;
+    const double2* tw;
+    double2* C;           // [33][32] C_b, R_{b+1} as the next block launch reads them (prime2's
+    double2* R;           // outputs), and h_D's
+    double2* CD;
+    double2* RD;
+    // the smoothers' upkeep over the streamed samples (stream_upkeep_kernel), upkeep != 0
+    int upkeep, N;
+    double* pg;
+    const double* pin;
+    double* gin;
+    double sp_m, sg_m;
+    const double* line;
+    long last;
+    double* xhist;
+    int skip;             // (diagnostic, HZ_SETTER_SKIP: bit 0 columns, 1 taps, 2 upkeep return at once)
+    unsigned long long* stamps;   // (diagnostic, HZ_SETTER_STAMPS) [64][33][8] column phase times
+    unsigned long long* wstart;   // (diagnostic) [64][512] every workgroup's start
+};
+#define SET_STAMP(k)                                                                                     \
+    if (a.stamps) {                                                                                      \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                      \
+        if (t == 0) a.stamps[c * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                           \
     }
-    h[tau] += d;
-    hD[tau] = rebase * hD[tau] - d;
-    dv[tau] = d;
+
+
+// A gain setter as a transient, in ONE launch, by linearity (the transient algebra:
+// fb_stream_gain_setter).  With d = sum_i delta_i r_{band_i} (the setter's bands in list order):
+//   taps      h += d, h_D = rebase h_D - d                              (workgroups [33, 33 + K/256))
+//   spectra   dS_p = sum_i delta_i (S_ip . Phi_i) (partition 0: the r0 spectra), HS_p += dS_p,
+//             HS_D,p = rebase HS_D,p - dS_p                             (column workgroups [0, 33))
+//   parities  the C_b / R_{b+1} the next block launch reads (stream_prime2_kernel's outputs) move by
+//             the same MAC over the ring with dS: dY = sum_{p>=1} dS_p Z_{b-p}, C += inverse column(dY),
+//             R += sum_{p>=3} dS_p Z_{b+1-p}; h_D's C_D = rebase C_D - inverse(dY), R_D likewise --
+//             so no prime launch follows the setter
+//   upkeep    the smoothers over the streamed samples toward the targets they ran with, then the
+//             setter's new targets into gin (one thread reads and writes a band's)  (the last workgroups)
+// QI = Q / 8 partitions per column thread (p = g + 8 i).
+// Latency, not work, sets this launch's time (a handful of FMAs per operand): a load that waits for
+// an earlier load's value costs a whole memory round trip (~1 us).  So every load that does not
+// depend on the setter's bands is issued first, the bands' indices and weights come from the kernel
+// arguments (uniform: scalar loads), and each batch of kSetBatch bands issues all of its operand loads
+// before using any -- one round trip per batch.  (A first version with a band loop whose loads
+// waited on the previous band's took 17-21 us.)
+constexpr int kSetBatch = 12;
+struct SetterLds {
+    ColLds col;
+    double S[kSetBatch * 128 * 4];          // the batch's states S_np, [band][p][k] (Q <= 128, O <= 4)
+    double2 Ph[kSetBatch][5][32];           // the batch's spectra at this column (r0, phi_k)
+};
+template <int QI>
+__global__ __launch_bounds__(kT) void stream_setter_kernel(SetterArgs a) {
+    __shared__ SetterLds u;
+    const int t = threadIdx.x;
+    const int nt = (int)(a.K / kT);
+    const int mq = a.L.m;
+    const int O = a.O, Q = a.Q;
+    if (a.wstart && t == 0 && blockIdx.x < 512) a.wstart[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    if ((int)blockIdx.x >= kCols + nt) {   // upkeep
+        if (a.skip & 4) return;
+        const int b = (blockIdx.x - kCols - nt) * kT + t;
+        if (b < a.N) {
+            double gb = a.gin[b];
+            if (a.upkeep) {
+                const double P0 = a.pg[2 * b], G0 = a.pg[2 * b + 1], pb = a.pin[b];
+                a.pg[2 * b] = pb + a.sp_m * (P0 - pb);
+                a.pg[2 * b + 1] = gb + a.sg_m * (G0 - gb);
+            }
+#pragma unroll
+            for (int i = 0; i < kChurnArg; ++i) {   // (unrolled: the list's scalar loads issued together)
+                const bool hit = i < a.L.m && a.L.band[i] == b;
+                gb = hit ? a.L.gin[i] : gb;
+            }
+            a.gin[b] = gb;
+        }
+        if (a.upkeep && b < O) a.xhist[b] = a.line[a.last - b];
+        return;
+    }
+    if ((int)blockIdx.x >= kCols) {   // taps: 256 of partition tp (uniform over the workgroup)
+        if (a.skip & 2) return;
+        const long tau = (long)(blockIdx.x - kCols) * kT + t;
+        const int tp = (int)(tau / kSP), tj = (int)(tau % kSP);
+        const double hv = a.h[tau], hdv = a.dfirst ? 0.0 : a.hD[tau];
+        double d = 0.0;
+        for (int q0 = 0; q0 < mq; q0 += kSetBatch) {
+            long bl[kSetBatch];
+            double dl[kSetBatch], v[kSetBatch][4], sv[kSetBatch][4];
+#pragma unroll
+            for (int e = 0; e < kSetBatch; ++e) {   // (past the list: the last band again, weight 0)
+                const int q = min(q0 + e, mq - 1);
+                bl[e] = a.L.band[q];
+                dl[e] = q0 + e < mq ? a.L.delta[q] : 0.0;
+            }
+#pragma unroll
+            for (int e = 0; e < kSetBatch; ++e) {
+                if (tp == 0) {
+                    v[e][0] = a.r0[bl[e] * kSP + tj];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int kk = min(k, O - 1);
+                        v[e][k] = a.phi[(bl[e] * O + kk) * kSP + tj];
+                        sv[e][k] = a.st[(bl[e] * Q + tp) * O + kk];
+                    }
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < kSetBatch; ++e) {
+                double wv = v[e][0];
+                if (tp != 0) {
+                    wv = 0.0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) wv = fma(k < O ? sv[e][k] : 0.0, v[e][k], wv);
+                }
+                d = fma(dl[e], wv, d);
+            }
+        }
+        a.h[tau] = hv + d;
+        a.hD[tau] = a.dfirst ? -d : a.rebase * hdv - d;
+        return;
+    }
+    // column c
+    if (a.skip & 1) return;
+    const int c = blockIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
+    SET_STAMP(0)
+    // everything that does not depend on the setter's bands, in flight first
+    double2 z1[QI], z3[QI], hs[QI], hd[QI];
+#pragma unroll
+    for (int i = 0; i < QI; ++i) {
+        const int p = g + 8 * i;
+        const long at = ((long)p * kCols + c) * 32 + j;
+        z1[i] = a.ZS[((long)ring_slot(a.head, p, Q) * kCols + c) * 32 + j];   // Z_{b-p}
+        z3[i] = a.ZS[((long)ring_slot(a.head, p > 0 ? p - 1 : 0, Q) * kCols + c) * 32 + j];   // Z_{b+1-p}
+        hs[i] = a.HS[at];
+        hd[i] = a.dfirst ? make_double2(0.0, 0.0) : a.HSD[at];
+    }
+    ColTw ct;
+    ct.load(a.tw, c, j, g);
+    const double2 tcol = a.tw[kTw2k + j * c];
+    const int cat = c * 32 + (t & 31);
+    const double2 zero2 = make_double2(0.0, 0.0);
+    const double2 Cv = a.C[cat], Rv = a.R[cat];
+    const double2 CDv = a.dfirst ? zero2 : a.CD[cat], RDv = a.dfirst ? zero2 : a.RD[cat];
+    double2 dS[QI];
+#pragma unroll
+    for (int i = 0; i < QI; ++i) dS[i] = zero2;
+    const int QO = Q * O, n2 = (O + 1) * 32;
+    for (int q0 = 0; q0 < ((a.skip & 8) ? 0 : mq); q0 += kSetBatch) {
+        const int nb = min(kSetBatch, mq - q0), nS = nb * QO, nP = nb * n2;
+        long bl[kSetBatch];
+#pragma unroll
+        for (int e = 0; e < kSetBatch; ++e) bl[e] = a.L.band[min(q0 + e, mq - 1)];
+        // the batch's S rows and Ph columns into LDS: four of each per thread per round, every load of
+        // a round issued before its stores (indices clamped: always valid)
+        for (int e0 = 0; e0 < max(nS, nP); e0 += 4 * kT) {
+            double sv[4];
+            double2 pv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int e = e0 + t + r * kT;
+                const int es = min(e, nS - 1), qs = es / QO;
+                long bs = bl[0];
+#pragma unroll
+                for (int q = 1; q < kSetBatch; ++q) bs = qs == q ? bl[q] : bs;
+                sv[r] = a.st[bs * QO + (es - qs * QO)];
+                const int ep = min(e, nP - 1), qp = ep / n2, rest = ep - qp * n2;
+                long bp = bl[0];
+#pragma unroll
+                for (int q = 1; q < kSetBatch; ++q) bp = qp == q ? bl[q] : bp;
+                pv[r] = a.sp[((bp * (O + 1) + (rest >> 5)) * kCols + c) * 32 + (rest & 31)];
+            }
+            // (unconditional stores at the clamped indices -- past the batch they rewrite the last
+            // element with its own value -- so no load is sunk into a conditional store's block
+            // behind its own wait)
+            SET_STAMP(1)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int e = e0 + t + r * kT;
+                const int es = min(e, nS - 1), ep = min(e, nP - 1);
+                u.S[es] = sv[r];
+                (&u.Ph[0][0][0])[(ep / n2) * 5 * 32 + (ep % n2)] = pv[r];
+            }
+        }
+        __syncthreads();
+        SET_STAMP(2)
+        for (int qb = 0; qb < nb; ++qb) {
+            const double dq = a.L.delta[q0 + qb];
+#pragma unroll
+            for (int i = 0; i < QI; ++i) {
+                const int p = g + 8 * i;
+                double2 v;
+                if (p == 0) {
+                    v = u.Ph[qb][0][j];
+                } else {
+                    v = zero2;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (k < O) {
+                            const double sk = u.S[qb * QO + p * O + k];
+                            const double2 ph = u.Ph[qb][1 + k][j];
+                            v.x = fma(sk, ph.x, v.x);
+                            v.y = fma(sk, ph.y, v.y);
+                        }
+                    }
+                }
+                dS[i].x = fma(dq, v.x, dS[i].x);
+                dS[i].y = fma(dq, v.y, dS[i].y);
+            }
+        }
+        __syncthreads();
+    }
+    SET_STAMP(3)
+    if (a.skip & 16) return;
+    double2 y = zero2, r = zero2;
+#pragma unroll
+    for (int i = 0; i < QI; ++i) {
+        const int p = g + 8 * i;
+        const long at = ((long)p * kCols + c) * 32 + j;
+        a.HS[at] = cadd(hs[i], dS[i]);
+        a.HSD[at] = make_double2(a.rebase * hd[i].x - dS[i].x, a.rebase * hd[i].y - dS[i].y);
+        if (p >= 1) y = cadd(y, cmul(dS[i], z1[i]));
+        if (p >= 3) r = cadd(r, cmul(dS[i], z3[i]));
+    }
+    SET_STAMP(4)
+    ColLds& s = u.col;
+    y = half_sum(y);
+    r = half_sum(r);
+    if (l < 32) {
+        s.m[w][j] = y;
+        s.x[w][j] = r;
+    }
+    __syncthreads();
+    if (t < 32) {
+        s.y[t] = cadd(cadd(s.m[0][t], s.m[1][t]), cadd(s.m[2][t], s.m[3][t]));
+        const double2 dr = cadd(cadd(s.x[0][t], s.x[1][t]), cadd(s.x[2][t], s.x[3][t]));
+        a.R[cat] = cadd(Rv, dr);
+        a.RD[cat] = make_double2(a.rebase * RDv.x - dr.x, a.rebase * RDv.y - dr.y);
+    }
+    __syncthreads();
+    double2 cp = zero2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cp = cadd(cp, cmulc(ct.t32[q], s.y[4 * g + q]));
+    cp = half_sum(cp);
+    if (l < 32) s.c[w][j] = cp;
+    __syncthreads();
+    if (t < 32) {
+        const double2 dc = cmulc(tcol, cadd(cadd(s.c[0][t], s.c[1][t]), cadd(s.c[2][t], s.c[3][t])));
+        a.C[cat] = cadd(Cv, dc);
+        a.CD[cat] = make_double2(a.rebase * CDv.x - dc.x, a.rebase * CDv.y - dc.y);
+    }
+    SET_STAMP(5)
 }
+
+typedef void (*SetterKernel)(SetterArgs);
+template <int... I>
+SetterKernel pick_setter_impl(int qi, std::integer_sequence<int, I...>) {
+    SetterKernel k = nullptr;
+    ((qi == I + 1 ? (k = stream_setter_kernel<I + 1>, 0) : 0), ...);
+    return k;
+}
+SetterKernel pick_setter(int qi) { return pick_setter_impl(qi, std::make_integer_sequence<int, 16>()); }
 
 // line[i] = line[i + R] = src[i], i < n, from write position wpos
 __global__ __launch_bounds__(256) void stream_put_kernel(const double* __restrict__ src, long n, double* __restrict__ line,
@@ -766,6 +1057,7 @@ StreamArgs stream_args(hz_fb* h) {
     a.CDout = a.RDout = nullptr;
     a.dscale = 0.0;
     a.sgpow = nullptr;
+    a.wst = nullptr;
     return a;
 }
 
@@ -919,6 +1211,7 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
         HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
         h->ev_skip[(e - h->ev.data()) / 5] |= 2 | 8;
     }
+    if (S.d_stamps) a.wst = S.d_stamps + 64 * kCols * 8 + 64 * 512 + (size_t)(S.blk & 7) * 320;
     if (S.dmode) {   // a gain transient: + s_g^(t - dref + 1) conv(h_D, x), its roles in the same launch
         d_args(h, &a);
         // (compute() smooths before the sample's output, filterbank.h:172-173: D is g(dref - 1) -
@@ -1050,10 +1343,10 @@ void fb_stream_dclear(hz_fb* h) {
 
 // A setter that changed only gains (mix / open) while the bank streams stationary: keep streaming.
 // h += sum_n (gin'_n - gin_n) r_n, h_D = s_g^(pos - dref) h_D - (the same sum), dref = pos; both
-// responses' spectra again; the next block re-primes both passes' C / R from the (valid) ring.
+// responses' spectra and the C / R parities of the next block move by linearity in the same launch
+// (stream_setter_kernel, which also brings the smoothers up to date: fb_upload skips its upkeep).
 // Returns 0: not applicable here (the caller invalidates the response as before); 1: applied, d_gin
-// written by the update kernel (a short list: no host copy, no synchronisation); 2: applied, the
-// caller uploads d_gin.
+// written by the update launch (no host copy, no synchronisation).
 int fb_stream_gain_setter(hz_fb* h) {
     hz_fb::Resp& R = h->resp;
     hz_fb::Resp::Stream& S = R.st;
@@ -1063,7 +1356,8 @@ int fb_stream_gain_setter(hz_fb* h) {
         (int)S.gin_base.size() != N)
         return 0;
     const long K = S.K1;
-    if ((double)K * N * 8.0 > 8.0 * (1L << 30)) return 0;   // the per-band responses stay <= 8 GiB
+    if ((double)N * ((O + 1) * kSP + (double)(K / kSP) * O + (O + 1) * kCols * 64) * 8.0 > 8.0 * (1L << 30))
+        return 0;   // the per-band responses stay <= 8 GiB
     if (!S.dmode) {
         // the first transient: pre-amps converged (boost() invalidates instead, so this holds until
         // the transient ends) and gains converged to gin_base (later setters: g_n(t) - gin_base_n =
@@ -1079,36 +1373,39 @@ int fb_stream_gain_setter(hz_fb* h) {
             if (!(std::fabs(h->pg_host[2 * (size_t)b + 1] - S.gin_base[b]) <= 0x1p-60 * gmax)) return 0;
         }
     }
-    // the setter's bands
-    ChurnList L{};
+    // the setter's bands: one launch per kChurnArg of them (the updates add up; an all-band mix() of
+    // the 4096-band bank takes 171 launches, under a millisecond)
+    std::vector<ChurnList> lists;
     S.h_delta.clear();
     double dmx = 0;
     for (int b = 0; b < N; ++b) {
         const double d = h->gin[b] - S.gin_base[b];
         if (d != 0.0) {
-            if (L.m < kChurnArg) {
-                L.band[L.m] = b;
-                L.delta[L.m] = d;
-                L.gin[L.m] = h->gin[b];
+            if (lists.empty() || lists.back().m == kChurnArg) {
+                lists.emplace_back();
+                lists.back().m = 0;
             }
+            ChurnList& L = lists.back();
+            L.band[L.m] = b;
+            L.delta[L.m] = d;
+            L.gin[L.m] = h->gin[b];
             ++L.m;
             S.h_delta.push_back((double)b);
-            S.h_delta.push_back(d);
             dmx = std::max(dmx, std::fabs(d));
         }
     }
-    const int m = (int)(S.h_delta.size() / 2);
-    if (m == 0) return 1;
-    const bool by_value = m <= kChurnArg;
-    if (!by_value) L.m = 0;
+    if (lists.empty()) return 1;
     const size_t col = (size_t)kCols * 32 * 2;
     const int Q = (int)(K / kSP);
-    if (s_alloc(&S.d_rband, &S.rband_cap, (size_t)K * N) != HZ_OK || s_alloc(&S.d_hD, &S.hD_cap, (size_t)K) != HZ_OK ||
-        s_alloc(&S.d_dv, &S.dv_cap, (size_t)K) != HZ_OK ||
-        s_alloc(&S.d_delta, &S.delta_cap, S.h_delta.size()) != HZ_OK)
+    if (Q % 8 || Q / 8 > 16) return 0;   // (stream_setter_kernel: p = g + 8 i over QI = Q / 8)
+    if (s_alloc(&S.d_r0, &S.r0_cap, (size_t)N * kSP) != HZ_OK ||
+        s_alloc(&S.d_phi, &S.phi_cap, (size_t)N * O * kSP) != HZ_OK ||
+        s_alloc(&S.d_st, &S.st_cap, (size_t)N * Q * O) != HZ_OK ||
+        s_alloc(&S.d_rsp, &S.rsp_cap, (size_t)N * (O + 1) * col) != HZ_OK ||
+        s_alloc(&S.d_hD, &S.hD_cap, (size_t)K) != HZ_OK)
         return 0;
     const size_t hcap = S.hsd_cap;
-    if (s_alloc(&S.d_HSD, &S.hsd_cap, (size_t)(Q + 8) * col) != HZ_OK) return 0;
+    if (s_alloc(&S.d_HSD, &S.hsd_cap, (size_t)(Q + 8) * col) != HZ_OK) return 0;   // rows past Q stay zero
     if (S.hsd_cap != hcap && hipMemset(S.d_HSD, 0, sizeof(double) * S.hsd_cap) != hipSuccess) return 0;
     if (!S.d_CRD && hipMalloc(&S.d_CRD, sizeof(double) * 4 * col) != hipSuccess) return 0;
     if (S.sgpow_of != h->sg) {
@@ -1121,47 +1418,153 @@ int fb_stream_gain_setter(hz_fb* h) {
     if (!S.rband_valid) {   // r_n at the current coefficients and pre-amps (R.d_coef: resp_build_h)
         const double* F = R.d_coef;
         const double* Bc = R.d_coef + (size_t)N * (O + 1);
-        const unsigned g = (unsigned)((N + 63) / 64);
+        const dim3 g((unsigned)N, 2);
+        const double* pin = h->d_pin;
         switch (O) {
-        case 1: hipLaunchKernelGGL(stream_rband_kernel<1>, dim3(g), dim3(64), 0, h->stream, F, Bc, (const double*)h->d_pin, N, K, S.d_rband); break;
-        case 2: hipLaunchKernelGGL(stream_rband_kernel<2>, dim3(g), dim3(64), 0, h->stream, F, Bc, (const double*)h->d_pin, N, K, S.d_rband); break;
-        case 3: hipLaunchKernelGGL(stream_rband_kernel<3>, dim3(g), dim3(64), 0, h->stream, F, Bc, (const double*)h->d_pin, N, K, S.d_rband); break;
-        default: hipLaunchKernelGGL(stream_rband_kernel<4>, dim3(g), dim3(64), 0, h->stream, F, Bc, (const double*)h->d_pin, N, K, S.d_rband); break;
+        case 1: hipLaunchKernelGGL(stream_rbasis_kernel<1>, g, dim3(128), 0, h->stream, F, Bc, pin, Q, S.d_r0, S.d_phi, S.d_st); break;
+        case 2: hipLaunchKernelGGL(stream_rbasis_kernel<2>, g, dim3(128), 0, h->stream, F, Bc, pin, Q, S.d_r0, S.d_phi, S.d_st); break;
+        case 3: hipLaunchKernelGGL(stream_rbasis_kernel<3>, g, dim3(128), 0, h->stream, F, Bc, pin, Q, S.d_r0, S.d_phi, S.d_st); break;
+        default: hipLaunchKernelGGL(stream_rbasis_kernel<4>, g, dim3(128), 0, h->stream, F, Bc, pin, Q, S.d_r0, S.d_phi, S.d_st); break;
         }
+        hipLaunchKernelGGL(stream_rspec_kernel, dim3(kCols, (unsigned)(O + 1), (unsigned)N), dim3(kT), 0, h->stream,
+                           (const double*)S.d_r0, (const double*)S.d_phi, O, (const double2*)S.d_tw, (double2*)S.d_rsp);
         if (hipGetLastError() != hipSuccess) return 0;
         S.rband_valid = true;
     }
-    if (!S.dmode && (hipMemsetAsync(S.d_hD, 0, sizeof(double) * K, h->stream) != hipSuccess ||
-                     hipMemsetAsync(S.d_HSD, 0, sizeof(double) * (size_t)Q * col, h->stream) != hipSuccess))
-        return 0;
-    const double rebase = S.dmode ? (double)powl((long double)h->sg, (long double)(S.pos - S.dref)) : 0.0;
-    // (a long list from device memory: the caller's upload synchronises the stream before h_delta
-    // changes again)
-    if (!by_value && hipMemcpyAsync(S.d_delta, S.h_delta.data(), sizeof(double) * S.h_delta.size(),
-                                    hipMemcpyHostToDevice, h->stream) != hipSuccess)
-        return 0;
-    hipLaunchKernelGGL(stream_churn_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, h->stream,
-                       (const double*)S.d_rband, N, K, L, (const double*)S.d_delta, m, rebase, R.d_h, S.d_hD, S.d_dv,
-                       h->d_gin);
-    hipLaunchKernelGGL(stream_hsd_kernel, dim3(kCols, (unsigned)Q), dim3(kT), 0, h->stream, (const double*)S.d_dv,
-                       (const double2*)S.d_tw, rebase, (double2*)S.d_HS, (double2*)S.d_HSD);
+    const bool dfirst = !S.dmode;
+    const double rebase = dfirst ? 0.0 : (double)powl((long double)h->sg, (long double)(S.pos - S.dref));
+    // the C / R parities the next block launch reads: the outputs of launch blk - 1 (as prime2)
+    const long blk = S.blk;
+    S.blk = blk - 1;
+    StreamArgs ap = stream_args(h);
+    d_args(h, &ap);
+    S.blk = blk;
+    SetterArgs sa{};
+    sa.r0 = S.d_r0;
+    sa.phi = S.d_phi;
+    sa.st = S.d_st;
+    sa.sp = (const double2*)S.d_rsp;
+    sa.K = K;
+    sa.Q = Q;
+    sa.O = O;
+    sa.rebase = rebase;
+    sa.dfirst = dfirst ? 1 : 0;
+    sa.h = R.d_h;
+    sa.hD = S.d_hD;
+    sa.HS = (double2*)S.d_HS;
+    sa.HSD = (double2*)S.d_HSD;
+    sa.ZS = (const double2*)S.d_ZS;
+    sa.head = S.head;
+    sa.tw = (const double2*)S.d_tw;
+    sa.C = ap.Cout;
+    sa.R = ap.Rout;
+    sa.CD = ap.CDout;
+    sa.RD = ap.RDout;
+    sa.N = N;
+    sa.pg = h->d_pg[h->scur];
+    sa.pin = h->d_pin;
+    sa.gin = h->d_gin;
+    sa.line = S.d_line;
+    sa.xhist = h->d_xhist[h->xcur];
+    if (S.pend > 0) {   // fb_stream_upkeep's work, folded into the launch
+        sa.upkeep = 1;
+        sa.sp_m = (double)powl((long double)h->sp, (long double)S.pend);
+        sa.sg_m = (double)powl((long double)h->sg, (long double)S.pend);
+        sa.last = ring_index(S, S.pos - 1) + S.R;
+        S.pend = 0;
+    }
+    static const int skip = getenv("HZ_SETTER_SKIP") ? atoi(getenv("HZ_SETTER_SKIP")) : 0;
+    sa.skip = skip;
+    if (getenv("HZ_SETTER_STAMPS")) {   // (diagnostic) mean column phase times every 64 setters, ns
+        const size_t nstamp = 64 * kCols * 8 + 64 * 512 + 8 * 320;
+        if (!S.d_stamps && hipMalloc(&S.d_stamps, sizeof(unsigned long long) * nstamp) != hipSuccess) return 0;
+        static long nst = 0, blk_at[64];
+        const unsigned nwg = (unsigned)std::min<long>(512, kCols + K / kT + (N + kT - 1) / kT);
+        if (nst == 64) {
+            std::vector<unsigned long long> st(nstamp);
+            if (hipMemcpy(st.data(), S.d_stamps, sizeof(unsigned long long) * st.size(), hipMemcpyDeviceToHost) == hipSuccess) {
+                double acc[8] = {0}, c0 = 0, cmax = 0, wmax = 0;
+                for (long i = 0; i < 64; ++i) {
+                    const unsigned long long* ws = &st[64 * kCols * 8 + i * 512];
+                    unsigned long long w0 = ws[0], w1 = ws[0];
+                    for (unsigned b = 0; b < nwg; ++b) {
+                        w0 = std::min(w0, ws[b]);
+                        w1 = std::max(w1, ws[b]);
+                    }
+                    wmax += 10.0 * (double)(w1 - w0);
+                    unsigned long long cs = ~0ull, ce = 0;
+                    for (int c = 0; c < kCols; ++c) {
+                        const unsigned long long* e = &st[(i * kCols + c) * 8];
+                        for (int k = 1; k < 6; ++k) acc[k] += 10.0 * (double)(e[k] - e[0]);
+                        cs = std::min(cs, e[0]);
+                        ce = std::max(ce, e[5]);
+                    }
+                    c0 += 10.0 * (double)(cs - w0);
+                    cmax += 10.0 * (double)(ce - w0);
+                }
+                {   // the latest setter (nst - 1 == 63) against the block before it (blk - 1) and after it
+                    const unsigned long long* ws = &st[64 * kCols * 8 + 63 * 512];
+                    unsigned long long w0 = ~0ull;
+                    for (unsigned b = 0; b < nwg; ++b) w0 = std::min(w0, ws[b]);
+                    unsigned long long ce = 0;
+                    for (int c = 0; c < kCols; ++c) ce = std::max(ce, st[(63 * kCols + c) * 8 + 5]);
+                    const unsigned long long* bp = &st[64 * kCols * 8 + 64 * 512 + (size_t)((blk_at[63] - 1) & 7) * 320];
+                    const unsigned long long* bn = &st[64 * kCols * 8 + 64 * 512 + (size_t)(blk_at[63] & 7) * 320];
+                    unsigned long long be = 0, bs = ~0ull, ns0 = ~0ull, ne = 0;
+                    for (int b = 0; b < kBlockWG; ++b) {
+                        be = std::max(be, bp[160 + b]);
+                        bs = std::min(bs, bp[b]);
+                        ne = std::max(ne, bn[160 + b]);
+                        ns0 = std::min(ns0, bn[b]);
+                    }
+                    std::fprintf(stderr, "block before: %.0f ns; its last end -> setter first start %.0f ns; setter last "
+                                 "column end -> next block first start %.0f ns; next block %.0f ns\n",
+                                 10.0 * (double)(be - bs), 10.0 * (double)((long long)(w0 - be)),
+                                 10.0 * (double)((long long)(ns0 - ce)), 10.0 * (double)(ne - ns0));
+                }
+                std::fprintf(stderr, "setter column phases, ns after the workgroup's start:");
+                for (int k = 1; k < 6; ++k) std::fprintf(stderr, " %d:%.0f", k, acc[k] / (64.0 * kCols));
+                std::fprintf(stderr, "; first column start %.0f, last column end %.0f, last workgroup start %.0f ns after the first\n",
+                             c0 / 64, cmax / 64, wmax / 64);
+            }
+            nst = 0;
+        }
+        blk_at[nst] = S.blk;
+        sa.stamps = S.d_stamps + (size_t)nst * kCols * 8;
+        sa.wstart = S.d_stamps + 64 * kCols * 8 + (size_t)nst * 512;
+        ++nst;
+    }
+    const unsigned wg = (unsigned)(kCols + K / kT + (N + kT - 1) / kT);
+    for (size_t i = 0; i < lists.size(); ++i) {   // (later lists: h_D already rebased, upkeep done)
+        sa.L = lists[i];
+        if (i > 0) {
+            sa.rebase = 1.0;
+            sa.dfirst = 0;
+            sa.upkeep = 0;
+        }
+        hipLaunchKernelGGL(pick_setter(Q / 8), dim3(wg), dim3(kT), 0, h->stream, sa);
+    }
     if (hipGetLastError() != hipSuccess) return 0;
     S.dmax = rebase * S.dmax + dmx;
     S.dref = S.pos;
     S.dmode = true;
-    S.prime_main = S.prime_d = true;
+    // (the parities moved with the spectra: no prime; a prime already pending recomputes them from the
+    // updated spectra anyway -- h_D's start exact at the first transient)
+    if (dfirst) S.prime_d = false;
     ++S.dsetters;
-    for (size_t i = 0; i < S.h_delta.size(); i += 2) S.gin_base[(size_t)S.h_delta[i]] = h->gin[(size_t)S.h_delta[i]];
+    for (double b : S.h_delta) S.gin_base[(size_t)b] = h->gin[(size_t)b];
     S.gin_max = 0;
     for (double v : S.gin_base) S.gin_max = std::max(S.gin_max, std::fabs(v));
-    return by_value ? 1 : 2;
+    return 1;
 }
 
 void fb_stream_free(hz_fb* h) {
     hz_fb::Resp::Stream& S = h->resp.st;
     (void)tail_quiet(S);
+    if (S.d_stamps) (void)hipFree(S.d_stamps);
+    S.d_stamps = nullptr;
     for (double* p : {S.d_line, S.d_ZS, S.d_HS, S.d_CR, S.d_tw, S.d_tH, S.d_tZ, S.d_tY, S.d_tout, S.d_hD, S.d_HSD,
-                      S.d_CRD, S.d_rband, S.d_sgpow, S.d_delta, S.d_dv})
+                      S.d_CRD, S.d_r0, S.d_phi, S.d_st, S.d_rsp, S.d_sgpow})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : {S.ev_main, S.ev_tail[0], S.ev_tail[1]})
         if (e) (void)hipEventDestroy(e);

@@ -639,9 +639,14 @@ int fb_upload(hz_fb* h) {
     // LAZY band states of a stationary call follow from the coefficients and pre-amps it ran
     // with: materialise them before new ones reach the device
     if (h->resp.implicit && (h->dirty_coef || h->dirty_pin || h->tv_pending)) HZ_TRY(hz_fbi::fb_resp_materialize(h));
+    // gains only, while the bank streams stationary: a transient of the streaming engine instead of
+    // a new response and K samples of history (hz_fb_stream.hip fb_stream_gain_setter; its launch
+    // also brings the smoothers up to date and writes d_gin)
+    const int transient = (h->dirty_gin && !h->dirty_pin && !h->dirty_coef && !h->tv_pending)
+                              ? hz_fbi::fb_stream_gain_setter(h) : 0;
     // streamed samples bring the smoothers up to date lazily, toward the targets they ran with:
     // apply them before new targets (mix / boost) reach the device
-    if (h->dirty_pin || h->dirty_gin) HZ_TRY(hz_fbi::fb_stream_upkeep(h));
+    if (!transient && (h->dirty_pin || h->dirty_gin)) HZ_TRY(hz_fbi::fb_stream_upkeep(h));
     HZ_TRY(hz_fbi::fb_tv_materialize(h));
     if (h->dirty_coef) {
         const int O = h->order;
@@ -660,9 +665,6 @@ int fb_upload(hz_fb* h) {
         uploaded = true;
     }
     if (h->dirty_pin) h->resp.st.rband_valid = false;   // r_n are at pre = pin
-    // gains only, while the bank streams stationary: a transient of the streaming engine instead of
-    // a new response and K samples of history (hz_fb_stream.hip fb_stream_gain_setter)
-    const int transient = (h->dirty_gin && !h->dirty_pin && !uploaded && !h->tv_pending) ? hz_fbi::fb_stream_gain_setter(h) : 0;
     if (h->dirty_pin || h->dirty_gin) {
         for (auto& st : h->lti_set) st.fmix_valid = false;
         if (!transient) hz_fbi::fb_resp_invalidate(h, false);

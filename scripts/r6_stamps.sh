@@ -1,0 +1,15 @@
+#!/bin/bash
+# (diagnostic) per-phase times of the setter launch's column workgroups (HZ_SETTER_STAMPS)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+D=gpurun_out/r6/stamps
+mkdir -p $D
+python3 - <<'PY'
+import sys, numpy as np
+sys.path.insert(0, ".")
+import bench
+f, b = bench.c2_coefficients()
+np.concatenate([np.asarray(f)[:, :3], np.asarray(b)[:, :2]], axis=1).astype(np.float64).tofile("gpurun_out/r6/stamps/coef.bin")
+np.random.default_rng(1).uniform(-1, 1, 480000).tofile("gpurun_out/r6/stamps/x.bin")
+PY
+/opt/rocm/bin/hipcc -std=c++17 -O2 -I include tests/cpp/churn.cpp -o $D/churn -L huygens_amd/lib -lhuygens_hip -Wl,-rpath,$PWD/huygens_amd/lib || exit 1
+for sk in 0 6; do HZ_SETTER_SKIP=$sk HZ_SETTER_STAMPS=1 timeout -k 10 120 $D/churn $D 2> $D/err$sk.log && echo "skip $sk" && sort $D/err$sk.log | uniq -c | head -5; done

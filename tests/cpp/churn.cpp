@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -47,6 +48,8 @@ int main(int argc, char** argv) {
     if (hipMalloc((void**)&dx, sizeof(double) * n) || hipMalloc((void**)&dy, sizeof(double) * n)) return 3;
     if (hipMemcpy(dx, x.data(), sizeof(double) * n, hipMemcpyHostToDevice)) return 3;
     for (int i = 0; i < 3; ++i) CHECK(hz_fb_process_device(h, dx, dy, n));   // converge, fill the history
+    // (diagnostic) HZ_CHURN_SPAN: the setters' bands drawn from [0, span) instead of all N
+    const int span = std::getenv("HZ_CHURN_SPAN") ? std::max(9, std::min(N, std::atoi(std::getenv("HZ_CHURN_SPAN")))) : N;
     unsigned long long lcg = 12345;
     auto rnd = [&]() { lcg = lcg * 6364136223846793005ULL + 1442695040888963407ULL; return (unsigned)(lcg >> 33); };
     double us[2] = {0, 0};
@@ -62,7 +65,7 @@ int main(int argc, char** argv) {
             bool set = false;
             auto c0 = std::chrono::steady_clock::now();
             if (pass == 1 && (i * B) / 4800 != ((i - 1) * B) / 4800) {
-                for (int j = 0; j < 9; ++j) CHECK(hz_fb_mix(h, (int)(rnd() % N), 0.5 + (rnd() % 1000) / 1000.0));
+                for (int j = 0; j < 9; ++j) CHECK(hz_fb_mix(h, (int)(rnd() % span), 0.5 + (rnd() % 1000) / 1000.0));
                 ++setters;
                 set = true;
             }
