@@ -14,12 +14,13 @@ input already resident in HBM; the result is identical to 469 x {1024-sample blo
 Multi-GPU (one process per GPU): `bench.py --gpus N` outside a launcher reruns itself under
 `torch.distributed.run --nproc-per-node N` as a child process before any torch / HIP import and
 forwards rank 0's JSON line; under a launcher WORLD_SIZE must equal --gpus (else exit 2).  At
-N > 1 `value` is north_star's decomposition, STRONG scaling: a fixed 10 s call per step with the
-4096 bands partitioned over the ranks (each rank's engine on its own band shard) and the partial
-mixes summed to rank 0 by an RCCL reduce, src/filterbank.h:130's mixdown sum sharded (the reduce
-of one step overlaps the next step's compute, double-buffered).  The time-split stationary call
-(N x 10 s per step, each rank outputs its 10 s from the shared input with a K-sample halo; weak
-scaling, no data-path collective) is reported beside it as side.time_split_weak.
+N > 1 `value` is the fixed 10 s call split by TIME over the ranks (STRONG scaling): every rank holds
+the whole bank's response (one all-reduce at setup) and its own band shard's states, convolves its
+run of 2048-sample output blocks from the shared input, and keeps its share -- no data-path
+collective in the step.  side.gather_to_rank0 adds one RCCL gather of the shares per
+step; side.band_partition_stationary is north_star's band partition (each rank's band shard over the
+whole call, partial mixes summed to rank 0 by an RCCL reduce).  `--emulate-world P --emulate-rank r`
+runs rank r of P alone on one GPU (its per-rank step; value = the whole job's band-samples over it).
 """
 from __future__ import annotations
 

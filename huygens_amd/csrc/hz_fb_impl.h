@@ -294,7 +294,8 @@ struct hz_fb {
             double* d_sgpow = nullptr;   // s_g^j, j < 1024
             double sgpow_of = -1;        // the s_g it holds
             std::vector<double> h_delta;   // the last setter's bands
-            unsigned long long* d_stamps = nullptr;   // (diagnostic) setter launch phase stamps
+            unsigned long long* d_trace = nullptr;   // (diagnostic, HZ_STREAM_TRACE) launch timelines
+            int trace_n = 0, trace_kind[1024] = {}, trace_wg[1024] = {};
             std::vector<double> gin_base;   // the gins d_h is built with
             bool prime_main = false;     // C / R of the main pass to recompute (h changed, ring valid)
             bool prime_d = false;        // ... of the D pass

@@ -178,7 +178,7 @@ struct StreamArgs {
     double2* RDout;
     double dscale;
     const double* sgpow;
-    unsigned long long* wst;   // (diagnostic, HZ_SETTER_STAMPS) [2][160]: every workgroup's start and end
+    unsigned long long* trace;   // (diagnostic, HZ_STREAM_TRACE) [2][512]: every workgroup's start and end
 };
 
 // all of this workgroup's stores complete, then one system-scope release of the flag
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
     using Lds = typename std::conditional<DUAL, StreamLdsD, StreamLds>::type;
     __shared__ Lds u;
     const int blk = blockIdx.x;
-    if (a.wst && threadIdx.x == 0) a.wst[blk] = __builtin_amdgcn_s_memrealtime();
+    if (a.trace && threadIdx.x == 0) a.trace[blk] = __builtin_amdgcn_s_memrealtime();
     constexpr int kOut0 = 2 * kCols, kOut1 = 2 * kCols + kSP / 64;
     if (blk < kCols) {
         role_transform<true>(a, a.HS, a.Rin, a.Cout, u.col, blk);
@@ -493,9 +493,9 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
         else role_mac<QI>(a, a.HSD, a.RDout, u.col, blk - kOut1 - kCols);
     }
     post_done(a);
-    if (a.wst) {
+    if (a.trace) {
         __syncthreads();
-        if (threadIdx.x == 0) a.wst[160 + blk] = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) a.trace[512 + blk] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -650,14 +650,8 @@ struct SetterArgs {
     long last;
     double* xhist;
     int skip;             // (diagnostic, HZ_SETTER_SKIP: bit 0 columns, 1 taps, 2 upkeep return at once)
-    unsigned long long* stamps;   // (diagnostic, HZ_SETTER_STAMPS) [64][33][8] column phase times
-    unsigned long long* wstart;   // (diagnostic) [64][512] every workgroup's start
+    unsigned long long* trace;    // (diagnostic, HZ_STREAM_TRACE) [2][512]: every workgroup's start and end
 };
-#define SET_STAMP(k)                                                                                     \
-    if (a.stamps) {                                                                                      \
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                      \
-        if (t == 0) a.stamps[c * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                           \
-    }
 
 
 // A gain setter as a transient, in ONE launch, by linearity (the transient algebra:
@@ -685,13 +679,11 @@ struct SetterLds {
     double2 Ph[kSetBatch][5][32];           // the batch's spectra at this column (r0, phi_k)
 };
 template <int QI>
-__global__ __launch_bounds__(kT) void stream_setter_kernel(SetterArgs a) {
-    __shared__ SetterLds u;
+__device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) {
     const int t = threadIdx.x;
     const int nt = (int)(a.K / kT);
     const int mq = a.L.m;
     const int O = a.O, Q = a.Q;
-    if (a.wstart && t == 0 && blockIdx.x < 512) a.wstart[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     if ((int)blockIdx.x >= kCols + nt) {   // upkeep
         if (a.skip & 4) return;
         const int b = (blockIdx.x - kCols - nt) * kT + t;
@@ -758,7 +750,6 @@ __global__ __launch_bounds__(kT) void stream_setter_kernel(SetterArgs a) {
     // column c
     if (a.skip & 1) return;
     const int c = blockIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
-    SET_STAMP(0)
     // everything that does not depend on the setter's bands, in flight first
     double2 z1[QI], z3[QI], hs[QI], hd[QI];
 #pragma unroll
@@ -808,7 +799,6 @@ __global__ __launch_bounds__(kT) void stream_setter_kernel(SetterArgs a) {
             // (unconditional stores at the clamped indices -- past the batch they rewrite the last
             // element with its own value -- so no load is sunk into a conditional store's block
             // behind its own wait)
-            SET_STAMP(1)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int e = e0 + t + r * kT;
@@ -818,7 +808,6 @@ __global__ __launch_bounds__(kT) void stream_setter_kernel(SetterArgs a) {
             }
         }
         __syncthreads();
-        SET_STAMP(2)
         for (int qb = 0; qb < nb; ++qb) {
             const double dq = a.L.delta[q0 + qb];
 #pragma unroll
@@ -845,7 +834,6 @@ __global__ __launch_bounds__(kT) void stream_setter_kernel(SetterArgs a) {
         }
         __syncthreads();
     }
-    SET_STAMP(3)
     if (a.skip & 16) return;
     double2 y = zero2, r = zero2;
 #pragma unroll
@@ -857,7 +845,6 @@ __global__ __launch_bounds__(kT) void stream_setter_kernel(SetterArgs a) {
         if (p >= 1) y = cadd(y, cmul(dS[i], z1[i]));
         if (p >= 3) r = cadd(r, cmul(dS[i], z3[i]));
     }
-    SET_STAMP(4)
     ColLds& s = u.col;
     y = half_sum(y);
     r = half_sum(r);
@@ -884,7 +871,17 @@ __global__ __launch_bounds__(kT) void stream_setter_kernel(SetterArgs a) {
         a.C[cat] = cadd(Cv, dc);
         a.CD[cat] = make_double2(a.rebase * CDv.x - dc.x, a.rebase * CDv.y - dc.y);
     }
-    SET_STAMP(5)
+}
+
+template <int QI>
+__global__ __launch_bounds__(kT) void stream_setter_kernel(SetterArgs a) {
+    __shared__ SetterLds u;
+    if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    setter_roles<QI>(a, u);
+    if (a.trace) {
+        __syncthreads();
+        if (threadIdx.x == 0) a.trace[512 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 typedef void (*SetterKernel)(SetterArgs);
@@ -1057,7 +1054,7 @@ StreamArgs stream_args(hz_fb* h) {
     a.CDout = a.RDout = nullptr;
     a.dscale = 0.0;
     a.sgpow = nullptr;
-    a.wst = nullptr;
+    a.trace = nullptr;
     return a;
 }
 
@@ -1120,6 +1117,40 @@ int tail_schedule(hz_fb* h) {
         S.tail_launched = e + 1;
     }
     return HZ_OK;
+}
+
+// (diagnostic, HZ_STREAM_TRACE=<file>) every streaming launch's workgroup start / end times
+// (s_memrealtime, 100 MHz): launches are logged in a device buffer of kTraceN slots and appended to
+// the file as {int32 kind (0 block, 1 block with a transient, 2 setter), int32 workgroups,
+// uint64 start[512], uint64 end[512]} records when it fills and when the handle's stream state is freed
+constexpr int kTraceN = 1024;
+void trace_flush(hz_fb* h) {
+    hz_fb::Resp::Stream& S = h->resp.st;
+    if (!S.d_trace || S.trace_n == 0) return;
+    std::vector<unsigned long long> buf((size_t)S.trace_n * 1024);
+    if (hipStreamSynchronize(h->stream) == hipSuccess &&
+        hipMemcpy(buf.data(), S.d_trace, sizeof(unsigned long long) * buf.size(), hipMemcpyDeviceToHost) == hipSuccess) {
+        if (FILE* f = std::fopen(getenv("HZ_STREAM_TRACE"), "ab")) {
+            for (int i = 0; i < S.trace_n; ++i) {
+                const int hdr[2] = {S.trace_kind[i], S.trace_wg[i]};
+                std::fwrite(hdr, sizeof(int), 2, f);
+                std::fwrite(&buf[(size_t)i * 1024], sizeof(unsigned long long), 1024, f);
+            }
+            std::fclose(f);
+        }
+    }
+    S.trace_n = 0;
+}
+unsigned long long* trace_slot(hz_fb* h, int kind) {
+    static const bool on = getenv("HZ_STREAM_TRACE") != nullptr;
+    if (!on) return nullptr;
+    hz_fb::Resp::Stream& S = h->resp.st;
+    if (!S.d_trace && hipMalloc(&S.d_trace, sizeof(unsigned long long) * kTraceN * 1024) != hipSuccess) return nullptr;
+    if (S.trace_n == kTraceN) trace_flush(h);
+    const int i = S.trace_n++;
+    S.trace_kind[i] = kind;
+    S.trace_wg[i] = kind == 2 ? (int)(kCols + S.K1 / kT + (h->N + kT - 1) / kT) : (kind == 1 ? kBlockWGD : kBlockWG);
+    return S.d_trace + (size_t)i * 1024;
 }
 
 }  // namespace
@@ -1211,7 +1242,7 @@ int fb_launch_stream(hz_fb* h, const double* d_in, double* d_out, long n) {
         HZ_TRY_HIP(hipEventRecord(e[0], h->stream));
         h->ev_skip[(e - h->ev.data()) / 5] |= 2 | 8;
     }
-    if (S.d_stamps) a.wst = S.d_stamps + 64 * kCols * 8 + 64 * 512 + (size_t)(S.blk & 7) * 320;
+    a.trace = trace_slot(h, S.dmode ? 1 : 0);
     if (S.dmode) {   // a gain transient: + s_g^(t - dref + 1) conv(h_D, x), its roles in the same launch
         d_args(h, &a);
         // (compute() smooths before the sample's output, filterbank.h:172-173: D is g(dref - 1) -
@@ -1475,65 +1506,7 @@ int fb_stream_gain_setter(hz_fb* h) {
     }
     static const int skip = getenv("HZ_SETTER_SKIP") ? atoi(getenv("HZ_SETTER_SKIP")) : 0;
     sa.skip = skip;
-    if (getenv("HZ_SETTER_STAMPS")) {   // (diagnostic) mean column phase times every 64 setters, ns
-        const size_t nstamp = 64 * kCols * 8 + 64 * 512 + 8 * 320;
-        if (!S.d_stamps && hipMalloc(&S.d_stamps, sizeof(unsigned long long) * nstamp) != hipSuccess) return 0;
-        static long nst = 0, blk_at[64];
-        const unsigned nwg = (unsigned)std::min<long>(512, kCols + K / kT + (N + kT - 1) / kT);
-        if (nst == 64) {
-            std::vector<unsigned long long> st(nstamp);
-            if (hipMemcpy(st.data(), S.d_stamps, sizeof(unsigned long long) * st.size(), hipMemcpyDeviceToHost) == hipSuccess) {
-                double acc[8] = {0}, c0 = 0, cmax = 0, wmax = 0;
-                for (long i = 0; i < 64; ++i) {
-                    const unsigned long long* ws = &st[64 * kCols * 8 + i * 512];
-                    unsigned long long w0 = ws[0], w1 = ws[0];
-                    for (unsigned b = 0; b < nwg; ++b) {
-                        w0 = std::min(w0, ws[b]);
-                        w1 = std::max(w1, ws[b]);
-                    }
-                    wmax += 10.0 * (double)(w1 - w0);
-                    unsigned long long cs = ~0ull, ce = 0;
-                    for (int c = 0; c < kCols; ++c) {
-                        const unsigned long long* e = &st[(i * kCols + c) * 8];
-                        for (int k = 1; k < 6; ++k) acc[k] += 10.0 * (double)(e[k] - e[0]);
-                        cs = std::min(cs, e[0]);
-                        ce = std::max(ce, e[5]);
-                    }
-                    c0 += 10.0 * (double)(cs - w0);
-                    cmax += 10.0 * (double)(ce - w0);
-                }
-                {   // the latest setter (nst - 1 == 63) against the block before it (blk - 1) and after it
-                    const unsigned long long* ws = &st[64 * kCols * 8 + 63 * 512];
-                    unsigned long long w0 = ~0ull;
-                    for (unsigned b = 0; b < nwg; ++b) w0 = std::min(w0, ws[b]);
-                    unsigned long long ce = 0;
-                    for (int c = 0; c < kCols; ++c) ce = std::max(ce, st[(63 * kCols + c) * 8 + 5]);
-                    const unsigned long long* bp = &st[64 * kCols * 8 + 64 * 512 + (size_t)((blk_at[63] - 1) & 7) * 320];
-                    const unsigned long long* bn = &st[64 * kCols * 8 + 64 * 512 + (size_t)(blk_at[63] & 7) * 320];
-                    unsigned long long be = 0, bs = ~0ull, ns0 = ~0ull, ne = 0;
-                    for (int b = 0; b < kBlockWG; ++b) {
-                        be = std::max(be, bp[160 + b]);
-                        bs = std::min(bs, bp[b]);
-                        ne = std::max(ne, bn[160 + b]);
-                        ns0 = std::min(ns0, bn[b]);
-                    }
-                    std::fprintf(stderr, "block before: %.0f ns; its last end -> setter first start %.0f ns; setter last "
-                                 "column end -> next block first start %.0f ns; next block %.0f ns\n",
-                                 10.0 * (double)(be - bs), 10.0 * (double)((long long)(w0 - be)),
-                                 10.0 * (double)((long long)(ns0 - ce)), 10.0 * (double)(ne - ns0));
-                }
-                std::fprintf(stderr, "setter column phases, ns after the workgroup's start:");
-                for (int k = 1; k < 6; ++k) std::fprintf(stderr, " %d:%.0f", k, acc[k] / (64.0 * kCols));
-                std::fprintf(stderr, "; first column start %.0f, last column end %.0f, last workgroup start %.0f ns after the first\n",
-                             c0 / 64, cmax / 64, wmax / 64);
-            }
-            nst = 0;
-        }
-        blk_at[nst] = S.blk;
-        sa.stamps = S.d_stamps + (size_t)nst * kCols * 8;
-        sa.wstart = S.d_stamps + 64 * kCols * 8 + (size_t)nst * 512;
-        ++nst;
-    }
+    sa.trace = trace_slot(h, 2);
     const unsigned wg = (unsigned)(kCols + K / kT + (N + kT - 1) / kT);
     for (size_t i = 0; i < lists.size(); ++i) {   // (later lists: h_D already rebased, upkeep done)
         sa.L = lists[i];
@@ -1561,8 +1534,9 @@ int fb_stream_gain_setter(hz_fb* h) {
 void fb_stream_free(hz_fb* h) {
     hz_fb::Resp::Stream& S = h->resp.st;
     (void)tail_quiet(S);
-    if (S.d_stamps) (void)hipFree(S.d_stamps);
-    S.d_stamps = nullptr;
+    trace_flush(h);
+    if (S.d_trace) (void)hipFree(S.d_trace);
+    S.d_trace = nullptr;
     for (double* p : {S.d_line, S.d_ZS, S.d_HS, S.d_CR, S.d_tw, S.d_tH, S.d_tZ, S.d_tY, S.d_tout, S.d_hD, S.d_HSD,
                       S.d_CRD, S.d_r0, S.d_phi, S.d_st, S.d_rsp, S.d_sgpow})
         if (p) (void)hipFree(p);
