@@ -267,6 +267,7 @@ struct OutLds {
     double2 tw[64];
     double part[32][65];      // head partials [tap group][output]
     double tpart[4][64];      // tail partials [column group][output]
+    double red[4][64];        // head partials summed over 8 tap groups
 };
 // (a gain transient, FUSED) the same for h_D
 struct OutLdsD {
@@ -275,6 +276,7 @@ struct OutLdsD {
     double2 colD[kCols][32];
     double partD[32][65];
     double tpartD[4][64];
+    double redD[4][64];
 };
 union StreamLds {
     ColLds col;
@@ -449,16 +451,26 @@ __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
         tail_partials(u.colD, s.tw, t0, u.tpartD);
     }
     __syncthreads();
-    if (t < 64) {
-        double y = 0.0;
+    // the 32 head partials of each output: 8 per thread over all 256 threads (independent LDS reads,
+    // one round trip), then 4 per output -- a 32-read chain on one wave was the role's critical path
+    {
+        const int o = t & 63, qg = t >> 6;
+        double h8[8], h8d[8];
 #pragma unroll
-        for (int q = 0; q < 32; ++q) y += s.part[q][t];
+        for (int i = 0; i < 8; ++i) {
+            h8[i] = s.part[8 * qg + i][o];
+            if constexpr (DUAL) h8d[i] = u.partD[8 * qg + i][o];
+        }
+        s.red[qg][o] = ((h8[0] + h8[1]) + (h8[2] + h8[3])) + ((h8[4] + h8[5]) + (h8[6] + h8[7]));
+        if constexpr (DUAL) u.redD[qg][o] = ((h8d[0] + h8d[1]) + (h8d[2] + h8d[3])) + ((h8d[4] + h8d[5]) + (h8d[6] + h8d[7]));
+    }
+    __syncthreads();
+    if (t < 64) {
+        const double y = (s.red[0][t] + s.red[1][t]) + (s.red[2][t] + s.red[3][t]);
         const double tail = (s.tpart[0][t] + s.tpart[1][t]) + (s.tpart[2][t] + s.tpart[3][t]);
         double o = a.tail2 ? (y + tail) + a.tail2[t0 + t] : y + tail;
         if constexpr (DUAL) {
-            double yd = 0.0;
-#pragma unroll
-            for (int q = 0; q < 32; ++q) yd += u.partD[q][t];
+            const double yd = (u.redD[0][t] + u.redD[1][t]) + (u.redD[2][t] + u.redD[3][t]);
             const double taild = (u.tpartD[0][t] + u.tpartD[1][t]) + (u.tpartD[2][t] + u.tpartD[3][t]);
             o += (a.dscale * a.sgpow[t0 + t]) * (yd + taild);
         }
@@ -678,12 +690,27 @@ struct SetterLds {
     double S[kSetBatch * 128 * 4];          // the batch's states S_np, [band][p][k] (Q <= 128, O <= 4)
     double2 Ph[kSetBatch][5][32];           // the batch's spectra at this column (r0, phi_k)
 };
+// arr[i] for a uniform runtime i by a select chain (no dynamic indexing of registers)
+template <class T>
+__device__ __forceinline__ T pick24(const T (&arr)[kChurnArg], int i) {
+    T v = arr[0];
+#pragma unroll
+    for (int e = 1; e < kChurnArg; ++e) v = i == e ? arr[e] : v;
+    return v;
+}
+// (diagnostic) column workgroup c's phase times into trace[768 + 6 c + k]
+#define COL_MARK(k)                                                                                      \
+    if (a.trace && t == 0) a.trace[768 + 6 * c + (k)] = __builtin_amdgcn_s_memrealtime();
 template <int QI>
 __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) {
     const int t = threadIdx.x;
     const int nt = (int)(a.K / kT);
     const int mq = a.L.m;
     const int O = a.O, Q = a.Q;
+    // the band list with constant indices (wide scalar loads, one wait), picked by select chains
+    int lb[kChurnArg];
+#pragma unroll
+    for (int e = 0; e < kChurnArg; ++e) lb[e] = a.L.band[e];
     if ((int)blockIdx.x >= kCols + nt) {   // upkeep
         if (a.skip & 4) return;
         const int b = (blockIdx.x - kCols - nt) * kT + t;
@@ -696,7 +723,7 @@ __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) 
             }
 #pragma unroll
             for (int i = 0; i < kChurnArg; ++i) {   // (unrolled: the list's scalar loads issued together)
-                const bool hit = i < a.L.m && a.L.band[i] == b;
+                const bool hit = i < mq && lb[i] == b;
                 gb = hit ? a.L.gin[i] : gb;
             }
             a.gin[b] = gb;
@@ -710,17 +737,18 @@ __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) 
         const int tp = (int)(tau / kSP), tj = (int)(tau % kSP);
         const double hv = a.h[tau], hdv = a.dfirst ? 0.0 : a.hD[tau];
         double d = 0.0;
-        for (int q0 = 0; q0 < mq; q0 += kSetBatch) {
-            long bl[kSetBatch];
-            double dl[kSetBatch], v[kSetBatch][4], sv[kSetBatch][4];
+        constexpr int kTapBatch = 6;
+        for (int q0 = 0; q0 < mq; q0 += kTapBatch) {
+            long bl[kTapBatch];
+            double dl[kTapBatch], v[kTapBatch][4], sv[kTapBatch][4];
 #pragma unroll
-            for (int e = 0; e < kSetBatch; ++e) {   // (past the list: the last band again, weight 0)
+            for (int e = 0; e < kTapBatch; ++e) {   // (past the list: the last band again, weight 0)
                 const int q = min(q0 + e, mq - 1);
-                bl[e] = a.L.band[q];
+                bl[e] = pick24(lb, q);
                 dl[e] = q0 + e < mq ? a.L.delta[q] : 0.0;
             }
 #pragma unroll
-            for (int e = 0; e < kSetBatch; ++e) {
+            for (int e = 0; e < kTapBatch; ++e) {
                 if (tp == 0) {
                     v[e][0] = a.r0[bl[e] * kSP + tj];
                 } else {
@@ -733,7 +761,7 @@ __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) 
                 }
             }
 #pragma unroll
-            for (int e = 0; e < kSetBatch; ++e) {
+            for (int e = 0; e < kTapBatch; ++e) {
                 double wv = v[e][0];
                 if (tp != 0) {
                     wv = 0.0;
@@ -772,11 +800,12 @@ __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) 
 #pragma unroll
     for (int i = 0; i < QI; ++i) dS[i] = zero2;
     const int QO = Q * O, n2 = (O + 1) * 32;
+    COL_MARK(0)
     for (int q0 = 0; q0 < ((a.skip & 8) ? 0 : mq); q0 += kSetBatch) {
         const int nb = min(kSetBatch, mq - q0), nS = nb * QO, nP = nb * n2;
         long bl[kSetBatch];
 #pragma unroll
-        for (int e = 0; e < kSetBatch; ++e) bl[e] = a.L.band[min(q0 + e, mq - 1)];
+        for (int e = 0; e < kSetBatch; ++e) bl[e] = pick24(lb, min(q0 + e, mq - 1));
         // the batch's S rows and Ph columns into LDS: four of each per thread per round, every load of
         // a round issued before its stores (indices clamped: always valid)
         for (int e0 = 0; e0 < max(nS, nP); e0 += 4 * kT) {
@@ -808,24 +837,30 @@ __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) 
             }
         }
         __syncthreads();
+        COL_MARK(1)
         for (int qb = 0; qb < nb; ++qb) {
+            // every LDS read of the band first (indices clamped to O - 1, masked below): one LDS
+            // round trip per band, not one per term
             const double dq = a.L.delta[q0 + qb];
+            double sk[QI][4];
+            double2 ph[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) ph[k] = u.Ph[qb][min(k, O)][j];
+#pragma unroll
+            for (int i = 0; i < QI; ++i)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) sk[i][k] = u.S[qb * QO + (g + 8 * i) * O + min(k, O - 1)];
 #pragma unroll
             for (int i = 0; i < QI; ++i) {
-                const int p = g + 8 * i;
-                double2 v;
-                if (p == 0) {
-                    v = u.Ph[qb][0][j];
+                double2 v = zero2;
+                if (g + 8 * i == 0) {
+                    v = ph[0];
                 } else {
-                    v = zero2;
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
-                        if (k < O) {
-                            const double sk = u.S[qb * QO + p * O + k];
-                            const double2 ph = u.Ph[qb][1 + k][j];
-                            v.x = fma(sk, ph.x, v.x);
-                            v.y = fma(sk, ph.y, v.y);
-                        }
+                        const double w = k < O ? sk[i][k] : 0.0;
+                        v.x = fma(w, ph[1 + k].x, v.x);
+                        v.y = fma(w, ph[1 + k].y, v.y);
                     }
                 }
                 dS[i].x = fma(dq, v.x, dS[i].x);
@@ -834,6 +869,7 @@ __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) 
         }
         __syncthreads();
     }
+    COL_MARK(2)
     if (a.skip & 16) return;
     double2 y = zero2, r = zero2;
 #pragma unroll
@@ -845,6 +881,7 @@ __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) 
         if (p >= 1) y = cadd(y, cmul(dS[i], z1[i]));
         if (p >= 3) r = cadd(r, cmul(dS[i], z3[i]));
     }
+    COL_MARK(3)
     ColLds& s = u.col;
     y = half_sum(y);
     r = half_sum(r);
@@ -871,6 +908,7 @@ __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) 
         a.C[cat] = cadd(Cv, dc);
         a.CD[cat] = make_double2(a.rebase * CDv.x - dc.x, a.rebase * CDv.y - dc.y);
     }
+    COL_MARK(4)
 }
 
 template <int QI>

@@ -36,3 +36,45 @@ f = kinds.index(2)
 tot = (ends[-1] - starts[f]) / 100.0
 nb = sum(1 for k in kinds[f:] if k != 2)
 print(f"  from the first setter: {tot:.1f} us over {nb} blocks = {tot / max(1, nb):.2f} us per block")
+# setter launches: per role (columns [0, 33), taps [33, 33 + K/256), upkeep), the workgroups' start and
+# end after the launch's first start
+nt = int(sys.argv[2]) if len(sys.argv) > 2 else 192
+roles = collections.defaultdict(lambda: [[], []])
+for i in range(n):
+    if kinds[i] != 2:
+        continue
+    k, wg = np.frombuffer(raw, dtype=np.int32, count=2, offset=i * rec)
+    st = np.frombuffer(raw, dtype=np.uint64, count=1024, offset=i * rec + 8).astype(np.int64)
+    s0 = st[:wg].min()
+    for name, lo, hi in (("columns", 0, 33), ("taps", 33, 33 + nt), ("upkeep", 33 + nt, wg)):
+        roles[name][0].append((st[lo:hi] - s0).mean() / 100.0)
+        roles[name][1].append((st[512 + lo:512 + hi] - s0).max() / 100.0)
+for name, (a, b) in roles.items():
+    print(f"  setter {name:8s} start mean {np.mean(a):6.2f} us, last end {np.mean(b):6.2f} us after the launch's first start")
+# column phase marks (trace[768 + 6 c + k], k = 0 before the batch, 1 after its loads and barrier,
+# 2 after its compute, 3 after the spectra stores, 4 at the end), after the launch's first start
+marks = [[] for _ in range(5)]
+for i in range(n):
+    if kinds[i] != 2:
+        continue
+    k, wg = np.frombuffer(raw, dtype=np.int32, count=2, offset=i * rec)
+    st = np.frombuffer(raw, dtype=np.uint64, count=1024, offset=i * rec + 8).astype(np.int64)
+    s0 = st[:wg].min()
+    for m in range(5):
+        marks[m].append(np.mean([st[768 + 6 * c + m] - s0 for c in range(33)]) / 100.0)
+print("  column marks (us after the launch's first start):", " ".join(f"{m}:{np.mean(v):.2f}" for m, v in enumerate(marks)))
+# block launches: per role, the last workgroup end after the launch's first start
+brole = {0: (("transform", 0, 33), ("mac", 33, 66), ("out", 66, 82)),
+         1: (("transform", 0, 33), ("mac", 33, 66), ("out", 66, 82), ("D transform", 82, 115), ("D mac", 115, 148))}
+for kind in (0, 1):
+    acc = collections.defaultdict(list)
+    for i in range(n):
+        if kinds[i] != kind:
+            continue
+        k, wg = np.frombuffer(raw, dtype=np.int32, count=2, offset=i * rec)
+        st = np.frombuffer(raw, dtype=np.uint64, count=1024, offset=i * rec + 8).astype(np.int64)
+        s0 = st[:wg].min()
+        for name, lo, hi in brole[kind]:
+            acc[name].append((st[512 + lo:512 + hi] - s0).max() / 100.0)
+    if acc:
+        print(f"  {names[kind]} role ends:", " ".join(f"{k} {np.mean(v):.2f}" for k, v in acc.items()))
