@@ -20,12 +20,15 @@
 //     16-sample chunk (seed = z(t0) (w^16)^p (w^256)^r from per-partial tables,
 //     z(t0+1024) = z(t0) w^1024) and run the two-term sine recurrence inside the chunk;
 //   * time segments need no carry (closed form), so small banks still fill the chip;
-//   * waves' mixes are summed through LDS and a second kernel sums the group rows.
+//   * a wave takes tpw tasks in turn (the envelope applied per task); the waves' mixes are summed
+//     through LDS and written once per workgroup: straight to the output when one group of
+//     workgroups covers every task (long calls), else as group rows a second kernel sums.
 // PI: the reference's truncated PI enters only through sin(2 PI frac(phi)); using 2 pi
 // changes the argument by <= 4.2e-13 rad.
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -71,9 +74,11 @@ struct AddArgs {
     const double* c0;      // [P] output weights of the call's first sample, or null when
                            // equal to the records' (Sinusoids::operator() runs before tick()
                            // applies a decaymod, sinusoids.h:34-57)
-    double* partial;       // [G][n_pad]
+    double* partial;       // [G][n_pad]: one row per group (G > 1), or the output itself (G == 1)
+    double scale;          // (G == 1) the output scale, applied here
     long n, n_pad, seg_len;
     int ntasks, nseg;
+    int tpw;               // tasks per wave: workgroup g's wave w takes tasks (g tpw + k) kWaves + w
     double a;              // attack smoothing coefficient
     double s;              // oscillator stiffness
 };
@@ -83,6 +88,14 @@ __device__ __forceinline__ void cmul(double ar, double ai, double br, double bi,
     const double i = fma(ar, bi, ai * br);
     cr = r;
     ci = i;
+}
+
+// lane q's double (q uniform)
+__device__ __forceinline__ double lane_d(double v, int q) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), q);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), q);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
 
 // frac(phi0 + A t + D (1 - s^t)) with the A t product kept exact (fma residual)
@@ -96,19 +109,21 @@ __device__ __forceinline__ double phase_at(double phi0, double A, double D, doub
 
 // kL samples of one partial in its frequency transient, exact closed form per sample, added to
 // the LDS column `col` (stride kPad); out of line so sinpi's registers stay out of the main loop
+// (scaled by the voice envelope amp(t), advanced per sample as in the mix)
 __device__ __attribute__((noinline)) void add_transient(double* col, double phi0, double A, double c, double D,
-                                                        double s, long tc, double st) {
+                                                        double s, long tc, double st, double amp, double ea,
+                                                        double act) {
     for (int j = 0; j < kL; ++j) {
         const double ph = phase_at(phi0, A, D, s, (double)(tc + j), st);
-        col[j * kPad] = fma(c, sinpi(2.0 * ph), col[j * kPad]);
+        col[j * kPad] = fma(amp, c * sinpi(2.0 * ph), col[j * kPad]);
         st *= s;
+        amp = fma(ea, amp, (1.0 - ea) * act);
     }
 }
 
 __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __restrict__ rec, AddArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* part = lds;                           // [W][16][66]
-    double* zt = lds + kWaves * kL * kPad;        // [W][64][2]
+    double* part = lds;                           // [W][kL][kPad] the waves' mix rows
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int p16 = lane & 15, r4 = lane >> 4;
@@ -116,141 +131,121 @@ __global__ __launch_bounds__(64 * kWaves) void add_mix_kernel(const double* __re
     const long seg_t0 = (long)seg * a.seg_len;
     const long seg_end = min(seg_t0 + a.seg_len, a.n);
     const int ntiles = (int)((seg_end - seg_t0 + kTile - 1) / kTile);
-    const int task = blockIdx.x * kWaves + wave;
-    Task tk;
-    tk.first = 0;
-    tk.count = 0;
-    tk.voice = 0;
-    if (task < a.ntasks) tk = a.tasks[task];
-    double* myzt = zt + wave * (2 * kMaxPerWave);
     const double a_lane = pow(a.a, (double)(kL * lane));
     double a_t = seg_t0 ? pow(a.a, (double)seg_t0) : 1.0;
-    const double amp0 = tk.count ? a.amp0[tk.voice] : 0.0;
-    const double act = tk.count ? a.act[tk.voice] : 0.0;
-
-    // tile-start phasors at the segment start (transient taken as complete; chunks where
-    // it is not are evaluated per sample below)
     const double inv_trans = 1.0 / ((1.0 - a.s) * hz::kSR);
-    for (int q = 0; q < tk.count; ++q) {
-        const int pi = tk.first + q;
-        const double* rr = rec + (long)pi * PRec::SIZE;
-        const double D = (a.f[pi] - a.ft[pi]) * inv_trans;
-        const double ph = phase_at(a.phi[pi], rr[PRec::A], D, a.s, (double)seg_t0, 0.0);
-        double sv, cv;
-        sincospi(2.0 * ph, &sv, &cv);
-        if (lane == 0) {
-            myzt[2 * q] = cv;
-            myzt[2 * q + 1] = sv;
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
+    double* my = part + wave * (kL * kPad);
 
     for (int tile = 0; tile < ntiles; ++tile) {
         const long t0 = seg_t0 + (long)tile * kTile;
         const long tc = t0 + (long)kL * lane;
-        double acc[kL];
-#pragma unroll
-        for (int j = 0; j < kL; ++j) acc[j] = 0.0;
         const double s_tc = pow(a.s, (double)tc);  // transient decay at this chunk
-        bool trans = false;
-        // the next partial's record, frequency pair and tile phasor are fetched one iteration
-        // ahead (software pipeline: their global / LDS latency runs under this partial's
-        // recurrence instead of in front of it)
-        struct Fetch {
-            double c, D, wtr, wti, t1r, t1i, t2r, t2i, w1r, w1i, sr, si;
-        };
-        auto fetch = [&](int q, Fetch& p) {
-            const int pi = tk.first + q;
-            const double* rr = rec + (long)pi * PRec::SIZE;
-            p.c = rr[PRec::C];
-            p.D = (a.f[pi] - a.ft[pi]) * inv_trans;
-            p.wtr = rr[PRec::WT];
-            p.wti = rr[PRec::WT + 1];
-            p.t1r = rr[PRec::T1 + 2 * p16];
-            p.t1i = rr[PRec::T1 + 2 * p16 + 1];
-            p.t2r = rr[PRec::T2 + 2 * r4];
-            p.t2i = rr[PRec::T2 + 2 * r4 + 1];
-            p.w1r = rr[PRec::W1];
-            p.w1i = rr[PRec::W1 + 1];
-            p.sr = myzt[2 * q];
-            p.si = myzt[2 * q + 1];
-        };
-        Fetch cur;
-        if (tk.count) fetch(0, cur);
-        for (int q = 0; q < tk.count; ++q) {
-            const int pi = tk.first + q;
-            Fetch nxt;
-            if (q + 1 < tk.count) fetch(q + 1, nxt);
-            const double c = cur.c, D = cur.D, sr = cur.sr, si = cur.si;
-            double nr, ni;
-            cmul(sr, si, cur.wtr, cur.wti, nr, ni);
-            if (lane == 0) {
-                myzt[2 * q] = nr;
-                myzt[2 * q + 1] = ni;
-            }
-            if (a.c0 && tc == 0) acc[0] = fma(a.c0[pi] - c, sinpi(2.0 * a.phi[pi]), acc[0]);
-            if (fabs(D) * s_tc > 0x1p-60) {
-                trans = true;   // frequency transient: the second pass below
-            } else {
-                // seed z(tc) = z(t0) w^(16 p) w^(256 r); inside the chunk the sines follow the
-                // two-term recurrence sin((k+1) th) = 2 cos th sin(k th) - sin((k-1) th): one
-                // FMA per sample instead of a complex multiply (4), re-seeded every kL samples
-                // (error <= kL eps / |sin th| of the partial's amplitude)
-                double ur, ui, zr, zi;
-                cmul(cur.t1r, cur.t1i, cur.t2r, cur.t2i, ur, ui);
-                cmul(sr, si, ur, ui, zr, zi);
-                const double w1r = cur.w1r, w1i = cur.w1i;
-                const double c2 = 2.0 * w1r;
-                double s0 = zi, s1 = fma(zr, w1i, zi * w1r);
-                acc[0] = fma(c, s0, acc[0]);
-                acc[1] = fma(c, s1, acc[1]);
+        // the wave's mix of the tile accumulates in its LDS rows (registers hold one task's)
 #pragma unroll
-                for (int j = 2; j < kL; ++j) {
-                    const double s2 = fma(c2, s1, -s0);
-                    acc[j] = fma(c, s2, acc[j]);
-                    s0 = s1;
-                    s1 = s2;
-                }
-            }
-            cur = nxt;
-        }
-        __builtin_amdgcn_wave_barrier();   // lane 0's phasor updates before the next tile's reads
-        // voice envelope amp(t) = act + a^t (amp0 - act), advanced per sample
-        double amp = act + (a_lane * a_t) * (amp0 - act);
-        double* my = part + wave * (kL * kPad);
-        if (__builtin_amdgcn_ballot_w64(trans) == 0) {
-#pragma unroll
-            for (int j = 0; j < kL; ++j) {
-                my[j * kPad + lane] = amp * acc[j];
-                amp = fma(a.a, amp, (1.0 - a.a) * act);
-            }
-        } else {
-            // chunks still inside a frequency transient (the first tiles of a retune): the
-            // exact closed form per sample, accumulated through this wave's LDS rows after the
-            // settled partials (the register accumulators are dead here, so sinpi's registers
-            // do not spill the 32 accumulators of the main loop)
-#pragma unroll
-            for (int j = 0; j < kL; ++j) my[j * kPad + lane] = acc[j];
-            for (int q = 0; q < tk.count; ++q) {
-                const int pi = tk.first + q;
+        for (int j = 0; j < kL; ++j) my[j * kPad + lane] = 0.0;
+        for (int k = 0; k < a.tpw; ++k) {
+            const int task = (blockIdx.x * a.tpw + k) * kWaves + wave;
+            if (task >= a.ntasks) break;
+            const Task tk = a.tasks[task];
+            const double amp0 = a.amp0[tk.voice], act = a.act[tk.voice];
+            // tile-start phasor of partial `lane` of the task (lanes in parallel; read below with
+            // readlane; transient taken as complete -- chunks where it is not are evaluated per sample)
+            double zr0 = 0.0, zi0 = 0.0;
+            if (lane < tk.count) {
+                const int pi = tk.first + lane;
                 const double* rr = rec + (long)pi * PRec::SIZE;
                 const double D = (a.f[pi] - a.ft[pi]) * inv_trans;
-                if (fabs(D) * s_tc > 0x1p-60)
-                    add_transient(my + lane, a.phi[pi], rr[PRec::A], rr[PRec::C], D, a.s, tc, s_tc);
+                const double ph = phase_at(a.phi[pi], rr[PRec::A], D, a.s, (double)t0, 0.0);
+                sincospi(2.0 * ph, &zi0, &zr0);
             }
+            double acc[kL];
+#pragma unroll
+            for (int j = 0; j < kL; ++j) acc[j] = 0.0;
+            bool trans = false;
+            // the next partial's record and frequency pair are fetched one iteration ahead (their
+            // global latency runs under this partial's recurrence)
+            struct Fetch {
+                double c, D, t1r, t1i, t2r, t2i, w1r, w1i;
+            };
+            auto fetch = [&](int q, Fetch& p) {
+                const int pi = tk.first + q;
+                const double* rr = rec + (long)pi * PRec::SIZE;
+                p.c = rr[PRec::C];
+                p.D = (a.f[pi] - a.ft[pi]) * inv_trans;
+                p.t1r = rr[PRec::T1 + 2 * p16];
+                p.t1i = rr[PRec::T1 + 2 * p16 + 1];
+                p.t2r = rr[PRec::T2 + 2 * r4];
+                p.t2i = rr[PRec::T2 + 2 * r4 + 1];
+                p.w1r = rr[PRec::W1];
+                p.w1i = rr[PRec::W1 + 1];
+            };
+            Fetch cur;
+            if (tk.count) fetch(0, cur);
+            for (int q = 0; q < tk.count; ++q) {
+                const int pi = tk.first + q;
+                Fetch nxt;
+                if (q + 1 < tk.count) fetch(q + 1, nxt);
+                const double c = cur.c, D = cur.D;
+                const double sr = lane_d(zr0, q), si = lane_d(zi0, q);
+                if (a.c0 && tc == 0) acc[0] = fma(a.c0[pi] - c, sinpi(2.0 * a.phi[pi]), acc[0]);
+                if (fabs(D) * s_tc > 0x1p-60) {
+                    trans = true;   // frequency transient: the second pass below
+                } else {
+                    // seed z(tc) = z(t0) w^(kL p) w^(16 kL r); inside the chunk the sines follow the
+                    // two-term recurrence sin((k+1) th) = 2 cos th sin(k th) - sin((k-1) th): one
+                    // FMA per sample instead of a complex multiply (4), re-seeded every kL samples
+                    // (error <= kL eps / |sin th| of the partial's amplitude)
+                    double ur, ui, zr, zi;
+                    cmul(cur.t1r, cur.t1i, cur.t2r, cur.t2i, ur, ui);
+                    cmul(sr, si, ur, ui, zr, zi);
+                    const double w1r = cur.w1r, w1i = cur.w1i;
+                    const double c2 = 2.0 * w1r;
+                    double s0 = zi, s1 = fma(zr, w1i, zi * w1r);
+                    acc[0] = fma(c, s0, acc[0]);
+                    acc[1] = fma(c, s1, acc[1]);
+#pragma unroll
+                    for (int j = 2; j < kL; ++j) {
+                        const double s2 = fma(c2, s1, -s0);
+                        acc[j] = fma(c, s2, acc[j]);
+                        s0 = s1;
+                        s1 = s2;
+                    }
+                }
+                cur = nxt;
+            }
+            // voice envelope amp(t) = act + a^t (amp0 - act), advanced per sample
+            double amp = act + (a_lane * a_t) * (amp0 - act);
+            // the settled partials, then (chunks still inside a frequency transient: the first tiles
+            // of a retune) the exact closed form per sample, out of line so sinpi's registers do not
+            // spill the accumulators
+            const double amp_c = amp;
+#pragma unroll
             for (int j = 0; j < kL; ++j) {
-                my[j * kPad + lane] *= amp;
+                my[j * kPad + lane] = fma(amp, acc[j], my[j * kPad + lane]);
                 amp = fma(a.a, amp, (1.0 - a.a) * act);
+            }
+            if (__builtin_amdgcn_ballot_w64(trans) != 0) {
+                for (int q = 0; q < tk.count; ++q) {
+                    const int pi = tk.first + q;
+                    const double* rr = rec + (long)pi * PRec::SIZE;
+                    const double D = (a.f[pi] - a.ft[pi]) * inv_trans;
+                    if (fabs(D) * s_tc > 0x1p-60)
+                        add_transient(my + lane, a.phi[pi], rr[PRec::A], rr[PRec::C], D, a.s, tc, s_tc, amp_c, a.a, act);
+                }
             }
         }
         __syncthreads();
+        const bool direct = gridDim.x == 1;   // one group: the output itself, scaled
         for (int tl = threadIdx.x; tl < kTile; tl += blockDim.x) {
             const int src = tl / kL, j = tl % kL;
             double s0 = 0.0;
 #pragma unroll
             for (int w = 0; w < kWaves; ++w) s0 += part[w * (kL * kPad) + j * kPad + src];
             const long t = t0 + tl;
-            if (t < a.n) a.partial[(long)blockIdx.x * a.n_pad + t] = s0;
+            if (t < a.n) {
+                if (direct) a.partial[t] = s0 * a.scale;
+                else a.partial[(long)blockIdx.x * a.n_pad + t] = s0;
+            }
         }
         __syncthreads();
         a_t *= pow(a.a, (double)kTile);
@@ -467,20 +462,30 @@ struct PhaseBank {
         if (ntasks == 0) {
             HZ_TRY_HIP(hipMemsetAsync(d_dst, 0, sizeof(double) * n, stream));
         } else {
-            const int G = (ntasks + kWaves - 1) / kWaves;
+            // groups: one task per wave by default.  Fewer groups (a wave taking several tasks in turn)
+            // cut the partial rows -- one group writes the output directly, 146 -> 67 MB counted per
+            // C3 step -- but measured slower (C3: 19 groups 1.19 ms, 4: 1.46, 2: 1.86; one group for the
+            // long call 1.47 ms: every workgroup then streams all 3.7 MB of partial records per tile);
+            // HZ_ADD_GROUPS sets it (A/B, scripts/r6_c3ab.sh)
             const long ntiles = (n + kTile - 1) / kTile;
+            const int gmax = (ntasks + kWaves - 1) / kWaves;
+            int G = gmax;
+            static const int g_env = getenv("HZ_ADD_GROUPS") ? atoi(getenv("HZ_ADD_GROUPS")) : 0;
+            if (g_env > 0) G = std::min(gmax, g_env);
+            const int tpw = (ntasks + G * kWaves - 1) / (G * kWaves);
+            G = (ntasks + tpw * kWaves - 1) / (tpw * kWaves);
             long nseg = std::max<long>(1, std::min<long>(ntiles, (target_groups + G - 1) / G));
             const long seg_tiles = (ntiles + nseg - 1) / nseg;
             nseg = (ntiles + seg_tiles - 1) / seg_tiles;
             const long n_pad = ntiles * kTile;
-            const size_t need = (size_t)G * n_pad;
+            const size_t need = G > 1 ? (size_t)G * n_pad : 1;
             if (need > partial_cap) {
                 if (d_partial) HZ_TRY_HIP(hipFree(d_partial));
                 d_partial = nullptr;
                 HZ_TRY_HIP(hipMalloc(&d_partial, sizeof(double) * need));
                 partial_cap = need;
             }
-            const size_t lds = sizeof(double) * (kWaves * kL * kPad + kWaves * 2 * kMaxPerWave);
+            const size_t lds = sizeof(double) * (kWaves * kL * kPad);
             static bool attr = false;
             if (!attr) {
                 HZ_TRY_HIP(hipFuncSetAttribute((const void*)add_mix_kernel,
@@ -495,7 +500,9 @@ struct PhaseBank {
             args.amp0 = d_amp;
             args.act = d_act;
             args.c0 = c0_differs ? d_c0 : nullptr;
-            args.partial = d_partial;
+            args.partial = G > 1 ? d_partial : d_dst;
+            args.scale = scale;
+            args.tpw = tpw;
             args.n = n;
             args.n_pad = n_pad;
             args.seg_len = seg_tiles * kTile;
@@ -506,9 +513,11 @@ struct PhaseBank {
             hipLaunchKernelGGL(add_mix_kernel, dim3(G, (unsigned)nseg), dim3(64 * kWaves), lds, stream,
                                (const double*)d_rec, args);
             HZ_TRY_HIP(hipGetLastError());
-            hipLaunchKernelGGL(add_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, stream,
-                               (const double*)d_partial, n_pad, G, n, scale, d_dst);
-            HZ_TRY_HIP(hipGetLastError());
+            if (G > 1) {
+                hipLaunchKernelGGL(add_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, stream,
+                                   (const double*)d_partial, n_pad, G, n, scale, d_dst);
+                HZ_TRY_HIP(hipGetLastError());
+            }
             const double s_n = (double)powl((long double)s, (long double)n);
             hipLaunchKernelGGL(add_advance_kernel, dim3(ntasks), dim3(64), 0, stream, (const double*)d_rec,
                                (const Task*)d_tasks, ntasks, n, s, s_n, (const double*)d_ft, d_phi, d_f);
