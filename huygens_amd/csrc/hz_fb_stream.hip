@@ -398,6 +398,9 @@ __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
     }();
     const int t = threadIdx.x;
     const int t0 = 64 * k;
+    // (diagnostic, HZ_STREAM_TRACE) phase marks of output workgroup k: trace[768 + 4 k + m]
+#define OUT_MARK(m) \
+    if (a.trace && t == 0) a.trace[768 + 4 * k + (m)] = __builtin_amdgcn_s_memrealtime();
     // every global load of the thread in flight before the first LDS store (a load -> store
     // chain per loop iteration waited one memory latency each): window positions 64k + 1 ..
     // 64k + 1087 (2048-sample window: previous block | this block), h[0..1023], the columns
@@ -437,6 +440,7 @@ __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
     }
     if (t < 64) s.tw[t] = twv;
     __syncthreads();
+    OUT_MARK(0)
     // the block's samples into the ring (both mirror positions), for the next calls
     if (t < 64) {
         const double xw = s.sx[1023 + t];
@@ -451,6 +455,7 @@ __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
         tail_partials(u.colD, s.tw, t0, u.tpartD);
     }
     __syncthreads();
+    OUT_MARK(1)
     // the 32 head partials of each output: 8 per thread over all 256 threads (independent LDS reads,
     // one round trip), then 4 per output -- a 32-read chain on one wave was the role's critical path
     {
@@ -465,6 +470,7 @@ __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
         if constexpr (DUAL) u.redD[qg][o] = ((h8d[0] + h8d[1]) + (h8d[2] + h8d[3])) + ((h8d[4] + h8d[5]) + (h8d[6] + h8d[7]));
     }
     __syncthreads();
+    OUT_MARK(2)
     if (t < 64) {
         const double y = (s.red[0][t] + s.red[1][t]) + (s.red[2][t] + s.red[3][t]);
         const double tail = (s.tpart[0][t] + s.tpart[1][t]) + (s.tpart[2][t] + s.tpart[3][t]);

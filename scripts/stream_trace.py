@@ -78,3 +78,19 @@ for kind in (0, 1):
             acc[name].append((st[512 + lo:512 + hi] - s0).max() / 100.0)
     if acc:
         print(f"  {names[kind]} role ends:", " ".join(f"{k} {np.mean(v):.2f}" for k, v in acc.items()))
+# output workgroups' phase marks (trace[768 + 4 k + m]: m = 0 after the operand loads and the first
+# barrier, 1 after the head / tail partials, 2 after the partial sums), after the launch's first start
+for kind in (0, 1):
+    mk = [[] for _ in range(3)]
+    ends = []
+    for i in range(n):
+        if kinds[i] != kind:
+            continue
+        k, wg = np.frombuffer(raw, dtype=np.int32, count=2, offset=i * rec)
+        st = np.frombuffer(raw, dtype=np.uint64, count=1024, offset=i * rec + 8).astype(np.int64)
+        s0 = st[:wg].min()
+        for m in range(3):
+            mk[m].append(np.mean([st[768 + 4 * kk + m] - s0 for kk in range(16)]) / 100.0)
+        ends.append(np.mean(st[512 + 66:512 + 82] - s0) / 100.0)
+    if ends:
+        print(f"  {names[kind]} output marks:", " ".join(f"{m}:{np.mean(v):.2f}" for m, v in enumerate(mk)), f"end {np.mean(ends):.2f}")
