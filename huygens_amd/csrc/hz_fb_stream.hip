@@ -31,6 +31,10 @@
 #include "hz_dd.h"
 #include "hz_fb_impl.h"
 
+#ifndef HZ_STREAM_OUTN
+#define HZ_STREAM_OUTN 16
+#endif
+
 namespace {
 
 constexpr int kSP = hz_fbi::kStreamBlock;   // partition = call length
@@ -182,8 +186,16 @@ struct StreamArgs {
 };
 
 // all of this workgroup's stores complete, then one system-scope release of the flag
+// (only the plain launch's workgroups post -- blockIdx < fb_stream_workgroups(), the host's flag
+// slots; a transient's extra roles write only the next launch's parities, stream-ordered)
+constexpr int kOutN = HZ_STREAM_OUTN;   // outputs per output workgroup (64: 4.4 us per plain block,
+                                        // 32: 3.8 us -- the role's head FMAs and LDS reads)
+constexpr int kOG = kOutN / 8;           // output groups of 8 per thread
+constexpr int kQG = kT / kOG;            // head tap groups
+constexpr int kTG = kSP / kQG;           // taps per group
+constexpr int kNG = kT / kOutN;          // partial-sum / tail column groups
 __device__ __forceinline__ void post_done(const StreamArgs& a) {
-    if (!a.flags) return;
+    if (!a.flags || (int)blockIdx.x >= 2 * kCols + kSP / kOutN) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
@@ -261,22 +273,22 @@ __global__ __launch_bounds__(kT) void stream_prime2_kernel(StreamArgs a) {
 }
 
 struct OutLds {
-    double sx[1088];          // x[t0 - 1023 .. t0 + 64]
+    double sx[1088];          // x[t0 - 1023 .. t0 + kOutN - 1]
     double sh[kSP];           // h[0 .. 1023]
     double2 col[kCols][32];   // the tail's inverse columns
     double2 tw[64];
-    double part[32][65];      // head partials [tap group][output]
-    double tpart[4][64];      // tail partials [column group][output]
-    double red[4][64];        // head partials summed over 8 tap groups
+    double part[kQG][kOutN + 1];   // head partials [tap group][output]
+    double tpart[kNG][kOutN];      // tail partials [column group][output]
+    double red[kNG][kOutN];        // head partials summed over 8 tap groups
 };
 // (a gain transient, FUSED) the same for h_D
 struct OutLdsD {
     OutLds m;
     double shD[kSP];
     double2 colD[kCols][32];
-    double partD[32][65];
-    double tpartD[4][64];
-    double redD[4][64];
+    double partD[kQG][kOutN + 1];
+    double tpartD[kNG][kOutN];
+    double redD[kNG][kOutN];
 };
 union StreamLds {
     ColLds col;
@@ -348,35 +360,35 @@ __device__ __forceinline__ void role_mac(const StreamArgs& a, const double2* __r
     if (t < 32) Rout[c * 32 + t] = cadd(cadd(s.m[0][t], s.m[1][t]), cadd(s.m[2][t], s.m[3][t]));
 }
 
-// head: thread = 8 outputs (o8) x 32 taps (q): y[j] += h[tau] x[t0 + j - tau], partials into part
+// head: thread = 8 outputs (o8) x kTG taps (q): y[j] += h[tau] x[t0 + j - tau], partials into part
 __device__ __forceinline__ void head_partials(const double* __restrict__ sx, const double* __restrict__ sh,
-                                              double (*part)[65]) {
-    const int t = threadIdx.x, o8 = t & 7, q = t >> 3;
-    const int j0 = 8 * o8, tau0 = 32 * q;
-    double xs[39], hs[32], acc[8];
+                                              double (*part)[kOutN + 1]) {
+    const int t = threadIdx.x, o8 = t % kOG, q = t / kOG;
+    const int j0 = 8 * o8, tau0 = kTG * q;
+    double xs[kTG + 7], hs[kTG], acc[8];
 #pragma unroll
-    for (int i = 0; i < 39; ++i) xs[i] = sx[1023 + j0 - tau0 - 31 + i];   // x[t0 + j0 - tau0 - 31 + i]
+    for (int i = 0; i < kTG + 7; ++i) xs[i] = sx[1023 + j0 - tau0 - (kTG - 1) + i];   // x[t0 + j0 - tau0 - kTG + 1 + i]
 #pragma unroll
-    for (int i = 0; i < 32; ++i) hs[i] = sh[tau0 + i];
+    for (int i = 0; i < kTG; ++i) hs[i] = sh[tau0 + i];
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r] = 0.0;
 #pragma unroll
-    for (int i = 0; i < 32; ++i)
+    for (int i = 0; i < kTG; ++i)
 #pragma unroll
-        for (int r = 0; r < 8; ++r) acc[r] = fma(hs[i], xs[31 + r - i], acc[r]);
+        for (int r = 0; r < 8; ++r) acc[r] = fma(hs[i], xs[kTG - 1 + r - i], acc[r]);
 #pragma unroll
     for (int r = 0; r < 8; ++r) part[q][j0 + r] = acc[r];
 }
 
-// tail partials: output o (t & 63), columns c = 1 + cg + 4 i (cg = t >> 6)
+// tail partials: output o (t % kOutN), columns c = 1 + cg + kNG i (cg = t / kOutN)
 __device__ __forceinline__ void tail_partials(const double2 (*col)[32], const double2* __restrict__ tw, int t0,
-                                              double (*tpart)[64]) {
-    const int t = threadIdx.x, o = t & 63, cg = t >> 6;
+                                              double (*tpart)[kOutN]) {
+    const int t = threadIdx.x, o = t % kOutN, cg = t / kOutN;
     const int n = t0 + o, m = n >> 5, n2 = n & 31, n1 = 32 + m;
     double acc = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int c = 1 + cg + 4 * i;
+    for (int i = 0; i < 32 / kNG; ++i) {
+        const int c = 1 + cg + kNG * i;
         if (c < 32) {
             const double2 C = col[c][n2], wv = tw[(n1 * c) & 63];
             acc = fma(wv.x, C.x, fma(wv.y, C.y, acc));
@@ -387,9 +399,9 @@ __device__ __forceinline__ void tail_partials(const double2 (*col)[32], const do
     tpart[cg][o] = acc;
 }
 
-// 64 outputs: head (h[0..1023] direct, the partition-0 term of overlap-save) + tail (the 33 columns
-// Cin of the previous launch, Hermitian-combined); DUAL (a gain transient): + s_g^(t - dref + 1) x
-// the same for h_D (its taps and columns)
+// kOutN outputs: head (h[0..1023] direct, the partition-0 term of overlap-save) + tail (the 33
+// columns Cin of the previous launch, Hermitian-combined); DUAL (a gain transient): + s_g^(t - dref
+// + 1) x the same for h_D (its taps and columns)
 template <bool DUAL, class L>
 __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
     OutLds& s = [&]() -> OutLds& {
@@ -397,18 +409,19 @@ __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
         else return u;
     }();
     const int t = threadIdx.x;
-    const int t0 = 64 * k;
+    const int t0 = kOutN * k;
+    constexpr int nwin = kSP - 1 + kOutN;   // window x[t0 - 1023 .. t0 + kOutN - 1]
     // (diagnostic, HZ_STREAM_TRACE) phase marks of output workgroup k: trace[768 + 4 k + m]
 #define OUT_MARK(m) \
     if (a.trace && t == 0) a.trace[768 + 4 * k + (m)] = __builtin_amdgcn_s_memrealtime();
     // every global load of the thread in flight before the first LDS store (a load -> store
-    // chain per loop iteration waited one memory latency each): window positions 64k + 1 ..
-    // 64k + 1087 (2048-sample window: previous block | this block), h[0..1023], the columns
+    // chain per loop iteration waited one memory latency each): window positions t0 + 1 ..
+    // t0 + nwin (2048-sample window: previous block | this block), h[0..1023], the columns
     double xv[5], hv[4], hvD[4];
     double2 cv[5], cvD[5];
 #pragma unroll
     for (int q = 0; q < 5; ++q) {
-        const int i = min(t + q * kT, 1086);
+        const int i = min(t + q * kT, nwin - 1);
         const int wp = t0 + 1 + i;
         xv[q] = wp < kSP ? a.line[a.prev + wp] : a.x[wp - kSP];
     }
@@ -425,7 +438,7 @@ __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
     const double2 twv = a.tw[kTw64 + (t & 63)];
 #pragma unroll
     for (int q = 0; q < 5; ++q)
-        if (t + q * kT < 1087) s.sx[t + q * kT] = xv[q];
+        if (t + q * kT < nwin) s.sx[t + q * kT] = xv[q];
 #pragma unroll
     for (int q = 0; q < 4; ++q) s.sh[t + q * kT] = hv[q];
 #pragma unroll
@@ -442,7 +455,7 @@ __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
     __syncthreads();
     OUT_MARK(0)
     // the block's samples into the ring (both mirror positions), for the next calls
-    if (t < 64) {
+    if (t < kOutN) {
         const double xw = s.sx[1023 + t];
         const long kk = a.wpos + t0 + t;
         a.line[kk] = xw;
@@ -456,10 +469,10 @@ __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
     }
     __syncthreads();
     OUT_MARK(1)
-    // the 32 head partials of each output: 8 per thread over all 256 threads (independent LDS reads,
-    // one round trip), then 4 per output -- a 32-read chain on one wave was the role's critical path
+    // the kQG head partials of each output: 8 per thread over all 256 threads (independent LDS reads,
+    // one round trip), then kNG per output
     {
-        const int o = t & 63, qg = t >> 6;
+        const int o = t % kOutN, qg = t / kOutN;
         double h8[8], h8d[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -471,15 +484,20 @@ __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
     }
     __syncthreads();
     OUT_MARK(2)
-    if (t < 64) {
-        const double y = (s.red[0][t] + s.red[1][t]) + (s.red[2][t] + s.red[3][t]);
-        const double tail = (s.tpart[0][t] + s.tpart[1][t]) + (s.tpart[2][t] + s.tpart[3][t]);
+    if (t < kOutN) {
+        auto sumg = [&](const double (*v)[kOutN]) {
+            double r[kNG];
+#pragma unroll
+            for (int g = 0; g < kNG; ++g) r[g] = v[g][t];
+#pragma unroll
+            for (int w = kNG / 2; w >= 1; w /= 2)
+#pragma unroll
+                for (int g = 0; g < w; ++g) r[g] = r[g] + r[g + w];
+            return r[0];
+        };
+        const double y = sumg(s.red), tail = sumg(s.tpart);
         double o = a.tail2 ? (y + tail) + a.tail2[t0 + t] : y + tail;
-        if constexpr (DUAL) {
-            const double yd = (u.redD[0][t] + u.redD[1][t]) + (u.redD[2][t] + u.redD[3][t]);
-            const double taild = (u.tpartD[0][t] + u.tpartD[1][t]) + (u.tpartD[2][t] + u.tpartD[3][t]);
-            o += (a.dscale * a.sgpow[t0 + t]) * (yd + taild);
-        }
+        if constexpr (DUAL) o += (a.dscale * a.sgpow[t0 + t]) * (sumg(u.redD) + sumg(u.tpartD));
         a.out[t0 + t] = o;
     }
 }
@@ -487,11 +505,11 @@ __device__ __forceinline__ void role_out(const StreamArgs& a, L& u, int k) {
 // One 1024-sample block, three roles with no data shared inside the launch (tests/stream_model.py):
 //   blocks [0, 33)  transform column c
 //   blocks [33, 66) MAC column c
-//   blocks [66, 82) 64 outputs each: head + tail
+//   blocks [66, 98) kOutN = 32 outputs each: head + tail
 // DUAL (a gain transient, hz_fb_stream fb_stream_gain_setter): the transient response's roles in
 // the same launch -- its own transform columns (Z_b transformed again: no dependence on the main
 // transform role), its MAC columns (h_D's spectra, its C / R parities), and the output role adds
-// s_g^(t - dref + 1) (head_D + tail_D).  [82, 115) D transform, [115, 148) D MAC.
+// s_g^(t - dref + 1) (head_D + tail_D).  [98, 131) D transform, [131, 164) D MAC.
 // QI = Q / 8: partitions per MAC thread.
 template <int QI, bool DUAL>
 __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
@@ -499,7 +517,7 @@ __global__ __launch_bounds__(kT) void stream_block_kernel(StreamArgs a) {
     __shared__ Lds u;
     const int blk = blockIdx.x;
     if (a.trace && threadIdx.x == 0) a.trace[blk] = __builtin_amdgcn_s_memrealtime();
-    constexpr int kOut0 = 2 * kCols, kOut1 = 2 * kCols + kSP / 64;
+    constexpr int kOut0 = 2 * kCols, kOut1 = 2 * kCols + kSP / kOutN;
     if (blk < kCols) {
         role_transform<true>(a, a.HS, a.Rin, a.Cout, u.col, blk);
     } else if (blk < 2 * kCols) {
@@ -532,7 +550,7 @@ template <int QI>
 struct BlockKD {
     static constexpr BlockKernel fn = stream_block_kernel<QI, true>;
 };
-constexpr int kBlockWG = 2 * kCols + kSP / 64, kBlockWGD = 4 * kCols + kSP / 64;
+constexpr int kBlockWG = 2 * kCols + kSP / kOutN, kBlockWGD = 4 * kCols + kSP / kOutN;
 template <int QI>
 struct Prime2K {
     static constexpr BlockKernel fn = stream_prime2_kernel<QI>;
@@ -1201,7 +1219,7 @@ unsigned long long* trace_slot(hz_fb* h, int kind) {
 
 namespace hz_fbi {
 
-int fb_stream_workgroups() { return 2 * kCols + kSP / 64; }
+int fb_stream_workgroups() { return kBlockWG; }
 
 bool fb_stream_trackable(hz_fb* h, long n, bool conv) {
     hz_fb::Resp& R = h->resp;

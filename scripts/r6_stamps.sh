@@ -12,4 +12,4 @@ np.concatenate([np.asarray(f)[:, :3], np.asarray(b)[:, :2]], axis=1).astype(np.f
 np.random.default_rng(1).uniform(-1, 1, 480000).tofile("gpurun_out/r6/stamps/x.bin")
 PY
 /opt/rocm/bin/hipcc -std=c++17 -O2 -I include tests/cpp/churn.cpp -o $D/churn -L huygens_amd/lib -lhuygens_hip -Wl,-rpath,$PWD/huygens_amd/lib || exit 1
-rm -f $D/trace*.bin; for sk in 0; do HZ_SETTER_SKIP=$sk HZ_STREAM_TRACE=$D/trace$sk.bin timeout -k 10 120 $D/churn $D && echo "skip $sk" && python3 scripts/stream_trace.py $D/trace$sk.bin; done
+rm -f $D/trace*.bin; for sk in 0; do HZ_SETTER_SKIP=$sk HZ_STREAM_TRACE=$D/trace$sk.bin timeout -k 10 120 $D/churn $D && echo "skip $sk" && OUTWG=64 python3 scripts/stream_trace.py $D/trace$sk.bin; done

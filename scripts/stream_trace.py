@@ -64,8 +64,9 @@ for i in range(n):
         marks[m].append(np.mean([st[768 + 6 * c + m] - s0 for c in range(33)]) / 100.0)
 print("  column marks (us after the launch's first start):", " ".join(f"{m}:{np.mean(v):.2f}" for m, v in enumerate(marks)))
 # block launches: per role, the last workgroup end after the launch's first start
-brole = {0: (("transform", 0, 33), ("mac", 33, 66), ("out", 66, 82)),
-         1: (("transform", 0, 33), ("mac", 33, 66), ("out", 66, 82), ("D transform", 82, 115), ("D mac", 115, 148))}
+OUTWG = int(__import__("os").environ.get("OUTWG", "64"))
+brole = {0: (("transform", 0, 33), ("mac", 33, 66), ("out", 66, 66 + OUTWG)),
+         1: (("transform", 0, 33), ("mac", 33, 66), ("out", 66, 66 + OUTWG), ("D transform", 66 + OUTWG, 99 + OUTWG), ("D mac", 99 + OUTWG, 132 + OUTWG))}
 for kind in (0, 1):
     acc = collections.defaultdict(list)
     for i in range(n):
@@ -90,7 +91,7 @@ for kind in (0, 1):
         st = np.frombuffer(raw, dtype=np.uint64, count=1024, offset=i * rec + 8).astype(np.int64)
         s0 = st[:wg].min()
         for m in range(3):
-            mk[m].append(np.mean([st[768 + 4 * kk + m] - s0 for kk in range(16)]) / 100.0)
-        ends.append(np.mean(st[512 + 66:512 + 82] - s0) / 100.0)
+            mk[m].append(np.mean([st[768 + 4 * kk + m] - s0 for kk in range(min(OUTWG, 64))]) / 100.0)
+        ends.append(np.mean(st[512 + 66:512 + 66 + OUTWG] - s0) / 100.0)
     if ends:
         print(f"  {names[kind]} output marks:", " ".join(f"{m}:{np.mean(v):.2f}" for m, v in enumerate(mk)), f"end {np.mean(ends):.2f}")
