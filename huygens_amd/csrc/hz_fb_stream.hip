@@ -726,7 +726,7 @@ __device__ __forceinline__ T pick24(const T (&arr)[kChurnArg], int i) {
 #define COL_MARK(k)                                                                                      \
     if (a.trace && t == 0) a.trace[768 + 6 * c + (k)] = __builtin_amdgcn_s_memrealtime();
 template <int QI>
-__device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) {
+__device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u, const int vblk) {
     const int t = threadIdx.x;
     const int nt = (int)(a.K / kT);
     const int mq = a.L.m;
@@ -735,9 +735,9 @@ __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) 
     int lb[kChurnArg];
 #pragma unroll
     for (int e = 0; e < kChurnArg; ++e) lb[e] = a.L.band[e];
-    if ((int)blockIdx.x >= kCols + nt) {   // upkeep
+    if ((int)vblk >= kCols + nt) {   // upkeep
         if (a.skip & 4) return;
-        const int b = (blockIdx.x - kCols - nt) * kT + t;
+        const int b = (vblk - kCols - nt) * kT + t;
         if (b < a.N) {
             double gb = a.gin[b];
             if (a.upkeep) {
@@ -755,9 +755,9 @@ __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) 
         if (a.upkeep && b < O) a.xhist[b] = a.line[a.last - b];
         return;
     }
-    if ((int)blockIdx.x >= kCols) {   // taps: 256 of partition tp (uniform over the workgroup)
+    if ((int)vblk >= kCols) {   // taps: 256 of partition tp (uniform over the workgroup)
         if (a.skip & 2) return;
-        const long tau = (long)(blockIdx.x - kCols) * kT + t;
+        const long tau = (long)(vblk - kCols) * kT + t;
         const int tp = (int)(tau / kSP), tj = (int)(tau % kSP);
         const double hv = a.h[tau], hdv = a.dfirst ? 0.0 : a.hD[tau];
         double d = 0.0;
@@ -801,7 +801,7 @@ __device__ __forceinline__ void setter_roles(const SetterArgs& a, SetterLds& u) 
     }
     // column c
     if (a.skip & 1) return;
-    const int c = blockIdx.x, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
+    const int c = vblk, l = t & 63, w = t >> 6, j = l & 31, g = 2 * w + (l >> 5);
     // everything that does not depend on the setter's bands, in flight first
     double2 z1[QI], z3[QI], hs[QI], hd[QI];
 #pragma unroll
@@ -939,7 +939,19 @@ template <int QI>
 __global__ __launch_bounds__(kT) void stream_setter_kernel(SetterArgs a) {
     __shared__ SetterLds u;
     if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    setter_roles<QI>(a, u);
+    setter_roles<QI>(a, u, (int)blockIdx.x);
+    if (a.trace) {
+        __syncthreads();
+        if (threadIdx.x == 0) a.trace[512 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+// (A/B, HZ_SETTER_SPLIT=1) the taps and upkeep roles as a kernel of their own, without the column
+// workgroups' LDS (the column kernel then runs kCols workgroups)
+__global__ __launch_bounds__(kT) void stream_setter_taps_kernel(SetterArgs a) {
+    extern __shared__ double no_lds[];
+    if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    setter_roles<1>(a, *reinterpret_cast<SetterLds*>(no_lds), kCols + (int)blockIdx.x);
     if (a.trace) {
         __syncthreads();
         if (threadIdx.x == 0) a.trace[512 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -1211,7 +1223,10 @@ unsigned long long* trace_slot(hz_fb* h, int kind) {
     if (S.trace_n == kTraceN) trace_flush(h);
     const int i = S.trace_n++;
     S.trace_kind[i] = kind;
-    S.trace_wg[i] = kind == 2 ? (int)(kCols + S.K1 / kT + (h->N + kT - 1) / kT) : (kind == 1 ? kBlockWGD : kBlockWG);
+    static const bool split = getenv("HZ_SETTER_SPLIT") && atoi(getenv("HZ_SETTER_SPLIT"));
+    S.trace_wg[i] = kind == 3   ? (int)(S.K1 / kT + (h->N + kT - 1) / kT)
+                    : kind == 2 ? (split ? kCols : (int)(kCols + S.K1 / kT + (h->N + kT - 1) / kT))
+                                : (kind == 1 ? kBlockWGD : kBlockWG);
     return S.d_trace + (size_t)i * 1024;
 }
 
@@ -1577,7 +1592,15 @@ int fb_stream_gain_setter(hz_fb* h) {
             sa.dfirst = 0;
             sa.upkeep = 0;
         }
-        hipLaunchKernelGGL(pick_setter(Q / 8), dim3(wg), dim3(kT), 0, h->stream, sa);
+        static const bool split = getenv("HZ_SETTER_SPLIT") && atoi(getenv("HZ_SETTER_SPLIT"));
+        if (split) {
+            SetterArgs st = sa;
+            st.trace = trace_slot(h, 3);
+            hipLaunchKernelGGL(stream_setter_taps_kernel, dim3(wg - kCols), dim3(kT), 0, h->stream, st);
+            hipLaunchKernelGGL(pick_setter(Q / 8), dim3(kCols), dim3(kT), 0, h->stream, sa);
+        } else {
+            hipLaunchKernelGGL(pick_setter(Q / 8), dim3(wg), dim3(kT), 0, h->stream, sa);
+        }
     }
     if (hipGetLastError() != hipSuccess) return 0;
     S.dmax = rebase * S.dmax + dmx;

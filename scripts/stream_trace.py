@@ -17,7 +17,7 @@ for i in range(n):
     kinds.append(int(k))
     starts.append(int(s0.min()))
     ends.append(int(e0.max()))
-names = {0: "block", 1: "block+transient", 2: "setter"}
+names = {0: "block", 1: "block+transient", 2: "setter", 3: "setter taps"}
 print(f"{n} launches")
 span = collections.defaultdict(list)
 for k, s, e in zip(kinds, starts, ends):
@@ -32,7 +32,7 @@ for i in range(1, n):
 for k, v in gaps.items():
     print(f"  gap {k[0]:16s} -> {k[1]:16s} n={len(v):5d} mean {np.mean(v):6.2f} median {np.median(v):6.2f} us")
 # the churn pass: from the first setter to the last launch
-f = kinds.index(2)
+f = kinds.index(2) if 2 in kinds else 0
 tot = (ends[-1] - starts[f]) / 100.0
 nb = sum(1 for k in kinds[f:] if k != 2)
 print(f"  from the first setter: {tot:.1f} us over {nb} blocks = {tot / max(1, nb):.2f} us per block")
@@ -47,6 +47,8 @@ for i in range(n):
     st = np.frombuffer(raw, dtype=np.uint64, count=1024, offset=i * rec + 8).astype(np.int64)
     s0 = st[:wg].min()
     for name, lo, hi in (("columns", 0, 33), ("taps", 33, 33 + nt), ("upkeep", 33 + nt, wg)):
+        if hi > wg or hi <= lo:
+            continue
         roles[name][0].append((st[lo:hi] - s0).mean() / 100.0)
         roles[name][1].append((st[512 + lo:512 + hi] - s0).max() / 100.0)
 for name, (a, b) in roles.items():
