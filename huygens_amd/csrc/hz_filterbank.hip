@@ -1251,9 +1251,9 @@ int hz_fb_process(hz_fb* h, const double* in, double* out, size_t n) {
         fb_stream_eligible(h, (long)n, h->order > 0 && fb_converged(h))) {
         const int nwg = hz_fbi::fb_stream_workgroups();
         if (!h->pin_io) {
-            HZ_TRY_HIP(hipHostMalloc((void**)&h->pin_io, sizeof(double) * (2 * kStreamBlock + 128),
+            HZ_TRY_HIP(hipHostMalloc((void**)&h->pin_io, sizeof(double) * (2 * kStreamBlock + 256),
                                      hipHostMallocCoherent | hipHostMallocMapped));
-            std::memset(h->pin_io + 2 * kStreamBlock, 0, sizeof(double) * 128);
+            std::memset(h->pin_io + 2 * kStreamBlock, 0, sizeof(double) * 256);
         }
         void* dio = nullptr;
         HZ_TRY_HIP(hipHostGetDevicePointer(&dio, h->pin_io, 0));
@@ -1265,7 +1265,7 @@ int hz_fb_process(hz_fb* h, const double* in, double* out, size_t n) {
         const int rc = fb_launch(h, (const double*)dio, (double*)dio + kStreamBlock, (long)n);
         S.flags_dev = nullptr;
         HZ_TRY(rc);
-        if (h->last_path == HZ_FB_PATH_STREAM && nwg <= 128) {
+        if (h->last_path == HZ_FB_PATH_STREAM && nwg <= 256) {   // (256 flag slots)
             // every workgroup has read the input and written the output: no stream synchronisation
             // (a fault or a lost flag falls back to it after 1 s and reports the stream's error)
             const auto t0 = std::chrono::steady_clock::now();
