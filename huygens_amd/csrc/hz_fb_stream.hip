@@ -1599,6 +1599,14 @@ int fb_stream_gain_setter(hz_fb* h) {
             hipLaunchKernelGGL(stream_setter_taps_kernel, dim3(wg - kCols), dim3(kT), 0, h->stream, st);
             hipLaunchKernelGGL(pick_setter(Q / 8), dim3(kCols), dim3(kT), 0, h->stream, sa);
         } else {
+            // (diagnostic, HZ_SETTER_TWICE=1: the same launch twice -- wrong results, the second
+            // launch's trace shows the cost with its code and operands warm)
+            static const bool twice = getenv("HZ_SETTER_TWICE") && atoi(getenv("HZ_SETTER_TWICE"));
+            if (twice) {
+                SetterArgs s1 = sa;
+                s1.trace = trace_slot(h, 2);
+                hipLaunchKernelGGL(pick_setter(Q / 8), dim3(wg), dim3(kT), 0, h->stream, s1);
+            }
             hipLaunchKernelGGL(pick_setter(Q / 8), dim3(wg), dim3(kT), 0, h->stream, sa);
         }
     }
