@@ -213,7 +213,9 @@ struct RespArgs {
     const double2* tw;    // W_F^k, k < kH
     double2* Z;           // [Q + B - 1 (+ pad)][kH] window spectra
     double* Zn;           // [..] their bin kH
-    const double2* Y;     // [B][kH] output spectra (bins < kH)
+    const double2* Y;     // [ys][B][kH] output spectra (bins < kH): ys partial sums over the partitions
+    int ys;               // (the long-horizon MAC split over chunks of partitions, summed here)
+    long ystride;
     const double* Hn;     // [Q] partition spectra at bin kH
     double* out;          // [n]
     // state upkeep, done by the inverse kernel's threads: the history after the call (the last K
@@ -476,7 +478,8 @@ template <int BINS, int BPW>
 constexpr size_t macc_lds_bytes() { return sizeof(double2) * BINS * (kMacChunk + (256 / BINS) * BPW + kMacChunk - 1); }
 template <int BINS, int BPW>
 __global__ __launch_bounds__(256) void resp_mac_kernel_ldsc(const double2* __restrict__ H, const double2* __restrict__ Z,
-                                                            double2* __restrict__ Y, int Q, int B, int nch) {
+                                                            double2* __restrict__ Y, int Q, int B, int nch, int cps,
+                                                            long ystride) {
     constexpr int QP = kMacChunk, SL = 256 / BINS, kMacBlk = SL * BPW, kZr = kMacBlk + QP - 1;
     constexpr int kHL = (QP + SL - 1) / SL, kZL = (kZr + SL - 1) / SL;
     extern __shared__ double2 mac_lds[];
@@ -501,8 +504,11 @@ __global__ __launch_bounds__(256) void resp_mac_kernel_ldsc(const double2* __res
     double ar[BPW], ai[BPW];
 #pragma unroll
     for (int r = 0; r < BPW; ++r) ar[r] = ai[r] = 0.0;
-    fetch(0);
-    for (int c = 0; c < nch; ++c) {
+    // split blockIdx.y: chunks [c0, c1) into its own partial-sum plane of Y
+    const int c0 = blockIdx.y * cps, c1 = min(nch, c0 + cps);
+    Y += blockIdx.y * ystride;
+    if (c0 < c1) fetch(c0);
+    for (int c = c0; c < c1; ++c) {
 #pragma unroll
         for (int k = 0; k < kHL; ++k)
             if (sl + SL * k < QP) hs[sl + SL * k][lq] = hv[k];
@@ -510,7 +516,7 @@ __global__ __launch_bounds__(256) void resp_mac_kernel_ldsc(const double2* __res
         for (int k = 0; k < kZL; ++k)
             if (sl + SL * k < kZr) zs[sl + SL * k][lq] = zv[k];
         __syncthreads();
-        if (c + 1 < nch) fetch(c + 1);   // in flight under this chunk's MACs
+        if (c + 1 < c1) fetch(c + 1);   // in flight under this chunk's MACs
         double zr[BPW], zi[BPW];
 #pragma unroll
         for (int r = 0; r < BPW; ++r) {
@@ -547,18 +553,37 @@ __global__ __launch_bounds__(256) void resp_mac_kernel_ldsc(const double2* __res
         if (b < B) Y[(long)b * kH + q] = make_double2(ar[r], ai[r]);
     }
 }
-template <int BINS>
-void launch_macc(int Qp, int B, const double2* H, const double2* Z, double2* Y, int Q, hipStream_t s) {
+template <int BINS, int BPW>
+void launch_macc_t(int Qp, int B, const double2* H, const double2* Z, double2* Y, int Q, int ns, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_ldsc<BINS, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)macc_lds_bytes<BINS, 8>());
+        (void)hipFuncSetAttribute((const void*)resp_mac_kernel_ldsc<BINS, BPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)macc_lds_bytes<BINS, BPW>());
         attr = true;
     }
-    constexpr int blk = (256 / BINS) * 8;
-    const dim3 grid((unsigned)((kH / BINS) * ((B + blk - 1) / blk)));
-    hipLaunchKernelGGL((resp_mac_kernel_ldsc<BINS, 8>), grid, dim3(256), (macc_lds_bytes<BINS, 8>()), s, H, Z, Y, Q, B,
-                       Qp / kMacChunk);
+    constexpr int blk = (256 / BINS) * BPW;
+    const int nch = Qp / kMacChunk, cps = (nch + ns - 1) / ns;
+    const dim3 grid((unsigned)((kH / BINS) * ((B + blk - 1) / blk)), (unsigned)ns);
+    hipLaunchKernelGGL((resp_mac_kernel_ldsc<BINS, BPW>), grid, dim3(256), (macc_lds_bytes<BINS, BPW>()), s, H, Z, Y, Q, B,
+                       nch, cps, (long)B * kH);
+}
+// The long-horizon MAC is latency-bound per chunk (each chunk's operands are fetched one chunk ahead,
+// and a 10 s call gives (kH / BINS) x ceil(B / blk) = 128 workgroups whatever the tile: twice as many,
+// 4 blocks per thread, measured the same 35 us), so the chunks are split over `ns` workgroup planes
+// whose partial sums the inverse launch adds (HZ_MACC_SPLIT = 1 for the unsplit kernel, A/B).  The
+// gain is small (the MAC at 4 planes: 32.5 us), so chunk latency is not what bounds it either
+int macc_splits(int Qp) {
+    static const int env = std::getenv("HZ_MACC_SPLIT") ? std::atoi(std::getenv("HZ_MACC_SPLIT")) : 0;
+    const int nch = Qp / kMacChunk;
+    const int ns = env > 0 ? env : 2;   // R = 0.9999, alternating: 1: 0.0645 / 0.0644, 2: 0.0632 / 0.0628, 4: 0.0640 /
+                                         // 0.0639 ms per call (MAC 35.0 -> 32.5 us, the inverse's sums +1 us)
+    return std::max(1, std::min(ns, nch));
+}
+template <int BINS>
+void launch_macc(int Qp, int B, const double2* H, const double2* Z, double2* Y, int Q, int ns, hipStream_t s) {
+    static const int bpw = std::getenv("HZ_MACC_BPW") ? std::atoi(std::getenv("HZ_MACC_BPW")) : 8;
+    if (bpw == 4) launch_macc_t<BINS, 4>(Qp, B, H, Z, Y, Q, ns, s);
+    else launch_macc_t<BINS, 8>(Qp, B, H, Z, Y, Q, ns, s);
 }
 
 // the LDS-staged MAC for Qp = 8, 16, 24 when no modal phase rides in the MAC launch (C2: 6.1
@@ -585,9 +610,10 @@ void launch_mac_lds_t(int Qp, int B, const double2* H, const double2* Z, double2
         // 16 bins x 128 blocks: 35.5 us per R = 0.9999 call against 37.4 (32 x 64) and 46.2 (64 x 32),
         // alternating on one box (profiles/r6/highq)
         static const int bins = std::getenv("HZ_MACC_BINS") ? std::atoi(std::getenv("HZ_MACC_BINS")) : 16;
-        if (bins == 64) launch_macc<64>(Qp, B, H, Z, Y, Q, s);
-        else if (bins == 16) launch_macc<16>(Qp, B, H, Z, Y, Q, s);
-        else launch_macc<32>(Qp, B, H, Z, Y, Q, s);
+        const int ns = macc_splits(Qp);
+        if (bins == 64) launch_macc<64>(Qp, B, H, Z, Y, Q, ns, s);
+        else if (bins == 16) launch_macc<16>(Qp, B, H, Z, Y, Q, ns, s);
+        else launch_macc<32>(Qp, B, H, Z, Y, Q, ns, s);
         return;
     }
     if (Qp == 8) hipLaunchKernelGGL((resp_mac_kernel_lds<8, BPW>), grid, dim3(256), (mac_lds_bytes<8, BPW>()), s, H, Z, Y, Q, B);
@@ -707,7 +733,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         yb[i] = y[(kH - k) & (kH - 1)];   // k = 0: replaced by (Y_kH, 0) below
         w[i] = a.tw[k];
     }
-    const double2 ym = y[kH / 2];
+    double2 ym = y[kH / 2];
+    for (int sp = 1; sp < a.ys; ++sp) {   // the split MAC's partial sums, in split order
+        const double2* ys = y + sp * a.ystride;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = t + i * kThreads;
+            const double2 u = ys[k], v = ys[(kH - k) & (kH - 1)];
+            ya[i] = make_double2(ya[i].x + u.x, ya[i].y + u.y);
+            yb[i] = make_double2(yb[i].x + v.x, yb[i].y + v.y);
+        }
+        const double2 um = ys[kH / 2];
+        ym = make_double2(ym.x + um.x, ym.y + um.y);
+    }
     hz2k::InvTw it;
     it.load(a.tw);
     const UpkeepPre up = a.upkeep ? resp_upkeep_pre(a, b) : UpkeepPre();
@@ -1206,7 +1244,8 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         HZ_TRY_HIP(hipMemsetAsync(R.d_Z, 0, sizeof(double) * R.Z_cap, h->stream));
     }
     const size_t zn_at = (size_t)zrows * 2 * kH;   // [zrows] bin kH after the rows
-    HZ_TRY(resp_alloc(&R.d_Y, &R.Y_cap, (size_t)B * kH * 2));
+    const int ys = (mac_lds_ok(Qp, false) && Qp > kMacChunk) ? macc_splits(Qp) : 1;   // (launch_mac_lds's split)
+    HZ_TRY(resp_alloc(&R.d_Y, &R.Y_cap, (size_t)ys * B * kH * 2));
     hipEvent_t* e = nullptr;
     if (h->prof) {
         HZ_TRY(fb_prof_events(h, &e));
@@ -1226,6 +1265,8 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
     a.Z = (double2*)R.d_Z;
     a.Zn = R.d_Z + zn_at;
     a.Y = (const double2*)R.d_Y;
+    a.ys = ys;
+    a.ystride = (long)B * kH;
     a.Hn = R.d_H + (size_t)Qp * 2 * kH;
     a.out = d_out;
     a.hist_next = R.d_hist[R.hcur ^ 1];
@@ -1324,6 +1365,7 @@ int fb_launch_resp(hz_fb* h, const double* d_in, double* d_out, long n) {
         mdi.on = modal && p2 != 0;
         mdi.first2 = p2 == 2 ? 0 : B;
         mdi.n2 = nm2;
+        a.ys = (mac_lds_ok(Qp, mdm.on) && Qp > kMacChunk) ? macc_splits(Qp) : 1;   // launch_mac_lds's planes
         for (int r = 0; r < rep; ++r) {
             if (mac_lds_ok(Qp, mdm.on))
                 launch_mac_lds(Qp, B, (const double2*)R.d_H, (const double2*)R.d_Z, (double2*)R.d_Y, Q, h->stream);
@@ -1480,6 +1522,7 @@ int fb_resp_tail_conv(hz_fb* h, const double* u, long n, double* out, hipStream_
     a.Z = (double2*)S.d_tZ;
     a.Zn = S.d_tZ + (size_t)zrows * 2 * kH;
     a.Y = (const double2*)S.d_tY;
+    a.ys = 1;
     a.Hn = S.d_tH + (size_t)Qp * 2 * kH;
     a.out = out;
     a.upkeep = 0;
