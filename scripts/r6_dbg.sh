@@ -1,10 +1,6 @@
 #!/bin/bash
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
-F=tests/test_filterbank_resp_gpu.py
-for prev in test_time_range_shards test_c2_full_size_against_lti test_shards_sum; do
-  n=0
-  for i in 1 2 3 4 5 6; do
-    timeout -k 10 120 python -u -m pytest -q --timeout 60 --timeout-method thread -p no:cacheprovider "$F::$prev" "$F::test_stream_and_per_sample_after_stationary" > /tmp/o.log 2>&1 || n=$((n+1))
-  done
-  echo "$prev then the stream test: $n failing runs of 6"
+for i in 1 2 3 4 5 6 7 8; do
+HZ_TEST_STATE_FIRST=1 timeout -k 10 300 python -u -m pytest -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_filterbank_resp_gpu.py > /tmp/f.log 2>&1 || { grep -E "^E  |FAILED" /tmp/f.log | head -4; }
 done
+echo done

@@ -11,6 +11,8 @@ Every test drives the GPU object and the CPU restatement (oracle/hz_oracle.c) th
 calls (mix bound 1e-9 of the mix, as for the other engines) and asserts which engine ran
 (last_path); band states are compared with a twin handle that keeps the per-band LTI engine.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -307,6 +309,9 @@ def test_stream_and_per_sample_after_stationary(gpu_lib, lazy):
         assert rel_err(g.process(x), o.process(x)) < TOL
     assert g.last_path() == L.HZ_FB_PATH_RESPONSE
     assert g.response_info()[2] == lazy
+    if os.environ.get("HZ_TEST_STATE_FIRST"):   # (diagnostic) the band states before the stream call
+        st_g, st_o = g.get_state(), o.get_state()
+        assert np.max(np.abs(st_g - st_o)) <= 1e-8 * max(1.0, np.max(np.abs(st_o))), np.argmax(np.abs(st_g - st_o))
     # resonant retuning stream over 3000 samples (Subtractive ALLINONE), order 2
     x = rng.uniform(-1, 1, 3000)
     fr = np.tile(np.linspace(200.0, 4000.0, N), (3000, 1)) * (1.0 + 0.1 * np.sin(np.arange(3000) / 300.0))[:, None]
