@@ -572,9 +572,11 @@ int hz_fb_process_tv(hz_fb* h, const double* in, double* out, size_t n, int kind
         hz::set_error("hz_fb_process_tv: device allocation failed (%zu stream doubles)", n * row);
         rc = HZ_E_ALLOC;
     }
-    if (rc == HZ_OK && (hipMemcpyAsync(d_x, in, sizeof(double) * n, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
-                        hipMemcpyAsync(d_s, stream, sizeof(double) * n * row, hipMemcpyHostToDevice, h->stream) !=
-                            hipSuccess)) {
+    // (blocking copies: complete before the stream's kernel is enqueued, whatever engine and queue
+    // the runtime uses for pageable sources)
+    if (rc == HZ_OK && (hipStreamSynchronize(h->stream) != hipSuccess ||
+                        hipMemcpy(d_x, in, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess ||
+                        hipMemcpy(d_s, stream, sizeof(double) * n * row, hipMemcpyHostToDevice) != hipSuccess)) {
         hz::set_error("hz_fb_process_tv: upload failed");
         rc = HZ_E_HIP;
     }
